@@ -1,0 +1,84 @@
+# Locust-MI355X build (replaces the reference's CMake + vendored FindCUDA,
+# /root/reference/MapReduce/CMakeLists.txt:1-35 and GNUmakefile:1-31).
+#
+#   make            -> locust_amd/_lib/liblocust.so, locust_amd/_locust*.so, build/MapReduce
+#   make debug      -> same with -O0 -g
+#   make asan       -> host-only ASan/UBSan build of the CPU engine + CLI (build/asan/)
+#   make clean
+#
+# Device code targets gfx950 (MI355X) only.  Device helpers are header-only, so no
+# relocatable device code (-fgpu-rdc) is needed, unlike the reference.
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+PYTHON    ?= python3
+ARCH      ?= gfx950
+OPT       ?= -O3
+BUILD     := build
+OBJ       := $(BUILD)/obj
+LIBDIR    := locust_amd/_lib
+
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+COMMON    := -std=c++17 -fPIC -Icsrc/include -Wall -Wextra -Wno-unused-parameter
+HIPFLAGS  := $(COMMON) $(OPT) --offload-arch=$(ARCH) -munsafe-fp-atomics
+CXXFLAGS  := $(COMMON) $(OPT)
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lpthread
+
+HIP_SRCS  := $(wildcard csrc/kernels/*.hip csrc/engine/*.hip csrc/comm/*.hip)
+CPP_SRCS  := $(wildcard csrc/engine/*.cpp csrc/io/*.cpp csrc/comm/*.cpp)
+HDRS      := $(wildcard csrc/include/locust/*.hpp csrc/include/locust/device/*.hpp)
+
+HIP_OBJS  := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
+CPP_OBJS  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))
+
+LIB       := $(LIBDIR)/liblocust.so
+PYMOD     := locust_amd/_locust$(PY_EXT)
+CLI       := $(BUILD)/MapReduce
+
+.PHONY: all clean debug asan
+all: $(LIB) $(PYMOD) $(CLI)
+
+$(OBJ)/%.o: csrc/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.o: csrc/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS) $(CPP_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ $(LDLIBS) -Wl,-soname,liblocust.so
+
+$(OBJ)/python/bindings.o: csrc/python/bindings.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -c $< -o $@
+
+$(PYMOD): $(OBJ)/python/bindings.o $(LIB)
+	$(CXX) -shared -o $@ $< -L$(LIBDIR) -llocust -Wl,-rpath,'$$ORIGIN/_lib'
+
+$(OBJ)/cli/main.o: csrc/cli/main.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(CLI): $(OBJ)/cli/main.o $(LIB)
+	$(CXX) -o $@ $< -L$(LIBDIR) -llocust -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+debug:
+	$(MAKE) OPT="-O0 -g" all
+
+# Host-only sanitizer build: the CPU engine, I/O, TCP comm and the CLI with
+# --backend cpu.  (GPU ASan / xnack+ is not available on the GPU pool.)
+ASAN_SRCS := csrc/engine/common.cpp csrc/engine/cpu_wordcount.cpp csrc/engine/dist.cpp \
+             csrc/io/io.cpp csrc/comm/tcp_comm.cpp csrc/cli/main.cpp csrc/cli/asan_stubs.cpp
+asan: $(BUILD)/asan/MapReduce
+$(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) -std=c++17 -Icsrc/include -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
+	  -o $@ $(ASAN_SRCS) -lpthread
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR) locust_amd/_locust*.so

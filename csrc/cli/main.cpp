@@ -1,0 +1,293 @@
+// ./MapReduce -- command line driver (SURVEY.md §2.6 API surface; /root/reference/
+// MapReduce/src/main.cu:358-532).
+//
+// Positional CLI of the reference, byte-compatible stdout:
+//   MapReduce <file>                                   whole file, one process
+//   MapReduce <file> <line_start> <line_end>           window [start, end)
+//   MapReduce <file> <start> <end> <node_num> <stage>  stage 0 = all, 1 = map only
+//                                                      (writes a spill), 2 = reduce only
+// plus long flags (runtime switches replacing the reference's #defines):
+//   --backend gpu|cpu  --reduce-path lds|global  --map-path compat|fast
+//   --sort radix|dict  --gpus N  --emits-per-line N  --max-key N  --ref-compat
+//   --stage map|reduce  --spill-dir DIR  --spill-format text|binary  --inputs a,b,...
+//   --warmup N  --iters N  --json FILE  --quiet  --check  --device N
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "locust/dist.hpp"
+#include "locust/engine.hpp"
+#include "locust/io.hpp"
+
+using namespace locust;
+
+namespace {
+
+struct CliArgs {
+  std::string file;
+  i64 line_start = -1, line_end = -1;
+  int node = 0;
+  int stage = 0;
+  bool window = false;
+  JobConfig cfg;
+  int gpus = 1;
+  std::string spill_dir = "/tmp";
+  SpillFormat spill_fmt = SpillFormat::kText;
+  std::vector<std::string> inputs;
+  int warmup = 0, iters = 1;
+  std::string json;
+  bool quiet = false;
+};
+
+void usage() {
+  std::printf("Missing or invalid arguments.\n");
+  std::printf("mapreduce <filename> [line_start] [line_end] [node_num] [stage]\n");
+}
+
+std::vector<std::string> split(const std::string& s, char c) {
+  std::vector<std::string> out;
+  size_t p = 0;
+  while (p <= s.size()) {
+    size_t q = s.find(c, p);
+    if (q == std::string::npos) q = s.size();
+    if (q > p) out.push_back(s.substr(p, q - p));
+    p = q + 1;
+  }
+  return out;
+}
+
+bool parse(int argc, char** argv, CliArgs* a) {
+  std::vector<std::string> pos;
+  apply_env_overrides(a->cfg);
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto need = [&](const char* name) -> std::string {
+      if (i + 1 >= argc) throw Error(std::string("missing value for ") + name);
+      return argv[++i];
+    };
+    if (s == "--backend") {
+      std::string v = need("--backend");
+      a->cfg.backend = v == "cpu" ? Backend::kCpu : Backend::kGpu;
+    } else if (s == "--reduce-path") {
+      a->cfg.reduce_path = need("--reduce-path") == "global" ? ReducePath::kGlobal : ReducePath::kLds;
+    } else if (s == "--map-path") {
+      a->cfg.map_path = need("--map-path") == "compat" ? MapPath::kCompat : MapPath::kFast;
+    } else if (s == "--sort") {
+      a->cfg.sort_path = need("--sort") == "dict" ? SortPath::kDict : SortPath::kRadix;
+    } else if (s == "--gpus") {
+      a->gpus = std::atoi(need("--gpus").c_str());
+    } else if (s == "--device") {
+      a->cfg.device = std::atoi(need("--device").c_str());
+    } else if (s == "--emits-per-line") {
+      a->cfg.emits_per_line = std::atoi(need("--emits-per-line").c_str());
+    } else if (s == "--max-key") {
+      a->cfg.max_key_len = std::atoi(need("--max-key").c_str());
+    } else if (s == "--ref-compat") {
+      a->cfg.ref_compat = true;
+    } else if (s == "--check") {
+      a->cfg.check = true;
+    } else if (s == "--combine") {
+      a->cfg.combine = true;
+    } else if (s == "--no-sync-plan") {
+      a->cfg.sync_plan = false;
+    } else if (s == "--stage") {
+      std::string v = need("--stage");
+      a->stage = v == "map" || v == "1" ? 1 : (v == "reduce" || v == "2" ? 2 : 0);
+    } else if (s == "--spill-dir") {
+      a->spill_dir = need("--spill-dir");
+    } else if (s == "--spill-format") {
+      a->spill_fmt = need("--spill-format") == "binary" ? SpillFormat::kBinary : SpillFormat::kText;
+    } else if (s == "--inputs") {
+      a->inputs = split(need("--inputs"), ',');
+    } else if (s == "--warmup") {
+      a->warmup = std::atoi(need("--warmup").c_str());
+    } else if (s == "--iters") {
+      a->iters = std::max(1, std::atoi(need("--iters").c_str()));
+    } else if (s == "--json") {
+      a->json = need("--json");
+    } else if (s == "--quiet") {
+      a->quiet = true;
+    } else if (s.size() > 2 && s[0] == '-' && s[1] == '-') {
+      throw Error("unknown flag " + s);
+    } else {
+      pos.push_back(s);
+    }
+  }
+  if (pos.empty()) return false;
+  a->file = pos[0];
+  if (pos.size() > 1) {
+    a->window = true;
+    a->line_start = std::strtol(pos[1].c_str(), nullptr, 10);
+    a->line_end = pos.size() > 2 ? std::strtol(pos[2].c_str(), nullptr, 10) : -1;
+  }
+  if (pos.size() > 3) {
+    a->node = (int)std::strtol(pos[3].c_str(), nullptr, 10);
+    if (pos.size() > 4) a->stage = (int)std::strtol(pos[4].c_str(), nullptr, 10);
+  }
+  return true;
+}
+
+std::string spill_path(const CliArgs& a, int node) {
+  return a.spill_dir + "/out." + std::to_string(node) +
+         (a.spill_fmt == SpillFormat::kBinary ? ".kv" : ".txt");
+}
+
+void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
+  if (a.json.empty()) return;
+  std::FILE* f = a.json == "-" ? stderr : std::fopen(a.json.c_str(), "w");
+  if (!f) throw Error("cannot write json: " + a.json);
+  std::vector<double> w = walls;
+  std::sort(w.begin(), w.end());
+  const double med = w.empty() ? 0 : w[w.size() / 2];
+  std::fprintf(f,
+               "{\"backend\": \"%s\", \"gpus\": %d, \"lines\": %llu, \"tokens\": %llu, "
+               "\"unique\": %llu, \"overflow_lines\": %llu, \"truncated\": %llu, "
+               "\"map_ms\": %.6f, \"process_ms\": %.6f, \"reduce_ms\": %.6f, \"h2d_ms\": %.6f, "
+               "\"d2h_ms\": %.6f, \"wall_ms_median\": %.6f, \"iters\": %d, \"map_path\": \"%s\", "
+               "\"reduce_path\": \"%s\", \"sort\": \"%s\"}\n",
+               a.cfg.backend == Backend::kCpu ? "cpu" : "gpu", a.gpus,
+               (unsigned long long)r.num_lines, (unsigned long long)r.num_tokens,
+               (unsigned long long)r.num_unique, (unsigned long long)r.overflow_lines,
+               (unsigned long long)r.truncated, r.times.map_ms, r.times.process_ms,
+               r.times.reduce_ms, r.times.h2d_ms, r.times.d2h_ms, med, (int)w.size(),
+               to_string(a.cfg.map_path), to_string(a.cfg.reduce_path), to_string(a.cfg.sort_path));
+  if (f != stderr) std::fclose(f);
+}
+
+long long ns(double ms) { return (long long)(ms * 1e6 + 0.5); }
+
+int run(const CliArgs& a) {
+  const bool cpu = a.cfg.backend == Backend::kCpu;
+  const char* dev = cpu ? "CPU" : "GPU";
+  if (a.window)
+    std::printf("Using custom start and end locations: (%i, %i)\n", (int)a.line_start,
+                (int)a.line_end);
+
+  // ---------------- stage 2: reduce only ----------------
+  if (a.stage == 2) {
+    std::vector<std::string> files = a.inputs;
+    if (files.empty()) files.push_back(spill_path(a, a.node));
+    std::vector<KeyCount> recs;
+    for (const auto& f : files) {
+      auto r = read_spill(f);
+      recs.insert(recs.end(), r.begin(), r.end());
+    }
+    std::vector<PackedKey> toks = records_to_tokens(recs);
+    WordCountResult r;
+    if (cpu) {
+      CpuWordCount eng(a.cfg);
+      r = eng.run_reduce_stage(toks.data(), toks.size());
+    } else {
+      GpuWordCount eng(a.cfg, 1, std::max<u64>(1, div_up(toks.size(), a.cfg.emits_per_line)) + 1);
+      r = eng.run_reduce_stage(toks.data(), toks.size());
+    }
+    std::printf("%s reduce %lld nanoseconds \n", dev, ns(r.times.process_ms + r.times.reduce_ms));
+    std::string out;
+    if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r.entries, &out);
+    std::fflush(stdout);
+    write_all(stdout, out);
+    std::printf("\nDone\n");
+    return 0;
+  }
+
+  // CPU build ignores the line window (its loadFile takes none, main.cu:242) -- only
+  // reproduced under --ref-compat.
+  const bool use_window = a.window && !(cpu && a.cfg.ref_compat);
+  LoadedText text = load_lines(a.file, use_window ? a.line_start : -1,
+                               use_window ? a.line_end : -1, a.cfg.ref_compat);
+  if (!cpu) std::printf("Length: %i\n", (int)text.input.num_lines);
+
+  // ---------------- multi-GPU in one process (loopback over the node's GPUs) -----------
+  if (a.gpus > 1 && a.stage == 0) {
+    DistConfig dc;
+    dc.job = a.cfg;
+    dc.world = a.gpus;
+    DistResult dr = run_single_process_multi_gpu(dc, text.input);
+    std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
+    std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
+    std::printf("%s reduce %lld nanoseconds \n", dev, ns(dr.reduce_ms));
+    std::string out;
+    if (!a.quiet) format_gpu_output(dr.result.entries, &out);
+    std::fflush(stdout);
+    write_all(stdout, out);
+    std::printf("\nDone\n");
+    return 0;
+  }
+
+  // ---------------- stage 1: map only -> spill ----------------
+  if (a.stage == 1) {
+    WordCountResult stats;
+    std::vector<PackedKey> toks;
+    const u64 t0 = now_ns();
+    if (cpu) {
+      CpuWordCount eng(a.cfg);
+      toks = eng.run_map_stage(text.input, &stats);
+    } else {
+      GpuWordCount eng(a.cfg, text.input.bytes, text.input.num_lines);
+      toks = eng.run_map_stage(text.input, &stats);
+    }
+    const u64 t1 = now_ns();
+    for (u64 k = 0; k < stats.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
+    std::printf("%s mapping %lld nanoseconds \n", dev, 0ll);
+    std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, (long long)(t1 - t0));
+    write_spill(spill_path(a, a.node), tokens_to_records(toks), a.spill_fmt);
+    std::printf("MODE_MULTI: Finished map\n");
+    return 0;
+  }
+
+  // ---------------- stage 0: full pipeline ----------------
+  WordCountResult r;
+  std::vector<double> walls;
+  if (cpu) {
+    CpuWordCount eng(a.cfg);
+    for (int i = 0; i < a.warmup; ++i) eng.run(text.input);
+    for (int i = 0; i < a.iters; ++i) {
+      r = eng.run(text.input);
+      walls.push_back(r.times.wall_ms);
+    }
+    std::printf("CPU mapping %lld nanoseconds \n", ns(r.times.map_ms));
+    std::printf("CPU sorting %lld nanoseconds \n", ns(r.times.process_ms));
+    std::printf("CPU reducing %lld nanoseconds \n", ns(r.times.reduce_ms));
+  } else {
+    GpuWordCount eng(a.cfg, text.input.bytes, text.input.num_lines);
+    for (int i = 0; i < a.warmup; ++i) eng.run(text.input);
+    for (int i = 0; i < a.iters; ++i) {
+      r = eng.run(text.input);
+      walls.push_back(r.times.wall_ms);
+    }
+    std::printf("GPU mapping %lld nanoseconds \n", ns(r.times.map_ms));
+    for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
+    std::printf("GPU stream compaction and sorting %lld nanoseconds \n", ns(r.times.process_ms));
+    std::printf("GPU reduce %lld nanoseconds \n", ns(r.times.reduce_ms));
+  }
+  if (r.truncated)
+    LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",
+                    (unsigned long long)r.truncated, a.cfg.max_key_len);
+  std::string out;
+  if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r.entries, &out);
+  std::fflush(stdout);
+  write_all(stdout, out);
+  write_json(a, r, walls);
+  std::printf("\nDone\n");
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::printf("Running\n");
+  CliArgs a;
+  try {
+    if (!parse(argc, argv, &a)) {
+      usage();
+      return -1;
+    }
+    return run(a);
+  } catch (const std::exception& e) {
+    std::fflush(stdout);
+    std::fprintf(stderr, "MapReduce: error: %s\n", e.what());
+    return 2;
+  }
+}

@@ -1,0 +1,197 @@
+// RCCL communicator: one rank per GPU, collectives over xGMI.
+//
+// Bootstrap: the ncclUniqueId is created by rank 0 and shared over the TCP control channel
+// (the MI355X-native replacement of the reference's TCP command socket, slave.py:5-16).
+// Data plane: the shuffle is ONE grouped ncclSend/ncclRecv per peer (an all-to-all-v), so
+// every point-to-point xGMI link of the node carries 1/P of each rank's records at once
+// -- unlike a ring, which would serialise on one link per step.  The self bucket is a
+// device-to-device copy.  Small control collectives (samples, counts, totals) are
+// ncclAllGather on a device staging buffer.  Every wait polls ncclCommGetAsyncError with
+// a timeout and aborts the communicator instead of hanging.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <thread>
+
+#include "locust/dist.hpp"
+#include "locust/hip_check.hpp"
+
+#define LOCUST_RCCL_CHECK(expr)                                                        \
+  do {                                                                                 \
+    ncclResult_t _r = (expr);                                                          \
+    if (_r != ncclSuccess)                                                             \
+      ::locust::throw_error(__FILE__, __LINE__,                                        \
+                            std::string("RCCL error: ") + ncclGetErrorString(_r) +     \
+                                " in `" #expr "`");                                    \
+  } while (0)
+
+namespace locust {
+namespace {
+
+class RcclComm final : public Communicator {
+ public:
+  RcclComm(int rank, int world, int device, const std::string& host, int port, double timeout_s)
+      : rank_(rank), world_(world), timeout_s_(timeout_s) {
+    tcp_ = make_tcp_comm(rank, world, host, port, timeout_s);
+    ncclUniqueId id;
+    if (rank == 0) LOCUST_RCCL_CHECK(ncclGetUniqueId(&id));
+    std::vector<ncclUniqueId> ids((size_t)world);
+    tcp_->allgather_host(&id, ids.data(), sizeof(id));
+    id = ids[0];
+    LOCUST_HIP_CHECK(hipSetDevice(device));
+    LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    LOCUST_RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    stage_cap_ = 1 << 20;
+    LOCUST_HIP_CHECK(hipMalloc(&d_stage_, stage_cap_ * (u64)(world + 1)));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_stage_, stage_cap_ * (u64)(world + 1), hipHostMallocDefault));
+  }
+
+  ~RcclComm() override {
+    if (comm_) {
+      if (aborted_)
+        (void)ncclCommAbort(comm_);
+      else
+        (void)ncclCommDestroy(comm_);
+    }
+    if (d_stage_) (void)hipFree(d_stage_);
+    if (h_stage_) (void)hipHostFree(h_stage_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  int rank() const override { return rank_; }
+  int size() const override { return world_; }
+  const char* name() const override { return "rccl"; }
+  bool device_buffers() const override { return true; }
+
+  void allgather_host(const void* send, void* recv, u64 bytes) override {
+    ensure_stage(bytes);
+    char* dsend = d_stage_ + (u64)world_ * stage_cap_;
+    LOCUST_HIP_CHECK(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_));
+    LOCUST_RCCL_CHECK(ncclAllGather(dsend, d_stage_, bytes, ncclUint8, comm_, stream_));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(h_stage_, d_stage_, bytes * (u64)world_,
+                                    hipMemcpyDeviceToHost, stream_));
+    wait(stream_);
+    std::memcpy(recv, h_stage_, bytes * (u64)world_);
+  }
+
+  void gatherv_host(const void* send, u64 bytes, std::vector<char>* recv_at_root,
+                    std::vector<u64>* sizes_at_root, int root) override {
+    // Sizes over RCCL, payload over grouped send/recv through device staging buffers.
+    std::vector<u64> sizes((size_t)world_);
+    allgather_host(&bytes, sizes.data(), sizeof(u64));
+    u64 total = 0, maxb = 0;
+    for (u64 s : sizes) {
+      total += s;
+      maxb = std::max(maxb, s);
+    }
+    char* dsend = nullptr;
+    char* drecv = nullptr;
+    LOCUST_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dsend), std::max<u64>(bytes, 1), stream_));
+    if (rank_ == root)
+      LOCUST_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&drecv), std::max<u64>(total, 1), stream_));
+    if (bytes) LOCUST_HIP_CHECK(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_));
+    LOCUST_RCCL_CHECK(ncclGroupStart());
+    if (rank_ == root) {
+      u64 off = 0;
+      for (int r = 0; r < world_; ++r) {
+        if (r == root) {
+          if (bytes) LOCUST_HIP_CHECK(hipMemcpyAsync(drecv + off, dsend, bytes, hipMemcpyDeviceToDevice, stream_));
+        } else if (sizes[(size_t)r]) {
+          LOCUST_RCCL_CHECK(ncclRecv(drecv + off, sizes[(size_t)r], ncclUint8, r, comm_, stream_));
+        }
+        off += sizes[(size_t)r];
+      }
+    } else if (bytes) {
+      LOCUST_RCCL_CHECK(ncclSend(dsend, bytes, ncclUint8, root, comm_, stream_));
+    }
+    LOCUST_RCCL_CHECK(ncclGroupEnd());
+    if (rank_ == root) {
+      recv_at_root->resize(total);
+      if (total)
+        LOCUST_HIP_CHECK(hipMemcpyAsync(recv_at_root->data(), drecv, total, hipMemcpyDeviceToHost, stream_));
+      if (sizes_at_root) *sizes_at_root = sizes;
+    }
+    LOCUST_HIP_CHECK(hipFreeAsync(dsend, stream_));
+    if (drecv) LOCUST_HIP_CHECK(hipFreeAsync(drecv, stream_));
+    wait(stream_);
+    (void)maxb;
+  }
+
+  void barrier() override {
+    int v = 0;
+    std::vector<int> all((size_t)world_);
+    allgather_host(&v, all.data(), sizeof(int));
+  }
+
+  void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
+                 const u64* recv_bytes, const u64* recv_off, void* stream) override {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
+    const char* sb = static_cast<const char*>(send);
+    char* rb = static_cast<char*>(recv);
+    if (send_bytes[rank_])
+      LOCUST_HIP_CHECK(hipMemcpyAsync(rb + recv_off[rank_], sb + send_off[rank_], send_bytes[rank_],
+                                      hipMemcpyDeviceToDevice, s));
+    LOCUST_RCCL_CHECK(ncclGroupStart());
+    for (int p = 0; p < world_; ++p) {
+      if (p == rank_) continue;
+      if (send_bytes[p])
+        LOCUST_RCCL_CHECK(ncclSend(sb + send_off[p], send_bytes[p], ncclUint8, p, comm_, s));
+      if (recv_bytes[p])
+        LOCUST_RCCL_CHECK(ncclRecv(rb + recv_off[p], recv_bytes[p], ncclUint8, p, comm_, s));
+    }
+    LOCUST_RCCL_CHECK(ncclGroupEnd());
+    wait(s);
+  }
+
+ private:
+  void ensure_stage(u64 bytes) {
+    if (bytes <= stage_cap_) return;
+    wait(stream_);
+    (void)hipFree(d_stage_);
+    (void)hipHostFree(h_stage_);
+    stage_cap_ = align_up(bytes, 4096);
+    LOCUST_HIP_CHECK(hipMalloc(&d_stage_, stage_cap_ * (u64)(world_ + 1)));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_stage_, stage_cap_ * (u64)(world_ + 1), hipHostMallocDefault));
+  }
+
+  // Wait for the stream while watching for asynchronous RCCL errors and a timeout.
+  void wait(hipStream_t s) {
+    const u64 deadline = now_ns() + (u64)(timeout_s_ * 1e9);
+    u64 spins = 0;
+    for (;;) {
+      hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) LOCUST_HIP_CHECK(e);
+      ncclResult_t ae = ncclSuccess;
+      LOCUST_RCCL_CHECK(ncclCommGetAsyncError(comm_, &ae));
+      if (ae != ncclSuccess && ae != ncclInProgress) {
+        aborted_ = true;
+        throw Error(std::string("RCCL async error: ") + ncclGetErrorString(ae));
+      }
+      if (now_ns() > deadline) {
+        aborted_ = true;
+        throw Error("RCCL operation timed out after " + std::to_string(timeout_s_) + " s");
+      }
+      if (++spins > 1000) std::this_thread::yield();
+    }
+  }
+
+  int rank_, world_;
+  double timeout_s_;
+  bool aborted_ = false;
+  std::unique_ptr<Communicator> tcp_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  char* d_stage_ = nullptr;
+  char* h_stage_ = nullptr;
+  u64 stage_cap_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
+                                             const std::string& host, int port, double timeout_s) {
+  return std::unique_ptr<Communicator>(new RcclComm(rank, world, device, host, port, timeout_s));
+}
+
+}  // namespace locust

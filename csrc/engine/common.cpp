@@ -1,0 +1,153 @@
+// Shared host-side pieces: logging, errors, env config, tokenizer oracle, result checks.
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstring>
+#include <string>
+
+#include "locust/config.hpp"
+#include "locust/dstring.hpp"
+#include "locust/engine.hpp"
+
+namespace locust {
+
+int& log_rank() {
+  static thread_local int r = -1;
+  return r;
+}
+
+LogLevel log_level() {
+  static LogLevel lvl = [] {
+    const char* e = std::getenv("LOCUST_LOG");
+    if (!e) return LogLevel::kWarn;
+    std::string s(e);
+    if (s == "error") return LogLevel::kError;
+    if (s == "info") return LogLevel::kInfo;
+    if (s == "debug") return LogLevel::kDebug;
+    return LogLevel::kWarn;
+  }();
+  return lvl;
+}
+
+void log_msg(LogLevel lvl, const char* fmt, ...) {
+  if ((int)lvl > (int)log_level()) return;
+  static const char* names[] = {"ERROR", "WARN", "INFO", "DEBUG"};
+  char buf[2048];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  // stderr only: stdout stays byte-compatible with the reference.
+  if (log_rank() >= 0)
+    std::fprintf(stderr, "[locust %s r%d] %s\n", names[(int)lvl], log_rank(), buf);
+  else
+    std::fprintf(stderr, "[locust %s] %s\n", names[(int)lvl], buf);
+}
+
+void throw_error(const char* file, int line, const std::string& msg) {
+  std::string where = std::string(file) + ":" + std::to_string(line);
+  std::string rank = log_rank() >= 0 ? ("rank " + std::to_string(log_rank()) + ": ") : "";
+  throw Error(rank + msg + " (" + where + ")");
+}
+
+bool fault_injected(int rank, const char* stage) {
+  const char* e = std::getenv("LOCUST_FAULT");
+  if (!e || !*e) return false;
+  std::string s(e);
+  auto colon = s.find(':');
+  if (colon == std::string::npos) return false;
+  int r = std::atoi(s.substr(0, colon).c_str());
+  return r == rank && s.substr(colon + 1) == stage;
+}
+
+u64 now_ns() {
+  return (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void apply_env_overrides(JobConfig& cfg) {
+  if (const char* e = std::getenv("LOCUST_CHECK")) cfg.check = std::atoi(e) != 0;
+  if (const char* e = std::getenv("LOCUST_REDUCE_PATH")) {
+    std::string s(e);
+    if (s == "lds") cfg.reduce_path = ReducePath::kLds;
+    if (s == "global") cfg.reduce_path = ReducePath::kGlobal;
+  }
+  if (const char* e = std::getenv("LOCUST_MAP_PATH")) {
+    std::string s(e);
+    if (s == "compat") cfg.map_path = MapPath::kCompat;
+    if (s == "fast") cfg.map_path = MapPath::kFast;
+  }
+  if (const char* e = std::getenv("LOCUST_SORT")) {
+    std::string s(e);
+    if (s == "radix") cfg.sort_path = SortPath::kRadix;
+    if (s == "dict") cfg.sort_path = SortPath::kDict;
+  }
+}
+
+const char* to_string(ReducePath p) { return p == ReducePath::kLds ? "lds" : "global"; }
+const char* to_string(MapPath p) { return p == MapPath::kCompat ? "compat" : "fast"; }
+const char* to_string(SortPath p) { return p == SortPath::kRadix ? "radix" : "dict"; }
+
+int tokenize_line(const char* line, u64 len, const JobConfig& cfg, std::vector<PackedKey>* out,
+                  u64* truncated) {
+  // The reference works on a NUL-terminated copy (main.cu:55-59); text after an embedded
+  // NUL is invisible to strtok_r, exactly as here.
+  std::string buf(line, len);
+  char* save = nullptr;
+  char* tok = d_strtok_r(&buf[0], cfg.delimiters.c_str(), &save);
+  int count = 0;
+  int dropped = 0;
+  while (tok != nullptr) {
+    if (count >= cfg.emits_per_line) {
+      dropped = 1;
+      break;
+    }
+    int n = d_strlen(tok);
+    if (n > cfg.max_key_len) {
+      if (truncated) ++*truncated;
+      n = cfg.max_key_len;
+    }
+    PackedKey k;
+    pack_key(tok, n, k.w);
+    out->push_back(k);
+    ++count;
+    tok = d_strtok_r(nullptr, cfg.delimiters.c_str(), &save);
+  }
+  return dropped;
+}
+
+void entries_from_sorted_tokens(const PackedKey* sorted, u64 n, std::vector<WordCountEntry>* out) {
+  out->clear();
+  u64 i = 0;
+  while (i < n) {
+    u64 j = i + 1;
+    while (j < n && key_compare(sorted[j].w, sorted[i].w) == 0) ++j;
+    out->push_back(WordCountEntry{sorted[i], i, j - i});
+    i = j;
+  }
+}
+
+// LOCUST_CHECK invariants: keys strictly increasing, runs contiguous
+// (val[j+1] == val[j] + count[j]), counts sum to the token count.
+void validate_result(const WordCountResult& r) {
+  u64 expect_val = r.entries.empty() ? 0 : r.entries.front().val;
+  u64 sum = 0;
+  for (size_t j = 0; j < r.entries.size(); ++j) {
+    const auto& e = r.entries[j];
+    if (j && key_compare(r.entries[j - 1].key.w, e.key.w) >= 0)
+      throw Error("LOCUST_CHECK: output keys not strictly increasing at entry " +
+                  std::to_string(j));
+    if (e.val != expect_val)
+      throw Error("LOCUST_CHECK: val discontinuity at entry " + std::to_string(j));
+    if (e.count == 0) throw Error("LOCUST_CHECK: zero count at entry " + std::to_string(j));
+    expect_val += e.count;
+    sum += e.count;
+  }
+  if (sum != r.num_tokens)
+    throw Error("LOCUST_CHECK: sum(count)=" + std::to_string(sum) +
+                " != num_tokens=" + std::to_string(r.num_tokens));
+  if (r.entries.size() != r.num_unique) throw Error("LOCUST_CHECK: num_unique mismatch");
+}
+
+}  // namespace locust

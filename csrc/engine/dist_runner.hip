@@ -1,0 +1,47 @@
+// Single-process multi-rank driver: one thread per rank, loopback communicator, ranks
+// placed round-robin on the visible GPUs (or the CPU engine).  Used by `MapReduce --gpus N`
+// and by the tests that rehearse the 2/4/8-rank shuffle on a single GPU.
+#include <exception>
+#include <thread>
+
+#include "locust/dist.hpp"
+#include "locust/hip_check.hpp"
+
+namespace locust {
+
+DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole) {
+  const int P = cfg.world;
+  LOCUST_CHECK_ARG(P >= 1, "world must be >= 1");
+  const bool gpu = cfg.job.backend == Backend::kGpu;
+  int ndev = 1;
+  if (gpu) {
+    LOCUST_HIP_CHECK(hipGetDeviceCount(&ndev));
+    LOCUST_CHECK_ARG(ndev >= 1, "no GPU visible");
+  }
+  std::vector<TextInput> shards = shard_text(whole, P);
+  LoopbackGroup group(P, gpu);
+  std::vector<DistResult> results((size_t)P);
+  std::vector<std::exception_ptr> errors((size_t)P);
+  std::vector<std::thread> threads;
+  for (int r = 0; r < P; ++r) {
+    threads.emplace_back([&, r] {
+      try {
+        JobConfig job = cfg.job;
+        job.device = gpu ? (cfg.job.device + r) % ndev : 0;
+        std::unique_ptr<ShardEngine> eng =
+            gpu ? make_gpu_shard_engine(job, shards[(size_t)r].bytes, shards[(size_t)r].num_lines)
+                : make_cpu_shard_engine(job);
+        std::unique_ptr<Communicator> comm = group.comm(r);
+        results[(size_t)r] = run_distributed(cfg, *comm, *eng, shards[(size_t)r]);
+      } catch (...) {
+        errors[(size_t)r] = std::current_exception();
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  for (auto& e : errors)
+    if (e) std::rethrow_exception(e);
+  return results[0];
+}
+
+}  // namespace locust

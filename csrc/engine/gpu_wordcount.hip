@@ -1,0 +1,563 @@
+// Single-GPU WordCount pipeline and the per-rank GPU shard engine (host orchestration of
+// the HIP kernels).
+//
+// Reference orchestration: /root/reference/MapReduce/src/main.cu:388-487 (cudaMalloc per
+// run, synchronous cudaMemcpy of fixed 5,800/116,000-slot arrays, thrust calls that block,
+// no error checks).  Here: one device arena allocated at construction, pinned host staging,
+// a single stream, hipEvents at every stage boundary, exact-size transfers, and look-back
+// scratch zeroed by ONE memset per run.
+#include <algorithm>
+#include <cstring>
+
+#include "locust/dist.hpp"
+#include "locust/engine.hpp"
+#include "locust/hip_check.hpp"
+#include "locust/kernels.hpp"
+
+namespace locust {
+
+void validate_result(const WordCountResult& r);  // engine/common.cpp
+
+namespace {
+
+struct Arena {
+  char* base = nullptr;
+  u64 size = 0, used = 0;
+  template <typename T>
+  T* take(u64 count) {
+    used = align_up(used, 256);
+    T* p = reinterpret_cast<T*>(base + used);
+    used += count * sizeof(T);
+    if (used > size) throw Error("device arena overflow (internal sizing bug)");
+    return p;
+  }
+};
+
+struct SizingPlan {
+  u64 bytes = 0;
+  template <typename T>
+  void add(u64 count) {
+    bytes = align_up(bytes, 256) + count * sizeof(T);
+  }
+};
+
+constexpr u32 kMaxSamples = 4096;
+constexpr u32 kMaxRanks = 1024;
+
+// Device pipeline: every buffer of one engine instance.  cap_records is the number of
+// records (tokens or received KeyCount records) the sort/reduce side can hold.
+struct DevicePipeline {
+  JobConfig cfg;
+  u64 cap_bytes = 0, cap_lines = 0, cap = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  Arena arena;
+
+  char* d_text = nullptr;
+  u64* d_nl = nullptr;
+  char* d_delims = nullptr;
+  KeysSoA slots{}, tokens{}, sorted{}, heads{};
+  u32* d_line_counts = nullptr;
+  u64* d_counts = nullptr;         // per-record counts of received records
+  u64* d_sorted_counts = nullptr;  // counts in sorted order
+  u64* d_prefix = nullptr;         // exclusive scan of sorted counts
+  u64* d_head_val = nullptr;
+  u64* d_head_count = nullptr;
+  u32* d_perm = nullptr;
+  OutRecord* d_out = nullptr;
+  KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
+  PackedKey* d_samples = nullptr;
+  PackedKey* d_splitters = nullptr;
+  u64* d_offsets = nullptr;
+  u64* d_offset = nullptr;
+
+  // zeroed once per run: counters + every look-back region
+  char* d_sync = nullptr;
+  u64 sync_bytes = 0;
+  MapCounters* d_ctr = nullptr;
+  LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{};
+  RadixWorkspace rx{};
+
+  char* h_text = nullptr;
+  MapCounters* h_ctr = nullptr;
+  SortPlan* h_plan = nullptr;
+  OutRecord* h_out = nullptr;
+  u64* h_keys = nullptr;  // staging for key up/downloads (4 words x cap)
+  PackedKey* h_small = nullptr;
+  u64* h_u64 = nullptr;
+
+  DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines, u64 cap_records = 0)
+      : cfg(c) {
+    LOCUST_CHECK_ARG(cfg.emits_per_line > 0, "emits_per_line must be > 0");
+    LOCUST_CHECK_ARG(cfg.max_key_len > 0 && cfg.max_key_len <= kKeyBytes - 1,
+                     "max_key_len must be in [1, 31]");
+    cap_bytes = std::max<u64>(max_bytes, 1);
+    cap_lines = std::max<u64>(max_lines, 1);
+    cap = cap_records ? cap_records
+                      : std::min<u64>(cap_lines * (u64)cfg.emits_per_line, cap_bytes / 2 + 1);
+    cap = std::max<u64>(cap, 1);
+    LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
+    LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
+    LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (auto& e : ev) LOCUST_HIP_CHECK(hipEventCreate(&e));
+
+    const bool compat = cfg.map_path == MapPath::kCompat;
+    const u64 slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
+    const u64 t_line = div_up(cap_bytes, kLineIdxTile) + 1;
+    const u64 t_compact = div_up(cap_lines, 256) + 1;
+    const u64 t_map = div_up(cap_bytes, kMapTileBytes) + 1;
+    const u64 t_heads = div_up(cap, kReduceTile) + 1;
+    const u64 t_scan = div_up(cap, kReduceTile) + 1;
+    const u64 rx_zero_words = (u64)kNumPositions * 256 + kNumPositions +
+                              (u64)kNumPositions * radix_status_words(cap);
+    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan);
+
+    SizingPlan sz;
+    sz.add<char>(cap_bytes + 64);
+    sz.add<u64>(cap_lines + 1);
+    sz.add<char>(64);
+    for (int j = 0; j < kKeyWords; ++j) {
+      sz.add<u64>(slot_cap);
+      sz.add<u64>(cap);
+      sz.add<u64>(cap);
+      sz.add<u64>(cap);
+    }
+    sz.add<u32>(compat ? cap_lines : 1);
+    for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
+    sz.add<u32>(cap);
+    sz.add<OutRecord>(cap);
+    sz.add<KeyCount>(cap);
+    sz.add<PackedKey>(kMaxSamples);
+    sz.add<PackedKey>(kMaxRanks);
+    sz.add<u64>(kMaxRanks + 1);
+    sz.add<u64>(1);
+    sz.add<char>(sync_bytes);
+    sz.add<u32>(rx_zero_words);
+    sz.add<SortPlan>(1);
+    for (int b = 0; b < 2; ++b) {
+      sz.add<u64>(cap);
+      sz.add<u32>(cap);
+    }
+    arena.size = sz.bytes + 4096;
+    LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
+
+    d_text = arena.take<char>(cap_bytes + 64);
+    d_nl = arena.take<u64>(cap_lines + 1);
+    d_delims = arena.take<char>(64);
+    for (int j = 0; j < kKeyWords; ++j) {
+      slots.w[j] = arena.take<u64>(slot_cap);
+      tokens.w[j] = arena.take<u64>(cap);
+      sorted.w[j] = arena.take<u64>(cap);
+      heads.w[j] = arena.take<u64>(cap);
+    }
+    d_line_counts = arena.take<u32>(compat ? cap_lines : 1);
+    d_counts = arena.take<u64>(cap);
+    d_sorted_counts = arena.take<u64>(cap);
+    d_prefix = arena.take<u64>(cap);
+    d_head_val = arena.take<u64>(cap);
+    d_head_count = arena.take<u64>(cap);
+    d_perm = arena.take<u32>(cap);
+    d_out = arena.take<OutRecord>(cap);
+    d_records = arena.take<KeyCount>(cap);
+    d_samples = arena.take<PackedKey>(kMaxSamples);
+    d_splitters = arena.take<PackedKey>(kMaxRanks);
+    d_offsets = arena.take<u64>(kMaxRanks + 1);
+    d_offset = arena.take<u64>(1);
+
+    // sync block: [MapCounters | tile counters | status regions]
+    d_sync = arena.take<char>(sync_bytes);
+    d_ctr = reinterpret_cast<MapCounters*>(d_sync);
+    u32* counters = reinterpret_cast<u32*>(d_sync + 128);
+    u64* st = reinterpret_cast<u64*>(d_sync + 256);
+    lb_line = {st, counters + 0};
+    st += t_line;
+    lb_compact = {st, counters + 1};
+    st += t_compact;
+    lb_map = {st, counters + 2};
+    st += t_map;
+    lb_heads = {st, counters + 3};
+    st += t_heads;
+    lb_scan = {st, counters + 4};
+
+    rx.cap = cap;
+    rx.hist = arena.take<u32>(rx_zero_words);
+    rx.tile_counters = rx.hist + (u64)kNumPositions * 256;
+    rx.status = rx.tile_counters + kNumPositions;
+    rx.plan = arena.take<SortPlan>(1);
+    for (int b = 0; b < 2; ++b) {
+      rx.keys[b] = arena.take<u64>(cap);
+      rx.vals[b] = arena.take<u32>(cap);
+    }
+
+    char delim_buf[64] = {0};
+    LOCUST_CHECK_ARG(cfg.delimiters.size() < sizeof(delim_buf), "too many delimiters");
+    std::memcpy(delim_buf, cfg.delimiters.data(), cfg.delimiters.size());
+    LOCUST_HIP_CHECK(hipMemcpy(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice));
+
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, cap * sizeof(OutRecord), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, cap * kKeyWords * sizeof(u64), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
+    std::memset(h_ctr, 0, sizeof(MapCounters));
+  }
+
+  ~DevicePipeline() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (arena.base) (void)hipFree(arena.base);
+    for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_out, (void*)h_keys,
+                    (void*)h_small, (void*)h_u64})
+      if (p) (void)hipHostFree(p);
+  }
+
+  void check_input(const TextInput& in) const {
+    if (in.bytes > cap_bytes || in.num_lines > cap_lines)
+      throw Error("input (" + std::to_string(in.bytes) + " B, " + std::to_string(in.num_lines) +
+                  " lines) exceeds engine capacity (" + std::to_string(cap_bytes) + " B, " +
+                  std::to_string(cap_lines) + " lines)");
+  }
+
+  void sync() { LOCUST_HIP_CHECK(hipStreamSynchronize(stream)); }
+
+  // H2D of the text; zero counters and look-back scratch.
+  void enqueue_upload(const TextInput& in) {
+    if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
+    std::memset(h_text + in.bytes, 0, 16);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+  }
+
+  void enqueue_map(const TextInput& in) {
+    if (cfg.map_path == MapPath::kCompat) {
+      launch_line_index(d_text, in.bytes, d_nl, d_ctr, lb_line, stream);
+      launch_map_compat(d_text, in.bytes, d_nl, (u32)in.num_lines, d_delims, cfg.emits_per_line,
+                        cfg.max_key_len, slots, d_line_counts, d_ctr, stream);
+    } else {
+      launch_map_fast(d_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
+                      cfg.emits_per_line, cfg.max_key_len, tokens, cap, d_ctr, lb_map, stream);
+    }
+  }
+
+  // Compaction (compat path) + radix sort of `tokens` into `sorted` (and counts).
+  void enqueue_process(u32 num_lines, bool compat, bool with_counts) {
+    if (compat)
+      launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
+                           lb_compact, stream);
+    radix_sort_prepare(tokens, &d_ctr->num_records, rx, stream);
+    const SortPlan* hp = nullptr;
+    if (cfg.sync_plan) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(h_plan, rx.plan, offsetof(SortPlan, digit_offset),
+                                      hipMemcpyDeviceToHost, stream));
+      sync();
+      hp = h_plan;
+    }
+    radix_sort_run(tokens, &d_ctr->num_records, rx, hp, stream);
+    launch_gather_sorted(tokens, rx, sorted, d_perm, with_counts ? d_counts : nullptr,
+                         with_counts ? d_sorted_counts : nullptr, hp ? hp->n : cap, stream);
+  }
+
+  // Head mark + compaction + adjacent difference over `sorted` (weighted when counts).
+  void enqueue_reduce_core(bool with_counts) {
+    const u64* prefix = nullptr;
+    if (with_counts) {
+      launch_scan_counts(d_sorted_counts, cap, d_prefix, d_ctr, lb_scan, stream);
+      prefix = d_prefix;
+    }
+    launch_mark_compact_heads(sorted, prefix, cap, cfg.reduce_path, heads, d_head_val, d_ctr,
+                              lb_heads, stream);
+    launch_adjacent_diff(d_head_val, cap, cfg.reduce_path, d_head_count, d_ctr, stream);
+  }
+
+  void enqueue_pack_output() {
+    launch_pack_output(heads, d_head_val, d_head_count, cap, d_ctr, d_out, stream);
+  }
+
+  void read_counters() {
+    LOCUST_HIP_CHECK(
+        hipMemcpyAsync(h_ctr, d_ctr, sizeof(MapCounters), hipMemcpyDeviceToHost, stream));
+    sync();
+  }
+
+  void download_output(WordCountResult& r, hipEvent_t done) {
+    read_counters();
+    const u64 u = h_ctr->num_unique;
+    if (u)
+      LOCUST_HIP_CHECK(
+          hipMemcpyAsync(h_out, d_out, u * sizeof(OutRecord), hipMemcpyDeviceToHost, stream));
+    if (done) LOCUST_HIP_CHECK(hipEventRecord(done, stream));
+    sync();
+    fill_counters(r);
+    r.entries.resize(u);
+    for (u64 j = 0; j < u; ++j) {
+      for (int w = 0; w < kKeyWords; ++w) r.entries[j].key.w[w] = h_out[j].w[w];
+      r.entries[j].val = h_out[j].val;
+      r.entries[j].count = h_out[j].count;
+    }
+  }
+
+  void fill_counters(WordCountResult& r) const {
+    r.num_tokens = h_ctr->total_count ? h_ctr->total_count : h_ctr->num_records;
+    r.num_unique = h_ctr->num_unique;
+    r.overflow_lines = h_ctr->overflow_lines;
+    r.truncated = h_ctr->truncated;
+    r.max_key_len = h_ctr->max_key_len;
+  }
+
+  static double ms_between(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    LOCUST_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+  }
+
+  WordCountResult run(const TextInput& in) {
+    check_input(in);
+    WordCountResult r;
+    r.num_lines = in.num_lines;
+    const u64 t0 = now_ns();
+    const bool compat = cfg.map_path == MapPath::kCompat;
+    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+    enqueue_upload(in);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+    enqueue_map(in);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+    enqueue_process((u32)in.num_lines, compat, false);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+    enqueue_reduce_core(false);
+    enqueue_pack_output();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+    download_output(r, ev[5]);
+    r.times.wall_ms = (now_ns() - t0) * 1e-6;
+    r.times.h2d_ms = ms_between(ev[0], ev[1]);
+    r.times.map_ms = ms_between(ev[1], ev[2]);
+    r.times.process_ms = ms_between(ev[2], ev[3]);
+    r.times.reduce_ms = ms_between(ev[3], ev[4]);
+    r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    if (cfg.check) validate_result(r);
+    return r;
+  }
+
+  void download_keys(const KeysSoA& src, u64 n, std::vector<PackedKey>* out) {
+    out->resize(n);
+    if (!n) return;
+    for (int w = 0; w < kKeyWords; ++w)
+      LOCUST_HIP_CHECK(hipMemcpyAsync(h_keys + (u64)w * n, src.w[w], n * sizeof(u64),
+                                      hipMemcpyDeviceToHost, stream));
+    sync();
+    for (u64 i = 0; i < n; ++i)
+      for (int w = 0; w < kKeyWords; ++w) (*out)[i].w[w] = h_keys[(u64)w * n + i];
+  }
+
+  void set_num_records(u64 n) {
+    LOCUST_CHECK_ARG(n <= cap, "too many records for engine capacity");
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+    h_u64[0] = n;  // little endian: low 32 bits == num_records
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_records, h_u64, sizeof(u32),
+                                    hipMemcpyHostToDevice, stream));
+  }
+
+  void upload_tokens(const PackedKey* keys, u64 n) {
+    set_num_records(n);
+    for (u64 i = 0; i < n; ++i)
+      for (int w = 0; w < kKeyWords; ++w) h_keys[(u64)w * n + i] = keys[i].w[w];
+    if (n)
+      for (int w = 0; w < kKeyWords; ++w)
+        LOCUST_HIP_CHECK(hipMemcpyAsync(tokens.w[w], h_keys + (u64)w * n, n * sizeof(u64),
+                                        hipMemcpyHostToDevice, stream));
+  }
+};
+
+}  // namespace
+
+// =====================================================================================
+// GpuWordCount
+// =====================================================================================
+struct GpuWordCount::Impl : DevicePipeline {
+  using DevicePipeline::DevicePipeline;
+};
+
+GpuWordCount::GpuWordCount(const JobConfig& cfg, u64 max_text_bytes, u64 max_lines)
+    : impl_(new Impl(cfg, max_text_bytes, max_lines)) {}
+GpuWordCount::~GpuWordCount() = default;
+
+const JobConfig& GpuWordCount::config() const { return impl_->cfg; }
+u64 GpuWordCount::token_capacity() const { return impl_->cap; }
+
+WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); }
+
+std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCountResult* stats) {
+  Impl& m = *impl_;
+  m.check_input(in);
+  m.enqueue_upload(in);
+  m.enqueue_map(in);
+  m.enqueue_process((u32)in.num_lines, m.cfg.map_path == MapPath::kCompat, false);
+  m.read_counters();
+  std::vector<PackedKey> out;
+  m.download_keys(m.sorted, m.h_ctr->num_records, &out);
+  if (stats) {
+    stats->num_lines = in.num_lines;
+    m.fill_counters(*stats);
+  }
+  return out;
+}
+
+WordCountResult GpuWordCount::run_reduce_stage(const PackedKey* keys, u64 n) {
+  Impl& m = *impl_;
+  WordCountResult r;
+  const u64 t0 = now_ns();
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[0], m.stream));
+  m.upload_tokens(keys, n);
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[1], m.stream));
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[2], m.stream));
+  m.enqueue_process(0, false, false);  // B7 fix: the reducer always sorts its input
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[3], m.stream));
+  m.enqueue_reduce_core(false);
+  m.enqueue_pack_output();
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[4], m.stream));
+  m.download_output(r, m.ev[5]);
+  r.times.wall_ms = (now_ns() - t0) * 1e-6;
+  r.times.h2d_ms = DevicePipeline::ms_between(m.ev[0], m.ev[1]);
+  r.times.process_ms = DevicePipeline::ms_between(m.ev[2], m.ev[3]);
+  r.times.reduce_ms = DevicePipeline::ms_between(m.ev[3], m.ev[4]);
+  r.times.d2h_ms = DevicePipeline::ms_between(m.ev[4], m.ev[5]);
+  if (m.cfg.check) validate_result(r);
+  return r;
+}
+
+std::vector<u32> GpuWordCount::sort_keys(const PackedKey* keys, u64 n,
+                                         std::vector<PackedKey>* sorted) {
+  Impl& m = *impl_;
+  m.upload_tokens(keys, n);
+  m.enqueue_process(0, false, false);
+  std::vector<u32> perm(n);
+  if (n)
+    LOCUST_HIP_CHECK(hipMemcpyAsync(perm.data(), m.d_perm, n * sizeof(u32),
+                                    hipMemcpyDeviceToHost, m.stream));
+  m.sync();
+  if (sorted) m.download_keys(m.sorted, n, sorted);
+  return perm;
+}
+
+// =====================================================================================
+// GPU shard engine (one rank of the distributed job)
+// =====================================================================================
+namespace {
+
+class GpuShardEngine final : public ShardEngine {
+ public:
+  GpuShardEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
+      : cfg_(cfg), mp_(new DevicePipeline(cfg, max_bytes, max_lines)) {}
+
+  bool device_buffers() const override { return true; }
+  void* stream() override { return mp_->stream; }
+
+  u64 map_local(const TextInput& shard, bool combine) override {
+    DevicePipeline& m = *mp_;
+    m.check_input(shard);
+    m.enqueue_upload(shard);
+    m.enqueue_map(shard);
+    m.enqueue_process((u32)shard.num_lines, cfg_.map_path == MapPath::kCompat, false);
+    combine_ = combine;
+    if (combine) {
+      // Map-side combine: local (key, count) runs become the shuffle records.
+      m.enqueue_reduce_core(false);
+      launch_pack_records(m.heads, m.d_head_count, &m.d_ctr->num_unique, m.cap, m.d_records,
+                          m.stream);
+    } else {
+      launch_pack_records(m.sorted, nullptr, &m.d_ctr->num_records, m.cap, m.d_records, m.stream);
+    }
+    m.read_counters();
+    local_stats_ = WordCountResult();
+    local_stats_.num_lines = shard.num_lines;
+    m.fill_counters(local_stats_);
+    local_stats_.num_tokens = m.h_ctr->num_records;
+    return combine ? m.h_ctr->num_unique : m.h_ctr->num_records;
+  }
+
+  std::vector<PackedKey> sample(u32 s) override {
+    DevicePipeline& m = *mp_;
+    LOCUST_CHECK_ARG(s <= kMaxSamples, "too many samples");
+    launch_sample_keys(local_keys(), local_n(), s, m.d_samples, m.stream);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, s * sizeof(PackedKey),
+                                    hipMemcpyDeviceToHost, m.stream));
+    m.sync();
+    return std::vector<PackedKey>(m.h_small, m.h_small + s);
+  }
+
+  std::vector<u64> bucket_offsets(const std::vector<PackedKey>& splitters) override {
+    DevicePipeline& m = *mp_;
+    const u32 P = (u32)splitters.size() + 1;
+    LOCUST_CHECK_ARG(P <= kMaxRanks, "too many ranks");
+    if (!splitters.empty()) {
+      std::memcpy(m.h_small, splitters.data(), splitters.size() * sizeof(PackedKey));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.d_splitters, m.h_small,
+                                      splitters.size() * sizeof(PackedKey), hipMemcpyHostToDevice,
+                                      m.stream));
+    }
+    launch_bucket_offsets(local_keys(), local_n(), m.d_splitters, P, m.d_offsets, m.stream);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_u64, m.d_offsets, (P + 1) * sizeof(u64),
+                                    hipMemcpyDeviceToHost, m.stream));
+    m.sync();
+    return std::vector<u64>(m.h_u64, m.h_u64 + P + 1);
+  }
+
+  const void* send_records() override { return mp_->d_records; }
+
+  void* recv_records(u64 n) override {
+    if (!rp_ || rp_->cap < n) {
+      const u64 want = std::max<u64>(std::max<u64>(n + n / 4, 4096), rp_ ? rp_->cap * 2 : 0);
+      rp_.reset();
+      rp_.reset(new DevicePipeline(cfg_, 1, 1, want));
+    }
+    return rp_->d_records;
+  }
+
+  void reduce_received(u64 n, u64* total_count, u64* num_unique) override {
+    DevicePipeline& r = *rp_;
+    // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
+    r.set_num_records(n);
+    launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.stream);
+    r.enqueue_process(0, false, true);
+    r.enqueue_reduce_core(true);
+    r.read_counters();
+    *total_count = r.h_ctr->total_count;
+    *num_unique = r.h_ctr->num_unique;
+  }
+
+  void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
+    DevicePipeline& r = *rp_;
+    r.h_u64[0] = global_offset;
+    LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_offset, r.h_u64, sizeof(u64), hipMemcpyHostToDevice, r.stream));
+    launch_add_offset(r.d_head_val, r.cap, r.d_offset, r.d_ctr, r.stream);
+    r.enqueue_pack_output();
+    WordCountResult tmp;
+    r.download_output(tmp, nullptr);
+    *out = std::move(tmp.entries);
+  }
+
+  void map_stats(WordCountResult* r) override { *r = local_stats_; }
+
+ private:
+  ConstKeysSoA local_keys() const { return combine_ ? mp_->heads : mp_->sorted; }
+  const u32* local_n() const {
+    return combine_ ? &mp_->d_ctr->num_unique : &mp_->d_ctr->num_records;
+  }
+
+  JobConfig cfg_;
+  std::unique_ptr<DevicePipeline> mp_, rp_;
+  bool combine_ = false;
+  WordCountResult local_stats_;
+};
+
+}  // namespace
+
+std::unique_ptr<ShardEngine> make_gpu_shard_engine(const JobConfig& cfg, u64 max_bytes,
+                                                   u64 max_lines) {
+  return std::unique_ptr<ShardEngine>(new GpuShardEngine(cfg, max_bytes, max_lines));
+}
+
+}  // namespace locust

@@ -1,0 +1,56 @@
+// Runtime job configuration.
+//
+// The reference fixes everything at compile time (/root/reference/MapReduce/src/
+// main.cu:18-37: MAX_LINES_FILE_READ=5800, EMITS_PER_LINE=20, GPU_IMPLEMENTATION,
+// SHARE_MEMORY, GRID_SIZE=128, BLOCK_SIZE=256).  Here every switch is a runtime field of
+// JobConfig (CLI flags and LOCUST_* env vars map onto it) and there is no
+// line cap: buffers are sized from the input.
+#pragma once
+
+#include <string>
+
+#include "locust/dstring.hpp"
+
+namespace locust {
+
+enum class Backend { kGpu, kCpu };
+
+// Reduce-stage boundary/adjacent-difference kernels: LDS-staged tiles (the reference's
+// SHARE_MEMORY=1 column of README.md:84-88) or plain global loads (SHARE_MEMORY=0).
+enum class ReducePath { kLds, kGlobal };
+
+// Map kernel: kCompat = one thread per line running device strtok_r into fixed
+// [line*E + k] slots (reference layout, main.cu:136-159) followed by a scan-based
+// compaction; kFast = wave-cooperative byte-parallel tokenizer that emits compacted
+// tokens in one pass (decoupled look-back).
+enum class MapPath { kCompat, kFast };
+
+// Process-stage key sort: kRadix = LSD radix sort of packed keys (8-bit digits, constant
+// digit positions skipped); kDict = dictionary sort: hash the keys into a GPU table,
+// radix-sort only the unique keys, counting-sort the tokens by unique rank.
+enum class SortPath { kRadix, kDict };
+
+struct JobConfig {
+  Backend backend = Backend::kGpu;
+  int device = 0;
+  int emits_per_line = 20;                   // EMITS_PER_LINE (main.cu:19)
+  int max_key_len = kMaxKeyLen;              // longer tokens are truncated and counted
+  std::string delimiters = kDefaultDelims;   // main.cu:138
+  bool ref_compat = false;                   // reproduce B1: whole-file load drops last line
+  ReducePath reduce_path = ReducePath::kLds;
+  MapPath map_path = MapPath::kFast;
+  SortPath sort_path = SortPath::kRadix;
+  bool combine = false;                      // map-side combine (distributed shuffle)
+  bool check = false;                        // LOCUST_CHECK invariants after each stage
+  bool sync_plan = true;                     // read the sort plan back: launch only live passes
+};
+
+// Fills the fields that have LOCUST_* environment overrides (LOCUST_CHECK=1,
+// LOCUST_REDUCE_PATH=lds|global, LOCUST_MAP_PATH=compat|fast, LOCUST_SORT=radix|dict).
+void apply_env_overrides(JobConfig& cfg);
+
+const char* to_string(ReducePath p);
+const char* to_string(MapPath p);
+const char* to_string(SortPath p);
+
+}  // namespace locust

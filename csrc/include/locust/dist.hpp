@@ -1,0 +1,130 @@
+// Distributed (multi-GPU / multi-process) WordCount.
+//
+// Replaces the reference's distribution layer: a TCP
+// "slave" that runs shell commands (/root/reference/Distributor/slave.py:1-38), a missing
+// master, and a shuffle that is a local file (/tmp/out.txt, main.cu:428-441) with the
+// network hop missing.  Here every rank (one process or thread per GPU) runs:
+//
+//   map_local      tokenize its byte-range shard, sort, optionally combine (sum counts)
+//   sample         S evenly spaced local keys -> allgather -> P-1 splitters (sample sort)
+//   partition      lower_bound of each splitter in the sorted local records
+//   shuffle        all-to-all of bucket sizes, then ONE all-to-all-v of 40-B KeyCount
+//                  records (RCCL grouped send/recv over xGMI: every link busy at once)
+//   reduce         sort received records, weighted head-mark + adjacent difference
+//   offsets        allgather of per-rank token totals -> global `val` = exclusive prefix
+//   gather         rank 0 receives every rank's entries in rank order (== key order)
+//
+// Output is byte-identical to the single-GPU run, including the global `val` indices.
+// Every stage boundary runs an agreement collective on a status word, so a rank that
+// fails (or is told to fail via LOCUST_FAULT) turns into a clean error on all ranks.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "locust/engine.hpp"
+
+namespace locust {
+
+class Communicator {
+ public:
+  virtual ~Communicator() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual const char* name() const = 0;
+  // true: data-plane buffers are device pointers (RCCL, GPU loopback).
+  virtual bool device_buffers() const = 0;
+
+  // ---- control plane: host buffers, blocking ----
+  // recv gets size() * bytes, rank r's contribution at offset r * bytes.
+  virtual void allgather_host(const void* send, void* recv, u64 bytes) = 0;
+  // Rank `root` receives every rank's variable-length blob, concatenated in rank order.
+  virtual void gatherv_host(const void* send, u64 bytes, std::vector<char>* recv_at_root,
+                            std::vector<u64>* sizes_at_root, int root) = 0;
+  virtual void barrier() = 0;
+
+  // ---- data plane: engine buffers, byte counts/offsets per peer (host arrays) ----
+  // Blocking: returns when this rank's receives are complete and its sends may be reused.
+  virtual void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
+                         const u64* recv_bytes, const u64* recv_off, void* stream) = 0;
+
+  // Status agreement: every rank contributes `local_error` (0 = ok); returns the lowest
+  // failing rank or -1.  One allgather of 4 bytes per rank.
+  int agree(int local_error);
+};
+
+// Star-topology TCP communicator (rank 0 relays).  Control plane for everything and the
+// data plane of the CPU backend; also the bootstrap channel for RCCL unique ids.
+std::unique_ptr<Communicator> make_tcp_comm(int rank, int world, const std::string& host, int port,
+                                            double timeout_s = 120.0);
+// RCCL communicator for one GPU per rank; bootstraps its ncclUniqueId over TCP.
+std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
+                                             const std::string& host, int port,
+                                             double timeout_s = 300.0);
+
+// N virtual ranks inside one process (threads).  With device buffers the all-to-all is
+// done with hipMemcpyAsync between the ranks' buffers, so a single GPU can rehearse the
+// 2/4/8-rank shuffle (RCCL refuses two ranks on one device).
+class LoopbackGroup {
+ public:
+  LoopbackGroup(int world, bool device_buffers);
+  ~LoopbackGroup();
+  std::unique_ptr<Communicator> comm(int rank);
+  struct State;
+
+ private:
+  std::shared_ptr<State> state_;
+};
+
+// Per-rank local engine used by the distributed driver.
+class ShardEngine {
+ public:
+  virtual ~ShardEngine() = default;
+  virtual bool device_buffers() const = 0;
+  virtual void* stream() = 0;
+  // Map + sort (+ combine) this rank's shard.  Returns the number of local records.
+  virtual u64 map_local(const TextInput& shard, bool combine) = 0;
+  virtual std::vector<PackedKey> sample(u32 num_samples) = 0;
+  // Record offsets [0 .. P] of the P buckets defined by P-1 sorted splitters.
+  virtual std::vector<u64> bucket_offsets(const std::vector<PackedKey>& splitters) = 0;
+  virtual const void* send_records() = 0;      // KeyCount[num local records], sorted
+  virtual void* recv_records(u64 n) = 0;       // room for n incoming KeyCount records
+  // Sort + weighted reduce of the n received records; returns {total_count, num_unique}.
+  virtual void reduce_received(u64 n, u64* total_count, u64* num_unique) = 0;
+  virtual void finalize(u64 global_offset, std::vector<WordCountEntry>* out) = 0;
+  // Map-stage counters of the last map_local.
+  virtual void map_stats(WordCountResult* r) = 0;
+};
+
+std::unique_ptr<ShardEngine> make_gpu_shard_engine(const JobConfig& cfg, u64 max_bytes,
+                                                   u64 max_lines);
+std::unique_ptr<ShardEngine> make_cpu_shard_engine(const JobConfig& cfg);
+
+struct DistConfig {
+  JobConfig job;
+  int world = 1;
+  u32 samples_per_rank = 64;
+  bool gather = true;   // rank 0 receives the whole output
+};
+
+struct DistResult {
+  WordCountResult result;  // rank 0 (gather=true): global output; otherwise this rank's range
+  double map_ms = 0, shuffle_ms = 0, reduce_ms = 0, gather_ms = 0, total_ms = 0;
+  u64 local_records = 0;   // records this rank sent into the shuffle
+  u64 sent_bytes = 0, recv_bytes = 0;
+  u64 range_tokens = 0, range_unique = 0;  // this rank's key range after the shuffle
+};
+
+DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
+                           const TextInput& shard);
+
+// Split a line-aligned text into `parts` line-aligned shards of ~equal bytes.
+std::vector<TextInput> shard_text(const TextInput& in, int parts);
+
+// One process drives `cfg.world` ranks (threads) over the visible GPUs (round robin) with
+// the loopback communicator; rank 0's result is returned.  With Backend::kCpu the ranks
+// use the CPU shard engine.
+DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole);
+
+}  // namespace locust

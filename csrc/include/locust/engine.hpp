@@ -1,0 +1,105 @@
+// WordCount engines: the single-GPU HIP pipeline and the CPU reference pipeline.
+//
+// GpuWordCount reproduces the reference's GPU path (/root/reference/
+// MapReduce/src/main.cu:388-487) stage for stage -- Map (tokenize/emit), Process
+// (stream compaction + key sort), Reduce (boundary mark + head compaction + adjacent
+// difference) -- with every buffer preallocated at construction so a run performs no
+// allocation and, apart from reading back result sizes, no host synchronisation.
+// CpuWordCount is the golden oracle and the `--backend cpu` path (main.cu:489-527).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "locust/common.hpp"
+#include "locust/config.hpp"
+#include "locust/kv.hpp"
+
+namespace locust {
+
+// A window of input lines: `bytes` bytes of text, lines separated by '\n' (the last line
+// may lack one).  `first_line` is the global index of the first line (the reference's
+// KeyValuePair.key, main.cu:58).
+struct TextInput {
+  const char* data = nullptr;
+  u64 bytes = 0;
+  u64 num_lines = 0;
+  u64 first_line = 0;
+};
+
+struct StageTimes {
+  // Honest device time from hipEvents on the compute stream (ms).
+  double h2d_ms = 0, map_ms = 0, process_ms = 0, reduce_ms = 0, d2h_ms = 0;
+  // Host wall clock of the whole run() call (ms).
+  double wall_ms = 0;
+  // Host timers placed where the reference placed them (launch-only map etc., BASELINE.md
+  // "How the reference measured these"), filled when JobConfig.ref_timers is set.
+  double ref_map_ms = 0, ref_process_ms = 0, ref_reduce_ms = 0;
+};
+
+// One output entry: a unique key, the start index of its run in the globally sorted
+// token array (the reference's `val`) and the run length (`count`).
+struct WordCountEntry {
+  PackedKey key;
+  u64 val;
+  u64 count;
+};
+
+struct WordCountResult {
+  std::vector<WordCountEntry> entries;  // sorted by key
+  u64 num_lines = 0;
+  u64 num_tokens = 0;       // kv_num_map
+  u64 num_unique = 0;       // kv_num_reduce
+  u64 overflow_lines = 0;   // lines that printed "WARN: Exceeded emit limit"
+  u64 truncated = 0;        // tokens longer than max_key_len
+  u64 max_key_len = 0;
+  StageTimes times;
+};
+
+class GpuWordCount {
+ public:
+  // Capacity is fixed at construction: inputs up to max_text_bytes / max_lines.
+  GpuWordCount(const JobConfig& cfg, u64 max_text_bytes, u64 max_lines);
+  ~GpuWordCount();
+  GpuWordCount(const GpuWordCount&) = delete;
+  GpuWordCount& operator=(const GpuWordCount&) = delete;
+
+  WordCountResult run(const TextInput& in);
+
+  // Stage split: map + process only, returning the sorted tokens of
+  // this input; and reduce-only over (possibly unsorted) tokens.
+  std::vector<PackedKey> run_map_stage(const TextInput& in, WordCountResult* stats);
+  WordCountResult run_reduce_stage(const PackedKey* keys, u64 n);
+
+  // Sort arbitrary packed keys on the device (used by tests and the shuffle receiver).
+  std::vector<u32> sort_keys(const PackedKey* keys, u64 n, std::vector<PackedKey>* sorted);
+
+  const JobConfig& config() const;
+  u64 token_capacity() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
+class CpuWordCount {
+ public:
+  explicit CpuWordCount(const JobConfig& cfg);
+  WordCountResult run(const TextInput& in);
+  std::vector<PackedKey> run_map_stage(const TextInput& in, WordCountResult* stats);
+  WordCountResult run_reduce_stage(const PackedKey* keys, u64 n);
+
+ private:
+  JobConfig cfg_;
+};
+
+// Tokenize one line with the reference rules (delimiters, emit cap, truncation).  Used by
+// the CPU engine and the tests; returns the number of tokens dropped by the emit cap.
+int tokenize_line(const char* line, u64 len, const JobConfig& cfg, std::vector<PackedKey>* out,
+                  u64* truncated);
+
+// Sorted unique keys + counts -> entries with val = exclusive prefix of counts.
+void entries_from_sorted_tokens(const PackedKey* sorted, u64 n, std::vector<WordCountEntry>* out);
+
+}  // namespace locust

@@ -1,0 +1,53 @@
+// Host I/O: input loader with line windows, intermediate spill files, output printer.
+//
+// Reference (/root/reference/MapReduce/src/main.cu:40-134):
+//   loadFile             getline loop into a fixed 5,800-slot stack array; whole-file mode
+//                        drops the last line (B1); window [line_start, line_end).
+//   writeKeyIntValues    "%s \t%d\n" per non-empty record -> /tmp/out.txt
+//   loadIntermediateFile split at the first TAB (key keeps the trailing space, B8)
+//   printKeyIntValues    "print key: %s \t val: %d \t count: %d\n"
+#pragma once
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "locust/engine.hpp"
+
+namespace locust {
+
+struct LoadedText {
+  std::vector<char> storage;  // the selected lines, '\n'-separated
+  TextInput input;            // points into storage
+  u64 file_lines = 0;         // lines in the whole file
+  bool window = false;        // a [line_start, line_end) window was requested
+};
+
+// line_start < 0 selects the whole file.  With ref_compat the reference's line-count
+// quirks are reproduced (B1: the whole-file load and a window running past EOF lose the
+// last line).
+LoadedText load_lines(const std::string& path, i64 line_start, i64 line_end, bool ref_compat);
+LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
+                            bool ref_compat);
+u64 count_lines(const char* data, u64 bytes);
+
+// ---- spill files (map-output checkpoint) ----
+enum class SpillFormat { kText, kBinary };
+// Text: the reference's "%s \t%d\n" (one line per record).  Binary: 32-byte header
+// ("LCSTSPL1", version, key words, record count) then 40-B KeyCount records.
+void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt);
+// Reads either format (detected by magic).  Text keys lose the writer's trailing space.
+std::vector<KeyCount> read_spill(const std::string& path);
+std::vector<KeyCount> tokens_to_records(const std::vector<PackedKey>& toks);
+std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs);
+
+// ---- output ----
+// GPU build format (main.cu:132): "print key: %s \t val: %d \t count: %d\n".
+void format_gpu_output(const std::vector<WordCountEntry>& e, std::string* out);
+// CPU build format (main.cu:286): "print key: %s \t value: %s\n" with value = count.
+void format_cpu_output(const std::vector<WordCountEntry>& e, std::string* out);
+void write_all(std::FILE* f, const std::string& s);
+
+std::string key_to_string(const PackedKey& k);
+
+}  // namespace locust

@@ -1,0 +1,229 @@
+#include "locust/io.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+namespace locust {
+
+u64 count_lines(const char* data, u64 bytes) {
+  u64 n = 0;
+  const char* p = data;
+  const char* end = data + bytes;
+  while (p < end) {
+    const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+    ++n;
+    p = nl ? nl + 1 : end;
+  }
+  return n;
+}
+
+LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
+                            bool ref_compat) {
+  LoadedText lt;
+  lt.window = line_start >= 0;
+  // Byte offset of every line start (one pass, memchr speed).
+  std::vector<u64> starts;
+  {
+    const char* p = data;
+    const char* end = data + bytes;
+    while (p < end) {
+      starts.push_back((u64)(p - data));
+      const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+      p = nl ? nl + 1 : end;
+    }
+  }
+  const u64 total = starts.size();
+  lt.file_lines = total;
+  u64 first = 0, last = total;  // [first, last)
+  if (line_start >= 0) {
+    first = std::min<u64>((u64)line_start, total);
+    last = line_end < 0 ? total : std::min<u64>(std::max<i64>(line_end, line_start), total);
+    // Reference quirk (main.cu:62-63): a window that reaches EOF reports
+    // line_num - line_start lines, i.e. loses the last line.
+    if (ref_compat && line_end >= 0 && (u64)line_end >= total && last > first) --last;
+  } else if (ref_compat && total > 0) {
+    last = total - 1;  // B1: whole-file mode drops the last line
+  }
+  const u64 b0 = first < total ? starts[first] : bytes;
+  const u64 b1 = last < total ? starts[last] : bytes;
+  lt.storage.assign(data + b0, data + b1);
+  lt.storage.reserve(lt.storage.size() + 64);
+  lt.input.data = lt.storage.data();
+  lt.input.bytes = lt.storage.size();
+  lt.input.num_lines = last > first ? last - first : 0;
+  lt.input.first_line = first;
+  return lt;
+}
+
+LoadedText load_lines(const std::string& path, i64 line_start, i64 line_end, bool ref_compat) {
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw Error("cannot open input file: " + path);
+  std::fseek(f, 0, SEEK_END);
+  long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  std::vector<char> buf((size_t)std::max<long>(sz, 0));
+  if (sz > 0 && std::fread(buf.data(), 1, (size_t)sz, f) != (size_t)sz) {
+    std::fclose(f);
+    throw Error("short read: " + path);
+  }
+  std::fclose(f);
+  return text_from_buffer(buf.data(), buf.size(), line_start, line_end, ref_compat);
+}
+
+std::string key_to_string(const PackedKey& k) {
+  char buf[kKeyBytes + 1];
+  int n = unpack_key(k.w, buf);
+  return std::string(buf, (size_t)n);
+}
+
+// ---------------- spill ----------------
+namespace {
+constexpr char kMagic[8] = {'L', 'C', 'S', 'T', 'S', 'P', 'L', '1'};
+struct SpillHeader {
+  char magic[8];
+  u32 version;
+  u32 key_words;
+  u64 count;
+  u64 reserved;
+};
+static_assert(sizeof(SpillHeader) == 32, "spill header 32 B");
+
+void append_u64(std::string* s, u64 v) {
+  char tmp[24];
+  int n = 0;
+  do {
+    tmp[n++] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  while (n) s->push_back(tmp[--n]);
+}
+}  // namespace
+
+void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt) {
+  std::FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw Error("cannot write spill file: " + path);
+  if (fmt == SpillFormat::kBinary) {
+    SpillHeader h{};
+    std::memcpy(h.magic, kMagic, 8);
+    h.version = 1;
+    h.key_words = kKeyWords;
+    h.count = recs.size();
+    std::fwrite(&h, sizeof(h), 1, f);
+    if (!recs.empty()) std::fwrite(recs.data(), sizeof(KeyCount), recs.size(), f);
+  } else {
+    std::string s;
+    s.reserve(recs.size() * 12);
+    char buf[kKeyBytes + 1];
+    for (const auto& r : recs) {
+      int n = unpack_key(r.w, buf);
+      if (n == 0) continue;  // the reference skips empty keys (main.cu:118)
+      s.append(buf, (size_t)n);
+      s.append(" \t");
+      append_u64(&s, r.count);
+      s.push_back('\n');
+    }
+    write_all(f, s);
+  }
+  if (std::fclose(f) != 0) throw Error("error closing spill file: " + path);
+}
+
+std::vector<KeyCount> read_spill(const std::string& path) {
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw Error("cannot open spill file: " + path);
+  std::fseek(f, 0, SEEK_END);
+  long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  std::string data((size_t)std::max<long>(sz, 0), '\0');
+  if (sz > 0 && std::fread(&data[0], 1, (size_t)sz, f) != (size_t)sz) {
+    std::fclose(f);
+    throw Error("short read: " + path);
+  }
+  std::fclose(f);
+  std::vector<KeyCount> recs;
+  if (data.size() >= sizeof(SpillHeader) && std::memcmp(data.data(), kMagic, 8) == 0) {
+    SpillHeader h;
+    std::memcpy(&h, data.data(), sizeof(h));
+    if (h.version != 1 || h.key_words != kKeyWords) throw Error("unsupported spill file: " + path);
+    if (data.size() < sizeof(h) + h.count * sizeof(KeyCount)) throw Error("truncated spill: " + path);
+    recs.resize(h.count);
+    if (h.count) std::memcpy(recs.data(), data.data() + sizeof(h), h.count * sizeof(KeyCount));
+    return recs;
+  }
+  // text format: "<key> \t<count>\n"
+  size_t p = 0;
+  while (p < data.size()) {
+    size_t nl = data.find('\n', p);
+    if (nl == std::string::npos) nl = data.size();
+    std::string line = data.substr(p, nl - p);
+    p = nl + 1;
+    if (line.empty()) continue;
+    size_t tab = line.find('\t');
+    std::string key = tab == std::string::npos ? line : line.substr(0, tab);
+    if (!key.empty() && key.back() == ' ') key.pop_back();  // B8 fix
+    const u64 cnt = tab == std::string::npos ? 1 : std::strtoull(line.c_str() + tab + 1, nullptr, 10);
+    KeyCount r{};
+    pack_key(key.data(), (int)key.size(), r.w);
+    r.count = cnt;
+    recs.push_back(r);
+  }
+  return recs;
+}
+
+std::vector<KeyCount> tokens_to_records(const std::vector<PackedKey>& toks) {
+  std::vector<KeyCount> recs(toks.size());
+  for (size_t i = 0; i < toks.size(); ++i) {
+    for (int w = 0; w < kKeyWords; ++w) recs[i].w[w] = toks[i].w[w];
+    recs[i].count = 1;
+  }
+  return recs;
+}
+
+std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs) {
+  std::vector<PackedKey> toks;
+  toks.reserve(recs.size());
+  for (const auto& r : recs) {
+    PackedKey k;
+    for (int w = 0; w < kKeyWords; ++w) k.w[w] = r.w[w];
+    for (u64 c = 0; c < r.count; ++c) toks.push_back(k);
+  }
+  return toks;
+}
+
+// ---------------- output ----------------
+void format_gpu_output(const std::vector<WordCountEntry>& e, std::string* out) {
+  out->reserve(out->size() + e.size() * 48);
+  char buf[kKeyBytes + 1];
+  for (const auto& x : e) {
+    int n = unpack_key(x.key.w, buf);
+    if (n == 0) continue;
+    out->append("print key: ");
+    out->append(buf, (size_t)n);
+    out->append(" \t val: ");
+    append_u64(out, x.val);
+    out->append(" \t count: ");
+    append_u64(out, x.count);
+    out->push_back('\n');
+  }
+}
+
+void format_cpu_output(const std::vector<WordCountEntry>& e, std::string* out) {
+  out->reserve(out->size() + e.size() * 32);
+  char buf[kKeyBytes + 1];
+  for (const auto& x : e) {
+    int n = unpack_key(x.key.w, buf);
+    if (n == 0) continue;
+    out->append("print key: ");
+    out->append(buf, (size_t)n);
+    out->append(" \t value: ");
+    append_u64(out, x.count);
+    out->push_back('\n');
+  }
+}
+
+void write_all(std::FILE* f, const std::string& s) {
+  if (!s.empty() && std::fwrite(s.data(), 1, s.size(), f) != s.size())
+    throw Error("short write");
+}
+
+}  // namespace locust

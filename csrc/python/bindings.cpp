@@ -1,0 +1,311 @@
+// Python bindings (pybind11) for the native engine: `locust_amd._locust`.
+//
+// The hot path stays in C++/HIP; Python only moves the input bytes in and formatted
+// results out.  The GPU engine is created lazily, so importing the module never touches
+// the HIP runtime (the driver's CPU-only build check imports it on a machine without GPU).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <string>
+
+#include "locust/dist.hpp"
+#include "locust/dstring.hpp"
+#include "locust/engine.hpp"
+#include "locust/io.hpp"
+
+namespace py = pybind11;
+using namespace locust;
+
+namespace {
+
+struct PyResult {
+  WordCountResult r;
+  py::list entries() const {
+    py::list out;
+    for (const auto& e : r.entries)
+      out.append(py::make_tuple(py::bytes(key_to_string(e.key)), e.val, e.count));
+    return out;
+  }
+  py::dict times() const {
+    py::dict d;
+    d["h2d_ms"] = r.times.h2d_ms;
+    d["map_ms"] = r.times.map_ms;
+    d["process_ms"] = r.times.process_ms;
+    d["reduce_ms"] = r.times.reduce_ms;
+    d["d2h_ms"] = r.times.d2h_ms;
+    d["wall_ms"] = r.times.wall_ms;
+    return d;
+  }
+  py::bytes format(bool cpu_format) const {
+    std::string s;
+    (cpu_format ? format_cpu_output : format_gpu_output)(r.entries, &s);
+    return py::bytes(s);
+  }
+};
+
+TextInput as_input(const std::string& text, u64 first_line = 0) {
+  TextInput in;
+  in.data = text.data();
+  in.bytes = text.size();
+  in.num_lines = count_lines(text.data(), text.size());
+  in.first_line = first_line;
+  return in;
+}
+
+PackedKey to_key(const std::string& s) {
+  PackedKey k;
+  pack_key(s.data(), (int)std::min<size_t>(s.size(), kKeyBytes), k.w);
+  return k;
+}
+
+class PyGpuEngine {
+ public:
+  PyGpuEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
+      : eng_(cfg, max_bytes, max_lines) {}
+  PyResult run(const std::string& text) {
+    py::gil_scoped_release nogil;
+    return PyResult{eng_.run(as_input(text))};
+  }
+  std::vector<py::bytes> map_stage(const std::string& text) {
+    std::vector<PackedKey> toks;
+    {
+      py::gil_scoped_release nogil;
+      toks = eng_.run_map_stage(as_input(text), nullptr);
+    }
+    std::vector<py::bytes> out;
+    for (const auto& k : toks) out.emplace_back(key_to_string(k));
+    return out;
+  }
+  PyResult reduce_stage(const std::vector<std::string>& keys) {
+    std::vector<PackedKey> toks;
+    for (const auto& s : keys) toks.push_back(to_key(s));
+    py::gil_scoped_release nogil;
+    return PyResult{eng_.run_reduce_stage(toks.data(), toks.size())};
+  }
+  py::tuple sort_keys(const std::vector<std::string>& keys) {
+    std::vector<PackedKey> toks;
+    for (const auto& s : keys) toks.push_back(to_key(s));
+    std::vector<PackedKey> sorted;
+    std::vector<u32> perm;
+    {
+      py::gil_scoped_release nogil;
+      perm = eng_.sort_keys(toks.data(), toks.size(), &sorted);
+    }
+    std::vector<py::bytes> out;
+    for (const auto& k : sorted) out.emplace_back(key_to_string(k));
+    return py::make_tuple(out, perm);
+  }
+  u64 capacity() const { return eng_.token_capacity(); }
+
+ private:
+  GpuWordCount eng_;
+};
+
+py::list strtok_r_tokens(const std::string& line, const std::string& delims) {
+  std::string buf = line;
+  py::list out;
+  char* save = nullptr;
+  for (char* t = d_strtok_r(&buf[0], delims.c_str(), &save); t;
+       t = d_strtok_r(nullptr, delims.c_str(), &save))
+    out.append(py::bytes(t));
+  return out;
+}
+
+PyResult run_multi(const std::string& text, const DistConfig& cfg) {
+  TextInput in = as_input(text);
+  py::gil_scoped_release nogil;
+  DistResult d = run_single_process_multi_gpu(cfg, in);
+  return PyResult{d.result};
+}
+
+py::dict dist_to_dict(const DistResult& d) {
+  py::dict x;
+  x["map_ms"] = d.map_ms;
+  x["shuffle_ms"] = d.shuffle_ms;
+  x["reduce_ms"] = d.reduce_ms;
+  x["gather_ms"] = d.gather_ms;
+  x["total_ms"] = d.total_ms;
+  x["local_records"] = d.local_records;
+  x["sent_bytes"] = d.sent_bytes;
+  x["recv_bytes"] = d.recv_bytes;
+  x["range_tokens"] = d.range_tokens;
+  x["range_unique"] = d.range_unique;
+  return x;
+}
+
+// A rank of a multi-process job: its communicator and engine live across runs.
+class PyDistRank {
+ public:
+  PyDistRank(const DistConfig& cfg, int rank, const std::string& comm, const std::string& host,
+             int port, u64 max_bytes, u64 max_lines, double timeout_s)
+      : cfg_(cfg) {
+    py::gil_scoped_release nogil;
+    if (comm == "tcp") {
+      comm_ = make_tcp_comm(rank, cfg.world, host, port, timeout_s);
+    } else if (comm == "rccl") {
+      comm_ = make_rccl_comm(rank, cfg.world, cfg.job.device, host, port, timeout_s);
+    } else {
+      throw Error("unknown communicator " + comm);
+    }
+    eng_ = cfg.job.backend == Backend::kGpu ? make_gpu_shard_engine(cfg.job, max_bytes, max_lines)
+                                            : make_cpu_shard_engine(cfg.job);
+  }
+  py::tuple run(const std::string& shard_text_bytes, u64 first_line) {
+    TextInput in = as_input(shard_text_bytes, first_line);
+    DistResult d;
+    {
+      py::gil_scoped_release nogil;
+      d = run_distributed(cfg_, *comm_, *eng_, in);
+    }
+    return py::make_tuple(PyResult{d.result}, dist_to_dict(d));
+  }
+  void barrier() {
+    py::gil_scoped_release nogil;
+    comm_->barrier();
+  }
+  // Max over ranks of a double (timing aggregation for the benchmark).
+  double allreduce_max(double v) {
+    std::vector<double> all((size_t)comm_->size());
+    {
+      py::gil_scoped_release nogil;
+      comm_->allgather_host(&v, all.data(), sizeof(double));
+    }
+    double m = v;
+    for (double x : all) m = std::max(m, x);
+    return m;
+  }
+  int rank() const { return comm_->rank(); }
+  int size() const { return comm_->size(); }
+
+ private:
+  DistConfig cfg_;
+  std::unique_ptr<Communicator> comm_;
+  std::unique_ptr<ShardEngine> eng_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_locust, m) {
+  m.doc() = "Locust-MI355X native engine (HIP/CDNA4 kernels, RCCL shuffle)";
+
+  py::enum_<Backend>(m, "Backend").value("gpu", Backend::kGpu).value("cpu", Backend::kCpu);
+  py::enum_<ReducePath>(m, "ReducePath")
+      .value("lds", ReducePath::kLds)
+      .value("global_", ReducePath::kGlobal);
+  py::enum_<MapPath>(m, "MapPath").value("compat", MapPath::kCompat).value("fast", MapPath::kFast);
+  py::enum_<SortPath>(m, "SortPath").value("radix", SortPath::kRadix).value("dict", SortPath::kDict);
+
+  py::class_<JobConfig>(m, "JobConfig")
+      .def(py::init<>())
+      .def_readwrite("backend", &JobConfig::backend)
+      .def_readwrite("device", &JobConfig::device)
+      .def_readwrite("emits_per_line", &JobConfig::emits_per_line)
+      .def_readwrite("max_key_len", &JobConfig::max_key_len)
+      .def_readwrite("delimiters", &JobConfig::delimiters)
+      .def_readwrite("ref_compat", &JobConfig::ref_compat)
+      .def_readwrite("reduce_path", &JobConfig::reduce_path)
+      .def_readwrite("map_path", &JobConfig::map_path)
+      .def_readwrite("sort_path", &JobConfig::sort_path)
+      .def_readwrite("combine", &JobConfig::combine)
+      .def_readwrite("check", &JobConfig::check)
+      .def_readwrite("sync_plan", &JobConfig::sync_plan);
+
+  py::class_<DistConfig>(m, "DistConfig")
+      .def(py::init<>())
+      .def_readwrite("job", &DistConfig::job)
+      .def_readwrite("world", &DistConfig::world)
+      .def_readwrite("samples_per_rank", &DistConfig::samples_per_rank)
+      .def_readwrite("gather", &DistConfig::gather);
+
+  py::class_<PyResult>(m, "Result")
+      .def("entries", &PyResult::entries)
+      .def("times", &PyResult::times)
+      .def("format", &PyResult::format, py::arg("cpu_format") = false)
+      .def_property_readonly("num_lines", [](const PyResult& p) { return p.r.num_lines; })
+      .def_property_readonly("num_tokens", [](const PyResult& p) { return p.r.num_tokens; })
+      .def_property_readonly("num_unique", [](const PyResult& p) { return p.r.num_unique; })
+      .def_property_readonly("overflow_lines", [](const PyResult& p) { return p.r.overflow_lines; })
+      .def_property_readonly("truncated", [](const PyResult& p) { return p.r.truncated; })
+      .def_property_readonly("max_key_len", [](const PyResult& p) { return p.r.max_key_len; });
+
+  py::class_<PyGpuEngine>(m, "GpuEngine")
+      .def(py::init<const JobConfig&, u64, u64>(), py::arg("cfg"), py::arg("max_bytes"),
+           py::arg("max_lines"))
+      .def("run", &PyGpuEngine::run)
+      .def("map_stage", &PyGpuEngine::map_stage)
+      .def("reduce_stage", &PyGpuEngine::reduce_stage)
+      .def("sort_keys", &PyGpuEngine::sort_keys)
+      .def_property_readonly("capacity", &PyGpuEngine::capacity);
+
+  m.def("cpu_run", [](const JobConfig& cfg, const std::string& text) {
+    CpuWordCount eng(cfg);
+    return PyResult{eng.run(as_input(text))};
+  });
+  m.def("cpu_map_stage", [](const JobConfig& cfg, const std::string& text) {
+    CpuWordCount eng(cfg);
+    std::vector<py::bytes> out;
+    for (const auto& k : eng.run_map_stage(as_input(text), nullptr)) out.emplace_back(key_to_string(k));
+    return out;
+  });
+  m.def("run_multi", &run_multi, py::arg("text"), py::arg("cfg"),
+        "Loopback multi-rank WordCount in this process (one thread per rank).");
+
+  py::class_<PyDistRank>(m, "DistRank")
+      .def(py::init<const DistConfig&, int, const std::string&, const std::string&, int, u64, u64,
+                    double>(),
+           py::arg("cfg"), py::arg("rank"), py::arg("comm"), py::arg("host"), py::arg("port"),
+           py::arg("max_bytes"), py::arg("max_lines"), py::arg("timeout_s") = 300.0)
+      .def("run", &PyDistRank::run, py::arg("shard"), py::arg("first_line") = 0)
+      .def("barrier", &PyDistRank::barrier)
+      .def("allreduce_max", &PyDistRank::allreduce_max)
+      .def_property_readonly("rank", &PyDistRank::rank)
+      .def_property_readonly("size", &PyDistRank::size);
+
+  m.def("load_lines",
+        [](const std::string& path, i64 start, i64 end, bool ref_compat) {
+          LoadedText t = load_lines(path, start, end, ref_compat);
+          return py::make_tuple(py::bytes(t.storage.data(), t.storage.size()), t.input.num_lines,
+                                t.input.first_line, t.file_lines);
+        },
+        py::arg("path"), py::arg("line_start") = -1, py::arg("line_end") = -1,
+        py::arg("ref_compat") = false);
+  m.def("shard_bounds", [](const std::string& text, int parts) {
+    TextInput in = as_input(text);
+    py::list out;
+    for (const auto& s : shard_text(in, parts))
+      out.append(py::make_tuple((u64)(s.data - in.data), s.bytes, s.num_lines, s.first_line));
+    return out;
+  });
+  m.def("strtok_r_tokens", &strtok_r_tokens, py::arg("line"), py::arg("delims") = std::string(kDefaultDelims));
+  m.def("itoa", [](int n, int base) {
+    char buf[40];
+    return std::string(d_itoa(n, buf, base));
+  });
+  m.def("strcmp", [](const std::string& a, const std::string& b) { return d_strcmp(a.c_str(), b.c_str()); });
+  m.def("pack_key", [](const std::string& s) {
+    PackedKey k = to_key(s);
+    return std::vector<u64>(k.w, k.w + kKeyWords);
+  });
+  m.def("write_spill",
+        [](const std::string& path, const std::vector<std::pair<std::string, u64>>& recs, bool binary) {
+          std::vector<KeyCount> v;
+          for (const auto& r : recs) {
+            KeyCount kc{};
+            PackedKey k = to_key(r.first);
+            for (int w = 0; w < kKeyWords; ++w) kc.w[w] = k.w[w];
+            kc.count = r.second;
+            v.push_back(kc);
+          }
+          write_spill(path, v, binary ? SpillFormat::kBinary : SpillFormat::kText);
+        });
+  m.def("read_spill", [](const std::string& path) {
+    py::list out;
+    for (const auto& r : read_spill(path)) {
+      PackedKey k;
+      for (int w = 0; w < kKeyWords; ++w) k.w[w] = r.w[w];
+      out.append(py::make_tuple(py::bytes(key_to_string(k)), r.count));
+    }
+    return out;
+  });
+  py::register_exception<Error>(m, "LocustError");
+}

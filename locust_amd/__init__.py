@@ -1,0 +1,55 @@
+"""Locust-MI355X: a GPU MapReduce engine for AMD Instinct MI355X (gfx950).
+
+Capabilities of wuyan33/Locust (GPU WordCount MapReduce with a CPU reference path and a
+socket-based distributor), re-designed MI355X-first:
+
+* Map / Process / Reduce are hand-written HIP kernels for CDNA4 wave64 (device strtok_r,
+  byte-parallel tokenizer, decoupled look-back scans, LSD radix sort on packed keys,
+  LDS-staged boundary-mark / adjacent-difference reduce) -- see ``csrc/kernels``.
+* Multi-GPU runs shard the input by bytes, range-partition with sample-sort splitters and
+  shuffle 40-byte records with one RCCL all-to-all-v over xGMI (``csrc/comm``).
+* The reference's ``./MapReduce <file> [start end] [node stage]`` CLI and output format are
+  kept byte-for-byte (``build/MapReduce``).
+
+Quick start::
+
+    import locust_amd as lc
+    res = lc.wordcount_file("data/hamlet.txt", 0, 700)          # GPU
+    print(res.format().decode()[:200])
+    res_cpu = lc.wordcount_file("data/hamlet.txt", 0, 700, backend="cpu")
+"""
+from __future__ import annotations
+
+from ._native import REPO_ROOT, build, cli_path, load
+
+_C = load()
+
+from .config import make_config, make_dist_config  # noqa: E402
+from .models.wordcount import (  # noqa: E402
+    Engine,
+    WordCount,
+    run_multi,
+    wordcount_file,
+    wordcount_text,
+)
+
+JobConfig = _C.JobConfig
+DistConfig = _C.DistConfig
+LocustError = _C.LocustError
+
+__all__ = [
+    "REPO_ROOT",
+    "build",
+    "cli_path",
+    "make_config",
+    "make_dist_config",
+    "Engine",
+    "WordCount",
+    "run_multi",
+    "wordcount_file",
+    "wordcount_text",
+    "JobConfig",
+    "DistConfig",
+    "LocustError",
+]
+__version__ = "0.1.0"

@@ -1,0 +1,56 @@
+"""`./MapReduce` CLI: reference positional arguments and byte-compatible stdout."""
+import subprocess
+
+from locust_amd.utils import oracle
+
+
+def run(cli, *args, check=True):
+    p = subprocess.run([cli, *map(str, args)], capture_output=True)
+    if check:
+        assert p.returncode == 0, p.stderr.decode()
+    return p
+
+
+def result_lines(out: bytes) -> bytes:
+    return b"".join(l + b"\n" for l in out.split(b"\n") if l.startswith(b"print key:"))
+
+
+def test_usage(cli):
+    p = run(cli, check=False)
+    assert p.returncode == 255
+    assert p.stdout == (b"Running\nMissing or invalid arguments.\n"
+                        b"mapreduce <filename> [line_start] [line_end] [node_num] [stage]\n")
+
+
+def test_cpu_window_output(cli, hamlet):
+    p = run(cli, "data/hamlet.txt", 0, 700, "--backend", "cpu")
+    lines = p.stdout.split(b"\n")
+    assert lines[0] == b"Running"
+    assert lines[1] == b"Using custom start and end locations: (0, 700)"
+    assert lines[2].startswith(b"CPU mapping ") and lines[2].endswith(b" nanoseconds ")
+    entries = oracle.wordcount(oracle.window(hamlet, 0, 700))[0]
+    assert result_lines(p.stdout) == oracle.format_cpu(entries)
+    assert p.stdout.endswith(b"\nDone\n")
+
+
+def test_stage_split_cpu(cli, hamlet, tmp_path):
+    for node, (s, e) in enumerate([(0, 2000), (2000, 4463)]):
+        p = run(cli, "data/hamlet.txt", s, e, node, 1, "--backend", "cpu", "--spill-dir", tmp_path)
+        assert b"MODE_MULTI: Finished map" in p.stdout
+    files = f"{tmp_path}/out.0.txt,{tmp_path}/out.1.txt"
+    p = run(cli, "data/hamlet.txt", 0, 0, 0, 2, "--backend", "cpu", "--inputs", files)
+    entries = oracle.wordcount(hamlet)[0]
+    assert result_lines(p.stdout) == oracle.format_cpu(entries)
+
+
+def test_spill_text_format(cli, tmp_path):
+    (tmp_path / "in.txt").write_bytes(b"b a b\n")
+    run(cli, tmp_path / "in.txt", 0, 1, 3, 1, "--backend", "cpu", "--spill-dir", tmp_path)
+    # reference writer format "%s \t%d\n" (main.cu:121), sorted
+    assert (tmp_path / "out.3.txt").read_bytes() == b"a \t1\nb \t1\nb \t1\n"
+
+
+def test_multi_rank_cpu_cli(cli, hamlet):
+    p = run(cli, "data/hamlet.txt", "--backend", "cpu", "--gpus", 4)
+    entries = oracle.wordcount(hamlet)[0]
+    assert result_lines(p.stdout) == oracle.format_gpu(entries)

@@ -1,0 +1,120 @@
+"""GPU pipeline vs oracle: every kernel path (map compat/fast, reduce lds/global, planned
+and device-planned radix passes), edge cases, and sizes around the reference's 32,768-thread
+truncation (bug B3)."""
+import random
+
+import pytest
+
+import locust_amd as lc
+from locust_amd.utils import oracle
+
+pytestmark = pytest.mark.gpu
+
+PATHS = [
+    dict(map_path="fast", reduce_path="lds"),
+    dict(map_path="fast", reduce_path="global"),
+    dict(map_path="compat", reduce_path="lds"),
+    dict(map_path="compat", reduce_path="global"),
+    dict(map_path="fast", reduce_path="lds", sync_plan=False),
+]
+
+
+def gpu(text, **kw):
+    return lc.wordcount_text(text, backend="gpu", check=True, **kw)
+
+
+@pytest.mark.parametrize("opts", PATHS, ids=lambda o: "-".join(f"{v}" for v in o.values()))
+@pytest.mark.parametrize("start,end", [(0, 700), (-1, -1)])
+def test_hamlet_matches_oracle(hamlet, opts, start, end):
+    text = oracle.window(hamlet, start, end)
+    ent, ntok, _ = oracle.wordcount(text)
+    r = gpu(text, **opts)
+    assert r.num_tokens == ntok
+    assert r.entries() == ent
+    assert r.format() == oracle.format_gpu(ent)
+
+
+def test_hamlet_known_numbers(hamlet):
+    r = gpu(hamlet)
+    assert (r.num_tokens, r.num_unique) == (32940, 5608)
+    d = {k: (v, c) for k, v, c in r.entries()}
+    assert d[b"the"][1] == 930 and d[b"THE"][1] == 2
+    # B3 regression: keys whose runs start past index 32,768 get their own heads
+    for k in (b"yours", b"yourself", b"yourselves", b"youth", b"zone"):
+        assert k in d
+
+
+@pytest.mark.parametrize("opts", PATHS[:3], ids=["fast-lds", "fast-global", "compat-lds"])
+def test_random_texts(opts):
+    rng = random.Random(11)
+    words = [b"alpha", b"Beta", b"gamma", b"d", b"e-mail", b"x" * 35, b"it's", b"\xc3\xa9t\xc3\xa9"]
+    for trial in range(12):
+        lines = []
+        for _ in range(rng.randint(0, 400)):
+            n = rng.choice([0, 1, 5, 19, 20, 21, 40])
+            sep = rng.choice([b" ", b",  ", b"--", b"\t"])
+            lines.append(sep.join(rng.choice(words) for _ in range(n)))
+        text = b"\n".join(lines) + (b"\n" if trial % 2 else b"")
+        ent, ntok, overflow = oracle.wordcount(text)
+        r = gpu(text, **opts)
+        assert r.entries() == ent
+        assert r.num_tokens == ntok
+        assert r.overflow_lines == overflow
+
+
+@pytest.mark.parametrize("ntok", [1, 2, 4095, 4096, 4097, 32768, 32769, 100003])
+def test_sizes_around_tiles(ntok):
+    rng = random.Random(ntok)
+    vocab = [bytes(rng.choice(b"abcdefghij") for _ in range(rng.randint(1, 12))) for _ in range(3000)]
+    toks = [rng.choice(vocab) for _ in range(ntok)]
+    text = b"\n".join(b" ".join(toks[i:i + 10]) for i in range(0, ntok, 10)) + b"\n"
+    ent, n, _ = oracle.wordcount(text)
+    assert n == ntok
+    assert gpu(text).entries() == ent
+
+
+def test_long_lines_segment_boundaries():
+    # lines far longer than a 1 KiB wave segment and the 4 KiB tile: the carried per-line
+    # ordinal (20-emit cap) must survive segment and tile boundaries.
+    rng = random.Random(5)
+    lines = []
+    for _ in range(50):
+        n = rng.randint(0, 3000)
+        lines.append(b" " * rng.randint(0, 3000) + b" ".join(b"w%d" % rng.randint(0, 50) for _ in range(n)))
+    text = b"\n".join(lines)
+    ent, ntok, overflow = oracle.wordcount(text)
+    r = gpu(text)
+    assert r.entries() == ent and r.overflow_lines == overflow
+
+
+def test_empty_and_delimiter_only():
+    for text in (b"", b"\n\n\n", b" ,.;\n--\n"):
+        r = gpu(text)
+        assert r.num_tokens == 0 and r.entries() == []
+
+
+def test_sort_keys_random():
+    rng = random.Random(2)
+    keys = [bytes(rng.choice(b"aZ09\x80\xff~") for _ in range(rng.randint(1, 31))) for _ in range(50000)]
+    eng = lc.Engine(lc.make_config("gpu"), 1 << 20, 1 << 16)
+    s, perm = eng.sort_keys(keys)
+    assert s == sorted(keys)
+    assert [keys[i] for i in perm] == s
+    # stability: equal keys keep input order
+    for a, b in zip(perm, perm[1:]):
+        if keys[a] == keys[b]:
+            assert a < b
+
+
+def test_engine_reuse_and_stage_split(hamlet):
+    text = oracle.window(hamlet, 0, 1000)
+    eng = lc.Engine(lc.make_config("gpu"), len(hamlet) + 1, 5000)
+    r1 = eng.run(text).entries()
+    r2 = eng.run(oracle.window(hamlet, 1000, 2000)).entries()
+    r3 = eng.run(text).entries()
+    assert r1 == r3 == oracle.wordcount(text)[0]
+    assert r2 == oracle.wordcount(oracle.window(hamlet, 1000, 2000))[0]
+    toks = eng.map_stage(text)
+    assert toks == sorted(toks) and len(toks) == 7061 or len(toks) == oracle.wordcount(text)[1]
+    red = eng.reduce_stage(list(reversed(toks)))
+    assert red.entries() == r1

@@ -1,0 +1,71 @@
+"""Device string library (host side of the __host__ __device__ functions), SURVEY §4 item 1."""
+import random
+
+import pytest
+
+from locust_amd.ops import itoa, pack_key, strcmp, strtok_r_tokens
+from locust_amd.utils.oracle import DEFAULT_DELIMS
+
+
+def py_strtok(line: bytes, delims: bytes):
+    out, cur = [], bytearray()
+    for c in line.split(b"\0", 1)[0]:
+        if c in delims:
+            if cur:
+                out.append(bytes(cur))
+                cur = bytearray()
+        else:
+            cur.append(c)
+    if cur:
+        out.append(bytes(cur))
+    return out
+
+
+@pytest.mark.parametrize("line", [
+    b"", b"   ", b"word", b"  lead and trail  ", b"a,b.c-d;e:f'g(h)i\"j\tk",
+    b"to be, or not to be: that is the question",
+    b"--..,,", b"x" * 80, b"one,,,,two;;;three",
+])
+def test_strtok_r_cases(line):
+    assert strtok_r_tokens(line, DEFAULT_DELIMS.decode()) == py_strtok(line, DEFAULT_DELIMS)
+
+
+def test_strtok_r_random():
+    rng = random.Random(1)
+    alphabet = b"abcXYZ019 ,.-;:'()\"\t"
+    for _ in range(2000):
+        line = bytes(rng.choice(alphabet) for _ in range(rng.randint(0, 60)))
+        assert strtok_r_tokens(line, DEFAULT_DELIMS.decode()) == py_strtok(line, DEFAULT_DELIMS)
+
+
+@pytest.mark.parametrize("n,base", [(0, 10), (7, 10), (-42, 10), (2147483647, 10),
+                                    (-2147483648, 10), (255, 16), (5, 2), (35, 36)])
+def test_itoa(n, base):
+    digits = "0123456789abcdefghijklmnopqrstuvwxyz"
+    def ref(n, b):
+        if n == 0:
+            return "0"
+        neg = n < 0 and b == 10
+        u = -n if neg else n & 0xFFFFFFFF
+        s = ""
+        while u:
+            s = digits[u % b] + s
+            u //= b
+        return ("-" if neg else "") + s
+    assert itoa(n, base) == ref(n, base)
+
+
+def test_strcmp_unsigned_order():
+    assert strcmp(b"abc", b"abc") == 0
+    assert strcmp(b"ab", b"abc") == -1
+    assert strcmp(b"b", b"abc") == 1
+    assert strcmp(b"Z", b"a") == -1  # uppercase sorts first
+    assert strcmp(b"\xe9", b"z") == 1  # unsigned bytes
+
+
+def test_pack_key_order_matches_bytes_order():
+    rng = random.Random(7)
+    keys = [bytes(rng.choice(b"abAB\x7f\x80\xff") for _ in range(rng.randint(1, 31)))
+            for _ in range(500)]
+    packed = sorted(keys, key=lambda k: pack_key(k))
+    assert packed == sorted(keys)
