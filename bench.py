@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Headline benchmark: WordCount Map/Process/Reduce on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config hamlet4500|hamlet700]
+
+One "step" is one complete WordCount job: H2D of the text, Map (tokenize/emit), Process
+(compaction + radix sort), Reduce (boundary mark + head compaction + adjacent difference)
+and D2H of the sorted (key, val, count) results -- the reference's timed stages
+(main.cu:405-468) plus the transfers it leaves untimed.  The reference numbers are on a
+GTX 1060 (README.md:72-88): 4,500-line whole-Hamlet LDS-reduce total 77.393 ms, 700-line
+total 29.405 ms.
+
+N = 1: one process, one GPU.  N > 1 (launched by torch.distributed.run, one process per
+GPU, RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT from the env): weak scaling --
+every rank maps its own copy of the text, then the ranks range-partition and shuffle the
+map output with one RCCL all-to-all-v over xGMI, reduce their key range and gather the
+globally sorted result on rank 0.  Steps are timed between barriers with the device
+synchronised on both sides; the MAX over ranks is reported.
+
+This process never imports torch: the engine drives HIP/RCCL directly (torch's bundled
+HIP runtime must not be loaded next to the system one).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "WordCount ms (Map/Process/Reduce) at 700 & 4500 lines; 1/2/4/8-GPU scaling"
+BASELINE_MS = {"hamlet4500": 77.393, "hamlet700": 29.405}  # README.md:74-76, 86-88 (GPU/LDS)
+BASELINE_STAGES = {
+    "hamlet4500": {"map_ms": 0.040, "process_ms": 73.015, "reduce_ms": 4.338},
+    "hamlet700": {"map_ms": 0.047, "process_ms": 27.646, "reduce_ms": 1.712},
+}
+
+
+def load_text(config: str) -> bytes:
+    import locust_amd as lc
+    from locust_amd.utils import oracle
+
+    with open(os.path.join(ROOT, "data", "hamlet.txt"), "rb") as f:
+        hamlet = f.read()
+    if config == "hamlet700":
+        return oracle.window(hamlet, 0, 700)
+    return hamlet
+
+
+def bench_single(text: bytes, steps: int, warmup: int):
+    import locust_amd as lc
+
+    cfg = lc.make_config("gpu", reduce_path="lds")
+    nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
+    eng = lc._C.GpuEngine(cfg, len(text), nlines)
+    eng.load(text)
+    for _ in range(warmup):
+        res = eng.run_loaded()
+    stage = {"map_ms": [], "process_ms": [], "reduce_ms": [], "h2d_ms": [], "d2h_ms": []}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = eng.run_loaded()
+        t = res.times()
+        for k in stage:
+            stage[k].append(t[k])
+    t1 = time.perf_counter()
+    ms = (t1 - t0) * 1e3 / steps
+    med = {k: statistics.median(v) for k, v in stage.items()}
+    return ms, med, res
+
+
+def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, local_rank: int):
+    import locust_amd as lc
+
+    job = lc.make_config("gpu", device=local_rank, reduce_path="lds", combine=True)
+    dcfg = lc.make_dist_config(world, job)
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("LOCUST_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+    nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
+    dr = lc._C.DistRank(dcfg, rank, "rccl", host, port, len(text), nlines, 300.0)
+    for _ in range(warmup):
+        dr.run(text, 0)
+    parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": []}
+    dr.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res, info = dr.run(text, 0)
+        for k in parts:
+            parts[k].append(info[k])
+    dr.barrier()
+    t1 = time.perf_counter()
+    mine = (t1 - t0) * 1e3 / steps
+    ms = dr.allreduce_max(mine)
+    med = {k: statistics.median(v) for k, v in parts.items()}
+    return ms, med, res, dr
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="hamlet4500", choices=sorted(BASELINE_MS))
+    ap.add_argument("--no-extra", action="store_true", help="skip the 700-line side measurement")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world != 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    n = max(world, 1)
+
+    text = load_text(args.config)
+    nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
+    extra = {}
+    if n == 1:
+        ms, stages, res = bench_single(text, args.steps, args.warmup)
+        if not args.no_extra and args.config == "hamlet4500":
+            ms700, st700, _ = bench_single(load_text("hamlet700"), args.steps, args.warmup)
+            extra["hamlet700"] = {"ms_per_step": round(ms700, 4), "vs_baseline":
+                                  round(ms700 / BASELINE_MS["hamlet700"], 6),
+                                  "stages_ms": {k: round(v, 4) for k, v in st700.items()}}
+    else:
+        ms, stages, res, dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank)
+    if rank != 0:
+        return 0
+    base = BASELINE_MS[args.config]
+    line = {
+        "metric": METRIC,
+        "value": round(ms, 4),
+        "unit": "ms",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": False,
+        "scaling": "weak",
+        "vs_baseline": round(ms / base, 6),
+        "dtype": "int (u8 text, u64 packed keys/counts)",
+        "data": "hamlet.txt fixture (real text); N>1: every rank maps its own copy",
+        "config": {
+            "model": f"WordCount {args.config} ({nlines} lines/GPU), LDS reduce path, "
+                     "radix-sort Process, full H2D->D2H job per step",
+            "global_batch": nlines * n,
+            "seq_len": len(text),
+            "parallelism": f"dp{n}" + ("+rccl_alltoallv_shuffle" if n > 1 else ""),
+        },
+        "baseline_ms": base,
+        "baseline_stages_ms": BASELINE_STAGES[args.config],
+        "stages_ms_median": {k: round(v, 4) for k, v in stages.items()},
+        "tokens_per_gpu": res.num_tokens // n if n > 1 else res.num_tokens,
+        "unique": res.num_unique,
+    }
+    line.update(extra)
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

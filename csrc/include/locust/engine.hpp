@@ -77,6 +77,10 @@ class GpuWordCount {
 
   const JobConfig& config() const;
   u64 token_capacity() const;
+  // Pinned host staging buffer of the text (capacity max_text_bytes + 64).  A TextInput
+  // whose data points here is uploaded without the host-side staging copy -- the
+  // analogue of the reference loading the file into its host array before any timer.
+  char* input_buffer();
 
  private:
   struct Impl;

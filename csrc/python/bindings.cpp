@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
 #include <string>
 
 #include "locust/dist.hpp"
@@ -61,7 +62,7 @@ PackedKey to_key(const std::string& s) {
 class PyGpuEngine {
  public:
   PyGpuEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
-      : eng_(cfg, max_bytes, max_lines) {}
+      : eng_(cfg, max_bytes, max_lines), max_bytes_(max_bytes) {}
   PyResult run(const std::string& text) {
     py::gil_scoped_release nogil;
     return PyResult{eng_.run(as_input(text))};
@@ -96,9 +97,25 @@ class PyGpuEngine {
     return py::make_tuple(out, perm);
   }
   u64 capacity() const { return eng_.token_capacity(); }
+  // Stage the text in the engine's pinned buffer once; run_loaded() then skips the copy.
+  void load(const std::string& text) {
+    LOCUST_CHECK_ARG(text.size() <= max_bytes_, "text exceeds engine capacity");
+    std::memcpy(eng_.input_buffer(), text.data(), text.size());
+    loaded_ = eng_.input_buffer();
+    loaded_in_ = as_input(text);
+    loaded_in_.data = loaded_;
+  }
+  PyResult run_loaded() {
+    LOCUST_CHECK_ARG(loaded_ != nullptr, "call load() first");
+    py::gil_scoped_release nogil;
+    return PyResult{eng_.run(loaded_in_)};
+  }
 
  private:
   GpuWordCount eng_;
+  u64 max_bytes_;
+  char* loaded_ = nullptr;
+  TextInput loaded_in_;
 };
 
 py::list strtok_r_tokens(const std::string& line, const std::string& delims) {
@@ -232,6 +249,8 @@ PYBIND11_MODULE(_locust, m) {
       .def(py::init<const JobConfig&, u64, u64>(), py::arg("cfg"), py::arg("max_bytes"),
            py::arg("max_lines"))
       .def("run", &PyGpuEngine::run)
+      .def("load", &PyGpuEngine::load)
+      .def("run_loaded", &PyGpuEngine::run_loaded)
       .def("map_stage", &PyGpuEngine::map_stage)
       .def("reduce_stage", &PyGpuEngine::reduce_stage)
       .def("sort_keys", &PyGpuEngine::sort_keys)
