@@ -51,10 +51,10 @@ def load_text(config: str) -> bytes:
     return hamlet
 
 
-def bench_single(text: bytes, steps: int, warmup: int):
+def bench_single(text: bytes, steps: int, warmup: int, sort: str = "dict"):
     import locust_amd as lc
 
-    cfg = lc.make_config("gpu", reduce_path="lds")
+    cfg = lc.make_config("gpu", reduce_path="lds", sort=sort)
     nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
     eng = lc._C.GpuEngine(cfg, len(text), nlines)
     eng.load(text)
@@ -125,6 +125,11 @@ def main() -> int:
             extra["hamlet700"] = {"ms_per_step": round(ms700, 4), "vs_baseline":
                                   round(ms700 / BASELINE_MS["hamlet700"], 6),
                                   "stages_ms": {k: round(v, 4) for k, v in st700.items()}}
+            # The reference's own algorithm on the device: sort every token (LSD radix),
+            # boundary-mark + compact + adjacent-difference (reported, not the headline).
+            msr, str_, _ = bench_single(text, args.steps, args.warmup, sort="radix")
+            extra["radix_path"] = {"ms_per_step": round(msr, 4),
+                                   "stages_ms": {k: round(v, 4) for k, v in str_.items()}}
     else:
         ms, stages, res, dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank)
     if rank != 0:
@@ -145,7 +150,8 @@ def main() -> int:
         "data": "hamlet.txt fixture (real text); N>1: every rank maps its own copy",
         "config": {
             "model": f"WordCount {args.config} ({nlines} lines/GPU), LDS reduce path, "
-                     "radix-sort Process, full H2D->D2H job per step",
+                     "dictionary Process (hash + rank sort of distinct keys), "
+                     "full H2D->D2H job per step",
             "global_batch": nlines * n,
             "seq_len": len(text),
             "parallelism": f"dp{n}" + ("+rccl_alltoallv_shuffle" if n > 1 else ""),

@@ -78,6 +78,12 @@ struct DevicePipeline {
   LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{};
   RadixWorkspace rx{};
 
+  // dictionary path: [table | ucount | rank] is one zeroed block
+  DictWorkspace dict{};
+  u64 dict_slots = 0;
+  u32* d_rank = nullptr;
+  u64 dict_zero_bytes = 0;
+
   char* h_text = nullptr;
   MapCounters* h_ctr = nullptr;
   SortPlan* h_plan = nullptr;
@@ -105,11 +111,17 @@ struct DevicePipeline {
     const u64 slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
     const u64 t_line = div_up(cap_bytes, kLineIdxTile) + 1;
     const u64 t_compact = div_up(cap_lines, 256) + 1;
-    const u64 t_map = div_up(cap_bytes, kMapTileBytes) + 1;
+    const u64 t_map = div_up(cap_bytes, kMapTileBytesMin) + 1;
     const u64 t_heads = div_up(cap, kReduceTile) + 1;
     const u64 t_scan = div_up(cap, kReduceTile) + 1;
-    const u64 rx_zero_words = (u64)kNumPositions * 256 + kNumPositions +
-                              (u64)kNumPositions * radix_status_words(cap);
+    const u64 rx_zero_words = radix_zero_bytes(cap) / 4;
+    // Hash table: >= 2x the distinct keys it can see (load factor <= 0.5), capped at
+    // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
+    dict_slots = 1024;
+    while (dict_slots < 2 * std::min<u64>(cap, 1ull << 24)) dict_slots <<= 1;
+    dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + align_up(cap * 8, 256) +
+                      cap * 4;
+    const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
     sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan);
 
     SizingPlan sz;
@@ -133,11 +145,14 @@ struct DevicePipeline {
     sz.add<u64>(1);
     sz.add<char>(sync_bytes);
     sz.add<u32>(rx_zero_words);
+    sz.add<u32>(rx_part_words);
     sz.add<SortPlan>(1);
     for (int b = 0; b < 2; ++b) {
       sz.add<u64>(cap);
       sz.add<u32>(cap);
     }
+    for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(cap);
+    sz.add<char>(dict_zero_bytes);
     arena.size = sz.bytes + 4096;
     LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
 
@@ -180,13 +195,21 @@ struct DevicePipeline {
     lb_scan = {st, counters + 4};
 
     rx.cap = cap;
-    rx.hist = arena.take<u32>(rx_zero_words);
-    rx.tile_counters = rx.hist + (u64)kNumPositions * 256;
+    rx.tile_counters = arena.take<u32>(rx_zero_words);
     rx.status = rx.tile_counters + kNumPositions;
+    rx.hist_part = arena.take<u32>(rx_part_words);
     rx.plan = arena.take<SortPlan>(1);
     for (int b = 0; b < 2; ++b) {
       rx.keys[b] = arena.take<u64>(cap);
       rx.vals[b] = arena.take<u32>(cap);
+    }
+    for (int j = 0; j < kKeyWords; ++j) dict.ukeys.w[j] = arena.take<u64>(cap);
+    {
+      char* z = arena.take<char>(dict_zero_bytes);
+      dict.table = reinterpret_cast<DictSlot*>(z);
+      dict.ucount = reinterpret_cast<u64*>(z + align_up(dict_slots * sizeof(DictSlot), 256));
+      d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.ucount) + align_up(cap * 8, 256));
+      dict.mask = (u32)(dict_slots - 1);
     }
 
     char delim_buf[64] = {0};
@@ -244,21 +267,23 @@ struct DevicePipeline {
   }
 
   // Compaction (compat path) + radix sort of `tokens` into `sorted` (and counts).
-  void enqueue_process(u32 num_lines, bool compat, bool with_counts) {
+  // host_n: record count when the host already knows it.  With sync_plan the count is
+  // read back (one 4-byte D2H) so the sort can pick its regime and exact grids; without
+  // it everything stays on the device (graph-capturable).
+  void enqueue_process(u32 num_lines, bool compat, bool with_counts, u64 host_n = kUnknownCount) {
     if (compat)
       launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
                            lb_compact, stream);
-    radix_sort_prepare(tokens, &d_ctr->num_records, rx, stream);
-    const SortPlan* hp = nullptr;
-    if (cfg.sync_plan) {
-      LOCUST_HIP_CHECK(hipMemcpyAsync(h_plan, rx.plan, offsetof(SortPlan, digit_offset),
+    if (!cfg.sync_plan) {
+      host_n = kUnknownCount;
+    } else if (host_n == kUnknownCount) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(h_u64, &d_ctr->num_records, sizeof(u32),
                                       hipMemcpyDeviceToHost, stream));
       sync();
-      hp = h_plan;
+      host_n = *reinterpret_cast<const u32*>(h_u64);
     }
-    radix_sort_run(tokens, &d_ctr->num_records, rx, hp, stream);
-    launch_gather_sorted(tokens, rx, sorted, d_perm, with_counts ? d_counts : nullptr,
-                         with_counts ? d_sorted_counts : nullptr, hp ? hp->n : cap, stream);
+    radix_sort(tokens, &d_ctr->num_records, host_n, rx, with_counts ? d_counts : nullptr, sorted,
+               with_counts ? d_sorted_counts : nullptr, d_perm, h_plan, stream);
   }
 
   // Head mark + compaction + adjacent difference over `sorted` (weighted when counts).
@@ -275,6 +300,45 @@ struct DevicePipeline {
 
   void enqueue_pack_output() {
     launch_pack_output(heads, d_head_val, d_head_count, cap, d_ctr, d_out, stream);
+  }
+
+  // ---- dictionary path (SortPath::kDict): no host synchronisation inside ----
+  void enqueue_process_dict(u32 num_lines, bool compat, bool with_counts = false) {
+    if (compat)
+      launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
+                           lb_compact, stream);
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
+                       d_ctr, stream);
+    launch_rank_sort(dict.ukeys, &d_ctr->num_unique, cap, d_rank, stream);
+    launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, cap, sorted,
+                        d_sorted_counts, stream);
+  }
+  void enqueue_reduce_dict() {
+    launch_scan_pack(sorted, d_sorted_counts, cap, d_ctr, d_out, lb_scan, stream);
+  }
+  // After the counters are read: a dictionary run whose distinct-key count exceeded the
+  // rank sort's range (or whose table overflowed) is finished on the radix path.
+  bool dict_fallback_needed() const {
+    return (h_ctr->flags & kCtrDictOverflow) || h_ctr->num_unique > (u32)kRankSortMax;
+  }
+  void finish_dict_with_radix(u32 num_lines, bool with_counts = false) {
+    if (h_ctr->flags & kCtrDictOverflow) {
+      // table overflow: sort every record and reduce the reference way
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.tile_counter, 0, 4, stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.tile_counter, 0, 4, stream));
+      enqueue_process(num_lines, false, with_counts, h_ctr->num_records);
+      enqueue_reduce_core(with_counts);
+      enqueue_pack_output();
+      return;
+    }
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.tile_counter, 0, 4, stream));
+    radix_sort(dict.ukeys, &d_ctr->num_unique, h_ctr->num_unique, rx, dict.ucount, sorted,
+               d_sorted_counts, d_perm, h_plan, stream);
+    enqueue_reduce_dict();
   }
 
   void read_counters() {
@@ -325,11 +389,25 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
     enqueue_map(in);
     LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
-    enqueue_process((u32)in.num_lines, compat, false);
-    LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
-    enqueue_reduce_core(false);
-    enqueue_pack_output();
+    const bool dict_path = cfg.sort_path == SortPath::kDict;
+    if (dict_path) {
+      enqueue_process_dict((u32)in.num_lines, compat);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+      enqueue_reduce_dict();
+    } else {
+      enqueue_process((u32)in.num_lines, compat, false);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+      enqueue_reduce_core(false);
+      enqueue_pack_output();
+    }
     LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+    if (dict_path) {
+      read_counters();
+      if (dict_fallback_needed()) {
+        finish_dict_with_radix((u32)in.num_lines);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      }
+    }
     download_output(r, ev[5]);
     r.times.wall_ms = (now_ns() - t0) * 1e-6;
     r.times.h2d_ms = ms_between(ev[0], ev[1]);
@@ -414,7 +492,7 @@ WordCountResult GpuWordCount::run_reduce_stage(const PackedKey* keys, u64 n) {
   m.upload_tokens(keys, n);
   LOCUST_HIP_CHECK(hipEventRecord(m.ev[1], m.stream));
   LOCUST_HIP_CHECK(hipEventRecord(m.ev[2], m.stream));
-  m.enqueue_process(0, false, false);  // B7 fix: the reducer always sorts its input
+  m.enqueue_process(0, false, false, n);  // B7 fix: the reducer always sorts its input
   LOCUST_HIP_CHECK(hipEventRecord(m.ev[3], m.stream));
   m.enqueue_reduce_core(false);
   m.enqueue_pack_output();
@@ -433,7 +511,7 @@ std::vector<u32> GpuWordCount::sort_keys(const PackedKey* keys, u64 n,
                                          std::vector<PackedKey>* sorted) {
   Impl& m = *impl_;
   m.upload_tokens(keys, n);
-  m.enqueue_process(0, false, false);
+  m.enqueue_process(0, false, false, n);
   std::vector<u32> perm(n);
   if (n)
     LOCUST_HIP_CHECK(hipMemcpyAsync(perm.data(), m.d_perm, n * sizeof(u32),
@@ -461,16 +539,35 @@ class GpuShardEngine final : public ShardEngine {
     m.check_input(shard);
     m.enqueue_upload(shard);
     m.enqueue_map(shard);
-    m.enqueue_process((u32)shard.num_lines, cfg_.map_path == MapPath::kCompat, false);
-    combine_ = combine;
-    if (combine) {
-      // Map-side combine: local (key, count) runs become the shuffle records.
-      m.enqueue_reduce_core(false);
-      launch_pack_records(m.heads, m.d_head_count, &m.d_ctr->num_unique, m.cap, m.d_records,
-                          m.stream);
+    const bool compat = cfg_.map_path == MapPath::kCompat;
+    if (combine && cfg_.sort_path == SortPath::kDict) {
+      // Map-side combine through the dictionary: sorted distinct keys + counts.
+      m.enqueue_process_dict((u32)shard.num_lines, compat);
+      m.read_counters();
+      if (m.dict_fallback_needed()) {
+        if (m.h_ctr->flags & kCtrDictOverflow) {
+          m.enqueue_process(0, false, false, m.h_ctr->num_records);
+          m.enqueue_reduce_core(false);
+          set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
+        } else {
+          radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx,
+                     m.dict.ucount, m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+          set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+        }
+      } else {
+        set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      }
     } else {
-      launch_pack_records(m.sorted, nullptr, &m.d_ctr->num_records, m.cap, m.d_records, m.stream);
+      m.enqueue_process((u32)shard.num_lines, compat, false);
+      if (combine) {
+        // Map-side combine: local (key, count) runs become the shuffle records.
+        m.enqueue_reduce_core(false);
+        set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
+      } else {
+        set_local(m.sorted, nullptr, &m.d_ctr->num_records);
+      }
     }
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
     m.read_counters();
     local_stats_ = WordCountResult();
     local_stats_.num_lines = shard.num_lines;
@@ -522,35 +619,47 @@ class GpuShardEngine final : public ShardEngine {
     // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
     r.set_num_records(n);
     launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.stream);
-    r.enqueue_process(0, false, true);
-    r.enqueue_reduce_core(true);
-    r.read_counters();
+    if (cfg_.sort_path == SortPath::kDict) {
+      r.enqueue_process_dict(0, false, true);
+      r.enqueue_reduce_dict();
+      r.read_counters();
+      if (r.dict_fallback_needed()) {
+        r.finish_dict_with_radix(0, true);
+        r.read_counters();
+      }
+    } else {
+      r.enqueue_process(0, false, true, n);
+      r.enqueue_reduce_core(true);
+      r.enqueue_pack_output();
+      r.read_counters();
+    }
     *total_count = r.h_ctr->total_count;
     *num_unique = r.h_ctr->num_unique;
   }
 
   void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
-    DevicePipeline& r = *rp_;
-    r.h_u64[0] = global_offset;
-    LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_offset, r.h_u64, sizeof(u64), hipMemcpyHostToDevice, r.stream));
-    launch_add_offset(r.d_head_val, r.cap, r.d_offset, r.d_ctr, r.stream);
-    r.enqueue_pack_output();
     WordCountResult tmp;
-    r.download_output(tmp, nullptr);
+    rp_->download_output(tmp, nullptr);
+    for (auto& e : tmp.entries) e.val += global_offset;
     *out = std::move(tmp.entries);
   }
 
   void map_stats(WordCountResult* r) override { *r = local_stats_; }
 
  private:
-  ConstKeysSoA local_keys() const { return combine_ ? mp_->heads : mp_->sorted; }
-  const u32* local_n() const {
-    return combine_ ? &mp_->d_ctr->num_unique : &mp_->d_ctr->num_records;
+  void set_local(ConstKeysSoA k, const u64* c, const u32* n) {
+    local_keys_ = k;
+    local_counts_ = c;
+    local_n_ = n;
   }
+  ConstKeysSoA local_keys() const { return local_keys_; }
+  const u32* local_n() const { return local_n_; }
 
   JobConfig cfg_;
   std::unique_ptr<DevicePipeline> mp_, rp_;
-  bool combine_ = false;
+  ConstKeysSoA local_keys_{};
+  const u64* local_counts_ = nullptr;
+  const u32* local_n_ = nullptr;
   WordCountResult local_stats_;
 };
 

@@ -39,7 +39,7 @@ struct JobConfig {
   bool ref_compat = false;                   // reproduce B1: whole-file load drops last line
   ReducePath reduce_path = ReducePath::kLds;
   MapPath map_path = MapPath::kFast;
-  SortPath sort_path = SortPath::kRadix;
+  SortPath sort_path = SortPath::kDict;
   bool combine = false;                      // map-side combine (distributed shuffle)
   bool check = false;                        // LOCUST_CHECK invariants after each stage
   bool sync_plan = true;                     // read the sort plan back: launch only live passes

@@ -35,7 +35,10 @@ struct MapCounters {
   u32 num_newlines;     // line index size
   u32 max_key_len;      // longest token seen (before truncation)
   u64 total_count;      // sum of record counts (== num_records when every count is 1)
+  u32 flags;            // kCtr* status bits
+  u32 pad;
 };
+constexpr u32 kCtrDictOverflow = 1u;  // dictionary table full: rerun on the radix path
 
 // Look-back scratch: a zeroed region of 64-bit status words plus a tile counter.
 struct LookbackScratch {
@@ -45,8 +48,12 @@ struct LookbackScratch {
 
 // ---------------- map.hip ----------------
 constexpr int kMapBlock = 256;
-constexpr int kMapSegSteps = 16;                              // 64-B steps per wave
-constexpr int kMapTileBytes = (kMapBlock / 64) * kMapSegSteps * 64;  // 4 KiB per workgroup
+// Tile = 4 waves x steps x 64 B.  Small inputs use 4 steps (1 KiB tiles: more workgroups
+// in flight), large inputs 16 steps (4 KiB tiles: fewer look-back hops and overlaps).
+constexpr int kMapSegStepsSmall = 4;
+constexpr int kMapSegStepsLarge = 16;
+constexpr int kMapTileBytesMin = (kMapBlock / 64) * kMapSegStepsSmall * 64;
+constexpr u64 kMapLargeInput = 8ull << 20;  // switch to large tiles above 8 MiB
 constexpr int kLineIdxBlock = 256;
 constexpr int kLineIdxItems = 16;                             // bytes per thread
 constexpr int kLineIdxTile = kLineIdxBlock * kLineIdxItems;
@@ -78,45 +85,44 @@ constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortBlock * kSortItems;  // 4096 keys per tile
 constexpr int kNumPositions = kKeyBytes;            // one 8-bit digit per key byte
 
+constexpr int kSmallSortMax = 8192;                  // single-workgroup LDS sort up to here
+constexpr u64 kUnknownCount = ~0ull;                 // "n only known on the device"
+
 struct SortPassInfo {
   u32 active;      // digit position not constant -> needs a pass
-  u32 src;         // 0 = (keys_a, vals_a), 1 = (keys_b, vals_b)
+  u32 src;         // reserved
 };
 struct SortPlan {
   u32 n;
-  u32 word_active[kKeyWords];  // any live pass in this word
-  u32 word_src[kKeyWords];     // buffer holding the permutation when the word starts
-  u32 final_src;               // buffer holding the final permutation (vals)
-  u32 num_active;
-  u32 pad[2];
+  u32 pad[3];
   SortPassInfo pass[kNumPositions];           // indexed by key byte position
   u32 digit_offset[kNumPositions][256];       // exclusive scan of the digit histogram
 };
 
 struct RadixWorkspace {
-  u32* hist;           // [kNumPositions][256], zeroed per sort
+  u32* hist_part;      // [radix_hist_blocks(cap)][kNumPositions * 256] partial histograms
   SortPlan* plan;      // device plan
   u64* keys[2];        // ping-pong key words
   u32* vals[2];        // ping-pong permutation
+  u32* tile_counters;  // [kNumPositions], followed immediately by `status`
   u32* status;         // per-pass look-back status [tiles][256]: [31:30] flag, [29:0] count
-  u32* tile_counters;  // [kNumPositions]
   u64 cap;             // max keys
 };
 
 u64 radix_status_words(u64 cap);  // u32 status words needed for one pass
+u32 radix_hist_blocks(u64 cap);   // histogram blocks (partials) for `cap` keys
+u64 radix_zero_bytes(u64 cap);    // bytes of tile_counters + status zeroed per sort
 
-// Phase 1: zero scratch, digit histograms for all 32 byte positions, plan on device.
-void radix_sort_prepare(ConstKeysSoA keys, const u32* d_n, RadixWorkspace& ws, hipStream_t s);
-// Phase 2: run the passes.  When `host_plan` is non-null (a copy of the device plan read
-// back by the caller), only live passes are launched with exactly-sized grids; otherwise
-// every pass is launched and inactive ones early-exit on the device plan (graph mode).
-void radix_sort_run(ConstKeysSoA keys, const u32* d_n, RadixWorkspace& ws,
-                    const SortPlan* host_plan, hipStream_t s);
-// After radix_sort_run: gathers keys (and optional u64 counts) into sorted order; the final permutation is
-// ws.vals[plan.final_src] (resolved on the device).
-void launch_gather_sorted(ConstKeysSoA keys, const RadixWorkspace& ws, KeysSoA sorted,
-                          u32* perm_out, const u64* counts_in, u64* counts_out, u64 cap,
-                          hipStream_t s);
+// Sorts the *d_n packed keys (SoA) into `sorted` (+ optional counts permuted alongside,
+// + optional permutation).  host_n: the count if the host knows it (then n <= 8192 runs
+// the single-workgroup LDS sort, larger n reads the plan back and launches only live
+// passes with exact grids), or kUnknownCount (graph mode: every kernel is launched and
+// the ones not needed early-exit on the device-side count / plan).
+// skip_upto: in graph mode, every kernel also exits when *d_n <= skip_upto (another sort
+// handles that range; 0 = none).
+void radix_sort(ConstKeysSoA keys, const u32* d_n, u64 host_n, RadixWorkspace& ws,
+                const u64* counts_in, KeysSoA sorted, u64* counts_out, u32* perm_out,
+                SortPlan* h_plan, hipStream_t s, u32 skip_upto = 0);
 
 // ---------------- reduce.hip ----------------
 constexpr int kReduceBlock = 256;
@@ -151,6 +157,33 @@ struct OutRecord {
 static_assert(sizeof(OutRecord) == 48, "OutRecord 48 B");
 void launch_pack_output(ConstKeysSoA head_keys, const u64* head_val, const u64* head_count,
                         u64 cap, const MapCounters* ctr, OutRecord* out, hipStream_t s);
+
+// ---------------- dict.hip ----------------
+constexpr int kRankSortMax = 32768;  // all-pairs rank sort up to here, radix above
+
+struct DictSlot {  // one hash-table slot (40 B): key words 1..3 stored XOR a magic value
+  u64 w[kKeyWords];
+  u32 id;          // dense id + 1 (0 = not yet published)
+  u32 pad;
+};
+struct DictWorkspace {
+  DictSlot* table;  // power-of-two slots, zeroed per run
+  u32 mask;         // slots - 1 (this run)
+  KeysSoA ukeys;    // dense distinct keys (ids from ctr->num_unique)
+  u64* ucount;      // per-id occurrence counts, zeroed per run
+};
+// Hash every token (with its count; null = 1) into the table; distinct keys land in
+// ukeys[0 .. ctr->num_unique) with summed counts in ucount.
+void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,
+                        const DictWorkspace& dw, MapCounters* ctr, hipStream_t s);
+// rank[i] = number of keys smaller than key i (distinct keys; rank zeroed by the caller).
+// Early-exits (device-side) when *d_u > kRankSortMax.
+void launch_rank_sort(ConstKeysSoA keys, const u32* d_u, u64 cap, u32* rank, hipStream_t s);
+void launch_rank_scatter(ConstKeysSoA keys, const u64* counts, const u32* rank, const u32* d_u,
+                         u64 cap, KeysSoA sorted, u64* sorted_counts, hipStream_t s);
+// val = exclusive scan of the sorted counts; writes OutRecords and ctr->total_count.
+void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounters* ctr,
+                      OutRecord* out, LookbackScratch lb, hipStream_t s);
 
 // ---------------- shuffle.hip ----------------
 // SoA keys (+ counts, null = 1) -> AoS KeyCount records (the all-to-all payload).

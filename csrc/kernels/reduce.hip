@@ -83,12 +83,25 @@ __global__ __launch_bounds__(kReduceBlock) void mark_compact_heads_kernel(
   const u32 first = base + threadIdx.x * kReduceItems;  // blocked: items [first, first+8)
   u32 flags = 0;
   if constexpr (kLds) {
-    // Coalesced striped load into LDS, then blocked reads.
-    for (int i = threadIdx.x; i < kReduceTile + 1; i += kReduceBlock) {
-      const i64 g = (i64)base + i - 1;
-      const bool ok = g >= 0 && g < (i64)n;
+    // Coalesced striped load into LDS, then blocked reads.  All of a thread's global loads
+    // are issued before any LDS store (a rolled loop would pay one load latency per trip).
+    constexpr int kTrips = (kReduceTile + 1 + kReduceBlock - 1) / kReduceBlock;
+    u64 v[kTrips][kKeyWords];
 #pragma unroll
-      for (int j = 0; j < kKeyWords; ++j) s_keys[j][i] = ok ? sorted.w[j][g] : ~0ull;
+    for (int r = 0; r < kTrips; ++r) {
+      const int i = threadIdx.x + r * kReduceBlock;
+      const i64 g = (i64)base + i - 1;
+      const bool ok = i < kReduceTile + 1 && g >= 0 && g < (i64)n;
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) v[r][j] = ok ? sorted.w[j][g] : ~0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kTrips; ++r) {
+      const int i = threadIdx.x + r * kReduceBlock;
+      if (i < kReduceTile + 1) {
+#pragma unroll
+        for (int j = 0; j < kKeyWords; ++j) s_keys[j][i] = v[r][j];
+      }
     }
     __syncthreads();
 #pragma unroll

@@ -1,0 +1,254 @@
+// Byte-parallel wave64 tokenizer (Map stage, fast path).
+//
+// Semantics are those of the reference map() (/root/reference/MapReduce/src/main.cu:136-153:
+// strtok_r over " ,.-;:'()\"\t", at most EMITS_PER_LINE tokens per line, value 1), but the
+// work is spread over bytes instead of lines:
+//
+//  * A 256-thread workgroup owns a tile of 4 wave segments (STEPS x 64 bytes each).  The
+//    tile plus 64 bytes of left context and 64 bytes of right overhang is staged into LDS
+//    with 16-byte vector loads, so every later byte access is an LDS read.
+//  * Each step, every lane looks at one byte.  The delimiter set lives in four u64 kernel
+//    arguments (SGPRs), so the membership test is a few VALU ops.  Ballots give the step's
+//    delimiter mask; token start = not-delimiter && previous byte is a delimiter.  The
+//    per-line ordinal (for the 20-emit cap) is the popcount of starts since the last
+//    '\n', carried across steps; the ordinal carried INTO a segment comes from a backward
+//    scan to the previous newline, stopped once it exceeds the cap.
+//  * Emit counts are scanned across the 4 waves and across tiles with a decoupled
+//    look-back, then each emitting lane finds its token's length from the delimiter
+//    masks (count-trailing-zeros, no per-byte loop), reads 40 bytes of LDS as five
+//    aligned u64 words, funnel-shifts, masks and byte-swaps them into the big-endian
+//    packed key, and writes it straight into the dense SoA output.  The map output is
+//    born compacted, in text order, so the reference's 116,000-slot thrust::partition
+//    (main.cu:411) has nothing left to do.
+#include "locust/device/lookback.hpp"
+#include "locust/device/wave.hpp"
+#include "locust/hip_check.hpp"
+#include "locust/kernels.hpp"
+
+namespace locust {
+namespace {
+
+using dev::ballot;
+using dev::lane_id;
+using dev::lanes_below;
+using dev::wave_id;
+
+constexpr int kPre = 64;   // left context staged before the tile
+constexpr int kPost = 64;  // right overhang staged after the tile (>= 40 for packing)
+
+// Delimiter set incl. '\n' and NUL, held in scalar registers.
+struct Delims {
+  u64 m0, m1, m2, m3;
+  __device__ __forceinline__ bool has(u32 c) const {
+    const u64 m = (c & 128u) ? ((c & 64u) ? m3 : m2) : ((c & 64u) ? m1 : m0);
+    return (m >> (c & 63u)) & 1ull;
+  }
+};
+
+__device__ __forceinline__ u32 global_byte(const char* text, u64 bytes, i64 pos) {
+  // Bytes outside [0, bytes) behave like a newline (a line boundary).
+  return (pos >= 0 && (u64)pos < bytes) ? (u32)(unsigned char)text[pos] : (u32)'\n';
+}
+
+template <int kStaged>
+struct TileText {
+  const unsigned char* lds;  // staged bytes [lo, lo + kStaged)
+  i64 lo;
+  const char* text;
+  u64 bytes;
+  __device__ __forceinline__ u32 at(i64 pos) const {
+    const i64 r = pos - lo;
+    if (r >= 0 && r < kStaged) return lds[r];
+    return global_byte(text, bytes, pos);
+  }
+};
+
+// Token starts since the last '\n' strictly before `pos`, saturated at cap + 1.
+template <typename TT>
+__device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32 cap) {
+  const int lane = lane_id();
+  u32 count = 0;
+  i64 hi = pos;  // scan [hi - 64, hi)
+  while (hi > 0) {
+    const i64 p = hi - 64 + lane;
+    const u32 c = tt.at(p);  // p < 0 reads as '\n'
+    const u32 cprev = tt.at(p - 1);
+    const bool start = !d.has(c) && d.has(cprev);
+    const u64 nl = ballot(c == '\n');
+    u64 st = ballot(start);
+    if (nl) {
+      const int last_nl = 63 - __clzll((long long)nl);
+      st &= (last_nl >= 63) ? 0ull : (~0ull << (last_nl + 1));
+      count += __popcll(st);
+      break;
+    }
+    count += __popcll(st);
+    if (count > cap) break;
+    hi -= 64;
+  }
+  return count > cap + 1 ? cap + 1 : count;
+}
+
+template <int kSteps>
+__global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
+    const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
+    u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
+    u32* __restrict__ tile_ctr) {
+  constexpr int kSeg = kSteps * 64;
+  constexpr int kTile = (kMapBlock / 64) * kSeg;
+  constexpr int kStaged = kPre + kTile + kPost;
+  __shared__ __attribute__((aligned(16))) unsigned char s_text[kStaged];
+  __shared__ u32 s_tile;
+  __shared__ u64 s_prefix;
+  __shared__ u32 s_wave_cnt[kMapBlock / 64];
+  const int lane = lane_id(), w = wave_id();
+  const u64 num_tiles = div_up(bytes, (u64)kTile);
+  const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);  // contains __syncthreads
+  if (tile >= num_tiles) return;
+
+  // ---- stage the tile (+ context) into LDS with 16-B loads ----
+  const i64 tile_base = (i64)tile * kTile;
+  const i64 lo = tile_base - kPre;
+  for (int c = threadIdx.x; c < kStaged / 16; c += kMapBlock) {
+    const i64 g = lo + (i64)c * 16;
+    if (g >= 0 && (u64)(g + 16) <= bytes) {
+      *reinterpret_cast<uint4*>(s_text + c * 16) = *reinterpret_cast<const uint4*>(text + g);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s_text[c * 16 + k] = (unsigned char)global_byte(text, bytes, g + k);
+    }
+  }
+  __syncthreads();
+  const TileText<kStaged> tt{s_text, lo, text, bytes};
+  const i64 seg = tile_base + (i64)w * kSeg;
+  const int seg_lds = kPre + w * kSeg;
+
+  // ---- phase 1: delimiter masks, token starts, in-line ordinals, emit masks ----
+  u32 line_ord = backward_line_ordinal(tt, seg, d, (u32)E);
+  bool prev_delim = d.has(s_text[seg_lds - 1]);
+  u64 emit_mask[kSteps];
+  u64 dmask[kSteps + 1];
+  u32 emitted = 0, overflow = 0;
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int s = 0; s < kSteps; ++s) {
+    const i64 p = seg + s * 64 + lane;
+    const bool in = (u64)p < bytes;
+    const u32 c = s_text[seg_lds + s * 64 + lane];
+    const bool is_d = d.has(c);
+    dmask[s] = ballot(is_d);
+    const bool pd = lane == 0 ? prev_delim : ((dmask[s] >> (lane - 1)) & 1ull);
+    prev_delim = (dmask[s] >> 63) & 1ull;
+    const bool start = in && !is_d && pd;
+    const u64 st = ballot(start);
+    const u64 nl = ballot(in && c == '\n');
+    const u64 nl_below = nl & below;
+    u32 ord;
+    if (nl_below) {
+      const int q = 63 - __clzll((long long)nl_below);
+      ord = __popcll(st & below & (~0ull << (q + 1)));
+    } else {
+      ord = line_ord + __popcll(st & below);
+    }
+    const bool emit = start && ord < (u32)E;
+    overflow += __popcll(ballot(start && ord == (u32)E));
+    emit_mask[s] = ballot(emit);
+    emitted += __popcll(emit_mask[s]);
+    if (nl) {
+      const int q = 63 - __clzll((long long)nl);
+      line_ord = (q >= 63) ? 0 : __popcll(st & (~0ull << (q + 1)));
+    } else {
+      line_ord += __popcll(st);
+    }
+    if (line_ord > (u32)E + 1) line_ord = (u32)E + 1;
+  }
+  dmask[kSteps] = ballot(d.has(s_text[seg_lds + kSteps * 64 + lane]));  // lookahead
+
+  // ---- phase 2: wave counts -> tile prefix (look-back) ----
+  if (lane == 0) s_wave_cnt[w] = emitted;
+  __syncthreads();
+  u32 wave_excl = 0, tile_total = 0;
+#pragma unroll
+  for (int i = 0; i < kMapBlock / 64; ++i) {
+    const u32 v = s_wave_cnt[i];
+    if (i < w) wave_excl += v;
+    tile_total += v;
+  }
+  const u64 prefix = dev::block_lookback(status, tile, tile_total, &s_prefix);
+  if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
+
+  // ---- phase 3: length from masks, pack from LDS words, write ----
+  u64 dst = prefix + wave_excl;
+  u32 trunc = 0, maxlen = 0;
+#pragma unroll
+  for (int s = 0; s < kSteps; ++s) {
+    const u64 m = emit_mask[s];
+    if (m & (1ull << lane)) {
+      const u64 idx = dst + lanes_below(m);
+      const u64 rest = dmask[s] >> lane;  // bit 0 is this (non-delimiter) byte
+      u32 len;
+      if (rest) {
+        len = (u32)__ffsll((unsigned long long)rest) - 1;
+      } else {
+        const u64 nx = dmask[s + 1];
+        len = (u32)(64 - lane) + (nx ? (u32)__ffsll((unsigned long long)nx) - 1 : 64u);
+      }
+      if (len > (u32)max_key) ++trunc;
+      maxlen = len > maxlen ? len : maxlen;
+      const u32 keep = len < (u32)max_key ? len : (u32)max_key;
+      const int o = seg_lds + s * 64 + lane;
+      const int base = o & ~7;
+      const u32 sh = (u32)(o & 7) * 8u;
+      u64 q[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) q[k] = *reinterpret_cast<const u64*>(s_text + base + 8 * k);
+      u64 kw[kKeyWords];
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) {
+        u64 raw = sh ? ((q[j] >> sh) | (q[j + 1] << (64u - sh))) : q[j];
+        const int rem = (int)keep - 8 * j;
+        if (rem <= 0) raw = 0;
+        else if (rem < 8) raw &= (1ull << (8 * rem)) - 1ull;
+        kw[j] = __builtin_bswap64(raw);
+      }
+      if (idx < out_cap) {
+#pragma unroll
+        for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
+      }
+    }
+    dst += __popcll(m);
+  }
+  // Rare events only: one atomic per wave that actually truncated a token.  (A per-wave
+  // atomicMax on one shared word serialises the waves at the memory side, so the longest
+  // token is only recorded when it exceeded the key width.)
+  trunc = dev::wave_reduce_sum(trunc);
+  maxlen = dev::wave_reduce_max(maxlen);
+  if (lane == 0 && trunc) atomicAdd(&ctr->truncated, trunc);
+  if (lane == 0 && maxlen > (u32)max_key) atomicMax(&ctr->max_key_len, maxlen);
+  if (tile == num_tiles - 1 && threadIdx.x == 0) ctr->num_records = (u32)(prefix + tile_total);
+}
+
+}  // namespace
+
+void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
+                     int max_key_len, KeysSoA out, u64 out_cap, MapCounters* ctr,
+                     LookbackScratch lb, hipStream_t s) {
+  if (bytes == 0) return;
+  const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
+  if (bytes < kMapLargeInput) {
+    constexpr int kTile = (kMapBlock / 64) * kMapSegStepsSmall * 64;
+    const u64 tiles = div_up(bytes, (u64)kTile);
+    map_fast_kernel<kMapSegStepsSmall><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
+        text, bytes, d, emits_per_line, max_key_len, out, out_cap, ctr, lb.status,
+        lb.tile_counter);
+  } else {
+    constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
+    const u64 tiles = div_up(bytes, (u64)kTile);
+    map_fast_kernel<kMapSegStepsLarge><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
+        text, bytes, d, emits_per_line, max_key_len, out, out_cap, ctr, lb.status,
+        lb.tile_counter);
+  }
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace locust

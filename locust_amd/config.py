@@ -39,7 +39,7 @@ def make_config(
     cfg.device = device
     reduce_path = reduce_path or os.environ.get("LOCUST_REDUCE_PATH", "lds")
     map_path = map_path or os.environ.get("LOCUST_MAP_PATH", "fast")
-    sort = sort or os.environ.get("LOCUST_SORT", "radix")
+    sort = sort or os.environ.get("LOCUST_SORT", "dict")
     cfg.reduce_path = _REDUCE[reduce_path]
     cfg.map_path = _MAP[map_path]
     cfg.sort_path = _SORT[sort]

@@ -75,9 +75,9 @@ def test_fault_injection_clean_failure(hamlet, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
-@pytest.mark.parametrize("combine", [True, False])
-def test_gpu_loopback(hamlet, world, combine):
-    r = lc.run_multi(hamlet, world, backend="gpu", combine=combine, check=True)
+@pytest.mark.parametrize("combine,sort", [(True, "dict"), (True, "radix"), (False, "radix")])
+def test_gpu_loopback(hamlet, world, combine, sort):
+    r = lc.run_multi(hamlet, world, backend="gpu", combine=combine, check=True, sort=sort)
     ent, ntok, _ = oracle.wordcount(hamlet)
     assert r.num_tokens == ntok
     assert r.entries() == ent

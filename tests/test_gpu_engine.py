@@ -11,6 +11,8 @@ from locust_amd.utils import oracle
 pytestmark = pytest.mark.gpu
 
 PATHS = [
+    dict(map_path="fast", reduce_path="lds", sort="dict"),
+    dict(map_path="compat", reduce_path="lds", sort="dict"),
     dict(map_path="fast", reduce_path="lds"),
     dict(map_path="fast", reduce_path="global"),
     dict(map_path="compat", reduce_path="lds"),
@@ -44,7 +46,7 @@ def test_hamlet_known_numbers(hamlet):
         assert k in d
 
 
-@pytest.mark.parametrize("opts", PATHS[:3], ids=["fast-lds", "fast-global", "compat-lds"])
+@pytest.mark.parametrize("opts", PATHS[:5], ids=["dict", "compat-dict", "fast-lds", "fast-global", "compat-lds"])
 def test_random_texts(opts):
     rng = random.Random(11)
     words = [b"alpha", b"Beta", b"gamma", b"d", b"e-mail", b"x" * 35, b"it's", b"\xc3\xa9t\xc3\xa9"]
@@ -62,15 +64,29 @@ def test_random_texts(opts):
         assert r.overflow_lines == overflow
 
 
-@pytest.mark.parametrize("ntok", [1, 2, 4095, 4096, 4097, 32768, 32769, 100003])
-def test_sizes_around_tiles(ntok):
+@pytest.mark.parametrize("sort", ["radix", "dict"])
+@pytest.mark.parametrize("ntok", [1, 2, 4095, 4096, 8192, 8193, 32768, 32769, 100003])
+def test_sizes_around_tiles(ntok, sort):
     rng = random.Random(ntok)
     vocab = [bytes(rng.choice(b"abcdefghij") for _ in range(rng.randint(1, 12))) for _ in range(3000)]
     toks = [rng.choice(vocab) for _ in range(ntok)]
     text = b"\n".join(b" ".join(toks[i:i + 10]) for i in range(0, ntok, 10)) + b"\n"
     ent, n, _ = oracle.wordcount(text)
     assert n == ntok
-    assert gpu(text).entries() == ent
+    assert gpu(text, sort=sort).entries() == ent
+
+
+@pytest.mark.parametrize("nuniq", [32768, 32769, 70000])
+def test_dict_many_distinct_keys(nuniq):
+    # distinct-key counts around the rank-sort / radix-fallback boundary
+    rng = random.Random(nuniq)
+    vocab = [b"k%07d%s" % (i, bytes(rng.choice(b"xyz") for _ in range(rng.randint(0, 20)))) for i in range(nuniq)]
+    toks = vocab + [rng.choice(vocab) for _ in range(nuniq // 3)]
+    rng.shuffle(toks)
+    text = b"\n".join(b" ".join(toks[i:i + 8]) for i in range(0, len(toks), 8))
+    ent, n, _ = oracle.wordcount(text)
+    r = gpu(text, sort="dict")
+    assert r.num_unique == nuniq and r.entries() == ent
 
 
 def test_long_lines_segment_boundaries():

@@ -10,4 +10,6 @@ timeout -k 10 300 ./build/MapReduce data/hamlet.txt --warmup 20 --iters 50 --qui
 cat gpurun_out/$TAG/cli4500.txt gpurun_out/$TAG/cli4500.json
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof -o run --output-format csv -- $GRAFT_REPO_ROOT/build/MapReduce $GRAFT_REPO_ROOT/data/hamlet.txt --warmup 5 --iters 20 --quiet > /dev/null
 cd $GRAFT_REPO_ROOT
-find gpurun_out/$TAG/prof -name "*kernel_stats.csv" | head -1 | xargs cat | cut -d, -f1-8 | head -30
+python3 tools/kstats.py gpurun_out/$TAG/prof/run_kernel_stats.csv
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof700 -o run --output-format csv -- $GRAFT_REPO_ROOT/build/MapReduce $GRAFT_REPO_ROOT/data/hamlet.txt 0 700 --warmup 5 --iters 20 --quiet > /dev/null
+cd $GRAFT_REPO_ROOT && python3 tools/kstats.py gpurun_out/$TAG/prof700/run_kernel_stats.csv
