@@ -82,3 +82,8 @@ $(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
 
 clean:
 	rm -rf $(BUILD) $(LIBDIR) locust_amd/_locust*.so
+
+# diagnostics: kernel micro-benchmarks
+kbench: $(BUILD)/kbench
+$(BUILD)/kbench: tools/kbench/kbench.hip $(LIB) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-value -Wno-unused-result -o $@ $< -L$(LIBDIR) -llocust -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'

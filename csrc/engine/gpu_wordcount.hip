@@ -87,7 +87,10 @@ struct DevicePipeline {
   char* h_text = nullptr;
   MapCounters* h_ctr = nullptr;
   SortPlan* h_plan = nullptr;
-  OutRecord* h_out = nullptr;
+  OutRecord* h_out = nullptr;         // host-mapped output records
+  OutRecord* d_out_mapped = nullptr;  // device view of h_out
+  MapCounters* h_ctr_mapped = nullptr;
+  MapCounters* d_ctr_mapped = nullptr;
   u64* h_keys = nullptr;  // staging for key up/downloads (4 words x cap)
   PackedKey* h_small = nullptr;
   u64* h_u64 = nullptr;
@@ -119,7 +122,8 @@ struct DevicePipeline {
     // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
     dict_slots = 1024;
     while (dict_slots < 2 * std::min<u64>(cap, 1ull << 24)) dict_slots <<= 1;
-    dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + align_up(cap * 8, 256) +
+    // [table | ucount | uval | rank]
+    dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(cap * 8, 256) +
                       cap * 4;
     const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
     sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan);
@@ -208,7 +212,8 @@ struct DevicePipeline {
       char* z = arena.take<char>(dict_zero_bytes);
       dict.table = reinterpret_cast<DictSlot*>(z);
       dict.ucount = reinterpret_cast<u64*>(z + align_up(dict_slots * sizeof(DictSlot), 256));
-      d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.ucount) + align_up(cap * 8, 256));
+      dict.uval = reinterpret_cast<u64*>(reinterpret_cast<char*>(dict.ucount) + align_up(cap * 8, 256));
+      d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.uval) + align_up(cap * 8, 256));
       dict.mask = (u32)(dict_slots - 1);
     }
 
@@ -220,7 +225,15 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
-    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, cap * sizeof(OutRecord), hipHostMallocDefault));
+    // Output records and the counter snapshot are host-mapped: the emit kernel writes them
+    // over PCIe directly (zero-copy), so a dictionary run needs no D2H copy at all.
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, cap * sizeof(OutRecord),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out_mapped), h_out, 0));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_ctr_mapped), h_ctr_mapped, 0));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, cap * kKeyWords * sizeof(u64), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
@@ -234,7 +247,7 @@ struct DevicePipeline {
     if (stream) (void)hipStreamDestroy(stream);
     if (arena.base) (void)hipFree(arena.base);
     for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_out, (void*)h_keys,
-                    (void*)h_small, (void*)h_u64})
+                    (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped})
       if (p) (void)hipHostFree(p);
   }
 
@@ -310,17 +323,28 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
     launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
                        d_ctr, stream);
-    launch_rank_sort(dict.ukeys, &d_ctr->num_unique, cap, d_rank, stream);
+    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, cap, d_rank, dict.uval, stream);
+  }
+  // Sorted distinct keys + counts (for the shuffle's range partition).
+  void enqueue_sorted_from_dict() {
     launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, cap, sorted,
                         d_sorted_counts, stream);
   }
+  // Output records from the weighted ranks; `mapped` writes them (and the counters)
+  // straight into host memory.
+  void enqueue_emit_dict(bool mapped) {
+    launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, cap, d_ctr,
+                     mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
+  }
+  // Radix-fallback reduce: scan of the sorted counts -> records in d_out.
   void enqueue_reduce_dict() {
     launch_scan_pack(sorted, d_sorted_counts, cap, d_ctr, d_out, lb_scan, stream);
   }
   // After the counters are read: a dictionary run whose distinct-key count exceeded the
   // rank sort's range (or whose table overflowed) is finished on the radix path.
   bool dict_fallback_needed() const {
-    return (h_ctr->flags & kCtrDictOverflow) || h_ctr->num_unique > (u32)kRankSortMax;
+    return (h_ctr->flags & (kCtrDictOverflow | kCtrNotEmitted)) ||
+           h_ctr->num_unique > (u32)kRankSortMax;
   }
   void finish_dict_with_radix(u32 num_lines, bool with_counts = false) {
     if (h_ctr->flags & kCtrDictOverflow) {
@@ -393,22 +417,33 @@ struct DevicePipeline {
     if (dict_path) {
       enqueue_process_dict((u32)in.num_lines, compat);
       LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
-      enqueue_reduce_dict();
+      enqueue_emit_dict(/*mapped=*/true);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+      sync();  // the one host synchronisation of a dictionary run
+      *h_ctr = *h_ctr_mapped;
+      if (dict_fallback_needed()) {
+        finish_dict_with_radix((u32)in.num_lines);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+        download_output(r, ev[5]);
+      } else {
+        fill_counters(r);
+        const u64 u = h_ctr->num_unique;
+        r.entries.resize(u);
+        for (u64 j = 0; j < u; ++j) {
+          for (int w = 0; w < kKeyWords; ++w) r.entries[j].key.w[w] = h_out[j].w[w];
+          r.entries[j].val = h_out[j].val;
+          r.entries[j].count = h_out[j].count;
+        }
+      }
     } else {
       enqueue_process((u32)in.num_lines, compat, false);
       LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
       enqueue_reduce_core(false);
       enqueue_pack_output();
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      download_output(r, ev[5]);
     }
-    LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
-    if (dict_path) {
-      read_counters();
-      if (dict_fallback_needed()) {
-        finish_dict_with_radix((u32)in.num_lines);
-        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
-      }
-    }
-    download_output(r, ev[5]);
     r.times.wall_ms = (now_ns() - t0) * 1e-6;
     r.times.h2d_ms = ms_between(ev[0], ev[1]);
     r.times.map_ms = ms_between(ev[1], ev[2]);
@@ -543,6 +578,7 @@ class GpuShardEngine final : public ShardEngine {
     if (combine && cfg_.sort_path == SortPath::kDict) {
       // Map-side combine through the dictionary: sorted distinct keys + counts.
       m.enqueue_process_dict((u32)shard.num_lines, compat);
+      m.enqueue_sorted_from_dict();
       m.read_counters();
       if (m.dict_fallback_needed()) {
         if (m.h_ctr->flags & kCtrDictOverflow) {
@@ -619,29 +655,39 @@ class GpuShardEngine final : public ShardEngine {
     // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
     r.set_num_records(n);
     launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.stream);
+    WordCountResult tmp;
+    bool downloaded = false;
     if (cfg_.sort_path == SortPath::kDict) {
       r.enqueue_process_dict(0, false, true);
-      r.enqueue_reduce_dict();
-      r.read_counters();
+      r.enqueue_emit_dict(/*mapped=*/true);
+      r.sync();
+      *r.h_ctr = *r.h_ctr_mapped;
       if (r.dict_fallback_needed()) {
         r.finish_dict_with_radix(0, true);
-        r.read_counters();
+      } else {
+        r.fill_counters(tmp);
+        tmp.entries.resize(r.h_ctr->num_unique);
+        for (u64 j = 0; j < tmp.entries.size(); ++j) {
+          for (int w = 0; w < kKeyWords; ++w) tmp.entries[j].key.w[w] = r.h_out[j].w[w];
+          tmp.entries[j].val = r.h_out[j].val;
+          tmp.entries[j].count = r.h_out[j].count;
+        }
+        downloaded = true;
       }
     } else {
       r.enqueue_process(0, false, true, n);
       r.enqueue_reduce_core(true);
       r.enqueue_pack_output();
-      r.read_counters();
     }
+    if (!downloaded) r.download_output(tmp, nullptr);
     *total_count = r.h_ctr->total_count;
     *num_unique = r.h_ctr->num_unique;
+    range_entries_ = std::move(tmp.entries);
   }
 
   void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
-    WordCountResult tmp;
-    rp_->download_output(tmp, nullptr);
-    for (auto& e : tmp.entries) e.val += global_offset;
-    *out = std::move(tmp.entries);
+    for (auto& e : range_entries_) e.val += global_offset;
+    *out = std::move(range_entries_);
   }
 
   void map_stats(WordCountResult* r) override { *r = local_stats_; }
@@ -658,6 +704,7 @@ class GpuShardEngine final : public ShardEngine {
   JobConfig cfg_;
   std::unique_ptr<DevicePipeline> mp_, rp_;
   ConstKeysSoA local_keys_{};
+  std::vector<WordCountEntry> range_entries_;
   const u64* local_counts_ = nullptr;
   const u32* local_n_ = nullptr;
   WordCountResult local_stats_;

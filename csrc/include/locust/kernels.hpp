@@ -39,6 +39,7 @@ struct MapCounters {
   u32 pad;
 };
 constexpr u32 kCtrDictOverflow = 1u;  // dictionary table full: rerun on the radix path
+constexpr u32 kCtrNotEmitted = 0x80000000u;  // rank_emit skipped (too many distinct keys)
 
 // Look-back scratch: a zeroed region of 64-bit status words plus a tile counter.
 struct LookbackScratch {
@@ -171,14 +172,21 @@ struct DictWorkspace {
   u32 mask;         // slots - 1 (this run)
   KeysSoA ukeys;    // dense distinct keys (ids from ctr->num_unique)
   u64* ucount;      // per-id occurrence counts, zeroed per run
+  u64* uval;        // per-id weighted rank (= output val), zeroed per run
 };
 // Hash every token (with its count; null = 1) into the table; distinct keys land in
 // ukeys[0 .. ctr->num_unique) with summed counts in ucount.
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,
                         const DictWorkspace& dw, MapCounters* ctr, hipStream_t s);
-// rank[i] = number of keys smaller than key i (distinct keys; rank zeroed by the caller).
+// rank[i] = number of keys smaller than key i (distinct keys; rank zeroed by the caller);
+// with counts/val also val[i] = total count of the smaller keys (zeroed by the caller).
 // Early-exits (device-side) when *d_u > kRankSortMax.
-void launch_rank_sort(ConstKeysSoA keys, const u32* d_u, u64 cap, u32* rank, hipStream_t s);
+void launch_rank_sort(ConstKeysSoA keys, const u64* counts, const u32* d_u, u64 cap, u32* rank,
+                      u64* val, hipStream_t s);
+// out[rank[i]] = {key i, val i, count i}; optional host-mapped counter snapshot.
+void launch_rank_emit(ConstKeysSoA keys, const u64* counts, const u32* rank, const u64* val,
+                      u64 cap, const MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                      hipStream_t s);
 void launch_rank_scatter(ConstKeysSoA keys, const u64* counts, const u32* rank, const u32* d_u,
                          u64 cap, KeysSoA sorted, u64* sorted_counts, hipStream_t s);
 // val = exclusive scan of the sorted counts; writes OutRecords and ctr->total_count.

@@ -70,7 +70,12 @@ __device__ bool global_insert(const DictWorkspace& dw, const u64* k, u64 count,
     if (w0 == 0) {
       w0 = cas_agent(&sl->w[0], 0, k[0]);
       if (w0 == 0) {  // claimed: dense id, dense key, then publish the other words
-        const u32 id = atomicAdd(&ctr->num_unique, 1u);
+        // One id-counter atomic per wave: the claiming lanes of this step share it.
+        const u64 claim = ballot(true);
+        const int leader = __ffsll((unsigned long long)claim) - 1;
+        u32 base = 0;
+        if (lane_id() == leader) base = atomicAdd(&ctr->num_unique, (u32)__popcll(claim));
+        const u32 id = (u32)__shfl((int)base, leader, 64) + dev::lanes_below(claim);
 #pragma unroll
         for (int j = 0; j < kKeyWords; ++j) dw.ukeys.w[j][id] = k[j];
         // ucount is zero-initialised and only ever updated by device-scope atomics (a
@@ -100,16 +105,50 @@ __device__ bool global_insert(const DictWorkspace& dw, const u64* k, u64 count,
   return false;
 }
 
-// LDS pre-aggregation table: 2,048 slots for a chunk of 1,024 tokens (load <= 0.5).
+// Persistent LDS cache of a workgroup: 1,024 slots (40 KB).  A workgroup streams its
+// tokens 256 at a time (one per thread) through the cache; a key found in (or claimed
+// in) the first kLdsProbes slots of its probe sequence is counted in LDS, any other key
+// goes straight to the HBM table.  Frequent keys get cached by the first chunks and stay
+// cached for the whole stream, so a Zipfian input costs ~one HBM atomic per frequent key
+// per workgroup.  The cache is flushed to the HBM table at the end.
 constexpr int kInsBlock = 256;
-constexpr int kInsPerThread = 4;
-constexpr int kInsChunk = kInsBlock * kInsPerThread;
-constexpr int kLdsSlots = 2048;
+constexpr int kLdsSlots = 1024;
+constexpr int kLdsProbes = 8;
 
 struct LdsSlot {
   u64 w[kKeyWords];  // w[0] raw (0 = empty), w[1..3] XOR kWordMagic (0 = not written)
   u64 count;
 };
+
+__device__ __forceinline__ bool lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h) {
+  u32 slot = (u32)(h >> 40) & (kLdsSlots - 1);
+  for (int probe = 0; probe < kLdsProbes;) {
+    LdsSlot& sl = tab[slot];
+    u64 w0 = sl.w[0];
+    if (w0 == 0) {
+      w0 = atomicCAS(reinterpret_cast<unsigned long long*>(&sl.w[0]), 0ull, (unsigned long long)k[0]);
+      if (w0 == 0) {
+#pragma unroll
+        for (int j = 1; j < kKeyWords; ++j) sl.w[j] = k[j] ^ kWordMagic;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c);
+        return true;
+      }
+    }
+    if (w0 == k[0]) {
+      const u64 x1 = __hip_atomic_load(&sl.w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const u64 x2 = __hip_atomic_load(&sl.w[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const u64 x3 = __hip_atomic_load(&sl.w[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (x1 == 0 || x2 == 0 || x3 == 0) continue;  // claimer (another wave) still writing
+      if ((x1 ^ kWordMagic) == k[1] && (x2 ^ kWordMagic) == k[2] && (x3 ^ kWordMagic) == k[3]) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c);
+        return true;
+      }
+    }
+    slot = (slot + 1) & (kLdsSlots - 1);
+    ++probe;
+  }
+  return false;
+}
 
 __global__ __launch_bounds__(kInsBlock) void dict_insert_kernel(ConstKeysSoA tokens,
                                                                 const u64* __restrict__ counts,
@@ -117,72 +156,37 @@ __global__ __launch_bounds__(kInsBlock) void dict_insert_kernel(ConstKeysSoA tok
                                                                 DictWorkspace dw,
                                                                 MapCounters* __restrict__ ctr) {
   __shared__ LdsSlot s_tab[kLdsSlots];
-  const u32 n = *d_n;
-  for (u32 c0 = blockIdx.x * kInsChunk; c0 < n; c0 += gridDim.x * kInsChunk) {
-    for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) {
+  for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) {
 #pragma unroll
-      for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
-      s_tab[i].count = 0;
-    }
-    // all loads of the chunk first (one latency), then the LDS inserts
-    u64 k[kInsPerThread][kKeyWords];
-    u64 c[kInsPerThread];
-#pragma unroll
-    for (int t = 0; t < kInsPerThread; ++t) {
-      const u32 i = c0 + t * kInsBlock + threadIdx.x;
-      const bool ok = i < n;
-#pragma unroll
-      for (int j = 0; j < kKeyWords; ++j) k[t][j] = ok ? tokens.w[j][i] : 0;
-      c[t] = ok ? (counts ? counts[i] : 1ull) : 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < kInsPerThread; ++t) {
-      if (!c[t] || k[t][0] == 0) continue;
-      u32 slot = (u32)key_hash(k[t]) & (kLdsSlots - 1);
-      for (;;) {
-        LdsSlot& sl = s_tab[slot];
-        u64 w0 = sl.w[0];
-        if (w0 == 0) {
-          w0 = atomicCAS(reinterpret_cast<unsigned long long*>(&sl.w[0]), 0ull,
-                         (unsigned long long)k[t][0]);
-          if (w0 == 0) {
-#pragma unroll
-            for (int j = 1; j < kKeyWords; ++j) sl.w[j] = k[t][j] ^ kWordMagic;
-            atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c[t]);
-            break;
-          }
-        }
-        if (w0 == k[t][0]) {
-          const u64 x1 = __hip_atomic_load(&sl.w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const u64 x2 = __hip_atomic_load(&sl.w[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const u64 x3 = __hip_atomic_load(&sl.w[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (x1 == 0 || x2 == 0 || x3 == 0) continue;  // claimer still writing
-          if ((x1 ^ kWordMagic) == k[t][1] && (x2 ^ kWordMagic) == k[t][2] &&
-              (x3 ^ kWordMagic) == k[t][3]) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c[t]);
-            break;
-          }
-        }
-        slot = (slot + 1) & (kLdsSlots - 1);
-      }
-    }
-    __syncthreads();
-    // flush the chunk's distinct keys to the HBM table
-    for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) {
-      const LdsSlot& sl = s_tab[i];
-      if (sl.w[0] == 0) continue;
-      const u64 kk[kKeyWords] = {sl.w[0], sl.w[1] ^ kWordMagic, sl.w[2] ^ kWordMagic,
-                                 sl.w[3] ^ kWordMagic};
-      if (!global_insert(dw, kk, sl.count, ctr, key_hash(kk))) atomicOr(&ctr->flags, kCtrDictOverflow);
-    }
-    __syncthreads();
+    for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
+    s_tab[i].count = 0;
   }
+  __syncthreads();
+  const u32 n = *d_n;
+  bool overflow = false;
+  for (u32 i = blockIdx.x * kInsBlock + threadIdx.x; i < n; i += gridDim.x * kInsBlock) {
+    u64 k[kKeyWords];
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) k[j] = tokens.w[j][i];
+    const u64 c = counts ? counts[i] : 1ull;
+    if (k[0] == 0 || c == 0) continue;
+    const u64 h = key_hash(k);
+    if (!lds_insert(s_tab, k, c, h)) overflow |= !global_insert(dw, k, c, ctr, h);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) {
+    const LdsSlot& sl = s_tab[i];
+    if (sl.w[0] == 0) continue;
+    const u64 kk[kKeyWords] = {sl.w[0], sl.w[1] ^ kWordMagic, sl.w[2] ^ kWordMagic,
+                               sl.w[3] ^ kWordMagic};
+    overflow |= !global_insert(dw, kk, sl.count, ctr, key_hash(kk));
+  }
+  if (overflow) atomicOr(&ctr->flags, kCtrDictOverflow);
 }
 
 // rank[i] += #{ j in tile : key[j] < key[i] }, persistent over (i-tile, j-tile) pairs.
 constexpr int kRankI = 256;
-constexpr int kRankJ = 1024;
+constexpr int kRankJ = 256;
 
 __device__ __forceinline__ bool key_lt(const u64* a, const u64* b) {
 #pragma unroll
@@ -191,10 +195,16 @@ __device__ __forceinline__ bool key_lt(const u64* a, const u64* b) {
   return false;
 }
 
+// With `counts`, val[i] also accumulates the total count of the smaller keys: the
+// "weighted rank" IS the reference's val (start of the key's run in the sorted token
+// array), so no scan over the sorted counts is needed afterwards.
 __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
+                                                           const u64* __restrict__ counts,
                                                            const u32* __restrict__ d_u,
-                                                           u32* __restrict__ rank) {
+                                                           u32* __restrict__ rank,
+                                                           u64* __restrict__ val) {
   __shared__ __attribute__((aligned(16))) u64 s_w0[kRankJ];
+  __shared__ __attribute__((aligned(16))) u64 s_cnt[kRankJ];
   __shared__ u64 s_rest[kRankJ][kKeyWords - 1];
   const u32 u = *d_u;
   if (u > (u32)kRankSortMax) return;  // radix path handles it
@@ -206,18 +216,20 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
     __syncthreads();  // previous pair's readers are done with the tile
     {
       constexpr int kTrips = kRankJ / kRankI;
-      u64 v[kTrips][kKeyWords];  // issue every load before any LDS store
+      u64 v[kTrips][kKeyWords], cv[kTrips];  // issue every load before any LDS store
 #pragma unroll
       for (int r = 0; r < kTrips; ++r) {
         const u32 t = threadIdx.x + r * kRankI;
 #pragma unroll
         for (int q = 0; q < kKeyWords; ++q) v[r][q] = t < jn ? keys.w[q][j0 + t] : 0;
+        cv[r] = (counts && t < jn) ? counts[j0 + t] : 0;
       }
 #pragma unroll
       for (int r = 0; r < kTrips; ++r) {
         const u32 t = threadIdx.x + r * kRankI;
         // padding keys are all-ones: never smaller than a real key
         s_w0[t] = t < jn ? v[r][0] : ~0ull;
+        s_cnt[t] = cv[r];
 #pragma unroll
         for (int q = 1; q < kKeyWords; ++q) s_rest[t][q - 1] = v[r][q];
       }
@@ -229,19 +241,22 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
 #pragma unroll
     for (int q = 0; q < kKeyWords; ++q) me[q] = keys.w[q][i];
     u32 cnt = 0, eq = 0;
-    // 16-byte broadcast reads, 8 keys per step, independent accumulations
-    for (u32 t = 0; t < (u32)kRankJ; t += 8) {
+    u64 acc = 0;
+    // 16-byte broadcast reads, 4 keys per step, independent accumulations
+    for (u32 t = 0; t < (u32)kRankJ; t += 4) {
       const uint4 a = *reinterpret_cast<const uint4*>(&s_w0[t]);
       const uint4 b = *reinterpret_cast<const uint4*>(&s_w0[t + 2]);
-      const uint4 c = *reinterpret_cast<const uint4*>(&s_w0[t + 4]);
-      const uint4 d = *reinterpret_cast<const uint4*>(&s_w0[t + 6]);
-      const u64 o[8] = {((u64)a.y << 32) | a.x, ((u64)a.w << 32) | a.z,
-                        ((u64)b.y << 32) | b.x, ((u64)b.w << 32) | b.z,
-                        ((u64)c.y << 32) | c.x, ((u64)c.w << 32) | c.z,
-                        ((u64)d.y << 32) | d.x, ((u64)d.w << 32) | d.z};
+      const uint4 ca = *reinterpret_cast<const uint4*>(&s_cnt[t]);
+      const uint4 cb = *reinterpret_cast<const uint4*>(&s_cnt[t + 2]);
+      const u64 o[4] = {((u64)a.y << 32) | a.x, ((u64)a.w << 32) | a.z,
+                        ((u64)b.y << 32) | b.x, ((u64)b.w << 32) | b.z};
+      const u64 oc[4] = {((u64)ca.y << 32) | ca.x, ((u64)ca.w << 32) | ca.z,
+                         ((u64)cb.y << 32) | cb.x, ((u64)cb.w << 32) | cb.z};
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        cnt += o[q] < me[0];
+      for (int q = 0; q < 4; ++q) {
+        const bool lt = o[q] < me[0];
+        cnt += lt;
+        acc += lt ? oc[q] : 0;
         eq += o[q] == me[0];
       }
     }
@@ -251,10 +266,52 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
       for (u32 t = 0; t < jn; ++t) {
         if (s_w0[t] != me[0] || j0 + t == i) continue;
         u64 other[kKeyWords] = {s_w0[t], s_rest[t][0], s_rest[t][1], s_rest[t][2]};
-        cnt += key_lt(other, me);
+        if (key_lt(other, me)) {
+          ++cnt;
+          acc += s_cnt[t];
+        }
       }
     }
-    if (cnt) atomicAdd(&rank[i], cnt);
+    if (cnt) {
+      atomicAdd(&rank[i], cnt);
+      if (val) atomicAdd(reinterpret_cast<unsigned long long*>(&val[i]), (unsigned long long)acc);
+    }
+  }
+}
+
+// Output records straight from the weighted ranks: out[rank[i]] = {key i, val i, count i}.
+// `out` may be host-mapped pinned memory (zero-copy: the records travel over PCIe as the
+// kernel writes them, and the host needs no D2H copy).  `ctr_out` (optional, host-mapped)
+// receives the final counters.
+__global__ __launch_bounds__(256) void rank_emit_kernel(ConstKeysSoA keys,
+                                                        const u64* __restrict__ counts,
+                                                        const u32* __restrict__ rank,
+                                                        const u64* __restrict__ val,
+                                                        const MapCounters* __restrict__ ctr,
+                                                        OutRecord* __restrict__ out,
+                                                        MapCounters* __restrict__ ctr_out) {
+  const u32 u = ctr->num_unique;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
+    // field by field: total_count belongs to the thread that emits rank u-1
+    ctr_out->num_records = ctr->num_records;
+    ctr_out->num_unique = u;
+    ctr_out->overflow_lines = ctr->overflow_lines;
+    ctr_out->truncated = ctr->truncated;
+    ctr_out->num_newlines = ctr->num_newlines;
+    ctr_out->max_key_len = ctr->max_key_len;
+    ctr_out->flags = ctr->flags | (u > (u32)kRankSortMax ? kCtrNotEmitted : 0u);
+    if (u == 0) ctr_out->total_count = 0;
+  }
+  if (u > (u32)kRankSortMax) return;
+  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < u; i += gridDim.x * 256) {
+    const u32 r = rank[i];
+    OutRecord rec;
+#pragma unroll
+    for (int q = 0; q < kKeyWords; ++q) rec.w[q] = keys.w[q][i];
+    rec.val = val[i];
+    rec.count = counts[i];
+    out[r] = rec;
+    if (r == u - 1 && ctr_out) ctr_out->total_count = rec.val + rec.count;
   }
 }
 
@@ -327,17 +384,26 @@ u32 grid_for(u64 n, u32 block, u32 max_blocks = 2048) {
 
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,
                         const DictWorkspace& dw, MapCounters* ctr, hipStream_t s) {
-  dict_insert_kernel<<<dim3(grid_for(cap, kInsChunk, 4096)), dim3(kInsBlock), 0, s>>>(
+  dict_insert_kernel<<<dim3(grid_for(cap, kInsBlock, 1024)), dim3(kInsBlock), 0, s>>>(
       tokens, counts, d_n, dw, ctr);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
-void launch_rank_sort(ConstKeysSoA keys, const u32* d_u, u64 cap, u32* rank, hipStream_t s) {
+void launch_rank_sort(ConstKeysSoA keys, const u64* counts, const u32* d_u, u64 cap, u32* rank,
+                      u64* val, hipStream_t s) {
   // persistent grid: enough blocks to cover every CU a few times for the largest U
   const u64 umax = cap < (u64)kRankSortMax ? cap : (u64)kRankSortMax;
   const u64 pairs = div_up(umax, kRankI) * div_up(umax, kRankJ);
   const u32 grid = (u32)(pairs < 2048 ? (pairs ? pairs : 1) : 2048);
-  rank_sort_kernel<<<dim3(grid), dim3(kRankI), 0, s>>>(keys, d_u, rank);
+  rank_sort_kernel<<<dim3(grid), dim3(kRankI), 0, s>>>(keys, counts, d_u, rank, val);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_rank_emit(ConstKeysSoA keys, const u64* counts, const u32* rank, const u64* val,
+                      u64 cap, const MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                      hipStream_t s) {
+  rank_emit_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(keys, counts, rank, val, ctr,
+                                                                 out, ctr_out);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
