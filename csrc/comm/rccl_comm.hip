@@ -55,6 +55,8 @@ class RcclComm final : public Communicator {
     }
     if (d_stage_) (void)hipFree(d_stage_);
     if (h_stage_) (void)hipHostFree(h_stage_);
+    if (d_gsend_) (void)hipFree(d_gsend_);
+    if (d_grecv_) (void)hipFree(d_grecv_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
 
@@ -76,45 +78,42 @@ class RcclComm final : public Communicator {
 
   void gatherv_host(const void* send, u64 bytes, std::vector<char>* recv_at_root,
                     std::vector<u64>* sizes_at_root, int root) override {
-    // Sizes over RCCL, payload over grouped send/recv through device staging buffers.
     std::vector<u64> sizes((size_t)world_);
     allgather_host(&bytes, sizes.data(), sizeof(u64));
-    u64 total = 0, maxb = 0;
-    for (u64 s : sizes) {
-      total += s;
-      maxb = std::max(maxb, s);
+    u64 total = 0;
+    for (u64 s : sizes) total += s;
+    if (rank_ == root) recv_at_root->resize(total);
+    gatherv_known(send, bytes, sizes.data(), rank_ == root ? recv_at_root->data() : nullptr, root);
+    if (rank_ == root && sizes_at_root) *sizes_at_root = sizes;
+  }
+
+  // Payload over grouped send/recv through persistent device staging buffers.
+  void gatherv_known(const void* send, u64 bytes, const u64* sizes, void* recv_at_root,
+                     int root) override {
+    u64 total = 0;
+    for (int r = 0; r < world_; ++r) total += sizes[r];
+    ensure_gather(std::max<u64>(bytes, 1), rank_ == root ? std::max<u64>(total, 1) : 1);
+    if (bytes) LOCUST_HIP_CHECK(hipMemcpyAsync(d_gsend_, send, bytes, hipMemcpyHostToDevice, stream_));
+    if (rank_ == root && bytes) {
+      u64 off = 0;
+      for (int r = 0; r < root; ++r) off += sizes[r];
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_grecv_ + off, d_gsend_, bytes, hipMemcpyDeviceToDevice, stream_));
     }
-    char* dsend = nullptr;
-    char* drecv = nullptr;
-    LOCUST_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dsend), std::max<u64>(bytes, 1), stream_));
-    if (rank_ == root)
-      LOCUST_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&drecv), std::max<u64>(total, 1), stream_));
-    if (bytes) LOCUST_HIP_CHECK(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_));
     LOCUST_RCCL_CHECK(ncclGroupStart());
     if (rank_ == root) {
       u64 off = 0;
       for (int r = 0; r < world_; ++r) {
-        if (r == root) {
-          if (bytes) LOCUST_HIP_CHECK(hipMemcpyAsync(drecv + off, dsend, bytes, hipMemcpyDeviceToDevice, stream_));
-        } else if (sizes[(size_t)r]) {
-          LOCUST_RCCL_CHECK(ncclRecv(drecv + off, sizes[(size_t)r], ncclUint8, r, comm_, stream_));
-        }
-        off += sizes[(size_t)r];
+        if (r != root && sizes[r])
+          LOCUST_RCCL_CHECK(ncclRecv(d_grecv_ + off, sizes[r], ncclUint8, r, comm_, stream_));
+        off += sizes[r];
       }
     } else if (bytes) {
-      LOCUST_RCCL_CHECK(ncclSend(dsend, bytes, ncclUint8, root, comm_, stream_));
+      LOCUST_RCCL_CHECK(ncclSend(d_gsend_, bytes, ncclUint8, root, comm_, stream_));
     }
     LOCUST_RCCL_CHECK(ncclGroupEnd());
-    if (rank_ == root) {
-      recv_at_root->resize(total);
-      if (total)
-        LOCUST_HIP_CHECK(hipMemcpyAsync(recv_at_root->data(), drecv, total, hipMemcpyDeviceToHost, stream_));
-      if (sizes_at_root) *sizes_at_root = sizes;
-    }
-    LOCUST_HIP_CHECK(hipFreeAsync(dsend, stream_));
-    if (drecv) LOCUST_HIP_CHECK(hipFreeAsync(drecv, stream_));
+    if (rank_ == root && total)
+      LOCUST_HIP_CHECK(hipMemcpyAsync(recv_at_root, d_grecv_, total, hipMemcpyDeviceToHost, stream_));
     wait(stream_);
-    (void)maxb;
   }
 
   void barrier() override {
@@ -144,6 +143,21 @@ class RcclComm final : public Communicator {
   }
 
  private:
+  void ensure_gather(u64 send_bytes, u64 recv_bytes) {
+    if (send_bytes > gsend_cap_) {
+      wait(stream_);
+      if (d_gsend_) (void)hipFree(d_gsend_);
+      gsend_cap_ = align_up(send_bytes * 2, 1 << 16);
+      LOCUST_HIP_CHECK(hipMalloc(&d_gsend_, gsend_cap_));
+    }
+    if (recv_bytes > grecv_cap_) {
+      wait(stream_);
+      if (d_grecv_) (void)hipFree(d_grecv_);
+      grecv_cap_ = align_up(recv_bytes * 2, 1 << 16);
+      LOCUST_HIP_CHECK(hipMalloc(&d_grecv_, grecv_cap_));
+    }
+  }
+
   void ensure_stage(u64 bytes) {
     if (bytes <= stage_cap_) return;
     wait(stream_);
@@ -185,6 +199,9 @@ class RcclComm final : public Communicator {
   char* d_stage_ = nullptr;
   char* h_stage_ = nullptr;
   u64 stage_cap_ = 0;
+  char* d_gsend_ = nullptr;
+  char* d_grecv_ = nullptr;
+  u64 gsend_cap_ = 0, grecv_cap_ = 0;
 };
 
 }  // namespace

@@ -33,6 +33,18 @@ int Communicator::agree(int local_error) {
   return -1;
 }
 
+void Communicator::gatherv_known(const void* send, u64 bytes, const u64* sizes,
+                                 void* recv_at_root, int root) {
+  std::vector<char> buf;
+  gatherv_host(send, bytes, &buf, nullptr, root);
+  u64 total = 0;
+  for (int r = 0; r < size(); ++r) total += sizes[r];
+  if (rank() == root && total) {
+    if (buf.size() != total) throw Error("gatherv_known: size mismatch");
+    std::memcpy(recv_at_root, buf.data(), total);
+  }
+}
+
 namespace {
 
 void set_timeouts(int fd, double timeout_s) {

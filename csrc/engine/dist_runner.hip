@@ -9,6 +9,14 @@
 
 namespace locust {
 
+void copy_device(void* dst, const void* src, u64 bytes, bool to_host, void* stream) {
+  if (!bytes) return;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  LOCUST_HIP_CHECK(hipMemcpyAsync(dst, src, bytes,
+                                  to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice, s));
+  LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole) {
   const int P = cfg.world;
   LOCUST_CHECK_ARG(P >= 1, "world must be >= 1");

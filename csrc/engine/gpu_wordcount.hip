@@ -568,6 +568,7 @@ class GpuShardEngine final : public ShardEngine {
 
   bool device_buffers() const override { return true; }
   void* stream() override { return mp_->stream; }
+  char* input_buffer() override { return mp_->h_text; }
 
   u64 map_local(const TextInput& shard, bool combine) override {
     DevicePipeline& m = *mp_;
@@ -575,11 +576,28 @@ class GpuShardEngine final : public ShardEngine {
     m.enqueue_upload(shard);
     m.enqueue_map(shard);
     const bool compat = cfg_.map_path == MapPath::kCompat;
+    samples_valid_ = false;
     if (combine && cfg_.sort_path == SortPath::kDict) {
-      // Map-side combine through the dictionary: sorted distinct keys + counts.
+      // Map-side combine through the dictionary: sorted distinct keys + counts.  The
+      // shuffle records and the splitter samples are produced speculatively in the same
+      // stream, so the common case costs ONE host synchronisation.
       m.enqueue_process_dict((u32)shard.num_lines, compat);
       m.enqueue_sorted_from_dict();
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+      launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                      hipMemcpyDeviceToHost, m.stream));
       m.read_counters();
+      if (!m.dict_fallback_needed()) {
+        samples_.assign(m.h_small, m.h_small + kSpecSamples);
+        samples_valid_ = true;
+        local_stats_ = WordCountResult();
+        local_stats_.num_lines = shard.num_lines;
+        m.fill_counters(local_stats_);
+        local_stats_.num_tokens = m.h_ctr->num_records;
+        return m.h_ctr->num_unique;
+      }
       if (m.dict_fallback_needed()) {
         if (m.h_ctr->flags & kCtrDictOverflow) {
           m.enqueue_process(0, false, false, m.h_ctr->num_records);
@@ -614,6 +632,7 @@ class GpuShardEngine final : public ShardEngine {
 
   std::vector<PackedKey> sample(u32 s) override {
     DevicePipeline& m = *mp_;
+    if (samples_valid_ && s == kSpecSamples) return samples_;
     LOCUST_CHECK_ARG(s <= kMaxSamples, "too many samples");
     launch_sample_keys(local_keys(), local_n(), s, m.d_samples, m.stream);
     LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, s * sizeof(PackedKey),
@@ -703,7 +722,10 @@ class GpuShardEngine final : public ShardEngine {
 
   JobConfig cfg_;
   std::unique_ptr<DevicePipeline> mp_, rp_;
+  static constexpr u32 kSpecSamples = 64;  // DistConfig::samples_per_rank default
   ConstKeysSoA local_keys_{};
+  std::vector<PackedKey> samples_;
+  bool samples_valid_ = false;
   std::vector<WordCountEntry> range_entries_;
   const u64* local_counts_ = nullptr;
   const u32* local_n_ = nullptr;

@@ -26,6 +26,7 @@ using u8 = uint8_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
 using i64 = int64_t;
+using i32 = int32_t;
 
 class Error : public std::runtime_error {
  public:

@@ -43,6 +43,9 @@ class Communicator {
   virtual void gatherv_host(const void* send, u64 bytes, std::vector<char>* recv_at_root,
                             std::vector<u64>* sizes_at_root, int root) = 0;
   virtual void barrier() = 0;
+  // gatherv when every rank already knows all sizes (host buffers; recv only at root).
+  virtual void gatherv_known(const void* send, u64 bytes, const u64* sizes, void* recv_at_root,
+                             int root);
 
   // ---- data plane: engine buffers, byte counts/offsets per peer (host arrays) ----
   // Blocking: returns when this rank's receives are complete and its sends may be reused.
@@ -83,6 +86,9 @@ class ShardEngine {
   virtual ~ShardEngine() = default;
   virtual bool device_buffers() const = 0;
   virtual void* stream() = 0;
+  // Pinned host staging buffer for the shard text (nullptr if the engine has none).  A
+  // shard whose data already points here is uploaded without a host copy.
+  virtual char* input_buffer() { return nullptr; }
   // Map + sort (+ combine) this rank's shard.  Returns the number of local records.
   virtual u64 map_local(const TextInput& shard, bool combine) = 0;
   virtual std::vector<PackedKey> sample(u32 num_samples) = 0;
@@ -118,6 +124,9 @@ struct DistResult {
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
                            const TextInput& shard);
+
+// Synchronous device<->host copy on `stream` (implemented in the HIP part of the library).
+void copy_device(void* dst, const void* src, u64 bytes, bool to_host, void* stream);
 
 // Split a line-aligned text into `parts` line-aligned shards of ~equal bytes.
 std::vector<TextInput> shard_text(const TextInput& in, int parts);

@@ -155,7 +155,7 @@ class PyDistRank {
  public:
   PyDistRank(const DistConfig& cfg, int rank, const std::string& comm, const std::string& host,
              int port, u64 max_bytes, u64 max_lines, double timeout_s)
-      : cfg_(cfg) {
+      : cfg_(cfg), max_bytes_(max_bytes) {
     py::gil_scoped_release nogil;
     if (comm == "tcp") {
       comm_ = make_tcp_comm(rank, cfg.world, host, port, timeout_s);
@@ -173,6 +173,30 @@ class PyDistRank {
     {
       py::gil_scoped_release nogil;
       d = run_distributed(cfg_, *comm_, *eng_, in);
+    }
+    return py::make_tuple(PyResult{d.result}, dist_to_dict(d));
+  }
+  // Keep the shard resident (in the engine's pinned buffer when it has one) so repeated
+  // runs skip the Python->native copy, like GpuEngine.load().
+  void load(const std::string& shard_text_bytes, u64 first_line) {
+    loaded_in_ = as_input(shard_text_bytes, first_line);
+    char* pinned = eng_->input_buffer();
+    if (pinned) {
+      LOCUST_CHECK_ARG(shard_text_bytes.size() <= max_bytes_, "shard exceeds engine capacity");
+      std::memcpy(pinned, shard_text_bytes.data(), shard_text_bytes.size());
+      loaded_in_.data = pinned;
+    } else {
+      loaded_text_ = shard_text_bytes;
+      loaded_in_.data = loaded_text_.data();
+    }
+    loaded_ = true;
+  }
+  py::tuple run_loaded() {
+    LOCUST_CHECK_ARG(loaded_, "call load() first");
+    DistResult d;
+    {
+      py::gil_scoped_release nogil;
+      d = run_distributed(cfg_, *comm_, *eng_, loaded_in_);
     }
     return py::make_tuple(PyResult{d.result}, dist_to_dict(d));
   }
@@ -196,8 +220,12 @@ class PyDistRank {
 
  private:
   DistConfig cfg_;
+  u64 max_bytes_;
   std::unique_ptr<Communicator> comm_;
   std::unique_ptr<ShardEngine> eng_;
+  bool loaded_ = false;
+  std::string loaded_text_;
+  TextInput loaded_in_;
 };
 
 }  // namespace
@@ -275,6 +303,8 @@ PYBIND11_MODULE(_locust, m) {
            py::arg("cfg"), py::arg("rank"), py::arg("comm"), py::arg("host"), py::arg("port"),
            py::arg("max_bytes"), py::arg("max_lines"), py::arg("timeout_s") = 300.0)
       .def("run", &PyDistRank::run, py::arg("shard"), py::arg("first_line") = 0)
+      .def("load", &PyDistRank::load, py::arg("shard"), py::arg("first_line") = 0)
+      .def("run_loaded", &PyDistRank::run_loaded)
       .def("barrier", &PyDistRank::barrier)
       .def("allreduce_max", &PyDistRank::allreduce_max)
       .def_property_readonly("rank", &PyDistRank::rank)
