@@ -96,6 +96,13 @@ def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, loca
         os.dup2(saved, 1)
         os.close(saved)
     dr.load(text, 0)  # the shard sits in the engine's pinned buffer, like a loaded file
+    return dr
+
+
+def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
+    import locust_amd as lc
+
+    dr.set_strategy(getattr(lc._C.DistStrategy, strategy))
     for _ in range(warmup):
         dr.run_loaded()
     parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": []}
@@ -110,7 +117,7 @@ def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, loca
     mine = (t1 - t0) * 1e3 / steps
     ms = dr.allreduce_max(mine)
     med = {k: statistics.median(v) for k, v in parts.items()}
-    return ms, med, res, dr
+    return ms, med, res, info["strategy"]
 
 
 def main() -> int:
@@ -122,6 +129,9 @@ def main() -> int:
     ap.add_argument("--no-extra", action="store_true", help="skip the 700-line side measurement")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "tcp"],
                     help="communicator for N>1 (tcp: rehearsal with ranks sharing one GPU)")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "shuffle", "gather"],
+                    help="N>1: after-map strategy (auto: gather-to-root for small combined "
+                         "outputs, sample-sort all-to-all shuffle otherwise)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the distributed path even for one rank")
     args = ap.parse_args()
@@ -136,6 +146,7 @@ def main() -> int:
     text = load_text(args.config)
     nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
     extra = {}
+    strategy = None
     if n == 1 and not args.force_dist:
         ms, stages, res = bench_single(text, args.steps, args.warmup)
         if not args.no_extra and args.config == "hamlet4500":
@@ -149,8 +160,13 @@ def main() -> int:
             extra["radix_path"] = {"ms_per_step": round(msr, 4),
                                    "stages_ms": {k: round(v, 4) for k, v in str_.items()}}
     else:
-        ms, stages, res, dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank,
-                                         args.comm)
+        dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank, args.comm)
+        ms, stages, res, strategy = time_dist(dr, args.steps, args.warmup, args.strategy)
+        if not args.no_extra and args.strategy == "auto":
+            # The sample-sort all-to-all shuffle on the same job (the path large inputs take).
+            mss, sts, _, _ = time_dist(dr, args.steps, args.warmup, "shuffle")
+            extra["shuffle_path"] = {"ms_per_step": round(mss, 4),
+                                     "stages_ms": {k: round(v, 4) for k, v in sts.items()}}
     if rank != 0:
         return 0
     base = BASELINE_MS[args.config]
@@ -173,7 +189,8 @@ def main() -> int:
                      "full H2D->D2H job per step",
             "global_batch": nlines * n,
             "seq_len": len(text),
-            "parallelism": f"dp{n}" + ("+rccl_alltoallv_shuffle" if n > 1 else ""),
+            "parallelism": f"dp{n}" + ({"gather": "+rccl_p2p_gather_merge",
+                                        "shuffle": "+rccl_alltoallv_shuffle"}.get(strategy, "")),
         },
         "baseline_ms": base,
         "baseline_stages_ms": BASELINE_STAGES[args.config],

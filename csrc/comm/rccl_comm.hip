@@ -68,7 +68,10 @@ class RcclComm final : public Communicator {
   void allgather_host(const void* send, void* recv, u64 bytes) override {
     ensure_stage(bytes);
     char* dsend = d_stage_ + (u64)world_ * stage_cap_;
-    LOCUST_HIP_CHECK(hipMemcpyAsync(dsend, send, bytes, hipMemcpyHostToDevice, stream_));
+    // through the pinned slot: a pageable H2D would be a synchronous staged copy
+    char* hsend = h_stage_ + (u64)world_ * stage_cap_;
+    std::memcpy(hsend, send, bytes);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(dsend, hsend, bytes, hipMemcpyHostToDevice, stream_));
     LOCUST_RCCL_CHECK(ncclAllGather(dsend, d_stage_, bytes, ncclUint8, comm_, stream_));
     LOCUST_HIP_CHECK(hipMemcpyAsync(h_stage_, d_stage_, bytes * (u64)world_,
                                     hipMemcpyDeviceToHost, stream_));

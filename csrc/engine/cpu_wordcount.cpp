@@ -111,7 +111,7 @@ class CpuShardEngine final : public ShardEngine {
   bool device_buffers() const override { return false; }
   void* stream() override { return nullptr; }
 
-  u64 map_local(const TextInput& shard, bool combine) override {
+  u64 map_local(const TextInput& shard, bool combine, DistStrategy) override {
     CpuWordCount eng(cfg_);
     stats_ = WordCountResult();
     std::vector<PackedKey> toks = eng.run_map_stage(shard, &stats_);
@@ -191,6 +191,12 @@ class CpuShardEngine final : public ShardEngine {
     }
     *total_count = pos;
     *num_unique = out_.size();
+  }
+
+  void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) override {
+    recv_.resize(std::max<u64>(n_other + local_.size(), 1));
+    std::copy(local_.begin(), local_.end(), recv_.begin() + (long)n_other);
+    reduce_received(n_other + local_.size(), total_count, num_unique);
   }
 
   void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {

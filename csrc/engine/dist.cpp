@@ -77,16 +77,17 @@ std::vector<PackedKey> choose_splitters(const std::vector<PackedKey>& samples, u
 }  // namespace
 
 // Control-plane messages: every allgather carries the status word of the stage before it,
-// so failure agreement costs no extra collective.  Three allgathers per job.
+// so failure agreement costs no extra collective.  Msg1 also carries the map statistics,
+// so the gather strategy needs no further control traffic.
 struct alignas(8) Msg1 {  // after map + sampling
   i32 status;
   u32 pad;
-  u64 n_local;
+  u64 n_local, lines, tokens, overflow, truncated, max_key_len;
 };
-struct alignas(8) Msg3 {  // after the reduce of the received key range
+struct alignas(8) Msg3 {  // after the reduce of the received key range (shuffle strategy)
   i32 status;
   u32 pad;
-  u64 total, uniq, lines, tokens, overflow, truncated, max_key_len;
+  u64 total, uniq;
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
@@ -119,15 +120,44 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
                     std::to_string(r) + (r == me ? ": " + local_msg : ""));
     }
   };
+  // Data-plane exchange through the engine's buffers; a device engine over a host-only
+  // communicator (TCP) stages through host memory -- that is how several GPU ranks can
+  // share one device in tests (RCCL refuses that).
+  auto exchange = [&](u64 n_send, const u64* sb, const u64* so, void* recv, u64 n_recv,
+                      const u64* rb, const u64* ro, bool recv_ok) {
+    if (eng.device_buffers() && !comm.device_buffers()) {
+      std::vector<KeyCount> hs(std::max<u64>(n_send, 1)), hr(std::max<u64>(n_recv, 1));
+      copy_device(hs.data(), eng.send_records(), n_send * sizeof(KeyCount), /*to_host=*/true,
+                  eng.stream());
+      comm.alltoallv(hs.data(), sb, so, hr.data(), rb, ro, nullptr);
+      if (recv_ok && n_recv)
+        copy_device(recv, hr.data(), n_recv * sizeof(KeyCount), /*to_host=*/false, eng.stream());
+    } else {
+      comm.alltoallv(eng.send_records(), sb, so, recv, rb, ro, eng.stream());
+    }
+    for (int p = 0; p < P; ++p) {
+      if (p != me) {
+        res.sent_bytes += sb[p];
+        res.recv_bytes += rb[p];
+      }
+    }
+  };
 
   const u64 t0 = now_ns();
   const u32 S = std::max<u32>(cfg.samples_per_rank, 1);
   // ---------------- map + sample, one allgather ----------------
   u64 n_local = 0;
   std::vector<PackedKey> mine_samples;
+  WordCountResult local_stats;
+  // The strategy is only known after the first allgather; the engine prepares for the
+  // predicted one (kAuto: whatever the previous job took) and patches up a mispredict.
+  const DistStrategy plan = !cfg.gather ? DistStrategy::kShuffle
+                            : cfg.strategy == DistStrategy::kAuto ? eng.last_strategy
+                                                                  : cfg.strategy;
   const i32 st1 = local("map", [&] {
-    n_local = eng.map_local(shard, cfg.job.combine);
-    mine_samples = eng.sample(S);
+    n_local = eng.map_local(shard, cfg.job.combine, plan);
+    if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
+    eng.map_stats(&local_stats);
   });
   if (mine_samples.size() != S) mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});
   res.local_records = n_local;
@@ -135,7 +165,8 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const u64 m1 = sizeof(Msg1) + (u64)S * sizeof(PackedKey);
   std::vector<char> out1(m1), all1(m1 * (u64)P);
   {
-    Msg1 h{st1, 0, n_local};
+    Msg1 h{st1, 0, n_local, shard.num_lines, local_stats.num_tokens, local_stats.overflow_lines,
+           local_stats.truncated, local_stats.max_key_len};
     std::memcpy(out1.data(), &h, sizeof(h));
     std::memcpy(out1.data() + sizeof(h), mine_samples.data(), (u64)S * sizeof(PackedKey));
   }
@@ -143,12 +174,87 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   check("map", reinterpret_cast<const i32*>(all1.data()), m1);
   std::vector<PackedKey> samples((size_t)P * S);
   std::vector<u64> counts((size_t)P);
-  for (int r = 0; r < P; ++r) {
-    const char* base = all1.data() + (u64)r * m1;
+  u64 sum_records = 0;
+  WordCountResult& r = res.result;
+  for (int p = 0; p < P; ++p) {
+    const char* base = all1.data() + (u64)p * m1;
     Msg1 h;
     std::memcpy(&h, base, sizeof(h));
-    counts[(size_t)r] = h.n_local;
-    std::memcpy(&samples[(size_t)r * S], base + sizeof(h), (u64)S * sizeof(PackedKey));
+    counts[(size_t)p] = h.n_local;
+    sum_records += h.n_local;
+    std::memcpy(&samples[(size_t)p * S], base + sizeof(h), (u64)S * sizeof(PackedKey));
+    r.num_lines += h.lines;
+    r.num_tokens += h.tokens;
+    r.overflow_lines += h.overflow;
+    r.truncated += h.truncated;
+    r.max_key_len = std::max(r.max_key_len, h.max_key_len);
+  }
+  const bool use_gather =
+      cfg.gather && (cfg.strategy == DistStrategy::kGather ||
+                     (cfg.strategy == DistStrategy::kAuto && sum_records <= cfg.gather_max_records));
+  res.strategy = use_gather ? DistStrategy::kGather : DistStrategy::kShuffle;
+  eng.last_strategy = res.strategy;
+  std::vector<u64> sb((size_t)P, 0), so((size_t)P, 0), rb((size_t)P, 0), ro((size_t)P, 0);
+
+  if (use_gather) {
+    // ---------------- gather-to-root: one grouped send/recv ----------------
+    const u64 rec = sizeof(KeyCount);
+    sb[0] = n_local * rec;
+    void* recv = nullptr;
+    i32 st = 0;
+    if (me == 0) {
+      // The root's own records stay put (reduce_gathered merges them in place); the
+      // others land back to back at the start of the receive buffer.
+      sb[0] = 0;
+      u64 off = 0;
+      for (int p = 1; p < P; ++p) {
+        rb[(size_t)p] = counts[(size_t)p] * rec;
+        ro[(size_t)p] = off;
+        off += rb[(size_t)p];
+      }
+      st = local("shuffle", [&] { recv = eng.recv_records(sum_records); });
+    }
+    exchange(n_local, sb.data(), so.data(), recv, me == 0 ? sum_records : 0, rb.data(), ro.data(),
+             st == 0);
+    const u64 t2 = now_ns();
+    if (me == 0) {
+      // The root merges: a failure here is the job's failure (only the root holds output).
+      u64 total = 0, uniq = 0;
+      if (!st)
+        st = local("reduce", [&] { eng.reduce_gathered(sum_records - n_local, &total, &uniq); });
+      if (st)
+        throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
+      eng.finalize(0, &r.entries);
+      res.range_tokens = total;
+      res.range_unique = uniq;
+    }
+    r.num_unique = r.entries.size();
+    const u64 t3 = now_ns();
+    res.map_ms = (t1 - t0) * 1e-6;
+    res.shuffle_ms = (t2 - t1) * 1e-6;
+    res.reduce_ms = (t3 - t2) * 1e-6;
+    res.gather_ms = 0;
+    res.total_ms = (t3 - t0) * 1e-6;
+    r.times.map_ms = res.map_ms;
+    r.times.process_ms = res.shuffle_ms;
+    r.times.reduce_ms = res.reduce_ms;
+    r.times.wall_ms = res.total_ms;
+    return res;
+  }
+
+  if (plan == DistStrategy::kGather) {
+    // Mispredicted: the map prepared for the gather (no samples).  Sort locally and run
+    // the sampling round now.
+    std::vector<char> out2(sizeof(i32) + (u64)S * sizeof(PackedKey)), all2(out2.size() * (u64)P);
+    const i32 st = local("map", [&] { mine_samples = eng.sample(S); });
+    if (mine_samples.size() != S) mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});
+    std::memcpy(out2.data(), &st, sizeof(i32));
+    std::memcpy(out2.data() + sizeof(i32), mine_samples.data(), (u64)S * sizeof(PackedKey));
+    comm.allgather_host(out2.data(), all2.data(), out2.size());
+    check("map", reinterpret_cast<const i32*>(all2.data()), out2.size());
+    for (int p = 0; p < P; ++p)
+      std::memcpy(&samples[(size_t)p * S], all2.data() + (u64)p * out2.size() + sizeof(i32),
+                  (u64)S * sizeof(PackedKey));
   }
   const std::vector<PackedKey> splitters = choose_splitters(samples, S, counts, P);
 
@@ -161,15 +267,14 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   for (int p = 0; p < P; ++p) msg2[(size_t)p + 1] = offs[(size_t)p + 1] - offs[(size_t)p];
   comm.allgather_host(msg2.data(), matrix.data(), ((u64)P + 1) * sizeof(u64));
   check("partition", reinterpret_cast<const i32*>(matrix.data()), ((u64)P + 1) * sizeof(u64));
-  std::vector<u64> sb((size_t)P), so((size_t)P), rb((size_t)P), ro((size_t)P);
   u64 n_recv = 0;
   for (int p = 0; p < P; ++p) {
     sb[(size_t)p] = msg2[(size_t)p + 1] * sizeof(KeyCount);
     so[(size_t)p] = offs[(size_t)p] * sizeof(KeyCount);
-    const u64 r = matrix[(size_t)p * (P + 1) + 1 + me];
-    rb[(size_t)p] = r * sizeof(KeyCount);
+    const u64 c = matrix[(size_t)p * (P + 1) + 1 + me];
+    rb[(size_t)p] = c * sizeof(KeyCount);
     ro[(size_t)p] = n_recv * sizeof(KeyCount);
-    n_recv += r;
+    n_recv += c;
   }
 
   // ---------------- shuffle ----------------
@@ -177,34 +282,13 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   // status below (the all-to-all itself must be entered by every rank).
   void* recv = nullptr;
   i32 st3 = local("shuffle", [&] { recv = eng.recv_records(n_recv); });
-  if (st3) n_recv = 0;  // still participate with empty receives
-  if (eng.device_buffers() && !comm.device_buffers()) {
-    // Device engine over a host-only communicator (TCP): stage through host memory.  This
-    // is how several GPU ranks can share one device in tests (RCCL refuses that).
-    std::vector<KeyCount> hs(n_local), hr(std::max<u64>(n_recv, 1));
-    copy_device(hs.data(), eng.send_records(), n_local * sizeof(KeyCount), /*to_host=*/true,
-                eng.stream());
-    comm.alltoallv(hs.data(), sb.data(), so.data(), hr.data(), rb.data(), ro.data(), nullptr);
-    if (!st3) copy_device(recv, hr.data(), n_recv * sizeof(KeyCount), /*to_host=*/false, eng.stream());
-  } else {
-    comm.alltoallv(eng.send_records(), sb.data(), so.data(), recv, rb.data(), ro.data(),
-                   eng.stream());
-  }
-  for (int p = 0; p < P; ++p) {
-    if (p != me) {
-      res.sent_bytes += sb[(size_t)p];
-      res.recv_bytes += rb[(size_t)p];
-    }
-  }
+  exchange(n_local, sb.data(), so.data(), recv, n_recv, rb.data(), ro.data(), st3 == 0);
   const u64 t2 = now_ns();
 
-  // ---------------- reduce, one allgather of {status, totals, map stats} ----------------
+  // ---------------- reduce, one allgather of {status, totals} ----------------
   u64 total = 0, uniq = 0;
   if (!st3) st3 = local("reduce", [&] { eng.reduce_received(n_recv, &total, &uniq); });
-  WordCountResult local_stats;
-  eng.map_stats(&local_stats);
-  Msg3 m3{st3, 0, total, uniq, shard.num_lines, local_stats.num_tokens, local_stats.overflow_lines,
-          local_stats.truncated, local_stats.max_key_len};
+  Msg3 m3{st3, 0, total, uniq};
   std::vector<Msg3> all3((size_t)P);
   comm.allgather_host(&m3, all3.data(), sizeof(Msg3));
   check("reduce", &all3[0].status, sizeof(Msg3));
@@ -217,14 +301,6 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const u64 t3 = now_ns();
 
   // ---------------- gather ----------------
-  WordCountResult& r = res.result;
-  for (const auto& s : all3) {
-    r.num_lines += s.lines;
-    r.num_tokens += s.tokens;
-    r.overflow_lines += s.overflow;
-    r.truncated += s.truncated;
-    r.max_key_len = std::max(r.max_key_len, s.max_key_len);
-  }
   if (cfg.gather) {
     std::vector<u64> sizes((size_t)P);
     u64 all_uniq = 0;

@@ -17,9 +17,15 @@ void copy_device(void* dst, const void* src, u64 bytes, bool to_host, void* stre
   LOCUST_HIP_CHECK(hipStreamSynchronize(s));
 }
 
-DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole) {
+std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig>& schedule,
+                                                    const TextInput& whole) {
+  LOCUST_CHECK_ARG(!schedule.empty(), "empty job schedule");
+  const DistConfig& cfg = schedule[0];
   const int P = cfg.world;
   LOCUST_CHECK_ARG(P >= 1, "world must be >= 1");
+  for (const auto& c : schedule)
+    LOCUST_CHECK_ARG(c.world == P && c.job.backend == cfg.job.backend,
+                     "every job of a schedule runs on the same ranks");
   const bool gpu = cfg.job.backend == Backend::kGpu;
   int ndev = 1;
   if (gpu) {
@@ -28,7 +34,7 @@ DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& 
   }
   std::vector<TextInput> shards = shard_text(whole, P);
   LoopbackGroup group(P, gpu);
-  std::vector<DistResult> results((size_t)P);
+  std::vector<DistResult> results(schedule.size());
   std::vector<std::exception_ptr> errors((size_t)P);
   std::vector<std::thread> threads;
   for (int r = 0; r < P; ++r) {
@@ -40,7 +46,11 @@ DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& 
             gpu ? make_gpu_shard_engine(job, shards[(size_t)r].bytes, shards[(size_t)r].num_lines)
                 : make_cpu_shard_engine(job);
         std::unique_ptr<Communicator> comm = group.comm(r);
-        results[(size_t)r] = run_distributed(cfg, *comm, *eng, shards[(size_t)r]);
+        // the same engines and communicators across jobs, like a long-lived rank
+        for (size_t j = 0; j < schedule.size(); ++j) {
+          DistResult d = run_distributed(schedule[j], *comm, *eng, shards[(size_t)r]);
+          if (r == 0) results[j] = std::move(d);
+        }
       } catch (...) {
         errors[(size_t)r] = std::current_exception();
       }
@@ -49,7 +59,11 @@ DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& 
   for (auto& t : threads) t.join();
   for (auto& e : errors)
     if (e) std::rethrow_exception(e);
-  return results[0];
+  return results;
+}
+
+DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole) {
+  return run_single_process_schedule({cfg}, whole)[0];
 }
 
 }  // namespace locust

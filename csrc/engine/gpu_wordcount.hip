@@ -215,6 +215,7 @@ struct DevicePipeline {
       dict.uval = reinterpret_cast<u64*>(reinterpret_cast<char*>(dict.ucount) + align_up(cap * 8, 256));
       d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.uval) + align_up(cap * 8, 256));
       dict.mask = (u32)(dict_slots - 1);
+      dict.ucap = (u32)cap;
     }
 
     char delim_buf[64] = {0};
@@ -317,13 +318,26 @@ struct DevicePipeline {
 
   // ---- dictionary path (SortPath::kDict): no host synchronisation inside ----
   void enqueue_process_dict(u32 num_lines, bool compat, bool with_counts = false) {
+    enqueue_dict_insert(num_lines, compat, with_counts);
+    enqueue_rank();
+  }
+  // Fresh table, then every token (or weighted record) into it.
+  void enqueue_dict_insert(u32 num_lines, bool compat, bool with_counts) {
     if (compat)
       launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
                            lb_compact, stream);
     LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
     launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
                        d_ctr, stream);
+  }
+  // Weighted ranks of the distinct keys (rank and uval must be zero).
+  void enqueue_rank() {
     launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, cap, d_rank, dict.uval, stream);
+  }
+  // [uval | rank] of the zeroed block, for re-ranking after more keys were inserted.
+  void enqueue_zero_ranks() {
+    const u64 off = reinterpret_cast<char*>(dict.uval) - reinterpret_cast<char*>(dict.table);
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.uval, 0, dict_zero_bytes - off, stream));
   }
   // Sorted distinct keys + counts (for the shuffle's range partition).
   void enqueue_sorted_from_dict() {
@@ -570,14 +584,31 @@ class GpuShardEngine final : public ShardEngine {
   void* stream() override { return mp_->stream; }
   char* input_buffer() override { return mp_->h_text; }
 
-  u64 map_local(const TextInput& shard, bool combine) override {
+  u64 map_local(const TextInput& shard, bool combine, DistStrategy plan) override {
     DevicePipeline& m = *mp_;
     m.check_input(shard);
     m.enqueue_upload(shard);
     m.enqueue_map(shard);
     const bool compat = cfg_.map_path == MapPath::kCompat;
     samples_valid_ = false;
+    dict_local_ = false;
+    sorted_local_ = true;
     if (combine && cfg_.sort_path == SortPath::kDict) {
+      if (plan == DistStrategy::kGather) {
+        // Gather plan: the combined records go to rank 0 unsorted, straight from the
+        // dictionary's dense arrays; no local sort at all.
+        m.enqueue_dict_insert((u32)shard.num_lines, compat, false);
+        launch_pack_records(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique, m.cap,
+                            m.d_records, m.stream);
+        m.read_counters();
+        if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+          set_local(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique);
+          dict_local_ = true;
+          sorted_local_ = false;
+          return finish_map_stats(shard, m.h_ctr->num_unique);
+        }
+        return map_overflow_fallback(shard);
+      }
       // Map-side combine through the dictionary: sorted distinct keys + counts.  The
       // shuffle records and the splitter samples are produced speculatively in the same
       // stream, so the common case costs ONE host synchronisation.
@@ -592,25 +623,15 @@ class GpuShardEngine final : public ShardEngine {
       if (!m.dict_fallback_needed()) {
         samples_.assign(m.h_small, m.h_small + kSpecSamples);
         samples_valid_ = true;
-        local_stats_ = WordCountResult();
-        local_stats_.num_lines = shard.num_lines;
-        m.fill_counters(local_stats_);
-        local_stats_.num_tokens = m.h_ctr->num_records;
-        return m.h_ctr->num_unique;
+        dict_local_ = true;
+        return finish_map_stats(shard, m.h_ctr->num_unique);
       }
-      if (m.dict_fallback_needed()) {
-        if (m.h_ctr->flags & kCtrDictOverflow) {
-          m.enqueue_process(0, false, false, m.h_ctr->num_records);
-          m.enqueue_reduce_core(false);
-          set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
-        } else {
-          radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx,
-                     m.dict.ucount, m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
-          set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
-        }
-      } else {
-        set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
-      }
+      if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
+      // more distinct keys than the rank sort takes: radix-sort the dictionary's keys
+      radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                 m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      dict_local_ = true;
     } else {
       m.enqueue_process((u32)shard.num_lines, compat, false);
       if (combine) {
@@ -623,15 +644,29 @@ class GpuShardEngine final : public ShardEngine {
     }
     launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
     m.read_counters();
-    local_stats_ = WordCountResult();
-    local_stats_.num_lines = shard.num_lines;
-    m.fill_counters(local_stats_);
-    local_stats_.num_tokens = m.h_ctr->num_records;
-    return combine ? m.h_ctr->num_unique : m.h_ctr->num_records;
+    return finish_map_stats(shard, combine ? m.h_ctr->num_unique : m.h_ctr->num_records);
+  }
+
+  // Shuffle after a gather-planned map: sort the dictionary's keys, repack, resample.
+  void prepare_shuffle() override {
+    if (sorted_local_) return;
+    DevicePipeline& m = *mp_;
+    if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
+      m.enqueue_rank();  // ranks are still zero from the insert's table reset
+      m.enqueue_sorted_from_dict();
+    } else {
+      radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                 m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+    }
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.sync();
+    sorted_local_ = true;
   }
 
   std::vector<PackedKey> sample(u32 s) override {
     DevicePipeline& m = *mp_;
+    prepare_shuffle();
     if (samples_valid_ && s == kSpecSamples) return samples_;
     LOCUST_CHECK_ARG(s <= kMaxSamples, "too many samples");
     launch_sample_keys(local_keys(), local_n(), s, m.d_samples, m.stream);
@@ -645,6 +680,7 @@ class GpuShardEngine final : public ShardEngine {
     DevicePipeline& m = *mp_;
     const u32 P = (u32)splitters.size() + 1;
     LOCUST_CHECK_ARG(P <= kMaxRanks, "too many ranks");
+    prepare_shuffle();
     if (!splitters.empty()) {
       std::memcpy(m.h_small, splitters.data(), splitters.size() * sizeof(PackedKey));
       LOCUST_HIP_CHECK(hipMemcpyAsync(m.d_splitters, m.h_small,
@@ -704,6 +740,46 @@ class GpuShardEngine final : public ShardEngine {
     range_entries_ = std::move(tmp.entries);
   }
 
+  void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) override {
+    DevicePipeline& m = *mp_;
+    DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
+    if (dict_local_) {
+      // Merge into this rank's own dictionary: only the other ranks' records are
+      // inserted, then the merged distinct keys are ranked and emitted (zero-copy).
+      launch_unpack_records(r.d_records, n_other, r.tokens, r.d_counts, m.stream);
+      m.h_u64[0] = n_other;
+      LOCUST_HIP_CHECK(hipMemcpyAsync(&r.d_ctr->num_records, m.h_u64, sizeof(u32),
+                                      hipMemcpyHostToDevice, m.stream));
+      m.enqueue_zero_ranks();
+      launch_dict_insert(r.tokens, r.d_counts, &r.d_ctr->num_records, std::max<u64>(n_other, 1),
+                         m.dict, m.d_ctr, m.stream);
+      m.enqueue_rank();
+      m.enqueue_emit_dict(/*mapped=*/true);
+      m.sync();
+      *m.h_ctr = *m.h_ctr_mapped;
+      if (!m.dict_fallback_needed()) {
+        const u64 u = m.h_ctr->num_unique;
+        range_entries_.resize(u);
+        for (u64 j = 0; j < u; ++j) {
+          for (int w = 0; w < kKeyWords; ++w) range_entries_[j].key.w[w] = m.h_out[j].w[w];
+          range_entries_[j].val = m.h_out[j].val;
+          range_entries_[j].count = m.h_out[j].count;
+        }
+        *total_count = m.h_ctr->total_count;
+        *num_unique = u;
+        return;
+      }
+    }
+    // General case: this rank's records behind the received ones, then the usual reduce.
+    LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
+    if (local_count_)
+      LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
+                                      local_count_ * sizeof(KeyCount), hipMemcpyDeviceToDevice,
+                                      m.stream));
+    m.sync();
+    reduce_received(n_other + local_count_, total_count, num_unique);
+  }
+
   void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
     for (auto& e : range_entries_) e.val += global_offset;
     *out = std::move(range_entries_);
@@ -712,6 +788,25 @@ class GpuShardEngine final : public ShardEngine {
   void map_stats(WordCountResult* r) override { *r = local_stats_; }
 
  private:
+  u64 finish_map_stats(const TextInput& shard, u64 n_records) {
+    DevicePipeline& m = *mp_;
+    local_stats_ = WordCountResult();
+    local_stats_.num_lines = shard.num_lines;
+    m.fill_counters(local_stats_);
+    local_stats_.num_tokens = m.h_ctr->num_records;
+    local_count_ = n_records;
+    return n_records;
+  }
+  // Dictionary table overflow: sort every token and combine the reference way.
+  u64 map_overflow_fallback(const TextInput& shard) {
+    DevicePipeline& m = *mp_;
+    m.enqueue_process(0, false, false, m.h_ctr->num_records);
+    m.enqueue_reduce_core(false);
+    set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.read_counters();
+    return finish_map_stats(shard, m.h_ctr->num_unique);
+  }
   void set_local(ConstKeysSoA k, const u64* c, const u32* n) {
     local_keys_ = k;
     local_counts_ = c;
@@ -730,6 +825,9 @@ class GpuShardEngine final : public ShardEngine {
   const u64* local_counts_ = nullptr;
   const u32* local_n_ = nullptr;
   WordCountResult local_stats_;
+  u64 local_count_ = 0;
+  bool dict_local_ = false;   // the dictionary holds this rank's combined keys (mergeable)
+  bool sorted_local_ = true;  // d_records are sorted (shuffle-ready)
 };
 
 }  // namespace

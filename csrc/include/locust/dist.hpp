@@ -17,6 +17,17 @@
 // Output is byte-identical to the single-GPU run, including the global `val` indices.
 // Every stage boundary runs an agreement collective on a status word, so a rank that
 // fails (or is told to fail via LOCUST_FAULT) turns into a clean error on all ranks.
+//
+// Two strategies follow the map stage (DistStrategy):
+//   shuffle   the sample-sort all-to-all above: every rank reduces 1/P of the key space.
+//             Scales with the number of distinct keys; costs 3 more collectives.
+//   gather    every rank's combined (key, count) records go straight to rank 0 over
+//             point-to-point xGMI (one grouped send/recv) and rank 0 merges them.  When
+//             the combined records are few (Hamlet-sized shards: ~5.6K distinct keys per
+//             rank) the job is latency-bound and one collective beats four; rank 0 has
+//             to receive the whole result anyway.
+//   auto      gather when the total combined records <= gather_max_records, else shuffle.
+//             Decided from the first allgather, so every rank takes the same branch.
 #pragma once
 
 #include <memory>
@@ -80,6 +91,8 @@ class LoopbackGroup {
   std::shared_ptr<State> state_;
 };
 
+enum class DistStrategy : int { kAuto = 0, kShuffle = 1, kGather = 2 };
+
 // Per-rank local engine used by the distributed driver.
 class ShardEngine {
  public:
@@ -90,7 +103,12 @@ class ShardEngine {
   // shard whose data already points here is uploaded without a host copy.
   virtual char* input_buffer() { return nullptr; }
   // Map + sort (+ combine) this rank's shard.  Returns the number of local records.
-  virtual u64 map_local(const TextInput& shard, bool combine) = 0;
+  // `plan` is the strategy the driver expects to take: kGather lets an engine skip the
+  // local sort (records may be unsorted); prepare_shuffle() must then be called before
+  // sample()/bucket_offsets() if the driver switches to the shuffle after all.
+  virtual u64 map_local(const TextInput& shard, bool combine,
+                        DistStrategy plan = DistStrategy::kShuffle) = 0;
+  virtual void prepare_shuffle() {}
   virtual std::vector<PackedKey> sample(u32 num_samples) = 0;
   // Record offsets [0 .. P] of the P buckets defined by P-1 sorted splitters.
   virtual std::vector<u64> bucket_offsets(const std::vector<PackedKey>& splitters) = 0;
@@ -98,6 +116,11 @@ class ShardEngine {
   virtual void* recv_records(u64 n) = 0;       // room for n incoming KeyCount records
   // Sort + weighted reduce of the n received records; returns {total_count, num_unique}.
   virtual void reduce_received(u64 n, u64* total_count, u64* num_unique) = 0;
+  // Gather strategy, root only: reduce this rank's own records together with the n_other
+  // records the other ranks sent (already in recv_records(), which holds room for both).
+  virtual void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) = 0;
+  // Strategy of the previous job (the driver's prediction for the next one under kAuto).
+  DistStrategy last_strategy = DistStrategy::kShuffle;
   virtual void finalize(u64 global_offset, std::vector<WordCountEntry>* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;
@@ -112,6 +135,11 @@ struct DistConfig {
   int world = 1;
   u32 samples_per_rank = 64;
   bool gather = true;   // rank 0 receives the whole output
+  DistStrategy strategy = DistStrategy::kAuto;
+  // auto: gather-to-root when the combined records of all ranks fit this bound.  The root
+  // merge is one dictionary pass over them (~1 record/ns), the shuffle costs three extra
+  // collective round trips (~15-25 us each over xGMI), so the break-even is ~10^5.
+  u64 gather_max_records = 1u << 17;
 };
 
 struct DistResult {
@@ -120,6 +148,7 @@ struct DistResult {
   u64 local_records = 0;   // records this rank sent into the shuffle
   u64 sent_bytes = 0, recv_bytes = 0;
   u64 range_tokens = 0, range_unique = 0;  // this rank's key range after the shuffle
+  DistStrategy strategy = DistStrategy::kShuffle;  // the one this job took
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
@@ -135,5 +164,9 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts);
 // the loopback communicator; rank 0's result is returned.  With Backend::kCpu the ranks
 // use the CPU shard engine.
 DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole);
+// Several jobs back to back on the same ranks (engines and communicators persist, as in a
+// long-lived multi-process job); rank 0's result of every job.
+std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig>& schedule,
+                                                    const TextInput& whole);
 
 }  // namespace locust

@@ -173,6 +173,8 @@ struct DictWorkspace {
   KeysSoA ukeys;    // dense distinct keys (ids from ctr->num_unique)
   u64* ucount;      // per-id occurrence counts, zeroed per run
   u64* uval;        // per-id weighted rank (= output val), zeroed per run
+  u32 ucap;         // capacity of ukeys/ucount/uval: a key that would get id >= ucap sets
+                    // kCtrDictOverflow (num_unique may then exceed ucap; consumers clamp)
 };
 // Hash every token (with its count; null = 1) into the table; distinct keys land in
 // ukeys[0 .. ctr->num_unique) with summed counts in ucount.

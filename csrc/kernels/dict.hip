@@ -23,6 +23,8 @@
 //   rank_scatter  sorted[rank[i]] = key[i], counts alongside.
 //   scan_pack     exclusive scan of the counts with decoupled look-back -> val, and the
 //                 final (key, val, count) records for the D2H.
+#include <algorithm>
+
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
@@ -39,6 +41,7 @@ using dev::wave_id;
 // (bytes 00 00 FF FF 00 00 FF FF: a NUL followed by non-NUL bytes), so a stored 0 means
 // "not written yet" and a zero-initialised table needs no sentinel fill.
 constexpr u64 kWordMagic = 0x0000FFFF0000FFFFull;
+constexpr u32 kIdFull = 0xFFFFFFFFu;  // slot id of a key that did not fit the dense arrays
 
 __device__ __forceinline__ u64 mix64(u64 x) {
   x ^= x >> 33;
@@ -76,15 +79,20 @@ __device__ bool global_insert(const DictWorkspace& dw, const u64* k, u64 count,
         u32 base = 0;
         if (lane_id() == leader) base = atomicAdd(&ctr->num_unique, (u32)__popcll(claim));
         const u32 id = (u32)__shfl((int)base, leader, 64) + dev::lanes_below(claim);
+        const bool fits = id < dw.ucap;
+        if (fits) {
 #pragma unroll
-        for (int j = 0; j < kKeyWords; ++j) dw.ukeys.w[j][id] = k[j];
-        // ucount is zero-initialised and only ever updated by device-scope atomics (a
-        // plain store could sit dirty in this XCD's L2 and later overwrite other adds)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&dw.ucount[id]), (unsigned long long)count);
+          for (int j = 0; j < kKeyWords; ++j) dw.ukeys.w[j][id] = k[j];
+          // ucount is zero-initialised and only ever updated by device-scope atomics (a
+          // plain store could sit dirty in this XCD's L2 and later overwrite other adds)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&dw.ucount[id]), (unsigned long long)count);
+        }
 #pragma unroll
         for (int j = 1; j < kKeyWords; ++j) dev::st_agent(&sl->w[j], k[j] ^ kWordMagic);
-        dev::st_agent(&sl->id, id + 1);
-        return true;
+        // a key past the dense capacity is still published (as kIdFull), so later
+        // inserters of it stop probing instead of waiting for an id that never comes
+        dev::st_agent(&sl->id, fits ? id + 1 : kIdFull);
+        return fits;
       }
     }
     if (w0 == k[0]) {
@@ -94,6 +102,7 @@ __device__ bool global_insert(const DictWorkspace& dw, const u64* k, u64 count,
       const u64 x3 = dev::ld_agent(&sl->w[3]);
       if (sid == 0 || x1 == 0 || x2 == 0 || x3 == 0) continue;  // claimer still writing
       if ((x1 ^ kWordMagic) == k[1] && (x2 ^ kWordMagic) == k[2] && (x3 ^ kWordMagic) == k[3]) {
+        if (sid == kIdFull) return false;
         atomicAdd(reinterpret_cast<unsigned long long*>(&dw.ucount[sid - 1]),
                   (unsigned long long)count);
         return true;
@@ -202,11 +211,12 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
                                                            const u64* __restrict__ counts,
                                                            const u32* __restrict__ d_u,
                                                            u32* __restrict__ rank,
-                                                           u64* __restrict__ val) {
+                                                           u64* __restrict__ val,
+                                                           u32 ucap) {
   __shared__ __attribute__((aligned(16))) u64 s_w0[kRankJ];
   __shared__ __attribute__((aligned(16))) u64 s_cnt[kRankJ];
   __shared__ u64 s_rest[kRankJ][kKeyWords - 1];
-  const u32 u = *d_u;
+  const u32 u = min(*d_u, ucap);  // > ucap only after a dictionary overflow (result unused)
   if (u > (u32)kRankSortMax) return;  // radix path handles it
   const u32 ti = (u32)div_up(u, kRankI), tj = (u32)div_up(u, kRankJ);
   for (u32 pair = blockIdx.x; pair < ti * tj; pair += gridDim.x) {
@@ -289,8 +299,9 @@ __global__ __launch_bounds__(256) void rank_emit_kernel(ConstKeysSoA keys,
                                                         const u64* __restrict__ val,
                                                         const MapCounters* __restrict__ ctr,
                                                         OutRecord* __restrict__ out,
-                                                        MapCounters* __restrict__ ctr_out) {
-  const u32 u = ctr->num_unique;
+                                                        MapCounters* __restrict__ ctr_out,
+                                                        u32 ucap) {
+  const u32 u = min(ctr->num_unique, ucap);
   if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
     // field by field: total_count belongs to the thread that emits rank u-1
     ctr_out->num_records = ctr->num_records;
@@ -320,8 +331,9 @@ __global__ __launch_bounds__(256) void rank_scatter_kernel(ConstKeysSoA keys,
                                                            const u32* __restrict__ rank,
                                                            const u32* __restrict__ d_u,
                                                            KeysSoA sorted,
-                                                           u64* __restrict__ sorted_counts) {
-  const u32 u = *d_u;
+                                                           u64* __restrict__ sorted_counts,
+                                                           u32 ucap) {
+  const u32 u = min(*d_u, ucap);
   if (u > (u32)kRankSortMax) return;
   for (u32 i = blockIdx.x * 256 + threadIdx.x; i < u; i += gridDim.x * 256) {
     const u32 r = rank[i];
@@ -395,22 +407,23 @@ void launch_rank_sort(ConstKeysSoA keys, const u64* counts, const u32* d_u, u64 
   const u64 umax = cap < (u64)kRankSortMax ? cap : (u64)kRankSortMax;
   const u64 pairs = div_up(umax, kRankI) * div_up(umax, kRankJ);
   const u32 grid = (u32)(pairs < 2048 ? (pairs ? pairs : 1) : 2048);
-  rank_sort_kernel<<<dim3(grid), dim3(kRankI), 0, s>>>(keys, counts, d_u, rank, val);
+  rank_sort_kernel<<<dim3(grid), dim3(kRankI), 0, s>>>(keys, counts, d_u, rank, val,
+                                                       (u32)std::min<u64>(cap, 0xFFFFFFFFu));
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
 void launch_rank_emit(ConstKeysSoA keys, const u64* counts, const u32* rank, const u64* val,
                       u64 cap, const MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                       hipStream_t s) {
-  rank_emit_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(keys, counts, rank, val, ctr,
-                                                                 out, ctr_out);
+  rank_emit_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(
+      keys, counts, rank, val, ctr, out, ctr_out, (u32)std::min<u64>(cap, 0xFFFFFFFFu));
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
 void launch_rank_scatter(ConstKeysSoA keys, const u64* counts, const u32* rank, const u32* d_u,
                          u64 cap, KeysSoA sorted, u64* sorted_counts, hipStream_t s) {
-  rank_scatter_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(keys, counts, rank, d_u,
-                                                                    sorted, sorted_counts);
+  rank_scatter_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(
+      keys, counts, rank, d_u, sorted, sorted_counts, (u32)std::min<u64>(cap, 0xFFFFFFFFu));
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -135,6 +135,20 @@ PyResult run_multi(const std::string& text, const DistConfig& cfg) {
   return PyResult{d.result};
 }
 
+py::dict dist_to_dict(const DistResult& d);
+
+py::list run_multi_schedule(const std::string& text, const std::vector<DistConfig>& schedule) {
+  TextInput in = as_input(text);
+  std::vector<DistResult> rs;
+  {
+    py::gil_scoped_release nogil;
+    rs = run_single_process_schedule(schedule, in);
+  }
+  py::list out;
+  for (const auto& d : rs) out.append(py::make_tuple(PyResult{d.result}, dist_to_dict(d)));
+  return out;
+}
+
 py::dict dist_to_dict(const DistResult& d) {
   py::dict x;
   x["map_ms"] = d.map_ms;
@@ -147,6 +161,7 @@ py::dict dist_to_dict(const DistResult& d) {
   x["recv_bytes"] = d.recv_bytes;
   x["range_tokens"] = d.range_tokens;
   x["range_unique"] = d.range_unique;
+  x["strategy"] = d.strategy == DistStrategy::kGather ? "gather" : "shuffle";
   return x;
 }
 
@@ -217,6 +232,7 @@ class PyDistRank {
   }
   int rank() const { return comm_->rank(); }
   int size() const { return comm_->size(); }
+  void set_strategy(DistStrategy s) { cfg_.strategy = s; }
 
  private:
   DistConfig cfg_;
@@ -255,12 +271,18 @@ PYBIND11_MODULE(_locust, m) {
       .def_readwrite("check", &JobConfig::check)
       .def_readwrite("sync_plan", &JobConfig::sync_plan);
 
+  py::enum_<DistStrategy>(m, "DistStrategy")
+      .value("auto", DistStrategy::kAuto)
+      .value("shuffle", DistStrategy::kShuffle)
+      .value("gather", DistStrategy::kGather);
   py::class_<DistConfig>(m, "DistConfig")
       .def(py::init<>())
       .def_readwrite("job", &DistConfig::job)
       .def_readwrite("world", &DistConfig::world)
       .def_readwrite("samples_per_rank", &DistConfig::samples_per_rank)
-      .def_readwrite("gather", &DistConfig::gather);
+      .def_readwrite("gather", &DistConfig::gather)
+      .def_readwrite("strategy", &DistConfig::strategy)
+      .def_readwrite("gather_max_records", &DistConfig::gather_max_records);
 
   py::class_<PyResult>(m, "Result")
       .def("entries", &PyResult::entries)
@@ -294,6 +316,8 @@ PYBIND11_MODULE(_locust, m) {
     for (const auto& k : eng.run_map_stage(as_input(text), nullptr)) out.emplace_back(key_to_string(k));
     return out;
   });
+  m.def("run_multi_schedule", &run_multi_schedule, py::arg("text"), py::arg("schedule"),
+        "Several loopback jobs back to back on the same ranks; [(Result, info)] of rank 0.");
   m.def("run_multi", &run_multi, py::arg("text"), py::arg("cfg"),
         "Loopback multi-rank WordCount in this process (one thread per rank).");
 
@@ -305,6 +329,7 @@ PYBIND11_MODULE(_locust, m) {
       .def("run", &PyDistRank::run, py::arg("shard"), py::arg("first_line") = 0)
       .def("load", &PyDistRank::load, py::arg("shard"), py::arg("first_line") = 0)
       .def("run_loaded", &PyDistRank::run_loaded)
+      .def("set_strategy", &PyDistRank::set_strategy)
       .def("barrier", &PyDistRank::barrier)
       .def("allreduce_max", &PyDistRank::allreduce_max)
       .def_property_readonly("rank", &PyDistRank::rank)

@@ -56,9 +56,19 @@ def make_config(
     return cfg
 
 
+_STRATEGY = {"auto": _C.DistStrategy.auto, "shuffle": _C.DistStrategy.shuffle,
+             "gather": _C.DistStrategy.gather}
+
+
 def make_dist_config(world: int, job=None, *, samples_per_rank: int = 64, gather: bool = True,
+                     strategy: str | None = None, gather_max_records: int | None = None,
                      **job_kwargs):
+    """Distributed job config.  ``strategy``: auto (default, or ``LOCUST_DIST_STRATEGY``),
+    shuffle (sample-sort all-to-all) or gather (combined records straight to rank 0)."""
     d = _C.DistConfig()
+    d.strategy = _STRATEGY[strategy or os.environ.get("LOCUST_DIST_STRATEGY", "auto")]
+    if gather_max_records is not None:
+        d.gather_max_records = gather_max_records
     d.job = job if job is not None else make_config(**job_kwargs)
     d.world = world
     d.samples_per_rank = samples_per_rank

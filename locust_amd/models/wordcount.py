@@ -67,10 +67,10 @@ def wordcount_file(path: str, line_start: int = -1, line_end: int = -1, backend:
 
 
 def run_multi(text: bytes, world: int, backend: str = "gpu", combine: bool = True,
-              samples_per_rank: int = 64, **kw):
+              samples_per_rank: int = 64, strategy: str | None = None, **kw):
     """Multi-rank WordCount in this process (loopback communicator, one thread per rank)."""
     dcfg = make_dist_config(world, make_config(backend, combine=combine, **kw),
-                            samples_per_rank=samples_per_rank)
+                            samples_per_rank=samples_per_rank, strategy=strategy)
     return _C.run_multi(text, dcfg)
 
 

@@ -23,8 +23,9 @@ def free_port():
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("combine", [True, False])
-def test_cpu_loopback(hamlet, world, combine):
-    r = lc.run_multi(hamlet, world, backend="cpu", combine=combine)
+@pytest.mark.parametrize("strategy", ["shuffle", "gather", "auto"])
+def test_cpu_loopback(hamlet, world, combine, strategy):
+    r = lc.run_multi(hamlet, world, backend="cpu", combine=combine, strategy=strategy)
     ent, ntok, _ = oracle.wordcount(hamlet)
     assert r.entries() == ent
     assert r.num_tokens == ntok
@@ -70,14 +71,95 @@ def test_cpu_multiprocess_tcp(hamlet, world):
 def test_fault_injection_clean_failure(hamlet, monkeypatch):
     monkeypatch.setenv("LOCUST_FAULT", "1:reduce")
     with pytest.raises(lc.LocustError, match="stage 'reduce' on rank 1"):
-        lc.run_multi(hamlet, 3, backend="cpu")
+        lc.run_multi(hamlet, 3, backend="cpu", strategy="shuffle")
+
+
+@pytest.mark.parametrize("fault,match", [("2:map", "stage 'map' on rank 2"),
+                                         ("0:reduce", "rank 0")])
+def test_fault_injection_gather_strategy(hamlet, monkeypatch, fault, match):
+    monkeypatch.setenv("LOCUST_FAULT", fault)
+    with pytest.raises(lc.LocustError, match=match):
+        lc.run_multi(hamlet, 3, backend="cpu", strategy="gather")
+
+
+def test_auto_strategy_threshold(hamlet):
+    """auto picks gather below gather_max_records and the shuffle above; same output."""
+    ent = oracle.wordcount(hamlet)[0]
+    for bound, want in [(1 << 20, "gather"), (10, "shuffle")]:
+        d = lc.make_dist_config(2, lc.make_config("cpu", combine=True), gather_max_records=bound)
+        r = lc._C.run_multi(hamlet, d)
+        assert r.entries() == ent, want
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
-@pytest.mark.parametrize("combine,sort", [(True, "dict"), (True, "radix"), (False, "radix")])
-def test_gpu_loopback(hamlet, world, combine, sort):
-    r = lc.run_multi(hamlet, world, backend="gpu", combine=combine, check=True, sort=sort)
+@pytest.mark.parametrize("combine,sort,strategy", [(True, "dict", "auto"), (True, "dict", "shuffle"),
+                                                   (True, "radix", "shuffle"),
+                                                   (False, "radix", "shuffle"),
+                                                   (False, "dict", "gather")])
+def test_gpu_loopback(hamlet, world, combine, sort, strategy):
+    r = lc.run_multi(hamlet, world, backend="gpu", combine=combine, check=True, sort=sort,
+                     strategy=strategy)
     ent, ntok, _ = oracle.wordcount(hamlet)
     assert r.num_tokens == ntok
     assert r.entries() == ent
+
+
+def _schedule(backend, world):
+    job = lc.make_config(backend, combine=True, check=backend == "gpu")
+    plan = [("auto", 1 << 20, "gather"),   # predicted shuffle, takes gather
+            ("auto", 1 << 20, "gather"),   # predicted gather: unsorted records, root merge
+            ("auto", 10, "shuffle"),       # predicted gather, mispredict -> late sampling
+            ("auto", 10, "shuffle"),
+            ("auto", 1 << 20, "gather"),   # predicted shuffle (sorted records) -> gather
+            ("gather", 0, "gather"),
+            ("shuffle", 0, "shuffle")]
+    cfgs = [lc.make_dist_config(world, job, strategy=s, gather_max_records=m) for s, m, _ in plan]
+    return cfgs, [w for _, _, w in plan]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_cpu_strategy_schedule(hamlet, world):
+    """Long-lived ranks switching strategies between jobs (plan/mispredict paths)."""
+    cfgs, want = _schedule("cpu", world)
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    for (res, info), w in zip(lc._C.run_multi_schedule(hamlet, cfgs), want):
+        assert info["strategy"] == w
+        assert res.entries() == ent
+        assert res.num_tokens == ntok
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_gpu_strategy_schedule(hamlet, world):
+    cfgs, want = _schedule("gpu", world)
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    for (res, info), w in zip(lc._C.run_multi_schedule(hamlet, cfgs), want):
+        assert info["strategy"] == w
+        assert res.entries() == ent
+        assert res.num_tokens == ntok
+
+
+def _distinct_text(n_words, per_line=10):
+    words = [b"w%06d" % i for i in range(n_words)]
+    return b"".join(b" ".join(words[i:i + per_line]) + b"\n" for i in range(0, n_words, per_line))
+
+
+@pytest.mark.parametrize("strategy", ["gather", "shuffle"])
+def test_cpu_many_distinct(strategy):
+    text = _distinct_text(20000)
+    r = lc.run_multi(text, 3, backend="cpu", strategy=strategy)
+    assert r.entries() == oracle.wordcount(text)[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_words", [30000, 70000])
+def test_gpu_gather_merge_overflow(n_words):
+    """Root merge past the root's dense dictionary capacity / the rank-sort range falls
+    back to the general reduce; repeated jobs cover the unsorted (gather-planned) records."""
+    text = _distinct_text(n_words)
+    ent = oracle.wordcount(text)[0]
+    job = lc.make_config("gpu", combine=True, check=True)
+    cfgs = [lc.make_dist_config(4, job, strategy=s) for s in ("gather", "gather", "shuffle")]
+    for res, info in lc._C.run_multi_schedule(text, cfgs):
+        assert res.entries() == ent

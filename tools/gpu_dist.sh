@@ -3,7 +3,7 @@ set -e
 cd $GRAFT_REPO_ROOT
 TAG=${1:-dist}
 mkdir -p gpurun_out/$TAG
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 1 --steps 50 --warmup 5 --force-dist > gpurun_out/$TAG/rccl1.json 2> gpurun_out/$TAG/rccl1.err || { tail -30 gpurun_out/$TAG/rccl1.err; exit 1; }
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 1 --steps 100 --warmup 10 --force-dist > gpurun_out/$TAG/rccl1.json 2> gpurun_out/$TAG/rccl1.err || { tail -30 gpurun_out/$TAG/rccl1.err; exit 1; }
 cat gpurun_out/$TAG/rccl1.json
 for n in 2 4; do
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2962$n bench.py --gpus $n --steps 30 --warmup 3 --comm tcp > gpurun_out/$TAG/tcp$n.json 2> gpurun_out/$TAG/tcp$n.err || { tail -30 gpurun_out/$TAG/tcp$n.err; exit 1; }
