@@ -10,7 +10,9 @@
 //   --backend gpu|cpu  --reduce-path lds|global  --map-path compat|fast
 //   --sort radix|dict  --gpus N  --emits-per-line N  --max-key N  --ref-compat
 //   --stage map|reduce  --spill-dir DIR  --spill-format text|binary  --inputs a,b,...
-//   --warmup N  --iters N  --json FILE  --quiet  --check  --device N
+//   --warmup N  --iters N  --json FILE  --quiet  --check  --device N  --chunk-mb N
+// and a synthetic-text generator (BASELINE configs "1M lines" / "10 GB"):
+//   MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -19,6 +21,7 @@
 
 #include "locust/dist.hpp"
 #include "locust/engine.hpp"
+#include "locust/gen.hpp"
 #include "locust/io.hpp"
 
 using namespace locust;
@@ -39,6 +42,8 @@ struct CliArgs {
   int warmup = 0, iters = 1;
   std::string json;
   bool quiet = false;
+  std::string gen_out;  // generator mode
+  GenSpec gen;
 };
 
 void usage() {
@@ -109,12 +114,25 @@ bool parse(int argc, char** argv, CliArgs* a) {
       a->json = need("--json");
     } else if (s == "--quiet") {
       a->quiet = true;
+    } else if (s == "--chunk-mb") {
+      a->cfg.chunk_bytes = (u64)std::atoll(need("--chunk-mb").c_str()) << 20;
+    } else if (s == "--gen") {
+      a->gen_out = need("--gen");
+    } else if (s == "--gen-lines") {
+      a->gen.lines = (u64)std::atoll(need("--gen-lines").c_str());
+    } else if (s == "--gen-bytes") {
+      a->gen.bytes = (u64)std::atoll(need("--gen-bytes").c_str());
+    } else if (s == "--seed") {
+      a->gen.seed = (u64)std::atoll(need("--seed").c_str());
+    } else if (s == "--vocab") {
+      a->gen.vocab = (u32)std::atoll(need("--vocab").c_str());
     } else if (s.size() > 2 && s[0] == '-' && s[1] == '-') {
       throw Error("unknown flag " + s);
     } else {
       pos.push_back(s);
     }
   }
+  if (!a->gen_out.empty()) return true;
   if (pos.empty()) return false;
   a->file = pos[0];
   if (pos.size() > 1) {
@@ -146,19 +164,58 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
                "\"unique\": %llu, \"overflow_lines\": %llu, \"truncated\": %llu, "
                "\"map_ms\": %.6f, \"process_ms\": %.6f, \"reduce_ms\": %.6f, \"h2d_ms\": %.6f, "
                "\"d2h_ms\": %.6f, \"wall_ms_median\": %.6f, \"iters\": %d, \"map_path\": \"%s\", "
-               "\"reduce_path\": \"%s\", \"sort\": \"%s\"}\n",
+               "\"reduce_path\": \"%s\", \"sort\": \"%s\", \"chunks\": %llu}\n",
                a.cfg.backend == Backend::kCpu ? "cpu" : "gpu", a.gpus,
                (unsigned long long)r.num_lines, (unsigned long long)r.num_tokens,
                (unsigned long long)r.num_unique, (unsigned long long)r.overflow_lines,
                (unsigned long long)r.truncated, r.times.map_ms, r.times.process_ms,
                r.times.reduce_ms, r.times.h2d_ms, r.times.d2h_ms, med, (int)w.size(),
-               to_string(a.cfg.map_path), to_string(a.cfg.reduce_path), to_string(a.cfg.sort_path));
+               to_string(a.cfg.map_path), to_string(a.cfg.reduce_path), to_string(a.cfg.sort_path),
+               (unsigned long long)r.chunks);
   if (f != stderr) std::fclose(f);
 }
 
 long long ns(double ms) { return (long long)(ms * 1e6 + 0.5); }
 
+// Writes the synthetic text in 64 MiB pieces (bounded memory for 10 GB files).
+int generate(const CliArgs& a) {
+  std::FILE* f = std::fopen(a.gen_out.c_str(), "wb");
+  if (!f) throw Error("cannot write " + a.gen_out);
+  const u64 piece_lines = 1u << 20;  // whole 1,024-line blocks per piece
+  u64 lines = 0, bytes = 0;
+  std::string buf;
+  for (u64 first = 0;; first += piece_lines / kGenBlockLines) {
+    GenSpec g = a.gen;
+    g.first_block = first;
+    if (a.gen.lines) {
+      if (lines >= a.gen.lines) break;
+      g.lines = std::min<u64>(piece_lines, a.gen.lines - lines);
+      g.bytes = 0;
+    } else {
+      if (bytes >= a.gen.bytes) break;
+      g.lines = std::min<u64>(piece_lines, a.gen.bytes);  // cut below by bytes
+    }
+    buf.clear();
+    u64 nl = gen_text(g, &buf);
+    if (!a.gen.lines && bytes + buf.size() > a.gen.bytes) {
+      const size_t cut = buf.rfind('\n', a.gen.bytes - bytes - 1);
+      if (cut == std::string::npos || a.gen.bytes == bytes) break;
+      buf.resize(cut + 1);
+      nl = (u64)std::count(buf.begin(), buf.end(), '\n');
+    }
+    write_all(f, buf);
+    lines += nl;
+    bytes += buf.size();
+    if (!a.gen.lines && nl < piece_lines) break;
+  }
+  std::fclose(f);
+  std::printf("generated %llu lines, %llu bytes -> %s\n", (unsigned long long)lines,
+              (unsigned long long)bytes, a.gen_out.c_str());
+  return 0;
+}
+
 int run(const CliArgs& a) {
+  if (!a.gen_out.empty()) return generate(a);
   const bool cpu = a.cfg.backend == Backend::kCpu;
   const char* dev = cpu ? "CPU" : "GPU";
   if (a.window)

@@ -84,6 +84,15 @@ struct DevicePipeline {
   u32* d_rank = nullptr;
   u64 dict_zero_bytes = 0;
 
+  // streaming (inputs larger than one chunk), allocated on first use
+  char* d_text_alt = nullptr;        // second device text buffer (double buffering)
+  char* h_stage[2] = {nullptr, nullptr};  // pinned staging halves for pageable inputs
+  hipStream_t cstream = nullptr;     // H2D copy stream
+  hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
+  MapCounters* d_dctr = nullptr;     // dictionary counters that persist across chunks
+  MapCounters* h_chunk_ctr = nullptr;  // pinned per-chunk map counter snapshots
+  u64 h_chunk_cap = 0;
+
   char* h_text = nullptr;
   MapCounters* h_ctr = nullptr;
   SortPlan* h_plan = nullptr;
@@ -102,6 +111,11 @@ struct DevicePipeline {
                      "max_key_len must be in [1, 31]");
     cap_bytes = std::max<u64>(max_bytes, 1);
     cap_lines = std::max<u64>(max_lines, 1);
+    if (cfg.chunk_bytes && cap_bytes > cfg.chunk_bytes && !cap_records) {
+      // streaming engine: one pass holds a chunk; its token capacity is bounded by bytes
+      cap_bytes = cfg.chunk_bytes;
+      cap_lines = cap_bytes;
+    }
     cap = cap_records ? cap_records
                       : std::min<u64>(cap_lines * (u64)cfg.emits_per_line, cap_bytes / 2 + 1);
     cap = std::max<u64>(cap, 1);
@@ -243,8 +257,18 @@ struct DevicePipeline {
 
   ~DevicePipeline() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (cstream) (void)hipStreamSynchronize(cstream);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (int b = 0; b < 2; ++b) {
+      if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
+      if (ev_consumed[b]) (void)hipEventDestroy(ev_consumed[b]);
+      if (h_stage[b]) (void)hipHostFree(h_stage[b]);
+    }
+    if (cstream) (void)hipStreamDestroy(cstream);
+    if (d_text_alt) (void)hipFree(d_text_alt);
+    if (d_dctr) (void)hipFree(d_dctr);
+    if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
     if (stream) (void)hipStreamDestroy(stream);
     if (arena.base) (void)hipFree(arena.base);
     for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_out, (void*)h_keys,
@@ -417,6 +441,9 @@ struct DevicePipeline {
   }
 
   WordCountResult run(const TextInput& in) {
+    if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
+        cfg.map_path == MapPath::kFast)
+      return run_stream(in);
     check_input(in);
     WordCountResult r;
     r.num_lines = in.num_lines;
@@ -460,6 +487,171 @@ struct DevicePipeline {
     }
     r.times.wall_ms = (now_ns() - t0) * 1e-6;
     r.times.h2d_ms = ms_between(ev[0], ev[1]);
+    r.times.map_ms = ms_between(ev[1], ev[2]);
+    r.times.process_ms = ms_between(ev[2], ev[3]);
+    r.times.reduce_ms = ms_between(ev[3], ev[4]);
+    r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    if (cfg.check) validate_result(r);
+    return r;
+  }
+
+  // ---------------------------------------------------------------------------------
+  // Streaming: an input larger than the engine's text capacity is processed in
+  // line-aligned chunks of <= cap_bytes.  Chunk k+1's H2D runs on the copy
+  // stream while chunk k is mapped and folded into ONE dictionary that persists across
+  // chunks; the distinct keys are ranked and emitted once at the end.  Device memory is
+  // therefore bounded by the chunk size plus the dictionary, not by the input size.
+  // ---------------------------------------------------------------------------------
+  static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+      (void)hipGetLastError();  // pageable memory: clear the sticky error
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  }
+
+  void ensure_stream_buffers(bool staging, u64 nchunks) {
+    if (!cstream) {
+      LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_copied[b], hipEventDisableTiming));
+        LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_consumed[b], hipEventDisableTiming));
+      }
+      LOCUST_HIP_CHECK(hipMalloc(&d_text_alt, cap_bytes + 64));
+      LOCUST_HIP_CHECK(hipMalloc(&d_dctr, sizeof(MapCounters)));
+    }
+    if (staging && !h_stage[0])
+      for (int b = 0; b < 2; ++b)
+        LOCUST_HIP_CHECK(hipHostMalloc(&h_stage[b], cap_bytes + 64, hipHostMallocDefault));
+    if (nchunks > h_chunk_cap) {
+      if (h_chunk_ctr) LOCUST_HIP_CHECK(hipHostFree(h_chunk_ctr));
+      h_chunk_cap = std::max<u64>(nchunks, 64);
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_chunk_ctr, h_chunk_cap * sizeof(MapCounters),
+                                     hipHostMallocDefault));
+    }
+  }
+
+  // Line-aligned chunk boundaries, each <= cap_bytes.
+  std::vector<std::pair<u64, u64>> plan_chunks(const TextInput& in) const {
+    std::vector<std::pair<u64, u64>> out;
+    u64 pos = 0;
+    while (pos < in.bytes) {
+      u64 end = std::min<u64>(pos + cap_bytes, in.bytes);
+      if (end < in.bytes) {
+        const void* nl = memrchr(in.data + pos, '\n', (size_t)(end - pos));
+        if (!nl)
+          throw Error("a line longer than the engine's chunk size (" + std::to_string(cap_bytes) +
+                      " B) at byte " + std::to_string(pos));
+        end = (u64)(static_cast<const char*>(nl) - in.data) + 1;
+      }
+      out.emplace_back(pos, end - pos);
+      pos = end;
+    }
+    return out;
+  }
+
+  // Streams every chunk of `in` through map + dictionary insert (the table is reset
+  // first).  When the stream has drained, d_ctr->num_unique / flags describe the whole
+  // dictionary and h_chunk_ctr[0 .. chunks) holds each chunk's map counters.
+  size_t enqueue_stream_insert(const TextInput& in) {
+    LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
+                     "inputs larger than the engine capacity stream through the dictionary "
+                     "path with the fast map (sort=dict, map=fast)");
+    LOCUST_CHECK_ARG(cap >= cap_bytes / 2 + 1,
+                     "a streaming engine must be sized by bytes (max_lines >= max_bytes / 40)");
+    const auto chunks = plan_chunks(in);
+    const bool pinned = host_pinned(in.data);
+    ensure_stream_buffers(!pinned, chunks.size());
+    const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));
+    // the copy stream must not overwrite a text buffer before the reset is queued
+    LOCUST_HIP_CHECK(hipEventRecord(ev_copied[1], stream));
+    LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_copied[1], 0));
+    for (size_t k = 0; k < chunks.size(); ++k) {
+      const int b = (int)(k & 1);
+      char* dtext = b ? d_text_alt : d_text;
+      const u64 off = chunks[k].first, len = chunks[k].second;
+      const char* src = in.data + off;
+      if (!pinned) {
+        // pageable input: host copy into a pinned half (overlapping the GPU's work on the
+        // previous chunks) once that half's previous H2D has drained
+        if (k >= 2) LOCUST_HIP_CHECK(hipEventSynchronize(ev_copied[b]));
+        std::memcpy(h_stage[b], src, len);
+        src = h_stage[b];
+      }
+      if (k >= 2) LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[b], 0));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(dtext, src, len, hipMemcpyHostToDevice, cstream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(dtext + len, 0, 16, cstream));
+      LOCUST_HIP_CHECK(hipEventRecord(ev_copied[b], cstream));
+
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+      launch_map_fast(dtext, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, cap, d_ctr,
+                      lb_map, stream);
+      LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
+                                      hipMemcpyDeviceToHost, stream));
+      launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
+    }
+    // hand the dictionary's counters to the single-pass stages that follow
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_unique, &d_dctr->num_unique, sizeof(u32),
+                                    hipMemcpyDeviceToDevice, stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->flags, &d_dctr->flags, sizeof(u32),
+                                    hipMemcpyDeviceToDevice, stream));
+    return chunks.size();
+  }
+
+  // After the stream has drained: whole-input map statistics from the chunk snapshots.
+  void stream_stats(size_t nchunks, WordCountResult& r) const {
+    r.num_tokens = r.overflow_lines = r.truncated = r.max_key_len = 0;
+    for (size_t k = 0; k < nchunks; ++k) {
+      const MapCounters& c = h_chunk_ctr[k];
+      r.num_tokens += c.num_records;
+      r.overflow_lines += c.overflow_lines;
+      r.truncated += c.truncated;
+      r.max_key_len = std::max<u64>(r.max_key_len, c.max_key_len);
+    }
+    r.chunks = nchunks;
+  }
+
+  WordCountResult run_stream(const TextInput& in) {
+    WordCountResult r;
+    r.num_lines = in.num_lines;
+    const u64 t0 = now_ns();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+    LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+    const size_t nchunks = enqueue_stream_insert(in);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+    enqueue_rank();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+    enqueue_emit_dict(/*mapped=*/true);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+    LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+    sync();
+    *h_ctr = *h_ctr_mapped;
+    if (h_ctr->flags & kCtrDictOverflow)
+      throw Error("streaming dictionary overflow: more than " + std::to_string(cap) +
+                  " distinct keys; use a larger chunk size");
+    if (dict_fallback_needed()) {
+      // more distinct keys than the rank sort takes: LSD radix sort of the dictionary
+      finish_dict_with_radix(0);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      download_output(r, ev[5]);
+    } else {
+      const u64 u = h_ctr->num_unique;
+      r.entries.resize(u);
+      for (u64 j = 0; j < u; ++j) {
+        for (int w = 0; w < kKeyWords; ++w) r.entries[j].key.w[w] = h_out[j].w[w];
+        r.entries[j].val = h_out[j].val;
+        r.entries[j].count = h_out[j].count;
+      }
+    }
+    stream_stats(nchunks, r);
+    r.num_unique = r.entries.size();
+    r.times.wall_ms = (now_ns() - t0) * 1e-6;
+    r.times.h2d_ms = 0;  // overlapped with the map: included in map_ms
     r.times.map_ms = ms_between(ev[1], ev[2]);
     r.times.process_ms = ms_between(ev[2], ev[3]);
     r.times.reduce_ms = ms_between(ev[3], ev[4]);
@@ -514,6 +706,7 @@ GpuWordCount::~GpuWordCount() = default;
 const JobConfig& GpuWordCount::config() const { return impl_->cfg; }
 u64 GpuWordCount::token_capacity() const { return impl_->cap; }
 char* GpuWordCount::input_buffer() { return impl_->h_text; }
+u64 GpuWordCount::text_capacity() const { return impl_->cap_bytes; }
 
 WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); }
 
@@ -586,18 +779,27 @@ class GpuShardEngine final : public ShardEngine {
 
   u64 map_local(const TextInput& shard, bool combine, DistStrategy plan) override {
     DevicePipeline& m = *mp_;
-    m.check_input(shard);
-    m.enqueue_upload(shard);
-    m.enqueue_map(shard);
     const bool compat = cfg_.map_path == MapPath::kCompat;
     samples_valid_ = false;
     dict_local_ = false;
     sorted_local_ = true;
+    stream_chunks_ = 0;
+    const bool streamed = shard.bytes > m.cap_bytes;
+    if (streamed) {
+      // a shard larger than one device pass: chunked H2D + map into one dictionary
+      LOCUST_CHECK_ARG(combine && cfg_.sort_path == SortPath::kDict,
+                       "streaming shards need the map-side combine of the dictionary path");
+      stream_chunks_ = m.enqueue_stream_insert(shard);
+    } else {
+      m.check_input(shard);
+      m.enqueue_upload(shard);
+      m.enqueue_map(shard);
+    }
     if (combine && cfg_.sort_path == SortPath::kDict) {
       if (plan == DistStrategy::kGather) {
         // Gather plan: the combined records go to rank 0 unsorted, straight from the
         // dictionary's dense arrays; no local sort at all.
-        m.enqueue_dict_insert((u32)shard.num_lines, compat, false);
+        if (!streamed) m.enqueue_dict_insert((u32)shard.num_lines, compat, false);
         launch_pack_records(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique, m.cap,
                             m.d_records, m.stream);
         m.read_counters();
@@ -612,7 +814,10 @@ class GpuShardEngine final : public ShardEngine {
       // Map-side combine through the dictionary: sorted distinct keys + counts.  The
       // shuffle records and the splitter samples are produced speculatively in the same
       // stream, so the common case costs ONE host synchronisation.
-      m.enqueue_process_dict((u32)shard.num_lines, compat);
+      if (streamed)
+        m.enqueue_rank();
+      else
+        m.enqueue_process_dict((u32)shard.num_lines, compat);
       m.enqueue_sorted_from_dict();
       set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
       launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
@@ -794,12 +999,16 @@ class GpuShardEngine final : public ShardEngine {
     local_stats_.num_lines = shard.num_lines;
     m.fill_counters(local_stats_);
     local_stats_.num_tokens = m.h_ctr->num_records;
+    if (stream_chunks_) m.stream_stats(stream_chunks_, local_stats_);
     local_count_ = n_records;
     return n_records;
   }
   // Dictionary table overflow: sort every token and combine the reference way.
   u64 map_overflow_fallback(const TextInput& shard) {
     DevicePipeline& m = *mp_;
+    if (stream_chunks_)
+      throw Error("streaming dictionary overflow: more than " + std::to_string(m.cap) +
+                  " distinct keys in one shard; use a larger chunk size");
     m.enqueue_process(0, false, false, m.h_ctr->num_records);
     m.enqueue_reduce_core(false);
     set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
@@ -826,6 +1035,7 @@ class GpuShardEngine final : public ShardEngine {
   const u32* local_n_ = nullptr;
   WordCountResult local_stats_;
   u64 local_count_ = 0;
+  size_t stream_chunks_ = 0;  // > 0: the last shard streamed through in this many chunks
   bool dict_local_ = false;   // the dictionary holds this rank's combined keys (mergeable)
   bool sorted_local_ = true;  // d_records are sorted (shuffle-ready)
 };

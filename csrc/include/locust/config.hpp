@@ -9,6 +9,7 @@
 
 #include <string>
 
+#include "locust/common.hpp"
 #include "locust/dstring.hpp"
 
 namespace locust {
@@ -27,7 +28,8 @@ enum class MapPath { kCompat, kFast };
 
 // Process-stage key sort: kRadix = LSD radix sort of packed keys (8-bit digits, constant
 // digit positions skipped); kDict = dictionary sort: hash the keys into a GPU table,
-// radix-sort only the unique keys, counting-sort the tokens by unique rank.
+// rank only the distinct keys (all-pairs weighted rank, or radix past 32K distinct); the
+// output (val = start of the key's run in the sorted token order) follows from the ranks.
 enum class SortPath { kRadix, kDict };
 
 struct JobConfig {
@@ -43,6 +45,9 @@ struct JobConfig {
   bool combine = false;                      // map-side combine (distributed shuffle)
   bool check = false;                        // LOCUST_CHECK invariants after each stage
   bool sync_plan = true;                     // read the sort plan back: launch only live passes
+  // > 0: a device pass holds at most this many text bytes; larger inputs stream through
+  // in line-aligned chunks (dictionary path).  0: one pass holds the whole input.
+  u64 chunk_bytes = 0;
 };
 
 // Fills the fields that have LOCUST_* environment overrides (LOCUST_CHECK=1,

@@ -54,12 +54,15 @@ struct WordCountResult {
   u64 overflow_lines = 0;   // lines that printed "WARN: Exceeded emit limit"
   u64 truncated = 0;        // tokens longer than max_key_len
   u64 max_key_len = 0;
+  u64 chunks = 1;           // > 1: the input streamed through the engine in chunks
   StageTimes times;
 };
 
 class GpuWordCount {
  public:
-  // Capacity is fixed at construction: inputs up to max_text_bytes / max_lines.
+  // Capacity is fixed at construction: max_text_bytes / max_lines per device pass.  With
+  // the dictionary path and the fast map, larger inputs stream through in line-aligned
+  // chunks of max_text_bytes (double-buffered H2D; one dictionary across chunks).
   GpuWordCount(const JobConfig& cfg, u64 max_text_bytes, u64 max_lines);
   ~GpuWordCount();
   GpuWordCount(const GpuWordCount&) = delete;
@@ -77,6 +80,7 @@ class GpuWordCount {
 
   const JobConfig& config() const;
   u64 token_capacity() const;
+  u64 text_capacity() const;  // bytes per device pass (input_buffer() size)
   // Pinned host staging buffer of the text (capacity max_text_bytes + 64).  A TextInput
   // whose data points here is uploaded without the host-side staging copy -- the
   // analogue of the reference loading the file into its host array before any timer.
@@ -85,6 +89,30 @@ class GpuWordCount {
  private:
   struct Impl;
   std::unique_ptr<Impl> impl_;
+};
+
+// Input text in page-locked host memory: the GPU engine DMAs it (whole, or chunk by chunk
+// when streaming) without a staging copy.  Falls back to ordinary memory when no GPU
+// runtime is present (CPU engine, build machine).
+class HostText {
+ public:
+  explicit HostText(u64 capacity);
+  ~HostText();
+  HostText(const HostText&) = delete;
+  HostText& operator=(const HostText&) = delete;
+  char* data() { return data_; }
+  const char* data() const { return data_; }
+  u64 size() const { return size_; }
+  u64 lines() const { return lines_; }
+  u64 capacity() const { return cap_; }
+  bool pinned() const { return pinned_; }
+  void set_size(u64 bytes, u64 lines);
+  TextInput input(u64 first_line = 0) const;
+
+ private:
+  char* data_ = nullptr;
+  u64 cap_ = 0, size_ = 0, lines_ = 0;
+  bool pinned_ = false;
 };
 
 class CpuWordCount {

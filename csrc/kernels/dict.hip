@@ -163,7 +163,8 @@ __global__ __launch_bounds__(kInsBlock) void dict_insert_kernel(ConstKeysSoA tok
                                                                 const u64* __restrict__ counts,
                                                                 const u32* __restrict__ d_n,
                                                                 DictWorkspace dw,
-                                                                MapCounters* __restrict__ ctr) {
+                                                                MapCounters* __restrict__ ctr,
+                                                                u32 n_cap) {
   __shared__ LdsSlot s_tab[kLdsSlots];
   for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) {
 #pragma unroll
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(kInsBlock) void dict_insert_kernel(ConstKeysSoA tok
     s_tab[i].count = 0;
   }
   __syncthreads();
-  const u32 n = *d_n;
+  const u32 n = min(*d_n, n_cap);  // the producer never writes past its capacity
   bool overflow = false;
   for (u32 i = blockIdx.x * kInsBlock + threadIdx.x; i < n; i += gridDim.x * kInsBlock) {
     u64 k[kKeyWords];
@@ -397,7 +398,7 @@ u32 grid_for(u64 n, u32 block, u32 max_blocks = 2048) {
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,
                         const DictWorkspace& dw, MapCounters* ctr, hipStream_t s) {
   dict_insert_kernel<<<dim3(grid_for(cap, kInsBlock, 1024)), dim3(kInsBlock), 0, s>>>(
-      tokens, counts, d_n, dw, ctr);
+      tokens, counts, d_n, dw, ctr, (u32)std::min<u64>(cap, 0xFFFFFFFFu));
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -12,6 +12,7 @@
 #include "locust/dist.hpp"
 #include "locust/dstring.hpp"
 #include "locust/engine.hpp"
+#include "locust/gen.hpp"
 #include "locust/io.hpp"
 
 namespace py = pybind11;
@@ -99,10 +100,17 @@ class PyGpuEngine {
   u64 capacity() const { return eng_.token_capacity(); }
   // Stage the text in the engine's pinned buffer once; run_loaded() then skips the copy.
   void load(const std::string& text) {
-    LOCUST_CHECK_ARG(text.size() <= max_bytes_, "text exceeds engine capacity");
-    std::memcpy(eng_.input_buffer(), text.data(), text.size());
-    loaded_ = eng_.input_buffer();
     loaded_in_ = as_input(text);
+    if (text.size() <= eng_.text_capacity()) {
+      std::memcpy(eng_.input_buffer(), text.data(), text.size());
+      loaded_ = eng_.input_buffer();
+    } else {
+      // larger than one device pass: keep it pinned, the engine streams it in chunks
+      big_ = std::make_unique<HostText>(text.size());
+      std::memcpy(big_->data(), text.data(), text.size());
+      big_->set_size(text.size(), loaded_in_.num_lines);
+      loaded_ = big_->data();
+    }
     loaded_in_.data = loaded_;
   }
   PyResult run_loaded() {
@@ -110,10 +118,16 @@ class PyGpuEngine {
     py::gil_scoped_release nogil;
     return PyResult{eng_.run(loaded_in_)};
   }
+  // Text in pinned host memory, any size (larger than the capacity: streamed in chunks).
+  PyResult run_text(const HostText& t) {
+    py::gil_scoped_release nogil;
+    return PyResult{eng_.run(t.input())};
+  }
 
  private:
   GpuWordCount eng_;
   u64 max_bytes_;
+  std::unique_ptr<HostText> big_;
   char* loaded_ = nullptr;
   TextInput loaded_in_;
 };
@@ -198,12 +212,24 @@ class PyDistRank {
     char* pinned = eng_->input_buffer();
     if (pinned) {
       LOCUST_CHECK_ARG(shard_text_bytes.size() <= max_bytes_, "shard exceeds engine capacity");
-      std::memcpy(pinned, shard_text_bytes.data(), shard_text_bytes.size());
-      loaded_in_.data = pinned;
+      if (shard_text_bytes.size() <= cfg_.job.chunk_bytes || !cfg_.job.chunk_bytes) {
+        std::memcpy(pinned, shard_text_bytes.data(), shard_text_bytes.size());
+        loaded_in_.data = pinned;
+      } else {
+        big_ = std::make_unique<HostText>(shard_text_bytes.size());
+        std::memcpy(big_->data(), shard_text_bytes.data(), shard_text_bytes.size());
+        loaded_in_.data = big_->data();
+      }
     } else {
       loaded_text_ = shard_text_bytes;
       loaded_in_.data = loaded_text_.data();
     }
+    loaded_ = true;
+  }
+  // A HostText shard (pinned; may exceed the engine capacity: streamed).  The caller
+  // keeps it alive (the binding ties its lifetime to this rank).
+  void load_text(const HostText& t, u64 first_line) {
+    loaded_in_ = t.input(first_line);
     loaded_ = true;
   }
   py::tuple run_loaded() {
@@ -240,6 +266,7 @@ class PyDistRank {
   std::unique_ptr<Communicator> comm_;
   std::unique_ptr<ShardEngine> eng_;
   bool loaded_ = false;
+  std::unique_ptr<HostText> big_;
   std::string loaded_text_;
   TextInput loaded_in_;
 };
@@ -269,7 +296,8 @@ PYBIND11_MODULE(_locust, m) {
       .def_readwrite("sort_path", &JobConfig::sort_path)
       .def_readwrite("combine", &JobConfig::combine)
       .def_readwrite("check", &JobConfig::check)
-      .def_readwrite("sync_plan", &JobConfig::sync_plan);
+      .def_readwrite("sync_plan", &JobConfig::sync_plan)
+      .def_readwrite("chunk_bytes", &JobConfig::chunk_bytes);
 
   py::enum_<DistStrategy>(m, "DistStrategy")
       .value("auto", DistStrategy::kAuto)
@@ -301,6 +329,7 @@ PYBIND11_MODULE(_locust, m) {
       .def("run", &PyGpuEngine::run)
       .def("load", &PyGpuEngine::load)
       .def("run_loaded", &PyGpuEngine::run_loaded)
+      .def("run_text", &PyGpuEngine::run_text, py::arg("text"))
       .def("map_stage", &PyGpuEngine::map_stage)
       .def("reduce_stage", &PyGpuEngine::reduce_stage)
       .def("sort_keys", &PyGpuEngine::sort_keys)
@@ -321,6 +350,76 @@ PYBIND11_MODULE(_locust, m) {
   m.def("run_multi", &run_multi, py::arg("text"), py::arg("cfg"),
         "Loopback multi-rank WordCount in this process (one thread per rank).");
 
+  m.def(
+      "gen_text",
+      [](u64 lines, u64 bytes, u64 seed, u32 vocab, double zipf_s, u64 first_block, u32 threads) {
+        GenSpec g;
+        g.lines = lines;
+        g.bytes = bytes;
+        g.seed = seed;
+        g.vocab = vocab;
+        g.zipf_s = zipf_s;
+        g.first_block = first_block;
+        g.threads = threads;
+        std::string out;
+        {
+          py::gil_scoped_release nogil;
+          gen_text(g, &out);
+        }
+        return py::bytes(out);
+      },
+      py::arg("lines") = 0, py::arg("bytes") = 0, py::arg("seed") = 1, py::arg("vocab") = 50000,
+      py::arg("zipf_s") = 1.0, py::arg("first_block") = 0, py::arg("threads") = 0,
+      "Synthetic Hamlet-shaped text (deterministic in seed and 1,024-line block).");
+  m.def("gen_vocabulary", [](u32 vocab, u64 seed) {
+    std::vector<py::bytes> out;
+    for (const auto& w : gen_vocabulary(vocab, seed)) out.emplace_back(w);
+    return out;
+  }, py::arg("vocab"), py::arg("seed") = 1);
+
+  py::class_<HostText>(m, "HostText",
+                       "Input text in pinned host memory (DMA without staging; any size).")
+      .def(py::init<u64>(), py::arg("capacity"))
+      .def_static(
+          "from_bytes",
+          [](const std::string& b) {
+            auto t = std::make_unique<HostText>(b.size());
+            std::memcpy(t->data(), b.data(), b.size());
+            t->set_size(b.size(), count_lines(b.data(), b.size()));
+            return t;
+          },
+          py::arg("data"))
+      .def_static(
+          "generate",
+          [](u64 lines, u64 bytes, u64 seed, u32 vocab, double zipf_s, u64 first_block,
+             u32 threads, u64 capacity) {
+            GenSpec g;
+            g.lines = lines;
+            g.bytes = bytes;
+            g.seed = seed;
+            g.vocab = vocab;
+            g.zipf_s = zipf_s;
+            g.first_block = first_block;
+            g.threads = threads;
+            // lines mode: ~44 B per line on average, 100 B at most
+            const u64 cap = capacity ? capacity : (bytes ? bytes : lines * 100 + 64);
+            auto t = std::make_unique<HostText>(cap);
+            u64 nl = 0, n = 0;
+            {
+              py::gil_scoped_release nogil;
+              n = gen_text_into(g, t->data(), cap, &nl);
+            }
+            t->set_size(n, nl);
+            return t;
+          },
+          py::arg("lines") = 0, py::arg("bytes") = 0, py::arg("seed") = 1,
+          py::arg("vocab") = 50000, py::arg("zipf_s") = 1.0, py::arg("first_block") = 0,
+          py::arg("threads") = 0, py::arg("capacity") = 0)
+      .def_property_readonly("size", &HostText::size)
+      .def_property_readonly("lines", &HostText::lines)
+      .def_property_readonly("pinned", &HostText::pinned)
+      .def("to_bytes", [](const HostText& t) { return py::bytes(t.data(), t.size()); });
+
   py::class_<PyDistRank>(m, "DistRank")
       .def(py::init<const DistConfig&, int, const std::string&, const std::string&, int, u64, u64,
                     double>(),
@@ -329,6 +428,8 @@ PYBIND11_MODULE(_locust, m) {
       .def("run", &PyDistRank::run, py::arg("shard"), py::arg("first_line") = 0)
       .def("load", &PyDistRank::load, py::arg("shard"), py::arg("first_line") = 0)
       .def("run_loaded", &PyDistRank::run_loaded)
+      .def("load_text", &PyDistRank::load_text, py::arg("text"), py::arg("first_line") = 0,
+           py::keep_alive<1, 2>())
       .def("set_strategy", &PyDistRank::set_strategy)
       .def("barrier", &PyDistRank::barrier)
       .def("allreduce_max", &PyDistRank::allreduce_max)

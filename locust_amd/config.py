@@ -32,6 +32,7 @@ def make_config(
     combine: bool = False,
     check: bool | None = None,
     sync_plan: bool = True,
+    chunk_bytes: int | None = None,
 ):
     """Build a native ``JobConfig``.  ``None`` means: environment override or default."""
     cfg = _C.JobConfig()
@@ -53,6 +54,9 @@ def make_config(
         check = os.environ.get("LOCUST_CHECK", "0") not in ("", "0")
     cfg.check = check
     cfg.sync_plan = sync_plan
+    if chunk_bytes is None:
+        chunk_bytes = int(os.environ.get("LOCUST_CHUNK_MB", "0")) << 20
+    cfg.chunk_bytes = chunk_bytes
     return cfg
 
 
