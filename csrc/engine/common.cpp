@@ -84,6 +84,7 @@ void apply_env_overrides(JobConfig& cfg) {
     if (s == "dict") cfg.sort_path = SortPath::kDict;
   }
   if (const char* e = std::getenv("LOCUST_CHUNK_MB")) cfg.chunk_bytes = (u64)std::atoll(e) << 20;
+  if (const char* e = std::getenv("LOCUST_ZERO_COPY")) cfg.zero_copy_text = std::atoi(e);
 }
 
 const char* to_string(ReducePath p) { return p == ReducePath::kLds ? "lds" : "global"; }

@@ -64,6 +64,8 @@ struct DevicePipeline {
   u64* d_head_val = nullptr;
   u64* d_head_count = nullptr;
   u32* d_perm = nullptr;
+  u8* d_parts = nullptr;           // hash partition tag per token (partitioned dict build)
+  bool parts_ready = false;        // d_parts describes the current `tokens`
   OutRecord* d_out = nullptr;
   KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
   PackedKey* d_samples = nullptr;
@@ -81,6 +83,9 @@ struct DevicePipeline {
   // dictionary path: [table | ucount | rank] is one zeroed block
   DictWorkspace dict{};
   u64 dict_slots = 0;
+  u64 ucap = 0;       // dense distinct-key capacity of the dictionary
+  u64 h_out_cap = 0;  // records h_out holds
+  u64 h_keys_cap = 0;
   u32* d_rank = nullptr;
   u64 dict_zero_bytes = 0;
 
@@ -94,6 +99,8 @@ struct DevicePipeline {
   u64 h_chunk_cap = 0;
 
   char* h_text = nullptr;
+  char* d_h_text = nullptr;    // device view of the pinned h_text (zero-copy map input)
+  const char* map_text = nullptr;  // what the map kernel reads this run
   MapCounters* h_ctr = nullptr;
   SortPlan* h_plan = nullptr;
   OutRecord* h_out = nullptr;         // host-mapped output records
@@ -111,13 +118,18 @@ struct DevicePipeline {
                      "max_key_len must be in [1, 31]");
     cap_bytes = std::max<u64>(max_bytes, 1);
     cap_lines = std::max<u64>(max_lines, 1);
+    bool streaming = false;
     if (cfg.chunk_bytes && cap_bytes > cfg.chunk_bytes && !cap_records) {
       // streaming engine: one pass holds a chunk; its token capacity is bounded by bytes
       cap_bytes = cfg.chunk_bytes;
       cap_lines = cap_bytes;
+      streaming = true;
     }
     cap = cap_records ? cap_records
                       : std::min<u64>(cap_lines * (u64)cfg.emits_per_line, cap_bytes / 2 + 1);
+    // The dictionary of a streamed input collects the distinct keys of ALL chunks, and
+    // its sort/emit buffers are record-sized: give small chunks room for 2^20 of them.
+    if (streaming) cap = std::max<u64>(cap, 1ull << 20);
     cap = std::max<u64>(cap, 1);
     LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
     LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
@@ -135,10 +147,12 @@ struct DevicePipeline {
     // Hash table: >= 2x the distinct keys it can see (load factor <= 0.5), capped at
     // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
     dict_slots = 1024;
-    while (dict_slots < 2 * std::min<u64>(cap, 1ull << 24)) dict_slots <<= 1;
+    // dense distinct-key capacity: every key of a pass, at most 16M (a 2^25-slot table)
+    ucap = std::min<u64>(cap, 1ull << 24);
+    while (dict_slots < 2 * ucap) dict_slots <<= 1;
     // [table | ucount | uval | rank]
-    dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(cap * 8, 256) +
-                      cap * 4;
+    dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
+                      ucap * 4;
     const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
     sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan);
 
@@ -155,6 +169,7 @@ struct DevicePipeline {
     sz.add<u32>(compat ? cap_lines : 1);
     for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
     sz.add<u32>(cap);
+    sz.add<u8>(align_up(cap, 16) + 16);
     sz.add<OutRecord>(cap);
     sz.add<KeyCount>(cap);
     sz.add<PackedKey>(kMaxSamples);
@@ -169,7 +184,7 @@ struct DevicePipeline {
       sz.add<u64>(cap);
       sz.add<u32>(cap);
     }
-    for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(cap);
+    for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
     sz.add<char>(dict_zero_bytes);
     arena.size = sz.bytes + 4096;
     LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
@@ -190,6 +205,7 @@ struct DevicePipeline {
     d_head_val = arena.take<u64>(cap);
     d_head_count = arena.take<u64>(cap);
     d_perm = arena.take<u32>(cap);
+    d_parts = arena.take<u8>(align_up(cap, 16) + 16);
     d_out = arena.take<OutRecord>(cap);
     d_records = arena.take<KeyCount>(cap);
     d_samples = arena.take<PackedKey>(kMaxSamples);
@@ -221,15 +237,16 @@ struct DevicePipeline {
       rx.keys[b] = arena.take<u64>(cap);
       rx.vals[b] = arena.take<u32>(cap);
     }
-    for (int j = 0; j < kKeyWords; ++j) dict.ukeys.w[j] = arena.take<u64>(cap);
+    for (int j = 0; j < kKeyWords; ++j) dict.ukeys.w[j] = arena.take<u64>(ucap);
     {
       char* z = arena.take<char>(dict_zero_bytes);
       dict.table = reinterpret_cast<DictSlot*>(z);
       dict.ucount = reinterpret_cast<u64*>(z + align_up(dict_slots * sizeof(DictSlot), 256));
-      dict.uval = reinterpret_cast<u64*>(reinterpret_cast<char*>(dict.ucount) + align_up(cap * 8, 256));
-      d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.uval) + align_up(cap * 8, 256));
+      dict.uval = reinterpret_cast<u64*>(reinterpret_cast<char*>(dict.ucount) + align_up(ucap * 8, 256));
+      d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.uval) + align_up(ucap * 8, 256));
       dict.mask = (u32)(dict_slots - 1);
-      dict.ucap = (u32)cap;
+      dict.ucap = (u32)ucap;
+      dict.urank = d_rank;
     }
 
     char delim_buf[64] = {0};
@@ -238,18 +255,19 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipMemcpy(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice));
 
     LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      d_h_text = nullptr;  // not device-visible: always DMA
+    }
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
     // Output records and the counter snapshot are host-mapped: the emit kernel writes them
     // over PCIe directly (zero-copy), so a dictionary run needs no D2H copy at all.
-    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, cap * sizeof(OutRecord),
-                                   hipHostMallocMapped | hipHostMallocCoherent));
-    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out_mapped), h_out, 0));
+    grow_host_out(ucap);
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                    hipHostMallocMapped | hipHostMallocCoherent));
     LOCUST_HIP_CHECK(
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_ctr_mapped), h_ctr_mapped, 0));
-    LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, cap * kKeyWords * sizeof(u64), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
     std::memset(h_ctr, 0, sizeof(MapCounters));
@@ -276,6 +294,28 @@ struct DevicePipeline {
       if (p) (void)hipHostFree(p);
   }
 
+  // Host-mapped output records (zero-copy emit target); grown when a radix-path result
+  // has more distinct keys than the dictionary's capacity.
+  void grow_host_out(u64 n) {
+    if (n <= h_out_cap) return;
+    if (h_out) {
+      sync();
+      LOCUST_HIP_CHECK(hipHostFree(h_out));
+    }
+    h_out_cap = std::max<u64>(n, 1);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, h_out_cap * sizeof(OutRecord),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out_mapped), h_out, 0));
+  }
+  // Pinned staging for key up/downloads (stage-split paths only), allocated on demand.
+  void grow_host_keys(u64 n) {
+    if (n <= h_keys_cap) return;
+    if (h_keys) LOCUST_HIP_CHECK(hipHostFree(h_keys));
+    h_keys_cap = std::max<u64>(n, 1);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, h_keys_cap * kKeyWords * sizeof(u64),
+                                   hipHostMallocDefault));
+  }
+
   void check_input(const TextInput& in) const {
     if (in.bytes > cap_bytes || in.num_lines > cap_lines)
       throw Error("input (" + std::to_string(in.bytes) + " B, " + std::to_string(in.num_lines) +
@@ -286,21 +326,43 @@ struct DevicePipeline {
   void sync() { LOCUST_HIP_CHECK(hipStreamSynchronize(stream)); }
 
   // H2D of the text; zero counters and look-back scratch.
+  //  * zero-copy (small inputs, fast map): no copy at all -- the map kernel's 16-byte
+  //    staging loads read the pinned host buffer over PCIe, which for a ~200 KB text is
+  //    cheaper than an SDMA transfer's fixed latency.
+  //  * pinned input elsewhere (HostText): DMA straight from it.
+  //  * otherwise: host copy into the pinned buffer, then DMA.
   void enqueue_upload(const TextInput& in) {
-    if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
-    std::memset(h_text + in.bytes, 0, 16);
-    LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
+    map_text = d_text;
+    if (use_zero_copy(in)) {
+      if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
+      std::memset(h_text + in.bytes, 0, 16);
+      map_text = d_h_text;
+    } else if (in.data != h_text && in.bytes && host_pinned(in.data)) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
+    } else {
+      if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
+      std::memset(h_text + in.bytes, 0, 16);
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
+    }
     LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+  }
+  bool use_zero_copy(const TextInput& in) const {
+    if (cfg.map_path != MapPath::kFast || !d_h_text) return false;
+    if (cfg.zero_copy_text >= 0) return cfg.zero_copy_text > 0;
+    return in.bytes <= kZeroCopyMaxBytes;
   }
 
   void enqueue_map(const TextInput& in) {
+    parts_ready = cfg.map_path == MapPath::kFast;
     if (cfg.map_path == MapPath::kCompat) {
       launch_line_index(d_text, in.bytes, d_nl, d_ctr, lb_line, stream);
       launch_map_compat(d_text, in.bytes, d_nl, (u32)in.num_lines, d_delims, cfg.emits_per_line,
                         cfg.max_key_len, slots, d_line_counts, d_ctr, stream);
     } else {
-      launch_map_fast(d_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
-                      cfg.emits_per_line, cfg.max_key_len, tokens, cap, d_ctr, lb_map, stream);
+      launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
+                      cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
+                      stream);
     }
   }
 
@@ -345,33 +407,34 @@ struct DevicePipeline {
     enqueue_dict_insert(num_lines, compat, with_counts);
     enqueue_rank();
   }
-  // Fresh table, then every token (or weighted record) into it.
+  // Every token (or weighted record) into a fresh dictionary: the partitioned LDS build
+  // when the tokens carry partition tags and the pass is small, else the HBM table.
   void enqueue_dict_insert(u32 num_lines, bool compat, bool with_counts) {
     if (compat)
       launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
                            lb_compact, stream);
+    if (!compat && parts_ready && cap <= kPartBuildMaxTokens) {
+      launch_dict_part_build(tokens, with_counts ? d_counts : nullptr, d_parts,
+                             &d_ctr->num_records, cap, dict, d_ctr, stream);
+      return;
+    }
     LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
     launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
                        d_ctr, stream);
   }
   // Weighted ranks of the distinct keys (rank and uval must be zero).
   void enqueue_rank() {
-    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, cap, d_rank, dict.uval, stream);
-  }
-  // [uval | rank] of the zeroed block, for re-ranking after more keys were inserted.
-  void enqueue_zero_ranks() {
-    const u64 off = reinterpret_cast<char*>(dict.uval) - reinterpret_cast<char*>(dict.table);
-    LOCUST_HIP_CHECK(hipMemsetAsync(dict.uval, 0, dict_zero_bytes - off, stream));
+    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank, dict.uval, stream);
   }
   // Sorted distinct keys + counts (for the shuffle's range partition).
   void enqueue_sorted_from_dict() {
-    launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, cap, sorted,
+    launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, ucap, sorted,
                         d_sorted_counts, stream);
   }
   // Output records from the weighted ranks; `mapped` writes them (and the counters)
   // straight into host memory.
   void enqueue_emit_dict(bool mapped) {
-    launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, cap, d_ctr,
+    launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, ucap, d_ctr,
                      mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
   }
   // Radix-fallback reduce: scan of the sorted counts -> records in d_out.
@@ -412,6 +475,7 @@ struct DevicePipeline {
   void download_output(WordCountResult& r, hipEvent_t done) {
     read_counters();
     const u64 u = h_ctr->num_unique;
+    grow_host_out(u);
     if (u)
       LOCUST_HIP_CHECK(
           hipMemcpyAsync(h_out, d_out, u * sizeof(OutRecord), hipMemcpyDeviceToHost, stream));
@@ -588,7 +652,7 @@ struct DevicePipeline {
 
       LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
       LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
-      launch_map_fast(dtext, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, cap, d_ctr,
+      launch_map_fast(dtext, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap, d_ctr,
                       lb_map, stream);
       LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
       LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
@@ -632,7 +696,7 @@ struct DevicePipeline {
     sync();
     *h_ctr = *h_ctr_mapped;
     if (h_ctr->flags & kCtrDictOverflow)
-      throw Error("streaming dictionary overflow: more than " + std::to_string(cap) +
+      throw Error("streaming dictionary overflow: more than " + std::to_string(ucap) +
                   " distinct keys; use a larger chunk size");
     if (dict_fallback_needed()) {
       // more distinct keys than the rank sort takes: LSD radix sort of the dictionary
@@ -663,6 +727,7 @@ struct DevicePipeline {
   void download_keys(const KeysSoA& src, u64 n, std::vector<PackedKey>* out) {
     out->resize(n);
     if (!n) return;
+    grow_host_keys(n);
     for (int w = 0; w < kKeyWords; ++w)
       LOCUST_HIP_CHECK(hipMemcpyAsync(h_keys + (u64)w * n, src.w[w], n * sizeof(u64),
                                       hipMemcpyDeviceToHost, stream));
@@ -680,7 +745,9 @@ struct DevicePipeline {
   }
 
   void upload_tokens(const PackedKey* keys, u64 n) {
+    parts_ready = false;
     set_num_records(n);
+    grow_host_keys(n);
     for (u64 i = 0; i < n; ++i)
       for (int w = 0; w < kKeyWords; ++w) h_keys[(u64)w * n + i] = keys[i].w[w];
     if (n)
@@ -800,7 +867,7 @@ class GpuShardEngine final : public ShardEngine {
         // Gather plan: the combined records go to rank 0 unsorted, straight from the
         // dictionary's dense arrays; no local sort at all.
         if (!streamed) m.enqueue_dict_insert((u32)shard.num_lines, compat, false);
-        launch_pack_records(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique, m.cap,
+        launch_pack_records(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique, m.ucap,
                             m.d_records, m.stream);
         m.read_counters();
         if (!(m.h_ctr->flags & kCtrDictOverflow)) {
@@ -857,7 +924,7 @@ class GpuShardEngine final : public ShardEngine {
     if (sorted_local_) return;
     DevicePipeline& m = *mp_;
     if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
-      m.enqueue_rank();  // ranks are still zero from the insert's table reset
+      m.enqueue_rank();  // ranks are zero: reset with the table / written by the build
       m.enqueue_sorted_from_dict();
     } else {
       radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
@@ -914,7 +981,8 @@ class GpuShardEngine final : public ShardEngine {
     DevicePipeline& r = *rp_;
     // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
     r.set_num_records(n);
-    launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.stream);
+    launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
+    r.parts_ready = true;
     WordCountResult tmp;
     bool downloaded = false;
     if (cfg_.sort_path == SortPath::kDict) {
@@ -945,37 +1013,11 @@ class GpuShardEngine final : public ShardEngine {
     range_entries_ = std::move(tmp.entries);
   }
 
+  // The root's own combined records go behind the received ones; one dictionary pass over
+  // all of them (partition tags come from the unpack) yields the merged, ranked output.
   void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) override {
     DevicePipeline& m = *mp_;
     DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
-    if (dict_local_) {
-      // Merge into this rank's own dictionary: only the other ranks' records are
-      // inserted, then the merged distinct keys are ranked and emitted (zero-copy).
-      launch_unpack_records(r.d_records, n_other, r.tokens, r.d_counts, m.stream);
-      m.h_u64[0] = n_other;
-      LOCUST_HIP_CHECK(hipMemcpyAsync(&r.d_ctr->num_records, m.h_u64, sizeof(u32),
-                                      hipMemcpyHostToDevice, m.stream));
-      m.enqueue_zero_ranks();
-      launch_dict_insert(r.tokens, r.d_counts, &r.d_ctr->num_records, std::max<u64>(n_other, 1),
-                         m.dict, m.d_ctr, m.stream);
-      m.enqueue_rank();
-      m.enqueue_emit_dict(/*mapped=*/true);
-      m.sync();
-      *m.h_ctr = *m.h_ctr_mapped;
-      if (!m.dict_fallback_needed()) {
-        const u64 u = m.h_ctr->num_unique;
-        range_entries_.resize(u);
-        for (u64 j = 0; j < u; ++j) {
-          for (int w = 0; w < kKeyWords; ++w) range_entries_[j].key.w[w] = m.h_out[j].w[w];
-          range_entries_[j].val = m.h_out[j].val;
-          range_entries_[j].count = m.h_out[j].count;
-        }
-        *total_count = m.h_ctr->total_count;
-        *num_unique = u;
-        return;
-      }
-    }
-    // General case: this rank's records behind the received ones, then the usual reduce.
     LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
     if (local_count_)
       LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
@@ -1007,7 +1049,7 @@ class GpuShardEngine final : public ShardEngine {
   u64 map_overflow_fallback(const TextInput& shard) {
     DevicePipeline& m = *mp_;
     if (stream_chunks_)
-      throw Error("streaming dictionary overflow: more than " + std::to_string(m.cap) +
+      throw Error("streaming dictionary overflow: more than " + std::to_string(m.ucap) +
                   " distinct keys in one shard; use a larger chunk size");
     m.enqueue_process(0, false, false, m.h_ctr->num_records);
     m.enqueue_reduce_core(false);

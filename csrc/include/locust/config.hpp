@@ -48,7 +48,11 @@ struct JobConfig {
   // > 0: a device pass holds at most this many text bytes; larger inputs stream through
   // in line-aligned chunks (dictionary path).  0: one pass holds the whole input.
   u64 chunk_bytes = 0;
+  // Map input read straight from pinned host memory instead of an H2D copy: -1 auto
+  // (inputs <= kZeroCopyMaxBytes), 0 never, 1 always (fast map path only).
+  int zero_copy_text = -1;
 };
+constexpr u64 kZeroCopyMaxBytes = 1ull << 20;
 
 // Fills the fields that have LOCUST_* environment overrides (LOCUST_CHECK=1,
 // LOCUST_REDUCE_PATH=lds|global, LOCUST_MAP_PATH=compat|fast, LOCUST_SORT=radix|dict).

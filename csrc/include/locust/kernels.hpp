@@ -77,7 +77,7 @@ void launch_compact_slots(const u32* line_counts, u32 num_lines, int emits_per_l
 
 // Byte-parallel tokenizer: tokens compacted in text order straight into `out`.
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
-                     int max_key_len, KeysSoA out, u64 out_cap, MapCounters* ctr,
+                     int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s);
 
 // ---------------- radix_sort.hip ----------------
@@ -175,7 +175,17 @@ struct DictWorkspace {
   u64* uval;        // per-id weighted rank (= output val), zeroed per run
   u32 ucap;         // capacity of ukeys/ucount/uval: a key that would get id >= ucap sets
                     // kCtrDictOverflow (num_unique may then exceed ucap; consumers clamp)
+  u32* urank;       // per-id rank (rank sort output), zeroed per run
 };
+// Partitioned build (small inputs): every token carries its hash partition (parts[i], one
+// byte, written by the map kernel or by unpack_records); workgroup p aggregates partition
+// p in LDS and appends its distinct keys to ukeys/ucount (and zeroes uval/urank for them).
+// No table and no reset needed.  parts must be readable up to align_up(n, 16).
+constexpr int kDictParts = 256;
+constexpr u64 kPartBuildMaxTokens = 1ull << 18;  // beyond: the HBM-table insert scales better
+void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* parts,
+                            const u32* d_n, u64 cap, const DictWorkspace& dw, MapCounters* ctr,
+                            hipStream_t s);
 // Hash every token (with its count; null = 1) into the table; distinct keys land in
 // ukeys[0 .. ctr->num_unique) with summed counts in ucount.
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,
@@ -200,7 +210,9 @@ void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounte
 void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u64 cap,
                          KeyCount* out, hipStream_t s);
 // AoS KeyCount -> SoA keys + counts; sets ctr->num_records = n (host-known).
-void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, hipStream_t s);
+// (parts, optional: hash partition tag per record for the partitioned dictionary build)
+void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,
+                           hipStream_t s);
 // S evenly spaced keys of a sorted array of *d_n keys: sample[k] = keys[floor((k+0.5)*n/S)].
 void launch_sample_keys(ConstKeysSoA sorted, const u32* d_n, u32 num_samples, PackedKey* out,
                         hipStream_t s);

@@ -25,6 +25,7 @@
 //                 final (key, val, count) records for the D2H.
 #include <algorithm>
 
+#include "locust/device/hash.hpp"
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
@@ -43,18 +44,8 @@ using dev::wave_id;
 constexpr u64 kWordMagic = 0x0000FFFF0000FFFFull;
 constexpr u32 kIdFull = 0xFFFFFFFFu;  // slot id of a key that did not fit the dense arrays
 
-__device__ __forceinline__ u64 mix64(u64 x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return x;
-}
-
-__device__ __forceinline__ u64 key_hash(const u64* k) {
-  return mix64(k[0] ^ mix64(k[1] ^ (k[2] * 0x9e3779b97f4a7c15ull) ^ (k[3] << 1)));
-}
+using dev::key_hash;
+using dev::key_part;
 
 __device__ __forceinline__ u64 cas_agent(u64* p, u64 expected, u64 desired) {
   __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -192,6 +183,136 @@ __global__ __launch_bounds__(kInsBlock) void dict_insert_kernel(ConstKeysSoA tok
     overflow |= !global_insert(dw, kk, sl.count, ctr, key_hash(kk));
   }
   if (overflow) atomicOr(&ctr->flags, kCtrDictOverflow);
+}
+
+// ---------------------------------------------------------------------------------
+// Partitioned build (small inputs): the map kernel tags every token with its hash
+// partition (top hash byte).  Workgroup p owns partition p: it streams the partition
+// bytes (16 per load), inserts ITS tokens into a private 2,048-slot LDS table, then writes
+// the partition's distinct keys densely at an offset drawn with one atomic.  Every key is
+// aggregated by exactly one workgroup, so there is no HBM table, no table reset, no
+// global atomics per token, and the counts are written with plain stores.
+// ---------------------------------------------------------------------------------
+constexpr int kPartBlock = 1024;       // 16 waves: latency hiding for the gathers
+constexpr int kPartSlots = 2048;       // 80 KB of LDS
+constexpr int kPartWindow = kPartBlock * 16;  // partition bytes scanned per round
+constexpr int kPartPerThread = kPartSlots / kPartBlock;
+
+__device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h) {
+  u32 slot = (u32)(h >> 8) & (kPartSlots - 1);
+  for (int probe = 0; probe < kPartSlots;) {
+    LdsSlot& sl = tab[slot];
+    u64 w0 = sl.w[0];
+    if (w0 == 0) {
+      w0 = atomicCAS(reinterpret_cast<unsigned long long*>(&sl.w[0]), 0ull, (unsigned long long)k[0]);
+      if (w0 == 0) {
+#pragma unroll
+        for (int j = 1; j < kKeyWords; ++j)
+          __hip_atomic_store(&sl.w[j], k[j] ^ kWordMagic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c);
+        return true;
+      }
+    }
+    if (w0 == k[0]) {
+      const u64 x1 = __hip_atomic_load(&sl.w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const u64 x2 = __hip_atomic_load(&sl.w[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const u64 x3 = __hip_atomic_load(&sl.w[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (x1 == 0 || x2 == 0 || x3 == 0) continue;  // claimer (another wave) still writing
+      if ((x1 ^ kWordMagic) == k[1] && (x2 ^ kWordMagic) == k[2] && (x3 ^ kWordMagic) == k[3]) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c);
+        return true;
+      }
+    }
+    slot = (slot + 1) & (kPartSlots - 1);
+    ++probe;
+  }
+  return false;
+}
+
+// Per round: every thread loads 16 partition bytes (the next round's load is issued before
+// this round's inserts), appends the indices of its partition's tokens to an LDS list,
+// then the whole workgroup gathers those tokens' keys (independent loads across threads)
+// and inserts them.
+__global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
+    ConstKeysSoA tokens, const u64* __restrict__ counts, const u8* __restrict__ parts,
+    const u32* __restrict__ d_n, u32 n_cap, DictWorkspace dw, MapCounters* __restrict__ ctr) {
+  __shared__ LdsSlot s_tab[kPartSlots];
+  __shared__ u32 s_list[kPartWindow];  // worst case: every byte of a round matches
+  __shared__ u32 s_count;
+  __shared__ u32 s_scan[kPartBlock / 64 + 1];
+  __shared__ u32 s_base;
+  for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
+    s_tab[i].count = 0;
+  }
+  if (threadIdx.x == 0) s_count = 0;
+  __syncthreads();
+  const u32 p = blockIdx.x;
+  const u32 n = min(*d_n, n_cap);
+  bool full = false;
+  u32 pos = threadIdx.x * 16u;
+  uint4 v = pos < n ? *reinterpret_cast<const uint4*>(parts + pos) : uint4{0, 0, 0, 0};
+  for (u32 round = 0; round < n; round += kPartWindow, pos += kPartWindow) {
+    // match mask of this thread's 16 bytes
+    u32 mask = 0;
+    const u32 wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (((wv[q] >> (8 * b)) & 0xffu) == p && pos + (u32)(q * 4 + b) < n) mask |= 1u << (q * 4 + b);
+    const u32 next = pos + kPartWindow;
+    if (next < n) v = *reinterpret_cast<const uint4*>(parts + next);  // prefetch next round
+    if (mask) {
+      u32 at = atomicAdd(&s_count, (u32)__popc(mask));
+      while (mask) {
+        const int b = __ffs(mask) - 1;
+        mask &= mask - 1;
+        s_list[at++] = pos + (u32)b;
+      }
+    }
+    __syncthreads();
+    const u32 cnt = s_count;
+    for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
+      const u32 i = s_list[e];
+      u64 k[kKeyWords];
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) k[j] = tokens.w[j][i];
+      const u64 c = counts ? counts[i] : 1ull;
+      if (k[0] == 0 || c == 0) continue;
+      full |= !part_lds_insert(s_tab, k, c, key_hash(k));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_count = 0;
+    __syncthreads();
+  }
+  // dense output: thread t owns slots [t * 2, t * 2 + 2)
+  u32 mine = 0;
+#pragma unroll
+  for (int r = 0; r < kPartPerThread; ++r) mine += s_tab[threadIdx.x * kPartPerThread + r].w[0] != 0;
+  u32 total = 0;
+  const u32 excl = dev::block_exclusive_scan<u32, kPartBlock>(mine, s_scan, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(&ctr->num_unique, total) : 0u;
+  __syncthreads();
+  u32 id = s_base + excl;
+#pragma unroll
+  for (int r = 0; r < kPartPerThread; ++r) {
+    const LdsSlot& sl = s_tab[threadIdx.x * kPartPerThread + r];
+    if (sl.w[0] == 0) continue;
+    if (id < dw.ucap) {
+      dw.ukeys.w[0][id] = sl.w[0];
+#pragma unroll
+      for (int j = 1; j < kKeyWords; ++j) dw.ukeys.w[j][id] = sl.w[j] ^ kWordMagic;
+      dw.ucount[id] = sl.count;
+      dw.uval[id] = 0;  // the rank sort accumulates into these
+      dw.urank[id] = 0;
+    } else {
+      full = true;
+    }
+    ++id;
+  }
+  if (full) atomicOr(&ctr->flags, kCtrDictOverflow);
 }
 
 // rank[i] += #{ j in tile : key[j] < key[i] }, persistent over (i-tile, j-tile) pairs.
@@ -399,6 +520,14 @@ void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, 
                         const DictWorkspace& dw, MapCounters* ctr, hipStream_t s) {
   dict_insert_kernel<<<dim3(grid_for(cap, kInsBlock, 1024)), dim3(kInsBlock), 0, s>>>(
       tokens, counts, d_n, dw, ctr, (u32)std::min<u64>(cap, 0xFFFFFFFFu));
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* parts,
+                            const u32* d_n, u64 cap, const DictWorkspace& dw, MapCounters* ctr,
+                            hipStream_t s) {
+  dict_part_build_kernel<<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+      tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu), dw, ctr);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -6,6 +6,7 @@
 // sorted records by sample-sort splitters (so every bucket is a contiguous slice and rank
 // order == key order), packs them as 40-B KeyCount records and exchanges them with one
 // RCCL all-to-all-v over xGMI.
+#include "locust/device/hash.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
 
@@ -33,12 +34,14 @@ __global__ __launch_bounds__(256) void pack_records_kernel(ConstKeysSoA keys,
 
 __global__ __launch_bounds__(256) void unpack_records_kernel(const KeyCount* __restrict__ in,
                                                              u64 n, KeysSoA keys,
-                                                             u64* __restrict__ counts) {
+                                                             u64* __restrict__ counts,
+                                                             u8* __restrict__ parts) {
   for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     const KeyCount r = in[i];
 #pragma unroll
     for (int w = 0; w < kKeyWords; ++w) keys.w[w][i] = r.w[w];
     counts[i] = r.count;
+    if (parts) parts[i] = (u8)dev::key_part(dev::key_hash(r.w));
   }
 }
 
@@ -100,9 +103,10 @@ void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
-void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, hipStream_t s) {
+void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,
+                           hipStream_t s) {
   if (!n) return;
-  unpack_records_kernel<<<dim3(grid_for(n, 256)), dim3(256), 0, s>>>(in, n, keys, counts);
+  unpack_records_kernel<<<dim3(grid_for(n, 256)), dim3(256), 0, s>>>(in, n, keys, counts, parts);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -20,6 +20,7 @@
 //    packed key, and writes it straight into the dense SoA output.  The map output is
 //    born compacted, in text order, so the reference's 116,000-slot thrust::partition
 //    (main.cu:411) has nothing left to do.
+#include "locust/device/hash.hpp"
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
@@ -92,7 +93,7 @@ __device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32
 template <int kSteps>
 __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
-    u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
+    u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
     u32* __restrict__ tile_ctr) {
   constexpr int kSeg = kSteps * 64;
   constexpr int kTile = (kMapBlock / 64) * kSeg;
@@ -214,6 +215,8 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
       if (idx < out_cap) {
 #pragma unroll
         for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
+        // hash partition tag for the dictionary's partitioned build
+        if (parts) parts[idx] = (u8)dev::key_part(dev::key_hash(kw));
       }
     }
     dst += __popcll(m);
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
 }  // namespace
 
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
-                     int max_key_len, KeysSoA out, u64 out_cap, MapCounters* ctr,
+                     int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
@@ -239,13 +242,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsSmall * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsSmall><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
-        text, bytes, d, emits_per_line, max_key_len, out, out_cap, ctr, lb.status,
+        text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
         lb.tile_counter);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
-        text, bytes, d, emits_per_line, max_key_len, out, out_cap, ctr, lb.status,
+        text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
         lb.tile_counter);
   }
   LOCUST_HIP_LAUNCH_CHECK();

@@ -297,7 +297,8 @@ PYBIND11_MODULE(_locust, m) {
       .def_readwrite("combine", &JobConfig::combine)
       .def_readwrite("check", &JobConfig::check)
       .def_readwrite("sync_plan", &JobConfig::sync_plan)
-      .def_readwrite("chunk_bytes", &JobConfig::chunk_bytes);
+      .def_readwrite("chunk_bytes", &JobConfig::chunk_bytes)
+      .def_readwrite("zero_copy_text", &JobConfig::zero_copy_text);
 
   py::enum_<DistStrategy>(m, "DistStrategy")
       .value("auto", DistStrategy::kAuto)

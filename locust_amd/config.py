@@ -33,6 +33,7 @@ def make_config(
     check: bool | None = None,
     sync_plan: bool = True,
     chunk_bytes: int | None = None,
+    zero_copy_text: int | None = None,
 ):
     """Build a native ``JobConfig``.  ``None`` means: environment override or default."""
     cfg = _C.JobConfig()
@@ -57,6 +58,9 @@ def make_config(
     if chunk_bytes is None:
         chunk_bytes = int(os.environ.get("LOCUST_CHUNK_MB", "0")) << 20
     cfg.chunk_bytes = chunk_bytes
+    if zero_copy_text is None:
+        zero_copy_text = int(os.environ.get("LOCUST_ZERO_COPY", "-1"))
+    cfg.zero_copy_text = zero_copy_text
     return cfg
 
 

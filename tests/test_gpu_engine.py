@@ -18,6 +18,8 @@ PATHS = [
     dict(map_path="compat", reduce_path="lds"),
     dict(map_path="compat", reduce_path="global"),
     dict(map_path="fast", reduce_path="lds", sync_plan=False),
+    dict(map_path="fast", reduce_path="lds", sort="dict", zero_copy_text=0),
+    dict(map_path="fast", reduce_path="lds", sort="dict", zero_copy_text=1),
 ]
 
 
