@@ -76,10 +76,21 @@ def synth_shard(config: str, rank: int, world: int):
     return lc._C.HostText.generate(bytes=per, seed=1, first_block=first)
 
 
-def bench_single(text, steps: int, warmup: int, sort: str = "dict"):
+def bench_single(text, steps: int, warmup: int, sort: str = "dict", graph: int = -1):
+    """Whole-job time of `steps` back-to-back jobs, plus the median per-stage split from a
+    short run with hipGraph replay off (a replayed graph is not split into stages)."""
+    ms, gst, res = _time_single(text, steps, warmup, sort, graph)
+    _, stages, _ = _time_single(text, min(steps, 30), min(warmup, 5), sort, 0)
+    stages["graph_gpu_ms"] = gst["gpu_ms"]
+    stages["graph_wall_ms"] = gst["wall_ms"]
+    return ms, stages, res
+
+
+def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
     import locust_amd as lc
 
-    cfg = lc.make_config("gpu", reduce_path="lds", sort=sort, chunk_bytes=CHUNK_BYTES)
+    cfg = lc.make_config("gpu", reduce_path="lds", sort=sort, chunk_bytes=CHUNK_BYTES,
+                         graph=graph)
     if isinstance(text, bytes):
         nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
         eng = lc._C.GpuEngine(cfg, len(text), nlines)
@@ -90,7 +101,8 @@ def bench_single(text, steps: int, warmup: int, sort: str = "dict"):
         run = lambda: eng.run_text(text)  # noqa: E731
     for _ in range(warmup):
         res = run()
-    stage = {"map_ms": [], "process_ms": [], "reduce_ms": [], "h2d_ms": [], "d2h_ms": []}
+    stage = {"map_ms": [], "process_ms": [], "reduce_ms": [], "h2d_ms": [], "d2h_ms": [],
+             "gpu_ms": [], "wall_ms": []}
     t0 = time.perf_counter()
     for _ in range(steps):
         res = run()

@@ -85,6 +85,7 @@ void apply_env_overrides(JobConfig& cfg) {
   }
   if (const char* e = std::getenv("LOCUST_CHUNK_MB")) cfg.chunk_bytes = (u64)std::atoll(e) << 20;
   if (const char* e = std::getenv("LOCUST_ZERO_COPY")) cfg.zero_copy_text = std::atoi(e);
+  if (const char* e = std::getenv("LOCUST_GRAPH")) cfg.graph = std::atoi(e);
 }
 
 const char* to_string(ReducePath p) { return p == ReducePath::kLds ? "lds" : "global"; }

@@ -7,6 +7,8 @@
 // a single stream, hipEvents at every stage boundary, exact-size transfers, and look-back
 // scratch zeroed by ONE memset per run.
 #include <algorithm>
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 
 #include "locust/dist.hpp"
@@ -275,6 +277,7 @@ struct DevicePipeline {
 
   ~DevicePipeline() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (cstream) (void)hipStreamSynchronize(cstream);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -332,20 +335,78 @@ struct DevicePipeline {
   //  * pinned input elsewhere (HostText): DMA straight from it.
   //  * otherwise: host copy into the pinned buffer, then DMA.
   void enqueue_upload(const TextInput& in) {
+    prepare_upload(in);
+    enqueue_upload_device(in);
+  }
+  // Host half: stage the text where the device half expects it and pick the map's source.
+  enum class Upload { kZeroCopy, kDirect, kStaged };
+  Upload upload_mode = Upload::kStaged;
+  void prepare_upload(const TextInput& in) {
     map_text = d_text;
     if (use_zero_copy(in)) {
-      if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
-      std::memset(h_text + in.bytes, 0, 16);
+      upload_mode = Upload::kZeroCopy;
       map_text = d_h_text;
     } else if (in.data != h_text && in.bytes && host_pinned(in.data)) {
+      upload_mode = Upload::kDirect;
+      return;
+    } else {
+      upload_mode = Upload::kStaged;
+    }
+    if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
+    std::memset(h_text + in.bytes, 0, 16);
+  }
+  // Device half (capturable): the DMA if any, then the per-run reset of counters and
+  // look-back scratch.
+  void enqueue_upload_device(const TextInput& in) {
+    if (upload_mode == Upload::kDirect) {
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
       LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
-    } else {
-      if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
-      std::memset(h_text + in.bytes, 0, 16);
+    } else if (upload_mode == Upload::kStaged) {
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
     }
     LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+  }
+
+  // ---- hipGraph replay of the dictionary job ----
+  hipGraphExec_t graph_exec = nullptr;
+  struct GraphKey {
+    u64 bytes = ~0ull;
+    u64 lines = 0;
+    const char* src = nullptr;
+    const char* map_text = nullptr;
+    Upload mode = Upload::kStaged;
+    bool operator==(const GraphKey& o) const {
+      return bytes == o.bytes && lines == o.lines && src == o.src && map_text == o.map_text &&
+             mode == o.mode;
+    }
+  } graph_key;
+  bool use_graph() const {
+    if (cfg.graph >= 0) return cfg.graph > 0 && cfg.sort_path == SortPath::kDict;
+    return cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast;
+  }
+  // Capture [upload DMA + reset, map, dictionary build, rank, emit] once per input shape
+  // and source; later runs replay it with one hipGraphLaunch.
+  void launch_dict_graph(const TextInput& in, bool compat) {
+    const GraphKey key{in.bytes, in.num_lines, upload_mode == Upload::kDirect ? in.data : nullptr,
+                       map_text, upload_mode};
+    if (!graph_exec || !(key == graph_key)) {
+      if (graph_exec) {
+        LOCUST_HIP_CHECK(hipGraphExecDestroy(graph_exec));
+        graph_exec = nullptr;
+      }
+      hipGraph_t g = nullptr;
+      LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      enqueue_upload_device(in);
+      enqueue_map(in);
+      enqueue_process_dict((u32)in.num_lines, compat);
+      enqueue_emit_dict(/*mapped=*/true);
+      LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
+      LOCUST_HIP_CHECK(hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0));
+      LOCUST_HIP_CHECK(hipGraphDestroy(g));
+      graph_key = key;
+    }
+    parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
+    LOCUST_HIP_CHECK(hipGraphLaunch(graph_exec, stream));
   }
   bool use_zero_copy(const TextInput& in) const {
     if (cfg.map_path != MapPath::kFast || !d_h_text) return false;
@@ -422,20 +483,38 @@ struct DevicePipeline {
     launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
                        d_ctr, stream);
   }
-  // Weighted ranks of the distinct keys (rank and uval must be zero).
+  // Ranks of the distinct keys (rank and uval must be zero).  Default: the weighted rank --
+  // the all-pairs pass also sums the counts of the smaller keys, which IS the output's
+  // val, and rank_emit writes the records straight from it.  LOCUST_RANK=scan counts
+  // ranks only and derives val from a look-back scan of the counts in rank order
+  // (scatter + scan_pack: one more launch; measured slower on MI355X, kept for A/B).
+  static bool weighted_rank() {
+    static const bool w = [] {
+      const char* e = std::getenv("LOCUST_RANK");
+      return !(e && std::string(e) == "scan");
+    }();
+    return w;
+  }
   void enqueue_rank() {
-    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank, dict.uval, stream);
+    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank,
+                     weighted_rank() ? dict.uval : nullptr, stream);
   }
   // Sorted distinct keys + counts (for the shuffle's range partition).
   void enqueue_sorted_from_dict() {
     launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, ucap, sorted,
                         d_sorted_counts, stream);
   }
-  // Output records from the weighted ranks; `mapped` writes them (and the counters)
-  // straight into host memory.
+  // Output records in key order; `mapped` writes them (and the counters) straight into
+  // host memory (zero-copy: the host needs no D2H).
   void enqueue_emit_dict(bool mapped) {
-    launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, ucap, d_ctr,
-                     mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
+    if (weighted_rank()) {
+      launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, ucap, d_ctr,
+                       mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
+      return;
+    }
+    enqueue_sorted_from_dict();
+    launch_scan_pack(sorted, d_sorted_counts, ucap, d_ctr, mapped ? d_out_mapped : d_out, lb_scan,
+                     stream, mapped ? d_ctr_mapped : nullptr, (u32)kRankSortMax);
   }
   // Radix-fallback reduce: scan of the sorted counts -> records in d_out.
   void enqueue_reduce_dict() {
@@ -483,11 +562,16 @@ struct DevicePipeline {
     sync();
     fill_counters(r);
     r.entries.resize(u);
-    for (u64 j = 0; j < u; ++j) {
-      for (int w = 0; w < kKeyWords; ++w) r.entries[j].key.w[w] = h_out[j].w[w];
-      r.entries[j].val = h_out[j].val;
-      r.entries[j].count = h_out[j].count;
-    }
+    copy_out(r.entries, u);
+  }
+
+  // Host output records -> result entries: identical 48-byte layouts, one memcpy.
+  void copy_out(std::vector<WordCountEntry>& e, u64 u) const {
+    static_assert(sizeof(WordCountEntry) == sizeof(OutRecord), "entry layout");
+    static_assert(offsetof(WordCountEntry, val) == offsetof(OutRecord, val), "entry layout");
+    static_assert(offsetof(WordCountEntry, count) == offsetof(OutRecord, count), "entry layout");
+    e.resize(u);
+    if (u) std::memcpy(static_cast<void*>(e.data()), h_out, u * sizeof(OutRecord));
   }
 
   void fill_counters(WordCountResult& r) const {
@@ -513,18 +597,28 @@ struct DevicePipeline {
     r.num_lines = in.num_lines;
     const u64 t0 = now_ns();
     const bool compat = cfg.map_path == MapPath::kCompat;
-    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
-    enqueue_upload(in);
-    LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
-    enqueue_map(in);
-    LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
     const bool dict_path = cfg.sort_path == SortPath::kDict;
+    const bool graphed = dict_path && use_graph();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+    if (graphed) {
+      prepare_upload(in);
+      launch_dict_graph(in, compat);
+      for (int e = 1; e <= 5; ++e) LOCUST_HIP_CHECK(hipEventRecord(ev[e], stream));
+      r.times.graph = true;
+    } else {
+      enqueue_upload(in);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+      enqueue_map(in);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+    }
     if (dict_path) {
-      enqueue_process_dict((u32)in.num_lines, compat);
-      LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
-      enqueue_emit_dict(/*mapped=*/true);
-      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
-      LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+      if (!graphed) {
+        enqueue_process_dict((u32)in.num_lines, compat);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+        enqueue_emit_dict(/*mapped=*/true);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+        LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+      }
       sync();  // the one host synchronisation of a dictionary run
       *h_ctr = *h_ctr_mapped;
       if (dict_fallback_needed()) {
@@ -535,11 +629,7 @@ struct DevicePipeline {
         fill_counters(r);
         const u64 u = h_ctr->num_unique;
         r.entries.resize(u);
-        for (u64 j = 0; j < u; ++j) {
-          for (int w = 0; w < kKeyWords; ++w) r.entries[j].key.w[w] = h_out[j].w[w];
-          r.entries[j].val = h_out[j].val;
-          r.entries[j].count = h_out[j].count;
-        }
+        copy_out(r.entries, u);
       }
     } else {
       enqueue_process((u32)in.num_lines, compat, false);
@@ -555,6 +645,7 @@ struct DevicePipeline {
     r.times.process_ms = ms_between(ev[2], ev[3]);
     r.times.reduce_ms = ms_between(ev[3], ev[4]);
     r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    r.times.gpu_ms = ms_between(ev[0], ev[5]);
     if (cfg.check) validate_result(r);
     return r;
   }
@@ -706,11 +797,7 @@ struct DevicePipeline {
     } else {
       const u64 u = h_ctr->num_unique;
       r.entries.resize(u);
-      for (u64 j = 0; j < u; ++j) {
-        for (int w = 0; w < kKeyWords; ++w) r.entries[j].key.w[w] = h_out[j].w[w];
-        r.entries[j].val = h_out[j].val;
-        r.entries[j].count = h_out[j].count;
-      }
+      copy_out(r.entries, u);
     }
     stream_stats(nchunks, r);
     r.num_unique = r.entries.size();
@@ -994,12 +1081,7 @@ class GpuShardEngine final : public ShardEngine {
         r.finish_dict_with_radix(0, true);
       } else {
         r.fill_counters(tmp);
-        tmp.entries.resize(r.h_ctr->num_unique);
-        for (u64 j = 0; j < tmp.entries.size(); ++j) {
-          for (int w = 0; w < kKeyWords; ++w) tmp.entries[j].key.w[w] = r.h_out[j].w[w];
-          tmp.entries[j].val = r.h_out[j].val;
-          tmp.entries[j].count = r.h_out[j].count;
-        }
+        r.copy_out(tmp.entries, r.h_ctr->num_unique);
         downloaded = true;
       }
     } else {

@@ -51,6 +51,10 @@ struct JobConfig {
   // Map input read straight from pinned host memory instead of an H2D copy: -1 auto
   // (inputs <= kZeroCopyMaxBytes), 0 never, 1 always (fast map path only).
   int zero_copy_text = -1;
+  // Replay the dictionary job as one captured hipGraph (one launch instead of ~6 launches
+  // and 6 event records): -1 auto (dictionary path, fast map), 0 off, 1 on.  Per-stage
+  // times are then not split (StageTimes.gpu_ms has the whole device time).
+  int graph = -1;
 };
 constexpr u64 kZeroCopyMaxBytes = 1ull << 20;
 

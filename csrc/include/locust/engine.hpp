@@ -33,6 +33,9 @@ struct StageTimes {
   double h2d_ms = 0, map_ms = 0, process_ms = 0, reduce_ms = 0, d2h_ms = 0;
   // Host wall clock of the whole run() call (ms).
   double wall_ms = 0;
+  // Device time of the whole job (first to last enqueued operation, hipEvents).
+  double gpu_ms = 0;
+  bool graph = false;  // replayed as one hipGraph: the stage fields above are not split
   // Host timers placed where the reference placed them (launch-only map etc., BASELINE.md
   // "How the reference measured these"), filled when JobConfig.ref_timers is set.
   double ref_map_ms = 0, ref_process_ms = 0, ref_reduce_ms = 0;

@@ -203,7 +203,8 @@ void launch_rank_scatter(ConstKeysSoA keys, const u64* counts, const u32* rank, 
                          u64 cap, KeysSoA sorted, u64* sorted_counts, hipStream_t s);
 // val = exclusive scan of the sorted counts; writes OutRecords and ctr->total_count.
 void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounters* ctr,
-                      OutRecord* out, LookbackScratch lb, hipStream_t s);
+                      OutRecord* out, LookbackScratch lb, hipStream_t s,
+                      MapCounters* ctr_out = nullptr, u32 emit_limit = 0xFFFFFFFFu);
 
 // ---------------- shuffle.hip ----------------
 // SoA keys (+ counts, null = 1) -> AoS KeyCount records (the all-to-all payload).

@@ -329,6 +329,7 @@ __device__ __forceinline__ bool key_lt(const u64* a, const u64* b) {
 // With `counts`, val[i] also accumulates the total count of the smaller keys: the
 // "weighted rank" IS the reference's val (start of the key's run in the sorted token
 // array), so no scan over the sorted counts is needed afterwards.
+template <bool kWeighted>
 __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
                                                            const u64* __restrict__ counts,
                                                            const u32* __restrict__ d_u,
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
         const u32 t = threadIdx.x + r * kRankI;
 #pragma unroll
         for (int q = 0; q < kKeyWords; ++q) v[r][q] = t < jn ? keys.w[q][j0 + t] : 0;
-        cv[r] = (counts && t < jn) ? counts[j0 + t] : 0;
+        cv[r] = (kWeighted && t < jn) ? counts[j0 + t] : 0;
       }
 #pragma unroll
       for (int r = 0; r < kTrips; ++r) {
@@ -378,8 +379,11 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
     for (u32 t = 0; t < (u32)kRankJ; t += 4) {
       const uint4 a = *reinterpret_cast<const uint4*>(&s_w0[t]);
       const uint4 b = *reinterpret_cast<const uint4*>(&s_w0[t + 2]);
-      const uint4 ca = *reinterpret_cast<const uint4*>(&s_cnt[t]);
-      const uint4 cb = *reinterpret_cast<const uint4*>(&s_cnt[t + 2]);
+      uint4 ca{0, 0, 0, 0}, cb{0, 0, 0, 0};
+      if (kWeighted) {
+        ca = *reinterpret_cast<const uint4*>(&s_cnt[t]);
+        cb = *reinterpret_cast<const uint4*>(&s_cnt[t + 2]);
+      }
       const u64 o[4] = {((u64)a.y << 32) | a.x, ((u64)a.w << 32) | a.z,
                         ((u64)b.y << 32) | b.x, ((u64)b.w << 32) | b.z};
       const u64 oc[4] = {((u64)ca.y << 32) | ca.x, ((u64)ca.w << 32) | ca.z,
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
       for (int q = 0; q < 4; ++q) {
         const bool lt = o[q] < me[0];
         cnt += lt;
-        acc += lt ? oc[q] : 0;
+        if (kWeighted) acc += lt ? oc[q] : 0;
         eq += o[q] == me[0];
       }
     }
@@ -400,13 +404,13 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
         u64 other[kKeyWords] = {s_w0[t], s_rest[t][0], s_rest[t][1], s_rest[t][2]};
         if (key_lt(other, me)) {
           ++cnt;
-          acc += s_cnt[t];
+          if (kWeighted) acc += s_cnt[t];
         }
       }
     }
     if (cnt) {
       atomicAdd(&rank[i], cnt);
-      if (val) atomicAdd(reinterpret_cast<unsigned long long*>(&val[i]), (unsigned long long)acc);
+      if (kWeighted) atomicAdd(reinterpret_cast<unsigned long long*>(&val[i]), (unsigned long long)acc);
     }
   }
 }
@@ -473,11 +477,25 @@ __global__ __launch_bounds__(256) void scan_pack_kernel(ConstKeysSoA sorted,
                                                         MapCounters* __restrict__ ctr,
                                                         OutRecord* __restrict__ out,
                                                         u64* __restrict__ status,
-                                                        u32* __restrict__ tile_ctr) {
+                                                        u32* __restrict__ tile_ctr,
+                                                        MapCounters* __restrict__ ctr_out,
+                                                        u32 emit_limit) {
   __shared__ u64 s_scan[256 / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
   const u32 u = ctr->num_unique;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
+    // field by field: total_count belongs to the last tile
+    ctr_out->num_records = ctr->num_records;
+    ctr_out->num_unique = u;
+    ctr_out->overflow_lines = ctr->overflow_lines;
+    ctr_out->truncated = ctr->truncated;
+    ctr_out->num_newlines = ctr->num_newlines;
+    ctr_out->max_key_len = ctr->max_key_len;
+    ctr_out->flags = ctr->flags | (u > emit_limit ? kCtrNotEmitted : 0u);
+    if (u == 0) ctr_out->total_count = 0;
+  }
+  if (u > emit_limit) return;  // the producer (rank scatter) did not run: radix fallback
   const u32 num_tiles = (u32)div_up(u, kPackTile);
   const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
   if (tile >= num_tiles) return;
@@ -506,7 +524,10 @@ __global__ __launch_bounds__(256) void scan_pack_kernel(ConstKeysSoA sorted,
     }
     run += c[t];
   }
-  if (tile == num_tiles - 1 && threadIdx.x == 0) ctr->total_count = base + total;
+  if (tile == num_tiles - 1 && threadIdx.x == 0) {
+    ctr->total_count = base + total;
+    if (ctr_out) ctr_out->total_count = base + total;
+  }
 }
 
 u32 grid_for(u64 n, u32 block, u32 max_blocks = 2048) {
@@ -537,8 +558,12 @@ void launch_rank_sort(ConstKeysSoA keys, const u64* counts, const u32* d_u, u64 
   const u64 umax = cap < (u64)kRankSortMax ? cap : (u64)kRankSortMax;
   const u64 pairs = div_up(umax, kRankI) * div_up(umax, kRankJ);
   const u32 grid = (u32)(pairs < 2048 ? (pairs ? pairs : 1) : 2048);
-  rank_sort_kernel<<<dim3(grid), dim3(kRankI), 0, s>>>(keys, counts, d_u, rank, val,
-                                                       (u32)std::min<u64>(cap, 0xFFFFFFFFu));
+  const u32 ucap = (u32)std::min<u64>(cap, 0xFFFFFFFFu);
+  if (val && counts)
+    rank_sort_kernel<true><<<dim3(grid), dim3(kRankI), 0, s>>>(keys, counts, d_u, rank, val, ucap);
+  else
+    rank_sort_kernel<false><<<dim3(grid), dim3(kRankI), 0, s>>>(keys, nullptr, d_u, rank, nullptr,
+                                                               ucap);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
@@ -558,10 +583,11 @@ void launch_rank_scatter(ConstKeysSoA keys, const u64* counts, const u32* rank, 
 }
 
 void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounters* ctr,
-                      OutRecord* out, LookbackScratch lb, hipStream_t s) {
+                      OutRecord* out, LookbackScratch lb, hipStream_t s, MapCounters* ctr_out,
+                      u32 emit_limit) {
   const u32 tiles = (u32)div_up(cap ? cap : 1, kPackTile);
   scan_pack_kernel<<<dim3(tiles), dim3(256), 0, s>>>(sorted, counts, ctr, out, lb.status,
-                                                     lb.tile_counter);
+                                                     lb.tile_counter, ctr_out, emit_limit);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -36,6 +36,8 @@ struct PyResult {
     d["reduce_ms"] = r.times.reduce_ms;
     d["d2h_ms"] = r.times.d2h_ms;
     d["wall_ms"] = r.times.wall_ms;
+    d["gpu_ms"] = r.times.gpu_ms;
+    d["graph"] = r.times.graph;
     return d;
   }
   py::bytes format(bool cpu_format) const {
@@ -298,7 +300,8 @@ PYBIND11_MODULE(_locust, m) {
       .def_readwrite("check", &JobConfig::check)
       .def_readwrite("sync_plan", &JobConfig::sync_plan)
       .def_readwrite("chunk_bytes", &JobConfig::chunk_bytes)
-      .def_readwrite("zero_copy_text", &JobConfig::zero_copy_text);
+      .def_readwrite("zero_copy_text", &JobConfig::zero_copy_text)
+      .def_readwrite("graph", &JobConfig::graph);
 
   py::enum_<DistStrategy>(m, "DistStrategy")
       .value("auto", DistStrategy::kAuto)

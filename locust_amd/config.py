@@ -34,6 +34,7 @@ def make_config(
     sync_plan: bool = True,
     chunk_bytes: int | None = None,
     zero_copy_text: int | None = None,
+    graph: int | None = None,
 ):
     """Build a native ``JobConfig``.  ``None`` means: environment override or default."""
     cfg = _C.JobConfig()
@@ -61,6 +62,9 @@ def make_config(
     if zero_copy_text is None:
         zero_copy_text = int(os.environ.get("LOCUST_ZERO_COPY", "-1"))
     cfg.zero_copy_text = zero_copy_text
+    if graph is None:
+        graph = int(os.environ.get("LOCUST_GRAPH", "-1"))
+    cfg.graph = graph
     return cfg
 
 

@@ -11,3 +11,7 @@ timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -30 
 python -c "import json;d=json.load(open('$O/bench.json'));print('bench', d['value'], d['stages_ms_median'], '700:', d['hamlet700']['ms_per_step'], 'radix:', d['radix_path']['ms_per_step'])"
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- $GRAFT_REPO_ROOT/build/MapReduce $GRAFT_REPO_ROOT/data/hamlet.txt --warmup 5 --iters 20 --quiet > /dev/null
 cd $GRAFT_REPO_ROOT && python3 tools/kstats.py $O/prof/run_kernel_stats.csv
+if [ -n "$AB_ENV" ]; then
+  env $AB_ENV timeout -k 10 300 python bench.py > $O/bench_ab.json 2> $O/bench_ab.err || { tail -30 $O/bench_ab.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/bench_ab.json'));print('A/B $AB_ENV', d['value'], d['stages_ms_median'], '700:', d['hamlet700']['ms_per_step'])"
+fi
