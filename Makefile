@@ -73,7 +73,8 @@ debug:
 # Host-only sanitizer build: the CPU engine, I/O, TCP comm and the CLI with
 # --backend cpu.  (GPU ASan / xnack+ is not available on the GPU pool.)
 ASAN_SRCS := csrc/engine/common.cpp csrc/engine/cpu_wordcount.cpp csrc/engine/dist.cpp \
-             csrc/io/io.cpp csrc/comm/tcp_comm.cpp csrc/cli/main.cpp csrc/cli/asan_stubs.cpp
+             csrc/io/io.cpp csrc/io/gen.cpp csrc/comm/tcp_comm.cpp csrc/cli/main.cpp \
+             csrc/cli/asan_stubs.cpp
 asan: $(BUILD)/asan/MapReduce
 $(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
 	@mkdir -p $(dir $@)

@@ -1,0 +1,310 @@
+"""Job launcher: the master the reference documents but never shipped.
+
+The reference's README describes a master that reads a hosts file, sends each worker a
+``MapReduce file start end node 1`` command over TCP, moves the intermediate files and
+starts the reducers (/root/reference/README.md:18-29).  Three
+modes here:
+
+1. Local ranks (single node, one process per GPU -- what ``bench.py`` uses via
+   ``torch.distributed.run``; this launcher needs no torch)::
+
+       python -m locust_amd.parallel.launch --nproc 8 -- python bench.py --gpus 8
+
+   Sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT; the ranks meet over
+   the framework's TCP bootstrap and RCCL.  The first failing rank stops the job: the
+   others' process groups are terminated and its exit code is the launcher's.
+
+2. Ranks on worker daemons (multi-node)::
+
+       python -m locust_amd.parallel.launch --hosts hosts.txt --nproc-per-host 8 -- CMD...
+
+   Each daemon starts its host's ranks with the same environment; a failed rank makes
+   the launcher drop every other connection, and the daemons kill those ranks.
+
+3. The reference's stage-split WordCount over daemons (map -> spill files -> reduce)::
+
+       python -m locust_amd.parallel.launch --hosts hosts.txt --wordcount data/hamlet.txt
+
+   Line ranges go to the hosts as stage-1 commands (``--spill-format binary``), the
+   spills are fetched, and the reduce stage (which sorts its inputs, unlike the
+   reference's, bug B7) runs here over all of them and prints the usual output.
+"""
+from __future__ import annotations
+
+import argparse
+import base64
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+from .hosts import Host, load_hosts
+from .protocol import ProtocolError, recv_msg, request, send_msg
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_env(rank: int, local_rank: int, world: int, master_addr: str, master_port: int) -> dict:
+    return {
+        "RANK": str(rank),
+        "LOCAL_RANK": str(local_rank),
+        "WORLD_SIZE": str(world),
+        "LOCAL_WORLD_SIZE": "",  # filled per host by the caller
+        "MASTER_ADDR": master_addr,
+        "MASTER_PORT": str(master_port),
+    }
+
+
+# --------------------------------------------------------------------------------------
+# mode 1: local ranks
+# --------------------------------------------------------------------------------------
+def launch_local(cmd: list[str], nproc: int, master_addr: str = "127.0.0.1",
+                 master_port: int | None = None, timeout: float | None = None,
+                 extra_env: dict | None = None) -> int:
+    port = master_port or _free_port()
+    procs: list[subprocess.Popen] = []
+    for r in range(nproc):
+        env = dict(os.environ)
+        env.update(rank_env(r, r, nproc, master_addr, port))
+        env["LOCAL_WORLD_SIZE"] = str(nproc)
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    return _supervise(procs, timeout)
+
+
+def _supervise(procs: list[subprocess.Popen], timeout: float | None) -> int:
+    deadline = time.time() + timeout if timeout else None
+    failed_rc = 0
+    while True:
+        alive = False
+        for p in procs:
+            rc = p.poll()
+            if rc is None:
+                alive = True
+            elif rc != 0 and not failed_rc:
+                failed_rc = rc if rc > 0 else 128 - rc
+        if failed_rc or not alive:
+            break
+        if deadline and time.time() > deadline:
+            failed_rc = 124
+            break
+        time.sleep(0.05)
+    if failed_rc:
+        for p in procs:
+            if p.poll() is None:
+                _kill_group(p)
+    for p in procs:
+        p.wait()
+    return failed_rc
+
+
+def _kill_group(p: subprocess.Popen) -> None:
+    for sig in (signal.SIGTERM, signal.SIGKILL):
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            return
+        try:
+            p.wait(timeout=3)
+            return
+        except subprocess.TimeoutExpired:
+            continue
+
+
+# --------------------------------------------------------------------------------------
+# mode 2: ranks on daemons
+# --------------------------------------------------------------------------------------
+class _RemoteRun(threading.Thread):
+    """One rank (or stage) on a daemon; holds the connection for the process lifetime."""
+
+    def __init__(self, host: Host, argv: list[str], env: dict, token: str | None,
+                 timeout: float | None = None):
+        super().__init__(daemon=True)
+        self.host, self.argv, self.env, self.token = host, argv, env, token
+        self.timeout = timeout
+        self.reply: dict | None = None
+        self.sock: socket.socket | None = None
+
+    def run(self) -> None:
+        try:
+            self.sock = socket.create_connection((self.host.addr, self.host.port), timeout=30)
+            self.sock.settimeout(None)
+            req = {"op": "run", "argv": self.argv, "env": self.env, "timeout": self.timeout}
+            if self.token:
+                req["token"] = self.token
+            send_msg(self.sock, req)
+            self.reply = recv_msg(self.sock)
+        except (OSError, ProtocolError) as e:
+            self.reply = self.reply or {"ok": False, "rc": 255, "error": f"{self.host}: {e}"}
+        finally:
+            self.close()
+
+    def close(self) -> None:
+        s, self.sock = self.sock, None
+        if s is not None:
+            try:
+                s.close()
+            except OSError:
+                pass
+
+
+def _join_all(runs: list[_RemoteRun], what: str) -> int:
+    for r in runs:
+        r.start()
+    failed = None
+    while any(r.is_alive() for r in runs):
+        for r in runs:
+            if not r.is_alive() and r.reply is not None and not r.reply.get("ok"):
+                failed = r
+                break
+        if failed:
+            break
+        time.sleep(0.05)
+    if failed is None:
+        failed = next((r for r in runs if not (r.reply or {}).get("ok")), None)
+    if failed is not None:
+        for r in runs:
+            r.close()  # the daemons kill the process groups of dropped connections
+        for r in runs:
+            r.join(timeout=10)
+        rep = failed.reply or {}
+        sys.stderr.write(f"locust launch: {what} failed on {failed.host}: rc={rep.get('rc')} "
+                         f"{rep.get('error', '')}\n{rep.get('stderr', '')[-4000:]}\n")
+        rc = rep.get("rc")
+        return rc if isinstance(rc, int) and rc > 0 else 1
+    return 0
+
+
+def launch_remote(cmd: list[str], hosts: list[Host], nproc_per_host: int,
+                  master_addr: str | None = None, master_port: int | None = None,
+                  token: str | None = None, replies: list | None = None) -> int:
+    """Start world = sum over hosts of min(nproc_per_host, gpus=) ranks on the daemons.
+    `replies` (optional) receives each rank's daemon reply, in rank order."""
+    placement: list[tuple[Host, int]] = []
+    for h in hosts:
+        for lr in range(min(nproc_per_host, h.gpus or nproc_per_host)):
+            placement.append((h, lr))
+    world = len(placement)
+    addr = master_addr or hosts[0].addr
+    port = master_port or _free_port()
+    runs = []
+    for rank, (h, lr) in enumerate(placement):
+        env = rank_env(rank, lr, world, addr, port)
+        env["LOCAL_WORLD_SIZE"] = str(sum(1 for hh, _ in placement if hh == h))
+        runs.append(_RemoteRun(h, cmd, env, token))
+    rc = _join_all(runs, "rank")
+    if replies is not None:
+        replies.extend(r.reply for r in runs)
+    return rc
+
+
+# --------------------------------------------------------------------------------------
+# mode 3: stage-split WordCount over daemons
+# --------------------------------------------------------------------------------------
+def _fetch(host: Host, path: str, dest: str, token: str | None) -> None:
+    off = 0
+    with open(dest, "wb") as f:
+        while True:
+            req = {"op": "get", "path": path, "offset": off, "length": 32 << 20}
+            if token:
+                req["token"] = token
+            rep = request(host.addr, host.port, req, timeout=120)
+            if not rep.get("ok"):
+                raise RuntimeError(f"fetch {path} from {host}: {rep.get('error')}")
+            data = base64.b64decode(rep["data"])
+            f.write(data)
+            off += len(data)
+            if rep.get("eof") or not data:
+                break
+
+
+def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | None = None,
+                          backend: str = "gpu", workdir: str | None = None,
+                          remote_root: str | None = None, extra: list[str] | None = None) -> int:
+    """Map on every host (line ranges), fetch the spills, reduce them here."""
+    import tempfile
+
+    with open(path, "rb") as f:
+        nlines = sum(1 for _ in f)
+    parts = len(hosts)
+    bounds = [(nlines * k // parts, nlines * (k + 1) // parts) for k in range(parts)]
+    hello = []
+    for h in hosts:
+        req = {"op": "hello"}
+        if token:
+            req["token"] = token
+        rep = request(h.addr, h.port, req)
+        if not rep.get("ok"):
+            raise RuntimeError(f"{h}: {rep.get('error')}")
+        hello.append(rep)
+    runs = []
+    for k, (h, (s, e)) in enumerate(zip(hosts, bounds)):
+        root = remote_root or hello[k]["root"]
+        argv = [cli, os.path.abspath(path), str(s), str(e), str(k), "1", "--spill-dir", root,
+                "--spill-format", "binary", "--backend", backend] + list(extra or [])
+        runs.append(_RemoteRun(h, argv, {}, token))
+    rc = _join_all(runs, "map stage")
+    if rc:
+        return rc
+    tmp = workdir or tempfile.mkdtemp(prefix="locust_spills_")
+    os.makedirs(tmp, exist_ok=True)
+    local = []
+    for k, h in enumerate(hosts):
+        dest = os.path.join(tmp, f"out.{k}.kv")
+        _fetch(h, f"out.{k}.kv", dest, token)
+        local.append(dest)
+    # reduce here over every spill: `MapReduce - 0 0 0 2 --inputs a,b,...`
+    r = subprocess.run([cli, path, "0", "0", "0", "2", "--inputs", ",".join(local),
+                        "--backend", backend] + list(extra or []))
+    return r.returncode
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m locust_amd.parallel.launch",
+                                 description="Locust job launcher (local ranks, daemons, "
+                                             "stage-split WordCount)")
+    ap.add_argument("--nproc", type=int, default=0, help="local ranks (mode 1)")
+    ap.add_argument("--hosts", help="hosts file of worker daemons (modes 2 and 3)")
+    ap.add_argument("--nproc-per-host", type=int, default=1)
+    ap.add_argument("--master-addr", default=None)
+    ap.add_argument("--master-port", type=int, default=None)
+    ap.add_argument("--token-file", default=None,
+                    help="the daemons' shared secret (default: LOCUST_TOKEN)")
+    ap.add_argument("--timeout", type=float, default=None)
+    ap.add_argument("--wordcount", metavar="FILE", help="stage-split WordCount of FILE (mode 3)")
+    ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--cli", default=None, help="path of the MapReduce binary")
+    ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
+    token = os.environ.get("LOCUST_TOKEN")
+    if a.token_file:
+        with open(a.token_file, encoding="utf-8") as f:
+            token = f.read().strip()
+    if a.wordcount:
+        if not a.hosts:
+            ap.error("--wordcount needs --hosts")
+        from .._native import cli_path
+
+        return stage_split_wordcount(a.wordcount, load_hosts(a.hosts), a.cli or cli_path(),
+                                     token, a.backend)
+    if not cmd:
+        ap.error("no command given (put it after --)")
+    if a.hosts:
+        return launch_remote(cmd, load_hosts(a.hosts), a.nproc_per_host, a.master_addr,
+                             a.master_port, token)
+    return launch_local(cmd, max(a.nproc, 1), a.master_addr or "127.0.0.1", a.master_port,
+                        a.timeout)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

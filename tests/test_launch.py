@@ -1,0 +1,131 @@
+"""Hosts files, the worker daemon and the launcher (CPU only; several daemons on one box
+-- which the reference's fixed 127.0.0.1:1337 slave could not do)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+import pytest
+
+import locust_amd as lc
+from locust_amd.parallel import daemon, launch, parse_hosts
+from locust_amd.parallel.hosts import Host
+from locust_amd.parallel.protocol import request
+from locust_amd.utils import oracle
+
+
+def test_parse_hosts():
+    hs = parse_hosts("# cluster\n10.0.0.1 1337\n\n10.0.0.2 7001 gpus=4  # half node\n")
+    assert hs == [Host("10.0.0.1", 1337), Host("10.0.0.2", 7001, 4)]
+    for bad in ["", "10.0.0.1\n", "a b\n", "h 1 cpus=3\n", "h 1\nh 1\n", "h 70000\n"]:
+        with pytest.raises(ValueError):
+            parse_hosts(bad)
+
+
+TOKEN = "test-token-0123"
+
+
+def start_daemon(tmp_path, token=TOKEN):
+    got = {}
+    ev = threading.Event()
+
+    def ready(port):
+        got["port"] = port
+        ev.set()
+
+    root = str(tmp_path / f"root{len(os.listdir(tmp_path))}")
+    t = threading.Thread(target=daemon.serve, kwargs=dict(port=0, root=root, token=token,
+                                                         ready=ready), daemon=True)
+    t.start()
+    assert ev.wait(10)
+    return Host("127.0.0.1", got["port"]), root
+
+
+SELFTEST = [sys.executable, "-m", "locust_amd.parallel.selftest"]
+
+
+def test_daemon_auth_allowlist_and_files(tmp_path):
+    h, root = start_daemon(tmp_path)
+    assert not request(h.addr, h.port, {"op": "hello"})["ok"]  # no token
+    assert not request(h.addr, h.port, {"op": "hello", "token": "wrong"})["ok"]
+    tok = {"token": TOKEN}
+    assert request(h.addr, h.port, {"op": "hello", **tok})["ok"]
+    rep = request(h.addr, h.port, {"op": "run", **tok, "argv": SELFTEST + ["--fail-rank", "3",
+                                   "--code", "5"], "env": {"RANK": "3", "WORLD_SIZE": "4"}})
+    assert rep["rc"] == 5 and not rep["ok"]
+    assert json.loads(rep["stdout"])["WORLD_SIZE"] == "4"
+    # only the framework's own programs, no interpreter flags, no loader hooks
+    for argv in (["/bin/rm", "-rf", "x"], [sys.executable, "-c", "print(1)"],
+                 [sys.executable, "-m", "locust_amd.parallel.launch", "--", "/bin/true"],
+                 [sys.executable, "/tmp/evil.py"]):
+        rep = request(h.addr, h.port, {"op": "run", **tok, "argv": argv})
+        assert not rep["ok"] and "framework" in rep["error"], argv
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build",
+                       "MapReduce")
+    rep = request(h.addr, h.port, {"op": "run", **tok, "argv": [cli, "--gen", "/tmp/x.txt",
+                                                                "--gen-lines", "1"]})
+    assert not rep["ok"] and "--gen" in rep["error"]
+    rep = request(h.addr, h.port, {"op": "run", **tok, "argv": SELFTEST,
+                                   "env": {"LD_PRELOAD": "/tmp/x.so"}})
+    assert not rep["ok"] and "env" in rep["error"]
+    assert request(h.addr, h.port, {"op": "put", **tok, "path": "a/b.bin", "data": "aGVsbG8="})["ok"]
+    rep = request(h.addr, h.port, {"op": "get", **tok, "path": "a/b.bin"})
+    assert rep["ok"] and rep["data"] == "aGVsbG8=" and rep["eof"]
+    assert not request(h.addr, h.port, {"op": "get", **tok, "path": "../../etc/passwd"})["ok"]
+
+
+def test_daemon_refuses_unauthenticated_text_protocol(tmp_path):
+    h, _ = start_daemon(tmp_path)
+    with socket.create_connection((h.addr, h.port)) as s:
+        s.sendall(b"x ./MapReduce hamlet.txt 0 700 1 1\n")
+        assert s.recv(64).startswith(b"NAK")
+
+
+def test_daemon_creates_private_token(tmp_path):
+    tok = daemon.load_or_create_token(str(tmp_path / "r"))
+    path = tmp_path / "r" / "token"
+    assert path.read_text().strip() == tok and len(tok) >= 32
+    assert (path.stat().st_mode & 0o077) == 0
+    assert daemon.load_or_create_token(str(tmp_path / "r")) == tok
+
+
+def test_launch_local_env_and_failure_propagation(tmp_path):
+    out = tmp_path / "ranks"
+    out.mkdir()
+    code = ("import os; open(os.path.join(%r, os.environ['RANK']), 'w').write("
+            "os.environ['WORLD_SIZE'] + ' ' + os.environ['MASTER_PORT'])" % str(out))
+    assert launch.launch_local([sys.executable, "-c", code], 3) == 0
+    vals = {p.name: p.read_text() for p in out.iterdir()}
+    assert sorted(vals) == ["0", "1", "2"] and len(set(vals.values())) == 1
+    # rank 1 fails fast, rank 0 would sleep: the launcher stops it and returns rank 1's code
+    code = "import os,sys,time; r=int(os.environ['RANK']); time.sleep(30 if r==0 else 0); sys.exit(7 if r==1 else 0)"
+    assert launch.launch_local([sys.executable, "-c", code], 2, timeout=60) == 7
+
+
+def test_launch_remote_ranks(tmp_path):
+    h1, _ = start_daemon(tmp_path)
+    h2, _ = start_daemon(tmp_path)
+    replies = []
+    assert launch.launch_remote(SELFTEST, [h1, h2], 2, token=TOKEN, replies=replies) == 0
+    got = [json.loads(r["stdout"]) for r in replies]
+    assert [(g["RANK"], g["LOCAL_RANK"], g["WORLD_SIZE"]) for g in got] == \
+        [("0", "0", "4"), ("1", "1", "4"), ("2", "0", "4"), ("3", "1", "4")]
+    assert launch.launch_remote(SELFTEST + ["--fail-rank", "2", "--code", "9"], [h1, h2], 2,
+                                token=TOKEN) == 9
+    assert launch.launch_remote(SELFTEST, [h1], 1, token="wrong") != 0
+
+
+def test_stage_split_wordcount_over_daemons(tmp_path, hamlet, cli, capfd):
+    hosts = [start_daemon(tmp_path)[0] for _ in range(3)]
+    f = tmp_path / "h.txt"
+    f.write_bytes(hamlet)
+    rc = launch.stage_split_wordcount(str(f), hosts, cli, token=TOKEN, backend="cpu",
+                                      workdir=str(tmp_path / "spills"))
+    assert rc == 0
+    out = capfd.readouterr().out
+    ent = oracle.wordcount(hamlet)[0]
+    body = out[out.index("print key:"):out.rindex("\nDone")].rstrip("\n")
+    same = body == oracle.format_cpu(ent).decode().rstrip("\n")
+    assert same, body[:300]  # (no full diff: the output is 5,608 lines)
