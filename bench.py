@@ -86,6 +86,27 @@ def bench_single(text, steps: int, warmup: int, sort: str = "dict", graph: int =
     return ms, stages, res
 
 
+def ref_semantics(text: bytes, steps: int = 50, warmup: int = 5):
+    """Median Map / Process / Reduce with host timers where the reference took them
+    (main.cu:405-468): the same semantics as its published GTX 1060 numbers."""
+    import locust_amd as lc
+
+    cfg = lc.make_config("gpu", reduce_path="lds", graph=0, ref_timers=True)
+    nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
+    eng = lc._C.GpuEngine(cfg, len(text), nlines)
+    eng.load(text)
+    for _ in range(warmup):
+        eng.run_loaded()
+    acc = {"ref_map_ms": [], "ref_process_ms": [], "ref_reduce_ms": []}
+    for _ in range(steps):
+        t = eng.run_loaded().times()
+        for k in acc:
+            acc[k].append(t[k])
+    med = {k[4:]: round(statistics.median(v), 4) for k, v in acc.items()}
+    med["total_ms"] = round(sum(med.values()), 4)
+    return med
+
+
 def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
     import locust_amd as lc
 
@@ -217,6 +238,11 @@ def main() -> int:
             msr, str_, _ = bench_single(text, args.steps, args.warmup, sort="radix")
             extra["radix_path"] = {"ms_per_step": round(msr, 4),
                                    "stages_ms": {k: round(v, 4) for k, v in str_.items()}}
+            # Host timers placed like the reference's (launch-only map, B2/B4): the
+            # like-for-like comparison with BASELINE.md's per-stage rows.
+            extra["reference_semantics_ms"] = {
+                "hamlet4500": ref_semantics(text), "hamlet700": ref_semantics(load_text("hamlet700")),
+                "baseline": BASELINE_STAGES}
     else:
         dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank, args.comm)
         ms, stages, res, strategy = time_dist(dr, args.steps, args.warmup, args.strategy)

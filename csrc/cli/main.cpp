@@ -11,6 +11,7 @@
 //   --sort radix|dict  --gpus N  --emits-per-line N  --max-key N  --ref-compat
 //   --stage map|reduce  --spill-dir DIR  --spill-format text|binary  --inputs a,b,...
 //   --warmup N  --iters N  --json FILE  --quiet  --check  --device N  --chunk-mb N
+//   --ref-timers (stage times taken where the reference's host timers were)
 // and a synthetic-text generator (BASELINE configs "1M lines" / "10 GB"):
 //   MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]
 #include <algorithm>
@@ -114,6 +115,8 @@ bool parse(int argc, char** argv, CliArgs* a) {
       a->json = need("--json");
     } else if (s == "--quiet") {
       a->quiet = true;
+    } else if (s == "--ref-timers") {
+      a->cfg.ref_timers = true;
     } else if (s == "--chunk-mb") {
       a->cfg.chunk_bytes = (u64)std::atoll(need("--chunk-mb").c_str()) << 20;
     } else if (s == "--gen") {
@@ -314,10 +317,13 @@ int run(const CliArgs& a) {
       r = eng.run(text.input);
       walls.push_back(r.times.wall_ms);
     }
-    std::printf("GPU mapping %lld nanoseconds \n", ns(r.times.map_ms));
+    const bool rt = a.cfg.ref_timers;
+    std::printf("GPU mapping %lld nanoseconds \n", ns(rt ? r.times.ref_map_ms : r.times.map_ms));
     for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
-    std::printf("GPU stream compaction and sorting %lld nanoseconds \n", ns(r.times.process_ms));
-    std::printf("GPU reduce %lld nanoseconds \n", ns(r.times.reduce_ms));
+    std::printf("GPU stream compaction and sorting %lld nanoseconds \n",
+                ns(rt ? r.times.ref_process_ms : r.times.process_ms));
+    std::printf("GPU reduce %lld nanoseconds \n",
+                ns(rt ? r.times.ref_reduce_ms : r.times.reduce_ms));
   }
   if (r.truncated)
     LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",

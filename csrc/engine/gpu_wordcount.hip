@@ -8,6 +8,7 @@
 // scratch zeroed by ONE memset per run.
 #include <algorithm>
 #include <cstddef>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -79,7 +80,7 @@ struct DevicePipeline {
   char* d_sync = nullptr;
   u64 sync_bytes = 0;
   MapCounters* d_ctr = nullptr;
-  LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{};
+  LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{}, lb_dict{};
   RadixWorkspace rx{};
 
   // dictionary path: [table | ucount | rank] is one zeroed block
@@ -156,7 +157,7 @@ struct DevicePipeline {
     dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
                       ucap * 4;
     const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
-    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan);
+    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1);
 
     SizingPlan sz;
     sz.add<char>(cap_bytes + 64);
@@ -229,6 +230,8 @@ struct DevicePipeline {
     lb_heads = {st, counters + 3};
     st += t_heads;
     lb_scan = {st, counters + 4};
+    st += t_scan;
+    lb_dict = {st, counters + 5};
 
     rx.cap = cap;
     rx.tile_counters = arena.take<u32>(rx_zero_words);
@@ -278,6 +281,7 @@ struct DevicePipeline {
   ~DevicePipeline() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    if (d_ord_trace) (void)hipFree(d_ord_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -369,6 +373,7 @@ struct DevicePipeline {
 
   // ---- hipGraph replay of the dictionary job ----
   hipGraphExec_t graph_exec = nullptr;
+  bool graph_ordered = false;  // the captured job uses the ordered kernel
   struct GraphKey {
     u64 bytes = ~0ull;
     u64 lines = 0;
@@ -398,8 +403,7 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
       enqueue_upload_device(in);
       enqueue_map(in);
-      enqueue_process_dict((u32)in.num_lines, compat);
-      enqueue_emit_dict(/*mapped=*/true);
+      graph_ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr);
       LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
       LOCUST_HIP_CHECK(hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0));
       LOCUST_HIP_CHECK(hipGraphDestroy(g));
@@ -499,6 +503,70 @@ struct DevicePipeline {
     launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank,
                      weighted_rank() ? dict.uval : nullptr, stream);
   }
+  // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
+  // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
+  bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
+  void enqueue_dict_ordered(bool with_counts, bool mapped) {
+    launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
+                        cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
+                        lb_dict, stream, ord_trace());
+  }
+  // Diagnostics: LOCUST_ORD_TRACE=1 prints the ordered kernel's per-partition phase times
+  // (shader clock ticks) after each run.
+  u64* d_ord_trace = nullptr;
+  u64* ord_trace() {
+    static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
+    if (!on) return nullptr;
+    if (!d_ord_trace) {
+      LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 8 * sizeof(u64)));
+    }
+    return d_ord_trace;
+  }
+  void print_ord_trace() {
+    if (!d_ord_trace) return;
+    std::vector<u64> t(kDictParts * 8);
+    LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    u64 t0 = ~0ull;
+    for (int p = 0; p < kDictParts; ++p)
+      if (t[p * 8]) t0 = std::min(t0, t[p * 8]);
+    for (int p = 0; p < kDictParts; ++p) {
+      const u64* x = &t[p * 8];
+      if (!x[0] || !x[6]) continue;
+      std::fprintf(stderr,
+                   "ord p=%3d m=%5llu start=%6llu build=%6llu publish=%5llu wait=%6llu sort=%6llu "
+                   "write=%6llu end=%6llu\n",
+                   p, (unsigned long long)x[6], (unsigned long long)(x[0] - t0),
+                   (unsigned long long)(x[1] - x[0]), (unsigned long long)(x[2] - x[1]),
+                   (unsigned long long)(x[3] - x[2]), (unsigned long long)(x[4] - x[3]),
+                   (unsigned long long)(x[5] - x[4]), (unsigned long long)(x[5] - t0));
+    }
+  }
+  // Process + emit of a dictionary run; returns true if the ordered kernel was used.
+  bool enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process) {
+    if (!compat && ordered_ok()) {
+      enqueue_dict_ordered(with_counts, /*mapped=*/true);
+      if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+      return true;
+    }
+    enqueue_process_dict(num_lines, compat, with_counts);
+    if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+    enqueue_emit_dict(/*mapped=*/true);
+    return false;
+  }
+  // After an ordered run reported a partition overflow: redo Process + emit through the
+  // HBM table (the map output is still in `tokens`).
+  void redo_dict_on_table(u32 num_lines, bool with_counts) {
+    LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->num_unique, 0, sizeof(u32), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->flags, 0, sizeof(u32), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
+                       d_ctr, stream);
+    enqueue_rank();
+    enqueue_emit_dict(/*mapped=*/true);
+    sync();
+    *h_ctr = *h_ctr_mapped;
+  }
   // Sorted distinct keys + counts (for the shuffle's range partition).
   void enqueue_sorted_from_dict() {
     launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, ucap, sorted,
@@ -588,10 +656,61 @@ struct DevicePipeline {
     return ms;
   }
 
+  // Reference-semantics timing (JobConfig.ref_timers): the same device work, with host
+  // timestamps where main.cu:405-468 took them.  The H2D happens before the first timer,
+  // as main.cu:403 does.
+  WordCountResult run_ref_timed(const TextInput& in) {
+    check_input(in);
+    WordCountResult r;
+    r.num_lines = in.num_lines;
+    const bool compat = cfg.map_path == MapPath::kCompat;
+    const bool dict_path = cfg.sort_path == SortPath::kDict;
+    const u64 w0 = now_ns();
+    enqueue_upload(in);
+    sync();
+    const u64 t0 = now_ns();
+    enqueue_map(in);  // map timer: the launch only (main.cu:405-407)
+    const u64 t1 = now_ns();
+    if (dict_path) {
+      enqueue_process_dict((u32)in.num_lines, compat);
+    } else {
+      enqueue_process((u32)in.num_lines, compat, false);
+    }
+    sync();  // process timer ends once the sort is done (thrust::sort returns)
+    const u64 t2 = now_ns();
+    if (dict_path) {
+      enqueue_emit_dict(/*mapped=*/true);  // the last reduce kernel: launch only (B4)
+    } else {
+      enqueue_reduce_core(false);
+      enqueue_pack_output();
+    }
+    const u64 t3 = now_ns();
+    if (dict_path) {
+      sync();
+      *h_ctr = *h_ctr_mapped;
+      if (dict_fallback_needed()) {
+        finish_dict_with_radix((u32)in.num_lines);
+        download_output(r, nullptr);
+      } else {
+        fill_counters(r);
+        copy_out(r.entries, h_ctr->num_unique);
+      }
+    } else {
+      download_output(r, nullptr);
+    }
+    r.times.ref_map_ms = (t1 - t0) * 1e-6;
+    r.times.ref_process_ms = (t2 - t1) * 1e-6;
+    r.times.ref_reduce_ms = (t3 - t2) * 1e-6;
+    r.times.wall_ms = (now_ns() - w0) * 1e-6;
+    if (cfg.check) validate_result(r);
+    return r;
+  }
+
   WordCountResult run(const TextInput& in) {
     if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
         cfg.map_path == MapPath::kFast)
       return run_stream(in);
+    if (cfg.ref_timers) return run_ref_timed(in);
     check_input(in);
     WordCountResult r;
     r.num_lines = in.num_lines;
@@ -612,16 +731,18 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
     }
     if (dict_path) {
+      bool ordered = graph_ordered;
       if (!graphed) {
-        enqueue_process_dict((u32)in.num_lines, compat);
-        LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
-        enqueue_emit_dict(/*mapped=*/true);
+        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, ev[3]);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
       }
       sync();  // the one host synchronisation of a dictionary run
       *h_ctr = *h_ctr_mapped;
-      if (dict_fallback_needed()) {
+      const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
+      if (ordered) print_ord_trace();
+      if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, false);
+      if (!ordered_done && dict_fallback_needed()) {
         finish_dict_with_radix((u32)in.num_lines);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         download_output(r, ev[5]);
@@ -1073,11 +1194,12 @@ class GpuShardEngine final : public ShardEngine {
     WordCountResult tmp;
     bool downloaded = false;
     if (cfg_.sort_path == SortPath::kDict) {
-      r.enqueue_process_dict(0, false, true);
-      r.enqueue_emit_dict(/*mapped=*/true);
+      const bool ordered = r.enqueue_dict_job(0, false, true, nullptr);
       r.sync();
       *r.h_ctr = *r.h_ctr_mapped;
-      if (r.dict_fallback_needed()) {
+      const bool ordered_done = ordered && !(r.h_ctr->flags & kCtrDictOverflow);
+      if (ordered && !ordered_done) r.redo_dict_on_table(0, true);
+      if (!ordered_done && r.dict_fallback_needed()) {
         r.finish_dict_with_radix(0, true);
       } else {
         r.fill_counters(tmp);

@@ -55,6 +55,11 @@ struct JobConfig {
   // and 6 event records): -1 auto (dictionary path, fast map), 0 off, 1 on.  Per-stage
   // times are then not split (StageTimes.gpu_ms has the whole device time).
   int graph = -1;
+  // Also take host timers where the reference put them (main.cu:405-468, BASELINE.md "How
+  // the reference measured these"): Map = kernel launch only, Process = until the sort is
+  // done (includes the map kernel), Reduce = until the last reduce kernel is LAUNCHED.
+  // Adds host synchronisations, so it is a separate measurement mode.
+  bool ref_timers = false;
 };
 constexpr u64 kZeroCopyMaxBytes = 1ull << 20;
 

@@ -177,15 +177,26 @@ struct DictWorkspace {
                     // kCtrDictOverflow (num_unique may then exceed ucap; consumers clamp)
   u32* urank;       // per-id rank (rank sort output), zeroed per run
 };
-// Partitioned build (small inputs): every token carries its hash partition (parts[i], one
-// byte, written by the map kernel or by unpack_records); workgroup p aggregates partition
-// p in LDS and appends its distinct keys to ukeys/ucount (and zeroes uval/urank for them).
+// Partitioned build (small inputs): every token carries its partition (parts[i], the first
+// byte of its key, written by the map kernel or by unpack_records); workgroup p aggregates
+// partition p in LDS and appends its distinct keys to ukeys/ucount (and zeroes uval/urank).
 // No table and no reset needed.  parts must be readable up to align_up(n, 16).
 constexpr int kDictParts = 256;
 constexpr u64 kPartBuildMaxTokens = 1ull << 18;  // beyond: the HBM-table insert scales better
 void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                             const u32* d_n, u64 cap, const DictWorkspace& dw, MapCounters* ctr,
                             hipStream_t s);
+// Ordered build (partition = first key byte): aggregation, per-partition LDS sort,
+// look-back offsets and the final (key, val, count) records in ONE kernel.  `out` needs
+// room for every distinct key; `lb` needs kDictParts + 1 zeroed status words and a zeroed
+// tile counter.  Sets ctr->num_unique / total_count (and ctr_out, if given, like the
+// emit kernels); a partition past kPartSlots distinct keys sets kCtrDictOverflow.
+// `trace` (diagnostics, optional): per partition p, s_memtime stamps at trace[p*8 + 0..5]
+// (start, built, published, prefix known, sorted, written) and the key count at [p*8+6].
+void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
+                         const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
+                         MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
+                         u64* trace = nullptr);
 // Hash every token (with its count; null = 1) into the table; distinct keys land in
 // ukeys[0 .. ctr->num_unique) with summed counts in ucount.
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,

@@ -315,6 +315,246 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
   if (full) atomicOr(&ctr->flags, kCtrDictOverflow);
 }
 
+// ---------------------------------------------------------------------------------
+// Ordered build: Process AND Reduce in one kernel (small inputs).
+//
+// The partition of a token is its key's FIRST BYTE, so partitions are ordered: every key
+// of partition p sorts before every key of partition p+1.  Workgroup p (taken in launch
+// order from a ticket counter) aggregates its partition in LDS as above, compacts the
+// distinct keys, publishes (distinct keys, tokens) through a decoupled look-back, and --
+// while its predecessors resolve -- bitonic-sorts its keys in LDS.  Its output slice then
+// starts at the exclusive prefix of distinct keys, and each key's val (start of its run in
+// the sorted token order) is the prefix of tokens plus the scan of counts inside the
+// partition.  The records go straight to the output (host-mapped: zero-copy).  No rank
+// sort over all keys (U^2), no separate emit, one launch after the map.
+//
+// A partition with more than kPartSlots distinct keys (or any table overflow) marks the
+// run kCtrDictOverflow; the host then reruns the Process stage on the HBM-table path.
+// ---------------------------------------------------------------------------------
+constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
+constexpr int kOrdOvfShift = 20;
+constexpr int kOrdTokShift = 29;
+
+__device__ __forceinline__ bool ord_greater(u64 aw0, u32 as, u64 bw0, u32 bs, const LdsSlot* tab) {
+  if (aw0 != bw0) return aw0 > bw0;
+  if (as == 0xFFFFFFFFu || bs == 0xFFFFFFFFu) return as == 0xFFFFFFFFu && bs != 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 1; j < kKeyWords; ++j) {
+    const u64 x = tab[as].w[j] ^ kWordMagic, y = tab[bs].w[j] ^ kWordMagic;
+    if (x != y) return x > y;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
+    ConstKeysSoA tokens, const u64* __restrict__ counts, const u8* __restrict__ parts,
+    const u32* __restrict__ d_n, u32 n_cap, MapCounters* __restrict__ ctr,
+    OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace) {
+#define ORD_STAMP(k_)                                                          \
+  if (trace && threadIdx.x == 0) trace[(u64)p * 8 + (k_)] = __builtin_amdgcn_s_memtime()
+  __shared__ LdsSlot s_tab[kPartSlots];
+  __shared__ __attribute__((aligned(16))) u32 s_list[kPartWindow];  // later: sort arrays
+  __shared__ u32 s_count;
+  __shared__ u64 s_scan[kPartBlock / 64 + 1];
+  __shared__ u32 s_scan32[kPartBlock / 64 + 1];
+  __shared__ u32 s_tile;
+  __shared__ u64 s_prefix;
+  const u32 p = dev::acquire_tile(tile_ctr, &s_tile);  // partition = ticket: key order
+  ORD_STAMP(0);
+  for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
+    s_tab[i].count = 0;
+  }
+  if (threadIdx.x == 0) s_count = 0;
+  __syncthreads();
+  const u32 n = min(*d_n, n_cap);
+  bool full = false;
+  u32 pos = threadIdx.x * 16u;
+  uint4 v = pos < n ? *reinterpret_cast<const uint4*>(parts + pos) : uint4{0, 0, 0, 0};
+  for (u32 round = 0; round < n; round += kPartWindow, pos += kPartWindow) {
+    u32 mask = 0;
+    const u32 wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (((wv[q] >> (8 * b)) & 0xffu) == p && pos + (u32)(q * 4 + b) < n) mask |= 1u << (q * 4 + b);
+    const u32 next = pos + kPartWindow;
+    if (next < n) v = *reinterpret_cast<const uint4*>(parts + next);
+    {
+      // one LDS atomic per wave: the wave's matches are appended as one run
+      const u32 nm = (u32)__popc(mask);
+      const u32 incl = dev::wave_inclusive_scan(nm);
+      u32 wbase = 0;
+      if (dev::lane_id() == 63 && incl) wbase = atomicAdd(&s_count, incl);
+      wbase = (u32)__shfl((int)wbase, 63, 64);
+      u32 at = wbase + incl - nm;
+      while (mask) {
+        const int b = __ffs(mask) - 1;
+        mask &= mask - 1;
+        s_list[at++] = pos + (u32)b;
+      }
+    }
+    __syncthreads();
+    const u32 cnt = s_count;
+    for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
+      const u32 i = s_list[e];
+      u64 k[kKeyWords];
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) k[j] = tokens.w[j][i];
+      const u64 c = counts ? counts[i] : 1ull;
+      if (k[0] == 0 || c == 0) continue;
+      full |= !part_lds_insert(s_tab, k, c, key_hash(k));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_count = 0;
+    __syncthreads();
+  }
+  ORD_STAMP(1);
+  // ---- compact: dense (w0, slot) arrays in the list area ----
+  u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
+  u32* s_slot = s_list + 2 * kPartSlots;                 // [kPartSlots]
+  u32 mine = 0;
+  u64 wsum = 0;
+#pragma unroll
+  for (int r = 0; r < kPartPerThread; ++r) {
+    const LdsSlot& sl = s_tab[threadIdx.x * kPartPerThread + r];
+    if (sl.w[0]) {
+      ++mine;
+      wsum += sl.count;
+    }
+  }
+  u32 m = 0;
+  const u32 excl = dev::block_exclusive_scan<u32, kPartBlock>(mine, s_scan32, &m);
+  {
+    u32 d = excl;
+#pragma unroll
+    for (int r = 0; r < kPartPerThread; ++r) {
+      const u32 slot = threadIdx.x * kPartPerThread + r;
+      if (s_tab[slot].w[0]) {
+        s_w0[d] = s_tab[slot].w[0];
+        s_slot[d] = slot;
+        ++d;
+      }
+    }
+  }
+  u64 tok = 0;
+  (void)dev::block_exclusive_scan<u64, kPartBlock>(wsum, s_scan, &tok);
+  const int any_full = __syncthreads_or(full);
+  // ---- publish (distinct keys, tokens, overflow) and look back ----
+  const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
+  ORD_STAMP(2);
+  const u64 pre = dev::block_lookback(status, p, agg, &s_prefix);
+  ORD_STAMP(3);
+  const u64 base_m = pre & kOrdM;
+  const u64 base_tok = pre >> kOrdTokShift;
+  const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
+  // ---- sort the partition's keys: counting sort on the SECOND key byte (all keys here
+  // share the first), then rank inside each second-byte bucket by all-pairs compares --
+  // buckets are small, there are few barriers, and no bitonic network over m keys ----
+  u64* s_w0b = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);  // [kPartSlots]
+  u32* s_slotb = s_list + 5 * kPartSlots;                        // [kPartSlots]
+  u32* s_hist = s_list + 6 * kPartSlots;                         // [256]
+  u32* s_off = s_hist + 256;                                     // [256]
+  u32* s_cur = s_off + 256;                                      // [256]
+  if (threadIdx.x < 256) {
+    s_hist[threadIdx.x] = 0;
+    s_cur[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  if (!any_full && m > 1) {
+    for (u32 a = threadIdx.x; a < m; a += kPartBlock)
+      atomicAdd(&s_hist[(u32)(s_w0[a] >> 48) & 0xffu], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of 256 bucket sizes by one wave
+      const u32 l = threadIdx.x;
+      const u32 h0 = s_hist[4 * l], h1 = s_hist[4 * l + 1], h2 = s_hist[4 * l + 2],
+                h3 = s_hist[4 * l + 3];
+      const u32 sum4 = h0 + h1 + h2 + h3;
+      const u32 ex = dev::wave_inclusive_scan(sum4) - sum4;
+      s_off[4 * l] = ex;
+      s_off[4 * l + 1] = ex + h0;
+      s_off[4 * l + 2] = ex + h0 + h1;
+      s_off[4 * l + 3] = ex + h0 + h1 + h2;
+    }
+    __syncthreads();
+    for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
+      const u64 w = s_w0[a];
+      const u32 b = (u32)(w >> 48) & 0xffu;
+      const u32 q = s_off[b] + atomicAdd(&s_cur[b], 1u);
+      s_w0b[q] = w;
+      s_slotb[q] = s_slot[a];
+    }
+    __syncthreads();
+    for (u32 q = threadIdx.x; q < m; q += kPartBlock) {
+      const u64 w = s_w0b[q];
+      const u32 sl = s_slotb[q];
+      const u32 b = (u32)(w >> 48) & 0xffu;
+      const u32 lo = s_off[b], hi = lo + s_hist[b];
+      u32 rank = 0;
+      for (u32 r = lo; r < hi; ++r)
+        rank += (r != q) && ord_greater(w, sl, s_w0b[r], s_slotb[r], s_tab);
+      s_w0[lo + rank] = w;
+      s_slot[lo + rank] = sl;
+    }
+  }
+  __syncthreads();
+  ORD_STAMP(4);
+  // ---- vals: scan of the counts in sorted order; write the records ----
+  constexpr u32 kPer = kPartSlots / kPartBlock;  // items per thread (m <= kPartSlots)
+  u64 c[kPer];
+  u64 run = 0;
+#pragma unroll
+  for (u32 t = 0; t < kPer; ++t) {
+    const u32 i = threadIdx.x * kPer + t;
+    c[t] = i < m ? s_tab[s_slot[i]].count : 0;
+    run += c[t];
+  }
+  u64 tot2 = 0;
+  u64 at = dev::block_exclusive_scan<u64, kPartBlock>(run, s_scan, &tot2) + base_tok;
+  if (!any_full && ovf_before == 0) {
+#pragma unroll
+    for (u32 t = 0; t < kPer; ++t) {
+      const u32 i = threadIdx.x * kPer + t;
+      if (i < m) {
+        const LdsSlot& sl = s_tab[s_slot[i]];
+        OutRecord rec;
+        rec.w[0] = sl.w[0];
+#pragma unroll
+        for (int j = 1; j < kKeyWords; ++j) rec.w[j] = sl.w[j] ^ kWordMagic;
+        rec.val = at;
+        rec.count = c[t];
+        out[base_m + i] = rec;
+      }
+      at += c[t];
+    }
+  }
+  ORD_STAMP(5);
+  if (trace && threadIdx.x == 0) trace[(u64)p * 8 + 6] = m;
+  // ---- the last partition publishes the run's counters ----
+  if (p == kDictParts - 1 && threadIdx.x == 0) {
+    const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);
+    const u32 u = (u32)(base_m + m);
+    const u64 total = base_tok + tok;
+    ctr->num_unique = u;
+    ctr->total_count = total;
+    if (ovf_total) ctr->flags |= kCtrDictOverflow;
+    if (ctr_out) {
+      ctr_out->num_records = ctr->num_records;
+      ctr_out->num_unique = u;
+      ctr_out->overflow_lines = ctr->overflow_lines;
+      ctr_out->truncated = ctr->truncated;
+      ctr_out->num_newlines = ctr->num_newlines;
+      ctr_out->max_key_len = ctr->max_key_len;
+      ctr_out->total_count = total;
+      ctr_out->flags = ctr->flags | (ovf_total ? kCtrDictOverflow : 0u);
+    }
+  }
+}
+#undef ORD_STAMP
+
 // rank[i] += #{ j in tile : key[j] < key[i] }, persistent over (i-tile, j-tile) pairs.
 constexpr int kRankI = 256;
 constexpr int kRankJ = 256;
@@ -549,6 +789,15 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
                             hipStream_t s) {
   dict_part_build_kernel<<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
       tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu), dw, ctr);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
+                         const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
+                         MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace) {
+  dict_ordered_kernel<<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+      tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu), ctr, out, ctr_out,
+      lb.status, lb.tile_counter, trace);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -41,7 +41,7 @@ __global__ __launch_bounds__(256) void unpack_records_kernel(const KeyCount* __r
 #pragma unroll
     for (int w = 0; w < kKeyWords; ++w) keys.w[w][i] = r.w[w];
     counts[i] = r.count;
-    if (parts) parts[i] = (u8)dev::key_part(dev::key_hash(r.w));
+    if (parts) parts[i] = (u8)(r.w[0] >> 56);  // first key byte (see launch_dict_ordered)
   }
 }
 

@@ -215,8 +215,9 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
       if (idx < out_cap) {
 #pragma unroll
         for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
-        // hash partition tag for the dictionary's partitioned build
-        if (parts) parts[idx] = (u8)dev::key_part(dev::key_hash(kw));
+        // partition tag for the dictionary's partitioned builds: the first key byte
+        // (order-preserving, so per-partition sorts concatenate into the global order)
+        if (parts) parts[idx] = (u8)(kw[0] >> 56);
       }
     }
     dst += __popcll(m);

@@ -37,6 +37,9 @@ struct PyResult {
     d["d2h_ms"] = r.times.d2h_ms;
     d["wall_ms"] = r.times.wall_ms;
     d["gpu_ms"] = r.times.gpu_ms;
+    d["ref_map_ms"] = r.times.ref_map_ms;
+    d["ref_process_ms"] = r.times.ref_process_ms;
+    d["ref_reduce_ms"] = r.times.ref_reduce_ms;
     d["graph"] = r.times.graph;
     return d;
   }
@@ -301,7 +304,8 @@ PYBIND11_MODULE(_locust, m) {
       .def_readwrite("sync_plan", &JobConfig::sync_plan)
       .def_readwrite("chunk_bytes", &JobConfig::chunk_bytes)
       .def_readwrite("zero_copy_text", &JobConfig::zero_copy_text)
-      .def_readwrite("graph", &JobConfig::graph);
+      .def_readwrite("graph", &JobConfig::graph)
+      .def_readwrite("ref_timers", &JobConfig::ref_timers);
 
   py::enum_<DistStrategy>(m, "DistStrategy")
       .value("auto", DistStrategy::kAuto)

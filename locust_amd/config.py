@@ -35,6 +35,7 @@ def make_config(
     chunk_bytes: int | None = None,
     zero_copy_text: int | None = None,
     graph: int | None = None,
+    ref_timers: bool = False,
 ):
     """Build a native ``JobConfig``.  ``None`` means: environment override or default."""
     cfg = _C.JobConfig()
@@ -65,6 +66,7 @@ def make_config(
     if graph is None:
         graph = int(os.environ.get("LOCUST_GRAPH", "-1"))
     cfg.graph = graph
+    cfg.ref_timers = ref_timers
     return cfg
 
 

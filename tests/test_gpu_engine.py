@@ -136,3 +136,39 @@ def test_engine_reuse_and_stage_split(hamlet):
     assert toks == sorted(toks) and len(toks) == 7061 or len(toks) == oracle.wordcount(text)[1]
     red = eng.reduce_stage(list(reversed(toks)))
     assert red.entries() == r1
+
+
+@pytest.mark.parametrize("sort", ["dict", "radix"])
+def test_reference_semantics_timers(hamlet, sort):
+    """--ref-timers: same output; Map is launch-only, Process includes the map kernel."""
+    r = gpu(hamlet, sort=sort, ref_timers=True, graph=0)
+    assert r.entries() == oracle.wordcount(hamlet)[0]
+    t = r.times()
+    assert t["ref_map_ms"] > 0 and t["ref_process_ms"] > 0 and t["ref_reduce_ms"] > 0
+    assert t["ref_map_ms"] < t["ref_process_ms"]
+
+
+@pytest.mark.parametrize("graph", [0, 1])
+def test_graph_replay_repeated(hamlet, graph):
+    """The captured job replays correctly across runs and input changes (re-capture)."""
+    cfg = lc.make_config("gpu", check=True, graph=graph)
+    eng = lc._C.GpuEngine(cfg, len(hamlet), 5000)
+    for text in (hamlet, hamlet, oracle.window(hamlet, 0, 700), hamlet):
+        r = eng.run(text)
+        assert r.entries() == oracle.wordcount(text)[0]
+        assert r.times()["graph"] == bool(graph)
+
+
+@pytest.mark.parametrize("kind", ["one_partition_overflow", "many_keys_balanced"])
+def test_ordered_partitions_edge_cases(kind):
+    """The one-kernel ordered Process/Reduce: a partition (first key byte) with more
+    distinct keys than its LDS table falls back to the HBM table; > 32K distinct keys
+    spread over partitions are emitted directly."""
+    if kind == "one_partition_overflow":
+        words = [b"w%06d" % i for i in range(40000)]
+    else:
+        words = [bytes([97 + i % 26]) + b"%05d" % i for i in range(40000)]
+    text = b"".join(b" ".join(words[i:i + 10]) + b"\n" for i in range(0, len(words), 10))
+    ent, ntok, _ = oracle.wordcount(text)
+    r = gpu(text, graph=0)
+    assert r.num_tokens == ntok and r.entries() == ent
