@@ -1070,6 +1070,43 @@ class GpuShardEngine final : public ShardEngine {
       m.enqueue_upload(shard);
       m.enqueue_map(shard);
     }
+    if (combine && cfg_.sort_path == SortPath::kDict && !streamed && m.ordered_ok()) {
+      // Small pass: the ordered kernel gives this rank's distinct keys sorted, with counts,
+      // in one launch; one more kernel lays them out as shuffle records + SoA keys, and the
+      // splitter samples come along -- ONE host synchronisation for either strategy.
+      m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
+      launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
+                           m.d_records, m.stream);
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                      hipMemcpyDeviceToHost, m.stream));
+      m.read_counters();
+      if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+        samples_.assign(m.h_small, m.h_small + kSpecSamples);
+        samples_valid_ = true;
+        return finish_map_stats(shard, m.h_ctr->num_unique);
+      }
+      // a partition overflowed its LDS table: redo this rank's combine on the HBM table
+      LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->num_unique, 0, sizeof(u32), m.stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->flags, 0, sizeof(u32), m.stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(m.dict.table, 0, m.dict_zero_bytes, m.stream));
+      launch_dict_insert(m.tokens, nullptr, &m.d_ctr->num_records, m.cap, m.dict, m.d_ctr,
+                         m.stream);
+      m.read_counters();
+      if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
+      if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
+        m.enqueue_rank();
+        m.enqueue_sorted_from_dict();
+      } else {
+        radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                   m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+      }
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+      m.read_counters();
+      return finish_map_stats(shard, m.h_ctr->num_unique);
+    }
     if (combine && cfg_.sort_path == SortPath::kDict) {
       if (plan == DistStrategy::kGather) {
         // Gather plan: the combined records go to rank 0 unsorted, straight from the

@@ -222,7 +222,10 @@ void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounte
 void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u64 cap,
                          KeyCount* out, hipStream_t s);
 // AoS KeyCount -> SoA keys + counts; sets ctr->num_records = n (host-known).
-// (parts, optional: hash partition tag per record for the partitioned dictionary build)
+// Sorted OutRecords -> SoA sorted keys + counts and KeyCount shuffle records.
+void launch_out_to_sorted(const OutRecord* in, const u32* d_n, u64 cap, KeysSoA sorted,
+                          u64* counts, KeyCount* recs, hipStream_t s);
+// (parts, optional: partition tag per record for the partitioned dictionary builds)
 void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,
                            hipStream_t s);
 // S evenly spaced keys of a sorted array of *d_n keys: sample[k] = keys[floor((k+0.5)*n/S)].

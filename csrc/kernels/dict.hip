@@ -193,6 +193,21 @@ __global__ __launch_bounds__(kInsBlock) void dict_insert_kernel(ConstKeysSoA tok
 // aggregated by exactly one workgroup, so there is no HBM table, no table reset, no
 // global atomics per token, and the counts are written with plain stores.
 // ---------------------------------------------------------------------------------
+// Gather one packed key.  Keys are NUL-padded big-endian words, so a word whose last byte
+// is 0 ends the key and the remaining words are 0: most English words fit in the first
+// word, and the other three gathers are skipped.
+__device__ __forceinline__ void load_key(ConstKeysSoA t, u32 i, u64* k) {
+  k[0] = t.w[0][i];
+  k[1] = k[2] = k[3] = 0;
+  if (k[0] & 0xffull) {
+    k[1] = t.w[1][i];
+    if (k[1] & 0xffull) {
+      k[2] = t.w[2][i];
+      if (k[2] & 0xffull) k[3] = t.w[3][i];
+    }
+  }
+}
+
 constexpr int kPartBlock = 1024;       // 16 waves: latency hiding for the gathers
 constexpr int kPartSlots = 2048;       // 80 KB of LDS
 constexpr int kPartWindow = kPartBlock * 16;  // partition bytes scanned per round
@@ -277,8 +292,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
     for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
       const u32 i = s_list[e];
       u64 k[kKeyWords];
-#pragma unroll
-      for (int j = 0; j < kKeyWords; ++j) k[j] = tokens.w[j][i];
+      load_key(tokens, i, k);
       const u64 c = counts ? counts[i] : 1ull;
       if (k[0] == 0 || c == 0) continue;
       full |= !part_lds_insert(s_tab, k, c, key_hash(k));
@@ -402,8 +416,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
       const u32 i = s_list[e];
       u64 k[kKeyWords];
-#pragma unroll
-      for (int j = 0; j < kKeyWords; ++j) k[j] = tokens.w[j][i];
+      load_key(tokens, i, k);
       const u64 c = counts ? counts[i] : 1ull;
       if (k[0] == 0 || c == 0) continue;
       full |= !part_lds_insert(s_tab, k, c, key_hash(k));
@@ -494,8 +507,21 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       const u32 b = (u32)(w >> 48) & 0xffu;
       const u32 lo = s_off[b], hi = lo + s_hist[b];
       u32 rank = 0;
-      for (u32 r = lo; r < hi; ++r)
-        rank += (r != q) && ord_greater(w, sl, s_w0b[r], s_slotb[r], s_tab);
+      u32 r = lo;
+      for (; r + 4 <= hi; r += 4) {  // loads of 4 candidates in flight
+        u64 ow[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ow[t] = s_w0b[r + t];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (ow[t] != w) {
+            rank += ow[t] < w;
+          } else if (r + t != q) {
+            rank += ord_greater(w, sl, ow[t], s_slotb[r + t], s_tab);
+          }
+        }
+      }
+      for (; r < hi; ++r) rank += (r != q) && ord_greater(w, sl, s_w0b[r], s_slotb[r], s_tab);
       s_w0[lo + rank] = w;
       s_slot[lo + rank] = sl;
     }
