@@ -1,6 +1,7 @@
 // Distributed WordCount driver (backend-agnostic: any Communicator x any ShardEngine).
 // See locust/dist.hpp for the stage list and SURVEY.md §2.4/§5.8 for the design.
 #include "locust/dist.hpp"
+#include "locust/trace.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -154,7 +155,9 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const DistStrategy plan = !cfg.gather ? DistStrategy::kShuffle
                             : cfg.strategy == DistStrategy::kAuto ? eng.last_strategy
                                                                   : cfg.strategy;
+  TraceRange tr_job("locust:dist_job");
   const i32 st1 = local("map", [&] {
+    TraceRange tr("locust:map");
     n_local = eng.map_local(shard, cfg.job.combine, plan);
     if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
     eng.map_stats(&local_stats);
@@ -170,7 +173,10 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     std::memcpy(out1.data(), &h, sizeof(h));
     std::memcpy(out1.data() + sizeof(h), mine_samples.data(), (u64)S * sizeof(PackedKey));
   }
-  comm.allgather_host(out1.data(), all1.data(), m1);
+  {
+    TraceRange tr("locust:allgather_counts_samples");
+    comm.allgather_host(out1.data(), all1.data(), m1);
+  }
   check("map", reinterpret_cast<const i32*>(all1.data()), m1);
   std::vector<PackedKey> samples((size_t)P * S);
   std::vector<u64> counts((size_t)P);
@@ -214,8 +220,11 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       }
       st = local("shuffle", [&] { recv = eng.recv_records(sum_records); });
     }
-    exchange(n_local, sb.data(), so.data(), recv, me == 0 ? sum_records : 0, rb.data(), ro.data(),
-             st == 0);
+    {
+      TraceRange tr("locust:gather_to_root");
+      exchange(n_local, sb.data(), so.data(), recv, me == 0 ? sum_records : 0, rb.data(),
+               ro.data(), st == 0);
+    }
     const u64 t2 = now_ns();
     if (me == 0) {
       // The root merges: a failure here is the job's failure (only the root holds output).
@@ -282,7 +291,10 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   // status below (the all-to-all itself must be entered by every rank).
   void* recv = nullptr;
   i32 st3 = local("shuffle", [&] { recv = eng.recv_records(n_recv); });
-  exchange(n_local, sb.data(), so.data(), recv, n_recv, rb.data(), ro.data(), st3 == 0);
+  {
+    TraceRange tr("locust:alltoallv_shuffle");
+    exchange(n_local, sb.data(), so.data(), recv, n_recv, rb.data(), ro.data(), st3 == 0);
+  }
   const u64 t2 = now_ns();
 
   // ---------------- reduce, one allgather of {status, totals} ----------------

@@ -14,6 +14,7 @@
 
 #include "locust/dist.hpp"
 #include "locust/engine.hpp"
+#include "locust/trace.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
 
@@ -707,6 +708,7 @@ struct DevicePipeline {
   }
 
   WordCountResult run(const TextInput& in) {
+    TraceRange tr("locust:job");
     if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
         cfg.map_path == MapPath::kFast)
       return run_stream(in);
