@@ -137,4 +137,18 @@ int tokenize_line(const char* line, u64 len, const JobConfig& cfg, std::vector<P
 // Sorted unique keys + counts -> entries with val = exclusive prefix of counts.
 void entries_from_sorted_tokens(const PackedKey* sorted, u64 n, std::vector<WordCountEntry>* out);
 
+// Device self-test of the string library: one GPU thread per
+// string runs d_strlen / d_strcmp (with the next string) / d_strcpy_bounded / d_strtok_r /
+// d_itoa; the rows come back for comparison with the host build.
+constexpr int kStringTestMax = 128;
+struct StringTestOut {
+  int len, cmp_next, copy_len, ntok;
+  int tok_off[8];
+  char copy[30];
+  char itoa_buf[34];
+};
+std::vector<StringTestOut> run_string_selftest(const std::vector<std::string>& strings,
+                                               const std::vector<int>& ints,
+                                               const std::string& delims, int device = 0);
+
 }  // namespace locust

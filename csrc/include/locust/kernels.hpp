@@ -10,6 +10,7 @@
 #include "locust/common.hpp"
 #include "locust/config.hpp"
 #include "locust/dstring.hpp"
+#include "locust/engine.hpp"
 #include "locust/kv.hpp"
 
 namespace locust {
@@ -235,5 +236,9 @@ void launch_sample_keys(ConstKeysSoA sorted, const u32* d_n, u32 num_samples, Pa
 // offsets[P] = n.
 void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey* splitters,
                            u32 num_buckets, u64* offsets, hipStream_t s);
+
+// ---- device self-test of the string library (tests only; StringTestOut in engine.hpp) ----
+void launch_string_selftest(const char* blob, const u32* off, u32 n, const char* delims,
+                            const int* ints, StringTestOut* out, hipStream_t s);
 
 }  // namespace locust

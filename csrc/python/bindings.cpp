@@ -428,6 +428,27 @@ PYBIND11_MODULE(_locust, m) {
       .def_property_readonly("pinned", &HostText::pinned)
       .def("to_bytes", [](const HostText& t) { return py::bytes(t.data(), t.size()); });
 
+  m.def(
+      "device_string_selftest",
+      [](const std::vector<std::string>& strings, const std::vector<int>& ints,
+         const std::string& delims) {
+        std::vector<StringTestOut> rows;
+        {
+          py::gil_scoped_release nogil;
+          rows = run_string_selftest(strings, ints, delims);
+        }
+        py::list out;
+        for (const auto& o : rows) {
+          py::list offs;
+          for (int k = 0; k < std::min(o.ntok, 8); ++k) offs.append(o.tok_off[k]);
+          out.append(py::make_tuple(o.len, o.cmp_next, o.copy_len, py::bytes(o.copy), o.ntok,
+                                    offs, std::string(o.itoa_buf)));
+        }
+        return out;
+      },
+      py::arg("strings"), py::arg("ints"), py::arg("delims"),
+      "Run strlen/strcmp/strcpy_bounded/strtok_r/itoa on the GPU (one thread per string).");
+
   py::class_<PyDistRank>(m, "DistRank")
       .def(py::init<const DistConfig&, int, const std::string&, const std::string&, int, u64, u64,
                     double>(),

@@ -111,6 +111,31 @@ def test_empty_and_delimiter_only():
         assert r.num_tokens == 0 and r.entries() == []
 
 
+@pytest.mark.parametrize("kind,n", [("equal_runs", 50000), ("all_equal", 9000),
+                                    ("descending", 8192), ("descending", 8193),
+                                    ("every_length", 29 * 400), ("random", 100003)])
+def test_sort_keys_shapes(kind, n):
+    """radix sort vs Python sort on equal runs, all-equal, descending and
+    1..29-byte keys, across the single-workgroup / onesweep boundary (8,192)."""
+    rng = random.Random(n)
+    if kind == "equal_runs":
+        pool = [bytes(rng.choice(b"abcdefgh") for _ in range(rng.randint(1, 12))) for _ in range(300)]
+        keys = [rng.choice(pool) for _ in range(n)]
+    elif kind == "all_equal":
+        keys = [b"same"] * n
+    elif kind == "descending":
+        keys = sorted((b"k%08d" % i for i in range(n)), reverse=True)
+    elif kind == "every_length":
+        keys = [bytes(rng.choice(b"xyz") for _ in range(1 + i % 29)) for i in range(n)]
+    else:
+        keys = [bytes(rng.choice(b"aZ09~") for _ in range(rng.randint(1, 29))) for _ in range(n)]
+    eng = lc.Engine(lc.make_config("gpu"), 1 << 22, 1 << 18)
+    s, perm = eng.sort_keys(keys)
+    assert s == sorted(keys)
+    assert [keys[i] for i in perm] == s
+    assert all(a < b for a, b in zip(perm, perm[1:]) if keys[a] == keys[b])  # stable
+
+
 def test_sort_keys_random():
     rng = random.Random(2)
     keys = [bytes(rng.choice(b"aZ09\x80\xff~") for _ in range(rng.randint(1, 31))) for _ in range(50000)]

@@ -69,3 +69,29 @@ def test_pack_key_order_matches_bytes_order():
             for _ in range(500)]
     packed = sorted(keys, key=lambda k: pack_key(k))
     assert packed == sorted(keys)
+
+
+@pytest.mark.gpu
+def test_device_string_library_matches_host():
+    """the same cases on the device (one thread per string)."""
+    import locust_amd as lc
+
+    rng = random.Random(5)
+    alphabet = b"abcXYZ019 ,.-;:'()\"\t\x80\xff"
+    cases = [b"", b"   ", b"word", b"  lead and trail  ", b"a,b.c-d;e:f'g(h)i\"j\tk",
+             b"x" * 60, b"one,,,,two;;;three"]
+    cases += [bytes(rng.choice(alphabet) for _ in range(rng.randint(0, 100))).replace(b"\0", b"")
+              for _ in range(3000)]
+    ints = [rng.randint(-2**31, 2**31 - 1) for _ in cases]
+    rows = lc._C.device_string_selftest(cases, ints, DEFAULT_DELIMS.decode())
+    for i, (s, row) in enumerate(zip(cases, rows)):
+        ln, cmp_next, copy_len, copy, ntok, offs, it = row
+        assert ln == len(s)
+        if i + 1 < len(cases):
+            assert cmp_next == strcmp(s, cases[i + 1])
+        assert copy == s[:29] and copy_len == max(0, len(s) - 29)  # chars that did not fit
+        starts = [j for j in range(len(s)) if s[j] not in DEFAULT_DELIMS
+                  and (j == 0 or s[j - 1] in DEFAULT_DELIMS)]
+        assert ntok == len(py_strtok(s, DEFAULT_DELIMS)) == len(starts)
+        assert offs == starts[:8]
+        assert it == str(ints[i]) and it == itoa(ints[i], 10)
