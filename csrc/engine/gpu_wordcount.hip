@@ -1058,7 +1058,6 @@ class GpuShardEngine final : public ShardEngine {
     DevicePipeline& m = *mp_;
     const bool compat = cfg_.map_path == MapPath::kCompat;
     samples_valid_ = false;
-    dict_local_ = false;
     sorted_local_ = true;
     stream_chunks_ = 0;
     const bool streamed = shard.bytes > m.cap_bytes;
@@ -1119,7 +1118,6 @@ class GpuShardEngine final : public ShardEngine {
         m.read_counters();
         if (!(m.h_ctr->flags & kCtrDictOverflow)) {
           set_local(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique);
-          dict_local_ = true;
           sorted_local_ = false;
           return finish_map_stats(shard, m.h_ctr->num_unique);
         }
@@ -1142,7 +1140,6 @@ class GpuShardEngine final : public ShardEngine {
       if (!m.dict_fallback_needed()) {
         samples_.assign(m.h_small, m.h_small + kSpecSamples);
         samples_valid_ = true;
-        dict_local_ = true;
         return finish_map_stats(shard, m.h_ctr->num_unique);
       }
       if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
@@ -1150,7 +1147,6 @@ class GpuShardEngine final : public ShardEngine {
       radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
                  m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
       set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
-      dict_local_ = true;
     } else {
       m.enqueue_process((u32)shard.num_lines, compat, false);
       if (combine) {
@@ -1321,7 +1317,6 @@ class GpuShardEngine final : public ShardEngine {
   WordCountResult local_stats_;
   u64 local_count_ = 0;
   size_t stream_chunks_ = 0;  // > 0: the last shard streamed through in this many chunks
-  bool dict_local_ = false;   // the dictionary holds this rank's combined keys (mergeable)
   bool sorted_local_ = true;  // d_records are sorted (shuffle-ready)
 };
 
