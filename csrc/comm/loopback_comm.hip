@@ -39,8 +39,16 @@ struct LoopbackGroup::State {
       cv.notify_all();
       return;
     }
-    const bool ok = cv.wait_for(lk, std::chrono::seconds(300), [&] { return generation != gen; });
+    const bool ok = cv.wait_for(lk, std::chrono::seconds(300),
+                                [&] { return generation != gen || failed; });
+    if (failed) throw Error("loopback comm: another rank failed");
     if (!ok) throw Error("loopback comm: barrier timed out (a rank died?)");
+  }
+  // A rank failed outside a collective: wake every waiter so the group fails fast.
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    failed = true;
+    cv.notify_all();
   }
 };
 
@@ -120,6 +128,7 @@ LoopbackGroup::LoopbackGroup(int world, bool device_buffers)
   LOCUST_CHECK_ARG(world >= 1, "loopback world must be >= 1");
 }
 LoopbackGroup::~LoopbackGroup() = default;
+void LoopbackGroup::abort() { state_->abort(); }
 
 std::unique_ptr<Communicator> LoopbackGroup::comm(int rank) {
   LOCUST_CHECK_ARG(rank >= 0 && rank < state_->world, "bad loopback rank");

@@ -1,6 +1,7 @@
 // Single-process multi-rank driver: one thread per rank, loopback communicator, ranks
 // placed round-robin on the visible GPUs (or the CPU engine).  Used by `MapReduce --gpus N`
 // and by the tests that rehearse the 2/4/8-rank shuffle on a single GPU.
+#include <atomic>
 #include <exception>
 #include <thread>
 
@@ -36,12 +37,17 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
   LoopbackGroup group(P, gpu);
   std::vector<DistResult> results(schedule.size());
   std::vector<std::exception_ptr> errors((size_t)P);
+  std::vector<int> error_order((size_t)P, 0);
+  std::atomic<int> error_seq{0};
   std::vector<std::thread> threads;
   for (int r = 0; r < P; ++r) {
     threads.emplace_back([&, r] {
       try {
         JobConfig job = cfg.job;
         job.device = gpu ? (cfg.job.device + r) % ndev : 0;
+        // Ranks are threads of one process here: no stream capture while other ranks may
+        // allocate or copy (hipGraph replay is for one-process-per-GPU runs).
+        if (P > 1) job.graph = 0;
         std::unique_ptr<ShardEngine> eng =
             gpu ? make_gpu_shard_engine(job, shards[(size_t)r].bytes, shards[(size_t)r].num_lines)
                 : make_cpu_shard_engine(job);
@@ -53,12 +59,18 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
         }
       } catch (...) {
         errors[(size_t)r] = std::current_exception();
+        error_order[(size_t)r] = ++error_seq;
+        group.abort();  // ranks waiting in a collective fail now instead of timing out
       }
     });
   }
   for (auto& t : threads) t.join();
-  for (auto& e : errors)
-    if (e) std::rethrow_exception(e);
+  // report the root cause: the first rank that failed, not the ones that were woken up
+  int first = -1;
+  for (int r = 0; r < P; ++r)
+    if (errors[(size_t)r] && (first < 0 || error_order[(size_t)r] < error_order[(size_t)first]))
+      first = r;
+  if (first >= 0) std::rethrow_exception(errors[(size_t)first]);
   return results;
 }
 

@@ -7,6 +7,7 @@
 // a single stream, hipEvents at every stage boundary, exact-size transfers, and look-back
 // scratch zeroed by ONE memset per run.
 #include <algorithm>
+#include <array>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -258,7 +259,11 @@ struct DevicePipeline {
     char delim_buf[64] = {0};
     LOCUST_CHECK_ARG(cfg.delimiters.size() < sizeof(delim_buf), "too many delimiters");
     std::memcpy(delim_buf, cfg.delimiters.data(), cfg.delimiters.size());
-    LOCUST_HIP_CHECK(hipMemcpy(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice));
+    // on this pipeline's own stream: a legacy-stream copy would conflict with another
+    // thread's graph capture (loopback ranks share the process)
+    LOCUST_HIP_CHECK(
+        hipMemcpyAsync(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice, stream));
+    LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
 
     LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
     if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
@@ -282,6 +287,7 @@ struct DevicePipeline {
   ~DevicePipeline() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
     if (d_ord_trace) (void)hipFree(d_ord_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     for (auto& e : ev)
@@ -372,6 +378,37 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
   }
 
+  // ---- captured launch sequences (hipGraph), keyed by call site and shape ----
+  using GraphKeyArr = std::array<u64, 6>;
+  struct CachedGraph {
+    GraphKeyArr key;
+    hipGraphExec_t exec;
+  };
+  std::vector<CachedGraph> graph_cache;
+  // Replays the sequence `enqueue` captured for `key`, capturing it on first use.  The
+  // sequence may only enqueue work on `stream` (kernels, memsets, async copies).
+  template <class F>
+  void launch_cached(const GraphKeyArr& key, F&& enqueue) {
+    for (auto& g : graph_cache)
+      if (g.key == key) {
+        LOCUST_HIP_CHECK(hipGraphLaunch(g.exec, stream));
+        return;
+      }
+    if (graph_cache.size() >= 8) {  // shapes changed a lot: drop the oldest
+      LOCUST_HIP_CHECK(hipGraphExecDestroy(graph_cache.front().exec));
+      graph_cache.erase(graph_cache.begin());
+    }
+    hipGraph_t g = nullptr;
+    LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    enqueue();
+    LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
+    hipGraphExec_t exec = nullptr;
+    LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    LOCUST_HIP_CHECK(hipGraphDestroy(g));
+    graph_cache.push_back({key, exec});
+    LOCUST_HIP_CHECK(hipGraphLaunch(exec, stream));
+  }
+
   // ---- hipGraph replay of the dictionary job ----
   hipGraphExec_t graph_exec = nullptr;
   bool graph_ordered = false;  // the captured job uses the ordered kernel
@@ -401,7 +438,7 @@ struct DevicePipeline {
         graph_exec = nullptr;
       }
       hipGraph_t g = nullptr;
-      LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
       enqueue_upload_device(in);
       enqueue_map(in);
       graph_ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr);
@@ -1061,28 +1098,48 @@ class GpuShardEngine final : public ShardEngine {
     sorted_local_ = true;
     stream_chunks_ = 0;
     const bool streamed = shard.bytes > m.cap_bytes;
+    const bool small_ordered = combine && cfg_.sort_path == SortPath::kDict && !streamed &&
+                               cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
     if (streamed) {
       // a shard larger than one device pass: chunked H2D + map into one dictionary
       LOCUST_CHECK_ARG(combine && cfg_.sort_path == SortPath::kDict,
                        "streaming shards need the map-side combine of the dictionary path");
       stream_chunks_ = m.enqueue_stream_insert(shard);
-    } else {
+    } else if (!small_ordered) {
       m.check_input(shard);
       m.enqueue_upload(shard);
       m.enqueue_map(shard);
     }
-    if (combine && cfg_.sort_path == SortPath::kDict && !streamed && m.ordered_ok()) {
-      // Small pass: the ordered kernel gives this rank's distinct keys sorted, with counts,
-      // in one launch; one more kernel lays them out as shuffle records + SoA keys, and the
-      // splitter samples come along -- ONE host synchronisation for either strategy.
-      m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
-      launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
-                           m.d_records, m.stream);
+    if (small_ordered) {
+      // Small pass: upload, map and the ordered kernel give this rank's distinct keys
+      // sorted, with counts; one more kernel lays them out as shuffle records + SoA keys,
+      // and the splitter samples and counters come back -- one captured graph, ONE host
+      // synchronisation for either strategy.
+      m.check_input(shard);
+      m.prepare_upload(shard);
       set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
-      launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
-      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
-                                      hipMemcpyDeviceToHost, m.stream));
-      m.read_counters();
+      auto enqueue = [&] {
+        m.enqueue_upload_device(shard);
+        m.enqueue_map(shard);
+        m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
+        launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
+                             m.d_records, m.stream);
+        launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                        hipMemcpyDeviceToHost, m.stream));
+        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters),
+                                        hipMemcpyDeviceToHost, m.stream));
+      };
+      m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
+      if (m.use_graph())
+        m.launch_cached({2, shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text),
+                         (u64)m.upload_mode,
+                         m.upload_mode == DevicePipeline::Upload::kDirect
+                             ? reinterpret_cast<u64>(shard.data) : 0},
+                        enqueue);
+      else
+        enqueue();
+      m.sync();
       if (!(m.h_ctr->flags & kCtrDictOverflow)) {
         samples_.assign(m.h_small, m.h_small + kSpecSamples);
         samples_valid_ = true;
@@ -1258,6 +1315,39 @@ class GpuShardEngine final : public ShardEngine {
     DevicePipeline& m = *mp_;
     DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
     LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
+    const u64 n = n_other + local_count_;
+    if (cfg_.sort_path == SortPath::kDict && r.cap <= kPartBuildMaxTokens && r.use_graph()) {
+      // The whole merge as one captured sequence on the receive pipeline: own records
+      // behind the received ones, counters reset, unpack (with partition tags), the ordered
+      // kernel writing the final records into host-mapped memory.
+      r.h_u64[0] = n;  // read by the captured H2D at replay time
+      auto enqueue = [&] {
+        if (local_count_)
+          LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
+                                          local_count_ * sizeof(KeyCount),
+                                          hipMemcpyDeviceToDevice, r.stream));
+        LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, r.stream));
+        LOCUST_HIP_CHECK(hipMemcpyAsync(&r.d_ctr->num_records, r.h_u64, sizeof(u32),
+                                        hipMemcpyHostToDevice, r.stream));
+        launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
+        r.enqueue_dict_ordered(/*with_counts=*/true, /*mapped=*/true);
+      };
+      r.parts_ready = true;
+      r.launch_cached({3, n_other, local_count_, reinterpret_cast<u64>(m.d_records), 0, 0},
+                      enqueue);
+      r.sync();
+      *r.h_ctr = *r.h_ctr_mapped;
+      if (!(r.h_ctr->flags & kCtrDictOverflow)) {
+        WordCountResult tmp;
+        r.fill_counters(tmp);
+        r.copy_out(tmp.entries, r.h_ctr->num_unique);
+        *total_count = r.h_ctr->total_count;
+        *num_unique = r.h_ctr->num_unique;
+        range_entries_ = std::move(tmp.entries);
+        return;
+      }
+      // a partition overflowed: the general path below redoes the merge
+    }
     if (local_count_)
       LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
                                       local_count_ * sizeof(KeyCount), hipMemcpyDeviceToDevice,

@@ -85,6 +85,8 @@ class LoopbackGroup {
   LoopbackGroup(int world, bool device_buffers);
   ~LoopbackGroup();
   std::unique_ptr<Communicator> comm(int rank);
+  // A rank failed: collectives still waiting on it throw instead of timing out.
+  void abort();
   struct State;
 
  private:
