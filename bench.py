@@ -107,6 +107,23 @@ def ref_semantics(text: bytes, steps: int = 50, warmup: int = 5):
     return med
 
 
+def cold_first_run(text: bytes) -> dict:
+    """A fresh engine's first job (allocation excluded, first launches/captures included):
+    the regime of the reference's numbers, which include Thrust's first-call overhead."""
+    import locust_amd as lc
+
+    cfg = lc.make_config("gpu", reduce_path="lds")
+    nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
+    eng = lc._C.GpuEngine(cfg, len(text), nlines)
+    eng.load(text)
+    t0 = time.perf_counter()
+    eng.run_loaded()
+    t1 = time.perf_counter()
+    eng.run_loaded()
+    t2 = time.perf_counter()
+    return {"first_job_ms": round((t1 - t0) * 1e3, 4), "second_job_ms": round((t2 - t1) * 1e3, 4)}
+
+
 def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
     import locust_amd as lc
 
@@ -175,7 +192,8 @@ def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
     dr.set_strategy(getattr(lc._C.DistStrategy, strategy))
     for _ in range(warmup):
         dr.run_loaded()
-    parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": []}
+    parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": [],
+             "sent_bytes": [], "recv_bytes": []}
     dr.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -240,6 +258,8 @@ def main() -> int:
                                    "stages_ms": {k: round(v, 4) for k, v in str_.items()}}
             # Host timers placed like the reference's (launch-only map, B2/B4): the
             # like-for-like comparison with BASELINE.md's per-stage rows.
+            extra["cold_start"] = {"hamlet4500": cold_first_run(text),
+                                   "hamlet700": cold_first_run(load_text("hamlet700"))}
             extra["reference_semantics_ms"] = {
                 "hamlet4500": ref_semantics(text), "hamlet700": ref_semantics(load_text("hamlet700")),
                 "baseline": BASELINE_STAGES}

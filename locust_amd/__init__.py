@@ -36,6 +36,8 @@ from .models.wordcount import (  # noqa: E402
 JobConfig = _C.JobConfig
 DistConfig = _C.DistConfig
 LocustError = _C.LocustError
+HostText = _C.HostText
+gen_text = _C.gen_text  # synthetic Hamlet-shaped text (csrc/io/gen.cpp)
 
 __all__ = [
     "REPO_ROOT",
@@ -51,5 +53,7 @@ __all__ = [
     "JobConfig",
     "DistConfig",
     "LocustError",
+    "HostText",
+    "gen_text",
 ]
 __version__ = "0.1.0"

@@ -53,3 +53,17 @@ def test_distributed_streamed_shards(hamlet, strategy, world):
     ent, ntok, _ = oracle.wordcount(hamlet)
     for res, info in lc._C.run_multi_schedule(hamlet, cfgs):
         assert res.entries() == ent and res.num_tokens == ntok
+
+
+@pytest.mark.parametrize("sort", ["dict", "radix"])
+def test_ten_million_tokens_vs_cpu_engine(sort):
+    """SURVEY §4 item 2 sizes up to 10^7: ~10M tokens through the HBM-table dictionary /
+    the onesweep radix sort, checked against the C++ CPU engine (same semantics as the
+    oracle, fast enough at this size)."""
+    text = lc._C.gen_text(lines=1_600_000, seed=11)
+    gpu = lc._C.GpuEngine(lc.make_config("gpu", sort=sort, check=True), len(text), 1_700_000)
+    r = gpu.run(text)
+    c = lc._C.cpu_run(lc.make_config("cpu"), text)
+    assert r.num_tokens == c.num_tokens and r.num_tokens > 9_000_000
+    assert r.num_unique == c.num_unique
+    assert r.format(False) == c.format(False)
