@@ -29,7 +29,7 @@ LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lpthread
 
 HIP_SRCS  := $(wildcard csrc/kernels/*.hip csrc/engine/*.hip csrc/comm/*.hip)
 CPP_SRCS  := $(wildcard csrc/engine/*.cpp csrc/io/*.cpp csrc/comm/*.cpp)
-HDRS      := $(wildcard csrc/include/locust/*.hpp csrc/include/locust/device/*.hpp)
+HDRS      := $(wildcard csrc/include/locust/*.hpp csrc/include/locust/device/*.hpp csrc/engine/*.hpp)
 
 HIP_OBJS  := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 CPP_OBJS  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))

@@ -1,0 +1,1014 @@
+// Device pipeline: the buffers, streams and stage enqueuers of one GPU engine instance
+// (internal to csrc/engine: used by the single-GPU engine, gpu_wordcount.hip, and by the
+// per-rank shard engine, shard_engine.hip).
+//
+// Reference orchestration: /root/reference/MapReduce/src/main.cu:388-487 (cudaMalloc per
+// run, synchronous cudaMemcpy of fixed 5,800/116,000-slot arrays, thrust calls that block,
+// no error checks).  Here: one device arena allocated at construction, pinned host staging,
+// a single stream, hipEvents at every stage boundary, exact-size transfers, look-back
+// scratch zeroed by one memset per run, and captured hipGraphs for the repeated sequences.
+#pragma once
+
+#include <algorithm>
+#include <array>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "locust/dist.hpp"
+#include "locust/engine.hpp"
+#include "locust/hip_check.hpp"
+#include "locust/kernels.hpp"
+#include "locust/trace.hpp"
+
+namespace locust {
+
+void validate_result(const WordCountResult& r);  // engine/common.cpp
+
+namespace detail {
+
+struct Arena {
+  char* base = nullptr;
+  u64 size = 0, used = 0;
+  template <typename T>
+  T* take(u64 count) {
+    used = align_up(used, 256);
+    T* p = reinterpret_cast<T*>(base + used);
+    used += count * sizeof(T);
+    if (used > size) throw Error("device arena overflow (internal sizing bug)");
+    return p;
+  }
+};
+
+struct SizingPlan {
+  u64 bytes = 0;
+  template <typename T>
+  void add(u64 count) {
+    bytes = align_up(bytes, 256) + count * sizeof(T);
+  }
+};
+
+constexpr u32 kMaxSamples = 4096;
+constexpr u32 kMaxRanks = 1024;
+
+// Device pipeline: every buffer of one engine instance.  cap_records is the number of
+// records (tokens or received KeyCount records) the sort/reduce side can hold.
+struct DevicePipeline {
+  JobConfig cfg;
+  u64 cap_bytes = 0, cap_lines = 0, cap = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  Arena arena;
+
+  char* d_text = nullptr;
+  u64* d_nl = nullptr;
+  char* d_delims = nullptr;
+  KeysSoA slots{}, tokens{}, sorted{}, heads{};
+  u32* d_line_counts = nullptr;
+  u64* d_counts = nullptr;         // per-record counts of received records
+  u64* d_sorted_counts = nullptr;  // counts in sorted order
+  u64* d_prefix = nullptr;         // exclusive scan of sorted counts
+  u64* d_head_val = nullptr;
+  u64* d_head_count = nullptr;
+  u32* d_perm = nullptr;
+  u8* d_parts = nullptr;           // hash partition tag per token (partitioned dict build)
+  bool parts_ready = false;        // d_parts describes the current `tokens`
+  OutRecord* d_out = nullptr;
+  KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
+  PackedKey* d_samples = nullptr;
+  PackedKey* d_splitters = nullptr;
+  u64* d_offsets = nullptr;
+  u64* d_offset = nullptr;
+
+  // zeroed once per run: counters + every look-back region
+  char* d_sync = nullptr;
+  u64 sync_bytes = 0;
+  MapCounters* d_ctr = nullptr;
+  LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{}, lb_dict{};
+  RadixWorkspace rx{};
+
+  // dictionary path: [table | ucount | rank] is one zeroed block
+  DictWorkspace dict{};
+  u64 dict_slots = 0;
+  u64 ucap = 0;       // dense distinct-key capacity of the dictionary
+  u64 h_out_cap = 0;  // records h_out holds
+  u64 h_keys_cap = 0;
+  u32* d_rank = nullptr;
+  u64 dict_zero_bytes = 0;
+
+  // streaming (inputs larger than one chunk), allocated on first use
+  char* d_text_alt = nullptr;        // second device text buffer (double buffering)
+  char* h_stage[2] = {nullptr, nullptr};  // pinned staging halves for pageable inputs
+  hipStream_t cstream = nullptr;     // H2D copy stream
+  hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
+  MapCounters* d_dctr = nullptr;     // dictionary counters that persist across chunks
+  MapCounters* h_chunk_ctr = nullptr;  // pinned per-chunk map counter snapshots
+  u64 h_chunk_cap = 0;
+
+  char* h_text = nullptr;
+  char* d_h_text = nullptr;    // device view of the pinned h_text (zero-copy map input)
+  const char* map_text = nullptr;  // what the map kernel reads this run
+  MapCounters* h_ctr = nullptr;
+  SortPlan* h_plan = nullptr;
+  OutRecord* h_out = nullptr;         // host-mapped output records
+  OutRecord* d_out_mapped = nullptr;  // device view of h_out
+  MapCounters* h_ctr_mapped = nullptr;
+  MapCounters* d_ctr_mapped = nullptr;
+  u64* h_keys = nullptr;  // staging for key up/downloads (4 words x cap)
+  PackedKey* h_small = nullptr;
+  u64* h_u64 = nullptr;
+
+  DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines, u64 cap_records = 0)
+      : cfg(c) {
+    LOCUST_CHECK_ARG(cfg.emits_per_line > 0, "emits_per_line must be > 0");
+    LOCUST_CHECK_ARG(cfg.max_key_len > 0 && cfg.max_key_len <= kKeyBytes - 1,
+                     "max_key_len must be in [1, 31]");
+    cap_bytes = std::max<u64>(max_bytes, 1);
+    cap_lines = std::max<u64>(max_lines, 1);
+    bool streaming = false;
+    if (cfg.chunk_bytes && cap_bytes > cfg.chunk_bytes && !cap_records) {
+      // streaming engine: one pass holds a chunk; its token capacity is bounded by bytes
+      cap_bytes = cfg.chunk_bytes;
+      cap_lines = cap_bytes;
+      streaming = true;
+    }
+    cap = cap_records ? cap_records
+                      : std::min<u64>(cap_lines * (u64)cfg.emits_per_line, cap_bytes / 2 + 1);
+    // The dictionary of a streamed input collects the distinct keys of ALL chunks, and
+    // its sort/emit buffers are record-sized: give small chunks room for 2^20 of them.
+    if (streaming) cap = std::max<u64>(cap, 1ull << 20);
+    cap = std::max<u64>(cap, 1);
+    LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
+    LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
+    LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (auto& e : ev) LOCUST_HIP_CHECK(hipEventCreate(&e));
+
+    const bool compat = cfg.map_path == MapPath::kCompat;
+    const u64 slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
+    const u64 t_line = div_up(cap_bytes, kLineIdxTile) + 1;
+    const u64 t_compact = div_up(cap_lines, 256) + 1;
+    const u64 t_map = div_up(cap_bytes, kMapTileBytesMin) + 1;
+    const u64 t_heads = div_up(cap, kReduceTile) + 1;
+    const u64 t_scan = div_up(cap, kReduceTile) + 1;
+    const u64 rx_zero_words = radix_zero_bytes(cap) / 4;
+    // Hash table: >= 2x the distinct keys it can see (load factor <= 0.5), capped at
+    // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
+    dict_slots = 1024;
+    // dense distinct-key capacity: every key of a pass, at most 16M (a 2^25-slot table)
+    ucap = std::min<u64>(cap, 1ull << 24);
+    while (dict_slots < 2 * ucap) dict_slots <<= 1;
+    // [table | ucount | uval | rank]
+    dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
+                      ucap * 4;
+    const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
+    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1);
+
+    SizingPlan sz;
+    sz.add<char>(cap_bytes + 64);
+    sz.add<u64>(cap_lines + 1);
+    sz.add<char>(64);
+    for (int j = 0; j < kKeyWords; ++j) {
+      sz.add<u64>(slot_cap);
+      sz.add<u64>(cap);
+      sz.add<u64>(cap);
+      sz.add<u64>(cap);
+    }
+    sz.add<u32>(compat ? cap_lines : 1);
+    for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
+    sz.add<u32>(cap);
+    sz.add<u8>(align_up(cap, 16) + 16);
+    sz.add<OutRecord>(cap);
+    sz.add<KeyCount>(cap);
+    sz.add<PackedKey>(kMaxSamples);
+    sz.add<PackedKey>(kMaxRanks);
+    sz.add<u64>(kMaxRanks + 1);
+    sz.add<u64>(1);
+    sz.add<char>(sync_bytes);
+    sz.add<u32>(rx_zero_words);
+    sz.add<u32>(rx_part_words);
+    sz.add<SortPlan>(1);
+    for (int b = 0; b < 2; ++b) {
+      sz.add<u64>(cap);
+      sz.add<u32>(cap);
+    }
+    for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
+    sz.add<char>(dict_zero_bytes);
+    arena.size = sz.bytes + 4096;
+    LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
+
+    d_text = arena.take<char>(cap_bytes + 64);
+    d_nl = arena.take<u64>(cap_lines + 1);
+    d_delims = arena.take<char>(64);
+    for (int j = 0; j < kKeyWords; ++j) {
+      slots.w[j] = arena.take<u64>(slot_cap);
+      tokens.w[j] = arena.take<u64>(cap);
+      sorted.w[j] = arena.take<u64>(cap);
+      heads.w[j] = arena.take<u64>(cap);
+    }
+    d_line_counts = arena.take<u32>(compat ? cap_lines : 1);
+    d_counts = arena.take<u64>(cap);
+    d_sorted_counts = arena.take<u64>(cap);
+    d_prefix = arena.take<u64>(cap);
+    d_head_val = arena.take<u64>(cap);
+    d_head_count = arena.take<u64>(cap);
+    d_perm = arena.take<u32>(cap);
+    d_parts = arena.take<u8>(align_up(cap, 16) + 16);
+    d_out = arena.take<OutRecord>(cap);
+    d_records = arena.take<KeyCount>(cap);
+    d_samples = arena.take<PackedKey>(kMaxSamples);
+    d_splitters = arena.take<PackedKey>(kMaxRanks);
+    d_offsets = arena.take<u64>(kMaxRanks + 1);
+    d_offset = arena.take<u64>(1);
+
+    // sync block: [MapCounters | tile counters | status regions]
+    d_sync = arena.take<char>(sync_bytes);
+    d_ctr = reinterpret_cast<MapCounters*>(d_sync);
+    u32* counters = reinterpret_cast<u32*>(d_sync + 128);
+    u64* st = reinterpret_cast<u64*>(d_sync + 256);
+    lb_line = {st, counters + 0};
+    st += t_line;
+    lb_compact = {st, counters + 1};
+    st += t_compact;
+    lb_map = {st, counters + 2};
+    st += t_map;
+    lb_heads = {st, counters + 3};
+    st += t_heads;
+    lb_scan = {st, counters + 4};
+    st += t_scan;
+    lb_dict = {st, counters + 5};
+
+    rx.cap = cap;
+    rx.tile_counters = arena.take<u32>(rx_zero_words);
+    rx.status = rx.tile_counters + kNumPositions;
+    rx.hist_part = arena.take<u32>(rx_part_words);
+    rx.plan = arena.take<SortPlan>(1);
+    for (int b = 0; b < 2; ++b) {
+      rx.keys[b] = arena.take<u64>(cap);
+      rx.vals[b] = arena.take<u32>(cap);
+    }
+    for (int j = 0; j < kKeyWords; ++j) dict.ukeys.w[j] = arena.take<u64>(ucap);
+    {
+      char* z = arena.take<char>(dict_zero_bytes);
+      dict.table = reinterpret_cast<DictSlot*>(z);
+      dict.ucount = reinterpret_cast<u64*>(z + align_up(dict_slots * sizeof(DictSlot), 256));
+      dict.uval = reinterpret_cast<u64*>(reinterpret_cast<char*>(dict.ucount) + align_up(ucap * 8, 256));
+      d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.uval) + align_up(ucap * 8, 256));
+      dict.mask = (u32)(dict_slots - 1);
+      dict.ucap = (u32)ucap;
+      dict.urank = d_rank;
+    }
+
+    char delim_buf[64] = {0};
+    LOCUST_CHECK_ARG(cfg.delimiters.size() < sizeof(delim_buf), "too many delimiters");
+    std::memcpy(delim_buf, cfg.delimiters.data(), cfg.delimiters.size());
+    // on this pipeline's own stream: a legacy-stream copy would conflict with another
+    // thread's graph capture (loopback ranks share the process)
+    LOCUST_HIP_CHECK(
+        hipMemcpyAsync(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice, stream));
+    LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      d_h_text = nullptr;  // not device-visible: always DMA
+    }
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
+    // Output records and the counter snapshot are host-mapped: the emit kernel writes them
+    // over PCIe directly (zero-copy), so a dictionary run needs no D2H copy at all.
+    grow_host_out(ucap);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_ctr_mapped), h_ctr_mapped, 0));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
+    std::memset(h_ctr, 0, sizeof(MapCounters));
+  }
+
+  ~DevicePipeline() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
+    if (d_ord_trace) (void)hipFree(d_ord_trace);
+    if (cstream) (void)hipStreamSynchronize(cstream);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (int b = 0; b < 2; ++b) {
+      if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
+      if (ev_consumed[b]) (void)hipEventDestroy(ev_consumed[b]);
+      if (h_stage[b]) (void)hipHostFree(h_stage[b]);
+    }
+    if (cstream) (void)hipStreamDestroy(cstream);
+    if (d_text_alt) (void)hipFree(d_text_alt);
+    if (d_dctr) (void)hipFree(d_dctr);
+    if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (arena.base) (void)hipFree(arena.base);
+    for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_out, (void*)h_keys,
+                    (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped})
+      if (p) (void)hipHostFree(p);
+  }
+
+  // Host-mapped output records (zero-copy emit target); grown when a radix-path result
+  // has more distinct keys than the dictionary's capacity.
+  void grow_host_out(u64 n) {
+    if (n <= h_out_cap) return;
+    if (h_out) {
+      sync();
+      LOCUST_HIP_CHECK(hipHostFree(h_out));
+    }
+    h_out_cap = std::max<u64>(n, 1);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, h_out_cap * sizeof(OutRecord),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out_mapped), h_out, 0));
+  }
+  // Pinned staging for key up/downloads (stage-split paths only), allocated on demand.
+  void grow_host_keys(u64 n) {
+    if (n <= h_keys_cap) return;
+    if (h_keys) LOCUST_HIP_CHECK(hipHostFree(h_keys));
+    h_keys_cap = std::max<u64>(n, 1);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, h_keys_cap * kKeyWords * sizeof(u64),
+                                   hipHostMallocDefault));
+  }
+
+  void check_input(const TextInput& in) const {
+    if (in.bytes > cap_bytes || in.num_lines > cap_lines)
+      throw Error("input (" + std::to_string(in.bytes) + " B, " + std::to_string(in.num_lines) +
+                  " lines) exceeds engine capacity (" + std::to_string(cap_bytes) + " B, " +
+                  std::to_string(cap_lines) + " lines)");
+  }
+
+  void sync() { LOCUST_HIP_CHECK(hipStreamSynchronize(stream)); }
+
+  // H2D of the text; zero counters and look-back scratch.
+  //  * zero-copy (small inputs, fast map): no copy at all -- the map kernel's 16-byte
+  //    staging loads read the pinned host buffer over PCIe, which for a ~200 KB text is
+  //    cheaper than an SDMA transfer's fixed latency.
+  //  * pinned input elsewhere (HostText): DMA straight from it.
+  //  * otherwise: host copy into the pinned buffer, then DMA.
+  void enqueue_upload(const TextInput& in) {
+    prepare_upload(in);
+    enqueue_upload_device(in);
+  }
+  // Host half: stage the text where the device half expects it and pick the map's source.
+  enum class Upload { kZeroCopy, kDirect, kStaged };
+  Upload upload_mode = Upload::kStaged;
+  void prepare_upload(const TextInput& in) {
+    map_text = d_text;
+    if (use_zero_copy(in)) {
+      upload_mode = Upload::kZeroCopy;
+      map_text = d_h_text;
+    } else if (in.data != h_text && in.bytes && host_pinned(in.data)) {
+      upload_mode = Upload::kDirect;
+      return;
+    } else {
+      upload_mode = Upload::kStaged;
+    }
+    if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
+    std::memset(h_text + in.bytes, 0, 16);
+  }
+  // Device half (capturable): the DMA if any, then the per-run reset of counters and
+  // look-back scratch.
+  void enqueue_upload_device(const TextInput& in) {
+    if (upload_mode == Upload::kDirect) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
+    } else if (upload_mode == Upload::kStaged) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
+    }
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+  }
+
+  // ---- captured launch sequences (hipGraph), keyed by call site and shape ----
+  using GraphKeyArr = std::array<u64, 6>;
+  struct CachedGraph {
+    GraphKeyArr key;
+    hipGraphExec_t exec;
+  };
+  std::vector<CachedGraph> graph_cache;
+  // Replays the sequence `enqueue` captured for `key`, capturing it on first use.  The
+  // sequence may only enqueue work on `stream` (kernels, memsets, async copies).
+  template <class F>
+  void launch_cached(const GraphKeyArr& key, F&& enqueue) {
+    for (auto& g : graph_cache)
+      if (g.key == key) {
+        LOCUST_HIP_CHECK(hipGraphLaunch(g.exec, stream));
+        return;
+      }
+    if (graph_cache.size() >= 8) {  // shapes changed a lot: drop the oldest
+      LOCUST_HIP_CHECK(hipGraphExecDestroy(graph_cache.front().exec));
+      graph_cache.erase(graph_cache.begin());
+    }
+    hipGraph_t g = nullptr;
+    LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    enqueue();
+    LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
+    hipGraphExec_t exec = nullptr;
+    LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    LOCUST_HIP_CHECK(hipGraphDestroy(g));
+    graph_cache.push_back({key, exec});
+    LOCUST_HIP_CHECK(hipGraphLaunch(exec, stream));
+  }
+
+  // ---- hipGraph replay of the dictionary job ----
+  hipGraphExec_t graph_exec = nullptr;
+  bool graph_ordered = false;  // the captured job uses the ordered kernel
+  struct GraphKey {
+    u64 bytes = ~0ull;
+    u64 lines = 0;
+    const char* src = nullptr;
+    const char* map_text = nullptr;
+    Upload mode = Upload::kStaged;
+    bool operator==(const GraphKey& o) const {
+      return bytes == o.bytes && lines == o.lines && src == o.src && map_text == o.map_text &&
+             mode == o.mode;
+    }
+  } graph_key;
+  bool use_graph() const {
+    if (cfg.graph >= 0) return cfg.graph > 0 && cfg.sort_path == SortPath::kDict;
+    return cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast;
+  }
+  // Capture [upload DMA + reset, map, dictionary build, rank, emit] once per input shape
+  // and source; later runs replay it with one hipGraphLaunch.
+  void launch_dict_graph(const TextInput& in, bool compat) {
+    const GraphKey key{in.bytes, in.num_lines, upload_mode == Upload::kDirect ? in.data : nullptr,
+                       map_text, upload_mode};
+    if (!graph_exec || !(key == graph_key)) {
+      if (graph_exec) {
+        LOCUST_HIP_CHECK(hipGraphExecDestroy(graph_exec));
+        graph_exec = nullptr;
+      }
+      hipGraph_t g = nullptr;
+      LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+      enqueue_upload_device(in);
+      enqueue_map(in);
+      graph_ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr);
+      LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
+      LOCUST_HIP_CHECK(hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0));
+      LOCUST_HIP_CHECK(hipGraphDestroy(g));
+      graph_key = key;
+    }
+    parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
+    LOCUST_HIP_CHECK(hipGraphLaunch(graph_exec, stream));
+  }
+  bool use_zero_copy(const TextInput& in) const {
+    if (cfg.map_path != MapPath::kFast || !d_h_text) return false;
+    if (cfg.zero_copy_text >= 0) return cfg.zero_copy_text > 0;
+    return in.bytes <= kZeroCopyMaxBytes;
+  }
+
+  void enqueue_map(const TextInput& in) {
+    parts_ready = cfg.map_path == MapPath::kFast;
+    if (cfg.map_path == MapPath::kCompat) {
+      launch_line_index(d_text, in.bytes, d_nl, d_ctr, lb_line, stream);
+      launch_map_compat(d_text, in.bytes, d_nl, (u32)in.num_lines, d_delims, cfg.emits_per_line,
+                        cfg.max_key_len, slots, d_line_counts, d_ctr, stream);
+    } else {
+      launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
+                      cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
+                      stream);
+    }
+  }
+
+  // Compaction (compat path) + radix sort of `tokens` into `sorted` (and counts).
+  // host_n: record count when the host already knows it.  With sync_plan the count is
+  // read back (one 4-byte D2H) so the sort can pick its regime and exact grids; without
+  // it everything stays on the device (graph-capturable).
+  void enqueue_process(u32 num_lines, bool compat, bool with_counts, u64 host_n = kUnknownCount) {
+    if (compat)
+      launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
+                           lb_compact, stream);
+    if (!cfg.sync_plan) {
+      host_n = kUnknownCount;
+    } else if (host_n == kUnknownCount) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(h_u64, &d_ctr->num_records, sizeof(u32),
+                                      hipMemcpyDeviceToHost, stream));
+      sync();
+      host_n = *reinterpret_cast<const u32*>(h_u64);
+    }
+    radix_sort(tokens, &d_ctr->num_records, host_n, rx, with_counts ? d_counts : nullptr, sorted,
+               with_counts ? d_sorted_counts : nullptr, d_perm, h_plan, stream);
+  }
+
+  // Head mark + compaction + adjacent difference over `sorted` (weighted when counts).
+  void enqueue_reduce_core(bool with_counts) {
+    const u64* prefix = nullptr;
+    if (with_counts) {
+      launch_scan_counts(d_sorted_counts, cap, d_prefix, d_ctr, lb_scan, stream);
+      prefix = d_prefix;
+    }
+    launch_mark_compact_heads(sorted, prefix, cap, cfg.reduce_path, heads, d_head_val, d_ctr,
+                              lb_heads, stream);
+    launch_adjacent_diff(d_head_val, cap, cfg.reduce_path, d_head_count, d_ctr, stream);
+  }
+
+  void enqueue_pack_output() {
+    launch_pack_output(heads, d_head_val, d_head_count, cap, d_ctr, d_out, stream);
+  }
+
+  // ---- dictionary path (SortPath::kDict): no host synchronisation inside ----
+  void enqueue_process_dict(u32 num_lines, bool compat, bool with_counts = false) {
+    enqueue_dict_insert(num_lines, compat, with_counts);
+    enqueue_rank();
+  }
+  // Every token (or weighted record) into a fresh dictionary: the partitioned LDS build
+  // when the tokens carry partition tags and the pass is small, else the HBM table.
+  void enqueue_dict_insert(u32 num_lines, bool compat, bool with_counts) {
+    if (compat)
+      launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
+                           lb_compact, stream);
+    if (!compat && parts_ready && cap <= kPartBuildMaxTokens) {
+      launch_dict_part_build(tokens, with_counts ? d_counts : nullptr, d_parts,
+                             &d_ctr->num_records, cap, dict, d_ctr, stream);
+      return;
+    }
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
+                       d_ctr, stream);
+  }
+  // Ranks of the distinct keys (rank and uval must be zero).  Default: the weighted rank --
+  // the all-pairs pass also sums the counts of the smaller keys, which IS the output's
+  // val, and rank_emit writes the records straight from it.  LOCUST_RANK=scan counts
+  // ranks only and derives val from a look-back scan of the counts in rank order
+  // (scatter + scan_pack: one more launch; measured slower on MI355X, kept for A/B).
+  static bool weighted_rank() {
+    static const bool w = [] {
+      const char* e = std::getenv("LOCUST_RANK");
+      return !(e && std::string(e) == "scan");
+    }();
+    return w;
+  }
+  void enqueue_rank() {
+    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank,
+                     weighted_rank() ? dict.uval : nullptr, stream);
+  }
+  // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
+  // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
+  bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
+  void enqueue_dict_ordered(bool with_counts, bool mapped) {
+    launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
+                        cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
+                        lb_dict, stream, ord_trace());
+  }
+  // Diagnostics: LOCUST_ORD_TRACE=1 prints the ordered kernel's per-partition phase times
+  // (shader clock ticks) after each run.
+  u64* d_ord_trace = nullptr;
+  u64* ord_trace() {
+    static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
+    if (!on) return nullptr;
+    if (!d_ord_trace) {
+      LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 8 * sizeof(u64)));
+    }
+    return d_ord_trace;
+  }
+  void print_ord_trace() {
+    if (!d_ord_trace) return;
+    std::vector<u64> t(kDictParts * 8);
+    LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    u64 t0 = ~0ull;
+    for (int p = 0; p < kDictParts; ++p)
+      if (t[p * 8]) t0 = std::min(t0, t[p * 8]);
+    for (int p = 0; p < kDictParts; ++p) {
+      const u64* x = &t[p * 8];
+      if (!x[0] || !x[6]) continue;
+      std::fprintf(stderr,
+                   "ord p=%3d m=%5llu start=%6llu build=%6llu publish=%5llu wait=%6llu sort=%6llu "
+                   "write=%6llu end=%6llu\n",
+                   p, (unsigned long long)x[6], (unsigned long long)(x[0] - t0),
+                   (unsigned long long)(x[1] - x[0]), (unsigned long long)(x[2] - x[1]),
+                   (unsigned long long)(x[3] - x[2]), (unsigned long long)(x[4] - x[3]),
+                   (unsigned long long)(x[5] - x[4]), (unsigned long long)(x[5] - t0));
+    }
+  }
+  // Process + emit of a dictionary run; returns true if the ordered kernel was used.
+  bool enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process) {
+    if (!compat && ordered_ok()) {
+      enqueue_dict_ordered(with_counts, /*mapped=*/true);
+      if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+      return true;
+    }
+    enqueue_process_dict(num_lines, compat, with_counts);
+    if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+    enqueue_emit_dict(/*mapped=*/true);
+    return false;
+  }
+  // After an ordered run reported a partition overflow: redo Process + emit through the
+  // HBM table (the map output is still in `tokens`).
+  void redo_dict_on_table(u32 num_lines, bool with_counts) {
+    LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->num_unique, 0, sizeof(u32), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->flags, 0, sizeof(u32), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
+                       d_ctr, stream);
+    enqueue_rank();
+    enqueue_emit_dict(/*mapped=*/true);
+    sync();
+    *h_ctr = *h_ctr_mapped;
+  }
+  // Sorted distinct keys + counts (for the shuffle's range partition).
+  void enqueue_sorted_from_dict() {
+    launch_rank_scatter(dict.ukeys, dict.ucount, d_rank, &d_ctr->num_unique, ucap, sorted,
+                        d_sorted_counts, stream);
+  }
+  // Output records in key order; `mapped` writes them (and the counters) straight into
+  // host memory (zero-copy: the host needs no D2H).
+  void enqueue_emit_dict(bool mapped) {
+    if (weighted_rank()) {
+      launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, ucap, d_ctr,
+                       mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
+      return;
+    }
+    enqueue_sorted_from_dict();
+    launch_scan_pack(sorted, d_sorted_counts, ucap, d_ctr, mapped ? d_out_mapped : d_out, lb_scan,
+                     stream, mapped ? d_ctr_mapped : nullptr, (u32)kRankSortMax);
+  }
+  // Radix-fallback reduce: scan of the sorted counts -> records in d_out.
+  void enqueue_reduce_dict() {
+    launch_scan_pack(sorted, d_sorted_counts, cap, d_ctr, d_out, lb_scan, stream);
+  }
+  // After the counters are read: a dictionary run whose distinct-key count exceeded the
+  // rank sort's range (or whose table overflowed) is finished on the radix path.
+  bool dict_fallback_needed() const {
+    return (h_ctr->flags & (kCtrDictOverflow | kCtrNotEmitted)) ||
+           h_ctr->num_unique > (u32)kRankSortMax;
+  }
+  void finish_dict_with_radix(u32 num_lines, bool with_counts = false) {
+    if (h_ctr->flags & kCtrDictOverflow) {
+      // table overflow: sort every record and reduce the reference way
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.tile_counter, 0, 4, stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.tile_counter, 0, 4, stream));
+      enqueue_process(num_lines, false, with_counts, h_ctr->num_records);
+      enqueue_reduce_core(with_counts);
+      enqueue_pack_output();
+      return;
+    }
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.tile_counter, 0, 4, stream));
+    radix_sort(dict.ukeys, &d_ctr->num_unique, h_ctr->num_unique, rx, dict.ucount, sorted,
+               d_sorted_counts, d_perm, h_plan, stream);
+    enqueue_reduce_dict();
+  }
+
+  void read_counters() {
+    LOCUST_HIP_CHECK(
+        hipMemcpyAsync(h_ctr, d_ctr, sizeof(MapCounters), hipMemcpyDeviceToHost, stream));
+    sync();
+  }
+
+  void download_output(WordCountResult& r, hipEvent_t done) {
+    read_counters();
+    const u64 u = h_ctr->num_unique;
+    grow_host_out(u);
+    if (u)
+      LOCUST_HIP_CHECK(
+          hipMemcpyAsync(h_out, d_out, u * sizeof(OutRecord), hipMemcpyDeviceToHost, stream));
+    if (done) LOCUST_HIP_CHECK(hipEventRecord(done, stream));
+    sync();
+    fill_counters(r);
+    r.entries.resize(u);
+    copy_out(r.entries, u);
+  }
+
+  // Host output records -> result entries: identical 48-byte layouts, one memcpy.
+  void copy_out(std::vector<WordCountEntry>& e, u64 u) const {
+    static_assert(sizeof(WordCountEntry) == sizeof(OutRecord), "entry layout");
+    static_assert(offsetof(WordCountEntry, val) == offsetof(OutRecord, val), "entry layout");
+    static_assert(offsetof(WordCountEntry, count) == offsetof(OutRecord, count), "entry layout");
+    e.resize(u);
+    if (u) std::memcpy(static_cast<void*>(e.data()), h_out, u * sizeof(OutRecord));
+  }
+
+  void fill_counters(WordCountResult& r) const {
+    r.num_tokens = h_ctr->total_count ? h_ctr->total_count : h_ctr->num_records;
+    r.num_unique = h_ctr->num_unique;
+    r.overflow_lines = h_ctr->overflow_lines;
+    r.truncated = h_ctr->truncated;
+    r.max_key_len = h_ctr->max_key_len;
+  }
+
+  static double ms_between(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    LOCUST_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+  }
+
+  // Reference-semantics timing (JobConfig.ref_timers): the same device work, with host
+  // timestamps where main.cu:405-468 took them.  The H2D happens before the first timer,
+  // as main.cu:403 does.
+  WordCountResult run_ref_timed(const TextInput& in) {
+    check_input(in);
+    WordCountResult r;
+    r.num_lines = in.num_lines;
+    const bool compat = cfg.map_path == MapPath::kCompat;
+    const bool dict_path = cfg.sort_path == SortPath::kDict;
+    const u64 w0 = now_ns();
+    enqueue_upload(in);
+    sync();
+    const u64 t0 = now_ns();
+    enqueue_map(in);  // map timer: the launch only (main.cu:405-407)
+    const u64 t1 = now_ns();
+    if (dict_path) {
+      enqueue_process_dict((u32)in.num_lines, compat);
+    } else {
+      enqueue_process((u32)in.num_lines, compat, false);
+    }
+    sync();  // process timer ends once the sort is done (thrust::sort returns)
+    const u64 t2 = now_ns();
+    if (dict_path) {
+      enqueue_emit_dict(/*mapped=*/true);  // the last reduce kernel: launch only (B4)
+    } else {
+      enqueue_reduce_core(false);
+      enqueue_pack_output();
+    }
+    const u64 t3 = now_ns();
+    if (dict_path) {
+      sync();
+      *h_ctr = *h_ctr_mapped;
+      if (dict_fallback_needed()) {
+        finish_dict_with_radix((u32)in.num_lines);
+        download_output(r, nullptr);
+      } else {
+        fill_counters(r);
+        copy_out(r.entries, h_ctr->num_unique);
+      }
+    } else {
+      download_output(r, nullptr);
+    }
+    r.times.ref_map_ms = (t1 - t0) * 1e-6;
+    r.times.ref_process_ms = (t2 - t1) * 1e-6;
+    r.times.ref_reduce_ms = (t3 - t2) * 1e-6;
+    r.times.wall_ms = (now_ns() - w0) * 1e-6;
+    if (cfg.check) validate_result(r);
+    return r;
+  }
+
+  WordCountResult run(const TextInput& in) {
+    TraceRange tr("locust:job");
+    if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
+        cfg.map_path == MapPath::kFast)
+      return run_stream(in);
+    if (cfg.ref_timers) return run_ref_timed(in);
+    check_input(in);
+    WordCountResult r;
+    r.num_lines = in.num_lines;
+    const u64 t0 = now_ns();
+    const bool compat = cfg.map_path == MapPath::kCompat;
+    const bool dict_path = cfg.sort_path == SortPath::kDict;
+    const bool graphed = dict_path && use_graph();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+    if (graphed) {
+      prepare_upload(in);
+      launch_dict_graph(in, compat);
+      for (int e = 1; e <= 5; ++e) LOCUST_HIP_CHECK(hipEventRecord(ev[e], stream));
+      r.times.graph = true;
+    } else {
+      enqueue_upload(in);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+      enqueue_map(in);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+    }
+    if (dict_path) {
+      bool ordered = graph_ordered;
+      if (!graphed) {
+        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, ev[3]);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+        LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+      }
+      sync();  // the one host synchronisation of a dictionary run
+      *h_ctr = *h_ctr_mapped;
+      const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
+      if (ordered) print_ord_trace();
+      if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, false);
+      if (!ordered_done && dict_fallback_needed()) {
+        finish_dict_with_radix((u32)in.num_lines);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+        download_output(r, ev[5]);
+      } else {
+        fill_counters(r);
+        const u64 u = h_ctr->num_unique;
+        r.entries.resize(u);
+        copy_out(r.entries, u);
+      }
+    } else {
+      enqueue_process((u32)in.num_lines, compat, false);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+      enqueue_reduce_core(false);
+      enqueue_pack_output();
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      download_output(r, ev[5]);
+    }
+    r.times.wall_ms = (now_ns() - t0) * 1e-6;
+    r.times.h2d_ms = ms_between(ev[0], ev[1]);
+    r.times.map_ms = ms_between(ev[1], ev[2]);
+    r.times.process_ms = ms_between(ev[2], ev[3]);
+    r.times.reduce_ms = ms_between(ev[3], ev[4]);
+    r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    r.times.gpu_ms = ms_between(ev[0], ev[5]);
+    if (cfg.check) validate_result(r);
+    return r;
+  }
+
+  // ---------------------------------------------------------------------------------
+  // Streaming: an input larger than the engine's text capacity is processed in
+  // line-aligned chunks of <= cap_bytes.  Chunk k+1's H2D runs on the copy
+  // stream while chunk k is mapped and folded into ONE dictionary that persists across
+  // chunks; the distinct keys are ranked and emitted once at the end.  Device memory is
+  // therefore bounded by the chunk size plus the dictionary, not by the input size.
+  // ---------------------------------------------------------------------------------
+  static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+      (void)hipGetLastError();  // pageable memory: clear the sticky error
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  }
+
+  void ensure_stream_buffers(bool staging, u64 nchunks) {
+    if (!cstream) {
+      LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_copied[b], hipEventDisableTiming));
+        LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_consumed[b], hipEventDisableTiming));
+      }
+      LOCUST_HIP_CHECK(hipMalloc(&d_text_alt, cap_bytes + 64));
+      LOCUST_HIP_CHECK(hipMalloc(&d_dctr, sizeof(MapCounters)));
+    }
+    if (staging && !h_stage[0])
+      for (int b = 0; b < 2; ++b)
+        LOCUST_HIP_CHECK(hipHostMalloc(&h_stage[b], cap_bytes + 64, hipHostMallocDefault));
+    if (nchunks > h_chunk_cap) {
+      if (h_chunk_ctr) LOCUST_HIP_CHECK(hipHostFree(h_chunk_ctr));
+      h_chunk_cap = std::max<u64>(nchunks, 64);
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_chunk_ctr, h_chunk_cap * sizeof(MapCounters),
+                                     hipHostMallocDefault));
+    }
+  }
+
+  // Line-aligned chunk boundaries, each <= cap_bytes.
+  std::vector<std::pair<u64, u64>> plan_chunks(const TextInput& in) const {
+    std::vector<std::pair<u64, u64>> out;
+    u64 pos = 0;
+    while (pos < in.bytes) {
+      u64 end = std::min<u64>(pos + cap_bytes, in.bytes);
+      if (end < in.bytes) {
+        const void* nl = memrchr(in.data + pos, '\n', (size_t)(end - pos));
+        if (!nl)
+          throw Error("a line longer than the engine's chunk size (" + std::to_string(cap_bytes) +
+                      " B) at byte " + std::to_string(pos));
+        end = (u64)(static_cast<const char*>(nl) - in.data) + 1;
+      }
+      out.emplace_back(pos, end - pos);
+      pos = end;
+    }
+    return out;
+  }
+
+  // Streams every chunk of `in` through map + dictionary insert (the table is reset
+  // first).  When the stream has drained, d_ctr->num_unique / flags describe the whole
+  // dictionary and h_chunk_ctr[0 .. chunks) holds each chunk's map counters.
+  size_t enqueue_stream_insert(const TextInput& in) {
+    LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
+                     "inputs larger than the engine capacity stream through the dictionary "
+                     "path with the fast map (sort=dict, map=fast)");
+    LOCUST_CHECK_ARG(cap >= cap_bytes / 2 + 1,
+                     "a streaming engine must be sized by bytes (max_lines >= max_bytes / 40)");
+    const auto chunks = plan_chunks(in);
+    const bool pinned = host_pinned(in.data);
+    ensure_stream_buffers(!pinned, chunks.size());
+    const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));
+    // the copy stream must not overwrite a text buffer before the reset is queued
+    LOCUST_HIP_CHECK(hipEventRecord(ev_copied[1], stream));
+    LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_copied[1], 0));
+    for (size_t k = 0; k < chunks.size(); ++k) {
+      const int b = (int)(k & 1);
+      char* dtext = b ? d_text_alt : d_text;
+      const u64 off = chunks[k].first, len = chunks[k].second;
+      const char* src = in.data + off;
+      if (!pinned) {
+        // pageable input: host copy into a pinned half (overlapping the GPU's work on the
+        // previous chunks) once that half's previous H2D has drained
+        if (k >= 2) LOCUST_HIP_CHECK(hipEventSynchronize(ev_copied[b]));
+        std::memcpy(h_stage[b], src, len);
+        src = h_stage[b];
+      }
+      if (k >= 2) LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[b], 0));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(dtext, src, len, hipMemcpyHostToDevice, cstream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(dtext + len, 0, 16, cstream));
+      LOCUST_HIP_CHECK(hipEventRecord(ev_copied[b], cstream));
+
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+      launch_map_fast(dtext, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap, d_ctr,
+                      lb_map, stream);
+      LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
+                                      hipMemcpyDeviceToHost, stream));
+      launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
+    }
+    // hand the dictionary's counters to the single-pass stages that follow
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_unique, &d_dctr->num_unique, sizeof(u32),
+                                    hipMemcpyDeviceToDevice, stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->flags, &d_dctr->flags, sizeof(u32),
+                                    hipMemcpyDeviceToDevice, stream));
+    return chunks.size();
+  }
+
+  // After the stream has drained: whole-input map statistics from the chunk snapshots.
+  void stream_stats(size_t nchunks, WordCountResult& r) const {
+    r.num_tokens = r.overflow_lines = r.truncated = r.max_key_len = 0;
+    for (size_t k = 0; k < nchunks; ++k) {
+      const MapCounters& c = h_chunk_ctr[k];
+      r.num_tokens += c.num_records;
+      r.overflow_lines += c.overflow_lines;
+      r.truncated += c.truncated;
+      r.max_key_len = std::max<u64>(r.max_key_len, c.max_key_len);
+    }
+    r.chunks = nchunks;
+  }
+
+  WordCountResult run_stream(const TextInput& in) {
+    WordCountResult r;
+    r.num_lines = in.num_lines;
+    const u64 t0 = now_ns();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+    LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+    const size_t nchunks = enqueue_stream_insert(in);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+    enqueue_rank();
+    LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+    enqueue_emit_dict(/*mapped=*/true);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+    LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+    sync();
+    *h_ctr = *h_ctr_mapped;
+    if (h_ctr->flags & kCtrDictOverflow)
+      throw Error("streaming dictionary overflow: more than " + std::to_string(ucap) +
+                  " distinct keys; use a larger chunk size");
+    if (dict_fallback_needed()) {
+      // more distinct keys than the rank sort takes: LSD radix sort of the dictionary
+      finish_dict_with_radix(0);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      download_output(r, ev[5]);
+    } else {
+      const u64 u = h_ctr->num_unique;
+      r.entries.resize(u);
+      copy_out(r.entries, u);
+    }
+    stream_stats(nchunks, r);
+    r.num_unique = r.entries.size();
+    r.times.wall_ms = (now_ns() - t0) * 1e-6;
+    r.times.h2d_ms = 0;  // overlapped with the map: included in map_ms
+    r.times.map_ms = ms_between(ev[1], ev[2]);
+    r.times.process_ms = ms_between(ev[2], ev[3]);
+    r.times.reduce_ms = ms_between(ev[3], ev[4]);
+    r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    if (cfg.check) validate_result(r);
+    return r;
+  }
+
+  void download_keys(const KeysSoA& src, u64 n, std::vector<PackedKey>* out) {
+    out->resize(n);
+    if (!n) return;
+    grow_host_keys(n);
+    for (int w = 0; w < kKeyWords; ++w)
+      LOCUST_HIP_CHECK(hipMemcpyAsync(h_keys + (u64)w * n, src.w[w], n * sizeof(u64),
+                                      hipMemcpyDeviceToHost, stream));
+    sync();
+    for (u64 i = 0; i < n; ++i)
+      for (int w = 0; w < kKeyWords; ++w) (*out)[i].w[w] = h_keys[(u64)w * n + i];
+  }
+
+  void set_num_records(u64 n) {
+    LOCUST_CHECK_ARG(n <= cap, "too many records for engine capacity");
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+    h_u64[0] = n;  // little endian: low 32 bits == num_records
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_records, h_u64, sizeof(u32),
+                                    hipMemcpyHostToDevice, stream));
+  }
+
+  void upload_tokens(const PackedKey* keys, u64 n) {
+    parts_ready = false;
+    set_num_records(n);
+    grow_host_keys(n);
+    for (u64 i = 0; i < n; ++i)
+      for (int w = 0; w < kKeyWords; ++w) h_keys[(u64)w * n + i] = keys[i].w[w];
+    if (n)
+      for (int w = 0; w < kKeyWords; ++w)
+        LOCUST_HIP_CHECK(hipMemcpyAsync(tokens.w[w], h_keys + (u64)w * n, n * sizeof(u64),
+                                        hipMemcpyHostToDevice, stream));
+  }
+};
+
+
+}  // namespace detail
+}  // namespace locust

@@ -1,0 +1,352 @@
+// Per-rank GPU shard engine of the distributed driver (csrc/engine/dist.cpp): map +
+// combine of this rank's shard, shuffle records and splitter samples, reduce of the
+// received records, and the root's merge of the gather strategy.
+#include "pipeline.hpp"
+
+namespace locust {
+
+using detail::DevicePipeline;
+using detail::kMaxRanks;
+using detail::kMaxSamples;
+
+// =====================================================================================
+// GPU shard engine (one rank of the distributed job)
+// =====================================================================================
+namespace {
+
+class GpuShardEngine final : public ShardEngine {
+ public:
+  GpuShardEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
+      : cfg_(cfg), mp_(new DevicePipeline(cfg, max_bytes, max_lines)) {}
+
+  bool device_buffers() const override { return true; }
+  void* stream() override { return mp_->stream; }
+  char* input_buffer() override { return mp_->h_text; }
+
+  u64 map_local(const TextInput& shard, bool combine, DistStrategy plan) override {
+    DevicePipeline& m = *mp_;
+    const bool compat = cfg_.map_path == MapPath::kCompat;
+    samples_valid_ = false;
+    sorted_local_ = true;
+    stream_chunks_ = 0;
+    const bool streamed = shard.bytes > m.cap_bytes;
+    const bool small_ordered = combine && cfg_.sort_path == SortPath::kDict && !streamed &&
+                               cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
+    if (streamed) {
+      // a shard larger than one device pass: chunked H2D + map into one dictionary
+      LOCUST_CHECK_ARG(combine && cfg_.sort_path == SortPath::kDict,
+                       "streaming shards need the map-side combine of the dictionary path");
+      stream_chunks_ = m.enqueue_stream_insert(shard);
+    } else if (!small_ordered) {
+      m.check_input(shard);
+      m.enqueue_upload(shard);
+      m.enqueue_map(shard);
+    }
+    if (small_ordered) {
+      // Small pass: upload, map and the ordered kernel give this rank's distinct keys
+      // sorted, with counts; one more kernel lays them out as shuffle records + SoA keys,
+      // and the splitter samples and counters come back -- one captured graph, ONE host
+      // synchronisation for either strategy.
+      m.check_input(shard);
+      m.prepare_upload(shard);
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      auto enqueue = [&] {
+        m.enqueue_upload_device(shard);
+        m.enqueue_map(shard);
+        m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
+        launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
+                             m.d_records, m.stream);
+        launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                        hipMemcpyDeviceToHost, m.stream));
+        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters),
+                                        hipMemcpyDeviceToHost, m.stream));
+      };
+      m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
+      if (m.use_graph())
+        m.launch_cached({2, shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text),
+                         (u64)m.upload_mode,
+                         m.upload_mode == DevicePipeline::Upload::kDirect
+                             ? reinterpret_cast<u64>(shard.data) : 0},
+                        enqueue);
+      else
+        enqueue();
+      m.sync();
+      if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+        samples_.assign(m.h_small, m.h_small + kSpecSamples);
+        samples_valid_ = true;
+        return finish_map_stats(shard, m.h_ctr->num_unique);
+      }
+      // a partition overflowed its LDS table: redo this rank's combine on the HBM table
+      LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->num_unique, 0, sizeof(u32), m.stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->flags, 0, sizeof(u32), m.stream));
+      LOCUST_HIP_CHECK(hipMemsetAsync(m.dict.table, 0, m.dict_zero_bytes, m.stream));
+      launch_dict_insert(m.tokens, nullptr, &m.d_ctr->num_records, m.cap, m.dict, m.d_ctr,
+                         m.stream);
+      m.read_counters();
+      if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
+      if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
+        m.enqueue_rank();
+        m.enqueue_sorted_from_dict();
+      } else {
+        radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                   m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+      }
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+      m.read_counters();
+      return finish_map_stats(shard, m.h_ctr->num_unique);
+    }
+    if (combine && cfg_.sort_path == SortPath::kDict) {
+      if (plan == DistStrategy::kGather) {
+        // Gather plan: the combined records go to rank 0 unsorted, straight from the
+        // dictionary's dense arrays; no local sort at all.
+        if (!streamed) m.enqueue_dict_insert((u32)shard.num_lines, compat, false);
+        launch_pack_records(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique, m.ucap,
+                            m.d_records, m.stream);
+        m.read_counters();
+        if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+          set_local(m.dict.ukeys, m.dict.ucount, &m.d_ctr->num_unique);
+          sorted_local_ = false;
+          return finish_map_stats(shard, m.h_ctr->num_unique);
+        }
+        return map_overflow_fallback(shard);
+      }
+      // Map-side combine through the dictionary: sorted distinct keys + counts.  The
+      // shuffle records and the splitter samples are produced speculatively in the same
+      // stream, so the common case costs ONE host synchronisation.
+      if (streamed)
+        m.enqueue_rank();
+      else
+        m.enqueue_process_dict((u32)shard.num_lines, compat);
+      m.enqueue_sorted_from_dict();
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+      launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                      hipMemcpyDeviceToHost, m.stream));
+      m.read_counters();
+      if (!m.dict_fallback_needed()) {
+        samples_.assign(m.h_small, m.h_small + kSpecSamples);
+        samples_valid_ = true;
+        return finish_map_stats(shard, m.h_ctr->num_unique);
+      }
+      if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
+      // more distinct keys than the rank sort takes: radix-sort the dictionary's keys
+      radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                 m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    } else {
+      m.enqueue_process((u32)shard.num_lines, compat, false);
+      if (combine) {
+        // Map-side combine: local (key, count) runs become the shuffle records.
+        m.enqueue_reduce_core(false);
+        set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
+      } else {
+        set_local(m.sorted, nullptr, &m.d_ctr->num_records);
+      }
+    }
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.read_counters();
+    return finish_map_stats(shard, combine ? m.h_ctr->num_unique : m.h_ctr->num_records);
+  }
+
+  // Shuffle after a gather-planned map: sort the dictionary's keys, repack, resample.
+  void prepare_shuffle() override {
+    if (sorted_local_) return;
+    DevicePipeline& m = *mp_;
+    if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
+      m.enqueue_rank();  // ranks are zero: reset with the table / written by the build
+      m.enqueue_sorted_from_dict();
+    } else {
+      radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                 m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+    }
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.sync();
+    sorted_local_ = true;
+  }
+
+  std::vector<PackedKey> sample(u32 s) override {
+    DevicePipeline& m = *mp_;
+    prepare_shuffle();
+    if (samples_valid_ && s == kSpecSamples) return samples_;
+    LOCUST_CHECK_ARG(s <= kMaxSamples, "too many samples");
+    launch_sample_keys(local_keys(), local_n(), s, m.d_samples, m.stream);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, s * sizeof(PackedKey),
+                                    hipMemcpyDeviceToHost, m.stream));
+    m.sync();
+    return std::vector<PackedKey>(m.h_small, m.h_small + s);
+  }
+
+  std::vector<u64> bucket_offsets(const std::vector<PackedKey>& splitters) override {
+    DevicePipeline& m = *mp_;
+    const u32 P = (u32)splitters.size() + 1;
+    LOCUST_CHECK_ARG(P <= kMaxRanks, "too many ranks");
+    prepare_shuffle();
+    if (!splitters.empty()) {
+      std::memcpy(m.h_small, splitters.data(), splitters.size() * sizeof(PackedKey));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.d_splitters, m.h_small,
+                                      splitters.size() * sizeof(PackedKey), hipMemcpyHostToDevice,
+                                      m.stream));
+    }
+    launch_bucket_offsets(local_keys(), local_n(), m.d_splitters, P, m.d_offsets, m.stream);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_u64, m.d_offsets, (P + 1) * sizeof(u64),
+                                    hipMemcpyDeviceToHost, m.stream));
+    m.sync();
+    return std::vector<u64>(m.h_u64, m.h_u64 + P + 1);
+  }
+
+  const void* send_records() override { return mp_->d_records; }
+
+  void* recv_records(u64 n) override {
+    if (!rp_ || rp_->cap < n) {
+      const u64 want = std::max<u64>(std::max<u64>(n + n / 4, 4096), rp_ ? rp_->cap * 2 : 0);
+      rp_.reset();
+      rp_.reset(new DevicePipeline(cfg_, 1, 1, want));
+    }
+    return rp_->d_records;
+  }
+
+  void reduce_received(u64 n, u64* total_count, u64* num_unique) override {
+    DevicePipeline& r = *rp_;
+    // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
+    r.set_num_records(n);
+    launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
+    r.parts_ready = true;
+    WordCountResult tmp;
+    bool downloaded = false;
+    if (cfg_.sort_path == SortPath::kDict) {
+      const bool ordered = r.enqueue_dict_job(0, false, true, nullptr);
+      r.sync();
+      *r.h_ctr = *r.h_ctr_mapped;
+      const bool ordered_done = ordered && !(r.h_ctr->flags & kCtrDictOverflow);
+      if (ordered && !ordered_done) r.redo_dict_on_table(0, true);
+      if (!ordered_done && r.dict_fallback_needed()) {
+        r.finish_dict_with_radix(0, true);
+      } else {
+        r.fill_counters(tmp);
+        r.copy_out(tmp.entries, r.h_ctr->num_unique);
+        downloaded = true;
+      }
+    } else {
+      r.enqueue_process(0, false, true, n);
+      r.enqueue_reduce_core(true);
+      r.enqueue_pack_output();
+    }
+    if (!downloaded) r.download_output(tmp, nullptr);
+    *total_count = r.h_ctr->total_count;
+    *num_unique = r.h_ctr->num_unique;
+    range_entries_ = std::move(tmp.entries);
+  }
+
+  // The root's own combined records go behind the received ones; one dictionary pass over
+  // all of them (partition tags come from the unpack) yields the merged, ranked output.
+  void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) override {
+    DevicePipeline& m = *mp_;
+    DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
+    LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
+    const u64 n = n_other + local_count_;
+    if (cfg_.sort_path == SortPath::kDict && r.cap <= kPartBuildMaxTokens && r.use_graph()) {
+      // The whole merge as one captured sequence on the receive pipeline: own records
+      // behind the received ones, counters reset, unpack (with partition tags), the ordered
+      // kernel writing the final records into host-mapped memory.
+      r.h_u64[0] = n;  // read by the captured H2D at replay time
+      auto enqueue = [&] {
+        if (local_count_)
+          LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
+                                          local_count_ * sizeof(KeyCount),
+                                          hipMemcpyDeviceToDevice, r.stream));
+        LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, r.stream));
+        LOCUST_HIP_CHECK(hipMemcpyAsync(&r.d_ctr->num_records, r.h_u64, sizeof(u32),
+                                        hipMemcpyHostToDevice, r.stream));
+        launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
+        r.enqueue_dict_ordered(/*with_counts=*/true, /*mapped=*/true);
+      };
+      r.parts_ready = true;
+      r.launch_cached({3, n_other, local_count_, reinterpret_cast<u64>(m.d_records), 0, 0},
+                      enqueue);
+      r.sync();
+      *r.h_ctr = *r.h_ctr_mapped;
+      if (!(r.h_ctr->flags & kCtrDictOverflow)) {
+        WordCountResult tmp;
+        r.fill_counters(tmp);
+        r.copy_out(tmp.entries, r.h_ctr->num_unique);
+        *total_count = r.h_ctr->total_count;
+        *num_unique = r.h_ctr->num_unique;
+        range_entries_ = std::move(tmp.entries);
+        return;
+      }
+      // a partition overflowed: the general path below redoes the merge
+    }
+    if (local_count_)
+      LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
+                                      local_count_ * sizeof(KeyCount), hipMemcpyDeviceToDevice,
+                                      m.stream));
+    m.sync();
+    reduce_received(n_other + local_count_, total_count, num_unique);
+  }
+
+  void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
+    for (auto& e : range_entries_) e.val += global_offset;
+    *out = std::move(range_entries_);
+  }
+
+  void map_stats(WordCountResult* r) override { *r = local_stats_; }
+
+ private:
+  u64 finish_map_stats(const TextInput& shard, u64 n_records) {
+    DevicePipeline& m = *mp_;
+    local_stats_ = WordCountResult();
+    local_stats_.num_lines = shard.num_lines;
+    m.fill_counters(local_stats_);
+    local_stats_.num_tokens = m.h_ctr->num_records;
+    if (stream_chunks_) m.stream_stats(stream_chunks_, local_stats_);
+    local_count_ = n_records;
+    return n_records;
+  }
+  // Dictionary table overflow: sort every token and combine the reference way.
+  u64 map_overflow_fallback(const TextInput& shard) {
+    DevicePipeline& m = *mp_;
+    if (stream_chunks_)
+      throw Error("streaming dictionary overflow: more than " + std::to_string(m.ucap) +
+                  " distinct keys in one shard; use a larger chunk size");
+    m.enqueue_process(0, false, false, m.h_ctr->num_records);
+    m.enqueue_reduce_core(false);
+    set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.read_counters();
+    return finish_map_stats(shard, m.h_ctr->num_unique);
+  }
+  void set_local(ConstKeysSoA k, const u64* c, const u32* n) {
+    local_keys_ = k;
+    local_counts_ = c;
+    local_n_ = n;
+  }
+  ConstKeysSoA local_keys() const { return local_keys_; }
+  const u32* local_n() const { return local_n_; }
+
+  JobConfig cfg_;
+  std::unique_ptr<DevicePipeline> mp_, rp_;
+  static constexpr u32 kSpecSamples = 64;  // DistConfig::samples_per_rank default
+  ConstKeysSoA local_keys_{};
+  std::vector<PackedKey> samples_;
+  bool samples_valid_ = false;
+  std::vector<WordCountEntry> range_entries_;
+  const u64* local_counts_ = nullptr;
+  const u32* local_n_ = nullptr;
+  WordCountResult local_stats_;
+  u64 local_count_ = 0;
+  size_t stream_chunks_ = 0;  // > 0: the last shard streamed through in this many chunks
+  bool sorted_local_ = true;  // d_records are sorted (shuffle-ready)
+};
+
+}  // namespace
+
+std::unique_ptr<ShardEngine> make_gpu_shard_engine(const JobConfig& cfg, u64 max_bytes,
+                                                   u64 max_lines) {
+  return std::unique_ptr<ShardEngine>(new GpuShardEngine(cfg, max_bytes, max_lines));
+}
+
+}  // namespace locust

@@ -3,6 +3,9 @@
 // bounded copy into a 30-byte key field, strtok_r over the string (token count and the
 // byte offsets of the first 8 tokens) and itoa of an integer -- the Python test compares
 // every field with the host build of the same header and with Python references.
+#include <string>
+#include <vector>
+
 #include "locust/dstring.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
@@ -41,6 +44,46 @@ void launch_string_selftest(const char* blob, const u32* off, u32 n, const char*
   if (!n) return;
   string_selftest_kernel<<<dim3((n + 63) / 64), dim3(64), 0, s>>>(blob, off, n, delims, ints, out);
   LOCUST_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace locust
+
+namespace locust {
+
+std::vector<StringTestOut> run_string_selftest(const std::vector<std::string>& strings,
+                                               const std::vector<int>& ints,
+                                               const std::string& delims, int device) {
+  LOCUST_CHECK_ARG(ints.size() == strings.size(), "one integer per string");
+  LOCUST_HIP_CHECK(hipSetDevice(device));
+  std::string blob;
+  std::vector<u32> off;
+  for (const auto& x : strings) {
+    LOCUST_CHECK_ARG(x.size() < (size_t)kStringTestMax, "self-test strings are < 128 bytes");
+    off.push_back((u32)blob.size());
+    blob += x;
+    blob.push_back('\0');
+  }
+  const u32 n = (u32)strings.size();
+  std::vector<StringTestOut> out(n);
+  if (!n) return out;
+  char *d_blob = nullptr, *d_delims = nullptr;
+  u32* d_off = nullptr;
+  int* d_ints = nullptr;
+  StringTestOut* d_out = nullptr;
+  LOCUST_HIP_CHECK(hipMalloc(&d_blob, blob.size()));
+  LOCUST_HIP_CHECK(hipMalloc(&d_delims, delims.size() + 1));
+  LOCUST_HIP_CHECK(hipMalloc(&d_off, n * sizeof(u32)));
+  LOCUST_HIP_CHECK(hipMalloc(&d_ints, n * sizeof(int)));
+  LOCUST_HIP_CHECK(hipMalloc(&d_out, n * sizeof(StringTestOut)));
+  LOCUST_HIP_CHECK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  LOCUST_HIP_CHECK(hipMemcpy(d_delims, delims.c_str(), delims.size() + 1, hipMemcpyHostToDevice));
+  LOCUST_HIP_CHECK(hipMemcpy(d_off, off.data(), n * sizeof(u32), hipMemcpyHostToDevice));
+  LOCUST_HIP_CHECK(hipMemcpy(d_ints, ints.data(), n * sizeof(int), hipMemcpyHostToDevice));
+  launch_string_selftest(d_blob, d_off, n, d_delims, d_ints, d_out, nullptr);
+  LOCUST_HIP_CHECK(hipMemcpy(out.data(), d_out, n * sizeof(StringTestOut), hipMemcpyDeviceToHost));
+  for (void* p : {(void*)d_blob, (void*)d_delims, (void*)d_off, (void*)d_ints, (void*)d_out})
+    (void)hipFree(p);
+  return out;
 }
 
 }  // namespace locust
