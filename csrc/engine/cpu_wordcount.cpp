@@ -193,7 +193,10 @@ class CpuShardEngine final : public ShardEngine {
     *num_unique = out_.size();
   }
 
-  void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) override {
+  void reduce_gathered(const std::vector<u64>& run_lens, u64* total_count,
+                       u64* num_unique) override {
+    u64 n_other = 0;
+    for (u64 l : run_lens) n_other += l;
     recv_.resize(std::max<u64>(n_other + local_.size(), 1));
     std::copy(local_.begin(), local_.end(), recv_.begin() + (long)n_other);
     reduce_received(n_other + local_.size(), total_count, num_unique);

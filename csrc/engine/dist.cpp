@@ -230,7 +230,10 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       // The root merges: a failure here is the job's failure (only the root holds output).
       u64 total = 0, uniq = 0;
       if (!st)
-        st = local("reduce", [&] { eng.reduce_gathered(sum_records - n_local, &total, &uniq); });
+        st = local("reduce", [&] {
+          const std::vector<u64> runs(counts.begin() + 1, counts.end());
+          eng.reduce_gathered(runs, &total, &uniq);
+        });
       if (st)
         throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
       eng.finalize(0, &r.entries);

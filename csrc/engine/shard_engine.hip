@@ -243,30 +243,37 @@ class GpuShardEngine final : public ShardEngine {
 
   // The root's own combined records go behind the received ones; one dictionary pass over
   // all of them (partition tags come from the unpack) yields the merged, ranked output.
-  void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) override {
+  void reduce_gathered(const std::vector<u64>& run_lens, u64* total_count,
+                       u64* num_unique) override {
     DevicePipeline& m = *mp_;
     DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
+    u64 n_other = 0;
+    for (u64 l : run_lens) n_other += l;
     LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
-    const u64 n = n_other + local_count_;
-    if (cfg_.sort_path == SortPath::kDict && r.cap <= kPartBuildMaxTokens && r.use_graph()) {
-      // The whole merge as one captured sequence on the receive pipeline: own records
-      // behind the received ones, counters reset, unpack (with partition tags), the ordered
-      // kernel writing the final records into host-mapped memory.
-      r.h_u64[0] = n;  // read by the captured H2D at replay time
+    const int nruns = (int)run_lens.size() + 1;
+    if (cfg_.sort_path == SortPath::kDict && sorted_local_ && nruns <= kMaxMergeRunsHost &&
+        n_other + local_count_ <= kPartBuildMaxTokens) {
+      // Every run is sorted: the merge kernel finds each partition's range in every run by
+      // binary search and writes the final records into host-mapped memory -- one kernel
+      // (plus the counter reset and the run table), captured as one graph.
+      u32* meta = reinterpret_cast<u32*>(r.h_u64);  // pinned; read at replay time
+      meta[0] = (u32)nruns;
+      meta[1] = (u32)local_count_;
+      for (int q = 1; q < nruns; ++q) meta[1 + q] = (u32)run_lens[(size_t)q - 1];
+      u32* d_meta = reinterpret_cast<u32*>(r.d_offsets);
       auto enqueue = [&] {
-        if (local_count_)
-          LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
-                                          local_count_ * sizeof(KeyCount),
-                                          hipMemcpyDeviceToDevice, r.stream));
         LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, r.stream));
-        LOCUST_HIP_CHECK(hipMemcpyAsync(&r.d_ctr->num_records, r.h_u64, sizeof(u32),
+        LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + (u64)nruns) * sizeof(u32),
                                         hipMemcpyHostToDevice, r.stream));
-        launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
-        r.enqueue_dict_ordered(/*with_counts=*/true, /*mapped=*/true);
+        launch_dict_merge_runs(m.d_records, r.d_records, d_meta, r.d_ctr, r.d_out_mapped,
+                               r.d_ctr_mapped, r.lb_dict, r.stream);
       };
-      r.parts_ready = true;
-      r.launch_cached({3, n_other, local_count_, reinterpret_cast<u64>(m.d_records), 0, 0},
-                      enqueue);
+      if (r.use_graph())
+        r.launch_cached({4, (u64)nruns, reinterpret_cast<u64>(m.d_records),
+                         reinterpret_cast<u64>(r.d_records), 0, 0},
+                        enqueue);
+      else
+        enqueue();
       r.sync();
       *r.h_ctr = *r.h_ctr_mapped;
       if (!(r.h_ctr->flags & kCtrDictOverflow)) {
@@ -278,8 +285,9 @@ class GpuShardEngine final : public ShardEngine {
         range_entries_ = std::move(tmp.entries);
         return;
       }
-      // a partition overflowed: the general path below redoes the merge
+      // a partition overflowed its LDS table: the general path below redoes the merge
     }
+    // General path: this rank's records behind the received ones, then the usual reduce.
     if (local_count_)
       LOCUST_HIP_CHECK(hipMemcpyAsync(r.d_records + n_other, m.d_records,
                                       local_count_ * sizeof(KeyCount), hipMemcpyDeviceToDevice,

@@ -118,9 +118,11 @@ class ShardEngine {
   virtual void* recv_records(u64 n) = 0;       // room for n incoming KeyCount records
   // Sort + weighted reduce of the n received records; returns {total_count, num_unique}.
   virtual void reduce_received(u64 n, u64* total_count, u64* num_unique) = 0;
-  // Gather strategy, root only: reduce this rank's own records together with the n_other
-  // records the other ranks sent (already in recv_records(), which holds room for both).
-  virtual void reduce_gathered(u64 n_other, u64* total_count, u64* num_unique) = 0;
+  // Gather strategy, root only: reduce this rank's own records together with the records
+  // the other ranks sent (already in recv_records(), which holds room for both), back to
+  // back in rank order; run_lens[i] = records from rank i+1 (each such run is sorted).
+  virtual void reduce_gathered(const std::vector<u64>& run_lens, u64* total_count,
+                               u64* num_unique) = 0;
   // Strategy of the previous job (the driver's prediction for the next one under kAuto).
   DistStrategy last_strategy = DistStrategy::kShuffle;
   virtual void finalize(u64 global_offset, std::vector<WordCountEntry>* out) = 0;

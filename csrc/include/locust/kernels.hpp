@@ -198,6 +198,13 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
                          u64* trace = nullptr);
+// Same, over runs of KeyCount records each sorted by key (the gather strategy's per-rank
+// combined outputs); duplicates across runs are summed.  Run 0 is `own`, runs 1.. lie
+// back to back in `recv`; `meta` (device) = [nruns <= 64, len_0, len_1, ...].
+constexpr int kMaxMergeRunsHost = 64;
+void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
+                            MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                            LookbackScratch lb, hipStream_t s);
 // Hash every token (with its count; null = 1) into the table; distinct keys land in
 // ukeys[0 .. ctr->num_unique) with summed counts in ucount.
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,

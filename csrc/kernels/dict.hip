@@ -360,9 +360,134 @@ __device__ __forceinline__ bool ord_greater(u64 aw0, u32 as, u64 bw0, u32 bs, co
   return false;
 }
 
+// Token source of the ordered kernel: the map output (or unpacked records), found by
+// scanning the one-byte partition tags of every token.
+struct TagSource {
+  ConstKeysSoA tokens;
+  const u64* counts;
+  const u8* parts;
+  const u32* d_n;
+  u32 n_cap;
+  // Inserts partition p's tokens into `s_tab`; `s_list` / `s_count` are LDS scratch.
+  // Returns true if the table overflowed.
+  __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+    const u32 n = min(*d_n, n_cap);
+    bool full = false;
+    u32 pos = threadIdx.x * 16u;
+    uint4 v = pos < n ? *reinterpret_cast<const uint4*>(parts + pos) : uint4{0, 0, 0, 0};
+    for (u32 round = 0; round < n; round += kPartWindow, pos += kPartWindow) {
+      u32 mask = 0;
+      const u32 wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (((wv[q] >> (8 * b)) & 0xffu) == p && pos + (u32)(q * 4 + b) < n) mask |= 1u << (q * 4 + b);
+      const u32 next = pos + kPartWindow;
+      if (next < n) v = *reinterpret_cast<const uint4*>(parts + next);
+      {
+        // one LDS atomic per wave: the wave's matches are appended as one run
+        const u32 nm = (u32)__popc(mask);
+        const u32 incl = dev::wave_inclusive_scan(nm);
+        u32 wbase = 0;
+        if (dev::lane_id() == 63 && incl) wbase = atomicAdd(&s_count, incl);
+        wbase = (u32)__shfl((int)wbase, 63, 64);
+        u32 at = wbase + incl - nm;
+        while (mask) {
+          const int b = __ffs(mask) - 1;
+          mask &= mask - 1;
+          s_list[at++] = pos + (u32)b;
+        }
+      }
+      __syncthreads();
+      const u32 cnt = s_count;
+      for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
+        const u32 i = s_list[e];
+        u64 k[kKeyWords];
+        load_key(tokens, i, k);
+        const u64 c = counts ? counts[i] : 1ull;
+        if (k[0] == 0 || c == 0) continue;
+        full |= !part_lds_insert(s_tab, k, c, key_hash(k));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) s_count = 0;
+      __syncthreads();
+    }
+    return full;
+  }
+};
+
+// Token source of the gather-strategy merge: runs of KeyCount records, each sorted by
+// key (the ranks' combined outputs).  Run 0 is `own`; runs 1.. lie back to back in `recv`.
+// The run count and lengths are read from device memory (`meta` = [nruns, len0, len1,
+// ...]), so a captured graph stays valid when they change.  A workgroup binary-searches
+// its partition's range in every run and reads only those records (contiguous, no tag
+// scan, no unpack).
+constexpr int kMaxMergeRuns = 64;
+struct RunsSource {
+  const KeyCount* own;
+  const KeyCount* recv;
+  const u32* meta;
+  __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+    // s_list: [lo, hi) per run | exclusive prefix of the partition's records | run offsets
+    u32* s_lo = s_list;
+    u32* s_pre = s_list + 2 * kMaxMergeRuns;
+    u32* s_off = s_pre + kMaxMergeRuns + 1;
+    const u32 nruns = min(meta[0], (u32)kMaxMergeRuns);
+    if (threadIdx.x == 0) {
+      u32 acc = 0;
+      for (u32 q = 1; q < nruns; ++q) {
+        s_off[q] = acc;
+        acc += meta[1 + q];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < nruns) {
+      const u32 q = threadIdx.x;
+      const KeyCount* r = q == 0 ? own : recv + s_off[q];
+      const u32 n = meta[1 + q];
+      u32 a = 0, b = n;  // first record with first byte >= p
+      while (a < b) {
+        const u32 mid = (a + b) >> 1;
+        if ((u32)(r[mid].w[0] >> 56) < p) a = mid + 1; else b = mid;
+      }
+      u32 c = a, d = n;  // first record with first byte > p
+      while (c < d) {
+        const u32 mid = (c + d) >> 1;
+        if ((u32)(r[mid].w[0] >> 56) <= p) c = mid + 1; else d = mid;
+      }
+      s_lo[2 * q] = a;
+      s_lo[2 * q + 1] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u32 acc = 0;
+      for (u32 q = 0; q < nruns; ++q) {
+        s_pre[q] = acc;
+        acc += s_lo[2 * q + 1] - s_lo[2 * q];
+      }
+      s_pre[nruns] = acc;
+    }
+    __syncthreads();
+    const u32 total = s_pre[nruns];
+    bool full = false;
+    for (u32 e = threadIdx.x; e < total; e += kPartBlock) {
+      u32 q = 0;
+      while (q + 1 < nruns && s_pre[q + 1] <= e) ++q;
+      const KeyCount* r = q == 0 ? own : recv + s_off[q];
+      const KeyCount& rec = r[s_lo[2 * q] + (e - s_pre[q])];
+      const u64 k[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
+      if (k[0] == 0 || rec.count == 0) continue;
+      full |= !part_lds_insert(s_tab, k, rec.count, key_hash(k));
+    }
+    __syncthreads();
+    return full;
+  }
+};
+
+template <class Src>
 __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
-    ConstKeysSoA tokens, const u64* __restrict__ counts, const u8* __restrict__ parts,
-    const u32* __restrict__ d_n, u32 n_cap, MapCounters* __restrict__ ctr,
+    Src src, MapCounters* __restrict__ ctr,
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace) {
 #define ORD_STAMP(k_)                                                          \
@@ -383,48 +508,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   if (threadIdx.x == 0) s_count = 0;
   __syncthreads();
-  const u32 n = min(*d_n, n_cap);
-  bool full = false;
-  u32 pos = threadIdx.x * 16u;
-  uint4 v = pos < n ? *reinterpret_cast<const uint4*>(parts + pos) : uint4{0, 0, 0, 0};
-  for (u32 round = 0; round < n; round += kPartWindow, pos += kPartWindow) {
-    u32 mask = 0;
-    const u32 wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        if (((wv[q] >> (8 * b)) & 0xffu) == p && pos + (u32)(q * 4 + b) < n) mask |= 1u << (q * 4 + b);
-    const u32 next = pos + kPartWindow;
-    if (next < n) v = *reinterpret_cast<const uint4*>(parts + next);
-    {
-      // one LDS atomic per wave: the wave's matches are appended as one run
-      const u32 nm = (u32)__popc(mask);
-      const u32 incl = dev::wave_inclusive_scan(nm);
-      u32 wbase = 0;
-      if (dev::lane_id() == 63 && incl) wbase = atomicAdd(&s_count, incl);
-      wbase = (u32)__shfl((int)wbase, 63, 64);
-      u32 at = wbase + incl - nm;
-      while (mask) {
-        const int b = __ffs(mask) - 1;
-        mask &= mask - 1;
-        s_list[at++] = pos + (u32)b;
-      }
-    }
-    __syncthreads();
-    const u32 cnt = s_count;
-    for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
-      const u32 i = s_list[e];
-      u64 k[kKeyWords];
-      load_key(tokens, i, k);
-      const u64 c = counts ? counts[i] : 1ull;
-      if (k[0] == 0 || c == 0) continue;
-      full |= !part_lds_insert(s_tab, k, c, key_hash(k));
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) s_count = 0;
-    __syncthreads();
-  }
+  const bool full = src.build(p, s_tab, s_list, s_count);
   ORD_STAMP(1);
   // ---- compact: dense (w0, slot) arrays in the list area ----
   u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
@@ -821,9 +905,18 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace) {
-  dict_ordered_kernel<<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
-      tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu), ctr, out, ctr_out,
-      lb.status, lb.tile_counter, trace);
+  const TagSource src{tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
+  dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+      src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
+                            MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                            LookbackScratch lb, hipStream_t s) {
+  const RunsSource src{own, recv, meta};
+  dict_ordered_kernel<RunsSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+      src, ctr, out, ctr_out, lb.status, lb.tile_counter, nullptr);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
