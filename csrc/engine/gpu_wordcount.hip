@@ -77,4 +77,43 @@ std::vector<u32> GpuWordCount::sort_keys(const PackedKey* keys, u64 n,
   return perm;
 }
 
+std::vector<PackedKey> GpuWordCount::compact_slots(const u32* line_counts, u32 num_lines,
+                                                   const PackedKey* slot_keys) {
+  Impl& m = *impl_;
+  LOCUST_CHECK_ARG(m.cfg.map_path == MapPath::kCompat, "compact_slots needs a compat engine");
+  LOCUST_CHECK_ARG(num_lines <= m.cap_lines, "too many lines for engine capacity");
+  const u64 E = (u64)m.cfg.emits_per_line;
+  u64 live = 0;
+  for (u32 l = 0; l < num_lines; ++l) {
+    LOCUST_CHECK_ARG(line_counts[l] <= E, "line count above emits_per_line");
+    live += line_counts[l];
+  }
+  LOCUST_CHECK_ARG(live <= m.cap, "too many live slots for engine capacity");
+  m.set_num_records(0);
+  m.upload_keys(m.slots, slot_keys, (u64)num_lines * E);
+  m.sync();  // the key staging is reused below
+  if (num_lines)
+    LOCUST_HIP_CHECK(hipMemcpy(m.d_line_counts, line_counts, num_lines * sizeof(u32),
+                               hipMemcpyHostToDevice));
+  launch_compact_slots(m.d_line_counts, num_lines, (int)E, m.slots, m.tokens, m.d_ctr,
+                       m.lb_compact, m.stream);
+  LOCUST_HIP_CHECK(
+      hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters), hipMemcpyDeviceToHost, m.stream));
+  m.sync();
+  std::vector<PackedKey> out;
+  m.download_keys(m.tokens, m.h_ctr->num_records, &out);
+  return out;
+}
+
+WordCountResult GpuWordCount::reduce_sorted(const PackedKey* sorted, u64 n) {
+  Impl& m = *impl_;
+  WordCountResult r;
+  m.set_num_records(n);
+  m.upload_keys(m.sorted, sorted, n);
+  m.enqueue_reduce_core(false);
+  m.enqueue_pack_output();
+  m.download_output(r, m.ev[5]);
+  return r;
+}
+
 }  // namespace locust

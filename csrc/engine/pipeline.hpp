@@ -999,12 +999,16 @@ struct DevicePipeline {
   void upload_tokens(const PackedKey* keys, u64 n) {
     parts_ready = false;
     set_num_records(n);
+    upload_keys(tokens, keys, n);
+  }
+  // Host keys (AoS) into device SoA words through the pinned key staging.
+  void upload_keys(const KeysSoA& dst, const PackedKey* keys, u64 n) {
     grow_host_keys(n);
     for (u64 i = 0; i < n; ++i)
       for (int w = 0; w < kKeyWords; ++w) h_keys[(u64)w * n + i] = keys[i].w[w];
     if (n)
       for (int w = 0; w < kKeyWords; ++w)
-        LOCUST_HIP_CHECK(hipMemcpyAsync(tokens.w[w], h_keys + (u64)w * n, n * sizeof(u64),
+        LOCUST_HIP_CHECK(hipMemcpyAsync(dst.w[w], h_keys + (u64)w * n, n * sizeof(u64),
                                         hipMemcpyHostToDevice, stream));
   }
 };

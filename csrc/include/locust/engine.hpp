@@ -81,6 +81,16 @@ class GpuWordCount {
   // Sort arbitrary packed keys on the device (used by tests and the shuffle receiver).
   std::vector<u32> sort_keys(const PackedKey* keys, u64 n, std::vector<PackedKey>* sorted);
 
+  // Single-stage entry points for the kernel unit tests.
+  // Stable compaction of the compat map's fixed slots (main.cu:411): slot_keys holds
+  // num_lines * emits_per_line keys, the first line_counts[l] slots of line l are live.
+  // Needs a MapPath::kCompat engine with capacity for num_lines lines.
+  std::vector<PackedKey> compact_slots(const u32* line_counts, u32 num_lines,
+                                       const PackedKey* slot_keys);
+  // Reduce steps over keys that are already sorted: boundary mark + head compaction +
+  // adjacent difference (main.cu:161-238, 462) on the configured reduce path.
+  WordCountResult reduce_sorted(const PackedKey* sorted, u64 n);
+
   const JobConfig& config() const;
   u64 token_capacity() const;
   u64 text_capacity() const;  // bytes per device pass (input_buffer() size)

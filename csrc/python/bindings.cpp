@@ -102,6 +102,27 @@ class PyGpuEngine {
     for (const auto& k : sorted) out.emplace_back(key_to_string(k));
     return py::make_tuple(out, perm);
   }
+  std::vector<py::bytes> compact_slots(const std::vector<u32>& line_counts,
+                                       const std::vector<std::string>& slot_keys) {
+    std::vector<PackedKey> slots;
+    for (const auto& s : slot_keys) slots.push_back(to_key(s));
+    LOCUST_CHECK_ARG(slots.size() == line_counts.size() * (u64)eng_.config().emits_per_line,
+                     "need num_lines * emits_per_line slot keys");
+    std::vector<PackedKey> dense;
+    {
+      py::gil_scoped_release nogil;
+      dense = eng_.compact_slots(line_counts.data(), (u32)line_counts.size(), slots.data());
+    }
+    std::vector<py::bytes> out;
+    for (const auto& k : dense) out.emplace_back(key_to_string(k));
+    return out;
+  }
+  PyResult reduce_sorted(const std::vector<std::string>& keys) {
+    std::vector<PackedKey> toks;
+    for (const auto& s : keys) toks.push_back(to_key(s));
+    py::gil_scoped_release nogil;
+    return PyResult{eng_.reduce_sorted(toks.data(), toks.size())};
+  }
   u64 capacity() const { return eng_.token_capacity(); }
   // Stage the text in the engine's pinned buffer once; run_loaded() then skips the copy.
   void load(const std::string& text) {
@@ -341,6 +362,8 @@ PYBIND11_MODULE(_locust, m) {
       .def("map_stage", &PyGpuEngine::map_stage)
       .def("reduce_stage", &PyGpuEngine::reduce_stage)
       .def("sort_keys", &PyGpuEngine::sort_keys)
+      .def("compact_slots", &PyGpuEngine::compact_slots)
+      .def("reduce_sorted", &PyGpuEngine::reduce_sorted)
       .def_property_readonly("capacity", &PyGpuEngine::capacity);
 
   m.def("cpu_run", [](const JobConfig& cfg, const std::string& text) {

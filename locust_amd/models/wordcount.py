@@ -52,6 +52,15 @@ class Engine:
             return [keys[i] for i in perm], perm
         return self._eng.sort_keys(keys)
 
+    def compact_slots(self, line_counts: list[int], slot_keys: list[bytes]) -> list[bytes]:
+        """Stable compaction of fixed [line * emits_per_line + k] slots (compat engine):
+        the first ``line_counts[l]`` slots of each line, in order."""
+        return self._eng.compact_slots(line_counts, slot_keys)
+
+    def reduce_sorted(self, keys: list[bytes]):
+        """Boundary mark + head compaction + adjacent difference over sorted keys."""
+        return self._eng.reduce_sorted(keys)
+
 
 def wordcount_text(text: bytes, backend: str = "gpu", cfg=None, **kw):
     cfg = cfg if cfg is not None else make_config(backend, **kw)
