@@ -193,8 +193,8 @@ class CpuShardEngine final : public ShardEngine {
     *num_unique = out_.size();
   }
 
-  void reduce_gathered(const std::vector<u64>& run_lens, u64* total_count,
-                       u64* num_unique) override {
+  void reduce_gathered(const std::vector<u64>& run_lens, u64 /*total_tokens*/, u32 /*run_flags*/,
+                       u64* total_count, u64* num_unique) override {
     u64 n_other = 0;
     for (u64 l : run_lens) n_other += l;
     recv_.resize(std::max<u64>(n_other + local_.size(), 1));

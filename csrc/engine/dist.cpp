@@ -82,7 +82,7 @@ std::vector<PackedKey> choose_splitters(const std::vector<PackedKey>& samples, u
 // so the gather strategy needs no further control traffic.
 struct alignas(8) Msg1 {  // after map + sampling
   i32 status;
-  u32 pad;
+  u32 record_flags;  // ShardEngine::record_flags() of the sender
   u64 n_local, lines, tokens, overflow, truncated, max_key_len;
 };
 struct alignas(8) Msg3 {  // after the reduce of the received key range (shuffle strategy)
@@ -168,7 +168,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const u64 m1 = sizeof(Msg1) + (u64)S * sizeof(PackedKey);
   std::vector<char> out1(m1), all1(m1 * (u64)P);
   {
-    Msg1 h{st1, 0, n_local, shard.num_lines, local_stats.num_tokens, local_stats.overflow_lines,
+    Msg1 h{st1, eng.record_flags(), n_local, shard.num_lines, local_stats.num_tokens, local_stats.overflow_lines,
            local_stats.truncated, local_stats.max_key_len};
     std::memcpy(out1.data(), &h, sizeof(h));
     std::memcpy(out1.data() + sizeof(h), mine_samples.data(), (u64)S * sizeof(PackedKey));
@@ -181,12 +181,14 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   std::vector<PackedKey> samples((size_t)P * S);
   std::vector<u64> counts((size_t)P);
   u64 sum_records = 0;
+  u32 run_flags = ~0u;
   WordCountResult& r = res.result;
   for (int p = 0; p < P; ++p) {
     const char* base = all1.data() + (u64)p * m1;
     Msg1 h;
     std::memcpy(&h, base, sizeof(h));
     counts[(size_t)p] = h.n_local;
+    run_flags &= h.record_flags;
     sum_records += h.n_local;
     std::memcpy(&samples[(size_t)p * S], base + sizeof(h), (u64)S * sizeof(PackedKey));
     r.num_lines += h.lines;
@@ -232,7 +234,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       if (!st)
         st = local("reduce", [&] {
           const std::vector<u64> runs(counts.begin() + 1, counts.end());
-          eng.reduce_gathered(runs, &total, &uniq);
+          eng.reduce_gathered(runs, r.num_tokens, run_flags, &total, &uniq);
         });
       if (st)
         throw Error(std::string("distributed job failed on rank 0: ") + local_msg);

@@ -116,4 +116,38 @@ WordCountResult GpuWordCount::reduce_sorted(const PackedKey* sorted, u64 n) {
   return r;
 }
 
+WordCountResult GpuWordCount::merge_runs(const std::vector<std::vector<KeyCount>>& runs) {
+  Impl& m = *impl_;
+  LOCUST_CHECK_ARG(!runs.empty() && runs.size() <= (size_t)kMaxMergeRunsHost,
+                   "need 1..64 runs");
+  u64 n = 0;
+  for (const auto& r : runs) n += r.size();
+  LOCUST_CHECK_ARG(n <= m.cap && n <= kMergeMaxRecords, "too many records for engine capacity");
+  m.set_num_records(0);
+  u32* meta = reinterpret_cast<u32*>(m.h_u64);
+  meta[0] = (u32)runs.size();
+  u64 off = 0;
+  for (size_t q = 0; q < runs.size(); ++q) {
+    meta[1 + q] = (u32)runs[q].size();
+    if (!runs[q].empty())
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.d_records + off, runs[q].data(),
+                                      runs[q].size() * sizeof(KeyCount), hipMemcpyHostToDevice,
+                                      m.stream));
+    off += runs[q].size();
+  }
+  u32* d_meta = reinterpret_cast<u32*>(m.d_offsets);
+  LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + runs.size()) * sizeof(u32),
+                                  hipMemcpyHostToDevice, m.stream));
+  m.grow_host_out(n);
+  launch_merge_sorted_runs(m.d_records, m.d_records + runs[0].size(), d_meta, m.cap,
+                           reinterpret_cast<KeyCount*>(m.d_out), m.d_ctr, m.d_out_mapped,
+                           m.d_ctr_mapped, m.lb_scan, m.stream);
+  m.sync();
+  *m.h_ctr = *m.h_ctr_mapped;
+  WordCountResult r;
+  m.fill_counters(r);
+  m.copy_out(r.entries, m.h_ctr->num_unique);
+  return r;
+}
+
 }  // namespace locust

@@ -28,6 +28,7 @@ class GpuShardEngine final : public ShardEngine {
     const bool compat = cfg_.map_path == MapPath::kCompat;
     samples_valid_ = false;
     sorted_local_ = true;
+    distinct_local_ = true;  // every path below yields distinct keys except combine=false
     stream_chunks_ = 0;
     const bool streamed = shard.bytes > m.cap_bytes;
     const bool small_ordered = combine && cfg_.sort_path == SortPath::kDict && !streamed &&
@@ -47,24 +48,30 @@ class GpuShardEngine final : public ShardEngine {
       // sorted, with counts; one more kernel lays them out as shuffle records + SoA keys,
       // and the splitter samples and counters come back -- one captured graph, ONE host
       // synchronisation for either strategy.
+      // The gather plan needs no splitter samples (a mispredict samples late).
       m.check_input(shard);
       m.prepare_upload(shard);
       set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+      const bool spec_samples = plan != DistStrategy::kGather;
       auto enqueue = [&] {
         m.enqueue_upload_device(shard);
         m.enqueue_map(shard);
         m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
         launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
                              m.d_records, m.stream);
-        launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
-        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
-                                        hipMemcpyDeviceToHost, m.stream));
+        if (spec_samples) {
+          launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+          LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples,
+                                          kSpecSamples * sizeof(PackedKey),
+                                          hipMemcpyDeviceToHost, m.stream));
+        }
         LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters),
                                         hipMemcpyDeviceToHost, m.stream));
       };
       m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
       if (m.use_graph())
-        m.launch_cached({2, shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text),
+        m.launch_cached({spec_samples ? 2u : 3u, shard.bytes, shard.num_lines,
+                         reinterpret_cast<u64>(m.map_text),
                          (u64)m.upload_mode,
                          m.upload_mode == DevicePipeline::Upload::kDirect
                              ? reinterpret_cast<u64>(shard.data) : 0},
@@ -73,8 +80,10 @@ class GpuShardEngine final : public ShardEngine {
         enqueue();
       m.sync();
       if (!(m.h_ctr->flags & kCtrDictOverflow)) {
-        samples_.assign(m.h_small, m.h_small + kSpecSamples);
-        samples_valid_ = true;
+        if (spec_samples) {
+          samples_.assign(m.h_small, m.h_small + kSpecSamples);
+          samples_valid_ = true;
+        }
         return finish_map_stats(shard, m.h_ctr->num_unique);
       }
       // a partition overflowed its LDS table: redo this rank's combine on the HBM table
@@ -144,6 +153,7 @@ class GpuShardEngine final : public ShardEngine {
         set_local(m.heads, m.d_head_count, &m.d_ctr->num_unique);
       } else {
         set_local(m.sorted, nullptr, &m.d_ctr->num_records);
+        distinct_local_ = false;
       }
     }
     launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
@@ -243,19 +253,61 @@ class GpuShardEngine final : public ShardEngine {
 
   // The root's own combined records go behind the received ones; one dictionary pass over
   // all of them (partition tags come from the unpack) yields the merged, ranked output.
-  void reduce_gathered(const std::vector<u64>& run_lens, u64* total_count,
-                       u64* num_unique) override {
+  u32 record_flags() const override {
+    return (sorted_local_ ? kRecordsSorted : 0u) | (distinct_local_ ? kRecordsDistinct : 0u);
+  }
+
+  void reduce_gathered(const std::vector<u64>& run_lens, u64 total_tokens, u32 run_flags,
+                       u64* total_count, u64* num_unique) override {
     DevicePipeline& m = *mp_;
     DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
     u64 n_other = 0;
     for (u64 l : run_lens) n_other += l;
     LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
     const int nruns = (int)run_lens.size() + 1;
-    if (cfg_.sort_path == SortPath::kDict && sorted_local_ && nruns <= kMaxMergeRunsHost &&
-        n_other + local_count_ <= kPartBuildMaxTokens) {
-      // Every run is sorted: the merge kernel finds each partition's range in every run by
-      // binary search and writes the final records into host-mapped memory -- one kernel
-      // (plus the counter reset and the run table), captured as one graph.
+    const u64 n_all = n_other + local_count_;
+    const bool runs_sorted = (run_flags & kRecordsSorted) && sorted_local_;
+    if (runs_sorted && (run_flags & kRecordsDistinct) && nruns <= kMaxMergeRunsHost &&
+        n_all <= kMergeMaxRecords && total_tokens <= kMergeMaxCount) {
+      // Every run is sorted with distinct keys: merge by binary search (position in the
+      // merged order, first copy of each key sums the others) + one look-back scan that
+      // writes the final records into host-mapped memory -- two kernels, one graph.
+      u32* meta = reinterpret_cast<u32*>(r.h_u64);  // pinned; read at replay time
+      meta[0] = (u32)nruns;
+      meta[1] = (u32)local_count_;
+      for (int q = 1; q < nruns; ++q) meta[1 + q] = (u32)run_lens[(size_t)q - 1];
+      u32* d_meta = reinterpret_cast<u32*>(r.d_offsets);
+      KeyCount* merged = reinterpret_cast<KeyCount*>(r.d_out);  // >= cap records of scratch
+      r.grow_host_out(n_all);
+      auto enqueue = [&] {
+        LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, r.stream));
+        LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + (u64)nruns) * sizeof(u32),
+                                        hipMemcpyHostToDevice, r.stream));
+        launch_merge_sorted_runs(m.d_records, r.d_records, d_meta, r.cap, merged, r.d_ctr,
+                                 r.d_out_mapped, r.d_ctr_mapped, r.lb_scan, r.stream);
+      };
+      if (r.use_graph())
+        r.launch_cached({5, (u64)nruns, reinterpret_cast<u64>(m.d_records),
+                         reinterpret_cast<u64>(r.d_records),
+                         reinterpret_cast<u64>(r.d_out_mapped), 0},
+                        enqueue);
+      else
+        enqueue();
+      r.sync();
+      *r.h_ctr = *r.h_ctr_mapped;
+      WordCountResult tmp;
+      r.fill_counters(tmp);
+      r.copy_out(tmp.entries, r.h_ctr->num_unique);
+      *total_count = r.h_ctr->total_count;
+      *num_unique = r.h_ctr->num_unique;
+      range_entries_ = std::move(tmp.entries);
+      return;
+    }
+    if (cfg_.sort_path == SortPath::kDict && runs_sorted && nruns <= kMaxMergeRunsHost &&
+        n_all <= kPartBuildMaxTokens) {
+      // Sorted runs that may repeat a key (no map-side combine): the ordered dictionary
+      // kernel finds each partition's range in every run by binary search and aggregates
+      // it in LDS -- one kernel (plus the counter reset and the run table), one graph.
       u32* meta = reinterpret_cast<u32*>(r.h_u64);  // pinned; read at replay time
       meta[0] = (u32)nruns;
       meta[1] = (u32)local_count_;
@@ -348,6 +400,7 @@ class GpuShardEngine final : public ShardEngine {
   u64 local_count_ = 0;
   size_t stream_chunks_ = 0;  // > 0: the last shard streamed through in this many chunks
   bool sorted_local_ = true;  // d_records are sorted (shuffle-ready)
+  bool distinct_local_ = true;  // d_records hold every key once (map-side combine)
 };
 
 }  // namespace

@@ -121,8 +121,13 @@ class ShardEngine {
   // Gather strategy, root only: reduce this rank's own records together with the records
   // the other ranks sent (already in recv_records(), which holds room for both), back to
   // back in rank order; run_lens[i] = records from rank i+1 (each such run is sorted).
-  virtual void reduce_gathered(const std::vector<u64>& run_lens, u64* total_count,
-                               u64* num_unique) = 0;
+  // total_tokens: the sum of every run's counts (known from the map statistics);
+  // run_flags: the AND of every rank's record_flags().
+  virtual void reduce_gathered(const std::vector<u64>& run_lens, u64 total_tokens,
+                               u32 run_flags, u64* total_count, u64* num_unique) = 0;
+  // What this rank's send_records() are after map_local: kRecordsSorted | kRecordsDistinct.
+  virtual u32 record_flags() const { return 0; }
+  static constexpr u32 kRecordsSorted = 1, kRecordsDistinct = 2;
   // Strategy of the previous job (the driver's prediction for the next one under kAuto).
   DistStrategy last_strategy = DistStrategy::kShuffle;
   virtual void finalize(u64 global_offset, std::vector<WordCountEntry>* out) = 0;

@@ -90,6 +90,9 @@ class GpuWordCount {
   // Reduce steps over keys that are already sorted: boundary mark + head compaction +
   // adjacent difference (main.cu:161-238, 462) on the configured reduce path.
   WordCountResult reduce_sorted(const PackedKey* sorted, u64 n);
+  // Root merge of the gather strategy (launch_merge_sorted_runs) over host-made runs, each
+  // sorted with distinct keys: the merged (key, val, count) entries.
+  WordCountResult merge_runs(const std::vector<std::vector<KeyCount>>& runs);
 
   const JobConfig& config() const;
   u64 token_capacity() const;

@@ -205,6 +205,18 @@ constexpr int kMaxMergeRunsHost = 64;
 void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                             MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                             LookbackScratch lb, hipStream_t s);
+// ---------------- merge.hip ----------------
+// Merge of sorted runs (same run layout and meta as launch_dict_merge_runs) by lock-step
+// binary search + one look-back scan: `merged` (room for every record, bounded by `cap`)
+// is scratch; out / ctr / ctr_out as for launch_dict_ordered.  `lb` needs
+// div_up(cap, kReduceTile) zeroed status words and a zeroed tile counter.  Requires fewer
+// than 2^22 records and a total count below 2^40 (checked by the caller).
+void launch_merge_sorted_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
+                              u64 cap, KeyCount* merged, MapCounters* ctr, OutRecord* out,
+                              MapCounters* ctr_out, LookbackScratch lb, hipStream_t s);
+constexpr u64 kMergeMaxRecords = (1ull << 22) - 1;
+constexpr u64 kMergeMaxCount = (1ull << 40) - 1;
+
 // Hash every token (with its count; null = 1) into the table; distinct keys land in
 // ukeys[0 .. ctr->num_unique) with summed counts in ucount.
 void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, u64 cap,

@@ -1,0 +1,218 @@
+// Root merge of the gather strategy: P sorted runs of combined (key, count) records -> the
+// globally sorted (key, val, count) output, in two short kernels.
+//
+// The reference has no merge at all: its reducer expects one pre-sorted /tmp/out.txt
+// (main.cu:437-465, bug B7), and the cross-node transfer that would feed it is missing
+// (README.md:24).  Here every rank's combined output arrives sorted, so the root does not
+// rebuild a dictionary over them; it merges:
+//
+//   merge_rank   one thread per record: lock-step binary searches in every other run give
+//                the record's position in the stable (key, run) merge order, whether a
+//                lower run already holds the key (then this copy is a duplicate), and --
+//                for the first copy -- the key's total count over all runs.  Records are
+//                scattered to their merged slots (duplicates with count 0).
+//   merge_emit   decoupled look-back scan over the merged slots of (#first copies, count
+//                sum): the first copies are compacted into the output with val = the
+//                exclusive prefix of the counts (the reference's val: start index of the
+//                key's run in the globally sorted token array, main.cu:161-208).
+//
+// Runs are at most 64 (one per rank), the lock-step search keeps up to 8 runs' probes in
+// flight per thread, and the output goes straight into host-mapped memory.
+#include "locust/device/lookback.hpp"
+#include "locust/hip_check.hpp"
+#include "locust/kernels.hpp"
+
+namespace locust {
+namespace {
+
+constexpr int kMergeBlock = 256;
+constexpr int kMergeLanes = 8;                        // runs searched in lock step
+constexpr int kEmitItems = kReduceTile / kMergeBlock;  // 8 merged slots per thread
+constexpr int kEmitCountBits = 40;                     // look-back value: [firsts:22][counts:40]
+constexpr u64 kEmitCountMask = (1ull << kEmitCountBits) - 1;
+
+// -1 / 0 / +1: order of record key `a` against key `k` (unsigned words, big-endian bytes).
+__device__ __forceinline__ int cmp_key(const KeyCount* a, const u64* k) {
+  const u64 a0 = a->w[0];
+  if (a0 != k[0]) return a0 < k[0] ? -1 : 1;
+#pragma unroll
+  for (int j = 1; j < kKeyWords; ++j) {
+    const u64 aj = a->w[j];
+    if (aj != k[j]) return aj < k[j] ? -1 : 1;
+  }
+  return 0;
+}
+
+struct RunTable {
+  u32 nruns;
+  u32 off[kMaxMergeRunsHost + 1];  // start of run q in the concatenated index space
+};
+
+__device__ __forceinline__ void load_runs(const u32* __restrict__ meta, RunTable& t) {
+  if (threadIdx.x == 0) {
+    const u32 nr = min(meta[0], (u32)kMaxMergeRunsHost);
+    u32 acc = 0;
+    for (u32 q = 0; q < nr; ++q) {
+      t.off[q] = acc;
+      acc += meta[1 + q];
+    }
+    t.off[nr] = acc;
+    t.nruns = nr;
+  }
+  __syncthreads();
+}
+
+// Run q's records: run 0 is `own`, runs 1.. lie back to back in `recv`.
+__device__ __forceinline__ const KeyCount* run_ptr(const KeyCount* own, const KeyCount* recv,
+                                                   const RunTable& t, u32 q) {
+  return q == 0 ? own : recv + (t.off[q] - t.off[1]);
+}
+
+__global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
+    const KeyCount* __restrict__ own, const KeyCount* __restrict__ recv,
+    const u32* __restrict__ meta, KeyCount* __restrict__ merged) {
+  __shared__ RunTable t;
+  load_runs(meta, t);
+  const u32 nruns = t.nruns;
+  const u32 total = t.off[nruns];
+  for (u32 g = blockIdx.x * kMergeBlock + threadIdx.x; g < total; g += gridDim.x * kMergeBlock) {
+    u32 q = 0;
+    while (q + 1 < nruns && t.off[q + 1] <= g) ++q;
+    const u32 i = g - t.off[q];
+    const KeyCount rec = run_ptr(own, recv, t, q)[i];
+    const u64 k[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
+    u64 pos = i;
+    u64 count = rec.count;
+    bool first = true;
+    for (u32 r0 = 0; r0 < nruns; r0 += kMergeLanes) {
+      const KeyCount* base[kMergeLanes];
+      u32 lo[kMergeLanes], len[kMergeLanes];
+      bool eq[kMergeLanes];
+#pragma unroll
+      for (int l = 0; l < kMergeLanes; ++l) {
+        const u32 r = r0 + l;
+        const bool live = r < nruns && r != q;
+        base[l] = live ? run_ptr(own, recv, t, r) : own;
+        lo[l] = 0;
+        len[l] = live ? t.off[r + 1] - t.off[r] : 0;
+        eq[l] = false;
+      }
+      // lower_bound in every live run, one probe per run per step (independent loads)
+      for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int l = 0; l < kMergeLanes; ++l) {
+          if (len[l]) {
+            any = true;
+            const u32 half = len[l] >> 1;
+            const int c = cmp_key(base[l] + lo[l] + half, k);
+            if (c < 0) {
+              lo[l] += half + 1;
+              len[l] -= half + 1;
+            } else {
+              eq[l] |= c == 0;  // keys are distinct within a run: lower_bound lands here
+              len[l] = half;
+            }
+          }
+        }
+        if (!any) break;
+      }
+#pragma unroll
+      for (int l = 0; l < kMergeLanes; ++l) {
+        const u32 r = r0 + l;
+        if (r >= nruns || r == q) continue;
+        if (r < q) {
+          pos += lo[l] + (eq[l] ? 1 : 0);  // equal keys of lower runs come first
+          first &= !eq[l];
+        } else {
+          pos += lo[l];
+          if (eq[l]) count += base[l][lo[l]].count;
+        }
+      }
+    }
+    KeyCount out;
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) out.w[j] = k[j];
+    out.count = first ? count : 0;  // later copies of a key carry nothing
+    merged[pos] = out;
+  }
+}
+
+__global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
+    const KeyCount* __restrict__ merged, const u32* __restrict__ meta,
+    MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
+    MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr) {
+  __shared__ u64 s_scan[kMergeBlock / 64 + 1];
+  __shared__ u32 s_tile;
+  __shared__ u64 s_prefix;
+  __shared__ RunTable t;
+  const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
+  load_runs(meta, t);
+  const u32 total = t.off[t.nruns];
+  const u32 ntiles = total ? (u32)div_up(total, (u64)kReduceTile) : 1u;
+  if (tile >= ntiles) return;  // uniform per workgroup; nobody waits on these tiles
+  const u32 i0 = tile * kReduceTile + threadIdx.x * kEmitItems;
+  KeyCount v[kEmitItems];
+  u64 agg = 0;
+#pragma unroll
+  for (int e = 0; e < kEmitItems; ++e) {
+    const u32 i = i0 + e;
+    if (i < total) {
+      v[e] = merged[i];
+    } else {
+      v[e].count = 0;
+    }
+    if (v[e].count) agg += (1ull << kEmitCountBits) + v[e].count;
+  }
+  u64 tile_sum = 0;
+  const u64 excl = dev::block_exclusive_scan<u64, kMergeBlock>(agg, s_scan, &tile_sum);
+  const u64 before = dev::block_lookback(status, tile, tile_sum, &s_prefix);
+  const u64 at = before + excl;
+  u64 idx = at >> kEmitCountBits;
+  u64 val = at & kEmitCountMask;
+#pragma unroll
+  for (int e = 0; e < kEmitItems; ++e) {
+    if (!v[e].count) continue;
+    OutRecord o;
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) o.w[j] = v[e].w[j];
+    o.val = val;
+    o.count = v[e].count;
+    out[idx++] = o;
+    val += v[e].count;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    const u64 all = before + tile_sum;
+    const u32 u = (u32)(all >> kEmitCountBits);
+    const u64 tok = all & kEmitCountMask;
+    ctr->num_unique = u;
+    ctr->total_count = tok;
+    if (ctr_out) {
+      ctr_out->num_records = ctr->num_records;
+      ctr_out->num_unique = u;
+      ctr_out->overflow_lines = ctr->overflow_lines;
+      ctr_out->truncated = ctr->truncated;
+      ctr_out->num_newlines = ctr->num_newlines;
+      ctr_out->max_key_len = ctr->max_key_len;
+      ctr_out->total_count = tok;
+      ctr_out->flags = ctr->flags;
+    }
+  }
+}
+
+}  // namespace
+
+void launch_merge_sorted_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
+                              u64 cap, KeyCount* merged, MapCounters* ctr, OutRecord* out,
+                              MapCounters* ctr_out, LookbackScratch lb, hipStream_t s) {
+  const u64 c = cap ? cap : 1;
+  const u32 rank_grid = (u32)std::min<u64>(div_up(c, kMergeBlock), 4096);
+  merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(own, recv, meta, merged);
+  LOCUST_HIP_LAUNCH_CHECK();
+  const u32 emit_grid = (u32)div_up(c, (u64)kReduceTile);
+  merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, meta, ctr, out, ctr_out,
+                                                                  lb.status, lb.tile_counter);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace locust

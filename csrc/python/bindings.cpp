@@ -123,6 +123,20 @@ class PyGpuEngine {
     py::gil_scoped_release nogil;
     return PyResult{eng_.reduce_sorted(toks.data(), toks.size())};
   }
+  // runs: lists of (key bytes, count), each sorted with distinct keys.
+  PyResult merge_runs(const std::vector<std::vector<std::pair<std::string, u64>>>& runs) {
+    std::vector<std::vector<KeyCount>> rr(runs.size());
+    for (size_t q = 0; q < runs.size(); ++q)
+      for (const auto& kc : runs[q]) {
+        KeyCount rec;
+        const PackedKey k = to_key(kc.first);
+        for (int w = 0; w < kKeyWords; ++w) rec.w[w] = k.w[w];
+        rec.count = kc.second;
+        rr[q].push_back(rec);
+      }
+    py::gil_scoped_release nogil;
+    return PyResult{eng_.merge_runs(rr)};
+  }
   u64 capacity() const { return eng_.token_capacity(); }
   // Stage the text in the engine's pinned buffer once; run_loaded() then skips the copy.
   void load(const std::string& text) {
@@ -364,6 +378,7 @@ PYBIND11_MODULE(_locust, m) {
       .def("sort_keys", &PyGpuEngine::sort_keys)
       .def("compact_slots", &PyGpuEngine::compact_slots)
       .def("reduce_sorted", &PyGpuEngine::reduce_sorted)
+      .def("merge_runs", &PyGpuEngine::merge_runs)
       .def_property_readonly("capacity", &PyGpuEngine::capacity);
 
   m.def("cpu_run", [](const JobConfig& cfg, const std::string& text) {

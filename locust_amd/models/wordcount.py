@@ -61,6 +61,11 @@ class Engine:
         """Boundary mark + head compaction + adjacent difference over sorted keys."""
         return self._eng.reduce_sorted(keys)
 
+    def merge_runs(self, runs: list[list[tuple[bytes, int]]]):
+        """Root merge of the gather strategy: runs of (key, count), each sorted with
+        distinct keys -> merged (key, val, count) entries."""
+        return self._eng.merge_runs(runs)
+
 
 def wordcount_text(text: bytes, backend: str = "gpu", cfg=None, **kw):
     cfg = cfg if cfg is not None else make_config(backend, **kw)

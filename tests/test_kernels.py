@@ -98,3 +98,52 @@ def test_radix_sort_ten_million():
     # the permutation is a stable one: equal keys keep input order
     assert all(keys[a] < keys[b] or (keys[a] == keys[b] and a < b)
                for a, b in zip(perm[:200000], perm[1:200001]))
+
+
+def merge_reference(runs):
+    """Python reference of the root merge: sum counts per key over all runs, sort, and
+    val = total count of the smaller keys."""
+    tot = {}
+    for run in runs:
+        for k, c in run:
+            tot[k] = tot.get(k, 0) + c
+    out, at = [], 0
+    for k in sorted(tot):
+        out.append((k, at, tot[k]))
+        at += tot[k]
+    return out
+
+
+def _random_runs(rng, nruns, vocab, per_run):
+    # keys sharing 8- and 16-byte prefixes exercise the later key words of the compare
+    words = ([b"w%d" % i for i in range(vocab // 2)] +
+             [b"abcdefgh%05d" % i for i in range(vocab // 4)] +
+             [b"abcdefghijklmnop%03d" % i for i in range(vocab - vocab // 2 - vocab // 4)])
+    runs = []
+    for _ in range(nruns):
+        n = rng.randint(0, per_run)
+        ks = sorted(rng.sample(words, min(n, len(words))))
+        runs.append([(k, rng.randint(1, 1000)) for k in ks])
+    return runs
+
+
+@pytest.mark.parametrize("nruns,vocab,per_run", [(1, 50, 50), (2, 100, 80), (3, 5000, 4000),
+                                                 (8, 8000, 5608), (9, 3000, 3000),
+                                                 (17, 2000, 300), (64, 400, 100)])
+def test_merge_sorted_runs(nruns, vocab, per_run):
+    """Gather-strategy root merge (lock-step binary search + look-back scan) against the
+    Python reference: overlapping, disjoint and empty runs, up to 64 runs, > 1 scan tile."""
+    rng = random.Random(nruns * 1000 + vocab)
+    runs = _random_runs(rng, nruns, vocab, per_run)
+    eng = lc.Engine(lc.make_config("gpu"), 1 << 20, 1 << 16)
+    res = eng.merge_runs(runs)
+    want = merge_reference(runs)
+    assert res.entries() == want
+    assert res.num_unique == len(want)
+    assert res.num_tokens == sum(c for run in runs for _, c in run)
+
+
+def test_merge_sorted_runs_empty():
+    eng = lc.Engine(lc.make_config("gpu"), 1 << 16, 1 << 10)
+    res = eng.merge_runs([[], []])
+    assert res.entries() == [] and res.num_unique == 0
