@@ -92,6 +92,31 @@ class LoopbackComm final : public Communicator {
 
   void barrier() override { st_->barrier(); }
 
+  // Blocking rehearsal of the stream-ordered all-gather: the send data must be complete
+  // before a peer pulls it, and no rank may overwrite its send buffer before every pull
+  // finished -- hence a stream sync before and a barrier after.
+  void allgather_device(const void* send, void* recv, u64 bytes, void* stream) override {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+    st_->ptr[(size_t)rank_] = send;
+    st_->barrier();
+    char* out = static_cast<char*>(recv);
+    for (int r = 0; r < size(); ++r) {
+      if (!bytes) break;
+      if (st_->device)
+        LOCUST_HIP_CHECK(hipMemcpyAsync(out + (u64)r * bytes, st_->ptr[(size_t)r], bytes,
+                                        hipMemcpyDefault, s));
+      else
+        std::memcpy(out + (u64)r * bytes, st_->ptr[(size_t)r], bytes);
+    }
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+    st_->barrier();
+  }
+
+  void sync_stream(void* stream) override {
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  }
+
   void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
                  const u64* recv_bytes, const u64* recv_off, void* stream) override {
     st_->ptr[(size_t)rank_] = send;

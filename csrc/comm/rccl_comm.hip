@@ -125,6 +125,15 @@ class RcclComm final : public Communicator {
     allgather_host(&v, all.data(), sizeof(int));
   }
 
+  void allgather_device(const void* send, void* recv, u64 bytes, void* stream) override {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
+    LOCUST_RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
+  }
+
+  void sync_stream(void* stream) override {
+    wait(stream ? static_cast<hipStream_t>(stream) : stream_);
+  }
+
   void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
                  const u64* recv_bytes, const u64* recv_off, void* stream) override {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;

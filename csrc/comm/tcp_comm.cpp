@@ -33,6 +33,15 @@ int Communicator::agree(int local_error) {
   return -1;
 }
 
+void Communicator::allgather_device(const void*, void*, u64, void*) {
+  throw Error(std::string("allgather_device: the ") + name() +
+              " communicator has no device data plane");
+}
+
+void Communicator::sync_stream(void*) {
+  throw Error(std::string("sync_stream: the ") + name() + " communicator has no device streams");
+}
+
 void Communicator::gatherv_known(const void* send, u64 bytes, const u64* sizes,
                                  void* recv_at_root, int root) {
   std::vector<char> buf;

@@ -156,7 +156,93 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
                             : cfg.strategy == DistStrategy::kAuto ? eng.last_strategy
                                                                   : cfg.strategy;
   TraceRange tr_job("locust:dist_job");
-  const i32 st1 = local("map", [&] {
+  WordCountResult& r = res.result;
+
+  // ---------------- gather strategy in ONE all-gather (predicted gather) ----------------
+  // map (+ slot header on the device) -> all-gather of fixed-size slots -> root merge, all
+  // enqueued on the engine's stream behind each other: one host synchronisation per job.
+  // Every rank sees every header, so the decisions below (failure, fallback, next slot
+  // size) are identical everywhere without another collective.
+  bool mapped = false;
+  i32 st_slot = 0;
+  const bool slot_path = plan == DistStrategy::kGather && cfg.gather && cfg.job.combine &&
+                         cfg.strategy != DistStrategy::kShuffle && P <= kMaxSlotRanks &&
+                         comm.device_buffers() && eng.device_buffers();
+  if (slot_path) {
+    TraceRange tr("locust:slot_gather");
+    const u32 slot_recs = eng.slot_records ? eng.slot_records : kSlotRecordsMin;
+    void* send = nullptr;
+    st_slot = local("map", [&] { send = eng.enqueue_map_slot(shard, slot_recs); });
+    if (st_slot) send = eng.write_slot_failure();  // the all-gather must still be entered
+    void* recv = eng.slot_buffer((u32)P, slot_recs);
+    const u64 slot_bytes = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
+    comm.allgather_device(send, recv, slot_bytes, eng.stream());
+    if (me == 0) eng.enqueue_merge_slots((u32)P, slot_recs);
+    eng.enqueue_slot_headers((u32)P, slot_recs);
+    comm.sync_stream(eng.stream());
+    const SlotHeader* hd = eng.slot_headers();
+    for (int p = 0; p < P; ++p)
+      if (hd[p].status == kSlotFailed)
+        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
+                    std::to_string(p) + (p == me ? ": " + local_msg : ""));
+    u64 sum = 0, max_n = 0, min_cap = ~0ull;
+    bool fallback = false;
+    for (int p = 0; p < P; ++p) {
+      sum += hd[p].n;
+      max_n = std::max(max_n, hd[p].n);
+      min_cap = std::min(min_cap, hd[p].slot_cap);
+      fallback |= hd[p].status != kSlotOk || hd[p].n > slot_recs;
+    }
+    // next job's slot: the largest rank's records + 25%, within every rank's send buffer
+    const u64 want = align_up(max_n + max_n / 4 + 1, 1024);
+    eng.slot_records = (u32)std::max<u64>(kSlotRecordsMin, std::min<u64>(want, min_cap));
+    fallback |= cfg.strategy == DistStrategy::kAuto && sum > cfg.gather_max_records;
+    st_slot = local("map", [&] {
+      n_local = eng.complete_map_slot(shard);
+      eng.map_stats(&local_stats);
+    });
+    if (!fallback) {
+      if (st_slot)
+        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
+                    std::to_string(me) + ": " + local_msg);
+      for (int p = 0; p < P; ++p) {
+        r.num_lines += hd[p].lines;
+        r.num_tokens += hd[p].tokens;
+        r.overflow_lines += hd[p].overflow_lines;
+        r.truncated += hd[p].truncated;
+        r.max_key_len = std::max<u64>(r.max_key_len, hd[p].max_key_len);
+      }
+      res.strategy = DistStrategy::kGather;
+      eng.last_strategy = DistStrategy::kGather;
+      res.local_records = n_local;
+      const u64 t1 = now_ns();
+      if (me == 0) {
+        u64 total = 0, uniq = 0;
+        if (local("reduce", [&] { eng.finish_merge_slots(&total, &uniq); }))
+          throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
+        eng.finalize(0, &r.entries);
+        res.range_tokens = total;
+        res.range_unique = uniq;
+      } else {
+        res.sent_bytes = slot_bytes * (u64)(P - 1);  // every peer receives this rank's slot
+        res.recv_bytes = slot_bytes * (u64)(P - 1);
+      }
+      r.num_unique = r.entries.size();
+      const u64 t2 = now_ns();
+      res.map_ms = (t1 - t0) * 1e-6;  // map + all-gather + merge, one synchronisation
+      res.reduce_ms = (t2 - t1) * 1e-6;
+      res.total_ms = (t2 - t0) * 1e-6;
+      r.times.map_ms = res.map_ms;
+      r.times.reduce_ms = res.reduce_ms;
+      r.times.wall_ms = res.total_ms;
+      return res;
+    }
+    // A rank needs a local redo, a slot overflowed or the records are too many for the
+    // root: every rank continues on the standard path with its map already done.
+    mapped = true;
+  }
+
+  const i32 st1 = mapped ? st_slot : local("map", [&] {
     TraceRange tr("locust:map");
     n_local = eng.map_local(shard, cfg.job.combine, plan);
     if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
@@ -182,7 +268,6 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   std::vector<u64> counts((size_t)P);
   u64 sum_records = 0;
   u32 run_flags = ~0u;
-  WordCountResult& r = res.result;
   for (int p = 0; p < P; ++p) {
     const char* base = all1.data() + (u64)p * m1;
     Msg1 h;

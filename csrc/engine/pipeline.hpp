@@ -78,6 +78,8 @@ struct DevicePipeline {
   bool parts_ready = false;        // d_parts describes the current `tokens`
   OutRecord* d_out = nullptr;
   KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
+  // Records d_records holds (>= cap; at least one minimum-size gather slot).
+  u64 slot_records_cap() const { return std::max<u64>(cap, kSlotRecordsMin); }
   PackedKey* d_samples = nullptr;
   PackedKey* d_splitters = nullptr;
   u64* d_offsets = nullptr;
@@ -181,7 +183,7 @@ struct DevicePipeline {
     sz.add<u32>(cap);
     sz.add<u8>(align_up(cap, 16) + 16);
     sz.add<OutRecord>(cap);
-    sz.add<KeyCount>(cap);
+    sz.add<KeyCount>(slot_records_cap() + kSlotHeaderRecords);
     sz.add<PackedKey>(kMaxSamples);
     sz.add<PackedKey>(kMaxRanks);
     sz.add<u64>(kMaxRanks + 1);
@@ -217,7 +219,8 @@ struct DevicePipeline {
     d_perm = arena.take<u32>(cap);
     d_parts = arena.take<u8>(align_up(cap, 16) + 16);
     d_out = arena.take<OutRecord>(cap);
-    d_records = arena.take<KeyCount>(cap);
+    // room for a gather slot header in front: d_records - kSlotHeaderRecords is the slot
+    d_records = arena.take<KeyCount>(slot_records_cap() + kSlotHeaderRecords) + kSlotHeaderRecords;
     d_samples = arena.take<PackedKey>(kMaxSamples);
     d_splitters = arena.take<PackedKey>(kMaxRanks);
     d_offsets = arena.take<u64>(kMaxRanks + 1);

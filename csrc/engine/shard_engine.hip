@@ -19,6 +19,12 @@ class GpuShardEngine final : public ShardEngine {
   GpuShardEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
       : cfg_(cfg), mp_(new DevicePipeline(cfg, max_bytes, max_lines)) {}
 
+  ~GpuShardEngine() override {
+    if (mp_) (void)hipStreamSynchronize(mp_->stream);  // pending copies from the pinned headers
+    if (h_headers_) (void)hipHostFree(h_headers_);
+    if (h_send_header_) (void)hipHostFree(h_send_header_);
+  }
+
   bool device_buffers() const override { return true; }
   void* stream() override { return mp_->stream; }
   char* input_buffer() override { return mp_->h_text; }
@@ -44,67 +50,9 @@ class GpuShardEngine final : public ShardEngine {
       m.enqueue_map(shard);
     }
     if (small_ordered) {
-      // Small pass: upload, map and the ordered kernel give this rank's distinct keys
-      // sorted, with counts; one more kernel lays them out as shuffle records + SoA keys,
-      // and the splitter samples and counters come back -- one captured graph, ONE host
-      // synchronisation for either strategy.
-      // The gather plan needs no splitter samples (a mispredict samples late).
-      m.check_input(shard);
-      m.prepare_upload(shard);
-      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
-      const bool spec_samples = plan != DistStrategy::kGather;
-      auto enqueue = [&] {
-        m.enqueue_upload_device(shard);
-        m.enqueue_map(shard);
-        m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
-        launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
-                             m.d_records, m.stream);
-        if (spec_samples) {
-          launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
-          LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples,
-                                          kSpecSamples * sizeof(PackedKey),
-                                          hipMemcpyDeviceToHost, m.stream));
-        }
-        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters),
-                                        hipMemcpyDeviceToHost, m.stream));
-      };
-      m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
-      if (m.use_graph())
-        m.launch_cached({spec_samples ? 2u : 3u, shard.bytes, shard.num_lines,
-                         reinterpret_cast<u64>(m.map_text),
-                         (u64)m.upload_mode,
-                         m.upload_mode == DevicePipeline::Upload::kDirect
-                             ? reinterpret_cast<u64>(shard.data) : 0},
-                        enqueue);
-      else
-        enqueue();
+      enqueue_small_ordered(shard, plan != DistStrategy::kGather, nullptr, 0);
       m.sync();
-      if (!(m.h_ctr->flags & kCtrDictOverflow)) {
-        if (spec_samples) {
-          samples_.assign(m.h_small, m.h_small + kSpecSamples);
-          samples_valid_ = true;
-        }
-        return finish_map_stats(shard, m.h_ctr->num_unique);
-      }
-      // a partition overflowed its LDS table: redo this rank's combine on the HBM table
-      LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->num_unique, 0, sizeof(u32), m.stream));
-      LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->flags, 0, sizeof(u32), m.stream));
-      LOCUST_HIP_CHECK(hipMemsetAsync(m.dict.table, 0, m.dict_zero_bytes, m.stream));
-      launch_dict_insert(m.tokens, nullptr, &m.d_ctr->num_records, m.cap, m.dict, m.d_ctr,
-                         m.stream);
-      m.read_counters();
-      if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
-      if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
-        m.enqueue_rank();
-        m.enqueue_sorted_from_dict();
-      } else {
-        radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
-                   m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
-      }
-      set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
-      launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
-      m.read_counters();
-      return finish_map_stats(shard, m.h_ctr->num_unique);
+      return complete_small_ordered(shard);
     }
     if (combine && cfg_.sort_path == SortPath::kDict) {
       if (plan == DistStrategy::kGather) {
@@ -159,6 +107,186 @@ class GpuShardEngine final : public ShardEngine {
     launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
     m.read_counters();
     return finish_map_stats(shard, combine ? m.h_ctr->num_unique : m.h_ctr->num_records);
+  }
+
+  // Small pass: upload, map and the ordered kernel give this rank's distinct keys sorted,
+  // with counts; one more kernel lays them out as shuffle records + SoA keys (and, with
+  // `hdr`, the gather slot's header), optionally the splitter samples, and the counters
+  // come back -- one captured graph.  The gather plan needs no samples (a mispredict
+  // samples late).
+  bool small_ordered_ok(const TextInput& shard, bool combine) const {
+    const DevicePipeline& m = *mp_;
+    return combine && cfg_.sort_path == SortPath::kDict && shard.bytes <= m.cap_bytes &&
+           cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
+  }
+  void enqueue_small_ordered(const TextInput& shard, bool spec_samples, SlotHeader* hdr,
+                             u32 slot_recs) {
+    DevicePipeline& m = *mp_;
+    m.check_input(shard);
+    m.prepare_upload(shard);
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    spec_samples_ = spec_samples;
+    SlotHeader tmpl{};
+    tmpl.status = kSlotOk;
+    tmpl.record_flags = kRecordsSorted | kRecordsDistinct;
+    tmpl.lines = shard.num_lines;
+    tmpl.slot_cap = slot_capacity();
+    auto enqueue = [&] {
+      m.enqueue_upload_device(shard);
+      m.enqueue_map(shard);
+      m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
+      launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
+                           m.d_records, m.stream, hdr, m.d_ctr, tmpl);
+      if (spec_samples) {
+        launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+        LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                        hipMemcpyDeviceToHost, m.stream));
+      }
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters),
+                                      hipMemcpyDeviceToHost, m.stream));
+    };
+    m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
+    if (m.use_graph())
+      m.launch_cached({(spec_samples ? 2u : 3u) | (hdr ? 0x100u : 0u) | ((u64)slot_recs << 32),
+                       shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text),
+                       (u64)m.upload_mode,
+                       m.upload_mode == DevicePipeline::Upload::kDirect
+                           ? reinterpret_cast<u64>(shard.data) : 0},
+                      enqueue);
+    else
+      enqueue();
+  }
+  // After the sync of an enqueue_small_ordered: the map statistics, or the local redo on
+  // the HBM table when a partition overflowed its LDS table.
+  u64 complete_small_ordered(const TextInput& shard) {
+    DevicePipeline& m = *mp_;
+    if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+      if (spec_samples_) {
+        samples_.assign(m.h_small, m.h_small + kSpecSamples);
+        samples_valid_ = true;
+      }
+      return finish_map_stats(shard, m.h_ctr->num_unique);
+    }
+    LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->num_unique, 0, sizeof(u32), m.stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->flags, 0, sizeof(u32), m.stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(m.dict.table, 0, m.dict_zero_bytes, m.stream));
+    launch_dict_insert(m.tokens, nullptr, &m.d_ctr->num_records, m.cap, m.dict, m.d_ctr,
+                       m.stream);
+    m.read_counters();
+    if (m.h_ctr->flags & kCtrDictOverflow) return map_overflow_fallback(shard);
+    if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
+      m.enqueue_rank();
+      m.enqueue_sorted_from_dict();
+    } else {
+      radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                 m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+    }
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.read_counters();
+    return finish_map_stats(shard, m.h_ctr->num_unique);
+  }
+
+  // ---- gather strategy in one all-gather (ShardEngine::enqueue_map_slot and friends) ----
+  u64 slot_capacity() const override { return mp_->slot_records_cap(); }
+
+  void* enqueue_map_slot(const TextInput& shard, u32 slot_recs) override {
+    DevicePipeline& m = *mp_;
+    LOCUST_CHECK_ARG(slot_recs <= m.slot_records_cap(), "slot larger than the send buffer");
+    SlotHeader* hdr = reinterpret_cast<SlotHeader*>(m.d_records - kSlotHeaderRecords);
+    slot_fast_ = small_ordered_ok(shard, true);
+    if (slot_fast_) {
+      samples_valid_ = false;
+      sorted_local_ = true;
+      distinct_local_ = true;
+      stream_chunks_ = 0;
+      enqueue_small_ordered(shard, false, hdr, slot_recs);
+      return hdr;
+    }
+    // Not a small pass: map synchronously (sorted, combined records), header from the host.
+    const u64 n = map_local(shard, true, DistStrategy::kShuffle);
+    SlotHeader* h = slot_host_header();
+    *h = SlotHeader{};
+    h->status = (sorted_local_ && distinct_local_ && n <= slot_recs) ? kSlotOk : kSlotRedo;
+    h->record_flags = record_flags();
+    h->n = n;
+    h->lines = local_stats_.num_lines;
+    h->tokens = local_stats_.num_tokens;
+    h->overflow_lines = local_stats_.overflow_lines;
+    h->truncated = local_stats_.truncated;
+    h->max_key_len = local_stats_.max_key_len;
+    h->slot_cap = slot_capacity();
+    LOCUST_HIP_CHECK(hipMemcpyAsync(hdr, h, sizeof(SlotHeader), hipMemcpyHostToDevice, m.stream));
+    return hdr;
+  }
+
+  void* write_slot_failure() override {
+    DevicePipeline& m = *mp_;
+    SlotHeader* h = slot_host_header();
+    *h = SlotHeader{};
+    h->status = kSlotFailed;
+    h->slot_cap = slot_capacity();
+    LOCUST_HIP_CHECK(hipMemcpyAsync(m.d_records - kSlotHeaderRecords, h, sizeof(SlotHeader),
+                                    hipMemcpyHostToDevice, m.stream));
+    slot_fast_ = false;
+    local_count_ = 0;
+    return m.d_records - kSlotHeaderRecords;
+  }
+
+  void* slot_buffer(u32 nslots, u32 slot_recs) override {
+    // rp_ holds the slots in d_records; its d_out (48-B records) is the merge scratch.
+    return recv_records((u64)nslots * (kSlotHeaderRecords + slot_recs));
+  }
+
+  void enqueue_merge_slots(u32 nslots, u32 slot_recs) override {
+    DevicePipeline& m = *mp_;
+    DevicePipeline& r = *rp_;
+    LOCUST_CHECK_ARG(nslots <= (u32)kMaxMergeRunsHost, "too many slots to merge");
+    r.grow_host_out((u64)nslots * slot_recs);
+    // on the engine's stream, behind the all-gather
+    auto enqueue = [&] {
+      LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, m.stream));
+      launch_merge_slots(r.d_records, nslots, slot_recs, reinterpret_cast<KeyCount*>(r.d_out),
+                         r.d_ctr, r.d_out_mapped, r.d_ctr_mapped, r.lb_scan, m.stream);
+    };
+    if (m.use_graph())
+      m.launch_cached({6, ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(r.d_records),
+                       reinterpret_cast<u64>(r.d_out_mapped),
+                       reinterpret_cast<u64>(r.d_ctr_mapped), 0},
+                      enqueue);
+    else
+      enqueue();
+  }
+
+  void enqueue_slot_headers(u32 nslots, u32 slot_recs) override {
+    DevicePipeline& m = *mp_;
+    if (h_headers_cap_ < nslots) {
+      if (h_headers_) LOCUST_HIP_CHECK(hipHostFree(h_headers_));
+      h_headers_cap_ = std::max<u32>(nslots, 64);
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_headers_, h_headers_cap_ * sizeof(SlotHeader),
+                                     hipHostMallocDefault));
+    }
+    const u64 pitch = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
+    LOCUST_HIP_CHECK(hipMemcpy2DAsync(h_headers_, sizeof(SlotHeader), rp_->d_records, pitch,
+                                      sizeof(SlotHeader), nslots, hipMemcpyDeviceToHost,
+                                      m.stream));
+  }
+  const SlotHeader* slot_headers() const override { return h_headers_; }
+
+  u64 complete_map_slot(const TextInput& shard) override {
+    if (!slot_fast_) return local_count_;  // mapped synchronously (or failed) already
+    return complete_small_ordered(shard);
+  }
+
+  void finish_merge_slots(u64* total_count, u64* num_unique) override {
+    DevicePipeline& r = *rp_;
+    *r.h_ctr = *r.h_ctr_mapped;
+    WordCountResult tmp;
+    r.fill_counters(tmp);
+    r.copy_out(tmp.entries, r.h_ctr->num_unique);
+    *total_count = r.h_ctr->total_count;
+    *num_unique = r.h_ctr->num_unique;
+    range_entries_ = std::move(tmp.entries);
   }
 
   // Shuffle after a gather-planned map: sort the dictionary's keys, repack, resample.
@@ -401,6 +529,16 @@ class GpuShardEngine final : public ShardEngine {
   size_t stream_chunks_ = 0;  // > 0: the last shard streamed through in this many chunks
   bool sorted_local_ = true;  // d_records are sorted (shuffle-ready)
   bool distinct_local_ = true;  // d_records hold every key once (map-side combine)
+  bool spec_samples_ = false;   // the last small pass produced splitter samples
+  bool slot_fast_ = false;      // enqueue_map_slot took the one-graph small pass
+  SlotHeader* h_headers_ = nullptr;  // pinned copies of the all-gathered slot headers
+  u32 h_headers_cap_ = 0;
+  SlotHeader* h_send_header_ = nullptr;  // pinned staging for a host-written header
+  SlotHeader* slot_host_header() {
+    if (!h_send_header_)
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_send_header_, sizeof(SlotHeader), hipHostMallocDefault));
+    return h_send_header_;
+  }
 };
 
 }  // namespace

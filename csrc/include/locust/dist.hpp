@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "locust/engine.hpp"
+#include "locust/slot.hpp"
 
 namespace locust {
 
@@ -62,6 +63,14 @@ class Communicator {
   // Blocking: returns when this rank's receives are complete and its sends may be reused.
   virtual void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
                          const u64* recv_bytes, const u64* recv_off, void* stream) = 0;
+
+  // Stream-ordered all-gather of device buffers (device_buffers() communicators): rank
+  // r's `bytes` land at recv + r * bytes.  Enqueued on `stream` behind the work that
+  // produces `send`, so no host synchronisation is needed first; complete after
+  // sync_stream(stream).  Host-only communicators throw.
+  virtual void allgather_device(const void* send, void* recv, u64 bytes, void* stream);
+  // Wait for `stream`, watching for communicator errors (timeouts abort the communicator).
+  virtual void sync_stream(void* stream);
 
   // Status agreement: every rank contributes `local_error` (0 = ok); returns the lowest
   // failing rank or -1.  One allgather of 4 bytes per rank.
@@ -130,6 +139,33 @@ class ShardEngine {
   static constexpr u32 kRecordsSorted = 1, kRecordsDistinct = 2;
   // Strategy of the previous job (the driver's prediction for the next one under kAuto).
   DistStrategy last_strategy = DistStrategy::kShuffle;
+
+  // ---- gather strategy in ONE all-gather of fixed-size slots (device engines) ----
+  // Slot = SlotHeader (two records) + slot_records KeyCount records.  The map writes the
+  // header on the device, the slots are all-gathered right behind it on the engine's
+  // stream, and the root merges them straight from the receive buffer: one host
+  // synchronisation per job.  Every slot_* call is made by every rank in the same order.
+  // Enqueue this rank's map and its slot; returns the device send slot.  A shard the fast
+  // path cannot take is mapped synchronously and its header written from the host.
+  virtual void* enqueue_map_slot(const TextInput& shard, u32 slot_records) { return nullptr; }
+  // After a host-side failure: this rank's slot says so (status kSlotFailed, no records);
+  // returns the send slot.
+  virtual void* write_slot_failure() { return nullptr; }
+  // Device receive buffer for `nslots` slots.
+  virtual void* slot_buffer(u32 nslots, u32 slot_records) { return nullptr; }
+  // Root: enqueue the merge of the received slots (output lands in host memory).
+  virtual void enqueue_merge_slots(u32 nslots, u32 slot_records) {}
+  // Enqueue the copy of every slot's header to host memory; read after the sync.
+  virtual void enqueue_slot_headers(u32 nslots, u32 slot_records) {}
+  virtual const SlotHeader* slot_headers() const { return nullptr; }
+  // After the sync: finish this rank's map (local redo after an LDS overflow); returns the
+  // number of local records (as map_local does).
+  virtual u64 complete_map_slot(const TextInput& shard) { return 0; }
+  // Root, after the sync: the merged output (as reduce_gathered).
+  virtual void finish_merge_slots(u64* total_count, u64* num_unique) {}
+  // Records a slot can hold on this rank (the all-gather uses the minimum over ranks).
+  virtual u64 slot_capacity() const { return 0; }
+  u32 slot_records = 0;  // agreed slot size for the next job (0: kSlotRecordsMin)
   virtual void finalize(u64 global_offset, std::vector<WordCountEntry>* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;

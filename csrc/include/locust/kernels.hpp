@@ -12,6 +12,7 @@
 #include "locust/dstring.hpp"
 #include "locust/engine.hpp"
 #include "locust/kv.hpp"
+#include "locust/slot.hpp"
 
 namespace locust {
 
@@ -201,7 +202,7 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
 // Same, over runs of KeyCount records each sorted by key (the gather strategy's per-rank
 // combined outputs); duplicates across runs are summed.  Run 0 is `own`, runs 1.. lie
 // back to back in `recv`; `meta` (device) = [nruns <= 64, len_0, len_1, ...].
-constexpr int kMaxMergeRunsHost = 64;
+constexpr int kMaxMergeRunsHost = kMaxSlotRanks;
 void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                             MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                             LookbackScratch lb, hipStream_t s);
@@ -214,6 +215,12 @@ void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32
 void launch_merge_sorted_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                               u64 cap, KeyCount* merged, MapCounters* ctr, OutRecord* out,
                               MapCounters* ctr_out, LookbackScratch lb, hipStream_t s);
+// Same over the all-gathered slots: `nslots` slots of kSlotHeaderRecords + slot_records
+// records each, run q = slot q's records, its length min(header.n, slot_records) (0 when
+// the header's status is not kSlotOk).  `merged` needs nslots * slot_records records.
+void launch_merge_slots(const KeyCount* slots, u32 nslots, u32 slot_records, KeyCount* merged,
+                        MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                        LookbackScratch lb, hipStream_t s);
 constexpr u64 kMergeMaxRecords = (1ull << 22) - 1;
 constexpr u64 kMergeMaxCount = (1ull << 40) - 1;
 
@@ -241,11 +248,15 @@ void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounte
 // SoA keys (+ counts, null = 1) -> AoS KeyCount records (the all-to-all payload).
 void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u64 cap,
                          KeyCount* out, hipStream_t s);
-// AoS KeyCount -> SoA keys + counts; sets ctr->num_records = n (host-known).
-// Sorted OutRecords -> SoA sorted keys + counts and KeyCount shuffle records.
+
+// Sorted OutRecords -> SoA sorted keys + counts and KeyCount shuffle records.  With `hdr`,
+// also the slot header: `tmpl` (host-known fields) completed from `ctr` and n = *d_n
+// (status kSlotRedo on a dictionary overflow).
 void launch_out_to_sorted(const OutRecord* in, const u32* d_n, u64 cap, KeysSoA sorted,
-                          u64* counts, KeyCount* recs, hipStream_t s);
-// (parts, optional: partition tag per record for the partitioned dictionary builds)
+                          u64* counts, KeyCount* recs, hipStream_t s, SlotHeader* hdr = nullptr,
+                          const MapCounters* ctr = nullptr, const SlotHeader& tmpl = {});
+// AoS KeyCount -> SoA keys + counts (+ parts, optional: partition tag per record for the
+// partitioned dictionary builds).
 void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,
                            hipStream_t s);
 // S evenly spaced keys of a sorted array of *d_n keys: sample[k] = keys[floor((k+0.5)*n/S)].

@@ -43,43 +43,65 @@ __device__ __forceinline__ int cmp_key(const KeyCount* a, const u64* k) {
   return 0;
 }
 
+// Where the runs are: packed (run 0 = `own`, runs 1.. back to back in `recv`, lengths in
+// `meta` = [nruns, len0, len1, ...]) or all-gathered slots (fixed stride, a SlotHeader in
+// front of each slot's records).  Read from device memory at run time, so a captured graph
+// stays valid when the lengths change.
+struct RunsView {
+  const KeyCount* own;
+  const KeyCount* recv;
+  const u32* meta;
+  const KeyCount* slots;  // non-null: slot layout
+  u32 nslots, slot_records;
+};
+
 struct RunTable {
   u32 nruns;
   u32 off[kMaxMergeRunsHost + 1];  // start of run q in the concatenated index space
+  const KeyCount* base[kMaxMergeRunsHost];
 };
 
-__device__ __forceinline__ void load_runs(const u32* __restrict__ meta, RunTable& t) {
+__device__ __forceinline__ void load_runs(const RunsView& v, RunTable& t) {
   if (threadIdx.x == 0) {
-    const u32 nr = min(meta[0], (u32)kMaxMergeRunsHost);
     u32 acc = 0;
-    for (u32 q = 0; q < nr; ++q) {
-      t.off[q] = acc;
-      acc += meta[1 + q];
+    if (v.slots) {
+      const u32 nr = min(v.nslots, (u32)kMaxMergeRunsHost);
+      const u64 stride = (u64)kSlotHeaderRecords + v.slot_records;
+      for (u32 q = 0; q < nr; ++q) {
+        const KeyCount* slot = v.slots + q * stride;
+        const SlotHeader* h = reinterpret_cast<const SlotHeader*>(slot);
+        const u32 len = h->status == kSlotOk ? (u32)min(h->n, (u64)v.slot_records) : 0u;
+        t.off[q] = acc;
+        t.base[q] = slot + kSlotHeaderRecords;
+        acc += len;
+      }
+      t.off[nr] = acc;
+      t.nruns = nr;
+    } else {
+      const u32 nr = min(v.meta[0], (u32)kMaxMergeRunsHost);
+      for (u32 q = 0; q < nr; ++q) {
+        t.off[q] = acc;
+        t.base[q] = q == 0 ? v.own : v.recv + (acc - v.meta[1]);  // runs 1.. back to back
+        acc += v.meta[1 + q];
+      }
+      t.off[nr] = acc;
+      t.nruns = nr;
     }
-    t.off[nr] = acc;
-    t.nruns = nr;
   }
   __syncthreads();
 }
 
-// Run q's records: run 0 is `own`, runs 1.. lie back to back in `recv`.
-__device__ __forceinline__ const KeyCount* run_ptr(const KeyCount* own, const KeyCount* recv,
-                                                   const RunTable& t, u32 q) {
-  return q == 0 ? own : recv + (t.off[q] - t.off[1]);
-}
-
 __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
-    const KeyCount* __restrict__ own, const KeyCount* __restrict__ recv,
-    const u32* __restrict__ meta, KeyCount* __restrict__ merged) {
+    RunsView view, KeyCount* __restrict__ merged) {
   __shared__ RunTable t;
-  load_runs(meta, t);
+  load_runs(view, t);
   const u32 nruns = t.nruns;
   const u32 total = t.off[nruns];
   for (u32 g = blockIdx.x * kMergeBlock + threadIdx.x; g < total; g += gridDim.x * kMergeBlock) {
     u32 q = 0;
     while (q + 1 < nruns && t.off[q + 1] <= g) ++q;
     const u32 i = g - t.off[q];
-    const KeyCount rec = run_ptr(own, recv, t, q)[i];
+    const KeyCount rec = t.base[q][i];
     const u64 k[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
     u64 pos = i;
     u64 count = rec.count;
@@ -92,7 +114,7 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
       for (int l = 0; l < kMergeLanes; ++l) {
         const u32 r = r0 + l;
         const bool live = r < nruns && r != q;
-        base[l] = live ? run_ptr(own, recv, t, r) : own;
+        base[l] = live ? t.base[r] : nullptr;
         lo[l] = 0;
         len[l] = live ? t.off[r + 1] - t.off[r] : 0;
         eq[l] = false;
@@ -139,15 +161,14 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
 }
 
 __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
-    const KeyCount* __restrict__ merged, const u32* __restrict__ meta,
-    MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
+    const KeyCount* __restrict__ merged, RunsView view, MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
     MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr) {
   __shared__ u64 s_scan[kMergeBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
   __shared__ RunTable t;
   const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
-  load_runs(meta, t);
+  load_runs(view, t);
   const u32 total = t.off[t.nruns];
   const u32 ntiles = total ? (u32)div_up(total, (u64)kReduceTile) : 1u;
   if (tile >= ntiles) return;  // uniform per workgroup; nobody waits on these tiles
@@ -200,19 +221,32 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
   }
 }
 
+void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters* ctr,
+                       OutRecord* out, MapCounters* ctr_out, LookbackScratch lb, hipStream_t s) {
+  const u64 c = cap ? cap : 1;
+  const u32 rank_grid = (u32)std::min<u64>(div_up(c, kMergeBlock), 4096);
+  merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(v, merged);
+  LOCUST_HIP_LAUNCH_CHECK();
+  const u32 emit_grid = (u32)div_up(c, (u64)kReduceTile);
+  merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, v, ctr, out, ctr_out,
+                                                                  lb.status, lb.tile_counter);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
 }  // namespace
 
 void launch_merge_sorted_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                               u64 cap, KeyCount* merged, MapCounters* ctr, OutRecord* out,
                               MapCounters* ctr_out, LookbackScratch lb, hipStream_t s) {
-  const u64 c = cap ? cap : 1;
-  const u32 rank_grid = (u32)std::min<u64>(div_up(c, kMergeBlock), 4096);
-  merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(own, recv, meta, merged);
-  LOCUST_HIP_LAUNCH_CHECK();
-  const u32 emit_grid = (u32)div_up(c, (u64)kReduceTile);
-  merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, meta, ctr, out, ctr_out,
-                                                                  lb.status, lb.tile_counter);
-  LOCUST_HIP_LAUNCH_CHECK();
+  launch_merge_view(RunsView{own, recv, meta, nullptr, 0, 0}, cap, merged, ctr, out, ctr_out, lb,
+                    s);
+}
+
+void launch_merge_slots(const KeyCount* slots, u32 nslots, u32 slot_records, KeyCount* merged,
+                        MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                        LookbackScratch lb, hipStream_t s) {
+  launch_merge_view(RunsView{nullptr, nullptr, nullptr, slots, nslots, slot_records},
+                    (u64)nslots * slot_records, merged, ctr, out, ctr_out, lb, s);
 }
 
 }  // namespace locust

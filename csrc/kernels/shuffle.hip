@@ -51,8 +51,20 @@ __global__ __launch_bounds__(256) void out_to_sorted_kernel(const OutRecord* __r
                                                             const u32* __restrict__ d_n,
                                                             KeysSoA sorted,
                                                             u64* __restrict__ counts,
-                                                            KeyCount* __restrict__ recs) {
+                                                            KeyCount* __restrict__ recs,
+                                                            SlotHeader* __restrict__ hdr,
+                                                            const MapCounters* __restrict__ ctr,
+                                                            SlotHeader h) {
   const u32 n = *d_n;
+  if (hdr && blockIdx.x == 0 && threadIdx.x == 0) {
+    h.status = (ctr->flags & kCtrDictOverflow) ? kSlotRedo : h.status;
+    h.n = n;
+    h.tokens = ctr->num_records;
+    h.overflow_lines = ctr->overflow_lines;
+    h.truncated = ctr->truncated;
+    h.max_key_len = ctr->max_key_len;
+    *hdr = h;
+  }
   for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const OutRecord o = in[i];
     KeyCount r;
@@ -126,9 +138,10 @@ void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u
 }
 
 void launch_out_to_sorted(const OutRecord* in, const u32* d_n, u64 cap, KeysSoA sorted,
-                          u64* counts, KeyCount* recs, hipStream_t s) {
-  out_to_sorted_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(in, d_n, sorted, counts,
-                                                                     recs);
+                          u64* counts, KeyCount* recs, hipStream_t s, SlotHeader* hdr,
+                          const MapCounters* ctr, const SlotHeader& tmpl) {
+  out_to_sorted_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(
+      in, d_n, sorted, counts, recs, hdr, ctr, tmpl);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -163,3 +163,30 @@ def test_gpu_gather_merge_overflow(n_words):
     cfgs = [lc.make_dist_config(4, job, strategy=s) for s in ("gather", "gather", "shuffle")]
     for res, info in lc._C.run_multi_schedule(text, cfgs):
         assert res.entries() == ent
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gpu_slot_gather_resizes(world):
+    """Gather in one all-gather of fixed-size slots: the first job's slots (8,192 records)
+    are too small for ~40,000/world distinct keys per rank, so every rank falls back to the
+    standard gather together; the next jobs use slots sized from the headers and merge
+    straight from the all-gather buffer."""
+    text = _distinct_text(40000) + b"w000001 w000002\n"
+    ent = oracle.wordcount(text)[0]
+    job = lc.make_config("gpu", combine=True, check=True)
+    cfgs = [lc.make_dist_config(world, job, strategy="gather") for _ in range(3)]
+    for res, info in lc._C.run_multi_schedule(text, cfgs):
+        assert info["strategy"] == "gather"
+        assert res.entries() == ent
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", ["1:map", "0:reduce"])
+def test_gpu_slot_gather_fault(hamlet, monkeypatch, fault):
+    """A failing rank's slot header carries the failure: every rank raises (no hang)."""
+    monkeypatch.setenv("LOCUST_FAULT", fault)
+    job = lc.make_config("gpu", combine=True)
+    cfgs = [lc.make_dist_config(3, job, strategy="gather") for _ in range(2)]
+    with pytest.raises(lc.LocustError, match="rank"):
+        lc._C.run_multi_schedule(hamlet, cfgs)
