@@ -141,7 +141,7 @@ WordCountResult GpuWordCount::merge_runs(const std::vector<std::vector<KeyCount>
   m.grow_host_out(n);
   launch_merge_sorted_runs(m.d_records, m.d_records + runs[0].size(), d_meta, m.cap,
                            reinterpret_cast<KeyCount*>(m.d_out), m.d_ctr, m.d_out_mapped,
-                           m.d_ctr_mapped, m.lb_scan, m.stream);
+                           m.d_ctr_mapped, m.lb_merge(m.cap), m.stream);
   m.sync();
   *m.h_ctr = *m.h_ctr_mapped;
   WordCountResult r;

@@ -90,6 +90,13 @@ struct DevicePipeline {
   u64 sync_bytes = 0;
   MapCounters* d_ctr = nullptr;
   LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{}, lb_dict{};
+  // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
+  // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
+  LookbackScratch lb_merge(u64 n) const {
+    LOCUST_CHECK_ARG(merge_scratch_words(n) <= 2 * (div_up(cap, kReduceTile) + 1),
+                     "merge larger than the engine's look-back scratch");
+    return lb_heads;
+  }
   RadixWorkspace rx{};
 
   // dictionary path: [table | ucount | rank] is one zeroed block

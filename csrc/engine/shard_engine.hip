@@ -131,19 +131,24 @@ class GpuShardEngine final : public ShardEngine {
     tmpl.record_flags = kRecordsSorted | kRecordsDistinct;
     tmpl.lines = shard.num_lines;
     tmpl.slot_cap = slot_capacity();
+    // The ordered kernel writes the records, the SoA keys + counts, the slot header and the
+    // host-mapped counters itself: no conversion kernel, no counter copy.
+    OrderedExtra ex;
+    ex.recs = m.d_records;
+    ex.sorted = m.sorted;
+    ex.counts = m.d_sorted_counts;
+    ex.hdr = hdr;
+    ex.tmpl = tmpl;
     auto enqueue = [&] {
       m.enqueue_upload_device(shard);
       m.enqueue_map(shard);
-      m.enqueue_dict_ordered(/*with_counts=*/false, /*mapped=*/false);
-      launch_out_to_sorted(m.d_out, &m.d_ctr->num_unique, m.cap, m.sorted, m.d_sorted_counts,
-                           m.d_records, m.stream, hdr, m.d_ctr, tmpl);
+      launch_dict_ordered(m.tokens, nullptr, m.d_parts, &m.d_ctr->num_records, m.cap, m.d_ctr,
+                          nullptr, m.d_ctr_mapped, m.lb_dict, m.stream, m.ord_trace(), ex);
       if (spec_samples) {
         launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
         LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
                                         hipMemcpyDeviceToHost, m.stream));
       }
-      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_ctr, m.d_ctr, sizeof(MapCounters),
-                                      hipMemcpyDeviceToHost, m.stream));
     };
     m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
     if (m.use_graph())
@@ -160,6 +165,7 @@ class GpuShardEngine final : public ShardEngine {
   // the HBM table when a partition overflowed its LDS table.
   u64 complete_small_ordered(const TextInput& shard) {
     DevicePipeline& m = *mp_;
+    *m.h_ctr = *m.h_ctr_mapped;
     if (!(m.h_ctr->flags & kCtrDictOverflow)) {
       if (spec_samples_) {
         samples_.assign(m.h_small, m.h_small + kSpecSamples);
@@ -243,16 +249,18 @@ class GpuShardEngine final : public ShardEngine {
     DevicePipeline& r = *rp_;
     LOCUST_CHECK_ARG(nslots <= (u32)kMaxMergeRunsHost, "too many slots to merge");
     r.grow_host_out((u64)nslots * slot_recs);
+    grow_headers(nslots);
+    merge_copied_headers_ = true;
     // on the engine's stream, behind the all-gather
     auto enqueue = [&] {
-      LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, m.stream));
       launch_merge_slots(r.d_records, nslots, slot_recs, reinterpret_cast<KeyCount*>(r.d_out),
-                         r.d_ctr, r.d_out_mapped, r.d_ctr_mapped, r.lb_scan, m.stream);
+                         r.d_ctr, r.d_out_mapped, r.d_ctr_mapped,
+                         r.lb_merge((u64)nslots * slot_recs), d_headers_, m.stream);
     };
     if (m.use_graph())
       m.launch_cached({6, ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(r.d_records),
                        reinterpret_cast<u64>(r.d_out_mapped),
-                       reinterpret_cast<u64>(r.d_ctr_mapped), 0},
+                       reinterpret_cast<u64>(r.d_ctr_mapped), reinterpret_cast<u64>(d_headers_)},
                       enqueue);
     else
       enqueue();
@@ -260,11 +268,10 @@ class GpuShardEngine final : public ShardEngine {
 
   void enqueue_slot_headers(u32 nslots, u32 slot_recs) override {
     DevicePipeline& m = *mp_;
-    if (h_headers_cap_ < nslots) {
-      if (h_headers_) LOCUST_HIP_CHECK(hipHostFree(h_headers_));
-      h_headers_cap_ = std::max<u32>(nslots, 64);
-      LOCUST_HIP_CHECK(hipHostMalloc(&h_headers_, h_headers_cap_ * sizeof(SlotHeader),
-                                     hipHostMallocDefault));
+    grow_headers(nslots);
+    if (merge_copied_headers_) {  // the root's merge kernel wrote them already
+      merge_copied_headers_ = false;
+      return;
     }
     const u64 pitch = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
     LOCUST_HIP_CHECK(hipMemcpy2DAsync(h_headers_, sizeof(SlotHeader), rp_->d_records, pitch,
@@ -408,11 +415,10 @@ class GpuShardEngine final : public ShardEngine {
       KeyCount* merged = reinterpret_cast<KeyCount*>(r.d_out);  // >= cap records of scratch
       r.grow_host_out(n_all);
       auto enqueue = [&] {
-        LOCUST_HIP_CHECK(hipMemsetAsync(r.d_sync, 0, r.sync_bytes, r.stream));
         LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + (u64)nruns) * sizeof(u32),
                                         hipMemcpyHostToDevice, r.stream));
         launch_merge_sorted_runs(m.d_records, r.d_records, d_meta, r.cap, merged, r.d_ctr,
-                                 r.d_out_mapped, r.d_ctr_mapped, r.lb_scan, r.stream);
+                                 r.d_out_mapped, r.d_ctr_mapped, r.lb_merge(r.cap), r.stream);
       };
       if (r.use_graph())
         r.launch_cached({5, (u64)nruns, reinterpret_cast<u64>(m.d_records),
@@ -531,8 +537,22 @@ class GpuShardEngine final : public ShardEngine {
   bool distinct_local_ = true;  // d_records hold every key once (map-side combine)
   bool spec_samples_ = false;   // the last small pass produced splitter samples
   bool slot_fast_ = false;      // enqueue_map_slot took the one-graph small pass
-  SlotHeader* h_headers_ = nullptr;  // pinned copies of the all-gathered slot headers
+  SlotHeader* h_headers_ = nullptr;  // host-mapped copies of the all-gathered slot headers
+  SlotHeader* d_headers_ = nullptr;  // device view of h_headers_
   u32 h_headers_cap_ = 0;
+  bool merge_copied_headers_ = false;  // this job's merge kernel copies the headers
+  void grow_headers(u32 nslots) {
+    if (h_headers_cap_ >= nslots) return;
+    if (h_headers_) {
+      LOCUST_HIP_CHECK(hipStreamSynchronize(mp_->stream));
+      LOCUST_HIP_CHECK(hipHostFree(h_headers_));
+    }
+    h_headers_cap_ = std::max<u32>(nslots, 64);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_headers_, h_headers_cap_ * sizeof(SlotHeader),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_headers_), h_headers_, 0));
+  }
   SlotHeader* h_send_header_ = nullptr;  // pinned staging for a host-written header
   SlotHeader* slot_host_header() {
     if (!h_send_header_)

@@ -195,10 +195,20 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
 // emit kernels); a partition past kPartSlots distinct keys sets kCtrDictOverflow.
 // `trace` (diagnostics, optional): per partition p, s_memtime stamps at trace[p*8 + 0..5]
 // (start, built, published, prefix known, sorted, written) and the key count at [p*8+6].
+// Optional extra outputs of the ordered build (the distributed map): the sorted distinct
+// keys as KeyCount records and/or SoA keys + counts, and the gather slot's header (`tmpl`
+// completed on the device by the last partition).  `out` may then be null.
+struct OrderedExtra {
+  KeyCount* recs = nullptr;
+  KeysSoA sorted{};
+  u64* counts = nullptr;
+  SlotHeader* hdr = nullptr;
+  SlotHeader tmpl{};
+};
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
-                         u64* trace = nullptr);
+                         u64* trace = nullptr, const OrderedExtra& ex = OrderedExtra{});
 // Same, over runs of KeyCount records each sorted by key (the gather strategy's per-rank
 // combined outputs); duplicates across runs are summed.  Run 0 is `own`, runs 1.. lie
 // back to back in `recv`; `meta` (device) = [nruns <= 64, len_0, len_1, ...].
@@ -210,17 +220,20 @@ void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32
 // Merge of sorted runs (same run layout and meta as launch_dict_merge_runs) by lock-step
 // binary search + one look-back scan: `merged` (room for every record, bounded by `cap`)
 // is scratch; out / ctr / ctr_out as for launch_dict_ordered.  `lb` needs
-// div_up(cap, kReduceTile) zeroed status words and a zeroed tile counter.  Requires fewer
-// than 2^22 records and a total count below 2^40 (checked by the caller).
+// merge_scratch_words(cap) status words and a tile counter; the merge resets them itself
+// (no memset needed).  Requires fewer than 2^22 records and a total count below 2^40
+// (checked by the caller).
+u64 merge_scratch_words(u64 cap);
 void launch_merge_sorted_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                               u64 cap, KeyCount* merged, MapCounters* ctr, OutRecord* out,
                               MapCounters* ctr_out, LookbackScratch lb, hipStream_t s);
 // Same over the all-gathered slots: `nslots` slots of kSlotHeaderRecords + slot_records
 // records each, run q = slot q's records, its length min(header.n, slot_records) (0 when
 // the header's status is not kSlotOk).  `merged` needs nslots * slot_records records.
+// hdr_out (optional, host-mapped): every slot's header, copied by the merge.
 void launch_merge_slots(const KeyCount* slots, u32 nslots, u32 slot_records, KeyCount* merged,
                         MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
-                        LookbackScratch lb, hipStream_t s);
+                        LookbackScratch lb, SlotHeader* hdr_out, hipStream_t s);
 constexpr u64 kMergeMaxRecords = (1ull << 22) - 1;
 constexpr u64 kMergeMaxCount = (1ull << 40) - 1;
 
@@ -249,12 +262,6 @@ void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounte
 void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u64 cap,
                          KeyCount* out, hipStream_t s);
 
-// Sorted OutRecords -> SoA sorted keys + counts and KeyCount shuffle records.  With `hdr`,
-// also the slot header: `tmpl` (host-known fields) completed from `ctr` and n = *d_n
-// (status kSlotRedo on a dictionary overflow).
-void launch_out_to_sorted(const OutRecord* in, const u32* d_n, u64 cap, KeysSoA sorted,
-                          u64* counts, KeyCount* recs, hipStream_t s, SlotHeader* hdr = nullptr,
-                          const MapCounters* ctr = nullptr, const SlotHeader& tmpl = {});
 // AoS KeyCount -> SoA keys + counts (+ parts, optional: partition tag per record for the
 // partitioned dictionary builds).
 void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,

@@ -489,7 +489,7 @@ template <class Src>
 __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     Src src, MapCounters* __restrict__ ctr,
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr, u64* __restrict__ trace) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
 #define ORD_STAMP(k_)                                                          \
   if (trace && threadIdx.x == 0) trace[(u64)p * 8 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
@@ -624,21 +624,56 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   u64 tot2 = 0;
   u64 at = dev::block_exclusive_scan<u64, kPartBlock>(run, s_scan, &tot2) + base_tok;
-  if (!any_full && ovf_before == 0) {
+  if (!any_full && ovf_before == 0) {  // uniform per workgroup
+    // vals into LDS (s_w0 is free after the sort), then every output is written with
+    // consecutive lanes on consecutive words: full-line writes, which matters most for the
+    // host-mapped output (each partial line would be its own PCIe write)
+    u64* s_val = s_w0;
 #pragma unroll
     for (u32 t = 0; t < kPer; ++t) {
       const u32 i = threadIdx.x * kPer + t;
-      if (i < m) {
-        const LdsSlot& sl = s_tab[s_slot[i]];
-        OutRecord rec;
-        rec.w[0] = sl.w[0];
-#pragma unroll
-        for (int j = 1; j < kKeyWords; ++j) rec.w[j] = sl.w[j] ^ kWordMagic;
-        rec.val = at;
-        rec.count = c[t];
-        out[base_m + i] = rec;
-      }
+      if (i < m) s_val[i] = at;
       at += c[t];
+    }
+    __syncthreads();
+    if (out) {
+      // 16-B chunk q of this partition's slice: record q / 3, part q % 3
+      u64* dst = reinterpret_cast<u64*>(out + base_m);
+      for (u32 q = threadIdx.x; q < 3 * m; q += kPartBlock) {
+        const u32 i = q / 3, part = q - 3 * i;
+        const LdsSlot& sl = s_tab[s_slot[i]];
+        u64 a, b;
+        if (part == 0) {
+          a = sl.w[0];
+          b = sl.w[1] ^ kWordMagic;
+        } else if (part == 1) {
+          a = sl.w[2] ^ kWordMagic;
+          b = sl.w[3] ^ kWordMagic;
+        } else {
+          a = s_val[i];
+          b = sl.count;
+        }
+        dst[2 * q] = a;
+        dst[2 * q + 1] = b;
+      }
+    }
+    if (ex.recs) {
+      // 8-B word q of the KeyCount slice: record q / 5, word q % 5
+      u64* dst = reinterpret_cast<u64*>(ex.recs + base_m);
+      for (u32 q = threadIdx.x; q < 5 * m; q += kPartBlock) {
+        const u32 i = q / 5, wd = q - 5 * i;
+        const LdsSlot& sl = s_tab[s_slot[i]];
+        dst[q] = wd == 0 ? sl.w[0] : wd < kKeyWords ? sl.w[wd] ^ kWordMagic : sl.count;
+      }
+    }
+    if (ex.sorted.w[0]) {
+      for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
+        const LdsSlot& sl = s_tab[s_slot[i]];
+        ex.sorted.w[0][base_m + i] = sl.w[0];
+#pragma unroll
+        for (int j = 1; j < kKeyWords; ++j) ex.sorted.w[j][base_m + i] = sl.w[j] ^ kWordMagic;
+        if (ex.counts) ex.counts[base_m + i] = sl.count;
+      }
     }
   }
   ORD_STAMP(5);
@@ -660,6 +695,16 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       ctr_out->max_key_len = ctr->max_key_len;
       ctr_out->total_count = total;
       ctr_out->flags = ctr->flags | (ovf_total ? kCtrDictOverflow : 0u);
+    }
+    if (ex.hdr) {  // the gather slot's header: this rank's records are complete
+      SlotHeader h = ex.tmpl;
+      h.status = ovf_total ? kSlotRedo : h.status;
+      h.n = u;
+      h.tokens = ctr->num_records;
+      h.overflow_lines = ctr->overflow_lines;
+      h.truncated = ctr->truncated;
+      h.max_key_len = ctr->max_key_len;
+      *ex.hdr = h;
     }
   }
 }
@@ -904,10 +949,11 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
 
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
-                         MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace) {
+                         MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace,
+                         const OrderedExtra& ex) {
   const TagSource src{tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
   dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
-      src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace);
+      src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
@@ -916,7 +962,7 @@ void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32
                             LookbackScratch lb, hipStream_t s) {
   const RunsSource src{own, recv, meta};
   dict_ordered_kernel<RunsSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
-      src, ctr, out, ctr_out, lb.status, lb.tile_counter, nullptr);
+      src, ctr, out, ctr_out, lb.status, lb.tile_counter, nullptr, OrderedExtra{});
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

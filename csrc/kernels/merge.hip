@@ -27,7 +27,8 @@ namespace {
 
 constexpr int kMergeBlock = 256;
 constexpr int kMergeLanes = 8;                        // runs searched in lock step
-constexpr int kEmitItems = kReduceTile / kMergeBlock;  // 8 merged slots per thread
+constexpr int kEmitItems = 4;                          // merged slots per thread
+constexpr int kEmitTile = kMergeBlock * kEmitItems;    // 1,024 slots: 48 KB of LDS staging
 constexpr int kEmitCountBits = 40;                     // look-back value: [firsts:22][counts:40]
 constexpr u64 kEmitCountMask = (1ull << kEmitCountBits) - 1;
 
@@ -92,8 +93,20 @@ __device__ __forceinline__ void load_runs(const RunsView& v, RunTable& t) {
 }
 
 __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
-    RunsView view, KeyCount* __restrict__ merged) {
+    RunsView view, KeyCount* __restrict__ merged, LookbackScratch lb, u32 emit_tiles,
+    SlotHeader* __restrict__ hdr_out) {
   __shared__ RunTable t;
+  if (blockIdx.x == 0) {
+    // merge_emit's look-back scratch, reset here (stream order) instead of by a memset
+    for (u32 i = threadIdx.x; i < emit_tiles; i += kMergeBlock) lb.status[i] = 0;
+    if (threadIdx.x == 0) *lb.tile_counter = 0;
+    // the slot headers for the host (the root needs no separate copy)
+    if (hdr_out && view.slots) {
+      const u64 stride = (u64)kSlotHeaderRecords + view.slot_records;
+      for (u32 q = threadIdx.x; q < view.nslots; q += kMergeBlock)
+        hdr_out[q] = *reinterpret_cast<const SlotHeader*>(view.slots + q * stride);
+    }
+  }
   load_runs(view, t);
   const u32 nruns = t.nruns;
   const u32 total = t.off[nruns];
@@ -161,18 +174,21 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
 }
 
 __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
-    const KeyCount* __restrict__ merged, RunsView view, MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
-    MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr) {
+    const KeyCount* __restrict__ merged, RunsView view, MapCounters* __restrict__ ctr,
+    OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
+    u32* __restrict__ tile_ctr) {
   __shared__ u64 s_scan[kMergeBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
   __shared__ RunTable t;
+  // the tile's output records, staged so that the (host-mapped) writes are full lines
+  __shared__ __attribute__((aligned(16))) u64 s_out[kEmitTile * 6];
   const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
   load_runs(view, t);
   const u32 total = t.off[t.nruns];
-  const u32 ntiles = total ? (u32)div_up(total, (u64)kReduceTile) : 1u;
+  const u32 ntiles = total ? (u32)div_up(total, (u64)kEmitTile) : 1u;
   if (tile >= ntiles) return;  // uniform per workgroup; nobody waits on these tiles
-  const u32 i0 = tile * kReduceTile + threadIdx.x * kEmitItems;
+  const u32 i0 = tile * kEmitTile + threadIdx.x * kEmitItems;
   KeyCount v[kEmitItems];
   u64 agg = 0;
 #pragma unroll
@@ -188,46 +204,52 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
   u64 tile_sum = 0;
   const u64 excl = dev::block_exclusive_scan<u64, kMergeBlock>(agg, s_scan, &tile_sum);
   const u64 before = dev::block_lookback(status, tile, tile_sum, &s_prefix);
-  const u64 at = before + excl;
-  u64 idx = at >> kEmitCountBits;
-  u64 val = at & kEmitCountMask;
+  u32 li = (u32)(excl >> kEmitCountBits);  // index inside the tile's output slice
+  u64 val = (before + excl) & kEmitCountMask;
 #pragma unroll
   for (int e = 0; e < kEmitItems; ++e) {
     if (!v[e].count) continue;
-    OutRecord o;
+    u64* o = s_out + 6 * li;
 #pragma unroll
-    for (int j = 0; j < kKeyWords; ++j) o.w[j] = v[e].w[j];
-    o.val = val;
-    o.count = v[e].count;
-    out[idx++] = o;
+    for (int j = 0; j < kKeyWords; ++j) o[j] = v[e].w[j];
+    o[4] = val;
+    o[5] = v[e].count;
+    ++li;
     val += v[e].count;
   }
+  __syncthreads();
+  const u32 m = (u32)(tile_sum >> kEmitCountBits);
+  const u64 base = before >> kEmitCountBits;
+  // consecutive lanes, consecutive 16-B chunks of out[base .. base + m)
+  const uint4* src = reinterpret_cast<const uint4*>(s_out);
+  uint4* dst = reinterpret_cast<uint4*>(out + base);
+  for (u32 q = threadIdx.x; q < 3 * m; q += kMergeBlock) dst[q] = src[q];
   if (tile == ntiles - 1 && threadIdx.x == 0) {
     const u64 all = before + tile_sum;
     const u32 u = (u32)(all >> kEmitCountBits);
     const u64 tok = all & kEmitCountMask;
+    ctr->num_records = total;
     ctr->num_unique = u;
     ctr->total_count = tok;
     if (ctr_out) {
-      ctr_out->num_records = ctr->num_records;
-      ctr_out->num_unique = u;
-      ctr_out->overflow_lines = ctr->overflow_lines;
-      ctr_out->truncated = ctr->truncated;
-      ctr_out->num_newlines = ctr->num_newlines;
-      ctr_out->max_key_len = ctr->max_key_len;
-      ctr_out->total_count = tok;
-      ctr_out->flags = ctr->flags;
+      MapCounters c{};
+      c.num_records = total;
+      c.num_unique = u;
+      c.total_count = tok;
+      *ctr_out = c;
     }
   }
 }
 
 void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters* ctr,
-                       OutRecord* out, MapCounters* ctr_out, LookbackScratch lb, hipStream_t s) {
+                       OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
+                       SlotHeader* hdr_out, hipStream_t s) {
   const u64 c = cap ? cap : 1;
   const u32 rank_grid = (u32)std::min<u64>(div_up(c, kMergeBlock), 4096);
-  merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(v, merged);
+  const u32 emit_grid = (u32)div_up(c, (u64)kEmitTile);
+  merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(v, merged, lb, emit_grid,
+                                                                  hdr_out);
   LOCUST_HIP_LAUNCH_CHECK();
-  const u32 emit_grid = (u32)div_up(c, (u64)kReduceTile);
   merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, v, ctr, out, ctr_out,
                                                                   lb.status, lb.tile_counter);
   LOCUST_HIP_LAUNCH_CHECK();
@@ -235,18 +257,20 @@ void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters
 
 }  // namespace
 
+u64 merge_scratch_words(u64 cap) { return div_up(cap ? cap : 1, (u64)kEmitTile); }
+
 void launch_merge_sorted_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                               u64 cap, KeyCount* merged, MapCounters* ctr, OutRecord* out,
                               MapCounters* ctr_out, LookbackScratch lb, hipStream_t s) {
   launch_merge_view(RunsView{own, recv, meta, nullptr, 0, 0}, cap, merged, ctr, out, ctr_out, lb,
-                    s);
+                    nullptr, s);
 }
 
 void launch_merge_slots(const KeyCount* slots, u32 nslots, u32 slot_records, KeyCount* merged,
                         MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
-                        LookbackScratch lb, hipStream_t s) {
+                        LookbackScratch lb, SlotHeader* hdr_out, hipStream_t s) {
   launch_merge_view(RunsView{nullptr, nullptr, nullptr, slots, nslots, slot_records},
-                    (u64)nslots * slot_records, merged, ctr, out, ctr_out, lb, s);
+                    (u64)nslots * slot_records, merged, ctr, out, ctr_out, lb, hdr_out, s);
 }
 
 }  // namespace locust

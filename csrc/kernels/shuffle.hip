@@ -47,38 +47,6 @@ __global__ __launch_bounds__(256) void unpack_records_kernel(const KeyCount* __r
 
 // Sorted output records (from the ordered dictionary kernel) -> SoA sorted keys + counts
 // (for sampling and the splitter search) and the 40-B shuffle records.
-__global__ __launch_bounds__(256) void out_to_sorted_kernel(const OutRecord* __restrict__ in,
-                                                            const u32* __restrict__ d_n,
-                                                            KeysSoA sorted,
-                                                            u64* __restrict__ counts,
-                                                            KeyCount* __restrict__ recs,
-                                                            SlotHeader* __restrict__ hdr,
-                                                            const MapCounters* __restrict__ ctr,
-                                                            SlotHeader h) {
-  const u32 n = *d_n;
-  if (hdr && blockIdx.x == 0 && threadIdx.x == 0) {
-    h.status = (ctr->flags & kCtrDictOverflow) ? kSlotRedo : h.status;
-    h.n = n;
-    h.tokens = ctr->num_records;
-    h.overflow_lines = ctr->overflow_lines;
-    h.truncated = ctr->truncated;
-    h.max_key_len = ctr->max_key_len;
-    *hdr = h;
-  }
-  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const OutRecord o = in[i];
-    KeyCount r;
-#pragma unroll
-    for (int w = 0; w < kKeyWords; ++w) {
-      sorted.w[w][i] = o.w[w];
-      r.w[w] = o.w[w];
-    }
-    counts[i] = o.count;
-    r.count = o.count;
-    recs[i] = r;
-  }
-}
-
 __global__ void sample_keys_kernel(ConstKeysSoA sorted, const u32* __restrict__ d_n, u32 s,
                                    PackedKey* __restrict__ out) {
   const u32 n = *d_n;
@@ -134,14 +102,6 @@ __global__ void bucket_offsets_kernel(ConstKeysSoA sorted, const u32* __restrict
 void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u64 cap,
                          KeyCount* out, hipStream_t s) {
   pack_records_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(keys, counts, d_n, out);
-  LOCUST_HIP_LAUNCH_CHECK();
-}
-
-void launch_out_to_sorted(const OutRecord* in, const u32* d_n, u64 cap, KeysSoA sorted,
-                          u64* counts, KeyCount* recs, hipStream_t s, SlotHeader* hdr,
-                          const MapCounters* ctr, const SlotHeader& tmpl) {
-  out_to_sorted_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(
-      in, d_n, sorted, counts, recs, hdr, ctr, tmpl);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
