@@ -31,7 +31,9 @@ void map_lines(const TextInput& in, const JobConfig& cfg, std::vector<PackedKey>
 }
 
 void reduce_sorted(const std::vector<PackedKey>& toks, WordCountResult* r) {
-  entries_from_sorted_tokens(toks.data(), toks.size(), &r->entries);
+  std::vector<WordCountEntry> e;
+  entries_from_sorted_tokens(toks.data(), toks.size(), &e);
+  r->entries = std::move(e);
   r->num_unique = r->entries.size();
 }
 
@@ -202,9 +204,9 @@ class CpuShardEngine final : public ShardEngine {
     reduce_received(n_other + local_.size(), total_count, num_unique);
   }
 
-  void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
+  void finalize(u64 global_offset, EntryList* out) override {
     for (auto& e : out_) e.val += global_offset;
-    *out = out_;
+    out->assign(out_.data(), out_.data() + out_.size());
   }
 
   void map_stats(WordCountResult* r) override { *r = stats_; }

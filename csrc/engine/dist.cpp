@@ -193,8 +193,9 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       min_cap = std::min(min_cap, hd[p].slot_cap);
       fallback |= hd[p].status != kSlotOk || hd[p].n > slot_recs;
     }
-    // next job's slot: the largest rank's records + 25%, within every rank's send buffer
-    const u64 want = align_up(max_n + max_n / 4 + 1, 1024);
+    // next job's slot: the largest rank's records + 1/8, within every rank's send buffer
+    // (every rank receives P slots: padding costs P x as much as it saves in refits)
+    const u64 want = align_up(max_n + max_n / 8 + 1, 512);
     eng.slot_records = (u32)std::max<u64>(kSlotRecordsMin, std::min<u64>(want, min_cap));
     fallback |= cfg.strategy == DistStrategy::kAuto && sum > cfg.gather_max_records;
     st_slot = local("map", [&] {
@@ -396,7 +397,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   check("reduce", &all3[0].status, sizeof(Msg3));
   u64 offset = 0;
   for (int p = 0; p < me; ++p) offset += all3[(size_t)p].total;
-  std::vector<WordCountEntry> entries;
+  EntryList entries;
   eng.finalize(offset, &entries);
   res.range_tokens = total;
   res.range_unique = uniq;

@@ -301,7 +301,7 @@ struct DevicePipeline {
 
   ~DevicePipeline() {
     if (stream) (void)hipStreamSynchronize(stream);
-    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    for (auto& g : dict_graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
     if (d_ord_trace) (void)hipFree(d_ord_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
@@ -318,23 +318,54 @@ struct DevicePipeline {
     if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
     if (stream) (void)hipStreamDestroy(stream);
     if (arena.base) (void)hipFree(arena.base);
-    for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_out, (void*)h_keys,
+    for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_keys,
                     (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped})
       if (p) (void)hipHostFree(p);
   }
 
-  // Host-mapped output records (zero-copy emit target); grown when a radix-path result
-  // has more distinct keys than the dictionary's capacity.
-  void grow_host_out(u64 n) {
-    if (n <= h_out_cap) return;
-    if (h_out) {
-      sync();
-      LOCUST_HIP_CHECK(hipHostFree(h_out));
+  // ---- host-mapped output buffers (zero-copy emit target AND zero-copy results) ----
+  // A result adopts the buffer its job wrote (EntryList keeps it alive); the next job
+  // takes a buffer no result holds any more, so jobs whose results are dropped in turn
+  // alternate between two buffers and nothing is ever copied out.
+  struct HostOut {
+    OutRecord* h = nullptr;
+    OutRecord* d = nullptr;
+    u64 cap = 0;
+    explicit HostOut(u64 n) : cap(std::max<u64>(n, 1)) {
+      LOCUST_HIP_CHECK(hipHostMalloc(&h, cap * sizeof(OutRecord),
+                                     hipHostMallocMapped | hipHostMallocCoherent));
+      LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
     }
-    h_out_cap = std::max<u64>(n, 1);
-    LOCUST_HIP_CHECK(hipHostMalloc(&h_out, h_out_cap * sizeof(OutRecord),
-                                   hipHostMallocMapped | hipHostMallocCoherent));
-    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_out_mapped), h_out, 0));
+    ~HostOut() {
+      if (h) (void)hipHostFree(h);
+    }
+    HostOut(const HostOut&) = delete;
+    HostOut& operator=(const HostOut&) = delete;
+  };
+  std::vector<std::shared_ptr<HostOut>> out_pool;
+  size_t out_idx = 0;
+  void use_out(size_t i) {
+    out_idx = i;
+    h_out = out_pool[i]->h;
+    d_out_mapped = out_pool[i]->d;
+    h_out_cap = out_pool[i]->cap;
+  }
+  // Before a job writes the mapped output: a buffer no earlier result still holds.
+  void select_out() {
+    if (!out_pool.empty() && out_pool[out_idx].use_count() == 1) return;
+    for (size_t i = 0; i < out_pool.size(); ++i)
+      if (out_pool[i].use_count() == 1) return use_out(i);
+    out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+    use_out(out_pool.size() - 1);
+  }
+  // ... with room for n records (grown when a radix-path result has more distinct keys
+  // than the dictionary's capacity).
+  void grow_host_out(u64 n) {
+    select_out();
+    if (n <= h_out_cap) return;
+    sync();  // the device may still write the buffer being replaced
+    out_pool[out_idx] = std::make_shared<HostOut>(n);
+    use_out(out_idx);
   }
   // Pinned staging for key up/downloads (stage-split paths only), allocated on demand.
   void grow_host_keys(u64 n) {
@@ -425,19 +456,25 @@ struct DevicePipeline {
   }
 
   // ---- hipGraph replay of the dictionary job ----
-  hipGraphExec_t graph_exec = nullptr;
-  bool graph_ordered = false;  // the captured job uses the ordered kernel
   struct GraphKey {
     u64 bytes = ~0ull;
     u64 lines = 0;
     const char* src = nullptr;
     const char* map_text = nullptr;
     Upload mode = Upload::kStaged;
+    const OutRecord* out = nullptr;  // the host-mapped output buffer the graph writes
     bool operator==(const GraphKey& o) const {
       return bytes == o.bytes && lines == o.lines && src == o.src && map_text == o.map_text &&
-             mode == o.mode;
+             mode == o.mode && out == o.out;
     }
-  } graph_key;
+  };
+  struct DictGraph {
+    GraphKey key;
+    hipGraphExec_t exec;
+    bool ordered;  // the captured job uses the ordered kernel
+  };
+  std::vector<DictGraph> dict_graphs;  // one per (input shape, output buffer)
+  bool graph_ordered = false;          // the last launched graph uses the ordered kernel
   bool use_graph() const {
     if (cfg.graph >= 0) return cfg.graph > 0 && cfg.sort_path == SortPath::kDict;
     return cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast;
@@ -446,24 +483,30 @@ struct DevicePipeline {
   // and source; later runs replay it with one hipGraphLaunch.
   void launch_dict_graph(const TextInput& in, bool compat) {
     const GraphKey key{in.bytes, in.num_lines, upload_mode == Upload::kDirect ? in.data : nullptr,
-                       map_text, upload_mode};
-    if (!graph_exec || !(key == graph_key)) {
-      if (graph_exec) {
-        LOCUST_HIP_CHECK(hipGraphExecDestroy(graph_exec));
-        graph_exec = nullptr;
+                       map_text, upload_mode, d_out_mapped};
+    const DictGraph* hit = nullptr;
+    for (const auto& g : dict_graphs)
+      if (g.key == key) hit = &g;
+    if (!hit) {
+      if (dict_graphs.size() >= 4) {  // shapes or buffers changed a lot: drop the oldest
+        LOCUST_HIP_CHECK(hipGraphExecDestroy(dict_graphs.front().exec));
+        dict_graphs.erase(dict_graphs.begin());
       }
       hipGraph_t g = nullptr;
       LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
       enqueue_upload_device(in);
       enqueue_map(in);
-      graph_ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr);
+      const bool ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr);
       LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
-      LOCUST_HIP_CHECK(hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0));
+      hipGraphExec_t exec = nullptr;
+      LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
       LOCUST_HIP_CHECK(hipGraphDestroy(g));
-      graph_key = key;
+      dict_graphs.push_back({key, exec, ordered});
+      hit = &dict_graphs.back();
     }
+    graph_ordered = hit->ordered;
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
-    LOCUST_HIP_CHECK(hipGraphLaunch(graph_exec, stream));
+    LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
   }
   bool use_zero_copy(const TextInput& in) const {
     if (cfg.map_path != MapPath::kFast || !d_h_text) return false;
@@ -682,19 +725,17 @@ struct DevicePipeline {
     if (done) LOCUST_HIP_CHECK(hipEventRecord(done, stream));
     sync();
     fill_counters(r);
-    r.entries.resize(u);
     copy_out(r.entries, u);
   }
 
-  // Host output records -> result entries: identical 48-byte layouts, one memcpy.
-  void copy_out(std::vector<WordCountEntry>& e, u64 u) const {
+  // Host output records -> result entries: identical 48-byte layouts, so the result
+  // simply adopts the buffer the device wrote (no copy; see select_out).
+  void copy_out(EntryList& e, u64 u) {
     static_assert(sizeof(WordCountEntry) == sizeof(OutRecord), "entry layout");
     static_assert(offsetof(WordCountEntry, val) == offsetof(OutRecord, val), "entry layout");
     static_assert(offsetof(WordCountEntry, count) == offsetof(OutRecord, count), "entry layout");
-    // assign, not resize + memcpy: resize would zero-fill the vector first (a second pass
-    // over ~270 KB for whole Hamlet, on the job's critical path)
-    const WordCountEntry* src = reinterpret_cast<const WordCountEntry*>(h_out);
-    e.assign(src, src + u);
+    LOCUST_CHECK_ARG(u <= h_out_cap, "output larger than its buffer");
+    e.adopt(out_pool[out_idx], reinterpret_cast<WordCountEntry*>(h_out), u);
   }
 
   void fill_counters(WordCountResult& r) const {
@@ -763,6 +804,7 @@ struct DevicePipeline {
 
   WordCountResult run(const TextInput& in) {
     TraceRange tr("locust:job");
+    select_out();  // the previous result may still hold the last output buffer
     if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
         cfg.map_path == MapPath::kFast)
       return run_stream(in);
@@ -793,7 +835,11 @@ struct DevicePipeline {
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
       }
+      const u64 t_launched = now_ns();
       sync();  // the one host synchronisation of a dictionary run
+      const u64 t_synced = now_ns();
+      r.times.host_launch_ms = (t_launched - t0) * 1e-6;
+      r.times.host_wait_ms = (t_synced - t_launched) * 1e-6;
       *h_ctr = *h_ctr_mapped;
       const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
       if (ordered) print_ord_trace();
@@ -805,6 +851,7 @@ struct DevicePipeline {
       } else {
         fill_counters(r);
         copy_out(r.entries, h_ctr->num_unique);
+        r.times.host_copy_ms = (now_ns() - t_synced) * 1e-6;
       }
     } else {
       enqueue_process((u32)in.num_lines, compat, false);
@@ -972,9 +1019,7 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
       download_output(r, ev[5]);
     } else {
-      const u64 u = h_ctr->num_unique;
-      r.entries.resize(u);
-      copy_out(r.entries, u);
+      copy_out(r.entries, h_ctr->num_unique);
     }
     stream_stats(nchunks, r);
     r.num_unique = r.entries.size();

@@ -356,6 +356,7 @@ class GpuShardEngine final : public ShardEngine {
 
   void reduce_received(u64 n, u64* total_count, u64* num_unique) override {
     DevicePipeline& r = *rp_;
+    r.select_out();  // the previous job's entries may still hold the last output buffer
     // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
     r.set_num_records(n);
     launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
@@ -396,6 +397,7 @@ class GpuShardEngine final : public ShardEngine {
                        u64* total_count, u64* num_unique) override {
     DevicePipeline& m = *mp_;
     DevicePipeline& r = *rp_;  // recv_records() created it; holds the other ranks' records
+    r.select_out();
     u64 n_other = 0;
     for (u64 l : run_lens) n_other += l;
     LOCUST_CHECK_ARG(n_other + local_count_ <= r.cap, "gather buffer too small");
@@ -482,7 +484,7 @@ class GpuShardEngine final : public ShardEngine {
     reduce_received(n_other + local_count_, total_count, num_unique);
   }
 
-  void finalize(u64 global_offset, std::vector<WordCountEntry>* out) override {
+  void finalize(u64 global_offset, EntryList* out) override {
     for (auto& e : range_entries_) e.val += global_offset;
     *out = std::move(range_entries_);
   }
@@ -527,7 +529,7 @@ class GpuShardEngine final : public ShardEngine {
   ConstKeysSoA local_keys_{};
   std::vector<PackedKey> samples_;
   bool samples_valid_ = false;
-  std::vector<WordCountEntry> range_entries_;
+  EntryList range_entries_;
   const u64* local_counts_ = nullptr;
   const u32* local_n_ = nullptr;
   WordCountResult local_stats_;

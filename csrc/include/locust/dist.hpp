@@ -166,7 +166,7 @@ class ShardEngine {
   // Records a slot can hold on this rank (the all-gather uses the minimum over ranks).
   virtual u64 slot_capacity() const { return 0; }
   u32 slot_records = 0;  // agreed slot size for the next job (0: kSlotRecordsMin)
-  virtual void finalize(u64 global_offset, std::vector<WordCountEntry>* out) = 0;
+  virtual void finalize(u64 global_offset, EntryList* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;
 };

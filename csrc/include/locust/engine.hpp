@@ -35,6 +35,9 @@ struct StageTimes {
   double wall_ms = 0;
   // Device time of the whole job (first to last enqueued operation, hipEvents).
   double gpu_ms = 0;
+  // Host-side split of wall_ms (single-GPU runs): enqueue/launch, waiting for the device,
+  // and copying the results out of the host-mapped output.
+  double host_launch_ms = 0, host_wait_ms = 0, host_copy_ms = 0;
   bool graph = false;  // replayed as one hipGraph: the stage fields above are not split
   // Host timers placed where the reference placed them (launch-only map etc., BASELINE.md
   // "How the reference measured these"), filled when JobConfig.ref_timers is set.
@@ -49,8 +52,67 @@ struct WordCountEntry {
   u64 count;
 };
 
+// The entries of a result: an owned vector, or -- zero-copy -- the engine's host-mapped
+// output buffer itself, which the device wrote and which this list keeps alive (`owner`)
+// until it is dropped; the engine then reuses the buffer for a later job.  Vector-like.
+class EntryList {
+ public:
+  EntryList() = default;
+  EntryList(std::vector<WordCountEntry>&& v) : vec_(std::move(v)) {}  // NOLINT: implicit
+  EntryList& operator=(std::vector<WordCountEntry>&& v) {
+    owner_.reset();
+    view_ = nullptr;
+    n_ = 0;
+    vec_ = std::move(v);
+    return *this;
+  }
+  // Borrow n entries at p, kept valid by `owner`.
+  void adopt(std::shared_ptr<void> owner, WordCountEntry* p, size_t n) {
+    vec_.clear();
+    vec_.shrink_to_fit();
+    owner_ = std::move(owner);
+    view_ = p;
+    n_ = n;
+  }
+  bool borrowed() const { return owner_ != nullptr; }
+  size_t size() const { return owner_ ? n_ : vec_.size(); }
+  bool empty() const { return size() == 0; }
+  WordCountEntry* data() { return owner_ ? view_ : vec_.data(); }
+  const WordCountEntry* data() const { return owner_ ? view_ : vec_.data(); }
+  WordCountEntry& operator[](size_t i) { return data()[i]; }
+  const WordCountEntry& operator[](size_t i) const { return data()[i]; }
+  const WordCountEntry& front() const { return data()[0]; }
+  WordCountEntry* begin() { return data(); }
+  WordCountEntry* end() { return data() + size(); }
+  const WordCountEntry* begin() const { return data(); }
+  const WordCountEntry* end() const { return data() + size(); }
+  // Owned storage of n entries (a borrowed prefix is copied over).
+  void resize(size_t n) {
+    if (owner_) {
+      std::vector<WordCountEntry> v(view_, view_ + std::min(n, n_));
+      owner_.reset();
+      view_ = nullptr;
+      n_ = 0;
+      vec_ = std::move(v);
+    }
+    vec_.resize(n);
+  }
+  void assign(const WordCountEntry* b, const WordCountEntry* e) {
+    owner_.reset();
+    view_ = nullptr;
+    n_ = 0;
+    vec_.assign(b, e);
+  }
+
+ private:
+  std::vector<WordCountEntry> vec_;
+  std::shared_ptr<void> owner_;
+  WordCountEntry* view_ = nullptr;
+  size_t n_ = 0;
+};
+
 struct WordCountResult {
-  std::vector<WordCountEntry> entries;  // sorted by key
+  EntryList entries;  // sorted by key
   u64 num_lines = 0;
   u64 num_tokens = 0;       // kv_num_map
   u64 num_unique = 0;       // kv_num_reduce

@@ -43,9 +43,9 @@ std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs);
 
 // ---- output ----
 // GPU build format (main.cu:132): "print key: %s \t val: %d \t count: %d\n".
-void format_gpu_output(const std::vector<WordCountEntry>& e, std::string* out);
+void format_gpu_output(const EntryList& e, std::string* out);
 // CPU build format (main.cu:286): "print key: %s \t value: %s\n" with value = count.
-void format_cpu_output(const std::vector<WordCountEntry>& e, std::string* out);
+void format_cpu_output(const EntryList& e, std::string* out);
 void write_all(std::FILE* f, const std::string& s);
 
 std::string key_to_string(const PackedKey& k);

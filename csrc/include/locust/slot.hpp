@@ -24,7 +24,7 @@ constexpr i32 kSlotOk = 0, kSlotFailed = 1, kSlotRedo = 2;
 // Smallest slot (records) of the one-all-gather gather strategy: the first job's slot
 // size before any rank's record count is known; later jobs size slots from the previous
 // job's largest rank.
-constexpr u32 kSlotRecordsMin = 8192;
+constexpr u32 kSlotRecordsMin = 2048;
 // Most ranks the one-all-gather gather strategy merges (the merge kernels' run table).
 constexpr int kMaxSlotRanks = 64;
 

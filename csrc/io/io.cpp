@@ -191,7 +191,7 @@ std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs) {
 }
 
 // ---------------- output ----------------
-void format_gpu_output(const std::vector<WordCountEntry>& e, std::string* out) {
+void format_gpu_output(const EntryList& e, std::string* out) {
   out->reserve(out->size() + e.size() * 48);
   char buf[kKeyBytes + 1];
   for (const auto& x : e) {
@@ -207,7 +207,7 @@ void format_gpu_output(const std::vector<WordCountEntry>& e, std::string* out) {
   }
 }
 
-void format_cpu_output(const std::vector<WordCountEntry>& e, std::string* out) {
+void format_cpu_output(const EntryList& e, std::string* out) {
   out->reserve(out->size() + e.size() * 32);
   char buf[kKeyBytes + 1];
   for (const auto& x : e) {

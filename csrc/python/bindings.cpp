@@ -37,6 +37,9 @@ struct PyResult {
     d["d2h_ms"] = r.times.d2h_ms;
     d["wall_ms"] = r.times.wall_ms;
     d["gpu_ms"] = r.times.gpu_ms;
+    d["host_launch_ms"] = r.times.host_launch_ms;
+    d["host_wait_ms"] = r.times.host_wait_ms;
+    d["host_copy_ms"] = r.times.host_copy_ms;
     d["ref_map_ms"] = r.times.ref_map_ms;
     d["ref_process_ms"] = r.times.ref_process_ms;
     d["ref_reduce_ms"] = r.times.ref_reduce_ms;

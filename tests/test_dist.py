@@ -168,7 +168,7 @@ def test_gpu_gather_merge_overflow(n_words):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_gpu_slot_gather_resizes(world):
-    """Gather in one all-gather of fixed-size slots: the first job's slots (8,192 records)
+    """Gather in one all-gather of fixed-size slots: the first job's slots (2,048 records)
     are too small for ~40,000/world distinct keys per rank, so every rank falls back to the
     standard gather together; the next jobs use slots sized from the headers and merge
     straight from the all-gather buffer."""

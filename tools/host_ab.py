@@ -33,6 +33,7 @@ def main():
     res = {g: [] for g in engines}
     walls = {g: [] for g in engines}
     gpus = {g: [] for g in engines}
+    split = {g: {"host_launch_ms": [], "host_wait_ms": [], "host_copy_ms": []} for g in engines}
     for _ in range(a.rounds):
         for g, e in engines.items():
             t0 = time.perf_counter()
@@ -41,11 +42,14 @@ def main():
                 t = r.times()
                 walls[g].append(t["wall_ms"])
                 gpus[g].append(t["gpu_ms"])
+                for k in split[g]:
+                    split[g][k].append(t[k])
             res[g].append((time.perf_counter() - t0) * 1e3 / a.steps)
     for g in engines:
         print(f"graph={g}: python loop ms/job mean-of-rounds {statistics.mean(res[g]):.4f} "
               f"min-round {min(res[g]):.4f} | C++ wall median {statistics.median(walls[g]):.4f} "
-              f"| gpu(event) median {statistics.median(gpus[g]):.4f}")
+              f"| gpu(event) median {statistics.median(gpus[g]):.4f} | " +
+              " ".join(f"{k[5:]} {statistics.median(v):.4f}" for k, v in split[g].items()))
 
 
 if __name__ == "__main__":
