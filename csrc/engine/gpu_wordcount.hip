@@ -26,6 +26,7 @@ WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); 
 
 std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCountResult* stats) {
   Impl& m = *impl_;
+  m.sync_clean = false;  // this entry point dirties d_sync
   m.check_input(in);
   m.enqueue_upload(in);
   m.enqueue_map(in);
@@ -42,6 +43,7 @@ std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCoun
 
 WordCountResult GpuWordCount::run_reduce_stage(const PackedKey* keys, u64 n) {
   Impl& m = *impl_;
+  m.sync_clean = false;  // this entry point dirties d_sync
   WordCountResult r;
   const u64 t0 = now_ns();
   LOCUST_HIP_CHECK(hipEventRecord(m.ev[0], m.stream));
@@ -66,6 +68,7 @@ WordCountResult GpuWordCount::run_reduce_stage(const PackedKey* keys, u64 n) {
 std::vector<u32> GpuWordCount::sort_keys(const PackedKey* keys, u64 n,
                                          std::vector<PackedKey>* sorted) {
   Impl& m = *impl_;
+  m.sync_clean = false;  // this entry point dirties d_sync
   m.upload_tokens(keys, n);
   m.enqueue_process(0, false, false, n);
   std::vector<u32> perm(n);
@@ -80,6 +83,7 @@ std::vector<u32> GpuWordCount::sort_keys(const PackedKey* keys, u64 n,
 std::vector<PackedKey> GpuWordCount::compact_slots(const u32* line_counts, u32 num_lines,
                                                    const PackedKey* slot_keys) {
   Impl& m = *impl_;
+  m.sync_clean = false;  // this entry point dirties d_sync
   LOCUST_CHECK_ARG(m.cfg.map_path == MapPath::kCompat, "compact_slots needs a compat engine");
   LOCUST_CHECK_ARG(num_lines <= m.cap_lines, "too many lines for engine capacity");
   const u64 E = (u64)m.cfg.emits_per_line;
@@ -107,6 +111,7 @@ std::vector<PackedKey> GpuWordCount::compact_slots(const u32* line_counts, u32 n
 
 WordCountResult GpuWordCount::reduce_sorted(const PackedKey* sorted, u64 n) {
   Impl& m = *impl_;
+  m.sync_clean = false;  // this entry point dirties d_sync
   WordCountResult r;
   m.set_num_records(n);
   m.upload_keys(m.sorted, sorted, n);
@@ -118,6 +123,7 @@ WordCountResult GpuWordCount::reduce_sorted(const PackedKey* sorted, u64 n) {
 
 WordCountResult GpuWordCount::merge_runs(const std::vector<std::vector<KeyCount>>& runs) {
   Impl& m = *impl_;
+  m.sync_clean = false;  // this entry point dirties d_sync
   LOCUST_CHECK_ARG(!runs.empty() && runs.size() <= (size_t)kMaxMergeRunsHost,
                    "need 1..64 runs");
   u64 n = 0;

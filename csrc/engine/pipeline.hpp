@@ -421,8 +421,12 @@ struct DevicePipeline {
     } else if (upload_mode == Upload::kStaged) {
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
     }
-    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+    if (!skip_sync_reset) LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
   }
+  // d_sync is all zero: the last job was a self-cleaning ordered run (see OrderedExtra).
+  // Only run() sets it; every other entry point must clear it before touching d_sync.
+  bool sync_clean = false;
+  bool skip_sync_reset = false;  // enqueue_upload_device leaves out the reset (run() only)
 
   // ---- captured launch sequences (hipGraph), keyed by call site and shape ----
   using GraphKeyArr = std::array<u64, 6>;
@@ -463,9 +467,10 @@ struct DevicePipeline {
     const char* map_text = nullptr;
     Upload mode = Upload::kStaged;
     const OutRecord* out = nullptr;  // the host-mapped output buffer the graph writes
+    bool no_reset = false;           // captured without the d_sync reset (clean start)
     bool operator==(const GraphKey& o) const {
       return bytes == o.bytes && lines == o.lines && src == o.src && map_text == o.map_text &&
-             mode == o.mode && out == o.out;
+             mode == o.mode && out == o.out && no_reset == o.no_reset;
     }
   };
   struct DictGraph {
@@ -483,12 +488,12 @@ struct DevicePipeline {
   // and source; later runs replay it with one hipGraphLaunch.
   void launch_dict_graph(const TextInput& in, bool compat) {
     const GraphKey key{in.bytes, in.num_lines, upload_mode == Upload::kDirect ? in.data : nullptr,
-                       map_text, upload_mode, d_out_mapped};
+                       map_text, upload_mode, d_out_mapped, skip_sync_reset};
     const DictGraph* hit = nullptr;
     for (const auto& g : dict_graphs)
       if (g.key == key) hit = &g;
     if (!hit) {
-      if (dict_graphs.size() >= 4) {  // shapes or buffers changed a lot: drop the oldest
+      if (dict_graphs.size() >= 6) {  // shapes or buffers changed a lot: drop the oldest
         LOCUST_HIP_CHECK(hipGraphExecDestroy(dict_graphs.front().exec));
         dict_graphs.erase(dict_graphs.begin());
       }
@@ -496,7 +501,8 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
       enqueue_upload_device(in);
       enqueue_map(in);
-      const bool ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr);
+      const bool ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr,
+                                            /*self_clean=*/true);
       LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
       hipGraphExec_t exec = nullptr;
       LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -602,10 +608,16 @@ struct DevicePipeline {
   // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
   // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
   bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
-  void enqueue_dict_ordered(bool with_counts, bool mapped) {
+  void enqueue_dict_ordered(bool with_counts, bool mapped, bool self_clean = false) {
+    OrderedExtra ex;
+    if (self_clean) {
+      ex.self_clean = true;
+      ex.map_lb = lb_map;
+      ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+    }
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
-                        lb_dict, stream, ord_trace());
+                        lb_dict, stream, ord_trace(), ex);
   }
   // Diagnostics: LOCUST_ORD_TRACE=1 prints the ordered kernel's per-partition phase times
   // (shader clock ticks) after each run.
@@ -639,9 +651,10 @@ struct DevicePipeline {
     }
   }
   // Process + emit of a dictionary run; returns true if the ordered kernel was used.
-  bool enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process) {
+  bool enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process,
+                        bool self_clean = false) {
     if (!compat && ordered_ok()) {
-      enqueue_dict_ordered(with_counts, /*mapped=*/true);
+      enqueue_dict_ordered(with_counts, /*mapped=*/true, self_clean && cfg.map_path == MapPath::kFast);
       if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
       return true;
     }
@@ -805,6 +818,9 @@ struct DevicePipeline {
   WordCountResult run(const TextInput& in) {
     TraceRange tr("locust:job");
     select_out();  // the previous result may still hold the last output buffer
+    // The previous job left d_sync zeroed (self-cleaning ordered run): no reset this time.
+    const bool clean_start = sync_clean;
+    sync_clean = false;
     if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
         cfg.map_path == MapPath::kFast)
       return run_stream(in);
@@ -816,6 +832,7 @@ struct DevicePipeline {
     const bool compat = cfg.map_path == MapPath::kCompat;
     const bool dict_path = cfg.sort_path == SortPath::kDict;
     const bool graphed = dict_path && use_graph();
+    skip_sync_reset = clean_start && dict_path && !compat;
     LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
     if (graphed) {
       prepare_upload(in);
@@ -831,10 +848,11 @@ struct DevicePipeline {
     if (dict_path) {
       bool ordered = graph_ordered;
       if (!graphed) {
-        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, ev[3]);
+        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, ev[3], /*self_clean=*/true);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
       }
+      skip_sync_reset = false;
       const u64 t_launched = now_ns();
       sync();  // the one host synchronisation of a dictionary run
       const u64 t_synced = now_ns();
@@ -842,6 +860,7 @@ struct DevicePipeline {
       r.times.host_wait_ms = (t_synced - t_launched) * 1e-6;
       *h_ctr = *h_ctr_mapped;
       const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
+      sync_clean = ordered_done && !compat;  // the kernel re-zeroed what this job dirtied
       if (ordered) print_ord_trace();
       if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, false);
       if (!ordered_done && dict_fallback_needed()) {

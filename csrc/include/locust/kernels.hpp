@@ -204,6 +204,13 @@ struct OrderedExtra {
   u64* counts = nullptr;
   SlotHeader* hdr = nullptr;
   SlotHeader tmpl{};
+  // Self-cleaning job (single-GPU run, nothing reads the counters afterwards): unless a
+  // partition overflowed, the last partition re-zeroes `ctr`, this kernel's look-back
+  // scratch and the map's (`map_lb`, map_words status words), so the next job needs no
+  // memset in front.
+  bool self_clean = false;
+  LookbackScratch map_lb{};
+  u32 map_words = 0;
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,

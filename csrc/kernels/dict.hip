@@ -679,8 +679,14 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   ORD_STAMP(5);
   if (trace && threadIdx.x == 0) trace[(u64)p * 8 + 6] = m;
   // ---- the last partition publishes the run's counters ----
+  const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
+  if (p == kDictParts - 1 && ex.self_clean && !ovf_total) {
+    // Every partition has published its inclusive prefix (this one saw them all), so no
+    // one reads the look-back words or the counters any more; the map finished before.
+    for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
+    for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
+  }
   if (p == kDictParts - 1 && threadIdx.x == 0) {
-    const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);
     const u32 u = (u32)(base_m + m);
     const u64 total = base_tok + tok;
     ctr->num_unique = u;
@@ -705,6 +711,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       h.truncated = ctr->truncated;
       h.max_key_len = ctr->max_key_len;
       *ex.hdr = h;
+    }
+    if (ex.self_clean && !ovf_total) {
+      *ctr = MapCounters{};
+      *tile_ctr = 0;
+      *ex.map_lb.tile_counter = 0;
     }
   }
 }
