@@ -610,10 +610,12 @@ struct DevicePipeline {
   bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
   void enqueue_dict_ordered(bool with_counts, bool mapped, bool self_clean = false) {
     OrderedExtra ex;
+    if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
     if (self_clean) {
       ex.self_clean = true;
       ex.map_lb = lb_map;
       ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+      ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
     }
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
@@ -641,13 +643,15 @@ struct DevicePipeline {
     for (int p = 0; p < kDictParts; ++p) {
       const u64* x = &t[p * 8];
       if (!x[0] || !x[6]) continue;
+      const u64 bucketed = x[7] ? x[7] - x[2] : 0;  // part of sort: counting sort by byte 2
       std::fprintf(stderr,
-                   "ord p=%3d m=%5llu start=%6llu build=%6llu publish=%5llu wait=%6llu sort=%6llu "
-                   "write=%6llu end=%6llu\n",
+                   "ord p=%3d m=%5llu start=%6llu build=%6llu publish=%5llu sort=%6llu wait=%6llu "
+                   "write=%6llu end=%6llu bucket=%6llu\n",
                    p, (unsigned long long)x[6], (unsigned long long)(x[0] - t0),
                    (unsigned long long)(x[1] - x[0]), (unsigned long long)(x[2] - x[1]),
                    (unsigned long long)(x[3] - x[2]), (unsigned long long)(x[4] - x[3]),
-                   (unsigned long long)(x[5] - x[4]), (unsigned long long)(x[5] - t0));
+                   (unsigned long long)(x[5] - x[4]), (unsigned long long)(x[5] - t0),
+                   (unsigned long long)bucketed);
     }
   }
   // Process + emit of a dictionary run; returns true if the ordered kernel was used.

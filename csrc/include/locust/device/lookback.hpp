@@ -64,6 +64,43 @@ __device__ __forceinline__ uint64_t wave_lookback(uint64_t* status, uint32_t til
   return excl;
 }
 
+// Split look-back: publish the tile's aggregate now (one lane), do independent work, and
+// resolve the prefix later with wave_lookback_resolve -- successors can already sum this
+// tile's aggregate while it works, so the wait overlaps that work.
+__device__ __forceinline__ void publish_aggregate(uint64_t* status, uint32_t tile,
+                                                  uint64_t aggregate) {
+  st_agent(&status[tile], (tile == 0 ? kLbInc : kLbAgg) | aggregate);
+}
+
+// Second half of a split look-back (all 64 lanes of ONE wave): accumulates the exclusive
+// prefix from predecessors and publishes the inclusive prefix.
+__device__ __forceinline__ uint64_t wave_lookback_resolve(uint64_t* status, uint32_t tile,
+                                                          uint64_t aggregate) {
+  const int lane = lane_id();
+  if (tile == 0) return 0;
+  uint64_t excl = 0;
+  int64_t base = (int64_t)tile - 1;
+  for (;;) {
+    const int64_t idx = base - lane;
+    uint64_t s = (idx >= 0) ? ld_agent(&status[idx]) : kLbInc;
+    const uint32_t flag = (uint32_t)(s >> kLbFlagShift);
+    const uint64_t inc_mask = ballot(flag == 2);
+    const uint64_t inv_mask = ballot(flag == 0);
+    const int first_inc = inc_mask ? (__ffsll((unsigned long long)inc_mask) - 1) : 64;
+    const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
+    if (inv_mask & upto) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    uint64_t v = (lane <= first_inc) ? (s & kLbValMask) : 0;
+    excl += wave_reduce_sum(v);
+    if (first_inc < 64) break;
+    base -= 64;
+  }
+  if (lane == 0) st_agent(&status[tile], kLbInc | (excl + aggregate));
+  return excl;
+}
+
 // Workgroup-level helper: all threads call; wave 0 performs the look-back and the
 // exclusive tile prefix is broadcast through `slot` (an LDS u64).
 __device__ __forceinline__ uint64_t block_lookback(uint64_t* status, uint32_t tile,

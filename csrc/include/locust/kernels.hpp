@@ -194,7 +194,7 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
 // tile counter.  Sets ctr->num_unique / total_count (and ctr_out, if given, like the
 // emit kernels); a partition past kPartSlots distinct keys sets kCtrDictOverflow.
 // `trace` (diagnostics, optional): per partition p, s_memtime stamps at trace[p*8 + 0..5]
-// (start, built, published, prefix known, sorted, written) and the key count at [p*8+6].
+// (start, built, published, sorted, prefix known, written) and the key count at [p*8+6].
 // Optional extra outputs of the ordered build (the distributed map): the sorted distinct
 // keys as KeyCount records and/or SoA keys + counts, and the gather slot's header (`tmpl`
 // completed on the device by the last partition).  `out` may then be null.
@@ -205,12 +205,14 @@ struct OrderedExtra {
   SlotHeader* hdr = nullptr;
   SlotHeader tmpl{};
   // Self-cleaning job (single-GPU run, nothing reads the counters afterwards): unless a
-  // partition overflowed, the last partition re-zeroes `ctr`, this kernel's look-back
-  // scratch and the map's (`map_lb`, map_words status words), so the next job needs no
-  // memset in front.
+  // partition overflowed, the last workgroup to finish re-zeroes `ctr`, this kernel's
+  // look-back scratch and the map's (`map_lb`, map_words status words), so the next job
+  // needs no memset in front.
   bool self_clean = false;
   LookbackScratch map_lb{};
   u32 map_words = 0;
+  u32* done_counter = nullptr;  // zeroed counter of finished workgroups (self_clean)
+  u32 variant = 0;              // A/B switches for kernel experiments (LOCUST_ORD_VARIANT)
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,

@@ -346,6 +346,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
 // run kCtrDictOverflow; the host then reruns the Process stage on the HBM-table path.
 // ---------------------------------------------------------------------------------
 constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
+constexpr u32 kRankChunk = 8;                  // candidates per rank work item
+__device__ __forceinline__ u32 div_up_u32(u32 a, u32 b) { return (a + b - 1) / b; }
 constexpr int kOrdOvfShift = 20;
 constexpr int kOrdTokShift = 29;
 
@@ -540,14 +542,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   u64 tok = 0;
   (void)dev::block_exclusive_scan<u64, kPartBlock>(wsum, s_scan, &tok);
   const int any_full = __syncthreads_or(full);
-  // ---- publish (distinct keys, tokens, overflow) and look back ----
+  // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
+  // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
+  if (threadIdx.x == 0) dev::publish_aggregate(status, p, agg);
   ORD_STAMP(2);
-  const u64 pre = dev::block_lookback(status, p, agg, &s_prefix);
-  ORD_STAMP(3);
-  const u64 base_m = pre & kOrdM;
-  const u64 base_tok = pre >> kOrdTokShift;
-  const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   // ---- sort the partition's keys: counting sort on the SECOND key byte (all keys here
   // share the first), then rank inside each second-byte bucket by all-pairs compares --
   // buckets are small, there are few barriers, and no bitonic network over m keys ----
@@ -556,6 +555,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   u32* s_hist = s_list + 6 * kPartSlots;                         // [256]
   u32* s_off = s_hist + 256;                                     // [256]
   u32* s_cur = s_off + 256;                                      // [256]
+  u32* s_ioff = s_cur + 256;                                     // [257] rank work items
+  u32* s_rank = s_ioff + 260;                                    // [kPartSlots]
   if (threadIdx.x < 256) {
     s_hist[threadIdx.x] = 0;
     s_cur[threadIdx.x] = 0;
@@ -575,7 +576,19 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       s_off[4 * l + 1] = ex + h0;
       s_off[4 * l + 2] = ex + h0 + h1;
       s_off[4 * l + 3] = ex + h0 + h1 + h2;
+      // rank work items of a bucket of B keys: B keys x ceil(B / kRankChunk) chunks
+      const u32 i0 = h0 * div_up_u32(h0, kRankChunk), i1 = h1 * div_up_u32(h1, kRankChunk),
+                i2 = h2 * div_up_u32(h2, kRankChunk), i3 = h3 * div_up_u32(h3, kRankChunk);
+      const u32 isum = i0 + i1 + i2 + i3;
+      const u32 iinc = dev::wave_inclusive_scan(isum);
+      const u32 iex = iinc - isum;
+      s_ioff[4 * l] = iex;
+      s_ioff[4 * l + 1] = iex + i0;
+      s_ioff[4 * l + 2] = iex + i0 + i1;
+      s_ioff[4 * l + 3] = iex + i0 + i1 + i2;
+      if (l == 63) s_ioff[256] = iinc;
     }
+    for (u32 a = threadIdx.x; a < m; a += kPartBlock) s_rank[a] = 0;
     __syncthreads();
     for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
       const u64 w = s_w0[a];
@@ -585,33 +598,56 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       s_slotb[q] = s_slot[a];
     }
     __syncthreads();
-    for (u32 q = threadIdx.x; q < m; q += kPartBlock) {
-      const u64 w = s_w0b[q];
-      const u32 sl = s_slotb[q];
-      const u32 b = (u32)(w >> 48) & 0xffu;
-      const u32 lo = s_off[b], hi = lo + s_hist[b];
-      u32 rank = 0;
-      u32 r = lo;
-      for (; r + 4 <= hi; r += 4) {  // loads of 4 candidates in flight
-        u64 ow[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) ow[t] = s_w0b[r + t];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (ow[t] != w) {
-            rank += ow[t] < w;
-          } else if (r + t != q) {
-            rank += ord_greater(w, sl, ow[t], s_slotb[r + t], s_tab);
-          }
+    ORD_STAMP(7);  // bucketed by the second byte
+    {
+      // Ranks inside each bucket, pair-parallel: work item = (key, chunk of kRankChunk
+      // candidates); consecutive lanes take consecutive keys of the same chunk, so the
+      // candidate reads are LDS broadcasts, and every lane of the workgroup is busy even
+      // when a partition has few keys and one big bucket.
+      const u32 items = s_ioff[256];
+      for (u32 e = threadIdx.x; e < items; e += kPartBlock) {
+        u32 lo = 0, hi = 256;  // bucket: the last b with s_ioff[b] <= e
+        while (hi - lo > 1) {
+          const u32 mid = (lo + hi) >> 1;
+          if (s_ioff[mid] <= e) lo = mid; else hi = mid;
         }
+        const u32 b = lo, B = s_hist[b], base = s_off[b];
+        const u32 local = e - s_ioff[b];
+        const u32 chunk = local / B, i = local - chunk * B;
+        const u32 q = base + i;
+        const u64 w = s_w0b[q];
+        const u32 j0 = base + chunk * kRankChunk, j1 = min(j0 + kRankChunk, base + B);
+        u32 cnt = 0;
+        for (u32 j = j0; j < j1; ++j) {
+          const u64 o = s_w0b[j];
+          if (o != w)
+            cnt += o < w;
+          else if (j != q)
+            cnt += ord_greater(w, s_slotb[q], o, s_slotb[j], s_tab);
+        }
+        if (cnt) atomicAdd(&s_rank[q], cnt);
       }
-      for (; r < hi; ++r) rank += (r != q) && ord_greater(w, sl, s_w0b[r], s_slotb[r], s_tab);
-      s_w0[lo + rank] = w;
-      s_slot[lo + rank] = sl;
+      __syncthreads();
+      for (u32 q = threadIdx.x; q < m; q += kPartBlock) {
+        const u64 w = s_w0b[q];
+        const u32 d = s_off[(u32)(w >> 48) & 0xffu] + s_rank[q];
+        s_w0[d] = w;
+        s_slot[d] = s_slotb[q];
+      }
     }
   }
   __syncthreads();
+  ORD_STAMP(3);
+  if (dev::wave_id() == 0) {
+    const u64 e = dev::wave_lookback_resolve(status, p, agg);
+    if (dev::lane_id() == 0) s_prefix = e;
+  }
+  __syncthreads();
+  const u64 pre = s_prefix;
   ORD_STAMP(4);
+  const u64 base_m = pre & kOrdM;
+  const u64 base_tok = pre >> kOrdTokShift;
+  const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   // ---- vals: scan of the counts in sorted order; write the records ----
   constexpr u32 kPer = kPartSlots / kPartBlock;  // items per thread (m <= kPartSlots)
   u64 c[kPer];
@@ -680,12 +716,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   if (trace && threadIdx.x == 0) trace[(u64)p * 8 + 6] = m;
   // ---- the last partition publishes the run's counters ----
   const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
-  if (p == kDictParts - 1 && ex.self_clean && !ovf_total) {
-    // Every partition has published its inclusive prefix (this one saw them all), so no
-    // one reads the look-back words or the counters any more; the map finished before.
-    for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
-    for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
-  }
   if (p == kDictParts - 1 && threadIdx.x == 0) {
     const u32 u = (u32)(base_m + m);
     const u64 total = base_tok + tok;
@@ -712,10 +742,32 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       h.max_key_len = ctr->max_key_len;
       *ex.hdr = h;
     }
-    if (ex.self_clean && !ovf_total) {
-      *ctr = MapCounters{};
-      *tile_ctr = 0;
-      *ex.map_lb.tile_counter = 0;
+  }
+  if (ex.self_clean) {
+    // Self-cleaning job: the LAST workgroup to finish (not partition 255 -- a partition
+    // resolves its prefix from its predecessors' aggregates, so later ones may finish
+    // first while earlier ones still read look-back words) re-zeroes the counters and
+    // every look-back word, unless a partition overflowed (the host then redoes the
+    // Process stage from these counters and resets everything itself).
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();  // release this workgroup's counter / status writes
+      s_count = atomicAdd(ex.done_counter, 1u) == (u32)kDictParts - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (s_count) {
+      __threadfence();  // acquire every other workgroup's
+      const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(flags & kCtrDictOverflow)) {
+        for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
+        for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
+        if (threadIdx.x == 0) {
+          *ctr = MapCounters{};
+          *tile_ctr = 0;
+          *ex.map_lb.tile_counter = 0;
+          *ex.done_counter = 0;
+        }
+      }
     }
   }
 }
