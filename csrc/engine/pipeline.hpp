@@ -288,8 +288,11 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
     // Output records and the counter snapshot are host-mapped: the emit kernel writes them
-    // over PCIe directly (zero-copy), so a dictionary run needs no D2H copy at all.
-    grow_host_out(ucap);
+    // over PCIe directly (zero-copy), so a dictionary run needs no D2H copy at all.  The
+    // kernels that write it directly emit at most kMappedOutMax records (larger results
+    // take the radix path, whose download grows the buffer), so a streaming engine with a
+    // 16M-key dictionary does not pin 800 MB per output buffer.
+    grow_host_out(std::min<u64>(ucap, kMappedOutMax));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                    hipHostMallocMapped | hipHostMallocCoherent));
     LOCUST_HIP_CHECK(
@@ -327,6 +330,8 @@ struct DevicePipeline {
   // A result adopts the buffer its job wrote (EntryList keeps it alive); the next job
   // takes a buffer no result holds any more, so jobs whose results are dropped in turn
   // alternate between two buffers and nothing is ever copied out.
+  static constexpr u64 kMappedOutMax =
+      kPartBuildMaxTokens > (u64)kRankSortMax ? kPartBuildMaxTokens : (u64)kRankSortMax;
   struct HostOut {
     OutRecord* h = nullptr;
     OutRecord* d = nullptr;
