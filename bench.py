@@ -50,6 +50,16 @@ REF_CHART_MB_PER_S = 1e9 / 18.390 / 1e6  # ~54.4 MB/s
 CHUNK_BYTES = 256 << 20  # one device pass; larger shards stream
 
 
+def chunk_bytes_for(nbytes: int) -> int:
+    """Device pass size: mid-size inputs stream in ~3 chunks so the H2D of one overlaps
+    the map + dictionary insert of the previous (43 MB / 1M lines: 3.01 ms in one pass,
+    2.57 ms in 16 MiB chunks, tools/chunk_ab.py, profiles/r1_s2/chunk_sweep.txt); large
+    inputs are PCIe-bound with 256 MiB chunks."""
+    if nbytes <= (32 << 20):
+        return CHUNK_BYTES
+    return max(16 << 20, min(CHUNK_BYTES, (nbytes // 3) & ~((1 << 20) - 1)))
+
+
 def load_text(config: str) -> bytes:
     from locust_amd.utils import oracle
 
@@ -127,7 +137,8 @@ def cold_first_run(text: bytes) -> dict:
 def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
     import locust_amd as lc
 
-    cfg = lc.make_config("gpu", reduce_path="lds", sort=sort, chunk_bytes=CHUNK_BYTES,
+    size = len(text) if isinstance(text, bytes) else text.size
+    cfg = lc.make_config("gpu", reduce_path="lds", sort=sort, chunk_bytes=chunk_bytes_for(size),
                          graph=graph)
     if isinstance(text, bytes):
         nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
@@ -161,7 +172,8 @@ def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, loca
     # refuses two ranks per device); the benchmark itself always uses RCCL.
     device = local_rank if comm == "rccl" else 0
     job = lc.make_config("gpu", device=device, reduce_path="lds", combine=True,
-                         chunk_bytes=CHUNK_BYTES)
+                         chunk_bytes=chunk_bytes_for(len(text) if isinstance(text, bytes)
+                                                     else text.size))
     dcfg = lc.make_dist_config(world, job)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("LOCUST_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
@@ -280,7 +292,7 @@ def main() -> int:
                 f"{'1M lines' if args.config == 'synth1m' else '10 GB'} in total, "
                 f"1/N per GPU generated into pinned host memory")
         model = (f"WordCount {args.config}: dictionary path, streamed in "
-                 f"{CHUNK_BYTES >> 20} MiB chunks, full H2D->D2H job per step")
+                 f"{chunk_bytes_for(nbytes) >> 20} MiB chunks, full H2D->D2H job per step")
         scaling = "strong"
         extra["GB_per_s"] = round(total_bytes / (ms * 1e-3) / 1e9, 3)
         extra["baseline_note"] = ("no published number at this size; baseline_ms = this byte "

@@ -6,8 +6,10 @@
 // every point-to-point xGMI link of the node carries 1/P of each rank's records at once
 // -- unlike a ring, which would serialise on one link per step.  The self bucket is a
 // device-to-device copy.  Small control collectives (samples, counts, totals) are
-// ncclAllGather on a device staging buffer.  Every wait polls ncclCommGetAsyncError with
-// a timeout and aborts the communicator instead of hanging.
+// ncclAllGather on a device staging buffer.  The gather strategy's slots are one
+// ncclAllGather enqueued on the engine's own stream right behind the map (no host round
+// trip; allgather_device).  Every wait polls ncclCommGetAsyncError with a timeout and
+// aborts the communicator instead of hanging.
 #include <rccl/rccl.h>
 
 #include <cstring>

@@ -197,3 +197,22 @@ def test_ordered_partitions_edge_cases(kind):
     ent, ntok, _ = oracle.wordcount(text)
     r = gpu(text, graph=0)
     assert r.num_tokens == ntok and r.entries() == ent
+
+
+@pytest.mark.parametrize("graph", [0, 1])
+def test_zero_copy_results_stay_valid(hamlet, graph):
+    """Results adopt the host-mapped buffer their job wrote: results kept alive across
+    later jobs (different texts, a radix-path fallback, a self-cleaned replay) keep their
+    own entries; dropped results give their buffers back for reuse."""
+    cfg = lc.make_config("gpu", check=True, graph=graph)
+    eng = lc._C.GpuEngine(cfg, len(hamlet) + 1, 1 << 16)
+    texts = [hamlet, oracle.window(hamlet, 0, 700), hamlet, oracle.window(hamlet, 2000, 4000)]
+    many = b"".join(b"k%06d\n" % i for i in range(40000))  # > 32K distinct: radix emit
+    kept = [(t, eng.run(t)) for t in texts + [many]]
+    for _ in range(6):  # dropped results: their buffers are reused
+        assert eng.run(hamlet).num_unique == 5608
+    for t, r in kept:
+        assert r.entries() == oracle.wordcount(t)[0]
+    kept.clear()
+    r = eng.run(hamlet)
+    assert r.entries() == oracle.wordcount(hamlet)[0]
