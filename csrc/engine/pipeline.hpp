@@ -307,6 +307,7 @@ struct DevicePipeline {
     for (auto& g : dict_graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
     if (d_ord_trace) (void)hipFree(d_ord_trace);
+    if (d_map_trace) (void)hipFree(d_map_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -336,9 +337,10 @@ struct DevicePipeline {
     OutRecord* h = nullptr;
     OutRecord* d = nullptr;
     u64 cap = 0;
-    explicit HostOut(u64 n) : cap(std::max<u64>(n, 1)) {
+    HostOut(u64 n, bool noncoherent) : cap(std::max<u64>(n, 1)) {
       LOCUST_HIP_CHECK(hipHostMalloc(&h, cap * sizeof(OutRecord),
-                                     hipHostMallocMapped | hipHostMallocCoherent));
+                                     hipHostMallocMapped | (noncoherent ? hipHostMallocNonCoherent
+                                                                        : hipHostMallocCoherent)));
       LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
     }
     ~HostOut() {
@@ -348,6 +350,12 @@ struct DevicePipeline {
     HostOut& operator=(const HostOut&) = delete;
   };
   std::vector<std::shared_ptr<HostOut>> out_pool;
+  // A/B switch: coarse-grained (non-coherent) output buffers, written through the GPU L2
+  // and flushed at kernel end, instead of fine-grained ones written straight over PCIe.
+  const bool out_noncoherent = [] {
+    const char* e = std::getenv("LOCUST_OUT_NONCOHERENT");
+    return e && std::atoi(e) != 0;
+  }();
   size_t out_idx = 0;
   void use_out(size_t i) {
     out_idx = i;
@@ -360,7 +368,7 @@ struct DevicePipeline {
     if (!out_pool.empty() && out_pool[out_idx].use_count() == 1) return;
     for (size_t i = 0; i < out_pool.size(); ++i)
       if (out_pool[i].use_count() == 1) return use_out(i);
-    out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+    out_pool.push_back(std::make_shared<HostOut>(h_out_cap, out_noncoherent));
     use_out(out_pool.size() - 1);
   }
   // ... with room for n records (grown when a radix-path result has more distinct keys
@@ -369,7 +377,7 @@ struct DevicePipeline {
     select_out();
     if (n <= h_out_cap) return;
     sync();  // the device may still write the buffer being replaced
-    out_pool[out_idx] = std::make_shared<HostOut>(n);
+    out_pool[out_idx] = std::make_shared<HostOut>(n, out_noncoherent);
     use_out(out_idx);
   }
   // Pinned staging for key up/downloads (stage-split paths only), allocated on demand.
@@ -534,7 +542,7 @@ struct DevicePipeline {
     } else {
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
-                      stream);
+                      stream, map_trace());
     }
   }
 
@@ -637,6 +645,34 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 8 * sizeof(u64)));
     }
     return d_ord_trace;
+  }
+  // Diagnostics: LOCUST_MAP_TRACE=1 prints the fast map kernel's per-tile timeline (us,
+  // device-wide real-time clock) after each run.
+  u64* d_map_trace = nullptr;
+  u64* map_trace() {
+    static const bool on = std::getenv("LOCUST_MAP_TRACE") != nullptr;
+    if (!on) return nullptr;
+    if (!d_map_trace) {
+      LOCUST_HIP_CHECK(hipMalloc(&d_map_trace, 4096 * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_map_trace, 0, 4096 * 8 * sizeof(u64)));
+    }
+    return d_map_trace;
+  }
+  void print_map_trace() {
+    if (!d_map_trace) return;
+    std::vector<u64> t(4096 * 8);
+    LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_map_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    u64 t0 = ~0ull;
+    for (int i = 0; i < 4096; ++i)
+      if (t[i * 8]) t0 = std::min(t0, t[i * 8]);
+    for (int i = 0; i < 4096; ++i) {
+      const u64* x = &t[i * 8];
+      if (!x[0] || !x[5]) continue;
+      std::fprintf(stderr, "map tile=%4d entry=%6.2f acquired=%6.2f staged=%6.2f masks=%6.2f "
+                   "prefix=%6.2f done=%6.2f us\n", i, (x[0] - t0) * 0.01, (x[1] - t0) * 0.01,
+                   (x[2] - t0) * 0.01, (x[3] - t0) * 0.01, (x[4] - t0) * 0.01,
+                   (x[5] - t0) * 0.01);
+    }
   }
   void print_ord_trace() {
     if (!d_ord_trace) return;
@@ -871,6 +907,7 @@ struct DevicePipeline {
       const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
       sync_clean = ordered_done && !compat;  // the kernel re-zeroed what this job dirtied
       if (ordered) print_ord_trace();
+      print_map_trace();
       if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, false);
       if (!ordered_done && dict_fallback_needed()) {
         finish_dict_with_radix((u32)in.num_lines);

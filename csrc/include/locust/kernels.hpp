@@ -78,9 +78,10 @@ void launch_compact_slots(const u32* line_counts, u32 num_lines, int emits_per_l
                           LookbackScratch lb, hipStream_t s);
 
 // Byte-parallel tokenizer: tokens compacted in text order straight into `out`.
+// trace (diagnostics, optional): per tile < 4096, s_memrealtime stamps at trace[t*8+0..5].
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
-                     LookbackScratch lb, hipStream_t s);
+                     LookbackScratch lb, hipStream_t s, u64* trace = nullptr);
 
 // ---------------- radix_sort.hip ----------------
 constexpr int kSortBlock = 256;

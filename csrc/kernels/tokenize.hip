@@ -13,13 +13,16 @@
 //    per-line ordinal (for the 20-emit cap) is the popcount of starts since the last
 //    '\n', carried across steps; the ordinal carried INTO a segment comes from a backward
 //    scan to the previous newline, stopped once it exceeds the cap.
-//  * Emit counts are scanned across the 4 waves and across tiles with a decoupled
-//    look-back, then each emitting lane finds its token's length from the delimiter
+//  * Emit counts are summed across the 4 waves; one atomic per tile reserves the tile's
+//    slice of the token array (tokens are not kept in text order across tiles: every
+//    consumer hashes or sorts them, so no ticket and no look-back chain is needed -- the
+//    tiles all start at once and the zero-copy text reads overlap), then each emitting
+//    lane finds its token's length from the delimiter
 //    masks (count-trailing-zeros, no per-byte loop), reads 40 bytes of LDS as five
 //    aligned u64 words, funnel-shifts, masks and byte-swaps them into the big-endian
 //    packed key, and writes it straight into the dense SoA output.  The map output is
-//    born compacted, in text order, so the reference's 116,000-slot thrust::partition
-//    (main.cu:411) has nothing left to do.
+//    born compacted, so the reference's 116,000-slot thrust::partition (main.cu:411) has
+//    nothing left to do.
 #include "locust/device/hash.hpp"
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
@@ -34,7 +37,7 @@ using dev::lane_id;
 using dev::lanes_below;
 using dev::wave_id;
 
-constexpr int kPre = 64;   // left context staged before the tile
+constexpr int kPre = 64;   // left context staged before the tile (line-ordinal scans)
 constexpr int kPost = 64;  // right overhang staged after the tile (>= 40 for packing)
 
 // Delimiter set incl. '\n' and NUL, held in scalar registers.
@@ -94,32 +97,47 @@ template <int kSteps>
 __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace) {
+  // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
+  // at entry, tile acquired, text staged, masks done, prefix known, keys written.
+  const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+#define MAP_STAMP(k_)                                                           \
+  if (trace && threadIdx.x == 0 && tile < 4096) trace[(u64)tile * 8 + (k_)] = __builtin_amdgcn_s_memrealtime()
   constexpr int kSeg = kSteps * 64;
   constexpr int kTile = (kMapBlock / 64) * kSeg;
   constexpr int kStaged = kPre + kTile + kPost;
   __shared__ __attribute__((aligned(16))) unsigned char s_text[kStaged];
-  __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
   __shared__ u32 s_wave_cnt[kMapBlock / 64];
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
-  const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);  // contains __syncthreads
+  // Tokens are emitted in no particular order across tiles (every consumer sorts or
+  // hashes them), so a tile is simply its block index: no ticket atomic, no look-back.
+  const u32 tile = blockIdx.x;
   if (tile >= num_tiles) return;
+  if (trace && threadIdx.x == 0 && tile < 4096) trace[(u64)tile * 8] = t_entry;
+  MAP_STAMP(1);
 
   // ---- stage the tile (+ context) into LDS with 16-B loads ----
   const i64 tile_base = (i64)tile * kTile;
   const i64 lo = tile_base - kPre;
+  // Every text buffer carries >= 16 readable bytes past its end (the engine's padding), so
+  // a chunk that starts inside the text is one 16-B load; its bytes past the end read as
+  // '\n' like global_byte's.  Only chunks wholly outside the text are synthesised.
   for (int c = threadIdx.x; c < kStaged / 16; c += kMapBlock) {
     const i64 g = lo + (i64)c * 16;
-    if (g >= 0 && (u64)(g + 16) <= bytes) {
-      *reinterpret_cast<uint4*>(s_text + c * 16) = *reinterpret_cast<const uint4*>(text + g);
+    if (g >= 0 && (u64)g < bytes) {
+      uint4 v = *reinterpret_cast<const uint4*>(text + g);
+      *reinterpret_cast<uint4*>(s_text + c * 16) = v;
+      if ((u64)(g + 16) > bytes)
+        for (int k = (int)(bytes - (u64)g); k < 16; ++k) s_text[c * 16 + k] = (unsigned char)'\n';
     } else {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) s_text[c * 16 + k] = (unsigned char)global_byte(text, bytes, g + k);
+      const uint32_t nl4 = 0x0a0a0a0au;
+      *reinterpret_cast<uint4*>(s_text + c * 16) = uint4{nl4, nl4, nl4, nl4};
     }
   }
   __syncthreads();
+  MAP_STAMP(2);
   const TileText<kStaged> tt{s_text, lo, text, bytes};
   const i64 seg = tile_base + (i64)w * kSeg;
   const int seg_lds = kPre + w * kSeg;
@@ -168,6 +186,7 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
   // ---- phase 2: wave counts -> tile prefix (look-back) ----
   if (lane == 0) s_wave_cnt[w] = emitted;
   __syncthreads();
+  MAP_STAMP(3);
   u32 wave_excl = 0, tile_total = 0;
 #pragma unroll
   for (int i = 0; i < kMapBlock / 64; ++i) {
@@ -175,7 +194,11 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
     if (i < w) wave_excl += v;
     tile_total += v;
   }
-  const u64 prefix = dev::block_lookback(status, tile, tile_total, &s_prefix);
+  // this tile's slice of the token array: one atomic per tile
+  if (threadIdx.x == 0) s_prefix = tile_total ? atomicAdd(&ctr->num_records, tile_total) : 0;
+  __syncthreads();
+  const u64 prefix = s_prefix;
+  MAP_STAMP(4);
   if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
 
   // ---- phase 3: length from masks, pack from LDS words, write ----
@@ -229,14 +252,15 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
   maxlen = dev::wave_reduce_max(maxlen);
   if (lane == 0 && trunc) atomicAdd(&ctr->truncated, trunc);
   if (lane == 0 && maxlen > (u32)max_key) atomicMax(&ctr->max_key_len, maxlen);
-  if (tile == num_tiles - 1 && threadIdx.x == 0) ctr->num_records = (u32)(prefix + tile_total);
+  MAP_STAMP(5);
+#undef MAP_STAMP
 }
 
 }  // namespace
 
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
-                     LookbackScratch lb, hipStream_t s) {
+                     LookbackScratch lb, hipStream_t s, u64* trace) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   if (bytes < kMapLargeInput) {
@@ -244,13 +268,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsSmall><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter);
+        lb.tile_counter, trace);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter);
+        lb.tile_counter, trace);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }
