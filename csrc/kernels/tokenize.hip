@@ -93,8 +93,8 @@ __device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32
   return count > cap + 1 ? cap + 1 : count;
 }
 
-template <int kSteps>
-__global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
+template <int kSteps, int kBlock>
+__global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace) {
@@ -104,11 +104,11 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
 #define MAP_STAMP(k_)                                                           \
   if (trace && threadIdx.x == 0 && tile < 4096) trace[(u64)tile * 8 + (k_)] = __builtin_amdgcn_s_memrealtime()
   constexpr int kSeg = kSteps * 64;
-  constexpr int kTile = (kMapBlock / 64) * kSeg;
+  constexpr int kTile = (kBlock / 64) * kSeg;
   constexpr int kStaged = kPre + kTile + kPost;
   __shared__ __attribute__((aligned(16))) unsigned char s_text[kStaged];
   __shared__ u64 s_prefix;
-  __shared__ u32 s_wave_cnt[kMapBlock / 64];
+  __shared__ u32 s_wave_cnt[kBlock / 64];
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
   // Tokens are emitted in no particular order across tiles (every consumer sorts or
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
   // Every text buffer carries >= 16 readable bytes past its end (the engine's padding), so
   // a chunk that starts inside the text is one 16-B load; its bytes past the end read as
   // '\n' like global_byte's.  Only chunks wholly outside the text are synthesised.
-  for (int c = threadIdx.x; c < kStaged / 16; c += kMapBlock) {
+  for (int c = threadIdx.x; c < kStaged / 16; c += kBlock) {
     const i64 g = lo + (i64)c * 16;
     if (g >= 0 && (u64)g < bytes) {
       uint4 v = *reinterpret_cast<const uint4*>(text + g);
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kMapBlock) void map_fast_kernel(
   MAP_STAMP(3);
   u32 wave_excl = 0, tile_total = 0;
 #pragma unroll
-  for (int i = 0; i < kMapBlock / 64; ++i) {
+  for (int i = 0; i < kBlock / 64; ++i) {
     const u32 v = s_wave_cnt[i];
     if (i < w) wave_excl += v;
     tile_total += v;
@@ -264,15 +264,19 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   if (bytes < kMapLargeInput) {
-    constexpr int kTile = (kMapBlock / 64) * kMapSegStepsSmall * 64;
-    const u64 tiles = div_up(bytes, (u64)kTile);
-    map_fast_kernel<kMapSegStepsSmall><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
+    // Small inputs: 1 KiB tiles as 16 waves x ONE 64-byte step -- the same text per
+    // workgroup (and the same PCIe reads), the least serial work per wave.  Measured A/B
+    // in one process against 4 waves x 4 steps, 8 x 2 and 8 x 1 (profiles/r1_s2/
+    // map_shape_ab.txt): 1-3 % faster whole jobs.
+    const u64 tiles = div_up(bytes, (u64)kMapTileBytesMin);
+    constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
+    map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
         lb.tile_counter, trace);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
-    map_fast_kernel<kMapSegStepsLarge><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
+    map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
         lb.tile_counter, trace);
   }
