@@ -211,6 +211,7 @@ __device__ __forceinline__ void load_key(ConstKeysSoA t, u32 i, u64* k) {
 constexpr int kPartBlock = 1024;       // 16 waves: latency hiding for the gathers
 constexpr int kPartSlots = 2048;       // 80 KB of LDS
 constexpr int kPartWindow = kPartBlock * 16;  // partition bytes scanned per round
+constexpr u32 kOrdTagWindow = kPartBlock * 32;  // ordered build: tags scanned per round
 constexpr int kPartPerThread = kPartSlots / kPartBlock;
 
 __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h) {
@@ -373,20 +374,27 @@ struct TagSource {
   // Inserts partition p's tokens into `s_tab`; `s_list` / `s_count` are LDS scratch.
   // Returns true if the table overflowed.
   __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+    // Rounds of kOrdTagWindow tags (32 per thread, two 16-B loads, the next round's
+    // prefetched): whole Hamlet (32,940 tokens) is one round + a short tail instead of
+    // three.  A round appends at most kPartWindow matches to the list; a partition with
+    // more in one window (over half of all tokens) reports an overflow, and the host
+    // redoes the Process stage on the HBM-table path.
     const u32 n = min(*d_n, n_cap);
     bool full = false;
-    u32 pos = threadIdx.x * 16u;
-    uint4 v = pos < n ? *reinterpret_cast<const uint4*>(parts + pos) : uint4{0, 0, 0, 0};
-    for (u32 round = 0; round < n; round += kPartWindow, pos += kPartWindow) {
+    u32 pos = threadIdx.x * 32u;
+    uint4 v0 = pos < n ? *reinterpret_cast<const uint4*>(parts + pos) : uint4{0, 0, 0, 0};
+    uint4 v1 = pos + 16 < n ? *reinterpret_cast<const uint4*>(parts + pos + 16) : uint4{0, 0, 0, 0};
+    for (u32 round = 0; round < n; round += kOrdTagWindow, pos += kOrdTagWindow) {
       u32 mask = 0;
-      const u32 wv[4] = {v.x, v.y, v.z, v.w};
+      const u32 wv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
           if (((wv[q] >> (8 * b)) & 0xffu) == p && pos + (u32)(q * 4 + b) < n) mask |= 1u << (q * 4 + b);
-      const u32 next = pos + kPartWindow;
-      if (next < n) v = *reinterpret_cast<const uint4*>(parts + next);
+      const u32 next = pos + kOrdTagWindow;
+      if (next < n) v0 = *reinterpret_cast<const uint4*>(parts + next);
+      if (next + 16 < n) v1 = *reinterpret_cast<const uint4*>(parts + next + 16);
       {
         // one LDS atomic per wave: the wave's matches are appended as one run
         const u32 nm = (u32)__popc(mask);
@@ -398,12 +406,14 @@ struct TagSource {
         while (mask) {
           const int b = __ffs(mask) - 1;
           mask &= mask - 1;
-          s_list[at++] = pos + (u32)b;
+          if (at < (u32)kPartWindow) s_list[at] = pos + (u32)b;
+          ++at;
         }
       }
       __syncthreads();
       const u32 cnt = s_count;
-      for (u32 e = threadIdx.x; e < cnt; e += kPartBlock) {
+      full |= cnt > (u32)kPartWindow;
+      for (u32 e = threadIdx.x; e < min(cnt, (u32)kPartWindow); e += kPartBlock) {
         const u32 i = s_list[e];
         u64 k[kKeyWords];
         load_key(tokens, i, k);
