@@ -508,7 +508,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __shared__ __attribute__((aligned(16))) u32 s_list[kPartWindow];  // later: sort arrays
   __shared__ u32 s_count;
   __shared__ u64 s_scan[kPartBlock / 64 + 1];
-  __shared__ u32 s_scan32[kPartBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
   const u32 p = dev::acquire_tile(tile_ctr, &s_tile);  // partition = ticket: key order
@@ -535,8 +534,15 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       wsum += sl.count;
     }
   }
-  u32 m = 0;
-  const u32 excl = dev::block_exclusive_scan<u32, kPartBlock>(mine, s_scan32, &m);
+  // ONE block scan carries all three sums: [tokens:41][full threads:11][distinct keys:12]
+  u64 packed_total = 0;
+  const u64 packed = (u64)mine | ((u64)(full ? 1 : 0) << 12) | (wsum << 23);
+  const u64 packed_excl =
+      dev::block_exclusive_scan<u64, kPartBlock>(packed, s_scan, &packed_total);
+  const u32 excl = (u32)(packed_excl & 0xfffu);
+  const u32 m = (u32)(packed_total & 0xfffu);
+  const int any_full = ((packed_total >> 12) & 0x7ffu) != 0;
+  const u64 tok = packed_total >> 23;
   {
     u32 d = excl;
 #pragma unroll
@@ -549,9 +555,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       }
     }
   }
-  u64 tok = 0;
-  (void)dev::block_exclusive_scan<u64, kPartBlock>(wsum, s_scan, &tok);
-  const int any_full = __syncthreads_or(full);
+  __syncthreads();  // the compacted (w0, slot) arrays are complete
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
