@@ -619,26 +619,38 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       // candidate reads are LDS broadcasts, and every lane of the workgroup is busy even
       // when a partition has few keys and one big bucket.
       const u32 items = s_ioff[256];
-      for (u32 e = threadIdx.x; e < items; e += kPartBlock) {
-        u32 lo = 0, hi = 256;  // bucket: the last b with s_ioff[b] <= e
+      u32 b = 0;
+      if (threadIdx.x < items) {  // bucket of the first item: the last b with s_ioff[b] <= e
+        u32 lo = 0, hi = 256;
         while (hi - lo > 1) {
           const u32 mid = (lo + hi) >> 1;
-          if (s_ioff[mid] <= e) lo = mid; else hi = mid;
+          if (s_ioff[mid] <= threadIdx.x) lo = mid; else hi = mid;
         }
-        const u32 b = lo, B = s_hist[b], base = s_off[b];
+        b = lo;
+      }
+      for (u32 e = threadIdx.x; e < items; e += kPartBlock) {
+        while (s_ioff[b + 1] <= e) ++b;  // later items: a few buckets further at most
+        const u32 B = s_hist[b], base = s_off[b];
         const u32 local = e - s_ioff[b];
         const u32 chunk = local / B, i = local - chunk * B;
         const u32 q = base + i;
         const u64 w = s_w0b[q];
         const u32 j0 = base + chunk * kRankChunk, j1 = min(j0 + kRankChunk, base + B);
+        // all candidates' loads in flight at once; past the bucket end the sentinel ~0
+        // (no key is all 0xFF bytes) counts as neither smaller nor equal
+        u64 o[kRankChunk];
+#pragma unroll
+        for (u32 t = 0; t < kRankChunk; ++t) o[t] = j0 + t < j1 ? s_w0b[j0 + t] : ~0ull;
         u32 cnt = 0;
-        for (u32 j = j0; j < j1; ++j) {
-          const u64 o = s_w0b[j];
-          if (o != w)
-            cnt += o < w;
-          else if (j != q)
-            cnt += ord_greater(w, s_slotb[q], o, s_slotb[j], s_tab);
+        bool tie = false;
+#pragma unroll
+        for (u32 t = 0; t < kRankChunk; ++t) {
+          cnt += o[t] < w ? 1u : 0u;
+          tie |= o[t] == w && j0 + t != q;
         }
+        if (tie)  // keys sharing their first 8 bytes: order by the remaining words
+          for (u32 j = j0; j < j1; ++j)
+            if (j != q && s_w0b[j] == w) cnt += ord_greater(w, s_slotb[q], w, s_slotb[j], s_tab);
         if (cnt) atomicAdd(&s_rank[q], cnt);
       }
       __syncthreads();
