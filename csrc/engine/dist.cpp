@@ -390,7 +390,12 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
 
   // ---------------- reduce, one allgather of {status, totals} ----------------
   u64 total = 0, uniq = 0;
-  if (!st3) st3 = local("reduce", [&] { eng.reduce_received(n_recv, &total, &uniq); });
+  if (!st3)
+    st3 = local("reduce", [&] {
+      std::vector<u64> runs((size_t)P);
+      for (int p = 0; p < P; ++p) runs[(size_t)p] = rb[(size_t)p] / sizeof(KeyCount);
+      eng.reduce_received_runs(runs, r.num_tokens, run_flags, &total, &uniq);
+    });
   Msg3 m3{st3, 0, total, uniq};
   std::vector<Msg3> all3((size_t)P);
   comm.allgather_host(&m3, all3.data(), sizeof(Msg3));

@@ -354,6 +354,39 @@ class GpuShardEngine final : public ShardEngine {
     return rp_->d_records;
   }
 
+  void reduce_received_runs(const std::vector<u64>& run_lens, u64 total_tokens, u32 run_flags,
+                            u64* total_count, u64* num_unique) override {
+    u64 n = 0;
+    for (u64 l : run_lens) n += l;
+    const bool mergeable = (run_flags & kRecordsSorted) && (run_flags & kRecordsDistinct) &&
+                           run_lens.size() <= (size_t)kMaxMergeRunsHost && n &&
+                           n <= kMergeMaxRecords && total_tokens <= kMergeMaxCount;
+    if (!mergeable) return reduce_received(n, total_count, num_unique);
+    // The shuffle delivered one sorted slice of distinct keys per rank, back to back in
+    // rank order: merge them (binary-search positions + one look-back scan) straight
+    // into host-mapped output -- no dictionary rebuild, no sort.
+    DevicePipeline& r = *rp_;
+    r.select_out();
+    r.grow_host_out(n);
+    u32* meta = reinterpret_cast<u32*>(r.h_u64);  // pinned; read by the copy below
+    meta[0] = (u32)run_lens.size();
+    for (size_t q = 0; q < run_lens.size(); ++q) meta[1 + q] = (u32)run_lens[q];
+    u32* d_meta = reinterpret_cast<u32*>(r.d_offsets);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + run_lens.size()) * sizeof(u32),
+                                    hipMemcpyHostToDevice, r.stream));
+    launch_merge_sorted_runs(r.d_records, r.d_records + run_lens[0], d_meta, n,
+                             reinterpret_cast<KeyCount*>(r.d_out), r.d_ctr, r.d_out_mapped,
+                             r.d_ctr_mapped, r.lb_merge(n), r.stream);
+    r.sync();
+    *r.h_ctr = *r.h_ctr_mapped;
+    WordCountResult tmp;
+    r.fill_counters(tmp);
+    r.copy_out(tmp.entries, r.h_ctr->num_unique);
+    *total_count = r.h_ctr->total_count;
+    *num_unique = r.h_ctr->num_unique;
+    range_entries_ = std::move(tmp.entries);
+  }
+
   void reduce_received(u64 n, u64* total_count, u64* num_unique) override {
     DevicePipeline& r = *rp_;
     r.select_out();  // the previous job's entries may still hold the last output buffer

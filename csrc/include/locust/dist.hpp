@@ -127,6 +127,16 @@ class ShardEngine {
   virtual void* recv_records(u64 n) = 0;       // room for n incoming KeyCount records
   // Sort + weighted reduce of the n received records; returns {total_count, num_unique}.
   virtual void reduce_received(u64 n, u64* total_count, u64* num_unique) = 0;
+  // Same, knowing the layout: run_lens[p] records from rank p, back to back in rank
+  // order, each run a slice of that rank's sorted records (run_flags: the AND of every
+  // rank's record_flags(); total_tokens bounds the runs' summed counts).  Sorted runs of
+  // distinct keys are merged instead of re-aggregated.
+  virtual void reduce_received_runs(const std::vector<u64>& run_lens, u64 total_tokens,
+                                    u32 run_flags, u64* total_count, u64* num_unique) {
+    u64 n = 0;
+    for (u64 l : run_lens) n += l;
+    reduce_received(n, total_count, num_unique);
+  }
   // Gather strategy, root only: reduce this rank's own records together with the records
   // the other ranks sent (already in recv_records(), which holds room for both), back to
   // back in rank order; run_lens[i] = records from rank i+1 (each such run is sorted).
