@@ -621,15 +621,17 @@ struct DevicePipeline {
   // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
   // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
   bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
+  // Fills the self-clean fields of an OrderedExtra (see OrderedExtra::self_clean).
+  void set_self_clean(OrderedExtra& ex) const {
+    ex.self_clean = true;
+    ex.map_lb = lb_map;
+    ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+    ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
+  }
   void enqueue_dict_ordered(bool with_counts, bool mapped, bool self_clean = false) {
     OrderedExtra ex;
     if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
-    if (self_clean) {
-      ex.self_clean = true;
-      ex.map_lb = lb_map;
-      ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
-      ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
-    }
+    if (self_clean) set_self_clean(ex);
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
                         lb_dict, stream, ord_trace(), ex);

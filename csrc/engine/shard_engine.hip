@@ -54,6 +54,7 @@ class GpuShardEngine final : public ShardEngine {
       m.sync();
       return complete_small_ordered(shard);
     }
+    m.sync_clean = false;  // the paths below dirty the scratch without re-zeroing it
     if (combine && cfg_.sort_path == SortPath::kDict) {
       if (plan == DistStrategy::kGather) {
         // Gather plan: the combined records go to rank 0 unsorted, straight from the
@@ -139,6 +140,12 @@ class GpuShardEngine final : public ShardEngine {
     ex.counts = m.d_sorted_counts;
     ex.hdr = hdr;
     ex.tmpl = tmpl;
+    // Back-to-back small passes: the ordered kernel re-zeroes the scratch it and the map
+    // dirtied, so the next pass skips the reset memset (m.sync_clean; any other use of this
+    // pipeline clears it).
+    m.set_self_clean(ex);
+    m.skip_sync_reset = m.sync_clean;
+    m.sync_clean = false;
     auto enqueue = [&] {
       m.enqueue_upload_device(shard);
       m.enqueue_map(shard);
@@ -152,7 +159,8 @@ class GpuShardEngine final : public ShardEngine {
     };
     m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
     if (m.use_graph())
-      m.launch_cached({(spec_samples ? 2u : 3u) | (hdr ? 0x100u : 0u) | ((u64)slot_recs << 32),
+      m.launch_cached({(spec_samples ? 2u : 3u) | (hdr ? 0x100u : 0u) |
+                           (m.skip_sync_reset ? 0x200u : 0u) | ((u64)slot_recs << 32),
                        shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text),
                        (u64)m.upload_mode,
                        m.upload_mode == DevicePipeline::Upload::kDirect
@@ -160,6 +168,7 @@ class GpuShardEngine final : public ShardEngine {
                       enqueue);
     else
       enqueue();
+    m.skip_sync_reset = false;
   }
   // After the sync of an enqueue_small_ordered: the map statistics, or the local redo on
   // the HBM table when a partition overflowed its LDS table.
@@ -167,6 +176,7 @@ class GpuShardEngine final : public ShardEngine {
     DevicePipeline& m = *mp_;
     *m.h_ctr = *m.h_ctr_mapped;
     if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+      m.sync_clean = true;  // the kernel re-zeroed the scratch (see enqueue_small_ordered)
       if (spec_samples_) {
         samples_.assign(m.h_small, m.h_small + kSpecSamples);
         samples_valid_ = true;
@@ -300,6 +310,7 @@ class GpuShardEngine final : public ShardEngine {
   void prepare_shuffle() override {
     if (sorted_local_) return;
     DevicePipeline& m = *mp_;
+    m.sync_clean = false;
     if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
       m.enqueue_rank();  // ranks are zero: reset with the table / written by the build
       m.enqueue_sorted_from_dict();

@@ -205,10 +205,10 @@ struct OrderedExtra {
   u64* counts = nullptr;
   SlotHeader* hdr = nullptr;
   SlotHeader tmpl{};
-  // Self-cleaning job (single-GPU run, nothing reads the counters afterwards): unless a
-  // partition overflowed, the last workgroup to finish re-zeroes `ctr`, this kernel's
-  // look-back scratch and the map's (`map_lb`, map_words status words), so the next job
-  // needs no memset in front.
+  // Self-cleaning job: unless a partition overflowed, the last workgroup to finish
+  // re-zeroes the accumulated counters of `ctr` (num_unique / total_count keep this run's
+  // values), this kernel's look-back scratch and the map's (`map_lb`, map_words status
+  // words), so the next job needs no memset in front.
   bool self_clean = false;
   LookbackScratch map_lb{};
   u32 map_words = 0;

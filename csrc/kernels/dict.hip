@@ -788,7 +788,14 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
         for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
         if (threadIdx.x == 0) {
-          *ctr = MapCounters{};
+          // the accumulated counters; num_unique / total_count are assignments the next
+          // run overwrites, and stay readable for what follows this kernel
+          ctr->num_records = 0;
+          ctr->overflow_lines = 0;
+          ctr->truncated = 0;
+          ctr->num_newlines = 0;
+          ctr->max_key_len = 0;
+          ctr->flags = 0;
           *tile_ctr = 0;
           *ex.map_lb.tile_counter = 0;
           *ex.done_counter = 0;
