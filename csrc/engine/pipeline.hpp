@@ -76,6 +76,12 @@ struct DevicePipeline {
   u32* d_perm = nullptr;
   u8* d_parts = nullptr;           // hash partition tag per token (partitioned dict build)
   bool parts_ready = false;        // d_parts describes the current `tokens`
+  // Per-tile partition table of the small-input fast map (launch_map_fast part_off), for
+  // engines whose passes can take the ordered kernel; part_tiles > 0: it describes the
+  // current `tokens`.
+  u32* d_part_off = nullptr;
+  u64 part_off_tiles = 0;  // capacity in tiles
+  u32 part_tiles = 0;
   OutRecord* d_out = nullptr;
   KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
   // Records d_records holds (>= cap; at least one minimum-size gather slot).
@@ -189,6 +195,9 @@ struct DevicePipeline {
     for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
     sz.add<u32>(cap);
     sz.add<u8>(align_up(cap, 16) + 16);
+    if (cap <= kPartBuildMaxTokens && cap_bytes < kMapLargeInput)
+      part_off_tiles = div_up(cap_bytes, kMapTileBytesMin);
+    if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartTable);
     sz.add<OutRecord>(cap);
     sz.add<KeyCount>(slot_records_cap() + kSlotHeaderRecords);
     sz.add<PackedKey>(kMaxSamples);
@@ -225,6 +234,7 @@ struct DevicePipeline {
     d_head_count = arena.take<u64>(cap);
     d_perm = arena.take<u32>(cap);
     d_parts = arena.take<u8>(align_up(cap, 16) + 16);
+    if (part_off_tiles) d_part_off = arena.take<u32>(part_off_tiles * kPartTable);
     d_out = arena.take<OutRecord>(cap);
     // room for a gather slot header in front: d_records - kSlotHeaderRecords is the slot
     d_records = arena.take<KeyCount>(slot_records_cap() + kSlotHeaderRecords) + kSlotHeaderRecords;
@@ -525,6 +535,7 @@ struct DevicePipeline {
     }
     graph_ordered = hit->ordered;
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
+    part_tiles = cfg.map_path == MapPath::kFast ? table_tiles(in.bytes) : 0u;
     LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
   }
   bool use_zero_copy(const TextInput& in) const {
@@ -540,9 +551,10 @@ struct DevicePipeline {
       launch_map_compat(d_text, in.bytes, d_nl, (u32)in.num_lines, d_delims, cfg.emits_per_line,
                         cfg.max_key_len, slots, d_line_counts, d_ctr, stream);
     } else {
+      part_tiles = table_tiles(in.bytes);
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
-                      stream, map_trace());
+                      stream, map_trace(), part_tiles ? d_part_off : nullptr);
     }
   }
 
@@ -621,6 +633,20 @@ struct DevicePipeline {
   // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
   // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
   bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
+  // Tiles of the per-tile partition table the fast map writes for an input of `bytes`
+  // (0: no table for this input).
+  u32 table_tiles(u64 bytes) const {
+    const u64 t = div_up(bytes, kMapTileBytesMin);
+    return d_part_off && bytes < kMapLargeInput && t <= part_off_tiles ? (u32)t : 0u;
+  }
+  // The ordered kernel reads partition runs from the map's per-tile table when the current
+  // tokens came from the small-input fast map (unweighted).
+  void set_tile_source(OrderedExtra& ex, bool with_counts) const {
+    if (part_tiles && parts_ready && !with_counts) {
+      ex.part_off = d_part_off;
+      ex.part_tiles = part_tiles;
+    }
+  }
   // Fills the self-clean fields of an OrderedExtra (see OrderedExtra::self_clean).
   void set_self_clean(OrderedExtra& ex) const {
     ex.self_clean = true;
@@ -632,6 +658,7 @@ struct DevicePipeline {
     OrderedExtra ex;
     if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
     if (self_clean) set_self_clean(ex);
+    set_tile_source(ex, with_counts);
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
                         lb_dict, stream, ord_trace(), ex);
@@ -1122,6 +1149,7 @@ struct DevicePipeline {
 
   void upload_tokens(const PackedKey* keys, u64 n) {
     parts_ready = false;
+    part_tiles = 0;
     set_num_records(n);
     upload_keys(tokens, keys, n);
   }

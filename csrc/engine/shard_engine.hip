@@ -149,6 +149,7 @@ class GpuShardEngine final : public ShardEngine {
     auto enqueue = [&] {
       m.enqueue_upload_device(shard);
       m.enqueue_map(shard);
+      m.set_tile_source(ex, false);
       launch_dict_ordered(m.tokens, nullptr, m.d_parts, &m.d_ctr->num_records, m.cap, m.d_ctr,
                           nullptr, m.d_ctr_mapped, m.lb_dict, m.stream, m.ord_trace(), ex);
       if (spec_samples) {
@@ -405,6 +406,7 @@ class GpuShardEngine final : public ShardEngine {
     r.set_num_records(n);
     launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
     r.parts_ready = true;
+    r.part_tiles = 0;  // tokens from records: partition tags only
     WordCountResult tmp;
     bool downloaded = false;
     if (cfg_.sort_path == SortPath::kDict) {

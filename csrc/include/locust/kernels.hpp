@@ -79,9 +79,15 @@ void launch_compact_slots(const u32* line_counts, u32 num_lines, int emits_per_l
 
 // Byte-parallel tokenizer: tokens compacted in text order straight into `out`.
 // trace (diagnostics, optional): per tile < 4096, s_memrealtime stamps at trace[t*8+0..5].
+// part_off (optional, inputs below kMapLargeInput): the tokens of each 1 KiB tile are
+// written grouped by partition (first key byte) and part_off[t * kPartTable + p] is the
+// absolute index of tile t's first partition-p token ([.. + kPartTable - 1] = the tile's
+// end), so a partition's tokens are found without scanning every token's tag.
+constexpr int kPartTable = 257;
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
-                     LookbackScratch lb, hipStream_t s, u64* trace = nullptr);
+                     LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
+                     u32* part_off = nullptr);
 
 // ---------------- radix_sort.hip ----------------
 constexpr int kSortBlock = 256;
@@ -213,6 +219,10 @@ struct OrderedExtra {
   LookbackScratch map_lb{};
   u32 map_words = 0;
   u32* done_counter = nullptr;  // zeroed counter of finished workgroups (self_clean)
+  // Tokens from the small-input fast map with its per-tile partition table (launch_map_fast
+  // part_off): partitions read their token ranges from it instead of scanning the tags.
+  const u32* part_off = nullptr;
+  u32 part_tiles = 0;
   u32 variant = 0;              // A/B switches for kernel experiments (LOCUST_ORD_VARIANT)
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,

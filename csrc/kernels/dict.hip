@@ -429,6 +429,53 @@ struct TagSource {
   }
 };
 
+// Token source of the ordered kernel after the small-input fast map: the map grouped each
+// 1 KiB tile's tokens by partition and recorded where every partition's run starts
+// (launch_map_fast part_off), so workgroup p reads two words per tile instead of
+// scanning the partition tags of every token.
+struct TileSource {
+  ConstKeysSoA tokens;
+  const u32* part_off;
+  u32 ntiles;
+  u32 n_cap;  // token capacity: indices past it were never written
+  __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+    bool full = false;
+    for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
+      const u32 t = t0 + threadIdx.x;
+      u32 a = 0, len = 0;
+      if (t < ntiles) {
+        a = part_off[(u64)t * kPartTable + p];
+        len = part_off[(u64)t * kPartTable + p + 1] - a;
+      }
+      {
+        // one LDS atomic per wave: the wave's runs are appended back to back
+        const u32 incl = dev::wave_inclusive_scan(len);
+        u32 wbase = 0;
+        if (dev::lane_id() == 63 && incl) wbase = atomicAdd(&s_count, incl);
+        wbase = (u32)__shfl((int)wbase, 63, 64);
+        u32 at = wbase + incl - len;
+        for (u32 j = 0; j < len; ++j, ++at)
+          if (at < (u32)kPartWindow) s_list[at] = a + j;
+      }
+      __syncthreads();
+      const u32 cnt = s_count;
+      full |= cnt > (u32)kPartWindow;  // the host redoes the Process stage on the HBM table
+      for (u32 e = threadIdx.x; e < min(cnt, (u32)kPartWindow); e += kPartBlock) {
+        const u32 i = s_list[e];
+        if (i >= n_cap) continue;
+        u64 k[kKeyWords];
+        load_key(tokens, i, k);
+        if (k[0] == 0) continue;
+        full |= !part_lds_insert(s_tab, k, 1ull, key_hash(k));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) s_count = 0;
+      __syncthreads();
+    }
+    return full;
+  }
+};
+
 // Token source of the gather-strategy merge: runs of KeyCount records, each sorted by
 // key (the ranks' combined outputs).  Run 0 is `own`; runs 1.. lie back to back in `recv`.
 // The run count and lengths are read from device memory (`meta` = [nruns, len0, len1,
@@ -1047,9 +1094,15 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace,
                          const OrderedExtra& ex) {
-  const TagSource src{tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
-  dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
-      src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
+  if (ex.part_off && !counts) {
+    const TileSource src{tokens, ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
+    dict_ordered_kernel<TileSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+        src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
+  } else {
+    const TagSource src{tokens, counts, parts, d_n, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
+    dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+        src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
+  }
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -93,11 +93,38 @@ __device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32
   return count > cap + 1 ? cap + 1 : count;
 }
 
+// Length of the token starting at this lane's byte: bit 0 of dmask >> lane is the token's
+// first (non-delimiter) byte; the next step's mask covers a token crossing the step.
+__device__ __forceinline__ u32 token_length(u64 dmask, u64 dmask_next, int lane) {
+  const u64 rest = dmask >> lane;
+  if (rest) return (u32)__ffsll((unsigned long long)rest) - 1;
+  return (u32)(64 - lane) + (dmask_next ? (u32)__ffsll((unsigned long long)dmask_next) - 1 : 64u);
+}
+
+// Big-endian packed key of the `keep` bytes at LDS offset o: five aligned u64 LDS words,
+// funnel-shifted, masked and byte-swapped.
+__device__ __forceinline__ void pack_token(const unsigned char* s_text, int o, u32 keep,
+                                           u64* kw) {
+  const int base = o & ~7;
+  const u32 sh = (u32)(o & 7) * 8u;
+  u64 q[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) q[k] = *reinterpret_cast<const u64*>(s_text + base + 8 * k);
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j) {
+    u64 raw = sh ? ((q[j] >> sh) | (q[j + 1] << (64u - sh))) : q[j];
+    const int rem = (int)keep - 8 * j;
+    if (rem <= 0) raw = 0;
+    else if (rem < 8) raw &= (1ull << (8 * rem)) - 1ull;
+    kw[j] = __builtin_bswap64(raw);
+  }
+}
+
 template <int kSteps, int kBlock>
 __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr, u64* __restrict__ trace) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, u32* __restrict__ part_off) {
   // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
   // at entry, tile acquired, text staged, masks done, prefix known, keys written.
   const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -109,6 +136,8 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char s_text[kStaged];
   __shared__ u64 s_prefix;
   __shared__ u32 s_wave_cnt[kBlock / 64];
+  // partition grouping (kSteps == 1 with part_off): per-partition counts, then offsets
+  __shared__ u32 s_pcnt[kSteps == 1 ? kPartTable : 1];
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
   // Tokens are emitted in no particular order across tiles (every consumer sorts or
@@ -117,6 +146,10 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   if (tile >= num_tiles) return;
   if (trace && threadIdx.x == 0 && tile < 4096) trace[(u64)tile * 8] = t_entry;
   MAP_STAMP(1);
+  if constexpr (kSteps == 1) {
+    if (part_off)
+      for (int i = threadIdx.x; i < kPartTable; i += kBlock) s_pcnt[i] = 0;  // before a barrier
+  }
 
   // ---- stage the tile (+ context) into LDS with 16-B loads ----
   const i64 tile_base = (i64)tile * kTile;
@@ -201,6 +234,55 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   MAP_STAMP(4);
   if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
 
+  // ---- phase 3 (grouped): keys by partition inside the tile's slice ----
+  if constexpr (kSteps == 1) {
+    if (part_off) {
+      const u64 m = emit_mask[0];
+      const bool em = (m >> lane) & 1ull;
+      u64 kw[kKeyWords] = {0, 0, 0, 0};
+      u32 part = 0, loc = 0, len = 0;
+      if (em) {
+        len = token_length(dmask[0], dmask[1], lane);
+        pack_token(s_text, seg_lds + lane, len < (u32)max_key ? len : (u32)max_key, kw);
+        part = (u32)(kw[0] >> 56);
+        loc = atomicAdd(&s_pcnt[part], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x < 64) {  // exclusive scan of the 256 partition counts by one wave
+        const u32 l = threadIdx.x;
+        const u32 h0 = s_pcnt[4 * l], h1 = s_pcnt[4 * l + 1], h2 = s_pcnt[4 * l + 2],
+                  h3 = s_pcnt[4 * l + 3];
+        const u32 sum4 = h0 + h1 + h2 + h3;
+        const u32 inc = dev::wave_inclusive_scan(sum4);
+        const u32 ex = inc - sum4;
+        s_pcnt[4 * l] = ex;
+        s_pcnt[4 * l + 1] = ex + h0;
+        s_pcnt[4 * l + 2] = ex + h0 + h1;
+        s_pcnt[4 * l + 3] = ex + h0 + h1 + h2;
+        if (l == 63) s_pcnt[kDictParts] = inc;
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < kPartTable; i += kBlock)
+        part_off[(u64)tile * kPartTable + i] = (u32)(prefix + s_pcnt[i]);
+      u32 trunc = 0, maxlen = 0;
+      if (em) {
+        const u64 idx = prefix + s_pcnt[part] + loc;
+        if (len > (u32)max_key) trunc = 1;
+        maxlen = len;
+        if (idx < out_cap) {
+#pragma unroll
+          for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
+          if (parts) parts[idx] = (u8)part;
+        }
+      }
+      trunc = dev::wave_reduce_sum(trunc);
+      maxlen = dev::wave_reduce_max(maxlen);
+      if (lane == 0 && trunc) atomicAdd(&ctr->truncated, trunc);
+      if (lane == 0 && maxlen > (u32)max_key) atomicMax(&ctr->max_key_len, maxlen);
+      MAP_STAMP(5);
+      return;
+    }
+  }
   // ---- phase 3: length from masks, pack from LDS words, write ----
   u64 dst = prefix + wave_excl;
   u32 trunc = 0, maxlen = 0;
@@ -209,32 +291,11 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const u64 m = emit_mask[s];
     if (m & (1ull << lane)) {
       const u64 idx = dst + lanes_below(m);
-      const u64 rest = dmask[s] >> lane;  // bit 0 is this (non-delimiter) byte
-      u32 len;
-      if (rest) {
-        len = (u32)__ffsll((unsigned long long)rest) - 1;
-      } else {
-        const u64 nx = dmask[s + 1];
-        len = (u32)(64 - lane) + (nx ? (u32)__ffsll((unsigned long long)nx) - 1 : 64u);
-      }
+      const u32 len = token_length(dmask[s], dmask[s + 1], lane);
       if (len > (u32)max_key) ++trunc;
       maxlen = len > maxlen ? len : maxlen;
-      const u32 keep = len < (u32)max_key ? len : (u32)max_key;
-      const int o = seg_lds + s * 64 + lane;
-      const int base = o & ~7;
-      const u32 sh = (u32)(o & 7) * 8u;
-      u64 q[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) q[k] = *reinterpret_cast<const u64*>(s_text + base + 8 * k);
       u64 kw[kKeyWords];
-#pragma unroll
-      for (int j = 0; j < kKeyWords; ++j) {
-        u64 raw = sh ? ((q[j] >> sh) | (q[j + 1] << (64u - sh))) : q[j];
-        const int rem = (int)keep - 8 * j;
-        if (rem <= 0) raw = 0;
-        else if (rem < 8) raw &= (1ull << (8 * rem)) - 1ull;
-        kw[j] = __builtin_bswap64(raw);
-      }
+      pack_token(s_text, seg_lds + s * 64 + lane, len < (u32)max_key ? len : (u32)max_key, kw);
       if (idx < out_cap) {
 #pragma unroll
         for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
@@ -260,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
 
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
-                     LookbackScratch lb, hipStream_t s, u64* trace) {
+                     LookbackScratch lb, hipStream_t s, u64* trace, u32* part_off) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   if (bytes < kMapLargeInput) {
@@ -272,13 +333,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace);
+        lb.tile_counter, trace, part_off);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace);
+        lb.tile_counter, trace, nullptr);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }
