@@ -670,8 +670,8 @@ struct DevicePipeline {
     static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
     if (!on) return nullptr;
     if (!d_ord_trace) {
-      LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 8 * sizeof(u64)));
-      LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 16 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 16 * sizeof(u64)));
     }
     return d_ord_trace;
   }
@@ -705,23 +705,19 @@ struct DevicePipeline {
   }
   void print_ord_trace() {
     if (!d_ord_trace) return;
-    std::vector<u64> t(kDictParts * 8);
+    std::vector<u64> t(kDictParts * 16);
     LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
-    u64 t0 = ~0ull;
-    for (int p = 0; p < kDictParts; ++p)
-      if (t[p * 8]) t0 = std::min(t0, t[p * 8]);
+    // stamps: 0 start, 1 built, 2 published, 8 histogram, 7 bucketed, 9 ranked, 3 sorted,
+    // 4 prefix known, 5 written; 6 = distinct keys
     for (int p = 0; p < kDictParts; ++p) {
-      const u64* x = &t[p * 8];
+      const u64* x = &t[p * 16];
       if (!x[0] || !x[6]) continue;
-      const u64 bucketed = x[7] ? x[7] - x[2] : 0;  // part of sort: counting sort by byte 2
+      auto d = [&](int a, int b) { return (unsigned long long)(x[a] && x[b] ? x[b] - x[a] : 0); };
       std::fprintf(stderr,
-                   "ord p=%3d m=%5llu start=%6llu build=%6llu publish=%5llu sort=%6llu wait=%6llu "
-                   "write=%6llu end=%6llu bucket=%6llu\n",
-                   p, (unsigned long long)x[6], (unsigned long long)(x[0] - t0),
-                   (unsigned long long)(x[1] - x[0]), (unsigned long long)(x[2] - x[1]),
-                   (unsigned long long)(x[3] - x[2]), (unsigned long long)(x[4] - x[3]),
-                   (unsigned long long)(x[5] - x[4]), (unsigned long long)(x[5] - t0),
-                   (unsigned long long)bucketed);
+                   "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
+                   " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu\n",
+                   p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
+                   d(2, 8), d(8, 7), d(7, 9), d(9, 3));
     }
   }
   // Process + emit of a dictionary run; returns true if the ordered kernel was used.

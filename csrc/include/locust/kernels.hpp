@@ -200,8 +200,9 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
 // room for every distinct key; `lb` needs kDictParts + 1 zeroed status words and a zeroed
 // tile counter.  Sets ctr->num_unique / total_count (and ctr_out, if given, like the
 // emit kernels); a partition past kPartSlots distinct keys sets kCtrDictOverflow.
-// `trace` (diagnostics, optional): per partition p, s_memtime stamps at trace[p*8 + 0..5]
-// (start, built, published, sorted, prefix known, written) and the key count at [p*8+6].
+// `trace` (diagnostics, optional): per partition p, s_memtime stamps at trace[p*16 + k]:
+// 0 start, 1 built, 2 published, 8 histogram, 7 bucketed, 9 ranked, 3 sorted, 4 prefix
+// known, 5 written; the key count at [p*16+6].
 // Optional extra outputs of the ordered build (the distributed map): the sorted distinct
 // keys as KeyCount records and/or SoA keys + counts, and the gather slot's header (`tmpl`
 // completed on the device by the last partition).  `out` may then be null.

@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
 #define ORD_STAMP(k_)                                                          \
-  if (trace && threadIdx.x == 0) trace[(u64)p * 8 + (k_)] = __builtin_amdgcn_s_memtime()
+  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
   __shared__ __attribute__((aligned(16))) u32 s_list[kPartWindow];  // later: sort arrays
   __shared__ u32 s_count;
@@ -651,6 +651,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     }
     for (u32 a = threadIdx.x; a < m; a += kPartBlock) s_rank[a] = 0;
     __syncthreads();
+    ORD_STAMP(8);  // histogram + bucket scan
     for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
       const u64 w = s_w0[a];
       const u32 b = (u32)(w >> 48) & 0xffu;
@@ -701,6 +702,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         if (cnt) atomicAdd(&s_rank[q], cnt);
       }
       __syncthreads();
+      ORD_STAMP(9);  // ranks
       for (u32 q = threadIdx.x; q < m; q += kPartBlock) {
         const u64 w = s_w0b[q];
         const u32 d = s_off[(u32)(w >> 48) & 0xffu] + s_rank[q];
@@ -786,7 +788,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     }
   }
   ORD_STAMP(5);
-  if (trace && threadIdx.x == 0) trace[(u64)p * 8 + 6] = m;
+  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 6] = m;
   // ---- the last partition publishes the run's counters ----
   const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
   if (p == kDictParts - 1 && threadIdx.x == 0) {
