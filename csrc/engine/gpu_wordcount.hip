@@ -145,9 +145,9 @@ WordCountResult GpuWordCount::merge_runs(const std::vector<std::vector<KeyCount>
   LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + runs.size()) * sizeof(u32),
                                   hipMemcpyHostToDevice, m.stream));
   m.grow_host_out(n);
-  launch_merge_sorted_runs(m.d_records, m.d_records + runs[0].size(), d_meta, m.cap,
+  launch_merge_sorted_runs(m.d_records, m.d_records + runs[0].size(), d_meta, n,
                            reinterpret_cast<KeyCount*>(m.d_out), m.d_ctr, m.d_out_mapped,
-                           m.d_ctr_mapped, m.lb_merge(m.cap), m.stream);
+                           m.d_ctr_mapped, m.lb_merge(n), m.stream);
   m.sync();
   *m.h_ctr = *m.h_ctr_mapped;
   WordCountResult r;

@@ -6,18 +6,21 @@
 // (README.md:24).  Here every rank's combined output arrives sorted, so the root does not
 // rebuild a dictionary over them; it merges:
 //
-//   merge_rank   one thread per record: lock-step binary searches in every other run give
-//                the record's position in the stable (key, run) merge order, whether a
-//                lower run already holds the key (then this copy is a duplicate), and --
-//                for the first copy -- the key's total count over all runs.  Records are
-//                scattered to their merged slots (duplicates with count 0).
+//   merge_rank   eight threads per record, one per other run: a binary search in that run
+//                gives the record's position in the stable (key, run) merge order, whether
+//                a lower run already holds the key (then this copy is a duplicate), and --
+//                for the first copy -- the key's total count over all runs; the group sums
+//                its parts by shuffles.  Records are scattered to their merged slots
+//                (duplicates with count 0).
 //   merge_emit   decoupled look-back scan over the merged slots of (#first copies, count
 //                sum): the first copies are compacted into the output with val = the
 //                exclusive prefix of the counts (the reference's val: start index of the
 //                key's run in the globally sorted token array, main.cu:161-208).
 //
-// Runs are at most 64 (one per rank), the lock-step search keeps up to 8 runs' probes in
-// flight per thread, and the output goes straight into host-mapped memory.
+// Runs are at most 64 (one per rank); the output goes straight into host-mapped memory.
+// The search is latency bound (one dependent load per step): a thread per record searching
+// all runs in turn took 41-49 us at 8 runs of ~1.5-5.6 K records, a thread per (record,
+// run) 8-12 us -- eight times the waves to overlap the probe chains (profiles/r1_s4).
 #include "locust/device/lookback.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
@@ -26,23 +29,11 @@ namespace locust {
 namespace {
 
 constexpr int kMergeBlock = 256;
-constexpr int kMergeLanes = 8;                        // runs searched in lock step
+constexpr int kMergeSub = 8;                          // threads per record (runs in flight)
 constexpr int kEmitItems = 4;                          // merged slots per thread
 constexpr int kEmitTile = kMergeBlock * kEmitItems;    // 1,024 slots: 48 KB of LDS staging
 constexpr int kEmitCountBits = 40;                     // look-back value: [firsts:22][counts:40]
 constexpr u64 kEmitCountMask = (1ull << kEmitCountBits) - 1;
-
-// -1 / 0 / +1: order of record key `a` against key `k` (unsigned words, big-endian bytes).
-__device__ __forceinline__ int cmp_key(const KeyCount* a, const u64* k) {
-  const u64 a0 = a->w[0];
-  if (a0 != k[0]) return a0 < k[0] ? -1 : 1;
-#pragma unroll
-  for (int j = 1; j < kKeyWords; ++j) {
-    const u64 aj = a->w[j];
-    if (aj != k[j]) return aj < k[j] ? -1 : 1;
-  }
-  return 0;
-}
 
 // Where the runs are: packed (run 0 = `own`, runs 1.. back to back in `recv`, lengths in
 // `meta` = [nruns, len0, len1, ...]) or all-gathered slots (fixed stride, a SlotHeader in
@@ -62,36 +53,76 @@ struct RunTable {
   const KeyCount* base[kMaxMergeRunsHost];
 };
 
+// Wave 0 builds the run table: lane q reads run q's length (all loads in flight at once --
+// a one-thread loop would pay a memory round trip per run) and a wave scan gives offsets.
 __device__ __forceinline__ void load_runs(const RunsView& v, RunTable& t) {
-  if (threadIdx.x == 0) {
-    u32 acc = 0;
+  static_assert(kMaxMergeRunsHost <= 64, "one lane per run");
+  if (threadIdx.x < 64) {
+    const u32 q = threadIdx.x;
+    u32 nr, len = 0;
+    const KeyCount* base = nullptr;
     if (v.slots) {
-      const u32 nr = min(v.nslots, (u32)kMaxMergeRunsHost);
+      nr = min(v.nslots, (u32)kMaxMergeRunsHost);
       const u64 stride = (u64)kSlotHeaderRecords + v.slot_records;
-      for (u32 q = 0; q < nr; ++q) {
+      if (q < nr) {
         const KeyCount* slot = v.slots + q * stride;
         const SlotHeader* h = reinterpret_cast<const SlotHeader*>(slot);
-        const u32 len = h->status == kSlotOk ? (u32)min(h->n, (u64)v.slot_records) : 0u;
-        t.off[q] = acc;
-        t.base[q] = slot + kSlotHeaderRecords;
-        acc += len;
+        const u32 status = h->status;
+        const u64 n = h->n;
+        len = status == kSlotOk ? (u32)min(n, (u64)v.slot_records) : 0u;
+        base = slot + kSlotHeaderRecords;
       }
-      t.off[nr] = acc;
-      t.nruns = nr;
     } else {
-      const u32 nr = min(v.meta[0], (u32)kMaxMergeRunsHost);
-      for (u32 q = 0; q < nr; ++q) {
-        t.off[q] = acc;
-        t.base[q] = q == 0 ? v.own : v.recv + (acc - v.meta[1]);  // runs 1.. back to back
-        acc += v.meta[1 + q];
-      }
-      t.off[nr] = acc;
+      nr = min(v.meta[0], (u32)kMaxMergeRunsHost);
+      if (q < nr) len = v.meta[1 + q];
+    }
+    const u32 incl = dev::wave_inclusive_scan(len);
+    const u32 excl = incl - len;
+    if (!v.slots && q < nr) base = q == 0 ? v.own : v.recv + (excl - v.meta[1]);  // back to back
+    if (q < nr) {
+      t.off[q] = excl;
+      t.base[q] = base;
+    }
+    if (q + 1 == max(nr, 1u)) {
+      t.off[nr] = nr ? incl : 0u;
       t.nruns = nr;
     }
   }
   __syncthreads();
 }
 
+// Lower bound of key k in one sorted run in global memory (rlen >= 1), on the first key word
+// (one load per step), then the landing record loaded whole; keys sharing their first word
+// with k but smaller walk on (rare).  Returns the position; *eq / *cnt: whether the record
+// there equals k, and its count.
+__device__ __forceinline__ u32 run_lower_bound(const KeyCount* __restrict__ run, u32 rlen,
+                                               const u64* k, bool* eq, u64* cnt) {
+  u32 lo = 0, len = rlen;
+  while (len) {
+    const u32 half = len >> 1;
+    const bool lt = run[lo + half].w[0] < k[0];
+    lo = lt ? lo + half + 1 : lo;
+    len = lt ? len - half - 1 : half;
+  }
+  *eq = false;
+  *cnt = 0;
+  for (; lo < rlen; ++lo) {
+    const KeyCount c = run[lo];
+    if (c.w[0] != k[0]) break;
+    const int cmp = c.w[1] != k[1] ? (c.w[1] < k[1] ? -1 : 1)
+                  : c.w[2] != k[2] ? (c.w[2] < k[2] ? -1 : 1)
+                  : c.w[3] != k[3] ? (c.w[3] < k[3] ? -1 : 1) : 0;
+    if (cmp >= 0) {
+      *eq = cmp == 0;
+      *cnt = c.count;
+      break;
+    }
+  }
+  return lo;
+}
+
+// kMergeSub threads per record, one per run of a group of kMergeSub runs: 8x the waves of a
+// thread-per-record search, so the dependent probe chains of many records overlap.
 __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
     RunsView view, KeyCount* __restrict__ merged, LookbackScratch lb, u32 emit_tiles,
     SlotHeader* __restrict__ hdr_out) {
@@ -99,7 +130,6 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
   if (blockIdx.x == 0) {
     // merge_emit's look-back scratch, reset here (stream order) instead of by a memset
     for (u32 i = threadIdx.x; i < emit_tiles; i += kMergeBlock) lb.status[i] = 0;
-    if (threadIdx.x == 0) *lb.tile_counter = 0;
     // the slot headers for the host (the root needs no separate copy)
     if (hdr_out && view.slots) {
       const u64 stride = (u64)kSlotHeaderRecords + view.slot_records;
@@ -109,81 +139,61 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
   }
   load_runs(view, t);
   const u32 nruns = t.nruns;
-  const u32 total = t.off[nruns];
-  for (u32 g = blockIdx.x * kMergeBlock + threadIdx.x; g < total; g += gridDim.x * kMergeBlock) {
+  const u64 work = (u64)t.off[nruns] * kMergeSub;
+  const u32 sub = threadIdx.x % kMergeSub;
+  // whole groups of kMergeSub lanes enter or leave the loop together (shuffles below)
+  for (u64 gt = (u64)blockIdx.x * kMergeBlock + threadIdx.x; gt < work;
+       gt += (u64)gridDim.x * kMergeBlock) {
+    const u32 g = (u32)(gt / kMergeSub);
     u32 q = 0;
     while (q + 1 < nruns && t.off[q + 1] <= g) ++q;
     const u32 i = g - t.off[q];
-    const KeyCount rec = t.base[q][i];
+    const KeyCount rec = t.base[q][i];  // the same address for the whole group
     const u64 k[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
-    u64 pos = i;
-    u64 count = rec.count;
-    bool first = true;
-    for (u32 r0 = 0; r0 < nruns; r0 += kMergeLanes) {
-      const KeyCount* base[kMergeLanes];
-      u32 lo[kMergeLanes], len[kMergeLanes];
-      bool eq[kMergeLanes];
-#pragma unroll
-      for (int l = 0; l < kMergeLanes; ++l) {
-        const u32 r = r0 + l;
-        const bool live = r < nruns && r != q;
-        base[l] = live ? t.base[r] : nullptr;
-        lo[l] = 0;
-        len[l] = live ? t.off[r + 1] - t.off[r] : 0;
-        eq[l] = false;
-      }
-      // lower_bound in every live run, one probe per run per step (independent loads)
-      for (;;) {
-        bool any = false;
-#pragma unroll
-        for (int l = 0; l < kMergeLanes; ++l) {
-          if (len[l]) {
-            any = true;
-            const u32 half = len[l] >> 1;
-            const int c = cmp_key(base[l] + lo[l] + half, k);
-            if (c < 0) {
-              lo[l] += half + 1;
-              len[l] -= half + 1;
-            } else {
-              eq[l] |= c == 0;  // keys are distinct within a run: lower_bound lands here
-              len[l] = half;
-            }
-          }
-        }
-        if (!any) break;
-      }
-#pragma unroll
-      for (int l = 0; l < kMergeLanes; ++l) {
-        const u32 r = r0 + l;
-        if (r >= nruns || r == q) continue;
-        if (r < q) {
-          pos += lo[l] + (eq[l] ? 1 : 0);  // equal keys of lower runs come first
-          first &= !eq[l];
-        } else {
-          pos += lo[l];
-          if (eq[l]) count += base[l][lo[l]].count;
-        }
+    u32 before = 0;   // records of other runs ordered before this one
+    u32 dup = 0;      // a lower run holds the key: this copy is not the first
+    u64 others = 0;   // counts of the key in higher runs
+    for (u32 r = sub; r < nruns; r += kMergeSub) {
+      const u32 rlen = t.off[r + 1] - t.off[r];
+      if (r == q || !rlen) continue;
+      bool eq;
+      u64 cnt;
+      const u32 lo = run_lower_bound(t.base[r], rlen, k, &eq, &cnt);
+      if (r < q) {
+        before += lo + (eq ? 1 : 0);  // equal keys of lower runs come first
+        dup |= eq ? 1u : 0u;
+      } else {
+        before += lo;
+        others += eq ? cnt : 0;
       }
     }
-    KeyCount out;
 #pragma unroll
-    for (int j = 0; j < kKeyWords; ++j) out.w[j] = k[j];
-    out.count = first ? count : 0;  // later copies of a key carry nothing
-    merged[pos] = out;
+    for (int m = 1; m < kMergeSub; m <<= 1) {
+      before += __shfl_xor(before, m, kMergeSub);
+      dup |= __shfl_xor(dup, m, kMergeSub);
+      others += __shfl_xor(others, m, kMergeSub);
+    }
+    if (sub == 0) {
+      KeyCount out;
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) out.w[j] = k[j];
+      out.count = dup ? 0 : rec.count + others;  // later copies of a key carry nothing
+      merged[(u64)i + before] = out;
+    }
   }
 }
 
 __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
     const KeyCount* __restrict__ merged, RunsView view, MapCounters* __restrict__ ctr,
-    OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr) {
+    OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status) {
   __shared__ u64 s_scan[kMergeBlock / 64 + 1];
-  __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
   __shared__ RunTable t;
   // the tile's output records, staged so that the (host-mapped) writes are full lines
   __shared__ __attribute__((aligned(16))) u64 s_out[kEmitTile * 6];
-  const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
+  // blockIdx order is launch order on CDNA (each XCD dispatches its workgroups in order),
+  // so the look-back needs no ticket: that atomic round trip is ~1 us of a ~5 us tile
+  const u32 tile = blockIdx.x;
   load_runs(view, t);
   const u32 total = t.off[t.nruns];
   const u32 ntiles = total ? (u32)div_up(total, (u64)kEmitTile) : 1u;
@@ -245,13 +255,13 @@ void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters
                        OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
                        SlotHeader* hdr_out, hipStream_t s) {
   const u64 c = cap ? cap : 1;
-  const u32 rank_grid = (u32)std::min<u64>(div_up(c, kMergeBlock), 4096);
+  const u32 rank_grid = (u32)std::min<u64>(div_up(c * kMergeSub, kMergeBlock), 8192);
   const u32 emit_grid = (u32)div_up(c, (u64)kEmitTile);
   merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(v, merged, lb, emit_grid,
                                                                   hdr_out);
   LOCUST_HIP_LAUNCH_CHECK();
   merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, v, ctr, out, ctr_out,
-                                                                  lb.status, lb.tile_counter);
+                                                                  lb.status);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -143,6 +143,22 @@ def test_merge_sorted_runs(nruns, vocab, per_run):
     assert res.num_tokens == sum(c for run in runs for _, c in run)
 
 
+def test_merge_sorted_runs_skewed():
+    """Runs whose key ranges barely overlap: disjoint blocks, one dense run packed between two
+    neighbouring keys of a sparse one, and a run holding every key."""
+    rng = random.Random(7)
+    runs = [[(b"%02d-%05d" % (r, i), rng.randint(1, 9)) for i in range(r * 300)]
+            for r in range(6)]
+    runs.append([(b"m%07d" % (i * 1000), 1) for i in range(3000)])   # sparse
+    runs.append([(b"m%07d" % i, 2) for i in range(1, 999)])          # inside one gap
+    runs.append([(k, 3) for k in sorted({k for run in runs for k, _ in run})])
+    eng = lc.Engine(lc.make_config("gpu"), 1 << 20, 1 << 16)
+    res = eng.merge_runs(runs)
+    want = merge_reference(runs)
+    assert res.entries() == want
+    assert res.num_tokens == sum(c for run in runs for _, c in run)
+
+
 def test_merge_sorted_runs_empty():
     eng = lc.Engine(lc.make_config("gpu"), 1 << 16, 1 << 10)
     res = eng.merge_runs([[], []])
