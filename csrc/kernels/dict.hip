@@ -373,7 +373,9 @@ struct TagSource {
   u32 n_cap;
   // Inserts partition p's tokens into `s_tab`; `s_list` / `s_count` are LDS scratch.
   // Returns true if the table overflowed.
-  __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+  struct Pre {};
+  __device__ Pre prefetch(u32) const { return {}; }
+  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
     // Rounds of kOrdTagWindow tags (32 per thread, two 16-B loads, the next round's
     // prefetched): whole Hamlet (32,940 tokens) is one round + a short tail instead of
     // three.  A round appends at most kPartWindow matches to the list; a partition with
@@ -438,12 +440,25 @@ struct TileSource {
   const u32* part_off;
   u32 ntiles;
   u32 n_cap;  // token capacity: indices past it were never written
-  __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+  // This thread's first run (tile threadIdx.x), loaded before the kernel clears its table
+  // so that the load overlaps the clear and its barrier.
+  struct Pre {
+    u32 a, b;
+  };
+  __device__ Pre prefetch(u32 p) const {
+    const u32 t = threadIdx.x;
+    if (t >= ntiles) return {0, 0};
+    return {part_off[(u64)t * kPartTable + p], part_off[(u64)t * kPartTable + p + 1]};
+  }
+  __device__ bool build(u32 p, Pre pre, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
     bool full = false;
     for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
       const u32 t = t0 + threadIdx.x;
       u32 a = 0, len = 0;
-      if (t < ntiles) {
+      if (t0 == 0) {
+        a = pre.a;
+        len = pre.b - pre.a;
+      } else if (t < ntiles) {
         a = part_off[(u64)t * kPartTable + p];
         len = part_off[(u64)t * kPartTable + p + 1] - a;
       }
@@ -487,7 +502,9 @@ struct RunsSource {
   const KeyCount* own;
   const KeyCount* recv;
   const u32* meta;
-  __device__ bool build(u32 p, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+  struct Pre {};
+  __device__ Pre prefetch(u32) const { return {}; }
+  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
     // s_list: [lo, hi) per run | exclusive prefix of the partition's records | run offsets
     u32* s_lo = s_list;
     u32* s_pre = s_list + 2 * kMaxMergeRuns;
@@ -557,8 +574,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __shared__ u64 s_scan[kPartBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
-  const u32 p = dev::acquire_tile(tile_ctr, &s_tile);  // partition = ticket: key order
+  // partition = blockIdx: workgroups dispatch in launch order (per XCD), which is all the
+  // look-back needs -- a ticket would cost an atomic round trip before any other load
+  const u32 p = blockIdx.x;
   ORD_STAMP(0);
+  const typename Src::Pre first = src.prefetch(p);
   for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
 #pragma unroll
     for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
@@ -566,7 +586,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   if (threadIdx.x == 0) s_count = 0;
   __syncthreads();
-  const bool full = src.build(p, s_tab, s_list, s_count);
+  const bool full = src.build(p, first, s_tab, s_list, s_count);
   ORD_STAMP(1);
   // ---- compact: dense (w0, slot) arrays in the list area ----
   u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
@@ -667,17 +687,15 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       // candidate reads are LDS broadcasts, and every lane of the workgroup is busy even
       // when a partition has few keys and one big bucket.
       const u32 items = s_ioff[256];
-      u32 b = 0;
-      if (threadIdx.x < items) {  // bucket of the first item: the last b with s_ioff[b] <= e
-        u32 lo = 0, hi = 256;
-        while (hi - lo > 1) {
-          const u32 mid = (lo + hi) >> 1;
-          if (s_ioff[mid] <= threadIdx.x) lo = mid; else hi = mid;
-        }
-        b = lo;
-      }
       for (u32 e = threadIdx.x; e < items; e += kPartBlock) {
-        while (s_ioff[b + 1] <= e) ++b;  // later items: a few buckets further at most
+        // bucket of the item: the last b with s_ioff[b] <= e, by an 8-step binary search
+        // every round -- walking on from the previous round's bucket crossed up to ~100
+        // small buckets per 1,024-item stride, one dependent LDS read each (the hot
+        // partitions' rank phase took 16-24 K cycles, most of it in that walk)
+        u32 b = 0;
+#pragma unroll
+        for (u32 step = 128; step; step >>= 1)
+          if (s_ioff[b + step] <= e) b += step;
         const u32 B = s_hist[b], base = s_off[b];
         const u32 local = e - s_ioff[b];
         const u32 chunk = local / B, i = local - chunk * B;
