@@ -574,9 +574,12 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __shared__ u64 s_scan[kPartBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
-  // partition = blockIdx: workgroups dispatch in launch order (per XCD), which is all the
-  // look-back needs -- a ticket would cost an atomic round trip before any other load
-  const u32 p = blockIdx.x;
+  // partition = ticket, not blockIdx: a workgroup then only ever waits in the look-back
+  // on workgroups that are already running.  With blockIdx, kernels of several processes
+  // sharing the GPU (the TCP / loopback rehearsals) could fill the CUs with spinning
+  // workgroups whose predecessors were never dispatched: measured as multi-second stalls
+  // and a hang with four ranks on one GPU.
+  const u32 p = dev::acquire_tile(tile_ctr, &s_tile);
   ORD_STAMP(0);
   const typename Src::Pre first = src.prefetch(p);
   for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
