@@ -193,9 +193,10 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       min_cap = std::min(min_cap, hd[p].slot_cap);
       fallback |= hd[p].status != kSlotOk || hd[p].n > slot_recs;
     }
-    // next job's slot: the largest rank's records + 1/8, within every rank's send buffer
-    // (every rank receives P slots: padding costs P x as much as it saves in refits)
-    const u64 want = align_up(max_n + max_n / 8 + 1, 512);
+    // next job's slot: the largest rank's records + 1/16, within every rank's send buffer
+    // (every rank receives P slots: padding costs P x as much as it saves in refits; at
+    // whole Hamlet 6,144 records instead of 6,656 -- 8 % less all-gather traffic)
+    const u64 want = align_up(max_n + max_n / 16 + 1, 256);
     eng.slot_records = (u32)std::max<u64>(kSlotRecordsMin, std::min<u64>(want, min_cap));
     fallback |= cfg.strategy == DistStrategy::kAuto && sum > cfg.gather_max_records;
     st_slot = local("map", [&] {
