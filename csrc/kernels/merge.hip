@@ -6,8 +6,8 @@
 // (README.md:24).  Here every rank's combined output arrives sorted, so the root does not
 // rebuild a dictionary over them; it merges:
 //
-//   merge_rank   eight threads per record, one per other run: a binary search in that run
-//                gives the record's position in the stable (key, run) merge order, whether
+//   merge_rank   eight threads per record, one per other run: a galloping search in that
+//                run gives the record's position in the stable (key, run) merge order, whether
 //                a lower run already holds the key (then this copy is a duplicate), and --
 //                for the first copy -- the key's total count over all runs; the group sums
 //                its parts by shuffles.  Records are scattered to their merged slots
@@ -20,7 +20,8 @@
 // Runs are at most 64 (one per rank); the output goes straight into host-mapped memory.
 // The search is latency bound (one dependent load per step): a thread per record searching
 // all runs in turn took 41-49 us at 8 runs of ~1.5-5.6 K records, a thread per (record,
-// run) 8-12 us -- eight times the waves to overlap the probe chains (profiles/r1_s4).
+// run) 8-12 us -- eight times the waves to overlap the probe chains -- and galloping from
+// the record's scaled position 9 us (profiles/r1_s4).
 #include "locust/device/lookback.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
