@@ -136,6 +136,8 @@ class RcclComm final : public Communicator {
     wait(stream ? static_cast<hipStream_t>(stream) : stream_);
   }
 
+  bool graph_capturable() const override { return true; }
+
   void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
                  const u64* recv_bytes, const u64* recv_off, void* stream) override {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;

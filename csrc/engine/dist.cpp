@@ -4,6 +4,7 @@
 #include "locust/trace.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <functional>
@@ -41,6 +42,13 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts) {
 }
 
 namespace {
+
+// LOCUST_SLOT_GRAPH=0 keeps the gather-slot job as separate launches (map graph, the
+// collective, merge graph) even when the communicator could be captured.
+bool slot_graph_enabled() {
+  const char* v = std::getenv("LOCUST_SLOT_GRAPH");
+  return !(v && v[0] == '0');
+}
 
 // Weighted quantile splitters from every rank's evenly spaced samples.
 std::vector<PackedKey> choose_splitters(const std::vector<PackedKey>& samples, u32 s,
@@ -171,14 +179,28 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   if (slot_path) {
     TraceRange tr("locust:slot_gather");
     const u32 slot_recs = eng.slot_records ? eng.slot_records : kSlotRecordsMin;
-    void* send = nullptr;
-    st_slot = local("map", [&] { send = eng.enqueue_map_slot(shard, slot_recs); });
-    if (st_slot) send = eng.write_slot_failure();  // the all-gather must still be entered
-    void* recv = eng.slot_buffer((u32)P, slot_recs);
     const u64 slot_bytes = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
-    comm.allgather_device(send, recv, slot_bytes, eng.stream());
-    if (me == 0) eng.enqueue_merge_slots((u32)P, slot_recs);
-    eng.enqueue_slot_headers((u32)P, slot_recs);
+    // One graph for the whole job when the collective can be captured (RCCL); every rank
+    // enters the all-gather exactly once either way.
+    bool fused = false;
+    if (comm.graph_capturable() && slot_graph_enabled()) {
+      st_slot = local("map", [&] {
+        fused = eng.enqueue_slot_job(shard, slot_recs, (u32)P, me == 0,
+                                     [&](const void* send, void* recv, u64 bytes) {
+                                       comm.allgather_device(send, recv, bytes, eng.stream());
+                                     });
+      });
+      // a failure before the capture: fall through to the step-by-step sequence
+    }
+    if (!fused) {
+      void* send = nullptr;
+      if (!st_slot) st_slot = local("map", [&] { send = eng.enqueue_map_slot(shard, slot_recs); });
+      if (st_slot) send = eng.write_slot_failure();  // the all-gather must still be entered
+      void* recv = eng.slot_buffer((u32)P, slot_recs);
+      comm.allgather_device(send, recv, slot_bytes, eng.stream());
+      if (me == 0) eng.enqueue_merge_slots((u32)P, slot_recs);
+      eng.enqueue_slot_headers((u32)P, slot_recs);
+    }
     comm.sync_stream(eng.stream());
     const SlotHeader* hd = eng.slot_headers();
     for (int p = 0; p < P; ++p)

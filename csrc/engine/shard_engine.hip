@@ -21,6 +21,7 @@ class GpuShardEngine final : public ShardEngine {
 
   ~GpuShardEngine() override {
     if (mp_) (void)hipStreamSynchronize(mp_->stream);  // pending copies from the pinned headers
+    for (auto& g : slot_graphs_) (void)hipGraphExecDestroy(g.exec);
     if (h_headers_) (void)hipHostFree(h_headers_);
     if (h_send_header_) (void)hipHostFree(h_send_header_);
   }
@@ -120,8 +121,12 @@ class GpuShardEngine final : public ShardEngine {
     return combine && cfg_.sort_path == SortPath::kDict && shard.bytes <= m.cap_bytes &&
            cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
   }
-  void enqueue_small_ordered(const TextInput& shard, bool spec_samples, SlotHeader* hdr,
-                             u32 slot_recs) {
+  // Host half of a small ordered pass (run for every job): returns the graph key of the
+  // device half and the device half itself, which captures everything it needs by value
+  // (so it can be captured later, inside a larger graph).
+  using DeviceHalf = std::function<void()>;
+  std::pair<DevicePipeline::GraphKeyArr, DeviceHalf> prepare_small_ordered(
+      const TextInput& shard, bool spec_samples, SlotHeader* hdr, u32 slot_recs) {
     DevicePipeline& m = *mp_;
     m.check_input(shard);
     m.prepare_upload(shard);
@@ -144,10 +149,19 @@ class GpuShardEngine final : public ShardEngine {
     // dirtied, so the next pass skips the reset memset (m.sync_clean; any other use of this
     // pipeline clears it).
     m.set_self_clean(ex);
-    m.skip_sync_reset = m.sync_clean;
+    const bool no_reset = m.sync_clean;
     m.sync_clean = false;
-    auto enqueue = [&] {
+    m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
+    const DevicePipeline::GraphKeyArr key{
+        (spec_samples ? 2u : 3u) | (hdr ? 0x100u : 0u) | (no_reset ? 0x200u : 0u) |
+            ((u64)slot_recs << 32),
+        shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text), (u64)m.upload_mode,
+        m.upload_mode == DevicePipeline::Upload::kDirect ? reinterpret_cast<u64>(shard.data) : 0};
+    DeviceHalf enqueue = [this, shard, spec_samples, ex, no_reset]() mutable {
+      DevicePipeline& m = *mp_;
+      m.skip_sync_reset = no_reset;
       m.enqueue_upload_device(shard);
+      m.skip_sync_reset = false;
       m.enqueue_map(shard);
       m.set_tile_source(ex, false);
       launch_dict_ordered(m.tokens, nullptr, m.d_parts, &m.d_ctr->num_records, m.cap, m.d_ctr,
@@ -158,18 +172,16 @@ class GpuShardEngine final : public ShardEngine {
                                         hipMemcpyDeviceToHost, m.stream));
       }
     };
-    m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
+    return {key, std::move(enqueue)};
+  }
+  void enqueue_small_ordered(const TextInput& shard, bool spec_samples, SlotHeader* hdr,
+                             u32 slot_recs) {
+    DevicePipeline& m = *mp_;
+    auto half = prepare_small_ordered(shard, spec_samples, hdr, slot_recs);
     if (m.use_graph())
-      m.launch_cached({(spec_samples ? 2u : 3u) | (hdr ? 0x100u : 0u) |
-                           (m.skip_sync_reset ? 0x200u : 0u) | ((u64)slot_recs << 32),
-                       shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text),
-                       (u64)m.upload_mode,
-                       m.upload_mode == DevicePipeline::Upload::kDirect
-                           ? reinterpret_cast<u64>(shard.data) : 0},
-                      enqueue);
+      m.launch_cached(half.first, half.second);
     else
-      enqueue();
-    m.skip_sync_reset = false;
+      half.second();
   }
   // After the sync of an enqueue_small_ordered: the map statistics, or the local redo on
   // the HBM table when a partition overflowed its LDS table.
@@ -255,39 +267,125 @@ class GpuShardEngine final : public ShardEngine {
     return recv_records((u64)nslots * (kSlotHeaderRecords + slot_recs));
   }
 
-  void enqueue_merge_slots(u32 nslots, u32 slot_recs) override {
-    DevicePipeline& m = *mp_;
+  // Host half of the root merge (buffers grown for this shape) + its device half.
+  std::pair<DevicePipeline::GraphKeyArr, DeviceHalf> prepare_merge_slots(u32 nslots,
+                                                                         u32 slot_recs) {
     DevicePipeline& r = *rp_;
     LOCUST_CHECK_ARG(nslots <= (u32)kMaxMergeRunsHost, "too many slots to merge");
     r.grow_host_out((u64)nslots * slot_recs);
     grow_headers(nslots);
     merge_copied_headers_ = true;
-    // on the engine's stream, behind the all-gather
-    auto enqueue = [&] {
+    const DevicePipeline::GraphKeyArr key{
+        6, ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(r.d_records),
+        reinterpret_cast<u64>(r.d_out_mapped), reinterpret_cast<u64>(r.d_ctr_mapped),
+        reinterpret_cast<u64>(d_headers_)};
+    DeviceHalf enqueue = [this, nslots, slot_recs]() {
+      DevicePipeline& m = *mp_;
+      DevicePipeline& r = *rp_;
+      // on the engine's stream, behind the all-gather
       launch_merge_slots(r.d_records, nslots, slot_recs, reinterpret_cast<KeyCount*>(r.d_out),
                          r.d_ctr, r.d_out_mapped, r.d_ctr_mapped,
                          r.lb_merge((u64)nslots * slot_recs), d_headers_, m.stream);
     };
+    return {key, std::move(enqueue)};
+  }
+  void enqueue_merge_slots(u32 nslots, u32 slot_recs) override {
+    DevicePipeline& m = *mp_;
+    auto half = prepare_merge_slots(nslots, slot_recs);
     if (m.use_graph())
-      m.launch_cached({6, ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(r.d_records),
-                       reinterpret_cast<u64>(r.d_out_mapped),
-                       reinterpret_cast<u64>(r.d_ctr_mapped), reinterpret_cast<u64>(d_headers_)},
-                      enqueue);
+      m.launch_cached(half.first, half.second);
     else
-      enqueue();
+      half.second();
   }
 
-  void enqueue_slot_headers(u32 nslots, u32 slot_recs) override {
-    DevicePipeline& m = *mp_;
+  // Device half of the header copy (non-root ranks; the root's merge copies them).
+  DeviceHalf header_copy(u32 nslots, u32 slot_recs) {
     grow_headers(nslots);
+    merge_copied_headers_ = false;
+    return [this, nslots, slot_recs]() {
+      const u64 pitch = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
+      LOCUST_HIP_CHECK(hipMemcpy2DAsync(h_headers_, sizeof(SlotHeader), rp_->d_records, pitch,
+                                        sizeof(SlotHeader), nslots, hipMemcpyDeviceToHost,
+                                        mp_->stream));
+    };
+  }
+  void enqueue_slot_headers(u32 nslots, u32 slot_recs) override {
     if (merge_copied_headers_) {  // the root's merge kernel wrote them already
+      grow_headers(nslots);
       merge_copied_headers_ = false;
       return;
     }
-    const u64 pitch = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
-    LOCUST_HIP_CHECK(hipMemcpy2DAsync(h_headers_, sizeof(SlotHeader), rp_->d_records, pitch,
-                                      sizeof(SlotHeader), nslots, hipMemcpyDeviceToHost,
-                                      m.stream));
+    header_copy(nslots, slot_recs)();
+  }
+
+  bool enqueue_slot_job(const TextInput& shard, u32 slot_recs, u32 nslots, bool root,
+                        const SlotAllgather& allgather) override {
+    DevicePipeline& m = *mp_;
+    if (!m.use_graph() || !small_ordered_ok(shard, true) || nslots > (u32)kMaxMergeRunsHost)
+      return false;
+    LOCUST_CHECK_ARG(slot_recs <= m.slot_records_cap(), "slot larger than the send buffer");
+    SlotHeader* hdr = reinterpret_cast<SlotHeader*>(m.d_records - kSlotHeaderRecords);
+    slot_fast_ = true;
+    samples_valid_ = false;
+    sorted_local_ = true;
+    distinct_local_ = true;
+    stream_chunks_ = 0;
+    // host halves first (they may grow buffers: the key records the pointers)
+    auto map_half = prepare_small_ordered(shard, false, hdr, slot_recs);
+    void* recv = slot_buffer(nslots, slot_recs);
+    std::pair<DevicePipeline::GraphKeyArr, DeviceHalf> tail;
+    if (root) {
+      tail = prepare_merge_slots(nslots, slot_recs);
+    } else {
+      tail.second = header_copy(nslots, slot_recs);
+      tail.first = {7, ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(h_headers_), 0, 0,
+                    0};
+    }
+    merge_copied_headers_ = false;  // this job's graph already holds the header copy
+    const u64 slot_bytes = ((u64)kSlotHeaderRecords + slot_recs) * sizeof(KeyCount);
+    SlotJobKey key;
+    std::copy(map_half.first.begin(), map_half.first.end(), key.begin());
+    std::copy(tail.first.begin(), tail.first.end(), key.begin() + 6);
+    key[12] = reinterpret_cast<u64>(recv);
+    key[13] = root ? 1 : 0;
+    for (auto& g : slot_graphs_)
+      if (g.key == key) {
+        LOCUST_HIP_CHECK(hipGraphLaunch(g.exec, m.stream));
+        return true;
+      }
+    // A new shape runs once without capture: the collective's first call with these
+    // buffers and this size (lazy connection / buffer setup inside the communicator)
+    // happens outside a capture; the next job with the same shape captures and replays.
+    if (std::find(slot_seen_.begin(), slot_seen_.end(), key) == slot_seen_.end()) {
+      if (slot_seen_.size() >= 16) slot_seen_.erase(slot_seen_.begin());
+      slot_seen_.push_back(key);
+      map_half.second();
+      allgather(hdr, recv, slot_bytes);
+      tail.second();
+      return true;
+    }
+    if (slot_graphs_.size() >= 4) {
+      LOCUST_HIP_CHECK(hipGraphExecDestroy(slot_graphs_.front().exec));
+      slot_graphs_.erase(slot_graphs_.begin());
+    }
+    hipGraph_t g = nullptr;
+    LOCUST_HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
+    try {
+      map_half.second();
+      allgather(hdr, recv, slot_bytes);
+      tail.second();
+    } catch (...) {
+      (void)hipStreamEndCapture(m.stream, &g);  // discard the partial capture
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    LOCUST_HIP_CHECK(hipStreamEndCapture(m.stream, &g));
+    hipGraphExec_t exec = nullptr;
+    LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    LOCUST_HIP_CHECK(hipGraphDestroy(g));
+    slot_graphs_.push_back({key, exec});
+    LOCUST_HIP_CHECK(hipGraphLaunch(exec, m.stream));
+    return true;
   }
   const SlotHeader* slot_headers() const override { return h_headers_; }
 
@@ -585,6 +683,14 @@ class GpuShardEngine final : public ShardEngine {
   bool distinct_local_ = true;  // d_records hold every key once (map-side combine)
   bool spec_samples_ = false;   // the last small pass produced splitter samples
   bool slot_fast_ = false;      // enqueue_map_slot took the one-graph small pass
+  // whole-job graphs of enqueue_slot_job, keyed by [map half | tail half | recv | root]
+  using SlotJobKey = std::array<u64, 14>;
+  struct SlotJobGraph {
+    SlotJobKey key;
+    hipGraphExec_t exec;
+  };
+  std::vector<SlotJobGraph> slot_graphs_;
+  std::vector<SlotJobKey> slot_seen_;  // shapes run once uncaptured (see enqueue_slot_job)
   SlotHeader* h_headers_ = nullptr;  // host-mapped copies of the all-gathered slot headers
   SlotHeader* d_headers_ = nullptr;  // device view of h_headers_
   u32 h_headers_cap_ = 0;
