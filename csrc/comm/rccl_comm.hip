@@ -12,6 +12,7 @@
 // aborts the communicator instead of hanging.
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -42,6 +43,11 @@ class RcclComm final : public Communicator {
     id = ids[0];
     LOCUST_HIP_CHECK(hipSetDevice(device));
     LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    // The slot job captures its all-gather into a hipGraph (graph_capturable): keep the
+    // captured collective on RCCL's own connection buffers, as the uncaptured calls are,
+    // instead of IPC-registering our slot buffers with every peer at capture time.
+    // A user's explicit setting wins.
+    setenv("NCCL_GRAPH_REGISTER", "0", 0);
     LOCUST_RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
     stage_cap_ = 1 << 20;
     LOCUST_HIP_CHECK(hipMalloc(&d_stage_, stage_cap_ * (u64)(world + 1)));
