@@ -356,33 +356,54 @@ class GpuShardEngine final : public ShardEngine {
     // A new shape runs once without capture: the collective's first call with these
     // buffers and this size (lazy connection / buffer setup inside the communicator)
     // happens outside a capture; the next job with the same shape captures and replays.
-    if (std::find(slot_seen_.begin(), slot_seen_.end(), key) == slot_seen_.end()) {
-      if (slot_seen_.size() >= 16) slot_seen_.erase(slot_seen_.begin());
-      slot_seen_.push_back(key);
+    // After a failed capture every job runs this way (same order, same single sync).
+    auto run_uncaptured = [&] {
       map_half.second();
       allgather(hdr, recv, slot_bytes);
       tail.second();
+    };
+    if (slot_capture_failed_ ||
+        std::find(slot_seen_.begin(), slot_seen_.end(), key) == slot_seen_.end()) {
+      if (slot_seen_.size() >= 16) slot_seen_.erase(slot_seen_.begin());
+      slot_seen_.push_back(key);
+      run_uncaptured();
       return true;
     }
     if (slot_graphs_.size() >= 4) {
       LOCUST_HIP_CHECK(hipGraphExecDestroy(slot_graphs_.front().exec));
       slot_graphs_.erase(slot_graphs_.begin());
     }
+    // Nothing captured has run, so a capture the runtime or the communicator refuses is
+    // not a job failure: discard it and run the same work uncaptured.
     hipGraph_t g = nullptr;
-    LOCUST_HIP_CHECK(hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed));
-    try {
-      map_half.second();
-      allgather(hdr, recv, slot_bytes);
-      tail.second();
-    } catch (...) {
-      (void)hipStreamEndCapture(m.stream, &g);  // discard the partial capture
-      if (g) (void)hipGraphDestroy(g);
-      throw;
-    }
-    LOCUST_HIP_CHECK(hipStreamEndCapture(m.stream, &g));
     hipGraphExec_t exec = nullptr;
-    LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
-    LOCUST_HIP_CHECK(hipGraphDestroy(g));
+    std::string why;
+    if (hipStreamBeginCapture(m.stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
+      why = "begin capture";
+    } else {
+      try {
+        // test hook: LOCUST_FAULT=0:slot_capture (root) / 1:slot_capture (non-root ranks)
+        if (fault_injected(root ? 0 : 1, "slot_capture"))
+          throw Error("injected fault (LOCUST_FAULT) in the slot job capture");
+        run_uncaptured();  // recorded, not run
+      } catch (const std::exception& e) {
+        why = e.what();
+      }
+      const hipError_t ec = hipStreamEndCapture(m.stream, &g);
+      if (why.empty() && ec != hipSuccess) why = hipGetErrorString(ec);
+      if (why.empty() && hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) != hipSuccess)
+        why = "instantiate";
+      if (g) (void)hipGraphDestroy(g);
+    }
+    if (!why.empty()) {
+      (void)hipGetLastError();
+      if (exec) (void)hipGraphExecDestroy(exec);
+      slot_capture_failed_ = true;
+      std::fprintf(stderr, "locust: slot job capture failed (%s); running it uncaptured\n",
+                   why.c_str());
+      run_uncaptured();
+      return true;
+    }
     slot_graphs_.push_back({key, exec});
     LOCUST_HIP_CHECK(hipGraphLaunch(exec, m.stream));
     return true;
@@ -691,6 +712,7 @@ class GpuShardEngine final : public ShardEngine {
   };
   std::vector<SlotJobGraph> slot_graphs_;
   std::vector<SlotJobKey> slot_seen_;  // shapes run once uncaptured (see enqueue_slot_job)
+  bool slot_capture_failed_ = false;   // a capture was refused: slot jobs stay uncaptured
   SlotHeader* h_headers_ = nullptr;  // host-mapped copies of the all-gathered slot headers
   SlotHeader* d_headers_ = nullptr;  // device view of h_headers_
   u32 h_headers_cap_ = 0;

@@ -193,13 +193,16 @@ def test_gpu_slot_gather_fault(hamlet, monkeypatch, fault):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("slot_graph", ["1", "0"])
+@pytest.mark.parametrize("slot_graph", ["1", "0", "refused"])
 def test_gpu_rccl_one_rank_gather_jobs(hamlet, monkeypatch, slot_graph):
     """One RCCL rank (the pool's boxes have one GPU): repeated gather-strategy jobs take
     the slot path -- with LOCUST_SLOT_GRAPH=1 map + all-gather + merge replay as ONE
     captured graph (the collective inside it), with 0 as separate launches -- and every
-    job matches the oracle, including the first (slot overflow -> standard path)."""
-    monkeypatch.setenv("LOCUST_SLOT_GRAPH", slot_graph)
+    job matches the oracle, including the first (slot overflow -> standard path).
+    "refused": the capture fails (injected), so the jobs run the same work uncaptured."""
+    if slot_graph == "refused":
+        monkeypatch.setenv("LOCUST_FAULT", "0:slot_capture")
+    monkeypatch.setenv("LOCUST_SLOT_GRAPH", "0" if slot_graph == "0" else "1")
     nlines = hamlet.count(b"\n") + (0 if hamlet.endswith(b"\n") else 1)
     dcfg = lc.make_dist_config(1, lc.make_config("gpu", combine=True), strategy="gather")
     dr = lc._C.DistRank(dcfg, 0, "rccl", "127.0.0.1", free_port(), len(hamlet), nlines, 60.0)
