@@ -406,7 +406,22 @@ struct DevicePipeline {
                   std::to_string(cap_lines) + " lines)");
   }
 
-  void sync() { LOCUST_HIP_CHECK(hipStreamSynchronize(stream)); }
+  // LOCUST_SPIN_SYNC=1: poll hipStreamQuery instead of hipStreamSynchronize (A/B knob for
+  // the host's wake-up latency after a short job).
+  void sync() {
+    static const bool spin = [] {
+      const char* v = std::getenv("LOCUST_SPIN_SYNC");
+      return v && v[0] == '1';
+    }();
+    if (spin) {
+      hipError_t e;
+      while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+      }
+      LOCUST_HIP_CHECK(e);
+      return;
+    }
+    LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+  }
 
   // H2D of the text; zero counters and look-back scratch.
   //  * zero-copy (small inputs, fast map): no copy at all -- the map kernel's 16-byte
