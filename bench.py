@@ -117,6 +117,26 @@ def ref_semantics(text: bytes, steps: int = 50, warmup: int = 5):
     return med
 
 
+BASELINE_CPU = {"map_ms": 2.333, "process_ms": 23.699, "reduce_ms": 1.100}  # README.md:74-76
+
+
+def cpu_path(text: bytes, steps: int = 20, warmup: int = 3) -> dict:
+    """BASELINE config 1: the CPU reference pipeline (single thread: tokenize, std::sort,
+    linear reduce -- the reference's GPU_IMPLEMENTATION 0 build, main.cu:489-527), median
+    stage times of `steps` runs against the reference's CPU column (700 lines)."""
+    import locust_amd as lc
+
+    cfg = lc.make_config("cpu")
+    for _ in range(warmup):
+        lc._C.cpu_run(cfg, text)
+    acc = {"map_ms": [], "process_ms": [], "reduce_ms": [], "wall_ms": []}
+    for _ in range(steps):
+        t = lc._C.cpu_run(cfg, text).times()
+        for k in acc:
+            acc[k].append(t[k])
+    return {k: round(statistics.median(v), 4) for k, v in acc.items()}
+
+
 def cold_first_run(text: bytes) -> dict:
     """A fresh engine's first job (allocation excluded, first launches/captures included):
     the regime of the reference's numbers, which include Thrust's first-call overhead."""
@@ -275,12 +295,21 @@ def main() -> int:
             extra["reference_semantics_ms"] = {
                 "hamlet4500": ref_semantics(text), "hamlet700": ref_semantics(load_text("hamlet700")),
                 "baseline": BASELINE_STAGES}
+            c700 = cpu_path(load_text("hamlet700"))
+            extra["cpu_path"] = {
+                "note": "BASELINE config 1: CPU reference pipeline, one thread, no GPU",
+                "hamlet700_ms": c700, "hamlet4500_ms": cpu_path(text),
+                "baseline_hamlet700_ms": dict(BASELINE_CPU, total_ms=27.132),
+                "vs_baseline_hamlet700": round(c700["wall_ms"] / 27.132, 4)}
     else:
         dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank, args.comm)
         ms, stages, res, strategy = time_dist(dr, args.steps, args.warmup, args.strategy)
-        if not args.no_extra and args.strategy == "auto" and not synth:
-            # The sample-sort all-to-all shuffle on the same job (the path large inputs take).
-            mss, sts, _, _ = time_dist(dr, args.steps, args.warmup, "shuffle")
+        if not args.no_extra and args.strategy == "auto" and strategy != "shuffle":
+            # The sample-sort all-to-all shuffle on the same job (the path large inputs
+            # take), so every scaling run also records the all-to-all path.
+            ks, kw = (args.steps, args.warmup) if not synth else (min(args.steps, 10),
+                                                                  min(args.warmup, 3))
+            mss, sts, _, _ = time_dist(dr, ks, kw, "shuffle")
             extra["shuffle_path"] = {"ms_per_step": round(mss, 4),
                                      "stages_ms": {k: round(v, 4) for k, v in sts.items()}}
     if rank != 0:
@@ -302,9 +331,10 @@ def main() -> int:
     else:
         base = BASELINE_MS[args.config]
         data = "hamlet.txt fixture (real text); N>1: every rank maps its own copy"
-        model = (f"WordCount {args.config} ({nlines} lines/GPU), LDS reduce path, "
-                 "dictionary Process (hash + rank sort of distinct keys), "
-                 "full H2D->D2H job per step")
+        model = (f"WordCount {args.config} ({nlines} lines/GPU): byte-parallel map + "
+                 "ordered-dictionary Process+Reduce (one kernel: LDS hash aggregate, in-LDS "
+                 "sort of distinct keys, look-back val offsets), full H2D->D2H job per step"
+                 + ("" if n == 1 else "; ranks merged on rank 0"))
         scaling = "weak"
         baseline_stages = BASELINE_STAGES[args.config]
     line = {
@@ -324,8 +354,9 @@ def main() -> int:
             "model": model,
             "global_batch": nlines * n,
             "seq_len": nbytes,
-            "parallelism": f"dp{n}" + ({"gather": "+rccl_p2p_gather_merge",
-                                        "shuffle": "+rccl_alltoallv_shuffle"}.get(strategy, "")),
+            "parallelism": f"dp{n}" + ("" if strategy is None else
+                                       f"+{args.comm}_" + {"gather": "gather_merge",
+                                                           "shuffle": "alltoallv_shuffle"}[strategy]),
         },
         "baseline_ms": round(base, 3),
         "baseline_stages_ms": baseline_stages,

@@ -18,6 +18,8 @@ WordCountResult GpuWordCount::run(const TextInput&) { no_gpu(); }
 std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput&, WordCountResult*) { no_gpu(); }
 WordCountResult GpuWordCount::run_reduce_stage(const PackedKey*, u64) { no_gpu(); }
 void copy_device(void*, const void*, u64, bool, void*) { no_gpu(); }
-DistResult run_single_process_multi_gpu(const DistConfig&, const TextInput&) { no_gpu(); }
+DistResult run_single_process_multi_gpu(const DistConfig&, const TextInput&, LocalComm) { no_gpu(); }
+int visible_device_count() { return 0; }
+LocalComm resolve_local_comm(const DistConfig&, LocalComm) { return LocalComm::kLoopback; }
 
 }  // namespace locust

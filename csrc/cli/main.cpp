@@ -8,7 +8,7 @@
 //                                                      (writes a spill), 2 = reduce only
 // plus long flags (runtime switches replacing the reference's #defines):
 //   --backend gpu|cpu  --reduce-path lds|global  --map-path compat|fast
-//   --sort radix|dict  --gpus N  --emits-per-line N  --max-key N  --ref-compat
+//   --sort radix|dict  --gpus N  --comm auto|rccl|loopback  --emits-per-line N  --max-key N  --ref-compat
 //   --stage map|reduce  --spill-dir DIR  --spill-format text|binary  --inputs a,b,...
 //   --warmup N  --iters N  --json FILE  --quiet  --check  --device N  --chunk-mb N
 //   --ref-timers (stage times taken where the reference's host timers were)
@@ -16,6 +16,7 @@
 //   MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,6 +38,8 @@ struct CliArgs {
   bool window = false;
   JobConfig cfg;
   int gpus = 1;
+  bool gpus_given = false;   // --gpus on the command line (even --gpus 1: RCCL rank)
+  LocalComm comm = LocalComm::kAuto;
   std::string spill_dir = "/tmp";
   SpillFormat spill_fmt = SpillFormat::kText;
   std::vector<std::string> inputs;
@@ -84,6 +87,11 @@ bool parse(int argc, char** argv, CliArgs* a) {
       a->cfg.sort_path = need("--sort") == "dict" ? SortPath::kDict : SortPath::kRadix;
     } else if (s == "--gpus") {
       a->gpus = std::atoi(need("--gpus").c_str());
+      a->gpus_given = true;
+    } else if (s == "--comm") {
+      const std::string v = need("--comm");
+      a->comm = v == "rccl" ? LocalComm::kRccl : v == "loopback" ? LocalComm::kLoopback
+                                                               : LocalComm::kAuto;
     } else if (s == "--device") {
       a->cfg.device = std::atoi(need("--device").c_str());
     } else if (s == "--emits-per-line") {
@@ -240,7 +248,9 @@ int run(const CliArgs& a) {
       CpuWordCount eng(a.cfg);
       r = eng.run_reduce_stage(toks.data(), toks.size());
     } else {
-      GpuWordCount eng(a.cfg, 1, std::max<u64>(1, div_up(toks.size(), a.cfg.emits_per_line)) + 1);
+      // capacity: records = min(lines x emits, bytes / 2 + 1) must hold every token
+      GpuWordCount eng(a.cfg, 2 * toks.size() + 2,
+                       std::max<u64>(1, div_up(toks.size(), a.cfg.emits_per_line)) + 1);
       r = eng.run_reduce_stage(toks.data(), toks.size());
     }
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(r.times.process_ms + r.times.reduce_ms));
@@ -259,12 +269,17 @@ int run(const CliArgs& a) {
                                use_window ? a.line_end : -1, a.cfg.ref_compat);
   if (!cpu) std::printf("Length: %i\n", (int)text.input.num_lines);
 
-  // ---------------- multi-GPU in one process (loopback over the node's GPUs) -----------
-  if (a.gpus > 1 && a.stage == 0) {
+  // ---------------- multi-GPU in one process (RCCL clique over the node's GPUs) ---------
+  // An explicit --gpus N (N >= 1) runs N ranks: an ncclCommInitAll clique over xGMI when
+  // the node has N GPUs (--gpus 1 included: one RCCL rank), loopback ranks otherwise.
+  if ((a.gpus > 1 || (a.gpus_given && !cpu)) && a.stage == 0) {
     DistConfig dc;
     dc.job = a.cfg;
-    dc.world = a.gpus;
-    DistResult dr = run_single_process_multi_gpu(dc, text.input);
+    dc.world = std::max(1, a.gpus);
+    LOCUST_LOG_INFO("%d ranks in one process over %s", dc.world,
+                    resolve_local_comm(dc, a.comm) == LocalComm::kRccl ? "an RCCL clique"
+                                                                       : "loopback");
+    DistResult dr = run_single_process_multi_gpu(dc, text.input, a.comm);
     std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(dr.reduce_ms));
@@ -340,6 +355,8 @@ int run(const CliArgs& a) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  // before any thread or RCCL use (see locust_amd/__init__.py); a user's setting wins
+  setenv("NCCL_GRAPH_REGISTER", "0", 0);
   std::printf("Running\n");
   CliArgs a;
   try {

@@ -43,12 +43,24 @@ class RcclComm final : public Communicator {
     id = ids[0];
     LOCUST_HIP_CHECK(hipSetDevice(device));
     LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    // The slot job captures its all-gather into a hipGraph (graph_capturable): keep the
-    // captured collective on RCCL's own connection buffers, as the uncaptured calls are,
-    // instead of IPC-registering our slot buffers with every peer at capture time.
-    // A user's explicit setting wins.
-    setenv("NCCL_GRAPH_REGISTER", "0", 0);
+    // The slot job captures its all-gather into a hipGraph (graph_capturable).  The
+    // package sets NCCL_GRAPH_REGISTER=0 at import / CLI start (before any thread or RCCL
+    // use; a user's setting wins) so captured collectives stay on RCCL's own connection
+    // buffers instead of IPC-registering our slot buffers; log what is in effect.
+    LOCUST_LOG_DEBUG("rccl rank %d/%d on device %d, NCCL_GRAPH_REGISTER=%s", rank, world,
+        device, std::getenv("NCCL_GRAPH_REGISTER") ? std::getenv("NCCL_GRAPH_REGISTER") : "(unset)");
     LOCUST_RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    stage_cap_ = 1 << 20;
+    LOCUST_HIP_CHECK(hipMalloc(&d_stage_, stage_cap_ * (u64)(world + 1)));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_stage_, stage_cap_ * (u64)(world + 1), hipHostMallocDefault));
+  }
+
+  // One rank of a single-process clique (ncclCommInitAll): no TCP bootstrap.  The calling
+  // thread drives `device`; every rank of the clique runs on its own thread.
+  RcclComm(ncclComm_t comm, int rank, int world, int device, double timeout_s)
+      : rank_(rank), world_(world), timeout_s_(timeout_s), comm_(comm) {
+    LOCUST_HIP_CHECK(hipSetDevice(device));
+    LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     stage_cap_ = 1 << 20;
     LOCUST_HIP_CHECK(hipMalloc(&d_stage_, stage_cap_ * (u64)(world + 1)));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_stage_, stage_cap_ * (u64)(world + 1), hipHostMallocDefault));
@@ -231,6 +243,27 @@ class RcclComm final : public Communicator {
 std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
                                              const std::string& host, int port, double timeout_s) {
   return std::unique_ptr<Communicator>(new RcclComm(rank, world, device, host, port, timeout_s));
+}
+
+std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) {
+  const int n = (int)devices.size();
+  LOCUST_CHECK_ARG(n >= 1, "empty device list");
+  std::vector<ncclComm_t> comms((size_t)n, nullptr);
+  // one process, one communicator per device: RCCL wires the clique over xGMI itself
+  LOCUST_RCCL_CHECK(ncclCommInitAll(comms.data(), n, devices.data()));
+  std::vector<RcclCliqueMember> out((size_t)n);
+  for (int r = 0; r < n; ++r) {
+    out[(size_t)r].handle = comms[(size_t)r];
+    out[(size_t)r].rank = r;
+    out[(size_t)r].world = n;
+    out[(size_t)r].device = devices[(size_t)r];
+  }
+  return out;
+}
+
+std::unique_ptr<Communicator> make_rccl_clique_comm(const RcclCliqueMember& m, double timeout_s) {
+  return std::unique_ptr<Communicator>(
+      new RcclComm(static_cast<ncclComm_t>(m.handle), m.rank, m.world, m.device, timeout_s));
 }
 
 }  // namespace locust

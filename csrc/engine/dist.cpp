@@ -184,13 +184,33 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     // enters the all-gather exactly once either way.
     bool fused = false;
     if (comm.graph_capturable() && slot_graph_enabled()) {
+      // `entered`: the all-gather was issued directly (uncaptured run) -- this rank is in
+      // the collective sequence whatever happens next.  A capture only records it; a
+      // refused capture runs the same work uncaptured, so a call made while capturing
+      // does not count.
+      bool entered = false;
       st_slot = local("map", [&] {
         fused = eng.enqueue_slot_job(shard, slot_recs, (u32)P, me == 0,
-                                     [&](const void* send, void* recv, u64 bytes) {
+                                     [&](const void* send, void* recv, u64 bytes,
+                                         bool capturing) {
                                        comm.allgather_device(send, recv, bytes, eng.stream());
+                                       if (!capturing) entered = true;
                                      });
+        if (fault_injected(me, "slot_after_allgather") && entered)
+          throw Error("injected fault (LOCUST_FAULT) after the slot all-gather");
       });
-      // a failure before the capture: fall through to the step-by-step sequence
+      if (st_slot && entered) {
+        // Failed after entering the collective (e.g. the root merge's launch): peers are
+        // not waiting for a second all-gather, so drain the stream and fail this rank
+        // only -- never enter the step-by-step sequence's all-gather as well.
+        try {
+          comm.sync_stream(eng.stream());
+        } catch (const std::exception&) {
+        }
+        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
+                    std::to_string(me) + ": " + local_msg);
+      }
+      // a failure before the collective: fall through to the step-by-step sequence
     }
     if (!fused) {
       void* send = nullptr;

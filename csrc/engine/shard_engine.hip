@@ -275,8 +275,11 @@ class GpuShardEngine final : public ShardEngine {
     r.grow_host_out((u64)nslots * slot_recs);
     grow_headers(nslots);
     merge_copied_headers_ = true;
+    // rp_gen_: graphs bake in rp_'s buffers beyond the ones in the key (d_out, d_ctr, the
+    // look-back scratch); a reallocated rp_ may reuse d_records' address, so its
+    // generation is part of every key that captures rp_ buffers.
     const DevicePipeline::GraphKeyArr key{
-        6, ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(r.d_records),
+        6 | (rp_gen_ << 8), ((u64)nslots << 32) | slot_recs, reinterpret_cast<u64>(r.d_records),
         reinterpret_cast<u64>(r.d_out_mapped), reinterpret_cast<u64>(r.d_ctr_mapped),
         reinterpret_cast<u64>(d_headers_)};
     DeviceHalf enqueue = [this, nslots, slot_recs]() {
@@ -347,7 +350,7 @@ class GpuShardEngine final : public ShardEngine {
     std::copy(map_half.first.begin(), map_half.first.end(), key.begin());
     std::copy(tail.first.begin(), tail.first.end(), key.begin() + 6);
     key[12] = reinterpret_cast<u64>(recv);
-    key[13] = root ? 1 : 0;
+    key[13] = (root ? 1 : 0) | (rp_gen_ << 1);
     for (auto& g : slot_graphs_)
       if (g.key == key) {
         LOCUST_HIP_CHECK(hipGraphLaunch(g.exec, m.stream));
@@ -357,16 +360,16 @@ class GpuShardEngine final : public ShardEngine {
     // buffers and this size (lazy connection / buffer setup inside the communicator)
     // happens outside a capture; the next job with the same shape captures and replays.
     // After a failed capture every job runs this way (same order, same single sync).
-    auto run_uncaptured = [&] {
+    auto run_uncaptured = [&](bool capturing) {
       map_half.second();
-      allgather(hdr, recv, slot_bytes);
+      allgather(hdr, recv, slot_bytes, capturing);
       tail.second();
     };
     if (slot_capture_failed_ ||
         std::find(slot_seen_.begin(), slot_seen_.end(), key) == slot_seen_.end()) {
       if (slot_seen_.size() >= 16) slot_seen_.erase(slot_seen_.begin());
       slot_seen_.push_back(key);
-      run_uncaptured();
+      run_uncaptured(false);
       return true;
     }
     if (slot_graphs_.size() >= 4) {
@@ -382,10 +385,14 @@ class GpuShardEngine final : public ShardEngine {
       why = "begin capture";
     } else {
       try {
-        // test hook: LOCUST_FAULT=0:slot_capture (root) / 1:slot_capture (non-root ranks)
-        if (fault_injected(root ? 0 : 1, "slot_capture"))
+        // test hooks: LOCUST_FAULT=<rank>:slot_capture fails the capture before anything
+        // is recorded, <rank>:slot_capture_late after the all-gather was recorded (the
+        // work then runs uncaptured: the recorded collective never ran)
+        if (fault_injected(log_rank(), "slot_capture"))
           throw Error("injected fault (LOCUST_FAULT) in the slot job capture");
-        run_uncaptured();  // recorded, not run
+        run_uncaptured(true);  // recorded, not run
+        if (fault_injected(log_rank(), "slot_capture_late"))
+          throw Error("injected fault (LOCUST_FAULT) late in the slot job capture");
       } catch (const std::exception& e) {
         why = e.what();
       }
@@ -401,7 +408,7 @@ class GpuShardEngine final : public ShardEngine {
       slot_capture_failed_ = true;
       std::fprintf(stderr, "locust: slot job capture failed (%s); running it uncaptured\n",
                    why.c_str());
-      run_uncaptured();
+      run_uncaptured(false);
       return true;
     }
     slot_graphs_.push_back({key, exec});
@@ -479,8 +486,13 @@ class GpuShardEngine final : public ShardEngine {
   void* recv_records(u64 n) override {
     if (!rp_ || rp_->cap < n) {
       const u64 want = std::max<u64>(std::max<u64>(n + n / 4, 4096), rp_ ? rp_->cap * 2 : 0);
+      if (rp_) (void)hipStreamSynchronize(mp_->stream);  // graphs may still read rp_
       rp_.reset();
       rp_.reset(new DevicePipeline(cfg_, 1, 1, want));
+      ++rp_gen_;  // graphs keyed on the old rp_ can never match again
+      for (auto& g : slot_graphs_) (void)hipGraphExecDestroy(g.exec);
+      slot_graphs_.clear();
+      slot_seen_.clear();
     }
     return rp_->d_records;
   }
@@ -588,7 +600,7 @@ class GpuShardEngine final : public ShardEngine {
                                  r.d_out_mapped, r.d_ctr_mapped, r.lb_merge(r.cap), r.stream);
       };
       if (r.use_graph())
-        r.launch_cached({5, (u64)nruns, reinterpret_cast<u64>(m.d_records),
+        r.launch_cached({5 | (rp_gen_ << 8), (u64)nruns, reinterpret_cast<u64>(m.d_records),
                          reinterpret_cast<u64>(r.d_records),
                          reinterpret_cast<u64>(r.d_out_mapped), 0},
                         enqueue);
@@ -622,7 +634,7 @@ class GpuShardEngine final : public ShardEngine {
                                r.d_ctr_mapped, r.lb_dict, r.stream);
       };
       if (r.use_graph())
-        r.launch_cached({4, (u64)nruns, reinterpret_cast<u64>(m.d_records),
+        r.launch_cached({4 | (rp_gen_ << 8), (u64)nruns, reinterpret_cast<u64>(m.d_records),
                          reinterpret_cast<u64>(r.d_records), 0, 0},
                         enqueue);
       else
@@ -690,6 +702,7 @@ class GpuShardEngine final : public ShardEngine {
 
   JobConfig cfg_;
   std::unique_ptr<DevicePipeline> mp_, rp_;
+  u64 rp_gen_ = 0;  // bumped whenever rp_ is reallocated (graph keys)
   static constexpr u32 kSpecSamples = 64;  // DistConfig::samples_per_rank default
   ConstKeysSoA local_keys_{};
   std::vector<PackedKey> samples_;

@@ -90,6 +90,17 @@ std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
                                              const std::string& host, int port,
                                              double timeout_s = 300.0);
 
+// Single-process RCCL clique (`ncclCommInitAll` over the node's GPUs):
+// make_rccl_clique creates one communicator per device from the calling thread; each
+// rank's thread then wraps its member (make_rccl_clique_comm sets that thread's device).
+struct RcclCliqueMember {
+  void* handle = nullptr;  // ncclComm_t
+  int rank = 0, world = 1, device = 0;
+};
+std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices);
+std::unique_ptr<Communicator> make_rccl_clique_comm(const RcclCliqueMember& m,
+                                                    double timeout_s = 300.0);
+
 // N virtual ranks inside one process (threads).  With device buffers the all-to-all is
 // done with hipMemcpyAsync between the ranks' buffers, so a single GPU can rehearse the
 // 2/4/8-rank shuffle (RCCL refuses two ranks on one device).
@@ -168,7 +179,12 @@ class ShardEngine {
   // enqueue_merge_slots + enqueue_slot_headers; returns false (nothing enqueued) when the
   // shard needs the synchronous map, so the caller takes that sequence instead.  Saves the
   // graph -> collective -> graph transitions (~9 us per job measured at one rank).
-  using SlotAllgather = std::function<void(const void* send, void* recv, u64 bytes)>;
+  // `allgather` is issued directly at most once per job (`capturing` = false) and may
+  // also be recorded into a capture (`capturing` = true; a refused capture then issues it
+  // directly).  The caller tracks whether it entered the collective, so an exception after
+  // that never makes it enter the all-gather a second time (see run_distributed).
+  using SlotAllgather =
+      std::function<void(const void* send, void* recv, u64 bytes, bool capturing)>;
   virtual bool enqueue_slot_job(const TextInput& shard, u32 slot_records, u32 nslots,
                                 bool root, const SlotAllgather& allgather) {
     return false;
@@ -233,10 +249,19 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts);
 // One process drives `cfg.world` ranks (threads) over the visible GPUs (round robin) with
 // the loopback communicator; rank 0's result is returned.  With Backend::kCpu the ranks
 // use the CPU shard engine.
-DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole);
+// comm: kAuto = an RCCL clique (ncclCommInitAll) when every rank gets a GPU of its own,
+// else loopback (N ranks rehearsed on fewer GPUs; RCCL refuses two ranks per device).
+enum class LocalComm : int { kAuto = 0, kLoopback = 1, kRccl = 2 };
+DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole,
+                                        LocalComm comm = LocalComm::kAuto);
 // Several jobs back to back on the same ranks (engines and communicators persist, as in a
 // long-lived multi-process job); rank 0's result of every job.
 std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig>& schedule,
-                                                    const TextInput& whole);
+                                                    const TextInput& whole,
+                                                    LocalComm comm = LocalComm::kAuto);
+// Visible GPUs (0 if none or the runtime fails).
+int visible_device_count();
+// Which communicator run_single_process_* would use for `world` ranks (for logging).
+LocalComm resolve_local_comm(const DistConfig& cfg, LocalComm comm);
 
 }  // namespace locust

@@ -40,7 +40,8 @@ using dev::wave_id;
 constexpr int kPre = 64;   // left context staged before the tile (line-ordinal scans)
 constexpr int kPost = 64;  // right overhang staged after the tile (>= 40 for packing)
 
-// Delimiter set incl. '\n' and NUL, held in scalar registers.
+// Delimiter set incl. '\n' and NUL (a NUL also kills the rest of its line, see
+// backward_line_ordinal), held in scalar registers.
 struct Delims {
   u64 m0, m1, m2, m3;
   __device__ __forceinline__ bool has(u32 c) const {
@@ -67,11 +68,19 @@ struct TileText {
   }
 };
 
-// Token starts since the last '\n' strictly before `pos`, saturated at cap + 1.
+// Token starts since the last '\n' strictly before `pos`, saturated at cap + 1, and whether
+// the line is already dead at `pos`: the reference tokenizes a NUL-terminated copy of the
+// line (my_strcpy, /root/reference/MapReduce/src/main.cu:55-59), so bytes after an embedded
+// NUL up to the next '\n' are invisible.  The scan stops at the line's '\n', at a NUL (the
+// rest of the line is dead), or once the count saturates: a saturated ordinal already
+// suppresses every later emit (and the overflow count) of the line, exactly as dead bytes
+// would, so a NUL further back need not be found.
 template <typename TT>
-__device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32 cap) {
+__device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32 cap,
+                                     bool* dead) {
   const int lane = lane_id();
   u32 count = 0;
+  *dead = false;
   i64 hi = pos;  // scan [hi - 64, hi)
   while (hi > 0) {
     const i64 p = hi - 64 + lane;
@@ -79,11 +88,20 @@ __device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32
     const u32 cprev = tt.at(p - 1);
     const bool start = !d.has(c) && d.has(cprev);
     const u64 nl = ballot(c == '\n');
+    const u64 nul = ballot(c == 0u);
     u64 st = ballot(start);
     if (nl) {
       const int last_nl = 63 - __clzll((long long)nl);
-      st &= (last_nl >= 63) ? 0ull : (~0ull << (last_nl + 1));
-      count += __popcll(st);
+      const u64 after = (last_nl >= 63) ? 0ull : (~0ull << (last_nl + 1));
+      if (nul & after) {
+        *dead = true;
+        break;
+      }
+      count += __popcll(st & after);
+      break;
+    }
+    if (nul) {
+      *dead = true;
       break;
     }
     count += __popcll(st);
@@ -176,7 +194,8 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   const int seg_lds = kPre + w * kSeg;
 
   // ---- phase 1: delimiter masks, token starts, in-line ordinals, emit masks ----
-  u32 line_ord = backward_line_ordinal(tt, seg, d, (u32)E);
+  bool line_dead;  // an embedded NUL earlier in the current line (see backward scan)
+  u32 line_ord = backward_line_ordinal(tt, seg, d, (u32)E, &line_dead);
   bool prev_delim = d.has(s_text[seg_lds - 1]);
   u64 emit_mask[kSteps];
   u64 dmask[kSteps + 1];
@@ -191,10 +210,17 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     dmask[s] = ballot(is_d);
     const bool pd = lane == 0 ? prev_delim : ((dmask[s] >> (lane - 1)) & 1ull);
     prev_delim = (dmask[s] >> 63) & 1ull;
-    const bool start = in && !is_d && pd;
-    const u64 st = ballot(start);
     const u64 nl = ballot(in && c == '\n');
+    const u64 nul = ballot(in && c == 0u);
     const u64 nl_below = nl & below;
+    // Dead byte: a NUL after the line's last '\n' below this lane (or carried in).
+    bool dead = line_dead && !nl_below;
+    if (const u64 nul_below = nul & below) {
+      dead = dead || !nl_below || (63 - __clzll((long long)nul_below)) >
+                                      (63 - __clzll((long long)nl_below));
+    }
+    const bool start = in && !is_d && pd && !dead;
+    const u64 st = ballot(start);
     u32 ord;
     if (nl_below) {
       const int q = 63 - __clzll((long long)nl_below);
@@ -209,8 +235,10 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     if (nl) {
       const int q = 63 - __clzll((long long)nl);
       line_ord = (q >= 63) ? 0 : __popcll(st & (~0ull << (q + 1)));
+      line_dead = (q >= 63) ? false : ((nul >> (q + 1)) != 0ull);
     } else {
       line_ord += __popcll(st);
+      line_dead = line_dead || nul != 0ull;
     }
     if (line_ord > (u32)E + 1) line_ord = (u32)E + 1;
   }

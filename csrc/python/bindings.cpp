@@ -185,21 +185,31 @@ py::list strtok_r_tokens(const std::string& line, const std::string& delims) {
   return out;
 }
 
-PyResult run_multi(const std::string& text, const DistConfig& cfg) {
+LocalComm local_comm(const std::string& c) {
+  if (c == "auto") return LocalComm::kAuto;
+  if (c == "loopback") return LocalComm::kLoopback;
+  if (c == "rccl") return LocalComm::kRccl;
+  throw Error("comm must be auto, loopback or rccl, not " + c);
+}
+
+PyResult run_multi(const std::string& text, const DistConfig& cfg, const std::string& comm) {
   TextInput in = as_input(text);
+  const LocalComm lc = local_comm(comm);
   py::gil_scoped_release nogil;
-  DistResult d = run_single_process_multi_gpu(cfg, in);
+  DistResult d = run_single_process_multi_gpu(cfg, in, lc);
   return PyResult{d.result};
 }
 
 py::dict dist_to_dict(const DistResult& d);
 
-py::list run_multi_schedule(const std::string& text, const std::vector<DistConfig>& schedule) {
+py::list run_multi_schedule(const std::string& text, const std::vector<DistConfig>& schedule,
+                            const std::string& comm) {
   TextInput in = as_input(text);
+  const LocalComm lc = local_comm(comm);
   std::vector<DistResult> rs;
   {
     py::gil_scoped_release nogil;
-    rs = run_single_process_schedule(schedule, in);
+    rs = run_single_process_schedule(schedule, in, lc);
   }
   py::list out;
   for (const auto& d : rs) out.append(py::make_tuple(PyResult{d.result}, dist_to_dict(d)));
@@ -395,9 +405,16 @@ PYBIND11_MODULE(_locust, m) {
     return out;
   });
   m.def("run_multi_schedule", &run_multi_schedule, py::arg("text"), py::arg("schedule"),
-        "Several loopback jobs back to back on the same ranks; [(Result, info)] of rank 0.");
-  m.def("run_multi", &run_multi, py::arg("text"), py::arg("cfg"),
-        "Loopback multi-rank WordCount in this process (one thread per rank).");
+        py::arg("comm") = "auto",
+        "Several jobs back to back on the same in-process ranks; [(Result, info)] of rank 0.");
+  m.def("run_multi", &run_multi, py::arg("text"), py::arg("cfg"), py::arg("comm") = "auto",
+        "Multi-rank WordCount in this process (one thread per rank): an RCCL clique "
+        "(ncclCommInitAll) when every rank has a GPU of its own, else loopback.");
+  m.def("device_count", &visible_device_count,
+        "Visible GPUs (initialises the HIP runtime in this process).");
+  m.def("local_comm_for", [](const DistConfig& cfg, const std::string& comm) {
+    return resolve_local_comm(cfg, local_comm(comm)) == LocalComm::kRccl ? "rccl" : "loopback";
+  }, py::arg("cfg"), py::arg("comm") = "auto");
 
   m.def(
       "gen_text",

@@ -20,7 +20,15 @@ Quick start::
 """
 from __future__ import annotations
 
-from ._native import REPO_ROOT, build, cli_path, load
+import os as _os
+
+# Captured RCCL collectives (the gather-slot job replays map + all-gather + merge as one
+# hipGraph) stay on RCCL's own connection buffers instead of IPC-registering ours.  Set
+# once, at import, before any RCCL communicator or engine thread exists; a user's explicit
+# setting wins.
+_os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
+
+from ._native import REPO_ROOT, build, cli_path, load  # noqa: E402
 
 _C = load()
 

@@ -81,11 +81,14 @@ def wordcount_file(path: str, line_start: int = -1, line_end: int = -1, backend:
 
 
 def run_multi(text: bytes, world: int, backend: str = "gpu", combine: bool = True,
-              samples_per_rank: int = 64, strategy: str | None = None, **kw):
-    """Multi-rank WordCount in this process (loopback communicator, one thread per rank)."""
+              samples_per_rank: int = 64, strategy: str | None = None, comm: str = "auto",
+              **kw):
+    """Multi-rank WordCount in this process, one thread per rank.  comm="auto": an RCCL
+    clique (ncclCommInitAll over xGMI) when every rank has a GPU of its own, else the
+    loopback communicator (device copies; rehearses N ranks on fewer GPUs)."""
     dcfg = make_dist_config(world, make_config(backend, combine=combine, **kw),
                             samples_per_rank=samples_per_rank, strategy=strategy)
-    return _C.run_multi(text, dcfg)
+    return _C.run_multi(text, dcfg, comm)
 
 
 @dataclass

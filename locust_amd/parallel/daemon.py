@@ -15,11 +15,15 @@ changes here:
   disconnects mid-run (the launcher aborting a failed job) gets its process group killed.
 * It ran any command anyone on the network sent it.  Here every request must carry the
   daemon's shared secret (``LOCUST_TOKEN`` or ``--token-file``; without one the daemon
-  creates a random token in ``<root>/token``, mode 0600), and it only starts the
+  creates a random token in ``<root>/token``, mode 0600; a token file or root that another
+  uid owns, that is group/world accessible or that is a symlink is refused, and the
+  default root is per-user: ``$XDG_RUNTIME_DIR/locust`` or ``~/.cache/locust``, mode
+  0700), and it only starts the
   framework's own programs (this repository's ``MapReduce`` binary, ``bench.py``, an
   allow-listed ``locust_amd`` module -- never a program that runs a command line it is
   given), from the repository root, with only rank-layout and ``LOCUST_*`` variables
-  settable.  File transfer (spill files) is confined to ``--root``.
+  settable.  File transfer (spill files) is confined to ``--root``; files
+  are opened with ``O_NOFOLLOW`` and the opened file's real path is checked again.
 
 Requests (JSON frames, see protocol.py): ``hello``, ``run`` {argv, env, timeout},
 ``get`` {path, offset, length}, ``put`` {path, data, append}.  The reference's
@@ -34,6 +38,7 @@ import os
 import signal
 import socket
 import socketserver
+import stat
 import subprocess
 import sys
 import threading
@@ -76,14 +81,50 @@ def _env_allowed(env: dict) -> bool:
                for k in env)
 
 
+def default_root() -> str:
+    """Per-user daemon root: $XDG_RUNTIME_DIR/locust, else ~/.cache/locust (never a shared
+    /tmp path another local user could create first)."""
+    base = os.environ.get("XDG_RUNTIME_DIR") or os.path.join(os.path.expanduser("~"), ".cache")
+    return os.path.join(base, "locust")
+
+
+def _check_private(path: str, what: str) -> None:
+    """Refuse a token file / root not owned by this uid or accessible by group/others."""
+    st = os.lstat(path)
+    if stat.S_ISLNK(st.st_mode):
+        raise PermissionError(f"{what} {path!r} is a symlink")
+    if st.st_uid != os.getuid():
+        raise PermissionError(f"{what} {path!r} is owned by uid {st.st_uid}, not {os.getuid()}")
+    if st.st_mode & 0o077:
+        raise PermissionError(f"{what} {path!r} is group/world accessible "
+                              f"(mode {stat.S_IMODE(st.st_mode):o}); chmod go= it")
+
+
+def ensure_private_dir(root: str) -> str:
+    """Create `root` mode 0700 (or verify an existing one is ours and private)."""
+    root = os.path.abspath(root)
+    os.makedirs(os.path.dirname(root), exist_ok=True)
+    try:
+        os.mkdir(root, 0o700)
+    except FileExistsError:
+        pass
+    _check_private(root, "daemon root")
+    return os.path.realpath(root)
+
+
 def load_or_create_token(root: str, token_file: str | None = None) -> str:
     """The daemon's shared secret: LOCUST_TOKEN, the token file, or a fresh random token
-    written to <root>/token (mode 0600) for the launcher to read."""
+    written to <root>/token (mode 0600) for the launcher to read.  A token file that is
+    not ours or is readable by others is refused (someone else may have planted it)."""
     if os.environ.get("LOCUST_TOKEN"):
         return os.environ["LOCUST_TOKEN"]
+    if token_file is None:
+        root = ensure_private_dir(root)
     path = token_file or os.path.join(root, "token")
-    if os.path.exists(path):
-        with open(path, encoding="utf-8") as f:
+    if os.path.lexists(path):
+        _check_private(path, "token file")
+        fd = os.open(path, os.O_RDONLY | os.O_NOFOLLOW)
+        with os.fdopen(fd, encoding="utf-8") as f:
             tok = f.read().strip()
         if tok:
             return tok
@@ -91,7 +132,7 @@ def load_or_create_token(root: str, token_file: str | None = None) -> str:
 
     tok = secrets.token_hex(24)
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_NOFOLLOW, 0o600)
     with os.fdopen(fd, "w", encoding="utf-8") as f:
         f.write(tok + "\n")
     return tok
@@ -105,9 +146,8 @@ class _Server(socketserver.ThreadingTCPServer):
         if not token:
             raise ValueError("the daemon needs a token (LOCUST_TOKEN or a token file)")
         super().__init__(addr, _Handler)
-        self.root = os.path.realpath(root)
+        self.root = ensure_private_dir(root)
         self.token = token
-        os.makedirs(self.root, exist_ok=True)
 
 
 class _Handler(socketserver.BaseRequestHandler):
@@ -172,7 +212,9 @@ class _Handler(socketserver.BaseRequestHandler):
         if op == "get":
             path = self._path(req.get("path", ""))
             off, length = int(req.get("offset", 0)), int(req.get("length", 64 << 20))
-            with open(path, "rb") as f:
+            # O_NOFOLLOW + a re-check of the opened file: a symlink planted between the
+            # realpath check and the open cannot redirect the read out of the root
+            with os.fdopen(self._open_checked(path, os.O_RDONLY), "rb") as f:
                 f.seek(off)
                 data = f.read(length)
                 eof = f.tell() >= os.fstat(f.fileno()).st_size
@@ -181,7 +223,8 @@ class _Handler(socketserver.BaseRequestHandler):
         if op == "put":
             path = self._path(req.get("path", ""))
             os.makedirs(os.path.dirname(path), exist_ok=True)
-            with open(path, "ab" if req.get("append") else "wb") as f:
+            flags = os.O_WRONLY | os.O_CREAT | (os.O_APPEND if req.get("append") else os.O_TRUNC)
+            with os.fdopen(self._open_checked(path, flags), "ab" if req.get("append") else "wb") as f:
                 f.write(base64.b64decode(req.get("data", "")))
             return {"ok": True}
         return {"ok": False, "error": f"unknown op {op!r}"}
@@ -196,6 +239,17 @@ class _Handler(socketserver.BaseRequestHandler):
                 except PermissionError:
                     return a
         return None
+
+    def _open_checked(self, path: str, flags: int) -> int:
+        fd = os.open(path, flags | os.O_NOFOLLOW, 0o600)
+        try:
+            real = os.path.realpath(f"/proc/self/fd/{fd}") if os.path.exists("/proc/self/fd") else path
+            if real != self.server.root and not real.startswith(self.server.root + os.sep):
+                raise PermissionError(f"path {path!r} escapes the daemon root")
+        except BaseException:
+            os.close(fd)
+            raise
+        return fd
 
     def _path(self, rel: str) -> str:
         p = os.path.realpath(os.path.join(self.server.root, rel))
@@ -274,8 +328,9 @@ def _kill_group(p: subprocess.Popen) -> None:
             continue
 
 
-def serve(bind: str = "127.0.0.1", port: int = 1337, root: str = "/tmp/locust",
+def serve(bind: str = "127.0.0.1", port: int = 1337, root: str | None = None,
           token: str | None = None, ready=None) -> None:
+    root = root or default_root()
     token = token or load_or_create_token(root)
     with _Server((bind, port), root, token) as srv:
         if ready is not None:
@@ -289,10 +344,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--bind", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=1337)
-    ap.add_argument("--root", default="/tmp/locust", help="directory for file transfers")
+    ap.add_argument("--root", default=None,
+                    help="directory for file transfers, mode 0700 (default: "
+                         "$XDG_RUNTIME_DIR/locust or ~/.cache/locust)")
     ap.add_argument("--token-file", default=None,
                     help="shared secret file (default: LOCUST_TOKEN, else <root>/token)")
     a = ap.parse_args(argv)
+    a.root = a.root or default_root()
     token = load_or_create_token(a.root, a.token_file)
     try:
         serve(a.bind, a.port, a.root, token)

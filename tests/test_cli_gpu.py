@@ -1,0 +1,99 @@
+"""`./MapReduce` on the GPU: the reference's minimum slice end to end --
+positional CLI, stdout protocol (main.cu:358-532: `Running`, `Using custom start and end
+locations`, `Length:`, `GPU mapping|stream compaction and sorting|reduce ... nanoseconds`,
+`print key: %s \\t val: %d \\t count: %d`, `Done`), both reduce paths, the stage split on
+the GPU and the in-process multi-rank mode (`--gpus N`: an RCCL clique when the node has
+N GPUs, loopback ranks otherwise)."""
+import re
+import subprocess
+
+import pytest
+
+from locust_amd.utils import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def run(cli, *args):
+    p = subprocess.run([cli, *map(str, args)], capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr.decode()
+    return p
+
+
+def result_lines(out: bytes) -> bytes:
+    return b"".join(l + b"\n" for l in out.split(b"\n") if l.startswith(b"print key:"))
+
+
+def check_protocol(out: bytes, text: bytes, window=None):
+    lines = out.split(b"\n")
+    assert lines[0] == b"Running"
+    i = 1
+    if window:
+        assert lines[i] == b"Using custom start and end locations: (%d, %d)" % window
+        i += 1
+    nlines = len(oracle.split_lines(text))
+    assert lines[i] == b"Length: %d" % nlines
+    stages = [l for l in lines if l.startswith(b"GPU ")]
+    assert [re.sub(rb"\d+", b"N", l) for l in stages] == [
+        b"GPU mapping N nanoseconds ", b"GPU stream compaction and sorting N nanoseconds ",
+        b"GPU reduce N nanoseconds "]
+    entries = oracle.wordcount(text)[0]
+    assert result_lines(out) == oracle.format_gpu(entries)
+    assert out.endswith(b"\nDone\n")
+
+
+@pytest.mark.parametrize("extra", [[], ["--sort", "radix", "--reduce-path", "lds"],
+                                   ["--sort", "radix", "--reduce-path", "global"],
+                                   ["--map-path", "compat"]],
+                         ids=["default", "radix-lds", "radix-global", "compat"])
+def test_window_0_700(cli, hamlet, extra):
+    p = run(cli, "data/hamlet.txt", 0, 700, *extra)
+    check_protocol(p.stdout, oracle.window(hamlet, 0, 700), window=(0, 700))
+    d = {k: c for k, _v, c in oracle.wordcount(oracle.window(hamlet, 0, 700))[0]}
+    assert d[b"the"] == 143 and len(d) == 1566
+
+
+@pytest.mark.parametrize("extra", [[], ["--reduce-path", "global", "--sort", "radix"]],
+                         ids=["default", "radix-global"])
+def test_whole_file(cli, hamlet, extra):
+    p = run(cli, "data/hamlet.txt", *extra)
+    check_protocol(p.stdout, hamlet)
+    assert p.stdout.count(b"print key:") == 5608
+
+
+def test_ref_compat_and_ref_timers(cli, hamlet):
+    p = run(cli, "data/hamlet.txt", "--ref-compat", "--ref-timers")
+    text = oracle.window(hamlet, ref_compat=True)
+    check_protocol(p.stdout, text)
+    assert b"print key: THE \t val: " in p.stdout and p.stdout.count(b"print key:") == 5607
+
+
+def test_stage_split_gpu(cli, hamlet, tmp_path):
+    for node, (s, e) in enumerate([(0, 1500), (1500, 3000), (3000, 4463)]):
+        p = run(cli, "data/hamlet.txt", s, e, node, 1, "--spill-dir", tmp_path)
+        assert b"MODE_MULTI: Finished map" in p.stdout
+    files = ",".join(f"{tmp_path}/out.{k}.txt" for k in range(3))
+    p = run(cli, "data/hamlet.txt", 0, 0, 0, 2, "--inputs", files)
+    assert result_lines(p.stdout) == oracle.format_gpu(oracle.wordcount(hamlet)[0])
+
+
+def test_stage_split_gpu_binary(cli, hamlet, tmp_path):
+    for node, (s, e) in enumerate([(0, 2200), (2200, 4463)]):
+        run(cli, "data/hamlet.txt", s, e, node, 1, "--spill-dir", tmp_path,
+            "--spill-format", "binary")
+    files = ",".join(f"{tmp_path}/out.{k}.kv" for k in range(2))
+    p = run(cli, "data/hamlet.txt", 0, 0, 0, 2, "--inputs", files)
+    assert result_lines(p.stdout) == oracle.format_gpu(oracle.wordcount(hamlet)[0])
+
+
+@pytest.mark.parametrize("gpus,comm", [(1, "auto"), (1, "rccl"), (2, "auto"), (3, "loopback")])
+def test_multi_rank_gpu_cli(cli, hamlet, gpus, comm):
+    """--gpus 1 is one RCCL rank (ncclCommInitAll); more ranks than GPUs fall back to
+    loopback ranks sharing the device.  Output byte-identical to one GPU incl. `val`."""
+    p = subprocess.run([cli, "data/hamlet.txt", "--gpus", str(gpus), "--comm", comm],
+                       capture_output=True, timeout=120, env={**__import__("os").environ,
+                                                              "LOCUST_LOG": "info"})
+    assert p.returncode == 0, p.stderr.decode()
+    assert result_lines(p.stdout) == oracle.format_gpu(oracle.wordcount(hamlet)[0])
+    if gpus == 1:
+        assert b"RCCL clique" in p.stderr

@@ -61,3 +61,19 @@ def test_random_texts():
 def test_empty_input():
     r = run_cpu(b"")
     assert r.num_tokens == 0 and r.entries() == []
+
+
+def test_nul_cr_high_bytes():
+    """Embedded NUL ends the line's tokens (main.cu:55-59 copies with my_strcpy); '\\r' and
+    bytes >= 0x80 are key bytes."""
+    rng = random.Random(8)
+    words = [b"abc", b"a\0b", b"\0", b"cr\r", b"\xff\xfe", b"caf\xc3\xa9", b"L" * 31, b"it's"]
+    for _ in range(20):
+        lines = []
+        for _ in range(rng.randint(1, 40)):
+            n = rng.choice([0, 1, 5, 20, 21, 25])
+            lines.append(rng.choice([b" ", b"\0", b"\t"]).join(rng.choice(words) for _ in range(n)))
+        text = b"\n".join(lines) + b"\n"
+        ent, ntok, overflow = oracle.wordcount(text)
+        r = run_cpu(text)
+        assert r.entries() == ent and r.num_tokens == ntok and r.overflow_lines == overflow

@@ -193,7 +193,7 @@ def test_gpu_slot_gather_fault(hamlet, monkeypatch, fault):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("slot_graph", ["1", "0", "refused"])
+@pytest.mark.parametrize("slot_graph", ["1", "0", "refused", "refused_late"])
 def test_gpu_rccl_one_rank_gather_jobs(hamlet, monkeypatch, slot_graph):
     """One RCCL rank (the pool's boxes have one GPU): repeated gather-strategy jobs take
     the slot path -- with LOCUST_SLOT_GRAPH=1 map + all-gather + merge replay as ONE
@@ -202,6 +202,8 @@ def test_gpu_rccl_one_rank_gather_jobs(hamlet, monkeypatch, slot_graph):
     "refused": the capture fails (injected), so the jobs run the same work uncaptured."""
     if slot_graph == "refused":
         monkeypatch.setenv("LOCUST_FAULT", "0:slot_capture")
+    if slot_graph == "refused_late":  # refused after the all-gather was recorded
+        monkeypatch.setenv("LOCUST_FAULT", "0:slot_capture_late")
     monkeypatch.setenv("LOCUST_SLOT_GRAPH", "0" if slot_graph == "0" else "1")
     nlines = hamlet.count(b"\n") + (0 if hamlet.endswith(b"\n") else 1)
     dcfg = lc.make_dist_config(1, lc.make_config("gpu", combine=True), strategy="gather")
@@ -211,3 +213,35 @@ def test_gpu_rccl_one_rank_gather_jobs(hamlet, monkeypatch, slot_graph):
         res, info = dr.run(hamlet, 0)
         assert res.num_tokens == ntok
         assert res.entries() == ent
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_failure_after_allgather_entered(hamlet, monkeypatch):
+    """A failure after this rank issued the slot all-gather fails the job on this rank
+    without entering a second all-gather (the collective sequence must stay in
+    step); the next job (replayed graph, hook silent) succeeds."""
+    monkeypatch.setenv("LOCUST_FAULT", "0:slot_after_allgather")
+    monkeypatch.setenv("LOCUST_SLOT_GRAPH", "1")
+    nlines = hamlet.count(b"\n") + (0 if hamlet.endswith(b"\n") else 1)
+    dcfg = lc.make_dist_config(1, lc.make_config("gpu", combine=True), strategy="gather")
+    dr = lc._C.DistRank(dcfg, 0, "rccl", "127.0.0.1", free_port(), len(hamlet), nlines, 60.0)
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    # A slot-job shape runs once uncaptured (the hook fires: this rank entered the
+    # collective) and is captured + replayed after that (the hook stays silent); which
+    # jobs are new shapes depends on the slot size and the scratch state, so only the
+    # properties are asserted: failures are clean (no hang, no second all-gather), every
+    # successful job is right, and jobs after a failure succeed.
+    outcomes = []
+    for _ in range(6):
+        try:
+            res, _ = dr.run(hamlet, 0)
+            assert res.entries() == ent and res.num_tokens == ntok
+            outcomes.append("ok")
+        except lc.LocustError as e:
+            assert "after the slot all-gather" in str(e)
+            outcomes.append("fail")
+    assert "fail" in outcomes and "ok" in outcomes[outcomes.index("fail"):], outcomes
+    monkeypatch.delenv("LOCUST_FAULT")
+    for _ in range(3):
+        res, _ = dr.run(hamlet, 0)
+        assert res.entries() == ent and res.num_tokens == ntok

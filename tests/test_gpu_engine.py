@@ -105,6 +105,48 @@ def test_long_lines_segment_boundaries():
     assert r.entries() == ent and r.overflow_lines == overflow
 
 
+NASTY_WORDS = [b"abc", b"a\0b", b"\0", b"x\0\0y", b"cr\r", b"\r", b"\xff\xfe", b"\x80z",
+               b"caf\xc3\xa9", b"L" * 31, b"M" * 29, b"N" * 30, b"q" * 70, b"it's", b"\x01\x7f"]
+
+
+@pytest.mark.parametrize("opts", PATHS[:6], ids=["dict", "compat-dict", "fast-lds", "fast-global",
+                                                 "compat-lds", "compat-global"])
+def test_nul_cr_high_bytes_long_tokens(opts):
+    """An embedded NUL ends its line's token stream (my_strcpy stops there, main.cu:55-59);
+    '\r' and bytes >= 0x80 are ordinary key bytes; tokens over 29 bytes are truncated."""
+    rng = random.Random(77)
+    for trial in range(10):
+        lines = []
+        for _ in range(rng.randint(1, 300)):
+            n = rng.choice([0, 1, 3, 19, 20, 21, 25])
+            sep = rng.choice([b" ", b", ", b"\t", b"\0", b" \0 "])
+            lines.append(sep.join(rng.choice(NASTY_WORDS) for _ in range(n)))
+        text = b"\n".join(lines) + (b"\n" if trial % 2 else b"")
+        ent, ntok, overflow = oracle.wordcount(text)
+        r = gpu(text, **opts)
+        assert r.entries() == ent, trial
+        assert r.num_tokens == ntok
+        assert r.overflow_lines == overflow
+
+
+@pytest.mark.parametrize("sort", ["dict", "radix"])
+def test_nul_across_segments_and_tiles(sort):
+    """A NUL far before a wave segment / tile boundary still kills the rest of the line,
+    and the next line starts live again (the carried dead state resets at '\n')."""
+    rng = random.Random(9)
+    lines = []
+    for i in range(60):
+        pre = b" ".join(b"p%d" % rng.randint(0, 30) for _ in range(rng.randint(0, 25)))
+        post = b" ".join(b"d%d" % rng.randint(0, 30) for _ in range(rng.randint(0, 900)))
+        pad = b" " * rng.randint(0, 5000)
+        nul = b"\0" if i % 3 else b" "
+        lines.append(pre + pad + nul + pad + post)
+    text = b"\n".join(lines) + b"\n"
+    ent, ntok, overflow = oracle.wordcount(text)
+    r = gpu(text, sort=sort)
+    assert r.entries() == ent and r.num_tokens == ntok and r.overflow_lines == overflow
+
+
 def test_empty_and_delimiter_only():
     for text in (b"", b"\n\n\n", b" ,.;\n--\n"):
         r = gpu(text)

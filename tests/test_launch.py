@@ -91,6 +91,30 @@ def test_daemon_creates_private_token(tmp_path):
     assert daemon.load_or_create_token(str(tmp_path / "r")) == tok
 
 
+def test_daemon_refuses_planted_token_and_open_root(tmp_path):
+    """a token file someone else could have written (group/world readable, a
+    symlink) or a root others can enter is refused instead of trusted."""
+    root = tmp_path / "r"
+    root.mkdir(mode=0o700)
+    tok = root / "token"
+    tok.write_text("known-secret\n")
+    os.chmod(tok, 0o644)
+    with pytest.raises(PermissionError, match="token file"):
+        daemon.load_or_create_token(str(root))
+    tok.unlink()
+    (tmp_path / "elsewhere").write_text("known-secret\n")
+    os.chmod(tmp_path / "elsewhere", 0o600)
+    os.symlink(tmp_path / "elsewhere", tok)
+    with pytest.raises(PermissionError, match="symlink"):
+        daemon.load_or_create_token(str(root))
+    open_root = tmp_path / "open"
+    open_root.mkdir()
+    os.chmod(open_root, 0o755)
+    with pytest.raises(PermissionError, match="daemon root"):
+        daemon.load_or_create_token(str(open_root))
+    assert daemon.default_root().endswith("locust") and not daemon.default_root().startswith("/tmp/locust")
+
+
 def test_launch_local_env_and_failure_propagation(tmp_path):
     out = tmp_path / "ranks"
     out.mkdir()
