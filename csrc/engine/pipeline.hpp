@@ -22,6 +22,7 @@
 #include "locust/engine.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
+#include "locust/partmap.hpp"
 #include "locust/trace.hpp"
 
 namespace locust {
@@ -132,6 +133,15 @@ struct DevicePipeline {
   OutRecord* d_out_mapped = nullptr;  // device view of h_out
   MapCounters* h_ctr_mapped = nullptr;
   MapCounters* d_ctr_mapped = nullptr;
+  // Partition map of the ordered dictionary build (PartMap / locust/partmap.hpp): device
+  // tables (persist across jobs), a pinned staging image, and the per-partition work the
+  // ordered kernel reports each run (host-mapped) from which the host decides to retune.
+  PartMapTables* d_pmap = nullptr;
+  PartMapTables* h_pmap = nullptr;
+  u32* h_pw = nullptr;
+  u32* d_pw = nullptr;
+  u64 pm_predicted_max = 0;  // predicted max partition work of the current map (0: default)
+  u32 pm_retunes = 0;
   u64* h_keys = nullptr;  // staging for key up/downloads (4 words x cap)
   PackedKey* h_small = nullptr;
   u64* h_u64 = nullptr;
@@ -307,6 +317,16 @@ struct DevicePipeline {
                                    hipHostMallocMapped | hipHostMallocCoherent));
     LOCUST_HIP_CHECK(
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_ctr_mapped), h_ctr_mapped, 0));
+    LOCUST_HIP_CHECK(hipMalloc(&d_pmap, sizeof(PartMapTables)));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_pmap, sizeof(PartMapTables), hipHostMallocDefault));
+    part_map_default(h_pmap);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_pmap, h_pmap, sizeof(PartMapTables), hipMemcpyHostToDevice,
+                                    stream));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_pw, kDictParts * sizeof(u32),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h_pw, 0, kDictParts * sizeof(u32));
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_pw), h_pw, 0));
+    LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
     std::memset(h_ctr, 0, sizeof(MapCounters));
@@ -333,8 +353,10 @@ struct DevicePipeline {
     if (stream) (void)hipStreamDestroy(stream);
     if (arena.base) (void)hipFree(arena.base);
     for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_keys,
-                    (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped})
+                    (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped, (void*)h_pmap,
+                    (void*)h_pw})
       if (p) (void)hipHostFree(p);
+    if (d_pmap) (void)hipFree(d_pmap);
   }
 
   // ---- host-mapped output buffers (zero-copy emit target AND zero-copy results) ----
@@ -569,7 +591,7 @@ struct DevicePipeline {
       part_tiles = table_tiles(in.bytes);
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
-                      stream, map_trace(), part_tiles ? d_part_off : nullptr);
+                      stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map());
     }
   }
 
@@ -669,8 +691,72 @@ struct DevicePipeline {
     ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
     ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
   }
+  // Device view of this pipeline's partition map (tables live at fixed addresses, so
+  // captured graphs stay valid when the host retunes the contents).
+  PartMap part_map() const {
+    PartMap pm;
+    pm.base = d_pmap->base;
+    pm.thr = d_pmap->thr;
+    pm.lo = d_pmap->lo;
+    return pm;
+  }
+  // After a successful ordered run (ordered kernel wrote h_pw and the sorted output
+  // `e[0..n)`): if its partitions were badly unbalanced, rebuild the map from this output
+  // for the next job.  Cheap to check (256 words); a rebuild is one pass over the output.
+  // Largest reported partition work when a rebuild looks worthwhile, else 0.
+  u64 retune_wanted() const {
+    if (const char* v = std::getenv("LOCUST_PART_TUNE"))
+      if (v[0] == '0') return 0;
+    u64 sum = 0, mx = 0;
+    for (int p = 0; p < kDictParts; ++p) {
+      sum += h_pw[p];
+      mx = std::max<u64>(mx, h_pw[p]);
+    }
+    if (sum < (1u << 13) || mx * kDictParts <= 2 * sum) return 0;  // small or balanced
+    if (pm_predicted_max && mx * 4 <= pm_predicted_max * 5) return 0;  // as good as it gets
+    return mx;
+  }
+  void maybe_retune(const WordCountEntry* e, u64 n) {
+    if (const u64 mx = retune_wanted()) {
+      PartMapTables t;
+      retune_with(mx, part_map_from_entries(e, n, &t), t);
+    }
+  }
+  // The same when the sorted output is device KeyCount records (the distributed map): one
+  // D2H of them, only when a rebuild is due.
+  void maybe_retune_records(const KeyCount* d_recs, u64 n) {
+    const u64 mx = retune_wanted();
+    if (!mx || !n) return;
+    std::vector<KeyCount> h(n);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(h.data(), d_recs, n * sizeof(KeyCount), hipMemcpyDeviceToHost,
+                                    stream));
+    sync();
+    std::vector<WordCountEntry> e(n);
+    for (u64 i = 0; i < n; ++i) {
+      for (int w = 0; w < kKeyWords; ++w) e[i].key.w[w] = h[i].w[w];
+      e[i].count = h[i].count;
+      e[i].val = 0;
+    }
+    PartMapTables t;
+    retune_with(mx, part_map_from_entries(e.data(), n, &t), t);
+  }
+  void retune_with(u64 mx, u64 pred, const PartMapTables& t) {
+    if (!pred || pred * 5 >= mx * 4) {  // < 20 % better: keep the map, stop asking
+      pm_predicted_max = mx;
+      return;
+    }
+    *h_pmap = t;
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_pmap, h_pmap, sizeof(PartMapTables), hipMemcpyHostToDevice,
+                                    stream));
+    pm_predicted_max = pred;
+    ++pm_retunes;
+    LOCUST_LOG_DEBUG("partition map retuned (#%u): max partition work %llu -> %llu",
+                     pm_retunes, (unsigned long long)mx, (unsigned long long)pred);
+  }
   void enqueue_dict_ordered(bool with_counts, bool mapped, bool self_clean = false) {
     OrderedExtra ex;
+    ex.pm = part_map();
+    ex.part_w = d_pw;
     if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
     if (self_clean) set_self_clean(ex);
     set_tile_source(ex, with_counts);
@@ -723,16 +809,33 @@ struct DevicePipeline {
     std::vector<u64> t(kDictParts * 16);
     LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
     // stamps: 0 start, 1 built, 2 published, 8 histogram, 7 bucketed, 9 ranked, 3 sorted,
-    // 4 prefix known, 5 written; 6 = distinct keys
+    // 4 prefix known, 5 written; 6 = distinct keys; 10 / 11 = entry / exit on the 100 MHz
+    // device-wide clock (the kernel's critical path across workgroups)
+    u64 first_in = ~0ull, last_out = 0;
+    int last_p = -1;
+    for (int p = 0; p < kDictParts; ++p) {
+      const u64* x = &t[p * 16];
+      if (!x[10]) continue;
+      first_in = std::min(first_in, x[10]);
+      if (x[11] > last_out) {
+        last_out = x[11];
+        last_p = p;
+      }
+    }
+    if (last_p >= 0)
+      std::fprintf(stderr, "ord span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
+                   (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 16 + 6]);
     for (int p = 0; p < kDictParts; ++p) {
       const u64* x = &t[p * 16];
       if (!x[0] || !x[6]) continue;
       auto d = [&](int a, int b) { return (unsigned long long)(x[a] && x[b] ? x[b] - x[a] : 0); };
       std::fprintf(stderr,
                    "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
-                   " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu\n",
+                   " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
+                   " | clear=%5llu list=%5llu gather=%5llu\n",
                    p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
-                   d(2, 8), d(8, 7), d(7, 9), d(9, 3));
+                   d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
+                   (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13));
     }
   }
   // Process + emit of a dictionary run; returns true if the ordered kernel was used.
@@ -957,6 +1060,7 @@ struct DevicePipeline {
         fill_counters(r);
         copy_out(r.entries, h_ctr->num_unique);
         r.times.host_copy_ms = (now_ns() - t_synced) * 1e-6;
+        if (ordered_done) maybe_retune(r.entries.data(), r.entries.size());
       }
     } else {
       enqueue_process((u32)in.num_lines, compat, false);

@@ -140,6 +140,8 @@ class GpuShardEngine final : public ShardEngine {
     // The ordered kernel writes the records, the SoA keys + counts, the slot header and the
     // host-mapped counters itself: no conversion kernel, no counter copy.
     OrderedExtra ex;
+    ex.pm = m.part_map();
+    ex.part_w = m.d_pw;
     ex.recs = m.d_records;
     ex.sorted = m.sorted;
     ex.counts = m.d_sorted_counts;
@@ -190,6 +192,7 @@ class GpuShardEngine final : public ShardEngine {
     *m.h_ctr = *m.h_ctr_mapped;
     if (!(m.h_ctr->flags & kCtrDictOverflow)) {
       m.sync_clean = true;  // the kernel re-zeroed the scratch (see enqueue_small_ordered)
+      m.maybe_retune_records(m.d_records, m.h_ctr->num_unique);
       if (spec_samples_) {
         samples_.assign(m.h_small, m.h_small + kSpecSamples);
         samples_valid_ = true;
@@ -535,7 +538,8 @@ class GpuShardEngine final : public ShardEngine {
     r.select_out();  // the previous job's entries may still hold the last output buffer
     // The all-to-all finished on mp_'s stream (blocking), so rp_'s stream may start.
     r.set_num_records(n);
-    launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream);
+    launch_unpack_records(r.d_records, n, r.tokens, r.d_counts, r.d_parts, r.stream,
+                          r.part_map());
     r.parts_ready = true;
     r.part_tiles = 0;  // tokens from records: partition tags only
     WordCountResult tmp;
@@ -631,7 +635,7 @@ class GpuShardEngine final : public ShardEngine {
         LOCUST_HIP_CHECK(hipMemcpyAsync(d_meta, meta, (1 + (u64)nruns) * sizeof(u32),
                                         hipMemcpyHostToDevice, r.stream));
         launch_dict_merge_runs(m.d_records, r.d_records, d_meta, r.d_ctr, r.d_out_mapped,
-                               r.d_ctr_mapped, r.lb_dict, r.stream);
+                               r.d_ctr_mapped, r.lb_dict, r.stream, r.part_map());
       };
       if (r.use_graph())
         r.launch_cached({4 | (rp_gen_ << 8), (u64)nruns, reinterpret_cast<u64>(m.d_records),

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace locust {
 namespace dev {
@@ -25,16 +26,35 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-// Inclusive prefix sum across the 64 lanes of a wave.
+// DPP lane moves (GFX9 / CDNA: row_shr within 16-lane rows, row_bcast across rows): a
+// register-to-register move in the VALU, a few cycles -- unlike __shfl_* (ds_bpermute, an
+// LDS round trip).  Lanes without a source keep `old` (0 here).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint64_t dpp_mov(uint64_t v) {
+  const uint32_t lo = dpp_mov<kCtrl, kRowMask>((uint32_t)v);
+  const uint32_t hi = dpp_mov<kCtrl, kRowMask>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive prefix sum across the 64 lanes of a wave: Hillis-Steele inside each 16-lane
+// row by row_shr 1/2/4/8, then row 15's total broadcast into rows 1 and 3 and row 31's
+// into rows 2 and 3 (the classic GFX9 DPP scan; 6 moves + 6 adds, no LDS traffic).
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_scan(T v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    T n = __shfl_up(v, off, 64);
-    if (lane >= off) v += n;
-  }
-  return v;
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit scan");
+  using U = typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type;
+  U x = (U)v;
+  x += dpp_mov<0x111, 0xf>(x);  // row_shr:1
+  x += dpp_mov<0x112, 0xf>(x);  // row_shr:2
+  x += dpp_mov<0x114, 0xf>(x);  // row_shr:4
+  x += dpp_mov<0x118, 0xf>(x);  // row_shr:8
+  x += dpp_mov<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp_mov<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+  return (T)x;
 }
 
 template <typename T>
@@ -56,6 +76,9 @@ __device__ __forceinline__ T wave_reduce_max(T v) {
 
 // Workgroup-wide exclusive scan of one value per thread.  `smem` needs
 // (blockDim.x/64 + 1) slots.  Returns the exclusive prefix; *total receives the sum.
+// One barrier: every wave publishes its total, then each thread adds up the totals of
+// the waves below it (kWaves broadcast LDS reads) instead of one thread scanning them
+// serially between two barriers.
 template <typename T, int kBlock>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* smem, T* total) {
   constexpr int kWaves = kBlock / 64;
@@ -63,21 +86,16 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* smem, T* total) {
   T inc = wave_inclusive_scan(v);
   if (lane == 63) smem[w] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    T run = 0;
+  T below = 0, all = 0;
 #pragma unroll
-    for (int i = 0; i < kWaves; ++i) {
-      T t = smem[i];
-      smem[i] = run;
-      run += t;
-    }
-    smem[kWaves] = run;
+  for (int i = 0; i < kWaves; ++i) {
+    const T t = smem[i];
+    below += i < w ? t : T(0);
+    all += t;
   }
-  __syncthreads();
-  T res = smem[w] + inc - v;
-  *total = smem[kWaves];
+  *total = all;
   __syncthreads();  // smem reusable by the caller after return
-  return res;
+  return below + inc - v;
 }
 
 // ---- agent-scope (device-wide, cross-XCD) atomics used by look-back protocols ----

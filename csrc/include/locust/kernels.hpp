@@ -12,6 +12,7 @@
 #include "locust/dstring.hpp"
 #include "locust/engine.hpp"
 #include "locust/kv.hpp"
+#include "locust/partmap.hpp"
 #include "locust/slot.hpp"
 
 namespace locust {
@@ -77,6 +78,13 @@ void launch_compact_slots(const u32* line_counts, u32 num_lines, int emits_per_l
                           ConstKeysSoA slots, KeysSoA out, MapCounters* ctr,
                           LookbackScratch lb, hipStream_t s);
 
+// ---------------- partition map: see locust/partmap.hpp ----------------
+struct PartMap {                 // device view of a PartMapTables image
+  const u8* base = nullptr;      // [256]; null: partition = first key byte
+  const u64* thr = nullptr;      // [256] thresholds, one byte each, ascending, 0 = unused
+  const u32* lo = nullptr;       // [kDictParts + 1]
+};
+
 // Byte-parallel tokenizer: tokens compacted in text order straight into `out`.
 // trace (diagnostics, optional): per tile < 4096, s_memrealtime stamps at trace[t*8+0..5].
 // part_off (optional, inputs below kMapLargeInput): the tokens of each 1 KiB tile are
@@ -87,7 +95,7 @@ constexpr int kPartTable = 257;
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
-                     u32* part_off = nullptr);
+                     u32* part_off = nullptr, PartMap pm = PartMap{});
 
 // ---------------- radix_sort.hip ----------------
 constexpr int kSortBlock = 256;
@@ -190,12 +198,12 @@ struct DictWorkspace {
 // byte of its key, written by the map kernel or by unpack_records); workgroup p aggregates
 // partition p in LDS and appends its distinct keys to ukeys/ucount (and zeroes uval/urank).
 // No table and no reset needed.  parts must be readable up to align_up(n, 16).
-constexpr int kDictParts = 256;
 constexpr u64 kPartBuildMaxTokens = 1ull << 18;  // beyond: the HBM-table insert scales better
 void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                             const u32* d_n, u64 cap, const DictWorkspace& dw, MapCounters* ctr,
                             hipStream_t s);
-// Ordered build (partition = first key byte): aggregation, per-partition LDS sort,
+// Ordered build (partitions = PartMap ranges, default the first key byte): aggregation,
+// per-partition LDS sort,
 // look-back offsets and the final (key, val, count) records in ONE kernel.  `out` needs
 // room for every distinct key; `lb` needs kDictParts + 1 zeroed status words and a zeroed
 // tile counter.  Sets ctr->num_unique / total_count (and ctr_out, if given, like the
@@ -225,6 +233,11 @@ struct OrderedExtra {
   const u32* part_off = nullptr;
   u32 part_tiles = 0;
   u32 variant = 0;              // A/B switches for kernel experiments (LOCUST_ORD_VARIANT)
+  // The partition map the tokens' partitions were computed with (default: first byte).
+  PartMap pm{};
+  // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x
+  // distinct keys), written every run; the host retunes `pm` when it is unbalanced.
+  u32* part_w = nullptr;
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
@@ -236,7 +249,7 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
 constexpr int kMaxMergeRunsHost = kMaxSlotRanks;
 void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                             MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
-                            LookbackScratch lb, hipStream_t s);
+                            LookbackScratch lb, hipStream_t s, PartMap pm = PartMap{});
 // ---------------- merge.hip ----------------
 // Merge of sorted runs (same run layout and meta as launch_dict_merge_runs) by lock-step
 // binary search + one look-back scan: `merged` (room for every record, bounded by `cap`)
@@ -286,7 +299,7 @@ void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u
 // AoS KeyCount -> SoA keys + counts (+ parts, optional: partition tag per record for the
 // partitioned dictionary builds).
 void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,
-                           hipStream_t s);
+                           hipStream_t s, PartMap pm = PartMap{});
 // S evenly spaced keys of a sorted array of *d_n keys: sample[k] = keys[floor((k+0.5)*n/S)].
 void launch_sample_keys(ConstKeysSoA sorted, const u32* d_n, u32 num_samples, PackedKey* out,
                         hipStream_t s);

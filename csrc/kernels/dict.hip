@@ -245,6 +245,50 @@ __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 
   return false;
 }
 
+// Gathers and inserts the tokens s_list[0 .. lim): every thread issues the first-word
+// loads of up to kGatherBatch tokens before it inserts any, so a partition of up to
+// kGatherBatch x 1,024 tokens pays ONE global-load latency instead of one per 1,024-token
+// round (the tokens were written by the map on other XCDs: these are L2 misses).  Longer
+// keys' further words are rare (English words fit in 8 bytes) and gathered after.
+constexpr int kGatherBatch = 4;
+__device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* counts,
+                                              const u32* s_list, u32 lim, u32 n_cap,
+                                              LdsSlot* s_tab) {
+  bool full = false;
+  for (u32 e0 = 0; e0 < lim; e0 += kGatherBatch * kPartBlock) {
+    u32 idx[kGatherBatch];
+    u64 k[kGatherBatch][kKeyWords];
+    u64 c[kGatherBatch];
+#pragma unroll
+    for (int r = 0; r < kGatherBatch; ++r) {
+      const u32 e = e0 + (u32)r * kPartBlock + threadIdx.x;
+      idx[r] = e < lim ? s_list[e] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < kGatherBatch; ++r) {
+      const bool ok = idx[r] < n_cap;
+      k[r][0] = ok ? tokens.w[0][idx[r]] : 0;
+      c[r] = ok ? (counts ? counts[idx[r]] : 1ull) : 0;
+      k[r][1] = k[r][2] = k[r][3] = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kGatherBatch; ++r)
+      if (k[r][0] & 0xffull) k[r][1] = tokens.w[1][idx[r]];
+#pragma unroll
+    for (int r = 0; r < kGatherBatch; ++r)
+      if (k[r][1] & 0xffull) {
+        k[r][2] = tokens.w[2][idx[r]];
+        if (k[r][2] & 0xffull) k[r][3] = tokens.w[3][idx[r]];
+      }
+#pragma unroll
+    for (int r = 0; r < kGatherBatch; ++r) {
+      const bool live = k[r][0] != 0 && c[r] != 0;
+      if (live) full |= !part_lds_insert(s_tab, k[r], c[r], key_hash(k[r]));
+    }
+  }
+  return full;
+}
+
 // Per round: every thread loads 16 partition bytes (the next round's load is issued before
 // this round's inserts), appends the indices of its partition's tokens to an LDS list,
 // then the whole workgroup gathers those tokens' keys (independent loads across threads)
@@ -348,6 +392,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
 // ---------------------------------------------------------------------------------
 constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
 constexpr u32 kRankChunk = 8;                  // candidates per rank work item
+constexpr u32 kSmallRank = 256;                // partitions up to here: all-pairs ranks
+constexpr u32 kSmallChunk = 32;                // candidates per small-rank work item
 __device__ __forceinline__ u32 div_up_u32(u32 a, u32 b) { return (a + b - 1) / b; }
 constexpr int kOrdOvfShift = 20;
 constexpr int kOrdTokShift = 29;
@@ -375,7 +421,7 @@ struct TagSource {
   // Returns true if the table overflowed.
   struct Pre {};
   __device__ Pre prefetch(u32) const { return {}; }
-  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count, u64*) const {
     // Rounds of kOrdTagWindow tags (32 per thread, two 16-B loads, the next round's
     // prefetched): whole Hamlet (32,940 tokens) is one round + a short tail instead of
     // three.  A round appends at most kPartWindow matches to the list; a partition with
@@ -415,14 +461,7 @@ struct TagSource {
       __syncthreads();
       const u32 cnt = s_count;
       full |= cnt > (u32)kPartWindow;
-      for (u32 e = threadIdx.x; e < min(cnt, (u32)kPartWindow); e += kPartBlock) {
-        const u32 i = s_list[e];
-        u64 k[kKeyWords];
-        load_key(tokens, i, k);
-        const u64 c = counts ? counts[i] : 1ull;
-        if (k[0] == 0 || c == 0) continue;
-        full |= !part_lds_insert(s_tab, k, c, key_hash(k));
-      }
+      full |= gather_insert(tokens, counts, s_list, min(cnt, (u32)kPartWindow), n, s_tab);
       __syncthreads();
       if (threadIdx.x == 0) s_count = 0;
       __syncthreads();
@@ -450,7 +489,9 @@ struct TileSource {
     if (t >= ntiles) return {0, 0};
     return {part_off[(u64)t * kPartTable + p], part_off[(u64)t * kPartTable + p + 1]};
   }
-  __device__ bool build(u32 p, Pre pre, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+  // stamp (diagnostics, optional): [12] list built, [13] gathered + inserted
+  __device__ bool build(u32 p, Pre pre, LdsSlot* s_tab, u32* s_list, u32& s_count,
+                        u64* stamp) const {
     bool full = false;
     for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
       const u32 t = t0 + threadIdx.x;
@@ -473,16 +514,11 @@ struct TileSource {
           if (at < (u32)kPartWindow) s_list[at] = a + j;
       }
       __syncthreads();
+      if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
       const u32 cnt = s_count;
       full |= cnt > (u32)kPartWindow;  // the host redoes the Process stage on the HBM table
-      for (u32 e = threadIdx.x; e < min(cnt, (u32)kPartWindow); e += kPartBlock) {
-        const u32 i = s_list[e];
-        if (i >= n_cap) continue;
-        u64 k[kKeyWords];
-        load_key(tokens, i, k);
-        if (k[0] == 0) continue;
-        full |= !part_lds_insert(s_tab, k, 1ull, key_hash(k));
-      }
+      full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab);
+      if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
       __syncthreads();
       if (threadIdx.x == 0) s_count = 0;
       __syncthreads();
@@ -502,9 +538,14 @@ struct RunsSource {
   const KeyCount* own;
   const KeyCount* recv;
   const u32* meta;
+  PartMap pm;
+  __device__ u32 part(u64 w0) const {
+    const u32 c = (u32)(w0 >> 56);
+    return pm.base ? part_of_prefix(c, (u32)(w0 >> 48) & 0xffu, pm.base[c], pm.thr[c]) : c;
+  }
   struct Pre {};
   __device__ Pre prefetch(u32) const { return {}; }
-  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count) const {
+  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count, u64*) const {
     // s_list: [lo, hi) per run | exclusive prefix of the partition's records | run offsets
     u32* s_lo = s_list;
     u32* s_pre = s_list + 2 * kMaxMergeRuns;
@@ -525,12 +566,12 @@ struct RunsSource {
       u32 a = 0, b = n;  // first record with first byte >= p
       while (a < b) {
         const u32 mid = (a + b) >> 1;
-        if ((u32)(r[mid].w[0] >> 56) < p) a = mid + 1; else b = mid;
+        if (part(r[mid].w[0]) < p) a = mid + 1; else b = mid;
       }
       u32 c = a, d = n;  // first record with first byte > p
       while (c < d) {
         const u32 mid = (c + d) >> 1;
-        if ((u32)(r[mid].w[0] >> 56) <= p) c = mid + 1; else d = mid;
+        if (part(r[mid].w[0]) <= p) c = mid + 1; else d = mid;
       }
       s_lo[2 * q] = a;
       s_lo[2 * q + 1] = c;
@@ -574,22 +615,46 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __shared__ u64 s_scan[kPartBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
+  __shared__ u32 s_cm, s_cfull;  // compaction: distinct keys, overflow flag
+  __shared__ u64 s_ctok;         // compaction: tokens
   // partition = ticket, not blockIdx: a workgroup then only ever waits in the look-back
   // on workgroups that are already running.  With blockIdx, kernels of several processes
   // sharing the GPU (the TCP / loopback rehearsals) could fill the CUs with spinning
   // workgroups whose predecessors were never dispatched: measured as multi-second stalls
   // and a hang with four ranks on one GPU.
+  const u64 rt_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, device-wide
+  // Tickets almost always come out in dispatch order: prefetch the run table for
+  // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.
+  const typename Src::Pre guess = src.prefetch(blockIdx.x);
   const u32 p = dev::acquire_tile(tile_ctr, &s_tile);
   ORD_STAMP(0);
-  const typename Src::Pre first = src.prefetch(p);
+  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 10] = rt_entry;
+  const typename Src::Pre first = p == blockIdx.x ? guess : src.prefetch(p);
+  // This partition's 2-byte-prefix range [plo, phi) (PartMap; default: first byte p).  The
+  // in-partition counting sort buckets keys by their 3-byte prefix scaled into 256
+  // order-preserving buckets: the second byte for a first-byte partition, the third byte
+  // for a partition of one 2-byte prefix ('th').
+  const u32 plo = ex.pm.lo ? ex.pm.lo[p] : p << 8;
+  const u32 phi = ex.pm.lo ? ex.pm.lo[p + 1] : (p + 1) << 8;
+  const u32 span = phi > plo ? phi - plo : 1u;  // 2-byte prefixes in the partition
+  auto bucket_of = [&](u64 w0) -> u32 {
+    const u32 rel = (u32)(w0 >> 40) - (plo << 8);  // < span * 256
+    return span == 256u ? rel >> 8 : span == 1u ? rel : rel / span;
+  };
   for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
 #pragma unroll
     for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
     s_tab[i].count = 0;
   }
-  if (threadIdx.x == 0) s_count = 0;
+  if (threadIdx.x == 0) {
+    s_count = 0;
+    s_cm = 0;
+    s_ctok = 0;
+    s_cfull = 0;
+  }
   __syncthreads();
-  const bool full = src.build(p, first, s_tab, s_list, s_count);
+  ORD_STAMP(14);  // table cleared
+  const bool full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)p * 16 : nullptr);
   ORD_STAMP(1);
   // ---- compact: dense (w0, slot) arrays in the list area ----
   u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
@@ -604,33 +669,164 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       wsum += sl.count;
     }
   }
-  // ONE block scan carries all three sums: [tokens:41][full threads:11][distinct keys:12]
-  u64 packed_total = 0;
-  const u64 packed = (u64)mine | ((u64)(full ? 1 : 0) << 12) | (wsum << 23);
-  const u64 packed_excl =
-      dev::block_exclusive_scan<u64, kPartBlock>(packed, s_scan, &packed_total);
-  const u32 excl = (u32)(packed_excl & 0xfffu);
-  const u32 m = (u32)(packed_total & 0xfffu);
-  const int any_full = ((packed_total >> 12) & 0x7ffu) != 0;
-  const u64 tok = packed_total >> 23;
+  // Positions in the compacted arrays: any order will do (they are sorted next), so a wave
+  // takes its slice with ONE LDS atomic and its lanes' offsets come from two ballots --
+  // no block scan, one barrier.  Token sums and the overflow flag ride along.
+  u64* s_cnt = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);  // [kSmallRank] counts
+  u32* s_rk = s_list + 3 * kPartSlots + 2 * kSmallRank;         // [kSmallRank] ranks
+  u64* s_less = reinterpret_cast<u64*>(s_rk + kSmallRank);       // [kSmallRank] vals
+  u64* s_out = s_less + kSmallRank;                              // [6 x kSmallRank] records
   {
-    u32 d = excl;
+    const u64 b0 = dev::ballot(mine >= 1), b1 = dev::ballot(mine >= 2);
+    const u64 wfull = dev::ballot(full);
+    const u64 wtok_incl = dev::wave_inclusive_scan(wsum);
+    u32 wbase = 0;
+    if (dev::lane_id() == 63) {
+      wbase = atomicAdd(&s_cm, (u32)(__popcll(b0) + __popcll(b1)));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_ctok), (unsigned long long)wtok_incl);
+      if (wfull) s_cfull = 1u;
+    }
+    wbase = (u32)__builtin_amdgcn_readlane((int)wbase, 63);
+    u32 d = wbase + dev::lanes_below(b0) + dev::lanes_below(b1);
 #pragma unroll
     for (int r = 0; r < kPartPerThread; ++r) {
       const u32 slot = threadIdx.x * kPartPerThread + r;
       if (s_tab[slot].w[0]) {
         s_w0[d] = s_tab[slot].w[0];
         s_slot[d] = slot;
+        if (d < kSmallRank) s_cnt[d] = s_tab[slot].count;
         ++d;
       }
     }
+    if (threadIdx.x < kSmallRank) {
+      s_rk[threadIdx.x] = 0;
+      s_less[threadIdx.x] = 0;
+    }
   }
-  __syncthreads();  // the compacted (w0, slot) arrays are complete
+  __syncthreads();  // the compacted (w0, slot) arrays and the sums are complete
+  const u32 m = s_cm;
+  const int any_full = s_cfull != 0u;
+  const u64 tok = s_ctok;
+  // Small partitions (the common case once the partition map is balanced) skip the
+  // bucket sort: ranks AND vals come from one all-pairs pass (see below).
+  const bool small = !(ex.variant & 1u) && !any_full && m <= kSmallRank;  // variant 1: A/B
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
   if (threadIdx.x == 0) dev::publish_aggregate(status, p, agg);
   ORD_STAMP(2);
+  u64 pre = 0;
+  if (small) {
+    // ---- small partition: weighted all-pairs ranks.  Work item = (key i, chunk of
+    // kSmallChunk candidates j); rank_i += #{j < i}, val_i += sum of their counts -- the
+    // sorted position AND the reference's val (start of the key's run) in one pass, no
+    // bucket sort, no count scan.  Consecutive lanes take consecutive keys of one chunk,
+    // so candidate reads are LDS broadcasts.  Wave 0 resolves the look-back meanwhile. ----
+    if (dev::wave_id() == 0) {
+      // Look-back in ONE round trip: wave 0 reads every predecessor's status word at once
+      // (4 per lane, p < 256) instead of walking back 64 words per dependent round trip
+      // (~1-2 us each across XCDs).  prefix = the highest inclusive value found + the
+      // aggregates above it.  Predecessors hold lower tickets, so they are running and
+      // publish soon; a lane spins until its word is published.
+      const u32 lane = (u32)dev::lane_id();
+      u64 st[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32 q = lane + 64u * k;
+        st[k] = q < p ? dev::ld_agent(&status[q]) : dev::kLbAgg;  // beyond p: aggregate 0
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32 q = lane + 64u * k;
+        while (q < p && (st[k] >> dev::kLbFlagShift) == 0) {
+          __builtin_amdgcn_s_sleep(1);
+          st[k] = dev::ld_agent(&status[q]);
+        }
+      }
+      int hi_inc = -1;  // highest predecessor with an inclusive value
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u64 b = dev::ballot((st[k] >> dev::kLbFlagShift) == 2);
+        if (b) hi_inc = 64 * k + 63 - __clzll((long long)b);
+      }
+      u64 v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = (int)lane + 64 * k;
+        if (q >= hi_inc && q < (int)p) v += st[k] & dev::kLbValMask;
+      }
+      v = dev::wave_inclusive_scan(v);
+      if (lane == 63) s_prefix = v;
+    } else if (m > 1) {
+      const u32 items = m * div_up_u32(m, kSmallChunk);
+      for (u32 e = threadIdx.x - 64; e < items; e += kPartBlock - 64) {
+        const u32 chunk = e / m, i = e - chunk * m;
+        const u64 w = s_w0[i];
+        const u32 j0 = chunk * kSmallChunk, j1 = min(j0 + kSmallChunk, m);
+        u32 cnt = 0;
+        u64 less = 0;
+        bool tie = false;
+        for (u32 j = j0; j < j1; ++j) {
+          const u64 o = s_w0[j];
+          const bool lt = o < w;
+          cnt += lt ? 1u : 0u;
+          less += lt ? s_cnt[j] : 0ull;
+          tie |= o == w && j != i;
+        }
+        if (tie)  // keys sharing their first 8 bytes: order by the remaining words
+          for (u32 j = j0; j < j1; ++j)
+            if (j != i && s_w0[j] == w && ord_greater(w, s_slot[i], w, s_slot[j], s_tab)) {
+              ++cnt;
+              less += s_cnt[j];
+            }
+        if (cnt) {
+          atomicAdd(&s_rk[i], cnt);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&s_less[i]), (unsigned long long)less);
+        }
+      }
+    }
+    __syncthreads();
+    pre = s_prefix;
+    if (threadIdx.x == 0 && p != 0)  // inclusive value for later walkers (large partitions)
+      dev::st_agent(&status[p], dev::kLbInc | (pre + agg));
+    ORD_STAMP(3);
+    ORD_STAMP(4);
+    const u64 base_tok = pre >> kOrdTokShift;
+    // stage the records in sorted order, then write them with consecutive lanes on
+    // consecutive words (full lines: matters most for the host-mapped output)
+    for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
+      const LdsSlot& sl = s_tab[s_slot[i]];
+      u64* o = s_out + 6 * s_rk[i];
+      o[0] = sl.w[0];
+      o[1] = sl.w[1] ^ kWordMagic;
+      o[2] = sl.w[2] ^ kWordMagic;
+      o[3] = sl.w[3] ^ kWordMagic;
+      o[4] = base_tok + s_less[i];
+      o[5] = sl.count;
+    }
+    __syncthreads();
+    const u64 base_m = pre & kOrdM;
+    if (((pre >> kOrdOvfShift) & 511u) == 0) {  // uniform per workgroup
+      if (out) {
+        u64* dst = reinterpret_cast<u64*>(out + base_m);
+        for (u32 q = threadIdx.x; q < 6 * m; q += kPartBlock) dst[q] = s_out[q];
+      }
+      if (ex.recs) {  // 8-B word q of the KeyCount slice: record q / 5, word q % 5
+        u64* dst = reinterpret_cast<u64*>(ex.recs + base_m);
+        for (u32 q = threadIdx.x; q < 5 * m; q += kPartBlock) {
+          const u32 i = q / 5, wd = q - 5 * i;
+          dst[q] = s_out[6 * i + (wd < kKeyWords ? wd : 5)];
+        }
+      }
+      if (ex.sorted.w[0]) {
+        for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
+#pragma unroll
+          for (int j = 0; j < kKeyWords; ++j) ex.sorted.w[j][base_m + i] = s_out[6 * i + j];
+          if (ex.counts) ex.counts[base_m + i] = s_out[6 * i + 5];
+        }
+      }
+    }
+  } else {
   // ---- sort the partition's keys: counting sort on the SECOND key byte (all keys here
   // share the first), then rank inside each second-byte bucket by all-pairs compares --
   // buckets are small, there are few barriers, and no bitonic network over m keys ----
@@ -647,8 +843,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   __syncthreads();
   if (!any_full && m > 1) {
-    for (u32 a = threadIdx.x; a < m; a += kPartBlock)
-      atomicAdd(&s_hist[(u32)(s_w0[a] >> 48) & 0xffu], 1u);
+    for (u32 a = threadIdx.x; a < m; a += kPartBlock) atomicAdd(&s_hist[bucket_of(s_w0[a])], 1u);
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of 256 bucket sizes by one wave
       const u32 l = threadIdx.x;
@@ -677,7 +872,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     ORD_STAMP(8);  // histogram + bucket scan
     for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
       const u64 w = s_w0[a];
-      const u32 b = (u32)(w >> 48) & 0xffu;
+      const u32 b = bucket_of(w);
       const u32 q = s_off[b] + atomicAdd(&s_cur[b], 1u);
       s_w0b[q] = w;
       s_slotb[q] = s_slot[a];
@@ -726,7 +921,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       ORD_STAMP(9);  // ranks
       for (u32 q = threadIdx.x; q < m; q += kPartBlock) {
         const u64 w = s_w0b[q];
-        const u32 d = s_off[(u32)(w >> 48) & 0xffu] + s_rank[q];
+        const u32 d = s_off[bucket_of(w)] + s_rank[q];
         s_w0[d] = w;
         s_slot[d] = s_slotb[q];
       }
@@ -739,7 +934,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     if (dev::lane_id() == 0) s_prefix = e;
   }
   __syncthreads();
-  const u64 pre = s_prefix;
+  pre = s_prefix;
   ORD_STAMP(4);
   const u64 base_m = pre & kOrdM;
   const u64 base_tok = pre >> kOrdTokShift;
@@ -808,8 +1003,17 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       }
     }
   }
+  }  // bucket-sorted (large) partition
+  const u64 base_m = pre & kOrdM;
+  const u64 base_tok = pre >> kOrdTokShift;
+  const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   ORD_STAMP(5);
   if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 6] = m;
+  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  if (ex.part_w && threadIdx.x == 0) {  // this partition's work, for the host's retuning
+    const u64 w = tok + (u64)kPartDistinctWeight * m;
+    ex.part_w[p] = (u32)(w < 0xffffffffull ? w : 0xffffffffull);
+  }
   // ---- the last partition publishes the run's counters ----
   const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
   if (p == kDictParts - 1 && threadIdx.x == 0) {
@@ -1131,10 +1335,12 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
 
 void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                             MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
-                            LookbackScratch lb, hipStream_t s) {
-  const RunsSource src{own, recv, meta};
+                            LookbackScratch lb, hipStream_t s, PartMap pm) {
+  const RunsSource src{own, recv, meta, pm};
+  OrderedExtra ex;
+  ex.pm = pm;
   dict_ordered_kernel<RunsSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
-      src, ctr, out, ctr_out, lb.status, lb.tile_counter, nullptr, OrderedExtra{});
+      src, ctr, out, ctr_out, lb.status, lb.tile_counter, nullptr, ex);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -35,13 +35,16 @@ __global__ __launch_bounds__(256) void pack_records_kernel(ConstKeysSoA keys,
 __global__ __launch_bounds__(256) void unpack_records_kernel(const KeyCount* __restrict__ in,
                                                              u64 n, KeysSoA keys,
                                                              u64* __restrict__ counts,
-                                                             u8* __restrict__ parts) {
+                                                             u8* __restrict__ parts, PartMap pm) {
   for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     const KeyCount r = in[i];
 #pragma unroll
     for (int w = 0; w < kKeyWords; ++w) keys.w[w][i] = r.w[w];
     counts[i] = r.count;
-    if (parts) parts[i] = (u8)(r.w[0] >> 56);  // first key byte (see launch_dict_ordered)
+    if (parts) {  // partition of the key (see PartMap / launch_dict_ordered)
+      const u32 c = (u32)(r.w[0] >> 56), d = (u32)(r.w[0] >> 48) & 0xffu;
+      parts[i] = (u8)(pm.base ? part_of_prefix(c, d, pm.base[c], pm.thr[c]) : c);
+    }
   }
 }
 
@@ -106,9 +109,10 @@ void launch_pack_records(ConstKeysSoA keys, const u64* counts, const u32* d_n, u
 }
 
 void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts, u8* parts,
-                           hipStream_t s) {
+                           hipStream_t s, PartMap pm) {
   if (!n) return;
-  unpack_records_kernel<<<dim3(grid_for(n, 256)), dim3(256), 0, s>>>(in, n, keys, counts, parts);
+  unpack_records_kernel<<<dim3(grid_for(n, 256)), dim3(256), 0, s>>>(in, n, keys, counts, parts,
+                                                                     pm);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

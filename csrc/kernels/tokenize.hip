@@ -142,7 +142,8 @@ template <int kSteps, int kBlock>
 __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr, u64* __restrict__ trace, u32* __restrict__ part_off) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, u32* __restrict__ part_off,
+    PartMap pm) {
   // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
   // at entry, tile acquired, text staged, masks done, prefix known, keys written.
   const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -156,6 +157,9 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   __shared__ u32 s_wave_cnt[kBlock / 64];
   // partition grouping (kSteps == 1 with part_off): per-partition counts, then offsets
   __shared__ u32 s_pcnt[kSteps == 1 ? kPartTable : 1];
+  // the partition map's rows (PartMap), staged once per tile: 2.3 KB, read per token
+  __shared__ u64 s_pthr[256];
+  __shared__ u8 s_pbase[256];
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
   // Tokens are emitted in no particular order across tiles (every consumer sorts or
@@ -168,6 +172,18 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     if (part_off)
       for (int i = threadIdx.x; i < kPartTable; i += kBlock) s_pcnt[i] = 0;  // before a barrier
   }
+
+  if (pm.base) {  // visible after the staging barrier below
+    for (int i = threadIdx.x; i < 256; i += kBlock) {
+      s_pthr[i] = pm.thr[i];
+      s_pbase[i] = pm.base[i];
+    }
+  }
+  // Partition of a packed key: its row's base + thresholds passed (default: first byte).
+  auto part_of = [&](u64 w0) -> u32 {
+    const u32 c = (u32)(w0 >> 56);
+    return pm.base ? part_of_prefix(c, (u32)(w0 >> 48) & 0xffu, s_pbase[c], s_pthr[c]) : c;
+  };
 
   // ---- stage the tile (+ context) into LDS with 16-B loads ----
   const i64 tile_base = (i64)tile * kTile;
@@ -272,7 +288,7 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
       if (em) {
         len = token_length(dmask[0], dmask[1], lane);
         pack_token(s_text, seg_lds + lane, len < (u32)max_key ? len : (u32)max_key, kw);
-        part = (u32)(kw[0] >> 56);
+        part = part_of(kw[0]);
         loc = atomicAdd(&s_pcnt[part], 1u);
       }
       __syncthreads();
@@ -327,9 +343,9 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
       if (idx < out_cap) {
 #pragma unroll
         for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
-        // partition tag for the dictionary's partitioned builds: the first key byte
-        // (order-preserving, so per-partition sorts concatenate into the global order)
-        if (parts) parts[idx] = (u8)(kw[0] >> 56);
+        // partition tag for the dictionary's partitioned builds (order-preserving, so
+        // per-partition sorts concatenate into the global order)
+        if (parts) parts[idx] = (u8)part_of(kw[0]);
       }
     }
     dst += __popcll(m);
@@ -349,7 +365,8 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
 
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
-                     LookbackScratch lb, hipStream_t s, u64* trace, u32* part_off) {
+                     LookbackScratch lb, hipStream_t s, u64* trace, u32* part_off,
+                     PartMap pm) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   if (bytes < kMapLargeInput) {
@@ -361,13 +378,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace, part_off);
+        lb.tile_counter, trace, part_off, pm);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace, nullptr);
+        lb.tile_counter, trace, nullptr, pm);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }

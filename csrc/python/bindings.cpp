@@ -14,6 +14,7 @@
 #include "locust/engine.hpp"
 #include "locust/gen.hpp"
 #include "locust/io.hpp"
+#include "locust/partmap.hpp"
 
 namespace py = pybind11;
 using namespace locust;
@@ -544,6 +545,27 @@ PYBIND11_MODULE(_locust, m) {
     return std::string(d_itoa(n, buf, base));
   });
   m.def("strcmp", [](const std::string& a, const std::string& b) { return d_strcmp(a.c_str(), b.c_str()); });
+  m.def("part_map_build", [](const std::vector<std::pair<std::string, u64>>& keys) {
+    // Balanced partition map (locust/partmap.hpp) for sorted (key, count) pairs: the
+    // tables plus the predicted largest partition work.
+    std::vector<WordCountEntry> e(keys.size());
+    for (size_t i = 0; i < keys.size(); ++i) {
+      e[i].key = to_key(keys[i].first);
+      e[i].count = keys[i].second;
+      e[i].val = 0;
+    }
+    PartMapTables t;
+    const u64 pred = part_map_from_entries(e.data(), e.size(), &t);
+    py::dict d;
+    d["base"] = std::vector<u32>(t.base, t.base + 256);
+    d["thr"] = std::vector<u64>(t.thr, t.thr + 256);
+    d["lo"] = std::vector<u32>(t.lo, t.lo + kDictParts + 1);
+    d["predicted_max"] = pred;
+    std::vector<u32> part(65536);
+    for (u32 b = 0; b < 65536; ++b) part[b] = part_map_lookup(t, b);
+    d["part"] = part;
+    return d;
+  }, py::arg("keys"));
   m.def("pack_key", [](const std::string& s) {
     PackedKey k = to_key(s);
     return std::vector<u64>(k.w, k.w + kKeyWords);
