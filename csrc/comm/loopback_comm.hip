@@ -113,6 +113,44 @@ class LoopbackComm final : public Communicator {
     st_->barrier();
   }
 
+  // Blocking rehearsals of the stream-ordered all-to-all / gather (see allgather_device).
+  void alltoall_device(const void* send, void* recv, u64 bytes, void* stream) override {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+    st_->ptr[(size_t)rank_] = send;
+    st_->barrier();
+    char* out = static_cast<char*>(recv);
+    for (int r = 0; r < size() && bytes; ++r) {
+      const char* from = static_cast<const char*>(st_->ptr[(size_t)r]) + (u64)rank_ * bytes;
+      if (st_->device)
+        LOCUST_HIP_CHECK(hipMemcpyAsync(out + (u64)r * bytes, from, bytes, hipMemcpyDefault, s));
+      else
+        std::memcpy(out + (u64)r * bytes, from, bytes);
+    }
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+    st_->barrier();
+  }
+
+  void gather_device(const void* send, void* recv, u64 bytes, int root, void* stream) override {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+    st_->ptr[(size_t)rank_] = send;
+    st_->barrier();
+    if (rank_ == root) {
+      char* out = static_cast<char*>(recv);
+      for (int r = 0; r < size() && bytes; ++r) {
+        if (r == root) continue;
+        if (st_->device)
+          LOCUST_HIP_CHECK(hipMemcpyAsync(out + (u64)r * bytes, st_->ptr[(size_t)r], bytes,
+                                          hipMemcpyDefault, s));
+        else
+          std::memcpy(out + (u64)r * bytes, st_->ptr[(size_t)r], bytes);
+      }
+      if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    st_->barrier();
+  }
+
   void sync_stream(void* stream) override {
     if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   }

@@ -150,6 +150,29 @@ class RcclComm final : public Communicator {
     LOCUST_RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
 
+  // ncclAllToAll: every peer's chunk over its own xGMI link at once (no ring).
+  void alltoall_device(const void* send, void* recv, u64 bytes, void* stream) override {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
+    LOCUST_RCCL_CHECK(ncclAllToAll(send, recv, bytes, ncclUint8, comm_, s));
+  }
+
+  // Root receives every other rank's chunk (grouped point-to-point: P-1 links in
+  // parallel into the root); only the root needs the data, so no all-gather.
+  void gather_device(const void* send, void* recv, u64 bytes, int root, void* stream) override {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
+    if (world_ == 1 || !bytes) return;
+    LOCUST_RCCL_CHECK(ncclGroupStart());
+    if (rank_ == root) {
+      for (int r = 0; r < world_; ++r)
+        if (r != root)
+          LOCUST_RCCL_CHECK(ncclRecv(static_cast<char*>(recv) + (u64)r * bytes, bytes, ncclUint8,
+                                     r, comm_, s));
+    } else {
+      LOCUST_RCCL_CHECK(ncclSend(send, bytes, ncclUint8, root, comm_, s));
+    }
+    LOCUST_RCCL_CHECK(ncclGroupEnd());
+  }
+
   void sync_stream(void* stream) override {
     wait(stream ? static_cast<hipStream_t>(stream) : stream_);
   }

@@ -38,6 +38,16 @@ void Communicator::allgather_device(const void*, void*, u64, void*) {
               " communicator has no device data plane");
 }
 
+void Communicator::alltoall_device(const void*, void*, u64, void*) {
+  throw Error(std::string("alltoall_device: the ") + name() +
+              " communicator has no device data plane");
+}
+
+void Communicator::gather_device(const void*, void*, u64, int, void*) {
+  throw Error(std::string("gather_device: the ") + name() +
+              " communicator has no device data plane");
+}
+
 void Communicator::sync_stream(void*) {
   throw Error(std::string("sync_stream: the ") + name() + " communicator has no device streams");
 }

@@ -24,6 +24,7 @@ class GpuShardEngine final : public ShardEngine {
     for (auto& g : slot_graphs_) (void)hipGraphExecDestroy(g.exec);
     if (h_headers_) (void)hipHostFree(h_headers_);
     if (h_send_header_) (void)hipHostFree(h_send_header_);
+    free_exch();
   }
 
   bool device_buffers() const override { return true; }
@@ -420,6 +421,60 @@ class GpuShardEngine final : public ShardEngine {
   }
   const SlotHeader* slot_headers() const override { return h_headers_; }
 
+  // ---- device-resident shuffle (locust/exch.hpp) ----
+  void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples, u32 P,
+                        int me, int root, const ExchCollectives& coll) override {
+    DevicePipeline& m = *mp_;
+    const u32 S = (u32)samples.size();
+    const u32 C = exch_slot_records, G = exch_gather_records;
+    LOCUST_CHECK_ARG(P >= 1 && P <= kExchMaxRanks && C && G, "exchange: bad shape");
+    // everything that can allocate or synchronise happens before the first collective
+    if (!hdr.status) prepare_shuffle();
+    ensure_exch(P, S, C, G);
+    const bool is_root = me == root;
+    if (is_root) {
+      recv_records(std::max<u64>((u64)P * G, 4096));
+      rp_->grow_host_out((u64)P * G);
+    }
+    std::memcpy(xb_.h_msg1, &hdr, sizeof(ExchMsg1));
+    if (S) std::memcpy(xb_.h_msg1 + sizeof(ExchMsg1), samples.data(), (u64)S * sizeof(PackedKey));
+    const u64 mb = exch_msg1_bytes(S), sb = exch_slot_bytes(C);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.msg1_send, xb_.h_msg1, mb, hipMemcpyHostToDevice, m.stream));
+    coll.allgather(xb_.msg1_send, xb_.msg1_all, mb);
+    // a failed map has no valid records: the planner sees the status and every rank's
+    // kernels turn into no-ops, but the collectives still run
+    const u32* d_n = hdr.status ? xb_.zero_n : local_n();
+    launch_exch_plan(xb_.msg1_all, P, S, local_keys(), d_n, C, xb_.ctl, m.stream);
+    launch_exch_pack(m.d_records, d_n, m.cap, xb_.ctl, P, C, xb_.a2a_send, m.stream);
+    coll.alltoall(xb_.a2a_send, xb_.a2a_recv, sb);
+    OutRecord* out = is_root ? xb_.groot + (u64)root * G : xb_.gsend;
+    launch_merge_slots_limited(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, C, xb_.merged,
+                               xb_.rctr, out, G, LookbackScratch{xb_.lb_status, xb_.lb_tile},
+                               m.stream);
+    launch_exch_report(xb_.a2a_recv, P, C, xb_.ctl, xb_.rctr, G, xb_.msg3_send, m.stream);
+    coll.allgather(xb_.msg3_send, xb_.msg3_all, sizeof(ExchMsg3));
+    coll.gather(xb_.gsend, xb_.groot, exch_gslot_bytes(G), root);
+    if (is_root)
+      launch_exch_concat(xb_.groot, xb_.msg3_all, P, G, rp_->d_out_mapped, rp_->d_ctr_mapped,
+                         m.stream);
+    LOCUST_HIP_CHECK(hipMemcpy2DAsync(xb_.h_hdrs, sizeof(ExchMsg1), xb_.msg1_all, mb,
+                                      sizeof(ExchMsg1), P, hipMemcpyDeviceToHost, m.stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.h_msg3, xb_.msg3_all, (u64)P * sizeof(ExchMsg3),
+                                    hipMemcpyDeviceToHost, m.stream));
+  }
+  const ExchMsg1* exch_headers() const override { return xb_.h_hdrs; }
+  const ExchMsg3* exch_reports() const override { return xb_.h_msg3; }
+  void exch_finish_root(u64* total_count, u64* num_unique) override {
+    DevicePipeline& r = *rp_;
+    *r.h_ctr = *r.h_ctr_mapped;
+    WordCountResult tmp;
+    r.fill_counters(tmp);
+    r.copy_out(tmp.entries, r.h_ctr->num_unique);
+    *total_count = r.h_ctr->total_count;
+    *num_unique = r.h_ctr->num_unique;
+    range_entries_ = std::move(tmp.entries);
+  }
+
   u64 complete_map_slot(const TextInput& shard) override {
     if (!slot_fast_) return local_count_;  // mapped synchronously (or failed) already
     return complete_small_ordered(shard);
@@ -746,6 +801,75 @@ class GpuShardEngine final : public ShardEngine {
     LOCUST_HIP_CHECK(
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_headers_), h_headers_, 0));
   }
+  // Buffers of the device exchange, one device allocation sized for (P, S, C, G).
+  struct ExchBufs {
+    u32 P = 0, S = 0, C = 0, G = 0;
+    char* dev = nullptr;
+    char* msg1_send = nullptr;
+    char* msg1_all = nullptr;
+    ExchCtl* ctl = nullptr;
+    char* a2a_send = nullptr;
+    char* a2a_recv = nullptr;
+    ExchMsg3* msg3_send = nullptr;
+    ExchMsg3* msg3_all = nullptr;
+    OutRecord* gsend = nullptr;
+    OutRecord* groot = nullptr;
+    KeyCount* merged = nullptr;
+    u64* lb_status = nullptr;
+    u32* lb_tile = nullptr;
+    u32* zero_n = nullptr;
+    MapCounters* rctr = nullptr;
+    char* h_msg1 = nullptr;      // pinned staging of this rank's message
+    ExchMsg1* h_hdrs = nullptr;  // pinned: every rank's header after the job
+    ExchMsg3* h_msg3 = nullptr;  // pinned: every rank's report after the job
+  } xb_;
+  void free_exch() {
+    if (xb_.dev) (void)hipFree(xb_.dev);
+    for (void* p : {(void*)xb_.h_msg1, (void*)xb_.h_hdrs, (void*)xb_.h_msg3})
+      if (p) (void)hipHostFree(p);
+    xb_ = ExchBufs{};
+  }
+  void ensure_exch(u32 P, u32 S, u32 C, u32 G) {
+    if (xb_.dev && P == xb_.P && S <= xb_.S && C == xb_.C && G == xb_.G) return;
+    LOCUST_HIP_CHECK(hipStreamSynchronize(mp_->stream));  // nothing may still use the old ones
+    free_exch();
+    auto al = [](u64 x) { return align_up(x, (u64)256); };
+    const u64 mb = exch_msg1_bytes(S), sb = exch_slot_bytes(C), gb = exch_gslot_bytes(G);
+    const u64 merge_cap = (u64)P * C;
+    const u64 lbw = merge_scratch_words(merge_cap);
+    u64 off = 0;
+    auto take = [&](u64 bytes) { const u64 o = off; off += al(bytes); return o; };
+    const u64 o_m1 = take(mb), o_m1a = take(mb * P), o_ctl = take(sizeof(ExchCtl)),
+              o_as = take(sb * P), o_ar = take(sb * P), o_m3 = take(sizeof(ExchMsg3)),
+              o_m3a = take(sizeof(ExchMsg3) * P), o_gs = take(gb), o_gr = take(gb * P),
+              o_mg = take(merge_cap * sizeof(KeyCount)), o_lb = take(lbw * 8 + 8),
+              o_lt = take(8), o_zn = take(8), o_rc = take(sizeof(MapCounters));
+    LOCUST_HIP_CHECK(hipMalloc(&xb_.dev, off));
+    LOCUST_HIP_CHECK(hipMemset(xb_.dev, 0, off));
+    char* b = xb_.dev;
+    xb_.P = P;
+    xb_.S = S;
+    xb_.C = C;
+    xb_.G = G;
+    xb_.msg1_send = b + o_m1;
+    xb_.msg1_all = b + o_m1a;
+    xb_.ctl = reinterpret_cast<ExchCtl*>(b + o_ctl);
+    xb_.a2a_send = b + o_as;
+    xb_.a2a_recv = b + o_ar;
+    xb_.msg3_send = reinterpret_cast<ExchMsg3*>(b + o_m3);
+    xb_.msg3_all = reinterpret_cast<ExchMsg3*>(b + o_m3a);
+    xb_.gsend = reinterpret_cast<OutRecord*>(b + o_gs);
+    xb_.groot = reinterpret_cast<OutRecord*>(b + o_gr);
+    xb_.merged = reinterpret_cast<KeyCount*>(b + o_mg);
+    xb_.lb_status = reinterpret_cast<u64*>(b + o_lb);
+    xb_.lb_tile = reinterpret_cast<u32*>(b + o_lt);
+    xb_.zero_n = reinterpret_cast<u32*>(b + o_zn);
+    xb_.rctr = reinterpret_cast<MapCounters*>(b + o_rc);
+    LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_msg1, mb, hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_hdrs, sizeof(ExchMsg1) * P, hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_msg3, sizeof(ExchMsg3) * P, hipHostMallocDefault));
+  }
+
   SlotHeader* h_send_header_ = nullptr;  // pinned staging for a host-written header
   SlotHeader* slot_host_header() {
     if (!h_send_header_)

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "locust/engine.hpp"
+#include "locust/exch.hpp"
 #include "locust/slot.hpp"
 
 namespace locust {
@@ -70,6 +71,13 @@ class Communicator {
   // produces `send`, so no host synchronisation is needed first; complete after
   // sync_stream(stream).  Host-only communicators throw.
   virtual void allgather_device(const void* send, void* recv, u64 bytes, void* stream);
+  // Stream-ordered all-to-all of fixed-size chunks (device_buffers() communicators): chunk
+  // d of `send` goes to rank d, rank s's chunk for this rank lands at recv + s * bytes.
+  virtual void alltoall_device(const void* send, void* recv, u64 bytes, void* stream);
+  // Stream-ordered gather of fixed-size chunks to `root`: rank r's `bytes` land at
+  // recv + r * bytes on the root; the root's own chunk must already be in place there
+  // (recv is only used on the root).
+  virtual void gather_device(const void* send, void* recv, u64 bytes, int root, void* stream);
   // Wait for `stream`, watching for communicator errors (timeouts abort the communicator).
   virtual void sync_stream(void* stream);
   // true: allgather_device only enqueues stream work (no host waits), so it can be
@@ -207,6 +215,29 @@ class ShardEngine {
   // Records a slot can hold on this rank (the all-gather uses the minimum over ranks).
   virtual u64 slot_capacity() const { return 0; }
   u32 slot_records = 0;  // agreed slot size for the next job (0: kSlotRecordsMin)
+
+  // ---- shuffle strategy on the device (locust/exch.hpp): one host synchronisation ----
+  struct ExchCollectives {
+    std::function<void(const void* send, void* recv, u64 bytes)> allgather;
+    std::function<void(const void* send, void* recv, u64 bytes)> alltoall;
+    std::function<void(const void* send, void* recv, u64 bytes, int root)> gather;
+  };
+  // Enqueue the whole exchange of this rank's sorted, distinct records (after map_local
+  // and sample()) on stream(): `hdr` + `samples` are this rank's ExchMsg1; every buffer is
+  // sized before the first collective.  Each collective callback is called exactly once,
+  // in the order allgather, alltoall, allgather, gather.  Results after sync_stream:
+  virtual void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples,
+                                u32 P, int me, int root, const ExchCollectives& coll) {
+    throw Error("this engine has no device exchange");
+  }
+  virtual const ExchMsg1* exch_headers() const { return nullptr; }  // P ExchMsg1 headers
+  virtual const ExchMsg3* exch_reports() const { return nullptr; }  // P reports
+  // Root, after the sync: the concatenated output (as finish_merge_slots).
+  virtual void exch_finish_root(u64* total_count, u64* num_unique) {}
+  // Agreed exchange slot sizes (every rank computes the same from collective data; 0 =
+  // not known yet: the job takes the host-staged shuffle, which then sets them).
+  u32 exch_slot_records = 0, exch_gather_records = 0;
+  u64 exch_last_sum = 0;  // all ranks' records of the last job (auto: gather or shuffle)
   virtual void finalize(u64 global_offset, EntryList* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;
@@ -235,6 +266,7 @@ struct DistResult {
   u64 sent_bytes = 0, recv_bytes = 0;
   u64 range_tokens = 0, range_unique = 0;  // this rank's key range after the shuffle
   DistStrategy strategy = DistStrategy::kShuffle;  // the one this job took
+  bool device_exchange = false;  // the shuffle ran as the one-synchronisation device exchange
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,

@@ -1,0 +1,83 @@
+// Device-resident shuffle ("exchange") of the distributed job: message layouts shared by
+// the host driver (dist.cpp) and the kernels (exchange.hip).  No HIP dependency.
+//
+// The reference has no shuffle at all (/tmp/out.txt with the network hop
+// missing; the GIF's letter-range reducers are design only).  Round 1 built the
+// sample-sort all-to-all with every control step staged through host memory -- five host
+// round trips per job.  The exchange runs the same algorithm with every decision on the
+// device and ONE host synchronisation:
+//
+//   H2D      this rank's ExchMsg1 (status, record count, map statistics) + S samples
+//   C1       ncclAllGather of the messages
+//   plan     one workgroup: weighted-quantile splitters from all ranks' samples (every
+//            rank computes the same), 64-ary searches of them in the local sorted records
+//   pack     records -> P fixed-size slots (SlotHeader + up to `slot_records` records)
+//   C2       ncclAllToAll of the slots (every xGMI link busy at once)
+//   merge    the P received sorted runs -> this rank's key range, local val (merge.hip)
+//   report   ExchMsg3 (overflow flags, range size, token total, largest bucket)
+//   C3       ncclAllGather of the reports: every rank sees every flag and total
+//   C4       gather of the ranges to the root (grouped ncclSend/ncclRecv, fixed size)
+//   concat   root: ranges in rank order (= key order) into host-mapped output, val +=
+//            the token totals of the lower ranks (the reference's global val)
+//
+// Slot sizes are host numbers fixed before the launch: they come from the previous job
+// (largest bucket / range + 1/8).  A job whose data outgrows them is flagged in the
+// reports, which every rank holds, so every rank takes the step-by-step path for that job
+// together and grows the sizes.
+#pragma once
+
+#include "locust/common.hpp"
+#include "locust/kv.hpp"
+
+namespace locust {
+
+struct ExchMsg1 {       // 64 B, followed by S PackedKey samples
+  i32 status;           // 0 = ok
+  u32 record_flags;     // ShardEngine::kRecords* of this rank's records
+  u64 n_local;          // sorted distinct records of this rank
+  u64 lines, tokens, overflow_lines, truncated, max_key_len;
+  u64 pad;
+};
+static_assert(sizeof(ExchMsg1) == 64, "ExchMsg1 64 B");
+
+constexpr u32 kExchSendOverflow = 1;   // a bucket of this rank exceeded the slot
+constexpr u32 kExchRecvTruncated = 2;  // a received slot was truncated or failed
+constexpr u32 kExchAbort = 4;          // a rank's ExchMsg1 reported a failure
+constexpr u32 kExchTooManySamples = 8; // the device planner cannot take this many samples
+
+struct ExchMsg3 {       // 64 B
+  i32 status;           // 0 = ok
+  u32 flags;            // kExch*
+  u64 max_bucket;       // largest bucket this rank had to send
+  u64 n_out;            // distinct keys of this rank's key range
+  u64 total;            // token total of this rank's key range
+  u64 pad[4];
+};
+static_assert(sizeof(ExchMsg3) == 64, "ExchMsg3 64 B");
+
+constexpr u32 kExchGatherOverflow = 16; // this rank's range exceeded the gather slot
+
+constexpr u32 kExchMaxPlanSamples = 1024;  // P x S the one-workgroup planner sorts in LDS
+constexpr u32 kExchSamples = 64;           // samples per rank
+constexpr u32 kExchMaxRanks = 64;
+
+// Device scratch of one exchange, written by the plan kernel, read by pack and report.
+struct ExchCtl {
+  u64 off[kExchMaxRanks + 1];  // bucket offsets in this rank's sorted records
+  u64 max_bucket;
+  u32 flags;                   // kExchSendOverflow | kExchAbort | kExchTooManySamples
+  u32 pad;
+};
+
+LOCUST_HD inline u64 exch_msg1_bytes(u32 samples) { return sizeof(ExchMsg1) + (u64)samples * sizeof(PackedKey); }
+// All-to-all slot: a SlotHeader (two KeyCount records) + slot_records KeyCount records.
+LOCUST_HD inline u64 exch_slot_bytes(u32 slot_records) { return (u64)(2 + slot_records) * sizeof(KeyCount); }
+// Gather slot: gather_records (key, val, count) 48-B records (the size is in ExchMsg3).
+LOCUST_HD inline u64 exch_gslot_bytes(u32 gather_records) { return (u64)gather_records * 48; }
+// Next job's slot size for a largest observed bucket / range of `used` records.
+inline u32 exch_grow(u64 used) {
+  const u64 want = used + used / 8 + 64;
+  return (u32)((want + 63) & ~63ull);
+}
+
+}  // namespace locust

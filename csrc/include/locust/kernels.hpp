@@ -11,6 +11,7 @@
 #include "locust/config.hpp"
 #include "locust/dstring.hpp"
 #include "locust/engine.hpp"
+#include "locust/exch.hpp"
 #include "locust/kv.hpp"
 #include "locust/partmap.hpp"
 #include "locust/slot.hpp"
@@ -307,6 +308,22 @@ void launch_sample_keys(ConstKeysSoA sorted, const u32* d_n, u32 num_samples, Pa
 // offsets[P] = n.
 void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey* splitters,
                            u32 num_buckets, u64* offsets, hipStream_t s);
+
+// ---------------- exchange.hip (device-resident shuffle, locust/exch.hpp) ----------------
+// Merge of nslots all-to-all slots (as launch_merge_slots) writing at most out_limit
+// output records (counters still count all of them).
+void launch_merge_slots_limited(const KeyCount* slots, u32 nslots, u32 slot_records,
+                                KeyCount* merged, MapCounters* ctr, OutRecord* out,
+                                u64 out_limit, LookbackScratch lb, hipStream_t s);
+void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
+                      u32 slot_records, ExchCtl* ctl, hipStream_t s);
+void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchCtl* ctl, u32 P,
+                      u32 slot_records, char* send, hipStream_t s);
+void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
+                        const MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
+                        hipStream_t s);
+void launch_exch_concat(const OutRecord* groot, const ExchMsg3* msg3_all, u32 P,
+                        u32 gather_records, OutRecord* out, MapCounters* ctr_out, hipStream_t s);
 
 // ---- device self-test of the string library (tests only; StringTestOut in engine.hpp) ----
 void launch_string_selftest(const char* blob, const u32* off, u32 n, const char* delims,

@@ -1,0 +1,303 @@
+// Kernels of the device-resident shuffle (locust/exch.hpp): plan (splitters + bucket
+// offsets), pack (records -> fixed-size all-to-all slots), report (this rank's ExchMsg3)
+// and the root's concat (ranges in rank order -> host-mapped output with global val).
+// The merge of the received slots is merge.hip's.  Every decision the round-1 driver made
+// on the host between collectives (dist.cpp: choose_splitters, bucket_offsets, the count
+// and total all-gathers) is taken here on the device, so the whole exchange is enqueued
+// behind the map with no host round trip.
+#include "locust/device/wave.hpp"
+#include "locust/exch.hpp"
+#include "locust/hip_check.hpp"
+#include "locust/kernels.hpp"
+
+namespace locust {
+namespace {
+
+constexpr int kPlanBlock = 1024;
+
+__device__ __forceinline__ bool key4_less(const u64* a, const u64* b) {
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j)
+    if (a[j] != b[j]) return a[j] < b[j];
+  return false;
+}
+
+// ONE workgroup.  (1) every rank's status; (2) the P x S samples sorted in LDS by
+// all-pairs ranks (stable); (3) weighted quantiles -> P-1 splitters: splitter p is the
+// first sample (sorted) whose inclusive weight exceeds total * p / P, each sample of rank r
+// weighing n_local(r) -- every rank computes the same from the same all-gathered bytes;
+// (4) one wave per splitter: lower bound in this rank's sorted keys by a 64-ary search
+// (64 probes per dependent load round instead of one), (5) bucket counts and flags.
+__global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
+    const char* __restrict__ msg1_all, u32 P, u32 S, ConstKeysSoA keys,
+    const u32* __restrict__ d_n, u32 slot_records, ExchCtl* __restrict__ ctl) {
+  __shared__ u64 s_k[kExchMaxPlanSamples][kKeyWords];
+  __shared__ u64 s_w[kExchMaxPlanSamples];
+  __shared__ u32 s_at[kExchMaxPlanSamples];  // sorted position -> sample
+  __shared__ u64 s_incl[kExchMaxPlanSamples];
+  __shared__ u64 s_split[kExchMaxRanks][kKeyWords];
+  __shared__ u64 s_off[kExchMaxRanks + 1];
+  __shared__ u64 s_scan[kPlanBlock / 64 + 1];
+  __shared__ u32 s_flags;
+  __shared__ u64 s_maxb;
+  const u32 t = threadIdx.x;
+  const u64 mb = exch_msg1_bytes(S);
+  const u32 NS = P * S;
+  if (t == 0) {
+    s_flags = (NS > kExchMaxPlanSamples || P > kExchMaxRanks) ? kExchTooManySamples : 0u;
+    s_maxb = 0;
+  }
+  __syncthreads();
+  if (t < P) {
+    const ExchMsg1* h = reinterpret_cast<const ExchMsg1*>(msg1_all + (u64)t * mb);
+    if (h->status) atomicOr(&s_flags, kExchAbort);
+  }
+  const bool fits = NS <= kExchMaxPlanSamples && P <= kExchMaxRanks;
+  if (fits) {
+    for (u32 i = t; i < NS; i += kPlanBlock) {
+      const u32 r = i / S, q = i - r * S;
+      const char* base = msg1_all + (u64)r * mb;
+      const PackedKey* sp = reinterpret_cast<const PackedKey*>(base + sizeof(ExchMsg1));
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) s_k[i][j] = sp[q].w[j];
+      s_w[i] = reinterpret_cast<const ExchMsg1*>(base)->n_local;
+    }
+  }
+  __syncthreads();
+  if (fits) {
+    for (u32 i = t; i < NS; i += kPlanBlock) {  // stable rank of sample i
+      u32 r = 0;
+      for (u32 j = 0; j < NS; ++j) {
+        const bool lt = key4_less(s_k[j], s_k[i]);
+        const bool eq = !lt && !key4_less(s_k[i], s_k[j]);
+        r += (lt || (eq && j < i)) ? 1u : 0u;
+      }
+      s_at[r] = i;
+    }
+  }
+  __syncthreads();
+  // inclusive weight prefix in sorted order (NS <= kPlanBlock: one sample per thread)
+  const u64 w = (fits && t < NS) ? s_w[s_at[t]] : 0ull;
+  u64 total = 0;
+  const u64 excl = dev::block_exclusive_scan<u64, kPlanBlock>(w, s_scan, &total);
+  if (fits && t < NS) s_incl[t] = excl + w;
+  __syncthreads();
+  if (t >= 1 && t < P) {
+    // splitter t-1: first sorted sample with inclusive weight > total * t / P
+    const u64 target = fits ? total * t / P : 0;
+    u32 lo = 0, hi = fits ? NS : 0;
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (s_incl[mid] > target) hi = mid; else lo = mid + 1;
+    }
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) s_split[t - 1][j] = lo < NS && fits ? s_k[s_at[lo]][j] : ~0ull;
+  }
+  __syncthreads();
+  // bucket offsets: wave v searches splitters v, v + 16, ...
+  const u32 n = *d_n;
+  const int lane = dev::lane_id(), wv = dev::wave_id();
+  for (u32 p = (u32)wv; p + 1 < P; p += kPlanBlock / 64) {
+    u64 s[kKeyWords];
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) s[j] = s_split[p][j];
+    u32 lo = 0, hi = n;  // the answer (first key >= s, or n) lies in [lo, hi]
+    while (lo < hi) {
+      const u32 step = (hi - lo + 63) / 64;
+      const u32 pos = lo + (u32)lane * step;
+      bool lt = false;
+      if (pos < hi) {
+        u64 k[kKeyWords];
+#pragma unroll
+        for (int j = 0; j < kKeyWords; ++j) k[j] = keys.w[j][pos];
+        lt = key4_less(k, s);
+      }
+      const u64 b = dev::ballot(lt);
+      const u32 cnt = (u32)__popcll(b);  // probes below s: a prefix of the lanes
+      if (cnt == 0) {
+        hi = lo;
+      } else {
+        const u32 last = lo + (cnt - 1) * step;  // key[last] < s
+        const u32 nxt = lo + cnt * step;         // first probe >= s (if inside)
+        lo = last + 1;
+        if (nxt < hi) hi = nxt;
+      }
+    }
+    if (lane == 0) s_off[p + 1] = lo;
+  }
+  if (t == 0) {
+    s_off[0] = 0;
+    s_off[P < kExchMaxRanks ? P : kExchMaxRanks] = n;
+  }
+  __syncthreads();
+  if (t < P && P <= kExchMaxRanks) {
+    const u64 c = s_off[t + 1] - s_off[t];
+    atomicMax(reinterpret_cast<unsigned long long*>(&s_maxb), (unsigned long long)c);
+    if (c > slot_records) atomicOr(&s_flags, kExchSendOverflow);
+  }
+  __syncthreads();
+  for (u32 i = t; i <= P && i <= kExchMaxRanks; i += kPlanBlock) ctl->off[i] = s_off[i];
+  if (t == 0) {
+    ctl->flags = s_flags;
+    ctl->max_bucket = s_maxb;
+  }
+}
+
+// Records -> the P all-to-all slots: record i of bucket d goes to slot d position
+// i - off[d] (buckets are contiguous in the sorted records); block 0 writes the headers.
+__global__ __launch_bounds__(256) void exch_pack_kernel(const KeyCount* __restrict__ recs,
+                                                        const u32* __restrict__ d_n,
+                                                        const ExchCtl* __restrict__ ctl, u32 P,
+                                                        u32 slot_records, char* __restrict__ send) {
+  __shared__ u64 s_off[kExchMaxRanks + 1];
+  for (u32 i = threadIdx.x; i <= P; i += 256) s_off[i] = ctl->off[i];
+  const u32 flags = ctl->flags;
+  __syncthreads();
+  const u64 sb = exch_slot_bytes(slot_records);
+  if (blockIdx.x == 0 && threadIdx.x < P) {
+    const u32 d = threadIdx.x;
+    const u64 c = s_off[d + 1] - s_off[d];
+    SlotHeader h{};
+    h.status = (flags & (kExchAbort | kExchTooManySamples)) ? kSlotFailed
+               : c > slot_records                           ? kSlotRedo
+                                                            : kSlotOk;
+    h.record_flags = 3u;  // sorted, distinct (ShardEngine::kRecordsSorted | kRecordsDistinct)
+    h.n = c;
+    h.slot_cap = slot_records;
+    *reinterpret_cast<SlotHeader*>(send + (u64)d * sb) = h;
+  }
+  if (flags & (kExchAbort | kExchTooManySamples)) return;
+  const u32 n = *d_n;
+  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    u32 lo = 0, hi = P;  // last d with off[d] <= i
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) >> 1;
+      if (s_off[mid] <= i) lo = mid; else hi = mid;
+    }
+    const u64 j = i - s_off[lo];
+    if (j < slot_records) {
+      KeyCount* dst = reinterpret_cast<KeyCount*>(send + (u64)lo * sb) + kSlotHeaderRecords;
+      dst[j] = recs[i];
+    }
+  }
+}
+
+// This rank's report: flags (own plan + any truncated / failed incoming slot + a range
+// larger than the gather slot), largest bucket, range size and token total.
+__global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict__ recv, u32 P,
+                                                         u32 slot_records,
+                                                         const ExchCtl* __restrict__ ctl,
+                                                         const MapCounters* __restrict__ rctr,
+                                                         u32 gather_records,
+                                                         ExchMsg3* __restrict__ msg3) {
+  const u64 sb = exch_slot_bytes(slot_records);
+  bool bad = false;
+  for (u32 q = threadIdx.x; q < P; q += 64) {
+    const SlotHeader* h = reinterpret_cast<const SlotHeader*>(recv + (u64)q * sb);
+    bad |= h->status != kSlotOk || h->n > slot_records;
+  }
+  const u64 any = dev::ballot(bad);
+  if (threadIdx.x == 0) {
+    ExchMsg3 m{};
+    const u32 cf = ctl->flags;
+    const u64 n_out = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : rctr->num_unique;
+    m.status = 0;
+    m.flags = cf | (any ? kExchRecvTruncated : 0u) | (n_out > gather_records ? kExchGatherOverflow : 0u);
+    m.max_bucket = ctl->max_bucket;
+    m.n_out = n_out;
+    m.total = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : rctr->total_count;
+    *msg3 = m;
+  }
+}
+
+// Root: P gathered ranges (G records each, the first n_out(r) valid, val local to the
+// range) -> host-mapped output in rank order = key order, val += token totals of the lower
+// ranks.  16-B chunks, consecutive lanes on consecutive chunks (full PCIe lines).
+__global__ __launch_bounds__(256) void exch_concat_kernel(const OutRecord* __restrict__ groot,
+                                                          const ExchMsg3* __restrict__ msg3_all,
+                                                          u32 P, u32 gather_records,
+                                                          OutRecord* __restrict__ out,
+                                                          MapCounters* __restrict__ ctr_out) {
+  __shared__ u64 s_roff[kExchMaxRanks + 1], s_voff[kExchMaxRanks + 1];
+  __shared__ u32 s_bad;
+  if (threadIdx.x == 0) {
+    u64 r = 0, v = 0;
+    u32 bad = 0;
+    for (u32 q = 0; q < P && q < kExchMaxRanks; ++q) {
+      s_roff[q] = r;
+      s_voff[q] = v;
+      const ExchMsg3 m = msg3_all[q];
+      bad |= (u32)m.status | m.flags;
+      r += m.n_out <= gather_records ? m.n_out : gather_records;
+      v += m.total;
+    }
+    s_roff[P] = r;
+    s_voff[P] = v;
+    s_bad = bad;
+  }
+  __syncthreads();
+  if (s_bad) return;  // the host sees the reports and takes the step-by-step path
+  const u64 N = s_roff[P];
+  const uint4* src = reinterpret_cast<const uint4*>(groot);
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  for (u64 q = (u64)blockIdx.x * 256 + threadIdx.x; q < 3 * N; q += (u64)gridDim.x * 256) {
+    const u64 rec = q / 3;
+    const u32 part = (u32)(q - 3 * rec);
+    u32 lo = 0, hi = P;  // rank of output record `rec`: last r with roff[r] <= rec
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) >> 1;
+      if (s_roff[mid] <= rec) lo = mid; else hi = mid;
+    }
+    const u64 i = rec - s_roff[lo];
+    uint4 v = src[((u64)lo * gather_records + i) * 3 + part];
+    if (part == 2) {  // {val, count}: val becomes global
+      const u64 val = (((u64)v.y << 32) | v.x) + s_voff[lo];
+      v.x = (u32)val;
+      v.y = (u32)(val >> 32);
+    }
+    dst[q] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
+    MapCounters c{};
+    c.num_records = (u32)N;
+    c.num_unique = (u32)N;
+    c.total_count = s_voff[P];
+    *ctr_out = c;
+  }
+}
+
+}  // namespace
+
+void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
+                      u32 slot_records, ExchCtl* ctl, hipStream_t s) {
+  exch_plan_kernel<<<dim3(1), dim3(kPlanBlock), 0, s>>>(msg1_all, P, S, keys, d_n, slot_records,
+                                                         ctl);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchCtl* ctl, u32 P,
+                      u32 slot_records, char* send, hipStream_t s) {
+  const u64 blocks = std::min<u64>(std::max<u64>(div_up(cap ? cap : 1, 256), 1), 4096);
+  exch_pack_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(recs, d_n, ctl, P, slot_records, send);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
+                        const MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
+                        hipStream_t s) {
+  exch_report_kernel<<<dim3(1), dim3(64), 0, s>>>(recv, P, slot_records, ctl, rctr,
+                                                   gather_records, msg3);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_exch_concat(const OutRecord* groot, const ExchMsg3* msg3_all, u32 P,
+                        u32 gather_records, OutRecord* out, MapCounters* ctr_out,
+                        hipStream_t s) {
+  const u64 chunks = 3ull * P * gather_records;
+  const u64 blocks = std::min<u64>(std::max<u64>(div_up(chunks ? chunks : 1, 256), 1), 2048);
+  exch_concat_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(groot, msg3_all, P, gather_records,
+                                                             out, ctr_out);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace locust

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
 __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
     const KeyCount* __restrict__ merged, RunsView view, MapCounters* __restrict__ ctr,
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr) {
+    u32* __restrict__ tile_ctr, u64 out_limit) {
   __shared__ u64 s_scan[kMergeBlock / 64 + 1];
   __shared__ u32 s_tile;
   __shared__ u64 s_prefix;
@@ -260,10 +260,13 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
   __syncthreads();
   const u32 m = (u32)(tile_sum >> kEmitCountBits);
   const u64 base = before >> kEmitCountBits;
-  // consecutive lanes, consecutive 16-B chunks of out[base .. base + m)
+  // consecutive lanes, consecutive 16-B chunks of out[base .. base + m), at most
+  // out_limit records in all (the exchange's fixed gather slot: the count still says how
+  // many there were, and the report flags the overflow)
+  const u32 mw = base >= out_limit ? 0u : (u32)min((u64)m, out_limit - base);
   const uint4* src = reinterpret_cast<const uint4*>(s_out);
   uint4* dst = reinterpret_cast<uint4*>(out + base);
-  for (u32 q = threadIdx.x; q < 3 * m; q += kMergeBlock) dst[q] = src[q];
+  for (u32 q = threadIdx.x; q < 3 * mw; q += kMergeBlock) dst[q] = src[q];
   if (tile == ntiles - 1 && threadIdx.x == 0) {
     const u64 all = before + tile_sum;
     const u32 u = (u32)(all >> kEmitCountBits);
@@ -283,7 +286,7 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
 
 void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters* ctr,
                        OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
-                       SlotHeader* hdr_out, hipStream_t s) {
+                       SlotHeader* hdr_out, hipStream_t s, u64 out_limit = ~0ull) {
   const u64 c = cap ? cap : 1;
   const u32 rank_grid = (u32)std::min<u64>(div_up(c * kMergeSub, kMergeBlock), 8192);
   const u32 emit_grid = (u32)div_up(c, (u64)kEmitTile);
@@ -291,7 +294,8 @@ void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters
                                                                   hdr_out);
   LOCUST_HIP_LAUNCH_CHECK();
   merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, v, ctr, out, ctr_out,
-                                                                  lb.status, lb.tile_counter);
+                                                                  lb.status, lb.tile_counter,
+                                                                  out_limit);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
@@ -311,6 +315,14 @@ void launch_merge_slots(const KeyCount* slots, u32 nslots, u32 slot_records, Key
                         LookbackScratch lb, SlotHeader* hdr_out, hipStream_t s) {
   launch_merge_view(RunsView{nullptr, nullptr, nullptr, slots, nslots, slot_records},
                     (u64)nslots * slot_records, merged, ctr, out, ctr_out, lb, hdr_out, s);
+}
+
+void launch_merge_slots_limited(const KeyCount* slots, u32 nslots, u32 slot_records,
+                                KeyCount* merged, MapCounters* ctr, OutRecord* out,
+                                u64 out_limit, LookbackScratch lb, hipStream_t s) {
+  launch_merge_view(RunsView{nullptr, nullptr, nullptr, slots, nslots, slot_records},
+                    (u64)nslots * slot_records, merged, ctr, out, nullptr, lb, nullptr, s,
+                    out_limit);
 }
 
 }  // namespace locust

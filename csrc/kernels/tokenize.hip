@@ -37,7 +37,12 @@ using dev::lane_id;
 using dev::lanes_below;
 using dev::wave_id;
 
-constexpr int kPre = 64;   // left context staged before the tile (line-ordinal scans)
+// Left context staged before the tile for the backward line-ordinal scans: 128 bytes, so
+// the first wave of a tile finds the previous '\n' in LDS for any line up to 128 bytes
+// (Hamlet's longest is 75).  With 64 a wave whose segment starts more than 64 bytes into
+// a line read the text before the window byte by byte over PCIe (zero-copy input): a
+// dependent host round trip in the middle of the map (tile timeline: masks up to 2.6 us).
+constexpr int kPre = 128;
 constexpr int kPost = 64;  // right overhang staged after the tile (>= 40 for packing)
 
 // Delimiter set incl. '\n' and NUL (a NUL also kills the rest of its line, see

@@ -221,6 +221,7 @@ py::dict dist_to_dict(const DistResult& d) {
   py::dict x;
   x["map_ms"] = d.map_ms;
   x["shuffle_ms"] = d.shuffle_ms;
+  x["device_exchange"] = d.device_exchange;
   x["reduce_ms"] = d.reduce_ms;
   x["gather_ms"] = d.gather_ms;
   x["total_ms"] = d.total_ms;

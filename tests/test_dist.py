@@ -245,3 +245,76 @@ def test_gpu_rccl_failure_after_allgather_entered(hamlet, monkeypatch):
     for _ in range(3):
         res, _ = dr.run(hamlet, 0)
         assert res.entries() == ent and res.num_tokens == ntok
+
+
+# ---- device-resident shuffle (exch.hpp): one host synchronisation per job ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_gpu_device_exchange_loopback(hamlet, world):
+    """Shuffle jobs back to back: the first runs host-staged and sizes the slots, the next
+    run as the device exchange (plan/pack/all-to-all/merge/report/gather/concat) and match
+    the oracle byte for byte, including the global val."""
+    job = lc.make_config("gpu", combine=True, check=True)
+    cfgs = [lc.make_dist_config(world, job, strategy="shuffle") for _ in range(4)]
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback" if world > 1 else "auto")
+    for j, (res, info) in enumerate(out):
+        assert info["strategy"] == "shuffle"
+        assert info["device_exchange"] == (j > 0), (j, info)
+        assert res.entries() == ent and res.num_tokens == ntok
+
+
+@pytest.mark.gpu
+def test_gpu_device_exchange_many_keys():
+    text = _distinct_text(30000) + b"w000001 w000007 w029999\n" * 3
+    ent = oracle.wordcount(text)[0]
+    job = lc.make_config("gpu", combine=True, check=True)
+    cfgs = [lc.make_dist_config(4, job, strategy="shuffle") for _ in range(3)]
+    out = lc._C.run_multi_schedule(text, cfgs, "loopback")
+    assert [i["device_exchange"] for _, i in out] == [False, True, True]
+    for res, _ in out:
+        assert res.entries() == ent
+
+
+@pytest.mark.gpu
+def test_gpu_device_exchange_outgrown_slots(hamlet, monkeypatch):
+    """Slots capped below the data (test hook): every rank sees the overflow in the
+    all-gathered reports, the job takes the host-staged path together, the slots grow and
+    the next job is a device exchange again."""
+    monkeypatch.setenv("LOCUST_EXCH_SLOT", "16")
+    job = lc.make_config("gpu", combine=True, check=True)
+    cfgs = [lc.make_dist_config(3, job, strategy="shuffle") for _ in range(3)]
+    ent = oracle.wordcount(hamlet)[0]
+    out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback")
+    assert [i["device_exchange"] for _, i in out] == [False, False, True]
+    for res, _ in out:
+        assert res.entries() == ent
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", ["1:exchange", "0:exchange"])
+def test_gpu_device_exchange_fault(hamlet, monkeypatch, fault):
+    """A rank failing inside the device exchange: its header carries the failure through
+    the collectives, every rank raises (no hang)."""
+    monkeypatch.setenv("LOCUST_FAULT", fault)
+    job = lc.make_config("gpu", combine=True)
+    cfgs = [lc.make_dist_config(3, job, strategy="shuffle") for _ in range(2)]
+    with pytest.raises(lc.LocustError, match="stage 'exchange' on rank " + fault[0]):
+        lc._C.run_multi_schedule(hamlet, cfgs, "loopback")
+
+
+@pytest.mark.gpu
+def test_gpu_device_exchange_one_rccl_rank(hamlet):
+    """One RCCL rank: ncclAllGather / ncclAllToAll through the real communicator."""
+    nlines = hamlet.count(b"\n") + (0 if hamlet.endswith(b"\n") else 1)
+    dcfg = lc.make_dist_config(1, lc.make_config("gpu", combine=True, check=True),
+                               strategy="shuffle")
+    dr = lc._C.DistRank(dcfg, 0, "rccl", "127.0.0.1", free_port(), len(hamlet), nlines, 60.0)
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    used = []
+    for _ in range(4):
+        res, info = dr.run(hamlet, 0)
+        used.append(info["device_exchange"])
+        assert res.entries() == ent and res.num_tokens == ntok
+    assert used == [False, True, True, True]
