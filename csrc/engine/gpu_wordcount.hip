@@ -30,8 +30,13 @@ std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCoun
   m.check_input(in);
   m.enqueue_upload(in);
   m.enqueue_map(in);
-  m.enqueue_process((u32)in.num_lines, m.cfg.map_path == MapPath::kCompat, false);
+  m.enqueue_process((u32)in.num_lines, m.cfg.map_path == MapPath::kCompat, false, kUnknownCount,
+                    /*allow_psort=*/true);
   m.read_counters();
+  if (m.h_ctr->flags & kCtrSortOverflow) {  // a partition outgrew the LDS sort
+    m.redo_process_general((u32)in.num_lines);
+    m.read_counters();
+  }
   std::vector<PackedKey> out;
   m.download_keys(m.sorted, m.h_ctr->num_records, &out);
   if (stats) {

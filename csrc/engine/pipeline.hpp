@@ -540,9 +540,17 @@ struct DevicePipeline {
   };
   std::vector<DictGraph> dict_graphs;  // one per (input shape, output buffer)
   bool graph_ordered = false;          // the last launched graph uses the ordered kernel
-  bool use_graph() const {
+  // Dictionary jobs, and radix jobs that stay on the device end to end (partitioned sort
+  // from the fast map's table, records straight into the mapped output: no host sync).
+  bool use_graph() const {  // dictionary jobs (the shard engine's entry points)
     if (cfg.graph >= 0) return cfg.graph > 0 && cfg.sort_path == SortPath::kDict;
     return cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast;
+  }
+  bool use_job_graph(const TextInput& in) const {
+    const bool radix_ok = cfg.sort_path == SortPath::kRadix && cfg.map_path == MapPath::kFast &&
+                          table_tiles(in.bytes) > 0 && radix_mapped() && psort_enabled();
+    if (cfg.graph >= 0) return cfg.graph > 0 && (cfg.sort_path == SortPath::kDict || radix_ok);
+    return (cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast) || radix_ok;
   }
   // Capture [upload DMA + reset, map, dictionary build, rank, emit] once per input shape
   // and source; later runs replay it with one hipGraphLaunch.
@@ -561,8 +569,13 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
       enqueue_upload_device(in);
       enqueue_map(in);
-      const bool ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr,
-                                            /*self_clean=*/true);
+      bool ordered;  // dictionary: the ordered kernel; radix: the partitioned sort
+      if (cfg.sort_path == SortPath::kDict) {
+        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr, /*self_clean=*/true);
+      } else {
+        enqueue_radix_job((u32)in.num_lines, compat, nullptr, nullptr);
+        ordered = psort_used;
+      }
       LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
       hipGraphExec_t exec = nullptr;
       LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
@@ -571,6 +584,7 @@ struct DevicePipeline {
       hit = &dict_graphs.back();
     }
     graph_ordered = hit->ordered;
+    if (cfg.sort_path == SortPath::kRadix) psort_used = hit->ordered;
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
     part_tiles = cfg.map_path == MapPath::kFast ? table_tiles(in.bytes) : 0u;
     LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
@@ -599,7 +613,16 @@ struct DevicePipeline {
   // host_n: record count when the host already knows it.  With sync_plan the count is
   // read back (one 4-byte D2H) so the sort can pick its regime and exact grids; without
   // it everything stays on the device (graph-capturable).
-  void enqueue_process(u32 num_lines, bool compat, bool with_counts, u64 host_n = kUnknownCount) {
+  // allow_psort: the caller checks kCtrSortOverflow afterwards (psort_overflow_redo).
+  void enqueue_process(u32 num_lines, bool compat, bool with_counts, u64 host_n = kUnknownCount,
+                       bool allow_psort = false) {
+    if (allow_psort && psort_ok(compat, with_counts)) {
+      // one kernel, one workgroup per key range of the map's partition table (psort.hip)
+      launch_psort(tokens, d_part_off, part_tiles, cap, sorted, d_ctr, d_pw, stream, ord_trace());
+      psort_used = true;
+      return;
+    }
+    psort_used = false;
     if (compat)
       launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
                            lb_compact, stream);
@@ -613,6 +636,58 @@ struct DevicePipeline {
     }
     radix_sort(tokens, &d_ctr->num_records, host_n, rx, with_counts ? d_counts : nullptr, sorted,
                with_counts ? d_sorted_counts : nullptr, d_perm, h_plan, stream);
+  }
+
+  // The unweighted tokens of the small-input fast map (per-tile partition table present)
+  // take the partitioned LDS sort; everything else the device-wide LSD sort.
+  static bool psort_enabled() {  // LOCUST_PSORT=0: A/B against the device-wide sort
+    const char* v = std::getenv("LOCUST_PSORT");
+    return !(v && v[0] == '0');
+  }
+  bool psort_ok(bool compat, bool with_counts) const {
+    return psort_enabled() && !compat && !with_counts && parts_ready && part_tiles > 0;
+  }
+  bool psort_used = false;  // the last enqueue_process took the partitioned sort
+
+  // Process + Reduce of the reference algorithm (sort every token, boundary mark + head
+  // compaction + adjacent difference), records packed into the host-mapped output with a
+  // counter snapshot when every possible key fits it (then the host needs no D2H), else
+  // into d_out.  Events (optional; not while capturing) mark the stage ends.
+  bool radix_mapped() const { return h_out_cap >= cap; }
+  void enqueue_radix_job(u32 num_lines, bool compat, hipEvent_t after_process,
+                         hipEvent_t after_reduce) {
+    enqueue_process(num_lines, compat, false, kUnknownCount, /*allow_psort=*/true);
+    if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+    const bool mapped = radix_mapped();
+    if (cfg.reduce_path == ReducePath::kLds) {
+      // LDS path: mark + compact + adjacent difference + records in one kernel
+      launch_reduce_fused(sorted, cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? h_out_cap : cap,
+                          mapped ? d_ctr_mapped : nullptr, lb_heads, stream);
+    } else {
+      // global path: the reference's kernel sequence (kernFindUniqBool, partition,
+      // kernGetCount) as separate launches
+      enqueue_reduce_core(false);
+      if (mapped)
+        launch_pack_output(heads, d_head_val, d_head_count, cap, d_ctr, d_out_mapped, stream,
+                           d_ctr_mapped);
+      else
+        enqueue_pack_output();
+    }
+    if (after_reduce) LOCUST_HIP_CHECK(hipEventRecord(after_reduce, stream));
+  }
+  // After a psort partition overflowed (kCtrSortOverflow): sort the same tokens with the
+  // device-wide LSD sort and reduce again (the map output is still in `tokens`).
+  void redo_radix_general(u32 num_lines) {
+    redo_process_general(num_lines);
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.tile_counter, 0, 4, stream));
+    enqueue_reduce_core(false);
+    enqueue_pack_output();
+  }
+  // The Process stage alone, again, on the device-wide sort (flags cleared).
+  void redo_process_general(u32 num_lines) {
+    LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->flags, 0, sizeof(u32), stream));
+    enqueue_process(num_lines, false, false, h_ctr->num_records);
   }
 
   // Head mark + compaction + adjacent difference over `sorted` (weighted when counts).
@@ -804,6 +879,35 @@ struct DevicePipeline {
                    (x[5] - t0) * 0.01);
     }
   }
+  // LOCUST_ORD_TRACE=1 on the radix path: the partitioned sort's per-partition phases.
+  void print_psort_trace() {
+    if (!d_ord_trace) return;
+    std::vector<u64> t(kDictParts * 16);
+    LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    u64 first_in = ~0ull, last_out = 0;
+    int last_p = -1;
+    for (int p = 0; p < kDictParts; ++p) {
+      const u64* x = &t[p * 16];
+      if (!x[10]) continue;
+      first_in = std::min(first_in, x[10]);
+      if (x[11] > last_out) {
+        last_out = x[11];
+        last_p = p;
+      }
+    }
+    if (last_p >= 0)
+      std::fprintf(stderr, "psort span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
+                   (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 16 + 5]);
+    for (int p = 0; p < kDictParts; ++p) {
+      const u64* x = &t[p * 16];
+      if (!x[0] || !x[4]) continue;
+      auto d = [&](int a, int b) { return (unsigned long long)(x[a] && x[b] ? x[b] - x[a] : 0); };
+      std::fprintf(stderr, "psort p=%3d m=%5llu passes=%2llu list=%6llu keys=%6llu sort=%6llu "
+                   "write=%6llu | in=%6.2f out=%6.2f us\n", p, (unsigned long long)x[5],
+                   (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4),
+                   (x[10] - first_in) * 0.01, (x[11] - first_in) * 0.01);
+    }
+  }
   void print_ord_trace() {
     if (!d_ord_trace) return;
     std::vector<u64> t(kDictParts * 16);
@@ -971,9 +1075,16 @@ struct DevicePipeline {
     if (dict_path) {
       enqueue_process_dict((u32)in.num_lines, compat);
     } else {
-      enqueue_process((u32)in.num_lines, compat, false);
+      enqueue_process((u32)in.num_lines, compat, false, kUnknownCount, /*allow_psort=*/true);
     }
     sync();  // process timer ends once the sort is done (thrust::sort returns)
+    if (!dict_path && psort_used) {
+      read_counters();
+      if (h_ctr->flags & kCtrSortOverflow) {  // a partition outgrew the LDS sort
+        redo_process_general((u32)in.num_lines);
+        sync();
+      }
+    }
     const u64 t2 = now_ns();
     if (dict_path) {
       enqueue_emit_dict(/*mapped=*/true);  // the last reduce kernel: launch only (B4)
@@ -1019,7 +1130,7 @@ struct DevicePipeline {
     const u64 t0 = now_ns();
     const bool compat = cfg.map_path == MapPath::kCompat;
     const bool dict_path = cfg.sort_path == SortPath::kDict;
-    const bool graphed = dict_path && use_graph();
+    const bool graphed = use_job_graph(in);
     skip_sync_reset = clean_start && dict_path && !compat;
     LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
     if (graphed) {
@@ -1063,12 +1174,28 @@ struct DevicePipeline {
         if (ordered_done) maybe_retune(r.entries.data(), r.entries.size());
       }
     } else {
-      enqueue_process((u32)in.num_lines, compat, false);
-      LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
-      enqueue_reduce_core(false);
-      enqueue_pack_output();
-      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
-      download_output(r, ev[5]);
+      if (!graphed) enqueue_radix_job((u32)in.num_lines, compat, ev[3], ev[4]);
+      bool overflow;
+      if (radix_mapped()) {  // records and counters already in host memory
+        if (!graphed) LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+        sync();  // the one host synchronisation of a radix run
+        *h_ctr = *h_ctr_mapped;
+        overflow = (h_ctr->flags & kCtrSortOverflow) != 0;
+        if (psort_used) print_psort_trace();
+        if (!overflow) {
+          fill_counters(r);
+          copy_out(r.entries, h_ctr->num_unique);
+          if (psort_used) maybe_retune(r.entries.data(), r.entries.size());
+        }
+      } else {
+        download_output(r, ev[5]);
+        overflow = (h_ctr->flags & kCtrSortOverflow) != 0;
+      }
+      if (overflow) {  // a partition outgrew the LDS sort: the device-wide sort instead
+        redo_radix_general((u32)in.num_lines);
+        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+        download_output(r, ev[5]);
+      }
     }
     r.times.wall_ms = (now_ns() - t0) * 1e-6;
     if (!graphed) {

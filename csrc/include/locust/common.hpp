@@ -23,6 +23,7 @@
 namespace locust {
 
 using u8 = uint8_t;
+using u16 = uint16_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
 using i64 = int64_t;

@@ -43,6 +43,7 @@ struct MapCounters {
   u32 pad;
 };
 constexpr u32 kCtrDictOverflow = 1u;  // dictionary table full: rerun on the radix path
+constexpr u32 kCtrSortOverflow = 2u;  // a psort partition held more than kPsortMax tokens
 constexpr u32 kCtrNotEmitted = 0x80000000u;  // rank_emit skipped (too many distinct keys)
 
 // Look-back scratch: a zeroed region of 64-bit status words plus a tile counter.
@@ -143,6 +144,19 @@ void radix_sort(ConstKeysSoA keys, const u32* d_n, u64 host_n, RadixWorkspace& w
                 const u64* counts_in, KeysSoA sorted, u64* counts_out, u32* perm_out,
                 SortPlan* h_plan, hipStream_t s, u32 skip_upto = 0);
 
+// ---------------- psort.hip ----------------
+// Partitioned LDS radix sort of the tokens of a small-input fast map (part_off = its
+// per-tile partition table over `ntiles` tiles, launch_map_fast): workgroup p sorts the
+// tokens of PartMap partition p in LDS and writes them at their global sorted position.
+// The map's counters must still be in `ctr` (num_records); a partition with more than
+// kPsortMax tokens sets kCtrSortOverflow (then `sorted` is incomplete).  part_w
+// (optional, host-mapped): per-partition work (tokens + kPartDistinctWeight x distinct
+// first words), for the partition map's retuning.
+constexpr int kPsortMax = 5120;
+// trace (diagnostics, optional): per partition p, stamps at trace[p*16 + k] (see psort.hip).
+void launch_psort(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap, KeysSoA sorted,
+                  MapCounters* ctr, u32* part_w, hipStream_t s, u64* trace = nullptr);
+
 // ---------------- reduce.hip ----------------
 constexpr int kReduceBlock = 256;
 constexpr int kReduceItems = 8;
@@ -174,8 +188,17 @@ struct OutRecord {
   u64 count;
 };
 static_assert(sizeof(OutRecord) == 48, "OutRecord 48 B");
+// Unweighted reduce steps 1-3 + output records in one kernel (LDS-staged tiles): `out`
+// (room for out_cap records; host-mapped allowed) receives {key, val, count} in key order,
+// ctr->num_unique / total_count are set and ctr_out (optional, host-mapped) gets a
+// snapshot.  `lb` needs div_up(cap, kReduceTile) + 1 zeroed status words and a zeroed
+// tile counter.
+void launch_reduce_fused(ConstKeysSoA sorted, u64 cap, MapCounters* ctr, OutRecord* out,
+                         u64 out_cap, MapCounters* ctr_out, LookbackScratch lb, hipStream_t s);
+// ctr_out (optional, host-mapped): a snapshot of the final counters.
 void launch_pack_output(ConstKeysSoA head_keys, const u64* head_val, const u64* head_count,
-                        u64 cap, const MapCounters* ctr, OutRecord* out, hipStream_t s);
+                        u64 cap, const MapCounters* ctr, OutRecord* out, hipStream_t s,
+                        MapCounters* ctr_out = nullptr);
 
 // ---------------- dict.hip ----------------
 constexpr int kRankSortMax = 32768;  // all-pairs rank sort up to here, radix above

@@ -1,0 +1,271 @@
+// Partitioned LDS radix sort: the Process stage of the reference algorithm (sort every
+// emitted token) for passes whose map wrote a per-tile partition table.
+//
+// Reference: thrust::sort of 40-B KeyIntValuePair structs with a byte-loop comparator
+// (/root/reference/MapReduce/src/main.cu:414-415, KeyValue.h:20-33).  The device-wide LSD
+// sort (radix_sort.hip) needs one dependent kernel per live byte position -- 14 on whole
+// Hamlet, each only 8 tiles wide at 33K tokens, ~9 us apiece.  This kernel uses what the
+// small-input fast map already knows instead: it grouped every 1 KiB tile's tokens by
+// PartMap partition (order-preserving 2-byte-prefix ranges, locust/partmap.hpp) and
+// recorded where each partition's run starts (launch_map_fast part_off).  So the sort
+// splits into 256 independent key ranges, and workgroup p (one per partition):
+//   1. collects partition p's token indices from the table (two words per tile) and its
+//      output offset, sum over tiles of part_off[t][p] - part_off[t][0] (the tokens of
+//      lower partitions in tile t): no look-back, no workgroup waits on another;
+//   2. gathers its keys' first two words into LDS (once: every pass and the output read
+//      them there) and finds the byte positions that vary inside the partition (AND/OR
+//      reduction: the shared prefix and the NUL padding drop out);
+//   3. LSD-sorts the partition in LDS, one stable 8-bit counting pass per live position
+//      (dev::LdsRadix: wave64 match-any ranks, u16 local indices, 3 barriers a pass);
+//   4. writes its slice of the globally sorted token array.
+// One launch, no host synchronisation, graph-capturable.  A partition with more than
+// kPsortMax tokens sets kCtrSortOverflow and the host sorts the pass with radix_sort.
+#include "locust/device/lds_radix.hpp"
+#include "locust/device/wave.hpp"
+#include "locust/hip_check.hpp"
+#include "locust/kernels.hpp"
+
+namespace locust {
+namespace {
+
+using dev::lane_id;
+using dev::wave_id;
+
+constexpr int kPsBlock = 512;  // 8 waves: 256 VGPRs a lane (1,024 threads spilled the pass state)
+constexpr int kPsWaves = kPsBlock / 64;
+constexpr int kPsRounds = kPsortMax / kPsBlock;  // keys held per thread
+using PsRadix = dev::LdsRadix<kPsBlock, kPsortMax, u16>;
+
+__global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
+                                                         const u32* __restrict__ part_off,
+                                                         u32 ntiles, u32 n_cap, KeysSoA sorted,
+                                                         MapCounters* __restrict__ ctr,
+                                                         u32* __restrict__ part_w,
+                                                         u64* __restrict__ trace) {
+  // trace (diagnostics, LOCUST_ORD_TRACE): per partition, s_memtime at [p*16 + k]: 0 start,
+  // 1 list built, 2 keys loaded, 3 sorted, 4 written; [5] tokens, [6] passes; [10]/[11]
+  // entry/exit on the 100 MHz device-wide clock
+#define PS_STAMP(k_) \
+  if (trace && threadIdx.x == 0) trace[(u64)blockIdx.x * 16 + (k_)] = __builtin_amdgcn_s_memtime()
+  if (trace && threadIdx.x == 0) {
+    for (int k = 1; k < 16; ++k) trace[(u64)blockIdx.x * 16 + k] = 0;
+    trace[(u64)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+  }
+  PS_STAMP(0);
+  __shared__ u32 s_list[kPsortMax];   // global token index of local item i
+  __shared__ u64 s_w0[kPsortMax];     // key words 0 and 1 of local item i (LDS-resident:
+  __shared__ u64 s_w1[kPsortMax];     // gathered once, read by every pass and the output)
+  __shared__ u16 s_perm[2][kPsortMax];
+  __shared__ u16 s_cnt[kPsWaves][256];
+  __shared__ u16 s_wex[kPsWaves][256];
+  __shared__ u32 s_start[256];
+  __shared__ u32 s_wsum[4];
+  __shared__ u64 s_and[kPsWaves][kKeyWords], s_or[kPsWaves][kKeyWords];
+  __shared__ u32 s_count, s_below, s_heads;
+  const u32 p = blockIdx.x;
+  const int lane = lane_id(), w = wave_id(), t = (int)threadIdx.x;
+  const PsRadix rx{s_w0, s_perm, s_cnt, s_wex, s_start, s_wsum};
+  rx.init();
+  if (t == 0) {
+    s_count = 0;
+    s_below = 0;
+    s_heads = 0;
+  }
+  __syncthreads();
+
+  // ---- 1. this partition's tokens and its output offset ----
+  u32 below = 0;
+  for (u32 t0 = 0; t0 < ntiles; t0 += kPsBlock) {
+    const u32 tile = t0 + (u32)t;
+    u32 a = 0, len = 0;
+    if (tile < ntiles) {
+      const u32* row = part_off + (u64)tile * kPartTable;
+      const u32 z = row[0];
+      a = row[p];
+      len = row[p + 1] - a;
+      below += a - z;
+    }
+    // one LDS atomic per wave: the wave's runs are appended back to back (any order will
+    // do -- equal keys are indistinguishable in the output)
+    const u32 incl = dev::wave_inclusive_scan(len);
+    u32 wbase = 0;
+    if (lane == 63 && incl) wbase = atomicAdd(&s_count, incl);
+    wbase = (u32)__builtin_amdgcn_readlane((int)wbase, 63);
+    u32 at = wbase + incl - len;
+    for (u32 j = 0; j < len; ++j, ++at)
+      if (at < (u32)kPsortMax) s_list[at] = a + j;
+  }
+  below = dev::wave_reduce_sum(below);
+  if (lane == 0 && below) atomicAdd(&s_below, below);
+  __syncthreads();
+  const u32 m = s_count, base = s_below;
+  PS_STAMP(1);
+  if (trace && t == 0) trace[(u64)p * 16 + 5] = m;
+  if (m > (u32)kPsortMax) {  // uniform: the host sorts this pass with radix_sort
+    if (t == 0) atomicOr(&ctr->flags, kCtrSortOverflow);
+    return;
+  }
+  if (m == 0) {
+    if (part_w && t == 0) part_w[p] = 0;
+    return;
+  }
+
+  // ---- 2. keys: words 0-1 into LDS (all first-word loads in flight at once, second words
+  // only for keys that run past 8 bytes); AND/OR over the partition: which byte positions
+  // vary (words 2-3 only for keys past 16 bytes, re-gathered if a pass needs them) ----
+  u64 a[kKeyWords], o[kKeyWords];
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j) {
+    a[j] = ~0ull;
+    o[j] = 0;
+  }
+  {
+    u32 gi[kPsRounds];
+    u64 x0[kPsRounds], x1[kPsRounds];
+#pragma unroll
+    for (int r = 0; r < kPsRounds; ++r) {
+      const u32 i = (u32)t + (u32)r * kPsBlock;
+      gi[r] = i < m ? s_list[i] : 0xFFFFFFFFu;
+    }
+    // words 0 and 1 in one round trip (word 1 is read even for short keys, where it is 0:
+    // a second dependent round of gathers costs more than the extra bytes)
+#pragma unroll
+    for (int r = 0; r < kPsRounds; ++r) {
+      x0[r] = gi[r] < n_cap ? tokens.w[0][gi[r]] : 0;
+      x1[r] = gi[r] < n_cap ? tokens.w[1][gi[r]] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kPsRounds; ++r) {
+      if (gi[r] >= n_cap) continue;
+      const u32 i = (u32)t + (u32)r * kPsBlock;
+      s_w0[i] = x0[r];
+      s_w1[i] = x1[r];
+      u64 x2 = 0, x3 = 0;
+      if (x1[r] & 0xffull) {
+        x2 = tokens.w[2][gi[r]];
+        if (x2 & 0xffull) x3 = tokens.w[3][gi[r]];
+      }
+      a[0] &= x0[r];
+      o[0] |= x0[r];
+      a[1] &= x1[r];
+      o[1] |= x1[r];
+      a[2] &= x2;
+      o[2] |= x2;
+      a[3] &= x3;
+      o[3] |= x3;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      a[j] &= __shfl_xor(a[j], off, 64);
+      o[j] |= __shfl_xor(o[j], off, 64);
+    }
+    if (lane == 0) {
+      s_and[w][j] = a[j];
+      s_or[w][j] = o[j];
+    }
+  }
+  for (u32 i = (u32)t; i < m; i += kPsBlock) s_perm[0][i] = (u16)i;
+  __syncthreads();
+  u64 diff[kKeyWords];
+  bool long_keys = false;  // some key of the partition runs past 16 bytes
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j) {
+    u64 aa = ~0ull, oo = 0;
+#pragma unroll
+    for (int ww = 0; ww < kPsWaves; ++ww) {
+      aa &= s_and[ww][j];
+      oo |= s_or[ww][j];
+    }
+    diff[j] = aa ^ oo;
+    if (j >= 2) long_keys |= oo != 0;
+  }
+
+  PS_STAMP(2);
+  // ---- 3. LSD passes over the live byte positions, least significant first ----
+  int cur = 0;
+  for (int wd = kKeyWords - 1; wd >= 0; --wd) {
+    if (!diff[wd]) continue;
+    const u64* warr = wd == 0 ? s_w0 : s_w1;
+    if (wd >= 2) {
+      // rare (keys past 16 bytes): word wd into the word-1 array for its passes, word 1
+      // itself restored afterwards
+      for (u32 i = (u32)t; i < m; i += kPsBlock) {
+        const u32 g = s_list[i];
+        u64 x = (g < n_cap && (s_w1[i] & 0xffull)) ? tokens.w[2][g] : 0;
+        if (wd == 3) x = (x & 0xffull) ? tokens.w[3][g] : 0;
+        s_w1[i] = x;
+      }
+      __syncthreads();
+    }
+    for (int b = 7; b >= 0; --b) {
+      const u32 shift = 56u - 8u * (u32)b;
+      if (!((diff[wd] >> shift) & 0xffull)) continue;
+      rx.pass(warr, m, shift, cur);
+      cur ^= 1;
+    }
+    if (wd >= 2) {
+      for (u32 i = (u32)t; i < m; i += kPsBlock) {
+        const u32 g = s_list[i];
+        s_w1[i] = (g < n_cap && (s_w0[i] & 0xffull)) ? tokens.w[1][g] : 0;
+      }
+      __syncthreads();
+    }
+  }
+
+  PS_STAMP(3);
+  if (trace && t == 0) {
+    u32 np = 0;
+    for (int j = 0; j < kKeyWords; ++j)
+      for (int b = 0; b < 8; ++b) np += ((diff[j] >> (8 * b)) & 0xffull) ? 1u : 0u;
+    trace[(u64)p * 16 + 6] = np;
+  }
+  // ---- 4. the partition's slice of the sorted token array, from LDS (words 2-3 gathered
+  // only when the partition has keys past 16 bytes); distinct first words counted on the
+  // way for the partition map's retuning ----
+  u32 heads = 0;
+  for (u32 i = (u32)t; i < m; i += kPsBlock) {
+    const u32 li = s_perm[cur][i];
+    const u64 out = (u64)base + i;
+    const u64 k0 = s_w0[li], k1 = s_w1[li];
+    if (out < n_cap) {
+      u64 k2 = 0, k3 = 0;
+      if (long_keys && (k1 & 0xffull)) {
+        const u32 g = s_list[li];
+        k2 = tokens.w[2][g];
+        if (k2 & 0xffull) k3 = tokens.w[3][g];
+      }
+      sorted.w[0][out] = k0;
+      sorted.w[1][out] = k1;
+      sorted.w[2][out] = k2;
+      sorted.w[3][out] = k3;
+    }
+    heads += (i == 0 || k0 != s_w0[s_perm[cur][i - 1]]) ? 1u : 0u;
+  }
+  PS_STAMP(4);
+  if (trace && t == 0) trace[(u64)p * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  if (part_w) {
+    heads = dev::wave_reduce_sum(heads);
+    if (lane == 0 && heads) atomicAdd(&s_heads, heads);
+    __syncthreads();
+    if (t == 0) {
+      const u64 wk = (u64)m + (u64)kPartDistinctWeight * s_heads;
+      part_w[p] = (u32)(wk < 0xffffffffull ? wk : 0xffffffffull);
+    }
+  }
+}
+#undef PS_STAMP
+
+}  // namespace
+
+void launch_psort(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap, KeysSoA sorted,
+                  MapCounters* ctr, u32* part_w, hipStream_t s, u64* trace) {
+  LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
+  psort_kernel<<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(tokens, part_off, ntiles, (u32)cap,
+                                                           sorted, ctr, part_w, trace);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+}  // namespace locust

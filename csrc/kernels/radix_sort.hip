@@ -20,6 +20,7 @@
 //    pairs move per pass; the next word is gathered once through the permutation.
 #include <algorithm>
 
+#include "locust/device/lds_radix.hpp"
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
@@ -76,22 +77,25 @@ __device__ __forceinline__ u32 live_mask(const SortPlan* plan) {
 // ---------------------------------------------------------------------------------
 constexpr int kSmallBlock = 1024;
 constexpr int kSmallWaves = kSmallBlock / 64;
-constexpr int kSmallRounds = kSmallSortMax / kSmallBlock;  // items per lane
+using SmallRadix = dev::LdsRadix<kSmallBlock, kSmallSortMax, u16>;
 
 __global__ __launch_bounds__(kSmallBlock) void radix_small_kernel(
     ConstKeysSoA keys, const u32* __restrict__ d_n, const u64* __restrict__ counts_in,
     KeysSoA sorted, u64* __restrict__ counts_out, u32* __restrict__ perm_out,
     SortPlan* __restrict__ plan) {
   __shared__ u64 s_word[kSmallSortMax];
-  __shared__ u32 s_perm[2][kSmallSortMax];
-  __shared__ u32 s_cnt[kSmallWaves][256];
-  __shared__ u32 s_base[256];
+  __shared__ u16 s_perm[2][kSmallSortMax];
+  __shared__ u16 s_cnt[kSmallWaves][256];
+  __shared__ u16 s_wex[kSmallWaves][256];
+  __shared__ u32 s_start[256];
   __shared__ u64 s_and[kSmallWaves][kKeyWords], s_or[kSmallWaves][kKeyWords];
   __shared__ u32 s_wsum[4];
   const u32 n = *d_n;
   if (threadIdx.x == 0 && plan) plan->n = n;
   if (n > (u32)kSmallSortMax) return;  // the multi-tile path handles it
   const int lane = lane_id(), w = wave_id(), t = threadIdx.x;
+  const SmallRadix rx{s_word, s_perm, s_cnt, s_wex, s_start, s_wsum};
+  rx.init();
 
   // ---- constant digit positions: AND/OR of every key word ----
   u64 a[kKeyWords], o[kKeyWords];
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(kSmallBlock) void radix_small_kernel(
       s_or[w][j] = o[j];
     }
   }
-  for (u32 i = t; i < n; i += kSmallBlock) s_perm[0][i] = i;
+  for (u32 i = t; i < n; i += kSmallBlock) s_perm[0][i] = (u16)i;
   __syncthreads();
   u64 diff[kKeyWords];
 #pragma unroll
@@ -133,78 +137,16 @@ __global__ __launch_bounds__(kSmallBlock) void radix_small_kernel(
     diff[j] = aa ^ oo;  // bits that differ between keys
   }
 
-  // Each wave owns a contiguous chunk of positions (stable order = wave, round, lane).
-  const u32 chunk = (u32)div_up(div_up(n, kSmallWaves), 64) * 64;
-  const u32 c0 = (u32)w * chunk;
   int cur = 0;
   for (int wd = kKeyWords - 1; wd >= 0; --wd) {
     if (!diff[wd]) continue;
-    __syncthreads();
     for (u32 i = t; i < n; i += kSmallBlock) s_word[i] = keys.w[wd][i];
+    __syncthreads();
     for (int b = 7; b >= 0; --b) {
       const u32 shift = 56u - 8u * (u32)b;
       if (!((diff[wd] >> shift) & 0xffull)) continue;  // constant position
-      for (int i = t; i < kSmallWaves * 256; i += kSmallBlock) (&s_cnt[0][0])[i] = 0;
-      __syncthreads();
-      // phase A: wave-local stable ranks
-      u32 idx[kSmallRounds], dig[kSmallRounds], rank[kSmallRounds];
-#pragma unroll
-      for (int r = 0; r < kSmallRounds; ++r) {
-        const u32 p = c0 + (u32)r * 64 + lane;
-        const bool valid = (u32)r * 64 < chunk && p < n;
-        idx[r] = valid ? s_perm[cur][p] : 0;
-        dig[r] = valid ? (u32)(s_word[idx[r]] >> shift) & 0xffu : 256u;
-      }
-#pragma unroll
-      for (int r = 0; r < kSmallRounds; ++r) {
-        const bool valid = dig[r] < 256u;
-        const u32 d = dig[r] & 0xffu;
-        u64 m = ballot(valid);
-        if (!m) continue;  // wave-uniform
-#pragma unroll
-        for (int bb = 0; bb < 8; ++bb) {
-          const bool bit = (d >> bb) & 1u;
-          const u64 x = ballot(bit);
-          m &= bit ? x : ~x;
-        }
-        u32 prev = 0;
-        if (valid) prev = s_cnt[w][d];
-        __builtin_amdgcn_wave_barrier();
-        const u32 below = lanes_below(m);
-        if (valid && below == 0) s_cnt[w][d] = prev + (u32)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
-        rank[r] = prev + below;
-      }
-      __syncthreads();
-      // phase B: per digit, exclusive over waves; then exclusive over digits
-      if (t < 256) {
-        u32 run = 0;
-        for (int ww = 0; ww < kSmallWaves; ++ww) {
-          const u32 c = s_cnt[ww][t];
-          s_cnt[ww][t] = run;
-          run += c;
-        }
-        const u32 inc = dev::wave_inclusive_scan(run);
-        if (lane == 63) s_wsum[w] = inc;
-        s_base[t] = inc - run;  // wave-local exclusive; wave offsets added below
-      }
-      __syncthreads();
-      if (t < 256) {
-        u32 add = 0;
-        for (int ww = 0; ww < w; ++ww) add += s_wsum[ww];
-        s_base[t] += add;
-      }
-      __syncthreads();
-      // phase C: stable scatter of indices
-#pragma unroll
-      for (int r = 0; r < kSmallRounds; ++r) {
-        if (dig[r] < 256u) {
-          const u32 d = dig[r];
-          s_perm[cur ^ 1][s_base[d] + s_cnt[w][d] + rank[r]] = idx[r];
-        }
-      }
+      rx.pass(n, shift, cur);
       cur ^= 1;
-      __syncthreads();
     }
   }
   __syncthreads();

@@ -144,6 +144,148 @@ __global__ __launch_bounds__(kReduceBlock) void mark_compact_heads_kernel(
   }
 }
 
+// ---- fused LDS reduce: steps 1-3 and the output records in one kernel ----
+// The tile (plus a one-key halo on each side) is staged in LDS as for the LDS head mark;
+// heads are marked and compacted (block scan + look-back for the global head index); each
+// head's count is the distance to the next head -- inside the tile from the LDS list of
+// head positions, for the tile's last head by looking past the tile end (the halo key,
+// then 64 keys per step by one wave for a run that continues: rare); and the records go
+// straight to `out` (host-mapped: zero-copy) as consecutive 8-B words.  Replaces the
+// separate mark/compact, adjacent-difference and pack launches -- and their two extra
+// round trips through memory -- for unweighted reduces.
+__global__ __launch_bounds__(kReduceBlock) void reduce_fused_kernel(
+    ConstKeysSoA sorted, MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
+    MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr,
+    u32 out_cap) {
+  __shared__ u64 s_keys[kKeyWords][kReduceTile + 2];  // [0] left halo, [kReduceTile+1] right
+  __shared__ u16 s_hpos[kReduceTile + 1];             // local positions of the tile's heads
+  __shared__ u32 s_scan[kReduceBlock / 64 + 1];
+  __shared__ u32 s_tile;
+  __shared__ u64 s_prefix;
+  __shared__ u32 s_end;  // end of the tile's last run (absolute)
+  const u32 n = ctr->num_records;
+  const u32 num_tiles = (u32)div_up(n, kReduceTile);
+  if (n == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      ctr->num_unique = 0;
+      ctr->total_count = 0;
+      if (ctr_out) *ctr_out = *ctr;
+    }
+    return;
+  }
+  // Tickets almost always come out in dispatch order: the keys of tile blockIdx.x are
+  // loaded while the ticket atomic is in flight, and reloaded only on a mismatch.
+  constexpr int kTrips = (kReduceTile + 2 + kReduceBlock - 1) / kReduceBlock;
+  u64 v[kTrips][kKeyWords];
+  auto load_tile = [&](u32 tl) {
+#pragma unroll
+    for (int r = 0; r < kTrips; ++r) {
+      const int i = threadIdx.x + r * kReduceBlock;
+      const i64 g = (i64)tl * kReduceTile + i - 1;
+      const bool ok = i < kReduceTile + 2 && g >= 0 && g < (i64)n;
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) v[r][j] = ok ? sorted.w[j][g] : ~0ull;
+    }
+  };
+  if (blockIdx.x < num_tiles) load_tile(blockIdx.x);
+  const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
+  if (tile >= num_tiles) return;
+  if (tile != blockIdx.x) load_tile(tile);
+  const u32 base = tile * kReduceTile;
+  const u32 tn = min((u32)kReduceTile, n - base);  // items in this tile
+  {
+#pragma unroll
+    for (int r = 0; r < kTrips; ++r) {
+      const int i = threadIdx.x + r * kReduceBlock;
+      if (i < kReduceTile + 2) {
+#pragma unroll
+        for (int j = 0; j < kKeyWords; ++j) s_keys[j][i] = v[r][j];
+      }
+    }
+  }
+  __syncthreads();
+  u32 flags = 0;
+  const u32 first = threadIdx.x * kReduceItems;  // local, blocked
+#pragma unroll
+  for (int t = 0; t < kReduceItems; ++t) {
+    const u32 li = first + t;
+    if (li >= tn) break;
+    bool head = base + li == 0;
+    if (!head) {
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) head |= s_keys[j][li + 1] != s_keys[j][li];
+    }
+    if (head) flags |= 1u << t;
+  }
+  u32 total;
+  const u32 excl =
+      dev::block_exclusive_scan<u32, kReduceBlock>((u32)__popc(flags), s_scan, &total);
+  {
+    u32 at = excl, f = flags;
+    while (f) {
+      const int t = __ffs(f) - 1;
+      f &= f - 1;
+      s_hpos[at++] = (u16)(first + t);
+    }
+  }
+  if (threadIdx.x == 0) s_end = base + tn;
+  __syncthreads();
+  // End of the last head's run: the tile end unless the key continues past it.
+  if (total && base + tn < n && dev::wave_id() == 0) {
+    const u32 lh = s_hpos[total - 1];
+    bool same = true;
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) same &= s_keys[j][tn + 1] == s_keys[j][lh + 1];
+    if (same) {  // wave-uniform: the run continues into the next tile
+      u32 pos = base + tn;
+      for (;;) {
+        const u32 g = pos + (u32)dev::lane_id();
+        bool diff = g >= n;
+        if (!diff) {
+#pragma unroll
+          for (int j = 0; j < kKeyWords; ++j) diff |= sorted.w[j][g] != s_keys[j][lh + 1];
+        }
+        const u64 b = dev::ballot(diff);
+        if (b) {
+          pos += (u32)(__ffsll((unsigned long long)b) - 1);
+          break;
+        }
+        pos += 64;
+      }
+      if (dev::lane_id() == 0) s_end = min(pos, n);
+    }
+  }
+  const u64 pfx = dev::block_lookback(status, tile, total, &s_prefix);  // syncs
+  if (total) {
+    u64* o = reinterpret_cast<u64*>(out + pfx);
+    const u32 lim = pfx >= out_cap ? 0u : (u32)min<u64>(total, (u64)out_cap - pfx);
+    for (u32 q = threadIdx.x; q < 6u * lim; q += kReduceBlock) {
+      const u32 h = q / 6, f = q - 6 * h;
+      const u32 li = s_hpos[h];
+      u64 v;
+      if (f < (u32)kKeyWords) {
+        v = s_keys[f][li + 1];
+      } else if (f == 4) {
+        v = (u64)base + li;
+      } else {
+        const u32 end = h + 1 < total ? base + s_hpos[h + 1] : s_end;
+        v = (u64)end - (base + li);
+      }
+      o[q] = v;
+    }
+  }
+  if (tile == num_tiles - 1 && threadIdx.x == 0) {
+    ctr->num_unique = (u32)(pfx + total);
+    ctr->total_count = n;
+    if (ctr_out) {
+      MapCounters c = *ctr;
+      c.num_unique = (u32)(pfx + total);
+      c.total_count = n;
+      *ctr_out = c;
+    }
+  }
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kReduceBlock) void adjacent_diff_kernel(
     const u64* __restrict__ head_val, u64* __restrict__ head_count,
@@ -176,19 +318,23 @@ __global__ __launch_bounds__(256) void add_offset_kernel(u64* __restrict__ head_
   for (u32 j = blockIdx.x * 256 + threadIdx.x; j < u; j += gridDim.x * 256) head_val[j] += off;
 }
 
+// Output records, written as consecutive 8-B words by consecutive lanes (word q = record
+// q / 6, field q % 6): full cache lines, which matters when `out` is host-mapped memory
+// (zero-copy results: every partial line would be its own PCIe write).  `ctr_out`
+// (optional, host-mapped) receives the final counters; the host waits for the kernel.
 __global__ __launch_bounds__(256) void pack_output_kernel(ConstKeysSoA head_keys,
                                                           const u64* __restrict__ head_val,
                                                           const u64* __restrict__ head_count,
                                                           const MapCounters* __restrict__ ctr,
-                                                          OutRecord* __restrict__ out) {
+                                                          OutRecord* __restrict__ out,
+                                                          MapCounters* __restrict__ ctr_out) {
   const u32 u = ctr->num_unique;
-  for (u32 j = blockIdx.x * 256 + threadIdx.x; j < u; j += gridDim.x * 256) {
-    OutRecord r;
-#pragma unroll
-    for (int w = 0; w < kKeyWords; ++w) r.w[w] = head_keys.w[w][j];
-    r.val = head_val[j];
-    r.count = head_count[j];
-    out[j] = r;
+  if (ctr_out && blockIdx.x == 0 && threadIdx.x == 0) *ctr_out = *ctr;
+  u64* o = reinterpret_cast<u64*>(out);
+  const u64 words = 6ull * u;
+  for (u64 q = blockIdx.x * 256ull + threadIdx.x; q < words; q += gridDim.x * 256ull) {
+    const u32 j = (u32)(q / 6), f = (u32)(q - 6ull * j);
+    o[q] = f < (u32)kKeyWords ? head_keys.w[f][j] : f == 4 ? head_val[j] : head_count[j];
   }
 }
 
@@ -220,6 +366,15 @@ void launch_mark_compact_heads(ConstKeysSoA sorted, const u64* prefix, u64 cap, 
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+void launch_reduce_fused(ConstKeysSoA sorted, u64 cap, MapCounters* ctr, OutRecord* out,
+                         u64 out_cap, MapCounters* ctr_out, LookbackScratch lb, hipStream_t s) {
+  const u32 tiles = (u32)div_up(cap ? cap : 1, kReduceTile);
+  reduce_fused_kernel<<<dim3(tiles), dim3(kReduceBlock), 0, s>>>(
+      sorted, ctr, out, ctr_out, lb.status, lb.tile_counter,
+      (u32)(out_cap < 0xffffffffull ? out_cap : 0xffffffffull));
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
 void launch_adjacent_diff(const u64* head_val, u64 cap, ReducePath path, u64* head_count,
                           const MapCounters* ctr, hipStream_t s) {
   const u32 grid = grid_for(cap, kReduceBlock);
@@ -237,9 +392,10 @@ void launch_add_offset(u64* head_val, u64 cap, const u64* d_offset, const MapCou
 }
 
 void launch_pack_output(ConstKeysSoA head_keys, const u64* head_val, const u64* head_count,
-                        u64 cap, const MapCounters* ctr, OutRecord* out, hipStream_t s) {
-  pack_output_kernel<<<dim3(grid_for(cap, 256)), dim3(256), 0, s>>>(head_keys, head_val,
-                                                                   head_count, ctr, out);
+                        u64 cap, const MapCounters* ctr, OutRecord* out, hipStream_t s,
+                        MapCounters* ctr_out) {
+  pack_output_kernel<<<dim3(grid_for(6 * cap, 256)), dim3(256), 0, s>>>(
+      head_keys, head_val, head_count, ctr, out, ctr_out);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
