@@ -51,13 +51,10 @@ CHUNK_BYTES = 256 << 20  # one device pass; larger shards stream
 
 
 def chunk_bytes_for(nbytes: int) -> int:
-    """Device pass size: mid-size inputs stream in ~3 chunks so the H2D of one overlaps
-    the map + dictionary insert of the previous (43 MB / 1M lines: 3.01 ms in one pass,
-    2.57 ms in 16 MiB chunks, tools/chunk_ab.py, profiles/r1_s2/chunk_sweep.txt); large
-    inputs are PCIe-bound with 256 MiB chunks."""
-    if nbytes <= (32 << 20):
-        return CHUNK_BYTES
-    return max(16 << 20, min(CHUNK_BYTES, (nbytes // 3) & ~((1 << 20) - 1)))
+    """Device pass size: inputs up to 256 MiB are ONE pass (the engine uploads them in
+    line-aligned 4 MiB pieces, each mapped as it lands, and aggregates on the two-kernel
+    ordered build); larger ones stream in 256 MiB chunks (PCIe-bound)."""
+    return CHUNK_BYTES
 
 
 def load_text(config: str) -> bytes:
@@ -326,8 +323,11 @@ def main() -> int:
         data = (f"synthetic Hamlet-shaped text (native generator, seed 1), "
                 f"{'1M lines' if args.config == 'synth1m' else '10 GB'} in total, "
                 f"1/N per GPU generated into pinned host memory")
-        model = (f"WordCount {args.config}: dictionary path, streamed in "
-                 f"{chunk_bytes_for(nbytes) >> 20} MiB chunks, full H2D->D2H job per step")
+        model = (f"WordCount {args.config}: dictionary path, "
+                 + ("one pass, 4 MiB upload pieces, two-kernel ordered build"
+                    if nbytes <= CHUNK_BYTES else
+                    f"streamed in {chunk_bytes_for(nbytes) >> 20} MiB chunks")
+                 + ", full H2D->D2H job per step")
         scaling = "strong"
         extra["GB_per_s"] = round(total_bytes / (ms * 1e-3) / 1e9, 3)
         extra["baseline_note"] = ("no published number at this size; baseline_ms = this byte "

@@ -83,6 +83,21 @@ struct DevicePipeline {
   u32* d_part_off = nullptr;
   u64 part_off_tiles = 0;  // capacity in tiles
   u32 part_tiles = 0;
+  // Large single passes: the two-kernel ordered build's partial slots (dict.hip).
+  bool large_ordered = false;
+  KeyCount* d_partials = nullptr;
+  u32* d_partial_n = nullptr;
+  // Large single-pass inputs travel in line-aligned pieces on the copy stream, each mapped
+  // as soon as it lands (the H2D overlaps the map); set by prepare_upload.
+  static constexpr u64 kPieceBytes = 4ull << 20;
+  static constexpr u64 kMaxPieces = 256;
+  std::vector<std::pair<u64, u64>> pieces;
+  // run() opts a large dictionary pass into the combining map (records + d_counts);
+  // map_combined: the current `tokens` came from it (consumers must weigh by d_counts).
+  bool combine_map = false;
+  bool map_combined = false;
+  std::vector<hipEvent_t> ev_piece;
+  hipEvent_t ev_fork = nullptr;
   OutRecord* d_out = nullptr;
   KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
   // Records d_records holds (>= cap; at least one minimum-size gather slot).
@@ -205,9 +220,21 @@ struct DevicePipeline {
     for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
     sz.add<u32>(cap);
     sz.add<u8>(align_up(cap, 16) + 16);
-    if (cap <= kPartBuildMaxTokens && cap_bytes < kMapLargeInput)
+    if (cap <= kPartBuildMaxTokens && cap_bytes < kMapLargeInput) {
       part_off_tiles = div_up(cap_bytes, kMapTileBytesMin);
+    } else if (!streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
+      // large single passes (the two-kernel ordered build): 1 KiB tiles below
+      // kMapLargeInput, 4 KiB tiles (whole inputs or upload pieces) above
+      part_off_tiles = std::max<u64>(div_up(std::min<u64>(cap_bytes, kMapLargeInput), kMapTileBytesMin),
+                                     div_up(cap_bytes, kMapTileBytesLarge) + kMaxPieces);
+      large_ordered = cap > kPartBuildMaxTokens;
+    }
     if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartTable);
+    const u64 partial_slots = large_ordered ? (u64)kDictParts * kOrdWorkers : 0;
+    if (partial_slots) {
+      sz.add<KeyCount>(partial_slots * kPartSlotsHost);
+      sz.add<u32>(partial_slots);
+    }
     sz.add<OutRecord>(cap);
     sz.add<KeyCount>(slot_records_cap() + kSlotHeaderRecords);
     sz.add<PackedKey>(kMaxSamples);
@@ -245,6 +272,10 @@ struct DevicePipeline {
     d_perm = arena.take<u32>(cap);
     d_parts = arena.take<u8>(align_up(cap, 16) + 16);
     if (part_off_tiles) d_part_off = arena.take<u32>(part_off_tiles * kPartTable);
+    if (partial_slots) {
+      d_partials = arena.take<KeyCount>(partial_slots * kPartSlotsHost);
+      d_partial_n = arena.take<u32>(partial_slots);
+    }
     d_out = arena.take<OutRecord>(cap);
     // room for a gather slot header in front: d_records - kSlotHeaderRecords is the slot
     d_records = arena.take<KeyCount>(slot_records_cap() + kSlotHeaderRecords) + kSlotHeaderRecords;
@@ -337,6 +368,7 @@ struct DevicePipeline {
     for (auto& g : dict_graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
     if (d_ord_trace) (void)hipFree(d_ord_trace);
+    if (d_partials_trace) (void)hipFree(d_partials_trace);
     if (d_map_trace) (void)hipFree(d_map_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     for (auto& e : ev)
@@ -346,6 +378,8 @@ struct DevicePipeline {
       if (ev_consumed[b]) (void)hipEventDestroy(ev_consumed[b]);
       if (h_stage[b]) (void)hipHostFree(h_stage[b]);
     }
+    for (auto e : ev_piece) (void)hipEventDestroy(e);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (cstream) (void)hipStreamDestroy(cstream);
     if (d_text_alt) (void)hipFree(d_text_alt);
     if (d_dctr) (void)hipFree(d_dctr);
@@ -460,22 +494,59 @@ struct DevicePipeline {
   Upload upload_mode = Upload::kStaged;
   void prepare_upload(const TextInput& in) {
     map_text = d_text;
+    pieces.clear();
     if (use_zero_copy(in)) {
       upload_mode = Upload::kZeroCopy;
       map_text = d_h_text;
     } else if (in.data != h_text && in.bytes && host_pinned(in.data)) {
       upload_mode = Upload::kDirect;
+      plan_pieces(in);
       return;
     } else {
       upload_mode = Upload::kStaged;
     }
     if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
     std::memset(h_text + in.bytes, 0, 16);
+    plan_pieces(in);
+  }
+  // Line-aligned pieces of a large single-pass input (none: one copy, one map launch).
+  void plan_pieces(const TextInput& in) {
+    if (cfg.map_path != MapPath::kFast || !large_ordered || in.bytes < 2 * kPieceBytes) return;
+    u64 pos = 0;
+    while (pos < in.bytes && pieces.size() < kMaxPieces) {
+      u64 end = std::min<u64>(pos + kPieceBytes, in.bytes);
+      if (end < in.bytes) {
+        const void* nl = memrchr(in.data + pos, '\n', (size_t)(end - pos));
+        if (!nl) {  // a line longer than a piece: no pieces at all
+          pieces.clear();
+          return;
+        }
+        end = (u64)(static_cast<const char*>(nl) - in.data) + 1;
+      }
+      pieces.emplace_back(pos, end - pos);
+      pos = end;
+    }
+    if (pos < in.bytes) pieces.clear();
+  }
+  u32 piece_tiles() const {
+    u64 t = 0;
+    for (const auto& pc : pieces) t += div_up(pc.second, kMapTileBytesLarge);
+    return t <= part_off_tiles ? (u32)t : 0u;
+  }
+  void ensure_piece_events(size_t n) {
+    if (!cstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    if (!ev_fork) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    while (ev_piece.size() < n) {
+      hipEvent_t e;
+      LOCUST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev_piece.push_back(e);
+    }
   }
   // Device half (capturable): the DMA if any, then the per-run reset of counters and
   // look-back scratch.
   void enqueue_upload_device(const TextInput& in) {
-    if (upload_mode == Upload::kDirect) {
+    if (!pieces.empty()) {  // the pieces travel with the map (enqueue_map)
+    } else if (upload_mode == Upload::kDirect) {
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
       LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
     } else if (upload_mode == Upload::kStaged) {
@@ -528,25 +599,30 @@ struct DevicePipeline {
     Upload mode = Upload::kStaged;
     const OutRecord* out = nullptr;  // the host-mapped output buffer the graph writes
     bool no_reset = false;           // captured without the d_sync reset (clean start)
+    u64 pieces_sig = 0;              // the upload pieces (line-aligned: content dependent)
     bool operator==(const GraphKey& o) const {
       return bytes == o.bytes && lines == o.lines && src == o.src && map_text == o.map_text &&
-             mode == o.mode && out == o.out && no_reset == o.no_reset;
+             mode == o.mode && out == o.out && no_reset == o.no_reset && pieces_sig == o.pieces_sig;
     }
   };
   struct DictGraph {
     GraphKey key;
     hipGraphExec_t exec;
     bool ordered;  // the captured job uses the ordered kernel
+    bool clean;    // ... and re-zeroes its scratch (job_self_cleaned)
   };
   std::vector<DictGraph> dict_graphs;  // one per (input shape, output buffer)
   bool graph_ordered = false;          // the last launched graph uses the ordered kernel
   // Dictionary jobs, and radix jobs that stay on the device end to end (partitioned sort
   // from the fast map's table, records straight into the mapped output: no host sync).
+  // (A piecewise upload is never captured: its copy/map fork-join replayed from a graph
+  // lost the overlap -- measured 1.91 vs 1.52 ms on 1M synthetic lines.)
   bool use_graph() const {  // dictionary jobs (the shard engine's entry points)
     if (cfg.graph >= 0) return cfg.graph > 0 && cfg.sort_path == SortPath::kDict;
     return cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast;
   }
   bool use_job_graph(const TextInput& in) const {
+    if (cfg.map_path == MapPath::kFast && large_ordered && in.bytes >= 2 * kPieceBytes) return false;
     const bool radix_ok = cfg.sort_path == SortPath::kRadix && cfg.map_path == MapPath::kFast &&
                           table_tiles(in.bytes) > 0 && radix_mapped() && psort_enabled();
     if (cfg.graph >= 0) return cfg.graph > 0 && (cfg.sort_path == SortPath::kDict || radix_ok);
@@ -555,8 +631,11 @@ struct DevicePipeline {
   // Capture [upload DMA + reset, map, dictionary build, rank, emit] once per input shape
   // and source; later runs replay it with one hipGraphLaunch.
   void launch_dict_graph(const TextInput& in, bool compat) {
+    u64 sig = 0;
+    for (const auto& pc : pieces) sig = (sig ^ pc.first) * 0x100000001b3ull;
+    if (!pieces.empty()) sig |= 1;
     const GraphKey key{in.bytes, in.num_lines, upload_mode == Upload::kDirect ? in.data : nullptr,
-                       map_text, upload_mode, d_out_mapped, skip_sync_reset};
+                       map_text, upload_mode, d_out_mapped, skip_sync_reset, sig};
     const DictGraph* hit = nullptr;
     for (const auto& g : dict_graphs)
       if (g.key == key) hit = &g;
@@ -575,18 +654,21 @@ struct DevicePipeline {
       } else {
         enqueue_radix_job((u32)in.num_lines, compat, nullptr, nullptr);
         ordered = psort_used;
+        job_self_cleaned = false;
       }
       LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
       hipGraphExec_t exec = nullptr;
       LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
       LOCUST_HIP_CHECK(hipGraphDestroy(g));
-      dict_graphs.push_back({key, exec, ordered});
+      dict_graphs.push_back({key, exec, ordered, job_self_cleaned});
       hit = &dict_graphs.back();
     }
     graph_ordered = hit->ordered;
+    job_self_cleaned = hit->clean;
     if (cfg.sort_path == SortPath::kRadix) psort_used = hit->ordered;
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
-    part_tiles = cfg.map_path == MapPath::kFast ? table_tiles(in.bytes) : 0u;
+    part_tiles = cfg.map_path != MapPath::kFast ? 0u : pieces.empty() ? table_tiles(in.bytes)
+                                                                         : piece_tiles();
     LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
   }
   bool use_zero_copy(const TextInput& in) const {
@@ -597,15 +679,43 @@ struct DevicePipeline {
 
   void enqueue_map(const TextInput& in) {
     parts_ready = cfg.map_path == MapPath::kFast;
+    // combining needs the 4 KiB grouped map: upload pieces, or one launch past kMapLargeInput
+    map_combined = combine_map && large_ordered && cfg.map_path == MapPath::kFast &&
+                   (!pieces.empty() ? piece_tiles() > 0
+                                    : in.bytes >= kMapLargeInput && table_tiles(in.bytes) > 0);
     if (cfg.map_path == MapPath::kCompat) {
       launch_line_index(d_text, in.bytes, d_nl, d_ctr, lb_line, stream);
       launch_map_compat(d_text, in.bytes, d_nl, (u32)in.num_lines, d_delims, cfg.emits_per_line,
                         cfg.max_key_len, slots, d_line_counts, d_ctr, stream);
+    } else if (!pieces.empty()) {
+      // piece k: H2D on the copy stream, then its map on the compute stream once it landed
+      // (4 KiB tiles; the table rows of the pieces follow each other)
+      ensure_piece_events(pieces.size());
+      part_tiles = piece_tiles();
+      const char* src = upload_mode == Upload::kDirect ? in.data : h_text;
+      const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
+      LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
+      u64 tile_off = 0;
+      for (size_t k = 0; k < pieces.size(); ++k) {
+        const u64 off = pieces[k].first, len = pieces[k].second;
+        LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cstream));
+        if (k + 1 == pieces.size())
+          LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, cstream));
+        LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cstream));
+        LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_piece[k], 0));
+        launch_map_fast(d_text + off, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, d_parts,
+                        cap, d_ctr, lb_map, stream, nullptr,
+                        part_tiles ? d_part_off + tile_off * kPartTable : nullptr, part_map(),
+                        /*large_tiles=*/true, map_combined ? d_counts : nullptr);
+        tile_off += div_up(len, kMapTileBytesLarge);
+      }
     } else {
       part_tiles = table_tiles(in.bytes);
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
-                      stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map());
+                      stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
+                      map_combined ? d_counts : nullptr);
     }
   }
 
@@ -645,7 +755,8 @@ struct DevicePipeline {
     return !(v && v[0] == '0');
   }
   bool psort_ok(bool compat, bool with_counts) const {
-    return psort_enabled() && !compat && !with_counts && parts_ready && part_tiles > 0;
+    return psort_enabled() && !compat && !with_counts && parts_ready && part_tiles > 0 &&
+           cap <= kPartBuildMaxTokens;
   }
   bool psort_used = false;  // the last enqueue_process took the partitioned sort
 
@@ -745,11 +856,15 @@ struct DevicePipeline {
   // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
   // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
   bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
+  // Two-kernel ordered build of a large pass (the map wrote its partition table).
+  bool large_ordered_ok() const {
+    return large_ordered && parts_ready && part_tiles > 0 && cap > kPartBuildMaxTokens;
+  }
   // Tiles of the per-tile partition table the fast map writes for an input of `bytes`
   // (0: no table for this input).
   u32 table_tiles(u64 bytes) const {
-    const u64 t = div_up(bytes, kMapTileBytesMin);
-    return d_part_off && bytes < kMapLargeInput && t <= part_off_tiles ? (u32)t : 0u;
+    const u64 t = div_up(bytes, map_tile_bytes(bytes));
+    return d_part_off && t <= part_off_tiles ? (u32)t : 0u;
   }
   // The ordered kernel reads partition runs from the map's per-tile table when the current
   // tokens came from the small-input fast map (unweighted).
@@ -770,8 +885,6 @@ struct DevicePipeline {
   // captured graphs stay valid when the host retunes the contents).
   PartMap part_map() const {
     PartMap pm;
-    pm.base = d_pmap->base;
-    pm.thr = d_pmap->thr;
     pm.lo = d_pmap->lo;
     return pm;
   }
@@ -790,6 +903,16 @@ struct DevicePipeline {
     if (sum < (1u << 13) || mx * kDictParts <= 2 * sum) return 0;  // small or balanced
     if (pm_predicted_max && mx * 4 <= pm_predicted_max * 5) return 0;  // as good as it gets
     return mx;
+  }
+  // After an ordered run overflowed a partition (or the output): rebuild the map from the
+  // fallback's output so the next job's partitions fit (kept if it would not help).
+  void force_retune(const WordCountEntry* e, u64 n) {
+    if (const char* v = std::getenv("LOCUST_PART_TUNE"))
+      if (v[0] == '0') return;
+    if (!n) return;
+    PartMapTables t;
+    const u64 pred = part_map_from_entries(e, n, &t);
+    retune_with(~0ull / 8, pred, t);
   }
   void maybe_retune(const WordCountEntry* e, u64 n) {
     if (const u64 mx = retune_wanted()) {
@@ -879,6 +1002,41 @@ struct DevicePipeline {
                    (x[5] - t0) * 0.01);
     }
   }
+  // LOCUST_ORD_TRACE=1 on a large pass: the partials kernel's per-workgroup timeline.
+  u64* d_partials_trace = nullptr;
+  u64* partials_trace() {
+    static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
+    if (!on) return nullptr;
+    if (!d_partials_trace) {
+      LOCUST_HIP_CHECK(hipMalloc(&d_partials_trace, (u64)kDictParts * kOrdWorkers * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_partials_trace, 0, (u64)kDictParts * kOrdWorkers * 8 * sizeof(u64)));
+    }
+    return d_partials_trace;
+  }
+  void print_partials_trace() {
+    if (!d_partials_trace) return;
+    const u64 nb = (u64)kDictParts * kOrdWorkers;
+    std::vector<u64> t(nb * 8);
+    LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_partials_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    u64 t0 = ~0ull, t1 = 0, tok = 0;
+    for (u64 b = 0; b < nb; ++b) {
+      if (!t[b * 8]) continue;
+      t0 = std::min(t0, t[b * 8]);
+      t1 = std::max(t1, t[b * 8 + 3]);
+      tok += t[b * 8 + 4];
+    }
+    std::fprintf(stderr, "partials span=%.2f us, tokens=%llu\n", (t1 - t0) * 0.01,
+                 (unsigned long long)tok);
+    for (u64 b = 0; b < nb; ++b) {
+      const u64* x = &t[b * 8];
+      if (!x[0]) continue;
+      std::fprintf(stderr, "partials b=%4llu p=%3llu k=%llu in=%7.2f clear=%6.2f insert=%7.2f "
+                   "out=%7.2f tok=%7llu distinct=%5llu\n", (unsigned long long)b,
+                   (unsigned long long)(b % kDictParts), (unsigned long long)(b / kDictParts),
+                   (x[0] - t0) * 0.01, (x[1] - x[0]) * 0.01, (x[2] - x[1]) * 0.01,
+                   (x[3] - t0) * 0.01, (unsigned long long)x[4], (unsigned long long)x[5]);
+    }
+  }
   // LOCUST_ORD_TRACE=1 on the radix path: the partitioned sort's per-partition phases.
   void print_psort_trace() {
     if (!d_ord_trace) return;
@@ -942,12 +1100,30 @@ struct DevicePipeline {
                    (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13));
     }
   }
+  // The last enqueue_dict_job's kernels re-zero the scratch they dirty (small ordered
+  // build with self_clean): the next run() may skip the reset.
+  bool job_self_cleaned = false;
   // Process + emit of a dictionary run; returns true if the ordered kernel was used.
   bool enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process,
                         bool self_clean = false) {
+    job_self_cleaned = false;
     if (!compat && ordered_ok()) {
-      enqueue_dict_ordered(with_counts, /*mapped=*/true, self_clean && cfg.map_path == MapPath::kFast);
+      job_self_cleaned = self_clean && cfg.map_path == MapPath::kFast;
+      enqueue_dict_ordered(with_counts, /*mapped=*/true, job_self_cleaned);
       if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+      return true;
+    }
+    if (!compat && !with_counts && large_ordered_ok()) {
+      // large pass: per-slice partials (Process), then merge + sort + records (Reduce)
+      launch_dict_partials(tokens, map_combined ? d_counts : nullptr, d_part_off, part_tiles, cap,
+                           d_partials, d_partial_n, stream, partials_trace());
+      if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+      OrderedExtra ex;
+      ex.pm = part_map();
+      ex.part_w = d_pw;
+      ex.out_cap = h_out_cap;
+      launch_dict_ordered_partials(d_partials, d_partial_n, d_ctr, d_out_mapped, d_ctr_mapped,
+                                   lb_dict, stream, ord_trace(), ex);
       return true;
     }
     enqueue_process_dict(num_lines, compat, with_counts);
@@ -1130,6 +1306,11 @@ struct DevicePipeline {
     const u64 t0 = now_ns();
     const bool compat = cfg.map_path == MapPath::kCompat;
     const bool dict_path = cfg.sort_path == SortPath::kDict;
+    struct ClearOnExit {  // only this entry point's dictionary pass combines in the map
+      bool& f;
+      ~ClearOnExit() { f = false; }
+    } clear_combine{combine_map};
+    combine_map = dict_path && !compat && large_ordered;
     const bool graphed = use_job_graph(in);
     skip_sync_reset = clean_start && dict_path && !compat;
     LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
@@ -1158,20 +1339,24 @@ struct DevicePipeline {
       r.times.host_launch_ms = (t_launched - t0) * 1e-6;
       r.times.host_wait_ms = (t_synced - t_launched) * 1e-6;
       *h_ctr = *h_ctr_mapped;
+      if (ordered && h_ctr->num_unique > h_out_cap) h_ctr->flags |= kCtrDictOverflow;  // no records
       const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
-      sync_clean = ordered_done && !compat;  // the kernel re-zeroed what this job dirtied
+      sync_clean = ordered_done && !compat && job_self_cleaned;  // the kernel re-zeroed its scratch
       if (ordered) print_ord_trace();
+      print_partials_trace();
       print_map_trace();
-      if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, false);
+      if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, map_combined);
       if (!ordered_done && dict_fallback_needed()) {
-        finish_dict_with_radix((u32)in.num_lines);
+        finish_dict_with_radix((u32)in.num_lines, map_combined);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         download_output(r, ev[5]);
+        if (ordered) force_retune(r.entries.data(), r.entries.size());
       } else {
         fill_counters(r);
         copy_out(r.entries, h_ctr->num_unique);
         r.times.host_copy_ms = (now_ns() - t_synced) * 1e-6;
         if (ordered_done) maybe_retune(r.entries.data(), r.entries.size());
+        else if (ordered) force_retune(r.entries.data(), r.entries.size());
       }
     } else {
       if (!graphed) enqueue_radix_job((u32)in.num_lines, compat, ev[3], ev[4]);

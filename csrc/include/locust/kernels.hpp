@@ -82,22 +82,34 @@ void launch_compact_slots(const u32* line_counts, u32 num_lines, int emits_per_l
 
 // ---------------- partition map: see locust/partmap.hpp ----------------
 struct PartMap {                 // device view of a PartMapTables image
-  const u8* base = nullptr;      // [256]; null: partition = first key byte
-  const u64* thr = nullptr;      // [256] thresholds, one byte each, ascending, 0 = unused
-  const u32* lo = nullptr;       // [kDictParts + 1]
+  const u64* lo = nullptr;       // [kDictParts + 1] range starts; null: first key byte
 };
+__device__ __forceinline__ u32 part_of(const PartMap& pm, u64 w0) {
+  return pm.lo ? part_of_w0(pm.lo, w0) : (u32)(w0 >> 56);
+}
 
 // Byte-parallel tokenizer: tokens compacted in text order straight into `out`.
 // trace (diagnostics, optional): per tile < 4096, s_memrealtime stamps at trace[t*8+0..5].
-// part_off (optional, inputs below kMapLargeInput): the tokens of each 1 KiB tile are
-// written grouped by partition (first key byte) and part_off[t * kPartTable + p] is the
-// absolute index of tile t's first partition-p token ([.. + kPartTable - 1] = the tile's
-// end), so a partition's tokens are found without scanning every token's tag.
+// part_off (optional): the tokens of each tile (map_tile_bytes(bytes): 1 KiB below
+// kMapLargeInput, else 4 KiB) are written grouped by PartMap partition and
+// part_off[t * kPartTable + p] is the absolute index of tile t's first partition-p token
+// ([.. + kPartTable - 1] = the tile's end), so a partition's tokens are found without
+// scanning every token's tag.
+// counts (optional, 4 KiB tiles with part_off): per-tile combining -- in every tile, the
+// first one-word key (<= 7 bytes) of each partition and all its repeats become ONE record
+// at the head of the partition's run, with counts[i] = its multiplicity (1 for the other
+// records); num_records then counts records, not tokens.  Zipfian text loses most of its
+// hot-key volume before it is ever written.
 constexpr int kPartTable = 257;
+constexpr int kMapTileBytesLarge = (kMapBlock / 64) * kMapSegStepsLarge * 64;
+inline u64 map_tile_bytes(u64 bytes) {
+  return bytes < kMapLargeInput ? (u64)kMapTileBytesMin : (u64)kMapTileBytesLarge;
+}
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
-                     u32* part_off = nullptr, PartMap pm = PartMap{});
+                     u32* part_off = nullptr, PartMap pm = PartMap{}, bool large_tiles = false,
+                     u64* counts = nullptr);
 
 // ---------------- radix_sort.hip ----------------
 constexpr int kSortBlock = 256;
@@ -262,11 +274,31 @@ struct OrderedExtra {
   // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x
   // distinct keys), written every run; the host retunes `pm` when it is unbalanced.
   u32* part_w = nullptr;
+  // Records `out` holds: a job with more distinct keys writes none (the host sees
+  // num_unique > out_cap and takes another path).
+  u64 out_cap = ~0ull;
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
                          u64* trace = nullptr, const OrderedExtra& ex = OrderedExtra{});
+// Large ordered build (passes past kPartBuildMaxTokens whose map wrote a partition table,
+// dict.hip): launch_dict_partials aggregates partition p's tokens of tile slice k in
+// workgroup (p, k) and writes the distinct keys + counts to partial slot p * kOrdWorkers + k
+// (`partials`: kDictParts * kOrdWorkers * kPartSlots records, `partial_n`: one length per
+// slot, all ones if its table overflowed); launch_dict_ordered_partials merges each
+// partition's slots and finishes like launch_dict_ordered (overflow: kCtrDictOverflow).
+constexpr int kOrdWorkers = 4;
+constexpr int kPartSlotsHost = 2048;  // distinct keys per LDS table (dict.hip kPartSlots)
+// trace (diagnostics, optional): kDictParts * kOrdWorkers * 8 stamps (see dict.hip).
+// counts: per-record multiplicities of a combining map (null: every record is 1).
+void launch_dict_partials(ConstKeysSoA tokens, const u64* counts, const u32* part_off,
+                          u32 ntiles, u64 cap, KeyCount* partials, u32* partial_n, hipStream_t s,
+                          u64* trace = nullptr);
+void launch_dict_ordered_partials(const KeyCount* partials, const u32* partial_n,
+                                  MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                                  LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
+                                  const OrderedExtra& ex = OrderedExtra{});
 // Same, over runs of KeyCount records each sorted by key (the gather strategy's per-rank
 // combined outputs); duplicates across runs are summed.  Run 0 is `own`, runs 1.. lie
 // back to back in `recv`; `meta` (device) = [nruns <= 64, len_0, len_1, ...].

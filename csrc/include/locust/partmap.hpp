@@ -1,12 +1,15 @@
 // Host side of the partition map (PartMap, kernels.hpp): the order-preserving assignment
-// of 2-byte key prefixes to the ordered dictionary kernel's kDictParts workgroups.
+// of key ranges to the ordered dictionary kernel's kDictParts workgroups (and to the
+// partitioned radix sort's).
 //
 // The reference has no counterpart -- its Process stage is one comparison sort over every
-// record (/root/reference/MapReduce/src/main.cu:414-415).  Here the Process+Reduce kernel
-// gives each workgroup one key range; with ranges = first letters (the default) the
-// 's'/'c'/'t' workgroups of English text carry 10-15 % of the tokens each and form the
-// critical path while most others idle.  part_map_build splits hot letters by their second
-// byte and merges rare ones so every workgroup gets ~1/256 of the work.
+// record (/root/reference/MapReduce/src/main.cu:414-415).  Here each workgroup owns one key
+// range; with ranges = first letters (the default) the 's'/'c'/'t' workgroups of English
+// text carry 10-15 % of the tokens each and form the critical path while most others idle,
+// and a large vocabulary puts thousands of distinct keys into one letter -- more than a
+// workgroup's LDS table holds.  part_map_from_entries cuts the key space at the first key
+// WORD (an 8-byte prefix) wherever the work or the distinct keys of a range reach their
+// share: only keys sharing all of their first 8 bytes always stay together.
 #pragma once
 
 #include <cstddef>
@@ -17,48 +20,35 @@ namespace locust {
 
 struct WordCountEntry;
 
-// The ordered dictionary build gives each of its kDictParts workgroups one PARTITION of
-// the key space: a contiguous range of 2-byte key prefixes, so concatenating the
-// partitions in order is the global key order.  partition(c, d) = base[c] +
-// #{ thresholds t of row c : t != 0 && t <= d }, at most kPartMaxThr thresholds per first
-// byte c, so the lookup is 2.3 KB of table that the map kernel stages in LDS.  lo[p] =
-// first 2-byte prefix of partition p (lo[kDictParts] = 65536), for the in-partition sort.
 constexpr int kDictParts = 256;
-constexpr int kPartMaxThr = 8;
 constexpr u32 kPartDistinctWeight = 3;  // work of one distinct key, in tokens
-LOCUST_HD inline u32 part_of_prefix(u32 c, u32 d, u32 base, u64 thr) {
-  u32 n = 0;
-  for (int i = 0; i < kPartMaxThr; ++i) {  // constant trip count: unrolled at -O3
-    const u32 t = (u32)(thr >> (8 * i)) & 0xffu;
-    n += (t != 0u && t <= d) ? 1u : 0u;
-  }
-  return base + n;
-}
 
-// Device image of a partition map (one H2D copy): base[256], thr[256], lo[257].
+// Device image of a partition map (one H2D copy): partition p holds the keys whose first
+// word w0 satisfies lo[p] <= w0 < lo[p + 1]; lo[0] = 0, ascending (equal neighbours = an
+// empty partition), lo[kDictParts] = ~0 (unused by the lookup).
 struct PartMapTables {
-  u64 thr[256];
-  u32 lo[kDictParts + 1];
-  u8 base[256];
+  u64 lo[kDictParts + 1];
 };
 
-// partition = first key byte (what the ordered kernel did before balancing)
+// Partition of a first key word: the largest p with lo[p] <= w0 (8-step binary search over
+// lo[1..255]; monotone in w0, so partitions concatenate in key order).
+LOCUST_HD inline u32 part_of_w0(const u64* lo, u64 w0) {
+  u32 p = 0;
+  for (u32 step = kDictParts / 2; step; step >>= 1)
+    if (lo[p + step] <= w0) p += step;
+  return p;
+}
+
+// partition = first key byte
 void part_map_default(PartMapTables* t);
 
-// Balanced map from per-2-byte-prefix work (`weight`, 65,536 entries) and distinct-key
-// counts (`distinct`): greedy ranges of ~total/256 work, at most kPartMaxThr splits per
-// first byte, at most `max_distinct` distinct keys per partition where splitting allows.
-// Returns the largest partition's predicted work.
-u64 part_map_build(const u64* weight, const u32* distinct, PartMapTables* t,
-                   u32 max_distinct = 1024);
+// Balanced map from a job's sorted (key, count) output: greedy key ranges of ~total/256
+// work (count + kPartDistinctWeight per distinct key, the ordered kernel's part_w measure)
+// and at most `max_distinct` distinct keys each, cut only between different first words.
+// Returns the largest partition's predicted work (0 for no entries: default map).
+u64 part_map_from_entries(const WordCountEntry* e, size_t n, PartMapTables* t,
+                          u32 max_distinct = 1024);
 
-// The same from a job's sorted (key, count) output: work = count + kPartDistinctWeight per
-// distinct key (the ordered kernel's part_w measure).
-u64 part_map_from_entries(const WordCountEntry* e, size_t n, PartMapTables* t);
-
-// Partition of a 2-byte prefix under `t` (host mirror of the device lookup).
-inline u32 part_map_lookup(const PartMapTables& t, u32 prefix) {
-  return part_of_prefix(prefix >> 8, prefix & 0xffu, t.base[prefix >> 8], t.thr[prefix >> 8]);
-}
+inline u32 part_map_lookup(const PartMapTables& t, u64 w0) { return part_of_w0(t.lo, w0); }
 
 }  // namespace locust

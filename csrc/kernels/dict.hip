@@ -210,13 +210,17 @@ __device__ __forceinline__ void load_key(ConstKeysSoA t, u32 i, u64* k) {
 
 constexpr int kPartBlock = 1024;       // 16 waves: latency hiding for the gathers
 constexpr int kPartSlots = 2048;       // 80 KB of LDS
+static_assert(kPartSlots == kPartSlotsHost, "partial slot size");
 constexpr int kPartWindow = kPartBlock * 16;  // partition bytes scanned per round
 constexpr u32 kOrdTagWindow = kPartBlock * 32;  // ordered build: tags scanned per round
 constexpr int kPartPerThread = kPartSlots / kPartBlock;
 
+// A key not placed within kPartProbes slots reports the table full (the caller falls back):
+// probing a nearly full table to the end made an overflowing pass quadratic.
+constexpr int kPartProbes = 128;
 __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h) {
   u32 slot = (u32)(h >> 8) & (kPartSlots - 1);
-  for (int probe = 0; probe < kPartSlots;) {
+  for (int probe = 0; probe < kPartProbes;) {
     LdsSlot& sl = tab[slot];
     u64 w0 = sl.w[0];
     if (w0 == 0) {
@@ -251,6 +255,7 @@ __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 
 // round (the tokens were written by the map on other XCDs: these are L2 misses).  Longer
 // keys' further words are rare (English words fit in 8 bytes) and gathered after.
 constexpr int kGatherBatch = 4;
+template <int kGatherBatch = kGatherBatch>
 __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* counts,
                                               const u32* s_list, u32 lim, u32 n_cap,
                                               LdsSlot* s_tab) {
@@ -282,7 +287,27 @@ __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* co
       }
 #pragma unroll
     for (int r = 0; r < kGatherBatch; ++r) {
-      const bool live = k[r][0] != 0 && c[r] != 0;
+      bool live = k[r][0] != 0 && c[r] != 0;
+      // Hot keys: the lanes holding the same key as the wave's first live lane are combined
+      // into one insert by that lane (Zipfian text: a hot partition's waves are mostly one
+      // or two keys, and 64 LDS atomics on one slot serialise).
+      const u64 lm = dev::ballot(live);
+      if (lm) {
+        const int L = __ffsll((unsigned long long)lm) - 1;
+        bool same = live;
+#pragma unroll
+        for (int j = 0; j < kKeyWords; ++j) {
+          const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)k[r][j], L);
+          const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(k[r][j] >> 32), L);
+          same &= k[r][j] == (((u64)hi << 32) | lo);
+        }
+        const u64 sm = dev::ballot(same);
+        if (__popcll(sm) > 1) {
+          const u64 tot = counts ? dev::wave_reduce_sum(same ? c[r] : 0ull) : (u64)__popcll(sm);
+          if (dev::lane_id() == L) c[r] = tot;
+          else if (same) live = false;
+        }
+      }
       if (live) full |= !part_lds_insert(s_tab, k[r], c[r], key_hash(k[r]));
     }
   }
@@ -539,10 +564,7 @@ struct RunsSource {
   const KeyCount* recv;
   const u32* meta;
   PartMap pm;
-  __device__ u32 part(u64 w0) const {
-    const u32 c = (u32)(w0 >> 56);
-    return pm.base ? part_of_prefix(c, (u32)(w0 >> 48) & 0xffu, pm.base[c], pm.thr[c]) : c;
-  }
+  __device__ u32 part(u64 w0) const { return part_of(pm, w0); }
   struct Pre {};
   __device__ Pre prefetch(u32) const { return {}; }
   __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count, u64*) const {
@@ -602,6 +624,189 @@ struct RunsSource {
   }
 };
 
+// ---------------------------------------------------------------------------------
+// Large ordered build (passes past kPartBuildMaxTokens, fast map with a partition table):
+// the single-kernel build would give one workgroup a hot partition's hundreds of
+// thousands of tokens, so the aggregation is split in two launches.
+//  dict_partials_kernel: workgroup (p, k) aggregates partition p's tokens in the k-th of
+//    kOrdWorkers tile slices in an LDS table and writes the distinct keys with their
+//    counts to its partial slot (KeyCount records, kPartSlots per slot) -- no global
+//    atomics, no HBM hash table, hot keys combined per wave before the LDS insert.
+//  dict_ordered_kernel<PartialsSource>: workgroup p merges its kOrdWorkers partials in LDS
+//    and runs the ordered kernel's sort, look-back and record output.
+// ---------------------------------------------------------------------------------
+constexpr u32 kPartialFull = 0xFFFFFFFFu;  // partial_n of a slot whose table overflowed
+
+// Every thread walks the partition's runs of its own tiles (no LDS list: the table is the
+// workgroup's only LDS, so two workgroups share a CU), kPartialBatch gathers in flight.
+constexpr int kPartialBatch = 8;
+__global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
+    ConstKeysSoA tokens, const u64* __restrict__ counts, const u32* __restrict__ part_off,
+    u32 ntiles, u32 n_cap, KeyCount* __restrict__ partials, u32* __restrict__ partial_n,
+    u32 variant, u64* __restrict__ trace) {
+  // trace (diagnostics, LOCUST_ORD_TRACE): per workgroup b, at trace[b*8 + k] (100 MHz
+  // device clock): 0 entry, 1 table cleared, 2 inserts done, 3 exit; 4 tokens, 5 distinct
+  if (trace && threadIdx.x == 0) trace[(u64)blockIdx.x * 8] = __builtin_amdgcn_s_memrealtime();
+  __shared__ LdsSlot s_tab[kPartSlots];
+  __shared__ u32 s_scan[kPartBlock / 64 + 1];
+  __shared__ u32 s_tok;
+  if (threadIdx.x == 0) s_tok = 0;
+  // worker k of partition p: the workers of one partition are kDictParts apart in
+  // dispatch order, so a hot partition's slices land on different CUs and XCDs
+  const u32 p = blockIdx.x % kDictParts, k = blockIdx.x / kDictParts;
+  const u32 t0 = (u32)((u64)ntiles * k / kOrdWorkers);
+  const u32 t1 = (u32)((u64)ntiles * (k + 1) / kOrdWorkers);
+  // this thread's first run, loaded before the table clear (overlaps it)
+  u32 a = 0, len = 0;
+  u32 t = t0 + threadIdx.x;
+  if (t < t1) {
+    a = part_off[(u64)t * kPartTable + p];
+    len = part_off[(u64)t * kPartTable + p + 1] - a;
+  }
+  for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
+    s_tab[i].count = 0;
+  }
+  __syncthreads();
+  if (trace && threadIdx.x == 0) trace[(u64)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+  bool full = false;
+  u32 ntok = 0;
+  // The loop trip counts are per lane; the wave keeps going while any lane has work.
+  while (dev::ballot(t < t1)) {
+    u32 na = 0, nlen = 0;  // the next tile's run, prefetched
+    const u32 tn = t + kPartBlock;
+    if (tn < t1) {
+      na = part_off[(u64)tn * kPartTable + p];
+      nlen = part_off[(u64)tn * kPartTable + p + 1] - na;
+    }
+    for (u32 j0 = 0; dev::ballot(j0 < len); j0 += kPartialBatch) {
+      u64 kk[kPartialBatch][kKeyWords];
+      u64 cc[kPartialBatch];
+#pragma unroll
+      for (int r = 0; r < kPartialBatch; ++r) {
+        const u32 idx = a + j0 + (u32)r;
+        const bool ok = j0 + (u32)r < len && idx < n_cap;
+        kk[r][0] = ok ? tokens.w[0][idx] : 0;
+        cc[r] = ok && counts ? counts[idx] : 1ull;
+        kk[r][1] = kk[r][2] = kk[r][3] = 0;
+      }
+#pragma unroll
+      for (int r = 0; r < kPartialBatch; ++r) {
+        const u32 idx = a + j0 + (u32)r;
+        if (kk[r][0] & 0xffull) {
+          kk[r][1] = tokens.w[1][idx];
+          if (kk[r][1] & 0xffull) {
+            kk[r][2] = tokens.w[2][idx];
+            if (kk[r][2] & 0xffull) kk[r][3] = tokens.w[3][idx];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kPartialBatch; ++r) {
+        bool live = kk[r][0] != 0 && cc[r] != 0;
+        u64 c = cc[r];
+        // hot keys: lanes holding the wave's first live key are one insert
+        const u64 lm = dev::ballot(live);
+        if (lm && !(variant & 4u)) {
+          const int L = __ffsll((unsigned long long)lm) - 1;
+          bool same = live;
+#pragma unroll
+          for (int j = 0; j < kKeyWords; ++j) {
+            const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)kk[r][j], L);
+            const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(kk[r][j] >> 32), L);
+            same &= kk[r][j] == (((u64)hi << 32) | lo);
+          }
+          const u64 sm = dev::ballot(same);
+          if (__popcll(sm) > 1) {
+            const u64 tot = counts ? dev::wave_reduce_sum(same ? c : 0ull) : (u64)__popcll(sm);
+            if (dev::lane_id() == L) c = tot;
+            else if (same) live = false;
+          }
+        }
+        if (live) full |= !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]));
+      }
+    }
+    ntok += len;
+    t = tn;
+    a = na;
+    len = nlen;
+  }
+  if (trace) atomicAdd(&s_tok, ntok);
+  __syncthreads();  // every wave's inserts are in the table before it is read
+  if (trace && threadIdx.x == 0) {
+    trace[(u64)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+    trace[(u64)blockIdx.x * 8 + 4] = s_tok;
+  }
+  // dense records: thread t owns slots [t * kPartPerThread, (t + 1) * kPartPerThread)
+  u32 mine = 0;
+#pragma unroll
+  for (int r = 0; r < kPartPerThread; ++r) mine += s_tab[threadIdx.x * kPartPerThread + r].w[0] != 0;
+  u32 total = 0;
+  const u32 excl = dev::block_exclusive_scan<u32, kPartBlock>(mine, s_scan, &total);
+  const int any_full = __syncthreads_or(full ? 1 : 0);
+  const u64 slot = (u64)p * kOrdWorkers + k;
+  if (threadIdx.x == 0) partial_n[slot] = any_full ? kPartialFull : total;
+  if (trace && threadIdx.x == 0) {
+    trace[(u64)blockIdx.x * 8 + 5] = total;
+    trace[(u64)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // before the writes
+  }
+  if (any_full) return;
+  KeyCount* out = partials + slot * kPartSlots;
+  u32 id = excl;
+#pragma unroll
+  for (int r = 0; r < kPartPerThread; ++r) {
+    const LdsSlot& sl = s_tab[threadIdx.x * kPartPerThread + r];
+    if (sl.w[0] == 0) continue;
+    KeyCount kc;
+    kc.w[0] = sl.w[0];
+#pragma unroll
+    for (int j = 1; j < kKeyWords; ++j) kc.w[j] = sl.w[j] ^ kWordMagic;
+    kc.count = sl.count;
+    out[id++] = kc;
+  }
+}
+
+// Token source of the ordered kernel after dict_partials_kernel: partition p's
+// kOrdWorkers partial slots, each a dense run of distinct keys with counts.
+struct PartialsSource {
+  const KeyCount* partials;
+  const u32* partial_n;
+  struct Pre {};
+  __device__ Pre prefetch(u32) const { return {}; }
+  __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count, u64*) const {
+    // s_list: [0, kOrdWorkers] exclusive prefix of the slots' lengths (full: overflow)
+    if (threadIdx.x == 0) {
+      u32 acc = 0, bad = 0;
+      for (int q = 0; q < kOrdWorkers; ++q) {
+        const u32 nq = partial_n[(u64)p * kOrdWorkers + q];
+        s_list[q] = acc;
+        if (nq == kPartialFull) bad = 1;
+        else acc += nq;
+      }
+      s_list[kOrdWorkers] = acc;
+      s_count = bad;
+    }
+    __syncthreads();
+    const u32 total = s_list[kOrdWorkers];
+    bool full = s_count != 0;
+    if (!full) {
+      for (u32 e = threadIdx.x; e < total; e += kPartBlock) {
+        u32 q = 0;
+        while (q + 1 < (u32)kOrdWorkers && s_list[q + 1] <= e) ++q;
+        const KeyCount& rec = partials[((u64)p * kOrdWorkers + q) * kPartSlots + (e - s_list[q])];
+        const u64 kk[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
+        if (kk[0] == 0 || rec.count == 0) continue;
+        full |= !part_lds_insert(s_tab, kk, rec.count, key_hash(kk));
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_count = 0;  // the ordered kernel reuses it
+    __syncthreads();
+    return full;
+  }
+};
+
 template <class Src>
 __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     Src src, MapCounters* __restrict__ ctr,
@@ -630,16 +835,19 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   ORD_STAMP(0);
   if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 10] = rt_entry;
   const typename Src::Pre first = p == blockIdx.x ? guess : src.prefetch(p);
-  // This partition's 2-byte-prefix range [plo, phi) (PartMap; default: first byte p).  The
-  // in-partition counting sort buckets keys by their 3-byte prefix scaled into 256
-  // order-preserving buckets: the second byte for a first-byte partition, the third byte
-  // for a partition of one 2-byte prefix ('th').
-  const u32 plo = ex.pm.lo ? ex.pm.lo[p] : p << 8;
-  const u32 phi = ex.pm.lo ? ex.pm.lo[p + 1] : (p + 1) << 8;
-  const u32 span = phi > plo ? phi - plo : 1u;  // 2-byte prefixes in the partition
-  auto bucket_of = [&](u64 w0) -> u32 {
-    const u32 rel = (u32)(w0 >> 40) - (plo << 8);  // < span * 256
-    return span == 256u ? rel >> 8 : span == 1u ? rel : rel / span;
+  // This partition's first-word range [plo, phi) (PartMap; default: first byte p).  The
+  // in-partition counting sort buckets keys by the 8 bits of (w0 - plo) just below the
+  // range's width: 256 order-preserving buckets -- the second byte for a first-byte
+  // partition, finer bytes for a narrow one ('th').
+  const u64 plo = ex.pm.lo ? ex.pm.lo[p] : (u64)p << 56;
+  const u64 phi = ex.pm.lo ? (p + 1 < (u32)kDictParts ? ex.pm.lo[p + 1] : ~0ull)
+                           : (p + 1 < (u32)kDictParts ? (u64)(p + 1) << 56 : ~0ull);
+  const u64 span = phi > plo ? phi - plo : 1ull;  // first words in the range (~0: to the end)
+  const u32 span_bits = 64u - (u32)__clzll((long long)(span - 1 | 1));
+  const u32 bshift = span_bits > 8u ? span_bits - 8u : 0u;
+  auto bucket_of = [&](u64 w0) -> u32 {  // w0 = ~0 in an open-ended range may reach 256
+    const u64 b = (w0 - plo) >> bshift;
+    return b < 255u ? (u32)b : 255u;
   };
   for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
 #pragma unroll
@@ -807,7 +1015,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     __syncthreads();
     const u64 base_m = pre & kOrdM;
     if (((pre >> kOrdOvfShift) & 511u) == 0) {  // uniform per workgroup
-      if (out) {
+      if (out && base_m + m <= ex.out_cap) {
         u64* dst = reinterpret_cast<u64*>(out + base_m);
         for (u32 q = threadIdx.x; q < 6 * m; q += kPartBlock) dst[q] = s_out[q];
       }
@@ -963,7 +1171,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       at += c[t];
     }
     __syncthreads();
-    if (out) {
+    if (out && base_m + m <= ex.out_cap) {
       // 16-B chunk q of this partition's slice: record q / 3, part q % 3
       u64* dst = reinterpret_cast<u64*>(out + base_m);
       for (u32 q = threadIdx.x; q < 3 * m; q += kPartBlock) {
@@ -1330,6 +1538,26 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
     dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
         src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   }
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_dict_partials(ConstKeysSoA tokens, const u64* counts, const u32* part_off,
+                          u32 ntiles, u64 cap, KeyCount* partials, u32* partial_n, hipStream_t s,
+                          u64* trace) {
+  dict_partials_kernel<<<dim3(kDictParts * kOrdWorkers), dim3(kPartBlock), 0, s>>>(
+      tokens, counts, part_off, ntiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu), partials, partial_n,
+      std::getenv("LOCUST_ORD_VARIANT") ? (u32)std::atoi(std::getenv("LOCUST_ORD_VARIANT")) : 0u,
+      trace);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_dict_ordered_partials(const KeyCount* partials, const u32* partial_n,
+                                  MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
+                                  LookbackScratch lb, hipStream_t s, u64* trace,
+                                  const OrderedExtra& ex) {
+  const PartialsSource src{partials, partial_n};
+  dict_ordered_kernel<PartialsSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
+      src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -41,10 +41,7 @@ __global__ __launch_bounds__(256) void unpack_records_kernel(const KeyCount* __r
 #pragma unroll
     for (int w = 0; w < kKeyWords; ++w) keys.w[w][i] = r.w[w];
     counts[i] = r.count;
-    if (parts) {  // partition of the key (see PartMap / launch_dict_ordered)
-      const u32 c = (u32)(r.w[0] >> 56), d = (u32)(r.w[0] >> 48) & 0xffu;
-      parts[i] = (u8)(pm.base ? part_of_prefix(c, d, pm.base[c], pm.thr[c]) : c);
-    }
+    if (parts) parts[i] = (u8)part_of(pm, r.w[0]);  // see PartMap / launch_dict_ordered
   }
 }
 

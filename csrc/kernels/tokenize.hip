@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace, u32* __restrict__ part_off,
-    PartMap pm) {
+    PartMap pm, u64* __restrict__ counts) {
   // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
   // at entry, tile acquired, text staged, masks done, prefix known, keys written.
   const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -160,11 +160,16 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char s_text[kStaged];
   __shared__ u64 s_prefix;
   __shared__ u32 s_wave_cnt[kBlock / 64];
-  // partition grouping (kSteps == 1 with part_off): per-partition counts, then offsets
-  __shared__ u32 s_pcnt[kSteps == 1 ? kPartTable : 1];
-  // the partition map's rows (PartMap), staged once per tile: 2.3 KB, read per token
-  __shared__ u64 s_pthr[256];
-  __shared__ u8 s_pbase[256];
+  // partition grouping (with part_off): per-partition counts, then offsets
+  __shared__ u32 s_pcnt[kPartTable];
+  // per-tile combining (large grouped tiles with `counts`): the first short key (<= 7 bytes,
+  // one word) of each partition claims a slot; its repeats in the tile become one record
+  constexpr bool kCombineTile = kSteps > 1;
+  __shared__ u64 s_hot[kCombineTile ? kDictParts : 1];
+  __shared__ u32 s_hotc[kCombineTile ? kDictParts : 1];
+  const bool combine = kCombineTile && part_off && counts;
+  // the partition map's range starts (PartMap), staged once per tile: 2 KB, searched per token
+  __shared__ u64 s_plo[kDictParts + 1];
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
   // Tokens are emitted in no particular order across tiles (every consumer sorts or
@@ -173,22 +178,18 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   if (tile >= num_tiles) return;
   if (trace && threadIdx.x == 0 && tile < 4096) trace[(u64)tile * 8] = t_entry;
   MAP_STAMP(1);
-  if constexpr (kSteps == 1) {
-    if (part_off)
-      for (int i = threadIdx.x; i < kPartTable; i += kBlock) s_pcnt[i] = 0;  // before a barrier
-  }
-
-  if (pm.base) {  // visible after the staging barrier below
-    for (int i = threadIdx.x; i < 256; i += kBlock) {
-      s_pthr[i] = pm.thr[i];
-      s_pbase[i] = pm.base[i];
+  if (part_off)
+    for (int i = threadIdx.x; i < kPartTable; i += kBlock) s_pcnt[i] = 0;  // before a barrier
+  if (combine)
+    for (int i = threadIdx.x; i < kDictParts; i += kBlock) {
+      s_hot[i] = 0;
+      s_hotc[i] = 0;
     }
-  }
-  // Partition of a packed key: its row's base + thresholds passed (default: first byte).
-  auto part_of = [&](u64 w0) -> u32 {
-    const u32 c = (u32)(w0 >> 56);
-    return pm.base ? part_of_prefix(c, (u32)(w0 >> 48) & 0xffu, s_pbase[c], s_pthr[c]) : c;
-  };
+
+  if (pm.lo)  // visible after the staging barrier below
+    for (int i = threadIdx.x; i <= kDictParts; i += kBlock) s_plo[i] = pm.lo[i];
+  // Partition of a packed key: binary search of its first word (default: first byte).
+  auto part_of = [&](u64 w0) -> u32 { return pm.lo ? part_of_w0(s_plo, w0) : (u32)(w0 >> 56); };
 
   // ---- stage the tile (+ context) into LDS with 16-B loads ----
   const i64 tile_base = (i64)tile * kTile;
@@ -276,8 +277,9 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     if (i < w) wave_excl += v;
     tile_total += v;
   }
-  // this tile's slice of the token array: one atomic per tile
-  if (threadIdx.x == 0) s_prefix = tile_total ? atomicAdd(&ctr->num_records, tile_total) : 0;
+  // this tile's slice of the token array: one atomic per tile (a combining tile reserves
+  // its records once it has counted them)
+  if (threadIdx.x == 0 && !combine) s_prefix = tile_total ? atomicAdd(&ctr->num_records, tile_total) : 0;
   __syncthreads();
   const u64 prefix = s_prefix;
   MAP_STAMP(4);
@@ -332,6 +334,101 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
       return;
     }
   }
+  if constexpr (kSteps > 1) {
+    if (part_off) {
+      // ---- phase 3 (grouped, large tiles): a lane emits up to kSteps tokens, so the
+      // partition ranks are drawn in a first sweep (first key word only) and the keys are
+      // packed again, in full, by a second sweep once the tile's partition offsets are
+      // known (repacking from LDS is cheaper than holding kSteps keys in registers) ----
+      constexpr u16 kCombined = 0xFFFF;  // folded into its partition's hot record
+      u16 loc[kSteps];
+#pragma unroll
+      for (int s = 0; s < kSteps; ++s) {
+        loc[s] = 0;
+        if ((emit_mask[s] >> lane) & 1ull) {
+          const u32 len = token_length(dmask[s], dmask[s + 1], lane);
+          u64 kw[kKeyWords];
+          pack_token(s_text, seg_lds + s * 64 + lane, len < (u32)max_key ? len : (u32)max_key, kw);
+          const u32 part = part_of(kw[0]);
+          bool folded = false;
+          if (combine && (kw[0] & 0xffull) == 0) {  // a one-word key
+            const u64 old = atomicCAS(reinterpret_cast<unsigned long long*>(&s_hot[part]), 0ull,
+                                      (unsigned long long)kw[0]);
+            if (old == 0 || old == kw[0]) {
+              atomicAdd(&s_hotc[part], 1u);
+              folded = true;
+            }
+          }
+          loc[s] = folded ? kCombined : (u16)atomicAdd(&s_pcnt[part], 1u);
+        }
+      }
+      __syncthreads();
+      if (combine) {  // a partition with a hot record: it leads the partition's run
+        for (int i = threadIdx.x; i < kDictParts; i += kBlock) s_pcnt[i] += s_hotc[i] ? 1u : 0u;
+        __syncthreads();
+      }
+      if (threadIdx.x < 64) {  // exclusive scan of the 256 partition counts by one wave
+        const u32 l = threadIdx.x;
+        const u32 h0 = s_pcnt[4 * l], h1 = s_pcnt[4 * l + 1], h2 = s_pcnt[4 * l + 2],
+                  h3 = s_pcnt[4 * l + 3];
+        const u32 sum4 = h0 + h1 + h2 + h3;
+        const u32 inc = dev::wave_inclusive_scan(sum4);
+        const u32 ex = inc - sum4;
+        s_pcnt[4 * l] = ex;
+        s_pcnt[4 * l + 1] = ex + h0;
+        s_pcnt[4 * l + 2] = ex + h0 + h1;
+        s_pcnt[4 * l + 3] = ex + h0 + h1 + h2;
+        if (l == 63) {
+          s_pcnt[kDictParts] = inc;
+          // a combining tile reserves its records (hot records + the rest) only now
+          if (combine) s_prefix = inc ? atomicAdd(&ctr->num_records, inc) : 0;
+        }
+      }
+      __syncthreads();
+      const u64 gprefix = combine ? s_prefix : prefix;
+      for (int i = threadIdx.x; i < kPartTable; i += kBlock)
+        part_off[(u64)tile * kPartTable + i] = (u32)(gprefix + s_pcnt[i]);
+      if (combine) {  // the hot records
+        for (int i = threadIdx.x; i < kDictParts; i += kBlock) {
+          const u32 c = s_hotc[i];
+          const u64 idx = gprefix + s_pcnt[i];
+          if (c && idx < out_cap) {
+            out.w[0][idx] = s_hot[i];
+#pragma unroll
+            for (int j = 1; j < kKeyWords; ++j) out.w[j][idx] = 0;
+            counts[idx] = c;
+            if (parts) parts[idx] = (u8)i;
+          }
+        }
+      }
+      u32 trunc = 0, maxlen = 0;
+#pragma unroll
+      for (int s = 0; s < kSteps; ++s) {
+        if ((emit_mask[s] >> lane) & 1ull) {
+          const u32 len = token_length(dmask[s], dmask[s + 1], lane);
+          if (len > (u32)max_key) ++trunc;
+          maxlen = len > maxlen ? len : maxlen;
+          if (loc[s] == kCombined) continue;
+          u64 kw[kKeyWords];
+          pack_token(s_text, seg_lds + s * 64 + lane, len < (u32)max_key ? len : (u32)max_key, kw);
+          const u32 part = part_of(kw[0]);
+          const u64 idx = gprefix + s_pcnt[part] + (combine && s_hotc[part] ? 1u : 0u) + loc[s];
+          if (idx < out_cap) {
+#pragma unroll
+            for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
+            if (parts) parts[idx] = (u8)part;
+            if (combine) counts[idx] = 1;
+          }
+        }
+      }
+      trunc = dev::wave_reduce_sum(trunc);
+      maxlen = dev::wave_reduce_max(maxlen);
+      if (lane == 0 && trunc) atomicAdd(&ctr->truncated, trunc);
+      if (lane == 0 && maxlen > (u32)max_key) atomicMax(&ctr->max_key_len, maxlen);
+      MAP_STAMP(5);
+      return;
+    }
+  }
   // ---- phase 3: length from masks, pack from LDS words, write ----
   u64 dst = prefix + wave_excl;
   u32 trunc = 0, maxlen = 0;
@@ -371,10 +468,10 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace, u32* part_off,
-                     PartMap pm) {
+                     PartMap pm, bool large_tiles, u64* counts) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
-  if (bytes < kMapLargeInput) {
+  if (bytes < kMapLargeInput && !large_tiles) {
     // Small inputs: 1 KiB tiles as 16 waves x ONE 64-byte step -- the same text per
     // workgroup (and the same PCIe reads), the least serial work per wave.  Measured A/B
     // in one process against 4 waves x 4 steps, 8 x 2 and 8 x 1 (profiles/r1_s2/
@@ -383,13 +480,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace, part_off, pm);
+        lb.tile_counter, trace, part_off, pm, nullptr);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace, nullptr, pm);
+        lb.tile_counter, trace, part_off, pm, part_off ? counts : nullptr);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }

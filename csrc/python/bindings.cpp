@@ -546,7 +546,7 @@ PYBIND11_MODULE(_locust, m) {
     return std::string(d_itoa(n, buf, base));
   });
   m.def("strcmp", [](const std::string& a, const std::string& b) { return d_strcmp(a.c_str(), b.c_str()); });
-  m.def("part_map_build", [](const std::vector<std::pair<std::string, u64>>& keys) {
+  m.def("part_map_build", [](const std::vector<std::pair<std::string, u64>>& keys, u32 max_distinct) {
     // Balanced partition map (locust/partmap.hpp) for sorted (key, count) pairs: the
     // tables plus the predicted largest partition work.
     std::vector<WordCountEntry> e(keys.size());
@@ -556,17 +556,19 @@ PYBIND11_MODULE(_locust, m) {
       e[i].val = 0;
     }
     PartMapTables t;
-    const u64 pred = part_map_from_entries(e.data(), e.size(), &t);
+    const u64 pred = part_map_from_entries(e.data(), e.size(), &t, max_distinct);
     py::dict d;
-    d["base"] = std::vector<u32>(t.base, t.base + 256);
-    d["thr"] = std::vector<u64>(t.thr, t.thr + 256);
-    d["lo"] = std::vector<u32>(t.lo, t.lo + kDictParts + 1);
+    d["lo"] = std::vector<u64>(t.lo, t.lo + kDictParts + 1);
     d["predicted_max"] = pred;
-    std::vector<u32> part(65536);
-    for (u32 b = 0; b < 65536; ++b) part[b] = part_map_lookup(t, b);
+    std::vector<u32> part(e.size());  // partition of every input key
+    for (size_t i = 0; i < e.size(); ++i) part[i] = part_map_lookup(t, e[i].key.w[0]);
     d["part"] = part;
     return d;
-  }, py::arg("keys"));
+  }, py::arg("keys"), py::arg("max_distinct") = 1024);
+  m.def("part_of_key", [](const std::vector<u64>& lo, const std::string& key) {
+    LOCUST_CHECK_ARG(lo.size() == (size_t)kDictParts + 1, "lo needs kDictParts + 1 entries");
+    return part_of_w0(lo.data(), to_key(key).w[0]);
+  });
   m.def("pack_key", [](const std::string& s) {
     PackedKey k = to_key(s);
     return std::vector<u64>(k.w, k.w + kKeyWords);

@@ -1,53 +1,56 @@
 """Partition map of the ordered dictionary build (locust/partmap.hpp): order-preserving
-2-byte-prefix ranges balanced by work, checked on the host (no GPU)."""
+first-word ranges balanced by work and distinct keys, checked on the host (no GPU)."""
 import collections
+import random
 
 import locust_amd as lc
 from locust_amd.utils import oracle
 
+W = 3  # kPartDistinctWeight
 
-def _weights(entries):
-    w = collections.Counter()
-    for k, _v, c in entries:
-        b = (k + b"\0\0")[:2]
-        w[b[0] << 8 | b[1]] += c + 3
-    return w
+
+def _check(ent, m, max_distinct):
+    part, lo = m["part"], m["lo"]
+    assert len(lo) == 257 and lo[0] == 0
+    assert all(a <= b for a, b in zip(lo, lo[1:])), "range starts not ascending"
+    assert all(a <= b for a, b in zip(part, part[1:])), "not order-preserving"
+    for (k, _v, _c), p in zip(ent, part):  # the device lookup agrees with the host's
+        assert lc._C.part_of_key(lo, k) == p
+    work, dist = collections.Counter(), collections.Counter()
+    for (k, _v, c), p in zip(ent, part):
+        work[p] += c + W
+        dist[p] += 1
+    assert max(work.values()) == m["predicted_max"]
+    # keys sharing their first 8 bytes never split; others respect max_distinct
+    first = collections.Counter((k + b"\0" * 8)[:8] for k, _v, _c in ent)
+    for p, d in dist.items():
+        assert d <= max(max_distinct, max(first.values()))
+    return work
 
 
 def test_balanced_map_is_monotone_and_covers(hamlet):
     ent = oracle.wordcount(hamlet)[0]
     m = lc._C.part_map_build([(k, c) for k, _v, c in ent])
-    part = m["part"]
-    assert all(part[b] <= part[b + 1] for b in range(65535)), "not order-preserving"
-    assert part[0] == 0 and part[65535] <= 255
-    lo = m["lo"]
-    for p in range(257):
-        if p <= part[65535]:
-            assert part[lo[p]] == p and (lo[p] == 0 or part[lo[p] - 1] < p)
-        else:
-            assert lo[p] == 65536
-    # every row uses at most 8 thresholds, and the lookup formula reproduces `part`
-    for c in range(256):
-        thr = [(m["thr"][c] >> (8 * i)) & 0xFF for i in range(8)]
-        for d in range(256):
-            assert part[c << 8 | d] == m["base"][c] + sum(1 for t in thr if t and t <= d)
-    # balance: far below the first-letter map's largest partition
-    w = _weights(ent)
-    first = collections.Counter()
-    for b, x in w.items():
-        first[b >> 8] += x
-    by_part = collections.Counter()
-    for b, x in w.items():
-        by_part[part[b]] += x
-    assert max(by_part.values()) == m["predicted_max"]
-    # 't' (4,555) and 's' split; the largest partition is the unsplittable 'th' prefix
-    hot = max(w.values())
-    assert m["predicted_max"] < max(first.values()) and m["predicted_max"] == hot
-    # every other partition is at most ~8 x the ideal share (8 thresholds per first byte)
-    second = sorted(by_part.values())[-2]
-    assert second <= 8 * sum(w.values()) // 256
+    work = _check(ent, m, 1024)
+    by_letter = collections.Counter()
+    for k, _v, c in ent:
+        by_letter[k[:1]] += c + W
+    # far below the first-letter map's largest partition; the largest is one hot word
+    assert m["predicted_max"] < max(by_letter.values()) // 2
+    hottest = max(c + W for _k, _v, c in ent)
+    assert m["predicted_max"] < 2 * max(hottest, sum(work.values()) // 256)
+
+
+def test_large_vocabulary_respects_distinct_cap():
+    rng = random.Random(3)
+    words = sorted({bytes(rng.choice(b"etaoinsh") for _ in range(rng.randint(2, 9)))
+                    for _ in range(120000)})
+    ent = [(w, 0, rng.randint(1, 20)) for w in words]
+    m = lc._C.part_map_build([(k, c) for k, _v, c in ent], max_distinct=512)
+    _check(ent, m, 512)
 
 
 def test_default_map_for_empty_input():
     m = lc._C.part_map_build([])
-    assert m["part"][0x7468] == 0x74 and m["predicted_max"] == 0
+    assert m["lo"][0x74] == 0x74 << 56 and m["predicted_max"] == 0
+    assert lc._C.part_of_key(m["lo"], b"the") == 0x74
