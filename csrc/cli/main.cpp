@@ -9,7 +9,8 @@
 // plus long flags (runtime switches replacing the reference's #defines):
 //   --backend gpu|cpu  --reduce-path lds|global  --map-path compat|fast
 //   --sort radix|dict  --gpus N  --comm auto|rccl|loopback  --emits-per-line N  --max-key N  --ref-compat
-//   --stage map|reduce  --spill-dir DIR  --spill-format text|binary  --inputs a,b,...
+//   --stage map|reduce  --spill-dir DIR  --spill-format text|binary|kiv  --inputs a,b,...
+//   --export-kiv FILE (results as the reference's 40-B KeyIntValuePair records)
 //   --warmup N  --iters N  --json FILE  --quiet  --check  --device N  --chunk-mb N
 //   --ref-timers (stage times taken where the reference's host timers were)
 // and a synthetic-text generator (BASELINE configs "1M lines" / "10 GB"):
@@ -45,6 +46,7 @@ struct CliArgs {
   std::vector<std::string> inputs;
   int warmup = 0, iters = 1;
   std::string json;
+  std::string export_kiv;  // final results as KeyIntValuePair records (--export-kiv FILE)
   bool quiet = false;
   std::string gen_out;  // generator mode
   GenSpec gen;
@@ -112,7 +114,11 @@ bool parse(int argc, char** argv, CliArgs* a) {
     } else if (s == "--spill-dir") {
       a->spill_dir = need("--spill-dir");
     } else if (s == "--spill-format") {
-      a->spill_fmt = need("--spill-format") == "binary" ? SpillFormat::kBinary : SpillFormat::kText;
+      const std::string v = need("--spill-format");
+      a->spill_fmt = v == "binary" ? SpillFormat::kBinary : v == "kiv" ? SpillFormat::kKiv
+                                                                     : SpillFormat::kText;
+    } else if (s == "--export-kiv") {
+      a->export_kiv = need("--export-kiv");
     } else if (s == "--inputs") {
       a->inputs = split(need("--inputs"), ',');
     } else if (s == "--warmup") {
@@ -160,7 +166,8 @@ bool parse(int argc, char** argv, CliArgs* a) {
 
 std::string spill_path(const CliArgs& a, int node) {
   return a.spill_dir + "/out." + std::to_string(node) +
-         (a.spill_fmt == SpillFormat::kBinary ? ".kv" : ".txt");
+         (a.spill_fmt == SpillFormat::kBinary ? ".kv" : a.spill_fmt == SpillFormat::kKiv ? ".kiv"
+                                                                                   : ".txt");
 }
 
 void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
@@ -348,6 +355,7 @@ int run(const CliArgs& a) {
   std::fflush(stdout);
   write_all(stdout, out);
   write_json(a, r, walls);
+  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r.entries);
   std::printf("\nDone\n");
   return 0;
 }

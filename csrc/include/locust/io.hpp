@@ -32,12 +32,26 @@ LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 lin
 u64 count_lines(const char* data, u64 bytes);
 
 // ---- spill files (map-output checkpoint) ----
-enum class SpillFormat { kText, kBinary };
+enum class SpillFormat { kText, kBinary, kKiv };
 // Text: the reference's "%s \t%d\n" (one line per record).  Binary: 32-byte header
-// ("LCSTSPL1", version, key words, record count) then 40-B KeyCount records.
+// ("LCSTSPL1", version, key words, record count) then 40-B KeyCount records.  Kiv: the
+// reference's own 40-B record, KeyIntValuePair (/root/reference/MapReduce/src/
+// KeyValue.h:13-18: char key[30], int value @32, int count @36), after a 32-byte header
+// ("LCSTKIV1", version, record size 40, record count); a spill stores value = the
+// record's count and count = 0, as the reference's map emits (key, 1, 0).
 void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt);
-// Reads either format (detected by magic).  Text keys lose the writer's trailing space.
+// Reads any of the three (detected by magic).  Text keys lose the writer's trailing space.
 std::vector<KeyCount> read_spill(const std::string& path);
+// Final (key, val, count) results as KeyIntValuePair records (value = val), the reference's
+// reduce output array (main.cu:470-473); the same header.  Values past INT_MAX and keys
+// past 29 bytes are refused.
+void write_kiv_results(const std::string& path, const EntryList& e);
+// KeyIntValuePair records of a kiv file: (key, value, count).
+struct KivRecord {
+  PackedKey key;
+  i64 value, count;
+};
+std::vector<KivRecord> read_kiv(const std::string& path);
 std::vector<KeyCount> tokens_to_records(const std::vector<PackedKey>& toks);
 std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs);
 

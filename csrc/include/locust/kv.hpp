@@ -3,8 +3,9 @@
 // Reference records (/root/reference/MapReduce/src/KeyValue.h:6-18):
 //   KeyValuePair    : char key[100]; char value[100]; int ind;       -> 204 B input record
 //   KeyIntValuePair : char key[30]; (2 B pad) int value; int count;  -> 40 B map/reduce record
-// Both layouts are reproduced byte-for-byte here (static_asserts below) because they are
-// the framework's external record format (stage-1 spill files, Python API, final output).
+// Both layouts are reproduced byte-for-byte here (static_asserts below).  KeyIntValuePair
+// is a real external format: the kiv stage-1 spill and the --export-kiv result file
+// (io.hpp write_spill / write_kiv_results).
 //
 // Internally the GPU pipeline never sorts 40-B structs with a byte comparator (the
 // reference's thrust::sort + KIVComparator, KeyValue.h:20-33).  A key is packed into

@@ -80,6 +80,7 @@ std::string key_to_string(const PackedKey& k) {
 // ---------------- spill ----------------
 namespace {
 constexpr char kMagic[8] = {'L', 'C', 'S', 'T', 'S', 'P', 'L', '1'};
+constexpr char kKivMagic[8] = {'L', 'C', 'S', 'T', 'K', 'I', 'V', '1'};
 struct SpillHeader {
   char magic[8];
   u32 version;
@@ -98,9 +99,75 @@ void append_u64(std::string* s, u64 v) {
   } while (v);
   while (n) s->push_back(tmp[--n]);
 }
+
+// One reference record from a packed key: NUL-padded key[30], int value, int count.
+KeyIntValuePair to_kiv(const u64* w, i64 value, i64 count, const std::string& path) {
+  KeyIntValuePair r;
+  std::memset(&r, 0, sizeof(r));
+  char buf[kKeyBytes + 1];
+  const int n = unpack_key(w, buf);
+  if (n > kMaxKeyLen) throw Error("key longer than KeyIntValuePair::key[30] holds: " + path);
+  if (value < INT32_MIN || value > INT32_MAX || count < INT32_MIN || count > INT32_MAX)
+    throw Error("value beyond KeyIntValuePair's int fields: " + path);
+  std::memcpy(r.key, buf, (size_t)n);
+  r.value = (int)value;
+  r.count = (int)count;
+  return r;
+}
+
+void write_kiv_file(const std::string& path, const std::vector<KeyIntValuePair>& recs) {
+  std::FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw Error("cannot write kiv file: " + path);
+  SpillHeader h{};
+  std::memcpy(h.magic, kKivMagic, 8);
+  h.version = 1;
+  h.key_words = (u32)sizeof(KeyIntValuePair);  // record size
+  h.count = recs.size();
+  std::fwrite(&h, sizeof(h), 1, f);
+  if (!recs.empty()) std::fwrite(recs.data(), sizeof(KeyIntValuePair), recs.size(), f);
+  if (std::fclose(f) != 0) throw Error("error closing kiv file: " + path);
+}
 }  // namespace
 
+void write_kiv_results(const std::string& path, const EntryList& e) {
+  std::vector<KeyIntValuePair> v;
+  v.reserve(e.size());
+  for (size_t i = 0; i < e.size(); ++i)
+    v.push_back(to_kiv(e[i].key.w, (i64)e[i].val, (i64)e[i].count, path));
+  write_kiv_file(path, v);
+}
+
+std::vector<KivRecord> read_kiv(const std::string& path) {
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw Error("cannot open kiv file: " + path);
+  SpillHeader h{};
+  const bool ok = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, kKivMagic, 8) == 0 &&
+                  h.version == 1 && h.key_words == sizeof(KeyIntValuePair);
+  std::vector<KeyIntValuePair> raw(ok ? h.count : 0);
+  const bool full = ok && (raw.empty() ||
+                           std::fread(raw.data(), sizeof(KeyIntValuePair), raw.size(), f) == raw.size());
+  std::fclose(f);
+  if (!ok) throw Error("not a kiv file: " + path);
+  if (!full) throw Error("truncated kiv file: " + path);
+  std::vector<KivRecord> out(raw.size());
+  for (size_t i = 0; i < raw.size(); ++i) {
+    const int n = (int)strnlen(raw[i].key, sizeof(raw[i].key));  // bounded (reference bug B11)
+    pack_key(raw[i].key, n, out[i].key.w);
+    out[i].value = raw[i].value;
+    out[i].count = raw[i].count;
+  }
+  return out;
+}
+
 void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt) {
+  if (fmt == SpillFormat::kKiv) {
+    std::vector<KeyIntValuePair> v;
+    v.reserve(recs.size());
+    for (const auto& r : recs)
+      if (r.w[0]) v.push_back(to_kiv(r.w, (i64)r.count, 0, path));
+    write_kiv_file(path, v);
+    return;
+  }
   std::FILE* f = std::fopen(path.c_str(), "wb");
   if (!f) throw Error("cannot write spill file: " + path);
   if (fmt == SpillFormat::kBinary) {
@@ -141,6 +208,16 @@ std::vector<KeyCount> read_spill(const std::string& path) {
   }
   std::fclose(f);
   std::vector<KeyCount> recs;
+  if (data.size() >= sizeof(SpillHeader) && std::memcmp(data.data(), kKivMagic, 8) == 0) {
+    for (const auto& k : read_kiv(path)) {  // value = the record's count (map output)
+      KeyCount r{};
+      for (int w = 0; w < kKeyWords; ++w) r.w[w] = k.key.w[w];
+      if (k.value < 0) throw Error("negative count in kiv spill: " + path);
+      r.count = (u64)k.value;
+      recs.push_back(r);
+    }
+    return recs;
+  }
   if (data.size() >= sizeof(SpillHeader) && std::memcmp(data.data(), kMagic, 8) == 0) {
     SpillHeader h;
     std::memcpy(&h, data.data(), sizeof(h));

@@ -374,6 +374,8 @@ PYBIND11_MODULE(_locust, m) {
       .def("entries", &PyResult::entries)
       .def("times", &PyResult::times)
       .def("format", &PyResult::format, py::arg("cpu_format") = false)
+      .def("write_kiv", [](const PyResult& p, const std::string& path) { write_kiv_results(path, p.r.entries); },
+           py::arg("path"), "The results as the reference's 40-B KeyIntValuePair records.")
       .def_property_readonly("num_lines", [](const PyResult& p) { return p.r.num_lines; })
       .def_property_readonly("num_tokens", [](const PyResult& p) { return p.r.num_tokens; })
       .def_property_readonly("num_unique", [](const PyResult& p) { return p.r.num_unique; })
@@ -574,7 +576,8 @@ PYBIND11_MODULE(_locust, m) {
     return std::vector<u64>(k.w, k.w + kKeyWords);
   });
   m.def("write_spill",
-        [](const std::string& path, const std::vector<std::pair<std::string, u64>>& recs, bool binary) {
+        [](const std::string& path, const std::vector<std::pair<std::string, u64>>& recs,
+           const std::string& fmt) {
           std::vector<KeyCount> v;
           for (const auto& r : recs) {
             KeyCount kc{};
@@ -583,8 +586,16 @@ PYBIND11_MODULE(_locust, m) {
             kc.count = r.second;
             v.push_back(kc);
           }
-          write_spill(path, v, binary ? SpillFormat::kBinary : SpillFormat::kText);
-        });
+          write_spill(path, v, fmt == "binary" ? SpillFormat::kBinary
+                               : fmt == "kiv"  ? SpillFormat::kKiv
+                                               : SpillFormat::kText);
+        }, py::arg("path"), py::arg("recs"), py::arg("fmt") = "text");
+  m.def("read_kiv", [](const std::string& path) {
+    py::list out;
+    for (const auto& r : read_kiv(path))
+      out.append(py::make_tuple(py::bytes(key_to_string(r.key)), r.value, r.count));
+    return out;
+  }, py::arg("path"), "KeyIntValuePair records of a kiv file: (key, value, count).");
   m.def("read_spill", [](const std::string& path) {
     py::list out;
     for (const auto& r : read_spill(path)) {
