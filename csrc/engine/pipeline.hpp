@@ -922,8 +922,8 @@ struct DevicePipeline {
   }
   // The same when the sorted output is device KeyCount records (the distributed map): one
   // D2H of them, only when a rebuild is due.
-  void maybe_retune_records(const KeyCount* d_recs, u64 n) {
-    const u64 mx = retune_wanted();
+  void maybe_retune_records(const KeyCount* d_recs, u64 n, bool force = false) {
+    const u64 mx = force ? ~0ull / 8 : retune_wanted();
     if (!mx || !n) return;
     std::vector<KeyCount> h(n);
     LOCUST_HIP_CHECK(hipMemcpyAsync(h.data(), d_recs, n * sizeof(KeyCount), hipMemcpyDeviceToHost,
@@ -961,6 +961,11 @@ struct DevicePipeline {
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
                         lb_dict, stream, ord_trace(), ex);
+    static const bool twice = std::getenv("LOCUST_ORD_TWICE") != nullptr;  // diagnostics only
+    if (twice)
+      launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
+                          cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
+                          lb_dict, stream, ord_trace(), ex);
   }
   // Diagnostics: LOCUST_ORD_TRACE=1 prints the ordered kernel's per-partition phase times
   // (shader clock ticks) after each run.
@@ -969,8 +974,8 @@ struct DevicePipeline {
     static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
     if (!on) return nullptr;
     if (!d_ord_trace) {
-      LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 16 * sizeof(u64)));
-      LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 16 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 32 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 32 * sizeof(u64)));
     }
     return d_ord_trace;
   }
@@ -1068,7 +1073,7 @@ struct DevicePipeline {
   }
   void print_ord_trace() {
     if (!d_ord_trace) return;
-    std::vector<u64> t(kDictParts * 16);
+    std::vector<u64> t(kDictParts * 32);
     LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
     // stamps: 0 start, 1 built, 2 published, 8 histogram, 7 bucketed, 9 ranked, 3 sorted,
     // 4 prefix known, 5 written; 6 = distinct keys; 10 / 11 = entry / exit on the 100 MHz
@@ -1076,7 +1081,7 @@ struct DevicePipeline {
     u64 first_in = ~0ull, last_out = 0;
     int last_p = -1;
     for (int p = 0; p < kDictParts; ++p) {
-      const u64* x = &t[p * 16];
+      const u64* x = &t[p * 32];
       if (!x[10]) continue;
       first_in = std::min(first_in, x[10]);
       if (x[11] > last_out) {
@@ -1086,18 +1091,18 @@ struct DevicePipeline {
     }
     if (last_p >= 0)
       std::fprintf(stderr, "ord span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
-                   (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 16 + 6]);
+                   (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 32 + 6]);
     for (int p = 0; p < kDictParts; ++p) {
-      const u64* x = &t[p * 16];
+      const u64* x = &t[p * 32];
       if (!x[0] || !x[6]) continue;
       auto d = [&](int a, int b) { return (unsigned long long)(x[a] && x[b] ? x[b] - x[a] : 0); };
       std::fprintf(stderr,
                    "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
                    " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
-                   " | clear=%5llu list=%5llu gather=%5llu\n",
+                   " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu ranks=%6llu\n",
                    p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
                    d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
-                   (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13));
+                   (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 16));
     }
   }
   // The last enqueue_dict_job's kernels re-zero the scratch they dirty (small ordered

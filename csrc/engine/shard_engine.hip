@@ -48,14 +48,19 @@ class GpuShardEngine final : public ShardEngine {
       stream_chunks_ = m.enqueue_stream_insert(shard);
     } else if (!small_ordered) {
       m.check_input(shard);
+      // a large dictionary pass maps in upload pieces with per-tile combining
+      m.combine_map = combine && cfg_.sort_path == SortPath::kDict && m.large_ordered;
       m.enqueue_upload(shard);
       m.enqueue_map(shard);
+      m.combine_map = false;
     }
     if (small_ordered) {
       enqueue_small_ordered(shard, plan != DistStrategy::kGather, nullptr, 0);
       m.sync();
       return complete_small_ordered(shard);
     }
+    if (combine && cfg_.sort_path == SortPath::kDict && !streamed && m.large_ordered_ok())
+      return large_ordered_map(shard, plan);
     m.sync_clean = false;  // the paths below dirty the scratch without re-zeroing it
     if (combine && cfg_.sort_path == SortPath::kDict) {
       if (plan == DistStrategy::kGather) {
@@ -110,6 +115,63 @@ class GpuShardEngine final : public ShardEngine {
     launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
     m.read_counters();
     return finish_map_stats(shard, combine ? m.h_ctr->num_unique : m.h_ctr->num_records);
+  }
+
+  // Large pass (past kPartBuildMaxTokens, mapped above with the partition table): the
+  // two-kernel ordered build writes this rank's sorted distinct keys straight into the
+  // shuffle records and the SoA keys + counts the exchange reads; ONE host sync.  A table
+  // overflow (e.g. the first job, on the first-byte map) redoes the pass on the HBM table
+  // and retunes the map from its output.
+  u64 large_ordered_map(const TextInput& shard, DistStrategy plan) {
+    DevicePipeline& m = *mp_;
+    const bool weighted = m.map_combined;
+    launch_dict_partials(m.tokens, weighted ? m.d_counts : nullptr, m.d_part_off, m.part_tiles,
+                         m.cap, m.d_partials, m.d_partial_n, m.stream, m.partials_trace());
+    OrderedExtra ex;
+    ex.pm = m.part_map();
+    ex.part_w = m.d_pw;
+    ex.recs = m.d_records;
+    ex.sorted = m.sorted;
+    ex.counts = m.d_sorted_counts;
+    launch_dict_ordered_partials(m.d_partials, m.d_partial_n, m.d_ctr, nullptr, m.d_ctr_mapped,
+                                 m.lb_dict, m.stream, nullptr, ex);
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    const bool spec = plan != DistStrategy::kGather;
+    if (spec) {
+      launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
+      LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),
+                                      hipMemcpyDeviceToHost, m.stream));
+    }
+    m.sync();
+    *m.h_ctr = *m.h_ctr_mapped;
+    if (!(m.h_ctr->flags & kCtrDictOverflow)) {
+      m.maybe_retune_records(m.d_records, m.h_ctr->num_unique);
+      if (spec) {
+        samples_.assign(m.h_small, m.h_small + kSpecSamples);
+        samples_valid_ = true;
+      }
+      return finish_map_stats(shard, m.h_ctr->num_unique);
+    }
+    LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->num_unique, 0, sizeof(u32), m.stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(&m.d_ctr->flags, 0, sizeof(u32), m.stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(m.dict.table, 0, m.dict_zero_bytes, m.stream));
+    launch_dict_insert(m.tokens, weighted ? m.d_counts : nullptr, &m.d_ctr->num_records, m.cap,
+                       m.dict, m.d_ctr, m.stream);
+    m.read_counters();
+    if (m.h_ctr->flags & kCtrDictOverflow)
+      throw Error("large map pass: more distinct keys than the dictionary holds");
+    if (m.h_ctr->num_unique <= (u32)kRankSortMax) {
+      m.enqueue_rank();
+      m.enqueue_sorted_from_dict();
+    } else {
+      radix_sort(m.dict.ukeys, &m.d_ctr->num_unique, m.h_ctr->num_unique, m.rx, m.dict.ucount,
+                 m.sorted, m.d_sorted_counts, m.d_perm, m.h_plan, m.stream);
+    }
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
+    m.read_counters();
+    m.maybe_retune_records(m.d_records, m.h_ctr->num_unique, /*force=*/true);
+    return finish_map_stats(shard, m.h_ctr->num_unique);
   }
 
   // Small pass: upload, map and the ordered kernel give this rank's distinct keys sorted,
@@ -733,7 +795,7 @@ class GpuShardEngine final : public ShardEngine {
     local_stats_ = WordCountResult();
     local_stats_.num_lines = shard.num_lines;
     m.fill_counters(local_stats_);
-    local_stats_.num_tokens = m.h_ctr->num_records;
+    local_stats_.num_tokens = m.map_combined ? m.h_ctr->map_tokens : m.h_ctr->num_records;
     if (stream_chunks_) m.stream_stats(stream_chunks_, local_stats_);
     local_count_ = n_records;
     return n_records;

@@ -40,7 +40,7 @@ struct MapCounters {
   u32 max_key_len;      // longest token seen (before truncation)
   u64 total_count;      // sum of record counts (== num_records when every count is 1)
   u32 flags;            // kCtr* status bits
-  u32 pad;
+  u32 map_tokens;       // tokens a combining map emitted (num_records counts its records)
 };
 constexpr u32 kCtrDictOverflow = 1u;  // dictionary table full: rerun on the radix path
 constexpr u32 kCtrSortOverflow = 2u;  // a psort partition held more than kPsortMax tokens

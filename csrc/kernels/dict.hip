@@ -813,7 +813,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
 #define ORD_STAMP(k_)                                                          \
-  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + (k_)] = __builtin_amdgcn_s_memtime()
+  if (trace && threadIdx.x == 0) trace[(u64)p * 32 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
   __shared__ __attribute__((aligned(16))) u32 s_list[kPartWindow];  // later: sort arrays
   __shared__ u32 s_count;
@@ -833,7 +833,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   const typename Src::Pre guess = src.prefetch(blockIdx.x);
   const u32 p = dev::acquire_tile(tile_ctr, &s_tile);
   ORD_STAMP(0);
-  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 10] = rt_entry;
+  if (trace && threadIdx.x == 0) {
+    trace[(u64)p * 32 + 10] = rt_entry;
+    trace[(u64)p * 32 + 16] = 0;
+    trace[(u64)p * 32 + 17] = ~0ull;
+  }
   const typename Src::Pre first = p == blockIdx.x ? guess : src.prefetch(p);
   // This partition's first-word range [plo, phi) (PartMap; default: first byte p).  The
   // in-partition counting sort buckets keys by the 8 bits of (w0 - plo) just below the
@@ -862,7 +866,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   __syncthreads();
   ORD_STAMP(14);  // table cleared
-  const bool full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)p * 16 : nullptr);
+  const bool full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)p * 32 : nullptr);
   ORD_STAMP(1);
   // ---- compact: dense (w0, slot) arrays in the list area ----
   u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
@@ -965,7 +969,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       }
       v = dev::wave_inclusive_scan(v);
       if (lane == 63) s_prefix = v;
+      if (trace && lane == 0) trace[(u64)p * 32 + 15] = __builtin_amdgcn_s_memtime();  // resolved
     } else if (m > 1) {
+      if (trace && dev::lane_id() == 0)  // the first ranking wave's start
+        atomicMin(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 17]),
+                  (unsigned long long)__builtin_amdgcn_s_memtime());
       const u32 items = m * div_up_u32(m, kSmallChunk);
       for (u32 e = threadIdx.x - 64; e < items; e += kPartBlock - 64) {
         const u32 chunk = e / m, i = e - chunk * m;
@@ -974,12 +982,23 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         u32 cnt = 0;
         u64 less = 0;
         bool tie = false;
-        for (u32 j = j0; j < j1; ++j) {
-          const u64 o = s_w0[j];
-          const bool lt = o < w;
-          cnt += lt ? 1u : 0u;
-          less += lt ? s_cnt[j] : 0ull;
-          tie |= o == w && j != i;
+        // 8 candidates per step, all their LDS loads in flight before any compare (a
+        // rolled loop waited one LDS round trip per candidate)
+        for (u32 j = j0; j < j1; j += 8) {
+          u64 o[8], cj[8];
+#pragma unroll
+          for (u32 k = 0; k < 8; ++k) {
+            const bool in = j + k < j1;
+            o[k] = in ? s_w0[j + k] : ~0ull;  // ~0: no key is all 0xFF bytes
+            cj[k] = in ? s_cnt[j + k] : 0ull;
+          }
+#pragma unroll
+          for (u32 k = 0; k < 8; ++k) {
+            const bool lt = o[k] < w;
+            cnt += lt ? 1u : 0u;
+            less += lt ? cj[k] : 0ull;
+            tie |= o[k] == w && j + k != i;
+          }
         }
         if (tie)  // keys sharing their first 8 bytes: order by the remaining words
           for (u32 j = j0; j < j1; ++j)
@@ -992,6 +1011,9 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
           atomicAdd(reinterpret_cast<unsigned long long*>(&s_less[i]), (unsigned long long)less);
         }
       }
+      if (trace && dev::lane_id() == 0)  // the slowest ranking wave's end
+        atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 16]),
+                  (unsigned long long)__builtin_amdgcn_s_memtime());
     }
     __syncthreads();
     pre = s_prefix;
@@ -1216,8 +1238,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   const u64 base_tok = pre >> kOrdTokShift;
   const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   ORD_STAMP(5);
-  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 6] = m;
-  if (trace && threadIdx.x == 0) trace[(u64)p * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  if (trace && threadIdx.x == 0) trace[(u64)p * 32 + 6] = m;
+  if (trace && threadIdx.x == 0) trace[(u64)p * 32 + 11] = __builtin_amdgcn_s_memrealtime();
   if (ex.part_w && threadIdx.x == 0) {  // this partition's work, for the host's retuning
     const u64 w = tok + (u64)kPartDistinctWeight * m;
     ex.part_w[p] = (u32)(w < 0xffffffffull ? w : 0xffffffffull);

@@ -381,7 +381,10 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
         if (l == 63) {
           s_pcnt[kDictParts] = inc;
           // a combining tile reserves its records (hot records + the rest) only now
-          if (combine) s_prefix = inc ? atomicAdd(&ctr->num_records, inc) : 0;
+          if (combine) {
+            s_prefix = inc ? atomicAdd(&ctr->num_records, inc) : 0;
+            if (tile_total) atomicAdd(&ctr->map_tokens, tile_total);
+          }
         }
       }
       __syncthreads();
