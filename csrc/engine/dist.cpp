@@ -43,11 +43,16 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts) {
 
 namespace {
 
-// LOCUST_SLOT_GRAPH=0 keeps the gather-slot job as separate launches (map graph, the
-// collective, merge graph) even when the communicator could be captured.
-bool slot_graph_enabled() {
+// The gather-slot job as ONE graph with the RCCL all-gather captured inside it: measured
+// at one rank (79 vs 88 us per job).  A captured collective has never run with real peers
+// (no multi-GPU box in development), so with several ranks the default is the separate
+// launches (map graph, the collective on the stream, merge graph) -- the conventional RCCL
+// use.  LOCUST_SLOT_GRAPH=1 captures at any world size, =0 never.
+bool slot_graph_enabled(int world) {
   const char* v = std::getenv("LOCUST_SLOT_GRAPH");
-  return !(v && v[0] == '0');
+  if (v && v[0] == '0') return false;
+  if (v && v[0] == '1') return true;
+  return world == 1;
 }
 
 // LOCUST_EXCHANGE=0 keeps every shuffle job on the host-staged path.
@@ -189,7 +194,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     // One graph for the whole job when the collective can be captured (RCCL); every rank
     // enters the all-gather exactly once either way.
     bool fused = false;
-    if (comm.graph_capturable() && slot_graph_enabled()) {
+    if (comm.graph_capturable() && slot_graph_enabled(P)) {
       // `entered`: the all-gather was issued directly (uncaptured run) -- this rank is in
       // the collective sequence whatever happens next.  A capture only records it; a
       // refused capture runs the same work uncaptured, so a call made while capturing

@@ -961,11 +961,6 @@ struct DevicePipeline {
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
                         lb_dict, stream, ord_trace(), ex);
-    static const bool twice = std::getenv("LOCUST_ORD_TWICE") != nullptr;  // diagnostics only
-    if (twice)
-      launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
-                          cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
-                          lb_dict, stream, ord_trace(), ex);
   }
   // Diagnostics: LOCUST_ORD_TRACE=1 prints the ordered kernel's per-partition phase times
   // (shader clock ticks) after each run.
