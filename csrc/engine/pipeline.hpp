@@ -1094,10 +1094,10 @@ struct DevicePipeline {
       std::fprintf(stderr,
                    "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
                    " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
-                   " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu ranks=%6llu\n",
+                   " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu\n",
                    p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
                    d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
-                   (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 16));
+                   (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16));
     }
   }
   // The last enqueue_dict_job's kernels re-zero the scratch they dirty (small ordered

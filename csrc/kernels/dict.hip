@@ -418,7 +418,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
 constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
 constexpr u32 kRankChunk = 8;                  // candidates per rank work item
 constexpr u32 kSmallRank = 256;                // partitions up to here: all-pairs ranks
-constexpr u32 kSmallChunk = 32;                // candidates per small-rank work item
 __device__ __forceinline__ u32 div_up_u32(u32 a, u32 b) { return (a + b - 1) / b; }
 constexpr int kOrdOvfShift = 20;
 constexpr int kOrdTokShift = 29;
@@ -837,6 +836,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     trace[(u64)p * 32 + 10] = rt_entry;
     trace[(u64)p * 32 + 16] = 0;
     trace[(u64)p * 32 + 17] = ~0ull;
+    trace[(u64)p * 32 + 18] = 0;
+    trace[(u64)p * 32 + 19] = 0;
   }
   const typename Src::Pre first = p == blockIdx.x ? guess : src.prefetch(p);
   // This partition's first-word range [plo, phi) (PartMap; default: first byte p).  The
@@ -888,6 +889,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   u32* s_rk = s_list + 3 * kPartSlots + 2 * kSmallRank;         // [kSmallRank] ranks
   u64* s_less = reinterpret_cast<u64*>(s_rk + kSmallRank);       // [kSmallRank] vals
   u64* s_out = s_less + kSmallRank;                              // [6 x kSmallRank] records
+  u64* s_k123 = s_out + 6 * kSmallRank;                          // [3 x kSmallRank] words 1-3
   {
     const u64 b0 = dev::ballot(mine >= 1), b1 = dev::ballot(mine >= 2);
     const u64 wfull = dev::ballot(full);
@@ -906,7 +908,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       if (s_tab[slot].w[0]) {
         s_w0[d] = s_tab[slot].w[0];
         s_slot[d] = slot;
-        if (d < kSmallRank) s_cnt[d] = s_tab[slot].count;
+        if (d < kSmallRank) {
+          s_cnt[d] = s_tab[slot].count;
+#pragma unroll
+          for (int j = 1; j < kKeyWords; ++j) s_k123[3 * d + j - 1] = s_tab[slot].w[j] ^ kWordMagic;
+        }
         ++d;
       }
     }
@@ -929,11 +935,10 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   ORD_STAMP(2);
   u64 pre = 0;
   if (small) {
-    // ---- small partition: weighted all-pairs ranks.  Work item = (key i, chunk of
-    // kSmallChunk candidates j); rank_i += #{j < i}, val_i += sum of their counts -- the
-    // sorted position AND the reference's val (start of the key's run) in one pass, no
-    // bucket sort, no count scan.  Consecutive lanes take consecutive keys of one chunk,
-    // so candidate reads are LDS broadcasts.  Wave 0 resolves the look-back meanwhile. ----
+    // ---- small partition: weighted all-pairs ranks: rank_i = #{j : key_j < key_i},
+    // val_i += the counts of those keys -- the sorted position AND the reference's val
+    // (start of the key's run) in one pass, no bucket sort, no count scan.  Wave 0
+    // resolves the look-back meanwhile. ----
     if (dev::wave_id() == 0) {
       // Look-back in ONE round trip: wave 0 reads every predecessor's status word at once
       // (4 per lane, p < 256) instead of walking back 64 words per dependent round trip
@@ -974,39 +979,51 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       if (trace && dev::lane_id() == 0)  // the first ranking wave's start
         atomicMin(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 17]),
                   (unsigned long long)__builtin_amdgcn_s_memtime());
-      const u32 items = m * div_up_u32(m, kSmallChunk);
-      for (u32 e = threadIdx.x - 64; e < items; e += kPartBlock - 64) {
-        const u32 chunk = e / m, i = e - chunk * m;
-        const u64 w = s_w0[i];
-        const u32 j0 = chunk * kSmallChunk, j1 = min(j0 + kSmallChunk, m);
+      // Waves 1..15 split the work as (key group of 64, candidate slice): lane i of its
+      // group compares its full key with every candidate of the slice -- the candidates'
+      // words are LDS broadcasts, four in flight -- and the partial rank / weighted val
+      // go to LDS with one atomic each.  Full-key compares: no tie pass.
+      const u32 G = (m + 63) / 64;                 // key groups (m <= kSmallRank = 256)
+      const u32 S = (u32)(kPartBlock / 64 - 1) / G;  // candidate slices per group (>= 3)
+      const u32 wv = (u32)dev::wave_id() - 1u, g = wv % G, sl = wv / G;
+      if (sl < S) {
+        const u32 i = g * 64 + (u32)dev::lane_id();
+        const bool own = i < m;
+        u64 k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+        if (own) {
+          k0 = s_w0[i];
+          k1 = s_k123[3 * i];
+          k2 = s_k123[3 * i + 1];
+          k3 = s_k123[3 * i + 2];
+        }
+        const u32 j0 = sl * m / S, j1 = (sl + 1) * m / S;
         u32 cnt = 0;
         u64 less = 0;
-        bool tie = false;
-        // 8 candidates per step, all their LDS loads in flight before any compare (a
-        // rolled loop waited one LDS round trip per candidate)
-        for (u32 j = j0; j < j1; j += 8) {
-          u64 o[8], cj[8];
+        for (u32 j = j0; j < j1; j += 4) {
+          u64 c0[4], c1[4], c2[4], c3[4], cc[4];
 #pragma unroll
-          for (u32 k = 0; k < 8; ++k) {
-            const bool in = j + k < j1;
-            o[k] = in ? s_w0[j + k] : ~0ull;  // ~0: no key is all 0xFF bytes
-            cj[k] = in ? s_cnt[j + k] : 0ull;
+          for (u32 q = 0; q < 4; ++q) {
+            const bool in = j + q < j1;
+            const u32 jj = in ? j + q : j0;
+            c0[q] = s_w0[jj];
+            c1[q] = s_k123[3 * jj];
+            c2[q] = s_k123[3 * jj + 1];
+            c3[q] = s_k123[3 * jj + 2];
+            cc[q] = in ? s_cnt[jj] : 0ull;
           }
 #pragma unroll
-          for (u32 k = 0; k < 8; ++k) {
-            const bool lt = o[k] < w;
+          for (u32 q = 0; q < 4; ++q) {
+            const bool lt = j + q < j1 &&
+                            (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
+                             (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
             cnt += lt ? 1u : 0u;
-            less += lt ? cj[k] : 0ull;
-            tie |= o[k] == w && j + k != i;
+            less += lt ? cc[q] : 0ull;
           }
         }
-        if (tie)  // keys sharing their first 8 bytes: order by the remaining words
-          for (u32 j = j0; j < j1; ++j)
-            if (j != i && s_w0[j] == w && ord_greater(w, s_slot[i], w, s_slot[j], s_tab)) {
-              ++cnt;
-              less += s_cnt[j];
-            }
-        if (cnt) {
+        if (trace)
+          atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 18]),
+                    (unsigned long long)__builtin_amdgcn_s_memtime());
+        if (own && cnt) {
           atomicAdd(&s_rk[i], cnt);
           atomicAdd(reinterpret_cast<unsigned long long*>(&s_less[i]), (unsigned long long)less);
         }
