@@ -87,17 +87,24 @@ struct DevicePipeline {
   bool large_ordered = false;
   KeyCount* d_partials = nullptr;
   u32* d_partial_n = nullptr;
+  u32 partial_slots_cap = 0;  // slots per partition d_partials holds
+  // Slots per partition of the current pass's partials; nonzero: the piecewise map
+  // already aggregated each piece into its own slot (enqueue_partials adds nothing).
+  u32 partial_nslots = 0;
   // Large single-pass inputs travel in line-aligned pieces on the copy stream, each mapped
-  // as soon as it lands (the H2D overlaps the map); set by prepare_upload.
+  // and aggregated as soon as it lands (the H2D overlaps map + partials); set by
+  // prepare_upload.  At least kPieceBytes each, at most partial_slots_cap of them.
   static constexpr u64 kPieceBytes = 4ull << 20;
-  static constexpr u64 kMaxPieces = 256;
+  static constexpr u64 kMaxPieces = kMaxPartialSlots;
   std::vector<std::pair<u64, u64>> pieces;
   // run() opts a large dictionary pass into the combining map (records + d_counts);
   // map_combined: the current `tokens` came from it (consumers must weigh by d_counts).
   bool combine_map = false;
   bool map_combined = false;
   std::vector<hipEvent_t> ev_piece;
+  std::vector<hipEvent_t> ev_mapped;  // piece k's map done (its partials may start)
   hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_pdone = nullptr;      // the last piece's partials done
   OutRecord* d_out = nullptr;
   KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
   // Records d_records holds (>= cap; at least one minimum-size gather slot).
@@ -134,6 +141,12 @@ struct DevicePipeline {
   char* d_text_alt = nullptr;        // second device text buffer (double buffering)
   char* h_stage[2] = {nullptr, nullptr};  // pinned staging halves for pageable inputs
   hipStream_t cstream = nullptr;     // H2D copy stream
+  // Second copy stream for upload pieces: back-to-back copies on one stream leave the link
+  // idle between commands (measured 43 GB/s for 4 MiB pieces on one stream, 52 GB/s
+  // alternating over two -- the single-copy rate)
+  hipStream_t cstream2 = nullptr;
+  // Per-piece partials run here, beside the next piece's map on `stream`.
+  hipStream_t pstream = nullptr;
   hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
   MapCounters* d_dctr = nullptr;     // dictionary counters that persist across chunks
   MapCounters* h_chunk_ctr = nullptr;  // pinned per-chunk map counter snapshots
@@ -230,7 +243,10 @@ struct DevicePipeline {
       large_ordered = cap > kPartBuildMaxTokens;
     }
     if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartTable);
-    const u64 partial_slots = large_ordered ? (u64)kDictParts * kOrdWorkers : 0;
+    partial_slots_cap = large_ordered ? (u32)std::clamp<u64>(div_up(cap_bytes, kPieceBytes) + 3,
+                                                             kOrdWorkers, kMaxPartialSlots)
+                                      : 0u;
+    const u64 partial_slots = (u64)kDictParts * partial_slots_cap;
     if (partial_slots) {
       sz.add<KeyCount>(partial_slots * kPartSlotsHost);
       sz.add<u32>(partial_slots);
@@ -371,6 +387,8 @@ struct DevicePipeline {
     if (d_partials_trace) (void)hipFree(d_partials_trace);
     if (d_map_trace) (void)hipFree(d_map_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
+    if (cstream2) (void)hipStreamSynchronize(cstream2);
+    if (pstream) (void)hipStreamSynchronize(pstream);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (int b = 0; b < 2; ++b) {
@@ -381,6 +399,10 @@ struct DevicePipeline {
     for (auto e : ev_piece) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (cstream) (void)hipStreamDestroy(cstream);
+    if (cstream2) (void)hipStreamDestroy(cstream2);
+    if (pstream) (void)hipStreamDestroy(pstream);
+    for (auto e : ev_mapped) (void)hipEventDestroy(e);
+    if (ev_pdone) (void)hipEventDestroy(ev_pdone);
     if (d_text_alt) (void)hipFree(d_text_alt);
     if (d_dctr) (void)hipFree(d_dctr);
     if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
@@ -512,9 +534,21 @@ struct DevicePipeline {
   // Line-aligned pieces of a large single-pass input (none: one copy, one map launch).
   void plan_pieces(const TextInput& in) {
     if (cfg.map_path != MapPath::kFast || !large_ordered || in.bytes < 2 * kPieceBytes) return;
+    const u64 npieces = std::min<u64>(partial_slots_cap, kMaxPieces);
+    const u64 piece = std::max<u64>(kPieceBytes, div_up(in.bytes, npieces > 3 ? npieces - 3 : 1));
     u64 pos = 0;
-    while (pos < in.bytes && pieces.size() < kMaxPieces) {
-      u64 end = std::min<u64>(pos + kPieceBytes, in.bytes);
+    while (pos < in.bytes && pieces.size() < npieces) {
+      // Short first pieces start the map early, a short last piece keeps the work after
+      // the final copy small: P/4, P/2, P, ..., P, (rest - P/4), P/4.  The last piece
+      // allowed takes the rest (line alignment shortens the others).
+      const u64 rest = in.bytes - pos;
+      u64 want = piece;
+      if (pieces.size() == 0) want = piece / 4;
+      else if (pieces.size() == 1) want = piece / 2;
+      else if (rest <= piece / 4 + piece / 8) want = rest;
+      else if (rest <= piece + piece / 4) want = rest - piece / 4;
+      want = std::min(want, rest);
+      u64 end = pieces.size() + 1 == npieces ? in.bytes : pos + want;
       if (end < in.bytes) {
         const void* nl = memrchr(in.data + pos, '\n', (size_t)(end - pos));
         if (!nl) {  // a line longer than a piece: no pieces at all
@@ -535,11 +569,16 @@ struct DevicePipeline {
   }
   void ensure_piece_events(size_t n) {
     if (!cstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    if (!cstream2) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream2, hipStreamNonBlocking));
     if (!ev_fork) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    if (!pstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
+    if (!ev_pdone) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_pdone, hipEventDisableTiming));
     while (ev_piece.size() < n) {
       hipEvent_t e;
       LOCUST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       ev_piece.push_back(e);
+      LOCUST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev_mapped.push_back(e);
     }
   }
   // Device half (capturable): the DMA if any, then the per-run reset of counters and
@@ -679,6 +718,7 @@ struct DevicePipeline {
 
   void enqueue_map(const TextInput& in) {
     parts_ready = cfg.map_path == MapPath::kFast;
+    partial_nslots = 0;
     // combining needs the 4 KiB grouped map: upload pieces, or one launch past kMapLargeInput
     map_combined = combine_map && large_ordered && cfg.map_path == MapPath::kFast &&
                    (!pieces.empty() ? piece_tiles() > 0
@@ -696,19 +736,37 @@ struct DevicePipeline {
       const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
       LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
       LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream2, ev_fork, 0));
+      // a combining large pass (run() / the shard engine take the two-kernel ordered build
+      // next): aggregate each piece right after its map, into slot k
+      const bool agg = map_combined && large_ordered_ok() && pieces.size() <= partial_slots_cap;
       u64 tile_off = 0;
       for (size_t k = 0; k < pieces.size(); ++k) {
         const u64 off = pieces[k].first, len = pieces[k].second;
-        LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cstream));
+        hipStream_t cs = (k & 1) ? cstream2 : cstream;
+        LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
         if (k + 1 == pieces.size())
-          LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, cstream));
-        LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cstream));
+          LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, cs));
+        LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_piece[k], 0));
         launch_map_fast(d_text + off, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, d_parts,
-                        cap, d_ctr, lb_map, stream, nullptr,
+                        cap, d_ctr, lb_map, stream, map_trace(),
                         part_tiles ? d_part_off + tile_off * kPartTable : nullptr, part_map(),
                         /*large_tiles=*/true, map_combined ? d_counts : nullptr);
-        tile_off += div_up(len, kMapTileBytesLarge);
+        const u64 t1 = tile_off + div_up(len, kMapTileBytesLarge);
+        if (agg) {  // beside the next piece's map
+          LOCUST_HIP_CHECK(hipEventRecord(ev_mapped[k], stream));
+          LOCUST_HIP_CHECK(hipStreamWaitEvent(pstream, ev_mapped[k], 0));
+          launch_dict_partials(tokens, d_counts, d_part_off, (u32)tile_off, (u32)t1, 1, (u32)k,
+                               (u32)pieces.size(), cap, d_partials, d_partial_n, pstream,
+                               partials_trace());
+        }
+        tile_off = t1;
+      }
+      if (agg) {
+        partial_nslots = (u32)pieces.size();
+        LOCUST_HIP_CHECK(hipEventRecord(ev_pdone, pstream));
+        LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_pdone, 0));
       }
     } else {
       part_tiles = table_tiles(in.bytes);
@@ -860,6 +918,15 @@ struct DevicePipeline {
   bool large_ordered_ok() const {
     return large_ordered && parts_ready && part_tiles > 0 && cap > kPartBuildMaxTokens;
   }
+  // Its first kernel: the partials of kOrdWorkers tile slices, unless the piecewise map
+  // already wrote one slot per piece (partial_nslots).
+  void enqueue_partials() {
+    if (partial_nslots) return;
+    partial_nslots = kOrdWorkers;
+    launch_dict_partials(tokens, map_combined ? d_counts : nullptr, d_part_off, 0, part_tiles,
+                         kOrdWorkers, 0, kOrdWorkers, cap, d_partials, d_partial_n, stream,
+                         partials_trace());
+  }
   // Tiles of the per-tile partition table the fast map writes for an input of `bytes`
   // (0: no table for this input).
   u32 table_tiles(u64 bytes) const {
@@ -997,9 +1064,9 @@ struct DevicePipeline {
       const u64* x = &t[i * 8];
       if (!x[0] || !x[5]) continue;
       std::fprintf(stderr, "map tile=%4d entry=%6.2f acquired=%6.2f staged=%6.2f masks=%6.2f "
-                   "prefix=%6.2f done=%6.2f us\n", i, (x[0] - t0) * 0.01, (x[1] - t0) * 0.01,
-                   (x[2] - t0) * 0.01, (x[3] - t0) * 0.01, (x[4] - t0) * 0.01,
-                   (x[5] - t0) * 0.01);
+                   "prefix=%6.2f reserved=%6.2f done=%6.2f us\n", i, (x[0] - t0) * 0.01,
+                   (x[1] - t0) * 0.01, (x[2] - t0) * 0.01, (x[3] - t0) * 0.01,
+                   (x[4] - t0) * 0.01, x[6] ? (x[6] - t0) * 0.01 : 0.0, (x[5] - t0) * 0.01);
     }
   }
   // LOCUST_ORD_TRACE=1 on a large pass: the partials kernel's per-workgroup timeline.
@@ -1008,16 +1075,17 @@ struct DevicePipeline {
     static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
     if (!on) return nullptr;
     if (!d_partials_trace) {
-      LOCUST_HIP_CHECK(hipMalloc(&d_partials_trace, (u64)kDictParts * kOrdWorkers * 8 * sizeof(u64)));
-      LOCUST_HIP_CHECK(hipMemset(d_partials_trace, 0, (u64)kDictParts * kOrdWorkers * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMalloc(&d_partials_trace, (u64)kDictParts * kMaxPartialSlots * 8 * sizeof(u64)));
+      LOCUST_HIP_CHECK(hipMemset(d_partials_trace, 0, (u64)kDictParts * kMaxPartialSlots * 8 * sizeof(u64)));
     }
     return d_partials_trace;
   }
   void print_partials_trace() {
     if (!d_partials_trace) return;
-    const u64 nb = (u64)kDictParts * kOrdWorkers;
-    std::vector<u64> t(nb * 8);
+    const u64 ns = std::max<u32>(partial_nslots, 1), nb = (u64)kDictParts * ns;
+    std::vector<u64> t(nb * 8);  // slot b = p * ns + k
     LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_partials_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    LOCUST_HIP_CHECK(hipMemset(d_partials_trace, 0, t.size() * 8));
     u64 t0 = ~0ull, t1 = 0, tok = 0;
     for (u64 b = 0; b < nb; ++b) {
       if (!t[b * 8]) continue;
@@ -1032,7 +1100,7 @@ struct DevicePipeline {
       if (!x[0]) continue;
       std::fprintf(stderr, "partials b=%4llu p=%3llu k=%llu in=%7.2f clear=%6.2f insert=%7.2f "
                    "out=%7.2f tok=%7llu distinct=%5llu\n", (unsigned long long)b,
-                   (unsigned long long)(b % kDictParts), (unsigned long long)(b / kDictParts),
+                   (unsigned long long)(b / ns), (unsigned long long)(b % ns),
                    (x[0] - t0) * 0.01, (x[1] - x[0]) * 0.01, (x[2] - x[1]) * 0.01,
                    (x[3] - t0) * 0.01, (unsigned long long)x[4], (unsigned long long)x[5]);
     }
@@ -1115,14 +1183,14 @@ struct DevicePipeline {
     }
     if (!compat && !with_counts && large_ordered_ok()) {
       // large pass: per-slice partials (Process), then merge + sort + records (Reduce)
-      launch_dict_partials(tokens, map_combined ? d_counts : nullptr, d_part_off, part_tiles, cap,
-                           d_partials, d_partial_n, stream, partials_trace());
+      enqueue_partials();
       if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
       OrderedExtra ex;
       ex.pm = part_map();
       ex.part_w = d_pw;
       ex.out_cap = h_out_cap;
-      launch_dict_ordered_partials(d_partials, d_partial_n, d_ctr, d_out_mapped, d_ctr_mapped,
+      launch_dict_ordered_partials(d_partials, d_partial_n, partial_nslots, d_ctr, d_out_mapped,
+                                   d_ctr_mapped,
                                    lb_dict, stream, ord_trace(), ex);
       return true;
     }

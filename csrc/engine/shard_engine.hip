@@ -125,15 +125,15 @@ class GpuShardEngine final : public ShardEngine {
   u64 large_ordered_map(const TextInput& shard, DistStrategy plan) {
     DevicePipeline& m = *mp_;
     const bool weighted = m.map_combined;
-    launch_dict_partials(m.tokens, weighted ? m.d_counts : nullptr, m.d_part_off, m.part_tiles,
-                         m.cap, m.d_partials, m.d_partial_n, m.stream, m.partials_trace());
+    m.enqueue_partials();
     OrderedExtra ex;
     ex.pm = m.part_map();
     ex.part_w = m.d_pw;
     ex.recs = m.d_records;
     ex.sorted = m.sorted;
     ex.counts = m.d_sorted_counts;
-    launch_dict_ordered_partials(m.d_partials, m.d_partial_n, m.d_ctr, nullptr, m.d_ctr_mapped,
+    launch_dict_ordered_partials(m.d_partials, m.d_partial_n, m.partial_nslots, m.d_ctr, nullptr,
+                                 m.d_ctr_mapped,
                                  m.lb_dict, m.stream, nullptr, ex);
     set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
     const bool spec = plan != DistStrategy::kGather;

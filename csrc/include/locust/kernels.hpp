@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "locust/common.hpp"
 #include "locust/config.hpp"
 #include "locust/dstring.hpp"
@@ -31,8 +33,11 @@ struct ConstKeysSoA {
 };
 
 // Device-side counters written by the pipeline stages.
-struct MapCounters {
+struct alignas(8) MapCounters {
   u32 num_records;      // records to sort: emitted tokens (kv_num_map) or received records
+  // tokens a combining map emitted (num_records counts its records); shares one 64-bit
+  // word with num_records, so a combining tile updates both with a single atomic
+  u32 map_tokens;
   u32 num_unique;       // kv_num_reduce
   u32 overflow_lines;   // lines that had more than emits_per_line tokens (WARN lines)
   u32 truncated;        // tokens longer than max_key_len (truncated)
@@ -40,8 +45,9 @@ struct MapCounters {
   u32 max_key_len;      // longest token seen (before truncation)
   u64 total_count;      // sum of record counts (== num_records when every count is 1)
   u32 flags;            // kCtr* status bits
-  u32 map_tokens;       // tokens a combining map emitted (num_records counts its records)
+  u32 pad;
 };
+static_assert(offsetof(MapCounters, map_tokens) == 4, "num_records + map_tokens: one u64");
 constexpr u32 kCtrDictOverflow = 1u;  // dictionary table full: rerun on the radix path
 constexpr u32 kCtrSortOverflow = 2u;  // a psort partition held more than kPsortMax tokens
 constexpr u32 kCtrNotEmitted = 0x80000000u;  // rank_emit skipped (too many distinct keys)
@@ -283,19 +289,24 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
                          u64* trace = nullptr, const OrderedExtra& ex = OrderedExtra{});
 // Large ordered build (passes past kPartBuildMaxTokens whose map wrote a partition table,
-// dict.hip): launch_dict_partials aggregates partition p's tokens of tile slice k in
-// workgroup (p, k) and writes the distinct keys + counts to partial slot p * kOrdWorkers + k
-// (`partials`: kDictParts * kOrdWorkers * kPartSlots records, `partial_n`: one length per
-// slot, all ones if its table overflowed); launch_dict_ordered_partials merges each
-// partition's slots and finishes like launch_dict_ordered (overflow: kCtrDictOverflow).
-constexpr int kOrdWorkers = 4;
+// dict.hip): launch_dict_partials splits tiles [tile_begin, tile_end) into `nslices`
+// slices; workgroup (p, k) aggregates partition p's records of slice k and writes the
+// distinct keys + counts to partial slot p * nslots + slot_base + k (`partials`:
+// kDictParts * nslots * kPartSlotsHost records, `partial_n`: one length per slot, all ones
+// if its table overflowed).  Upload pieces each get their own slot, filled right after the
+// piece's map (the aggregation overlaps the remaining H2D).  launch_dict_ordered_partials
+// merges each partition's nslots slots and finishes like launch_dict_ordered (overflow:
+// kCtrDictOverflow).
+constexpr int kOrdWorkers = 4;         // slices of a one-launch large pass
+constexpr int kMaxPartialSlots = 32;   // slots per partition (pieces of a piecewise pass)
 constexpr int kPartSlotsHost = 2048;  // distinct keys per LDS table (dict.hip kPartSlots)
 // trace (diagnostics, optional): kDictParts * kOrdWorkers * 8 stamps (see dict.hip).
 // counts: per-record multiplicities of a combining map (null: every record is 1).
 void launch_dict_partials(ConstKeysSoA tokens, const u64* counts, const u32* part_off,
-                          u32 ntiles, u64 cap, KeyCount* partials, u32* partial_n, hipStream_t s,
+                          u32 tile_begin, u32 tile_end, u32 nslices, u32 slot_base, u32 nslots,
+                          u64 cap, KeyCount* partials, u32* partial_n, hipStream_t s,
                           u64* trace = nullptr);
-void launch_dict_ordered_partials(const KeyCount* partials, const u32* partial_n,
+void launch_dict_ordered_partials(const KeyCount* partials, const u32* partial_n, u32 nslots,
                                   MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                                   LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
                                   const OrderedExtra& ex = OrderedExtra{});

@@ -628,10 +628,10 @@ struct RunsSource {
 // the single-kernel build would give one workgroup a hot partition's hundreds of
 // thousands of tokens, so the aggregation is split in two launches.
 //  dict_partials_kernel: workgroup (p, k) aggregates partition p's tokens in the k-th of
-//    kOrdWorkers tile slices in an LDS table and writes the distinct keys with their
+//    `nslices` slices of a tile range in an LDS table and writes the distinct keys with their
 //    counts to its partial slot (KeyCount records, kPartSlots per slot) -- no global
 //    atomics, no HBM hash table, hot keys combined per wave before the LDS insert.
-//  dict_ordered_kernel<PartialsSource>: workgroup p merges its kOrdWorkers partials in LDS
+//  dict_ordered_kernel<PartialsSource>: workgroup p merges its `nslots` partials in LDS
 //    and runs the ordered kernel's sort, look-back and record output.
 // ---------------------------------------------------------------------------------
 constexpr u32 kPartialFull = 0xFFFFFFFFu;  // partial_n of a slot whose table overflowed
@@ -641,20 +641,23 @@ constexpr u32 kPartialFull = 0xFFFFFFFFu;  // partial_n of a slot whose table ov
 constexpr int kPartialBatch = 8;
 __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
     ConstKeysSoA tokens, const u64* __restrict__ counts, const u32* __restrict__ part_off,
-    u32 ntiles, u32 n_cap, KeyCount* __restrict__ partials, u32* __restrict__ partial_n,
-    u32 variant, u64* __restrict__ trace) {
-  // trace (diagnostics, LOCUST_ORD_TRACE): per workgroup b, at trace[b*8 + k] (100 MHz
-  // device clock): 0 entry, 1 table cleared, 2 inserts done, 3 exit; 4 tokens, 5 distinct
-  if (trace && threadIdx.x == 0) trace[(u64)blockIdx.x * 8] = __builtin_amdgcn_s_memrealtime();
+    u32 tile_begin, u32 tile_end, u32 nslices, u32 slot_base, u32 nslots, u32 n_cap,
+    KeyCount* __restrict__ partials, u32* __restrict__ partial_n, u32 variant,
+    u64* __restrict__ trace) {
+  // worker k of partition p: the workers of one partition are kDictParts apart in
+  // dispatch order, so a hot partition's slices land on different CUs and XCDs
+  const u32 p = blockIdx.x % kDictParts, k = blockIdx.x / kDictParts;
+  const u64 slot = (u64)p * nslots + slot_base + k;
+  // trace (diagnostics, LOCUST_ORD_TRACE): per slot, at trace[slot*8 + i] (100 MHz device
+  // clock): 0 entry, 1 table cleared, 2 inserts done, 3 exit; 4 tokens, 5 distinct
+  if (trace && threadIdx.x == 0) trace[slot * 8] = __builtin_amdgcn_s_memrealtime();
   __shared__ LdsSlot s_tab[kPartSlots];
   __shared__ u32 s_scan[kPartBlock / 64 + 1];
   __shared__ u32 s_tok;
   if (threadIdx.x == 0) s_tok = 0;
-  // worker k of partition p: the workers of one partition are kDictParts apart in
-  // dispatch order, so a hot partition's slices land on different CUs and XCDs
-  const u32 p = blockIdx.x % kDictParts, k = blockIdx.x / kDictParts;
-  const u32 t0 = (u32)((u64)ntiles * k / kOrdWorkers);
-  const u32 t1 = (u32)((u64)ntiles * (k + 1) / kOrdWorkers);
+  const u32 ntiles = tile_end - tile_begin;
+  const u32 t0 = tile_begin + (u32)((u64)ntiles * k / nslices);
+  const u32 t1 = tile_begin + (u32)((u64)ntiles * (k + 1) / nslices);
   // this thread's first run, loaded before the table clear (overlaps it)
   u32 a = 0, len = 0;
   u32 t = t0 + threadIdx.x;
@@ -668,7 +671,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
     s_tab[i].count = 0;
   }
   __syncthreads();
-  if (trace && threadIdx.x == 0) trace[(u64)blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+  if (trace && threadIdx.x == 0) trace[slot * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   bool full = false;
   u32 ntok = 0;
   // The loop trip counts are per lane; the wave keeps going while any lane has work.
@@ -734,8 +737,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   if (trace) atomicAdd(&s_tok, ntok);
   __syncthreads();  // every wave's inserts are in the table before it is read
   if (trace && threadIdx.x == 0) {
-    trace[(u64)blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-    trace[(u64)blockIdx.x * 8 + 4] = s_tok;
+    trace[slot * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+    trace[slot * 8 + 4] = s_tok;
   }
   // dense records: thread t owns slots [t * kPartPerThread, (t + 1) * kPartPerThread)
   u32 mine = 0;
@@ -744,11 +747,10 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   u32 total = 0;
   const u32 excl = dev::block_exclusive_scan<u32, kPartBlock>(mine, s_scan, &total);
   const int any_full = __syncthreads_or(full ? 1 : 0);
-  const u64 slot = (u64)p * kOrdWorkers + k;
   if (threadIdx.x == 0) partial_n[slot] = any_full ? kPartialFull : total;
   if (trace && threadIdx.x == 0) {
-    trace[(u64)blockIdx.x * 8 + 5] = total;
-    trace[(u64)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // before the writes
+    trace[slot * 8 + 5] = total;
+    trace[slot * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // before the writes
   }
   if (any_full) return;
   KeyCount* out = partials + slot * kPartSlots;
@@ -766,34 +768,35 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   }
 }
 
-// Token source of the ordered kernel after dict_partials_kernel: partition p's
-// kOrdWorkers partial slots, each a dense run of distinct keys with counts.
+// Token source of the ordered kernel after dict_partials_kernel: partition p's `nslots`
+// partial slots, each a dense run of distinct keys with counts.
 struct PartialsSource {
   const KeyCount* partials;
   const u32* partial_n;
+  u32 nslots;  // slots per partition (<= kMaxPartialSlots)
   struct Pre {};
   __device__ Pre prefetch(u32) const { return {}; }
   __device__ bool build(u32 p, Pre, LdsSlot* s_tab, u32* s_list, u32& s_count, u64*) const {
-    // s_list: [0, kOrdWorkers] exclusive prefix of the slots' lengths (full: overflow)
-    if (threadIdx.x == 0) {
-      u32 acc = 0, bad = 0;
-      for (int q = 0; q < kOrdWorkers; ++q) {
-        const u32 nq = partial_n[(u64)p * kOrdWorkers + q];
-        s_list[q] = acc;
-        if (nq == kPartialFull) bad = 1;
-        else acc += nq;
-      }
-      s_list[kOrdWorkers] = acc;
-      s_count = bad;
+    // s_list: [0, nslots] exclusive prefix of the slots' lengths (full: overflow)
+    if (dev::wave_id() == 0) {
+      const u32 q = (u32)dev::lane_id();
+      const u32 nq = q < nslots ? partial_n[(u64)p * nslots + q] : 0u;
+      const bool bad = q < nslots && nq == kPartialFull;
+      const u32 v = bad ? 0u : nq;
+      const u32 inc = dev::wave_inclusive_scan(v);
+      if (q <= nslots) s_list[q] = inc - v;
+      if (q == 0) s_count = dev::ballot(bad) ? 1u : 0u;
     }
     __syncthreads();
-    const u32 total = s_list[kOrdWorkers];
+    const u32 total = s_list[nslots];
     bool full = s_count != 0;
     if (!full) {
       for (u32 e = threadIdx.x; e < total; e += kPartBlock) {
-        u32 q = 0;
-        while (q + 1 < (u32)kOrdWorkers && s_list[q + 1] <= e) ++q;
-        const KeyCount& rec = partials[((u64)p * kOrdWorkers + q) * kPartSlots + (e - s_list[q])];
+        u32 q = 0;  // the slot holding record e: binary search of the prefix
+#pragma unroll
+        for (u32 step = 32; step; step >>= 1)
+          if (q + step < nslots && s_list[q + step] <= e) q += step;
+        const KeyCount& rec = partials[((u64)p * nslots + q) * kPartSlots + (e - s_list[q])];
         const u64 kk[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
         if (kk[0] == 0 || rec.count == 0) continue;
         full |= !part_lds_insert(s_tab, kk, rec.count, key_hash(kk));
@@ -821,6 +824,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __shared__ u64 s_prefix;
   __shared__ u32 s_cm, s_cfull;  // compaction: distinct keys, overflow flag
   __shared__ u64 s_ctok;         // compaction: tokens
+  __shared__ u64 s_wlo, s_whi;   // large partitions: first-word range of the keys present
   // partition = ticket, not blockIdx: a workgroup then only ever waits in the look-back
   // on workgroups that are already running.  With blockIdx, kernels of several processes
   // sharing the GPU (the TCP / loopback rehearsals) could fill the CUs with spinning
@@ -840,18 +844,16 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     trace[(u64)p * 32 + 19] = 0;
   }
   const typename Src::Pre first = p == blockIdx.x ? guess : src.prefetch(p);
-  // This partition's first-word range [plo, phi) (PartMap; default: first byte p).  The
-  // in-partition counting sort buckets keys by the 8 bits of (w0 - plo) just below the
-  // range's width: 256 order-preserving buckets -- the second byte for a first-byte
-  // partition, finer bytes for a narrow one ('th').
-  const u64 plo = ex.pm.lo ? ex.pm.lo[p] : (u64)p << 56;
-  const u64 phi = ex.pm.lo ? (p + 1 < (u32)kDictParts ? ex.pm.lo[p + 1] : ~0ull)
-                           : (p + 1 < (u32)kDictParts ? (u64)(p + 1) << 56 : ~0ull);
-  const u64 span = phi > plo ? phi - plo : 1ull;  // first words in the range (~0: to the end)
-  const u32 span_bits = 64u - (u32)__clzll((long long)(span - 1 | 1));
-  const u32 bshift = span_bits > 8u ? span_bits - 8u : 0u;
-  auto bucket_of = [&](u64 w0) -> u32 {  // w0 = ~0 in an open-ended range may reach 256
-    const u64 b = (w0 - plo) >> bshift;
+  // The in-partition counting sort of a large partition buckets keys by the 8 bits of
+  // (w0 - wlo) just below the width of [wlo, whi], the first words actually present: 256
+  // order-preserving buckets -- the second byte for keys sharing a first byte, finer bytes
+  // for a narrow range ('th').  (The partition map's own bounds are no substitute: the
+  // first partition starts at 0, so its keys -- all 'A...', say -- fell into 2 buckets
+  // and their all-pairs ranking ran 7x longer than any other partition's.)
+  u64 wlo = 0;
+  u32 bshift = 0;
+  auto bucket_of = [&](u64 w0) -> u32 {
+    const u64 b = (w0 - wlo) >> bshift;
     return b < 255u ? (u32)b : 255u;
   };
   for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
@@ -864,6 +866,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     s_cm = 0;
     s_ctok = 0;
     s_cfull = 0;
+    s_wlo = ~0ull;
+    s_whi = 0;
   }
   __syncthreads();
   ORD_STAMP(14);  // table cleared
@@ -1090,6 +1094,25 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   __syncthreads();
   if (!any_full && m > 1) {
+    {
+      u64 lo = ~0ull, hi = 0;
+      for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
+        const u64 w = s_w0[a];
+        lo = w < lo ? w : lo;
+        hi = w > hi ? w : hi;
+      }
+      lo = ~dev::wave_reduce_max(~lo);
+      hi = dev::wave_reduce_max(hi);
+      if (dev::lane_id() == 0) {
+        atomicMin(reinterpret_cast<unsigned long long*>(&s_wlo), (unsigned long long)lo);
+        atomicMax(reinterpret_cast<unsigned long long*>(&s_whi), (unsigned long long)hi);
+      }
+      __syncthreads();
+      wlo = s_wlo;
+      const u64 span = s_whi - wlo + 1;  // > 0: w0 = ~0 is no key
+      const u32 span_bits = 64u - (u32)__clzll((long long)(span - 1 | 1));
+      bshift = span_bits > 8u ? span_bits - 8u : 0u;
+    }
     for (u32 a = threadIdx.x; a < m; a += kPartBlock) atomicAdd(&s_hist[bucket_of(s_w0[a])], 1u);
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of 256 bucket sizes by one wave
@@ -1581,20 +1604,25 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
 }
 
 void launch_dict_partials(ConstKeysSoA tokens, const u64* counts, const u32* part_off,
-                          u32 ntiles, u64 cap, KeyCount* partials, u32* partial_n, hipStream_t s,
+                          u32 tile_begin, u32 tile_end, u32 nslices, u32 slot_base, u32 nslots,
+                          u64 cap, KeyCount* partials, u32* partial_n, hipStream_t s,
                           u64* trace) {
-  dict_partials_kernel<<<dim3(kDictParts * kOrdWorkers), dim3(kPartBlock), 0, s>>>(
-      tokens, counts, part_off, ntiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu), partials, partial_n,
+  LOCUST_CHECK_ARG(nslices >= 1 && slot_base + nslices <= nslots &&
+                       nslots <= (u32)kMaxPartialSlots && tile_begin <= tile_end,
+                   "partials: bad slot layout");
+  dict_partials_kernel<<<dim3(kDictParts * nslices), dim3(kPartBlock), 0, s>>>(
+      tokens, counts, part_off, tile_begin, tile_end, nslices, slot_base, nslots, (u32)std::min<u64>(cap, 0xFFFFFFFFu), partials, partial_n,
       std::getenv("LOCUST_ORD_VARIANT") ? (u32)std::atoi(std::getenv("LOCUST_ORD_VARIANT")) : 0u,
       trace);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
-void launch_dict_ordered_partials(const KeyCount* partials, const u32* partial_n,
+void launch_dict_ordered_partials(const KeyCount* partials, const u32* partial_n, u32 nslots,
                                   MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                                   LookbackScratch lb, hipStream_t s, u64* trace,
                                   const OrderedExtra& ex) {
-  const PartialsSource src{partials, partial_n};
+  LOCUST_CHECK_ARG(nslots >= 1 && nslots <= (u32)kMaxPartialSlots, "partials: bad slot count");
+  const PartialsSource src{partials, partial_n, nslots};
   dict_ordered_kernel<PartialsSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
       src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   LOCUST_HIP_LAUNCH_CHECK();

@@ -170,6 +170,11 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   const bool combine = kCombineTile && part_off && counts;
   // the partition map's range starts (PartMap), staged once per tile: 2 KB, searched per token
   __shared__ u64 s_plo[kDictParts + 1];
+  // grouped large tiles: each wave's token starts (LDS offset | length << 16), at most one
+  // per two bytes of its segment
+  constexpr int kListPerWave = kSteps > 1 ? kSeg / 2 : 1;
+  constexpr int kListRounds = kListPerWave / 64 > 0 ? kListPerWave / 64 : 1;
+  __shared__ u32 s_list[(kBlock / 64) * kListPerWave];
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
   // Tokens are emitted in no particular order across tiles (every consumer sorts or
@@ -336,19 +341,38 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
   }
   if constexpr (kSteps > 1) {
     if (part_off) {
-      // ---- phase 3 (grouped, large tiles): a lane emits up to kSteps tokens, so the
-      // partition ranks are drawn in a first sweep (first key word only) and the keys are
-      // packed again, in full, by a second sweep once the tile's partition offsets are
-      // known (repacking from LDS is cheaper than holding kSteps keys in registers) ----
-      constexpr u16 kCombined = 0xFFFF;  // folded into its partition's hot record
-      u16 loc[kSteps];
+      // ---- phase 3 (grouped, large tiles): a lane owns a byte, so only the ~1 in 7 lanes
+      // at a token start would work per step.  Each wave first compacts its segment's
+      // token starts into an LDS list (offset + length); two dense sweeps over the list
+      // then draw the partition ranks (first sweep) and write the keys once the tile's
+      // partition offsets are known (second sweep, keys repacked from LDS) ----
+      constexpr u32 kCombined = 0xFFFFu;  // folded into its partition's hot record
+      u32* my_list = s_list + w * kListPerWave;
+      u32 n_w = 0;
 #pragma unroll
       for (int s = 0; s < kSteps; ++s) {
-        loc[s] = 0;
-        if ((emit_mask[s] >> lane) & 1ull) {
+        const u64 m = emit_mask[s];
+        if ((m >> lane) & 1ull) {
           const u32 len = token_length(dmask[s], dmask[s + 1], lane);
+          my_list[n_w + lanes_below(m)] =
+              (u32)(seg_lds + s * 64 + lane) | ((len < 255u ? len : 255u) << 16);
+        }
+        n_w += __popcll(m);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      u32 info[kListRounds];  // partition << 16 | rank in the partition (kCombined: folded)
+#pragma unroll
+      for (int r = 0; r < kListRounds; ++r) {
+        info[r] = 0;
+        const u32 i = (u32)r * 64 + lane;
+        if ((u32)r * 64 >= n_w) break;  // wave-uniform
+        if (i < n_w) {
+          const u32 e = my_list[i];
+          const u32 len = e >> 16;
           u64 kw[kKeyWords];
-          pack_token(s_text, seg_lds + s * 64 + lane, len < (u32)max_key ? len : (u32)max_key, kw);
+          pack_token(s_text, (int)(e & 0xffffu), len < (u32)max_key ? len : (u32)max_key, kw);
           const u32 part = part_of(kw[0]);
           bool folded = false;
           if (combine && (kw[0] & 0xffull) == 0) {  // a one-word key
@@ -359,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
               folded = true;
             }
           }
-          loc[s] = folded ? kCombined : (u16)atomicAdd(&s_pcnt[part], 1u);
+          info[r] = (part << 16) | (folded ? kCombined : atomicAdd(&s_pcnt[part], 1u));
         }
       }
       __syncthreads();
@@ -380,14 +404,19 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
         s_pcnt[4 * l + 3] = ex + h0 + h1 + h2;
         if (l == 63) {
           s_pcnt[kDictParts] = inc;
-          // a combining tile reserves its records (hot records + the rest) only now
+          // a combining tile reserves its records (hot records + the rest) only now, and
+          // counts its tokens in the same atomic: (map_tokens : num_records) is one u64
+          // (same-address atomics serialise at the memory side -- one per tile, not two)
           if (combine) {
-            s_prefix = inc ? atomicAdd(&ctr->num_records, inc) : 0;
-            if (tile_total) atomicAdd(&ctr->map_tokens, tile_total);
+            const u64 add = ((u64)tile_total << 32) | inc;
+            s_prefix = add ? (u32)atomicAdd(reinterpret_cast<unsigned long long*>(&ctr->num_records),
+                                            (unsigned long long)add)
+                           : 0u;
           }
         }
       }
       __syncthreads();
+      MAP_STAMP(6);
       const u64 gprefix = combine ? s_prefix : prefix;
       for (int i = threadIdx.x; i < kPartTable; i += kBlock)
         part_off[(u64)tile * kPartTable + i] = (u32)(gprefix + s_pcnt[i]);
@@ -406,16 +435,20 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
       }
       u32 trunc = 0, maxlen = 0;
 #pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        if ((emit_mask[s] >> lane) & 1ull) {
-          const u32 len = token_length(dmask[s], dmask[s + 1], lane);
+      for (int r = 0; r < kListRounds; ++r) {
+        const u32 i = (u32)r * 64 + lane;
+        if ((u32)r * 64 >= n_w) break;  // wave-uniform
+        if (i < n_w) {
+          const u32 e = my_list[i];
+          const u32 len = e >> 16;
           if (len > (u32)max_key) ++trunc;
           maxlen = len > maxlen ? len : maxlen;
-          if (loc[s] == kCombined) continue;
+          const u32 rank = info[r] & 0xffffu;
+          if (rank == kCombined) continue;
+          const u32 part = info[r] >> 16;
           u64 kw[kKeyWords];
-          pack_token(s_text, seg_lds + s * 64 + lane, len < (u32)max_key ? len : (u32)max_key, kw);
-          const u32 part = part_of(kw[0]);
-          const u64 idx = gprefix + s_pcnt[part] + (combine && s_hotc[part] ? 1u : 0u) + loc[s];
+          pack_token(s_text, (int)(e & 0xffffu), len < (u32)max_key ? len : (u32)max_key, kw);
+          const u64 idx = gprefix + s_pcnt[part] + (combine && s_hotc[part] ? 1u : 0u) + rank;
           if (idx < out_cap) {
 #pragma unroll
             for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
