@@ -102,9 +102,7 @@ struct DevicePipeline {
   bool combine_map = false;
   bool map_combined = false;
   std::vector<hipEvent_t> ev_piece;
-  std::vector<hipEvent_t> ev_mapped;  // piece k's map done (its partials may start)
   hipEvent_t ev_fork = nullptr;
-  hipEvent_t ev_pdone = nullptr;      // the last piece's partials done
   OutRecord* d_out = nullptr;
   KeyCount* d_records = nullptr;   // shuffle payload (send on the map side, recv on reduce)
   // Records d_records holds (>= cap; at least one minimum-size gather slot).
@@ -145,8 +143,6 @@ struct DevicePipeline {
   // idle between commands (measured 43 GB/s for 4 MiB pieces on one stream, 52 GB/s
   // alternating over two -- the single-copy rate)
   hipStream_t cstream2 = nullptr;
-  // Per-piece partials run here, beside the next piece's map on `stream`.
-  hipStream_t pstream = nullptr;
   hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
   MapCounters* d_dctr = nullptr;     // dictionary counters that persist across chunks
   MapCounters* h_chunk_ctr = nullptr;  // pinned per-chunk map counter snapshots
@@ -388,7 +384,7 @@ struct DevicePipeline {
     if (d_map_trace) (void)hipFree(d_map_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     if (cstream2) (void)hipStreamSynchronize(cstream2);
-    if (pstream) (void)hipStreamSynchronize(pstream);
+
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (int b = 0; b < 2; ++b) {
@@ -400,9 +396,7 @@ struct DevicePipeline {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (cstream) (void)hipStreamDestroy(cstream);
     if (cstream2) (void)hipStreamDestroy(cstream2);
-    if (pstream) (void)hipStreamDestroy(pstream);
-    for (auto e : ev_mapped) (void)hipEventDestroy(e);
-    if (ev_pdone) (void)hipEventDestroy(ev_pdone);
+
     if (d_text_alt) (void)hipFree(d_text_alt);
     if (d_dctr) (void)hipFree(d_dctr);
     if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
@@ -456,8 +450,11 @@ struct DevicePipeline {
     if (!out_pool.empty() && out_pool[out_idx].use_count() == 1) return;
     for (size_t i = 0; i < out_pool.size(); ++i)
       if (out_pool[i].use_count() == 1) return use_out(i);
+    const u64 t0 = now_ns();
     out_pool.push_back(std::make_shared<HostOut>(h_out_cap, out_noncoherent));
     use_out(out_pool.size() - 1);
+    LOCUST_LOG_DEBUG("output buffer #%zu: %llu records, %.2f ms", out_pool.size(),
+                     (unsigned long long)h_out_cap, (now_ns() - t0) * 1e-6);
   }
   // ... with room for n records (grown when a radix-path result has more distinct keys
   // than the dictionary's capacity).
@@ -508,8 +505,13 @@ struct DevicePipeline {
   //  * pinned input elsewhere (HostText): DMA straight from it.
   //  * otherwise: host copy into the pinned buffer, then DMA.
   void enqueue_upload(const TextInput& in) {
+    const u64 t0 = now_ns();
     prepare_upload(in);
+    const u64 t1 = now_ns();
     enqueue_upload_device(in);
+    if ((int)log_level() >= (int)LogLevel::kDebug)
+      LOCUST_LOG_DEBUG("upload: mode %d, %zu pieces, host %.3f ms, enqueue %.3f ms",
+                       (int)upload_mode, pieces.size(), (t1 - t0) * 1e-6, (now_ns() - t1) * 1e-6);
   }
   // Host half: stage the text where the device half expects it and pick the map's source.
   enum class Upload { kZeroCopy, kDirect, kStaged };
@@ -571,14 +573,10 @@ struct DevicePipeline {
     if (!cstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     if (!cstream2) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream2, hipStreamNonBlocking));
     if (!ev_fork) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    if (!pstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
-    if (!ev_pdone) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_pdone, hipEventDisableTiming));
     while (ev_piece.size() < n) {
       hipEvent_t e;
       LOCUST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       ev_piece.push_back(e);
-      LOCUST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      ev_mapped.push_back(e);
     }
   }
   // Device half (capturable): the DMA if any, then the per-run reset of counters and
@@ -734,19 +732,31 @@ struct DevicePipeline {
       part_tiles = piece_tiles();
       const char* src = upload_mode == Upload::kDirect ? in.data : h_text;
       const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
-      LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
-      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
-      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream2, ev_fork, 0));
+      // The copies need no fork from `stream` outside a graph capture (nothing earlier in
+      // the job touches d_text, and the previous job ended with a host sync).  A fork made
+      // the first copy on a copy stream wait on the host for the compute queue's marker:
+      // one job in ~8 stalled 8-9 ms inside hipMemcpyAsync (measured; none without it).
+      hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+      LOCUST_HIP_CHECK(hipStreamIsCapturing(stream, &cst));
+      if (cst != hipStreamCaptureStatusNone) {
+        LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
+        LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
+        LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream2, ev_fork, 0));
+      }
       // a combining large pass (run() / the shard engine take the two-kernel ordered build
-      // next): aggregate each piece right after its map, into slot k
+      // next): aggregate each piece right after its map, into slot k -- on the same stream:
+      // beside the next map on a third stream both kernels ran ~1.6x slower and every
+      // cross-queue hand-off cost ~20 us (measured), while the copies leave room for both
       const bool agg = map_combined && large_ordered_ok() && pieces.size() <= partial_slots_cap;
+      const u64 t_enq = now_ns();
+      // the padding after the text: off the copy streams (a 16-byte fill at an unaligned
+      // address is two blit kernels there, ~15 us in front of the last piece's event)
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
       u64 tile_off = 0;
       for (size_t k = 0; k < pieces.size(); ++k) {
         const u64 off = pieces[k].first, len = pieces[k].second;
         hipStream_t cs = (k & 1) ? cstream2 : cstream;
         LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
-        if (k + 1 == pieces.size())
-          LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, cs));
         LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_piece[k], 0));
         launch_map_fast(d_text + off, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, d_parts,
@@ -754,20 +764,15 @@ struct DevicePipeline {
                         part_tiles ? d_part_off + tile_off * kPartTable : nullptr, part_map(),
                         /*large_tiles=*/true, map_combined ? d_counts : nullptr);
         const u64 t1 = tile_off + div_up(len, kMapTileBytesLarge);
-        if (agg) {  // beside the next piece's map
-          LOCUST_HIP_CHECK(hipEventRecord(ev_mapped[k], stream));
-          LOCUST_HIP_CHECK(hipStreamWaitEvent(pstream, ev_mapped[k], 0));
+        if (agg)
           launch_dict_partials(tokens, d_counts, d_part_off, (u32)tile_off, (u32)t1, 1, (u32)k,
-                               (u32)pieces.size(), cap, d_partials, d_partial_n, pstream,
+                               (u32)pieces.size(), cap, d_partials, d_partial_n, stream,
                                partials_trace());
-        }
         tile_off = t1;
       }
-      if (agg) {
-        partial_nslots = (u32)pieces.size();
-        LOCUST_HIP_CHECK(hipEventRecord(ev_pdone, pstream));
-        LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_pdone, 0));
-      }
+      if ((int)log_level() >= (int)LogLevel::kDebug)
+        LOCUST_LOG_DEBUG("piecewise map enqueued in %.3f ms", (now_ns() - t_enq) * 1e-6);
+      if (agg) partial_nslots = (u32)pieces.size();
     } else {
       part_tiles = table_tiles(in.bytes);
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
@@ -1392,11 +1397,15 @@ struct DevicePipeline {
       LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
       enqueue_map(in);
       LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+      // a piecewise pass interleaves Process (the per-piece partials) with Map: one
+      // boundary, and no marker between the last partials and the ordered kernel
+      if (!pieces.empty()) LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
     }
     if (dict_path) {
       bool ordered = graph_ordered;
       if (!graphed) {
-        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, ev[3], /*self_clean=*/true);
+        ordered = enqueue_dict_job((u32)in.num_lines, compat, false,
+                                   pieces.empty() ? ev[3] : nullptr, /*self_clean=*/true);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
       }

@@ -1058,9 +1058,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     __syncthreads();
     const u64 base_m = pre & kOrdM;
     if (((pre >> kOrdOvfShift) & 511u) == 0) {  // uniform per workgroup
-      if (out && base_m + m <= ex.out_cap) {
-        u64* dst = reinterpret_cast<u64*>(out + base_m);
-        for (u32 q = threadIdx.x; q < 6 * m; q += kPartBlock) dst[q] = s_out[q];
+      if (out && base_m + m <= ex.out_cap) {  // 16 B per lane, consecutive lanes
+        using v2u64 = u64 __attribute__((ext_vector_type(2)));
+        v2u64* dst = reinterpret_cast<v2u64*>(out + base_m);
+        const v2u64* src = reinterpret_cast<const v2u64*>(s_out);
+        for (u32 q = threadIdx.x; q < 3 * m; q += kPartBlock) dst[q] = src[q];
       }
       if (ex.recs) {  // 8-B word q of the KeyCount slice: record q / 5, word q % 5
         u64* dst = reinterpret_cast<u64*>(ex.recs + base_m);
@@ -1234,8 +1236,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     }
     __syncthreads();
     if (out && base_m + m <= ex.out_cap) {
-      // 16-B chunk q of this partition's slice: record q / 3, part q % 3
-      u64* dst = reinterpret_cast<u64*>(out + base_m);
+      // 16-B chunk q of this partition's slice: record q / 3, part q % 3, ONE 16-B store
+      // per lane (two 8-B stores at a 16-B stride left every line half written per
+      // instruction: twice the partial-line PCIe writes)
+      using v2u64 = u64 __attribute__((ext_vector_type(2)));
+      v2u64* dst = reinterpret_cast<v2u64*>(out + base_m);
       for (u32 q = threadIdx.x; q < 3 * m; q += kPartBlock) {
         const u32 i = q / 3, part = q - 3 * i;
         const LdsSlot& sl = s_tab[s_slot[i]];
@@ -1250,8 +1255,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
           a = s_val[i];
           b = sl.count;
         }
-        dst[2 * q] = a;
-        dst[2 * q + 1] = b;
+        dst[q] = v2u64{a, b};
       }
     }
     if (ex.recs) {

@@ -46,3 +46,10 @@ for name, fn in [("one 43MiB", one), ("4MiB x1", pieces(4 << 20, [s1])),
                  ("8MiB x2", pieces(8 << 20, [s1, s2]))]:
     ms = timeit(fn)
     print(f"{name:12s} {ms:.3f} ms  {N / ms / 1e6:.1f} GB/s")
+
+# D2H: one 9.7 MB copy (the synth1m output size) from device memory into pinned memory
+M = 9728 << 10
+dh = torch.empty(M, dtype=torch.uint8).pin_memory()
+dd = torch.empty(M, dtype=torch.uint8, device="cuda")
+ms = timeit(lambda: dh.copy_(dd, non_blocking=True))
+print(f"D2H 9.5MiB   {ms:.3f} ms  {M / ms / 1e6:.1f} GB/s")
