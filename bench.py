@@ -222,8 +222,9 @@ def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
     import locust_amd as lc
 
     dr.set_strategy(getattr(lc._C.DistStrategy, strategy))
-    for _ in range(warmup):
-        dr.run_loaded()
+    res = None
+    for _ in range(warmup):  # holds each result like the timed loop (steady buffer pool)
+        res, _info = dr.run_loaded()
     parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": [],
              "sent_bytes": [], "recv_bytes": []}
     infos = []
@@ -366,7 +367,8 @@ def main() -> int:
             "seq_len": nbytes,
             "parallelism": f"dp{n}" + ("" if strategy is None else
                                        f"+{args.comm}_" + {"gather": "gather_merge",
-                                                           "shuffle": "alltoallv_shuffle"}[strategy]),
+                                                           "shuffle": "alltoallv_shuffle",
+                                                           "local": "one_rank_local"}[strategy]),
         },
         "baseline_ms": round(base, 3),
         "baseline_stages_ms": baseline_stages,

@@ -110,6 +110,15 @@ struct alignas(8) Msg3 {  // after the reduce of the received key range (shuffle
   u64 total, uniq;
 };
 
+// LOCUST_DIST_LOCAL=0: one-rank kAuto jobs run the exchange with themselves too.
+static bool dist_local_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("LOCUST_DIST_LOCAL");
+    return !e || e[0] != '0';
+  }();
+  return on;
+}
+
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
                            const TextInput& shard) {
   const int P = comm.size();
@@ -176,6 +185,24 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
                                                                   : cfg.strategy;
   TraceRange tr_job("locust:dist_job");
   WordCountResult& r = res.result;
+
+  // ---------------- one rank: no exchange (kLocal) ----------------
+  LOCUST_CHECK_ARG(cfg.strategy != DistStrategy::kLocal || P == 1,
+                   "strategy 'local' is the one-rank job; use auto, gather or shuffle");
+  if (P == 1 && (cfg.strategy == DistStrategy::kAuto || cfg.strategy == DistStrategy::kLocal) &&
+      (dist_local_enabled() || cfg.strategy == DistStrategy::kLocal)) {
+    bool whole = false;
+    if (local("map", [&] { whole = eng.run_whole(shard, &r); }))
+      throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
+    if (whole) {
+      res.strategy = DistStrategy::kLocal;
+      res.local_records = r.num_unique;
+      res.range_tokens = r.num_tokens;
+      res.range_unique = r.num_unique;
+      res.total_ms = res.map_ms = (now_ns() - t0) * 1e-6;
+      return res;
+    }
+  }
 
   // ---------------- gather strategy in ONE all-gather (predicted gather) ----------------
   // map (+ slot header on the device) -> all-gather of fixed-size slots -> root merge, all

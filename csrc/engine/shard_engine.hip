@@ -29,6 +29,11 @@ class GpuShardEngine final : public ShardEngine {
 
   bool device_buffers() const override { return true; }
   void* stream() override { return mp_->stream; }
+  bool run_whole(const TextInput& shard, WordCountResult* r) override {
+    *r = mp_->run(shard);
+    mp_->sync_clean = false;  // the shard entry points reset the scratch themselves
+    return true;
+  }
   char* input_buffer() override { return mp_->h_text; }
 
   u64 map_local(const TextInput& shard, bool combine, DistStrategy plan) override {

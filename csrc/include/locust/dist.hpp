@@ -125,7 +125,11 @@ class LoopbackGroup {
   std::shared_ptr<State> state_;
 };
 
-enum class DistStrategy : int { kAuto = 0, kShuffle = 1, kGather = 2 };
+// kLocal: a one-rank job under kAuto -- there is no peer to exchange with, so the job is
+// the local device pipeline end to end (result straight into host memory), the way a
+// one-rank collective is a local copy.  Forcing kShuffle / kGather still runs the full
+// exchange machinery with one rank (the tests and the overhead measurement do).
+enum class DistStrategy : int { kAuto = 0, kShuffle = 1, kGather = 2, kLocal = 3 };
 
 // Per-rank local engine used by the distributed driver.
 class ShardEngine {
@@ -133,6 +137,9 @@ class ShardEngine {
   virtual ~ShardEngine() = default;
   virtual bool device_buffers() const = 0;
   virtual void* stream() = 0;
+  // One rank (DistStrategy::kLocal): the whole job on the local engine; false when the
+  // engine has no such path (the driver then runs the exchange with itself).
+  virtual bool run_whole(const TextInput& /*shard*/, WordCountResult* /*r*/) { return false; }
   // Pinned host staging buffer for the shard text (nullptr if the engine has none).  A
   // shard whose data already points here is uploaded without a host copy.
   virtual char* input_buffer() { return nullptr; }

@@ -230,7 +230,9 @@ py::dict dist_to_dict(const DistResult& d) {
   x["recv_bytes"] = d.recv_bytes;
   x["range_tokens"] = d.range_tokens;
   x["range_unique"] = d.range_unique;
-  x["strategy"] = d.strategy == DistStrategy::kGather ? "gather" : "shuffle";
+  x["strategy"] = d.strategy == DistStrategy::kGather  ? "gather"
+                  : d.strategy == DistStrategy::kLocal ? "local"
+                                                       : "shuffle";
   return x;
 }
 
@@ -360,7 +362,8 @@ PYBIND11_MODULE(_locust, m) {
   py::enum_<DistStrategy>(m, "DistStrategy")
       .value("auto", DistStrategy::kAuto)
       .value("shuffle", DistStrategy::kShuffle)
-      .value("gather", DistStrategy::kGather);
+      .value("gather", DistStrategy::kGather)
+      .value("local", DistStrategy::kLocal);
   py::class_<DistConfig>(m, "DistConfig")
       .def(py::init<>())
       .def_readwrite("job", &DistConfig::job)
