@@ -10,6 +10,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cstddef>
 #include <cstdio>
@@ -157,6 +158,10 @@ struct DevicePipeline {
   OutRecord* d_out_mapped = nullptr;  // device view of h_out
   MapCounters* h_ctr_mapped = nullptr;
   MapCounters* d_ctr_mapped = nullptr;
+  // Lean jobs: completion word the last kernel publishes (host-mapped) and its sequence.
+  u32* h_done = nullptr;
+  u32* d_done = nullptr;
+  u32 done_seq = 0;
   // Partition map of the ordered dictionary build (PartMap / locust/partmap.hpp): device
   // tables (persist across jobs), a pinned staging image, and the per-partition work the
   // ordered kernel reports each run (host-mapped) from which the host decides to retune.
@@ -358,6 +363,9 @@ struct DevicePipeline {
     grow_host_out(std::min<u64>(ucap, kMappedOutMax));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                    hipHostMallocMapped | hipHostMallocCoherent));
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_done, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *h_done = 0;
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_done), h_done, 0));
     LOCUST_HIP_CHECK(
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_ctr_mapped), h_ctr_mapped, 0));
     LOCUST_HIP_CHECK(hipMalloc(&d_pmap, sizeof(PartMapTables)));
@@ -404,7 +412,7 @@ struct DevicePipeline {
     if (arena.base) (void)hipFree(arena.base);
     for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_keys,
                     (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped, (void*)h_pmap,
-                    (void*)h_pw})
+                    (void*)h_pw, (void*)h_done})
       if (p) (void)hipHostFree(p);
     if (d_pmap) (void)hipFree(d_pmap);
   }
@@ -496,6 +504,20 @@ struct DevicePipeline {
       return;
     }
     LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+  }
+  // Lean jobs: the stream's last kernel publishes `seq` to h_done; poll it (bounded, then
+  // a real synchronisation -- a long job does not burn the core, a failed one reports).
+  void publish_done(u32 seq) { launch_signal_host(d_done, seq, stream); }
+  void wait_done(u32 seq) {
+    const u64 t0 = now_ns();
+    while (__atomic_load_n(h_done, __ATOMIC_ACQUIRE) != seq) {
+      if (now_ns() - t0 > 2000000) {  // 2 ms
+        sync();
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
   }
 
   // H2D of the text; zero counters and look-back scratch.
@@ -660,10 +682,26 @@ struct DevicePipeline {
   }
   bool use_job_graph(const TextInput& in) const {
     if (cfg.map_path == MapPath::kFast && large_ordered && in.bytes >= 2 * kPieceBytes) return false;
+    if (cfg.graph < 0 && lean_job(in)) return false;  // auto: lean direct launches instead
     const bool radix_ok = cfg.sort_path == SortPath::kRadix && cfg.map_path == MapPath::kFast &&
                           table_tiles(in.bytes) > 0 && radix_mapped() && psort_enabled();
     if (cfg.graph >= 0) return cfg.graph > 0 && (cfg.sort_path == SortPath::kDict || radix_ok);
     return (cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast) || radix_ok;
+  }
+  // Lean jobs: what auto mode used to replay as a graph (small single-pass dictionary jobs,
+  // device-resident radix jobs) launched directly and completed by polling a host word.
+  // Measured on the box: a 3-node graph replay + sync costs ~20 us of launch/wake-up per
+  // job, 3 direct launches + a polled completion word ~11 us (tools/micro/launch_lat.hip).
+  // LOCUST_LEAN=0: the graph replay (cfg.graph < 0) / event-timed path instead.
+  bool lean_job(const TextInput& in) const {
+    static const bool on = [] {
+      const char* e = std::getenv("LOCUST_LEAN");
+      return !e || e[0] != '0';
+    }();
+    if (!on || cfg.graph >= 0 || cfg.map_path != MapPath::kFast) return false;
+    if (large_ordered && in.bytes >= 2 * kPieceBytes) return false;
+    if (cfg.sort_path == SortPath::kDict) return true;
+    return table_tiles(in.bytes) > 0 && radix_mapped() && psort_enabled();
   }
   // Capture [upload DMA + reset, map, dictionary build, rank, emit] once per input shape
   // and source; later runs replay it with one hipGraphLaunch.
@@ -1385,9 +1423,14 @@ struct DevicePipeline {
     } clear_combine{combine_map};
     combine_map = dict_path && !compat && large_ordered;
     const bool graphed = use_job_graph(in);
+    // lean: a small single-pass job launched directly, no stage events, completion polled
+    const bool lean = !graphed && lean_job(in);
     skip_sync_reset = clean_start && dict_path && !compat;
-    LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
-    if (graphed) {
+    if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+    if (lean) {
+      enqueue_upload(in);
+      enqueue_map(in);
+    } else if (graphed) {
       prepare_upload(in);
       launch_dict_graph(in, compat);
       LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));  // a replay has no stage split
@@ -1403,7 +1446,10 @@ struct DevicePipeline {
     }
     if (dict_path) {
       bool ordered = graph_ordered;
-      if (!graphed) {
+      if (lean) {
+        ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr, /*self_clean=*/true);
+        publish_done(++done_seq);
+      } else if (!graphed) {
         ordered = enqueue_dict_job((u32)in.num_lines, compat, false,
                                    pieces.empty() ? ev[3] : nullptr, /*self_clean=*/true);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
@@ -1411,7 +1457,10 @@ struct DevicePipeline {
       }
       skip_sync_reset = false;
       const u64 t_launched = now_ns();
-      sync();  // the one host synchronisation of a dictionary run
+      if (lean)
+        wait_done(done_seq);
+      else
+        sync();  // the one host synchronisation of a dictionary run
       const u64 t_synced = now_ns();
       r.times.host_launch_ms = (t_launched - t0) * 1e-6;
       r.times.host_wait_ms = (t_synced - t_launched) * 1e-6;
@@ -1436,11 +1485,19 @@ struct DevicePipeline {
         else if (ordered) force_retune(r.entries.data(), r.entries.size());
       }
     } else {
-      if (!graphed) enqueue_radix_job((u32)in.num_lines, compat, ev[3], ev[4]);
+      if (lean)
+        enqueue_radix_job((u32)in.num_lines, compat, nullptr, nullptr);
+      else if (!graphed)
+        enqueue_radix_job((u32)in.num_lines, compat, ev[3], ev[4]);
       bool overflow;
       if (radix_mapped()) {  // records and counters already in host memory
-        if (!graphed) LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
-        sync();  // the one host synchronisation of a radix run
+        if (lean) {
+          publish_done(++done_seq);
+          wait_done(done_seq);
+        } else {
+          if (!graphed) LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+          sync();  // the one host synchronisation of a radix run
+        }
         *h_ctr = *h_ctr_mapped;
         overflow = (h_ctr->flags & kCtrSortOverflow) != 0;
         if (psort_used) print_psort_trace();
@@ -1460,14 +1517,19 @@ struct DevicePipeline {
       }
     }
     r.times.wall_ms = (now_ns() - t0) * 1e-6;
-    if (!graphed) {
-      r.times.h2d_ms = ms_between(ev[0], ev[1]);
-      r.times.map_ms = ms_between(ev[1], ev[2]);
-      r.times.process_ms = ms_between(ev[2], ev[3]);
-      r.times.reduce_ms = ms_between(ev[3], ev[4]);
-      r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    r.times.lean = lean;
+    if (lean) {  // no device timestamps: the job's wall time
+      r.times.gpu_ms = r.times.wall_ms;
+    } else {
+      if (!graphed) {
+        r.times.h2d_ms = ms_between(ev[0], ev[1]);
+        r.times.map_ms = ms_between(ev[1], ev[2]);
+        r.times.process_ms = ms_between(ev[2], ev[3]);
+        r.times.reduce_ms = ms_between(ev[3], ev[4]);
+        r.times.d2h_ms = ms_between(ev[4], ev[5]);
+      }
+      r.times.gpu_ms = ms_between(ev[0], ev[5]);
     }
-    r.times.gpu_ms = ms_between(ev[0], ev[5]);
     if (cfg.check) validate_result(r);
     return r;
   }

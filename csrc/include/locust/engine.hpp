@@ -39,6 +39,7 @@ struct StageTimes {
   // and copying the results out of the host-mapped output.
   double host_launch_ms = 0, host_wait_ms = 0, host_copy_ms = 0;
   bool graph = false;  // replayed as one hipGraph: the stage fields above are not split
+  bool lean = false;   // direct launches, polled completion: no device stage timestamps
   // Host timers placed where the reference placed them (launch-only map etc., BASELINE.md
   // "How the reference measured these"), filled when JobConfig.ref_timers is set.
   double ref_map_ms = 0, ref_process_ms = 0, ref_reduce_ms = 0;

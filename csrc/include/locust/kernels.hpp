@@ -288,6 +288,10 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
                          u64* trace = nullptr, const OrderedExtra& ex = OrderedExtra{});
+// Writes `value` to the host-mapped `word` once everything earlier on `s` has completed
+// (signal.hip; the lean job path polls it instead of synchronising the stream).
+void launch_signal_host(u32* word, u32 value, hipStream_t s);
+
 // Large ordered build (passes past kPartBuildMaxTokens whose map wrote a partition table,
 // dict.hip): launch_dict_partials splits tiles [tile_begin, tile_end) into `nslices`
 // slices; workgroup (p, k) aggregates partition p's records of slice k and writes the

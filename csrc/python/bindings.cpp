@@ -45,6 +45,7 @@ struct PyResult {
     d["ref_process_ms"] = r.times.ref_process_ms;
     d["ref_reduce_ms"] = r.times.ref_reduce_ms;
     d["graph"] = r.times.graph;
+    d["lean"] = r.times.lean;
     return d;
   }
   py::bytes format(bool cpu_format) const {
