@@ -508,11 +508,12 @@ struct DevicePipeline {
   // Lean jobs: the stream's last kernel publishes `seq` to h_done; poll it (bounded, then
   // a real synchronisation -- a long job does not burn the core, a failed one reports).
   void publish_done(u32 seq) { launch_signal_host(d_done, seq, stream); }
-  void wait_done(u32 seq) {
+  // bounded_sync=false: just return after the bound (the caller synchronises itself).
+  void wait_done(u32 seq, bool bounded_sync = true) {
     const u64 t0 = now_ns();
     while (__atomic_load_n(h_done, __ATOMIC_ACQUIRE) != seq) {
       if (now_ns() - t0 > 2000000) {  // 2 ms
-        sync();
+        if (bounded_sync) sync();
         break;
       }
       __builtin_ia32_pause();
