@@ -110,6 +110,15 @@ struct alignas(8) Msg3 {  // after the reduce of the received key range (shuffle
   u64 total, uniq;
 };
 
+// LOCUST_EXCH_ASYNC=0: the device exchange waits for a synchronised map (two host syncs).
+static bool exch_async_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("LOCUST_EXCH_ASYNC");
+    return !e || e[0] != '0';
+  }();
+  return on;
+}
+
 // LOCUST_DIST_LOCAL=0: one-rank kAuto jobs run the exchange with themselves too.
 static bool dist_local_enabled() {
   static const bool on = [] {
@@ -324,131 +333,168 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     mapped = true;
   }
 
-  const i32 st1 = mapped ? st_slot : local("map", [&] {
-    TraceRange tr("locust:map");
-    n_local = eng.map_local(shard, cfg.job.combine, plan);
-    if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
-    eng.map_stats(&local_stats);
-  });
-  if (mine_samples.size() != S) mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});
-  res.local_records = n_local;
-  const u64 t1 = now_ns();
-
   // ---------------- shuffle on the device: one host synchronisation ----------------
   // (locust/exch.hpp) every control step of the sample sort -- splitters, bucket offsets,
   // overflow and failure agreement, global val offsets -- runs in kernels between four
   // stream-ordered collectives.  Slot sizes come from the previous shuffle job, so the
-  // first one takes the host-staged path below, which sets them.
+  // first one takes the host-staged path below, which sets them.  With an asynchronous
+  // map (exch_async) even the map is not synchronised: its header and samples are built on
+  // the device in front of the first all-gather -- the whole job is ONE host sync.
   const bool exch_path =
       exch_enabled() && cfg.gather && cfg.job.combine && !mapped && plan == DistStrategy::kShuffle &&
       cfg.strategy != DistStrategy::kGather && comm.device_buffers() && eng.device_buffers() &&
       eng.exch_slot_records && eng.exch_gather_records && S == kExchSamples &&
       (cfg.strategy == DistStrategy::kShuffle || eng.exch_last_sum > cfg.gather_max_records) &&
       (u32)P <= kExchMaxRanks && (u32)P * S <= kExchMaxPlanSamples;
-  if (exch_path) {
-    TraceRange tr("locust:device_exchange");
-    ExchMsg1 h{};
-    h.status = st1;
-    h.record_flags = eng.record_flags();
-    h.n_local = st1 ? 0 : n_local;
-    h.lines = shard.num_lines;
-    h.tokens = local_stats.num_tokens;
-    h.overflow_lines = local_stats.overflow_lines;
-    h.truncated = local_stats.truncated;
-    h.max_key_len = local_stats.max_key_len;
-    if (!st1 && fault_injected(me, "exchange")) {
-      h.status = 2;  // 1: the map failed, 2: the exchange
-      local_msg = "injected fault (LOCUST_FAULT) in stage 'exchange'";
+  bool async_ok = exch_path && exch_async_enabled() && eng.exch_map_async_ok(shard);
+  i32 st1 = 0;
+  u64 t1 = 0;
+  for (;;) {  // a second round only when an asynchronous map must be redone
+    const bool exch_async = async_ok;
+    if (exch_async) {
+      st1 = local("map", [&] {
+        TraceRange tr("locust:map_async");
+        eng.exch_map_enqueue(shard, (u32)P, S);
+      });
+      mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});  // (written on the device)
+    } else {
+      st1 = mapped ? st_slot : local("map", [&] {
+        TraceRange tr("locust:map");
+        n_local = eng.map_local(shard, cfg.job.combine, plan);
+        if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
+        eng.map_stats(&local_stats);
+      });
+      if (mine_samples.size() != S) mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});
     }
-    int entered = 0;
-    ShardEngine::ExchCollectives coll;
-    coll.allgather = [&](const void* snd, void* rcv, u64 b) {
-      ++entered;
-      comm.allgather_device(snd, rcv, b, eng.stream());
-    };
-    coll.alltoall = [&](const void* snd, void* rcv, u64 b) {
-      comm.alltoall_device(snd, rcv, b, eng.stream());
-    };
-    coll.gather = [&](const void* snd, void* rcv, u64 b, int root) {
-      comm.gather_device(snd, rcv, b, root, eng.stream());
-    };
-    const i32 stx = local("shuffle", [&] { eng.enqueue_exchange(h, mine_samples, (u32)P, me, 0, coll); });
-    if (stx) {
-      // Failed after (or before) entering the collectives: peers cannot be kept in step
-      // from here; fail this rank (theirs time out and abort in their waits).
-      try {
-        comm.sync_stream(eng.stream());
-      } catch (const std::exception&) {
+    res.local_records = n_local;
+    t1 = now_ns();
+
+    if (exch_path) {
+      TraceRange tr("locust:device_exchange");
+      ExchMsg1 h{};
+      h.status = st1;
+      h.record_flags = eng.record_flags();
+      h.n_local = st1 ? 0 : n_local;
+      h.lines = shard.num_lines;
+      h.tokens = local_stats.num_tokens;
+      h.overflow_lines = local_stats.overflow_lines;
+      h.truncated = local_stats.truncated;
+      h.max_key_len = local_stats.max_key_len;
+      if (!st1 && fault_injected(me, "exchange")) {
+        h.status = 2;  // 1: the map failed, 2: the exchange
+        local_msg = "injected fault (LOCUST_FAULT) in stage 'exchange'";
       }
-      throw Error(std::string("distributed job failed in stage 'shuffle' on rank ") +
-                  std::to_string(me) + ": " + local_msg);
-    }
-    comm.sync_stream(eng.stream());
-    const ExchMsg1* H = eng.exch_headers();
-    const ExchMsg3* R = eng.exch_reports();
-    for (int p = 0; p < P; ++p)
-      if (H[p].status)
-        throw Error(std::string("distributed job failed in stage '") +
-                    (H[p].status == 2 ? "exchange" : "map") + "' on rank " +
-                    std::to_string(p) + (p == me ? ": " + local_msg : ""));
-    u32 flags = 0;
-    u64 maxb = 0, maxo = 0;
-    for (int p = 0; p < P; ++p) {
-      if (R[p].status)
-        throw Error("distributed job failed in stage 'shuffle' on rank " + std::to_string(p));
-      flags |= R[p].flags;
-      maxb = std::max<u64>(maxb, R[p].max_bucket);
-      maxo = std::max<u64>(maxo, R[p].n_out);
-    }
-    // next job's slot sizes: identical on every rank (computed from all-gathered reports)
-    if (flags & (kExchSendOverflow | kExchRecvTruncated))
-      eng.exch_slot_records = std::max(eng.exch_slot_records, exch_grow(maxb));
-    if (flags & kExchGatherOverflow)
-      eng.exch_gather_records = std::max(eng.exch_gather_records, exch_grow(maxo));
-    if (flags & kExchTooManySamples) eng.exch_slot_records = eng.exch_gather_records = 0;
-    eng.exch_last_sum = 0;
-    for (int p = 0; p < P; ++p) eng.exch_last_sum += H[p].n_local;
-    if (!flags) {
+      int entered = 0;
+      ShardEngine::ExchCollectives coll;
+      coll.allgather = [&](const void* snd, void* rcv, u64 b) {
+        ++entered;
+        comm.allgather_device(snd, rcv, b, eng.stream());
+      };
+      coll.alltoall = [&](const void* snd, void* rcv, u64 b) {
+        comm.alltoall_device(snd, rcv, b, eng.stream());
+      };
+      coll.gather = [&](const void* snd, void* rcv, u64 b, int root) {
+        comm.gather_device(snd, rcv, b, root, eng.stream());
+      };
+      const i32 stx = local("shuffle", [&] {
+        eng.enqueue_exchange(h, mine_samples, (u32)P, me, 0, coll, exch_async ? &shard : nullptr);
+      });
+      if (stx) {
+        // Failed after (or before) entering the collectives: peers cannot be kept in step
+        // from here; fail this rank (theirs time out and abort in their waits).
+        try {
+          comm.sync_stream(eng.stream());
+        } catch (const std::exception&) {
+        }
+        throw Error(std::string("distributed job failed in stage 'shuffle' on rank ") +
+                    std::to_string(me) + ": " + local_msg);
+      }
+      comm.sync_stream(eng.stream());
+      const ExchMsg1* H = eng.exch_headers();
+      const ExchMsg3* R = eng.exch_reports();
+      bool redo = false;  // an asynchronous map overflowed a partition somewhere
+      for (int p = 0; p < P; ++p) redo |= H[p].status == kExchMapRedo;
+      for (int p = 0; p < P && !redo; ++p)
+        if (H[p].status)
+          throw Error(std::string("distributed job failed in stage '") +
+                      (H[p].status == 2 ? "exchange" : "map") + "' on rank " +
+                      std::to_string(p) + (p == me ? ": " + local_msg : ""));
+      if (redo) {  // every rank saw it: map again synchronously, then exchange again
+        LOCUST_LOG_INFO("asynchronous map overflowed a partition: map again, exchange again");
+        async_ok = false;
+        continue;
+      }
+      if (exch_async &&
+          local("map", [&] {
+            n_local = eng.exch_map_complete(shard);
+            eng.map_stats(&local_stats);
+          }))
+        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
+                    std::to_string(me) + ": " + local_msg);
+      res.local_records = n_local;
+      u32 flags = 0;
+      u64 maxb = 0, maxo = 0;
       for (int p = 0; p < P; ++p) {
-        r.num_lines += H[p].lines;
-        r.num_tokens += H[p].tokens;
-        r.overflow_lines += H[p].overflow_lines;
-        r.truncated += H[p].truncated;
-        r.max_key_len = std::max<u64>(r.max_key_len, H[p].max_key_len);
+        if (R[p].status)
+          throw Error("distributed job failed in stage 'shuffle' on rank " + std::to_string(p));
+        flags |= R[p].flags;
+        maxb = std::max<u64>(maxb, R[p].max_bucket);
+        maxo = std::max<u64>(maxo, R[p].n_out);
       }
-      const u64 sb = exch_slot_bytes(eng.exch_slot_records);
-      res.sent_bytes = sb * (u64)(P - 1);
-      res.recv_bytes = sb * (u64)(P - 1);
-      res.range_tokens = R[me].total;
-      res.range_unique = R[me].n_out;
-      res.strategy = DistStrategy::kShuffle;
-      res.device_exchange = true;
-      // auto: a job small enough for the gather strategy predicts it for the next one
-      eng.last_strategy = cfg.strategy == DistStrategy::kAuto &&
-                                  eng.exch_last_sum <= cfg.gather_max_records
-                              ? DistStrategy::kGather
-                              : DistStrategy::kShuffle;
-      const u64 t2 = now_ns();
-      if (me == 0) {
-        u64 total = 0, uniq = 0;
-        if (local("reduce", [&] { eng.exch_finish_root(&total, &uniq); }))
-          throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
-        eng.finalize(0, &r.entries);
+      // next job's slot sizes: identical on every rank (computed from all-gathered reports)
+      if (flags & (kExchSendOverflow | kExchRecvTruncated))
+        eng.exch_slot_records = std::max(eng.exch_slot_records, exch_grow(maxb));
+      if (flags & kExchGatherOverflow)
+        eng.exch_gather_records = std::max(eng.exch_gather_records, exch_grow(maxo));
+      if (flags & kExchTooManySamples) eng.exch_slot_records = eng.exch_gather_records = 0;
+      eng.exch_last_sum = 0;
+      for (int p = 0; p < P; ++p) eng.exch_last_sum += H[p].n_local;
+      if (!flags) {
+        for (int p = 0; p < P; ++p) {
+          r.num_lines += H[p].lines;
+          r.num_tokens += H[p].tokens;
+          r.overflow_lines += H[p].overflow_lines;
+          r.truncated += H[p].truncated;
+          r.max_key_len = std::max<u64>(r.max_key_len, H[p].max_key_len);
+        }
+        const u64 sb = exch_slot_bytes(eng.exch_slot_records);
+        res.sent_bytes = sb * (u64)(P - 1);
+        res.recv_bytes = sb * (u64)(P - 1);
+        res.range_tokens = R[me].total;
+        res.range_unique = R[me].n_out;
+        res.strategy = DistStrategy::kShuffle;
+        res.device_exchange = true;
+        // auto: a job small enough for the gather strategy predicts it for the next one
+        eng.last_strategy = cfg.strategy == DistStrategy::kAuto &&
+                                    eng.exch_last_sum <= cfg.gather_max_records
+                                ? DistStrategy::kGather
+                                : DistStrategy::kShuffle;
+        const u64 t2 = now_ns();
+        if (me == 0) {
+          u64 total = 0, uniq = 0;
+          if (local("reduce", [&] { eng.exch_finish_root(&total, &uniq); }))
+            throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
+          eng.finalize(0, &r.entries);
+        }
+        r.num_unique = me == 0 ? r.entries.size() : R[me].n_out;
+        const u64 t3 = now_ns();
+        res.map_ms = (t1 - t0) * 1e-6;
+        res.shuffle_ms = (t2 - t1) * 1e-6;  // the whole device exchange, one synchronisation
+        res.reduce_ms = (t3 - t2) * 1e-6;
+        res.total_ms = (t3 - t0) * 1e-6;
+        r.times.map_ms = res.map_ms;
+        r.times.process_ms = res.shuffle_ms;
+        r.times.reduce_ms = res.reduce_ms;
+        r.times.wall_ms = res.total_ms;
+        return res;
       }
-      r.num_unique = me == 0 ? r.entries.size() : R[me].n_out;
-      const u64 t3 = now_ns();
-      res.map_ms = (t1 - t0) * 1e-6;
-      res.shuffle_ms = (t2 - t1) * 1e-6;  // the whole device exchange, one synchronisation
-      res.reduce_ms = (t3 - t2) * 1e-6;
-      res.total_ms = (t3 - t0) * 1e-6;
-      r.times.map_ms = res.map_ms;
-      r.times.process_ms = res.shuffle_ms;
-      r.times.reduce_ms = res.reduce_ms;
-      r.times.wall_ms = res.total_ms;
-      return res;
+      // outgrown slots: every rank saw the same reports, so all take the step-by-step path
+      LOCUST_LOG_INFO("device exchange slots outgrown (flags %u): host-staged shuffle this job", flags);
+      if (exch_async && local("map", [&] { mine_samples = eng.sample(S); }))
+        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
+                    std::to_string(me) + ": " + local_msg);
     }
-    // outgrown slots: every rank saw the same reports, so all take the step-by-step path
-    LOCUST_LOG_INFO("device exchange slots outgrown (flags %u): host-staged shuffle this job", flags);
+    break;
   }
   const u64 m1 = sizeof(Msg1) + (u64)S * sizeof(PackedKey);
   std::vector<char> out1(m1), all1(m1 * (u64)P);

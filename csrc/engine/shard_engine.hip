@@ -284,6 +284,8 @@ class GpuShardEngine final : public ShardEngine {
     set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
     launch_pack_records(local_keys_, local_counts_, local_n_, m.cap, m.d_records, m.stream);
     m.read_counters();
+    // the next pass should fit: rebuild the partition map from this one's keys
+    m.maybe_retune_records(m.d_records, m.h_ctr->num_unique, /*force=*/true);
     return finish_map_stats(shard, m.h_ctr->num_unique);
   }
 
@@ -489,24 +491,91 @@ class GpuShardEngine final : public ShardEngine {
   const SlotHeader* slot_headers() const override { return h_headers_; }
 
   // ---- device-resident shuffle (locust/exch.hpp) ----
+  // ---- one-sync shuffle: the map runs inside the exchange's enqueue ----
+  // Small ordered passes (one kernel writes the sorted records) and large piecewise passes
+  // (map + per-piece partials + merge) leave everything the exchange reads on the device.
+  bool exch_map_async_ok(const TextInput& shard) const override {
+    const DevicePipeline& m = *mp_;
+    if (cfg_.sort_path != SortPath::kDict || cfg_.map_path != MapPath::kFast) return false;
+    if (shard.bytes > m.cap_bytes || shard.num_lines > m.cap_lines) return false;
+    if (small_ordered_ok(shard, true)) return true;
+    return m.large_ordered && m.cap > kPartBuildMaxTokens && m.table_tiles(shard.bytes) > 0;
+  }
+  // Enqueues this rank's map (the sorted distinct records end in d_records / sorted keys)
+  // and its S samples into the exchange's all-gather send slot.
+  void exch_map_enqueue(const TextInput& shard, u32 P, u32 S) override {
+    ensure_exch(P, S, exch_slot_records, exch_gather_records);
+    async_combined_ = enqueue_async_map(shard);
+    if (S)
+      launch_sample_keys(local_keys_, local_n_, S,
+                         reinterpret_cast<PackedKey*>(xb_.msg1_send + sizeof(ExchMsg1)), mp_->stream);
+  }
+  // Returns whether the token count is the combining map's (map_tokens).
+  bool enqueue_async_map(const TextInput& shard) {
+    DevicePipeline& m = *mp_;
+    stream_chunks_ = 0;
+    sorted_local_ = distinct_local_ = true;
+    async_small_ = small_ordered_ok(shard, true);
+    if (async_small_) {
+      enqueue_small_ordered(shard, /*spec_samples=*/false, nullptr, 0);
+      return false;
+    }
+    m.check_input(shard);
+    m.combine_map = true;
+    m.enqueue_upload(shard);
+    m.enqueue_map(shard);
+    m.combine_map = false;
+    LOCUST_CHECK_ARG(m.large_ordered_ok(), "asynchronous map: no partition table for this pass");
+    m.sync_clean = false;
+    m.enqueue_partials();
+    OrderedExtra ex;
+    ex.pm = m.part_map();
+    ex.part_w = m.d_pw;
+    ex.recs = m.d_records;
+    ex.sorted = m.sorted;
+    ex.counts = m.d_sorted_counts;
+    launch_dict_ordered_partials(m.d_partials, m.d_partial_n, m.partial_nslots, m.d_ctr, nullptr,
+                                 m.d_ctr_mapped, m.lb_dict, m.stream, nullptr, ex);
+    set_local(m.sorted, m.d_sorted_counts, &m.d_ctr->num_unique);
+    return m.map_combined;
+  }
+  u64 exch_map_complete(const TextInput& shard) override {
+    DevicePipeline& m = *mp_;
+    *m.h_ctr = *m.h_ctr_mapped;
+    LOCUST_CHECK_ARG(!(m.h_ctr->flags & kCtrDictOverflow), "asynchronous map needs a redo");
+    if (async_small_) m.sync_clean = true;  // the ordered kernel re-zeroed its scratch
+    samples_valid_ = false;  // the samples went to the device only
+    m.maybe_retune_records(m.d_records, m.h_ctr->num_unique);
+    return finish_map_stats(shard, m.h_ctr->num_unique);
+  }
+
   void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples, u32 P,
-                        int me, int root, const ExchCollectives& coll) override {
+                        int me, int root, const ExchCollectives& coll,
+                        const TextInput* map_shard) override {
     DevicePipeline& m = *mp_;
     const u32 S = (u32)samples.size();
     const u32 C = exch_slot_records, G = exch_gather_records;
     LOCUST_CHECK_ARG(P >= 1 && P <= kExchMaxRanks && C && G, "exchange: bad shape");
     // everything that can allocate or synchronise happens before the first collective
-    if (!hdr.status) prepare_shuffle();
+    if (!hdr.status && !map_shard) prepare_shuffle();
     ensure_exch(P, S, C, G);
     const bool is_root = me == root;
     if (is_root) {
       recv_records(std::max<u64>((u64)P * G, 4096));
       rp_->grow_host_out((u64)P * G);
     }
-    std::memcpy(xb_.h_msg1, &hdr, sizeof(ExchMsg1));
-    if (S) std::memcpy(xb_.h_msg1 + sizeof(ExchMsg1), samples.data(), (u64)S * sizeof(PackedKey));
     const u64 mb = exch_msg1_bytes(S), sb = exch_slot_bytes(C);
-    LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.msg1_send, xb_.h_msg1, mb, hipMemcpyHostToDevice, m.stream));
+    if (map_shard) {
+      // exch_map_enqueue ran the map and wrote the samples; the header from the counters
+      // (hdr.status != 0: the map failed or was not enqueued -- n_local 0, plan aborts)
+      // (from the ordered kernel's counter snapshot: a small pass re-zeroes d_ctr itself)
+      launch_exch_header(m.d_ctr_mapped, hdr, async_combined_,
+                         reinterpret_cast<ExchMsg1*>(xb_.msg1_send), m.stream);
+    } else {
+      std::memcpy(xb_.h_msg1, &hdr, sizeof(ExchMsg1));
+      if (S) std::memcpy(xb_.h_msg1 + sizeof(ExchMsg1), samples.data(), (u64)S * sizeof(PackedKey));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.msg1_send, xb_.h_msg1, mb, hipMemcpyHostToDevice, m.stream));
+    }
     coll.allgather(xb_.msg1_send, xb_.msg1_all, mb);
     // a failed map has no valid records: the planner sees the status and every rank's
     // kernels turn into no-ops, but the collectives still run
@@ -831,6 +900,8 @@ class GpuShardEngine final : public ShardEngine {
   u64 rp_gen_ = 0;  // bumped whenever rp_ is reallocated (graph keys)
   static constexpr u32 kSpecSamples = 64;  // DistConfig::samples_per_rank default
   ConstKeysSoA local_keys_{};
+  bool async_small_ = false;     // the last asynchronous map was a small ordered pass
+  bool async_combined_ = false;  // ... and its token count is the combining map's
   std::vector<PackedKey> samples_;
   bool samples_valid_ = false;
   EntryList range_entries_;

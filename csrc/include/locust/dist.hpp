@@ -233,10 +233,25 @@ class ShardEngine {
   // and sample()) on stream(): `hdr` + `samples` are this rank's ExchMsg1; every buffer is
   // sized before the first collective.  Each collective callback is called exactly once,
   // in the order allgather, alltoall, allgather, gather.  Results after sync_stream:
+  // map_shard (exch_map_async_ok): this rank has NOT mapped yet -- the exchange enqueues
+  // the map first and builds hdr's counts and the samples on the device (hdr carries the
+  // status, record flags and lines; `samples` only its size), so the job has ONE host
+  // synchronisation; afterwards exch_map_complete() (or, if any header says kExchMapRedo,
+  // every rank maps again synchronously).
   virtual void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples,
-                                u32 P, int me, int root, const ExchCollectives& coll) {
+                                u32 P, int me, int root, const ExchCollectives& coll,
+                                const TextInput* map_shard = nullptr) {
     throw Error("this engine has no device exchange");
   }
+  virtual bool exch_map_async_ok(const TextInput& /*shard*/) const { return false; }
+  // The map half of an asynchronous-map exchange (before enqueue_exchange, P ranks, S
+  // samples); a throw here becomes the header's failure status.
+  virtual void exch_map_enqueue(const TextInput& /*shard*/, u32 /*P*/, u32 /*S*/) {
+    throw Error("this engine has no asynchronous-map exchange");
+  }
+  // After the one sync of an asynchronous-map exchange: this rank's record count; the local
+  // statistics are then available from map_stats().
+  virtual u64 exch_map_complete(const TextInput& /*shard*/) { return 0; }
   virtual const ExchMsg1* exch_headers() const { return nullptr; }  // P ExchMsg1 headers
   virtual const ExchMsg3* exch_reports() const { return nullptr; }  // P reports
   // Root, after the sync: the concatenated output (as finish_merge_slots).

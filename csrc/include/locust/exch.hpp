@@ -44,6 +44,9 @@ constexpr u32 kExchSendOverflow = 1;   // a bucket of this rank exceeded the slo
 constexpr u32 kExchRecvTruncated = 2;  // a received slot was truncated or failed
 constexpr u32 kExchAbort = 4;          // a rank's ExchMsg1 reported a failure
 constexpr u32 kExchTooManySamples = 8; // the device planner cannot take this many samples
+// ExchMsg1::status of a rank whose asynchronous map must be redone (an LDS partition of the
+// ordered build overflowed): every rank sees it and the job continues on the standard path
+constexpr i32 kExchMapRedo = 3;
 
 struct ExchMsg3 {       // 64 B
   i32 status;           // 0 = ok

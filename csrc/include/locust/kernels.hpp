@@ -374,6 +374,11 @@ void launch_unpack_records(const KeyCount* in, u64 n, KeysSoA keys, u64* counts,
 // S evenly spaced keys of a sorted array of *d_n keys: sample[k] = keys[floor((k+0.5)*n/S)].
 void launch_sample_keys(ConstKeysSoA sorted, const u32* d_n, u32 num_samples, PackedKey* out,
                         hipStream_t s);
+// This rank's ExchMsg1 from the device counters (asynchronous-map exchange, exchange.hip):
+// tmpl's status (host-side failure) or kExchMapRedo on a partition overflow; n_local,
+// tokens (map_tokens of a combining map, else num_records) and the map statistics.
+void launch_exch_header(const MapCounters* ctr, const ExchMsg1& tmpl, bool combined,
+                        ExchMsg1* out, hipStream_t s);
 // offsets[p] = lower_bound(sorted, splitter[p-1]) for p in 1..P-1, offsets[0] = 0,
 // offsets[P] = n.
 void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey* splitters,

@@ -1298,6 +1298,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     if (ovf_total) ctr->flags |= kCtrDictOverflow;
     if (ctr_out) {
       ctr_out->num_records = ctr->num_records;
+      ctr_out->map_tokens = ctr->map_tokens;
       ctr_out->num_unique = u;
       ctr_out->overflow_lines = ctr->overflow_lines;
       ctr_out->truncated = ctr->truncated;
@@ -1470,6 +1471,7 @@ __global__ __launch_bounds__(256) void rank_emit_kernel(ConstKeysSoA keys,
   if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
     // field by field: total_count belongs to the thread that emits rank u-1
     ctr_out->num_records = ctr->num_records;
+    ctr_out->map_tokens = ctr->map_tokens;
     ctr_out->num_unique = u;
     ctr_out->overflow_lines = ctr->overflow_lines;
     ctr_out->truncated = ctr->truncated;
@@ -1526,6 +1528,7 @@ __global__ __launch_bounds__(256) void scan_pack_kernel(ConstKeysSoA sorted,
   if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
     // field by field: total_count belongs to the last tile
     ctr_out->num_records = ctr->num_records;
+    ctr_out->map_tokens = ctr->map_tokens;
     ctr_out->num_unique = u;
     ctr_out->overflow_lines = ctr->overflow_lines;
     ctr_out->truncated = ctr->truncated;

@@ -266,7 +266,25 @@ __global__ __launch_bounds__(256) void exch_concat_kernel(const OutRecord* __res
   }
 }
 
+__global__ void exch_header_kernel(const MapCounters* __restrict__ ctr, ExchMsg1 h,
+                                   u32 combined, ExchMsg1* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  if (!h.status && (ctr->flags & kCtrDictOverflow)) h.status = kExchMapRedo;
+  h.n_local = h.status ? 0 : ctr->num_unique;
+  h.tokens = combined ? ctr->map_tokens : ctr->num_records;
+  h.overflow_lines = ctr->overflow_lines;
+  h.truncated = ctr->truncated;
+  h.max_key_len = ctr->max_key_len;
+  *out = h;
+}
+
 }  // namespace
+
+void launch_exch_header(const MapCounters* ctr, const ExchMsg1& tmpl, bool combined,
+                        ExchMsg1* out, hipStream_t s) {
+  exch_header_kernel<<<dim3(1), dim3(64), 0, s>>>(ctr, tmpl, combined ? 1u : 0u, out);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
 
 void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
                       u32 slot_records, ExchCtl* ctl, hipStream_t s) {

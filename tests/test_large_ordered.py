@@ -68,3 +68,29 @@ def test_many_distinct_keys_fall_back():
     eng = lc._C.GpuEngine(lc.make_config("gpu", check=True), len(text), text.count(b"\n"))
     for _ in range(2):
         assert eng.run(text).entries() == want
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("strategy", ["shuffle", "gather", "auto"])
+def test_one_rank_distributed_large_shard(strategy):
+    """A large shard on one RCCL rank: the combining piecewise map + partials + ordered
+    build feed the exchange (shuffle), the gather, or -- auto -- the local pipeline; every
+    job matches the CPU engine, token count included (the counter snapshot the exchange
+    header is built from carries the combining map's token count)."""
+    text = gen(220_000, seed=9).to_bytes()
+    want = cpu_entries(text)
+    ntok = sum(c for _k, _v, c in want)
+    dcfg = lc.make_dist_config(1, lc.make_config("gpu", combine=True), strategy=strategy)
+    dr = lc._C.DistRank(dcfg, 0, "rccl", "127.0.0.1", _free_port(), len(text),
+                        text.count(b"\n"), 60.0)
+    for _ in range(3):
+        res, info = dr.run(text, 0)
+        assert info["strategy"] == ("local" if strategy == "auto" else strategy)
+        assert res.num_tokens == ntok
+        assert res.entries() == want
