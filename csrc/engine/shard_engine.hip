@@ -857,7 +857,8 @@ class GpuShardEngine final : public ShardEngine {
   }
 
   void finalize(u64 global_offset, EntryList* out) override {
-    for (auto& e : range_entries_) e.val += global_offset;
+    if (global_offset)  // (a pass over every entry: 0.2 ms for 200K of them)
+      for (auto& e : range_entries_) e.val += global_offset;
     *out = std::move(range_entries_);
   }
 

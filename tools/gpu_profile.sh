@@ -15,7 +15,7 @@ $CLI --gen /tmp/synth1m.txt --gen-lines 1000000 --seed 1 > /dev/null && timeout 
 P=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   P=$((P+1))
-  timeout -k 10 300 rocprofv3 --pmc $set -d $O/pmc$P -o run --output-format csv -- $CLI $H --warmup 2 --iters 5 --quiet > /dev/null || echo "pmc set $P failed: $set"
+  timeout -s KILL 90 rocprofv3 --pmc $set -d $O/pmc$P -o run --output-format csv -- $CLI $H --warmup 2 --iters 5 --quiet > /dev/null || echo "pmc set $P failed: $set"
 done
 cd $GRAFT_REPO_ROOT
 for k in k4500 k700 kradix ksynth; do
