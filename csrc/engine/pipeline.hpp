@@ -162,6 +162,9 @@ struct DevicePipeline {
   u32* h_done = nullptr;
   u32* d_done = nullptr;
   u32 done_seq = 0;
+  // set before enqueue_dict_job: a self-cleaning ordered kernel publishes this value
+  // itself (and clears it); still set afterwards -> publish_done() behind the job
+  u32 done_pending = 0;
   // Partition map of the ordered dictionary build (PartMap / locust/partmap.hpp): device
   // tables (persist across jobs), a pinned staging image, and the per-partition work the
   // ordered kernel reports each run (host-mapped) from which the host decides to retune.
@@ -1068,6 +1071,11 @@ struct DevicePipeline {
     ex.part_w = d_pw;
     if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
     if (self_clean) set_self_clean(ex);
+    if (self_clean && done_pending) {  // the kernel itself tells the host it is done
+      ex.host_done = d_done;
+      ex.host_done_value = done_pending;
+      done_pending = 0;
+    }
     set_tile_source(ex, with_counts);
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
@@ -1448,8 +1456,10 @@ struct DevicePipeline {
     if (dict_path) {
       bool ordered = graph_ordered;
       if (lean) {
+        done_pending = ++done_seq;
         ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr, /*self_clean=*/true);
-        publish_done(++done_seq);
+        if (done_pending) publish_done(done_seq);
+        done_pending = 0;
       } else if (!graphed) {
         ordered = enqueue_dict_job((u32)in.num_lines, compat, false,
                                    pieces.empty() ? ev[3] : nullptr, /*self_clean=*/true);

@@ -270,6 +270,11 @@ struct OrderedExtra {
   LookbackScratch map_lb{};
   u32 map_words = 0;
   u32* done_counter = nullptr;  // zeroed counter of finished workgroups (self_clean)
+  // With self_clean (optional, host-mapped): the last workgroup publishes host_done_value
+  // here once every workgroup's writes are visible system-wide -- the lean job's completion
+  // word without a kernel of its own behind this one.
+  u32* host_done = nullptr;
+  u32 host_done_value = 0;
   // Tokens from the small-input fast map with its per-tile partition table (launch_map_fast
   // part_off): partitions read their token ranges from it instead of scanning the tags.
   const u32* part_off = nullptr;

@@ -1326,7 +1326,12 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     // Process stage from these counters and resets everything itself).
     __syncthreads();
     if (threadIdx.x == 0) {
-      __threadfence();  // release this workgroup's counter / status writes
+      // release this workgroup's counter / status writes (and, when the host is told of the
+      // end, its host-mapped records: system scope)
+      if (ex.host_done)
+        __threadfence_system();
+      else
+        __threadfence();
       s_count = atomicAdd(ex.done_counter, 1u) == (u32)kDictParts - 1 ? 1u : 0u;
     }
     __syncthreads();
@@ -1349,6 +1354,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
           *ex.map_lb.tile_counter = 0;
           *ex.done_counter = 0;
         }
+      }
+      if (ex.host_done && threadIdx.x == 0) {  // every workgroup's writes are out
+        __threadfence_system();
+        __hip_atomic_store(ex.host_done, ex.host_done_value, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
