@@ -697,12 +697,18 @@ struct DevicePipeline {
   // Measured on the box: a 3-node graph replay + sync costs ~20 us of launch/wake-up per
   // job, 3 direct launches + a polled completion word ~11 us (tools/micro/launch_lat.hip).
   // LOCUST_LEAN=0: the graph replay (cfg.graph < 0) / event-timed path instead.
-  bool lean_job(const TextInput& in) const {
+  static bool lean_enabled() {
     static const bool on = [] {
       const char* e = std::getenv("LOCUST_LEAN");
       return !e || e[0] != '0';
     }();
-    if (!on || cfg.graph >= 0 || cfg.map_path != MapPath::kFast) return false;
+    return on;
+  }
+  // The shard engine's cached sequences (small pass, merge tails): replayed graphs only
+  // when asked for (graph=1); in auto mode direct launches are cheaper (see lean_job).
+  bool graph_launches() const { return use_graph() && !(cfg.graph < 0 && lean_enabled()); }
+  bool lean_job(const TextInput& in) const {
+    if (!lean_enabled() || cfg.graph >= 0 || cfg.map_path != MapPath::kFast) return false;
     if (large_ordered && in.bytes >= 2 * kPieceBytes) return false;
     if (cfg.sort_path == SortPath::kDict) return true;
     return table_tiles(in.bytes) > 0 && radix_mapped() && psort_enabled();

@@ -248,7 +248,7 @@ class GpuShardEngine final : public ShardEngine {
                              u32 slot_recs) {
     DevicePipeline& m = *mp_;
     auto half = prepare_small_ordered(shard, spec_samples, hdr, slot_recs);
-    if (m.use_graph())
+    if (m.graph_launches())
       m.launch_cached(half.first, half.second);
     else
       half.second();
@@ -368,7 +368,7 @@ class GpuShardEngine final : public ShardEngine {
   void enqueue_merge_slots(u32 nslots, u32 slot_recs) override {
     DevicePipeline& m = *mp_;
     auto half = prepare_merge_slots(nslots, slot_recs);
-    if (m.use_graph())
+    if (m.graph_launches())
       m.launch_cached(half.first, half.second);
     else
       half.second();
@@ -794,7 +794,7 @@ class GpuShardEngine final : public ShardEngine {
         launch_merge_sorted_runs(m.d_records, r.d_records, d_meta, r.cap, merged, r.d_ctr,
                                  r.d_out_mapped, r.d_ctr_mapped, r.lb_merge(r.cap), r.stream);
       };
-      if (r.use_graph())
+      if (r.graph_launches())
         r.launch_cached({5 | (rp_gen_ << 8), (u64)nruns, reinterpret_cast<u64>(m.d_records),
                          reinterpret_cast<u64>(r.d_records),
                          reinterpret_cast<u64>(r.d_out_mapped), 0},
@@ -828,7 +828,7 @@ class GpuShardEngine final : public ShardEngine {
         launch_dict_merge_runs(m.d_records, r.d_records, d_meta, r.d_ctr, r.d_out_mapped,
                                r.d_ctr_mapped, r.lb_dict, r.stream, r.part_map());
       };
-      if (r.use_graph())
+      if (r.graph_launches())
         r.launch_cached({4 | (rp_gen_ << 8), (u64)nruns, reinterpret_cast<u64>(m.d_records),
                          reinterpret_cast<u64>(r.d_records), 0, 0},
                         enqueue);
