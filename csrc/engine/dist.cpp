@@ -450,6 +450,11 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       eng.exch_last_sum = 0;
       for (int p = 0; p < P; ++p) eng.exch_last_sum += H[p].n_local;
       if (!flags) {
+        if ((int)log_level() >= (int)LogLevel::kDebug)
+          for (int p = 0; p < P; ++p)
+            LOCUST_LOG_DEBUG("exchange header %d: n_local %llu tokens %llu lines %llu", p,
+                             (unsigned long long)H[p].n_local, (unsigned long long)H[p].tokens,
+                             (unsigned long long)H[p].lines);
         for (int p = 0; p < P; ++p) {
           r.num_lines += H[p].lines;
           r.num_tokens += H[p].tokens;

@@ -580,7 +580,7 @@ class GpuShardEngine final : public ShardEngine {
     // a failed map has no valid records: the planner sees the status and every rank's
     // kernels turn into no-ops, but the collectives still run
     const u32* d_n = hdr.status ? xb_.zero_n : local_n();
-    launch_exch_plan(xb_.msg1_all, P, S, local_keys(), d_n, C, xb_.ctl, m.stream);
+    launch_exch_plan(xb_.msg1_all, P, S, local_keys(), d_n, C, xb_.ctl, m.stream, exch_trace());
     launch_exch_pack(m.d_records, d_n, m.cap, xb_.ctl, P, C, xb_.a2a_send, m.stream);
     coll.alltoall(xb_.a2a_send, xb_.a2a_recv, sb);
     OutRecord* out = is_root ? xb_.groot + (u64)root * G : xb_.gsend;
@@ -598,7 +598,31 @@ class GpuShardEngine final : public ShardEngine {
     LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.h_msg3, xb_.msg3_all, (u64)P * sizeof(ExchMsg3),
                                     hipMemcpyDeviceToHost, m.stream));
   }
-  const ExchMsg1* exch_headers() const override { return xb_.h_hdrs; }
+  // LOCUST_EXCH_TRACE=1: the plan kernel's phase stamps, printed after each exchange.
+  u64* h_exch_trace_ = nullptr;  // host-mapped (leaked with the engine: diagnostics only)
+  u64* exch_trace() {
+    static const bool on = std::getenv("LOCUST_EXCH_TRACE") != nullptr;
+    if (!on) return nullptr;
+    if (!h_exch_trace_)
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_exch_trace_, 16 * sizeof(u64),
+                                     hipHostMallocMapped | hipHostMallocCoherent));
+    u64* d = nullptr;
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h_exch_trace_, 0));
+    return d;
+  }
+  void print_exch_trace() const {
+    if (!h_exch_trace_) return;
+    const u64* t = h_exch_trace_;
+    std::fprintf(stderr, "exch_plan us: status %.2f load %.2f sort %.2f split %.2f search %.2f "
+                 "out %.2f | shader clock %.0f MHz\n", (t[1] - t[0]) * 0.01,
+                 (t[2] - t[1]) * 0.01, (t[3] - t[2]) * 0.01, (t[4] - t[3]) * 0.01,
+                 (t[5] - t[4]) * 0.01, (t[6] - t[5]) * 0.01,
+                 t[6] > t[0] ? (double)(t[8] - t[7]) / ((t[6] - t[0]) * 0.01) : 0.0);
+  }
+  const ExchMsg1* exch_headers() const override {
+    print_exch_trace();
+    return xb_.h_hdrs;
+  }
   const ExchMsg3* exch_reports() const override { return xb_.h_msg3; }
   void exch_finish_root(u64* total_count, u64* num_unique) override {
     DevicePipeline& r = *rp_;
@@ -984,7 +1008,10 @@ class GpuShardEngine final : public ShardEngine {
               o_mg = take(merge_cap * sizeof(KeyCount)), o_lb = take(lbw * 8 + 8),
               o_lt = take(8), o_zn = take(8), o_rc = take(sizeof(MapCounters));
     LOCUST_HIP_CHECK(hipMalloc(&xb_.dev, off));
-    LOCUST_HIP_CHECK(hipMemset(xb_.dev, 0, off));
+    // zeroed in stream order: a null-stream hipMemset is not ordered with the engine's
+    // non-blocking stream, and with four ranks sharing a GPU it landed after this job's
+    // header upload now and then (a rank's header all-gathered as zeros: wrong token sum)
+    LOCUST_HIP_CHECK(hipMemsetAsync(xb_.dev, 0, off, mp_->stream));
     char* b = xb_.dev;
     xb_.P = P;
     xb_.S = S;

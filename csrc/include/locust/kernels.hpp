@@ -396,7 +396,8 @@ void launch_merge_slots_limited(const KeyCount* slots, u32 nslots, u32 slot_reco
                                 KeyCount* merged, MapCounters* ctr, OutRecord* out,
                                 u64 out_limit, LookbackScratch lb, hipStream_t s);
 void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
-                      u32 slot_records, ExchCtl* ctl, hipStream_t s);
+                      u32 slot_records, ExchCtl* ctl, hipStream_t s,
+                      u64* trace = nullptr);
 void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchCtl* ctl, u32 P,
                       u32 slot_records, char* send, hipStream_t s);
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,

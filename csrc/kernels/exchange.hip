@@ -5,6 +5,8 @@
 // on the host between collectives (dist.cpp: choose_splitters, bucket_offsets, the count
 // and total all-gathers) is taken here on the device, so the whole exchange is enqueued
 // behind the map with no host round trip.
+#include <cstdlib>
+
 #include "locust/device/wave.hpp"
 #include "locust/exch.hpp"
 #include "locust/hip_check.hpp"
@@ -30,10 +32,17 @@ __device__ __forceinline__ bool key4_less(const u64* a, const u64* b) {
 // (64 probes per dependent load round instead of one), (5) bucket counts and flags.
 __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
     const char* __restrict__ msg1_all, u32 P, u32 S, ConstKeysSoA keys,
-    const u32* __restrict__ d_n, u32 slot_records, ExchCtl* __restrict__ ctl) {
+    const u32* __restrict__ d_n, u32 slot_records, ExchCtl* __restrict__ ctl,
+    u64* __restrict__ trace, u32 variant) {
+  // trace (diagnostics, LOCUST_EXCH_TRACE): device clock at entry and after each phase
+#define PLAN_STAMP(k_) \
+  if (trace && threadIdx.x == 0) trace[k_] = __builtin_amdgcn_s_memrealtime()
+  PLAN_STAMP(0);
+  if (trace && threadIdx.x == 0) trace[7] = __builtin_amdgcn_s_memtime();  // shader clock
   __shared__ u64 s_k[kExchMaxPlanSamples][kKeyWords];
   __shared__ u64 s_w[kExchMaxPlanSamples];
   __shared__ u32 s_at[kExchMaxPlanSamples];  // sorted position -> sample
+  __shared__ u32 s_unsorted;
   __shared__ u64 s_incl[kExchMaxPlanSamples];
   __shared__ u64 s_split[kExchMaxRanks][kKeyWords];
   __shared__ u64 s_off[kExchMaxRanks + 1];
@@ -53,6 +62,7 @@ __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
     if (h->status) atomicOr(&s_flags, kExchAbort);
   }
   const bool fits = NS <= kExchMaxPlanSamples && P <= kExchMaxRanks;
+  PLAN_STAMP(1);
   if (fits) {
     for (u32 i = t; i < NS; i += kPlanBlock) {
       const u32 r = i / S, q = i - r * S;
@@ -64,18 +74,52 @@ __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
     }
   }
   __syncthreads();
-  if (fits) {
-    for (u32 i = t; i < NS; i += kPlanBlock) {  // stable rank of sample i
-      u32 r = 0;
+  PLAN_STAMP(2);
+  // Stable ranks (order: key, then rank, then index).  Every rank's samples arrive sorted
+  // (picked at increasing positions of its sorted keys), so a sample's rank is its index in
+  // its own list plus, per other list, a binary search: an upper bound in the lists before
+  // its own, a lower bound in those after.  An all-pairs walk (one thread per sample over
+  // all NS candidates) took 26 us at NS = 64 -- every step a dependent LDS load with a
+  // divergent tie branch.  A list that is not sorted falls back to that walk.
+  if (t == 0) s_unsorted = variant & 1u;  // variant 1 (A/B): the all-pairs walk
+  __syncthreads();
+  if (fits)
+    for (u32 i = t; i < NS; i += kPlanBlock)
+      if (i % S && key4_less(s_k[i], s_k[i - 1])) s_unsorted = 1;
+  __syncthreads();
+  if (fits && !s_unsorted) {
+    for (u32 i = t; i < NS; i += kPlanBlock) {
+      const u32 r = i / S;
+      u64 ki[kKeyWords];
+#pragma unroll
+      for (int w = 0; w < kKeyWords; ++w) ki[w] = s_k[i][w];
+      u32 rank = i - r * S;
+      for (u32 rr = 0; rr < P; ++rr) {
+        if (rr == r) continue;
+        const u32 base = rr * S;
+        u32 lo = 0, hi = S;
+        while (lo < hi) {
+          const u32 mid = (lo + hi) >> 1;
+          const bool before = rr < r ? !key4_less(ki, s_k[base + mid])   // <= ki
+                                     : key4_less(s_k[base + mid], ki);   // <  ki
+          if (before) lo = mid + 1; else hi = mid;
+        }
+        rank += lo;
+      }
+      s_at[rank] = i;
+    }
+  } else if (fits) {
+    for (u32 i = t; i < NS; i += kPlanBlock) {
+      u32 rank = 0;
       for (u32 j = 0; j < NS; ++j) {
         const bool lt = key4_less(s_k[j], s_k[i]);
-        const bool eq = !lt && !key4_less(s_k[i], s_k[j]);
-        r += (lt || (eq && j < i)) ? 1u : 0u;
+        rank += (lt || (j < i && !key4_less(s_k[i], s_k[j]))) ? 1u : 0u;
       }
-      s_at[r] = i;
+      s_at[rank] = i;
     }
   }
   __syncthreads();
+  PLAN_STAMP(3);
   // inclusive weight prefix in sorted order (NS <= kPlanBlock: one sample per thread)
   const u64 w = (fits && t < NS) ? s_w[s_at[t]] : 0ull;
   u64 total = 0;
@@ -94,6 +138,7 @@ __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
     for (int j = 0; j < kKeyWords; ++j) s_split[t - 1][j] = lo < NS && fits ? s_k[s_at[lo]][j] : ~0ull;
   }
   __syncthreads();
+  PLAN_STAMP(4);
   // bucket offsets: wave v searches splitters v, v + 16, ...
   const u32 n = *d_n;
   const int lane = dev::lane_id(), wv = dev::wave_id();
@@ -136,11 +181,15 @@ __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
     if (c > slot_records) atomicOr(&s_flags, kExchSendOverflow);
   }
   __syncthreads();
+  PLAN_STAMP(5);
   for (u32 i = t; i <= P && i <= kExchMaxRanks; i += kPlanBlock) ctl->off[i] = s_off[i];
   if (t == 0) {
     ctl->flags = s_flags;
     ctl->max_bucket = s_maxb;
   }
+  PLAN_STAMP(6);
+  if (trace && threadIdx.x == 0) trace[8] = __builtin_amdgcn_s_memtime();
+#undef PLAN_STAMP
 }
 
 // Records -> the P all-to-all slots: record i of bucket d goes to slot d position
@@ -287,9 +336,13 @@ void launch_exch_header(const MapCounters* ctr, const ExchMsg1& tmpl, bool combi
 }
 
 void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
-                      u32 slot_records, ExchCtl* ctl, hipStream_t s) {
+                      u32 slot_records, ExchCtl* ctl, hipStream_t s, u64* trace) {
+  static const u32 variant = [] {
+    const char* e = std::getenv("LOCUST_PLAN_VARIANT");
+    return e ? (u32)std::atoi(e) : 0u;
+  }();
   exch_plan_kernel<<<dim3(1), dim3(kPlanBlock), 0, s>>>(msg1_all, P, S, keys, d_n, slot_records,
-                                                         ctl);
+                                                         ctl, trace, variant);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

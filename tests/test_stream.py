@@ -67,3 +67,18 @@ def test_ten_million_tokens_vs_cpu_engine(sort):
     assert r.num_tokens == c.num_tokens and r.num_tokens > 9_000_000
     assert r.num_unique == c.num_unique
     assert r.format(False) == c.format(False)
+
+
+@pytest.mark.gpu
+def test_device_exchange_first_job_is_ordered(hamlet):
+    """Four ranks sharing the GPU, streamed shards: the first device exchange allocates and
+    zeroes its buffers; the zeroing must be ordered with the same job's header upload
+    (a null-stream memset once landed after it now and then: a rank's header arrived as
+    zeros and the token total came out short).  Repeated, as the race was intermittent."""
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    for _ in range(20):
+        job = lc.make_config("gpu", combine=True, chunk_bytes=8 << 10)
+        cfgs = [lc.make_dist_config(4, job, strategy="shuffle") for _ in range(2)]
+        for res, info in lc._C.run_multi_schedule(hamlet, cfgs):
+            assert res.num_tokens == ntok
+            assert res.entries() == ent
