@@ -165,6 +165,7 @@ struct DevicePipeline {
   // set before enqueue_dict_job: a self-cleaning ordered kernel publishes this value
   // itself (and clears it); still set afterwards -> publish_done() behind the job
   u32 done_pending = 0;
+  bool split_stages = false;  // run(): this job records per-stage events
   // Partition map of the ordered dictionary build (PartMap / locust/partmap.hpp): device
   // tables (persist across jobs), a pinned staging image, and the per-partition work the
   // ordered kernel reports each run (host-mapped) from which the host decides to retune.
@@ -567,14 +568,15 @@ struct DevicePipeline {
     u64 pos = 0;
     while (pos < in.bytes && pieces.size() < npieces) {
       // Short first pieces start the map early, a short last piece keeps the work after
-      // the final copy small: P/4, P/2, P, ..., P, (rest - P/4), P/4.  The last piece
-      // allowed takes the rest (line alignment shortens the others).
-      const u64 rest = in.bytes - pos;
+      // the final copy small: P/4, P/2, P, ..., P, (rest - P/4), P/4 (a P/8 tail measured
+      // no better).  The last piece allowed takes the rest (line alignment shortens the
+      // others).
+      const u64 rest = in.bytes - pos, tail = piece / 4;
       u64 want = piece;
       if (pieces.size() == 0) want = piece / 4;
       else if (pieces.size() == 1) want = piece / 2;
-      else if (rest <= piece / 4 + piece / 8) want = rest;
-      else if (rest <= piece + piece / 4) want = rest - piece / 4;
+      else if (rest <= tail + tail / 2) want = rest;
+      else if (rest <= piece + tail) want = rest - tail;
       want = std::min(want, rest);
       u64 end = pieces.size() + 1 == npieces ? in.bytes : pos + want;
       if (end < in.bytes) {
@@ -1440,6 +1442,7 @@ struct DevicePipeline {
     const bool graphed = use_job_graph(in);
     // lean: a small single-pass job launched directly, no stage events, completion polled
     const bool lean = !graphed && lean_job(in);
+    split_stages = !lean && !graphed;
     skip_sync_reset = clean_start && dict_path && !compat;
     if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
     if (lean) {
@@ -1452,12 +1455,17 @@ struct DevicePipeline {
       r.times.graph = true;
     } else {
       enqueue_upload(in);
-      LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+      // Auto mode, piecewise pass: no stage markers between the kernels (the pass
+      // interleaves Map and Process anyway); graph=0 keeps the split
+      split_stages = pieces.empty() || cfg.graph == 0;
+      if (split_stages) LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
       enqueue_map(in);
-      LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
-      // a piecewise pass interleaves Process (the per-piece partials) with Map: one
-      // boundary, and no marker between the last partials and the ordered kernel
-      if (!pieces.empty()) LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+      if (split_stages) {
+        LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+        // a piecewise pass interleaves Process (the per-piece partials) with Map: one
+        // boundary, and no marker between the last partials and the ordered kernel
+        if (!pieces.empty()) LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+      }
     }
     if (dict_path) {
       bool ordered = graph_ordered;
@@ -1468,8 +1476,9 @@ struct DevicePipeline {
         done_pending = 0;
       } else if (!graphed) {
         ordered = enqueue_dict_job((u32)in.num_lines, compat, false,
-                                   pieces.empty() ? ev[3] : nullptr, /*self_clean=*/true);
-        LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+                                   split_stages && pieces.empty() ? ev[3] : nullptr,
+                                   /*self_clean=*/true);
+        if (split_stages) LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
       }
       skip_sync_reset = false;
@@ -1538,7 +1547,7 @@ struct DevicePipeline {
     if (lean) {  // no device timestamps: the job's wall time
       r.times.gpu_ms = r.times.wall_ms;
     } else {
-      if (!graphed) {
+      if (!graphed && split_stages) {
         r.times.h2d_ms = ms_between(ev[0], ev[1]);
         r.times.map_ms = ms_between(ev[1], ev[2]);
         r.times.process_ms = ms_between(ev[2], ev[3]);

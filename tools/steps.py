@@ -8,8 +8,9 @@ import locust_amd as lc
 
 lines = int(sys.argv[1]) if len(sys.argv) > 1 else 1000000
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+graph = int(sys.argv[3]) if len(sys.argv) > 3 else -1
 h = lc._C.HostText.generate(lines=lines, seed=1)
-cfg = lc.make_config("gpu", reduce_path="lds", chunk_bytes=256 << 20)
+cfg = lc.make_config("gpu", reduce_path="lds", chunk_bytes=256 << 20, graph=graph)
 eng = lc._C.GpuEngine(cfg, h.size, h.size)
 for _ in range(3):
     r = eng.run_text(h)
