@@ -433,6 +433,82 @@ __device__ __forceinline__ bool ord_greater(u64 aw0, u32 as, u64 bw0, u32 bs, co
   return false;
 }
 
+// Inserts partition p's records of tiles t, t + kPartBlock, ... (< t_end) into the LDS
+// table: every thread walks its own tiles' runs straight from the per-tile table (no LDS
+// list, no barrier between finding the runs and loading the keys), kPartialBatch key
+// gathers in flight, the next tile's run prefetched.  (a, len) is this thread's first run,
+// loaded by the caller before its table clear.  combine: lanes holding the wave's first
+// live key fold into one insert (hot keys).  Returns true if the table overflowed.
+constexpr int kPartialBatch = 8;
+__device__ __forceinline__ bool walk_runs_insert(ConstKeysSoA tokens, const u64* counts,
+                                                 const u32* part_off, u32 p, u32 t, u32 t_end,
+                                                 u32 a, u32 len, u32 n_cap, LdsSlot* s_tab,
+                                                 bool combine, u32* ntok_out) {
+  bool full = false;
+  u32 ntok = 0;
+  // The loop trip counts are per lane; the wave keeps going while any lane has work.
+  while (dev::ballot(t < t_end)) {
+    u32 na = 0, nlen = 0;  // the next tile's run, prefetched
+    const u32 tn = t + kPartBlock;
+    if (tn < t_end) {
+      na = part_off[(u64)tn * kPartTable + p];
+      nlen = part_off[(u64)tn * kPartTable + p + 1] - na;
+    }
+    for (u32 j0 = 0; dev::ballot(j0 < len); j0 += kPartialBatch) {
+      u64 kk[kPartialBatch][kKeyWords];
+      u64 cc[kPartialBatch];
+#pragma unroll
+      for (int r = 0; r < kPartialBatch; ++r) {
+        const u32 idx = a + j0 + (u32)r;
+        const bool ok = j0 + (u32)r < len && idx < n_cap;
+        kk[r][0] = ok ? tokens.w[0][idx] : 0;
+        cc[r] = ok && counts ? counts[idx] : 1ull;
+        kk[r][1] = kk[r][2] = kk[r][3] = 0;
+      }
+#pragma unroll
+      for (int r = 0; r < kPartialBatch; ++r) {
+        const u32 idx = a + j0 + (u32)r;
+        if (kk[r][0] & 0xffull) {
+          kk[r][1] = tokens.w[1][idx];
+          if (kk[r][1] & 0xffull) {
+            kk[r][2] = tokens.w[2][idx];
+            if (kk[r][2] & 0xffull) kk[r][3] = tokens.w[3][idx];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kPartialBatch; ++r) {
+        bool live = kk[r][0] != 0 && cc[r] != 0;
+        u64 c = cc[r];
+        const u64 lm = dev::ballot(live);
+        if (lm && combine) {
+          const int L = __ffsll((unsigned long long)lm) - 1;
+          bool same = live;
+#pragma unroll
+          for (int j = 0; j < kKeyWords; ++j) {
+            const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)kk[r][j], L);
+            const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(kk[r][j] >> 32), L);
+            same &= kk[r][j] == (((u64)hi << 32) | lo);
+          }
+          const u64 sm = dev::ballot(same);
+          if (__popcll(sm) > 1) {
+            const u64 tot = counts ? dev::wave_reduce_sum(same ? c : 0ull) : (u64)__popcll(sm);
+            if (dev::lane_id() == L) c = tot;
+            else if (same) live = false;
+          }
+        }
+        if (live) full |= !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]));
+      }
+    }
+    ntok += len;
+    t = tn;
+    a = na;
+    len = nlen;
+  }
+  if (ntok_out) *ntok_out = ntok;
+  return full;
+}
+
 // Token source of the ordered kernel: the map output (or unpacked records), found by
 // scanning the one-byte partition tags of every token.
 struct TagSource {
@@ -513,7 +589,10 @@ struct TileSource {
     if (t >= ntiles) return {0, 0};
     return {part_off[(u64)t * kPartTable + p], part_off[(u64)t * kPartTable + p + 1]};
   }
-  // stamp (diagnostics, optional): [12] list built, [13] gathered + inserted
+  // stamp (diagnostics, optional): [12] list built, [13] gathered + inserted.  (Walking
+  // each thread's own tile runs instead, as the partials kernel does, measured slower
+  // here: 21 vs 13.5 us span -- a small pass has ~180 tiles, so most lanes idle while the
+  // hot tiles' lanes insert serially; the list spreads the tokens over all 1,024.)
   __device__ bool build(u32 p, Pre pre, LdsSlot* s_tab, u32* s_list, u32& s_count,
                         u64* stamp) const {
     bool full = false;
@@ -636,9 +715,8 @@ struct RunsSource {
 // ---------------------------------------------------------------------------------
 constexpr u32 kPartialFull = 0xFFFFFFFFu;  // partial_n of a slot whose table overflowed
 
-// Every thread walks the partition's runs of its own tiles (no LDS list: the table is the
-// workgroup's only LDS, so two workgroups share a CU), kPartialBatch gathers in flight.
-constexpr int kPartialBatch = 8;
+// Every thread walks the partition's runs of its own tiles (walk_runs_insert; no LDS list:
+// the table is the workgroup's only LDS, so two workgroups share a CU).
 __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
     ConstKeysSoA tokens, const u64* __restrict__ counts, const u32* __restrict__ part_off,
     u32 tile_begin, u32 tile_end, u32 nslices, u32 slot_base, u32 nslots, u32 n_cap,
@@ -672,68 +750,9 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   }
   __syncthreads();
   if (trace && threadIdx.x == 0) trace[slot * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-  bool full = false;
   u32 ntok = 0;
-  // The loop trip counts are per lane; the wave keeps going while any lane has work.
-  while (dev::ballot(t < t1)) {
-    u32 na = 0, nlen = 0;  // the next tile's run, prefetched
-    const u32 tn = t + kPartBlock;
-    if (tn < t1) {
-      na = part_off[(u64)tn * kPartTable + p];
-      nlen = part_off[(u64)tn * kPartTable + p + 1] - na;
-    }
-    for (u32 j0 = 0; dev::ballot(j0 < len); j0 += kPartialBatch) {
-      u64 kk[kPartialBatch][kKeyWords];
-      u64 cc[kPartialBatch];
-#pragma unroll
-      for (int r = 0; r < kPartialBatch; ++r) {
-        const u32 idx = a + j0 + (u32)r;
-        const bool ok = j0 + (u32)r < len && idx < n_cap;
-        kk[r][0] = ok ? tokens.w[0][idx] : 0;
-        cc[r] = ok && counts ? counts[idx] : 1ull;
-        kk[r][1] = kk[r][2] = kk[r][3] = 0;
-      }
-#pragma unroll
-      for (int r = 0; r < kPartialBatch; ++r) {
-        const u32 idx = a + j0 + (u32)r;
-        if (kk[r][0] & 0xffull) {
-          kk[r][1] = tokens.w[1][idx];
-          if (kk[r][1] & 0xffull) {
-            kk[r][2] = tokens.w[2][idx];
-            if (kk[r][2] & 0xffull) kk[r][3] = tokens.w[3][idx];
-          }
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < kPartialBatch; ++r) {
-        bool live = kk[r][0] != 0 && cc[r] != 0;
-        u64 c = cc[r];
-        // hot keys: lanes holding the wave's first live key are one insert
-        const u64 lm = dev::ballot(live);
-        if (lm && !(variant & 4u)) {
-          const int L = __ffsll((unsigned long long)lm) - 1;
-          bool same = live;
-#pragma unroll
-          for (int j = 0; j < kKeyWords; ++j) {
-            const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)kk[r][j], L);
-            const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(kk[r][j] >> 32), L);
-            same &= kk[r][j] == (((u64)hi << 32) | lo);
-          }
-          const u64 sm = dev::ballot(same);
-          if (__popcll(sm) > 1) {
-            const u64 tot = counts ? dev::wave_reduce_sum(same ? c : 0ull) : (u64)__popcll(sm);
-            if (dev::lane_id() == L) c = tot;
-            else if (same) live = false;
-          }
-        }
-        if (live) full |= !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]));
-      }
-    }
-    ntok += len;
-    t = tn;
-    a = na;
-    len = nlen;
-  }
+  const bool full = walk_runs_insert(tokens, counts, part_off, p, t, t1, a, len, n_cap, s_tab,
+                                     !(variant & 4u), &ntok);
   if (trace) atomicAdd(&s_tok, ntok);
   __syncthreads();  // every wave's inserts are in the table before it is read
   if (trace && threadIdx.x == 0) {
@@ -956,12 +975,31 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         const u32 q = lane + 64u * k;
         st[k] = q < p ? dev::ld_agent(&status[q]) : dev::kLbAgg;  // beyond p: aggregate 0
       }
+      // unpublished words are re-read together, every round (one round trip per round, not
+      // one per group of 64 in turn)
+      auto pending = [&]() {
+        bool any = false;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const u32 q = lane + 64u * k;
-        while (q < p && (st[k] >> dev::kLbFlagShift) == 0) {
+        for (int k = 0; k < 4; ++k) any |= lane + 64u * k < p && (st[k] >> dev::kLbFlagShift) == 0;
+        return any;
+      };
+      if (ex.variant & 8u) {  // A/B: the previous per-group polling
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const u32 q = lane + 64u * k;
+          while (q < p && (st[k] >> dev::kLbFlagShift) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            st[k] = dev::ld_agent(&status[q]);
+          }
+        }
+      } else {
+        while (dev::ballot(pending())) {
           __builtin_amdgcn_s_sleep(1);
-          st[k] = dev::ld_agent(&status[q]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const u32 q = lane + 64u * k;
+            if (q < p && (st[k] >> dev::kLbFlagShift) == 0) st[k] = dev::ld_agent(&status[q]);
+          }
         }
       }
       int hi_inc = -1;  // highest predecessor with an inclusive value
