@@ -384,6 +384,8 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         h.status = 2;  // 1: the map failed, 2: the exchange
         local_msg = "injected fault (LOCUST_FAULT) in stage 'exchange'";
       }
+      // test hook: this rank's asynchronous map "overflowed" (every rank redoes the job)
+      if (exch_async && !st1 && fault_injected(me, "exch_map_redo")) h.status = kExchMapRedo;
       int entered = 0;
       ShardEngine::ExchCollectives coll;
       coll.allgather = [&](const void* snd, void* rcv, u64 b) {

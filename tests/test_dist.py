@@ -320,3 +320,19 @@ def test_gpu_device_exchange_one_rccl_rank(hamlet):
         used.append(info["device_exchange"])
         assert res.entries() == ent and res.num_tokens == ntok
     assert used == [False, True, True, True]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_gpu_device_exchange_async_map_redo(hamlet, monkeypatch, world):
+    """One rank's asynchronous map reports an LDS overflow in its exchange header
+    (LOCUST_FAULT=<rank>:exch_map_redo): every rank sees it, maps again synchronously and
+    runs the device exchange again in the same job; the output is exact."""
+    monkeypatch.setenv("LOCUST_FAULT", f"{world - 1}:exch_map_redo")
+    job = lc.make_config("gpu", combine=True, check=True)
+    cfgs = [lc.make_dist_config(world, job, strategy="shuffle") for _ in range(3)]
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback")
+    for j, (res, info) in enumerate(out):
+        assert info["device_exchange"] == (j > 0), (j, info)
+        assert res.entries() == ent and res.num_tokens == ntok
