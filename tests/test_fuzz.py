@@ -15,7 +15,8 @@ DELIMS = b" ,.-;:'()\"\t"
 ODD = b"\r\x00\x80\xc3\xa9\xff\x7f"
 
 
-def random_text(rng: random.Random, size: int) -> bytes:
+def random_text(rng: random.Random, size: int, fresh: float = 0.4) -> bytes:
+    """fresh: share of words drawn at random (the rest from a 300-word vocabulary)."""
     out = bytearray()
     while len(out) < size:
         r = rng.random()
@@ -31,7 +32,7 @@ def random_text(rng: random.Random, size: int) -> bytes:
             out += b" ".join(bytes([rng.choice(LETTERS)]) * rng.randint(1, 3)
                              for _ in range(rng.randint(21, 60)))
         else:  # a word from a small vocabulary (repeats) or a random one
-            if rng.random() < 0.6:
+            if rng.random() >= fresh:
                 out += b"w%d" % rng.randint(0, 300)
             else:
                 out += bytes(rng.choice(LETTERS) for _ in range(rng.randint(1, 12)))
@@ -88,3 +89,33 @@ def test_gpu_engine_reused_across_random_texts():
     for _ in range(30):
         text = random_text(rng, rng.choice([100, 5000, 60_000, 250_000]))
         assert eng.run(text).entries() == oracle.wordcount(text)[0]
+
+
+@pytest.mark.gpu
+def test_gpu_large_random_pass_matches_cpu_engine():
+    """A ~12 MB random text with a bounded vocabulary: upload pieces, per-piece partials and
+    the two-kernel ordered build (first job on the default partition map, then retuned),
+    against the CPU engine (itself checked against the oracle above)."""
+    rng = random.Random(5)
+    parts, size = [], 0
+    while size < 12 << 20:
+        chunk = random_text(rng, 256 << 10, fresh=0.002)
+        chunk = chunk[: chunk.rfind(b"\n") + 1] or b"x\n"
+        parts.append(chunk)
+        size += len(chunk)
+    text = b"".join(parts)
+    want = lc._C.cpu_run(lc.make_config("cpu"), text).entries()
+    eng = lc._C.GpuEngine(lc.make_config("gpu", check=True), len(text), text.count(b"\n") + 1)
+    for _ in range(3):
+        assert eng.run(text).entries() == want
+    # the same through the distributed shuffle on one RCCL rank (asynchronous map)
+    dcfg = lc.make_dist_config(1, lc.make_config("gpu", combine=True), strategy="shuffle")
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dr = lc._C.DistRank(dcfg, 0, "rccl", "127.0.0.1", port, len(text), text.count(b"\n") + 1,
+                        60.0)
+    for _ in range(3):
+        res, _info = dr.run(text, 0)
+        assert res.entries() == want
