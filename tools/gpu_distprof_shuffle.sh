@@ -1,5 +1,5 @@
 # Kernel timeline of the shuffle strategy (device exchange) on one
-# RCCL rank.  Usage: bash tools/gpu_distprof_gather.sh TAG
+# RCCL rank.  Usage: bash tools/gpu_distprof_shuffle.sh TAG
 set -e
 cd $GRAFT_REPO_ROOT
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-dpg}
