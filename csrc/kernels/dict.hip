@@ -26,6 +26,7 @@
 #include <algorithm>
 
 #include "locust/device/hash.hpp"
+#include "locust/device/lds_radix.hpp"
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
@@ -844,6 +845,9 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __shared__ u32 s_cm, s_cfull;  // compaction: distinct keys, overflow flag
   __shared__ u64 s_ctok;         // compaction: tokens
   __shared__ u64 s_wlo, s_whi;   // large partitions: first-word range of the keys present
+  __shared__ u64 s_wand[kKeyWords], s_wor[kKeyWords];  // large partitions: AND / OR per key
+                                                        // word (its varying bytes)
+  __shared__ u32 s_rstart[256], s_rwsum[4];  // large partitions: LdsRadix digit starts
   // partition = ticket, not blockIdx: a workgroup then only ever waits in the look-back
   // on workgroups that are already running.  With blockIdx, kernels of several processes
   // sharing the GPU (the TCP / loopback rehearsals) could fill the CUs with spinning
@@ -1133,7 +1137,74 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     s_cur[threadIdx.x] = 0;
   }
   __syncthreads();
-  if (!any_full && m > 1) {
+  if (!any_full && m > 1 && !(ex.variant & 16u)) {
+    // LSD radix sort of the partition's distinct keys in LDS over the bytes that vary
+    // (dev::LdsRadix, as the partitioned token sort): word 3 down to word 0, low byte to
+    // high, stable.  The bucket + all-pairs ranking below degenerated on skewed key sets
+    // -- most keys in one bucket, long keys tied on their first word: up to 295K cycles
+    // for one 1,003-key partition of the synthetic text (LOCUST_ORD_VARIANT=16 keeps it).
+    using Radix = dev::LdsRadix<kPartBlock, kPartSlots, u16>;
+    u64* s_word = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);          // [kPartSlots]
+    auto s_perm = reinterpret_cast<u16 (*)[kPartSlots]>(s_list + 5 * kPartSlots);  // [2][..]
+    auto s_rcnt = reinterpret_cast<u16 (*)[256]>(s_list + 6 * kPartSlots);   // [16][256]
+    auto s_rwex = reinterpret_cast<u16 (*)[256]>(s_list + 7 * kPartSlots);   // [16][256]
+    const Radix R{s_word, s_perm, s_rcnt, s_rwex, s_rstart, s_rwsum};
+    R.init();
+    for (u32 i = threadIdx.x; i < m; i += kPartBlock) s_perm[0][i] = (u16)i;
+    if (threadIdx.x < (u32)kKeyWords) {
+      s_wand[threadIdx.x] = ~0ull;
+      s_wor[threadIdx.x] = 0;
+    }
+    int cur = 0;
+    for (int j = kKeyWords - 1; j >= 0; --j) {
+      __syncthreads();  // the previous word's passes are done with s_word
+      u64 a_ = ~0ull, o_ = 0;
+      for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
+        const u64 w = j == 0 ? s_w0[i] : s_tab[s_slot[i]].w[j] ^ kWordMagic;
+        s_word[i] = w;
+        a_ &= w;
+        o_ |= w;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        a_ &= __shfl_xor(a_, off, 64);
+        o_ |= __shfl_xor(o_, off, 64);
+      }
+      if (dev::lane_id() == 0) {
+        atomicAnd(reinterpret_cast<unsigned long long*>(&s_wand[j]), (unsigned long long)a_);
+        atomicOr(reinterpret_cast<unsigned long long*>(&s_wor[j]), (unsigned long long)o_);
+      }
+      __syncthreads();
+      const u64 diff = s_wand[j] ^ s_wor[j];  // bits that differ between keys
+      for (u32 b = 0; b < 8; ++b)
+        if ((diff >> (8 * b)) & 0xffull) {
+          R.pass(s_word, m, 8 * b, cur);
+          cur ^= 1;
+        }
+    }
+    // sorted position d holds item s_perm[cur][d]: permute (w0, slot) through registers
+    constexpr u32 kPer2 = kPartSlots / kPartBlock;
+    u64 pw[kPer2];
+    u32 ps[kPer2];
+#pragma unroll
+    for (u32 r = 0; r < kPer2; ++r) {
+      const u32 d = threadIdx.x + r * kPartBlock;
+      if (d < m) {
+        const u32 it = s_perm[cur][d];
+        pw[r] = s_w0[it];
+        ps[r] = s_slot[it];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 r = 0; r < kPer2; ++r) {
+      const u32 d = threadIdx.x + r * kPartBlock;
+      if (d < m) {
+        s_w0[d] = pw[r];
+        s_slot[d] = ps[r];
+      }
+    }
+  } else if (!any_full && m > 1) {
     {
       u64 lo = ~0ull, hi = 0;
       for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
