@@ -94,8 +94,19 @@ struct DevicePipeline {
   u32 partial_nslots = 0;
   // Large single-pass inputs travel in line-aligned pieces on the copy stream, each mapped
   // and aggregated as soon as it lands (the H2D overlaps map + partials); set by
-  // prepare_upload.  At least kPieceBytes each, at most partial_slots_cap of them.
+  // prepare_upload.  At least kPieceBytes each (inputs from 2 x kPieceBytes on), middle
+  // pieces min(piece_target(), bytes / 4) (LOCUST_PIECE_MB, default 12: fewer copies run
+  // the link closer to a single DMA's rate -- synth1m with 4 / 8 / 12 / 16 MiB targets:
+  // 1.24 / 1.21 / 1.185 / 1.19 ms), at most partial_slots_cap of them.
   static constexpr u64 kPieceBytes = 4ull << 20;
+  static u64 piece_target() {
+    static const u64 b = [] {
+      const char* e = std::getenv("LOCUST_PIECE_MB");
+      const long mb = e ? std::atol(e) : 12;
+      return (u64)std::max<long>(mb, 4) << 20;
+    }();
+    return b;
+  }
   static constexpr u64 kMaxPieces = kMaxPartialSlots;
   std::vector<std::pair<u64, u64>> pieces;
   // run() opts a large dictionary pass into the combining map (records + d_counts);
@@ -564,7 +575,8 @@ struct DevicePipeline {
   void plan_pieces(const TextInput& in) {
     if (cfg.map_path != MapPath::kFast || !large_ordered || in.bytes < 2 * kPieceBytes) return;
     const u64 npieces = std::min<u64>(partial_slots_cap, kMaxPieces);
-    const u64 piece = std::max<u64>(kPieceBytes, div_up(in.bytes, npieces > 3 ? npieces - 3 : 1));
+    const u64 piece = std::max<u64>({kPieceBytes, std::min<u64>(piece_target(), in.bytes / 4),
+                                     div_up(in.bytes, npieces > 3 ? npieces - 3 : 1)});
     u64 pos = 0;
     while (pos < in.bytes && pieces.size() < npieces) {
       // Short first pieces start the map early, a short last piece keeps the work after
