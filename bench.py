@@ -198,7 +198,9 @@ def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, loca
                                                      else text.size))
     dcfg = lc.make_dist_config(world, job)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    port = int(os.environ.get("LOCUST_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+    from locust_amd.parallel import bootstrap_port
+
+    port = bootstrap_port(rank, world)
     if isinstance(text, bytes):
         nbytes, nlines = len(text), text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
     else:

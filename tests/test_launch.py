@@ -153,3 +153,37 @@ def test_stage_split_wordcount_over_daemons(tmp_path, hamlet, cli, capfd):
     body = out[out.index("print key:"):out.rindex("\nDone")].rstrip("\n")
     same = body == oracle.format_cpu(ent).decode().rstrip("\n")
     assert same, body[:300]  # (no full diff: the output is 5,608 lines)
+
+
+def test_bootstrap_port_from_torchrun_store(tmp_path):
+    """Under torch.distributed.run every rank gets the same bootstrap port from the agent's
+    rendezvous store (rank 0 picks a free one) instead of assuming MASTER_PORT + 1."""
+    script = tmp_path / "port.py"
+    script.write_text("import os\nfrom locust_amd.parallel import bootstrap_port\n"
+                      "print('PORT', os.environ['RANK'], bootstrap_port(), flush=True)\n")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    master = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k != "LOCUST_PORT"}
+    env["PYTHONPATH"] = lc.REPO_ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=3", "--master-addr", "127.0.0.1", "--master-port",
+                        str(master), str(script)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    ports = {ln.split()[1]: int(ln.split()[2]) for ln in p.stdout.splitlines()
+             if ln.startswith("PORT")}
+    assert sorted(ports) == ["0", "1", "2"] and len(set(ports.values())) == 1, p.stdout
+    assert "store unavailable" not in p.stderr
+
+
+def test_bootstrap_port_fixed_rules(monkeypatch):
+    from locust_amd.parallel import bootstrap_port
+
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "31000")
+    monkeypatch.delenv("LOCUST_PORT", raising=False)
+    assert bootstrap_port(0, 4) == 31001
+    monkeypatch.setenv("LOCUST_PORT", "32000")
+    assert bootstrap_port(1, 4) == 32000
