@@ -444,11 +444,20 @@ constexpr int kPartialBatch = 8;
 __device__ __forceinline__ bool walk_runs_insert(ConstKeysSoA tokens, const u64* counts,
                                                  const u32* part_off, u32 p, u32 t, u32 t_end,
                                                  u32 a, u32 len, u32 n_cap, LdsSlot* s_tab,
-                                                 bool combine, u32* ntok_out) {
+                                                 bool combine, u32* ntok_out,
+                                                 u32* s_full = nullptr) {
   bool full = false;
   u32 ntok = 0;
+  // s_full (LDS, zeroed by the caller before its barrier): set by the first failed insert
+  // of any wave; every wave stops at its next batch.  The slot's records are discarded once
+  // the table overflowed, so the rest of the walk is wasted work -- with a cold partition map
+  // (first key byte) a hot partition's remaining ~10^5 tokens each probed kPartProbes full
+  // slots: 3-8 ms per partials launch instead of ~25-55 us.
   // The loop trip counts are per lane; the wave keeps going while any lane has work.
   while (dev::ballot(t < t_end)) {
+    if (s_full && __builtin_amdgcn_readfirstlane(
+                      (int)__hip_atomic_load(s_full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+      break;
     u32 na = 0, nlen = 0;  // the next tile's run, prefetched
     const u32 tn = t + kPartBlock;
     if (tn < t_end) {
@@ -456,6 +465,9 @@ __device__ __forceinline__ bool walk_runs_insert(ConstKeysSoA tokens, const u64*
       nlen = part_off[(u64)tn * kPartTable + p + 1] - na;
     }
     for (u32 j0 = 0; dev::ballot(j0 < len); j0 += kPartialBatch) {
+      if (s_full && __builtin_amdgcn_readfirstlane(
+                        (int)__hip_atomic_load(s_full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+        break;
       u64 kk[kPartialBatch][kKeyWords];
       u64 cc[kPartialBatch];
 #pragma unroll
@@ -498,7 +510,10 @@ __device__ __forceinline__ bool walk_runs_insert(ConstKeysSoA tokens, const u64*
             else if (same) live = false;
           }
         }
-        if (live) full |= !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]));
+        if (live && !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]))) {
+          full = true;
+          if (s_full) __hip_atomic_store(s_full, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
     }
     ntok += len;
@@ -733,7 +748,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   __shared__ LdsSlot s_tab[kPartSlots];
   __shared__ u32 s_scan[kPartBlock / 64 + 1];
   __shared__ u32 s_tok;
-  if (threadIdx.x == 0) s_tok = 0;
+  __shared__ u32 s_full;  // the table overflowed: every wave stops walking
+  if (threadIdx.x == 0) {
+    s_tok = 0;
+    s_full = 0;
+  }
   const u32 ntiles = tile_end - tile_begin;
   const u32 t0 = tile_begin + (u32)((u64)ntiles * k / nslices);
   const u32 t1 = tile_begin + (u32)((u64)ntiles * (k + 1) / nslices);
@@ -753,7 +772,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   if (trace && threadIdx.x == 0) trace[slot * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   u32 ntok = 0;
   const bool full = walk_runs_insert(tokens, counts, part_off, p, t, t1, a, len, n_cap, s_tab,
-                                     !(variant & 4u), &ntok);
+                                     !(variant & 4u), &ntok, (variant & 32u) ? nullptr : &s_full);
   if (trace) atomicAdd(&s_tok, ntok);
   __syncthreads();  // every wave's inserts are in the table before it is read
   if (trace && threadIdx.x == 0) {
