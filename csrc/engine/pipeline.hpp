@@ -1340,13 +1340,23 @@ struct DevicePipeline {
     read_counters();
     const u64 u = h_ctr->num_unique;
     grow_host_out(u);
-    if (u)
+    if (u && copy_out_dma())  // A/B: LOCUST_OUT_COPY=dma
       LOCUST_HIP_CHECK(
           hipMemcpyAsync(h_out, d_out, u * sizeof(OutRecord), hipMemcpyDeviceToHost, stream));
+    else if (u)
+      launch_copy_to_mapped(d_out_mapped, d_out, u * sizeof(OutRecord), stream);
     if (done) LOCUST_HIP_CHECK(hipEventRecord(done, stream));
     sync();
     fill_counters(r);
     copy_out(r.entries, u);
+  }
+
+  static bool copy_out_dma() {
+    static const bool dma = [] {
+      const char* e = std::getenv("LOCUST_OUT_COPY");
+      return e && std::string(e) == "dma";
+    }();
+    return dma;
   }
 
   // Host output records -> result entries: identical 48-byte layouts, so the result

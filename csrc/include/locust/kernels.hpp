@@ -296,6 +296,9 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
 // Writes `value` to the host-mapped `word` once everything earlier on `s` has completed
 // (signal.hip; the lean job path polls it instead of synchronising the stream).
 void launch_signal_host(u32* word, u32 value, hipStream_t s);
+// bytes (a multiple of 16, 16-B aligned) from device memory into a host-mapped buffer
+// through its device pointer, by a kernel (signal.hip)
+void launch_copy_to_mapped(void* dst_mapped_dev, const void* src, u64 bytes, hipStream_t s);
 
 // Large ordered build (passes past kPartBuildMaxTokens whose map wrote a partition table,
 // dict.hip): launch_dict_partials splits tiles [tile_begin, tile_end) into `nslices`

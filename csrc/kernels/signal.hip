@@ -3,6 +3,9 @@
 // stream has completed.  The host polls that word instead of hipStreamSynchronize --
 // measured on the box (tools/micro/launch_lat.hip): 3 launches + sync 16.7 us per
 // iteration, the same + polling a mapped word 11.2 us, a 3-node graph replay + sync 20.1 us.
+#include <algorithm>
+
+#include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
 
 namespace locust {
@@ -13,7 +16,29 @@ __global__ void signal_host_kernel(u32* __restrict__ word, u32 value) {
     __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Device buffer -> host-mapped buffer (its device alias), 16 B per lane, grid-stride.  The
+// fallback paths' results reach the mapped output this way: a hipMemcpyAsync into the
+// fine-grained host buffer measured 7.3 ms for 9.7 MB on a cold engine (host-staged), a
+// kernel's posted writes run at the link rate like the ordered kernel's own record stores.
+__global__ __launch_bounds__(256) void copy_to_mapped_kernel(uint4* __restrict__ dst,
+                                                             const uint4* __restrict__ src, u64 n) {
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
 }  // namespace
+
+void launch_copy_to_mapped(void* dst_mapped_dev, const void* src, u64 bytes, hipStream_t s) {
+  LOCUST_CHECK_ARG(bytes % 16 == 0 && reinterpret_cast<uintptr_t>(dst_mapped_dev) % 16 == 0 &&
+                       reinterpret_cast<uintptr_t>(src) % 16 == 0,
+                   "copy_to_mapped: 16-byte aligned buffers and sizes");
+  const u64 n = bytes / 16;
+  if (!n) return;
+  const u64 blocks = std::min<u64>(div_up(n, 256), 1024);
+  copy_to_mapped_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(
+      reinterpret_cast<uint4*>(dst_mapped_dev), reinterpret_cast<const uint4*>(src), n);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
 
 void launch_signal_host(u32* word, u32 value, hipStream_t s) {
   signal_host_kernel<<<dim3(1), dim3(64), 0, s>>>(word, value);
