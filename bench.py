@@ -204,7 +204,7 @@ def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, loca
                                                      else text.size))
     dcfg = lc.make_dist_config(world, job)
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    from locust_amd.parallel import bootstrap_port
+    from locust_amd.parallel import bootstrap_port, release_bootstrap_port
 
     port = bootstrap_port(rank, world)
     if isinstance(text, bytes):
@@ -218,6 +218,7 @@ def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, loca
     os.dup2(2, 1)
     try:
         dr = lc._C.DistRank(dcfg, rank, comm, host, port, nbytes, nlines, 120.0)
+        release_bootstrap_port()  # every rank connected inside the constructor
     finally:
         os.dup2(saved, 1)
         os.close(saved)

@@ -16,7 +16,7 @@ from .hosts import Host, load_hosts, parse_hosts
 from .launch import launch_local, launch_remote, stage_split_wordcount
 
 
-_PORT_KEY = "locust_amd/bootstrap_port"
+_port_file: str | None = None
 
 
 def bootstrap_port(rank: int | None = None, world: int | None = None,
@@ -25,45 +25,61 @@ def bootstrap_port(rank: int | None = None, world: int | None = None,
     the TCP communicator's control messages go through it).
 
     * ``LOCUST_PORT`` if set (every rank must see the same value);
-    * under ``torch.distributed.run`` (``TORCHELASTIC_RUN_ID`` set, world > 1): rank 0 asks
-      the OS for a free port and publishes it in the agent's rendezvous store at
-      MASTER_ADDR:MASTER_PORT, the other ranks read it there -- no guess that
-      MASTER_PORT + 1 happens to be free on the node;
+    * under ``torch.distributed.run`` on one node (``TORCHELASTIC_RUN_ID`` set, world > 1,
+      every rank local): rank 0 asks the OS for a free port and publishes it in a file named
+      after MASTER_PORT and the launching agent's pid (the ranks' common parent); the other
+      ranks read it there -- no guess that MASTER_PORT + 1 happens to be free.  No torch
+      import: the engine's HIP/RCCL must stay the only ones in the process;
     * otherwise MASTER_PORT + 1 (this package's launcher keeps that one free)."""
+    global _port_file
     if "LOCUST_PORT" in os.environ:
         return int(os.environ["LOCUST_PORT"])
     rank = int(os.environ.get("RANK", "0")) if rank is None else rank
     world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else world
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     master = int(os.environ.get("MASTER_PORT", "29500"))
-    if world > 1 and "TORCHELASTIC_RUN_ID" in os.environ:
-        try:
-            return _port_from_store(host, master, rank, timeout)
-        except Exception as e:  # noqa: BLE001  (no torch / no store: the fixed rule)
-            import sys
-            print(f"locust_amd: rendezvous store unavailable ({e}); bootstrap on "
-                  f"MASTER_PORT+1", file=sys.stderr)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "0"))
+    if world > 1 and "TORCHELASTIC_RUN_ID" in os.environ and local_world == world:
+        import socket
+        import tempfile
+        import time
+
+        path = os.path.join(tempfile.gettempdir(),
+                            f"locust_port_{master}_{os.getppid()}_{os.getuid()}")
+        if rank == 0:
+            with socket.socket() as s:  # released just before the communicator binds it
+                s.bind((host, 0))
+                port = s.getsockname()[1]
+            tmp = f"{path}.{os.getpid()}"
+            with open(tmp, "w") as f:
+                f.write(str(port))
+            os.replace(tmp, path)  # readers never see a partial file
+            _port_file = path
+            return port
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            try:
+                with open(path) as f:
+                    txt = f.read().strip()
+                if txt:
+                    return int(txt)
+            except FileNotFoundError:
+                pass
+            time.sleep(0.005)
+        raise TimeoutError(f"rank {rank}: no bootstrap port from rank 0 in {path} "
+                           f"after {timeout:.0f} s")
     return master + 1
 
 
-def _port_from_store(host: str, master: int, rank: int, timeout: float) -> int:
-    import datetime
-    import socket
-
-    from torch.distributed import TCPStore
-
-    store = TCPStore(host, master, is_master=False,
-                     timeout=datetime.timedelta(seconds=timeout))
-    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
-    restart = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
-    key = f"{_PORT_KEY}/{run}/{restart}"
-    if rank == 0:
-        with socket.socket() as s:  # released just before the communicator binds it
-            s.bind((host, 0))
-            port = s.getsockname()[1]
-        store.set(key, str(port))
-        return port
-    return int(store.get(key).decode())
+def release_bootstrap_port() -> None:
+    """Rank 0, once every rank has connected: remove the published port file."""
+    global _port_file
+    if _port_file:
+        try:
+            os.unlink(_port_file)
+        except FileNotFoundError:
+            pass
+        _port_file = None
 
 
 def init_rank(cfg, max_bytes: int, max_lines: int, comm: str = "rccl", timeout: float = 300.0):
@@ -77,9 +93,11 @@ def init_rank(cfg, max_bytes: int, max_lines: int, comm: str = "rccl", timeout: 
     if cfg.world != world:
         raise ValueError(f"DistConfig.world={cfg.world} but WORLD_SIZE={world}")
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    return _C.DistRank(cfg, rank, comm, host, bootstrap_port(rank, world), max_bytes,
-                       max_lines, timeout)
+    dr = _C.DistRank(cfg, rank, comm, host, bootstrap_port(rank, world), max_bytes,
+                     max_lines, timeout)
+    release_bootstrap_port()  # every rank connected inside the constructor
+    return dr
 
 
 __all__ = ["Host", "load_hosts", "parse_hosts", "launch_local", "launch_remote",
-           "stage_split_wordcount", "init_rank", "bootstrap_port"]
+           "stage_split_wordcount", "init_rank", "bootstrap_port", "release_bootstrap_port"]
