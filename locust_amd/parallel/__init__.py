@@ -44,14 +44,17 @@ def bootstrap_port(rank: int | None = None, world: int | None = None,
         import tempfile
         import time
 
-        path = os.path.join(tempfile.gettempdir(),
-                            f"locust_port_{master}_{os.getppid()}_{os.getuid()}")
+        # a per-user directory when there is one; in a shared /tmp a reader only trusts a
+        # file this user owns and nobody else can write
+        base = os.environ.get("XDG_RUNTIME_DIR") or tempfile.gettempdir()
+        path = os.path.join(base, f"locust_port_{master}_{os.getppid()}_{os.getuid()}")
         if rank == 0:
             with socket.socket() as s:  # released just before the communicator binds it
                 s.bind((host, 0))
                 port = s.getsockname()[1]
             tmp = f"{path}.{os.getpid()}"
-            with open(tmp, "w") as f:
+            fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+            with os.fdopen(fd, "w") as f:
                 f.write(str(port))
             os.replace(tmp, path)  # readers never see a partial file
             _port_file = path
@@ -59,11 +62,13 @@ def bootstrap_port(rank: int | None = None, world: int | None = None,
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:
             try:
-                with open(path) as f:
+                fd = os.open(path, os.O_RDONLY | os.O_NOFOLLOW)
+                with os.fdopen(fd) as f:
+                    st = os.fstat(f.fileno())
                     txt = f.read().strip()
-                if txt:
+                if txt and st.st_uid == os.getuid() and not st.st_mode & 0o022:
                     return int(txt)
-            except FileNotFoundError:
+            except (FileNotFoundError, OSError):
                 pass
             time.sleep(0.005)
         raise TimeoutError(f"rank {rank}: no bootstrap port from rank 0 in {path} "
