@@ -46,7 +46,9 @@ def bootstrap_port(rank: int | None = None, world: int | None = None,
 
         # a per-user directory when there is one; in a shared /tmp a reader only trusts a
         # file this user owns and nobody else can write
-        base = os.environ.get("XDG_RUNTIME_DIR") or tempfile.gettempdir()
+        base = os.environ.get("XDG_RUNTIME_DIR", "")
+        if not (base and os.path.isdir(base) and os.access(base, os.W_OK)):
+            base = tempfile.gettempdir()
         path = os.path.join(base, f"locust_port_{master}_{os.getppid()}_{os.getuid()}")
         if rank == 0:
             with socket.socket() as s:  # released just before the communicator binds it
