@@ -11,12 +11,20 @@ and D2H of the sorted (key, val, count) results -- the reference's timed stages
 GTX 1060 (README.md:72-88): 4,500-line whole-Hamlet LDS-reduce total 77.393 ms, 700-line
 total 29.405 ms.
 
-N = 1: one process, one GPU.  N > 1 (launched by torch.distributed.run, one process per
-GPU, RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT from the env): weak scaling --
-every rank maps its own copy of the text, then the ranks range-partition and shuffle the
-map output with one RCCL all-to-all-v over xGMI, reduce their key range and gather the
-globally sorted result on rank 0.  Steps are timed between barriers with the device
-synchronised on both sides; the MAX over ranks is reported.
+Ranks.  N = 1: one process, one GPU.  N > 1: one process per GPU, RANK / WORLD_SIZE /
+LOCAL_RANK / MASTER_ADDR / MASTER_PORT from the env -- either set by
+``torch.distributed.run`` or, when ``--gpus N`` is given without a launcher, by this script
+itself: the parent starts N child rank processes (never an exec, before any GPU call of
+its own), relays rank 0's JSON line and fails if any rank fails.  A rank that cannot get a
+GPU of its own fails the run: a job never silently reports fewer GPUs than asked for.
+
+Headline (``value``): whole Hamlet, weak scaling -- every rank maps its own copy of the
+text, the ranks merge their combined (key, count) records on rank 0 (the gather strategy:
+one all-gather of device-written slots, one root merge).  The ``synth1m`` extra, at every
+N including 1, is BASELINE config 4 as strong scaling: 1M synthetic lines in total, 1/N per
+rank, range-partitioned by sample-sort splitters and exchanged with one fixed-slot
+``ncclAllToAll`` over xGMI, so N = 1, 2, 4, 8 form one curve.  Steps are timed between
+barriers with the device synchronised on both sides; the MAX over ranks is reported.
 
 This process never imports torch: the engine drives HIP/RCCL directly (torch's bundled
 HIP runtime must not be loaded next to the system one).
@@ -52,8 +60,8 @@ CHUNK_BYTES = 256 << 20  # one device pass; larger shards stream
 
 def chunk_bytes_for(nbytes: int) -> int:
     """Device pass size: inputs up to 256 MiB are ONE pass (the engine uploads them in
-    line-aligned 4 MiB pieces, each mapped as it lands, and aggregates on the two-kernel
-    ordered build); larger ones stream in 256 MiB chunks (PCIe-bound)."""
+    line-aligned pieces, each mapped as it lands, and aggregates on the two-kernel ordered
+    build); larger ones stream in 256 MiB chunks (PCIe-bound)."""
     return CHUNK_BYTES
 
 
@@ -67,20 +75,26 @@ def load_text(config: str) -> bytes:
     return hamlet
 
 
-def synth_shard(config: str, rank: int, world: int):
+def synth_shard(config: str, rank: int, world: int, lines: int | None = None):
     """This rank's part of the synthetic text, generated straight into pinned memory
     (strong scaling: the total is fixed, each of the N ranks owns 1/N of it)."""
     import locust_amd as lc
 
-    spec = SYNTH[config]
+    spec = dict(SYNTH[config])
+    if lines:
+        spec = {"lines": lines, "bytes": 0}
     if spec["lines"]:
         total_blocks = -(-spec["lines"] // 1024)
         b0, b1 = rank * total_blocks // world, (rank + 1) * total_blocks // world
-        lines = min(spec["lines"], b1 * 1024) - b0 * 1024
-        return lc._C.HostText.generate(lines=lines, seed=1, first_block=b0)
+        nl = min(spec["lines"], b1 * 1024) - b0 * 1024
+        return lc._C.HostText.generate(lines=max(nl, 0), seed=1, first_block=b0)
     per = spec["bytes"] // world
     first = rank * -(-per // (1024 * 30))  # blocks are ~44 KB: shards never overlap
     return lc._C.HostText.generate(bytes=per, seed=1, first_block=first)
+
+
+def _nlines(text: bytes) -> int:
+    return text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
 
 
 def bench_single(text, steps: int, warmup: int, sort: str = "dict", graph: int = -1):
@@ -101,8 +115,7 @@ def ref_semantics(text: bytes, steps: int = 50, warmup: int = 5):
     import locust_amd as lc
 
     cfg = lc.make_config("gpu", reduce_path="lds", graph=0, ref_timers=True)
-    nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
-    eng = lc._C.GpuEngine(cfg, len(text), nlines)
+    eng = lc._C.GpuEngine(cfg, len(text), _nlines(text))
     eng.load(text)
     for _ in range(warmup):
         eng.run_loaded()
@@ -136,15 +149,15 @@ def cpu_path(text: bytes, steps: int = 20, warmup: int = 3) -> dict:
     return {k: round(statistics.median(v), 4) for k, v in acc.items()}
 
 
-def cold_first_run(text: bytes) -> dict:
-    """A fresh engine's first job (allocation excluded, first launches/captures included):
-    the regime of the reference's numbers, which include Thrust's first-call overhead."""
+def cold_first_run(text) -> dict:
+    """A fresh engine's first job (allocation excluded, first launches included): the
+    regime of the reference's numbers, which include Thrust's first-call overhead -- and of
+    every `./MapReduce <file>` invocation, which runs one job per process."""
     import locust_amd as lc
 
     if isinstance(text, bytes):
         cfg = lc.make_config("gpu", reduce_path="lds")
-        nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
-        eng = lc._C.GpuEngine(cfg, len(text), nlines)
+        eng = lc._C.GpuEngine(cfg, len(text), _nlines(text))
         eng.load(text)
         run = eng.run_loaded
     else:  # HostText: the synthetic configs (a cold partition map on a large vocabulary)
@@ -166,8 +179,7 @@ def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
     cfg = lc.make_config("gpu", reduce_path="lds", sort=sort, chunk_bytes=chunk_bytes_for(size),
                          graph=graph)
     if isinstance(text, bytes):
-        nlines = text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
-        eng = lc._C.GpuEngine(cfg, len(text), nlines)
+        eng = lc._C.GpuEngine(cfg, len(text), _nlines(text))
         eng.load(text)
         run = eng.run_loaded
     else:  # HostText (pinned; streamed when larger than one pass)
@@ -192,41 +204,64 @@ def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
     return ms, med, res
 
 
-def bench_dist(text: bytes, steps: int, warmup: int, rank: int, world: int, local_rank: int,
-               comm: str = "rccl"):
+def untuned(text: bytes, steps: int, warmup: int) -> dict:
+    """The headline job with the partition map's between-job retuning switched off
+    (LOCUST_PART_TUNE=0): every job balances its partitions from its own map statistics
+    only, like the one job of a `./MapReduce <file>` process."""
+    old = os.environ.get("LOCUST_PART_TUNE")
+    os.environ["LOCUST_PART_TUNE"] = "0"
+    try:
+        ms, _st, _res = _time_single(text, steps, warmup, "dict", -1)
+    finally:
+        if old is None:
+            os.environ.pop("LOCUST_PART_TUNE", None)
+        else:
+            os.environ["LOCUST_PART_TUNE"] = old
+    return {"ms_per_step": round(ms, 4)}
+
+
+# ---------------------------------------------------------------------------------------
+# multi-rank
+# ---------------------------------------------------------------------------------------
+def dist_rank(text, world: int, rank: int, local_rank: int, comm: str, backend: str):
+    """This process's DistRank (communicator + engine for `text`), bootstrapped through
+    rank 0's listening socket (inherited from a launcher, or bound here)."""
     import locust_amd as lc
+    from locust_amd.parallel import connect_rank
 
     # comm="tcp" rehearses the multi-process path with several ranks on one GPU (RCCL
-    # refuses two ranks per device); the benchmark itself always uses RCCL.
+    # refuses two ranks per device); the benchmark itself uses RCCL.
     device = local_rank if comm == "rccl" else 0
-    job = lc.make_config("gpu", device=device, reduce_path="lds", combine=True,
+    job = lc.make_config(backend, device=device, reduce_path="lds", combine=True,
                          chunk_bytes=chunk_bytes_for(len(text) if isinstance(text, bytes)
                                                      else text.size))
     dcfg = lc.make_dist_config(world, job)
-    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    from locust_amd.parallel import bootstrap_port, release_bootstrap_port
-
-    port = bootstrap_port(rank, world)
-    if isinstance(text, bytes):
-        nbytes, nlines = len(text), text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
-    else:
-        nbytes = nlines = max(text.size, 1)
+    nbytes, nlines = _shape(text)
     # RCCL prints its version banner on stdout during init; keep stdout for the one JSON
     # line the driver parses by pointing fd 1 at stderr while the communicator comes up.
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        dr = lc._C.DistRank(dcfg, rank, comm, host, port, nbytes, nlines, 120.0)
-        release_bootstrap_port()  # every rank connected inside the constructor
+        dr = connect_rank(dcfg, rank, world, comm, nbytes, nlines, 120.0)
     finally:
         os.dup2(saved, 1)
         os.close(saved)
+    _load(dr, text)
+    return dr
+
+
+def _shape(text):
+    if isinstance(text, bytes):
+        return max(len(text), 1), max(_nlines(text), 1)
+    return max(text.size, 1), max(text.size, 1)
+
+
+def _load(dr, text) -> None:
     if isinstance(text, bytes):
         dr.load(text, 0)  # the shard sits in the engine's pinned buffer, like a loaded file
     else:
         dr.load_text(text, 0)
-    return dr
 
 
 def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
@@ -255,6 +290,120 @@ def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
     return ms, med, res, info["strategy"]
 
 
+def synth_point(args, rank: int, world: int, dr=None) -> dict:
+    """BASELINE config 4 (1M synthetic lines) as one point of the strong-scaling curve:
+    the total is fixed, this rank owns 1/N of it.  N = 1: the single-GPU engine (a
+    one-rank job is the local pipeline); N > 1: a second engine on the ranks'
+    communicator, exchanged with the sample-sort all-to-all."""
+    t_gen = time.perf_counter()
+    text = synth_shard("synth1m", rank, world, args.synth_lines)
+    gen_s = time.perf_counter() - t_gen
+    steps, warmup = min(args.steps, 20), min(args.warmup, 3)
+    lines = args.synth_lines or SYNTH["synth1m"]["lines"]
+    if dr is None:
+        ms, stages, res = bench_single(text, steps, warmup)
+        strategy, total_bytes = "local", text.size
+    else:
+        nbytes, nlines = _shape(text)
+        dr.use_engine(dr.add_engine(nbytes, nlines))
+        _load(dr, text)
+        ms, stages, res, strategy = time_dist(dr, steps, warmup, "auto")
+        sizes = [0.0] * world
+        total_bytes = int(sum(_allgather_float(dr, float(text.size), sizes)))
+        dr.use_engine(0)
+    return {"lines": lines, "n_gpus": world, "ms_per_step": round(ms, 4),
+            "GB_per_s": round(total_bytes / (ms * 1e-3) / 1e9, 3), "bytes": total_bytes,
+            "strategy": strategy, "tokens": res.num_tokens if rank == 0 else None,
+            "unique": res.num_unique if rank == 0 else None, "gen_s": round(gen_s, 2),
+            "stages_ms": {k: round(v, 4) for k, v in stages.items()}}
+
+
+def _allgather_float(dr, v: float, out: list) -> list:
+    # allreduce_max is the only float collective the binding has: sum via N max-rounds
+    # would be silly; every rank's shard size is the same to within one 1,024-line block,
+    # so rank r's size is gathered by masking: max over ranks of (v if r == me else 0).
+    for r in range(len(out)):
+        out[r] = dr.allreduce_max(v if r == dr.rank else 0.0)
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# self-spawned ranks (--gpus N without a launcher)
+# ---------------------------------------------------------------------------------------
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Start N rank processes of this script and relay rank 0's JSON line.  The parent
+    never touches the GPU (children, never an exec).  The first failing rank stops the
+    run: the others are killed and its exit code is returned."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    boot = socket.socket()  # the bootstrap listener, inherited by rank 0 (no port race)
+    boot.bind(("127.0.0.1", 0))
+    boot.listen(n)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        master_port = s.getsockname()[1]
+    procs = []
+    out0: list[bytes] = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(master_port), LOCUST_PORT=str(boot.getsockname()[1]))
+            env.pop("LOCUST_LISTEN_FD", None)
+            fds: tuple = ()
+            if r == 0:
+                env["LOCUST_LISTEN_FD"] = str(boot.fileno())
+                fds = (boot.fileno(),)
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                          env=env, pass_fds=fds, start_new_session=True,
+                                          stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    finally:
+        boot.close()
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = 0
+    while True:
+        alive = False
+        for r, p in enumerate(procs):
+            rc = p.poll()
+            if rc is None:
+                alive = True
+            elif rc != 0 and not failed:
+                failed = rc if rc > 0 else 128 - rc
+                print(f"bench: rank {r} failed with exit code {rc}", file=sys.stderr)
+        if failed or not alive:
+            break
+        time.sleep(0.05)
+    for p in procs:
+        if p.poll() is None:
+            for sig in (signal.SIGTERM, signal.SIGKILL):
+                try:
+                    os.killpg(p.pid, sig)
+                    p.wait(timeout=5)
+                    break
+                except (ProcessLookupError, subprocess.TimeoutExpired):
+                    continue
+        p.wait()
+    reader.join(timeout=10)
+    if failed:
+        return failed
+    lines = [ln for ln in b"".join(out0).decode(errors="replace").splitlines() if ln.strip()]
+    if not lines:
+        print("bench: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+def visible_gpus() -> int:
+    import locust_amd as lc
+
+    return lc._C.device_count()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,22 +411,40 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="hamlet4500",
                     choices=sorted(BASELINE_MS) + sorted(SYNTH))
-    ap.add_argument("--no-extra", action="store_true", help="skip the 700-line side measurement")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the side measurements (700 lines, radix path, synth1m, ...)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "tcp"],
                     help="communicator for N>1 (tcp: rehearsal with ranks sharing one GPU)")
+    ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"],
+                    help="cpu: rehearse the rank/communicator plumbing with the CPU engine")
     ap.add_argument("--strategy", default="auto", choices=["auto", "shuffle", "gather"],
                     help="N>1: after-map strategy (auto: gather-to-root for small combined "
                          "outputs, sample-sort all-to-all shuffle otherwise)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the distributed path even for one rank")
+    ap.add_argument("--synth-lines", type=int, default=0,
+                    help="lines of the synth1m strong-scaling extra (default 1M; tests)")
     args = ap.parse_args()
+    if args.backend == "cpu" and args.comm == "rccl" and args.gpus > 1:
+        ap.error("--backend cpu needs --comm tcp")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world != 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    n = max(world, 1)
+    if args.gpus != world:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"different GPU count than asked for", file=sys.stderr)
+        return 2
+    n = world
+    if args.backend == "gpu":
+        have = visible_gpus()
+        need = (local_rank + 1) if args.comm == "rccl" else 1
+        if have < need:
+            print(f"bench: rank {rank} needs GPU {need - 1} but {have} visible "
+                  f"(--gpus {n} --comm {args.comm})", file=sys.stderr)
+            return 3
 
     synth = args.config in SYNTH
     if synth:
@@ -288,10 +455,18 @@ def main() -> int:
         nbytes, nlines = text.size, text.lines
     else:
         text = load_text(args.config)
-        nbytes, nlines = len(text), text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
-    extra = {}
+        nbytes, nlines = len(text), _nlines(text)
+    extra: dict = {}
     strategy = None
-    if n == 1 and not args.force_dist:
+    rccl_ranks = None
+    cpu = args.backend == "cpu"
+    if n == 1 and not args.force_dist and cpu:
+        c = cpu_path(text, args.steps, args.warmup)
+        ms, stages = c["wall_ms"], c
+        import locust_amd as lc
+
+        res = lc._C.cpu_run(lc.make_config("cpu"), text)
+    elif n == 1 and not args.force_dist:
         if synth and not args.no_extra:
             extra["cold_start"] = cold_first_run(text)  # before any warm engine exists
         ms, stages, res = bench_single(text, args.steps, args.warmup)
@@ -300,6 +475,7 @@ def main() -> int:
             extra["hamlet700"] = {"ms_per_step": round(ms700, 4), "vs_baseline":
                                   round(ms700 / BASELINE_MS["hamlet700"], 6),
                                   "stages_ms": {k: round(v, 4) for k, v in st700.items()}}
+            extra["untuned"] = untuned(text, args.steps, args.warmup)
             # The reference's own algorithm on the device: sort every token (LSD radix),
             # boundary-mark + compact + adjacent-difference (reported, not the headline).
             msr, str_, _ = bench_single(text, args.steps, args.warmup, sort="radix")
@@ -318,8 +494,10 @@ def main() -> int:
                 "hamlet700_ms": c700, "hamlet4500_ms": cpu_path(text),
                 "baseline_hamlet700_ms": dict(BASELINE_CPU, total_ms=27.132),
                 "vs_baseline_hamlet700": round(c700["wall_ms"] / 27.132, 4)}
+            extra["synth1m"] = synth_point(args, rank, n)
     else:
-        dr = bench_dist(text, args.steps, args.warmup, rank, world, local_rank, args.comm)
+        dr = dist_rank(text, n, rank, local_rank, args.comm, args.backend)
+        rccl_ranks = dr.comm_count if dr.comm_name == "rccl" else None
         ms, stages, res, strategy = time_dist(dr, args.steps, args.warmup, args.strategy)
         if not args.no_extra and args.strategy == "auto" and strategy != "shuffle":
             # The sample-sort all-to-all shuffle on the same job (the path large inputs
@@ -333,6 +511,8 @@ def main() -> int:
             except Exception as e:  # noqa: BLE001
                 print(f"rank {rank}: shuffle extra failed: {e}", file=sys.stderr)
                 extra["shuffle_path"] = {"error": str(e)[:300]}
+        if not args.no_extra and not synth:
+            extra["synth1m"] = synth_point(args, rank, n, dr)
     if rank != 0:
         return 0
     if synth:
@@ -354,7 +534,8 @@ def main() -> int:
         baseline_stages = None
     else:
         base = BASELINE_MS[args.config]
-        data = "hamlet.txt fixture (real text); N>1: every rank maps its own copy"
+        data = ("hamlet.txt fixture (real text); N>1: every rank maps its own copy; "
+                "synth1m extra: synthetic text (native generator, seed 1)")
         model = (f"WordCount {args.config} ({nlines} lines/GPU): byte-parallel map + "
                  "ordered-dictionary Process+Reduce (one kernel: LDS hash aggregate, in-LDS "
                  "sort of distinct keys, look-back val offsets), full H2D->D2H job per step"
@@ -380,7 +561,7 @@ def main() -> int:
             "seq_len": nbytes,
             "parallelism": f"dp{n}" + ("" if strategy is None else
                                        f"+{args.comm}_" + {"gather": "gather_merge",
-                                                           "shuffle": "alltoallv_shuffle",
+                                                           "shuffle": "alltoall_shuffle",
                                                            "local": "one_rank_local"}[strategy]),
         },
         "baseline_ms": round(base, 3),
@@ -388,7 +569,10 @@ def main() -> int:
         "stages_ms_median": {k: round(v, 4) for k, v in stages.items()},
         "tokens": res.num_tokens,
         "unique": res.num_unique,
+        "rccl_ranks": rccl_ranks,
     }
+    if cpu:
+        line["backend"] = "cpu (rehearsal of the rank plumbing; not a GPU number)"
     line.update(extra)
     print(json.dumps(line), flush=True)
     return 0

@@ -12,7 +12,9 @@
 // aborts the communicator instead of hanging.
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstdlib>
+#include <memory>
 #include <cstring>
 #include <thread>
 
@@ -33,9 +35,10 @@ namespace {
 
 class RcclComm final : public Communicator {
  public:
-  RcclComm(int rank, int world, int device, const std::string& host, int port, double timeout_s)
+  RcclComm(int rank, int world, int device, const std::string& host, int port, double timeout_s,
+           int listen_fd)
       : rank_(rank), world_(world), timeout_s_(timeout_s) {
-    tcp_ = make_tcp_comm(rank, world, host, port, timeout_s);
+    tcp_ = make_tcp_comm(rank, world, host, port, timeout_s, listen_fd);
     ncclUniqueId id;
     if (rank == 0) LOCUST_RCCL_CHECK(ncclGetUniqueId(&id));
     std::vector<ncclUniqueId> ids((size_t)world);
@@ -57,8 +60,10 @@ class RcclComm final : public Communicator {
 
   // One rank of a single-process clique (ncclCommInitAll): no TCP bootstrap.  The calling
   // thread drives `device`; every rank of the clique runs on its own thread.
-  RcclComm(ncclComm_t comm, int rank, int world, int device, double timeout_s)
-      : rank_(rank), world_(world), timeout_s_(timeout_s), comm_(comm) {
+  RcclComm(ncclComm_t comm, int rank, int world, int device, double timeout_s,
+           std::shared_ptr<std::atomic<bool>> group_abort)
+      : rank_(rank), world_(world), timeout_s_(timeout_s), group_abort_(std::move(group_abort)),
+        comm_(comm) {
     LOCUST_HIP_CHECK(hipSetDevice(device));
     LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     stage_cap_ = 1 << 20;
@@ -83,6 +88,10 @@ class RcclComm final : public Communicator {
   int rank() const override { return rank_; }
   int size() const override { return world_; }
   const char* name() const override { return "rccl"; }
+  int comm_count() const override {
+    int n = -1;
+    return ncclCommCount(comm_, &n) == ncclSuccess ? n : -1;
+  }
   bool device_buffers() const override { return true; }
 
   void allgather_host(const void* send, void* recv, u64 bytes) override {
@@ -243,6 +252,10 @@ class RcclComm final : public Communicator {
         aborted_ = true;
         throw Error("RCCL operation timed out after " + std::to_string(timeout_s_) + " s");
       }
+      if (group_abort_ && group_abort_->load(std::memory_order_relaxed)) {
+        aborted_ = true;  // another rank of the clique failed: do not wait for it
+        throw Error("RCCL clique aborted: another rank failed");
+      }
       if (++spins > 1000) std::this_thread::yield();
     }
   }
@@ -250,6 +263,7 @@ class RcclComm final : public Communicator {
   int rank_, world_;
   double timeout_s_;
   bool aborted_ = false;
+  std::shared_ptr<std::atomic<bool>> group_abort_;
   std::unique_ptr<Communicator> tcp_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
@@ -264,8 +278,10 @@ class RcclComm final : public Communicator {
 }  // namespace
 
 std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
-                                             const std::string& host, int port, double timeout_s) {
-  return std::unique_ptr<Communicator>(new RcclComm(rank, world, device, host, port, timeout_s));
+                                             const std::string& host, int port, double timeout_s,
+                                             int listen_fd) {
+  return std::unique_ptr<Communicator>(
+      new RcclComm(rank, world, device, host, port, timeout_s, listen_fd));
 }
 
 std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) {
@@ -275,7 +291,9 @@ std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) 
   // one process, one communicator per device: RCCL wires the clique over xGMI itself
   LOCUST_RCCL_CHECK(ncclCommInitAll(comms.data(), n, devices.data()));
   std::vector<RcclCliqueMember> out((size_t)n);
+  auto abort = std::make_shared<std::atomic<bool>>(false);
   for (int r = 0; r < n; ++r) {
+    out[(size_t)r].abort = abort;
     out[(size_t)r].handle = comms[(size_t)r];
     out[(size_t)r].rank = r;
     out[(size_t)r].world = n;
@@ -286,7 +304,13 @@ std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) 
 
 std::unique_ptr<Communicator> make_rccl_clique_comm(const RcclCliqueMember& m, double timeout_s) {
   return std::unique_ptr<Communicator>(
-      new RcclComm(static_cast<ncclComm_t>(m.handle), m.rank, m.world, m.device, timeout_s));
+      new RcclComm(static_cast<ncclComm_t>(m.handle), m.rank, m.world, m.device, timeout_s, m.abort));
+}
+
+void release_rccl_clique_member(RcclCliqueMember& m) {
+  if (!m.handle) return;
+  (void)ncclCommAbort(static_cast<ncclComm_t>(m.handle));
+  m.handle = nullptr;
 }
 
 }  // namespace locust

@@ -120,12 +120,16 @@ sockaddr_in resolve(const std::string& host, int port) {
 
 class TcpComm final : public Communicator {
  public:
-  TcpComm(int rank, int world, const std::string& host, int port, double timeout_s)
+  TcpComm(int rank, int world, const std::string& host, int port, double timeout_s,
+          int listen_fd)
       : rank_(rank), world_(world), fds_((size_t)world, -1) {
     LOCUST_CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+    if (rank == 0 && listen_fd >= 0) listen_fd_ = listen_fd;  // owned from here on
     if (world == 1) return;
-    sockaddr_in addr = resolve(host, port);
-    if (rank == 0) {
+    if (rank == 0 && listen_fd_ >= 0) {
+      // inherited: already bound to `port` and listening (no window for another process)
+    } else if (rank == 0) {
+      sockaddr_in addr = resolve(host, port);
       listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
       int one = 1;
       setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
@@ -133,6 +137,8 @@ class TcpComm final : public Communicator {
         throw Error("tcp comm: bind " + host + ":" + std::to_string(port) + " failed: " +
                     std::strerror(errno));
       ::listen(listen_fd_, world);
+    }
+    if (rank == 0) {
       set_timeouts(listen_fd_, timeout_s);
       for (int i = 1; i < world; ++i) {
         int fd = ::accept(listen_fd_, nullptr, nullptr);
@@ -149,6 +155,7 @@ class TcpComm final : public Communicator {
         fds_[(size_t)r] = fd;
       }
     } else {
+      sockaddr_in addr = resolve(host, port);
       const u64 deadline = now_ns() + (u64)(timeout_s * 1e9);
       int fd = -1;
       for (;;) {
@@ -270,8 +277,8 @@ class TcpComm final : public Communicator {
 }  // namespace
 
 std::unique_ptr<Communicator> make_tcp_comm(int rank, int world, const std::string& host, int port,
-                                            double timeout_s) {
-  return std::unique_ptr<Communicator>(new TcpComm(rank, world, host, port, timeout_s));
+                                            double timeout_s, int listen_fd) {
+  return std::unique_ptr<Communicator>(new TcpComm(rank, world, host, port, timeout_s, listen_fd));
 }
 
 }  // namespace locust

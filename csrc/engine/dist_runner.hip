@@ -25,12 +25,12 @@ int visible_device_count() {
   return n;
 }
 
+// kAuto is the loopback communicator: with a GPU per rank its collectives are peer copies
+// between the ranks' devices over xGMI.  The RCCL clique is opt-in (`--comm rccl`) until a
+// run with real RCCL peers has been recorded on this pool (one-GPU boxes only so far).
 LocalComm resolve_local_comm(const DistConfig& cfg, LocalComm comm) {
   if (cfg.job.backend != Backend::kGpu) return LocalComm::kLoopback;
-  if (comm != LocalComm::kAuto) return comm;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess) return LocalComm::kLoopback;
-  return cfg.job.device + cfg.world <= ndev ? LocalComm::kRccl : LocalComm::kLoopback;
+  return comm == LocalComm::kAuto ? LocalComm::kLoopback : comm;
 }
 
 std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig>& schedule,
@@ -64,6 +64,8 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
     clique = make_rccl_clique(devs);
   }
   LoopbackGroup group(P, gpu);
+  // clique members whose handle a rank has wrapped (the wrapper owns it from then on)
+  std::vector<char> wrapped((size_t)P, 0);
   std::vector<DistResult> results(schedule.size());
   std::vector<std::exception_ptr> errors((size_t)P);
   std::vector<int> error_order((size_t)P, 0);
@@ -74,15 +76,20 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
       try {
         JobConfig job = cfg.job;
         job.device = gpu ? (cfg.job.device + r) % ndev : 0;
-        if (rccl) LOCUST_HIP_CHECK(hipSetDevice(job.device));
+        std::unique_ptr<Communicator> comm;
+        if (rccl) {
+          LOCUST_HIP_CHECK(hipSetDevice(job.device));
+          comm = make_rccl_clique_comm(clique[(size_t)r]);  // owns the handle from here on
+          wrapped[(size_t)r] = 1;
+        } else {
+          comm = group.comm(r);
+        }
         // Ranks are threads of one process here: no stream capture while other ranks may
         // allocate or copy (hipGraph replay is for one-process-per-GPU runs).
         if (P > 1) job.graph = 0;
         std::unique_ptr<ShardEngine> eng =
             gpu ? make_gpu_shard_engine(job, shards[(size_t)r].bytes, shards[(size_t)r].num_lines)
                 : make_cpu_shard_engine(job);
-        std::unique_ptr<Communicator> comm =
-            rccl ? make_rccl_clique_comm(clique[(size_t)r]) : group.comm(r);
         // the same engines and communicators across jobs, like a long-lived rank
         for (size_t j = 0; j < schedule.size(); ++j) {
           DistResult d = run_distributed(schedule[j], *comm, *eng, shards[(size_t)r]);
@@ -92,11 +99,14 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
         errors[(size_t)r] = std::current_exception();
         error_order[(size_t)r] = ++error_seq;
         group.abort();  // ranks waiting in a collective fail now instead of timing out
-        // (RCCL ranks: their waits poll ncclCommGetAsyncError and time out)
+        // RCCL clique: every member's wait sees the flag and aborts its communicator
+        if (rccl) clique[(size_t)r].abort->store(true);
       }
     });
   }
   for (auto& t : threads) t.join();
+  for (int r = 0; r < P && rccl; ++r)
+    if (!wrapped[(size_t)r]) release_rccl_clique_member(clique[(size_t)r]);
   // report the root cause: the first rank that failed, not the ones that were woken up
   int first = -1;
   for (int r = 0; r < P; ++r)

@@ -129,6 +129,16 @@ struct DevicePipeline {
   u64 sync_bytes = 0;
   MapCounters* d_ctr = nullptr;
   LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{}, lb_dict{};
+  // the fast map's per-partition token totals (kDictParts, zeroed with the sync block; the
+  // self-cleaning ordered kernel re-zeroes them): the in-job workgroup plan's statistics
+  u32* d_part_tot = nullptr;
+  // LOCUST_VPLAN=0 (read at construction): the ordered kernel keeps one workgroup per map
+  // partition (A/B of the in-job plan)
+  const bool vplan = [] {
+    const char* e = std::getenv("LOCUST_VPLAN");
+    return !e || e[0] != '0';
+  }();
+  bool tot_ready = false;  // the current pass's map wrote d_part_tot
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {
@@ -233,7 +243,8 @@ struct DevicePipeline {
     dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
                       ucap * 4;
     const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
-    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1);
+    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1) +
+                 4 * kDictParts;  // + the map's per-partition totals (d_part_tot)
 
     SizingPlan sz;
     sz.add<char>(cap_bytes + 64);
@@ -332,6 +343,8 @@ struct DevicePipeline {
     lb_scan = {st, counters + 4};
     st += t_scan;
     lb_dict = {st, counters + 5};
+    st += kDictParts + 1;
+    d_part_tot = reinterpret_cast<u32*>(st);
 
     rx.cap = cap;
     rx.tile_counters = arena.take<u32>(rx_zero_words);
@@ -768,6 +781,7 @@ struct DevicePipeline {
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
     part_tiles = cfg.map_path != MapPath::kFast ? 0u : pieces.empty() ? table_tiles(in.bytes)
                                                                          : piece_tiles();
+    tot_ready = vplan && !large_ordered && pieces.empty() && part_tiles > 0;  // as enqueue_map
     LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
   }
   bool use_zero_copy(const TextInput& in) const {
@@ -778,6 +792,7 @@ struct DevicePipeline {
 
   void enqueue_map(const TextInput& in) {
     parts_ready = cfg.map_path == MapPath::kFast;
+    tot_ready = false;
     partial_nslots = 0;
     // combining needs the 4 KiB grouped map: upload pieces, or one launch past kMapLargeInput
     map_combined = combine_map && large_ordered && cfg.map_path == MapPath::kFast &&
@@ -837,10 +852,12 @@ struct DevicePipeline {
       if (agg) partial_nslots = (u32)pieces.size();
     } else {
       part_tiles = table_tiles(in.bytes);
+      tot_ready = vplan && !large_ordered && part_tiles > 0;
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                       stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
-                      map_combined ? d_counts : nullptr);
+                      map_combined ? d_counts : nullptr,
+                      tot_ready ? d_part_tot : nullptr);
     }
   }
 
@@ -1006,6 +1023,7 @@ struct DevicePipeline {
     if (part_tiles && parts_ready && !with_counts) {
       ex.part_off = d_part_off;
       ex.part_tiles = part_tiles;
+      if (tot_ready) ex.part_tot = d_part_tot;
     }
   }
   // Fills the self-clean fields of an OrderedExtra (see OrderedExtra::self_clean).
@@ -1014,6 +1032,7 @@ struct DevicePipeline {
     ex.map_lb = lb_map;
     ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
     ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
+    ex.part_tot_zero = d_part_tot;
   }
   // Device view of this pipeline's partition map (tables live at fixed addresses, so
   // captured graphs stay valid when the host retunes the contents).
@@ -1046,6 +1065,9 @@ struct DevicePipeline {
     if (!n) return;
     PartMapTables t;
     const u64 pred = part_map_from_entries(e, n, &t);
+    // The same map again (e.g. one first word with more distinct keys than an LDS table:
+    // no cut can split it): a new upload would change nothing, so keep it.
+    if (std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;
     retune_with(~0ull / 8, pred, t);
   }
   void maybe_retune(const WordCountEntry* e, u64 n) {
@@ -1070,7 +1092,9 @@ struct DevicePipeline {
       e[i].val = 0;
     }
     PartMapTables t;
-    retune_with(mx, part_map_from_entries(e.data(), n, &t), t);
+    const u64 pred = part_map_from_entries(e.data(), n, &t);
+    if (force && std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;  // as force_retune
+    retune_with(mx, pred, t);
   }
   void retune_with(u64 mx, u64 pred, const PartMapTables& t) {
     if (!pred || pred * 5 >= mx * 4) {  // < 20 % better: keep the map, stop asking

@@ -8,8 +8,10 @@
 //   map_local      tokenize its byte-range shard, sort, optionally combine (sum counts)
 //   sample         S evenly spaced local keys -> allgather -> P-1 splitters (sample sort)
 //   partition      lower_bound of each splitter in the sorted local records
-//   shuffle        all-to-all of bucket sizes, then ONE all-to-all-v of 40-B KeyCount
-//                  records (RCCL grouped send/recv over xGMI: every link busy at once)
+//   shuffle        40-B KeyCount records over xGMI, every link busy at once: grouped
+//                  ncclSend/ncclRecv with exact bucket sizes, or (steady state, see
+//                  locust/exch.hpp) ONE fixed-slot ncclAllToAll padded to the previous
+//                  job's largest bucket
 //   reduce         sort received records, weighted head-mark + adjacent difference
 //   offsets        allgather of per-rank token totals -> global `val` = exclusive prefix
 //   gather         rank 0 receives every rank's entries in rank order (== key order)
@@ -30,6 +32,7 @@
 //             Decided from the first allgather, so every rank takes the same branch.
 #pragma once
 
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <string>
@@ -87,27 +90,38 @@ class Communicator {
   // Status agreement: every rank contributes `local_error` (0 = ok); returns the lowest
   // failing rank or -1.  One allgather of 4 bytes per rank.
   int agree(int local_error);
+  // Ranks the data-plane library itself reports (RCCL: ncclCommCount), else size().
+  virtual int comm_count() const { return size(); }
 };
 
 // Star-topology TCP communicator (rank 0 relays).  Control plane for everything and the
 // data plane of the CPU backend; also the bootstrap channel for RCCL unique ids.
+// listen_fd (rank 0, optional): a socket already bound to `port` and listening -- handed
+// over by the launcher so no other process can take the port between its choice and the
+// bind (the communicator owns and closes it).
 std::unique_ptr<Communicator> make_tcp_comm(int rank, int world, const std::string& host, int port,
-                                            double timeout_s = 120.0);
+                                            double timeout_s = 120.0, int listen_fd = -1);
 // RCCL communicator for one GPU per rank; bootstraps its ncclUniqueId over TCP.
 std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
                                              const std::string& host, int port,
-                                             double timeout_s = 300.0);
+                                             double timeout_s = 300.0, int listen_fd = -1);
 
 // Single-process RCCL clique (`ncclCommInitAll` over the node's GPUs):
 // make_rccl_clique creates one communicator per device from the calling thread; each
 // rank's thread then wraps its member (make_rccl_clique_comm sets that thread's device).
+// `abort` (shared by the clique): set when any rank fails; every member's wait then
+// throws at once and its communicator is aborted (ncclCommAbort) instead of destroyed, so
+// peers blocked on the failed rank fail fast rather than after the timeout.
 struct RcclCliqueMember {
   void* handle = nullptr;  // ncclComm_t
   int rank = 0, world = 1, device = 0;
+  std::shared_ptr<std::atomic<bool>> abort;
 };
 std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices);
 std::unique_ptr<Communicator> make_rccl_clique_comm(const RcclCliqueMember& m,
                                                     double timeout_s = 300.0);
+// A member whose handle was never wrapped (its rank failed first): abort it.
+void release_rccl_clique_member(RcclCliqueMember& m);
 
 // N virtual ranks inside one process (threads).  With device buffers the all-to-all is
 // done with hipMemcpyAsync between the ranks' buffers, so a single GPU can rehearse the

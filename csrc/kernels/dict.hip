@@ -24,6 +24,7 @@
 //   scan_pack     exclusive scan of the counts with decoupled look-back -> val, and the
 //                 final (key, val, count) records for the D2H.
 #include <algorithm>
+#include <type_traits>
 
 #include "locust/device/hash.hpp"
 #include "locust/device/lds_radix.hpp"
@@ -256,10 +257,13 @@ __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 
 // round (the tokens were written by the map on other XCDs: these are L2 misses).  Longer
 // keys' further words are rare (English words fit in 8 bytes) and gathered after.
 constexpr int kGatherBatch = 4;
+// [rlo, rhi) (rlast: no upper bound): only keys whose first word lies in the range are
+// inserted (a virtual partition's share of its map partition; the default takes all).
 template <int kGatherBatch = kGatherBatch>
 __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* counts,
                                               const u32* s_list, u32 lim, u32 n_cap,
-                                              LdsSlot* s_tab) {
+                                              LdsSlot* s_tab, u64 rlo = 0, u64 rhi = ~0ull,
+                                              bool rlast = true) {
   bool full = false;
   for (u32 e0 = 0; e0 < lim; e0 += kGatherBatch * kPartBlock) {
     u32 idx[kGatherBatch];
@@ -277,6 +281,9 @@ __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* co
       c[r] = ok ? (counts ? counts[idx[r]] : 1ull) : 0;
       k[r][1] = k[r][2] = k[r][3] = 0;
     }
+#pragma unroll
+    for (int r = 0; r < kGatherBatch; ++r)  // outside the range: neither gathered nor inserted
+      if (k[r][0] < rlo || (!rlast && k[r][0] >= rhi)) k[r][0] = 0;
 #pragma unroll
     for (int r = 0; r < kGatherBatch; ++r)
       if (k[r][0] & 0xffull) k[r][1] = tokens.w[1][idx[r]];
@@ -417,6 +424,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
 // run kCtrDictOverflow; the host then reruns the Process stage on the HBM-table path.
 // ---------------------------------------------------------------------------------
 constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
+constexpr u32 kSplitMinTokens = 128;           // planned workgroups: tokens per extra sibling
 constexpr u32 kRankChunk = 8;                  // candidates per rank work item
 constexpr u32 kSmallRank = 256;                // partitions up to here: all-pairs ranks
 __device__ __forceinline__ u32 div_up_u32(u32 a, u32 b) { return (a + b - 1) / b; }
@@ -644,6 +652,97 @@ struct TileSource {
     }
     return full;
   }
+  // Virtual partition j of K over map partition p (n_p tokens): the key range between the
+  // j-th and (j+1)-th K-quantile of a sample of the partition's tokens.  The sample is
+  // taken at fixed positions of the partition's tokens in tile order (a block scan of the
+  // runs, not the list's atomic order), so all K siblings draw the same sample, sort it
+  // the same way and agree on every cut: each key lands in exactly one sibling.  The
+  // siblings then all walk the partition's runs but insert only their own range.
+  static constexpr u32 kSplitSamples = 256;
+  __device__ bool build_split(u32 p, u32 j, u32 K, u32 n_p, LdsSlot* s_tab, u32* s_list,
+                              u32& s_count, u32* s_scan, u64* stamp) const {
+    u32* s_sidx = s_list + kPartWindow - 1280;                      // [256] sample tokens
+    u64* s_samp = reinterpret_cast<u64*>(s_list + kPartWindow - 1024);  // [256]
+    u64* s_sort = reinterpret_cast<u64*>(s_list + kPartWindow - 512);   // [256]
+    const u32 S = n_p < kSplitSamples ? n_p : kSplitSamples;
+    u32 a0 = 0, len0 = 0;  // this thread's round-0 run, kept for the inserts
+    u32 base = 0;
+    for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
+      const u32 t = t0 + threadIdx.x;
+      u32 a = 0, len = 0;
+      if (t < ntiles) {
+        a = part_off[(u64)t * kPartTable + p];
+        len = part_off[(u64)t * kPartTable + p + 1] - a;
+      }
+      if (t0 == 0) {
+        a0 = a;
+        len0 = len;
+      }
+      u32 tot = 0;
+      const u32 ex = base + dev::block_exclusive_scan<u32, kPartBlock>(len, s_scan, &tot);
+      if (len && S) {  // samples i at q_i = floor(i * n_p / S) inside [ex, ex + len)
+        for (u32 i = (u32)(((u64)ex * S + n_p - 1) / n_p); i < S; ++i) {
+          const u32 q = (u32)((u64)i * n_p / S);
+          if (q >= ex + len) break;
+          s_sidx[i] = a + (q - ex);
+        }
+      }
+      base += tot;
+    }
+    __syncthreads();
+    if (threadIdx.x < S) {
+      const u32 idx = s_sidx[threadIdx.x];
+      s_samp[threadIdx.x] = idx < n_cap ? tokens.w[0][idx] : 0ull;
+    }
+    __syncthreads();
+    if (threadIdx.x < S) {  // rank = sorted position (ties by sample index)
+      const u64 w = s_samp[threadIdx.x];
+      u32 r = 0;
+      for (u32 k = 0; k < S; ++k) {
+        const u64 o = s_samp[k];
+        r += (o < w || (o == w && k < threadIdx.x)) ? 1u : 0u;
+      }
+      s_sort[r] = w;
+    }
+    __syncthreads();
+    const bool last = j + 1 >= K;
+    const u64 lo = j == 0 || !S ? 0ull : s_sort[(u64)j * S / K];
+    const u64 hi = last || !S ? ~0ull : s_sort[(u64)(j + 1) * S / K];
+    __syncthreads();  // the sample area is list space again
+    if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
+    bool full = false;
+    if (lo == hi && !last) return false;  // an empty range (a hot first word took it)
+    for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
+      const u32 t = t0 + threadIdx.x;
+      u32 a = a0, len = len0;
+      if (t0 != 0) {
+        a = len = 0;
+        if (t < ntiles) {
+          a = part_off[(u64)t * kPartTable + p];
+          len = part_off[(u64)t * kPartTable + p + 1] - a;
+        }
+      }
+      {
+        const u32 incl = dev::wave_inclusive_scan(len);
+        u32 wbase = 0;
+        if (dev::lane_id() == 63 && incl) wbase = atomicAdd(&s_count, incl);
+        wbase = (u32)__shfl((int)wbase, 63, 64);
+        u32 at = wbase + incl - len;
+        for (u32 k = 0; k < len; ++k, ++at)
+          if (at < (u32)kPartWindow) s_list[at] = a + k;
+      }
+      __syncthreads();
+      const u32 cnt = s_count;
+      full |= cnt > (u32)kPartWindow;
+      full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab, lo,
+                            hi, last);
+      __syncthreads();
+      if (threadIdx.x == 0) s_count = 0;
+      __syncthreads();
+    }
+    if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
+    return full;
+  }
 };
 
 // Token source of the gather-strategy merge: runs of KeyCount records, each sorted by
@@ -854,7 +953,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
 #define ORD_STAMP(k_)                                                          \
-  if (trace && threadIdx.x == 0) trace[(u64)p * 32 + (k_)] = __builtin_amdgcn_s_memtime()
+  if (trace && threadIdx.x == 0) trace[(u64)v * 32 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
   __shared__ __attribute__((aligned(16))) u32 s_list[kPartWindow];  // later: sort arrays
   __shared__ u32 s_count;
@@ -873,19 +972,78 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   // workgroups whose predecessors were never dispatched: measured as multi-second stalls
   // and a hang with four ranks on one GPU.
   const u64 rt_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, device-wide
+  // v: this workgroup's virtual partition = its ticket (the look-back order); p: the map
+  // partition whose tokens it reads; (vj, vk): its share of p (see OrderedExtra::part_tot).
+  // Without a plan, v == p and vk == 1.
+  constexpr bool kTiles = std::is_same<Src, TileSource>::value;
+  const bool vplan = kTiles && ex.part_tot != nullptr;
+  __shared__ u32 s_vpre[kDictParts + 1];  // exclusive prefix of the workgroups per partition
+  __shared__ u32 s_vred[8];
+  u32 tp = 0;  // (plan) this thread's partition's tokens, loaded before the ticket
+  if (vplan && threadIdx.x < kDictParts) tp = ex.part_tot[threadIdx.x];
   // Tickets almost always come out in dispatch order: prefetch the run table for
   // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.
-  const typename Src::Pre guess = src.prefetch(blockIdx.x);
-  const u32 p = dev::acquire_tile(tile_ctr, &s_tile);
+  const typename Src::Pre guess = vplan ? typename Src::Pre{} : src.prefetch(blockIdx.x);
+  u32 v, p, vj = 0, vk = 1, np = 0;
+  if (!vplan) {
+    v = p = dev::acquire_tile(tile_ctr, &s_tile);
+  } else {
+    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    if (threadIdx.x < kDictParts) {
+      const u64 nz = dev::ballot(tp != 0);
+      const u32 tsum = dev::wave_reduce_sum(tp);
+      if (dev::lane_id() == 0) {
+        s_vred[dev::wave_id()] = (u32)__popcll(nz);
+        s_vred[4 + dev::wave_id()] = tsum;
+      }
+    }
+    __syncthreads();
+    v = s_tile;
+    const u32 E = s_vred[0] + s_vred[1] + s_vred[2] + s_vred[3];
+    const u32 T = s_vred[4] + s_vred[5] + s_vred[6] + s_vred[7];
+    // workgroups of partition q: 1 + its token share of the idle ones (at least
+    // kSplitMinTokens tokens per extra one); the sum is at most kDictParts
+    u32 K = 0;
+    if (tp) {
+      const u32 extra = (u32)((u64)tp * (u32)(kDictParts - E) / T);
+      K = 1u + min(extra, tp / kSplitMinTokens);
+    }
+    u32 kinc = 0;
+    if (threadIdx.x < kDictParts) {
+      kinc = dev::wave_inclusive_scan(K);
+      if (dev::lane_id() == 63) s_vred[dev::wave_id()] = kinc;
+    }
+    __syncthreads();
+    if (threadIdx.x < kDictParts) {
+      u32 off = 0;
+      for (int i = 0; i < dev::wave_id(); ++i) off += s_vred[i];
+      s_vpre[threadIdx.x] = off + kinc - K;
+      if (threadIdx.x == kDictParts - 1) s_vpre[kDictParts] = off + kinc;
+    }
+    __syncthreads();
+    const u32 V = s_vpre[kDictParts];
+    // the map partition holding v: the last q with s_vpre[q] <= v (s_vpre[256] = V > v)
+    p = 0;
+    vk = 0;  // v >= V: an idle workgroup -- an empty virtual partition in the chain
+    if (v < V) {
+#pragma unroll
+      for (u32 step = kDictParts / 2; step; step >>= 1)
+        if (s_vpre[p + step] <= v) p += step;
+      vj = v - s_vpre[p];
+      vk = s_vpre[p + 1] - s_vpre[p];
+      np = ex.part_tot[p];
+    }
+  }
   ORD_STAMP(0);
   if (trace && threadIdx.x == 0) {
-    trace[(u64)p * 32 + 10] = rt_entry;
-    trace[(u64)p * 32 + 16] = 0;
-    trace[(u64)p * 32 + 17] = ~0ull;
-    trace[(u64)p * 32 + 18] = 0;
-    trace[(u64)p * 32 + 19] = 0;
+    trace[(u64)v * 32 + 10] = rt_entry;
+    trace[(u64)v * 32 + 16] = 0;
+    trace[(u64)v * 32 + 17] = ~0ull;
+    trace[(u64)v * 32 + 18] = 0;
+    trace[(u64)v * 32 + 19] = 0;
   }
-  const typename Src::Pre first = p == blockIdx.x ? guess : src.prefetch(p);
+  const typename Src::Pre first =
+      vplan ? (vk == 1 ? src.prefetch(p) : typename Src::Pre{}) : p == blockIdx.x ? guess : src.prefetch(p);
   // The in-partition counting sort of a large partition buckets keys by the 8 bits of
   // (w0 - wlo) just below the width of [wlo, whi], the first words actually present: 256
   // order-preserving buckets -- the second byte for keys sharing a first byte, finer bytes
@@ -913,7 +1071,16 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   __syncthreads();
   ORD_STAMP(14);  // table cleared
-  const bool full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)p * 32 : nullptr);
+  bool full = false;
+  if constexpr (kTiles) {
+    if (vk > 1)
+      full = src.build_split(p, vj, vk, np, s_tab, s_list, s_count,
+                             reinterpret_cast<u32*>(s_scan), trace ? trace + (u64)v * 32 : nullptr);
+    else if (vk == 1)
+      full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr);
+  } else {
+    full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr);
+  }
   ORD_STAMP(1);
   // ---- compact: dense (w0, slot) arrays in the list area ----
   u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
@@ -977,7 +1144,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
-  if (threadIdx.x == 0) dev::publish_aggregate(status, p, agg);
+  if (threadIdx.x == 0) dev::publish_aggregate(status, v, agg);
   ORD_STAMP(2);
   u64 pre = 0;
   if (small) {
@@ -996,21 +1163,21 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const u32 q = lane + 64u * k;
-        st[k] = q < p ? dev::ld_agent(&status[q]) : dev::kLbAgg;  // beyond p: aggregate 0
+        st[k] = q < v ? dev::ld_agent(&status[q]) : dev::kLbAgg;  // beyond v: aggregate 0
       }
       // unpublished words are re-read together, every round (one round trip per round, not
       // one per group of 64 in turn)
       auto pending = [&]() {
         bool any = false;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) any |= lane + 64u * k < p && (st[k] >> dev::kLbFlagShift) == 0;
+        for (int k = 0; k < 4; ++k) any |= lane + 64u * k < v && (st[k] >> dev::kLbFlagShift) == 0;
         return any;
       };
       if (ex.variant & 8u) {  // A/B: the previous per-group polling
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const u32 q = lane + 64u * k;
-          while (q < p && (st[k] >> dev::kLbFlagShift) == 0) {
+          while (q < v && (st[k] >> dev::kLbFlagShift) == 0) {
             __builtin_amdgcn_s_sleep(1);
             st[k] = dev::ld_agent(&status[q]);
           }
@@ -1021,7 +1188,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const u32 q = lane + 64u * k;
-            if (q < p && (st[k] >> dev::kLbFlagShift) == 0) st[k] = dev::ld_agent(&status[q]);
+            if (q < v && (st[k] >> dev::kLbFlagShift) == 0) st[k] = dev::ld_agent(&status[q]);
           }
         }
       }
@@ -1031,18 +1198,18 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         const u64 b = dev::ballot((st[k] >> dev::kLbFlagShift) == 2);
         if (b) hi_inc = 64 * k + 63 - __clzll((long long)b);
       }
-      u64 v = 0;
+      u64 pv = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int q = (int)lane + 64 * k;
-        if (q >= hi_inc && q < (int)p) v += st[k] & dev::kLbValMask;
+        if (q >= hi_inc && q < (int)v) pv += st[k] & dev::kLbValMask;
       }
-      v = dev::wave_inclusive_scan(v);
-      if (lane == 63) s_prefix = v;
-      if (trace && lane == 0) trace[(u64)p * 32 + 15] = __builtin_amdgcn_s_memtime();  // resolved
+      pv = dev::wave_inclusive_scan(pv);
+      if (lane == 63) s_prefix = pv;
+      if (trace && lane == 0) trace[(u64)v * 32 + 15] = __builtin_amdgcn_s_memtime();  // resolved
     } else if (m > 1) {
       if (trace && dev::lane_id() == 0)  // the first ranking wave's start
-        atomicMin(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 17]),
+        atomicMin(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 17]),
                   (unsigned long long)__builtin_amdgcn_s_memtime());
       // Waves 1..15 split the work as (key group of 64, candidate slice): lane i of its
       // group compares its full key with every candidate of the slice -- the candidates'
@@ -1086,7 +1253,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
           }
         }
         if (trace)
-          atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 18]),
+          atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 18]),
                     (unsigned long long)__builtin_amdgcn_s_memtime());
         if (own && cnt) {
           atomicAdd(&s_rk[i], cnt);
@@ -1094,13 +1261,13 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         }
       }
       if (trace && dev::lane_id() == 0)  // the slowest ranking wave's end
-        atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)p * 32 + 16]),
+        atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 16]),
                   (unsigned long long)__builtin_amdgcn_s_memtime());
     }
     __syncthreads();
     pre = s_prefix;
-    if (threadIdx.x == 0 && p != 0)  // inclusive value for later walkers (large partitions)
-      dev::st_agent(&status[p], dev::kLbInc | (pre + agg));
+    if (threadIdx.x == 0 && v != 0)  // inclusive value for later walkers (large partitions)
+      dev::st_agent(&status[v], dev::kLbInc | (pre + agg));
     ORD_STAMP(3);
     ORD_STAMP(4);
     const u64 base_tok = pre >> kOrdTokShift;
@@ -1330,7 +1497,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   __syncthreads();
   ORD_STAMP(3);
   if (dev::wave_id() == 0) {
-    const u64 e = dev::wave_lookback_resolve(status, p, agg);
+    const u64 e = dev::wave_lookback_resolve(status, v, agg);
     if (dev::lane_id() == 0) s_prefix = e;
   }
   __syncthreads();
@@ -1410,15 +1577,16 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   const u64 base_tok = pre >> kOrdTokShift;
   const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   ORD_STAMP(5);
-  if (trace && threadIdx.x == 0) trace[(u64)p * 32 + 6] = m;
-  if (trace && threadIdx.x == 0) trace[(u64)p * 32 + 11] = __builtin_amdgcn_s_memrealtime();
-  if (ex.part_w && threadIdx.x == 0) {  // this partition's work, for the host's retuning
-    const u64 w = tok + (u64)kPartDistinctWeight * m;
+  if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 6] = m;
+  if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 11] = __builtin_amdgcn_s_memrealtime();
+  if (ex.part_w && threadIdx.x == 0 && vj == 0 && vk > 0) {  // partition work, for the retuning
+    // (a partition split over vk workgroups: its first one's share, times vk)
+    const u64 w = (tok + (u64)kPartDistinctWeight * m) * (vplan ? vk : 1u);
     ex.part_w[p] = (u32)(w < 0xffffffffull ? w : 0xffffffffull);
   }
   // ---- the last partition publishes the run's counters ----
   const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
-  if (p == kDictParts - 1 && threadIdx.x == 0) {
+  if (v == kDictParts - 1 && threadIdx.x == 0) {
     const u32 u = (u32)(base_m + m);
     const u64 total = base_tok + tok;
     ctr->num_unique = u;
@@ -1469,6 +1637,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       if (!(flags & kCtrDictOverflow)) {
         for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
         for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
+        if (ex.part_tot_zero)
+          for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) ex.part_tot_zero[i] = 0;
         if (threadIdx.x == 0) {
           // the accumulated counters; num_unique / total_count are assignments the next
           // run overwrites, and stay readable for what follows this kernel

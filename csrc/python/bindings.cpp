@@ -241,18 +241,32 @@ py::dict dist_to_dict(const DistResult& d) {
 class PyDistRank {
  public:
   PyDistRank(const DistConfig& cfg, int rank, const std::string& comm, const std::string& host,
-             int port, u64 max_bytes, u64 max_lines, double timeout_s)
+             int port, u64 max_bytes, u64 max_lines, double timeout_s, int listen_fd)
       : cfg_(cfg), max_bytes_(max_bytes) {
     py::gil_scoped_release nogil;
     if (comm == "tcp") {
-      comm_ = make_tcp_comm(rank, cfg.world, host, port, timeout_s);
+      comm_ = make_tcp_comm(rank, cfg.world, host, port, timeout_s, listen_fd);
     } else if (comm == "rccl") {
-      comm_ = make_rccl_comm(rank, cfg.world, cfg.job.device, host, port, timeout_s);
+      comm_ = make_rccl_comm(rank, cfg.world, cfg.job.device, host, port, timeout_s, listen_fd);
     } else {
       throw Error("unknown communicator " + comm);
     }
-    eng_ = cfg.job.backend == Backend::kGpu ? make_gpu_shard_engine(cfg.job, max_bytes, max_lines)
-                                            : make_cpu_shard_engine(cfg.job);
+    engines_.push_back(make_engine(max_bytes, max_lines));
+    eng_ = engines_[0].get();
+  }
+  // Another engine on the same communicator (a second input shape, e.g. the synthetic
+  // strong-scaling config next to the Hamlet headline); returns its index for use_engine.
+  // Every rank must add and select engines in the same order.
+  int add_engine(u64 max_bytes, u64 max_lines) {
+    py::gil_scoped_release nogil;
+    engines_.push_back(make_engine(max_bytes, max_lines));
+    return (int)engines_.size() - 1;
+  }
+  void use_engine(int i) {
+    LOCUST_CHECK_ARG(i >= 0 && (size_t)i < engines_.size(), "no such engine");
+    eng_ = engines_[(size_t)i].get();
+    engine_caps_idx_ = i;
+    loaded_ = false;  // load() the new engine's shard
   }
   py::tuple run(const std::string& shard_text_bytes, u64 first_line) {
     TextInput in = as_input(shard_text_bytes, first_line);
@@ -269,7 +283,8 @@ class PyDistRank {
     loaded_in_ = as_input(shard_text_bytes, first_line);
     char* pinned = eng_->input_buffer();
     if (pinned) {
-      LOCUST_CHECK_ARG(shard_text_bytes.size() <= max_bytes_, "shard exceeds engine capacity");
+      LOCUST_CHECK_ARG(shard_text_bytes.size() <= caps_[(size_t)engine_caps_idx_],
+                       "shard exceeds engine capacity");
       if (shard_text_bytes.size() <= cfg_.job.chunk_bytes || !cfg_.job.chunk_bytes) {
         std::memcpy(pinned, shard_text_bytes.data(), shard_text_bytes.size());
         loaded_in_.data = pinned;
@@ -316,13 +331,23 @@ class PyDistRank {
   }
   int rank() const { return comm_->rank(); }
   int size() const { return comm_->size(); }
+  int comm_count() const { return comm_->comm_count(); }
+  std::string comm_name() const { return comm_->name(); }
   void set_strategy(DistStrategy s) { cfg_.strategy = s; }
 
  private:
+  std::unique_ptr<ShardEngine> make_engine(u64 max_bytes, u64 max_lines) {
+    caps_.push_back(max_bytes);
+    return cfg_.job.backend == Backend::kGpu ? make_gpu_shard_engine(cfg_.job, max_bytes, max_lines)
+                                             : make_cpu_shard_engine(cfg_.job);
+  }
   DistConfig cfg_;
   u64 max_bytes_;
   std::unique_ptr<Communicator> comm_;
-  std::unique_ptr<ShardEngine> eng_;
+  std::vector<std::unique_ptr<ShardEngine>> engines_;
+  std::vector<u64> caps_;
+  int engine_caps_idx_ = 0;
+  ShardEngine* eng_ = nullptr;
   bool loaded_ = false;
   std::unique_ptr<HostText> big_;
   std::string loaded_text_;
@@ -517,9 +542,14 @@ PYBIND11_MODULE(_locust, m) {
 
   py::class_<PyDistRank>(m, "DistRank")
       .def(py::init<const DistConfig&, int, const std::string&, const std::string&, int, u64, u64,
-                    double>(),
+                    double, int>(),
            py::arg("cfg"), py::arg("rank"), py::arg("comm"), py::arg("host"), py::arg("port"),
-           py::arg("max_bytes"), py::arg("max_lines"), py::arg("timeout_s") = 300.0)
+           py::arg("max_bytes"), py::arg("max_lines"), py::arg("timeout_s") = 300.0,
+           py::arg("listen_fd") = -1)
+      .def("add_engine", &PyDistRank::add_engine, py::arg("max_bytes"), py::arg("max_lines"))
+      .def("use_engine", &PyDistRank::use_engine)
+      .def_property_readonly("comm_count", &PyDistRank::comm_count)
+      .def_property_readonly("comm_name", &PyDistRank::comm_name)
       .def("run", &PyDistRank::run, py::arg("shard"), py::arg("first_line") = 0)
       .def("load", &PyDistRank::load, py::arg("shard"), py::arg("first_line") = 0)
       .def("run_loaded", &PyDistRank::run_loaded)

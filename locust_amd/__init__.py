@@ -7,7 +7,11 @@ socket-based distributor), re-designed MI355X-first:
   byte-parallel tokenizer, decoupled look-back scans, LSD radix sort on packed keys,
   LDS-staged boundary-mark / adjacent-difference reduce) -- see ``csrc/kernels``.
 * Multi-GPU runs shard the input by bytes, range-partition with sample-sort splitters and
-  shuffle 40-byte records with one RCCL all-to-all-v over xGMI (``csrc/comm``).
+  exchange 40-byte (key, count) records over xGMI (``csrc/comm``): a fixed-slot
+  ``ncclAllToAll`` (every bucket padded to the previous job's largest bucket + 1/8) once a
+  job shape's slot size is known, grouped ``ncclSend``/``ncclRecv`` with exact sizes
+  otherwise; small combined outputs go straight to rank 0 (one ``ncclAllGather`` of
+  device-written slots, one root merge).
 * The reference's ``./MapReduce <file> [start end] [node stage]`` CLI and output format are
   kept byte-for-byte (``build/MapReduce``).
 

@@ -67,18 +67,51 @@ def rank_env(rank: int, local_rank: int, world: int, master_addr: str, master_po
 # --------------------------------------------------------------------------------------
 # mode 1: local ranks
 # --------------------------------------------------------------------------------------
+def bound_listener(addr: str, backlog: int) -> socket.socket:
+    """A listening socket on a free port of `addr`, for the framework's bootstrap: handed
+    to rank 0 (``LOCUST_LISTEN_FD``) so the port is never free between its choice and use."""
+    s = socket.socket()
+    s.bind((addr, 0))
+    s.listen(backlog)
+    return s
+
+
+def spawn_local_ranks(cmd: list[str], nproc: int, master_addr: str = "127.0.0.1",
+                      master_port: int | None = None, extra_env: dict | None = None,
+                      stdout_of_rank0=None) -> list[subprocess.Popen]:
+    """Start `nproc` local rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set;
+    the bootstrap socket bound here and inherited by rank 0).  Child processes, never an
+    exec: the caller may already have initialised the GPU."""
+    port = master_port or _free_port()
+    boot = bound_listener(master_addr, nproc)
+    procs: list[subprocess.Popen] = []
+    try:
+        for r in range(nproc):
+            env = dict(os.environ)
+            env.update(rank_env(r, r, nproc, master_addr, port))
+            env["LOCAL_WORLD_SIZE"] = str(nproc)
+            env["LOCUST_PORT"] = str(boot.getsockname()[1])
+            env.pop("LOCUST_LISTEN_FD", None)
+            fds: tuple = ()
+            if r == 0:
+                env["LOCUST_LISTEN_FD"] = str(boot.fileno())
+                fds = (boot.fileno(),)
+            env.update(extra_env or {})
+            procs.append(subprocess.Popen(cmd, env=env, start_new_session=True, pass_fds=fds,
+                                          stdout=stdout_of_rank0 if r == 0 else None))
+    except BaseException:
+        for p in procs:
+            _kill_group(p)
+        raise
+    finally:
+        boot.close()  # rank 0 holds its own copy
+    return procs
+
+
 def launch_local(cmd: list[str], nproc: int, master_addr: str = "127.0.0.1",
                  master_port: int | None = None, timeout: float | None = None,
                  extra_env: dict | None = None) -> int:
-    port = master_port or _free_port()
-    procs: list[subprocess.Popen] = []
-    for r in range(nproc):
-        env = dict(os.environ)
-        env.update(rank_env(r, r, nproc, master_addr, port))
-        env["LOCAL_WORLD_SIZE"] = str(nproc)
-        env.update(extra_env or {})
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
-    return _supervise(procs, timeout)
+    return _supervise(spawn_local_ranks(cmd, nproc, master_addr, master_port, extra_env), timeout)
 
 
 def _supervise(procs: list[subprocess.Popen], timeout: float | None) -> int:

@@ -1,6 +1,6 @@
 """One rank of a multi-process RCCL WordCount check (real peers, one GPU per rank).
 
-    RANK=r WORLD_SIZE=n LOCAL_RANK=r MASTER_ADDR=127.0.0.1 LOCUST_PORT=p \\
+    python -m locust_amd.parallel.launch --nproc N -- \\
         python -m locust_amd.parallel.rccl_check [--jobs J] [--text FILE]
 
 Every rank maps its own byte-range shard of the text (strong scaling) and runs J jobs per
@@ -30,8 +30,6 @@ def main(argv=None) -> int:
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    port = int(os.environ["LOCUST_PORT"])
 
     import locust_amd as lc
     from locust_amd.utils import oracle
@@ -49,8 +47,10 @@ def main(argv=None) -> int:
     saved = os.dup(1)  # RCCL's banner goes to stdout: keep stdout for the JSON line
     os.dup2(2, 1)
     try:
-        dr = lc._C.DistRank(lc.make_dist_config(world, job), rank, "rccl", host, port,
-                            max(nbytes, 1), max(shard.count(b"\n") + 1, 1), a.timeout)
+        from locust_amd.parallel import connect_rank
+
+        dr = connect_rank(lc.make_dist_config(world, job), rank, world, "rccl", max(nbytes, 1),
+                          max(shard.count(b"\n") + 1, 1), a.timeout)
     finally:
         os.dup2(saved, 1)
         os.close(saved)

@@ -88,12 +88,14 @@ def test_stage_split_gpu_binary(cli, hamlet, tmp_path):
 
 @pytest.mark.parametrize("gpus,comm", [(1, "auto"), (1, "rccl"), (2, "auto"), (3, "loopback")])
 def test_multi_rank_gpu_cli(cli, hamlet, gpus, comm):
-    """--gpus 1 is one RCCL rank (ncclCommInitAll); more ranks than GPUs fall back to
-    loopback ranks sharing the device.  Output byte-identical to one GPU incl. `val`."""
+    """--comm rccl: an ncclCommInitAll clique (one rank per GPU); auto (the default until a
+    run with real RCCL peers is on record) and loopback: ranks as threads, collectives as
+    device copies -- more ranks than GPUs share a device.  Output byte-identical to one GPU
+    incl. `val`."""
     p = subprocess.run([cli, "data/hamlet.txt", "--gpus", str(gpus), "--comm", comm],
                        capture_output=True, timeout=120, env={**__import__("os").environ,
                                                               "LOCUST_LOG": "info"})
     assert p.returncode == 0, p.stderr.decode()
     assert result_lines(p.stdout) == oracle.format_gpu(oracle.wordcount(hamlet)[0])
-    if gpus == 1:
-        assert b"RCCL clique" in p.stderr
+    want = b"RCCL clique" if comm == "rccl" else b"over loopback"
+    assert want in p.stderr

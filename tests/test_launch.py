@@ -156,31 +156,70 @@ def test_stage_split_wordcount_over_daemons(tmp_path, hamlet, cli, capfd):
 
 
 def test_bootstrap_port_from_torchrun_store(tmp_path):
-    """Under torch.distributed.run every rank gets the same bootstrap port, published by
-    rank 0 (a free one) instead of assuming MASTER_PORT + 1 -- without importing torch."""
+    """Under torch.distributed.run rank 0 binds a free port, keeps the socket listening and
+    hands it to the native communicator; the others read the port from the file it
+    publishes -- no window in which another process could take the port, no torch import.
+    The ranks then meet for real (TCP communicator, CPU engine)."""
     script = tmp_path / "port.py"
-    script.write_text("import os, sys\nfrom locust_amd.parallel import bootstrap_port\n"
-                      "p = bootstrap_port()\n"
-                      "print('PORT', os.environ['RANK'], p, 'torch' in sys.modules, flush=True)\n")
+    script.write_text(
+        "import os, sys\n"
+        "import locust_amd as lc\n"
+        "from locust_amd.parallel import bootstrap_listener, connect_rank\n"
+        "w = int(os.environ['WORLD_SIZE'])\n"
+        "dr = connect_rank(lc.make_dist_config(w, lc.make_config('cpu')), int(os.environ['RANK']),"
+        " w, 'tcp', 1, 1, 60.0)\n"
+        "dr.barrier()\n"
+        "from locust_amd import parallel\n"
+        "row = ' '.join(map(str, ['PORT', os.environ['RANK'], dr.size, 'torch' in sys.modules,"
+        " parallel._port_file is None]))\n"
+        "open(sys.argv[1] + '.' + os.environ['RANK'], 'w').write(row)\n")
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     master = s.getsockname()[1]
     s.close()
-    env = {k: v for k, v in os.environ.items() if k != "LOCUST_PORT"}
+    env = {k: v for k, v in os.environ.items() if k not in ("LOCUST_PORT", "LOCUST_LISTEN_FD")}
     env["PYTHONPATH"] = lc.REPO_ROOT + os.pathsep + env.get("PYTHONPATH", "")
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=3", "--master-addr", "127.0.0.1", "--master-port",
-                        str(master), str(script)], env=env, capture_output=True, text=True,
-                       timeout=300)
+                        str(master), str(script), str(tmp_path / "row")], env=env,
+                       capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
-    ports = {ln.split()[1]: int(ln.split()[2]) for ln in p.stdout.splitlines()
-             if ln.startswith("PORT")}
-    assert sorted(ports) == ["0", "1", "2"] and len(set(ports.values())) == 1, p.stdout
-    assert all(ln.split()[3] == "False" for ln in p.stdout.splitlines() if ln.startswith("PORT"))
+    rows = [(tmp_path / f"row.{r}").read_text().split() for r in range(3)]
+    assert sorted(r[1] for r in rows) == ["0", "1", "2"], p.stdout
+    assert all(r[2] == "3" and r[3] == "False" and r[4] == "True" for r in rows), p.stdout
+
+
+def test_bootstrap_stale_port_file_of_previous_attempt(monkeypatch, tmp_path):
+    """A restarted torchrun attempt (same run id, MASTER_PORT and agent) never reads the
+    port file a failed earlier attempt left behind: the restart count names the file."""
+    from locust_amd import parallel
+
+    monkeypatch.setenv("XDG_RUNTIME_DIR", str(tmp_path))
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job-7")
+    monkeypatch.setenv("MASTER_PORT", "31000")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    monkeypatch.delenv("LOCUST_PORT", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    stale = parallel._port_file_path(31000)
+    with open(stale, "w") as f:
+        f.write("1")  # attempt 0 died after publishing a port nobody listens on any more
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    assert parallel._port_file_path(31000) != stale
+    port, fd = parallel.bootstrap_listener(0, 2)
+    try:
+        assert fd >= 0 and port != 1
+        assert parallel.bootstrap_listener(1, 2, timeout=5) == (port, -1)
+        # the listener is really bound and listening on that port
+        c = socket.create_connection(("127.0.0.1", port), timeout=5)
+        c.close()
+    finally:
+        os.close(fd)
+        parallel.release_bootstrap_port()
+    assert not os.path.exists(parallel._port_file_path(31000))
 
 
 def test_bootstrap_port_fixed_rules(monkeypatch):
-    from locust_amd.parallel import bootstrap_port
+    from locust_amd.parallel import bootstrap_listener, bootstrap_port
 
     monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
     monkeypatch.setenv("MASTER_PORT", "31000")
@@ -188,3 +227,24 @@ def test_bootstrap_port_fixed_rules(monkeypatch):
     assert bootstrap_port(0, 4) == 31001
     monkeypatch.setenv("LOCUST_PORT", "32000")
     assert bootstrap_port(1, 4) == 32000
+    # an inherited listener goes to rank 0 only, and only once
+    monkeypatch.setenv("LOCUST_LISTEN_FD", "7")
+    assert bootstrap_listener(1, 4) == (32000, -1)
+    monkeypatch.setenv("LOCUST_LISTEN_FD", "7")
+    assert bootstrap_listener(0, 4) == (32000, 7)
+    assert "LOCUST_LISTEN_FD" not in os.environ
+
+
+def test_launch_local_hands_listener_to_rank0(tmp_path):
+    """launch_local binds the bootstrap socket itself and rank 0 inherits it."""
+    script = tmp_path / "meet.py"
+    script.write_text(
+        "import os\n"
+        "import locust_amd as lc\n"
+        "from locust_amd.parallel import connect_rank\n"
+        "w = int(os.environ['WORLD_SIZE'])\n"
+        "dr = connect_rank(lc.make_dist_config(w, lc.make_config('cpu')), int(os.environ['RANK']),"
+        " w, 'tcp', 1, 1, 60.0)\n"
+        "dr.barrier()\n")
+    env = {"PYTHONPATH": lc.REPO_ROOT}
+    assert launch.launch_local([sys.executable, str(script)], 3, timeout=120, extra_env=env) == 0
