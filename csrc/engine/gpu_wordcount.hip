@@ -23,6 +23,14 @@ char* GpuWordCount::input_buffer() { return impl_->h_text; }
 u64 GpuWordCount::text_capacity() const { return impl_->cap_bytes; }
 
 WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); }
+GpuWordCount::Stats GpuWordCount::stats() const {
+  Stats s;
+  s.retunes = impl_->pm_retunes;
+  s.fallbacks = impl_->fallbacks;
+  s.planned_passes = impl_->planned_passes;
+  s.devplan_failed = impl_->devplan_failed;
+  return s;
+}
 
 std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCountResult* stats) {
   Impl& m = *impl_;

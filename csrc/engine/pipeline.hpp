@@ -82,6 +82,7 @@ struct DevicePipeline {
   // engines whose passes can take the ordered kernel; part_tiles > 0: it describes the
   // current `tokens`.
   u32* d_part_off = nullptr;
+  u32* d_part_occ = nullptr;  // the small map's per-tile partition occupancy (the plan's input)
   u64 part_off_tiles = 0;  // capacity in tiles
   u32 part_tiles = 0;
   // Large single passes: the two-kernel ordered build's partial slots (dict.hip).
@@ -129,16 +130,13 @@ struct DevicePipeline {
   u64 sync_bytes = 0;
   MapCounters* d_ctr = nullptr;
   LookbackScratch lb_line{}, lb_compact{}, lb_map{}, lb_heads{}, lb_scan{}, lb_dict{};
-  // the fast map's per-partition token totals (kDictParts, zeroed with the sync block; the
-  // self-cleaning ordered kernel re-zeroes them): the in-job workgroup plan's statistics
-  u32* d_part_tot = nullptr;
   // LOCUST_VPLAN=0 (read at construction): the ordered kernel keeps one workgroup per map
   // partition (A/B of the in-job plan)
   const bool vplan = [] {
     const char* e = std::getenv("LOCUST_VPLAN");
     return !e || e[0] != '0';
   }();
-  bool tot_ready = false;  // the current pass's map wrote d_part_tot
+  bool plan_small() const { return vplan && pm_retunes == 0; }
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {
@@ -196,6 +194,66 @@ struct DevicePipeline {
   u32* d_pw = nullptr;
   u64 pm_predicted_max = 0;  // predicted max partition work of the current map (0: default)
   u32 pm_retunes = 0;
+  // ---- in-job partition plan of a large piecewise pass (partplan.hip) ----
+  // Before piece 0 is mapped: a <= 1 MiB line-aligned prefix of it is mapped into scratch,
+  // its distinct keys collected in a small HBM table, and launch_part_plan cuts the key
+  // space at equal counts of them into d_pmap -- the pass's partitions come from its own
+  // text, not from the previous job's output.  LOCUST_DEVPLAN=0 (read at construction):
+  // the host-tuned map instead.  A planned pass that overflows an LDS table falls back as
+  // before and hands this engine to the host-tuned map (devplan_failed).
+  const bool devplan_env = [] {
+    const char* e = std::getenv("LOCUST_DEVPLAN");
+    return !e || e[0] != '0';
+  }();
+  bool devplan_failed = false;
+  bool devplan_used = false;  // the current pass's map was planned on the device
+  // d_pmap was tuned from a large pass's exact output (retune_with): later passes of the
+  // engine take it (the plan costs ~0.1-0.2 ms of the pass; the tuned map is exact).
+  // LOCUST_PART_TUNE=0 never tunes: every pass plans itself.
+  bool pm_tuned = false;
+  u32 fallbacks = 0, planned_passes = 0;  // diagnostics (GpuWordCount::stats)
+  static constexpr u64 kPlanSampleBytes = 1ull << 20;
+  static constexpr u64 kPlanCap = 1ull << 19;  // sample tokens kept
+  char* d_plan = nullptr;                      // one allocation, made on first use
+  u64 plan_zero_bytes = 0;                     // [MapCounters | table | ucount], zeroed per pass
+  MapCounters* d_plan_ctr = nullptr;
+  KeysSoA plan_keys{};
+  DictWorkspace plan_dict{};
+  void ensure_plan() {
+    if (d_plan) return;
+    const u64 slots = 2 * kPlanCap;  // load factor <= 0.5
+    const u64 ctr_b = align_up(sizeof(MapCounters), 256), tab_b = align_up(slots * sizeof(DictSlot), 256);
+    plan_zero_bytes = ctr_b + tab_b + kPlanCap * 8;
+    const u64 total = plan_zero_bytes + 256 + (4 + 4 + 1) * kPlanCap * 8 + kPlanCap * 4 + 4096;
+    LOCUST_HIP_CHECK(hipMalloc(&d_plan, total));
+    char* c = d_plan;
+    d_plan_ctr = reinterpret_cast<MapCounters*>(c);
+    plan_dict.table = reinterpret_cast<DictSlot*>(c + ctr_b);
+    plan_dict.ucount = reinterpret_cast<u64*>(c + ctr_b + tab_b);
+    c = d_plan + align_up(plan_zero_bytes, 256);
+    for (int j = 0; j < kKeyWords; ++j, c += kPlanCap * 8) plan_dict.ukeys.w[j] = reinterpret_cast<u64*>(c);
+    for (int j = 0; j < kKeyWords; ++j, c += kPlanCap * 8) plan_keys.w[j] = reinterpret_cast<u64*>(c);
+    plan_dict.uval = reinterpret_cast<u64*>(c);
+    c += kPlanCap * 8;
+    plan_dict.urank = reinterpret_cast<u32*>(c);
+    plan_dict.mask = (u32)(slots - 1);
+    plan_dict.ucap = (u32)kPlanCap;
+  }
+  // The plan's kernels, on `stream` once piece 0 (`len0` bytes at d_text; host copy at
+  // `host`) has landed; the scratch was zeroed at the start of the pass.
+  void enqueue_devplan(const char* host, u64 len0, const DelimMask& dm) {
+    u64 n = std::min<u64>(len0, kPlanSampleBytes);
+    if (n < len0) {
+      const void* nl = memrchr(host, '\n', (size_t)n);
+      if (nl) n = (u64)(static_cast<const char*>(nl) - host) + 1;
+    }
+    launch_map_fast(d_text, n, dm, cfg.emits_per_line, cfg.max_key_len, plan_keys, nullptr,
+                    kPlanCap, d_plan_ctr, lb_map, stream);
+    launch_dict_insert(plan_keys, nullptr, &d_plan_ctr->num_records, kPlanCap, plan_dict,
+                       d_plan_ctr, stream);
+    launch_part_plan(plan_dict.ukeys.w[0], plan_dict.ucount, &d_plan_ctr->num_unique,
+                     plan_dict.ucap, d_pmap, stream);
+  }
   u64* h_keys = nullptr;  // staging for key up/downloads (4 words x cap)
   PackedKey* h_small = nullptr;
   u64* h_u64 = nullptr;
@@ -243,8 +301,7 @@ struct DevicePipeline {
     dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
                       ucap * 4;
     const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
-    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1) +
-                 4 * kDictParts;  // + the map's per-partition totals (d_part_tot)
+    sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1);
 
     SizingPlan sz;
     sz.add<char>(cap_bytes + 64);
@@ -270,6 +327,7 @@ struct DevicePipeline {
       large_ordered = cap > kPartBuildMaxTokens;
     }
     if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartTable);
+    if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartOccWords);
     partial_slots_cap = large_ordered ? (u32)std::clamp<u64>(div_up(cap_bytes, kPieceBytes) + 3,
                                                              kOrdWorkers, kMaxPartialSlots)
                                       : 0u;
@@ -315,6 +373,7 @@ struct DevicePipeline {
     d_perm = arena.take<u32>(cap);
     d_parts = arena.take<u8>(align_up(cap, 16) + 16);
     if (part_off_tiles) d_part_off = arena.take<u32>(part_off_tiles * kPartTable);
+    if (part_off_tiles) d_part_occ = arena.take<u32>(part_off_tiles * kPartOccWords);
     if (partial_slots) {
       d_partials = arena.take<KeyCount>(partial_slots * kPartSlotsHost);
       d_partial_n = arena.take<u32>(partial_slots);
@@ -343,8 +402,6 @@ struct DevicePipeline {
     lb_scan = {st, counters + 4};
     st += t_scan;
     lb_dict = {st, counters + 5};
-    st += kDictParts + 1;
-    d_part_tot = reinterpret_cast<u32*>(st);
 
     rx.cap = cap;
     rx.tile_counters = arena.take<u32>(rx_zero_words);
@@ -389,6 +446,11 @@ struct DevicePipeline {
     // take the radix path, whose download grows the buffer), so a streaming engine with a
     // 16M-key dictionary does not pin 800 MB per output buffer.
     grow_host_out(std::min<u64>(ucap, kMappedOutMax));
+    // and a second one: a job's result holds its buffer while the next job runs, so jobs
+    // alternate between two -- allocated here, not inside the second job (pinning a
+    // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job)
+    out_pool.push_back(std::make_shared<HostOut>(h_out_cap, out_noncoherent));
+    use_out(0);
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                    hipHostMallocMapped | hipHostMallocCoherent));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_done, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -409,6 +471,12 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
     std::memset(h_ctr, 0, sizeof(MapCounters));
+    if (large_ordered && cfg.map_path == MapPath::kFast) {
+      // what a piecewise pass needs, made here and not inside the first job: the copy
+      // streams and piece events, and the plan's scratch
+      ensure_piece_events(partial_slots_cap);
+      if (devplan_env) ensure_plan();
+    }
   }
 
   ~DevicePipeline() {
@@ -443,6 +511,7 @@ struct DevicePipeline {
                     (void*)h_pw, (void*)h_done})
       if (p) (void)hipHostFree(p);
     if (d_pmap) (void)hipFree(d_pmap);
+    if (d_plan) (void)hipFree(d_plan);
   }
 
   // ---- host-mapped output buffers (zero-copy emit target AND zero-copy results) ----
@@ -781,7 +850,6 @@ struct DevicePipeline {
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
     part_tiles = cfg.map_path != MapPath::kFast ? 0u : pieces.empty() ? table_tiles(in.bytes)
                                                                          : piece_tiles();
-    tot_ready = vplan && !large_ordered && pieces.empty() && part_tiles > 0;  // as enqueue_map
     LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
   }
   bool use_zero_copy(const TextInput& in) const {
@@ -792,7 +860,7 @@ struct DevicePipeline {
 
   void enqueue_map(const TextInput& in) {
     parts_ready = cfg.map_path == MapPath::kFast;
-    tot_ready = false;
+    devplan_used = false;
     partial_nslots = 0;
     // combining needs the 4 KiB grouped map: upload pieces, or one launch past kMapLargeInput
     map_combined = combine_map && large_ordered && cfg.map_path == MapPath::kFast &&
@@ -825,6 +893,11 @@ struct DevicePipeline {
       // beside the next map on a third stream both kernels ran ~1.6x slower and every
       // cross-queue hand-off cost ~20 us (measured), while the copies leave room for both
       const bool agg = map_combined && large_ordered_ok() && pieces.size() <= partial_slots_cap;
+      devplan_used = agg && devplan_env && !devplan_failed && !pm_tuned;
+      if (devplan_used) {  // zeroed while piece 0 is on its way
+        ensure_plan();
+        LOCUST_HIP_CHECK(hipMemsetAsync(d_plan, 0, plan_zero_bytes, stream));
+      }
       const u64 t_enq = now_ns();
       // the padding after the text: off the copy streams (a 16-byte fill at an unaligned
       // address is two blit kernels there, ~15 us in front of the last piece's event)
@@ -836,6 +909,7 @@ struct DevicePipeline {
         LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
         LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_piece[k], 0));
+        if (k == 0 && devplan_used) enqueue_devplan(src, len, dm);
         launch_map_fast(d_text + off, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, d_parts,
                         cap, d_ctr, lb_map, stream, map_trace(),
                         part_tiles ? d_part_off + tile_off * kPartTable : nullptr, part_map(),
@@ -852,12 +926,10 @@ struct DevicePipeline {
       if (agg) partial_nslots = (u32)pieces.size();
     } else {
       part_tiles = table_tiles(in.bytes);
-      tot_ready = vplan && !large_ordered && part_tiles > 0;
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                       stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
-                      map_combined ? d_counts : nullptr,
-                      tot_ready ? d_part_tot : nullptr);
+                      map_combined ? d_counts : nullptr, plan_small() ? d_part_occ : nullptr);
     }
   }
 
@@ -1023,7 +1095,9 @@ struct DevicePipeline {
     if (part_tiles && parts_ready && !with_counts) {
       ex.part_off = d_part_off;
       ex.part_tiles = part_tiles;
-      if (tot_ready) ex.part_tot = d_part_tot;
+      // the in-job plan while the map is untuned (a retuned map is already balanced: the
+      // plan would only add its ~2 us)
+      if (plan_small()) ex.part_occ = d_part_occ;
     }
   }
   // Fills the self-clean fields of an OrderedExtra (see OrderedExtra::self_clean).
@@ -1032,7 +1106,6 @@ struct DevicePipeline {
     ex.map_lb = lb_map;
     ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
     ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
-    ex.part_tot_zero = d_part_tot;
   }
   // Device view of this pipeline's partition map (tables live at fixed addresses, so
   // captured graphs stay valid when the host retunes the contents).
@@ -1046,6 +1119,11 @@ struct DevicePipeline {
   // for the next job.  Cheap to check (256 words); a rebuild is one pass over the output.
   // Largest reported partition work when a rebuild looks worthwhile, else 0.
   u64 retune_wanted() const {
+    if (devplan_used && !pm_tuned) {  // a planned pass: hand over to the exact map
+      if (const char* v = std::getenv("LOCUST_PART_TUNE"))
+        if (v[0] == '0') return 0;
+      return ~0ull / 8;
+    }
     if (const char* v = std::getenv("LOCUST_PART_TUNE"))
       if (v[0] == '0') return 0;
     u64 sum = 0, mx = 0;
@@ -1060,15 +1138,32 @@ struct DevicePipeline {
   // After an ordered run overflowed a partition (or the output): rebuild the map from the
   // fallback's output so the next job's partitions fit (kept if it would not help).
   void force_retune(const WordCountEntry* e, u64 n) {
-    if (const char* v = std::getenv("LOCUST_PART_TUNE"))
-      if (v[0] == '0') return;
-    if (!n) return;
+    // a device-planned map overflowed: this engine keeps the host-side map from now on
+    // (tuned from this output, or the default with tuning off) -- d_pmap holds the plan
+    const bool planned = devplan_used;
+    if (planned) {
+      devplan_failed = true;
+      devplan_used = false;
+    }
+    const char* v = std::getenv("LOCUST_PART_TUNE");
+    const bool tune = n && !(v && v[0] == '0');
     PartMapTables t;
-    const u64 pred = part_map_from_entries(e, n, &t);
+    u64 pred = 0;
+    if (tune)
+      pred = part_map_from_entries(e, n, &t);
+    else
+      part_map_default(&t);
     // The same map again (e.g. one first word with more distinct keys than an LDS table:
     // no cut can split it): a new upload would change nothing, so keep it.
-    if (std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;
+    if (!planned && (!tune || std::memcmp(&t, h_pmap, sizeof(t)) == 0)) return;
+    if (planned && !pred) return upload_pmap(t, 0);
     retune_with(~0ull / 8, pred, t);
+  }
+  void upload_pmap(const PartMapTables& t, u64 pred) {
+    *h_pmap = t;
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_pmap, h_pmap, sizeof(PartMapTables), hipMemcpyHostToDevice,
+                                    stream));
+    pm_predicted_max = pred;
   }
   void maybe_retune(const WordCountEntry* e, u64 n) {
     if (const u64 mx = retune_wanted()) {
@@ -1079,7 +1174,20 @@ struct DevicePipeline {
   // The same when the sorted output is device KeyCount records (the distributed map): one
   // D2H of them, only when a rebuild is due.
   void maybe_retune_records(const KeyCount* d_recs, u64 n, bool force = false) {
+    const bool planned = force && devplan_used;
+    if (planned) {  // as force_retune
+      devplan_failed = true;
+      devplan_used = false;
+    }
     const u64 mx = force ? ~0ull / 8 : retune_wanted();
+    if (planned && (!n || [] {
+          const char* v = std::getenv("LOCUST_PART_TUNE");
+          return v && v[0] == '0';
+        }())) {
+      PartMapTables t;
+      part_map_default(&t);
+      return upload_pmap(t, 0);
+    }
     if (!mx || !n) return;
     std::vector<KeyCount> h(n);
     LOCUST_HIP_CHECK(hipMemcpyAsync(h.data(), d_recs, n * sizeof(KeyCount), hipMemcpyDeviceToHost,
@@ -1093,7 +1201,7 @@ struct DevicePipeline {
     }
     PartMapTables t;
     const u64 pred = part_map_from_entries(e.data(), n, &t);
-    if (force && std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;  // as force_retune
+    if (force && !planned && std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;  // as force_retune
     retune_with(mx, pred, t);
   }
   void retune_with(u64 mx, u64 pred, const PartMapTables& t) {
@@ -1101,11 +1209,9 @@ struct DevicePipeline {
       pm_predicted_max = mx;
       return;
     }
-    *h_pmap = t;
-    LOCUST_HIP_CHECK(hipMemcpyAsync(d_pmap, h_pmap, sizeof(PartMapTables), hipMemcpyHostToDevice,
-                                    stream));
-    pm_predicted_max = pred;
+    upload_pmap(t, pred);
     ++pm_retunes;
+    if (large_ordered) pm_tuned = true;
     LOCUST_LOG_DEBUG("partition map retuned (#%u): max partition work %llu -> %llu",
                      pm_retunes, (unsigned long long)mx, (unsigned long long)pred);
   }
@@ -1543,6 +1649,8 @@ struct DevicePipeline {
       if (ordered) print_ord_trace();
       print_partials_trace();
       print_map_trace();
+      if (ordered && !ordered_done) ++fallbacks;
+      if (devplan_used) ++planned_passes;
       if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, map_combined);
       if (!ordered_done && dict_fallback_needed()) {
         finish_dict_with_radix((u32)in.num_lines, map_combined);

@@ -136,6 +136,15 @@ class GpuWordCount {
 
   WordCountResult run(const TextInput& in);
 
+  // How the engine's partition map has fared (diagnostics, tests): retunes of the map from
+  // a job's output, jobs whose ordered build overflowed an LDS table and fell back to the
+  // HBM table, and whether the in-job plan of large passes was given up.
+  struct Stats {
+    u32 retunes = 0, fallbacks = 0, planned_passes = 0;
+    bool devplan_failed = false;
+  };
+  Stats stats() const;
+
   // Stage split: map + process only, returning the sorted tokens of
   // this input; and reduce-only over (possibly unsorted) tokens.
   std::vector<PackedKey> run_map_stage(const TextInput& in, WordCountResult* stats);

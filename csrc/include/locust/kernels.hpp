@@ -111,14 +111,14 @@ constexpr int kMapTileBytesLarge = (kMapBlock / 64) * kMapSegStepsLarge * 64;
 inline u64 map_tile_bytes(u64 bytes) {
   return bytes < kMapLargeInput ? (u64)kMapTileBytesMin : (u64)kMapTileBytesLarge;
 }
-// part_tot (optional, with part_off; zeroed before the first tile): part_tot[p] += the
-// records of partition p every tile wrote -- the map statistics the ordered kernel plans
-// its workgroups from (OrderedExtra::part_tot).
+// part_occ (optional, small 1 KiB tiles with part_off): per tile, kPartOccWords words of a
+// 256-bit mask of its non-empty partitions (OrderedExtra::part_occ).
+constexpr int kPartOccWords = kDictParts / 32;
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
                      u32* part_off = nullptr, PartMap pm = PartMap{}, bool large_tiles = false,
-                     u64* counts = nullptr, u32* part_tot = nullptr);
+                     u64* counts = nullptr, u32* part_occ = nullptr);
 
 // ---------------- radix_sort.hip ----------------
 constexpr int kSortBlock = 256;
@@ -282,16 +282,17 @@ struct OrderedExtra {
   // part_off): partitions read their token ranges from it instead of scanning the tags.
   const u32* part_off = nullptr;
   u32 part_tiles = 0;
-  // With part_off: the map's per-partition token totals (launch_map_fast part_tot).  The
-  // workgroups are then planned inside the job from THIS job's statistics: the kDictParts
-  // workgroups are dealt out over the non-empty partitions in proportion to their tokens,
-  // and a partition with K > 1 workgroups is cut into K key ranges at quantiles of a sample
-  // of its own tokens (every sibling draws the same sample) -- virtual partitions in key
-  // order, one look-back over all of them.  A first-letter partition map on English text
-  // leaves ~200 of 256 workgroups idle and 's'/'t' on the critical path without it.
-  u32* part_tot = nullptr;
-  // Self-cleaning (with self_clean): the last workgroup re-zeroes these kDictParts totals.
-  u32* part_tot_zero = nullptr;
+  // With part_off and part_occ (the map's per-tile occupancy masks): plan the workgroups
+  // inside the job from THIS job's map statistics.  Every workgroup ORs the occupancy
+  // masks (which partitions are non-empty: exact), estimates the partitions' token counts
+  // from the same evenly spaced rows of the per-tile table, deals the kDictParts
+  // workgroups out over the non-empty partitions in proportion to them, and a partition
+  // with K > 1 workgroups is cut into K key ranges at quantiles of a sample of its own
+  // tokens (every sibling draws the same sample): virtual partitions in key order, one
+  // look-back over all of them.  A first-letter partition map on English text leaves ~200
+  // of 256 workgroups idle and puts 's'/'t' on the critical path without it.  (Inputs of
+  // at most kPartBlock tiles; larger ones keep one workgroup per partition.)
+  const u32* part_occ = nullptr;
   u32 variant = 0;              // A/B switches for kernel experiments (LOCUST_ORD_VARIANT)
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};
@@ -342,6 +343,12 @@ constexpr int kMaxMergeRunsHost = kMaxSlotRanks;
 void launch_dict_merge_runs(const KeyCount* own, const KeyCount* recv, const u32* meta,
                             MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                             LookbackScratch lb, hipStream_t s, PartMap pm = PartMap{});
+// ---------------- partplan.hip ----------------
+// A partition map cut at equal weights of a sample's distinct keys (first words
+// ukeys_w0[0 .. min(*d_u, ucap)), in any order, with their sample counts; a key seen once
+// weighs more: it stands for the rare keys not sampled yet): writes out->lo (device).
+void launch_part_plan(const u64* ukeys_w0, const u64* ucount, const u32* d_u, u32 ucap,
+                      PartMapTables* out, hipStream_t s);
 // ---------------- merge.hip ----------------
 // Merge of sorted runs (same run layout and meta as launch_dict_merge_runs) by lock-step
 // binary search + one look-back scan: `merged` (room for every record, bounded by `cap`)

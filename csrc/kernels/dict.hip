@@ -218,8 +218,10 @@ constexpr u32 kOrdTagWindow = kPartBlock * 32;  // ordered build: tags scanned p
 constexpr int kPartPerThread = kPartSlots / kPartBlock;
 
 // A key not placed within kPartProbes slots reports the table full (the caller falls back):
-// probing a nearly full table to the end made an overflowing pass quadratic.
-constexpr int kPartProbes = 128;
+// probing a nearly full table to the end made an overflowing pass quadratic.  (512: a
+// planned range holds up to ~1,500 of the 2,048 slots; linear probing at 75 % load runs
+// clusters past 128.)
+constexpr int kPartProbes = 512;
 __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h) {
   u32 slot = (u32)(h >> 8) & (kPartSlots - 1);
   for (int probe = 0; probe < kPartProbes;) {
@@ -425,6 +427,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
 // ---------------------------------------------------------------------------------
 constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
 constexpr u32 kSplitMinTokens = 128;           // planned workgroups: tokens per extra sibling
+constexpr u32 kPlanRows = 16;                  // table rows the plan estimates tokens from
 constexpr u32 kRankChunk = 8;                  // candidates per rank work item
 constexpr u32 kSmallRank = 256;                // partitions up to here: all-pairs ranks
 __device__ __forceinline__ u32 div_up_u32(u32 a, u32 b) { return (a + b - 1) / b; }
@@ -652,46 +655,27 @@ struct TileSource {
     }
     return full;
   }
-  // Virtual partition j of K over map partition p (n_p tokens): the key range between the
-  // j-th and (j+1)-th K-quantile of a sample of the partition's tokens.  The sample is
-  // taken at fixed positions of the partition's tokens in tile order (a block scan of the
-  // runs, not the list's atomic order), so all K siblings draw the same sample, sort it
-  // the same way and agree on every cut: each key lands in exactly one sibling.  The
-  // siblings then all walk the partition's runs but insert only their own range.
-  static constexpr u32 kSplitSamples = 256;
-  __device__ bool build_split(u32 p, u32 j, u32 K, u32 n_p, LdsSlot* s_tab, u32* s_list,
-                              u32& s_count, u32* s_scan, u64* stamp) const {
-    u32* s_sidx = s_list + kPartWindow - 1280;                      // [256] sample tokens
-    u64* s_samp = reinterpret_cast<u64*>(s_list + kPartWindow - 1024);  // [256]
-    u64* s_sort = reinterpret_cast<u64*>(s_list + kPartWindow - 512);   // [256]
-    const u32 S = n_p < kSplitSamples ? n_p : kSplitSamples;
-    u32 a0 = 0, len0 = 0;  // this thread's round-0 run, kept for the inserts
-    u32 base = 0;
-    for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
-      const u32 t = t0 + threadIdx.x;
-      u32 a = 0, len = 0;
-      if (t < ntiles) {
-        a = part_off[(u64)t * kPartTable + p];
-        len = part_off[(u64)t * kPartTable + p + 1] - a;
-      }
-      if (t0 == 0) {
-        a0 = a;
-        len0 = len;
-      }
-      u32 tot = 0;
-      const u32 ex = base + dev::block_exclusive_scan<u32, kPartBlock>(len, s_scan, &tot);
-      if (len && S) {  // samples i at q_i = floor(i * n_p / S) inside [ex, ex + len)
-        for (u32 i = (u32)(((u64)ex * S + n_p - 1) / n_p); i < S; ++i) {
-          const u32 q = (u32)((u64)i * n_p / S);
-          if (q >= ex + len) break;
-          s_sidx[i] = a + (q - ex);
-        }
-      }
-      base += tot;
-    }
+  // Virtual partition j of K over map partition p: the key range between the j-th and
+  // (j+1)-th K-quantile of a sample of the partition's tokens.  The list of the
+  // partition's tokens is built in tile order at positions from a block scan of the runs
+  // (not the atomic order of the plain build), so all K siblings draw the same sample, sort
+  // it the same way and agree on every cut: each key lands in exactly one sibling, which
+  // then inserts only its own range.  `pre`: this thread's run (tile threadIdx.x; the plan
+  // admits at most kPartBlock tiles).
+  static constexpr u32 kSplitSamples = 64;
+  __device__ bool build_split(u32 p, Pre pre, u32 j, u32 K, LdsSlot* s_tab, u32* s_list,
+                              u32* s_scan, u64* stamp) const {
+    u64* s_samp = reinterpret_cast<u64*>(s_list + kPartWindow - 256);  // [64]
+    u64* s_sort = reinterpret_cast<u64*>(s_list + kPartWindow - 128);  // [64]
+    const u32 a = pre.a, len = threadIdx.x < ntiles ? pre.b - pre.a : 0u;
+    u32 n = 0;
+    const u32 at = dev::block_exclusive_scan<u32, kPartBlock>(len, s_scan, &n);
+    const u32 lim = min(n, (u32)kPartWindow - 256);  // the sample area sits at the list's end
+    for (u32 k = 0; k < len && at + k < lim; ++k) s_list[at + k] = a + k;
     __syncthreads();
+    const u32 S = lim < kSplitSamples ? lim : kSplitSamples;
     if (threadIdx.x < S) {
-      const u32 idx = s_sidx[threadIdx.x];
+      const u32 idx = s_list[(u32)((u64)threadIdx.x * lim / S)];
       s_samp[threadIdx.x] = idx < n_cap ? tokens.w[0][idx] : 0ull;
     }
     __syncthreads();
@@ -708,39 +692,13 @@ struct TileSource {
     const bool last = j + 1 >= K;
     const u64 lo = j == 0 || !S ? 0ull : s_sort[(u64)j * S / K];
     const u64 hi = last || !S ? ~0ull : s_sort[(u64)(j + 1) * S / K];
-    __syncthreads();  // the sample area is list space again
     if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
-    bool full = false;
-    if (lo == hi && !last) return false;  // an empty range (a hot first word took it)
-    for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
-      const u32 t = t0 + threadIdx.x;
-      u32 a = a0, len = len0;
-      if (t0 != 0) {
-        a = len = 0;
-        if (t < ntiles) {
-          a = part_off[(u64)t * kPartTable + p];
-          len = part_off[(u64)t * kPartTable + p + 1] - a;
-        }
-      }
-      {
-        const u32 incl = dev::wave_inclusive_scan(len);
-        u32 wbase = 0;
-        if (dev::lane_id() == 63 && incl) wbase = atomicAdd(&s_count, incl);
-        wbase = (u32)__shfl((int)wbase, 63, 64);
-        u32 at = wbase + incl - len;
-        for (u32 k = 0; k < len; ++k, ++at)
-          if (at < (u32)kPartWindow) s_list[at] = a + k;
-      }
-      __syncthreads();
-      const u32 cnt = s_count;
-      full |= cnt > (u32)kPartWindow;
-      full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab, lo,
-                            hi, last);
-      __syncthreads();
-      if (threadIdx.x == 0) s_count = 0;
-      __syncthreads();
-    }
+    // a list cut short by the sample area is an overflow: the host redoes the pass
+    bool full = n > lim;
+    if (!(lo == hi && !last))  // else an empty range (a hot first word took it)
+      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last);
     if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
+    __syncthreads();  // the list area is reused after the build
     return full;
   }
 };
@@ -973,24 +931,52 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   // and a hang with four ranks on one GPU.
   const u64 rt_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, device-wide
   // v: this workgroup's virtual partition = its ticket (the look-back order); p: the map
-  // partition whose tokens it reads; (vj, vk): its share of p (see OrderedExtra::part_tot).
+  // partition whose tokens it reads; (vj, vk): its share of p (see OrderedExtra::part_occ).
   // Without a plan, v == p and vk == 1.
   constexpr bool kTiles = std::is_same<Src, TileSource>::value;
-  const bool vplan = kTiles && ex.part_tot != nullptr;
-  __shared__ u32 s_vpre[kDictParts + 1];  // exclusive prefix of the workgroups per partition
+  bool vplan = false;
+  if constexpr (kTiles) vplan = ex.part_occ != nullptr && src.ntiles > 0 && src.ntiles <= kPartBlock;
+  __shared__ u32 s_vpre[kDictParts + 1];
   __shared__ u32 s_vred[8];
-  u32 tp = 0;  // (plan) this thread's partition's tokens, loaded before the ticket
-  if (vplan && threadIdx.x < kDictParts) tp = ex.part_tot[threadIdx.x];
+  __shared__ u32 s_occ[kPartOccWords];
+  u32 tp = 0, occw = 0;  // (plan) loaded before the ticket: one round trip for all
+  if (vplan) {
+    if constexpr (kTiles) {
+      const u32 nt = src.ntiles;
+      if (threadIdx.x < kDictParts) {
+        // this partition's tokens, estimated from kPlanRows evenly spaced table rows
+        const u32 q = threadIdx.x;
+        u32 sum = 0;
+#pragma unroll
+        for (u32 r = 0; r < kPlanRows; ++r) {
+          const u32 t = (u32)((u64)r * nt / kPlanRows);
+          sum += src.part_off[(u64)t * kPartTable + q + 1] - src.part_off[(u64)t * kPartTable + q];
+        }
+        tp = (u32)((u64)sum * nt / kPlanRows);
+      } else {
+        // occupancy: thread (word w, tile slice) ORs its tiles' word w
+        const u32 i = threadIdx.x - kDictParts, w = i % kPartOccWords;
+        for (u32 t = i / kPartOccWords; t < nt; t += (kPartBlock - kDictParts) / kPartOccWords)
+          occw |= ex.part_occ[(u64)t * kPartOccWords + w];
+      }
+    }
+  }
   // Tickets almost always come out in dispatch order: prefetch the run table for
   // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.
   const typename Src::Pre guess = vplan ? typename Src::Pre{} : src.prefetch(blockIdx.x);
-  u32 v, p, vj = 0, vk = 1, np = 0;
+  u32 v, p, vj = 0, vk = 1;
   if (!vplan) {
     v = p = dev::acquire_tile(tile_ctr, &s_tile);
   } else {
     if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
-    if (threadIdx.x < kDictParts) {
-      const u64 nz = dev::ballot(tp != 0);
+    if (threadIdx.x < kPartOccWords) s_occ[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x >= kDictParts && occw) atomicOr(&s_occ[(threadIdx.x - kDictParts) % kPartOccWords], occw);
+    __syncthreads();
+    const bool occupied = threadIdx.x < kDictParts && ((s_occ[threadIdx.x >> 5] >> (threadIdx.x & 31)) & 1u);
+    if (threadIdx.x < kDictParts) {  // non-empty partitions E (exact), estimated tokens T
+      if (!occupied) tp = 0;
+      const u64 nz = dev::ballot(occupied);
       const u32 tsum = dev::wave_reduce_sum(tp);
       if (dev::lane_id() == 0) {
         s_vred[dev::wave_id()] = (u32)__popcll(nz);
@@ -1001,11 +987,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     v = s_tile;
     const u32 E = s_vred[0] + s_vred[1] + s_vred[2] + s_vred[3];
     const u32 T = s_vred[4] + s_vred[5] + s_vred[6] + s_vred[7];
-    // workgroups of partition q: 1 + its token share of the idle ones (at least
-    // kSplitMinTokens tokens per extra one); the sum is at most kDictParts
+    // workgroups of partition q: one if it has tokens, plus its token share of the idle
+    // ones (at least kSplitMinTokens tokens per extra one); the sum is at most kDictParts
     u32 K = 0;
-    if (tp) {
-      const u32 extra = (u32)((u64)tp * (u32)(kDictParts - E) / T);
+    if (occupied) {
+      const u32 extra = T ? (u32)((u64)tp * (u32)(kDictParts - E) / T) : 0u;
       K = 1u + min(extra, tp / kSplitMinTokens);
     }
     u32 kinc = 0;
@@ -1031,7 +1017,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         if (s_vpre[p + step] <= v) p += step;
       vj = v - s_vpre[p];
       vk = s_vpre[p + 1] - s_vpre[p];
-      np = ex.part_tot[p];
     }
   }
   ORD_STAMP(0);
@@ -1043,7 +1028,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     trace[(u64)v * 32 + 19] = 0;
   }
   const typename Src::Pre first =
-      vplan ? (vk == 1 ? src.prefetch(p) : typename Src::Pre{}) : p == blockIdx.x ? guess : src.prefetch(p);
+      vplan ? (vk ? src.prefetch(p) : typename Src::Pre{}) : p == blockIdx.x ? guess : src.prefetch(p);
   // The in-partition counting sort of a large partition buckets keys by the 8 bits of
   // (w0 - wlo) just below the width of [wlo, whi], the first words actually present: 256
   // order-preserving buckets -- the second byte for keys sharing a first byte, finer bytes
@@ -1074,8 +1059,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   bool full = false;
   if constexpr (kTiles) {
     if (vk > 1)
-      full = src.build_split(p, vj, vk, np, s_tab, s_list, s_count,
-                             reinterpret_cast<u32*>(s_scan), trace ? trace + (u64)v * 32 : nullptr);
+      full = src.build_split(p, first, vj, vk, s_tab, s_list, reinterpret_cast<u32*>(s_scan),
+                             trace ? trace + (u64)v * 32 : nullptr);
     else if (vk == 1)
       full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr);
   } else {
@@ -1637,8 +1622,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       if (!(flags & kCtrDictOverflow)) {
         for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
         for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
-        if (ex.part_tot_zero)
-          for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) ex.part_tot_zero[i] = 0;
         if (threadIdx.x == 0) {
           // the accumulated counters; num_unique / total_count are assignments the next
           // run overwrites, and stay readable for what follows this kernel

@@ -143,22 +143,12 @@ __device__ __forceinline__ void pack_token(const unsigned char* s_text, int o, u
   }
 }
 
-// The scan lane l's four partition counts into the job's totals (fire-and-forget atomics:
-// only the non-empty partitions of the tile, ~30 per 1 KiB tile of English text).
-__device__ __forceinline__ void add_part_totals(u32* part_tot, u32 l, u32 h0, u32 h1, u32 h2,
-                                                u32 h3) {
-  if (h0) atomicAdd(&part_tot[4 * l], h0);
-  if (h1) atomicAdd(&part_tot[4 * l + 1], h1);
-  if (h2) atomicAdd(&part_tot[4 * l + 2], h2);
-  if (h3) atomicAdd(&part_tot[4 * l + 3], h3);
-}
-
 template <int kSteps, int kBlock>
 __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace, u32* __restrict__ part_off,
-    PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_tot) {
+    PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_occ) {
   // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
   // at entry, tile acquired, text staged, masks done, prefix known, keys written.
   const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -318,7 +308,13 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
         const u32 l = threadIdx.x;
         const u32 h0 = s_pcnt[4 * l], h1 = s_pcnt[4 * l + 1], h2 = s_pcnt[4 * l + 2],
                   h3 = s_pcnt[4 * l + 3];
-        if (part_tot) add_part_totals(part_tot, l, h0, h1, h2, h3);
+        if (part_occ) {  // the tile's 256-bit partition occupancy: 8 words, lane 8w writes w
+          u32 occ = ((h0 ? 1u : 0u) | (h1 ? 2u : 0u) | (h2 ? 4u : 0u) | (h3 ? 8u : 0u)) << (4 * (l & 7));
+          occ |= (u32)__shfl_xor((int)occ, 1, 64);
+          occ |= (u32)__shfl_xor((int)occ, 2, 64);
+          occ |= (u32)__shfl_xor((int)occ, 4, 64);
+          if ((l & 7) == 0) part_occ[(u64)tile * kPartOccWords + (l >> 3)] = occ;
+        }
         const u32 sum4 = h0 + h1 + h2 + h3;
         const u32 inc = dev::wave_inclusive_scan(sum4);
         const u32 ex = inc - sum4;
@@ -406,7 +402,6 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
         const u32 l = threadIdx.x;
         const u32 h0 = s_pcnt[4 * l], h1 = s_pcnt[4 * l + 1], h2 = s_pcnt[4 * l + 2],
                   h3 = s_pcnt[4 * l + 3];
-        if (part_tot) add_part_totals(part_tot, l, h0, h1, h2, h3);
         const u32 sum4 = h0 + h1 + h2 + h3;
         const u32 inc = dev::wave_inclusive_scan(sum4);
         const u32 ex = inc - sum4;
@@ -516,8 +511,7 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace, u32* part_off,
-                     PartMap pm, bool large_tiles, u64* counts, u32* part_tot) {
-  if (!part_off) part_tot = nullptr;
+                     PartMap pm, bool large_tiles, u64* counts, u32* part_occ) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   if (bytes < kMapLargeInput && !large_tiles) {
@@ -529,13 +523,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace, part_off, pm, nullptr, part_tot);
+        lb.tile_counter, trace, part_off, pm, nullptr, part_off ? part_occ : nullptr);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, lb.status,
-        lb.tile_counter, trace, part_off, pm, part_off ? counts : nullptr, part_tot);
+        lb.tile_counter, trace, part_off, pm, part_off ? counts : nullptr, nullptr);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }

@@ -72,6 +72,15 @@ PackedKey to_key(const std::string& s) {
 
 class PyGpuEngine {
  public:
+  py::dict stats() const {
+    const GpuWordCount::Stats st = eng_.stats();
+    py::dict d;
+    d["retunes"] = st.retunes;
+    d["fallbacks"] = st.fallbacks;
+    d["planned_passes"] = st.planned_passes;
+    d["devplan_failed"] = st.devplan_failed;
+    return d;
+  }
   PyGpuEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
       : eng_(cfg, max_bytes, max_lines), max_bytes_(max_bytes) {}
   PyResult run(const std::string& text) {
@@ -418,6 +427,7 @@ PYBIND11_MODULE(_locust, m) {
       .def("run", &PyGpuEngine::run)
       .def("load", &PyGpuEngine::load)
       .def("run_loaded", &PyGpuEngine::run_loaded)
+      .def("stats", &PyGpuEngine::stats)
       .def("run_text", &PyGpuEngine::run_text, py::arg("text"))
       .def("map_stage", &PyGpuEngine::map_stage)
       .def("reduce_stage", &PyGpuEngine::reduce_stage)

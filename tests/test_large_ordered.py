@@ -2,9 +2,10 @@
 build: line-aligned upload pieces mapped as they land (4 KiB tiles), per-slice partials
 (dict_partials_kernel), merge + sort + records (dict_ordered_kernel<PartialsSource>).
 Checked against the CPU engine (an independent implementation) on Zipfian synthetic text:
-the first job of an engine overflows the first-byte partition map and falls back, the
-jobs after it run on the retuned map; graphs replayed with another text of the same size
-must not reuse the first text's pieces."""
+the first job of an engine plans its partition map from its own first piece (partplan.hip)
+instead of overflowing the first-byte map, the jobs after it run on the map retuned from
+the output; graphs replayed with another text of the same size must not reuse the first
+text's pieces."""
 import random
 
 import pytest
@@ -31,6 +32,21 @@ def test_pinned_pieces_match_cpu(graph):
         r = eng.run_text(h)
         assert r.num_unique == len(want)
         assert r.entries() == want
+
+
+@pytest.mark.parametrize("tune", ["1", "0"])
+def test_first_job_plans_its_own_map(monkeypatch, tune):
+    """A fresh engine's first large pass (no earlier output to tune from) neither overflows
+    nor falls back; with the between-job tuning off every pass plans itself."""
+    monkeypatch.setenv("LOCUST_PART_TUNE", tune)
+    h = gen(300_000, seed=11)  # ~13 MB
+    want = cpu_entries(h.to_bytes())
+    eng = lc._C.GpuEngine(lc.make_config("gpu", check=True), h.size, h.size)
+    for _ in range(3):
+        assert eng.run_text(h).entries() == want
+    st = eng.stats()
+    assert st["fallbacks"] == 0 and not st["devplan_failed"], st
+    assert st["planned_passes"] == (1 if tune == "1" else 3), st
 
 
 def test_staged_bytes_and_small_tiles():
