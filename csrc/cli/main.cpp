@@ -170,27 +170,109 @@ std::string spill_path(const CliArgs& a, int node) {
                                                                                    : ".txt");
 }
 
-void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
+// --json: one record per run, in every mode: counts, honest and
+// reference-semantics stage times, and for --gpus N every rank's stage times and the bytes
+// each of its links carried.
+struct JsonOut {
+  std::string body;
+  void kv(const char* k, const std::string& raw) {
+    body += (body.empty() ? "{" : ", ");
+    body += "\"" + std::string(k) + "\": " + raw;
+  }
+  void num(const char* k, double v) {
+    char b[64];
+    std::snprintf(b, sizeof(b), "%.6f", v);
+    kv(k, b);
+  }
+  void u(const char* k, unsigned long long v) { kv(k, std::to_string(v)); }
+  void str(const char* k, const std::string& v) { kv(k, "\"" + v + "\""); }
+  std::string done() const { return body + "}"; }
+};
+
+std::string u64_list(const std::vector<u64>& v) {
+  std::string s = "[";
+  for (size_t i = 0; i < v.size(); ++i) s += (i ? ", " : "") + std::to_string(v[i]);
+  return s + "]";
+}
+
+void emit_json(const CliArgs& a, const std::string& text) {
   if (a.json.empty()) return;
   std::FILE* f = a.json == "-" ? stderr : std::fopen(a.json.c_str(), "w");
   if (!f) throw Error("cannot write json: " + a.json);
+  std::fprintf(f, "%s\n", text.c_str());
+  if (f != stderr) std::fclose(f);
+}
+
+JsonOut json_head(const CliArgs& a, const char* mode) {
+  JsonOut j;
+  j.str("mode", mode);
+  j.str("backend", a.cfg.backend == Backend::kCpu ? "cpu" : "gpu");
+  j.kv("gpus", std::to_string(a.gpus));
+  j.str("map_path", to_string(a.cfg.map_path));
+  j.str("reduce_path", to_string(a.cfg.reduce_path));
+  j.str("sort", to_string(a.cfg.sort_path));
+  return j;
+}
+
+void json_counts(JsonOut& j, const WordCountResult& r) {
+  j.u("lines", r.num_lines);
+  j.u("tokens", r.num_tokens);
+  j.u("unique", r.num_unique);
+  j.u("overflow_lines", r.overflow_lines);
+  j.u("truncated", r.truncated);
+  j.u("max_key_len", r.max_key_len);
+}
+
+void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
+  if (a.json.empty()) return;
   std::vector<double> w = walls;
   std::sort(w.begin(), w.end());
   const double med = w.empty() ? 0 : w[w.size() / 2];
-  std::fprintf(f,
-               "{\"backend\": \"%s\", \"gpus\": %d, \"lines\": %llu, \"tokens\": %llu, "
-               "\"unique\": %llu, \"overflow_lines\": %llu, \"truncated\": %llu, "
-               "\"map_ms\": %.6f, \"process_ms\": %.6f, \"reduce_ms\": %.6f, \"h2d_ms\": %.6f, "
-               "\"d2h_ms\": %.6f, \"wall_ms_median\": %.6f, \"iters\": %d, \"map_path\": \"%s\", "
-               "\"reduce_path\": \"%s\", \"sort\": \"%s\", \"chunks\": %llu}\n",
-               a.cfg.backend == Backend::kCpu ? "cpu" : "gpu", a.gpus,
-               (unsigned long long)r.num_lines, (unsigned long long)r.num_tokens,
-               (unsigned long long)r.num_unique, (unsigned long long)r.overflow_lines,
-               (unsigned long long)r.truncated, r.times.map_ms, r.times.process_ms,
-               r.times.reduce_ms, r.times.h2d_ms, r.times.d2h_ms, med, (int)w.size(),
-               to_string(a.cfg.map_path), to_string(a.cfg.reduce_path), to_string(a.cfg.sort_path),
-               (unsigned long long)r.chunks);
-  if (f != stderr) std::fclose(f);
+  JsonOut j = json_head(a, "full");
+  json_counts(j, r);
+  j.num("map_ms", r.times.map_ms);
+  j.num("process_ms", r.times.process_ms);
+  j.num("reduce_ms", r.times.reduce_ms);
+  j.num("h2d_ms", r.times.h2d_ms);
+  j.num("d2h_ms", r.times.d2h_ms);
+  j.num("ref_map_ms", r.times.ref_map_ms);
+  j.num("ref_process_ms", r.times.ref_process_ms);
+  j.num("ref_reduce_ms", r.times.ref_reduce_ms);
+  j.num("wall_ms_median", med);
+  j.kv("iters", std::to_string(w.size()));
+  j.u("chunks", r.chunks);
+  emit_json(a, j.done());
+}
+
+void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector<DistResult>& ranks) {
+  if (a.json.empty()) return;
+  JsonOut j = json_head(a, "multi_gpu");
+  json_counts(j, root.result);
+  j.str("strategy", root.strategy == DistStrategy::kGather    ? "gather"
+                    : root.strategy == DistStrategy::kLocal   ? "local"
+                                                              : "shuffle");
+  j.num("wall_ms", root.total_ms);
+  std::string rk = "[";
+  for (size_t r = 0; r < ranks.size(); ++r) {
+    const DistResult& d = ranks[r];
+    JsonOut x;
+    x.kv("rank", std::to_string(r));
+    x.num("map_ms", d.map_ms);
+    x.num("shuffle_ms", d.shuffle_ms);
+    x.num("reduce_ms", d.reduce_ms);
+    x.num("gather_ms", d.gather_ms);
+    x.num("total_ms", d.total_ms);
+    x.u("local_records", d.local_records);
+    x.u("range_tokens", d.range_tokens);
+    x.u("range_unique", d.range_unique);
+    x.u("sent_bytes", d.sent_bytes);
+    x.u("recv_bytes", d.recv_bytes);
+    x.kv("sent_to", u64_list(d.sent_to));
+    x.kv("recv_from", u64_list(d.recv_from));
+    rk += (r ? ", " : "") + x.done();
+  }
+  j.kv("ranks", rk + "]");
+  emit_json(a, j.done());
 }
 
 long long ns(double ms) { return (long long)(ms * 1e6 + 0.5); }
@@ -265,6 +347,16 @@ int run(const CliArgs& a) {
     if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r.entries, &out);
     std::fflush(stdout);
     write_all(stdout, out);
+    if (!a.json.empty()) {
+      JsonOut j = json_head(a, "reduce_stage");
+      json_counts(j, r);
+      j.u("input_records", recs.size());
+      j.u("input_files", files.size());
+      j.num("process_ms", r.times.process_ms);
+      j.num("reduce_ms", r.times.reduce_ms);
+      j.num("wall_ms", r.times.wall_ms);
+      emit_json(a, j.done());
+    }
     std::printf("\nDone\n");
     return 0;
   }
@@ -286,7 +378,8 @@ int run(const CliArgs& a) {
     LOCUST_LOG_INFO("%d ranks in one process over %s", dc.world,
                     resolve_local_comm(dc, a.comm) == LocalComm::kRccl ? "an RCCL clique"
                                                                        : "loopback");
-    DistResult dr = run_single_process_multi_gpu(dc, text.input, a.comm);
+    std::vector<DistResult> ranks;
+    DistResult dr = run_single_process_multi_gpu(dc, text.input, a.comm, &ranks);
     std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(dr.reduce_ms));
@@ -294,6 +387,7 @@ int run(const CliArgs& a) {
     if (!a.quiet) format_gpu_output(dr.result.entries, &out);
     std::fflush(stdout);
     write_all(stdout, out);
+    write_json_dist(a, dr, ranks);
     std::printf("\nDone\n");
     return 0;
   }
@@ -314,7 +408,18 @@ int run(const CliArgs& a) {
     for (u64 k = 0; k < stats.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
     std::printf("%s mapping %lld nanoseconds \n", dev, 0ll);
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, (long long)(t1 - t0));
-    write_spill(spill_path(a, a.node), tokens_to_records(toks), a.spill_fmt);
+    const std::vector<KeyCount> recs = tokens_to_records(toks);
+    write_spill(spill_path(a, a.node), recs, a.spill_fmt);
+    if (!a.json.empty()) {
+      JsonOut j = json_head(a, "map_stage");
+      stats.num_lines = text.input.num_lines;
+      if (!stats.num_tokens) stats.num_tokens = toks.size();
+      json_counts(j, stats);
+      j.u("spill_records", recs.size());
+      j.str("spill", spill_path(a, a.node));
+      j.num("map_process_ms", (t1 - t0) * 1e-6);
+      emit_json(a, j.done());
+    }
     std::printf("MODE_MULTI: Finished map\n");
     return 0;
   }

@@ -134,6 +134,8 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const int me = comm.rank();
   log_rank() = me;
   DistResult res;
+  res.sent_to.assign((size_t)P, 0);
+  res.recv_from.assign((size_t)P, 0);
   std::string local_msg;
   // Runs a local step, returning its status (0 ok) instead of throwing.
   auto local = [&](const char* stage, const std::function<void()>& fn) -> i32 {
@@ -177,6 +179,8 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       if (p != me) {
         res.sent_bytes += sb[p];
         res.recv_bytes += rb[p];
+        res.sent_to[(size_t)p] += sb[p];
+        res.recv_from[(size_t)p] += rb[p];
       }
     }
   };
@@ -314,10 +318,13 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         eng.finalize(0, &r.entries);
         res.range_tokens = total;
         res.range_unique = uniq;
-      } else {
-        res.sent_bytes = slot_bytes * (u64)(P - 1);  // every peer receives this rank's slot
-        res.recv_bytes = slot_bytes * (u64)(P - 1);
       }
+      // the slot all-gather: every peer receives this rank's slot, and this rank every
+      // peer's (the root included: it merges them)
+      res.sent_bytes = slot_bytes * (u64)(P - 1);
+      res.recv_bytes = slot_bytes * (u64)(P - 1);
+      for (int p = 0; p < P; ++p)
+        if (p != me) res.sent_to[(size_t)p] = res.recv_from[(size_t)p] = slot_bytes;
       r.num_unique = r.entries.size();
       const u64 t2 = now_ns();
       res.map_ms = (t1 - t0) * 1e-6;  // map + all-gather + merge, one synchronisation
@@ -467,6 +474,14 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         const u64 sb = exch_slot_bytes(eng.exch_slot_records);
         res.sent_bytes = sb * (u64)(P - 1);
         res.recv_bytes = sb * (u64)(P - 1);
+        for (int p = 0; p < P; ++p)
+          if (p != me) res.sent_to[(size_t)p] = res.recv_from[(size_t)p] = sb;
+        // and the ranges' gather slots to rank 0
+        const u64 gb = exch_gslot_bytes(eng.exch_gather_records);
+        for (int p = 1; p < P; ++p) {
+          if (me == 0) res.recv_from[(size_t)p] += gb;
+          if (me == p) res.sent_to[0] += gb;
+        }
         res.range_tokens = R[me].total;
         res.range_unique = R[me].n_out;
         res.strategy = DistStrategy::kShuffle;
@@ -688,6 +703,10 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     if (me == 0) r.entries.resize(all_uniq);
     comm.gatherv_known(entries.data(), entries.size() * sizeof(WordCountEntry), sizes.data(),
                        me == 0 ? static_cast<void*>(r.entries.data()) : nullptr, 0);
+    for (int p = 1; p < P; ++p) {  // the ranges' trip to rank 0
+      if (me == 0) res.recv_from[(size_t)p] += sizes[(size_t)p];
+      if (me == p) res.sent_to[0] += sizes[(size_t)p];
+    }
   } else {
     r.entries = std::move(entries);
   }

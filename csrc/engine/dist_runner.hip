@@ -34,7 +34,8 @@ LocalComm resolve_local_comm(const DistConfig& cfg, LocalComm comm) {
 }
 
 std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig>& schedule,
-                                                    const TextInput& whole, LocalComm comm_kind) {
+                                                    const TextInput& whole, LocalComm comm_kind,
+                                                    std::vector<DistResult>* per_rank) {
   LOCUST_CHECK_ARG(!schedule.empty(), "empty job schedule");
   const DistConfig& cfg = schedule[0];
   const int P = cfg.world;
@@ -67,6 +68,7 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
   // clique members whose handle a rank has wrapped (the wrapper owns it from then on)
   std::vector<char> wrapped((size_t)P, 0);
   std::vector<DistResult> results(schedule.size());
+  if (per_rank) per_rank->assign((size_t)P, DistResult{});
   std::vector<std::exception_ptr> errors((size_t)P);
   std::vector<int> error_order((size_t)P, 0);
   std::atomic<int> error_seq{0};
@@ -93,6 +95,11 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
         // the same engines and communicators across jobs, like a long-lived rank
         for (size_t j = 0; j < schedule.size(); ++j) {
           DistResult d = run_distributed(schedule[j], *comm, *eng, shards[(size_t)r]);
+          if (per_rank && j + 1 == schedule.size()) {  // the last job's stats (no entries)
+            DistResult& pr = (*per_rank)[(size_t)r];
+            pr = d;
+            if (r == 0) pr.result.entries = EntryList{};
+          }
           if (r == 0) results[j] = std::move(d);
         }
       } catch (...) {
@@ -117,8 +124,8 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
 }
 
 DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole,
-                                        LocalComm comm) {
-  return run_single_process_schedule({cfg}, whole, comm)[0];
+                                        LocalComm comm, std::vector<DistResult>* per_rank) {
+  return run_single_process_schedule({cfg}, whole, comm, per_rank)[0];
 }
 
 }  // namespace locust

@@ -11,6 +11,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <future>
+#include <memory>
 #include <array>
 #include <cstddef>
 #include <cstdio>
@@ -480,6 +483,7 @@ struct DevicePipeline {
   }
 
   ~DevicePipeline() {
+    if (retune_job.valid()) retune_job.wait();
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& g : dict_graphs) (void)hipGraphExecDestroy(g.exec);
     for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
@@ -1167,9 +1171,37 @@ struct DevicePipeline {
   }
   void maybe_retune(const WordCountEntry* e, u64 n) {
     if (const u64 mx = retune_wanted()) {
+      if (large_ordered && n > (1u << 16)) return retune_async(mx, e, n);
       PartMapTables t;
       retune_with(mx, part_map_from_entries(e, n, &t), t);
     }
+  }
+  // A large output's map is built on a host thread (part_map_from_entries over 200K
+  // entries took ~2 ms of the first job's wall time); the next job takes it if it is ready
+  // and otherwise runs on what it has (the in-job plan, or the current map).  The task
+  // holds the output buffer, which the pool then skips.
+  struct RetuneTask {
+    u64 mx = 0, pred = 0;
+    PartMapTables t;
+  };
+  std::future<RetuneTask> retune_job;
+  void retune_async(u64 mx, const WordCountEntry* e, u64 n) {
+    if (retune_job.valid()) return;  // one at a time
+    std::shared_ptr<HostOut> hold = out_pool[out_idx];
+    retune_job = std::async(std::launch::async, [hold, mx, e, n] {
+      RetuneTask r;
+      r.mx = mx;
+      r.pred = part_map_from_entries(e, n, &r.t);
+      return r;
+    });
+  }
+  // Before a job: adopt a finished background retune (never waits).
+  void poll_retune() {
+    if (!retune_job.valid() ||
+        retune_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
+      return;
+    RetuneTask r = retune_job.get();
+    retune_with(r.mx, r.pred, r.t);
   }
   // The same when the sorted output is device KeyCount records (the distributed map): one
   // D2H of them, only when a rebuild is due.
@@ -1572,6 +1604,7 @@ struct DevicePipeline {
 
   WordCountResult run(const TextInput& in) {
     TraceRange tr("locust:job");
+    poll_retune();
     select_out();  // the previous result may still hold the last output buffer
     // The previous job left d_sync zeroed (self-cleaning ordered run): no reset this time.
     const bool clean_start = sync_clean;

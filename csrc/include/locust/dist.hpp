@@ -300,6 +300,8 @@ struct DistResult {
   double map_ms = 0, shuffle_ms = 0, reduce_ms = 0, gather_ms = 0, total_ms = 0;
   u64 local_records = 0;   // records this rank sent into the shuffle
   u64 sent_bytes = 0, recv_bytes = 0;
+  // the same per peer (this rank's link to rank p; [me] = 0): what each xGMI link carried
+  std::vector<u64> sent_to, recv_from;
   u64 range_tokens = 0, range_unique = 0;  // this rank's key range after the shuffle
   DistStrategy strategy = DistStrategy::kShuffle;  // the one this job took
   bool device_exchange = false;  // the shuffle ran as the one-synchronisation device exchange
@@ -321,12 +323,15 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts);
 // else loopback (N ranks rehearsed on fewer GPUs; RCCL refuses two ranks per device).
 enum class LocalComm : int { kAuto = 0, kLoopback = 1, kRccl = 2 };
 DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole,
-                                        LocalComm comm = LocalComm::kAuto);
+                                        LocalComm comm = LocalComm::kAuto,
+                                        std::vector<DistResult>* per_rank = nullptr);
 // Several jobs back to back on the same ranks (engines and communicators persist, as in a
 // long-lived multi-process job); rank 0's result of every job.
+// per_rank (optional): every rank's result of the last job, in rank order.
 std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig>& schedule,
                                                     const TextInput& whole,
-                                                    LocalComm comm = LocalComm::kAuto);
+                                                    LocalComm comm = LocalComm::kAuto,
+                                                    std::vector<DistResult>* per_rank = nullptr);
 // Visible GPUs (0 if none or the runtime fails).
 int visible_device_count();
 // Which communicator run_single_process_* would use for `world` ranks (for logging).

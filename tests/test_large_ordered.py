@@ -46,7 +46,10 @@ def test_first_job_plans_its_own_map(monkeypatch, tune):
         assert eng.run_text(h).entries() == want
     st = eng.stats()
     assert st["fallbacks"] == 0 and not st["devplan_failed"], st
-    assert st["planned_passes"] == (1 if tune == "1" else 3), st
+    if tune == "1":  # the map tuned from the first output (built on a host thread) takes over
+        assert st["planned_passes"] >= 1 and st["retunes"] >= 1, st
+    else:
+        assert st["planned_passes"] == 3 and st["retunes"] == 0, st
 
 
 def test_staged_bytes_and_small_tiles():
