@@ -15,6 +15,8 @@
 //   --ref-timers (stage times taken where the reference's host timers were)
 // and a synthetic-text generator (BASELINE configs "1M lines" / "10 GB"):
 //   MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]
+#include <sys/resource.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -241,6 +243,8 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
   j.num("wall_ms_median", med);
   j.kv("iters", std::to_string(w.size()));
   j.u("chunks", r.chunks);
+  struct rusage ru;
+  if (getrusage(RUSAGE_SELF, &ru) == 0) j.u("max_rss_kb", (unsigned long long)ru.ru_maxrss);
   emit_json(a, j.done());
 }
 
@@ -314,6 +318,60 @@ int generate(const CliArgs& a) {
   return 0;
 }
 
+void print_gpu_result(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
+  const bool rt = a.cfg.ref_timers;
+  std::printf("GPU mapping %lld nanoseconds \n", ns(rt ? r.times.ref_map_ms : r.times.map_ms));
+  for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
+  std::printf("GPU stream compaction and sorting %lld nanoseconds \n",
+              ns(rt ? r.times.ref_process_ms : r.times.process_ms));
+  std::printf("GPU reduce %lld nanoseconds \n", ns(rt ? r.times.ref_reduce_ms : r.times.reduce_ms));
+  if (r.truncated)
+    LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",
+                    (unsigned long long)r.truncated, a.cfg.max_key_len);
+  std::string out;
+  if (!a.quiet) format_gpu_output(r.entries, &out);
+  std::fflush(stdout);
+  write_all(stdout, out);
+  write_json(a, r, walls);
+  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r.entries);
+  std::printf("\nDone\n");
+}
+
+// Stream threshold: files past one device pass (--chunk-mb, default 256 MiB) stream.
+constexpr u64 kDefaultStreamChunk = 256ull << 20;
+
+int run_direct(const CliArgs& a) {
+  JobConfig cfg = a.cfg;
+  const u64 size = file_size(a.file);
+  const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
+  WordCountResult r;
+  std::vector<double> walls;
+  if (size > chunk) {
+    cfg.chunk_bytes = chunk;
+    GpuWordCount eng(cfg, size, size);
+    for (int i = 0; i < a.warmup + a.iters; ++i) {
+      auto src = open_file_source(a.file);
+      r = eng.run_source(*src);
+      if (i >= a.warmup) walls.push_back(r.times.wall_ms);
+    }
+  } else {
+    GpuWordCount eng(cfg, std::max<u64>(size, 1), std::max<u64>(size, 1));
+    TextInput in;
+    in.data = eng.input_buffer();
+    in.bytes = read_file_into(a.file, eng.input_buffer(), std::max<u64>(size, 1), &in.num_lines);
+    in.first_line = 0;
+    for (int i = 0; i < a.warmup; ++i) eng.run(in);
+    for (int i = 0; i < a.iters; ++i) {
+      r = eng.run(in);
+      walls.push_back(r.times.wall_ms);
+    }
+    r.num_lines = in.num_lines;
+  }
+  std::printf("Length: %i\n", (int)r.num_lines);
+  print_gpu_result(a, r, walls);
+  return 0;
+}
+
 int run(const CliArgs& a) {
   if (!a.gen_out.empty()) return generate(a);
   const bool cpu = a.cfg.backend == Backend::kCpu;
@@ -364,6 +422,13 @@ int run(const CliArgs& a) {
   // CPU build ignores the line window (its loadFile takes none, main.cu:242) -- only
   // reproduced under --ref-compat.
   const bool use_window = a.window && !(cpu && a.cfg.ref_compat);
+  // A whole file on one GPU (the fast dictionary path): no loader copy at all -- the file
+  // is read by parallel preads straight into the engine's pinned input buffer, or, past
+  // one device pass, streamed through two pinned chunks (host memory stays bounded).
+  const bool direct = !cpu && !use_window && a.stage == 0 && !a.gpus_given && a.gpus <= 1 &&
+                      !a.cfg.ref_compat && a.cfg.map_path == MapPath::kFast &&
+                      a.cfg.sort_path == SortPath::kDict;
+  if (direct) return run_direct(a);
   LoadedText text = load_lines(a.file, use_window ? a.line_start : -1,
                                use_window ? a.line_end : -1, a.cfg.ref_compat);
   if (!cpu) std::printf("Length: %i\n", (int)text.input.num_lines);
@@ -444,13 +509,8 @@ int run(const CliArgs& a) {
       r = eng.run(text.input);
       walls.push_back(r.times.wall_ms);
     }
-    const bool rt = a.cfg.ref_timers;
-    std::printf("GPU mapping %lld nanoseconds \n", ns(rt ? r.times.ref_map_ms : r.times.map_ms));
-    for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
-    std::printf("GPU stream compaction and sorting %lld nanoseconds \n",
-                ns(rt ? r.times.ref_process_ms : r.times.process_ms));
-    std::printf("GPU reduce %lld nanoseconds \n",
-                ns(rt ? r.times.ref_reduce_ms : r.times.reduce_ms));
+    print_gpu_result(a, r, walls);
+    return 0;
   }
   if (r.truncated)
     LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",

@@ -23,6 +23,11 @@ char* GpuWordCount::input_buffer() { return impl_->h_text; }
 u64 GpuWordCount::text_capacity() const { return impl_->cap_bytes; }
 
 WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); }
+WordCountResult GpuWordCount::run_source(TextSource& src) {
+  LOCUST_CHECK_ARG(impl_->cfg.chunk_bytes && impl_->cap_bytes <= impl_->cfg.chunk_bytes,
+                   "run_source needs a streaming engine (chunk_bytes set)");
+  return impl_->run_source(src);
+}
 GpuWordCount::Stats GpuWordCount::stats() const {
   Stats s;
   s.retunes = impl_->pm_retunes;

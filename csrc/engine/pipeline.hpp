@@ -308,7 +308,7 @@ struct DevicePipeline {
 
     SizingPlan sz;
     sz.add<char>(cap_bytes + 64);
-    sz.add<u64>(cap_lines + 1);
+    sz.add<u64>(compat ? cap_lines + 1 : 1);  // the line index: compat map only
     sz.add<char>(64);
     for (int j = 0; j < kKeyWords; ++j) {
       sz.add<u64>(slot_cap);
@@ -359,7 +359,7 @@ struct DevicePipeline {
     LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
 
     d_text = arena.take<char>(cap_bytes + 64);
-    d_nl = arena.take<u64>(cap_lines + 1);
+    d_nl = arena.take<u64>(compat ? cap_lines + 1 : 1);
     d_delims = arena.take<char>(64);
     for (int j = 0; j < kKeyWords; ++j) {
       slots.w[j] = arena.take<u64>(slot_cap);
@@ -1807,32 +1807,56 @@ struct DevicePipeline {
   // first).  When the stream has drained, d_ctr->num_unique / flags describe the whole
   // dictionary and h_chunk_ctr[0 .. chunks) holds each chunk's map counters.
   size_t enqueue_stream_insert(const TextInput& in) {
+    const auto chunks = plan_chunks(in);
+    const bool pinned = host_pinned(in.data);
+    size_t k = 0;
+    return enqueue_stream_chunks(!pinned, chunks.size(), [&](int b, const char** src) -> u64 {
+      if (k >= chunks.size()) return 0;
+      const u64 off = chunks[k].first, len = chunks[k].second;
+      ++k;
+      *src = in.data + off;
+      if (!pinned) {  // pageable input: host copy into the pinned half
+        std::memcpy(h_stage[b], in.data + off, len);
+        *src = h_stage[b];
+      }
+      return len;
+    });
+  }
+  // The same from a TextSource (a file): each chunk is read straight into a pinned half
+  // while the device works on the previous ones -- host memory stays two chunks.
+  size_t enqueue_stream_source(TextSource& src_text) {
+    const u64 max_chunks = div_up(std::max<u64>(src_text.size(), 1), cap_bytes / 2) + 2;
+    return enqueue_stream_chunks(true, max_chunks, [&](int b, const char** src) -> u64 {
+      *src = h_stage[b];
+      return src_text.next(h_stage[b], cap_bytes);
+    });
+  }
+  // produce(b, &src): the next chunk's bytes at *src (pinned) -- when `staging`, into
+  // h_stage[b], whose previous H2D has drained by then; returns its length, 0 at the end.
+  template <class Produce>
+  size_t enqueue_stream_chunks(bool staging, u64 max_chunks, Produce&& produce) {
     LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
                      "inputs larger than the engine capacity stream through the dictionary "
                      "path with the fast map (sort=dict, map=fast)");
     LOCUST_CHECK_ARG(cap >= cap_bytes / 2 + 1,
                      "a streaming engine must be sized by bytes (max_lines >= max_bytes / 40)");
-    const auto chunks = plan_chunks(in);
-    const bool pinned = host_pinned(in.data);
-    ensure_stream_buffers(!pinned, chunks.size());
+    ensure_stream_buffers(staging, max_chunks);
     const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
     LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
     LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));
     // the copy stream must not overwrite a text buffer before the reset is queued
     LOCUST_HIP_CHECK(hipEventRecord(ev_copied[1], stream));
     LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_copied[1], 0));
-    for (size_t k = 0; k < chunks.size(); ++k) {
+    size_t k = 0;
+    for (;; ++k) {
       const int b = (int)(k & 1);
       char* dtext = b ? d_text_alt : d_text;
-      const u64 off = chunks[k].first, len = chunks[k].second;
-      const char* src = in.data + off;
-      if (!pinned) {
-        // pageable input: host copy into a pinned half (overlapping the GPU's work on the
-        // previous chunks) once that half's previous H2D has drained
-        if (k >= 2) LOCUST_HIP_CHECK(hipEventSynchronize(ev_copied[b]));
-        std::memcpy(h_stage[b], src, len);
-        src = h_stage[b];
-      }
+      // the staging half's previous H2D must have drained before it is refilled
+      if (staging && k >= 2) LOCUST_HIP_CHECK(hipEventSynchronize(ev_copied[b]));
+      const char* src = nullptr;
+      const u64 len = produce(b, &src);
+      if (!len) break;
+      LOCUST_CHECK_ARG(k < h_chunk_cap, "more stream chunks than planned");
       if (k >= 2) LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[b], 0));
       LOCUST_HIP_CHECK(hipMemcpyAsync(dtext, src, len, hipMemcpyHostToDevice, cstream));
       LOCUST_HIP_CHECK(hipMemsetAsync(dtext + len, 0, 16, cstream));
@@ -1852,7 +1876,7 @@ struct DevicePipeline {
                                     hipMemcpyDeviceToDevice, stream));
     LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->flags, &d_dctr->flags, sizeof(u32),
                                     hipMemcpyDeviceToDevice, stream));
-    return chunks.size();
+    return k;
   }
 
   // After the stream has drained: whole-input map statistics from the chunk snapshots.
@@ -1869,12 +1893,23 @@ struct DevicePipeline {
   }
 
   WordCountResult run_stream(const TextInput& in) {
+    return finish_stream(in.num_lines, [&] { return enqueue_stream_insert(in); });
+  }
+  WordCountResult run_source(TextSource& src) {
+    sync_clean = false;
+    select_out();
+    WordCountResult r = finish_stream(0, [&] { return enqueue_stream_source(src); });
+    r.num_lines = src.lines();
+    return r;
+  }
+  template <class Enqueue>
+  WordCountResult finish_stream(u64 num_lines, Enqueue&& enqueue_chunks) {
     WordCountResult r;
-    r.num_lines = in.num_lines;
+    r.num_lines = num_lines;
     const u64 t0 = now_ns();
     LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
     LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
-    const size_t nchunks = enqueue_stream_insert(in);
+    const size_t nchunks = enqueue_chunks();
     LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
     enqueue_rank();
     LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));

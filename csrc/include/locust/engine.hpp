@@ -124,6 +124,20 @@ struct WordCountResult {
   StageTimes times;
 };
 
+// Text read piece by piece (a file too large to hold): whole lines go straight into the
+// engine's pinned staging, so host memory stays bounded by two chunks whatever the input.
+class TextSource {
+ public:
+  virtual ~TextSource() = default;
+  virtual u64 size() const = 0;  // total bytes (sizes the chunk bookkeeping)
+  // Fills dst (room for cap bytes) with the next whole lines (the last line of the input
+  // may lack its '\n'); returns the bytes written, 0 at the end.
+  virtual u64 next(char* dst, u64 cap) = 0;
+  virtual u64 lines() const = 0;  // lines handed out so far
+};
+// A file read with `threads` concurrent preads per chunk (0: up to 8); see io.cpp.
+std::unique_ptr<TextSource> open_file_source(const std::string& path, u32 threads = 0);
+
 class GpuWordCount {
  public:
   // Capacity is fixed at construction: max_text_bytes / max_lines per device pass.  With
@@ -135,6 +149,10 @@ class GpuWordCount {
   GpuWordCount& operator=(const GpuWordCount&) = delete;
 
   WordCountResult run(const TextInput& in);
+  // A streamed input (a streaming engine: JobConfig.chunk_bytes set, max_text_bytes larger
+  // than it): chunks of chunk_bytes read from `src` into pinned staging, overlapped with
+  // the H2D and the map of the previous chunk.
+  WordCountResult run_source(TextSource& src);
 
   // How the engine's partition map has fared (diagnostics, tests): retunes of the map from
   // a job's output, jobs whose ordered build overflowed an LDS table and fell back to the

@@ -25,8 +25,15 @@ struct LoadedText {
 
 // line_start < 0 selects the whole file.  With ref_compat the reference's line-count
 // quirks are reproduced (B1: the whole-file load and a window running past EOF lose the
-// last line).
+// last line).  A window is read block by block up to its last line and keeps only its own
+// bytes (file_lines then counts the lines scanned); the whole file is read with parallel
+// preads straight into the result.
 LoadedText load_lines(const std::string& path, i64 line_start, i64 line_end, bool ref_compat);
+// Bytes of a file (throws if it cannot be opened).
+u64 file_size(const std::string& path);
+// The whole file into dst (room for cap bytes) by parallel preads; returns its size and
+// sets *lines (a final line without '\n' counts).  dst may be pinned memory.
+u64 read_file_into(const std::string& path, char* dst, u64 cap, u64* lines, u32 threads = 0);
 LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
                             bool ref_compat);
 u64 count_lines(const char* data, u64 bytes);

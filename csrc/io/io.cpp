@@ -1,8 +1,14 @@
 #include "locust/io.hpp"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace locust {
 
@@ -56,19 +62,207 @@ LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 lin
   return lt;
 }
 
+namespace {
+
+u32 io_threads(u32 threads, u64 bytes) {
+  if (threads) return threads;
+  const u32 hw = std::max(1u, std::thread::hardware_concurrency());
+  // one thread per 8 MiB, at most 8 (the GPU box's CPU share is 16)
+  return (u32)std::max<u64>(1, std::min<u64>({(u64)std::min(hw, 8u), bytes >> 23}));
+}
+
+struct Fd {
+  int fd = -1;
+  explicit Fd(const std::string& path) : fd(::open(path.c_str(), O_RDONLY | O_CLOEXEC)) {
+    if (fd < 0) throw Error("cannot open input file: " + path + ": " + std::strerror(errno));
+  }
+  ~Fd() {
+    if (fd >= 0) ::close(fd);
+  }
+  u64 size() const {
+    struct stat st;
+    if (fstat(fd, &st) != 0) throw Error("cannot stat input file");
+    return (u64)st.st_size;
+  }
+};
+
+// [off, off + n) of the file into dst, `threads` preads at once (page-cache reads run at
+// memcpy speed per core); optionally counts the '\n' bytes read.
+u64 pread_parallel(int fd, char* dst, u64 off, u64 n, u32 threads, const std::string& path,
+                   bool count_nl) {
+  threads = std::max<u32>(1, std::min<u64>(threads, std::max<u64>(1, n >> 20)));
+  std::vector<u64> nls(threads, 0);
+  std::vector<std::string> errs(threads);
+  auto work = [&](u32 t) {
+    const u64 a = n * t / threads, b = n * (t + 1) / threads;
+    u64 pos = a;
+    while (pos < b) {
+      const ssize_t k = ::pread(fd, dst + pos, (size_t)std::min<u64>(b - pos, 1ull << 30),
+                                (off_t)(off + pos));
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) {
+        errs[t] = "short read: " + path;
+        return;
+      }
+      pos += (u64)k;
+    }
+    if (count_nl) nls[t] = (u64)std::count(dst + a, dst + b, '\n');
+  };
+  if (threads == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (u32 t = 0; t < threads; ++t) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
+  u64 total = 0;
+  for (u32 t = 0; t < threads; ++t) {
+    if (!errs[t].empty()) throw Error(errs[t]);
+    total += nls[t];
+  }
+  return total;
+}
+
+// A file as line-aligned chunks (TextSource): each chunk is the carried-over partial line
+// of the previous read, then parallel preads, cut after its last '\n'.
+class FileTextSource final : public TextSource {
+ public:
+  FileTextSource(const std::string& path, u32 threads) : path_(path), fd_(path) {
+    size_ = fd_.size();
+    threads_ = io_threads(threads, size_);
+  }
+  u64 size() const override { return size_; }
+  u64 lines() const override { return lines_; }
+  u64 next(char* dst, u64 cap) override {
+    if (pos_ >= size_ && carry_.empty()) return 0;
+    LOCUST_CHECK_ARG(carry_.size() < cap, "a line longer than the stream chunk in " + path_);
+    std::memcpy(dst, carry_.data(), carry_.size());
+    u64 n = carry_.size();
+    u64 nl = (u64)std::count(carry_.begin(), carry_.end(), '\n');
+    carry_.clear();
+    const u64 want = std::min<u64>(cap - n, size_ - pos_);
+    if (want) nl += pread_parallel(fd_.fd, dst + n, pos_, want, threads_, path_, true);
+    pos_ += want;
+    n += want;
+    if (pos_ < size_) {  // keep whole lines: the tail waits for the next chunk
+      const void* p = memrchr(dst, '\n', (size_t)n);
+      if (!p) throw Error("a line longer than the stream chunk (" + std::to_string(cap) +
+                          " B) in " + path_);
+      const u64 cut = (u64)(static_cast<const char*>(p) - dst) + 1;
+      carry_.assign(dst + cut, dst + n);
+      nl -= (u64)std::count(dst + cut, dst + n, '\n');  // (none: cut is after the last)
+      n = cut;
+    } else if (n && dst[n - 1] != '\n') {
+      ++nl;  // the final line without its newline
+    }
+    lines_ += nl;
+    return n;
+  }
+
+ private:
+  std::string path_;
+  Fd fd_;
+  u64 size_ = 0, pos_ = 0, lines_ = 0;
+  u32 threads_ = 1;
+  std::string carry_;
+};
+
+}  // namespace
+
+std::unique_ptr<TextSource> open_file_source(const std::string& path, u32 threads) {
+  return std::unique_ptr<TextSource>(new FileTextSource(path, threads));
+}
+
+u64 file_size(const std::string& path) { return Fd(path).size(); }
+
+u64 read_file_into(const std::string& path, char* dst, u64 cap, u64* lines, u32 threads) {
+  Fd f(path);
+  const u64 n = f.size();
+  LOCUST_CHECK_ARG(n <= cap, "file larger than its buffer: " + path);
+  u64 nl = n ? pread_parallel(f.fd, dst, 0, n, io_threads(threads, n), path, true) : 0;
+  if (n && dst[n - 1] != '\n') ++nl;
+  if (lines) *lines = nl;
+  return n;
+}
+
 LoadedText load_lines(const std::string& path, i64 line_start, i64 line_end, bool ref_compat) {
+  LoadedText lt;
+  lt.window = line_start >= 0;
+  if (!lt.window) {
+    // whole file: straight into the result's storage
+    Fd f(path);
+    const u64 n = f.size();
+    lt.storage.resize(n);
+    lt.storage.reserve(n + 64);
+    u64 nl = n ? pread_parallel(f.fd, lt.storage.data(), 0, n, io_threads(0, n), path, true) : 0;
+    const bool open_end = n && lt.storage[n - 1] != '\n';
+    lt.file_lines = nl + (open_end ? 1 : 0);
+    u64 keep = n, lines = lt.file_lines;
+    if (ref_compat && lines) {  // B1: whole-file mode drops the last line
+      const char* d = lt.storage.data();
+      const u64 end = open_end ? n : n - 1;  // the last line's terminator (or EOF)
+      const void* p = end ? memrchr(d, '\n', (size_t)end) : nullptr;
+      keep = p ? (u64)(static_cast<const char*>(p) - d) + 1 : 0;
+      --lines;
+    }
+    lt.storage.resize(keep);
+    lt.input.data = lt.storage.data();
+    lt.input.bytes = keep;
+    lt.input.num_lines = lines;
+    lt.input.first_line = 0;
+    return lt;
+  }
+  // window [first, last): read 8 MiB blocks up to the window's end, keep only its bytes
   std::FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) throw Error("cannot open input file: " + path);
-  std::fseek(f, 0, SEEK_END);
-  long sz = std::ftell(f);
-  std::fseek(f, 0, SEEK_SET);
-  std::vector<char> buf((size_t)std::max<long>(sz, 0));
-  if (sz > 0 && std::fread(buf.data(), 1, (size_t)sz, f) != (size_t)sz) {
-    std::fclose(f);
-    throw Error("short read: " + path);
+  const u64 first = (u64)line_start;
+  const u64 last = line_end < 0 ? ~0ull : (u64)std::max<i64>(line_end, line_start);
+  std::vector<char> buf(8u << 20);
+  u64 line = 0;          // current line number
+  bool at_start = true;  // the next byte starts a line
+  bool more = false;     // bytes remain after the window's last line (not at EOF)
+  for (;;) {
+    const size_t k = std::fread(buf.data(), 1, buf.size(), f);
+    if (k == 0) break;
+    if (line >= last) {  // the window ended exactly at the previous block's end
+      more = true;
+      break;
+    }
+    const char* p = buf.data();
+    const char* end = p + k;
+    while (p < end && line < last) {
+      const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+      const char* stop = nl ? nl + 1 : end;
+      if (line >= first) lt.storage.insert(lt.storage.end(), p, stop);
+      at_start = nl != nullptr;
+      if (nl) ++line;
+      p = stop;
+    }
+    if (line >= last && p < end) {
+      more = true;
+      break;
+    }
   }
   std::fclose(f);
-  return text_from_buffer(buf.data(), buf.size(), line_start, line_end, ref_compat);
+  if (!at_start) ++line;  // a final line without its newline
+  lt.file_lines = line;   // lines scanned (the whole file when the window reaches EOF)
+  u64 got = line > first ? std::min(line, last) - first : 0;
+  // Reference quirk (main.cu:62-63): a window that reaches EOF reports
+  // line_num - line_start lines, i.e. loses the last line.
+  if (ref_compat && line_end >= 0 && !more && got) {
+    const char* d = lt.storage.data();
+    const u64 n = lt.storage.size();
+    const u64 end = d[n - 1] == '\n' ? n - 1 : n;
+    const void* q = end ? memrchr(d, '\n', (size_t)end) : nullptr;
+    lt.storage.resize(q ? (u64)(static_cast<const char*>(q) - d) + 1 : 0);
+    --got;
+  }
+  lt.storage.reserve(lt.storage.size() + 64);
+  lt.input.data = lt.storage.data();
+  lt.input.bytes = lt.storage.size();
+  lt.input.num_lines = got;
+  lt.input.first_line = std::min<u64>(first, line);
+  return lt;
 }
 
 std::string key_to_string(const PackedKey& k) {

@@ -579,6 +579,22 @@ PYBIND11_MODULE(_locust, m) {
         },
         py::arg("path"), py::arg("line_start") = -1, py::arg("line_end") = -1,
         py::arg("ref_compat") = false);
+  m.def("file_source_chunks",  // the streamed file source's chunks (tests)
+        [](const std::string& path, u64 cap) {
+          auto src = open_file_source(path, 2);
+          std::vector<char> buf(cap);
+          py::list parts;
+          for (u64 n; (n = src->next(buf.data(), cap)) != 0;) parts.append(py::bytes(buf.data(), n));
+          return py::make_tuple(parts, src->lines());
+        });
+  m.def("text_window",  // the in-memory window (the loader's reference semantics)
+        [](const std::string& text, i64 start, i64 end, bool ref_compat) {
+          LoadedText t = text_from_buffer(text.data(), text.size(), start, end, ref_compat);
+          return py::make_tuple(py::bytes(t.storage.data(), t.storage.size()), t.input.num_lines,
+                                t.input.first_line, t.file_lines);
+        },
+        py::arg("text"), py::arg("line_start") = -1, py::arg("line_end") = -1,
+        py::arg("ref_compat") = false);
   m.def("shard_bounds", [](const std::string& text, int parts) {
     TextInput in = as_input(text);
     py::list out;

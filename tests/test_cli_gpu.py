@@ -99,3 +99,39 @@ def test_multi_rank_gpu_cli(cli, hamlet, gpus, comm):
     assert result_lines(p.stdout) == oracle.format_gpu(oracle.wordcount(hamlet)[0])
     want = b"RCCL clique" if comm == "rccl" else b"over loopback"
     assert want in p.stderr
+
+
+def _parse_gpu_out(out: bytes):
+    ent = []
+    for l in out.split(b"\n"):
+        if l.startswith(b"print key: "):
+            k, v, c = re.match(rb"print key: (.*) \t val: (\d+) \t count: (\d+)$", l).groups()
+            ent.append((k, int(v), int(c)))
+    return ent
+
+
+@pytest.mark.parametrize("chunk_mb", [64, 0])
+def test_file_read_direct_and_streamed(tmp_path, cli, chunk_mb):
+    """A generated 320 MB file: streamed through two pinned 64 MiB
+    chunks read by parallel preads (host memory bounded: max RSS far below the file), or
+    read whole straight into the engine's pinned buffer (one device pass); the output is
+    the CPU engine's, protocol lines included."""
+    import json
+
+    import locust_amd as lc
+
+    f = tmp_path / "big.txt"
+    run(cli, "--gen", f, "--gen-bytes", 320 << 20, "--seed", 5)
+    j = tmp_path / "r.json"
+    args = [f, "--json", j] + (["--chunk-mb", chunk_mb] if chunk_mb else [])
+    p = run(cli, *args)
+    text = f.read_bytes()
+    want = lc._C.cpu_run(lc.make_config("cpu"), text)
+    lines = p.stdout.split(b"\n")
+    assert lines[0] == b"Running" and lines[1] == b"Length: %d" % want.num_lines
+    assert _parse_gpu_out(p.stdout) == want.entries()
+    rec = json.loads(j.read_text())
+    assert rec["tokens"] == want.num_tokens and rec["unique"] == want.num_unique
+    if chunk_mb:
+        assert rec["chunks"] >= 5
+        assert rec["max_rss_kb"] < 1 << 20  # < 1 GiB for a 320 MB file
