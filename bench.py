@@ -433,6 +433,12 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gpu" and args.comm == "rccl":
+        # this rank's process on its GPU's NUMA node before the first GPU call (the pinned
+        # shard is first touched there; locust_amd/parallel/numa.py)
+        from locust_amd.parallel.numa import bind_to_gpu
+
+        bind_to_gpu(local_rank)
     if args.gpus != world:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
               f"different GPU count than asked for", file=sys.stderr)

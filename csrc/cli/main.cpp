@@ -15,7 +15,7 @@
 //   --ref-timers (stage times taken where the reference's host timers were)
 // and a synthetic-text generator (BASELINE configs "1M lines" / "10 GB"):
 //   MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]
-#include <sys/resource.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -32,6 +32,8 @@
 using namespace locust;
 
 namespace {
+
+unsigned long long peak_rss_kb();
 
 struct CliArgs {
   std::string file;
@@ -243,8 +245,9 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
   j.num("wall_ms_median", med);
   j.kv("iters", std::to_string(w.size()));
   j.u("chunks", r.chunks);
-  struct rusage ru;
-  if (getrusage(RUSAGE_SELF, &ru) == 0) j.u("max_rss_kb", (unsigned long long)ru.ru_maxrss);
+  // peak resident memory of this process image (VmHWM: unlike getrusage's ru_maxrss it is
+  // not inherited through the fork + exec that started us)
+  j.u("max_rss_kb", peak_rss_kb());
   emit_json(a, j.done());
 }
 
@@ -337,6 +340,28 @@ void print_gpu_result(const CliArgs& a, const WordCountResult& r, const std::vec
   std::printf("\nDone\n");
 }
 
+// Peak resident host memory (kB, VmHWM of /proc/self/status).
+unsigned long long peak_rss_kb() {
+  std::FILE* f = std::fopen("/proc/self/status", "r");
+  if (!f) return 0;
+  char line[256];
+  unsigned long long kb = 0;
+  while (std::fgets(line, sizeof(line), f))
+    if (std::sscanf(line, "VmHWM: %llu kB", &kb) == 1) break;
+  std::fclose(f);
+  return kb;
+}
+
+// Resident host memory now (kB, /proc/self/statm), for LOCUST_LOG=info.
+unsigned long long rss_kb() {
+  std::FILE* f = std::fopen("/proc/self/statm", "r");
+  if (!f) return 0;
+  unsigned long long size = 0, res = 0;
+  if (std::fscanf(f, "%llu %llu", &size, &res) != 2) res = 0;
+  std::fclose(f);
+  return res * (unsigned long long)sysconf(_SC_PAGESIZE) / 1024;
+}
+
 // Stream threshold: files past one device pass (--chunk-mb, default 256 MiB) stream.
 constexpr u64 kDefaultStreamChunk = 256ull << 20;
 
@@ -346,9 +371,11 @@ int run_direct(const CliArgs& a) {
   const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
   WordCountResult r;
   std::vector<double> walls;
+  LOCUST_LOG_INFO("rss before the engine: %llu kB", rss_kb());
   if (size > chunk) {
     cfg.chunk_bytes = chunk;
     GpuWordCount eng(cfg, size, size);
+    LOCUST_LOG_INFO("rss with the streaming engine: %llu kB", rss_kb());
     for (int i = 0; i < a.warmup + a.iters; ++i) {
       auto src = open_file_source(a.file);
       r = eng.run_source(*src);
@@ -367,8 +394,10 @@ int run_direct(const CliArgs& a) {
     }
     r.num_lines = in.num_lines;
   }
+  LOCUST_LOG_INFO("rss after the job: %llu kB", rss_kb());
   std::printf("Length: %i\n", (int)r.num_lines);
   print_gpu_result(a, r, walls);
+  LOCUST_LOG_INFO("rss after the output: %llu kB", rss_kb());
   return 0;
 }
 

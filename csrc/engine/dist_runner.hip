@@ -3,11 +3,13 @@
 // with fewer GPUs than ranks (tests rehearsing 2/4/8 ranks on the one GPU of a test box)
 // the loopback communicator moves data with device copies; the CPU engine uses loopback.
 #include <atomic>
+#include <cstring>
 #include <exception>
 #include <thread>
 
 #include "locust/dist.hpp"
 #include "locust/hip_check.hpp"
+#include "locust/numa.hpp"
 
 namespace locust {
 
@@ -78,6 +80,19 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
       try {
         JobConfig job = cfg.job;
         job.device = gpu ? (cfg.job.device + r) % ndev : 0;
+        if (gpu && numa_enabled()) {
+          // this rank's thread on its GPU's NUMA node before anything is allocated: the
+          // engine's pinned buffers (its copy of the shard below) are first touched there
+          char bdf[64] = {0};
+          if (hipDeviceGetPCIBusId(bdf, (int)sizeof(bdf), job.device) == hipSuccess) {
+            const GpuPlacement pl = placement_for_bdf(bdf);
+            const bool bound = bind_thread_to(pl);
+            LOCUST_LOG_INFO("rank %d on GPU %d (%s): NUMA node %d, %s", r, job.device, bdf,
+                            pl.numa_node, bound ? "thread bound to its CPUs" : "not bound");
+          } else {
+            (void)hipGetLastError();
+          }
+        }
         std::unique_ptr<Communicator> comm;
         if (rccl) {
           LOCUST_HIP_CHECK(hipSetDevice(job.device));
@@ -92,9 +107,18 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
         std::unique_ptr<ShardEngine> eng =
             gpu ? make_gpu_shard_engine(job, shards[(size_t)r].bytes, shards[(size_t)r].num_lines)
                 : make_cpu_shard_engine(job);
+        // the rank's own pinned copy of its shard (not a slice of one shared host buffer):
+        // written by this thread, so on its NUMA node, and uploaded without staging
+        TextInput shard = shards[(size_t)r];
+        if (char* buf = eng->input_buffer()) {
+          if (shard.bytes && (!job.chunk_bytes || shard.bytes <= job.chunk_bytes)) {
+            std::memcpy(buf, shard.data, shard.bytes);
+            shard.data = buf;
+          }
+        }
         // the same engines and communicators across jobs, like a long-lived rank
         for (size_t j = 0; j < schedule.size(); ++j) {
-          DistResult d = run_distributed(schedule[j], *comm, *eng, shards[(size_t)r]);
+          DistResult d = run_distributed(schedule[j], *comm, *eng, shard);
           if (per_rank && j + 1 == schedule.size()) {  // the last job's stats (no entries)
             DistResult& pr = (*per_rank)[(size_t)r];
             pr = d;

@@ -14,6 +14,7 @@
 #include "locust/engine.hpp"
 #include "locust/gen.hpp"
 #include "locust/io.hpp"
+#include "locust/numa.hpp"
 #include "locust/partmap.hpp"
 
 namespace py = pybind11;
@@ -579,6 +580,11 @@ PYBIND11_MODULE(_locust, m) {
         },
         py::arg("path"), py::arg("line_start") = -1, py::arg("line_end") = -1,
         py::arg("ref_compat") = false);
+  m.def("gpu_placement", [](const std::string& bdf, const std::string& sys_root) {
+    const GpuPlacement pl = placement_for_bdf(bdf, sys_root);
+    return py::make_tuple(pl.bdf, pl.numa_node, pl.cpus);
+  }, py::arg("bdf"), py::arg("sys_root") = "/sys");
+  m.def("parse_cpulist", &parse_cpulist);
   m.def("file_source_chunks",  // the streamed file source's chunks (tests)
         [](const std::string& path, u64 cap) {
           auto src = open_file_source(path, 2);

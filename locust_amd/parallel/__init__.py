@@ -145,6 +145,10 @@ def init_rank(cfg, max_bytes: int, max_lines: int, comm: str = "rccl", timeout: 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if cfg.world != world:
         raise ValueError(f"DistConfig.world={cfg.world} but WORLD_SIZE={world}")
+    if comm == "rccl":  # on the GPU's NUMA node before the engine allocates anything
+        from .numa import bind_to_gpu
+
+        bind_to_gpu(cfg.job.device)
     return connect_rank(cfg, rank, world, comm, max_bytes, max_lines, timeout)
 
 
