@@ -15,10 +15,15 @@ struct GpuWordCount::Impl {};
 GpuWordCount::GpuWordCount(const JobConfig&, u64, u64) { no_gpu(); }
 GpuWordCount::~GpuWordCount() = default;
 WordCountResult GpuWordCount::run(const TextInput&) { no_gpu(); }
+WordCountResult GpuWordCount::run_source(TextSource&) { no_gpu(); }
+char* GpuWordCount::input_buffer() { no_gpu(); }
 std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput&, WordCountResult*) { no_gpu(); }
 WordCountResult GpuWordCount::run_reduce_stage(const PackedKey*, u64) { no_gpu(); }
 void copy_device(void*, const void*, u64, bool, void*) { no_gpu(); }
-DistResult run_single_process_multi_gpu(const DistConfig&, const TextInput&, LocalComm) { no_gpu(); }
+DistResult run_single_process_multi_gpu(const DistConfig&, const TextInput&, LocalComm,
+                                        std::vector<DistResult>*) {
+  no_gpu();
+}
 int visible_device_count() { return 0; }
 LocalComm resolve_local_comm(const DistConfig&, LocalComm) { return LocalComm::kLoopback; }
 
