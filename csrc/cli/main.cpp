@@ -276,6 +276,9 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
     x.u("recv_bytes", d.recv_bytes);
     x.kv("sent_to", u64_list(d.sent_to));
     x.kv("recv_from", u64_list(d.recv_from));
+    x.u("output_bytes", d.output_bytes);
+    x.kv("device_exchange", d.device_exchange ? "true" : "false");
+    x.u("host_syncs", (u64)d.host_syncs);
     rk += (r ? ", " : "") + x.done();
   }
   j.kv("ranks", rk + "]");
@@ -371,11 +374,11 @@ int run_direct(const CliArgs& a) {
   const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
   WordCountResult r;
   std::vector<double> walls;
-  LOCUST_LOG_INFO("rss before the engine: %llu kB", rss_kb());
+  LOCUST_LOG_INFO("rss before the engine: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
   if (size > chunk) {
     cfg.chunk_bytes = chunk;
     GpuWordCount eng(cfg, size, size);
-    LOCUST_LOG_INFO("rss with the streaming engine: %llu kB", rss_kb());
+    LOCUST_LOG_INFO("rss with the streaming engine: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
     for (int i = 0; i < a.warmup + a.iters; ++i) {
       auto src = open_file_source(a.file);
       r = eng.run_source(*src);
@@ -394,10 +397,10 @@ int run_direct(const CliArgs& a) {
     }
     r.num_lines = in.num_lines;
   }
-  LOCUST_LOG_INFO("rss after the job: %llu kB", rss_kb());
+  LOCUST_LOG_INFO("rss after the job: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
   std::printf("Length: %i\n", (int)r.num_lines);
   print_gpu_result(a, r, walls);
-  LOCUST_LOG_INFO("rss after the output: %llu kB", rss_kb());
+  LOCUST_LOG_INFO("rss after the output: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
   return 0;
 }
 
@@ -468,6 +471,9 @@ int run(const CliArgs& a) {
   if ((a.gpus > 1 || (a.gpus_given && !cpu)) && a.stage == 0) {
     DistConfig dc;
     dc.job = a.cfg;
+    // ranks always combine map-side (the output is the same; the device exchange and the
+    // gather slots move one record per distinct key instead of one per token)
+    dc.job.combine = true;
     dc.world = std::max(1, a.gpus);
     LOCUST_LOG_INFO("%d ranks in one process over %s", dc.world,
                     resolve_local_comm(dc, a.comm) == LocalComm::kRccl ? "an RCCL clique"

@@ -11,6 +11,7 @@
 
 #include "locust/dist.hpp"
 #include "locust/hip_check.hpp"
+#include "locust/shm.hpp"
 
 namespace locust {
 
@@ -27,6 +28,8 @@ struct LoopbackGroup::State {
   std::vector<u64> bytes;
   std::vector<const u64*> sb, so;
   std::vector<char> gather_buf;
+
+  u64 group = new_group_token();
 
   State(int w, bool d) : world(w), device(d), ptr((size_t)w), bytes((size_t)w), sb((size_t)w), so((size_t)w) {}
 
@@ -61,6 +64,7 @@ class LoopbackComm final : public Communicator {
   int size() const override { return st_->world; }
   const char* name() const override { return "loopback"; }
   bool device_buffers() const override { return st_->device; }
+  u64 group_id() const override { return st_->group; }
 
   void allgather_host(const void* send, void* recv, u64 bytes) override {
     st_->ptr[(size_t)rank_] = send;
@@ -153,6 +157,14 @@ class LoopbackComm final : public Communicator {
 
   void sync_stream(void* stream) override {
     if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  }
+
+  // Blocking rehearsal of the stream-ordered all-to-all-v: the send buffers must be
+  // complete before a peer pulls from them.
+  void alltoallv_device(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
+                        const u64* recv_bytes, const u64* recv_off, void* stream) override {
+    if (st_->device) LOCUST_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    alltoallv(send, send_bytes, send_off, recv, recv_bytes, recv_off, stream);
   }
 
   void alltoallv(const void* send, const u64* send_bytes, const u64* send_off, void* recv,

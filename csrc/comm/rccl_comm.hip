@@ -20,6 +20,7 @@
 
 #include "locust/dist.hpp"
 #include "locust/hip_check.hpp"
+#include "locust/shm.hpp"
 
 #define LOCUST_RCCL_CHECK(expr)                                                        \
   do {                                                                                 \
@@ -39,6 +40,7 @@ class RcclComm final : public Communicator {
            int listen_fd)
       : rank_(rank), world_(world), timeout_s_(timeout_s) {
     tcp_ = make_tcp_comm(rank, world, host, port, timeout_s, listen_fd);
+    group_ = tcp_->group_id();
     ncclUniqueId id;
     if (rank == 0) LOCUST_RCCL_CHECK(ncclGetUniqueId(&id));
     std::vector<ncclUniqueId> ids((size_t)world);
@@ -61,9 +63,9 @@ class RcclComm final : public Communicator {
   // One rank of a single-process clique (ncclCommInitAll): no TCP bootstrap.  The calling
   // thread drives `device`; every rank of the clique runs on its own thread.
   RcclComm(ncclComm_t comm, int rank, int world, int device, double timeout_s,
-           std::shared_ptr<std::atomic<bool>> group_abort)
+           std::shared_ptr<std::atomic<bool>> group_abort, u64 group)
       : rank_(rank), world_(world), timeout_s_(timeout_s), group_abort_(std::move(group_abort)),
-        comm_(comm) {
+        comm_(comm), group_(group) {
     LOCUST_HIP_CHECK(hipSetDevice(device));
     LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     stage_cap_ = 1 << 20;
@@ -93,6 +95,7 @@ class RcclComm final : public Communicator {
     return ncclCommCount(comm_, &n) == ncclSuccess ? n : -1;
   }
   bool device_buffers() const override { return true; }
+  u64 group_id() const override { return group_; }
 
   void allgather_host(const void* send, void* recv, u64 bytes) override {
     ensure_stage(bytes);
@@ -208,6 +211,27 @@ class RcclComm final : public Communicator {
     wait(s);
   }
 
+  // The same, stream-ordered: the sizes come from a count matrix every rank holds.
+  void alltoallv_device(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
+                        const u64* recv_bytes, const u64* recv_off, void* stream) override {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
+    const char* sb = static_cast<const char*>(send);
+    char* rb = static_cast<char*>(recv);
+    if (send_bytes[rank_])
+      LOCUST_HIP_CHECK(hipMemcpyAsync(rb + recv_off[rank_], sb + send_off[rank_], send_bytes[rank_],
+                                      hipMemcpyDeviceToDevice, s));
+    if (world_ == 1) return;
+    LOCUST_RCCL_CHECK(ncclGroupStart());
+    for (int p = 0; p < world_; ++p) {
+      if (p == rank_) continue;
+      if (send_bytes[p])
+        LOCUST_RCCL_CHECK(ncclSend(sb + send_off[p], send_bytes[p], ncclUint8, p, comm_, s));
+      if (recv_bytes[p])
+        LOCUST_RCCL_CHECK(ncclRecv(rb + recv_off[p], recv_bytes[p], ncclUint8, p, comm_, s));
+    }
+    LOCUST_RCCL_CHECK(ncclGroupEnd());
+  }
+
  private:
   void ensure_gather(u64 send_bytes, u64 recv_bytes) {
     if (send_bytes > gsend_cap_) {
@@ -266,6 +290,7 @@ class RcclComm final : public Communicator {
   std::shared_ptr<std::atomic<bool>> group_abort_;
   std::unique_ptr<Communicator> tcp_;
   ncclComm_t comm_ = nullptr;
+  u64 group_ = 0;
   hipStream_t stream_ = nullptr;
   char* d_stage_ = nullptr;
   char* h_stage_ = nullptr;
@@ -292,8 +317,10 @@ std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) 
   LOCUST_RCCL_CHECK(ncclCommInitAll(comms.data(), n, devices.data()));
   std::vector<RcclCliqueMember> out((size_t)n);
   auto abort = std::make_shared<std::atomic<bool>>(false);
+  const u64 group = new_group_token();
   for (int r = 0; r < n; ++r) {
     out[(size_t)r].abort = abort;
+    out[(size_t)r].group = group;
     out[(size_t)r].handle = comms[(size_t)r];
     out[(size_t)r].rank = r;
     out[(size_t)r].world = n;
@@ -304,7 +331,8 @@ std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) 
 
 std::unique_ptr<Communicator> make_rccl_clique_comm(const RcclCliqueMember& m, double timeout_s) {
   return std::unique_ptr<Communicator>(
-      new RcclComm(static_cast<ncclComm_t>(m.handle), m.rank, m.world, m.device, timeout_s, m.abort));
+      new RcclComm(static_cast<ncclComm_t>(m.handle), m.rank, m.world, m.device, timeout_s, m.abort,
+                   m.group));
 }
 
 void release_rccl_clique_member(RcclCliqueMember& m) {

@@ -21,6 +21,7 @@
 #include <thread>
 
 #include "locust/dist.hpp"
+#include "locust/shm.hpp"
 
 namespace locust {
 
@@ -45,6 +46,12 @@ void Communicator::alltoall_device(const void*, void*, u64, void*) {
 
 void Communicator::gather_device(const void*, void*, u64, int, void*) {
   throw Error(std::string("gather_device: the ") + name() +
+              " communicator has no device data plane");
+}
+
+void Communicator::alltoallv_device(const void*, const u64*, const u64*, void*, const u64*,
+                                    const u64*, void*) {
+  throw Error(std::string("alltoallv_device: the ") + name() +
               " communicator has no device data plane");
 }
 
@@ -125,6 +132,7 @@ class TcpComm final : public Communicator {
       : rank_(rank), world_(world), fds_((size_t)world, -1) {
     LOCUST_CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
     if (rank == 0 && listen_fd >= 0) listen_fd_ = listen_fd;  // owned from here on
+    group_ = new_group_token();  // rank 0's is sent to every peer with the handshake
     if (world == 1) return;
     if (rank == 0 && listen_fd_ >= 0) {
       // inherited: already bound to `port` and listening (no window for another process)
@@ -154,6 +162,7 @@ class TcpComm final : public Communicator {
         }
         fds_[(size_t)r] = fd;
       }
+      for (int r = 1; r < world; ++r) send_all(fds_[(size_t)r], &group_, sizeof(group_), r);
     } else {
       sockaddr_in addr = resolve(host, port);
       const u64 deadline = now_ns() + (u64)(timeout_s * 1e9);
@@ -170,6 +179,7 @@ class TcpComm final : public Communicator {
       set_timeouts(fd, timeout_s);
       send_all(fd, &rank_, sizeof(rank_), 0);
       fds_[0] = fd;
+      recv_all(fd, &group_, sizeof(group_), 0);
     }
   }
 
@@ -183,6 +193,7 @@ class TcpComm final : public Communicator {
   int size() const override { return world_; }
   const char* name() const override { return "tcp"; }
   bool device_buffers() const override { return false; }
+  u64 group_id() const override { return group_; }
 
   void allgather_host(const void* send, void* recv, u64 bytes) override {
     char* out = static_cast<char*>(recv);
@@ -270,6 +281,7 @@ class TcpComm final : public Communicator {
 
  private:
   int rank_, world_;
+  u64 group_ = 0;
   int listen_fd_ = -1;
   std::vector<int> fds_;
 };

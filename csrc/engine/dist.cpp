@@ -340,44 +340,92 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     mapped = true;
   }
 
-  // ---------------- shuffle on the device: one host synchronisation ----------------
-  // (locust/exch.hpp) every control step of the sample sort -- splitters, bucket offsets,
-  // overflow and failure agreement, global val offsets -- runs in kernels between four
-  // stream-ordered collectives.  Slot sizes come from the previous shuffle job, so the
-  // first one takes the host-staged path below, which sets them.  With an asynchronous
-  // map (exch_async) even the map is not synchronised: its header and samples are built on
-  // the device in front of the first all-gather -- the whole job is ONE host sync.
-  const bool exch_path =
-      exch_enabled() && cfg.gather && cfg.job.combine && !mapped && plan == DistStrategy::kShuffle &&
-      cfg.strategy != DistStrategy::kGather && comm.device_buffers() && eng.device_buffers() &&
-      eng.exch_slot_records && eng.exch_gather_records && S == kExchSamples &&
-      (cfg.strategy == DistStrategy::kShuffle || eng.exch_last_sum > cfg.gather_max_records) &&
-      (u32)P <= kExchMaxRanks && (u32)P * S <= kExchMaxPlanSamples;
-  bool async_ok = exch_path && exch_async_enabled() && eng.exch_map_async_ok(shard);
-  i32 st1 = 0;
+  // ---------------- shuffle on the device (locust/exch.hpp) ----------------
+  // Every control step of the sample sort -- splitters, bucket offsets, overflow and
+  // failure agreement, global val offsets -- runs in kernels between stream-ordered
+  // collectives, and every rank writes its key range straight into the shared host output
+  // (locust/shm.hpp).  With slot sizes agreed by an earlier job: ONE host sync (with an
+  // asynchronous map even the map is not synchronised).  Otherwise (the first job, a job
+  // whose data outgrew the slots, a gather job that fell back): TWO -- the all-gathered
+  // plans give every rank the exact count matrix, then an all-to-all-v of exact sizes.
+  // The host-staged sequence further down is only the path of host-only communicators
+  // and CPU engines.
+  eng.exch_group = comm.group_id();
+  eng.exch_rank = me;
+  i32 st1 = mapped ? st_slot : 0;
   u64 t1 = 0;
-  for (;;) {  // a second round only when an asynchronous map must be redone
-    const bool exch_async = async_ok;
-    if (exch_async) {
-      st1 = local("map", [&] {
-        TraceRange tr("locust:map_async");
-        eng.exch_map_enqueue(shard, (u32)P, S);
-      });
-      mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});  // (written on the device)
-    } else {
-      st1 = mapped ? st_slot : local("map", [&] {
-        TraceRange tr("locust:map");
-        n_local = eng.map_local(shard, cfg.job.combine, plan);
-        if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
-        eng.map_stats(&local_stats);
-      });
+  const bool dev_exch = exch_enabled() && cfg.gather && cfg.job.combine && comm.device_buffers() &&
+                        eng.device_buffers() && eng.exch_group != 0 && S == kExchSamples &&
+                        (u32)P <= kExchMaxRanks && (u32)P * S <= kExchMaxPlanSamples;
+  if (dev_exch) {
+    TraceRange tr("locust:device_exchange");
+    bool one_sync = !mapped && eng.exch_slot_records && eng.exch_gather_records &&
+                    (cfg.strategy == DistStrategy::kShuffle ||
+                     (cfg.strategy == DistStrategy::kAuto && eng.exch_last_sum > cfg.gather_max_records));
+    bool to_root = false;  // the sized exchange as the gather strategy
+    bool async_ok = !mapped && exch_async_enabled() && eng.exch_map_async_ok(shard);
+    bool map_done = mapped;
+    int syncs = 0;
+    ShardEngine::ExchCollectives coll;
+    coll.allgather = [&](const void* snd, void* rcv, u64 b) {
+      comm.allgather_device(snd, rcv, b, eng.stream());
+    };
+    coll.alltoall = [&](const void* snd, void* rcv, u64 b) {
+      comm.alltoall_device(snd, rcv, b, eng.stream());
+    };
+    coll.alltoallv = [&](const void* snd, const u64* sb, const u64* so, void* rcv, const u64* rb,
+                         const u64* ro) {
+      comm.alltoallv_device(snd, sb, so, rcv, rb, ro, eng.stream());
+    };
+    // A failure after this rank entered the collectives: peers cannot be kept in step from
+    // here; fail this rank (theirs time out or abort in their waits).
+    auto enqueue = [&](const char* stage, const std::function<void()>& fn) {
+      if (local(stage, fn)) {
+        try {
+          comm.sync_stream(eng.stream());
+        } catch (const std::exception&) {
+        }
+        throw Error(std::string("distributed job failed in stage '") + stage + "' on rank " +
+                    std::to_string(me) + ": " + local_msg);
+      }
+    };
+    auto sync = [&] {
+      comm.sync_stream(eng.stream());
+      ++syncs;
+    };
+    auto header_failures = [&](const ExchMsg1* H) {
+      bool redo = false;  // an asynchronous map overflowed a partition somewhere
+      for (int p = 0; p < P; ++p) redo |= H[p].status == kExchMapRedo;
+      for (int p = 0; p < P && !redo; ++p)
+        if (H[p].status)
+          throw Error(std::string("distributed job failed in stage '") +
+                      (H[p].status == 2 ? "exchange" : "map") + "' on rank " +
+                      std::to_string(p) + (p == me ? ": " + local_msg : ""));
+      return redo;
+    };
+    for (;;) {
+      const bool exch_async = async_ok && !map_done;
+      if (exch_async) {
+        st1 = local("map", [&] {
+          TraceRange trm("locust:map_async");
+          eng.exch_map_enqueue(shard, (u32)P, S);
+        });
+        mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});  // (written on the device)
+      } else if (!map_done) {
+        st1 = local("map", [&] {
+          TraceRange trm("locust:map");
+          n_local = eng.map_local(shard, cfg.job.combine, DistStrategy::kShuffle);
+          mine_samples = eng.sample(S);
+          eng.map_stats(&local_stats);
+        });
+        map_done = true;
+      } else if (!st1) {
+        // mapped already (a gather job that fell back, or a one-sync exchange that was
+        // outgrown): the records are sorted for the shuffle, the samples drawn now
+        st1 = local("map", [&] { mine_samples = eng.sample(S); });
+      }
       if (mine_samples.size() != S) mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});
-    }
-    res.local_records = n_local;
-    t1 = now_ns();
-
-    if (exch_path) {
-      TraceRange tr("locust:device_exchange");
+      if (!t1) t1 = now_ns();
       ExchMsg1 h{};
       h.status = st1;
       h.record_flags = eng.record_flags();
@@ -393,54 +441,42 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       }
       // test hook: this rank's asynchronous map "overflowed" (every rank redoes the job)
       if (exch_async && !st1 && fault_injected(me, "exch_map_redo")) h.status = kExchMapRedo;
-      int entered = 0;
-      ShardEngine::ExchCollectives coll;
-      coll.allgather = [&](const void* snd, void* rcv, u64 b) {
-        ++entered;
-        comm.allgather_device(snd, rcv, b, eng.stream());
-      };
-      coll.alltoall = [&](const void* snd, void* rcv, u64 b) {
-        comm.alltoall_device(snd, rcv, b, eng.stream());
-      };
-      coll.gather = [&](const void* snd, void* rcv, u64 b, int root) {
-        comm.gather_device(snd, rcv, b, root, eng.stream());
-      };
-      const i32 stx = local("shuffle", [&] {
-        eng.enqueue_exchange(h, mine_samples, (u32)P, me, 0, coll, exch_async ? &shard : nullptr);
-      });
-      if (stx) {
-        // Failed after (or before) entering the collectives: peers cannot be kept in step
-        // from here; fail this rank (theirs time out and abort in their waits).
-        try {
-          comm.sync_stream(eng.stream());
-        } catch (const std::exception&) {
-        }
-        throw Error(std::string("distributed job failed in stage 'shuffle' on rank ") +
-                    std::to_string(me) + ": " + local_msg);
+      const TextInput* map_shard = exch_async ? &shard : nullptr;
+      if (one_sync) {
+        enqueue("shuffle", [&] { eng.enqueue_exchange(h, mine_samples, (u32)P, me, coll, map_shard); });
+      } else {
+        enqueue("shuffle", [&] {
+          eng.enqueue_exchange_plan(h, mine_samples, (u32)P, me, coll, map_shard);
+        });
       }
-      comm.sync_stream(eng.stream());
-      const ExchMsg1* H = eng.exch_headers();
-      const ExchMsg3* R = eng.exch_reports();
-      bool redo = false;  // an asynchronous map overflowed a partition somewhere
-      for (int p = 0; p < P; ++p) redo |= H[p].status == kExchMapRedo;
-      for (int p = 0; p < P && !redo; ++p)
-        if (H[p].status)
-          throw Error(std::string("distributed job failed in stage '") +
-                      (H[p].status == 2 ? "exchange" : "map") + "' on rank " +
-                      std::to_string(p) + (p == me ? ": " + local_msg : ""));
-      if (redo) {  // every rank saw it: map again synchronously, then exchange again
+      sync();
+      if (header_failures(eng.exch_headers())) {
         LOCUST_LOG_INFO("asynchronous map overflowed a partition: map again, exchange again");
         async_ok = false;
+        map_done = false;
         continue;
       }
-      if (exch_async &&
-          local("map", [&] {
-            n_local = eng.exch_map_complete(shard);
-            eng.map_stats(&local_stats);
-          }))
-        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
-                    std::to_string(me) + ": " + local_msg);
-      res.local_records = n_local;
+      if (exch_async) {
+        if (local("map", [&] {
+              n_local = eng.exch_map_complete(shard);
+              eng.map_stats(&local_stats);
+            }))
+          throw Error(std::string("distributed job failed in stage 'map' on rank ") +
+                      std::to_string(me) + ": " + local_msg);
+        map_done = true;
+      }
+      if (!one_sync) {
+        // every rank holds every plan: the exact count matrix sizes the all-to-all-v.  Few
+        // records in all (auto) or the gather strategy: all of them to the root instead.
+        u64 sum = 0;
+        for (int p = 0; p < P; ++p) sum += eng.exch_plans()[p].off[P];
+        to_root = cfg.strategy == DistStrategy::kGather ||
+                  (cfg.strategy == DistStrategy::kAuto && sum <= cfg.gather_max_records);
+        enqueue("shuffle", [&] { eng.enqueue_exchange_sized((u32)P, me, coll, to_root); });
+        sync();
+      }
+      const ExchMsg1* H = eng.exch_headers();
+      const ExchMsg3* R = eng.exch_reports();
       u32 flags = 0;
       u64 maxb = 0, maxo = 0;
       for (int p = 0; p < P; ++p) {
@@ -450,74 +486,110 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         maxb = std::max<u64>(maxb, R[p].max_bucket);
         maxo = std::max<u64>(maxo, R[p].n_out);
       }
-      // next job's slot sizes: identical on every rank (computed from all-gathered reports)
-      if (flags & (kExchSendOverflow | kExchRecvTruncated))
-        eng.exch_slot_records = std::max(eng.exch_slot_records, exch_grow(maxb));
-      if (flags & kExchGatherOverflow)
-        eng.exch_gather_records = std::max(eng.exch_gather_records, exch_grow(maxo));
-      if (flags & kExchTooManySamples) eng.exch_slot_records = eng.exch_gather_records = 0;
       eng.exch_last_sum = 0;
       for (int p = 0; p < P; ++p) eng.exch_last_sum += H[p].n_local;
-      if (!flags) {
-        if ((int)log_level() >= (int)LogLevel::kDebug)
-          for (int p = 0; p < P; ++p)
-            LOCUST_LOG_DEBUG("exchange header %d: n_local %llu tokens %llu lines %llu", p,
-                             (unsigned long long)H[p].n_local, (unsigned long long)H[p].tokens,
-                             (unsigned long long)H[p].lines);
-        for (int p = 0; p < P; ++p) {
-          r.num_lines += H[p].lines;
-          r.num_tokens += H[p].tokens;
-          r.overflow_lines += H[p].overflow_lines;
-          r.truncated += H[p].truncated;
-          r.max_key_len = std::max<u64>(r.max_key_len, H[p].max_key_len);
-        }
+      if (flags & kExchTooManySamples) throw Error("device exchange: too many samples for the planner");
+      // next job's slot sizes: identical on every rank (computed from all-gathered reports;
+      // a gather-shaped job says nothing about the shuffle's buckets)
+      const bool first_sizing = eng.exch_slot_records == 0;
+      if (!to_root && (!one_sync || (flags & (kExchSendOverflow | kExchRecvTruncated))))
+        eng.exch_slot_records = std::max(eng.exch_slot_records, exch_grow(maxb));
+      if (!to_root && (!one_sync || (flags & kExchGatherOverflow)))
+        eng.exch_gather_records = std::max(eng.exch_gather_records, exch_grow(maxo));
+      {
+        // test hook: LOCUST_EXCH_SLOT=<records> caps the first slot size, so the next job
+        // outgrows it and exercises the agreed fallback + regrowth
+        const char* v = std::getenv("LOCUST_EXCH_SLOT");
+        if (v && first_sizing && !to_root)
+          eng.exch_slot_records = std::min<u32>(eng.exch_slot_records, (u32)std::max(1, std::atoi(v)));
+      }
+      if (flags && !one_sync)
+        throw Error("device exchange: the sized exchange reported overflow flags " +
+                    std::to_string(flags));
+      if (flags) {
+        // outgrown slots: every rank saw the same reports -- the sized exchange, this job
+        LOCUST_LOG_INFO("device exchange slots outgrown (flags %u): sized exchange this job", flags);
+        one_sync = false;
+        continue;
+      }
+      if (H[0].out_region == kExchNoRegion && one_sync) {
+        // the root's results hold every output region: grow the output, write again
+        enqueue("reduce", [&] { eng.enqueue_exchange_emit((u32)P, me); });
+        sync();
+      }
+      if ((int)log_level() >= (int)LogLevel::kDebug)
+        for (int p = 0; p < P; ++p)
+          LOCUST_LOG_DEBUG("exchange header %d: n_local %llu tokens %llu lines %llu", p,
+                           (unsigned long long)H[p].n_local, (unsigned long long)H[p].tokens,
+                           (unsigned long long)H[p].lines);
+      for (int p = 0; p < P; ++p) {
+        r.num_lines += H[p].lines;
+        r.num_tokens += H[p].tokens;
+        r.overflow_lines += H[p].overflow_lines;
+        r.truncated += H[p].truncated;
+        r.max_key_len = std::max<u64>(r.max_key_len, H[p].max_key_len);
+      }
+      res.local_records = n_local;
+      if (one_sync) {
         const u64 sb = exch_slot_bytes(eng.exch_slot_records);
-        res.sent_bytes = sb * (u64)(P - 1);
-        res.recv_bytes = sb * (u64)(P - 1);
         for (int p = 0; p < P; ++p)
           if (p != me) res.sent_to[(size_t)p] = res.recv_from[(size_t)p] = sb;
-        // and the ranges' gather slots to rank 0
-        const u64 gb = exch_gslot_bytes(eng.exch_gather_records);
-        for (int p = 1; p < P; ++p) {
-          if (me == 0) res.recv_from[(size_t)p] += gb;
-          if (me == p) res.sent_to[0] += gb;
-        }
-        res.range_tokens = R[me].total;
-        res.range_unique = R[me].n_out;
-        res.strategy = DistStrategy::kShuffle;
-        res.device_exchange = true;
-        // auto: a job small enough for the gather strategy predicts it for the next one
-        eng.last_strategy = cfg.strategy == DistStrategy::kAuto &&
-                                    eng.exch_last_sum <= cfg.gather_max_records
-                                ? DistStrategy::kGather
-                                : DistStrategy::kShuffle;
-        const u64 t2 = now_ns();
-        if (me == 0) {
-          u64 total = 0, uniq = 0;
-          if (local("reduce", [&] { eng.exch_finish_root(&total, &uniq); }))
-            throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
-          eng.finalize(0, &r.entries);
-        }
-        r.num_unique = me == 0 ? r.entries.size() : R[me].n_out;
-        const u64 t3 = now_ns();
-        res.map_ms = (t1 - t0) * 1e-6;
-        res.shuffle_ms = (t2 - t1) * 1e-6;  // the whole device exchange, one synchronisation
-        res.reduce_ms = (t3 - t2) * 1e-6;
-        res.total_ms = (t3 - t0) * 1e-6;
-        r.times.map_ms = res.map_ms;
-        r.times.process_ms = res.shuffle_ms;
-        r.times.reduce_ms = res.reduce_ms;
-        r.times.wall_ms = res.total_ms;
-        return res;
+      } else {
+        const ExchCtl* pl = eng.exch_plans();
+        for (int p = 0; p < P; ++p)
+          if (p != me) {
+            res.sent_to[(size_t)p] = exch_slot_bytes((u32)(pl[me].off[p + 1] - pl[me].off[p]));
+            res.recv_from[(size_t)p] = exch_slot_bytes((u32)(pl[p].off[me + 1] - pl[p].off[me]));
+          }
       }
-      // outgrown slots: every rank saw the same reports, so all take the step-by-step path
-      LOCUST_LOG_INFO("device exchange slots outgrown (flags %u): host-staged shuffle this job", flags);
-      if (exch_async && local("map", [&] { mine_samples = eng.sample(S); }))
-        throw Error(std::string("distributed job failed in stage 'map' on rank ") +
-                    std::to_string(me) + ": " + local_msg);
+      for (int p = 0; p < P; ++p) {
+        res.sent_bytes += res.sent_to[(size_t)p];
+        res.recv_bytes += res.recv_from[(size_t)p];
+      }
+      res.output_bytes = R[me].n_out * sizeof(WordCountEntry);
+      res.range_tokens = R[me].total;
+      res.range_unique = R[me].n_out;
+      res.strategy = to_root ? DistStrategy::kGather : DistStrategy::kShuffle;
+      res.device_exchange = true;
+      res.host_syncs = syncs;
+      // auto: a job small enough for the gather strategy predicts it for the next one
+      eng.last_strategy = cfg.strategy == DistStrategy::kAuto &&
+                                  eng.exch_last_sum <= cfg.gather_max_records
+                              ? DistStrategy::kGather
+                              : DistStrategy::kShuffle;
+      const u64 t2 = now_ns();
+      if (me == 0) {
+        u64 total = 0, uniq = 0;
+        if (local("reduce", [&] { eng.exch_finish_root((u32)P, &total, &uniq); }))
+          throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
+        eng.finalize(0, &r.entries);
+      }
+      eng.exch_job_done();
+      r.num_unique = me == 0 ? r.entries.size() : R[me].n_out;
+      const u64 t3 = now_ns();
+      res.map_ms = (t1 - t0) * 1e-6;
+      res.shuffle_ms = (t2 - t1) * 1e-6;  // the whole device exchange
+      res.reduce_ms = (t3 - t2) * 1e-6;
+      res.total_ms = (t3 - t0) * 1e-6;
+      r.times.map_ms = res.map_ms;
+      r.times.process_ms = res.shuffle_ms;
+      r.times.reduce_ms = res.reduce_ms;
+      r.times.wall_ms = res.total_ms;
+      return res;
     }
-    break;
   }
+  // ---------------- host-staged shuffle (host-only communicators, CPU engines) ----------------
+  if (!mapped) {
+    st1 = local("map", [&] {
+      TraceRange trm("locust:map");
+      n_local = eng.map_local(shard, cfg.job.combine, plan);
+      if (plan != DistStrategy::kGather) mine_samples = eng.sample(S);
+      eng.map_stats(&local_stats);
+    });
+  }
+  if (mine_samples.size() != S) mine_samples.assign(S, PackedKey{{~0ull, ~0ull, ~0ull, ~0ull}});
+  res.local_records = n_local;
+  t1 = now_ns();
   const u64 m1 = sizeof(Msg1) + (u64)S * sizeof(PackedKey);
   std::vector<char> out1(m1), all1(m1 * (u64)P);
   {

@@ -19,7 +19,7 @@ GpuWordCount::~GpuWordCount() = default;
 
 const JobConfig& GpuWordCount::config() const { return impl_->cfg; }
 u64 GpuWordCount::token_capacity() const { return impl_->cap; }
-char* GpuWordCount::input_buffer() { return impl_->h_text; }
+char* GpuWordCount::input_buffer() { return impl_->ensure_h_text(); }
 u64 GpuWordCount::text_capacity() const { return impl_->cap_bytes; }
 
 WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); }

@@ -161,6 +161,13 @@ struct DevicePipeline {
   // streaming (inputs larger than one chunk), allocated on first use
   char* d_text_alt = nullptr;        // second device text buffer (double buffering)
   char* h_stage[2] = {nullptr, nullptr};  // pinned staging halves for pageable inputs
+  // a TextSource's pinned read ring: kRingPieces pieces of ring_piece bytes, whatever the
+  // chunk size (host memory of a streamed file stays kRingPieces x ring_piece)
+  static constexpr int kRingPieces = 4;
+  static constexpr u64 kRingPieceMax = 16ull << 20;
+  char* h_ring[kRingPieces] = {};
+  hipEvent_t ev_ring[kRingPieces] = {};
+  u64 ring_piece = 0;
   hipStream_t cstream = nullptr;     // H2D copy stream
   // Second copy stream for upload pieces: back-to-back copies on one stream leave the link
   // idle between commands (measured 43 GB/s for 4 MiB pieces on one stream, 52 GB/s
@@ -436,11 +443,9 @@ struct DevicePipeline {
         hipMemcpyAsync(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice, stream));
     LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
 
-    LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      d_h_text = nullptr;  // not device-visible: always DMA
-    }
+    // A streaming engine reads files through its two staging halves; its one-pass buffer
+    // is pinned only when a caller stages text there (input_buffer(), a one-pass job).
+    if (!streaming) ensure_h_text();
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
     // Output records and the counter snapshot are host-mapped: the emit kernel writes them
@@ -499,6 +504,10 @@ struct DevicePipeline {
       if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
       if (ev_consumed[b]) (void)hipEventDestroy(ev_consumed[b]);
       if (h_stage[b]) (void)hipHostFree(h_stage[b]);
+    }
+    for (int i = 0; i < kRingPieces; ++i) {
+      if (h_ring[i]) (void)hipHostFree(h_ring[i]);
+      if (ev_ring[i]) (void)hipEventDestroy(ev_ring[i]);
     }
     for (auto e : ev_piece) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -641,6 +650,7 @@ struct DevicePipeline {
   enum class Upload { kZeroCopy, kDirect, kStaged };
   Upload upload_mode = Upload::kStaged;
   void prepare_upload(const TextInput& in) {
+    ensure_h_text();
     map_text = d_text;
     pieces.clear();
     if (use_zero_copy(in)) {
@@ -1784,6 +1794,16 @@ struct DevicePipeline {
     }
   }
 
+  char* ensure_h_text() {
+    if (h_text) return h_text;
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      d_h_text = nullptr;  // not device-visible: always DMA
+    }
+    return h_text;
+  }
+
   // Line-aligned chunk boundaries, each <= cap_bytes.
   std::vector<std::pair<u64, u64>> plan_chunks(const TextInput& in) const {
     std::vector<std::pair<u64, u64>> out;
@@ -1822,14 +1842,73 @@ struct DevicePipeline {
       return len;
     });
   }
-  // The same from a TextSource (a file): each chunk is read straight into a pinned half
-  // while the device works on the previous ones -- host memory stays two chunks.
+  // The same from a TextSource (a file): line-aligned pieces are read into a small ring of
+  // pinned buffers and copied into the current device chunk while the device maps the
+  // previous chunk -- host memory stays kRingPieces x ring_piece (64 MiB), independent of
+  // the chunk size.  A chunk closes when the next piece would not fit.
   size_t enqueue_stream_source(TextSource& src_text) {
+    LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
+                     "inputs larger than the engine capacity stream through the dictionary "
+                     "path with the fast map (sort=dict, map=fast)");
     const u64 max_chunks = div_up(std::max<u64>(src_text.size(), 1), cap_bytes / 2) + 2;
-    return enqueue_stream_chunks(true, max_chunks, [&](int b, const char** src) -> u64 {
-      *src = h_stage[b];
-      return src_text.next(h_stage[b], cap_bytes);
-    });
+    ensure_stream_buffers(false, max_chunks);
+    const u64 piece = std::min<u64>(cap_bytes, kRingPieceMax);
+    if (ring_piece != piece) {
+      for (int i = 0; i < kRingPieces; ++i) {
+        if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
+        LOCUST_HIP_CHECK(hipHostMalloc(&h_ring[i], piece + 64, hipHostMallocDefault));
+        if (!ev_ring[i]) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
+      }
+      ring_piece = piece;
+    }
+    const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
+    LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));
+    // the copy stream must not overwrite a text buffer before the reset is queued
+    LOCUST_HIP_CHECK(hipEventRecord(ev_copied[1], stream));
+    LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_copied[1], 0));
+    size_t k = 0;  // chunks closed
+    u64 fill = 0;  // bytes in chunk k
+    auto chunk_text = [&](size_t c) { return (c & 1) ? d_text_alt : d_text; };
+    auto close_chunk = [&] {
+      const int b = (int)(k & 1);
+      char* dtext = chunk_text(k);
+      LOCUST_CHECK_ARG(k < h_chunk_cap, "more stream chunks than planned");
+      LOCUST_HIP_CHECK(hipMemsetAsync(dtext + fill, 0, 16, cstream));
+      LOCUST_HIP_CHECK(hipEventRecord(ev_copied[b], cstream));
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+      launch_map_fast(dtext, fill, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap,
+                      d_ctr, lb_map, stream);
+      LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
+                                      hipMemcpyDeviceToHost, stream));
+      launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
+      ++k;
+      fill = 0;
+    };
+    for (u64 r = 0;; ++r) {
+      const int slot = (int)(r % kRingPieces);
+      // the slot's previous H2D must have drained before the source refills it
+      if (r >= (u64)kRingPieces) LOCUST_HIP_CHECK(hipEventSynchronize(ev_ring[slot]));
+      const u64 n = src_text.next(h_ring[slot], piece);
+      if (!n) break;
+      if (fill + n > cap_bytes) close_chunk();
+      // a chunk buffer is refilled only after the map two chunks back consumed it
+      if (fill == 0 && k >= 2)
+        LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[k & 1], 0));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(chunk_text(k) + fill, h_ring[slot], n, hipMemcpyHostToDevice,
+                                      cstream));
+      LOCUST_HIP_CHECK(hipEventRecord(ev_ring[slot], cstream));
+      fill += n;
+    }
+    if (fill) close_chunk();
+    // hand the dictionary's counters to the single-pass stages that follow
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_unique, &d_dctr->num_unique, sizeof(u32),
+                                    hipMemcpyDeviceToDevice, stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->flags, &d_dctr->flags, sizeof(u32),
+                                    hipMemcpyDeviceToDevice, stream));
+    return k;
   }
   // produce(b, &src): the next chunk's bytes at *src (pinned) -- when `staging`, into
   // h_stage[b], whose previous H2D has drained by then; returns its length, 0 at the end.

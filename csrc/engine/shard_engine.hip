@@ -1,6 +1,9 @@
 // Per-rank GPU shard engine of the distributed driver (csrc/engine/dist.cpp): map +
 // combine of this rank's shard, shuffle records and splitter samples, reduce of the
 // received records, and the root's merge of the gather strategy.
+#include <thread>
+
+#include "locust/shm.hpp"
 #include "pipeline.hpp"
 
 namespace locust {
@@ -34,7 +37,7 @@ class GpuShardEngine final : public ShardEngine {
     mp_->sync_clean = false;  // the shard entry points reset the scratch themselves
     return true;
   }
-  char* input_buffer() override { return mp_->h_text; }
+  char* input_buffer() override { return mp_->ensure_h_text(); }
 
   u64 map_local(const TextInput& shard, bool combine, DistStrategy plan) override {
     DevicePipeline& m = *mp_;
@@ -504,7 +507,7 @@ class GpuShardEngine final : public ShardEngine {
   // Enqueues this rank's map (the sorted distinct records end in d_records / sorted keys)
   // and its S samples into the exchange's all-gather send slot.
   void exch_map_enqueue(const TextInput& shard, u32 P, u32 S) override {
-    ensure_exch(P, S, exch_slot_records, exch_gather_records);
+    ensure_exch_ctl(P, S);
     async_combined_ = enqueue_async_map(shard);
     if (S)
       launch_sample_keys(local_keys_, local_n_, S,
@@ -549,8 +552,58 @@ class GpuShardEngine final : public ShardEngine {
     return finish_map_stats(shard, m.h_ctr->num_unique);
   }
 
+  // This rank's ExchMsg1 (+ samples) -> C1 -> plan.  slot_limit: the fixed slot pitch of
+  // the one-sync schedule (larger buckets are flagged), ~0u for the sized one.
+  void enqueue_msg1_plan(const ExchMsg1& h, const std::vector<PackedKey>& samples, u32 P,
+                         u32 slot_limit, const ExchCollectives& coll, const TextInput* map_shard) {
+    DevicePipeline& m = *mp_;
+    const u32 S = (u32)samples.size();
+    const u64 mb = exch_msg1_bytes(S);
+    if (map_shard) {
+      // exch_map_enqueue ran the map and wrote the samples; the header from the counters
+      // (from the ordered kernel's counter snapshot: a small pass re-zeroes d_ctr itself)
+      launch_exch_header(m.d_ctr_mapped, h, async_combined_,
+                         reinterpret_cast<ExchMsg1*>(xb_.msg1_send), m.stream);
+    } else {
+      std::memcpy(xb_.h_msg1, &h, sizeof(ExchMsg1));
+      if (S) std::memcpy(xb_.h_msg1 + sizeof(ExchMsg1), samples.data(), (u64)S * sizeof(PackedKey));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.msg1_send, xb_.h_msg1, mb, hipMemcpyHostToDevice, m.stream));
+    }
+    coll.allgather(xb_.msg1_send, xb_.msg1_all, mb);
+    // a failed map has no valid records: the planner sees the status and every rank's
+    // kernels turn into no-ops, but the collectives still run
+    launch_exch_plan(xb_.msg1_all, P, S, local_keys(), exch_n(h), slot_limit, xb_.ctl, m.stream,
+                     exch_trace());
+  }
+  const u32* exch_n(const ExchMsg1& h) const { return h.status ? xb_.zero_n : local_n(); }
+
+  // merge -> report -> C3 -> emit -> the headers and reports to the host.  region: the
+  // shared output region, or kExchNoRegion to take the root's from its all-gathered header.
+  void enqueue_range_tail(u32 P, int me, u32 C, u32 G, u64 region, const ExchCollectives& coll) {
+    DevicePipeline& m = *mp_;
+    launch_merge_slots_limited(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, C, xb_.merged,
+                               xb_.rctr, xb_.gsend, G, LookbackScratch{xb_.lb_status, xb_.lb_tile},
+                               m.stream);
+    launch_exch_report(xb_.a2a_recv, P, C, xb_.ctl, xb_.rctr, G, xb_.msg3_send, m.stream);
+    coll.allgather(xb_.msg3_send, xb_.msg3_all, sizeof(ExchMsg3));
+    enqueue_emit(P, me, G, region);
+    LOCUST_HIP_CHECK(hipMemcpy2DAsync(xb_.h_hdrs, sizeof(ExchMsg1), xb_.msg1_all,
+                                      exch_msg1_bytes(xb_.S_job), sizeof(ExchMsg1), P,
+                                      hipMemcpyDeviceToHost, m.stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.h_msg3, xb_.msg3_all, (u64)P * sizeof(ExchMsg3),
+                                    hipMemcpyDeviceToHost, m.stream));
+  }
+  void enqueue_emit(u32 P, int me, u32 G, u64 region) {
+    ++out_seq_;
+    launch_exch_emit(xb_.gsend, xb_.msg3_all,
+                     region == kExchNoRegion ? reinterpret_cast<const ExchMsg1*>(xb_.msg1_all)
+                                             : nullptr,
+                     region, out_->regions, out_->region_records, P, (u32)me, G,
+                     out_->d_records, out_->d_stamps, out_seq_, xb_.done, mp_->stream);
+  }
+
   void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples, u32 P,
-                        int me, int root, const ExchCollectives& coll,
+                        int me, const ExchCollectives& coll,
                         const TextInput* map_shard) override {
     DevicePipeline& m = *mp_;
     const u32 S = (u32)samples.size();
@@ -558,46 +611,95 @@ class GpuShardEngine final : public ShardEngine {
     LOCUST_CHECK_ARG(P >= 1 && P <= kExchMaxRanks && C && G, "exchange: bad shape");
     // everything that can allocate or synchronise happens before the first collective
     if (!hdr.status && !map_shard) prepare_shuffle();
-    ensure_exch(P, S, C, G);
-    const bool is_root = me == root;
-    if (is_root) {
-      recv_records(std::max<u64>((u64)P * G, 4096));
-      rp_->grow_host_out((u64)P * G);
-    }
-    const u64 mb = exch_msg1_bytes(S), sb = exch_slot_bytes(C);
-    if (map_shard) {
-      // exch_map_enqueue ran the map and wrote the samples; the header from the counters
-      // (hdr.status != 0: the map failed or was not enqueued -- n_local 0, plan aborts)
-      // (from the ordered kernel's counter snapshot: a small pass re-zeroes d_ctr itself)
-      launch_exch_header(m.d_ctr_mapped, hdr, async_combined_,
-                         reinterpret_cast<ExchMsg1*>(xb_.msg1_send), m.stream);
-    } else {
-      std::memcpy(xb_.h_msg1, &hdr, sizeof(ExchMsg1));
-      if (S) std::memcpy(xb_.h_msg1 + sizeof(ExchMsg1), samples.data(), (u64)S * sizeof(PackedKey));
-      LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.msg1_send, xb_.h_msg1, mb, hipMemcpyHostToDevice, m.stream));
-    }
-    coll.allgather(xb_.msg1_send, xb_.msg1_all, mb);
-    // a failed map has no valid records: the planner sees the status and every rank's
-    // kernels turn into no-ops, but the collectives still run
-    const u32* d_n = hdr.status ? xb_.zero_n : local_n();
-    launch_exch_plan(xb_.msg1_all, P, S, local_keys(), d_n, C, xb_.ctl, m.stream, exch_trace());
-    launch_exch_pack(m.d_records, d_n, m.cap, xb_.ctl, P, C, xb_.a2a_send, m.stream);
-    coll.alltoall(xb_.a2a_send, xb_.a2a_recv, sb);
-    OutRecord* out = is_root ? xb_.groot + (u64)root * G : xb_.gsend;
-    launch_merge_slots_limited(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, C, xb_.merged,
-                               xb_.rctr, out, G, LookbackScratch{xb_.lb_status, xb_.lb_tile},
-                               m.stream);
-    launch_exch_report(xb_.a2a_recv, P, C, xb_.ctl, xb_.rctr, G, xb_.msg3_send, m.stream);
-    coll.allgather(xb_.msg3_send, xb_.msg3_all, sizeof(ExchMsg3));
-    coll.gather(xb_.gsend, xb_.groot, exch_gslot_bytes(G), root);
-    if (is_root)
-      launch_exch_concat(xb_.groot, xb_.msg3_all, P, G, rp_->d_out_mapped, rp_->d_ctr_mapped,
-                         m.stream);
-    LOCUST_HIP_CHECK(hipMemcpy2DAsync(xb_.h_hdrs, sizeof(ExchMsg1), xb_.msg1_all, mb,
-                                      sizeof(ExchMsg1), P, hipMemcpyDeviceToHost, m.stream));
-    LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.h_msg3, xb_.msg3_all, (u64)P * sizeof(ExchMsg3),
+    ensure_exch_ctl(P, S);
+    ensure_exch_data(P, C, G);
+    ensure_out((u64)P * G, 0);
+    ExchMsg1 h = hdr;
+    h.out_region = me == 0 ? pick_region() : 0;
+    job_region_ = h.out_region;
+    enqueue_msg1_plan(h, samples, P, C, coll, map_shard);
+    launch_exch_pack(m.d_records, exch_n(h), m.cap, xb_.ctl, P, C, xb_.a2a_send, m.stream);
+    coll.alltoall(xb_.a2a_send, xb_.a2a_recv, exch_slot_bytes(C));
+    enqueue_range_tail(P, me, C, G, kExchNoRegion, coll);
+  }
+
+  void enqueue_exchange_plan(const ExchMsg1& hdr, const std::vector<PackedKey>& samples, u32 P,
+                             int me, const ExchCollectives& coll,
+                             const TextInput* map_shard) override {
+    DevicePipeline& m = *mp_;
+    const u32 S = (u32)samples.size();
+    LOCUST_CHECK_ARG(P >= 1 && P <= kExchMaxRanks, "exchange: bad shape");
+    if (!hdr.status && !map_shard) prepare_shuffle();
+    ensure_exch_ctl(P, S);
+    ExchMsg1 h = hdr;
+    h.out_region = me == 0 ? pick_region() : 0;
+    enqueue_msg1_plan(h, samples, P, ~0u, coll, map_shard);
+    coll.allgather(xb_.ctl, xb_.ctl_all, sizeof(ExchCtl));
+    LOCUST_HIP_CHECK(hipMemcpy2DAsync(xb_.h_hdrs, sizeof(ExchMsg1), xb_.msg1_all,
+                                      exch_msg1_bytes(S), sizeof(ExchMsg1), P,
+                                      hipMemcpyDeviceToHost, m.stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.h_ctl_all, xb_.ctl_all, (u64)P * sizeof(ExchCtl),
                                     hipMemcpyDeviceToHost, m.stream));
   }
+  const ExchCtl* exch_plans() const override { return xb_.h_ctl_all; }
+
+  void enqueue_exchange_sized(u32 P, int me, const ExchCollectives& coll, bool to_root) override {
+    DevicePipeline& m = *mp_;
+    ExchCtl* pl = xb_.h_ctl_all;
+    const ExchMsg1* H = xb_.h_hdrs;
+    LOCUST_CHECK_ARG(P == xb_.P, "sized exchange: plan of another shape");
+    if (to_root) {
+      // the gather strategy: every rank's records form one bucket, the root's
+      for (u32 p = 0; p < P; ++p) {
+        const u64 n = pl[p].off[P];
+        for (u32 d = 1; d <= P; ++d) pl[p].off[d] = n;
+        pl[p].max_bucket = n;
+      }
+      LOCUST_HIP_CHECK(hipMemcpyAsync(xb_.ctl, pl + me, sizeof(ExchCtl), hipMemcpyHostToDevice,
+                                      m.stream));
+    }
+    // the count matrix: rank p sends cnt(p, d) records to rank d
+    auto cnt = [&](u32 p, u32 d) { return pl[p].off[d + 1] - pl[p].off[d]; };
+    u64 C = 1, G = 1, total = 0;
+    std::vector<u64> recv(P, 0);
+    for (u32 p = 0; p < P; ++p)
+      for (u32 d = 0; d < P; ++d) {
+        const u64 c = cnt(p, d);
+        C = std::max(C, c);
+        recv[d] += c;
+        total += c;
+      }
+    for (u32 d = 0; d < P; ++d) G = std::max(G, recv[d]);
+    LOCUST_CHECK_ARG(C < (1ull << 31) && G < (1ull << 31), "sized exchange: buckets too large");
+    ensure_exch_data(P, (u32)C, (u32)G);
+    // the root's region, or region 0 of a grown output (every rank decides the same)
+    const bool none = H[0].out_region == kExchNoRegion;
+    const bool fresh = ensure_out(std::max<u64>(total, 1), none && out_ ? out_->regions + 1 : 0);
+    job_region_ = fresh ? 0 : H[0].out_region;
+    LOCUST_CHECK_ARG(job_region_ < out_->regions, "sized exchange: bad output region");
+    launch_exch_pack(m.d_records, local_n(), m.cap, xb_.ctl, P, (u32)C, xb_.a2a_send, m.stream);
+    // exact sizes: each slot's header + its records (the pitch stays C)
+    const u64 pitch = exch_slot_bytes((u32)C);
+    std::vector<u64> sb(P), so(P), rb(P), ro(P);
+    for (u32 q = 0; q < P; ++q) {
+      sb[q] = exch_slot_bytes((u32)cnt((u32)me, q));
+      so[q] = q * pitch;
+      rb[q] = exch_slot_bytes((u32)cnt(q, (u32)me));
+      ro[q] = q * pitch;
+    }
+    exch_sent_ = sb;
+    coll.alltoallv(xb_.a2a_send, sb.data(), so.data(), xb_.a2a_recv, rb.data(), ro.data());
+    enqueue_range_tail(P, me, (u32)C, (u32)G, job_region_, coll);
+  }
+  // bytes this rank sent to each peer in the last sized exchange (accounting)
+  std::vector<u64> exch_sent_;
+
+  void enqueue_exchange_emit(u32 P, int me) override {
+    ensure_out(out_->region_records, out_->regions + 1);
+    job_region_ = 0;
+    enqueue_emit(P, me, xb_.G, 0);
+  }
+
   // LOCUST_EXCH_TRACE=1: the plan kernel's phase stamps, printed after each exchange.
   u64* h_exch_trace_ = nullptr;  // host-mapped (leaked with the engine: diagnostics only)
   u64* exch_trace() {
@@ -624,15 +726,45 @@ class GpuShardEngine final : public ShardEngine {
     return xb_.h_hdrs;
   }
   const ExchMsg3* exch_reports() const override { return xb_.h_msg3; }
-  void exch_finish_root(u64* total_count, u64* num_unique) override {
-    DevicePipeline& r = *rp_;
-    *r.h_ctr = *r.h_ctr_mapped;
-    WordCountResult tmp;
-    r.fill_counters(tmp);
-    r.copy_out(tmp.entries, r.h_ctr->num_unique);
-    *total_count = r.h_ctr->total_count;
-    *num_unique = r.h_ctr->num_unique;
-    range_entries_ = std::move(tmp.entries);
+
+  void exch_finish_root(u32 P, u64* total_count, u64* num_unique) override {
+    const ExchMsg3* R = xb_.h_msg3;
+    const u64 G = xb_.G;
+    u64 n = 0, t = 0;
+    for (u32 p = 0; p < P; ++p) {
+      n += std::min<u64>(R[p].n_out, G);
+      t += R[p].total;
+    }
+    LOCUST_CHECK_ARG(n <= out_->region_records, "shared output: range larger than its region");
+    // every rank's range landed when its stamp says this job (its emit fenced its writes
+    // at system scope before the stamp's release store)
+    const u64* stamps = out_->seg.stamps();
+    const u64 deadline = now_ns() + (u64)(out_wait_s() * 1e9);
+    for (u32 p = 0; p < P; ++p) {
+      u64 spins = 0;
+      while (__atomic_load_n(stamps + p, __ATOMIC_ACQUIRE) != out_seq_) {
+        if (now_ns() > deadline)
+          throw Error("shared output: rank " + std::to_string(p) + " did not finish writing its "
+                      "key range within " + std::to_string(out_wait_s()) + " s");
+        if (++spins > 64) std::this_thread::yield();
+      }
+    }
+    range_entries_.adopt(leases_[job_region_],
+                         reinterpret_cast<WordCountEntry*>(out_->seg.records()) +
+                             job_region_ * out_->region_records,
+                         n);
+    *total_count = t;
+    *num_unique = n;
+  }
+  static double out_wait_s() {
+    static const double s = [] {
+      const char* e = std::getenv("LOCUST_OUT_WAIT_S");
+      return e ? std::atof(e) : 120.0;
+    }();
+    return s;
+  }
+  void exch_job_done() override {
+    if (out_) out_->seg.unlink();
   }
 
   u64 complete_map_slot(const TextInput& shard) override {
@@ -964,76 +1096,176 @@ class GpuShardEngine final : public ShardEngine {
     LOCUST_HIP_CHECK(
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_headers_), h_headers_, 0));
   }
-  // Buffers of the device exchange, one device allocation sized for (P, S, C, G).
+  // Buffers of the device exchange: control (sized by P, S) and data (by P x C and G, grown
+  // geometrically: the sized schedule's exact C and G change from job to job).
   struct ExchBufs {
-    u32 P = 0, S = 0, C = 0, G = 0;
-    char* dev = nullptr;
+    u32 P = 0, S = 0, S_job = 0;  // S_job: the samples of the current job's messages
+    u32 C = 0, G = 0;             // the current job's slot pitch and range buffer
+    u64 cap_pc = 0, cap_g = 0;    // data capacities (P x C records, G records)
+    char* ctl_dev = nullptr;
+    char* data_dev = nullptr;
     char* msg1_send = nullptr;
     char* msg1_all = nullptr;
     ExchCtl* ctl = nullptr;
-    char* a2a_send = nullptr;
-    char* a2a_recv = nullptr;
+    ExchCtl* ctl_all = nullptr;
     ExchMsg3* msg3_send = nullptr;
     ExchMsg3* msg3_all = nullptr;
-    OutRecord* gsend = nullptr;
-    OutRecord* groot = nullptr;
+    u32* zero_n = nullptr;
+    u32* done = nullptr;
+    MapCounters* rctr = nullptr;
+    char* a2a_send = nullptr;
+    char* a2a_recv = nullptr;
+    OutRecord* gsend = nullptr;  // this rank's merged range (val local)
     KeyCount* merged = nullptr;
     u64* lb_status = nullptr;
     u32* lb_tile = nullptr;
-    u32* zero_n = nullptr;
-    MapCounters* rctr = nullptr;
-    char* h_msg1 = nullptr;      // pinned staging of this rank's message
-    ExchMsg1* h_hdrs = nullptr;  // pinned: every rank's header after the job
-    ExchMsg3* h_msg3 = nullptr;  // pinned: every rank's report after the job
+    char* h_msg1 = nullptr;        // pinned staging of this rank's message
+    ExchMsg1* h_hdrs = nullptr;    // pinned: every rank's header after the job
+    ExchMsg3* h_msg3 = nullptr;    // pinned: every rank's report after the job
+    ExchCtl* h_ctl_all = nullptr;  // pinned: every rank's plan (sized schedule, phase 1)
   } xb_;
   void free_exch() {
-    if (xb_.dev) (void)hipFree(xb_.dev);
-    for (void* p : {(void*)xb_.h_msg1, (void*)xb_.h_hdrs, (void*)xb_.h_msg3})
+    if (xb_.ctl_dev) (void)hipFree(xb_.ctl_dev);
+    if (xb_.data_dev) (void)hipFree(xb_.data_dev);
+    for (void* p : {(void*)xb_.h_msg1, (void*)xb_.h_hdrs, (void*)xb_.h_msg3, (void*)xb_.h_ctl_all})
       if (p) (void)hipHostFree(p);
     xb_ = ExchBufs{};
   }
-  void ensure_exch(u32 P, u32 S, u32 C, u32 G) {
-    if (xb_.dev && P == xb_.P && S <= xb_.S && C == xb_.C && G == xb_.G) return;
+  void ensure_exch_ctl(u32 P, u32 S) {
+    xb_.S_job = S;
+    if (xb_.ctl_dev && P == xb_.P && S <= xb_.S) return;
     LOCUST_HIP_CHECK(hipStreamSynchronize(mp_->stream));  // nothing may still use the old ones
-    free_exch();
+    free_exch();  // the data buffers are sized for P too
     auto al = [](u64 x) { return align_up(x, (u64)256); };
-    const u64 mb = exch_msg1_bytes(S), sb = exch_slot_bytes(C), gb = exch_gslot_bytes(G);
-    const u64 merge_cap = (u64)P * C;
-    const u64 lbw = merge_scratch_words(merge_cap);
+    const u64 mb = exch_msg1_bytes(S);
     u64 off = 0;
     auto take = [&](u64 bytes) { const u64 o = off; off += al(bytes); return o; };
     const u64 o_m1 = take(mb), o_m1a = take(mb * P), o_ctl = take(sizeof(ExchCtl)),
-              o_as = take(sb * P), o_ar = take(sb * P), o_m3 = take(sizeof(ExchMsg3)),
-              o_m3a = take(sizeof(ExchMsg3) * P), o_gs = take(gb), o_gr = take(gb * P),
-              o_mg = take(merge_cap * sizeof(KeyCount)), o_lb = take(lbw * 8 + 8),
-              o_lt = take(8), o_zn = take(8), o_rc = take(sizeof(MapCounters));
-    LOCUST_HIP_CHECK(hipMalloc(&xb_.dev, off));
+              o_cta = take(sizeof(ExchCtl) * P), o_m3 = take(sizeof(ExchMsg3)),
+              o_m3a = take(sizeof(ExchMsg3) * P), o_zn = take(8), o_dn = take(8),
+              o_rc = take(sizeof(MapCounters));
+    LOCUST_HIP_CHECK(hipMalloc(&xb_.ctl_dev, off));
     // zeroed in stream order: a null-stream hipMemset is not ordered with the engine's
     // non-blocking stream, and with four ranks sharing a GPU it landed after this job's
     // header upload now and then (a rank's header all-gathered as zeros: wrong token sum)
-    LOCUST_HIP_CHECK(hipMemsetAsync(xb_.dev, 0, off, mp_->stream));
-    char* b = xb_.dev;
+    LOCUST_HIP_CHECK(hipMemsetAsync(xb_.ctl_dev, 0, off, mp_->stream));
+    char* b = xb_.ctl_dev;
     xb_.P = P;
     xb_.S = S;
-    xb_.C = C;
-    xb_.G = G;
+    xb_.S_job = S;
     xb_.msg1_send = b + o_m1;
     xb_.msg1_all = b + o_m1a;
     xb_.ctl = reinterpret_cast<ExchCtl*>(b + o_ctl);
-    xb_.a2a_send = b + o_as;
-    xb_.a2a_recv = b + o_ar;
+    xb_.ctl_all = reinterpret_cast<ExchCtl*>(b + o_cta);
     xb_.msg3_send = reinterpret_cast<ExchMsg3*>(b + o_m3);
     xb_.msg3_all = reinterpret_cast<ExchMsg3*>(b + o_m3a);
-    xb_.gsend = reinterpret_cast<OutRecord*>(b + o_gs);
-    xb_.groot = reinterpret_cast<OutRecord*>(b + o_gr);
-    xb_.merged = reinterpret_cast<KeyCount*>(b + o_mg);
-    xb_.lb_status = reinterpret_cast<u64*>(b + o_lb);
-    xb_.lb_tile = reinterpret_cast<u32*>(b + o_lt);
     xb_.zero_n = reinterpret_cast<u32*>(b + o_zn);
+    xb_.done = reinterpret_cast<u32*>(b + o_dn);
     xb_.rctr = reinterpret_cast<MapCounters*>(b + o_rc);
     LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_msg1, mb, hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_hdrs, sizeof(ExchMsg1) * P, hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_msg3, sizeof(ExchMsg3) * P, hipHostMallocDefault));
+    LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_ctl_all, sizeof(ExchCtl) * P, hipHostMallocDefault));
+  }
+  void ensure_exch_data(u32 P, u32 C, u32 G) {
+    LOCUST_CHECK_ARG(xb_.ctl_dev && P == xb_.P, "exchange: control buffers of another shape");
+    xb_.C = C;
+    xb_.G = G;
+    const u64 pc = (u64)P * C;
+    if (xb_.data_dev && pc <= xb_.cap_pc && G <= xb_.cap_g) return;
+    LOCUST_HIP_CHECK(hipStreamSynchronize(mp_->stream));
+    if (xb_.data_dev) (void)hipFree(xb_.data_dev);
+    xb_.cap_pc = std::max<u64>(pc, xb_.cap_pc + xb_.cap_pc / 4);
+    xb_.cap_g = std::max<u64>(G, xb_.cap_g + xb_.cap_g / 4);
+    auto al = [](u64 x) { return align_up(x, (u64)256); };
+    // slots: a header (2 records) per rank + the records
+    const u64 slots_bytes = ((u64)2 * P + xb_.cap_pc) * sizeof(KeyCount);
+    u64 off = 0;
+    auto take = [&](u64 bytes) { const u64 o = off; off += al(bytes); return o; };
+    const u64 o_as = take(slots_bytes), o_ar = take(slots_bytes),
+              o_gs = take(exch_gslot_bytes((u32)xb_.cap_g)),
+              o_mg = take(xb_.cap_pc * sizeof(KeyCount)),
+              o_lb = take(merge_scratch_words(xb_.cap_pc) * 8 + 8), o_lt = take(8);
+    LOCUST_HIP_CHECK(hipMalloc(&xb_.data_dev, off));
+    LOCUST_HIP_CHECK(hipMemsetAsync(xb_.data_dev, 0, off, mp_->stream));
+    char* b = xb_.data_dev;
+    xb_.a2a_send = b + o_as;
+    xb_.a2a_recv = b + o_ar;
+    xb_.gsend = reinterpret_cast<OutRecord*>(b + o_gs);
+    xb_.merged = reinterpret_cast<KeyCount*>(b + o_mg);
+    xb_.lb_status = reinterpret_cast<u64*>(b + o_lb);
+    xb_.lb_tile = reinterpret_cast<u32*>(b + o_lt);
+  }
+
+  // ---- the shared host output (locust/shm.hpp) ----
+  // One generation of it: `regions` regions of `region_records` records each.  The root
+  // lends a region to each result (EntryList::adopt); a region a live result still holds
+  // is not written again -- with none free the output grows by one region.
+  struct OutSegment {
+    ShmSegment seg;
+    u64 region_records = 0;
+    u32 regions = 0;
+    bool registered = false;
+    OutRecord* d_records = nullptr;  // device view of seg.records()
+    u64* d_stamps = nullptr;         // device view of seg.stamps()
+    ~OutSegment() {
+      if (registered) (void)hipHostUnregister(seg.data());
+    }
+  };
+  struct RegionLease {
+    std::shared_ptr<OutSegment> seg;  // keeps the mapping alive while a result holds it
+  };
+  std::shared_ptr<OutSegment> out_;
+  std::vector<std::shared_ptr<RegionLease>> leases_;  // root: one per region
+  u64 out_group_ = 0, out_seq_ = 0, job_region_ = 0;
+  // Room for `records` per region and at least `regions` regions (0: as now, 2 for a new
+  // output); returns whether a new generation was mapped.  Every rank calls it with the
+  // same arguments at the same point of the job sequence.
+  bool ensure_out(u64 records, u32 regions) {
+    LOCUST_CHECK_ARG(exch_group != 0, "device exchange: the communicator has no group id");
+    if (exch_group != out_group_) {
+      out_.reset();
+      leases_.clear();
+      out_group_ = exch_group;
+      out_seq_ = 0;
+    }
+    const u32 K = std::max<u32>(regions, out_ ? out_->regions : 2u);
+    if (out_ && records <= out_->region_records && K <= out_->regions) return false;
+    u64 R = std::max<u64>(records, 4096);
+    if (out_ && records > out_->region_records)
+      R = std::max<u64>(R, out_->region_records + out_->region_records / 2);
+    if (out_) R = std::max<u64>(R, out_->region_records);
+    R = align_up(R, (u64)1024);
+    LOCUST_HIP_CHECK(hipStreamSynchronize(mp_->stream));  // our writes into the old one
+    auto o = std::make_shared<OutSegment>();
+    o->seg.open(shm_segment_name(out_group_, next_segment_gen(out_group_, exch_rank)),
+                shm_segment_bytes(R * K, sizeof(OutRecord)));
+    LOCUST_HIP_CHECK(hipHostRegister(o->seg.data(), o->seg.bytes(),
+                                     hipHostRegisterMapped | hipHostRegisterPortable));
+    o->registered = true;
+    char* d = nullptr;
+    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), o->seg.data(), 0));
+    o->d_stamps = reinterpret_cast<u64*>(d);
+    o->d_records = reinterpret_cast<OutRecord*>(d + kShmHeaderBytes);
+    o->region_records = R;
+    o->regions = K;
+    out_ = o;
+    leases_.clear();
+    for (u32 i = 0; i < K; ++i) leases_.push_back(std::make_shared<RegionLease>(RegionLease{o}));
+    LOCUST_LOG_DEBUG("shared output %s: %u regions x %llu records", o->seg.name().c_str(), K,
+                     (unsigned long long)R);
+    return true;
+  }
+  // Root: a region no live result holds (the one after the last used first), else
+  // kExchNoRegion; region 0 before the output exists.
+  u64 pick_region() const {
+    if (!out_) return 0;
+    const u32 K = out_->regions;
+    for (u32 k = 1; k <= K; ++k) {
+      const u32 i = (u32)((job_region_ + k) % K);
+      if (leases_[i].use_count() == 1) return i;
+    }
+    return kExchNoRegion;
   }
 
   SlotHeader* h_send_header_ = nullptr;  // pinned staging for a host-written header

@@ -92,6 +92,15 @@ class Communicator {
   int agree(int local_error);
   // Ranks the data-plane library itself reports (RCCL: ncclCommCount), else size().
   virtual int comm_count() const { return size(); }
+  // Stream-ordered all-to-all-v of device buffers with exact per-peer byte counts (host
+  // arrays every rank derived from the same all-gathered count matrix): grouped
+  // point-to-point sends/receives, no host wait.  Complete after sync_stream(stream).
+  virtual void alltoallv_device(const void* send, const u64* send_bytes, const u64* send_off,
+                                void* recv, const u64* recv_bytes, const u64* recv_off,
+                                void* stream);
+  // A 64-bit id every rank of this communicator agrees on (fixed at construction, distinct
+  // between groups): names the group's shared output segment (locust/shm.hpp).
+  virtual u64 group_id() const = 0;
 };
 
 // Star-topology TCP communicator (rank 0 relays).  Control plane for everything and the
@@ -115,6 +124,7 @@ std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
 struct RcclCliqueMember {
   void* handle = nullptr;  // ncclComm_t
   int rank = 0, world = 1, device = 0;
+  u64 group = 0;  // the clique's group id (Communicator::group_id)
   std::shared_ptr<std::atomic<bool>> abort;
 };
 std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices);
@@ -237,43 +247,72 @@ class ShardEngine {
   virtual u64 slot_capacity() const { return 0; }
   u32 slot_records = 0;  // agreed slot size for the next job (0: kSlotRecordsMin)
 
-  // ---- shuffle strategy on the device (locust/exch.hpp): one host synchronisation ----
+  // ---- shuffle strategy on the device (locust/exch.hpp) ----
+  // Every rank's key range ends in ONE shared host output (locust/shm.hpp), written by
+  // each rank at its global offset; the root adopts it.  Each collective callback is
+  // called in the documented order on every rank.
   struct ExchCollectives {
     std::function<void(const void* send, void* recv, u64 bytes)> allgather;
     std::function<void(const void* send, void* recv, u64 bytes)> alltoall;
-    std::function<void(const void* send, void* recv, u64 bytes, int root)> gather;
+    std::function<void(const void* send, const u64* send_bytes, const u64* send_off, void* recv,
+                       const u64* recv_bytes, const u64* recv_off)>
+        alltoallv;
   };
-  // Enqueue the whole exchange of this rank's sorted, distinct records (after map_local
-  // and sample()) on stream(): `hdr` + `samples` are this rank's ExchMsg1; every buffer is
-  // sized before the first collective.  Each collective callback is called exactly once,
-  // in the order allgather, alltoall, allgather, gather.  Results after sync_stream:
-  // map_shard (exch_map_async_ok): this rank has NOT mapped yet -- the exchange enqueues
-  // the map first and builds hdr's counts and the samples on the device (hdr carries the
-  // status, record flags and lines; `samples` only its size), so the job has ONE host
-  // synchronisation; afterwards exch_map_complete() (or, if any header says kExchMapRedo,
-  // every rank maps again synchronously).
+  // ONE host synchronisation (slot sizes exch_slot_records / exch_gather_records agreed
+  // by an earlier job): enqueue the whole exchange of this rank's sorted, distinct records
+  // on stream() -- allgather (headers + samples), alltoall (fixed-pitch slots), allgather
+  // (reports), then this rank's range into the shared output.  `hdr` + `samples` are this
+  // rank's ExchMsg1 (the root's out_region is filled in here).  map_shard
+  // (exch_map_async_ok): this rank has NOT mapped yet -- the map is enqueued first and
+  // hdr's counts and the samples are built on the device; afterwards exch_map_complete()
+  // (or, if any header says kExchMapRedo, every rank maps again synchronously).
   virtual void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples,
-                                u32 P, int me, int root, const ExchCollectives& coll,
+                                u32 P, int me, const ExchCollectives& coll,
                                 const TextInput* map_shard = nullptr) {
     throw Error("this engine has no device exchange");
   }
+  // TWO host synchronisations, no sizes needed (the first job, or one whose data outgrew
+  // the agreed slots).  Phase 1: [map] + allgather (headers + samples) + plan + allgather
+  // of every rank's bucket offsets (ExchCtl) -- after its sync exch_headers() and
+  // exch_plans() hold the P x P count matrix.  Phase 2: pack + all-to-all-v with exact
+  // per-peer sizes + merge + allgather (reports) + this rank's range into the shared output.
+  virtual void enqueue_exchange_plan(const ExchMsg1& hdr, const std::vector<PackedKey>& samples,
+                                     u32 P, int me, const ExchCollectives& coll,
+                                     const TextInput* map_shard = nullptr) {
+    throw Error("this engine has no device exchange");
+  }
+  // to_root: the gather strategy on the same machinery -- every record goes to rank 0,
+  // which merges the P runs and writes the whole output.
+  virtual const ExchCtl* exch_plans() const { return nullptr; }  // P plans after phase 1
+  virtual void enqueue_exchange_sized(u32 P, int me, const ExchCollectives& coll, bool to_root) {
+    throw Error("this engine has no device exchange");
+  }
+  // The one-sync exchange found no free output region at the root (every region held by
+  // a live result): after growing the output, write this rank's range again.
+  virtual void enqueue_exchange_emit(u32 P, int me) {}
   virtual bool exch_map_async_ok(const TextInput& /*shard*/) const { return false; }
-  // The map half of an asynchronous-map exchange (before enqueue_exchange, P ranks, S
+  // The map half of an asynchronous-map exchange (before enqueue_exchange*, P ranks, S
   // samples); a throw here becomes the header's failure status.
   virtual void exch_map_enqueue(const TextInput& /*shard*/, u32 /*P*/, u32 /*S*/) {
     throw Error("this engine has no asynchronous-map exchange");
   }
-  // After the one sync of an asynchronous-map exchange: this rank's record count; the local
-  // statistics are then available from map_stats().
+  // After the first sync of an asynchronous-map exchange: this rank's record count; the
+  // local statistics are then available from map_stats().
   virtual u64 exch_map_complete(const TextInput& /*shard*/) { return 0; }
   virtual const ExchMsg1* exch_headers() const { return nullptr; }  // P ExchMsg1 headers
   virtual const ExchMsg3* exch_reports() const { return nullptr; }  // P reports
-  // Root, after the sync: the concatenated output (as finish_merge_slots).
-  virtual void exch_finish_root(u64* total_count, u64* num_unique) {}
+  // Root, after the last sync: wait until every rank's range is in the shared output
+  // (completion stamps), then adopt it as the result (finalize() hands it over).
+  virtual void exch_finish_root(u32 P, u64* total_count, u64* num_unique) {}
+  // Every rank, after the last sync of an exchange job: drop the names of shared output
+  // segments mapped during it (every rank has mapped them by then).
+  virtual void exch_job_done() {}
   // Agreed exchange slot sizes (every rank computes the same from collective data; 0 =
-  // not known yet: the job takes the host-staged shuffle, which then sets them).
+  // not known yet: the job takes the two-sync sized exchange, which then sets them).
   u32 exch_slot_records = 0, exch_gather_records = 0;
   u64 exch_last_sum = 0;  // all ranks' records of the last job (auto: gather or shuffle)
+  u64 exch_group = 0;     // the communicator's group id (names the shared output)
+  int exch_rank = 0;      // this rank in that group
   virtual void finalize(u64 global_offset, EntryList* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;
@@ -300,11 +339,13 @@ struct DistResult {
   double map_ms = 0, shuffle_ms = 0, reduce_ms = 0, gather_ms = 0, total_ms = 0;
   u64 local_records = 0;   // records this rank sent into the shuffle
   u64 sent_bytes = 0, recv_bytes = 0;
+  u64 output_bytes = 0;    // output records this rank wrote to host memory over its own link
   // the same per peer (this rank's link to rank p; [me] = 0): what each xGMI link carried
   std::vector<u64> sent_to, recv_from;
   u64 range_tokens = 0, range_unique = 0;  // this rank's key range after the shuffle
   DistStrategy strategy = DistStrategy::kShuffle;  // the one this job took
-  bool device_exchange = false;  // the shuffle ran as the one-synchronisation device exchange
+  bool device_exchange = false;  // the shuffle ran as the device exchange (locust/exch.hpp)
+  int host_syncs = 0;            // ... with this many host synchronisations
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,

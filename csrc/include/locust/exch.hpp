@@ -5,25 +5,30 @@
 // missing; the GIF's letter-range reducers are design only).  Round 1 built the
 // sample-sort all-to-all with every control step staged through host memory -- five host
 // round trips per job.  The exchange runs the same algorithm with every decision on the
-// device and ONE host synchronisation:
+// device:
 //
-//   H2D      this rank's ExchMsg1 (status, record count, map statistics) + S samples
+//   H2D      this rank's ExchMsg1 (status, record count, map statistics, the root's output
+//            region) + S samples (or both built on the device behind an asynchronous map)
 //   C1       ncclAllGather of the messages
 //   plan     one workgroup: weighted-quantile splitters from all ranks' samples (every
 //            rank computes the same), 64-ary searches of them in the local sorted records
-//   pack     records -> P fixed-size slots (SlotHeader + up to `slot_records` records)
-//   C2       ncclAllToAll of the slots (every xGMI link busy at once)
+//   pack     records -> P slots (SlotHeader + the bucket) at a fixed pitch
+//   C2       the slots to their ranks (every xGMI link busy at once)
 //   merge    the P received sorted runs -> this rank's key range, local val (merge.hip)
 //   report   ExchMsg3 (overflow flags, range size, token total, largest bucket)
 //   C3       ncclAllGather of the reports: every rank sees every flag and total
-//   C4       gather of the ranges to the root (grouped ncclSend/ncclRecv, fixed size)
-//   concat   root: ranges in rank order (= key order) into host-mapped output, val +=
-//            the token totals of the lower ranks (the reference's global val)
+//   emit     this rank's range -> the shared host output (locust/shm.hpp) at its global
+//            offset, val += the token totals of the lower ranks; a completion stamp.  Every
+//            rank drains its own range over its own PCIe link: no gather to the root.
 //
-// Slot sizes are host numbers fixed before the launch: they come from the previous job
-// (largest bucket / range + 1/8).  A job whose data outgrows them is flagged in the
-// reports, which every rank holds, so every rank takes the step-by-step path for that job
-// together and grows the sizes.
+// Two schedules:
+//   one sync   C2 is ncclAllToAll of fixed-size slots sized by an earlier job (largest
+//              bucket / range + 1/8).  A job whose data outgrows them is flagged in the
+//              reports, which every rank holds, and every rank redoes the exchange sized.
+//   two syncs  (the first job, or an outgrown one) C1 -> plan -> C1b: ncclAllGather of
+//              every rank's bucket offsets (ExchCtl) -> host sync: every rank holds the
+//              exact P x P count matrix -> C2 is grouped ncclSend/ncclRecv with exact
+//              per-peer sizes -> merge -> report -> C3 -> emit -> host sync.
 #pragma once
 
 #include "locust/common.hpp"
@@ -36,8 +41,10 @@ struct ExchMsg1 {       // 64 B, followed by S PackedKey samples
   u32 record_flags;     // ShardEngine::kRecords* of this rank's records
   u64 n_local;          // sorted distinct records of this rank
   u64 lines, tokens, overflow_lines, truncated, max_key_len;
-  u64 pad;
+  u64 out_region;       // the root's: shared output region of this job (kExchNoRegion)
 };
+// The root holds no free output region (live results hold them all): grow, then emit.
+constexpr u64 kExchNoRegion = ~0ull;
 static_assert(sizeof(ExchMsg1) == 64, "ExchMsg1 64 B");
 
 constexpr u32 kExchSendOverflow = 1;   // a bucket of this rank exceeded the slot
@@ -58,7 +65,7 @@ struct ExchMsg3 {       // 64 B
 };
 static_assert(sizeof(ExchMsg3) == 64, "ExchMsg3 64 B");
 
-constexpr u32 kExchGatherOverflow = 16; // this rank's range exceeded the gather slot
+constexpr u32 kExchGatherOverflow = 16; // this rank's range exceeded its range buffer
 
 constexpr u32 kExchMaxPlanSamples = 1024;  // P x S the one-workgroup planner sorts in LDS
 constexpr u32 kExchSamples = 64;           // samples per rank
@@ -75,7 +82,7 @@ struct ExchCtl {
 LOCUST_HD inline u64 exch_msg1_bytes(u32 samples) { return sizeof(ExchMsg1) + (u64)samples * sizeof(PackedKey); }
 // All-to-all slot: a SlotHeader (two KeyCount records) + slot_records KeyCount records.
 LOCUST_HD inline u64 exch_slot_bytes(u32 slot_records) { return (u64)(2 + slot_records) * sizeof(KeyCount); }
-// Gather slot: gather_records (key, val, count) 48-B records (the size is in ExchMsg3).
+// Range buffer: gather_records (key, val, count) 48-B records (the size is in ExchMsg3).
 LOCUST_HD inline u64 exch_gslot_bytes(u32 gather_records) { return (u64)gather_records * 48; }
 // Next job's slot size for a largest observed bucket / range of `used` records.
 inline u32 exch_grow(u64 used) {

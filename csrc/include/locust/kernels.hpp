@@ -426,8 +426,15 @@ void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchC
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
                         const MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
                         hipStream_t s);
-void launch_exch_concat(const OutRecord* groot, const ExchMsg3* msg3_all, u32 P,
-                        u32 gather_records, OutRecord* out, MapCounters* ctr_out, hipStream_t s);
+// This rank's range (`range`, val local) -> dst (the shared host output's records, device
+// view) in region `region` (root_msg != nullptr: the region the root's all-gathered
+// ExchMsg1 names) at its global offset with global val; the last workgroup stores `seq`
+// into stamps[me] (system-scope release) after every workgroup's writes.  `done`: a device
+// u32, zero before the launch and left zero.
+void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const ExchMsg1* root_msg,
+                      u64 region, u32 regions, u64 region_records, u32 P, u32 me,
+                      u32 gather_records, OutRecord* dst, u64* stamps, u64 seq, u32* done,
+                      hipStream_t s);
 
 // ---- device self-test of the string library (tests only; StringTestOut in engine.hpp) ----
 void launch_string_selftest(const char* blob, const u32* off, u32 n, const char* delims,

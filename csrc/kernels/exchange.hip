@@ -1,6 +1,6 @@
 // Kernels of the device-resident shuffle (locust/exch.hpp): plan (splitters + bucket
-// offsets), pack (records -> fixed-size all-to-all slots), report (this rank's ExchMsg3)
-// and the root's concat (ranges in rank order -> host-mapped output with global val).
+// offsets), pack (records -> fixed-pitch all-to-all slots), report (this rank's ExchMsg3)
+// and emit (this rank's range -> the shared host output at its global offset, global val).
 // The merge of the received slots is merge.hip's.  Every decision the round-1 driver made
 // on the host between collectives (dist.cpp: choose_splitters, bucket_offsets, the count
 // and total all-gathers) is taken here on the device, so the whole exchange is enqueued
@@ -259,59 +259,66 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
   }
 }
 
-// Root: P gathered ranges (G records each, the first n_out(r) valid, val local to the
-// range) -> host-mapped output in rank order = key order, val += token totals of the lower
-// ranks.  16-B chunks, consecutive lanes on consecutive chunks (full PCIe lines).
-__global__ __launch_bounds__(256) void exch_concat_kernel(const OutRecord* __restrict__ groot,
-                                                          const ExchMsg3* __restrict__ msg3_all,
-                                                          u32 P, u32 gather_records,
-                                                          OutRecord* __restrict__ out,
-                                                          MapCounters* __restrict__ ctr_out) {
-  __shared__ u64 s_roff[kExchMaxRanks + 1], s_voff[kExchMaxRanks + 1];
+// This rank's key range (n_out(me) records, val local to the range) -> the shared host
+// output at its global offset (the records of the lower ranks come first: rank order is key
+// order), val += the token totals of the lower ranks (the reference's global val).  Every
+// rank drains its own range over its own PCIe link at once -- no gather to the root, no
+// root-side concatenation.  16-B chunks, consecutive lanes on consecutive chunks (whole
+// PCIe write lines).  Completion: every workgroup fences its writes at system scope and
+// counts itself done; the last one stores `seq` into this rank's stamp with a system-scope
+// release, which the root's host polls before it reads the output (locust/shm.hpp).
+__global__ __launch_bounds__(256) void exch_emit_kernel(
+    const OutRecord* __restrict__ src, const ExchMsg3* __restrict__ msg3_all,
+    const ExchMsg1* __restrict__ root_msg, u64 region, u32 regions, u64 region_records, u32 P,
+    u32 me, u32 gather_records, OutRecord* __restrict__ dst, u64* __restrict__ stamps, u64 seq,
+    u32* __restrict__ done) {
+  __shared__ u64 s_roff, s_voff, s_n;
   __shared__ u32 s_bad;
   if (threadIdx.x == 0) {
+    // the region: the host's, or the one the root announced in its all-gathered header
+    if (root_msg) region = root_msg->out_region;
     u64 r = 0, v = 0;
     u32 bad = 0;
     for (u32 q = 0; q < P && q < kExchMaxRanks; ++q) {
-      s_roff[q] = r;
-      s_voff[q] = v;
       const ExchMsg3 m = msg3_all[q];
       bad |= (u32)m.status | m.flags;
-      r += m.n_out <= gather_records ? m.n_out : gather_records;
-      v += m.total;
+      if (q < me) {
+        r += m.n_out <= gather_records ? m.n_out : gather_records;
+        v += m.total;
+      }
     }
-    s_roff[P] = r;
-    s_voff[P] = v;
-    s_bad = bad;
+    const u64 n = msg3_all[me].n_out;
+    s_roff = r;
+    s_voff = v;
+    s_n = n <= gather_records ? n : gather_records;
+    // no free region (the host grows the output and emits again), or a range that would
+    // not fit its region (cannot happen with agreed sizes): write nothing, stamp nothing
+    s_bad = bad | (region >= regions || r + s_n > region_records ? 1u : 0u);
+    s_roff = region * region_records + r;
   }
   __syncthreads();
-  if (s_bad) return;  // the host sees the reports and takes the step-by-step path
-  const u64 N = s_roff[P];
-  const uint4* src = reinterpret_cast<const uint4*>(groot);
-  uint4* dst = reinterpret_cast<uint4*>(out);
+  if (s_bad) return;  // the host sees the reports: no output, no stamp
+  const u64 N = s_n, voff = s_voff;
+  const uint4* in = reinterpret_cast<const uint4*>(src);
+  uint4* out = reinterpret_cast<uint4*>(dst + s_roff);
   for (u64 q = (u64)blockIdx.x * 256 + threadIdx.x; q < 3 * N; q += (u64)gridDim.x * 256) {
-    const u64 rec = q / 3;
-    const u32 part = (u32)(q - 3 * rec);
-    u32 lo = 0, hi = P;  // rank of output record `rec`: last r with roff[r] <= rec
-    while (hi - lo > 1) {
-      const u32 mid = (lo + hi) >> 1;
-      if (s_roff[mid] <= rec) lo = mid; else hi = mid;
-    }
-    const u64 i = rec - s_roff[lo];
-    uint4 v = src[((u64)lo * gather_records + i) * 3 + part];
-    if (part == 2) {  // {val, count}: val becomes global
-      const u64 val = (((u64)v.y << 32) | v.x) + s_voff[lo];
+    uint4 v = in[q];
+    if (q % 3 == 2) {  // {val, count}: val becomes global
+      const u64 val = (((u64)v.y << 32) | v.x) + voff;
       v.x = (u32)val;
       v.y = (u32)(val >> 32);
     }
-    dst[q] = v;
+    out[q] = v;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && ctr_out) {
-    MapCounters c{};
-    c.num_records = (u32)N;
-    c.num_unique = (u32)N;
-    c.total_count = s_voff[P];
-    *ctr_out = c;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u32 prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {
+      __threadfence_system();
+      *done = 0u;  // the next job's launch is stream-ordered behind this one
+      __hip_atomic_store(stamps + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -361,13 +368,15 @@ void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
-void launch_exch_concat(const OutRecord* groot, const ExchMsg3* msg3_all, u32 P,
-                        u32 gather_records, OutRecord* out, MapCounters* ctr_out,
-                        hipStream_t s) {
-  const u64 chunks = 3ull * P * gather_records;
+void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const ExchMsg1* root_msg,
+                      u64 region, u32 regions, u64 region_records, u32 P, u32 me,
+                      u32 gather_records, OutRecord* dst, u64* stamps, u64 seq, u32* done,
+                      hipStream_t s) {
+  const u64 chunks = 3ull * gather_records;
   const u64 blocks = std::min<u64>(std::max<u64>(div_up(chunks ? chunks : 1, 256), 1), 2048);
-  exch_concat_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(groot, msg3_all, P, gather_records,
-                                                             out, ctr_out);
+  exch_emit_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(range, msg3_all, root_msg, region,
+                                                           regions, region_records, P, me,
+                                                           gather_records, dst, stamps, seq, done);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

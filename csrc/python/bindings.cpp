@@ -16,6 +16,7 @@
 #include "locust/io.hpp"
 #include "locust/numa.hpp"
 #include "locust/partmap.hpp"
+#include "locust/shm.hpp"
 
 namespace py = pybind11;
 using namespace locust;
@@ -233,6 +234,8 @@ py::dict dist_to_dict(const DistResult& d) {
   x["map_ms"] = d.map_ms;
   x["shuffle_ms"] = d.shuffle_ms;
   x["device_exchange"] = d.device_exchange;
+  x["host_syncs"] = d.host_syncs;
+  x["output_bytes"] = d.output_bytes;
   x["reduce_ms"] = d.reduce_ms;
   x["gather_ms"] = d.gather_ms;
   x["total_ms"] = d.total_ms;
@@ -585,6 +588,31 @@ PYBIND11_MODULE(_locust, m) {
     return py::make_tuple(pl.bdf, pl.numa_node, pl.cpus);
   }, py::arg("bdf"), py::arg("sys_root") = "/sys");
   m.def("parse_cpulist", &parse_cpulist);
+  // the shared output segment (locust/shm.hpp), for host-side tests
+  py::class_<ShmSegment>(m, "ShmSegment")
+      .def(py::init([](const std::string& name, u64 bytes) {
+             auto s = std::make_unique<ShmSegment>();
+             s->open(name, bytes);
+             return s;
+           }),
+           py::arg("name"), py::arg("bytes"))
+      .def_property_readonly("bytes", &ShmSegment::bytes)
+      .def_property_readonly("name", &ShmSegment::name)
+      .def_property_readonly("linked", &ShmSegment::linked)
+      .def("write", [](ShmSegment& s, u64 off, const std::string& b) {
+        LOCUST_CHECK_ARG(off + b.size() <= s.bytes(), "write past the segment");
+        std::memcpy(s.data() + off, b.data(), b.size());
+      })
+      .def("read", [](ShmSegment& s, u64 off, u64 n) {
+        LOCUST_CHECK_ARG(off + n <= s.bytes(), "read past the segment");
+        return py::bytes(s.data() + off, n);
+      })
+      .def("unlink", &ShmSegment::unlink)
+      .def("close", &ShmSegment::close);
+  m.def("shm_segment_name", &shm_segment_name);
+  m.def("shm_segment_bytes", &shm_segment_bytes);
+  m.def("next_segment_gen", &next_segment_gen);
+  m.def("new_group_token", &new_group_token);
   m.def("file_source_chunks",  // the streamed file source's chunks (tests)
         [](const std::string& path, u64 cap) {
           auto src = open_file_source(path, 2);

@@ -135,3 +135,27 @@ def test_file_read_direct_and_streamed(tmp_path, cli, mb, chunk_mb):
     if chunk_mb:
         assert rec["chunks"] >= mb // chunk_mb
         assert rec["max_rss_kb"] < 1 << 20  # < 1 GiB for a 320 MB file
+
+
+@pytest.mark.parametrize("gpus", [2, 4, 8])
+def test_multi_rank_cli_first_job_on_device(tmp_path, cli, gpus):
+    """the CLI runs ONE job per process, so its shuffle is always a
+    first job.  It runs on the device -- the all-gathered plans size an exact all-to-all-v,
+    every rank writes its key range into the shared host output -- with at most two host
+    synchronisations per rank; the output is the CPU engine's, byte for byte."""
+    import json
+
+    import locust_amd as lc
+
+    f = tmp_path / "synth.txt"
+    run(cli, "--gen", f, "--gen-lines", 1_000_000, "--seed", 1)
+    j = tmp_path / "r.json"
+    p = run(cli, f, "--gpus", gpus, "--comm", "loopback", "--json", j)
+    want = lc._C.cpu_run(lc.make_config("cpu"), f.read_bytes())
+    assert _parse_gpu_out(p.stdout) == want.entries()
+    rec = json.loads(j.read_text())
+    assert rec["strategy"] == "shuffle" and len(rec["ranks"]) == gpus
+    for rk in rec["ranks"]:
+        assert rk["device_exchange"] is True and 1 <= rk["host_syncs"] <= 2, rk
+        assert rk["output_bytes"] == rk["range_unique"] * 48
+    assert sum(rk["range_unique"] for rk in rec["ranks"]) == want.num_unique

@@ -254,16 +254,20 @@ def test_gpu_rccl_failure_after_allgather_entered(hamlet, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_gpu_device_exchange_loopback(hamlet, world):
-    """Shuffle jobs back to back: the first runs host-staged and sizes the slots, the next
-    run as the device exchange (plan/pack/all-to-all/merge/report/gather/concat) and match
-    the oracle byte for byte, including the global val."""
+    """Shuffle jobs back to back, all on the device: the first is the sized exchange (two
+    host syncs: the all-gathered plans give the exact count matrix), the next the one-sync
+    exchange with the slots it sized; every rank writes its range into the shared host
+    output, and rank 0's result matches the oracle byte for byte, including the global val."""
     job = lc.make_config("gpu", combine=True, check=True)
     cfgs = [lc.make_dist_config(world, job, strategy="shuffle") for _ in range(4)]
     ent, ntok, _ = oracle.wordcount(hamlet)
     out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback" if world > 1 else "auto")
+    # (the schedule keeps every result alive: once they hold both output regions, a job
+    # grows the output and writes again -- 2 syncs; see the regions test below)
+    assert [i["host_syncs"] for _, i in out][:2] == [2, 1]
     for j, (res, info) in enumerate(out):
         assert info["strategy"] == "shuffle"
-        assert info["device_exchange"] == (j > 0), (j, info)
+        assert info["device_exchange"], (j, info)
         assert res.entries() == ent and res.num_tokens == ntok
 
 
@@ -274,7 +278,8 @@ def test_gpu_device_exchange_many_keys():
     job = lc.make_config("gpu", combine=True, check=True)
     cfgs = [lc.make_dist_config(4, job, strategy="shuffle") for _ in range(3)]
     out = lc._C.run_multi_schedule(text, cfgs, "loopback")
-    assert [i["device_exchange"] for _, i in out] == [False, True, True]
+    assert [i["device_exchange"] for _, i in out] == [True, True, True]
+    assert [i["host_syncs"] for _, i in out][:2] == [2, 1]
     for res, _ in out:
         assert res.entries() == ent
 
@@ -282,14 +287,14 @@ def test_gpu_device_exchange_many_keys():
 @pytest.mark.gpu
 def test_gpu_device_exchange_outgrown_slots(hamlet, monkeypatch):
     """Slots capped below the data (test hook): every rank sees the overflow in the
-    all-gathered reports, the job takes the host-staged path together, the slots grow and
-    the next job is a device exchange again."""
+    all-gathered reports, every rank redoes the job with the sized exchange (1 + 2 host
+    syncs), the slots grow and the next job is a one-sync exchange again."""
     monkeypatch.setenv("LOCUST_EXCH_SLOT", "16")
     job = lc.make_config("gpu", combine=True, check=True)
     cfgs = [lc.make_dist_config(3, job, strategy="shuffle") for _ in range(3)]
     ent = oracle.wordcount(hamlet)[0]
     out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback")
-    assert [i["device_exchange"] for _, i in out] == [False, False, True]
+    assert [i["host_syncs"] for _, i in out][:2] == [2, 3]
     for res, _ in out:
         assert res.entries() == ent
 
@@ -317,9 +322,9 @@ def test_gpu_device_exchange_one_rccl_rank(hamlet):
     used = []
     for _ in range(4):
         res, info = dr.run(hamlet, 0)
-        used.append(info["device_exchange"])
+        used.append((info["device_exchange"], info["host_syncs"]))
         assert res.entries() == ent and res.num_tokens == ntok
-    assert used == [False, True, True, True]
+    assert used == [(True, 2), (True, 1), (True, 1), (True, 1)]
 
 
 @pytest.mark.gpu
@@ -334,5 +339,25 @@ def test_gpu_device_exchange_async_map_redo(hamlet, monkeypatch, world):
     ent, ntok, _ = oracle.wordcount(hamlet)
     out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback")
     for j, (res, info) in enumerate(out):
-        assert info["device_exchange"] == (j > 0), (j, info)
+        assert info["device_exchange"], (j, info)
         assert res.entries() == ent and res.num_tokens == ntok
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gpu_shared_output_regions_held_by_results(hamlet, world):
+    """The root lends a shared-output region to each result: results kept alive across
+    jobs (three at once, two regions) make the root announce 'no free region' -- every rank
+    grows the output and writes its range again -- and every kept result stays intact."""
+    job = lc.make_config("gpu", combine=True, check=True)
+    nlines = hamlet.count(b"\n") + (0 if hamlet.endswith(b"\n") else 1)
+    cfgs = [lc.make_dist_config(world, job, strategy="shuffle") for _ in range(5)]
+    ent, ntok, _ = oracle.wordcount(hamlet)
+    out = lc._C.run_multi_schedule(hamlet, cfgs, "loopback")
+    # every result of the schedule is alive at the end (the list holds them)
+    for res, info in out:
+        assert info["device_exchange"]
+        assert res.entries() == ent and res.num_tokens == ntok
+    syncs = [i["host_syncs"] for _, i in out]
+    assert syncs[0] == 2 and 2 in syncs[1:] and max(syncs) == 2, syncs
+    assert nlines > 0

@@ -1,0 +1,52 @@
+// Host RSS of the HIP runtime's own first-use steps (what a one-shot CLI job pays before
+// its engine allocates anything).  Build: hipcc --offload-arch=gfx950 -O2 tools/rss_probe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+// "RssAnon/RssFile/RssShmem" of /proc/self/status, kB.
+static void rss(char* out, size_t n) {
+  std::FILE* f = std::fopen("/proc/self/status", "r");
+  unsigned long long a = 0, fi = 0, sh = 0, v = 0;
+  char line[256];
+  while (f && std::fgets(line, sizeof(line), f)) {
+    if (std::sscanf(line, "RssAnon: %llu", &v) == 1) a = v;
+    if (std::sscanf(line, "RssFile: %llu", &v) == 1) fi = v;
+    if (std::sscanf(line, "RssShmem: %llu", &v) == 1) sh = v;
+  }
+  if (f) std::fclose(f);
+  std::snprintf(out, n, "rss %7llu kB (anon %7llu file %7llu shmem %7llu)", a + fi + sh, a, fi, sh);
+}
+
+__global__ void touch(int* p) { p[threadIdx.x] = threadIdx.x; }
+
+#define STEP(what, call)                                                         \
+  do {                                                                           \
+    hipError_t e_ = (call);                                                      \
+    char b_[160];                                                                \
+    rss(b_, sizeof(b_));                                                         \
+    std::printf("%-30s %s %s\n", what, e_ == hipSuccess ? "ok " : "ERR", b_);     \
+  } while (0)
+
+int main() {
+  char b0[160];
+  rss(b0, sizeof(b0));
+  std::printf("%-30s     %s\n", "start", b0);
+  STEP("hipInit", hipInit(0));
+  int n = 0;
+  STEP("hipGetDeviceCount", hipGetDeviceCount(&n));
+  STEP("hipSetDevice", hipSetDevice(0));
+  STEP("hipFree(0)", hipFree(nullptr));
+  hipStream_t s;
+  STEP("hipStreamCreate", hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  int* d = nullptr;
+  STEP("hipMalloc 1 GiB", hipMalloc(&d, 1ull << 30));
+  touch<<<1, 64, 0, s>>>(d);
+  STEP("first kernel", hipStreamSynchronize(s));
+  void* h = nullptr;
+  STEP("hipHostMalloc 64 MiB", hipHostMalloc(&h, 64ull << 20, hipHostMallocDefault));
+  void* m = nullptr;
+  STEP("hipHostMalloc mapped 16 MiB", hipHostMalloc(&m, 16ull << 20, hipHostMallocMapped));
+  STEP("hipMemcpyAsync H2D 64 MiB", hipMemcpyAsync(d, h, 64ull << 20, hipMemcpyHostToDevice, s));
+  STEP("sync", hipStreamSynchronize(s));
+  return 0;
+}
