@@ -565,8 +565,6 @@ int run(const CliArgs& a) {
 int main(int argc, char** argv) {
   // before any thread or RCCL use (see locust_amd/__init__.py); a user's setting wins
   setenv("NCCL_GRAPH_REGISTER", "0", 0);
-  // every code object loaded at runtime start, not lazily inside the (only) job
-  setenv("HIP_ENABLE_DEFERRED_LOADING", "0", 0);
   std::printf("Running\n");
   CliArgs a;
   try {

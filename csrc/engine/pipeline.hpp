@@ -14,6 +14,7 @@
 #include <chrono>
 #include <future>
 #include <memory>
+#include <mutex>
 #include <array>
 #include <cstddef>
 #include <cstdio>
@@ -268,6 +269,17 @@ struct DevicePipeline {
   PackedKey* h_small = nullptr;
   u64* h_u64 = nullptr;
 
+  // This library's code objects on `device`, once per process (kernels.hpp).
+  static void warm_modules_once(int device) {
+    static std::mutex mu;
+    static u64 warmed = 0;  // bit per device
+    std::lock_guard<std::mutex> lk(mu);
+    const u64 bit = 1ull << (device & 63);
+    if (warmed & bit) return;
+    warm_kernel_modules();
+    warmed |= bit;
+  }
+
   DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines, u64 cap_records = 0)
       : cfg(c) {
     LOCUST_CHECK_ARG(cfg.emits_per_line > 0, "emits_per_line must be > 0");
@@ -290,6 +302,7 @@ struct DevicePipeline {
     cap = std::max<u64>(cap, 1);
     LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
     LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
+    warm_modules_once(cfg.device);
     LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto& e : ev) LOCUST_HIP_CHECK(hipEventCreate(&e));
 
@@ -993,8 +1006,38 @@ struct DevicePipeline {
   // counter snapshot when every possible key fits it (then the host needs no D2H), else
   // into d_out.  Events (optional; not while capturing) mark the stage ends.
   bool radix_mapped() const { return h_out_cap >= cap; }
+  // LOCUST_RADIX_FUSED=0: A/B against the separate partitioned sort + fused reduce
+  static bool radix_fused_enabled() {
+    const char* v = std::getenv("LOCUST_RADIX_FUSED");
+    return !(v && v[0] == '0');
+  }
+  bool radix_fused = false;  // the last radix job took the fused sort + reduce kernel
   void enqueue_radix_job(u32 num_lines, bool compat, hipEvent_t after_process,
                          hipEvent_t after_reduce) {
+    radix_fused = radix_fused_enabled() && cfg.reduce_path == ReducePath::kLds &&
+                  radix_mapped() && psort_ok(compat, false);
+    if (radix_fused) {
+      // Process + Reduce in one kernel, records straight into the mapped output; it
+      // re-zeroes its scratch and, in a lean job, tells the host itself (psort.hip)
+      PsortReduceArgs ra;
+      ra.out = d_out_mapped;
+      ra.out_cap = h_out_cap;
+      ra.ctr_out = d_ctr_mapped;
+      ra.status = lb_dict.status;
+      ra.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
+      ra.map_lb = lb_map;
+      ra.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+      if (done_pending) {
+        ra.host_done = d_done;
+        ra.host_done_value = done_pending;
+        done_pending = 0;
+      }
+      launch_psort_reduce(tokens, d_part_off, part_tiles, cap, d_ctr, d_pw, ra, stream, ord_trace());
+      psort_used = true;
+      if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+      if (after_reduce) LOCUST_HIP_CHECK(hipEventRecord(after_reduce, stream));
+      return;
+    }
     enqueue_process(num_lines, compat, false, kUnknownCount, /*allow_psort=*/true);
     if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
     const bool mapped = radix_mapped();
@@ -1638,7 +1681,7 @@ struct DevicePipeline {
     // lean: a small single-pass job launched directly, no stage events, completion polled
     const bool lean = !graphed && lean_job(in);
     split_stages = !lean && !graphed;
-    skip_sync_reset = clean_start && dict_path && !compat;
+    skip_sync_reset = clean_start && !compat;
     if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
     if (lean) {
       enqueue_upload(in);
@@ -1708,14 +1751,18 @@ struct DevicePipeline {
         else if (ordered) force_retune(r.entries.data(), r.entries.size());
       }
     } else {
-      if (lean)
+      if (lean) {
+        done_pending = ++done_seq;  // the fused kernel publishes it itself
         enqueue_radix_job((u32)in.num_lines, compat, nullptr, nullptr);
-      else if (!graphed)
+        if (done_pending) publish_done(done_seq);
+        done_pending = 0;
+      } else if (!graphed) {
         enqueue_radix_job((u32)in.num_lines, compat, ev[3], ev[4]);
+      }
+      skip_sync_reset = false;
       bool overflow;
       if (radix_mapped()) {  // records and counters already in host memory
         if (lean) {
-          publish_done(++done_seq);
           wait_done(done_seq);
         } else {
           if (!graphed) LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
@@ -1723,6 +1770,8 @@ struct DevicePipeline {
         }
         *h_ctr = *h_ctr_mapped;
         overflow = (h_ctr->flags & kCtrSortOverflow) != 0;
+        // a fused run re-zeroed its scratch (not replayed from a graph: those reset it)
+        sync_clean = lean && radix_fused && !overflow && !compat;
         if (psort_used) print_psort_trace();
         if (!overflow) {
           fill_counters(r);

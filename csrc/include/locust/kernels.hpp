@@ -216,6 +216,33 @@ static_assert(sizeof(OutRecord) == 48, "OutRecord 48 B");
 // tile counter.
 void launch_reduce_fused(ConstKeysSoA sorted, u64 cap, MapCounters* ctr, OutRecord* out,
                          u64 out_cap, MapCounters* ctr_out, LookbackScratch lb, hipStream_t s);
+// Process + Reduce of the reference algorithm in ONE kernel (psort.hip): the partitioned
+// LDS sort above, then inside each partition's workgroup the head mark (key[i] !=
+// key[i-1]; runs never cross partitions, which are key ranges), counts as distances to the
+// next head, val = the head's global position in the sorted token order (the partition's
+// offset + local index, known up front), the record index from a look-back over the
+// partitions' head counts -- and the records straight into `out` (host-mapped allowed).
+// The sorted token array is never written.  Self-cleaning like the ordered dictionary
+// kernel: `status` (kDictParts look-back words) and `done_counter` must be zero before and
+// are left zero; the last workgroup to finish re-zeroes the map's look-back words
+// (map_lb, map_words) and counters, writes the ctr_out snapshot and, if given, publishes
+// host_done_value to host_done (the lean job's completion word).  A partition past
+// kPsortMax tokens sets kCtrSortOverflow: no records, nothing re-zeroed, the host redoes
+// the pass with the device-wide sort.
+struct PsortReduceArgs {
+  OutRecord* out = nullptr;
+  u64 out_cap = 0;
+  MapCounters* ctr_out = nullptr;
+  u64* status = nullptr;
+  u32* done_counter = nullptr;
+  LookbackScratch map_lb{};
+  u32 map_words = 0;
+  u32* host_done = nullptr;
+  u32 host_done_value = 0;
+};
+void launch_psort_reduce(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap,
+                         MapCounters* ctr, u32* part_w, const PsortReduceArgs& ra, hipStream_t s,
+                         u64* trace = nullptr);
 // ctr_out (optional, host-mapped): a snapshot of the final counters.
 void launch_pack_output(ConstKeysSoA head_keys, const u64* head_val, const u64* head_count,
                         u64 cap, const MapCounters* ctr, OutRecord* out, hipStream_t s,
@@ -439,5 +466,36 @@ void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const Ex
 // ---- device self-test of the string library (tests only; StringTestOut in engine.hpp) ----
 void launch_string_selftest(const char* blob, const u32* off, u32 n, const char* delims,
                             const int* ints, StringTestOut* out, hipStream_t s);
+
+// ---------------- code-object warm-up ----------------
+// The runtime loads a file's code object at the first launch of one of its kernels (lazy
+// loading); a one-shot job would pay that inside its first kernels.  warm_kernel_modules()
+// loads every kernel file of this library up front (engine construction) -- and only them:
+// HIP_ENABLE_DEFERRED_LOADING=0 would also load the RCCL library's device code (a
+// 573 MB fat binary), +1.3 GB of host memory and ~150 ms per process.
+void warm_module_dict();
+void warm_module_exchange();
+void warm_module_map();
+void warm_module_merge();
+void warm_module_partplan();
+void warm_module_psort();
+void warm_module_radix_sort();
+void warm_module_reduce();
+void warm_module_shuffle();
+void warm_module_signal();
+void warm_module_tokenize();
+inline void warm_kernel_modules() {
+  warm_module_dict();
+  warm_module_exchange();
+  warm_module_map();
+  warm_module_merge();
+  warm_module_partplan();
+  warm_module_psort();
+  warm_module_radix_sort();
+  warm_module_reduce();
+  warm_module_shuffle();
+  warm_module_signal();
+  warm_module_tokenize();
+}
 
 }  // namespace locust

@@ -1976,4 +1976,10 @@ void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounte
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_dict() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&dict_insert_kernel));
+}
+
 }  // namespace locust

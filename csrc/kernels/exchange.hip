@@ -380,4 +380,10 @@ void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const Ex
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_exchange() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&exch_header_kernel));
+}
+
 }  // namespace locust

@@ -157,4 +157,10 @@ void launch_compact_slots(const u32* line_counts, u32 num_lines, int emits_per_l
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_map() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&line_index_kernel));
+}
+
 }  // namespace locust

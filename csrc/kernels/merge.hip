@@ -325,4 +325,10 @@ void launch_merge_slots_limited(const KeyCount* slots, u32 nslots, u32 slot_reco
                     out_limit);
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_merge() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&merge_rank_kernel));
+}
+
 }  // namespace locust

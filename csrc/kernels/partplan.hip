@@ -112,4 +112,10 @@ void launch_part_plan(const u64* ukeys_w0, const u64* ucount, const u32* d_u, u3
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_partplan() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&part_plan_kernel));
+}
+
 }  // namespace locust

@@ -21,6 +21,7 @@
 // One launch, no host synchronisation, graph-capturable.  A partition with more than
 // kPsortMax tokens sets kCtrSortOverflow and the host sorts the pass with radix_sort.
 #include "locust/device/lds_radix.hpp"
+#include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
@@ -36,12 +37,65 @@ constexpr int kPsWaves = kPsBlock / 64;
 constexpr int kPsRounds = kPsortMax / kPsBlock;  // keys held per thread
 using PsRadix = dev::LdsRadix<kPsBlock, kPsortMax, u16>;
 
+// The end of every fused workgroup: its look-back (unless done already), the run's
+// counters from the last partition, and the completion count -- the last workgroup to
+// finish writes the counter snapshot, re-zeroes the scratch (unless a partition
+// overflowed) and tells the host.
+__device__ __forceinline__ void reduce_tail(u32 p, u32 U, u64 pfx, MapCounters* ctr,
+                                            const PsortReduceArgs& ra, u64& s_prefix,
+                                            u32& s_last, bool looked_back = false) {
+  if (!looked_back) pfx = dev::block_lookback(ra.status, p, U, &s_prefix);
+  if (p == (u32)kDictParts - 1 && threadIdx.x == 0) {
+    ctr->num_unique = (u32)(pfx + U);
+    ctr->total_count = ctr->num_records;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();  // this workgroup's records (host-mapped) and counter writes
+    s_last = atomicAdd(ra.done_counter, 1u) == (u32)kDictParts - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // acquire every other workgroup's
+  const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0 && ra.ctr_out) {
+    MapCounters c = *ctr;
+    *ra.ctr_out = c;
+  }
+  __syncthreads();
+  if (!(flags & kCtrSortOverflow)) {
+    for (u32 i = threadIdx.x; i < ra.map_words; i += kPsBlock) ra.map_lb.status[i] = 0;
+    for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPsBlock) ra.status[i] = 0;
+    if (threadIdx.x == 0) {
+      // the accumulated counters; num_unique / total_count are this run's assignments
+      ctr->num_records = 0;
+      ctr->overflow_lines = 0;
+      ctr->truncated = 0;
+      ctr->num_newlines = 0;
+      ctr->max_key_len = 0;
+      ctr->flags = 0;
+      *ra.map_lb.tile_counter = 0;
+      *ra.done_counter = 0;
+    }
+  }
+  if (ra.host_done && threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(ra.host_done, ra.host_done_value, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// kReduce: the fused Process + Reduce (launch_psort_reduce) -- step 4 marks heads and
+// writes the output records instead of the sorted slice, and every workgroup (empty and
+// overflowing partitions included) takes part in the look-back and the completion count.
+template <bool kReduce>
 __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
                                                          const u32* __restrict__ part_off,
                                                          u32 ntiles, u32 n_cap, KeysSoA sorted,
                                                          MapCounters* __restrict__ ctr,
                                                          u32* __restrict__ part_w,
-                                                         u64* __restrict__ trace) {
+                                                         u64* __restrict__ trace,
+                                                         PsortReduceArgs ra) {
   // trace (diagnostics, LOCUST_ORD_TRACE): per partition, s_memtime at [p*16 + k]: 0 start,
   // 1 list built, 2 keys loaded, 3 sorted, 4 written; [5] tokens, [6] passes; [10]/[11]
   // entry/exit on the 100 MHz device-wide clock
@@ -62,6 +116,10 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   __shared__ u32 s_wsum[4];
   __shared__ u64 s_and[kPsWaves][kKeyWords], s_or[kPsWaves][kKeyWords];
   __shared__ u32 s_count, s_below, s_heads;
+  __shared__ u16 s_hpos[kReduce ? kPsortMax + 1 : 1];  // local positions of the heads
+  __shared__ u32 s_scan[kPsWaves + 1];
+  __shared__ u64 s_prefix;
+  __shared__ u32 s_last;
   const u32 p = blockIdx.x;
   const int lane = lane_id(), w = wave_id(), t = (int)threadIdx.x;
   const PsRadix rx{s_w0, s_perm, s_cnt, s_wex, s_start, s_wsum};
@@ -103,10 +161,15 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   if (trace && t == 0) trace[(u64)p * 16 + 5] = m;
   if (m > (u32)kPsortMax) {  // uniform: the host sorts this pass with radix_sort
     if (t == 0) atomicOr(&ctr->flags, kCtrSortOverflow);
+    if constexpr (kReduce) {
+      reduce_tail(p, 0, 0, ctr, ra, s_prefix, s_last);
+      return;
+    }
     return;
   }
   if (m == 0) {
     if (part_w && t == 0) part_w[p] = 0;
+    if constexpr (kReduce) reduce_tail(p, 0, 0, ctr, ra, s_prefix, s_last);
     return;
   }
 
@@ -222,6 +285,65 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
       for (int b = 0; b < 8; ++b) np += ((diff[j] >> (8 * b)) & 0xffull) ? 1u : 0u;
     trace[(u64)p * 16 + 6] = np;
   }
+  if constexpr (kReduce) {
+    // ---- 4'. heads in sorted order (block scans over rounds of kPsBlock items), their
+    // positions in LDS, the record prefix from the look-back, then the records ----
+    auto word23 = [&](u32 li, int j) -> u64 {  // words 2-3 of a long key, from the tokens
+      if (!long_keys || !(s_w1[li] & 0xffull)) return 0;
+      const u32 g = s_list[li];
+      const u64 x2 = tokens.w[2][g];
+      return j == 2 ? x2 : (x2 & 0xffull) ? tokens.w[3][g] : 0;
+    };
+    u32 running = 0, firsts = 0;
+    for (u32 r0 = 0; r0 < m; r0 += kPsBlock) {
+      const u32 i = r0 + (u32)t;
+      bool head = false;
+      if (i < m) {
+        const u32 li = s_perm[cur][i];
+        head = i == 0;
+        if (!head) {
+          const u32 lp = s_perm[cur][i - 1];
+          firsts += s_w0[li] != s_w0[lp] ? 1u : 0u;
+          head = s_w0[li] != s_w0[lp] || s_w1[li] != s_w1[lp] ||
+                 word23(li, 2) != word23(lp, 2) || word23(li, 3) != word23(lp, 3);
+        } else {
+          firsts += 1;
+        }
+      }
+      u32 tot;
+      const u32 ex = dev::block_exclusive_scan<u32, kPsBlock>(head ? 1u : 0u, s_scan, &tot);
+      if (head) s_hpos[running + ex] = (u16)i;
+      running += tot;
+    }
+    const u32 U = running;
+    if (part_w) {
+      firsts = dev::wave_reduce_sum(firsts);
+      if (lane == 0 && firsts) atomicAdd(&s_heads, firsts);
+    }
+    PS_STAMP(4);
+    const u64 pfx = dev::block_lookback(ra.status, p, U, &s_prefix);  // syncs (s_hpos too)
+    u64* o = reinterpret_cast<u64*>(ra.out + pfx);
+    const u32 lim = pfx >= ra.out_cap ? 0u : (u32)min<u64>(U, ra.out_cap - pfx);
+    for (u32 q = (u32)t; q < 6u * lim; q += kPsBlock) {
+      const u32 h = q / 6, f = q - 6 * h;
+      const u32 i = s_hpos[h];
+      const u32 li = s_perm[cur][i];
+      u64 v;
+      if (f == 0) v = s_w0[li];
+      else if (f == 1) v = s_w1[li];
+      else if (f < 4) v = word23(li, (int)f);
+      else if (f == 4) v = (u64)base + i;
+      else v = (u64)((h + 1 < U ? s_hpos[h + 1] : m) - i);
+      o[q] = v;
+    }
+    if (trace && t == 0) trace[(u64)p * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+    if (part_w && t == 0) {
+      const u64 wk = (u64)m + (u64)kPartDistinctWeight * s_heads;
+      part_w[p] = (u32)(wk < 0xffffffffull ? wk : 0xffffffffull);
+    }
+    reduce_tail(p, U, pfx, ctr, ra, s_prefix, s_last, /*looked_back=*/true);
+    return;
+  }
   // ---- 4. the partition's slice of the sorted token array, from LDS (words 2-3 gathered
   // only when the partition has keys past 16 bytes); distinct first words counted on the
   // way for the partition map's retuning ----
@@ -263,9 +385,25 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
 void launch_psort(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap, KeysSoA sorted,
                   MapCounters* ctr, u32* part_w, hipStream_t s, u64* trace) {
   LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
-  psort_kernel<<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(tokens, part_off, ntiles, (u32)cap,
-                                                           sorted, ctr, part_w, trace);
+  psort_kernel<false><<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(
+      tokens, part_off, ntiles, (u32)cap, sorted, ctr, part_w, trace, PsortReduceArgs{});
   LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_psort_reduce(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap,
+                         MapCounters* ctr, u32* part_w, const PsortReduceArgs& ra, hipStream_t s,
+                         u64* trace) {
+  LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
+  LOCUST_CHECK_ARG(ra.out && ra.status && ra.done_counter, "psort_reduce: missing buffers");
+  psort_kernel<true><<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(
+      tokens, part_off, ntiles, (u32)cap, KeysSoA{}, ctr, part_w, trace, ra);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_psort() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&psort_kernel<true>));
 }
 
 }  // namespace locust

@@ -440,4 +440,10 @@ void radix_sort(ConstKeysSoA keys, const u32* d_n, u64 host_n, RadixWorkspace& w
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_radix_sort() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&radix_small_kernel));
+}
+
 }  // namespace locust

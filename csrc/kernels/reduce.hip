@@ -399,4 +399,10 @@ void launch_pack_output(ConstKeysSoA head_keys, const u64* head_val, const u64* 
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_reduce() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&scan_counts_kernel));
+}
+
 }  // namespace locust

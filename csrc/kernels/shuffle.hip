@@ -128,4 +128,10 @@ void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey*
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_shuffle() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&pack_records_kernel));
+}
+
 }  // namespace locust

@@ -44,4 +44,10 @@ void launch_signal_host(u32* word, u32 value, hipStream_t s) {
   signal_host_kernel<<<dim3(1), dim3(64), 0, s>>>(word, value);
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_signal() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&signal_host_kernel));
+}
+
 }  // namespace locust

@@ -534,4 +534,10 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
+// Loads this file's code object (one module per file) now rather than at its first launch.
+void warm_module_tokenize() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&map_fast_kernel<1, 1024>));
+}
+
 }  // namespace locust

@@ -31,12 +31,10 @@ import os as _os
 # once, at import, before any RCCL communicator or engine thread exists; a user's explicit
 # setting wins.
 _os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
-# Load every kernel's code object when the HIP runtime starts, not at each kernel's first
-# launch: otherwise a fresh process's first job pays tens of milliseconds of lazy loading
-# (measured: a one-job process -- the CLI's case -- saw every kernel load inside its job).
-# Read by the runtime at its first call, which happens after this import; a user's explicit
-# setting wins.
-_os.environ.setdefault("HIP_ENABLE_DEFERRED_LOADING", "0")
+# Code objects: the engines load this library's own kernel files at construction (see
+# warm_kernel_modules in csrc/include/locust/kernels.hpp), so a fresh process's first job
+# does not pay lazy loading inside it -- without HIP_ENABLE_DEFERRED_LOADING=0, which would
+# also load RCCL's 573 MB of device code into every process (+1.3 GB of host memory).
 
 from ._native import REPO_ROOT, build, cli_path, load  # noqa: E402
 
