@@ -413,7 +413,7 @@ def main() -> int:
                     choices=sorted(BASELINE_MS) + sorted(SYNTH))
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the side measurements (700 lines, radix path, synth1m, ...)")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "tcp"],
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "tcp", "tcpdev"],
                     help="communicator for N>1 (tcp: rehearsal with ranks sharing one GPU)")
     ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"],
                     help="cpu: rehearse the rank/communicator plumbing with the CPU engine")

@@ -115,6 +115,11 @@ std::unique_ptr<Communicator> make_rccl_comm(int rank, int world, int device,
                                              const std::string& host, int port,
                                              double timeout_s = 300.0, int listen_fd = -1);
 
+// A host communicator (TCP) with the device data plane staged through host memory
+// ("tcpdev", comm/staged_comm.hip): the multi-process device paths rehearsed with several
+// processes sharing one GPU (RCCL refuses two ranks per device).  Blocking; tests only.
+std::unique_ptr<Communicator> make_staged_device_comm(std::unique_ptr<Communicator> host);
+
 // Single-process RCCL clique (`ncclCommInitAll` over the node's GPUs):
 // make_rccl_clique creates one communicator per device from the calling thread; each
 // rank's thread then wraps its member (make_rccl_clique_comm sets that thread's device).

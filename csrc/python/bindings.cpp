@@ -259,6 +259,8 @@ class PyDistRank {
     py::gil_scoped_release nogil;
     if (comm == "tcp") {
       comm_ = make_tcp_comm(rank, cfg.world, host, port, timeout_s, listen_fd);
+    } else if (comm == "tcpdev") {
+      comm_ = make_staged_device_comm(make_tcp_comm(rank, cfg.world, host, port, timeout_s, listen_fd));
     } else if (comm == "rccl") {
       comm_ = make_rccl_comm(rank, cfg.world, cfg.job.device, host, port, timeout_s, listen_fd);
     } else {
