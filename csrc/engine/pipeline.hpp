@@ -252,14 +252,15 @@ struct DevicePipeline {
   }
   // The plan's kernels, on `stream` once piece 0 (`len0` bytes at d_text; host copy at
   // `host`) has landed; the scratch was zeroed at the start of the pass.
-  void enqueue_devplan(const char* host, u64 len0, const DelimMask& dm) {
+  void enqueue_devplan(const char* host, u64 len0, const DelimMask& dm,
+                       const char* dev_text = nullptr) {
     u64 n = std::min<u64>(len0, kPlanSampleBytes);
     if (n < len0) {
       const void* nl = memrchr(host, '\n', (size_t)n);
       if (nl) n = (u64)(static_cast<const char*>(nl) - host) + 1;
     }
-    launch_map_fast(d_text, n, dm, cfg.emits_per_line, cfg.max_key_len, plan_keys, nullptr,
-                    kPlanCap, d_plan_ctr, lb_map, stream);
+    launch_map_fast(dev_text ? dev_text : d_text, n, dm, cfg.emits_per_line, cfg.max_key_len,
+                    plan_keys, nullptr, kPlanCap, d_plan_ctr, lb_map, stream);
     launch_dict_insert(plan_keys, nullptr, &d_plan_ctr->num_records, kPlanCap, plan_dict,
                        d_plan_ctr, stream);
     launch_part_plan(plan_dict.ukeys.w[0], plan_dict.ucount, &d_plan_ctr->num_unique,
@@ -953,6 +954,19 @@ struct DevicePipeline {
       if (agg) partial_nslots = (u32)pieces.size();
     } else {
       part_tiles = table_tiles(in.bytes);
+      // A large pass in one launch (below the piecewise size): the same in-job plan as the
+      // piecewise pass, from the first MiB of the text, before the map tags the tokens --
+      // a first-letter map overflows the ordered kernel's LDS tables on ~80K distinct keys
+      // (measured: 1/8 of synth1m, 5.7 ms first job with the HBM-table fallback).
+      devplan_used = large_ordered && part_tiles && cfg.sort_path == SortPath::kDict &&
+                     devplan_env && !devplan_failed && !pm_tuned;
+      if (devplan_used) {
+        ensure_plan();
+        LOCUST_HIP_CHECK(hipMemsetAsync(d_plan, 0, plan_zero_bytes, stream));
+        enqueue_devplan(upload_mode == Upload::kDirect || upload_mode == Upload::kZeroCopy ? in.data
+                                                                                         : h_text,
+                        in.bytes, make_delim_mask(cfg.delimiters.c_str()), map_text);
+      }
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                       stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
