@@ -22,8 +22,9 @@ Headline (``value``): whole Hamlet, weak scaling -- every rank maps its own copy
 text, the ranks merge their combined (key, count) records on rank 0 (the gather strategy:
 one all-gather of device-written slots, one root merge).  The ``synth1m`` extra, at every
 N including 1, is BASELINE config 4 as strong scaling: 1M synthetic lines in total, 1/N per
-rank, range-partitioned by sample-sort splitters and exchanged with one fixed-slot
-``ncclAllToAll`` over xGMI, so N = 1, 2, 4, 8 form one curve.  Steps are timed between
+rank, range-partitioned by sample-sort splitters and exchanged over xGMI (one fixed-slot
+``ncclAllToAll`` in steady state), every rank writing its key range into the shared host
+output over its own PCIe link, so N = 1, 2, 4, 8 form one curve.  Steps are timed between
 barriers with the device synchronised on both sides; the MAX over ranks is reported.
 
 This process never imports torch: the engine drives HIP/RCCL directly (torch's bundled

@@ -7,11 +7,13 @@ socket-based distributor), re-designed MI355X-first:
   byte-parallel tokenizer, decoupled look-back scans, LSD radix sort on packed keys,
   LDS-staged boundary-mark / adjacent-difference reduce) -- see ``csrc/kernels``.
 * Multi-GPU runs shard the input by bytes, range-partition with sample-sort splitters and
-  exchange 40-byte (key, count) records over xGMI (``csrc/comm``): a fixed-slot
-  ``ncclAllToAll`` (every bucket padded to the previous job's largest bucket + 1/8) once a
-  job shape's slot size is known, grouped ``ncclSend``/``ncclRecv`` with exact sizes
-  otherwise; small combined outputs go straight to rank 0 (one ``ncclAllGather`` of
-  device-written slots, one root merge).
+  exchange 40-byte (key, count) records over xGMI (``csrc/comm``): a first job sizes the
+  exchange from an all-gathered count matrix (grouped ``ncclSend``/``ncclRecv`` with exact
+  sizes, two host syncs), later jobs use one fixed-slot ``ncclAllToAll`` (every bucket
+  padded to the previous job's largest bucket + 1/8, one host sync).  Every rank writes its
+  key range straight into one shared host output (a POSIX shm segment each rank registers
+  with HIP) at its global offset -- no gather to rank 0.  Small combined outputs of
+  repeated jobs go to rank 0 in one ``ncclAllGather`` of device-written slots.
 * The reference's ``./MapReduce <file> [start end] [node stage]`` CLI and output format are
   kept byte-for-byte (``build/MapReduce``).
 
