@@ -582,6 +582,14 @@ struct DevicePipeline {
     if (!out_pool.empty() && out_pool[out_idx].use_count() == 1) return;
     for (size_t i = 0; i < out_pool.size(); ++i)
       if (out_pool[i].use_count() == 1) return use_out(i);
+    if (retune_job.valid()) {
+      // a background retune reads a buffer a result no longer needs: let it finish (it is
+      // near the end by now) rather than pin a new buffer (~2 ms for a large engine's)
+      retune_job.wait();
+      poll_retune();
+      for (size_t i = 0; i < out_pool.size(); ++i)
+        if (out_pool[i].use_count() == 1) return use_out(i);
+    }
     const u64 t0 = now_ns();
     out_pool.push_back(std::make_shared<HostOut>(h_out_cap, out_noncoherent));
     use_out(out_pool.size() - 1);

@@ -247,9 +247,31 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   }
 
   PS_STAMP(2);
-  // ---- 3. LSD passes over the live byte positions, least significant first ----
   int cur = 0;
-  for (int wd = kKeyWords - 1; wd >= 0; --wd) {
+  bool any_diff = false;
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j) any_diff |= diff[j] != 0;
+  // ---- 3a. small partitions of short keys: one all-pairs ranking pass.  A partition of
+  // the tuned map holds a few hundred tokens whose keys still differ in 6-10 byte positions
+  // (words of one initial letter): as many LSD passes, each with three barriers and a
+  // 256-bin scan whatever m is (~3 us apiece; 9 passes put p=255 at 29K ticks on whole
+  // Hamlet).  Ranking every key against the partition's (LDS broadcast reads, no
+  // barriers) costs m compares a thread: ~1K cycles at m = 512. ----
+  if (any_diff && !long_keys && m <= 2u * kPsBlock) {
+    for (u32 i = (u32)t; i < m; i += kPsBlock) {
+      const u64 a0 = s_w0[i], a1 = s_w1[i];
+      u32 rank = 0;
+      for (u32 j = 0; j < m; ++j) {
+        const u64 b0 = s_w0[j], b1 = s_w1[j];
+        rank += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && j < i)))) ? 1u : 0u;
+      }
+      s_perm[0][rank] = (u16)i;
+    }
+    __syncthreads();
+    any_diff = false;  // sorted
+  }
+  // ---- 3. LSD passes over the live byte positions, least significant first ----
+  for (int wd = kKeyWords - 1; any_diff && wd >= 0; --wd) {
     if (!diff[wd]) continue;
     const u64* warr = wd == 0 ? s_w0 : s_w1;
     if (wd >= 2) {

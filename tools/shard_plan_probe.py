@@ -22,6 +22,7 @@ for r in range(shards):
         res = e.run_text(text)
         ts.append(1e3 * (time.perf_counter() - t0))
         tm = {k: round(v, 3) for k, v in res.times().items() if isinstance(v, float) and v}
-        print(f"  job: {ts[-1]:.3f} ms stats {e.stats()} times {tm}", file=sys.stderr, flush=True)
+        print(f"  job: {ts[-1]:.3f} ms (engine wall {tm.get('wall_ms', 0):.3f}) stats {e.stats()} "
+              f"times {tm}", file=sys.stderr, flush=True)
     print(f"shard {r}/{n}: {text.size} B, unique {res.num_unique}, jobs "
           + " / ".join(f"{t:.3f}" for t in ts) + f" ms, stats {e.stats()}", flush=True)
