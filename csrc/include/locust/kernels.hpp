@@ -239,6 +239,7 @@ struct PsortReduceArgs {
   u32 map_words = 0;
   u32* host_done = nullptr;
   u32 host_done_value = 0;
+  u32 variant = 0;  // A/B switches (LOCUST_PSORT_VARIANT; bit 0: no all-pairs ranking)
 };
 void launch_psort_reduce(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap,
                          MapCounters* ctr, u32* part_w, const PsortReduceArgs& ra, hipStream_t s,

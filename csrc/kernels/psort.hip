@@ -20,6 +20,8 @@
 //   4. writes its slice of the globally sorted token array.
 // One launch, no host synchronisation, graph-capturable.  A partition with more than
 // kPsortMax tokens sets kCtrSortOverflow and the host sorts the pass with radix_sort.
+#include <cstdlib>
+
 #include "locust/device/lds_radix.hpp"
 #include "locust/device/lookback.hpp"
 #include "locust/device/wave.hpp"
@@ -257,11 +259,29 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   // 256-bin scan whatever m is (~3 us apiece; 9 passes put p=255 at 29K ticks on whole
   // Hamlet).  Ranking every key against the partition's (LDS broadcast reads, no
   // barriers) costs m compares a thread: ~1K cycles at m = 512. ----
-  if (any_diff && !long_keys && m <= 2u * kPsBlock) {
+  if (any_diff && !long_keys && m <= 2u * kPsBlock && !(ra.variant & 1u)) {
+    // eight independent compares per step: the broadcast LDS reads of a step are all in
+    // flight together (one at a time, each compare waited out the LDS latency)
+    constexpr u32 kU = 8;
+    const u32 m8 = m & ~(kU - 1);
     for (u32 i = (u32)t; i < m; i += kPsBlock) {
       const u64 a0 = s_w0[i], a1 = s_w1[i];
+      u32 r[kU] = {};
+      for (u32 j = 0; j < m8; j += kU) {
+        u64 b0[kU], b1[kU];
+#pragma unroll
+        for (u32 u = 0; u < kU; ++u) {
+          b0[u] = s_w0[j + u];
+          b1[u] = s_w1[j + u];
+        }
+#pragma unroll
+        for (u32 u = 0; u < kU; ++u)
+          r[u] += (b0[u] < a0 || (b0[u] == a0 && (b1[u] < a1 || (b1[u] == a1 && j + u < i)))) ? 1u : 0u;
+      }
       u32 rank = 0;
-      for (u32 j = 0; j < m; ++j) {
+#pragma unroll
+      for (u32 u = 0; u < kU; ++u) rank += r[u];
+      for (u32 j = m8; j < m; ++j) {
         const u64 b0 = s_w0[j], b1 = s_w1[j];
         rank += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && j < i)))) ? 1u : 0u;
       }
@@ -404,11 +424,21 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
 
 }  // namespace
 
+u32 psort_variant() {
+  static const u32 v = [] {
+    const char* e = std::getenv("LOCUST_PSORT_VARIANT");
+    return e ? (u32)std::atoi(e) : 0u;
+  }();
+  return v;
+}
+
 void launch_psort(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap, KeysSoA sorted,
                   MapCounters* ctr, u32* part_w, hipStream_t s, u64* trace) {
   LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
+  PsortReduceArgs ra;
+  ra.variant = psort_variant();
   psort_kernel<false><<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(
-      tokens, part_off, ntiles, (u32)cap, sorted, ctr, part_w, trace, PsortReduceArgs{});
+      tokens, part_off, ntiles, (u32)cap, sorted, ctr, part_w, trace, ra);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
@@ -417,8 +447,10 @@ void launch_psort_reduce(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u
                          u64* trace) {
   LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
   LOCUST_CHECK_ARG(ra.out && ra.status && ra.done_counter, "psort_reduce: missing buffers");
+  PsortReduceArgs a = ra;
+  a.variant |= psort_variant();
   psort_kernel<true><<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(
-      tokens, part_off, ntiles, (u32)cap, KeysSoA{}, ctr, part_w, trace, ra);
+      tokens, part_off, ntiles, (u32)cap, KeysSoA{}, ctr, part_w, trace, a);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
