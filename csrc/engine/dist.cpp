@@ -310,6 +310,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       res.strategy = DistStrategy::kGather;
       eng.last_strategy = DistStrategy::kGather;
       res.local_records = n_local;
+      res.host_syncs = 1;  // the slot job's one synchronisation
       const u64 t1 = now_ns();
       if (me == 0) {
         u64 total = 0, uniq = 0;
