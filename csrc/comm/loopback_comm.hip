@@ -65,6 +65,7 @@ class LoopbackComm final : public Communicator {
   const char* name() const override { return "loopback"; }
   bool device_buffers() const override { return st_->device; }
   u64 group_id() const override { return st_->group; }
+  bool in_process() const override { return true; }
 
   void allgather_host(const void* send, void* recv, u64 bytes) override {
     st_->ptr[(size_t)rank_] = send;

@@ -96,6 +96,7 @@ class RcclComm final : public Communicator {
   }
   bool device_buffers() const override { return true; }
   u64 group_id() const override { return group_; }
+  bool in_process() const override { return !tcp_; }  // a clique member (no TCP bootstrap)
 
   void allgather_host(const void* send, void* recv, u64 bytes) override {
     ensure_stage(bytes);

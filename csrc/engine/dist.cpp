@@ -353,6 +353,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   // and CPU engines.
   eng.exch_group = comm.group_id();
   eng.exch_rank = me;
+  eng.exch_in_process = comm.in_process();
   i32 st1 = mapped ? st_slot : 0;
   u64 t1 = 0;
   const bool dev_exch = exch_enabled() && cfg.gather && cfg.job.combine && comm.device_buffers() &&

@@ -1,6 +1,8 @@
 // Per-rank GPU shard engine of the distributed driver (csrc/engine/dist.cpp): map +
 // combine of this rank's shard, shuffle records and splitter samples, reduce of the
 // received records, and the root's merge of the gather strategy.
+#include <map>
+#include <mutex>
 #include <thread>
 
 #include "locust/shm.hpp"
@@ -738,7 +740,7 @@ class GpuShardEngine final : public ShardEngine {
     LOCUST_CHECK_ARG(n <= out_->region_records, "shared output: range larger than its region");
     // every rank's range landed when its stamp says this job (its emit fenced its writes
     // at system scope before the stamp's release store)
-    const u64* stamps = out_->seg.stamps();
+    const u64* stamps = out_->stamps();
     const u64 deadline = now_ns() + (u64)(out_wait_s() * 1e9);
     for (u32 p = 0; p < P; ++p) {
       u64 spins = 0;
@@ -750,7 +752,7 @@ class GpuShardEngine final : public ShardEngine {
       }
     }
     range_entries_.adopt(leases_[job_region_],
-                         reinterpret_cast<WordCountEntry*>(out_->seg.records()) +
+                         reinterpret_cast<WordCountEntry*>(out_->records()) +
                              job_region_ * out_->region_records,
                          n);
     *total_count = t;
@@ -1201,13 +1203,42 @@ class GpuShardEngine final : public ShardEngine {
   // One generation of it: `regions` regions of `region_records` records each.  The root
   // lends a region to each result (EntryList::adopt); a region a live result still holds
   // is not written again -- with none free the output grows by one region.
+  // Ranks that are processes share a POSIX shm segment each maps and registers; ranks
+  // that are threads of one process (the CLI's clique, loopback rehearsals) share one
+  // pinned allocation instead (hipHostMalloc Portable | Mapped: GPU writes to it ran at
+  // ~48 GB/s where the registered 4 KiB shm pages gave ~35).
+  struct PinnedBlock {
+    char* p = nullptr;
+    ~PinnedBlock() {
+      if (p) (void)hipHostFree(p);
+    }
+  };
+  static std::shared_ptr<PinnedBlock> shared_block(const std::string& name, u64 bytes) {
+    static std::mutex mu;
+    static std::map<std::string, std::weak_ptr<PinnedBlock>> reg;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto it = reg.begin(); it != reg.end();)  // forget the released ones
+      it = it->second.expired() ? reg.erase(it) : std::next(it);
+    if (auto b = reg[name].lock()) return b;
+    auto b = std::make_shared<PinnedBlock>();
+    LOCUST_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b->p), bytes,
+                                   hipHostMallocPortable | hipHostMallocMapped |
+                                       hipHostMallocCoherent));
+    std::memset(b->p, 0, kShmHeaderBytes);  // the stamps
+    reg[name] = b;
+    return b;
+  }
   struct OutSegment {
-    ShmSegment seg;
+    ShmSegment seg;                       // processes
+    std::shared_ptr<PinnedBlock> block;   // threads of one process
+    char* base = nullptr;                 // host view: [stamps | records]
     u64 region_records = 0;
     u32 regions = 0;
     bool registered = false;
-    OutRecord* d_records = nullptr;  // device view of seg.records()
-    u64* d_stamps = nullptr;         // device view of seg.stamps()
+    OutRecord* d_records = nullptr;  // device view of the records
+    u64* d_stamps = nullptr;         // device view of the stamps
+    u64* stamps() const { return reinterpret_cast<u64*>(base); }
+    char* records() const { return base + kShmHeaderBytes; }
     ~OutSegment() {
       if (registered) (void)hipHostUnregister(seg.data());
     }
@@ -1238,13 +1269,21 @@ class GpuShardEngine final : public ShardEngine {
     R = align_up(R, (u64)1024);
     LOCUST_HIP_CHECK(hipStreamSynchronize(mp_->stream));  // our writes into the old one
     auto o = std::make_shared<OutSegment>();
-    o->seg.open(shm_segment_name(out_group_, next_segment_gen(out_group_, exch_rank)),
-                shm_segment_bytes(R * K, sizeof(OutRecord)));
-    LOCUST_HIP_CHECK(hipHostRegister(o->seg.data(), o->seg.bytes(),
-                                     hipHostRegisterMapped | hipHostRegisterPortable));
-    o->registered = true;
+    const std::string name = shm_segment_name(out_group_, next_segment_gen(out_group_, exch_rank));
+    const u64 bytes = shm_segment_bytes(R * K, sizeof(OutRecord));
     char* d = nullptr;
-    LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), o->seg.data(), 0));
+    if (exch_in_process) {
+      o->block = shared_block(name, bytes);
+      o->base = o->block->p;
+      LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), o->base, 0));
+    } else {
+      o->seg.open(name, bytes);
+      LOCUST_HIP_CHECK(hipHostRegister(o->seg.data(), o->seg.bytes(),
+                                       hipHostRegisterMapped | hipHostRegisterPortable));
+      o->registered = true;
+      o->base = o->seg.data();
+      LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), o->seg.data(), 0));
+    }
     o->d_stamps = reinterpret_cast<u64*>(d);
     o->d_records = reinterpret_cast<OutRecord*>(d + kShmHeaderBytes);
     o->region_records = R;
@@ -1252,7 +1291,8 @@ class GpuShardEngine final : public ShardEngine {
     out_ = o;
     leases_.clear();
     for (u32 i = 0; i < K; ++i) leases_.push_back(std::make_shared<RegionLease>(RegionLease{o}));
-    LOCUST_LOG_DEBUG("shared output %s: %u regions x %llu records", o->seg.name().c_str(), K,
+    LOCUST_LOG_DEBUG("shared output %s (%s): %u regions x %llu records", name.c_str(),
+                     exch_in_process ? "pinned, in-process" : "shm", K,
                      (unsigned long long)R);
     return true;
   }

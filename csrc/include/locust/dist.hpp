@@ -101,6 +101,8 @@ class Communicator {
   // A 64-bit id every rank of this communicator agrees on (fixed at construction, distinct
   // between groups): names the group's shared output segment (locust/shm.hpp).
   virtual u64 group_id() const = 0;
+  // true: every rank of the group is a thread of this process (loopback, RCCL clique)
+  virtual bool in_process() const { return false; }
 };
 
 // Star-topology TCP communicator (rank 0 relays).  Control plane for everything and the
@@ -318,6 +320,7 @@ class ShardEngine {
   u64 exch_last_sum = 0;  // all ranks' records of the last job (auto: gather or shuffle)
   u64 exch_group = 0;     // the communicator's group id (names the shared output)
   int exch_rank = 0;      // this rank in that group
+  bool exch_in_process = false;  // every rank of the group is a thread of this process
   virtual void finalize(u64 global_offset, EntryList* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;

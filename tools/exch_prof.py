@@ -45,6 +45,15 @@ def main():
               f"shuffle_ms {info['shuffle_ms']:.4f} reduce_ms {info['reduce_ms']:.4f} "
               f"output_bytes {info['output_bytes']}", flush=True)
         del dr
+    # the same forced shuffle as a one-rank RCCL clique (ranks = threads of this process:
+    # the shared output is one pinned allocation instead of a registered shm segment)
+    raw = text.to_bytes()
+    if raw:
+        cfgs = [lc.make_dist_config(1, job, strategy="shuffle") for _ in range(a.jobs)]
+        out = lc._C.run_multi_schedule(raw, cfgs, "rccl")
+        tm = [i["total_ms"] for _, i in out]
+        print(f"clique shuffle: first {tm[0]:.3f} ms, median {statistics.median(tm[2:]):.4f} ms; "
+              f"syncs {[i['host_syncs'] for _, i in out][:4]}", flush=True)
     ms, stages, res = bench.bench_single(text, a.jobs, 3)
     print(f"local (one-rank auto): {ms:.4f} ms; unique {res.num_unique}", flush=True)
 
