@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void exch_emit_kernel(
     const OutRecord* __restrict__ src, const ExchMsg3* __restrict__ msg3_all,
     const ExchMsg1* __restrict__ root_msg, u64 region, u32 regions, u64 region_records, u32 P,
     u32 me, u32 gather_records, OutRecord* __restrict__ dst, u64* __restrict__ stamps, u64 seq,
-    u32* __restrict__ done) {
+    u32* __restrict__ done, u32 nt) {
   __shared__ u64 s_roff, s_voff, s_n;
   __shared__ u32 s_bad;
   if (threadIdx.x == 0) {
@@ -301,14 +301,22 @@ __global__ __launch_bounds__(256) void exch_emit_kernel(
   const u64 N = s_n, voff = s_voff;
   const uint4* in = reinterpret_cast<const uint4*>(src);
   uint4* out = reinterpret_cast<uint4*>(dst + s_roff);
-  for (u64 q = (u64)blockIdx.x * 256 + threadIdx.x; q < 3 * N; q += (u64)gridDim.x * 256) {
+  // (chunk indices fit 32 bits: a range is < 2^30 records)
+  const u32 nq = (u32)(3 * N);
+  for (u32 q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
     uint4 v = in[q];
-    if (q % 3 == 2) {  // {val, count}: val becomes global
+    if (q % 3u == 2u) {  // {val, count}: val becomes global
       const u64 val = (((u64)v.y << 32) | v.x) + voff;
       v.x = (u32)val;
       v.y = (u32)(val >> 32);
     }
-    out[q] = v;
+    if (nt) {
+      using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+      const u32x4 w = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + q));
+    } else {
+      out[q] = v;
+    }
   }
   __threadfence_system();
   __syncthreads();
@@ -374,9 +382,14 @@ void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const Ex
                       hipStream_t s) {
   const u64 chunks = 3ull * gather_records;
   const u64 blocks = std::min<u64>(std::max<u64>(div_up(chunks ? chunks : 1, 256), 1), 2048);
+  static const u32 nt = [] {  // LOCUST_EMIT_NT=1: non-temporal stores (A/B)
+    const char* e = std::getenv("LOCUST_EMIT_NT");
+    return e && e[0] == '1' ? 1u : 0u;
+  }();
   exch_emit_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(range, msg3_all, root_msg, region,
                                                            regions, region_records, P, me,
-                                                           gather_records, dst, stamps, seq, done);
+                                                           gather_records, dst, stamps, seq, done,
+                                                           nt);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
