@@ -68,6 +68,14 @@ void ShmSegment::open(const std::string& name, u64 bytes) {
                   " B failed: " + std::strerror(e));
     }
   }
+  // reserve the pages now: a full /dev/shm (a container's default is 64 MiB) is a clean
+  // error here rather than a SIGBUS at the first write
+  const int fe = ::posix_fallocate(fd, 0, (off_t)bytes);
+  if (fe != 0 && fe != EOPNOTSUPP && fe != EINVAL) {
+    ::close(fd);
+    throw Error("shm segment " + name + ": cannot reserve " + std::to_string(bytes >> 20) +
+                " MiB in /dev/shm: " + std::strerror(fe));
+  }
   void* p = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   ::close(fd);
   if (p == MAP_FAILED)
