@@ -222,9 +222,20 @@ constexpr int kPartPerThread = kPartSlots / kPartBlock;
 // planned range holds up to ~1,500 of the 2,048 slots; linear probing at 75 % load runs
 // clusters past 128.)
 constexpr int kPartProbes = 512;
-__device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h) {
+// occ (optional, LDS, zeroed with the table): the table's claimed slots.  With it a key
+// probes past kPartProbes -- up to the whole table -- while the table is below 31/32 full,
+// so a planned range that lands at ~95 % load (in-job plans of large passes: measured up to
+// 1,936 of 2,048 on synth1m) still fits instead of sending the whole pass to the fallback;
+// a table at 31/32 stops at kPartProbes as before (no quadratic overflowing pass).
+constexpr u32 kPartOccFull = kPartSlots - kPartSlots / 32;
+__device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h,
+                                                u32* occ = nullptr) {
   u32 slot = (u32)(h >> 8) & (kPartSlots - 1);
-  for (int probe = 0; probe < kPartProbes;) {
+  const int limit = occ ? kPartSlots : kPartProbes;
+  for (int probe = 0; probe < limit;) {
+    if (occ && probe >= kPartProbes && (probe & 63) == 0 &&
+        __hip_atomic_load(occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= kPartOccFull)
+      return false;
     LdsSlot& sl = tab[slot];
     u64 w0 = sl.w[0];
     if (w0 == 0) {
@@ -234,6 +245,7 @@ __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 
         for (int j = 1; j < kKeyWords; ++j)
           __hip_atomic_store(&sl.w[j], k[j] ^ kWordMagic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         atomicAdd(reinterpret_cast<unsigned long long*>(&sl.count), (unsigned long long)c);
+        if (occ) atomicAdd(occ, 1u);
         return true;
       }
     }
@@ -456,7 +468,7 @@ __device__ __forceinline__ bool walk_runs_insert(ConstKeysSoA tokens, const u64*
                                                  const u32* part_off, u32 p, u32 t, u32 t_end,
                                                  u32 a, u32 len, u32 n_cap, LdsSlot* s_tab,
                                                  bool combine, u32* ntok_out,
-                                                 u32* s_full = nullptr) {
+                                                 u32* s_full = nullptr, u32* s_occ = nullptr) {
   bool full = false;
   u32 ntok = 0;
   // s_full (LDS, zeroed by the caller before its barrier): set by the first failed insert
@@ -521,7 +533,7 @@ __device__ __forceinline__ bool walk_runs_insert(ConstKeysSoA tokens, const u64*
             else if (same) live = false;
           }
         }
-        if (live && !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]))) {
+        if (live && !part_lds_insert(s_tab, kk[r], c, key_hash(kk[r]), s_occ)) {
           full = true;
           if (s_full) __hip_atomic_store(s_full, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -806,9 +818,11 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   __shared__ u32 s_scan[kPartBlock / 64 + 1];
   __shared__ u32 s_tok;
   __shared__ u32 s_full;  // the table overflowed: every wave stops walking
+  __shared__ u32 s_occ;   // claimed table slots (part_lds_insert)
   if (threadIdx.x == 0) {
     s_tok = 0;
     s_full = 0;
+    s_occ = 0;
   }
   const u32 ntiles = tile_end - tile_begin;
   const u32 t0 = tile_begin + (u32)((u64)ntiles * k / nslices);
@@ -829,7 +843,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   if (trace && threadIdx.x == 0) trace[slot * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   u32 ntok = 0;
   const bool full = walk_runs_insert(tokens, counts, part_off, p, t, t1, a, len, n_cap, s_tab,
-                                     !(variant & 4u), &ntok, (variant & 32u) ? nullptr : &s_full);
+                                     !(variant & 4u), &ntok, (variant & 32u) ? nullptr : &s_full,
+                                     &s_occ);
   if (trace) atomicAdd(&s_tok, ntok);
   __syncthreads();  // every wave's inserts are in the table before it is read
   if (trace && threadIdx.x == 0) {
@@ -883,6 +898,8 @@ struct PartialsSource {
       if (q <= nslots) s_list[q] = inc - v;
       if (q == 0) s_count = dev::ballot(bad) ? 1u : 0u;
     }
+    u32* occ = s_list + 128;  // claimed table slots (s_list[0 .. nslots] is the prefix)
+    if (threadIdx.x == 0) *occ = 0;
     __syncthreads();
     const u32 total = s_list[nslots];
     bool full = s_count != 0;
@@ -895,7 +912,7 @@ struct PartialsSource {
         const KeyCount& rec = partials[((u64)p * nslots + q) * kPartSlots + (e - s_list[q])];
         const u64 kk[kKeyWords] = {rec.w[0], rec.w[1], rec.w[2], rec.w[3]};
         if (kk[0] == 0 || rec.count == 0) continue;
-        full |= !part_lds_insert(s_tab, kk, rec.count, key_hash(kk));
+        full |= !part_lds_insert(s_tab, kk, rec.count, key_hash(kk), occ);
       }
     }
     __syncthreads();
