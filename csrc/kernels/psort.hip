@@ -259,7 +259,15 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   // 256-bin scan whatever m is (~3 us apiece; 9 passes put p=255 at 29K ticks on whole
   // Hamlet).  Ranking every key against the partition's (LDS broadcast reads, no
   // barriers) costs m compares a thread: ~1K cycles at m = 512. ----
-  if (any_diff && !long_keys && m <= 2u * kPsBlock && !(ra.variant & 1u)) {
+  // live byte positions = LSD passes; measured on whole Hamlet: ~3,000 ticks a pass vs
+  // ~135 ticks a key for the ranking -- rank only where that is cheaper
+  u32 lsd_passes = 0;
+#pragma unroll
+  for (int j = 0; j < kKeyWords; ++j)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) lsd_passes += ((diff[j] >> (8 * b)) & 0xffull) ? 1u : 0u;
+  if (any_diff && !long_keys && m <= 2u * kPsBlock && m < 22u * lsd_passes &&
+      !(ra.variant & 1u)) {
     // eight independent compares per step: the broadcast LDS reads of a step are all in
     // flight together (one at a time, each compare waited out the LDS latency)
     constexpr u32 kU = 8;
@@ -274,16 +282,18 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
           b0[u] = s_w0[j + u];
           b1[u] = s_w1[j + u];
         }
+        // bitwise, not short-circuit: no branches (and no exec-mask juggling) in the loop
 #pragma unroll
         for (u32 u = 0; u < kU; ++u)
-          r[u] += (b0[u] < a0 || (b0[u] == a0 && (b1[u] < a1 || (b1[u] == a1 && j + u < i)))) ? 1u : 0u;
+          r[u] += (u32)((b0[u] < a0) |
+                        ((b0[u] == a0) & ((b1[u] < a1) | ((b1[u] == a1) & (j + u < i)))));
       }
       u32 rank = 0;
 #pragma unroll
       for (u32 u = 0; u < kU; ++u) rank += r[u];
       for (u32 j = m8; j < m; ++j) {
         const u64 b0 = s_w0[j], b1 = s_w1[j];
-        rank += (b0 < a0 || (b0 == a0 && (b1 < a1 || (b1 == a1 && j < i)))) ? 1u : 0u;
+        rank += (u32)((b0 < a0) | ((b0 == a0) & ((b1 < a1) | ((b1 == a1) & (j < i)))));
       }
       s_perm[0][rank] = (u16)i;
     }
