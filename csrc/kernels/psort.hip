@@ -133,7 +133,11 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   }
   __syncthreads();
 
-  // ---- 1. this partition's tokens and its output offset ----
+  // ---- 1. this partition's tokens and its output offset; the first kEarly keys of each
+  // tile's run are loaded right behind the table row (their round trip overlaps the scan
+  // and the append), the rest -- flagged kLate in s_list -- in step 2 ----
+  constexpr u32 kEarly = 4;
+  constexpr u32 kLate = 0x80000000u;
   u32 below = 0;
   for (u32 t0 = 0; t0 < ntiles; t0 += kPsBlock) {
     const u32 tile = t0 + (u32)t;
@@ -145,6 +149,13 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
       len = row[p + 1] - a;
       below += a - z;
     }
+    u64 e0[kEarly], e1[kEarly];
+#pragma unroll
+    for (u32 j = 0; j < kEarly; ++j) {
+      const bool ok = j < len && a + j < n_cap;
+      e0[j] = ok ? tokens.w[0][a + j] : 0;
+      e1[j] = ok ? tokens.w[1][a + j] : 0;
+    }
     // one LDS atomic per wave: the wave's runs are appended back to back (any order will
     // do -- equal keys are indistinguishable in the output)
     const u32 incl = dev::wave_inclusive_scan(len);
@@ -152,8 +163,15 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
     if (lane == 63 && incl) wbase = atomicAdd(&s_count, incl);
     wbase = (u32)__builtin_amdgcn_readlane((int)wbase, 63);
     u32 at = wbase + incl - len;
-    for (u32 j = 0; j < len; ++j, ++at)
-      if (at < (u32)kPsortMax) s_list[at] = a + j;
+#pragma unroll
+    for (u32 j = 0; j < kEarly; ++j)
+      if (j < len && at + j < (u32)kPsortMax) {
+        s_list[at + j] = a + j;
+        s_w0[at + j] = e0[j];
+        s_w1[at + j] = e1[j];
+      }
+    for (u32 j = kEarly; j < len; ++j)
+      if (at + j < (u32)kPsortMax) s_list[at + j] = (a + j) | kLate;
   }
   below = dev::wave_reduce_sum(below);
   if (lane == 0 && below) atomicAdd(&s_below, below);
@@ -186,18 +204,25 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   }
   {
     u32 gi[kPsRounds];
+    bool late[kPsRounds];
     u64 x0[kPsRounds], x1[kPsRounds];
 #pragma unroll
     for (int r = 0; r < kPsRounds; ++r) {
       const u32 i = (u32)t + (u32)r * kPsBlock;
-      gi[r] = i < m ? s_list[i] : 0xFFFFFFFFu;
+      const u32 v = i < m ? s_list[i] : 0xFFFFFFFFu;
+      late[r] = i < m && (v & kLate);
+      gi[r] = i < m ? (v & ~kLate) : 0xFFFFFFFFu;
+      if (late[r]) s_list[i] = gi[r];  // plain indices from here on
     }
-    // words 0 and 1 in one round trip (word 1 is read even for short keys, where it is 0:
-    // a second dependent round of gathers costs more than the extra bytes)
+    // words 0 and 1: loaded in step 1 (in LDS), or now for the runs' later keys, all in
+    // one round trip (word 1 is read even for short keys, where it is 0: a second
+    // dependent round of gathers costs more than the extra bytes)
 #pragma unroll
     for (int r = 0; r < kPsRounds; ++r) {
-      x0[r] = gi[r] < n_cap ? tokens.w[0][gi[r]] : 0;
-      x1[r] = gi[r] < n_cap ? tokens.w[1][gi[r]] : 0;
+      const u32 i = (u32)t + (u32)r * kPsBlock;
+      const bool ok = gi[r] < n_cap;
+      x0[r] = !ok ? 0 : late[r] ? tokens.w[0][gi[r]] : s_w0[i];
+      x1[r] = !ok ? 0 : late[r] ? tokens.w[1][gi[r]] : s_w1[i];
     }
 #pragma unroll
     for (int r = 0; r < kPsRounds; ++r) {
