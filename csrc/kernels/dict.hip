@@ -1245,15 +1245,15 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
             c3[q] = s_k123[3 * jj + 2];
             cc[q] = in ? s_cnt[jj] : 0ull;
           }
-          if (ex.variant & 64u) {  // A/B: the short-circuit compare (branches)
 #pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-              const bool lt = j + q < j1 &&
-                              (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
-                               (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
-              cnt += lt ? 1u : 0u;
-              less += lt ? cc[q] : 0ull;
-            }
+          for (u32 q = 0; q < 4; ++q) {
+            // (a bitwise, branch-free form of this compare measured 1 % slower here: the
+            // short-circuit exits early for most candidates, whose first words differ)
+            const bool lt = j + q < j1 &&
+                            (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
+                             (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
+            cnt += lt ? 1u : 0u;
+            less += lt ? cc[q] : 0ull;
           } else {
             // bitwise: no branches, no exec-mask juggling per candidate
 #pragma unroll
