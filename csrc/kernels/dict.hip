@@ -1254,17 +1254,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
                              (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
             cnt += lt ? 1u : 0u;
             less += lt ? cc[q] : 0ull;
-          } else {
-            // bitwise: no branches, no exec-mask juggling per candidate
-#pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-              const bool lt = (j + q < j1) &
-                              ((c0[q] < k0) |
-                               ((c0[q] == k0) &
-                                ((c1[q] < k1) | ((c1[q] == k1) & ((c2[q] < k2) | ((c2[q] == k2) & (c3[q] < k3)))))));
-              cnt += (u32)lt;
-              less += lt ? cc[q] : 0ull;
-            }
           }
         }
         if (trace)
