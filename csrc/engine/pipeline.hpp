@@ -498,6 +498,29 @@ struct DevicePipeline {
       // streams and piece events, and the plan's scratch
       ensure_piece_events(partial_slots_cap);
       if (devplan_env) ensure_plan();
+      if (warm_streams_env()) warm_copy_streams();
+    }
+  }
+
+  // The copy streams' first use (queue bring-up, the runtime's copy and fill kernels) in the
+  // constructor, not in the first job: one piece-sized copy, a fill at an unaligned address
+  // and a short read-back on each, as a piecewise upload issues them.  LOCUST_WARM_STREAMS=0
+  // leaves them cold.
+  static bool warm_streams_env() {
+    static const bool on = [] {
+      const char* e = std::getenv("LOCUST_WARM_STREAMS");
+      return !e || e[0] != '0';
+    }();
+    return on;
+  }
+  void warm_copy_streams() {
+    if (!h_text || !cstream || !cstream2) return;
+    const u64 n = std::min<u64>(cap_bytes, kPieceBytes);
+    for (hipStream_t s : {cstream, cstream2, stream}) {
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, n, hipMemcpyHostToDevice, s));
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_text + 1, 0, 16, s));
+      LOCUST_HIP_CHECK(hipMemcpyAsync(h_u64, d_text, 8, hipMemcpyDeviceToHost, s));
+      LOCUST_HIP_CHECK(hipStreamSynchronize(s));
     }
   }
 
