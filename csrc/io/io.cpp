@@ -5,10 +5,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
+#include <vector>
 
 namespace locust {
 
@@ -86,27 +90,29 @@ struct Fd {
   }
 };
 
+// One slice [a, b) of a read into dst: preads until done; optionally counts its '\n'.
+bool pread_slice(int fd, char* dst, u64 off, u64 a, u64 b, bool count_nl, u64* nl) {
+  u64 pos = a;
+  while (pos < b) {
+    const ssize_t k = ::pread(fd, dst + pos, (size_t)std::min<u64>(b - pos, 1ull << 30),
+                              (off_t)(off + pos));
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    pos += (u64)k;
+  }
+  *nl = count_nl ? (u64)std::count(dst + a, dst + b, '\n') : 0;
+  return true;
+}
+
 // [off, off + n) of the file into dst, `threads` preads at once (page-cache reads run at
 // memcpy speed per core); optionally counts the '\n' bytes read.
 u64 pread_parallel(int fd, char* dst, u64 off, u64 n, u32 threads, const std::string& path,
                    bool count_nl) {
   threads = std::max<u32>(1, std::min<u64>(threads, std::max<u64>(1, n >> 20)));
   std::vector<u64> nls(threads, 0);
-  std::vector<std::string> errs(threads);
+  std::vector<char> ok(threads, 1);
   auto work = [&](u32 t) {
-    const u64 a = n * t / threads, b = n * (t + 1) / threads;
-    u64 pos = a;
-    while (pos < b) {
-      const ssize_t k = ::pread(fd, dst + pos, (size_t)std::min<u64>(b - pos, 1ull << 30),
-                                (off_t)(off + pos));
-      if (k < 0 && errno == EINTR) continue;
-      if (k <= 0) {
-        errs[t] = "short read: " + path;
-        return;
-      }
-      pos += (u64)k;
-    }
-    if (count_nl) nls[t] = (u64)std::count(dst + a, dst + b, '\n');
+    ok[t] = pread_slice(fd, dst, off, n * t / threads, n * (t + 1) / threads, count_nl, &nls[t]);
   };
   if (threads == 1) {
     work(0);
@@ -117,11 +123,95 @@ u64 pread_parallel(int fd, char* dst, u64 off, u64 n, u32 threads, const std::st
   }
   u64 total = 0;
   for (u32 t = 0; t < threads; ++t) {
-    if (!errs[t].empty()) throw Error(errs[t]);
+    if (!ok[t]) throw Error("short read: " + path);
     total += nls[t];
   }
   return total;
 }
+
+// The streamed source's readers: threads - 1 workers that live as long as the source, plus
+// the caller, split every read into equal slices.  A piece of a large file is one 16 MiB
+// read; starting and joining threads for each cost ~20 % of the read time (measured with
+// pread_parallel on a 10 GiB file: 14-15 GB/s).
+class ReadPool {
+ public:
+  explicit ReadPool(u32 threads) : n_(std::max<u32>(threads, 1)) {
+    for (u32 t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~ReadPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  ReadPool(const ReadPool&) = delete;
+  ReadPool& operator=(const ReadPool&) = delete;
+
+  // Reads [off, off + n) into dst; returns its '\n' count (false ok: a short read).
+  u64 read(int fd, char* dst, u64 off, u64 n, bool* ok) {
+    const u32 parts = (u32)std::max<u64>(1, std::min<u64>(n_, n >> 20));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = {fd, dst, off, n, parts};
+      nls_.assign(n_, 0);
+      ok_.assign(n_, 1);
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    run(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    u64 total = 0;
+    *ok = true;
+    for (u32 t = 0; t < n_; ++t) {
+      total += nls_[t];
+      *ok = *ok && ok_[t];
+    }
+    return total;
+  }
+
+ private:
+  struct Job {
+    int fd = -1;
+    char* dst = nullptr;
+    u64 off = 0, n = 0;
+    u32 parts = 1;
+  };
+  void run(u32 t) {
+    if (t >= job_.parts) return;
+    const u64 a = job_.n * t / job_.parts, b = job_.n * (t + 1) / job_.parts;
+    u64 nl = 0;
+    ok_[t] = pread_slice(job_.fd, job_.dst, job_.off, a, b, true, &nl);
+    nls_[t] = nl;
+  }
+  void loop(u32 t) {
+    u64 seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      run(t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  const u32 n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  Job job_;
+  std::vector<u64> nls_;
+  std::vector<char> ok_;
+  u32 pending_ = 0;
+  u64 gen_ = 0;
+  bool stop_ = false;
+};
 
 // A file as line-aligned chunks (TextSource): each chunk is the carried-over partial line
 // of the previous read, then parallel preads, cut after its last '\n'.
@@ -130,6 +220,7 @@ class FileTextSource final : public TextSource {
   FileTextSource(const std::string& path, u32 threads) : path_(path), fd_(path) {
     size_ = fd_.size();
     threads_ = io_threads(threads, size_);
+    if (threads_ > 1) pool_.reset(new ReadPool(threads_));
   }
   u64 size() const override { return size_; }
   u64 lines() const override { return lines_; }
@@ -141,7 +232,13 @@ class FileTextSource final : public TextSource {
     u64 nl = (u64)std::count(carry_.begin(), carry_.end(), '\n');
     carry_.clear();
     const u64 want = std::min<u64>(cap - n, size_ - pos_);
-    if (want) nl += pread_parallel(fd_.fd, dst + n, pos_, want, threads_, path_, true);
+    if (want && pool_) {
+      bool ok = true;
+      nl += pool_->read(fd_.fd, dst + n, pos_, want, &ok);
+      if (!ok) throw Error("short read: " + path_);
+    } else if (want) {
+      nl += pread_parallel(fd_.fd, dst + n, pos_, want, 1, path_, true);
+    }
     pos_ += want;
     n += want;
     if (pos_ < size_) {  // keep whole lines: the tail waits for the next chunk
@@ -165,6 +262,7 @@ class FileTextSource final : public TextSource {
   u64 size_ = 0, pos_ = 0, lines_ = 0;
   u32 threads_ = 1;
   std::string carry_;
+  std::unique_ptr<ReadPool> pool_;
 };
 
 }  // namespace

@@ -616,13 +616,14 @@ PYBIND11_MODULE(_locust, m) {
   m.def("next_segment_gen", &next_segment_gen);
   m.def("new_group_token", &new_group_token);
   m.def("file_source_chunks",  // the streamed file source's chunks (tests)
-        [](const std::string& path, u64 cap) {
-          auto src = open_file_source(path, 2);
+        [](const std::string& path, u64 cap, u32 threads) {
+          auto src = open_file_source(path, threads);
           std::vector<char> buf(cap);
           py::list parts;
           for (u64 n; (n = src->next(buf.data(), cap)) != 0;) parts.append(py::bytes(buf.data(), n));
           return py::make_tuple(parts, src->lines());
-        });
+        },
+        py::arg("path"), py::arg("cap"), py::arg("threads") = 2);
   m.def("text_window",  // the in-memory window (the loader's reference semantics)
         [](const std::string& text, i64 start, i64 end, bool ref_compat) {
           LoadedText t = text_from_buffer(text.data(), text.size(), start, end, ref_compat);

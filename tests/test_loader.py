@@ -46,3 +46,16 @@ def test_file_source_chunks(tmp_path, hamlet):
         assert b"".join(parts) == hamlet + b"tail without newline"
         assert all(p.endswith(b"\n") for p in parts[:-1]) and all(len(p) <= cap for p in parts)
         assert lines == hamlet.count(b"\n") + 1
+
+
+def test_file_source_read_pool(tmp_path, hamlet):
+    """Pieces of several MiB are read by the source's persistent reader threads: slices of
+    one read land in order and every piece still ends on a line boundary."""
+    f = tmp_path / "big.txt"
+    body = hamlet * 40  # ~7.6 MB
+    f.write_bytes(body)
+    for threads in (1, 3, 8):
+        parts, lines = lc._C.file_source_chunks(str(f), 3 << 20, threads)
+        assert b"".join(parts) == body
+        assert all(p.endswith(b"\n") for p in parts) and len(parts) >= 3
+        assert lines == body.count(b"\n")

@@ -18,6 +18,9 @@ def main() -> int:
     ap.add_argument("--jobs", type=int, default=3)
     ap.add_argument("--graph0", action="store_true", help="last engine with stage events")
     ap.add_argument("--keep", action="store_true", help="keep every engine alive")
+    ap.add_argument("--between", default="", choices=["", "hostfree", "engine"],
+                    help="after engine 0's jobs: free a pinned buffer / make and drop a small "
+                         "engine, then run engine 0's jobs again")
     a = ap.parse_args()
     import locust_amd as lc
 
@@ -41,6 +44,18 @@ def main() -> int:
               + " / ".join(f"{m:.1f}" for m in ms)
               + f" ms; unique {r.num_unique}; map {tm['map_ms']:.1f} wall {tm['wall_ms']:.1f}",
               flush=True)
+        if a.between and e == 0:
+            if a.between == "hostfree":
+                tmp = lc._C.HostText.generate(bytes=64 << 20, seed=2, first_block=0)
+            else:
+                tmp = lc._C.GpuEngine(cfg, 64 << 20, 64 << 20)
+            del tmp
+            ms = []
+            for _ in range(a.jobs):
+                t = time.perf_counter()
+                r = eng.run_text(text)
+                ms.append((time.perf_counter() - t) * 1e3)
+            print(f"engine 0 after {a.between}: jobs " + " / ".join(f"{m:.1f}" for m in ms), flush=True)
         if a.keep:
             kept.append(eng)
         del r, eng
