@@ -6,7 +6,7 @@
 
 One "step" is one complete WordCount job: H2D of the text, Map (tokenize/emit), Process
 (compaction + radix sort), Reduce (boundary mark + head compaction + adjacent difference)
-and D2H of the sorted (key, val, count) results -- the reference's timed stages
+and D2H of the sorted (key, count) results (val = the prefix of the counts, rebuilt on read) -- the reference's timed stages
 (main.cu:405-468) plus the transfers it leaves untimed.  The reference numbers are on a
 GTX 1060 (README.md:72-88): 4,500-line whole-Hamlet LDS-reduce total 77.393 ms, 700-line
 total 29.405 ms.

@@ -335,11 +335,11 @@ void print_gpu_result(const CliArgs& a, const WordCountResult& r, const std::vec
     LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",
                     (unsigned long long)r.truncated, a.cfg.max_key_len);
   std::string out;
-  if (!a.quiet) format_gpu_output(r.entries, &out);
+  if (!a.quiet) format_gpu_output(r, &out);
   std::fflush(stdout);
   write_all(stdout, out);
   write_json(a, r, walls);
-  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r.entries);
+  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r);
   std::printf("\nDone\n");
 }
 
@@ -434,7 +434,7 @@ int run(const CliArgs& a) {
     }
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(r.times.process_ms + r.times.reduce_ms));
     std::string out;
-    if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r.entries, &out);
+    if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r, &out);
     std::fflush(stdout);
     write_all(stdout, out);
     if (!a.json.empty()) {
@@ -484,7 +484,7 @@ int run(const CliArgs& a) {
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(dr.reduce_ms));
     std::string out;
-    if (!a.quiet) format_gpu_output(dr.result.entries, &out);
+    if (!a.quiet) format_gpu_output(dr.result, &out);
     std::fflush(stdout);
     write_all(stdout, out);
     write_json_dist(a, dr, ranks);
@@ -551,11 +551,11 @@ int run(const CliArgs& a) {
     LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",
                     (unsigned long long)r.truncated, a.cfg.max_key_len);
   std::string out;
-  if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r.entries, &out);
+  if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r, &out);
   std::fflush(stdout);
   write_all(stdout, out);
   write_json(a, r, walls);
-  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r.entries);
+  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r);
   std::printf("\nDone\n");
   return 0;
 }

@@ -185,7 +185,6 @@ class CpuShardEngine final : public ShardEngine {
       while (j < recs.size() && key_compare(recs[j].w, recs[i].w) == 0) c += recs[j++].count;
       WordCountEntry e;
       for (int w = 0; w < kKeyWords; ++w) e.key.w[w] = recs[i].w[w];
-      e.val = pos;
       e.count = c;
       out_.push_back(e);
       pos += c;
@@ -204,10 +203,7 @@ class CpuShardEngine final : public ShardEngine {
     reduce_received(n_other + local_.size(), total_count, num_unique);
   }
 
-  void finalize(u64 global_offset, EntryList* out) override {
-    for (auto& e : out_) e.val += global_offset;
-    out->assign(out_.data(), out_.data() + out_.size());
-  }
+  void finalize(EntryList* out) override { out->assign(out_.data(), out_.data() + out_.size()); }
 
   void map_stats(WordCountResult* r) override { *r = stats_; }
 

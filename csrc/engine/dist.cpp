@@ -316,7 +316,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         u64 total = 0, uniq = 0;
         if (local("reduce", [&] { eng.finish_merge_slots(&total, &uniq); }))
           throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
-        eng.finalize(0, &r.entries);
+        eng.finalize(&r.entries);
         res.range_tokens = total;
         res.range_unique = uniq;
       }
@@ -564,7 +564,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         u64 total = 0, uniq = 0;
         if (local("reduce", [&] { eng.exch_finish_root((u32)P, &total, &uniq); }))
           throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
-        eng.finalize(0, &r.entries);
+        eng.finalize(&r.entries);
       }
       eng.exch_job_done();
       r.num_unique = me == 0 ? r.entries.size() : R[me].n_out;
@@ -665,7 +665,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         });
       if (st)
         throw Error(std::string("distributed job failed on rank 0: ") + local_msg);
-      eng.finalize(0, &r.entries);
+      eng.finalize(&r.entries);
       res.range_tokens = total;
       res.range_unique = uniq;
     }
@@ -761,7 +761,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   u64 offset = 0;
   for (int p = 0; p < me; ++p) offset += all3[(size_t)p].total;
   EntryList entries;
-  eng.finalize(offset, &entries);
+  eng.finalize(&entries);
   res.range_tokens = total;
   res.range_unique = uniq;
   const u64 t3 = now_ns();
@@ -783,6 +783,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     }
   } else {
     r.entries = std::move(entries);
+    r.val_base = offset;  // this rank's range starts after the lower ranks' tokens
   }
   r.num_unique = me == 0 && cfg.gather ? r.entries.size() : uniq;
   const u64 t4 = now_ns();

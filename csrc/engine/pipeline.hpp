@@ -1327,7 +1327,6 @@ struct DevicePipeline {
     for (u64 i = 0; i < n; ++i) {
       for (int w = 0; w < kKeyWords; ++w) e[i].key.w[w] = h[i].w[w];
       e[i].count = h[i].count;
-      e[i].val = 0;
     }
     PartMapTables t;
     const u64 pred = part_map_from_entries(e.data(), n, &t);
@@ -1619,11 +1618,10 @@ struct DevicePipeline {
     return dma;
   }
 
-  // Host output records -> result entries: identical 48-byte layouts, so the result
+  // Host output records -> result entries: identical 40-byte layouts, so the result
   // simply adopts the buffer the device wrote (no copy; see select_out).
   void copy_out(EntryList& e, u64 u) {
     static_assert(sizeof(WordCountEntry) == sizeof(OutRecord), "entry layout");
-    static_assert(offsetof(WordCountEntry, val) == offsetof(OutRecord, val), "entry layout");
     static_assert(offsetof(WordCountEntry, count) == offsetof(OutRecord, count), "entry layout");
     LOCUST_CHECK_ARG(u <= h_out_cap, "output larger than its buffer");
     e.adopt(out_pool[out_idx], reinterpret_cast<WordCountEntry*>(h_out), u);

@@ -341,7 +341,7 @@ class GpuShardEngine final : public ShardEngine {
   }
 
   void* slot_buffer(u32 nslots, u32 slot_recs) override {
-    // rp_ holds the slots in d_records; its d_out (48-B records) is the merge scratch.
+    // rp_ holds the slots in d_records; its d_out (40-B records) is the merge scratch.
     return recv_records((u64)nslots * (kSlotHeaderRecords + slot_recs));
   }
 
@@ -1014,11 +1014,7 @@ class GpuShardEngine final : public ShardEngine {
     reduce_received(n_other + local_count_, total_count, num_unique);
   }
 
-  void finalize(u64 global_offset, EntryList* out) override {
-    if (global_offset)  // (a pass over every entry: 0.2 ms for 200K of them)
-      for (auto& e : range_entries_) e.val += global_offset;
-    *out = std::move(range_entries_);
-  }
+  void finalize(EntryList* out) override { *out = std::move(range_entries_); }
 
   void map_stats(WordCountResult* r) override { *r = local_stats_; }
 

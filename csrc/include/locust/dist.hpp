@@ -321,7 +321,8 @@ class ShardEngine {
   u64 exch_group = 0;     // the communicator's group id (names the shared output)
   int exch_rank = 0;      // this rank in that group
   bool exch_in_process = false;  // every rank of the group is a thread of this process
-  virtual void finalize(u64 global_offset, EntryList* out) = 0;
+  // Hands this rank's entries over (the caller sets the result's val_base).
+  virtual void finalize(EntryList* out) = 0;
   // Map-stage counters of the last map_local.
   virtual void map_stats(WordCountResult* r) = 0;
 };

@@ -45,13 +45,17 @@ struct StageTimes {
   double ref_map_ms = 0, ref_process_ms = 0, ref_reduce_ms = 0;
 };
 
-// One output entry: a unique key, the start index of its run in the globally sorted
-// token array (the reference's `val`) and the run length (`count`).
+// One output entry: a unique key and the length of its run in the globally sorted token
+// array (`count`); 40 B, the layout of KeyCount and of the device's output records.  The
+// reference's `val` (start index of the run, KeyValue.h:13-18 / main.cu:181-206) is the
+// exclusive prefix of the counts in key order: it is not stored per entry (it would be 8 B
+// of every record crossing PCIe) but rebuilt on the host from WordCountResult::val_base --
+// see EntryVals.
 struct WordCountEntry {
   PackedKey key;
-  u64 val;
   u64 count;
 };
+static_assert(sizeof(WordCountEntry) == 40, "WordCountEntry 40 B");
 
 // The entries of a result: an owned vector, or -- zero-copy -- the engine's host-mapped
 // output buffer itself, which the device wrote and which this list keeps alive (`owner`)
@@ -114,6 +118,9 @@ class EntryList {
 
 struct WordCountResult {
   EntryList entries;  // sorted by key
+  // val of entries[0]: 0 for a whole result, the token total of the lower ranks' key
+  // ranges for one rank's range of a distributed job.
+  u64 val_base = 0;
   u64 num_lines = 0;
   u64 num_tokens = 0;       // kv_num_map
   u64 num_unique = 0;       // kv_num_reduce
@@ -122,6 +129,22 @@ struct WordCountResult {
   u64 max_key_len = 0;
   u64 chunks = 1;           // > 1: the input streamed through the engine in chunks
   StageTimes times;
+};
+
+// The reference's val of each entry in order: val(i) = val_base + sum of counts before i.
+//   EntryVals v(res); for (auto& e : res.entries) { u64 val = v.next(e); ... }
+class EntryVals {
+ public:
+  explicit EntryVals(const WordCountResult& r) : at_(r.val_base) {}
+  explicit EntryVals(u64 base) : at_(base) {}
+  u64 next(const WordCountEntry& e) {
+    const u64 v = at_;
+    at_ += e.count;
+    return v;
+  }
+
+ private:
+  u64 at_;
 };
 
 // Text read piece by piece (a file too large to hold): whole lines go straight into the

@@ -14,11 +14,11 @@
 //            rank computes the same), 64-ary searches of them in the local sorted records
 //   pack     records -> P slots (SlotHeader + the bucket) at a fixed pitch
 //   C2       the slots to their ranks (every xGMI link busy at once)
-//   merge    the P received sorted runs -> this rank's key range, local val (merge.hip)
+//   merge    the P received sorted runs -> this rank's key range (merge.hip)
 //   report   ExchMsg3 (overflow flags, range size, token total, largest bucket)
 //   C3       ncclAllGather of the reports: every rank sees every flag and total
 //   emit     this rank's range -> the shared host output (locust/shm.hpp) at its global
-//            offset, val += the token totals of the lower ranks; a completion stamp.  Every
+//            offset (val is rebuilt on the host from the counts); a completion stamp.  Every
 //            rank drains its own range over its own PCIe link: no gather to the root.
 //
 // Two schedules:
@@ -82,8 +82,8 @@ struct ExchCtl {
 LOCUST_HD inline u64 exch_msg1_bytes(u32 samples) { return sizeof(ExchMsg1) + (u64)samples * sizeof(PackedKey); }
 // All-to-all slot: a SlotHeader (two KeyCount records) + slot_records KeyCount records.
 LOCUST_HD inline u64 exch_slot_bytes(u32 slot_records) { return (u64)(2 + slot_records) * sizeof(KeyCount); }
-// Range buffer: gather_records (key, val, count) 48-B records (the size is in ExchMsg3).
-LOCUST_HD inline u64 exch_gslot_bytes(u32 gather_records) { return (u64)gather_records * 48; }
+// Range buffer: gather_records (key, count) 40-B records (the size is in ExchMsg3).
+LOCUST_HD inline u64 exch_gslot_bytes(u32 gather_records) { return (u64)gather_records * 40; }
 // Next job's slot size for a largest observed bucket / range of `used` records.
 inline u32 exch_grow(u64 used) {
   const u64 want = used + used / 8 + 64;

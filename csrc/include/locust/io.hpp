@@ -52,7 +52,7 @@ std::vector<KeyCount> read_spill(const std::string& path);
 // Final (key, val, count) results as KeyIntValuePair records (value = val), the reference's
 // reduce output array (main.cu:470-473); the same header.  Values past INT_MAX and keys
 // past 29 bytes are refused.
-void write_kiv_results(const std::string& path, const EntryList& e);
+void write_kiv_results(const std::string& path, const WordCountResult& r);
 // KeyIntValuePair records of a kiv file: (key, value, count).
 struct KivRecord {
   PackedKey key;
@@ -64,9 +64,9 @@ std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs);
 
 // ---- output ----
 // GPU build format (main.cu:132): "print key: %s \t val: %d \t count: %d\n".
-void format_gpu_output(const EntryList& e, std::string* out);
+void format_gpu_output(const WordCountResult& r, std::string* out);
 // CPU build format (main.cu:286): "print key: %s \t value: %s\n" with value = count.
-void format_cpu_output(const EntryList& e, std::string* out);
+void format_cpu_output(const WordCountResult& r, std::string* out);
 void write_all(std::FILE* f, const std::string& s);
 
 std::string key_to_string(const PackedKey& k);

@@ -202,15 +202,18 @@ void launch_adjacent_diff(const u64* head_val, u64 cap, ReducePath path, u64* he
 void launch_add_offset(u64* head_val, u64 cap, const u64* d_offset, const MapCounters* ctr,
                        hipStream_t s);
 
-// Output records for the host: {packed key, val, count}.
+// Output records for the host: {packed key, count}, 40 B (KeyCount's layout).  The
+// reference's val (start of the key's run in the sorted token order) is the exclusive
+// prefix of the counts and is rebuilt on the host (EntryVals, engine.hpp) instead of
+// crossing PCIe with every record (round 2 wrote 48-B {key, val, count} records).
 struct OutRecord {
   u64 w[kKeyWords];
-  u64 val;
   u64 count;
 };
-static_assert(sizeof(OutRecord) == 48, "OutRecord 48 B");
+static_assert(sizeof(OutRecord) == 40, "OutRecord 40 B");
+constexpr u32 kOutWords = sizeof(OutRecord) / 8;  // 5 u64 words per record
 // Unweighted reduce steps 1-3 + output records in one kernel (LDS-staged tiles): `out`
-// (room for out_cap records; host-mapped allowed) receives {key, val, count} in key order,
+// (room for out_cap records; host-mapped allowed) receives {key, count} in key order,
 // ctr->num_unique / total_count are set and ctr_out (optional, host-mapped) gets a
 // snapshot.  `lb` needs div_up(cap, kReduceTile) + 1 zeroed status words and a zeroed
 // tile counter.
@@ -219,8 +222,7 @@ void launch_reduce_fused(ConstKeysSoA sorted, u64 cap, MapCounters* ctr, OutReco
 // Process + Reduce of the reference algorithm in ONE kernel (psort.hip): the partitioned
 // LDS sort above, then inside each partition's workgroup the head mark (key[i] !=
 // key[i-1]; runs never cross partitions, which are key ranges), counts as distances to the
-// next head, val = the head's global position in the sorted token order (the partition's
-// offset + local index, known up front), the record index from a look-back over the
+// next head, the record index from a look-back over the
 // partitions' head counts -- and the records straight into `out` (host-mapped allowed).
 // The sorted token array is never written.  Self-cleaning like the ordered dictionary
 // kernel: `status` (kDictParts look-back words) and `done_counter` must be zero before and
@@ -277,7 +279,7 @@ void launch_dict_part_build(ConstKeysSoA tokens, const u64* counts, const u8* pa
                             hipStream_t s);
 // Ordered build (partitions = PartMap ranges, default the first key byte): aggregation,
 // per-partition LDS sort,
-// look-back offsets and the final (key, val, count) records in ONE kernel.  `out` needs
+// look-back offsets and the final (key, count) records in ONE kernel.  `out` needs
 // room for every distinct key; `lb` needs kDictParts + 1 zeroed status words and a zeroed
 // tile counter.  Sets ctr->num_unique / total_count (and ctr_out, if given, like the
 // emit kernels); a partition past kPartSlots distinct keys sets kCtrDictOverflow.
@@ -407,13 +409,14 @@ void launch_dict_insert(ConstKeysSoA tokens, const u64* counts, const u32* d_n, 
 // Early-exits (device-side) when *d_u > kRankSortMax.
 void launch_rank_sort(ConstKeysSoA keys, const u64* counts, const u32* d_u, u64 cap, u32* rank,
                       u64* val, hipStream_t s);
-// out[rank[i]] = {key i, val i, count i}; optional host-mapped counter snapshot.
+// out[rank[i]] = {key i, count i} (val feeds total_count only); optional host-mapped
+// counter snapshot.
 void launch_rank_emit(ConstKeysSoA keys, const u64* counts, const u32* rank, const u64* val,
                       u64 cap, const MapCounters* ctr, OutRecord* out, MapCounters* ctr_out,
                       hipStream_t s);
 void launch_rank_scatter(ConstKeysSoA keys, const u64* counts, const u32* rank, const u32* d_u,
                          u64 cap, KeysSoA sorted, u64* sorted_counts, hipStream_t s);
-// val = exclusive scan of the sorted counts; writes OutRecords and ctr->total_count.
+// Scan of the sorted counts (-> ctr->total_count) and the OutRecords.
 void launch_scan_pack(ConstKeysSoA sorted, const u64* counts, u64 cap, MapCounters* ctr,
                       OutRecord* out, LookbackScratch lb, hipStream_t s,
                       MapCounters* ctr_out = nullptr, u32 emit_limit = 0xFFFFFFFFu);
@@ -454,9 +457,9 @@ void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchC
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
                         const MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
                         hipStream_t s);
-// This rank's range (`range`, val local) -> dst (the shared host output's records, device
-// view) in region `region` (root_msg != nullptr: the region the root's all-gathered
-// ExchMsg1 names) at its global offset with global val; the last workgroup stores `seq`
+// This rank's range (`range`) -> dst (the shared host output's records, device view) in
+// region `region` (root_msg != nullptr: the region the root's all-gathered ExchMsg1
+// names) at its global offset; the last workgroup stores `seq`
 // into stamps[me] (system-scope release) after every workgroup's writes.  `done`: a device
 // u32, zero before the launch and left zero.
 void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const ExchMsg1* root_msg,

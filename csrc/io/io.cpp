@@ -421,11 +421,13 @@ void write_kiv_file(const std::string& path, const std::vector<KeyIntValuePair>&
 }
 }  // namespace
 
-void write_kiv_results(const std::string& path, const EntryList& e) {
+void write_kiv_results(const std::string& path, const WordCountResult& r) {
+  const EntryList& e = r.entries;
   std::vector<KeyIntValuePair> v;
   v.reserve(e.size());
+  EntryVals vals(r);
   for (size_t i = 0; i < e.size(); ++i)
-    v.push_back(to_kiv(e[i].key.w, (i64)e[i].val, (i64)e[i].count, path));
+    v.push_back(to_kiv(e[i].key.w, (i64)vals.next(e[i]), (i64)e[i].count, path));
   write_kiv_file(path, v);
 }
 
@@ -560,23 +562,27 @@ std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs) {
 }
 
 // ---------------- output ----------------
-void format_gpu_output(const EntryList& e, std::string* out) {
+void format_gpu_output(const WordCountResult& r, std::string* out) {
+  const EntryList& e = r.entries;
   out->reserve(out->size() + e.size() * 48);
   char buf[kKeyBytes + 1];
+  EntryVals vals(r);
   for (const auto& x : e) {
+    const u64 val = vals.next(x);
     int n = unpack_key(x.key.w, buf);
     if (n == 0) continue;
     out->append("print key: ");
     out->append(buf, (size_t)n);
     out->append(" \t val: ");
-    append_u64(out, x.val);
+    append_u64(out, val);
     out->append(" \t count: ");
     append_u64(out, x.count);
     out->push_back('\n');
   }
 }
 
-void format_cpu_output(const EntryList& e, std::string* out) {
+void format_cpu_output(const WordCountResult& r, std::string* out) {
+  const EntryList& e = r.entries;
   out->reserve(out->size() + e.size() * 32);
   char buf[kKeyBytes + 1];
   for (const auto& x : e) {

@@ -6,7 +6,7 @@
 // then recovers per-key runs by boundary marking (main.cu:161-238).  The output it prints
 // is a function of the distinct keys and their multiplicities only: val = the start of a
 // key's run in the sorted token array = the exclusive prefix sum of the counts of all
-// smaller keys; count = the run length.  So:
+// smaller keys (rebuilt on the host, engine.hpp EntryVals); count = the run length.  So:
 //
 //   dict_insert   two-level hash aggregation.  A workgroup takes 1,024 consecutive tokens
 //                 and combines duplicates in an LDS hash table (LDS atomics); only the
@@ -21,8 +21,8 @@
 //                 over every CU in one launch instead of ~14 dependent radix passes.
 //                 Larger U goes to the LSD radix sort (radix_sort.hip).
 //   rank_scatter  sorted[rank[i]] = key[i], counts alongside.
-//   scan_pack     exclusive scan of the counts with decoupled look-back -> val, and the
-//                 final (key, val, count) records for the D2H.
+//   scan_pack     exclusive scan of the counts with decoupled look-back -> the token
+//                 total, and the final 40-B (key, count) records for the D2H.
 #include <algorithm>
 #include <type_traits>
 
@@ -1100,10 +1100,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   // Positions in the compacted arrays: any order will do (they are sorted next), so a wave
   // takes its slice with ONE LDS atomic and its lanes' offsets come from two ballots --
   // no block scan, one barrier.  Token sums and the overflow flag ride along.
-  u64* s_cnt = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);  // [kSmallRank] counts
   u32* s_rk = s_list + 3 * kPartSlots + 2 * kSmallRank;         // [kSmallRank] ranks
-  u64* s_less = reinterpret_cast<u64*>(s_rk + kSmallRank);       // [kSmallRank] vals
-  u64* s_out = s_less + kSmallRank;                              // [6 x kSmallRank] records
+  u64* s_out = reinterpret_cast<u64*>(s_rk + 2 * kSmallRank);    // [5 x kSmallRank] records
   u64* s_k123 = s_out + 6 * kSmallRank;                          // [3 x kSmallRank] words 1-3
   {
     const u64 b0 = dev::ballot(mine >= 1), b1 = dev::ballot(mine >= 2);
@@ -1124,24 +1122,20 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         s_w0[d] = s_tab[slot].w[0];
         s_slot[d] = slot;
         if (d < kSmallRank) {
-          s_cnt[d] = s_tab[slot].count;
 #pragma unroll
           for (int j = 1; j < kKeyWords; ++j) s_k123[3 * d + j - 1] = s_tab[slot].w[j] ^ kWordMagic;
         }
         ++d;
       }
     }
-    if (threadIdx.x < kSmallRank) {
-      s_rk[threadIdx.x] = 0;
-      s_less[threadIdx.x] = 0;
-    }
+    if (threadIdx.x < kSmallRank) s_rk[threadIdx.x] = 0;
   }
   __syncthreads();  // the compacted (w0, slot) arrays and the sums are complete
   const u32 m = s_cm;
   const int any_full = s_cfull != 0u;
   const u64 tok = s_ctok;
   // Small partitions (the common case once the partition map is balanced) skip the
-  // bucket sort: ranks AND vals come from one all-pairs pass (see below).
+  // bucket sort: ranks come from one all-pairs pass (see below).
   const bool small = !(ex.variant & 1u) && !any_full && m <= kSmallRank;  // variant 1: A/B
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
@@ -1150,10 +1144,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   ORD_STAMP(2);
   u64 pre = 0;
   if (small) {
-    // ---- small partition: weighted all-pairs ranks: rank_i = #{j : key_j < key_i},
-    // val_i += the counts of those keys -- the sorted position AND the reference's val
-    // (start of the key's run) in one pass, no bucket sort, no count scan.  Wave 0
-    // resolves the look-back meanwhile. ----
+    // ---- small partition: all-pairs ranks: rank_i = #{j : key_j < key_i}, the sorted
+    // position in one pass, no bucket sort.  Wave 0 resolves the look-back meanwhile. ----
     if (dev::wave_id() == 0) {
       // Look-back in ONE round trip: wave 0 reads every predecessor's status word at once
       // (4 per lane, p < 256) instead of walking back 64 words per dependent round trip
@@ -1215,8 +1207,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
                   (unsigned long long)__builtin_amdgcn_s_memtime());
       // Waves 1..15 split the work as (key group of 64, candidate slice): lane i of its
       // group compares its full key with every candidate of the slice -- the candidates'
-      // words are LDS broadcasts, four in flight -- and the partial rank / weighted val
-      // go to LDS with one atomic each.  Full-key compares: no tie pass.
+      // words are LDS broadcasts, four in flight -- and the partial rank goes to LDS with
+      // one atomic.  Full-key compares: no tie pass.
       const u32 G = (m + 63) / 64;                 // key groups (m <= kSmallRank = 256)
       const u32 S = (u32)(kPartBlock / 64 - 1) / G;  // candidate slices per group (>= 3)
       const u32 wv = (u32)dev::wave_id() - 1u, g = wv % G, sl = wv / G;
@@ -1232,9 +1224,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         }
         const u32 j0 = sl * m / S, j1 = (sl + 1) * m / S;
         u32 cnt = 0;
-        u64 less = 0;
         for (u32 j = j0; j < j1; j += 4) {
-          u64 c0[4], c1[4], c2[4], c3[4], cc[4];
+          u64 c0[4], c1[4], c2[4], c3[4];
 #pragma unroll
           for (u32 q = 0; q < 4; ++q) {
             const bool in = j + q < j1;
@@ -1243,7 +1234,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
             c1[q] = s_k123[3 * jj];
             c2[q] = s_k123[3 * jj + 1];
             c3[q] = s_k123[3 * jj + 2];
-            cc[q] = in ? s_cnt[jj] : 0ull;
           }
 #pragma unroll
           for (u32 q = 0; q < 4; ++q) {
@@ -1253,16 +1243,12 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
                             (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
                              (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
             cnt += lt ? 1u : 0u;
-            less += lt ? cc[q] : 0ull;
           }
         }
         if (trace)
           atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 18]),
                     (unsigned long long)__builtin_amdgcn_s_memtime());
-        if (own && cnt) {
-          atomicAdd(&s_rk[i], cnt);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&s_less[i]), (unsigned long long)less);
-        }
+        if (own && cnt) atomicAdd(&s_rk[i], cnt);
       }
       if (trace && dev::lane_id() == 0)  // the slowest ranking wave's end
         atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 16]),
@@ -1274,40 +1260,34 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       dev::st_agent(&status[v], dev::kLbInc | (pre + agg));
     ORD_STAMP(3);
     ORD_STAMP(4);
-    const u64 base_tok = pre >> kOrdTokShift;
-    // stage the records in sorted order, then write them with consecutive lanes on
-    // consecutive words (full lines: matters most for the host-mapped output)
+    // stage the 40-B records (= KeyCount) in sorted order, then write them with
+    // consecutive lanes on consecutive words (full lines: matters most for the host-mapped
+    // output)
     for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
       const LdsSlot& sl = s_tab[s_slot[i]];
-      u64* o = s_out + 6 * s_rk[i];
+      u64* o = s_out + kOutWords * s_rk[i];
       o[0] = sl.w[0];
       o[1] = sl.w[1] ^ kWordMagic;
       o[2] = sl.w[2] ^ kWordMagic;
       o[3] = sl.w[3] ^ kWordMagic;
-      o[4] = base_tok + s_less[i];
-      o[5] = sl.count;
+      o[4] = sl.count;
     }
     __syncthreads();
     const u64 base_m = pre & kOrdM;
     if (((pre >> kOrdOvfShift) & 511u) == 0) {  // uniform per workgroup
-      if (out && base_m + m <= ex.out_cap) {  // 16 B per lane, consecutive lanes
-        using v2u64 = u64 __attribute__((ext_vector_type(2)));
-        v2u64* dst = reinterpret_cast<v2u64*>(out + base_m);
-        const v2u64* src = reinterpret_cast<const v2u64*>(s_out);
-        for (u32 q = threadIdx.x; q < 3 * m; q += kPartBlock) dst[q] = src[q];
+      if (out && base_m + m <= ex.out_cap) {  // 8 B per lane, consecutive lanes
+        u64* dst = reinterpret_cast<u64*>(out + base_m);
+        for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = s_out[q];
       }
-      if (ex.recs) {  // 8-B word q of the KeyCount slice: record q / 5, word q % 5
+      if (ex.recs) {  // the same words as a KeyCount slice
         u64* dst = reinterpret_cast<u64*>(ex.recs + base_m);
-        for (u32 q = threadIdx.x; q < 5 * m; q += kPartBlock) {
-          const u32 i = q / 5, wd = q - 5 * i;
-          dst[q] = s_out[6 * i + (wd < kKeyWords ? wd : 5)];
-        }
+        for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = s_out[q];
       }
       if (ex.sorted.w[0]) {
         for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
 #pragma unroll
-          for (int j = 0; j < kKeyWords; ++j) ex.sorted.w[j][base_m + i] = s_out[6 * i + j];
-          if (ex.counts) ex.counts[base_m + i] = s_out[6 * i + 5];
+          for (int j = 0; j < kKeyWords; ++j) ex.sorted.w[j][base_m + i] = s_out[kOutWords * i + j];
+          if (ex.counts) ex.counts[base_m + i] = s_out[kOutWords * i + 4];
         }
       }
     }
@@ -1508,63 +1488,24 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   pre = s_prefix;
   ORD_STAMP(4);
   const u64 base_m = pre & kOrdM;
-  const u64 base_tok = pre >> kOrdTokShift;
   const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
-  // ---- vals: scan of the counts in sorted order; write the records ----
-  constexpr u32 kPer = kPartSlots / kPartBlock;  // items per thread (m <= kPartSlots)
-  u64 c[kPer];
-  u64 run = 0;
-#pragma unroll
-  for (u32 t = 0; t < kPer; ++t) {
-    const u32 i = threadIdx.x * kPer + t;
-    c[t] = i < m ? s_tab[s_slot[i]].count : 0;
-    run += c[t];
-  }
-  u64 tot2 = 0;
-  u64 at = dev::block_exclusive_scan<u64, kPartBlock>(run, s_scan, &tot2) + base_tok;
+  // ---- write the records ----
   if (!any_full && ovf_before == 0) {  // uniform per workgroup
-    // vals into LDS (s_w0 is free after the sort), then every output is written with
-    // consecutive lanes on consecutive words: full-line writes, which matters most for the
-    // host-mapped output (each partial line would be its own PCIe write)
-    u64* s_val = s_w0;
-#pragma unroll
-    for (u32 t = 0; t < kPer; ++t) {
-      const u32 i = threadIdx.x * kPer + t;
-      if (i < m) s_val[i] = at;
-      at += c[t];
-    }
-    __syncthreads();
+    // every output is written with consecutive lanes on consecutive words: full-line
+    // writes, which matters most for the host-mapped output (each partial line would be
+    // its own PCIe write).  The 40-B records and the KeyCount slice are the same words.
+    auto word = [&](u32 q) {
+      const u32 i = q / kOutWords, wd = q - kOutWords * i;
+      const LdsSlot& sl = s_tab[s_slot[i]];
+      return wd == 0 ? sl.w[0] : wd < (u32)kKeyWords ? sl.w[wd] ^ kWordMagic : sl.count;
+    };
     if (out && base_m + m <= ex.out_cap) {
-      // 16-B chunk q of this partition's slice: record q / 3, part q % 3, ONE 16-B store
-      // per lane (two 8-B stores at a 16-B stride left every line half written per
-      // instruction: twice the partial-line PCIe writes)
-      using v2u64 = u64 __attribute__((ext_vector_type(2)));
-      v2u64* dst = reinterpret_cast<v2u64*>(out + base_m);
-      for (u32 q = threadIdx.x; q < 3 * m; q += kPartBlock) {
-        const u32 i = q / 3, part = q - 3 * i;
-        const LdsSlot& sl = s_tab[s_slot[i]];
-        u64 a, b;
-        if (part == 0) {
-          a = sl.w[0];
-          b = sl.w[1] ^ kWordMagic;
-        } else if (part == 1) {
-          a = sl.w[2] ^ kWordMagic;
-          b = sl.w[3] ^ kWordMagic;
-        } else {
-          a = s_val[i];
-          b = sl.count;
-        }
-        dst[q] = v2u64{a, b};
-      }
+      u64* dst = reinterpret_cast<u64*>(out + base_m);
+      for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = word(q);
     }
     if (ex.recs) {
-      // 8-B word q of the KeyCount slice: record q / 5, word q % 5
       u64* dst = reinterpret_cast<u64*>(ex.recs + base_m);
-      for (u32 q = threadIdx.x; q < 5 * m; q += kPartBlock) {
-        const u32 i = q / 5, wd = q - 5 * i;
-        const LdsSlot& sl = s_tab[s_slot[i]];
-        dst[q] = wd == 0 ? sl.w[0] : wd < kKeyWords ? sl.w[wd] ^ kWordMagic : sl.count;
-      }
+      for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = word(q);
     }
     if (ex.sorted.w[0]) {
       for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
@@ -1765,7 +1706,7 @@ __global__ __launch_bounds__(kRankI) void rank_sort_kernel(ConstKeysSoA keys,
   }
 }
 
-// Output records straight from the weighted ranks: out[rank[i]] = {key i, val i, count i}.
+// Output records straight from the weighted ranks: out[rank[i]] = {key i, count i}.
 // `out` may be host-mapped pinned memory (zero-copy: the records travel over PCIe as the
 // kernel writes them, and the host needs no D2H copy).  `ctr_out` (optional, host-mapped)
 // receives the final counters.
@@ -1796,10 +1737,9 @@ __global__ __launch_bounds__(256) void rank_emit_kernel(ConstKeysSoA keys,
     OutRecord rec;
 #pragma unroll
     for (int q = 0; q < kKeyWords; ++q) rec.w[q] = keys.w[q][i];
-    rec.val = val[i];
     rec.count = counts[i];
     out[r] = rec;
-    if (r == u - 1 && ctr_out) ctr_out->total_count = rec.val + rec.count;
+    if (r == u - 1 && ctr_out) ctr_out->total_count = val[i] + rec.count;
   }
 }
 
@@ -1861,8 +1801,8 @@ __global__ __launch_bounds__(256) void scan_pack_kernel(ConstKeysSoA sorted,
   }
   u64 total;
   const u64 excl = dev::block_exclusive_scan<u64, 256>(sum, s_scan, &total);
+  (void)excl;
   const u64 base = dev::block_lookback(status, tile, total, &s_prefix);
-  u64 run = base + excl;
 #pragma unroll
   for (int t = 0; t < kPackItems; ++t) {
     const u32 i = first + t;
@@ -1870,11 +1810,9 @@ __global__ __launch_bounds__(256) void scan_pack_kernel(ConstKeysSoA sorted,
       OutRecord r;
 #pragma unroll
       for (int q = 0; q < kKeyWords; ++q) r.w[q] = sorted.w[q][i];
-      r.val = run;
       r.count = c[t];
       out[i] = r;
     }
-    run += c[t];
   }
   if (tile == num_tiles - 1 && threadIdx.x == 0) {
     ctr->total_count = base + total;

@@ -259,12 +259,12 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
   }
 }
 
-// This rank's key range (n_out(me) records, val local to the range) -> the shared host
-// output at its global offset (the records of the lower ranks come first: rank order is key
-// order), val += the token totals of the lower ranks (the reference's global val).  Every
+// This rank's key range (n_out(me) 40-B {key, count} records) -> the shared host output at
+// its global offset (the records of the lower ranks come first: rank order is key order;
+// the reference's global val is the prefix of the counts, rebuilt on the host).  Every
 // rank drains its own range over its own PCIe link at once -- no gather to the root, no
-// root-side concatenation.  16-B chunks, consecutive lanes on consecutive chunks (whole
-// PCIe write lines).  Completion: every workgroup fences its writes at system scope and
+// root-side concatenation.  8-B words, consecutive lanes on consecutive words (whole PCIe
+// write lines).  Completion: every workgroup fences its writes at system scope and
 // counts itself done; the last one stores `seq` into this rank's stamp with a system-scope
 // release, which the root's host polls before it reads the output (locust/shm.hpp).
 __global__ __launch_bounds__(256) void exch_emit_kernel(
@@ -272,24 +272,19 @@ __global__ __launch_bounds__(256) void exch_emit_kernel(
     const ExchMsg1* __restrict__ root_msg, u64 region, u32 regions, u64 region_records, u32 P,
     u32 me, u32 gather_records, OutRecord* __restrict__ dst, u64* __restrict__ stamps, u64 seq,
     u32* __restrict__ done, u32 nt) {
-  __shared__ u64 s_roff, s_voff, s_n;
+  __shared__ u64 s_roff, s_n;
   __shared__ u32 s_bad;
   if (threadIdx.x == 0) {
     // the region: the host's, or the one the root announced in its all-gathered header
     if (root_msg) region = root_msg->out_region;
-    u64 r = 0, v = 0;
+    u64 r = 0;
     u32 bad = 0;
     for (u32 q = 0; q < P && q < kExchMaxRanks; ++q) {
       const ExchMsg3 m = msg3_all[q];
       bad |= (u32)m.status | m.flags;
-      if (q < me) {
-        r += m.n_out <= gather_records ? m.n_out : gather_records;
-        v += m.total;
-      }
+      if (q < me) r += m.n_out <= gather_records ? m.n_out : gather_records;
     }
     const u64 n = msg3_all[me].n_out;
-    s_roff = r;
-    s_voff = v;
     s_n = n <= gather_records ? n : gather_records;
     // no free region (the host grows the output and emits again), or a range that would
     // not fit its region (cannot happen with agreed sizes): write nothing, stamp nothing
@@ -298,25 +293,17 @@ __global__ __launch_bounds__(256) void exch_emit_kernel(
   }
   __syncthreads();
   if (s_bad) return;  // the host sees the reports: no output, no stamp
-  const u64 N = s_n, voff = s_voff;
-  const uint4* in = reinterpret_cast<const uint4*>(src);
-  uint4* out = reinterpret_cast<uint4*>(dst + s_roff);
-  // (chunk indices fit 32 bits: a range is < 2^30 records)
-  const u32 nq = (u32)(3 * N);
+  const u64 N = s_n;
+  const u64* in = reinterpret_cast<const u64*>(src);
+  u64* out = reinterpret_cast<u64*>(dst + s_roff);
+  // (word indices fit 32 bits: a range is < 2^29 records)
+  const u32 nq = (u32)(kOutWords * N);
   for (u32 q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
-    uint4 v = in[q];
-    if (q % 3u == 2u) {  // {val, count}: val becomes global
-      const u64 val = (((u64)v.y << 32) | v.x) + voff;
-      v.x = (u32)val;
-      v.y = (u32)(val >> 32);
-    }
-    if (nt) {
-      using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-      const u32x4 w = {v.x, v.y, v.z, v.w};
-      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + q));
-    } else {
+    const u64 v = in[q];
+    if (nt)
+      __builtin_nontemporal_store(v, out + q);
+    else
       out[q] = v;
-    }
   }
   __threadfence_system();
   __syncthreads();
@@ -380,8 +367,8 @@ void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const Ex
                       u64 region, u32 regions, u64 region_records, u32 P, u32 me,
                       u32 gather_records, OutRecord* dst, u64* stamps, u64 seq, u32* done,
                       hipStream_t s) {
-  const u64 chunks = 3ull * gather_records;
-  const u64 blocks = std::min<u64>(std::max<u64>(div_up(chunks ? chunks : 1, 256), 1), 2048);
+  const u64 words = (u64)kOutWords * gather_records;
+  const u64 blocks = std::min<u64>(std::max<u64>(div_up(words ? words : 1, 256), 1), 2048);
   static const u32 nt = [] {  // LOCUST_EMIT_NT=1: non-temporal stores (A/B)
     const char* e = std::getenv("LOCUST_EMIT_NT");
     return e && e[0] == '1' ? 1u : 0u;

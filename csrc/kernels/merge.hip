@@ -1,5 +1,5 @@
 // Root merge of the gather strategy: P sorted runs of combined (key, count) records -> the
-// globally sorted (key, val, count) output, in two short kernels.
+// globally sorted (key, count) output, in two short kernels.
 //
 // The reference has no merge at all: its reducer expects one pre-sorted /tmp/out.txt
 // (main.cu:437-465, bug B7), and the cross-node transfer that would feed it is missing
@@ -13,9 +13,10 @@
 //                its parts by shuffles.  Records are scattered to their merged slots
 //                (duplicates with count 0).
 //   merge_emit   decoupled look-back scan over the merged slots of (#first copies, count
-//                sum): the first copies are compacted into the output with val = the
-//                exclusive prefix of the counts (the reference's val: start index of the
-//                key's run in the globally sorted token array, main.cu:161-208).
+//                sum): the first copies are compacted into the output (the reference's
+//                val, the exclusive prefix of the counts -- start index of the key's run
+//                in the globally sorted token array, main.cu:161-208 -- is rebuilt on the
+//                host) and the token total comes from the scan.
 //
 // Runs are at most 64 (one per rank); the output goes straight into host-mapped memory.
 // The search is latency bound (one dependent load per step): a thread per record searching
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
   __shared__ u64 s_prefix;
   __shared__ RunTable t;
   // the tile's output records, staged so that the (host-mapped) writes are full lines
-  __shared__ __attribute__((aligned(16))) u64 s_out[kEmitTile * 6];
+  __shared__ __attribute__((aligned(16))) u64 s_out[kEmitTile * kOutWords];
   // a ticket, not blockIdx: a tile only waits on tiles already running (see
   // dict_ordered_kernel: kernels of processes sharing a GPU could otherwise deadlock)
   const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
@@ -245,28 +246,24 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_kernel(
   const u64 excl = dev::block_exclusive_scan<u64, kMergeBlock>(agg, s_scan, &tile_sum);
   const u64 before = dev::block_lookback(status, tile, tile_sum, &s_prefix);
   u32 li = (u32)(excl >> kEmitCountBits);  // index inside the tile's output slice
-  u64 val = (before + excl) & kEmitCountMask;
 #pragma unroll
   for (int e = 0; e < kEmitItems; ++e) {
     if (!v[e].count) continue;
-    u64* o = s_out + 6 * li;
+    u64* o = s_out + kOutWords * li;
 #pragma unroll
     for (int j = 0; j < kKeyWords; ++j) o[j] = v[e].w[j];
-    o[4] = val;
-    o[5] = v[e].count;
+    o[4] = v[e].count;
     ++li;
-    val += v[e].count;
   }
   __syncthreads();
   const u32 m = (u32)(tile_sum >> kEmitCountBits);
   const u64 base = before >> kEmitCountBits;
-  // consecutive lanes, consecutive 16-B chunks of out[base .. base + m), at most
+  // consecutive lanes, consecutive 8-B words of out[base .. base + m), at most
   // out_limit records in all (the exchange's fixed gather slot: the count still says how
   // many there were, and the report flags the overflow)
   const u32 mw = base >= out_limit ? 0u : (u32)min((u64)m, out_limit - base);
-  const uint4* src = reinterpret_cast<const uint4*>(s_out);
-  uint4* dst = reinterpret_cast<uint4*>(out + base);
-  for (u32 q = threadIdx.x; q < 3 * mw; q += kMergeBlock) dst[q] = src[q];
+  u64* dst = reinterpret_cast<u64*>(out + base);
+  for (u32 q = threadIdx.x; q < kOutWords * mw; q += kMergeBlock) dst[q] = s_out[q];
   if (tile == ntiles - 1 && threadIdx.x == 0) {
     const u64 all = before + tile_sum;
     const u32 u = (u32)(all >> kEmitCountBits);

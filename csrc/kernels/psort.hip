@@ -401,15 +401,14 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
     const u64 pfx = dev::block_lookback(ra.status, p, U, &s_prefix);  // syncs (s_hpos too)
     u64* o = reinterpret_cast<u64*>(ra.out + pfx);
     const u32 lim = pfx >= ra.out_cap ? 0u : (u32)min<u64>(U, ra.out_cap - pfx);
-    for (u32 q = (u32)t; q < 6u * lim; q += kPsBlock) {
-      const u32 h = q / 6, f = q - 6 * h;
+    for (u32 q = (u32)t; q < kOutWords * lim; q += kPsBlock) {  // 40-B {key, count}
+      const u32 h = q / kOutWords, f = q - kOutWords * h;
       const u32 i = s_hpos[h];
       const u32 li = s_perm[cur][i];
       u64 v;
       if (f == 0) v = s_w0[li];
       else if (f == 1) v = s_w1[li];
       else if (f < 4) v = word23(li, (int)f);
-      else if (f == 4) v = (u64)base + i;
       else v = (u64)((h + 1 < U ? s_hpos[h + 1] : m) - i);
       o[q] = v;
     }

@@ -259,14 +259,12 @@ __global__ __launch_bounds__(kReduceBlock) void reduce_fused_kernel(
   if (total) {
     u64* o = reinterpret_cast<u64*>(out + pfx);
     const u32 lim = pfx >= out_cap ? 0u : (u32)min<u64>(total, (u64)out_cap - pfx);
-    for (u32 q = threadIdx.x; q < 6u * lim; q += kReduceBlock) {
-      const u32 h = q / 6, f = q - 6 * h;
+    for (u32 q = threadIdx.x; q < kOutWords * lim; q += kReduceBlock) {  // {key, count}
+      const u32 h = q / kOutWords, f = q - kOutWords * h;
       const u32 li = s_hpos[h];
       u64 v;
       if (f < (u32)kKeyWords) {
         v = s_keys[f][li + 1];
-      } else if (f == 4) {
-        v = (u64)base + li;
       } else {
         const u32 end = h + 1 < total ? base + s_hpos[h + 1] : s_end;
         v = (u64)end - (base + li);
@@ -319,7 +317,8 @@ __global__ __launch_bounds__(256) void add_offset_kernel(u64* __restrict__ head_
 }
 
 // Output records, written as consecutive 8-B words by consecutive lanes (word q = record
-// q / 6, field q % 6): full cache lines, which matters when `out` is host-mapped memory
+// q / 5, field q % 5: key words, count; the heads' vals only served the adjacent
+// difference): full cache lines, which matters when `out` is host-mapped memory
 // (zero-copy results: every partial line would be its own PCIe write).  `ctr_out`
 // (optional, host-mapped) receives the final counters; the host waits for the kernel.
 __global__ __launch_bounds__(256) void pack_output_kernel(ConstKeysSoA head_keys,
@@ -331,10 +330,10 @@ __global__ __launch_bounds__(256) void pack_output_kernel(ConstKeysSoA head_keys
   const u32 u = ctr->num_unique;
   if (ctr_out && blockIdx.x == 0 && threadIdx.x == 0) *ctr_out = *ctr;
   u64* o = reinterpret_cast<u64*>(out);
-  const u64 words = 6ull * u;
+  const u64 words = (u64)kOutWords * u;
   for (u64 q = blockIdx.x * 256ull + threadIdx.x; q < words; q += gridDim.x * 256ull) {
-    const u32 j = (u32)(q / 6), f = (u32)(q - 6ull * j);
-    o[q] = f < (u32)kKeyWords ? head_keys.w[f][j] : f == 4 ? head_val[j] : head_count[j];
+    const u32 j = (u32)(q / kOutWords), f = (u32)(q - (u64)kOutWords * j);
+    o[q] = f < (u32)kKeyWords ? head_keys.w[f][j] : head_count[j];
   }
 }
 

@@ -16,12 +16,14 @@ __global__ void signal_host_kernel(u32* __restrict__ word, u32 value) {
     __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Device buffer -> host-mapped buffer (its device alias), 16 B per lane, grid-stride.  The
-// fallback paths' results reach the mapped output this way: a hipMemcpyAsync into the
-// fine-grained host buffer measured 7.3 ms for 9.7 MB on a cold engine (host-staged), a
-// kernel's posted writes run at the link rate like the ordered kernel's own record stores.
-__global__ __launch_bounds__(256) void copy_to_mapped_kernel(uint4* __restrict__ dst,
-                                                             const uint4* __restrict__ src, u64 n) {
+// Device buffer -> host-mapped buffer (its device alias), 8 B per lane (40-B records:
+// sizes are multiples of 8), consecutive lanes on consecutive words (whole lines),
+// grid-stride.  The fallback paths' results reach the mapped output this way: a
+// hipMemcpyAsync into the fine-grained host buffer measured 7.3 ms for 9.7 MB on a cold
+// engine (host-staged), a kernel's posted writes run at the link rate like the ordered
+// kernel's own record stores.
+__global__ __launch_bounds__(256) void copy_to_mapped_kernel(u64* __restrict__ dst,
+                                                             const u64* __restrict__ src, u64 n) {
   for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
     dst[i] = src[i];
 }
@@ -29,14 +31,14 @@ __global__ __launch_bounds__(256) void copy_to_mapped_kernel(uint4* __restrict__
 }  // namespace
 
 void launch_copy_to_mapped(void* dst_mapped_dev, const void* src, u64 bytes, hipStream_t s) {
-  LOCUST_CHECK_ARG(bytes % 16 == 0 && reinterpret_cast<uintptr_t>(dst_mapped_dev) % 16 == 0 &&
-                       reinterpret_cast<uintptr_t>(src) % 16 == 0,
-                   "copy_to_mapped: 16-byte aligned buffers and sizes");
-  const u64 n = bytes / 16;
+  LOCUST_CHECK_ARG(bytes % 8 == 0 && reinterpret_cast<uintptr_t>(dst_mapped_dev) % 8 == 0 &&
+                       reinterpret_cast<uintptr_t>(src) % 8 == 0,
+                   "copy_to_mapped: 8-byte aligned buffers and sizes");
+  const u64 n = bytes / 8;
   if (!n) return;
-  const u64 blocks = std::min<u64>(div_up(n, 256), 1024);
+  const u64 blocks = std::min<u64>(div_up(n, 256), 2048);
   copy_to_mapped_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(
-      reinterpret_cast<uint4*>(dst_mapped_dev), reinterpret_cast<const uint4*>(src), n);
+      reinterpret_cast<u64*>(dst_mapped_dev), reinterpret_cast<const u64*>(src), n);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

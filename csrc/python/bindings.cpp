@@ -27,8 +27,9 @@ struct PyResult {
   WordCountResult r;
   py::list entries() const {
     py::list out;
+    EntryVals vals(r);
     for (const auto& e : r.entries)
-      out.append(py::make_tuple(py::bytes(key_to_string(e.key)), e.val, e.count));
+      out.append(py::make_tuple(py::bytes(key_to_string(e.key)), vals.next(e), e.count));
     return out;
   }
   py::dict times() const {
@@ -52,7 +53,7 @@ struct PyResult {
   }
   py::bytes format(bool cpu_format) const {
     std::string s;
-    (cpu_format ? format_cpu_output : format_gpu_output)(r.entries, &s);
+    (cpu_format ? format_cpu_output : format_gpu_output)(r, &s);
     return py::bytes(s);
   }
 };
@@ -418,7 +419,7 @@ PYBIND11_MODULE(_locust, m) {
       .def("entries", &PyResult::entries)
       .def("times", &PyResult::times)
       .def("format", &PyResult::format, py::arg("cpu_format") = false)
-      .def("write_kiv", [](const PyResult& p, const std::string& path) { write_kiv_results(path, p.r.entries); },
+      .def("write_kiv", [](const PyResult& p, const std::string& path) { write_kiv_results(path, p.r); },
            py::arg("path"), "The results as the reference's 40-B KeyIntValuePair records.")
       .def_property_readonly("num_lines", [](const PyResult& p) { return p.r.num_lines; })
       .def_property_readonly("num_tokens", [](const PyResult& p) { return p.r.num_tokens; })
@@ -652,7 +653,6 @@ PYBIND11_MODULE(_locust, m) {
     for (size_t i = 0; i < keys.size(); ++i) {
       e[i].key = to_key(keys[i].first);
       e[i].count = keys[i].second;
-      e[i].val = 0;
     }
     PartMapTables t;
     const u64 pred = part_map_from_entries(e.data(), e.size(), &t, max_distinct);

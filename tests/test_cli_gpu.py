@@ -157,5 +157,5 @@ def test_multi_rank_cli_first_job_on_device(tmp_path, cli, gpus):
     assert rec["strategy"] == "shuffle" and len(rec["ranks"]) == gpus
     for rk in rec["ranks"]:
         assert rk["device_exchange"] is True and 1 <= rk["host_syncs"] <= 2, rk
-        assert rk["output_bytes"] == rk["range_unique"] * 48
+        assert rk["output_bytes"] == rk["range_unique"] * 40
     assert sum(rk["range_unique"] for rk in rec["ranks"]) == want.num_unique

@@ -40,7 +40,7 @@ def test_device_exchange_across_processes(tmp_path, world):
         assert r["comm"] == "tcpdev"
         assert [i["device_exchange"] for i in r["infos"]] == [True] * 4
         assert [i["host_syncs"] for i in r["infos"]][:2] == [2, 1]
-        assert all(i["output_bytes"] == i["range_unique"] * 48 for i in r["infos"])
+        assert all(i["output_bytes"] == i["range_unique"] * 40 for i in r["infos"])
 
 
 @pytest.mark.gpu
