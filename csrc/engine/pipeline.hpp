@@ -104,6 +104,7 @@ struct DevicePipeline {
   // the link closer to a single DMA's rate -- synth1m with 4 / 8 / 12 / 16 MiB targets:
   // 1.24 / 1.21 / 1.185 / 1.19 ms), at most partial_slots_cap of them.
   static constexpr u64 kPieceBytes = 4ull << 20;
+  static constexpr u64 kDevPageBytes = 2ull << 20;  // device allocations: whole 2 MiB pages
   static u64 piece_target() {
     static const u64 b = [] {
       const char* e = std::getenv("LOCUST_PIECE_MB");
@@ -376,7 +377,7 @@ struct DevicePipeline {
     }
     for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
     sz.add<char>(dict_zero_bytes);
-    arena.size = sz.bytes + 4096;
+    arena.size = align_up(sz.bytes + 4096, kDevPageBytes);
     LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
 
     d_text = arena.take<char>(cap_bytes + 64);
@@ -1872,7 +1873,9 @@ struct DevicePipeline {
         LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_copied[b], hipEventDisableTiming));
         LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_consumed[b], hipEventDisableTiming));
       }
-      LOCUST_HIP_CHECK(hipMalloc(&d_text_alt, cap_bytes + 64));
+      // a whole number of 2 MiB pages (an odd size left the next engine's chunk copies at
+      // ~30 GB/s instead of ~57 in tools/s10g_probe.py; see docs/PERFORMANCE.md)
+      LOCUST_HIP_CHECK(hipMalloc(&d_text_alt, align_up(cap_bytes + 64, kDevPageBytes)));
       LOCUST_HIP_CHECK(hipMalloc(&d_dctr, sizeof(MapCounters)));
     }
     if (staging && !h_stage[0])

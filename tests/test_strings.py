@@ -95,3 +95,26 @@ def test_device_string_library_matches_host():
         assert ntok == len(py_strtok(s, DEFAULT_DELIMS)) == len(starts)
         assert offs == starts[:8]
         assert it == str(ints[i]) and it == itoa(ints[i], 10)
+
+
+def test_ops_tokenize_matches_oracle():
+    """locust_amd.ops.strings.tokenize (host build of d_strtok_r) against the Python strtok."""
+    from locust_amd.ops import strings as S
+
+    rng = random.Random(11)
+    alphabet = b"abcXYZ019 ,.-;:'()\"\t"
+    for _ in range(500):
+        s = bytes(rng.choice(alphabet) for _ in range(rng.randint(0, 80)))
+        assert S.tokenize(s) == py_strtok(s, DEFAULT_DELIMS)
+    assert S.DEFAULT_DELIMS.encode() == DEFAULT_DELIMS
+
+
+@pytest.mark.gpu
+def test_ops_device_check_reports_no_mismatch():
+    """The cross-check helper finds the device and host builds in agreement."""
+    from locust_amd.ops import strings as S
+
+    rng = random.Random(12)
+    cases = [b"", b"a b", b"x" * 40] + [bytes(rng.randrange(1, 256) for _ in range(rng.randint(0, 60)))
+                                         for _ in range(500)]
+    assert S.device_check(cases, [rng.randint(-2**31, 2**31 - 1) for _ in cases]) == []
