@@ -1,0 +1,124 @@
+// Process-wide device block cache; see locust/devcache.hpp.
+#include "locust/devcache.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "locust/common.hpp"
+#include "locust/hip_check.hpp"
+
+namespace locust {
+namespace {
+
+constexpr size_t kPage = 2ull << 20;
+
+struct Block {
+  int device;
+  void* p;
+  size_t bytes;
+};
+
+struct Cache {
+  std::mutex mu;
+  std::vector<Block> free;
+  size_t held = 0;
+  const bool on = [] {
+    const char* e = std::getenv("LOCUST_DEV_CACHE");
+    return !(e && e[0] == '0');
+  }();
+  const size_t cap = [] {
+    const char* e = std::getenv("LOCUST_DEV_CACHE_GB");
+    const double gb = e ? std::atof(e) : 64.0;
+    return (size_t)(gb > 0 ? gb * 1e9 : 0);
+  }();
+};
+
+Cache& cache() {
+  static Cache* c = new Cache();  // never destroyed: blocks may be freed at exit
+  return *c;
+}
+
+int current_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
+
+}  // namespace
+
+void* dev_block_alloc(size_t bytes, size_t* got) {
+  const size_t want = (bytes + kPage - 1) / kPage * kPage;
+  const int dev = current_device();
+  Cache& c = cache();
+  if (c.on) {
+    std::lock_guard<std::mutex> lk(c.mu);
+    size_t best = c.free.size();
+    for (size_t i = 0; i < c.free.size(); ++i) {
+      const Block& b = c.free[i];
+      if (b.device == dev && b.bytes >= want && b.bytes <= want + want / 4 &&
+          (best == c.free.size() || b.bytes < c.free[best].bytes))
+        best = i;
+    }
+    if (best < c.free.size()) {
+      const Block b = c.free[best];
+      c.free.erase(c.free.begin() + (long)best);
+      c.held -= b.bytes;
+      if (got) *got = b.bytes;
+      LOCUST_LOG_DEBUG("device block %zu MB reused (device %d)", b.bytes >> 20, dev);
+      return b.p;
+    }
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    dev_block_trim();
+    LOCUST_HIP_CHECK(hipMalloc(&p, want));
+  }
+  if (got) *got = want;
+  return p;
+}
+
+void dev_block_free(void* p, size_t bytes) {
+  if (!p) return;
+  Cache& c = cache();
+  const int dev = current_device();
+  if (c.on) {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.held + bytes <= c.cap) {
+      c.free.push_back(Block{dev, p, bytes});
+      c.held += bytes;
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+
+void dev_block_trim() {
+  Cache& c = cache();
+  std::vector<Block> blocks;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    blocks.swap(c.free);
+    c.held = 0;
+  }
+  int cur = current_device();
+  for (const Block& b : blocks) {
+    (void)hipSetDevice(b.device);
+    (void)hipFree(b.p);
+  }
+  (void)hipSetDevice(cur);
+}
+
+size_t dev_block_cached(size_t* bytes) {
+  Cache& c = cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (bytes) *bytes = c.held;
+  return c.free.size();
+}
+
+}  // namespace locust

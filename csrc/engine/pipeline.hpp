@@ -23,6 +23,7 @@
 #include <string>
 #include <vector>
 
+#include "locust/devcache.hpp"
 #include "locust/dist.hpp"
 #include "locust/engine.hpp"
 #include "locust/hip_check.hpp"
@@ -68,6 +69,7 @@ struct DevicePipeline {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   Arena arena;
+  size_t arena_block = 0;  // the arena's block size (devcache)
 
   char* d_text = nullptr;
   u64* d_nl = nullptr;
@@ -162,6 +164,7 @@ struct DevicePipeline {
 
   // streaming (inputs larger than one chunk), allocated on first use
   char* d_text_alt = nullptr;        // second device text buffer (double buffering)
+  size_t d_text_alt_block = 0;       // its block size (devcache)
   char* h_stage[2] = {nullptr, nullptr};  // pinned staging halves for pageable inputs
   // a TextSource's pinned read ring: kRingPieces pieces of ring_piece bytes, whatever the
   // chunk size (host memory of a streamed file stays kRingPieces x ring_piece)
@@ -378,7 +381,11 @@ struct DevicePipeline {
     for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
     sz.add<char>(dict_zero_bytes);
     arena.size = align_up(sz.bytes + 4096, kDevPageBytes);
-    LOCUST_HIP_CHECK(hipMalloc(&arena.base, arena.size));
+    {
+      size_t got = 0;  // the process-wide block cache (locust/devcache.hpp)
+      arena.base = static_cast<char*>(dev_block_alloc(arena.size, &got));
+      arena_block = got;
+    }
 
     d_text = arena.take<char>(cap_bytes + 64);
     d_nl = arena.take<u64>(compat ? cap_lines + 1 : 1);
@@ -552,11 +559,11 @@ struct DevicePipeline {
     if (cstream) (void)hipStreamDestroy(cstream);
     if (cstream2) (void)hipStreamDestroy(cstream2);
 
-    if (d_text_alt) (void)hipFree(d_text_alt);
+    if (d_text_alt) dev_block_free(d_text_alt, d_text_alt_block);
     if (d_dctr) (void)hipFree(d_dctr);
     if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
     if (stream) (void)hipStreamDestroy(stream);
-    if (arena.base) (void)hipFree(arena.base);
+    if (arena.base) dev_block_free(arena.base, arena_block);  // every stream synchronised above
     for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_keys,
                     (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped, (void*)h_pmap,
                     (void*)h_pw, (void*)h_done})
@@ -1873,9 +1880,9 @@ struct DevicePipeline {
         LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_copied[b], hipEventDisableTiming));
         LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_consumed[b], hipEventDisableTiming));
       }
-      // a whole number of 2 MiB pages (an odd size left the next engine's chunk copies at
-      // ~30 GB/s instead of ~57 in tools/s10g_probe.py; see docs/PERFORMANCE.md)
-      LOCUST_HIP_CHECK(hipMalloc(&d_text_alt, align_up(cap_bytes + 64, kDevPageBytes)));
+      size_t got = 0;  // the process-wide block cache, like the arena
+      d_text_alt = static_cast<char*>(dev_block_alloc(cap_bytes + 64, &got));
+      d_text_alt_block = got;
       LOCUST_HIP_CHECK(hipMalloc(&d_dctr, sizeof(MapCounters)));
     }
     if (staging && !h_stage[0])

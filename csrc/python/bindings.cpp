@@ -9,6 +9,7 @@
 #include <cstring>
 #include <string>
 
+#include "locust/devcache.hpp"
 #include "locust/dist.hpp"
 #include "locust/dstring.hpp"
 #include "locust/engine.hpp"
@@ -612,6 +613,15 @@ PYBIND11_MODULE(_locust, m) {
       })
       .def("unlink", &ShmSegment::unlink)
       .def("close", &ShmSegment::close);
+  m.def("dev_cache_stats", [] {  // the process-wide device block cache (devcache.hpp)
+    size_t bytes = 0;
+    const size_t n = dev_block_cached(&bytes);
+    py::dict d;
+    d["blocks"] = n;
+    d["bytes"] = bytes;
+    return d;
+  });
+  m.def("dev_cache_trim", &dev_block_trim);
   m.def("shm_segment_name", &shm_segment_name);
   m.def("shm_segment_bytes", &shm_segment_bytes);
   m.def("next_segment_gen", &next_segment_gen);
