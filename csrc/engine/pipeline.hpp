@@ -178,6 +178,34 @@ struct DevicePipeline {
   // idle between commands (measured 43 GB/s for 4 MiB pieces on one stream, 52 GB/s
   // alternating over two -- the single-copy rate)
   hipStream_t cstream2 = nullptr;
+  hipStream_t cstream3 = nullptr;  // LOCUST_COPY_STREAMS=3 (A/B)
+  // Piece copies: issued at the very start of the job's enqueue, ahead of the compute
+  // stream's resets (their fills delayed the first copy by ~20 us, profiles/r3_s4/), and
+  // spread over this many copy streams (LOCUST_COPY_FIRST=0 / LOCUST_COPY_STREAMS: A/B).
+  const bool copy_first = [] {
+    const char* e = std::getenv("LOCUST_COPY_FIRST");
+    return !(e && e[0] == '0');
+  }();
+  const u32 copy_streams = [] {
+    const char* e = std::getenv("LOCUST_COPY_STREAMS");
+    const int n = e ? std::atoi(e) : 2;
+    return (u32)std::clamp(n, 1, 3);
+  }();
+  bool pieces_issued = false;  // this job's piece copies are already on the copy streams
+  hipStream_t piece_stream(size_t k) const {
+    const u32 i = (u32)(k % copy_streams);
+    return i == 0 ? cstream : i == 1 ? cstream2 : cstream3;
+  }
+  void issue_piece_copies(const char* src) {
+    ensure_piece_events(pieces.size());
+    for (size_t k = 0; k < pieces.size(); ++k) {
+      const u64 off = pieces[k].first, len = pieces[k].second;
+      hipStream_t cs = piece_stream(k);
+      LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
+      LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
+    }
+    pieces_issued = true;
+  }
   hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
   MapCounters* d_dctr = nullptr;     // dictionary counters that persist across chunks
   MapCounters* h_chunk_ctr = nullptr;  // pinned per-chunk map counter snapshots
@@ -542,6 +570,7 @@ struct DevicePipeline {
     if (d_map_trace) (void)hipFree(d_map_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     if (cstream2) (void)hipStreamSynchronize(cstream2);
+    if (cstream3) (void)hipStreamSynchronize(cstream3);
 
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -558,6 +587,7 @@ struct DevicePipeline {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (cstream) (void)hipStreamDestroy(cstream);
     if (cstream2) (void)hipStreamDestroy(cstream2);
+    if (cstream3) (void)hipStreamDestroy(cstream3);
 
     if (d_text_alt) dev_block_free(d_text_alt, d_text_alt_block);
     if (d_dctr) (void)hipFree(d_dctr);
@@ -761,6 +791,8 @@ struct DevicePipeline {
   void ensure_piece_events(size_t n) {
     if (!cstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     if (!cstream2) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream2, hipStreamNonBlocking));
+    if (copy_streams > 2 && !cstream3)
+      LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream3, hipStreamNonBlocking));
     if (!ev_fork) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     while (ev_piece.size() < n) {
       hipEvent_t e;
@@ -771,7 +803,13 @@ struct DevicePipeline {
   // Device half (capturable): the DMA if any, then the per-run reset of counters and
   // look-back scratch.
   void enqueue_upload_device(const TextInput& in) {
-    if (!pieces.empty()) {  // the pieces travel with the map (enqueue_map)
+    if (!pieces.empty()) {
+      // the pieces' copies go out first (outside a graph capture: there they need the fork
+      // from `stream`, made in enqueue_map); their maps follow in enqueue_map
+      hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+      LOCUST_HIP_CHECK(hipStreamIsCapturing(stream, &cst));
+      if (copy_first && cst == hipStreamCaptureStatusNone)
+        issue_piece_copies(upload_mode == Upload::kDirect ? in.data : h_text);
     } else if (upload_mode == Upload::kDirect) {
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
       LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
@@ -954,6 +992,7 @@ struct DevicePipeline {
         LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream2, ev_fork, 0));
+        if (cstream3) LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream3, ev_fork, 0));
       }
       // a combining large pass (run() / the shard engine take the two-kernel ordered build
       // next): aggregate each piece right after its map, into slot k -- on the same stream:
@@ -970,11 +1009,15 @@ struct DevicePipeline {
       // address is two blit kernels there, ~15 us in front of the last piece's event)
       LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
       u64 tile_off = 0;
+      const bool issued = pieces_issued;
+      pieces_issued = false;
       for (size_t k = 0; k < pieces.size(); ++k) {
         const u64 off = pieces[k].first, len = pieces[k].second;
-        hipStream_t cs = (k & 1) ? cstream2 : cstream;
-        LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
-        LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
+        if (!issued) {
+          hipStream_t cs = piece_stream(k);
+          LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
+          LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
+        }
         LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_piece[k], 0));
         if (k == 0 && devplan_used) enqueue_devplan(src, len, dm);
         launch_map_fast(d_text + off, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, d_parts,
