@@ -39,8 +39,11 @@ LOCUST_HD inline u32 part_of_w0(const u64* lo, u64 w0) {
   return p;
 }
 
-// partition = first key byte
+// The starting map (no key seen yet): letters split on their second byte, digits and
+// UTF-8 lead bytes one partition each (partmap.cpp).
 void part_map_default(PartMapTables* t);
+// partition = first key byte (the round-2 default; A/B and tests)
+void part_map_default_first_byte(PartMapTables* t);
 
 // Balanced map from a job's sorted (key, count) output: greedy key ranges of ~total/256
 // work (count + kPartDistinctWeight per distinct key, the ordered kernel's part_w measure)

@@ -51,6 +51,25 @@ def test_large_vocabulary_respects_distinct_cap():
 
 
 def test_default_map_for_empty_input():
+    """The starting map: ascending ranges, letters split on their second byte, digits and
+    UTF-8 lead bytes one partition each, the empty tail past the last range."""
     m = lc._C.part_map_build([])
-    assert m["lo"][0x74] == 0x74 << 56 and m["predicted_max"] == 0
-    assert lc._C.part_of_key(m["lo"], b"the") == 0x74
+    lo = m["lo"]
+    assert m["predicted_max"] == 0 and lo[0] == 0 and len(lo) == 257
+    used = [x for x in lo[:256] if x != (1 << 64) - 1]
+    assert used == sorted(used) and len(set(used)) == len(used) == 248
+    part = lambda k: lc._C.part_of_key(lo, k)  # noqa: E731
+    # lowercase: four ranges per first letter, cut at the second letters g, n, t
+    assert len({part(b"t" + bytes([c])) for c in range(ord("a"), ord("z") + 1)}) == 4
+    assert part(b"the") == part(b"than")
+    assert part(b"tea") < part(b"the") < part(b"to") < part(b"tu")
+    assert part(b"ta") < part(b"tz") < part(b"ua")
+    # uppercase: ALL-CAPS / [a-m] / [n-z] second bytes
+    assert part(b"HAMLET") != part(b"Hamlet") != part(b"Horatio")
+    # a UTF-8 lead byte of its own, digits one each
+    assert part("\u4e2d".encode()) != part("\u6587".encode())
+    assert part(b"1999") != part(b"2000")
+    # ordered: the partition index is monotone in the key
+    keys = sorted([b"", b"0", b"9z", b"A", b"Zz", b"a", b"azz", b"b", b"zzz", "\u00e9".encode(),
+                   "\u4e2d".encode(), b"\xff"])
+    assert [part(k) for k in keys] == sorted(part(k) for k in keys)
