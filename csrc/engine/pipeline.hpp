@@ -143,7 +143,25 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_VPLAN");
     return !e || e[0] != '0';
   }();
-  bool plan_small() const { return vplan && pm_retunes == 0; }
+  // The plan pays for itself only on larger small passes: with the starting map splitting
+  // the letters (part_map_default), whole Hamlet (191 KB) ran 0.0436 ms without it and
+  // 0.0455 with it (profiles/r3_s4/default_map/split_ab.txt).  LOCUST_VPLAN_MIN_KB: the
+  // smallest pass that plans (default 256 KiB).
+  const u64 vplan_min_bytes = [] {
+    const char* e = std::getenv("LOCUST_VPLAN_MIN_KB");
+    return (u64)(e ? std::max(0, std::atoi(e)) : 256) << 10;
+  }();
+  bool plan_pass = false;  // this pass's map writes occupancy and its ordered kernel plans
+  bool plan_small() const { return plan_pass; }
+  void decide_plan(u64 pass_bytes) {
+    plan_pass = vplan && pm_retunes == 0 && pass_bytes >= vplan_min_bytes;
+  }
+  // LOCUST_SPLIT_MIN (read at construction): tokens per extra sibling workgroup of a
+  // planned partition (0: the kernel's default, kSplitMinTokens)
+  const u32 split_min = [] {
+    const char* e = std::getenv("LOCUST_SPLIT_MIN");
+    return e ? (u32)std::max(0, std::atoi(e)) : 0u;
+  }();
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {
@@ -964,6 +982,7 @@ struct DevicePipeline {
   }
 
   void enqueue_map(const TextInput& in) {
+    plan_pass = false;  // decided per pass (decide_plan) where the map can write occupancy
     parts_ready = cfg.map_path == MapPath::kFast;
     devplan_used = false;
     partial_nslots = 0;
@@ -1049,6 +1068,7 @@ struct DevicePipeline {
                                                                                          : h_text,
                         in.bytes, make_delim_mask(cfg.delimiters.c_str()), map_text);
       }
+      decide_plan(in.bytes);
       launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                       cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                       stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
@@ -1400,6 +1420,7 @@ struct DevicePipeline {
     ex.pm = part_map();
     ex.part_w = d_pw;
     if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
+    ex.split_min = split_min;
     if (self_clean) set_self_clean(ex);
     if (self_clean && done_pending) {  // the kernel itself tells the host it is done
       ex.host_done = d_done;

@@ -324,6 +324,7 @@ struct OrderedExtra {
   // at most kPartBlock tiles; larger ones keep one workgroup per partition.)
   const u32* part_occ = nullptr;
   u32 variant = 0;              // A/B switches for kernel experiments (LOCUST_ORD_VARIANT)
+  u32 split_min = 0;            // planned workgroups: tokens per extra sibling (0: default)
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};
   // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x

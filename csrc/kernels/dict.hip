@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     u32 K = 0;
     if (occupied) {
       const u32 extra = T ? (u32)((u64)tp * (u32)(kDictParts - E) / T) : 0u;
-      K = 1u + min(extra, tp / kSplitMinTokens);
+      K = 1u + min(extra, tp / (ex.split_min ? ex.split_min : kSplitMinTokens));
     }
     u32 kinc = 0;
     if (threadIdx.x < kDictParts) {

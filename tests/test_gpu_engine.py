@@ -258,3 +258,24 @@ def test_zero_copy_results_stay_valid(hamlet, graph):
     kept.clear()
     r = eng.run(hamlet)
     assert r.entries() == oracle.wordcount(hamlet)[0]
+
+
+@pytest.mark.parametrize("default_map", ["letters", "byte"])
+@pytest.mark.parametrize("plan_min_kb", ["0", "256"])
+def test_starting_map_and_in_job_plan_match_oracle(hamlet, monkeypatch, default_map, plan_min_kb):
+    """An untuned engine (LOCUST_PART_TUNE=0) on the starting partition map -- letters split
+    on the second byte, or the first-byte map -- with the in-job plan forced on (every pass
+    plans; the first-byte map then splits the hot letters over sibling workgroups) or left
+    to its size threshold: every job matches the oracle."""
+    monkeypatch.setenv("LOCUST_PART_TUNE", "0")
+    monkeypatch.setenv("LOCUST_VPLAN_MIN_KB", plan_min_kb)
+    if default_map == "byte":
+        monkeypatch.setenv("LOCUST_PART_DEFAULT", "byte")
+    for start, end in [(-1, -1), (0, 700), (1000, 3000)]:
+        text = oracle.window(hamlet, start, end)
+        ent, ntok, _ = oracle.wordcount(text)
+        eng = lc._C.GpuEngine(lc.make_config("gpu", reduce_path="lds", check=True), len(text),
+                              text.count(b"\n") + 1)
+        for _ in range(3):
+            r = eng.run(text)
+            assert r.num_tokens == ntok and r.entries() == ent
