@@ -143,13 +143,15 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_VPLAN");
     return !e || e[0] != '0';
   }();
-  // The plan pays for itself only on larger small passes: with the starting map splitting
-  // the letters (part_map_default), whole Hamlet (191 KB) ran 0.0436 ms without it and
-  // 0.0455 with it (profiles/r3_s4/default_map/split_ab.txt).  LOCUST_VPLAN_MIN_KB: the
-  // smallest pass that plans (default 256 KiB).
+  // LOCUST_VPLAN_MIN_KB: the smallest pass that plans (default 0: every untuned small
+  // pass).  Whole Hamlet with the letters map ran 0.0436 ms unplanned vs 0.0455 planned,
+  // but a size threshold cannot tell Hamlet from a pass of the same size whose keys crowd
+  // one partition (30,000 'w0...' keys: the unplanned job overflowed its LDS table and
+  // redid the exchange) -- the plan's split is what keeps such a first job on the LDS
+  // path (profiles/r3_s4/default_map/split_ab.txt).
   const u64 vplan_min_bytes = [] {
     const char* e = std::getenv("LOCUST_VPLAN_MIN_KB");
-    return (u64)(e ? std::max(0, std::atoi(e)) : 256) << 10;
+    return (u64)(e ? std::max(0, std::atoi(e)) : 0) << 10;
   }();
   bool plan_pass = false;  // this pass's map writes occupancy and its ordered kernel plans
   bool plan_small() const { return plan_pass; }
