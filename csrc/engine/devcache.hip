@@ -86,7 +86,14 @@ void* dev_block_alloc(size_t bytes, size_t* got) {
 void dev_block_free(void* p, size_t bytes) {
   if (!p) return;
   Cache& c = cache();
-  const int dev = current_device();
+  // the block's own device (an engine may be destroyed on another thread or device than
+  // the one that made it: clique ranks)
+  int dev = current_device();
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) == hipSuccess)
+    dev = a.device;
+  else
+    (void)hipGetLastError();
   if (c.on) {
     std::lock_guard<std::mutex> lk(c.mu);
     if (c.held + bytes <= c.cap) {
@@ -95,7 +102,10 @@ void dev_block_free(void* p, size_t bytes) {
       return;
     }
   }
+  const int cur = current_device();
+  (void)hipSetDevice(dev);
   (void)hipFree(p);
+  (void)hipSetDevice(cur);
 }
 
 void dev_block_trim() {
