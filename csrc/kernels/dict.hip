@@ -274,10 +274,13 @@ constexpr int kGatherBatch = 4;
 // [rlo, rhi) (rlast: no upper bound): only keys whose first word lies in the range are
 // inserted (a virtual partition's share of its map partition; the default takes all).
 template <int kGatherBatch = kGatherBatch>
+// eager_w1: load key word 1 of every token together with word 0 (one round trip for
+// the keys of 8-15 bytes, whose word 1 was a second, dependent load); word 1 of a
+// shorter key is not written by the map, so it is masked, never used.
 __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* counts,
                                               const u32* s_list, u32 lim, u32 n_cap,
                                               LdsSlot* s_tab, u64 rlo = 0, u64 rhi = ~0ull,
-                                              bool rlast = true) {
+                                              bool rlast = true, bool eager_w1 = false) {
   bool full = false;
   for (u32 e0 = 0; e0 < lim; e0 += kGatherBatch * kPartBlock) {
     u32 idx[kGatherBatch];
@@ -292,15 +295,20 @@ __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* co
     for (int r = 0; r < kGatherBatch; ++r) {
       const bool ok = idx[r] < n_cap;
       k[r][0] = ok ? tokens.w[0][idx[r]] : 0;
+      k[r][1] = ok && eager_w1 ? tokens.w[1][idx[r]] : 0;
       c[r] = ok ? (counts ? counts[idx[r]] : 1ull) : 0;
-      k[r][1] = k[r][2] = k[r][3] = 0;
+      k[r][2] = k[r][3] = 0;
     }
 #pragma unroll
     for (int r = 0; r < kGatherBatch; ++r)  // outside the range: neither gathered nor inserted
       if (k[r][0] < rlo || (!rlast && k[r][0] >= rhi)) k[r][0] = 0;
 #pragma unroll
-    for (int r = 0; r < kGatherBatch; ++r)
-      if (k[r][0] & 0xffull) k[r][1] = tokens.w[1][idx[r]];
+    for (int r = 0; r < kGatherBatch; ++r) {
+      if (!(k[r][0] & 0xffull))
+        k[r][1] = 0;
+      else if (!eager_w1)
+        k[r][1] = tokens.w[1][idx[r]];
+    }
 #pragma unroll
     for (int r = 0; r < kGatherBatch; ++r)
       if (k[r][1] & 0xffull) {
@@ -618,6 +626,7 @@ struct TileSource {
   const u32* part_off;
   u32 ntiles;
   u32 n_cap;  // token capacity: indices past it were never written
+  bool eager_w1 = true;  // gather_insert; LOCUST_ORD_VARIANT bit 256 clears it (A/B)
   // This thread's first run (tile threadIdx.x), loaded before the kernel clears its table
   // so that the load overlaps the clear and its barrier.
   struct Pre {
@@ -659,7 +668,8 @@ struct TileSource {
       if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
       const u32 cnt = s_count;
       full |= cnt > (u32)kPartWindow;  // the host redoes the Process stage on the HBM table
-      full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab);
+      full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab, 0,
+                            ~0ull, true, eager_w1);
       if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
       __syncthreads();
       if (threadIdx.x == 0) s_count = 0;
@@ -708,7 +718,7 @@ struct TileSource {
     // a list cut short by the sample area is an overflow: the host redoes the pass
     bool full = n > lim;
     if (!(lo == hi && !last))  // else an empty range (a hot first word took it)
-      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last);
+      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last, eager_w1);
     if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // the list area is reused after the build
     return full;
@@ -1847,7 +1857,8 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace,
                          const OrderedExtra& ex) {
   if (ex.part_off && !counts) {
-    const TileSource src{tokens, ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
+    const TileSource src{tokens, ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu),
+                         !(ex.variant & 256u)};
     dict_ordered_kernel<TileSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
         src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   } else {
