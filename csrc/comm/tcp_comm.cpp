@@ -134,6 +134,32 @@ class TcpComm final : public Communicator {
     if (rank == 0 && listen_fd >= 0) listen_fd_ = listen_fd;  // owned from here on
     group_ = new_group_token();  // rank 0's is sent to every peer with the handshake
     if (world == 1) return;
+    // A throwing constructor runs no destructor: close what the handshake opened (and the
+    // inherited listener) before rethrowing, so a failed bootstrap holds no port.
+    try {
+      handshake(host, port, timeout_s);
+    } catch (...) {
+      close_all();
+      throw;
+    }
+  }
+
+  ~TcpComm() override { close_all(); }
+
+ private:
+  void close_all() {
+    for (int& fd : fds_)
+      if (fd >= 0) {
+        ::close(fd);
+        fd = -1;
+      }
+    if (listen_fd_ >= 0) {
+      ::close(listen_fd_);
+      listen_fd_ = -1;
+    }
+  }
+  void handshake(const std::string& host, int port, double timeout_s) {
+    const int rank = rank_, world = world_;
     if (rank == 0 && listen_fd_ >= 0) {
       // inherited: already bound to `port` and listening (no window for another process)
     } else if (rank == 0) {
@@ -176,19 +202,14 @@ class TcpComm final : public Communicator {
                       ":" + std::to_string(port));
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
       }
+      fds_[0] = fd;  // owned (closed by close_all on a failed handshake)
       set_timeouts(fd, timeout_s);
       send_all(fd, &rank_, sizeof(rank_), 0);
-      fds_[0] = fd;
       recv_all(fd, &group_, sizeof(group_), 0);
     }
   }
 
-  ~TcpComm() override {
-    for (int fd : fds_)
-      if (fd >= 0) ::close(fd);
-    if (listen_fd_ >= 0) ::close(listen_fd_);
-  }
-
+ public:
   int rank() const override { return rank_; }
   int size() const override { return world_; }
   const char* name() const override { return "tcp"; }

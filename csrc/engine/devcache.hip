@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -30,10 +31,23 @@ struct Cache {
     const char* e = std::getenv("LOCUST_DEV_CACHE");
     return !(e && e[0] == '0');
   }();
+  // Bytes of idle blocks kept.  The cache is per process: with several rank processes on
+  // one GPU (LOCAL_WORLD_SIZE ranks on fewer devices, the tcpdev rehearsals) one rank's
+  // idle blocks could starve another's hipMalloc, so the default shares 64 GB between the
+  // processes per device.  LOCUST_DEV_CACHE_GB overrides it for this process.
   const size_t cap = [] {
-    const char* e = std::getenv("LOCUST_DEV_CACHE_GB");
-    const double gb = e ? std::atof(e) : 64.0;
-    return (size_t)(gb > 0 ? gb * 1e9 : 0);
+    if (const char* e = std::getenv("LOCUST_DEV_CACHE_GB")) {
+      const double gb = std::atof(e);
+      return (size_t)(gb > 0 ? gb * 1e9 : 0);
+    }
+    int per_dev = 1;
+    if (const char* w = std::getenv("LOCAL_WORLD_SIZE")) {
+      int ndev = 0;
+      // device_count is safe before the runtime is initialised (no GPU context)
+      if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) ndev = 1;
+      per_dev = std::max(1, (std::atoi(w) + ndev - 1) / ndev);
+    }
+    return (size_t)(64e9 / per_dev);
   }();
 };
 

@@ -7,7 +7,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <chrono>
 #include <functional>
+#include <thread>
 
 namespace locust {
 
@@ -515,8 +517,16 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         continue;
       }
       if (H[0].out_region == kExchNoRegion && one_sync) {
-        // the root's results hold every output region: grow the output, write again
+        // the root's results hold every output region: grow the output, write again.
+        // LOCUST_FAULT=<rank>:slow_regrow delays one rank here (test hook for the race below).
+        if (fault_injected(me, "slow_regrow"))
+          std::this_thread::sleep_for(std::chrono::milliseconds(300));
         enqueue("reduce", [&] { eng.enqueue_exchange_emit((u32)P, me); });
+        // No collective follows the new generation's shm_open(O_CREAT) in this branch: a fast
+        // rank could otherwise finish and unlink the name (exch_job_done) before a slow one
+        // opens it, which would then create a separate empty segment.  Every rank has mapped
+        // the new generation once this host barrier returns.
+        comm.barrier();
         sync();
       }
       if ((int)log_level() >= (int)LogLevel::kDebug)

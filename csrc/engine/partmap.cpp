@@ -19,8 +19,8 @@ void part_map_default_first_byte(PartMapTables* t) {
 // letter far more often than with any other byte, so the letters get several partitions
 // each, cut on the second byte: lowercase four ([.., 'g'), ['g', 'n'), ['n', 't'),
 // ['t', ..)), uppercase three (ALL-CAPS words / [a-m] / [n-z] second letters); digits and
-// every UTF-8 lead byte (0xC2-0xF4) one each; the remaining byte ranges one each.  249
-// partitions; the rest stay empty.  A first-byte map left ~50 of the 256 partitions
+// every UTF-8 lead byte (0xC2-0xF4) one each; the remaining byte ranges one each.  248
+// partitions (asserted below); the rest stay empty.  A first-byte map left ~50 of the 256 partitions
 // occupied on English text, so the ordered kernel split the hot letters across sibling
 // workgroups that each scan the whole letter's tokens (whole Hamlet: ordered kernel 28.1
 // vs 22.1 us with a tuned map, profiles/r3_s4/).  Data-independent: no input is sampled.
@@ -47,6 +47,8 @@ void part_map_default(PartMapTables* t) {
   cut(0x7B, 0);    // {|}~ DEL, UTF-8 continuation bytes, C0/C1
   for (u32 b = 0xC2; b <= 0xF4; ++b) cut(b, 0);
   cut(0xF5, 0);    // bytes no UTF-8 text starts with
+  LOCUST_CHECK_ARG(lo.size() == 248 && lo.size() <= (size_t)kDictParts,
+                   "default partition map: unexpected partition count");
   for (u32 p = 0; p < (u32)kDictParts; ++p) t->lo[p] = p < lo.size() ? lo[p] : ~0ull;
   t->lo[kDictParts] = ~0ull;
 }

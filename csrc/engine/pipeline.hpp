@@ -198,24 +198,11 @@ struct DevicePipeline {
   // idle between commands (measured 43 GB/s for 4 MiB pieces on one stream, 52 GB/s
   // alternating over two -- the single-copy rate)
   hipStream_t cstream2 = nullptr;
-  hipStream_t cstream3 = nullptr;  // LOCUST_COPY_STREAMS=3 (A/B)
   // Piece copies: issued at the very start of the job's enqueue, ahead of the compute
   // stream's resets (their fills delayed the first copy by ~20 us, profiles/r3_s4/), and
-  // spread over this many copy streams (LOCUST_COPY_FIRST=0 / LOCUST_COPY_STREAMS: A/B).
-  const bool copy_first = [] {
-    const char* e = std::getenv("LOCUST_COPY_FIRST");
-    return !(e && e[0] == '0');
-  }();
-  const u32 copy_streams = [] {
-    const char* e = std::getenv("LOCUST_COPY_STREAMS");
-    const int n = e ? std::atoi(e) : 2;
-    return (u32)std::clamp(n, 1, 3);
-  }();
+  // alternated over the two copy streams (one or three measured slower, copy_ab.txt).
   bool pieces_issued = false;  // this job's piece copies are already on the copy streams
-  hipStream_t piece_stream(size_t k) const {
-    const u32 i = (u32)(k % copy_streams);
-    return i == 0 ? cstream : i == 1 ? cstream2 : cstream3;
-  }
+  hipStream_t piece_stream(size_t k) const { return (k & 1) ? cstream2 : cstream; }
   void issue_piece_copies(const char* src) {
     ensure_piece_events(pieces.size());
     for (size_t k = 0; k < pieces.size(); ++k) {
@@ -527,7 +514,7 @@ struct DevicePipeline {
     // and a second one: a job's result holds its buffer while the next job runs, so jobs
     // alternate between two -- allocated here, not inside the second job (pinning a
     // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job)
-    out_pool.push_back(std::make_shared<HostOut>(h_out_cap, out_noncoherent));
+    out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
     use_out(0);
     LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                    hipHostMallocMapped | hipHostMallocCoherent));
@@ -554,21 +541,13 @@ struct DevicePipeline {
       // streams and piece events, and the plan's scratch
       ensure_piece_events(partial_slots_cap);
       if (devplan_env) ensure_plan();
-      if (warm_streams_env()) warm_copy_streams();
+      warm_copy_streams();
     }
   }
 
   // The copy streams' first use (queue bring-up, the runtime's copy and fill kernels) in the
   // constructor, not in the first job: one piece-sized copy, a fill at an unaligned address
-  // and a short read-back on each, as a piecewise upload issues them.  LOCUST_WARM_STREAMS=0
-  // leaves them cold.
-  static bool warm_streams_env() {
-    static const bool on = [] {
-      const char* e = std::getenv("LOCUST_WARM_STREAMS");
-      return !e || e[0] != '0';
-    }();
-    return on;
-  }
+  // and a short read-back on each, as a piecewise upload issues them.
   void warm_copy_streams() {
     if (!h_text || !cstream || !cstream2) return;
     const u64 n = std::min<u64>(cap_bytes, kPieceBytes);
@@ -590,7 +569,6 @@ struct DevicePipeline {
     if (d_map_trace) (void)hipFree(d_map_trace);
     if (cstream) (void)hipStreamSynchronize(cstream);
     if (cstream2) (void)hipStreamSynchronize(cstream2);
-    if (cstream3) (void)hipStreamSynchronize(cstream3);
 
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -607,7 +585,6 @@ struct DevicePipeline {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (cstream) (void)hipStreamDestroy(cstream);
     if (cstream2) (void)hipStreamDestroy(cstream2);
-    if (cstream3) (void)hipStreamDestroy(cstream3);
 
     if (d_text_alt) dev_block_free(d_text_alt, d_text_alt_block);
     if (d_dctr) (void)hipFree(d_dctr);
@@ -632,10 +609,11 @@ struct DevicePipeline {
     OutRecord* h = nullptr;
     OutRecord* d = nullptr;
     u64 cap = 0;
-    HostOut(u64 n, bool noncoherent) : cap(std::max<u64>(n, 1)) {
+    // fine-grained: the kernels write it straight over PCIe (coarse-grained buffers
+    // measured no faster, profiles/r1_s3/out_coherence_ab.txt)
+    explicit HostOut(u64 n) : cap(std::max<u64>(n, 1)) {
       LOCUST_HIP_CHECK(hipHostMalloc(&h, cap * sizeof(OutRecord),
-                                     hipHostMallocMapped | (noncoherent ? hipHostMallocNonCoherent
-                                                                        : hipHostMallocCoherent)));
+                                     hipHostMallocMapped | hipHostMallocCoherent));
       LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
     }
     ~HostOut() {
@@ -645,12 +623,6 @@ struct DevicePipeline {
     HostOut& operator=(const HostOut&) = delete;
   };
   std::vector<std::shared_ptr<HostOut>> out_pool;
-  // A/B switch: coarse-grained (non-coherent) output buffers, written through the GPU L2
-  // and flushed at kernel end, instead of fine-grained ones written straight over PCIe.
-  const bool out_noncoherent = [] {
-    const char* e = std::getenv("LOCUST_OUT_NONCOHERENT");
-    return e && std::atoi(e) != 0;
-  }();
   size_t out_idx = 0;
   void use_out(size_t i) {
     out_idx = i;
@@ -672,7 +644,7 @@ struct DevicePipeline {
         if (out_pool[i].use_count() == 1) return use_out(i);
     }
     const u64 t0 = now_ns();
-    out_pool.push_back(std::make_shared<HostOut>(h_out_cap, out_noncoherent));
+    out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
     use_out(out_pool.size() - 1);
     LOCUST_LOG_DEBUG("output buffer #%zu: %llu records, %.2f ms", out_pool.size(),
                      (unsigned long long)h_out_cap, (now_ns() - t0) * 1e-6);
@@ -683,7 +655,7 @@ struct DevicePipeline {
     select_out();
     if (n <= h_out_cap) return;
     sync();  // the device may still write the buffer being replaced
-    out_pool[out_idx] = std::make_shared<HostOut>(n, out_noncoherent);
+    out_pool[out_idx] = std::make_shared<HostOut>(n);
     use_out(out_idx);
   }
   // Pinned staging for key up/downloads (stage-split paths only), allocated on demand.
@@ -702,22 +674,8 @@ struct DevicePipeline {
                   std::to_string(cap_lines) + " lines)");
   }
 
-  // LOCUST_SPIN_SYNC=1: poll hipStreamQuery instead of hipStreamSynchronize (A/B knob for
-  // the host's wake-up latency after a short job).
-  void sync() {
-    static const bool spin = [] {
-      const char* v = std::getenv("LOCUST_SPIN_SYNC");
-      return v && v[0] == '1';
-    }();
-    if (spin) {
-      hipError_t e;
-      while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
-      }
-      LOCUST_HIP_CHECK(e);
-      return;
-    }
-    LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
-  }
+  // (Spinning on hipStreamQuery instead measured no faster, profiles/r3_s4/spin_sync_ab.txt.)
+  void sync() { LOCUST_HIP_CHECK(hipStreamSynchronize(stream)); }
   // Lean jobs: the stream's last kernel publishes `seq` to h_done; poll it (bounded, then
   // a real synchronisation -- a long job does not burn the core, a failed one reports).
   void publish_done(u32 seq) { launch_signal_host(d_done, seq, stream); }
@@ -811,8 +769,6 @@ struct DevicePipeline {
   void ensure_piece_events(size_t n) {
     if (!cstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     if (!cstream2) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream2, hipStreamNonBlocking));
-    if (copy_streams > 2 && !cstream3)
-      LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream3, hipStreamNonBlocking));
     if (!ev_fork) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     while (ev_piece.size() < n) {
       hipEvent_t e;
@@ -828,7 +784,7 @@ struct DevicePipeline {
       // from `stream`, made in enqueue_map); their maps follow in enqueue_map
       hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
       LOCUST_HIP_CHECK(hipStreamIsCapturing(stream, &cst));
-      if (copy_first && cst == hipStreamCaptureStatusNone)
+      if (cst == hipStreamCaptureStatusNone)
         issue_piece_copies(upload_mode == Upload::kDirect ? in.data : h_text);
     } else if (upload_mode == Upload::kDirect) {
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
@@ -1013,7 +969,6 @@ struct DevicePipeline {
         LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
         LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream2, ev_fork, 0));
-        if (cstream3) LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream3, ev_fork, 0));
       }
       // a combining large pass (run() / the shard engine take the two-kernel ordered build
       // next): aggregate each piece right after its map, into slot k -- on the same stream:
@@ -1124,15 +1079,10 @@ struct DevicePipeline {
   // counter snapshot when every possible key fits it (then the host needs no D2H), else
   // into d_out.  Events (optional; not while capturing) mark the stage ends.
   bool radix_mapped() const { return h_out_cap >= cap; }
-  // LOCUST_RADIX_FUSED=0: A/B against the separate partitioned sort + fused reduce
-  static bool radix_fused_enabled() {
-    const char* v = std::getenv("LOCUST_RADIX_FUSED");
-    return !(v && v[0] == '0');
-  }
   bool radix_fused = false;  // the last radix job took the fused sort + reduce kernel
   void enqueue_radix_job(u32 num_lines, bool compat, hipEvent_t after_process,
                          hipEvent_t after_reduce) {
-    radix_fused = radix_fused_enabled() && cfg.reduce_path == ReducePath::kLds &&
+    radix_fused = cfg.reduce_path == ReducePath::kLds &&
                   radix_mapped() && psort_ok(compat, false);
     if (radix_fused) {
       // Process + Reduce in one kernel, records straight into the mapped output; it
@@ -1226,21 +1176,13 @@ struct DevicePipeline {
     launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
                        d_ctr, stream);
   }
-  // Ranks of the distinct keys (rank and uval must be zero).  Default: the weighted rank --
-  // the all-pairs pass also sums the counts of the smaller keys, which IS the output's
-  // val, and rank_emit writes the records straight from it.  LOCUST_RANK=scan counts
-  // ranks only and derives val from a look-back scan of the counts in rank order
-  // (scatter + scan_pack: one more launch; measured slower on MI355X, kept for A/B).
-  static bool weighted_rank() {
-    static const bool w = [] {
-      const char* e = std::getenv("LOCUST_RANK");
-      return !(e && std::string(e) == "scan");
-    }();
-    return w;
-  }
+  // Ranks of the distinct keys (rank and uval must be zero): the weighted rank -- the
+  // all-pairs pass also sums the counts of the smaller keys, which IS the output's val,
+  // and rank_emit writes the records straight from it.  (Ranks only + a look-back scan of
+  // the counts in rank order measured slower; git history keeps it.)
   void enqueue_rank() {
-    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank,
-                     weighted_rank() ? dict.uval : nullptr, stream);
+    launch_rank_sort(dict.ukeys, dict.ucount, &d_ctr->num_unique, ucap, d_rank, dict.uval,
+                     stream);
   }
   // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
   // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
@@ -1421,7 +1363,6 @@ struct DevicePipeline {
     OrderedExtra ex;
     ex.pm = part_map();
     ex.part_w = d_pw;
-    if (const char* v = std::getenv("LOCUST_ORD_VARIANT")) ex.variant = (u32)std::atoi(v);
     ex.split_min = split_min;
     if (self_clean) set_self_clean(ex);
     if (self_clean && done_pending) {  // the kernel itself tells the host it is done
@@ -1625,14 +1566,8 @@ struct DevicePipeline {
   // Output records in key order; `mapped` writes them (and the counters) straight into
   // host memory (zero-copy: the host needs no D2H).
   void enqueue_emit_dict(bool mapped) {
-    if (weighted_rank()) {
-      launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, ucap, d_ctr,
-                       mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
-      return;
-    }
-    enqueue_sorted_from_dict();
-    launch_scan_pack(sorted, d_sorted_counts, ucap, d_ctr, mapped ? d_out_mapped : d_out, lb_scan,
-                     stream, mapped ? d_ctr_mapped : nullptr, (u32)kRankSortMax);
+    launch_rank_emit(dict.ukeys, dict.ucount, d_rank, dict.uval, ucap, d_ctr,
+                     mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr, stream);
   }
   // Radix-fallback reduce: scan of the sorted counts -> records in d_out.
   void enqueue_reduce_dict() {
@@ -1673,23 +1608,12 @@ struct DevicePipeline {
     read_counters();
     const u64 u = h_ctr->num_unique;
     grow_host_out(u);
-    if (u && copy_out_dma())  // A/B: LOCUST_OUT_COPY=dma
-      LOCUST_HIP_CHECK(
-          hipMemcpyAsync(h_out, d_out, u * sizeof(OutRecord), hipMemcpyDeviceToHost, stream));
-    else if (u)
+    if (u)
       launch_copy_to_mapped(d_out_mapped, d_out, u * sizeof(OutRecord), stream);
     if (done) LOCUST_HIP_CHECK(hipEventRecord(done, stream));
     sync();
     fill_counters(r);
     copy_out(r.entries, u);
-  }
-
-  static bool copy_out_dma() {
-    static const bool dma = [] {
-      const char* e = std::getenv("LOCUST_OUT_COPY");
-      return e && std::string(e) == "dma";
-    }();
-    return dma;
   }
 
   // Host output records -> result entries: identical 40-byte layouts, so the result

@@ -241,7 +241,6 @@ struct PsortReduceArgs {
   u32 map_words = 0;
   u32* host_done = nullptr;
   u32 host_done_value = 0;
-  u32 variant = 0;  // A/B switches (LOCUST_PSORT_VARIANT; bit 0: no all-pairs ranking)
 };
 void launch_psort_reduce(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap,
                          MapCounters* ctr, u32* part_w, const PsortReduceArgs& ra, hipStream_t s,
@@ -323,7 +322,6 @@ struct OrderedExtra {
   // of 256 workgroups idle and puts 's'/'t' on the critical path without it.  (Inputs of
   // at most kPartBlock tiles; larger ones keep one workgroup per partition.)
   const u32* part_occ = nullptr;
-  u32 variant = 0;              // A/B switches for kernel experiments (LOCUST_ORD_VARIANT)
   u32 split_min = 0;            // planned workgroups: tokens per extra sibling (0: default)
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};

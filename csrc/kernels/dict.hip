@@ -626,7 +626,6 @@ struct TileSource {
   const u32* part_off;
   u32 ntiles;
   u32 n_cap;  // token capacity: indices past it were never written
-  bool eager_w1 = true;  // gather_insert; LOCUST_ORD_VARIANT bit 256 clears it (A/B)
   // This thread's first run (tile threadIdx.x), loaded before the kernel clears its table
   // so that the load overlaps the clear and its barrier.
   struct Pre {
@@ -669,7 +668,7 @@ struct TileSource {
       const u32 cnt = s_count;
       full |= cnt > (u32)kPartWindow;  // the host redoes the Process stage on the HBM table
       full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab, 0,
-                            ~0ull, true, eager_w1);
+                            ~0ull, true, true);
       if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
       __syncthreads();
       if (threadIdx.x == 0) s_count = 0;
@@ -718,7 +717,7 @@ struct TileSource {
     // a list cut short by the sample area is an overflow: the host redoes the pass
     bool full = n > lim;
     if (!(lo == hi && !last))  // else an empty range (a hot first word took it)
-      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last, eager_w1);
+      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last, true);
     if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // the list area is reused after the build
     return full;
@@ -815,7 +814,7 @@ constexpr u32 kPartialFull = 0xFFFFFFFFu;  // partial_n of a slot whose table ov
 __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
     ConstKeysSoA tokens, const u64* __restrict__ counts, const u32* __restrict__ part_off,
     u32 tile_begin, u32 tile_end, u32 nslices, u32 slot_base, u32 nslots, u32 n_cap,
-    KeyCount* __restrict__ partials, u32* __restrict__ partial_n, u32 variant,
+    KeyCount* __restrict__ partials, u32* __restrict__ partial_n,
     u64* __restrict__ trace) {
   // worker k of partition p: the workers of one partition are kDictParts apart in
   // dispatch order, so a hot partition's slices land on different CUs and XCDs
@@ -853,8 +852,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_partials_kernel(
   if (trace && threadIdx.x == 0) trace[slot * 8 + 1] = __builtin_amdgcn_s_memrealtime();
   u32 ntok = 0;
   const bool full = walk_runs_insert(tokens, counts, part_off, p, t, t1, a, len, n_cap, s_tab,
-                                     !(variant & 4u), &ntok, (variant & 32u) ? nullptr : &s_full,
-                                     &s_occ);
+                                     true, &ntok, &s_full, &s_occ);
   if (trace) atomicAdd(&s_tok, ntok);
   __syncthreads();  // every wave's inserts are in the table before it is read
   if (trace && threadIdx.x == 0) {
@@ -1146,7 +1144,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   const u64 tok = s_ctok;
   // Small partitions (the common case once the partition map is balanced) skip the
   // bucket sort: ranks come from one all-pairs pass (see below).
-  const bool small = !(ex.variant & 1u) && !any_full && m <= kSmallRank;  // variant 1: A/B
+  const bool small = !any_full && m <= kSmallRank;
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
@@ -1177,23 +1175,12 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         for (int k = 0; k < 4; ++k) any |= lane + 64u * k < v && (st[k] >> dev::kLbFlagShift) == 0;
         return any;
       };
-      if (ex.variant & 8u) {  // A/B: the previous per-group polling
+      while (dev::ballot(pending())) {
+        __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const u32 q = lane + 64u * k;
-          while (q < v && (st[k] >> dev::kLbFlagShift) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            st[k] = dev::ld_agent(&status[q]);
-          }
-        }
-      } else {
-        while (dev::ballot(pending())) {
-          __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const u32 q = lane + 64u * k;
-            if (q < v && (st[k] >> dev::kLbFlagShift) == 0) st[k] = dev::ld_agent(&status[q]);
-          }
+          if (q < v && (st[k] >> dev::kLbFlagShift) == 0) st[k] = dev::ld_agent(&status[q]);
         }
       }
       int hi_inc = -1;  // highest predecessor with an inclusive value
@@ -1317,12 +1304,12 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     s_cur[threadIdx.x] = 0;
   }
   __syncthreads();
-  if (!any_full && m > 1 && !(ex.variant & 16u)) {
+  if (!any_full && m > 1) {
     // LSD radix sort of the partition's distinct keys in LDS over the bytes that vary
     // (dev::LdsRadix, as the partitioned token sort): word 3 down to word 0, low byte to
     // high, stable.  The bucket + all-pairs ranking below degenerated on skewed key sets
     // -- most keys in one bucket, long keys tied on their first word: up to 295K cycles
-    // for one 1,003-key partition of the synthetic text (LOCUST_ORD_VARIANT=16 keeps it).
+    // for one 1,003-key partition of the synthetic text (git history keeps that path).
     using Radix = dev::LdsRadix<kPartBlock, kPartSlots, u16>;
     u64* s_word = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);          // [kPartSlots]
     auto s_perm = reinterpret_cast<u16 (*)[kPartSlots]>(s_list + 5 * kPartSlots);  // [2][..]
@@ -1857,8 +1844,7 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s, u64* trace,
                          const OrderedExtra& ex) {
   if (ex.part_off && !counts) {
-    const TileSource src{tokens, ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu),
-                         !(ex.variant & 256u)};
+    const TileSource src{tokens, ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
     dict_ordered_kernel<TileSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
         src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   } else {
@@ -1877,9 +1863,7 @@ void launch_dict_partials(ConstKeysSoA tokens, const u64* counts, const u32* par
                        nslots <= (u32)kMaxPartialSlots && tile_begin <= tile_end,
                    "partials: bad slot layout");
   dict_partials_kernel<<<dim3(kDictParts * nslices), dim3(kPartBlock), 0, s>>>(
-      tokens, counts, part_off, tile_begin, tile_end, nslices, slot_base, nslots, (u32)std::min<u64>(cap, 0xFFFFFFFFu), partials, partial_n,
-      std::getenv("LOCUST_ORD_VARIANT") ? (u32)std::atoi(std::getenv("LOCUST_ORD_VARIANT")) : 0u,
-      trace);
+      tokens, counts, part_off, tile_begin, tile_end, nslices, slot_base, nslots, (u32)std::min<u64>(cap, 0xFFFFFFFFu), partials, partial_n, trace);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

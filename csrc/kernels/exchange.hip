@@ -33,7 +33,7 @@ __device__ __forceinline__ bool key4_less(const u64* a, const u64* b) {
 __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
     const char* __restrict__ msg1_all, u32 P, u32 S, ConstKeysSoA keys,
     const u32* __restrict__ d_n, u32 slot_records, ExchCtl* __restrict__ ctl,
-    u64* __restrict__ trace, u32 variant) {
+    u64* __restrict__ trace) {
   // trace (diagnostics, LOCUST_EXCH_TRACE): device clock at entry and after each phase
 #define PLAN_STAMP(k_) \
   if (trace && threadIdx.x == 0) trace[k_] = __builtin_amdgcn_s_memrealtime()
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kPlanBlock) void exch_plan_kernel(
   // its own, a lower bound in those after.  An all-pairs walk (one thread per sample over
   // all NS candidates) took 26 us at NS = 64 -- every step a dependent LDS load with a
   // divergent tie branch.  A list that is not sorted falls back to that walk.
-  if (t == 0) s_unsorted = variant & 1u;  // variant 1 (A/B): the all-pairs walk
+  if (t == 0) s_unsorted = 0;
   __syncthreads();
   if (fits)
     for (u32 i = t; i < NS; i += kPlanBlock)
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void exch_emit_kernel(
     const OutRecord* __restrict__ src, const ExchMsg3* __restrict__ msg3_all,
     const ExchMsg1* __restrict__ root_msg, u64 region, u32 regions, u64 region_records, u32 P,
     u32 me, u32 gather_records, OutRecord* __restrict__ dst, u64* __restrict__ stamps, u64 seq,
-    u32* __restrict__ done, u32 nt) {
+    u32* __restrict__ done) {
   __shared__ u64 s_roff, s_n;
   __shared__ u32 s_bad;
   if (threadIdx.x == 0) {
@@ -299,11 +299,7 @@ __global__ __launch_bounds__(256) void exch_emit_kernel(
   // (word indices fit 32 bits: a range is < 2^29 records)
   const u32 nq = (u32)(kOutWords * N);
   for (u32 q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
-    const u64 v = in[q];
-    if (nt)
-      __builtin_nontemporal_store(v, out + q);
-    else
-      out[q] = v;
+    out[q] = in[q];
   }
   __threadfence_system();
   __syncthreads();
@@ -339,12 +335,8 @@ void launch_exch_header(const MapCounters* ctr, const ExchMsg1& tmpl, bool combi
 
 void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
                       u32 slot_records, ExchCtl* ctl, hipStream_t s, u64* trace) {
-  static const u32 variant = [] {
-    const char* e = std::getenv("LOCUST_PLAN_VARIANT");
-    return e ? (u32)std::atoi(e) : 0u;
-  }();
   exch_plan_kernel<<<dim3(1), dim3(kPlanBlock), 0, s>>>(msg1_all, P, S, keys, d_n, slot_records,
-                                                         ctl, trace, variant);
+                                                         ctl, trace);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
@@ -369,14 +361,9 @@ void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const Ex
                       hipStream_t s) {
   const u64 words = (u64)kOutWords * gather_records;
   const u64 blocks = std::min<u64>(std::max<u64>(div_up(words ? words : 1, 256), 1), 2048);
-  static const u32 nt = [] {  // LOCUST_EMIT_NT=1: non-temporal stores (A/B)
-    const char* e = std::getenv("LOCUST_EMIT_NT");
-    return e && e[0] == '1' ? 1u : 0u;
-  }();
   exch_emit_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(range, msg3_all, root_msg, region,
                                                            regions, region_records, P, me,
-                                                           gather_records, dst, stamps, seq, done,
-                                                           nt);
+                                                           gather_records, dst, stamps, seq, done);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -291,8 +291,7 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
   for (int j = 0; j < kKeyWords; ++j)
 #pragma unroll
     for (int b = 0; b < 8; ++b) lsd_passes += ((diff[j] >> (8 * b)) & 0xffull) ? 1u : 0u;
-  if (any_diff && !long_keys && m <= 2u * kPsBlock && m < 22u * lsd_passes &&
-      !(ra.variant & 1u)) {
+  if (any_diff && !long_keys && m <= 2u * kPsBlock && m < 22u * lsd_passes) {
     // eight independent compares per step: the broadcast LDS reads of a step are all in
     // flight together (one at a time, each compare waited out the LDS latency)
     constexpr u32 kU = 8;
@@ -458,19 +457,10 @@ __global__ __launch_bounds__(kPsBlock) void psort_kernel(ConstKeysSoA tokens,
 
 }  // namespace
 
-u32 psort_variant() {
-  static const u32 v = [] {
-    const char* e = std::getenv("LOCUST_PSORT_VARIANT");
-    return e ? (u32)std::atoi(e) : 0u;
-  }();
-  return v;
-}
-
 void launch_psort(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u64 cap, KeysSoA sorted,
                   MapCounters* ctr, u32* part_w, hipStream_t s, u64* trace) {
   LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
   PsortReduceArgs ra;
-  ra.variant = psort_variant();
   psort_kernel<false><<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(
       tokens, part_off, ntiles, (u32)cap, sorted, ctr, part_w, trace, ra);
   LOCUST_HIP_LAUNCH_CHECK();
@@ -481,10 +471,8 @@ void launch_psort_reduce(ConstKeysSoA tokens, const u32* part_off, u32 ntiles, u
                          u64* trace) {
   LOCUST_CHECK_ARG(cap < (1ull << 32), "psort: capacity beyond 32-bit token indices");
   LOCUST_CHECK_ARG(ra.out && ra.status && ra.done_counter, "psort_reduce: missing buffers");
-  PsortReduceArgs a = ra;
-  a.variant |= psort_variant();
   psort_kernel<true><<<dim3(kDictParts), dim3(kPsBlock), 0, s>>>(
-      tokens, part_off, ntiles, (u32)cap, KeysSoA{}, ctr, part_w, trace, a);
+      tokens, part_off, ntiles, (u32)cap, KeysSoA{}, ctr, part_w, trace, ra);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -1,0 +1,51 @@
+"""One process of tests/test_switches.py: runs a fixed set of WordCount jobs under the
+LOCUST_* environment it was started with and checks every result against the oracle.
+
+    python tests/switch_worker.py single|stream|dist
+
+Exit status 0 = every job matched; the failure is printed otherwise.  A separate process
+per setting because many switches are read once per process (or per engine)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import locust_amd as lc  # noqa: E402
+from locust_amd.utils import oracle  # noqa: E402
+
+
+def check(res, text, what):
+    ent, ntok, _ = oracle.wordcount(text)
+    assert res.num_tokens == ntok, (what, res.num_tokens, ntok)
+    assert res.entries() == ent, f"{what}: entries differ from the oracle"
+
+
+def main(kind: str) -> None:
+    hamlet = open(os.path.join(ROOT, "data", "hamlet.txt"), "rb").read()
+    # ~2.6 MB of synthetic text: a one-pass "large" input (piecewise upload, partials build)
+    synth = lc.gen_text(lines=60_000, seed=7)
+    if kind == "single":
+        for text, what in ((hamlet, "hamlet"), (oracle.window(hamlet, 0, 700), "hamlet700"),
+                           (synth, "synth")):
+            eng = lc.Engine(lc.make_config("gpu"), len(text), text.count(b"\n") + 1)
+            for j in range(3):  # first job, retuned job, steady job
+                check(eng.run(text), text, f"{what} job {j}")
+    elif kind == "stream":
+        eng = lc.Engine(lc.make_config("gpu", chunk_bytes=1 << 20), len(synth),
+                        synth.count(b"\n") + 1)
+        for j in range(2):
+            check(eng.run(synth), synth, f"streamed job {j}")
+    elif kind == "dist":
+        for world in (1, 2, 3):
+            for strategy in ("shuffle", "auto"):
+                res = lc.run_multi(synth, world, strategy=strategy, comm="loopback")
+                check(res, synth, f"loopback {world} {strategy}")
+    else:
+        raise SystemExit(f"unknown kind {kind}")
+    print("switch worker ok:", kind, {k: v for k, v in os.environ.items()
+                                      if k.startswith("LOCUST_")})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

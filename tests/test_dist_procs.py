@@ -18,11 +18,11 @@ from locust_amd.parallel import launch
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_worker.py")
 
 
-def _run(tmp_path, world, comm, strategy, jobs, keep=False, text=None):
+def _run(tmp_path, world, comm, strategy, jobs, keep=False, text=None, env_extra=None):
     src = tmp_path / "text.txt"
     src.write_bytes(text if text is not None else open(os.path.join(lc.REPO_ROOT, "data", "hamlet.txt"), "rb").read())
     out = str(tmp_path / "res")
-    env = {"PYTHONPATH": lc.REPO_ROOT}
+    env = {"PYTHONPATH": lc.REPO_ROOT, **(env_extra or {})}
     rc = launch.launch_local([sys.executable, WORKER, str(src), out, comm, strategy, str(jobs),
                               "1" if keep else "0"], world, timeout=300, extra_env=env)
     assert rc == 0
@@ -60,3 +60,14 @@ def test_held_results_across_processes(tmp_path):
     assert all(recs[0]["ok"]), recs[0]["ok"]
     syncs = [i["host_syncs"] for i in recs[0]["infos"]]
     assert 2 in syncs[1:], syncs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slow", [0, 1])
+def test_held_results_slow_rank_regrow(tmp_path, slow):
+    """Grow-and-re-emit with one rank 300 ms late to open the new output generation
+    (LOCUST_FAULT=<rank>:slow_regrow): the host barrier after the open keeps the fast ranks
+    from unlinking the name first."""
+    recs = _run(tmp_path, 2, "tcpdev", "shuffle", 5, keep=True,
+                env_extra={"LOCUST_FAULT": f"{slow}:slow_regrow", "LOCUST_OUT_WAIT_S": "20"})
+    assert all(recs[0]["ok"]), recs[0]["ok"]
