@@ -24,6 +24,10 @@ DistResult run_single_process_multi_gpu(const DistConfig&, const TextInput&, Loc
                                         std::vector<DistResult>*) {
   no_gpu();
 }
+DistResult run_single_process_file(const DistConfig&, const std::string&, LocalComm,
+                                   std::vector<DistResult>*) {
+  no_gpu();
+}
 int visible_device_count() { return 0; }
 LocalComm resolve_local_comm(const DistConfig&, LocalComm) { return LocalComm::kLoopback; }
 

@@ -259,6 +259,7 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
                     : root.strategy == DistStrategy::kLocal   ? "local"
                                                               : "shuffle");
   j.num("wall_ms", root.total_ms);
+  j.u("peak_rss_kb", peak_rss_kb());
   std::string rk = "[";
   for (size_t r = 0; r < ranks.size(); ++r) {
     const DistResult& d = ranks[r];
@@ -279,6 +280,9 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
     x.u("output_bytes", d.output_bytes);
     x.kv("device_exchange", d.device_exchange ? "true" : "false");
     x.u("host_syncs", (u64)d.host_syncs);
+    x.u("input_bytes", d.input_bytes);
+    x.kv("input_streamed", d.input_streamed ? "true" : "false");
+    x.kv("peer_p2p", std::to_string(d.peer_p2p));
     rk += (r ? ", " : "") + x.done();
   }
   j.kv("ranks", rk + "]");
@@ -461,14 +465,21 @@ int run(const CliArgs& a) {
                       !a.cfg.ref_compat && a.cfg.map_path == MapPath::kFast &&
                       a.cfg.sort_path == SortPath::kDict;
   if (direct) return run_direct(a);
-  LoadedText text = load_lines(a.file, use_window ? a.line_start : -1,
-                               use_window ? a.line_end : -1, a.cfg.ref_compat);
-  if (!cpu) std::printf("Length: %i\n", (int)text.input.num_lines);
-
-  // ---------------- multi-GPU in one process (RCCL clique over the node's GPUs) ---------
-  // An explicit --gpus N (N >= 1) runs N ranks: an ncclCommInitAll clique over xGMI when
-  // the node has N GPUs (--gpus 1 included: one RCCL rank), loopback ranks otherwise.
-  if ((a.gpus > 1 || (a.gpus_given && !cpu)) && a.stage == 0) {
+  // ---------------- multi-GPU in one process (one thread per rank) ----------------------
+  // An explicit --gpus N (N >= 1) runs N ranks.  --comm auto: an ncclCommInitAll clique
+  // over xGMI when N > 1 and every rank has a GPU of its own, loopback ranks otherwise
+  // (one rank, or N ranks rehearsed on fewer GPUs); --comm rccl / loopback force either.
+  // A whole file is never loaded: every rank reads only its own line-aligned byte range
+  // (run_single_process_file); a line window is loaded first, then sharded.
+  const bool multi = (a.gpus > 1 || (a.gpus_given && !cpu)) && a.stage == 0;
+  const bool file_ranks = multi && !use_window && !a.cfg.ref_compat;
+  LoadedText text;
+  if (!file_ranks) {
+    text = load_lines(a.file, use_window ? a.line_start : -1, use_window ? a.line_end : -1,
+                      a.cfg.ref_compat);
+    if (!cpu) std::printf("Length: %i\n", (int)text.input.num_lines);
+  }
+  if (multi) {
     DistConfig dc;
     dc.job = a.cfg;
     // ranks always combine map-side (the output is the same; the device exchange and the
@@ -479,7 +490,10 @@ int run(const CliArgs& a) {
                     resolve_local_comm(dc, a.comm) == LocalComm::kRccl ? "an RCCL clique"
                                                                        : "loopback");
     std::vector<DistResult> ranks;
-    DistResult dr = run_single_process_multi_gpu(dc, text.input, a.comm, &ranks);
+    DistResult dr = file_ranks ? run_single_process_file(dc, a.file, a.comm, &ranks)
+                               : run_single_process_multi_gpu(dc, text.input, a.comm, &ranks);
+    LOCUST_LOG_INFO("rss after the job: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+    if (file_ranks && !cpu) std::printf("Length: %i\n", (int)dr.result.num_lines);
     std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(dr.reduce_ms));

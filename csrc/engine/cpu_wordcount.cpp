@@ -114,6 +114,7 @@ class CpuShardEngine final : public ShardEngine {
   void* stream() override { return nullptr; }
 
   u64 map_local(const TextInput& shard, bool combine, DistStrategy) override {
+    LOCUST_CHECK_ARG(!shard.source, "the CPU engine maps in-memory shards only");
     CpuWordCount eng(cfg_);
     stats_ = WordCountResult();
     std::vector<PackedKey> toks = eng.run_map_stage(shard, &stats_);

@@ -434,7 +434,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       h.status = st1;
       h.record_flags = eng.record_flags();
       h.n_local = st1 ? 0 : n_local;
-      h.lines = shard.num_lines;
+      h.lines = shard.lines();  // a streamed source is drained by the map's enqueue
       h.tokens = local_stats.num_tokens;
       h.overflow_lines = local_stats.overflow_lines;
       h.truncated = local_stats.truncated;
@@ -605,7 +605,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const u64 m1 = sizeof(Msg1) + (u64)S * sizeof(PackedKey);
   std::vector<char> out1(m1), all1(m1 * (u64)P);
   {
-    Msg1 h{st1, eng.record_flags(), n_local, shard.num_lines, local_stats.num_tokens, local_stats.overflow_lines,
+    Msg1 h{st1, eng.record_flags(), n_local, shard.lines(), local_stats.num_tokens, local_stats.overflow_lines,
            local_stats.truncated, local_stats.max_key_len};
     std::memcpy(out1.data(), &h, sizeof(h));
     std::memcpy(out1.data() + sizeof(h), mine_samples.data(), (u64)S * sizeof(PackedKey));

@@ -49,13 +49,16 @@ class GpuShardEngine final : public ShardEngine {
     distinct_local_ = true;  // every path below yields distinct keys except combine=false
     stream_chunks_ = 0;
     const bool streamed = shard.bytes > m.cap_bytes;
+    LOCUST_CHECK_ARG(!shard.source || streamed,
+                     "a shard read from a source must be larger than one device pass");
     const bool small_ordered = combine && cfg_.sort_path == SortPath::kDict && !streamed &&
                                cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
     if (streamed) {
       // a shard larger than one device pass: chunked H2D + map into one dictionary
       LOCUST_CHECK_ARG(combine && cfg_.sort_path == SortPath::kDict,
                        "streaming shards need the map-side combine of the dictionary path");
-      stream_chunks_ = m.enqueue_stream_insert(shard);
+      stream_chunks_ = shard.source ? m.enqueue_stream_source(*shard.source)
+                                    : m.enqueue_stream_insert(shard);
     } else if (!small_ordered) {
       m.check_input(shard);
       // a large dictionary pass maps in upload pieces with per-tile combining
@@ -1022,7 +1025,7 @@ class GpuShardEngine final : public ShardEngine {
   u64 finish_map_stats(const TextInput& shard, u64 n_records) {
     DevicePipeline& m = *mp_;
     local_stats_ = WordCountResult();
-    local_stats_.num_lines = shard.num_lines;
+    local_stats_.num_lines = shard.lines();
     m.fill_counters(local_stats_);
     local_stats_.num_tokens = m.map_combined ? m.h_ctr->map_tokens : m.h_ctr->num_records;
     if (stream_chunks_) m.stream_stats(stream_chunks_, local_stats_);

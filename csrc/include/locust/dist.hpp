@@ -355,6 +355,10 @@ struct DistResult {
   DistStrategy strategy = DistStrategy::kShuffle;  // the one this job took
   bool device_exchange = false;  // the shuffle ran as the device exchange (locust/exch.hpp)
   int host_syncs = 0;            // ... with this many host synchronisations
+  // single-process runs (run_single_process_*): this rank's input and its GPU's peers
+  u64 input_bytes = 0;           // bytes of its shard it read / mapped
+  bool input_streamed = false;   // ... streamed from its file range (larger than one pass)
+  int peer_p2p = -1;             // peers of its GPU with direct (xGMI) access; -1: no peers
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
@@ -366,11 +370,15 @@ void copy_device(void* dst, const void* src, u64 bytes, bool to_host, void* stre
 // Split a line-aligned text into `parts` line-aligned shards of ~equal bytes.
 std::vector<TextInput> shard_text(const TextInput& in, int parts);
 
-// One process drives `cfg.world` ranks (threads) over the visible GPUs (round robin) with
-// the loopback communicator; rank 0's result is returned.  With Backend::kCpu the ranks
-// use the CPU shard engine.
-// comm: kAuto = an RCCL clique (ncclCommInitAll) when every rank gets a GPU of its own,
-// else loopback (N ranks rehearsed on fewer GPUs; RCCL refuses two ranks per device).
+// One process drives `cfg.world` ranks (threads) over the visible GPUs (round robin);
+// rank 0's result is returned.  With Backend::kCpu the ranks use the CPU shard engine.
+// comm: kAuto = an RCCL clique (ncclCommInitAll over xGMI) when there are several ranks
+// and every rank gets a GPU of its own (falling back to loopback, with a warning, if the
+// clique cannot be created); else loopback (one rank, or N ranks rehearsed on fewer GPUs:
+// RCCL refuses two ranks per device).  Loopback ranks on distinct GPUs get peer access
+// enabled pairwise first, so their device copies go GPU to GPU.
+// Ranks in one process never share host memory for their input: each rank thread copies
+// (or reads) its own shard into its engine's pinned buffer, first touched on its NUMA node.
 enum class LocalComm : int { kAuto = 0, kLoopback = 1, kRccl = 2 };
 DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole,
                                         LocalComm comm = LocalComm::kAuto,
@@ -382,9 +390,21 @@ std::vector<DistResult> run_single_process_schedule(const std::vector<DistConfig
                                                     const TextInput& whole,
                                                     LocalComm comm = LocalComm::kAuto,
                                                     std::vector<DistResult>* per_rank = nullptr);
+// The same over a FILE: rank r reads only its own line-aligned byte range (file_shards)
+// -- straight into its engine's pinned buffer with parallel preads when the range fits
+// one device pass (cfg.job.chunk_bytes, default 256 MiB), else streamed through a small
+// pinned ring chunk by chunk (enqueue_stream_source).  The whole file is never held in
+// host memory.
+DistResult run_single_process_file(const DistConfig& cfg, const std::string& path,
+                                   LocalComm comm = LocalComm::kAuto,
+                                   std::vector<DistResult>* per_rank = nullptr);
 // Visible GPUs (0 if none or the runtime fails).
 int visible_device_count();
 // Which communicator run_single_process_* would use for `world` ranks (for logging).
 LocalComm resolve_local_comm(const DistConfig& cfg, LocalComm comm);
+// Peer access between every pair of `devices` (distinct ordinals): enabled where the
+// runtime reports it possible; m[i * n + j] = 1 when device i can access device j
+// directly.  Logged per pair at LOCUST_LOG=info.
+std::vector<int> enable_peer_access(const std::vector<int>& devices);
 
 }  // namespace locust

@@ -21,11 +21,17 @@ namespace locust {
 // A window of input lines: `bytes` bytes of text, lines separated by '\n' (the last line
 // may lack one).  `first_line` is the global index of the first line (the reference's
 // KeyValuePair.key, main.cu:58).
+class TextSource;
 struct TextInput {
   const char* data = nullptr;
   u64 bytes = 0;
   u64 num_lines = 0;
   u64 first_line = 0;
+  // Distributed shards only: a shard larger than one device pass may be streamed from a
+  // source (a rank's byte range of a file) instead of held in memory -- data is then null,
+  // bytes the range's size, and num_lines unknown until the source is drained.
+  TextSource* source = nullptr;
+  u64 lines() const;  // num_lines, or the lines the source has handed out
 };
 
 struct StageTimes {
@@ -160,6 +166,9 @@ class TextSource {
 };
 // A file read with `threads` concurrent preads per chunk (0: up to 8); see io.cpp.
 std::unique_ptr<TextSource> open_file_source(const std::string& path, u32 threads = 0);
+// The same over the byte range [begin, end) of the file (begin at a line start).
+std::unique_ptr<TextSource> open_file_range_source(const std::string& path, u64 begin, u64 end,
+                                                   u32 threads = 0);
 
 class GpuWordCount {
  public:

@@ -34,6 +34,16 @@ u64 file_size(const std::string& path);
 // The whole file into dst (room for cap bytes) by parallel preads; returns its size and
 // sets *lines (a final line without '\n' counts).  dst may be pinned memory.
 u64 read_file_into(const std::string& path, char* dst, u64 cap, u64* lines, u32 threads = 0);
+// Per-rank input shards of a file: P byte ranges cut at line starts,
+// found by reading small windows around the P-1 cut points only.  A line never spans two
+// ranges; a range may be empty (more ranks than lines).
+struct FileRange {
+  u64 offset = 0, bytes = 0;
+};
+std::vector<FileRange> file_shards(const std::string& path, int parts);
+// [off, off + n) of a file into dst by parallel preads; sets *lines like read_file_into.
+u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64* lines,
+                         u32 threads = 0);
 LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
                             bool ref_compat);
 u64 count_lines(const char* data, u64 bytes);

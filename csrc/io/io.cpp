@@ -16,6 +16,8 @@
 
 namespace locust {
 
+u64 TextInput::lines() const { return source ? source->lines() : num_lines; }
+
 u64 count_lines(const char* data, u64 bytes) {
   u64 n = 0;
   const char* p = data;
@@ -215,14 +217,20 @@ class ReadPool {
 
 // A file as line-aligned chunks (TextSource): each chunk is the carried-over partial line
 // of the previous read, then parallel preads, cut after its last '\n'.
+// [begin, end) restricts it to one byte range of the file (a rank's shard, file_shards).
 class FileTextSource final : public TextSource {
  public:
-  FileTextSource(const std::string& path, u32 threads) : path_(path), fd_(path) {
-    size_ = fd_.size();
-    threads_ = io_threads(threads, size_);
+  FileTextSource(const std::string& path, u32 threads, u64 begin = 0, u64 end = ~0ull)
+      : path_(path), fd_(path) {
+    const u64 fsize = fd_.size();
+    end = std::min<u64>(end, fsize);
+    LOCUST_CHECK_ARG(begin <= end, "file range beyond the end of " + path);
+    pos_ = begin_ = begin;
+    size_ = end;
+    threads_ = io_threads(threads, end - begin);
     if (threads_ > 1) pool_.reset(new ReadPool(threads_));
   }
-  u64 size() const override { return size_; }
+  u64 size() const override { return size_ - begin_; }
   u64 lines() const override { return lines_; }
   u64 next(char* dst, u64 cap) override {
     if (pos_ >= size_ && carry_.empty()) return 0;
@@ -259,7 +267,8 @@ class FileTextSource final : public TextSource {
  private:
   std::string path_;
   Fd fd_;
-  u64 size_ = 0, pos_ = 0, lines_ = 0;
+  u64 size_ = 0, pos_ = 0, lines_ = 0;  // size_: the range's end offset in the file
+  u64 begin_ = 0;
   u32 threads_ = 1;
   std::string carry_;
   std::unique_ptr<ReadPool> pool_;
@@ -269,6 +278,53 @@ class FileTextSource final : public TextSource {
 
 std::unique_ptr<TextSource> open_file_source(const std::string& path, u32 threads) {
   return std::unique_ptr<TextSource>(new FileTextSource(path, threads));
+}
+
+std::unique_ptr<TextSource> open_file_range_source(const std::string& path, u64 begin, u64 end,
+                                                   u32 threads) {
+  return std::unique_ptr<TextSource>(new FileTextSource(path, threads, begin, end));
+}
+
+// Cut k of P lies at the start of the first line that begins at or after byte size*k/P:
+// the byte after the first '\n' at or after offset size*k/P - 1 (the reference's per-node
+// line ranges, main.cu:369-374, as byte ranges).  Only small windows around the cuts are
+// read -- never the whole file.
+std::vector<FileRange> file_shards(const std::string& path, int parts) {
+  LOCUST_CHECK_ARG(parts >= 1, "parts must be >= 1");
+  Fd f(path);
+  const u64 n = f.size();
+  std::vector<u64> cut((size_t)parts + 1, n);
+  cut[0] = 0;
+  std::vector<char> buf(64 << 10);
+  for (int k = 1; k < parts; ++k) {
+    const u64 target = n * (u64)k / (u64)parts;
+    u64 at = std::max<u64>(target, 1) - 1, found = n;
+    while (at < n) {
+      const u64 len = std::min<u64>(buf.size(), n - at);
+      const ssize_t got = ::pread(f.fd, buf.data(), (size_t)len, (off_t)at);
+      if (got <= 0) throw Error("short read: " + path);
+      const void* nl = std::memchr(buf.data(), '\n', (size_t)got);
+      if (nl) {
+        found = at + (u64)(static_cast<const char*>(nl) - buf.data()) + 1;
+        break;
+      }
+      at += (u64)got;
+    }
+    cut[(size_t)k] = std::max(cut[(size_t)k - 1], target == 0 ? 0 : found);
+  }
+  std::vector<FileRange> out((size_t)parts);
+  for (int k = 0; k < parts; ++k) out[(size_t)k] = {cut[(size_t)k], cut[(size_t)k + 1] - cut[(size_t)k]};
+  return out;
+}
+
+u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64* lines,
+                         u32 threads) {
+  Fd f(path);
+  LOCUST_CHECK_ARG(off + n <= f.size(), "file range beyond the end of " + path);
+  u64 nl = n ? pread_parallel(f.fd, dst, off, n, io_threads(threads, n), path, true) : 0;
+  if (n && dst[n - 1] != '\n') ++nl;
+  if (lines) *lines = nl;
+  return n;
 }
 
 u64 file_size(const std::string& path) { return Fd(path).size(); }

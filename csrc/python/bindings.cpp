@@ -249,7 +249,24 @@ py::dict dist_to_dict(const DistResult& d) {
   x["strategy"] = d.strategy == DistStrategy::kGather  ? "gather"
                   : d.strategy == DistStrategy::kLocal ? "local"
                                                        : "shuffle";
+  x["input_bytes"] = d.input_bytes;
+  x["input_streamed"] = d.input_streamed;
+  x["peer_p2p"] = d.peer_p2p;
   return x;
+}
+
+// A file's multi-rank job in this process: every rank reads only its own byte range.
+py::tuple run_multi_file(const std::string& path, const DistConfig& cfg, const std::string& comm) {
+  const LocalComm lc = local_comm(comm);
+  std::vector<DistResult> ranks;
+  DistResult d;
+  {
+    py::gil_scoped_release nogil;
+    d = run_single_process_file(cfg, path, lc, &ranks);
+  }
+  py::list infos;
+  for (const auto& x : ranks) infos.append(dist_to_dict(x));
+  return py::make_tuple(PyResult{d.result}, infos);
 }
 
 // A rank of a multi-process job: its communicator and engine live across runs.
@@ -461,6 +478,19 @@ PYBIND11_MODULE(_locust, m) {
   m.def("run_multi", &run_multi, py::arg("text"), py::arg("cfg"), py::arg("comm") = "auto",
         "Multi-rank WordCount in this process (one thread per rank): an RCCL clique "
         "(ncclCommInitAll) when every rank has a GPU of its own, else loopback.");
+  m.def("run_multi_file", &run_multi_file, py::arg("path"), py::arg("cfg"),
+        py::arg("comm") = "auto",
+        "Multi-rank WordCount of a file in this process: rank r reads only its own "
+        "line-aligned byte range (pinned one-pass read, or streamed past one pass); "
+        "returns (rank 0's result, per-rank info dicts).");
+  m.def("file_shards", [](const std::string& path, int parts) {
+    py::list out;
+    for (const auto& r : file_shards(path, parts)) out.append(py::make_tuple(r.offset, r.bytes));
+    return out;
+  }, py::arg("path"), py::arg("parts"), "Line-aligned byte ranges (offset, bytes) of a file.");
+  m.def("peer_access", &enable_peer_access, py::arg("devices"),
+        "Enable peer access between every pair of the devices; returns the n x n matrix "
+        "(row-major) of direct-access flags.");
   m.def("device_count", &visible_device_count,
         "Visible GPUs (initialises the HIP runtime in this process).");
   m.def("local_comm_for", [](const DistConfig& cfg, const std::string& comm) {
