@@ -25,7 +25,7 @@ PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_v
 COMMON    := -std=c++17 -fPIC -Icsrc/include -Wall -Wextra -Wno-unused-parameter
 HIPFLAGS  := $(COMMON) $(OPT) --offload-arch=$(ARCH) -munsafe-fp-atomics
 CXXFLAGS  := $(COMMON) $(OPT) -I$(ROCM)/include
-LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lpthread
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -ldl -lpthread
 
 HIP_SRCS  := $(wildcard csrc/kernels/*.hip csrc/engine/*.hip csrc/comm/*.hip)
 CPP_SRCS  := $(wildcard csrc/engine/*.cpp csrc/io/*.cpp csrc/comm/*.cpp)
@@ -74,7 +74,7 @@ debug:
 # --backend cpu.  (GPU ASan / xnack+ is not available on the GPU pool.)
 ASAN_SRCS := csrc/engine/common.cpp csrc/engine/cpu_wordcount.cpp csrc/engine/dist.cpp \
              csrc/io/io.cpp csrc/io/gen.cpp csrc/comm/tcp_comm.cpp csrc/cli/main.cpp \
-             csrc/engine/trace.cpp csrc/engine/shm.cpp csrc/cli/asan_stubs.cpp
+             csrc/engine/trace.cpp csrc/engine/shm.cpp csrc/engine/numa.cpp csrc/cli/asan_stubs.cpp
 asan: $(BUILD)/asan/MapReduce
 $(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
 	@mkdir -p $(dir $@)

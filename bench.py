@@ -76,14 +76,18 @@ def load_text(config: str) -> bytes:
     return hamlet
 
 
-def synth_shard(config: str, rank: int, world: int, lines: int | None = None):
+def synth_shard(config: str, rank: int, world: int, lines: int | None = None,
+                nbytes: int | None = None):
     """This rank's part of the synthetic text, generated straight into pinned memory
-    (strong scaling: the total is fixed, each of the N ranks owns 1/N of it)."""
+    (strong scaling: the total is fixed, each of the N ranks owns 1/N of it).  `lines` /
+    `nbytes` scale a config down (tests: --synth-lines, --synth-bytes)."""
     import locust_amd as lc
 
     spec = dict(SYNTH[config])
     if lines:
         spec = {"lines": lines, "bytes": 0}
+    elif nbytes and not spec["lines"]:
+        spec = {"lines": 0, "bytes": nbytes}
     if spec["lines"]:
         total_blocks = -(-spec["lines"] // 1024)
         b0, b1 = rank * total_blocks // world, (rank + 1) * total_blocks // world
@@ -425,6 +429,8 @@ def main() -> int:
                     help="use the distributed path even for one rank")
     ap.add_argument("--synth-lines", type=int, default=0,
                     help="lines of the synth1m strong-scaling extra (default 1M; tests)")
+    ap.add_argument("--synth-bytes", type=int, default=0,
+                    help="total bytes of --config synth10g (default 10 GB; tests)")
     args = ap.parse_args()
     if args.backend == "cpu" and args.comm == "rccl" and args.gpus > 1:
         ap.error("--backend cpu needs --comm tcp")
@@ -456,7 +462,7 @@ def main() -> int:
     synth = args.config in SYNTH
     if synth:
         t_gen = time.perf_counter()
-        text = synth_shard(args.config, rank, n)
+        text = synth_shard(args.config, rank, n, nbytes=args.synth_bytes)
         print(f"rank {rank}: generated {text.size} B / {text.lines} lines in "
               f"{time.perf_counter() - t_gen:.1f} s", file=sys.stderr)
         nbytes, nlines = text.size, text.lines
@@ -526,7 +532,7 @@ def main() -> int:
         total_bytes = nbytes * n  # approximately: every rank's shard is the same size
         base = total_bytes / (REF_CHART_MB_PER_S * 1e6) * 1e3
         data = (f"synthetic Hamlet-shaped text (native generator, seed 1), "
-                f"{'1M lines' if args.config == 'synth1m' else '10 GB'} in total, "
+                f"{'1M lines' if args.config == 'synth1m' else f'{total_bytes / 1e9:.3g} GB'} in total, "
                 f"1/N per GPU generated into pinned host memory")
         model = (f"WordCount {args.config}: dictionary path, "
                  + ("one pass, line-aligned upload pieces of up to 12 MiB, two-kernel ordered build"

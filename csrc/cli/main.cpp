@@ -8,7 +8,8 @@
 //                                                      (writes a spill), 2 = reduce only
 // plus long flags (runtime switches replacing the reference's #defines):
 //   --backend gpu|cpu  --reduce-path lds|global  --map-path compat|fast
-//   --sort radix|dict  --gpus N  --comm auto|rccl|loopback  --emits-per-line N  --max-key N  --ref-compat
+//   --sort radix|dict  --gpus N  --comm auto|rccl|loopback  --strategy auto|gather|shuffle
+//   --emits-per-line N  --max-key N  --ref-compat
 //   --stage map|reduce  --spill-dir DIR  --spill-format text|binary|kiv  --inputs a,b,...
 //   --export-kiv FILE (results as the reference's 40-B KeyIntValuePair records)
 //   --warmup N  --iters N  --json FILE  --quiet  --check  --device N  --chunk-mb N
@@ -45,6 +46,7 @@ struct CliArgs {
   int gpus = 1;
   bool gpus_given = false;   // --gpus on the command line (even --gpus 1: RCCL rank)
   LocalComm comm = LocalComm::kAuto;
+  DistStrategy strategy = DistStrategy::kAuto;  // --gpus N: after-map strategy (--strategy)
   std::string spill_dir = "/tmp";
   SpillFormat spill_fmt = SpillFormat::kText;
   std::vector<std::string> inputs;
@@ -98,6 +100,11 @@ bool parse(int argc, char** argv, CliArgs* a) {
       const std::string v = need("--comm");
       a->comm = v == "rccl" ? LocalComm::kRccl : v == "loopback" ? LocalComm::kLoopback
                                                                : LocalComm::kAuto;
+    } else if (s == "--strategy") {
+      const std::string v = need("--strategy");
+      if (v != "auto" && v != "gather" && v != "shuffle") throw Error("--strategy auto|gather|shuffle");
+      a->strategy = v == "gather" ? DistStrategy::kGather : v == "shuffle" ? DistStrategy::kShuffle
+                                                                          : DistStrategy::kAuto;
     } else if (s == "--device") {
       a->cfg.device = std::atoi(need("--device").c_str());
     } else if (s == "--emits-per-line") {
@@ -227,6 +234,15 @@ void json_counts(JsonOut& j, const WordCountResult& r) {
   j.u("max_key_len", r.max_key_len);
 }
 
+// Where a one-shot single-GPU run's time goes, main() to the JSON line (run_direct):
+// runtime init (the first HIP call), engine construction (code objects, device arena,
+// pinned buffers), the file read, the first job, later jobs and the formatted output.
+// Process start to main() (loader, static init) is the caller's wall clock minus these.
+struct Startup {
+  u64 main = 0, init = 0, engine = 0, read = 0, first = 0, jobs = 0, out = 0;
+};
+Startup g_startup;
+
 void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
   if (a.json.empty()) return;
   std::vector<double> w = walls;
@@ -248,6 +264,20 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
   // peak resident memory of this process image (VmHWM: unlike getrusage's ru_maxrss it is
   // not inherited through the fork + exec that started us)
   j.u("max_rss_kb", peak_rss_kb());
+  if (g_startup.init) {
+    const Startup& t = g_startup;
+    const u64 end = now_ns();
+    auto ms = [](u64 a0, u64 a1) { return a1 > a0 ? (a1 - a0) * 1e-6 : 0.0; };
+    JsonOut st;
+    st.num("runtime_init_ms", ms(t.main, t.init));
+    st.num("engine_ms", ms(t.init, t.engine));
+    st.num("read_ms", ms(t.engine, t.read));
+    st.num("first_job_ms", ms(t.read, t.first));
+    st.num("later_jobs_ms", ms(t.first, t.jobs));
+    st.num("output_ms", ms(t.jobs, end));
+    st.num("main_to_json_ms", ms(t.main, end));
+    j.kv("startup", st.done());
+  }
   emit_json(a, j.done());
 }
 
@@ -342,6 +372,7 @@ void print_gpu_result(const CliArgs& a, const WordCountResult& r, const std::vec
   if (!a.quiet) format_gpu_output(r, &out);
   std::fflush(stdout);
   write_all(stdout, out);
+  std::fflush(stdout);
   write_json(a, r, walls);
   if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r);
   std::printf("\nDone\n");
@@ -379,28 +410,40 @@ int run_direct(const CliArgs& a) {
   WordCountResult r;
   std::vector<double> walls;
   LOCUST_LOG_INFO("rss before the engine: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+  Startup& st = g_startup;
+  (void)visible_device_count();  // the HIP runtime's own start-up, timed apart
+  st.init = now_ns();
   if (size > chunk) {
     cfg.chunk_bytes = chunk;
     GpuWordCount eng(cfg, size, size);
+    st.engine = st.read = now_ns();  // the file is read by the job, piece by piece
     LOCUST_LOG_INFO("rss with the streaming engine: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
     for (int i = 0; i < a.warmup + a.iters; ++i) {
       auto src = open_file_source(a.file);
       r = eng.run_source(*src);
       if (i >= a.warmup) walls.push_back(r.times.wall_ms);
+      if (i == 0) st.first = now_ns();
     }
   } else {
     GpuWordCount eng(cfg, std::max<u64>(size, 1), std::max<u64>(size, 1));
+    st.engine = now_ns();
     TextInput in;
     in.data = eng.input_buffer();
     in.bytes = read_file_into(a.file, eng.input_buffer(), std::max<u64>(size, 1), &in.num_lines);
     in.first_line = 0;
-    for (int i = 0; i < a.warmup; ++i) eng.run(in);
-    for (int i = 0; i < a.iters; ++i) {
-      r = eng.run(in);
-      walls.push_back(r.times.wall_ms);
+    st.read = now_ns();
+    for (int i = 0; i < a.warmup + a.iters; ++i) {
+      if (i < a.warmup) {
+        eng.run(in);
+      } else {
+        r = eng.run(in);
+        walls.push_back(r.times.wall_ms);
+      }
+      if (i == 0) st.first = now_ns();
     }
     r.num_lines = in.num_lines;
   }
+  st.jobs = now_ns();
   LOCUST_LOG_INFO("rss after the job: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
   std::printf("Length: %i\n", (int)r.num_lines);
   print_gpu_result(a, r, walls);
@@ -486,6 +529,7 @@ int run(const CliArgs& a) {
     // gather slots move one record per distinct key instead of one per token)
     dc.job.combine = true;
     dc.world = std::max(1, a.gpus);
+    dc.strategy = a.strategy;
     LOCUST_LOG_INFO("%d ranks in one process over %s", dc.world,
                     resolve_local_comm(dc, a.comm) == LocalComm::kRccl ? "an RCCL clique"
                                                                        : "loopback");
@@ -578,6 +622,7 @@ int run(const CliArgs& a) {
 
 int main(int argc, char** argv) {
   // before any thread or RCCL use (see locust_amd/__init__.py); a user's setting wins
+  g_startup.main = now_ns();
   setenv("NCCL_GRAPH_REGISTER", "0", 0);
   std::printf("Running\n");
   CliArgs a;

@@ -10,12 +10,17 @@
 // ncclAllGather enqueued on the engine's own stream right behind the map (no host round
 // trip; allgather_device).  Every wait polls ncclCommGetAsyncError with a timeout and
 // aborts the communicator instead of hanging.
+//
+// RCCL is loaded on first use (dlopen), not linked: a single-GPU job -- the CLI's default,
+// the headline bench -- never maps librccl.so and its code objects.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <atomic>
 #include <cstdlib>
 #include <memory>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "locust/dist.hpp"
@@ -27,12 +32,50 @@
     ncclResult_t _r = (expr);                                                          \
     if (_r != ncclSuccess)                                                             \
       ::locust::throw_error(__FILE__, __LINE__,                                        \
-                            std::string("RCCL error: ") + ncclGetErrorString(_r) +     \
+                            std::string("RCCL error: ") + rccl().GetErrorString(_r) +  \
                                 " in `" #expr "`");                                    \
   } while (0)
 
 namespace locust {
 namespace {
+
+// The RCCL entry points this communicator uses, resolved from librccl on first use.
+struct RcclApi {
+#define LOCUST_RCCL_FNS(X)                                                            \
+  X(GetErrorString) X(GetUniqueId) X(CommInitRank) X(CommInitAll) X(CommAbort)         \
+  X(CommDestroy) X(CommCount) X(CommGetAsyncError) X(AllGather) X(AllToAll)           \
+  X(Send) X(Recv) X(GroupStart) X(GroupEnd)
+#define LOCUST_RCCL_PTR(name) decltype(&nccl##name) name = nullptr;
+  LOCUST_RCCL_FNS(LOCUST_RCCL_PTR)
+#undef LOCUST_RCCL_PTR
+  void* lib = nullptr;
+};
+
+const RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  static std::string err;
+  std::call_once(once, [] {
+    // the soname first (ld.so.cache / LD_LIBRARY_PATH), then the ROCm install itself
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+      api.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (api.lib) break;
+    }
+    if (!api.lib) {
+      const char* e = dlerror();
+      err = std::string("cannot load librccl.so: ") + (e ? e : "not found");
+      return;
+    }
+#define LOCUST_RCCL_SYM(name)                                                          \
+  api.name = reinterpret_cast<decltype(api.name)>(dlsym(api.lib, "nccl" #name));        \
+  if (!api.name && err.empty()) err = "librccl.so lacks nccl" #name;
+    LOCUST_RCCL_FNS(LOCUST_RCCL_SYM)
+#undef LOCUST_RCCL_SYM
+    if (err.empty()) LOCUST_LOG_DEBUG("RCCL loaded on first use");
+  });
+  if (!err.empty()) throw Error(err);
+  return api;
+}
 
 class RcclComm final : public Communicator {
  public:
@@ -42,7 +85,7 @@ class RcclComm final : public Communicator {
     tcp_ = make_tcp_comm(rank, world, host, port, timeout_s, listen_fd);
     group_ = tcp_->group_id();
     ncclUniqueId id;
-    if (rank == 0) LOCUST_RCCL_CHECK(ncclGetUniqueId(&id));
+    if (rank == 0) LOCUST_RCCL_CHECK(rccl().GetUniqueId(&id));
     std::vector<ncclUniqueId> ids((size_t)world);
     tcp_->allgather_host(&id, ids.data(), sizeof(id));
     id = ids[0];
@@ -54,7 +97,7 @@ class RcclComm final : public Communicator {
     // buffers instead of IPC-registering our slot buffers; log what is in effect.
     LOCUST_LOG_DEBUG("rccl rank %d/%d on device %d, NCCL_GRAPH_REGISTER=%s", rank, world,
         device, std::getenv("NCCL_GRAPH_REGISTER") ? std::getenv("NCCL_GRAPH_REGISTER") : "(unset)");
-    LOCUST_RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    LOCUST_RCCL_CHECK(rccl().CommInitRank(&comm_, world, id, rank));
     stage_cap_ = 1 << 20;
     LOCUST_HIP_CHECK(hipMalloc(&d_stage_, stage_cap_ * (u64)(world + 1)));
     LOCUST_HIP_CHECK(hipHostMalloc(&h_stage_, stage_cap_ * (u64)(world + 1), hipHostMallocDefault));
@@ -76,9 +119,9 @@ class RcclComm final : public Communicator {
   ~RcclComm() override {
     if (comm_) {
       if (aborted_)
-        (void)ncclCommAbort(comm_);
+        (void)rccl().CommAbort(comm_);
       else
-        (void)ncclCommDestroy(comm_);
+        (void)rccl().CommDestroy(comm_);
     }
     if (d_stage_) (void)hipFree(d_stage_);
     if (h_stage_) (void)hipHostFree(h_stage_);
@@ -92,7 +135,7 @@ class RcclComm final : public Communicator {
   const char* name() const override { return "rccl"; }
   int comm_count() const override {
     int n = -1;
-    return ncclCommCount(comm_, &n) == ncclSuccess ? n : -1;
+    return rccl().CommCount(comm_, &n) == ncclSuccess ? n : -1;
   }
   bool device_buffers() const override { return true; }
   u64 group_id() const override { return group_; }
@@ -105,7 +148,7 @@ class RcclComm final : public Communicator {
     char* hsend = h_stage_ + (u64)world_ * stage_cap_;
     std::memcpy(hsend, send, bytes);
     LOCUST_HIP_CHECK(hipMemcpyAsync(dsend, hsend, bytes, hipMemcpyHostToDevice, stream_));
-    LOCUST_RCCL_CHECK(ncclAllGather(dsend, d_stage_, bytes, ncclUint8, comm_, stream_));
+    LOCUST_RCCL_CHECK(rccl().AllGather(dsend, d_stage_, bytes, ncclUint8, comm_, stream_));
     LOCUST_HIP_CHECK(hipMemcpyAsync(h_stage_, d_stage_, bytes * (u64)world_,
                                     hipMemcpyDeviceToHost, stream_));
     wait(stream_);
@@ -135,18 +178,18 @@ class RcclComm final : public Communicator {
       for (int r = 0; r < root; ++r) off += sizes[r];
       LOCUST_HIP_CHECK(hipMemcpyAsync(d_grecv_ + off, d_gsend_, bytes, hipMemcpyDeviceToDevice, stream_));
     }
-    LOCUST_RCCL_CHECK(ncclGroupStart());
+    LOCUST_RCCL_CHECK(rccl().GroupStart());
     if (rank_ == root) {
       u64 off = 0;
       for (int r = 0; r < world_; ++r) {
         if (r != root && sizes[r])
-          LOCUST_RCCL_CHECK(ncclRecv(d_grecv_ + off, sizes[r], ncclUint8, r, comm_, stream_));
+          LOCUST_RCCL_CHECK(rccl().Recv(d_grecv_ + off, sizes[r], ncclUint8, r, comm_, stream_));
         off += sizes[r];
       }
     } else if (bytes) {
-      LOCUST_RCCL_CHECK(ncclSend(d_gsend_, bytes, ncclUint8, root, comm_, stream_));
+      LOCUST_RCCL_CHECK(rccl().Send(d_gsend_, bytes, ncclUint8, root, comm_, stream_));
     }
-    LOCUST_RCCL_CHECK(ncclGroupEnd());
+    LOCUST_RCCL_CHECK(rccl().GroupEnd());
     if (rank_ == root && total)
       LOCUST_HIP_CHECK(hipMemcpyAsync(recv_at_root, d_grecv_, total, hipMemcpyDeviceToHost, stream_));
     wait(stream_);
@@ -160,13 +203,13 @@ class RcclComm final : public Communicator {
 
   void allgather_device(const void* send, void* recv, u64 bytes, void* stream) override {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
-    LOCUST_RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
+    LOCUST_RCCL_CHECK(rccl().AllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
 
   // ncclAllToAll: every peer's chunk over its own xGMI link at once (no ring).
   void alltoall_device(const void* send, void* recv, u64 bytes, void* stream) override {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
-    LOCUST_RCCL_CHECK(ncclAllToAll(send, recv, bytes, ncclUint8, comm_, s));
+    LOCUST_RCCL_CHECK(rccl().AllToAll(send, recv, bytes, ncclUint8, comm_, s));
   }
 
   // Root receives every other rank's chunk (grouped point-to-point: P-1 links in
@@ -174,16 +217,16 @@ class RcclComm final : public Communicator {
   void gather_device(const void* send, void* recv, u64 bytes, int root, void* stream) override {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : stream_;
     if (world_ == 1 || !bytes) return;
-    LOCUST_RCCL_CHECK(ncclGroupStart());
+    LOCUST_RCCL_CHECK(rccl().GroupStart());
     if (rank_ == root) {
       for (int r = 0; r < world_; ++r)
         if (r != root)
-          LOCUST_RCCL_CHECK(ncclRecv(static_cast<char*>(recv) + (u64)r * bytes, bytes, ncclUint8,
+          LOCUST_RCCL_CHECK(rccl().Recv(static_cast<char*>(recv) + (u64)r * bytes, bytes, ncclUint8,
                                      r, comm_, s));
     } else {
-      LOCUST_RCCL_CHECK(ncclSend(send, bytes, ncclUint8, root, comm_, s));
+      LOCUST_RCCL_CHECK(rccl().Send(send, bytes, ncclUint8, root, comm_, s));
     }
-    LOCUST_RCCL_CHECK(ncclGroupEnd());
+    LOCUST_RCCL_CHECK(rccl().GroupEnd());
   }
 
   void sync_stream(void* stream) override {
@@ -200,15 +243,15 @@ class RcclComm final : public Communicator {
     if (send_bytes[rank_])
       LOCUST_HIP_CHECK(hipMemcpyAsync(rb + recv_off[rank_], sb + send_off[rank_], send_bytes[rank_],
                                       hipMemcpyDeviceToDevice, s));
-    LOCUST_RCCL_CHECK(ncclGroupStart());
+    LOCUST_RCCL_CHECK(rccl().GroupStart());
     for (int p = 0; p < world_; ++p) {
       if (p == rank_) continue;
       if (send_bytes[p])
-        LOCUST_RCCL_CHECK(ncclSend(sb + send_off[p], send_bytes[p], ncclUint8, p, comm_, s));
+        LOCUST_RCCL_CHECK(rccl().Send(sb + send_off[p], send_bytes[p], ncclUint8, p, comm_, s));
       if (recv_bytes[p])
-        LOCUST_RCCL_CHECK(ncclRecv(rb + recv_off[p], recv_bytes[p], ncclUint8, p, comm_, s));
+        LOCUST_RCCL_CHECK(rccl().Recv(rb + recv_off[p], recv_bytes[p], ncclUint8, p, comm_, s));
     }
-    LOCUST_RCCL_CHECK(ncclGroupEnd());
+    LOCUST_RCCL_CHECK(rccl().GroupEnd());
     wait(s);
   }
 
@@ -222,15 +265,15 @@ class RcclComm final : public Communicator {
       LOCUST_HIP_CHECK(hipMemcpyAsync(rb + recv_off[rank_], sb + send_off[rank_], send_bytes[rank_],
                                       hipMemcpyDeviceToDevice, s));
     if (world_ == 1) return;
-    LOCUST_RCCL_CHECK(ncclGroupStart());
+    LOCUST_RCCL_CHECK(rccl().GroupStart());
     for (int p = 0; p < world_; ++p) {
       if (p == rank_) continue;
       if (send_bytes[p])
-        LOCUST_RCCL_CHECK(ncclSend(sb + send_off[p], send_bytes[p], ncclUint8, p, comm_, s));
+        LOCUST_RCCL_CHECK(rccl().Send(sb + send_off[p], send_bytes[p], ncclUint8, p, comm_, s));
       if (recv_bytes[p])
-        LOCUST_RCCL_CHECK(ncclRecv(rb + recv_off[p], recv_bytes[p], ncclUint8, p, comm_, s));
+        LOCUST_RCCL_CHECK(rccl().Recv(rb + recv_off[p], recv_bytes[p], ncclUint8, p, comm_, s));
     }
-    LOCUST_RCCL_CHECK(ncclGroupEnd());
+    LOCUST_RCCL_CHECK(rccl().GroupEnd());
   }
 
  private:
@@ -268,10 +311,10 @@ class RcclComm final : public Communicator {
       if (e == hipSuccess) return;
       if (e != hipErrorNotReady) LOCUST_HIP_CHECK(e);
       ncclResult_t ae = ncclSuccess;
-      LOCUST_RCCL_CHECK(ncclCommGetAsyncError(comm_, &ae));
+      LOCUST_RCCL_CHECK(rccl().CommGetAsyncError(comm_, &ae));
       if (ae != ncclSuccess && ae != ncclInProgress) {
         aborted_ = true;
-        throw Error(std::string("RCCL async error: ") + ncclGetErrorString(ae));
+        throw Error(std::string("RCCL async error: ") + rccl().GetErrorString(ae));
       }
       if (now_ns() > deadline) {
         aborted_ = true;
@@ -315,7 +358,7 @@ std::vector<RcclCliqueMember> make_rccl_clique(const std::vector<int>& devices) 
   LOCUST_CHECK_ARG(n >= 1, "empty device list");
   std::vector<ncclComm_t> comms((size_t)n, nullptr);
   // one process, one communicator per device: RCCL wires the clique over xGMI itself
-  LOCUST_RCCL_CHECK(ncclCommInitAll(comms.data(), n, devices.data()));
+  LOCUST_RCCL_CHECK(rccl().CommInitAll(comms.data(), n, devices.data()));
   std::vector<RcclCliqueMember> out((size_t)n);
   auto abort = std::make_shared<std::atomic<bool>>(false);
   const u64 group = new_group_token();
@@ -338,7 +381,7 @@ std::unique_ptr<Communicator> make_rccl_clique_comm(const RcclCliqueMember& m, d
 
 void release_rccl_clique_member(RcclCliqueMember& m) {
   if (!m.handle) return;
-  (void)ncclCommAbort(static_cast<ncclComm_t>(m.handle));
+  (void)rccl().CommAbort(static_cast<ncclComm_t>(m.handle));
   m.handle = nullptr;
 }
 

@@ -1,6 +1,7 @@
 // Distributed WordCount driver (backend-agnostic: any Communicator x any ShardEngine).
 // See locust/dist.hpp for the stage list and SURVEY.md §2.4/§5.8 for the design.
 #include "locust/dist.hpp"
+#include "locust/numa.hpp"
 #include "locust/trace.hpp"
 
 #include <algorithm>
@@ -361,6 +362,13 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   const bool dev_exch = exch_enabled() && cfg.gather && cfg.job.combine && comm.device_buffers() &&
                         eng.device_buffers() && eng.exch_group != 0 && S == kExchSamples &&
                         (u32)P <= kExchMaxRanks && (u32)P * S <= kExchMaxPlanSamples;
+  if (dev_exch && eng.exch_numa_nodes.size() != (size_t)P) {
+    // once per engine, before its first shared output exists: every rank's GPU node
+    const int mine = numa_enabled() ? eng.numa_node() : -1;
+    std::vector<int> nodes((size_t)P, -1);
+    comm.allgather_host(&mine, nodes.data(), sizeof(int));
+    eng.exch_numa_nodes = nodes;
+  }
   if (dev_exch) {
     TraceRange tr("locust:device_exchange");
     bool one_sync = !mapped && eng.exch_slot_records && eng.exch_gather_records &&

@@ -5,6 +5,9 @@
 #include <mutex>
 #include <thread>
 
+#include <sys/mman.h>
+
+#include "locust/numa.hpp"
 #include "locust/shm.hpp"
 #include "pipeline.hpp"
 
@@ -1206,13 +1209,23 @@ class GpuShardEngine final : public ShardEngine {
   // that are threads of one process (the CLI's clique, loopback rehearsals) share one
   // pinned allocation instead (hipHostMalloc Portable | Mapped: GPU writes to it ran at
   // ~48 GB/s where the registered 4 KiB shm pages gave ~35).
+  // Ranks spanning NUMA nodes: the block is mapped memory whose slices are bound to their
+  // ranks' nodes before the first touch (plan_rank_slices), then registered.
   struct PinnedBlock {
     char* p = nullptr;
+    u64 mapped = 0;  // > 0: mmap'ed + hipHostRegister'ed (NUMA-placed), else hipHostMalloc
     ~PinnedBlock() {
-      if (p) (void)hipHostFree(p);
+      if (!p) return;
+      if (mapped) {
+        (void)hipHostUnregister(p);
+        ::munmap(p, mapped);
+      } else {
+        (void)hipHostFree(p);
+      }
     }
   };
-  static std::shared_ptr<PinnedBlock> shared_block(const std::string& name, u64 bytes) {
+  static std::shared_ptr<PinnedBlock> shared_block(const std::string& name, u64 bytes,
+                                                   const std::vector<NumaSlice>& plan) {
     static std::mutex mu;
     static std::map<std::string, std::weak_ptr<PinnedBlock>> reg;
     std::lock_guard<std::mutex> lk(mu);
@@ -1220,12 +1233,33 @@ class GpuShardEngine final : public ShardEngine {
       it = it->second.expired() ? reg.erase(it) : std::next(it);
     if (auto b = reg[name].lock()) return b;
     auto b = std::make_shared<PinnedBlock>();
-    LOCUST_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b->p), bytes,
-                                   hipHostMallocPortable | hipHostMallocMapped |
-                                       hipHostMallocCoherent));
-    std::memset(b->p, 0, kShmHeaderBytes);  // the stamps
+    if (!plan.empty()) {
+      void* p = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (p == MAP_FAILED) throw Error("shared output: mmap of " + std::to_string(bytes) + " B failed");
+      b->p = static_cast<char*>(p);
+      b->mapped = bytes;
+      (void)::madvise(p, bytes, MADV_HUGEPAGE);  // fewer GPU-side translations
+      place_slices(p, plan);
+      std::memset(p, 0, bytes);  // first touch: every page on its slice's node
+      LOCUST_HIP_CHECK(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    } else {
+      LOCUST_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b->p), bytes,
+                                     hipHostMallocPortable | hipHostMallocMapped |
+                                         hipHostMallocCoherent));
+      std::memset(b->p, 0, kShmHeaderBytes);  // the stamps
+    }
     reg[name] = b;
     return b;
+  }
+  int numa_node_ = -2;
+  int numa_node() override {
+    if (numa_node_ == -2) {
+      char bdf[64] = {0};
+      numa_node_ = hipDeviceGetPCIBusId(bdf, (int)sizeof(bdf), cfg_.device) == hipSuccess
+                       ? placement_for_bdf(bdf).numa_node
+                       : -1;
+    }
+    return numa_node_;
   }
   struct OutSegment {
     ShmSegment seg;                       // processes
@@ -1270,13 +1304,17 @@ class GpuShardEngine final : public ShardEngine {
     auto o = std::make_shared<OutSegment>();
     const std::string name = shm_segment_name(out_group_, next_segment_gen(out_group_, exch_rank));
     const u64 bytes = shm_segment_bytes(R * K, sizeof(OutRecord));
+    // pages on the node of the rank whose key range lands there (locust/numa.hpp)
+    std::vector<NumaSlice> plan;
+    if (spans_numa_nodes(exch_numa_nodes))
+      plan = plan_rank_slices(kShmHeaderBytes, R * sizeof(OutRecord), K, exch_numa_nodes);
     char* d = nullptr;
     if (exch_in_process) {
-      o->block = shared_block(name, bytes);
+      o->block = shared_block(name, bytes, plan);
       o->base = o->block->p;
       LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), o->base, 0));
     } else {
-      o->seg.open(name, bytes);
+      o->seg.open(name, bytes, plan.empty() ? nullptr : &plan);
       LOCUST_HIP_CHECK(hipHostRegister(o->seg.data(), o->seg.bytes(),
                                        hipHostRegisterMapped | hipHostRegisterPortable));
       o->registered = true;

@@ -52,7 +52,7 @@ u64 new_group_token() {
   return x ? x : 1;
 }
 
-void ShmSegment::open(const std::string& name, u64 bytes) {
+void ShmSegment::open(const std::string& name, u64 bytes, const std::vector<NumaSlice>* plan) {
   close();
   LOCUST_CHECK_ARG(bytes >= kShmHeaderBytes && bytes % 4096 == 0, "shm segment: bad size");
   const int fd = ::shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
@@ -68,18 +68,24 @@ void ShmSegment::open(const std::string& name, u64 bytes) {
                   " B failed: " + std::strerror(e));
     }
   }
+  void* p = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    const int e = errno;
+    ::close(fd);
+    throw Error("shm segment " + name + ": mmap failed: " + std::strerror(e));
+  }
+  // NUMA slices first: shmem keeps them as the object's policy, so the reservation below
+  // (whichever rank gets there first) already allocates each page on its slice's node
+  if (plan && !plan->empty()) place_slices(p, *plan);
   // reserve the pages now: a full /dev/shm (a container's default is 64 MiB) is a clean
   // error here rather than a SIGBUS at the first write
   const int fe = ::posix_fallocate(fd, 0, (off_t)bytes);
+  ::close(fd);
   if (fe != 0 && fe != EOPNOTSUPP && fe != EINVAL) {
-    ::close(fd);
+    ::munmap(p, bytes);
     throw Error("shm segment " + name + ": cannot reserve " + std::to_string(bytes >> 20) +
                 " MiB in /dev/shm: " + std::strerror(fe));
   }
-  void* p = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  ::close(fd);
-  if (p == MAP_FAILED)
-    throw Error("shm segment " + name + ": mmap failed: " + std::strerror(errno));
   base_ = static_cast<char*>(p);
   bytes_ = bytes;
   name_ = name;

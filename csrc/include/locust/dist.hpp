@@ -321,6 +321,10 @@ class ShardEngine {
   u64 exch_group = 0;     // the communicator's group id (names the shared output)
   int exch_rank = 0;      // this rank in that group
   bool exch_in_process = false;  // every rank of the group is a thread of this process
+  // NUMA node of every rank's GPU (all-gathered once per engine; -1: unknown): places the
+  // shared output's pages (locust/numa.hpp plan_rank_slices)
+  std::vector<int> exch_numa_nodes;
+  virtual int numa_node() { return -1; }  // this engine's GPU's node
   // Hands this rank's entries over (the caller sets the result's val_base).
   virtual void finalize(EntryList* out) = 0;
   // Map-stage counters of the last map_local.

@@ -18,6 +18,9 @@
 #pragma once
 
 #include <string>
+#include <vector>
+
+#include "locust/numa.hpp"
 
 #include "locust/common.hpp"
 
@@ -34,7 +37,9 @@ class ShmSegment {
   ~ShmSegment() { close(); }
 
   // Create-or-open `name` with `bytes` (every opener passes the same size) and map it.
-  void open(const std::string& name, u64 bytes);
+  // `plan` (optional): NUMA slices applied to the mapping before its pages are reserved
+  // (locust/numa.hpp place_slices; every opener passes the same plan).
+  void open(const std::string& name, u64 bytes, const std::vector<NumaSlice>* plan = nullptr);
   // Remove the name (mappings stay valid); idempotent, and a name another rank removed
   // first is not an error.
   void unlink();

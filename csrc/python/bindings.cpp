@@ -8,6 +8,7 @@
 
 #include <cstring>
 #include <string>
+#include <tuple>
 
 #include "locust/devcache.hpp"
 #include "locust/dist.hpp"
@@ -622,6 +623,30 @@ PYBIND11_MODULE(_locust, m) {
     return py::make_tuple(pl.bdf, pl.numa_node, pl.cpus);
   }, py::arg("bdf"), py::arg("sys_root") = "/sys");
   m.def("parse_cpulist", &parse_cpulist);
+  m.def("plan_rank_slices", [](u64 header, u64 region, u32 regions, const std::vector<int>& nodes,
+                               u64 page) {
+    py::list out;
+    for (const auto& s : plan_rank_slices(header, region, regions, nodes, page))
+      out.append(py::make_tuple(s.offset, s.bytes, s.node));
+    return out;
+  }, py::arg("header"), py::arg("region"), py::arg("regions"), py::arg("nodes"),
+        py::arg("page") = 4096, "NUMA slices (offset, bytes, node) of a shared output segment");
+  m.def("spans_numa_nodes", &spans_numa_nodes);
+  // A shm segment placed by `plan` ([(offset, bytes, node)]): returns the node of each
+  // page's first byte after the segment was reserved and touched (-1: unknown).
+  m.def("shm_placement_probe", [](u64 bytes, const std::vector<std::tuple<u64, u64, int>>& plan) {
+    std::vector<NumaSlice> pl;
+    for (const auto& t : plan) pl.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t)});
+    ShmSegment seg;
+    seg.open(shm_segment_name(new_group_token(), 1), align_up(bytes, 4096), &pl);
+    std::vector<int> nodes;
+    for (u64 o = 0; o < seg.bytes(); o += 4096) {
+      seg.data()[o] = 1;
+      nodes.push_back(page_node(seg.data() + o));
+    }
+    seg.close();
+    return nodes;
+  }, py::arg("bytes"), py::arg("plan"));
   // the shared output segment (locust/shm.hpp), for host-side tests
   py::class_<ShmSegment>(m, "ShmSegment")
       .def(py::init([](const std::string& name, u64 bytes) {

@@ -4,6 +4,7 @@ locations`, `Length:`, `GPU mapping|stream compaction and sorting|reduce ... nan
 `print key: %s \\t val: %d \\t count: %d`, `Done`), both reduce paths, the stage split on
 the GPU and the in-process multi-rank mode (`--gpus N`: an RCCL clique when the node has
 N GPUs, loopback ranks otherwise)."""
+import os
 import re
 import subprocess
 
@@ -159,3 +160,16 @@ def test_multi_rank_cli_first_job_on_device(tmp_path, cli, gpus):
         assert rk["device_exchange"] is True and 1 <= rk["host_syncs"] <= 2, rk
         assert rk["output_bytes"] == rk["range_unique"] * 40
     assert sum(rk["range_unique"] for rk in rec["ranks"]) == want.num_unique
+
+
+@pytest.mark.gpu
+def test_single_gpu_cli_never_loads_rccl(cli):
+    """RCCL is dlopen'ed on first use (csrc/comm/rccl_comm.hip): a single-GPU job maps
+    neither librccl nor its code objects.  LD_DEBUG=files lists every
+    library the dynamic loader opens, including dlopen'ed ones."""
+    env = dict(os.environ, LD_DEBUG="files")
+    p = subprocess.run([cli, "data/hamlet.txt"], capture_output=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    assert b"Done" in p.stdout or b"print key" in p.stdout
+    assert b"libamdhip64" in p.stderr  # LD_DEBUG did report the loads
+    assert b"librccl" not in p.stderr

@@ -91,4 +91,9 @@ def test_gpu_ranks_file_shards(tmp_path, cli, gpus, chunk_mb):
     rec = json.loads(j.read_text())
     assert sum(r["input_bytes"] for r in rec["ranks"]) == os.path.getsize(f)
     assert all(r["input_streamed"] == bool(chunk_mb) for r in rec["ranks"]), rec["ranks"]
-    assert rec["peak_rss_kb"] < (1 << 21)  # < 2 GiB, never the whole file per rank
+    # streamed ranks hold their rings, never their ranges; one-pass ranks hold their own
+    # range once each (the process baseline -- HIP runtime, code objects -- is ~0.5-1 GiB)
+    size_kb = os.path.getsize(f) >> 10
+    bound = (1 << 21) if chunk_mb else (1 << 21) + size_kb
+    print(f"--gpus {gpus} chunk {chunk_mb} MB: peak RSS {rec['peak_rss_kb']} kB")
+    assert rec["peak_rss_kb"] < bound

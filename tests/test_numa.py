@@ -75,3 +75,43 @@ def test_cpp_placement(tmp_path):
     assert lc._C.gpu_placement("0000:ff:00.0", sysr)[1] == -1
     assert lc._C.parse_cpulist("1-3,9") == [1, 2, 3, 9]
     assert lc._C.parse_cpulist("x") == []
+
+
+# ---- page placement of the shared distributed output ----
+def test_rank_slices_plan():
+    # 4 ranks on two sockets (0, 0, 1, 1): per region, the first half of the pages on node 0
+    # (ranks 0-1, merged), the second half on node 1; the header page with rank 0
+    hdr, region = 4096, 1_000_000 * 40
+    plan = lc._C.plan_rank_slices(hdr, region, 2, [0, 0, 1, 1])
+    assert plan[0] == (0, 4096 + ((region // 2 + 4095) // 4096) * 4096, 0)
+    pos = 0
+    for off, n, node in plan:  # contiguous, page-aligned, alternating nodes
+        assert off == pos and off % 4096 == 0 and n % 4096 == 0 and n > 0
+        pos += n
+    assert pos == ((hdr + 2 * region + 4095) // 4096) * 4096
+    assert [node for _o, _n, node in plan] == [0, 1, 0, 1]
+    # the seam of region 0 lies at its middle, rounded up to a page
+    assert plan[1][0] == ((hdr + region // 2 + 4095) // 4096) * 4096
+    # unknown nodes leave their slices to the default policy; one node: nothing to place
+    assert [s[2] for s in lc._C.plan_rank_slices(hdr, region, 1, [0, -1, 1, 1])] == [0, 1]
+    assert lc._C.spans_numa_nodes([0, 1]) and not lc._C.spans_numa_nodes([0, 0, -1])
+    # eight ranks, one node each: slice p of every region on node p
+    p8 = lc._C.plan_rank_slices(hdr, 8 * 4096 * 10, 3, list(range(8)))
+    assert [s[2] for s in p8] == [0] + list(range(1, 8)) + list(range(8)) * 2
+
+
+def test_shm_segment_placed_before_reserve(capfd):
+    """The plan is applied to the mapping before posix_fallocate reserves the pages (shmem
+    keeps it as the object's policy): every page lands on its slice's node.  This box has
+    node 0 only, so the plan binds everything there and a slice naming an absent node is
+    logged and skipped, not fatal."""
+    os.environ["LOCUST_LOG"] = "info"
+    try:
+        nodes = lc._C.shm_placement_probe(64 * 4096, [(0, 32 * 4096, 0), (32 * 4096, 32 * 4096, 0)])
+        assert nodes == [0] * 64
+        assert "preferred on NUMA node 0" in capfd.readouterr().err
+        nodes = lc._C.shm_placement_probe(8 * 4096, [(0, 8 * 4096, 1000)])
+        assert len(nodes) == 8
+        assert "to NUMA node 1000 failed" in capfd.readouterr().err
+    finally:
+        os.environ.pop("LOCUST_LOG", None)
