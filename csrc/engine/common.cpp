@@ -135,15 +135,18 @@ void entries_from_sorted_tokens(const PackedKey* sorted, u64 n, std::vector<Word
 // counts sum to the token count.  (Runs are contiguous by construction: val is the
 // prefix of the counts, EntryVals.)
 void validate_result(const WordCountResult& r) {
-  u64 sum = 0;
-  for (size_t j = 0; j < r.entries.size(); ++j) {
-    const auto& e = r.entries[j];
-    if (j && key_compare(r.entries[j - 1].key.w, e.key.w) >= 0)
+  u64 sum = 0, j = 0;
+  PackedKey prev{};
+  for (const WordCountEntry e : r.entries) {  // compact lists decode on the fly
+    if (j && key_compare(prev.w, e.key.w) >= 0)
       throw Error("LOCUST_CHECK: output keys not strictly increasing at entry " +
                   std::to_string(j));
     if (e.count == 0) throw Error("LOCUST_CHECK: zero count at entry " + std::to_string(j));
     sum += e.count;
+    prev = e.key;
+    ++j;
   }
+  if (j != r.entries.size()) throw Error("LOCUST_CHECK: entry count mismatch");
   if (sum != r.num_tokens)
     throw Error("LOCUST_CHECK: sum(count)=" + std::to_string(sum) +
                 " != num_tokens=" + std::to_string(r.num_tokens));

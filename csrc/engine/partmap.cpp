@@ -85,14 +85,13 @@ u32 assign(const std::vector<Group>& g, u64 target, u32 max_distinct, PartMapTab
 
 }  // namespace
 
-u64 part_map_from_entries(const WordCountEntry* e, size_t n, PartMapTables* t,
-                          u32 max_distinct) {
+u64 part_map_from_entries(const EntryList& entries, PartMapTables* t, u32 max_distinct) {
   part_map_default(t);
   std::vector<Group> g;
   u64 total = 0;
-  for (size_t i = 0; i < n; ++i) {
-    const u64 w0 = e[i].key.w[0];
-    const u64 work = e[i].count + kPartDistinctWeight;
+  for (const WordCountEntry e : entries) {  // compact lists decode on the fly
+    const u64 w0 = e.key.w[0];
+    const u64 work = e.count + kPartDistinctWeight;
     if (g.empty() || g.back().w0 != w0) g.push_back({w0, 0, 0});
     g.back().work += work;
     g.back().distinct += 1;

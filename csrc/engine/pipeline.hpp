@@ -225,6 +225,9 @@ struct DevicePipeline {
   SortPlan* h_plan = nullptr;
   OutRecord* h_out = nullptr;         // host-mapped output records
   OutRecord* d_out_mapped = nullptr;  // device view of h_out
+  u64* h_ctab = nullptr;              // its compact-output table (OrderedExtra::ctab)
+  u64* d_ctab_mapped = nullptr;
+  bool ord_compact = false;           // the last ordered launch wrote compact records
   MapCounters* h_ctr_mapped = nullptr;
   MapCounters* d_ctr_mapped = nullptr;
   // Lean jobs: completion word the last kernel publishes (host-mapped) and its sequence.
@@ -609,12 +612,16 @@ struct DevicePipeline {
     OutRecord* h = nullptr;
     OutRecord* d = nullptr;
     u64 cap = 0;
+    u64* ctab_h = nullptr;  // kDictParts words after the records: the compact table
+    u64* ctab_d = nullptr;
     // fine-grained: the kernels write it straight over PCIe (coarse-grained buffers
     // measured no faster, profiles/r1_s3/out_coherence_ab.txt)
     explicit HostOut(u64 n) : cap(std::max<u64>(n, 1)) {
-      LOCUST_HIP_CHECK(hipHostMalloc(&h, cap * sizeof(OutRecord),
+      LOCUST_HIP_CHECK(hipHostMalloc(&h, cap * sizeof(OutRecord) + kDictParts * sizeof(u64),
                                      hipHostMallocMapped | hipHostMallocCoherent));
       LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
+      ctab_h = reinterpret_cast<u64*>(h + cap);
+      ctab_d = reinterpret_cast<u64*>(d + cap);
     }
     ~HostOut() {
       if (h) (void)hipHostFree(h);
@@ -629,6 +636,8 @@ struct DevicePipeline {
     h_out = out_pool[i]->h;
     d_out_mapped = out_pool[i]->d;
     h_out_cap = out_pool[i]->cap;
+    h_ctab = out_pool[i]->ctab_h;
+    d_ctab_mapped = out_pool[i]->ctab_d;
   }
   // Before a job writes the mapped output: a buffer no earlier result still holds.
   void select_out() {
@@ -850,6 +859,7 @@ struct DevicePipeline {
     hipGraphExec_t exec;
     bool ordered;  // the captured job uses the ordered kernel
     bool clean;    // ... and re-zeroes its scratch (job_self_cleaned)
+    bool compact;  // ... writing compact records (ord_compact)
   };
   std::vector<DictGraph> dict_graphs;  // one per (input shape, output buffer)
   bool graph_ordered = false;          // the last launched graph uses the ordered kernel
@@ -922,11 +932,12 @@ struct DevicePipeline {
       hipGraphExec_t exec = nullptr;
       LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
       LOCUST_HIP_CHECK(hipGraphDestroy(g));
-      dict_graphs.push_back({key, exec, ordered, job_self_cleaned});
+      dict_graphs.push_back({key, exec, ordered, job_self_cleaned, ordered && ord_compact});
       hit = &dict_graphs.back();
     }
     graph_ordered = hit->ordered;
     job_self_cleaned = hit->clean;
+    ord_compact = hit->compact;
     if (cfg.sort_path == SortPath::kRadix) psort_used = hit->ordered;
     parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
     part_tiles = cfg.map_path != MapPath::kFast ? 0u : pieces.empty() ? table_tiles(in.bytes)
@@ -1254,7 +1265,8 @@ struct DevicePipeline {
   }
   // After an ordered run overflowed a partition (or the output): rebuild the map from the
   // fallback's output so the next job's partitions fit (kept if it would not help).
-  void force_retune(const WordCountEntry* e, u64 n) {
+  void force_retune(const EntryList& e) {
+    const u64 n = e.size();
     // a device-planned map overflowed: this engine keeps the host-side map from now on
     // (tuned from this output, or the default with tuning off) -- d_pmap holds the plan
     const bool planned = devplan_used;
@@ -1267,7 +1279,7 @@ struct DevicePipeline {
     PartMapTables t;
     u64 pred = 0;
     if (tune)
-      pred = part_map_from_entries(e, n, &t);
+      pred = part_map_from_entries(e, &t);
     else
       part_map_default(&t);
     // The same map again (e.g. one first word with more distinct keys than an LDS table:
@@ -1282,11 +1294,11 @@ struct DevicePipeline {
                                     stream));
     pm_predicted_max = pred;
   }
-  void maybe_retune(const WordCountEntry* e, u64 n) {
+  void maybe_retune(const EntryList& e) {
     if (const u64 mx = retune_wanted()) {
-      if (large_ordered && n > (1u << 16)) return retune_async(mx, e, n);
+      if (large_ordered && e.size() > (1u << 16)) return retune_async(mx, e);
       PartMapTables t;
-      retune_with(mx, part_map_from_entries(e, n, &t), t);
+      retune_with(mx, part_map_from_entries(e, &t), t);
     }
   }
   // A large output's map is built on a host thread (part_map_from_entries over 200K
@@ -1298,13 +1310,14 @@ struct DevicePipeline {
     PartMapTables t;
   };
   std::future<RetuneTask> retune_job;
-  void retune_async(u64 mx, const WordCountEntry* e, u64 n) {
+  void retune_async(u64 mx, const EntryList& e) {
     if (retune_job.valid()) return;  // one at a time
     std::shared_ptr<HostOut> hold = out_pool[out_idx];
-    retune_job = std::async(std::launch::async, [hold, mx, e, n] {
+    // a borrowed list: the copy shares the buffer (and its segments), not the entries
+    retune_job = std::async(std::launch::async, [hold, mx, e] {
       RetuneTask r;
       r.mx = mx;
-      r.pred = part_map_from_entries(e, n, &r.t);
+      r.pred = part_map_from_entries(e, &r.t);
       return r;
     });
   }
@@ -1344,7 +1357,7 @@ struct DevicePipeline {
       e[i].count = h[i].count;
     }
     PartMapTables t;
-    const u64 pred = part_map_from_entries(e.data(), n, &t);
+    const u64 pred = part_map_from_entries(EntryList(std::move(e)), &t);
     if (force && !planned && std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;  // as force_retune
     retune_with(mx, pred, t);
   }
@@ -1371,6 +1384,7 @@ struct DevicePipeline {
       done_pending = 0;
     }
     set_tile_source(ex, with_counts);
+    set_compact_out(ex, mapped);
     launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
                         cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
                         lb_dict, stream, ord_trace(), ex);
@@ -1535,6 +1549,7 @@ struct DevicePipeline {
       ex.pm = part_map();
       ex.part_w = d_pw;
       ex.out_cap = h_out_cap;
+      set_compact_out(ex, true);
       launch_dict_ordered_partials(d_partials, d_partial_n, partial_nslots, d_ctr, d_out_mapped,
                                    d_ctr_mapped,
                                    lb_dict, stream, ord_trace(), ex);
@@ -1616,13 +1631,39 @@ struct DevicePipeline {
     copy_out(r.entries, u);
   }
 
-  // Host output records -> result entries: identical 40-byte layouts, so the result
-  // simply adopts the buffer the device wrote (no copy; see select_out).
-  void copy_out(EntryList& e, u64 u) {
+  // An ordered launch writing the mapped output writes compact records (kv.hpp): the
+  // drain across PCIe shrinks from 40 B per entry to ~16-24 B.
+  void set_compact_out(OrderedExtra& ex, bool mapped) {
+    ord_compact = mapped;
+    if (!mapped) return;
+    ex.cout = reinterpret_cast<u64*>(d_out_mapped);
+    ex.ctab = d_ctab_mapped;
+    ex.out_cap = std::min<u64>(ex.out_cap, h_out_cap);
+  }
+
+  // Host output records -> result entries: the result simply adopts the buffer the device
+  // wrote (no copy; see select_out) -- 40-B records (the same layout as WordCountEntry),
+  // or with `compact` the ordered kernel's compact segments, one per virtual partition,
+  // listed in its table.
+  void copy_out(EntryList& e, u64 u, bool compact = false) {
     static_assert(sizeof(WordCountEntry) == sizeof(OutRecord), "entry layout");
     static_assert(offsetof(WordCountEntry, count) == offsetof(OutRecord, count), "entry layout");
     LOCUST_CHECK_ARG(u <= h_out_cap, "output larger than its buffer");
-    e.adopt(out_pool[out_idx], reinterpret_cast<WordCountEntry*>(h_out), u);
+    if (!compact) return e.adopt(out_pool[out_idx], reinterpret_cast<WordCountEntry*>(h_out), u);
+    std::vector<EntrySegment> segs;
+    segs.reserve(64);
+    const u64* words = reinterpret_cast<const u64*>(h_out);
+    u64 at = 0;  // entries before v: its segment starts at word kOutWords * at
+    for (int v = 0; v < kDictParts; ++v) {
+      const u64 t = h_ctab[v];
+      LOCUST_CHECK_ARG(t != ~0ull, "compact output: partition " + std::to_string(v) + " not written");
+      const u64 m = t & 0xffffffffull;
+      if (m) segs.push_back({words + kOutWords * at, m});
+      at += m;
+    }
+    LOCUST_CHECK_ARG(at == u, "compact output: " + std::to_string(at) + " entries, expected " +
+                                  std::to_string(u));
+    e.adopt_compact(out_pool[out_idx], std::move(segs), u);
   }
 
   void fill_counters(WordCountResult& r) const {
@@ -1783,13 +1824,13 @@ struct DevicePipeline {
         finish_dict_with_radix((u32)in.num_lines, map_combined);
         LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
         download_output(r, ev[5]);
-        if (ordered) force_retune(r.entries.data(), r.entries.size());
+        if (ordered) force_retune(r.entries);
       } else {
         fill_counters(r);
-        copy_out(r.entries, h_ctr->num_unique);
+        copy_out(r.entries, h_ctr->num_unique, ordered_done && ord_compact);
         r.times.host_copy_ms = (now_ns() - t_synced) * 1e-6;
-        if (ordered_done) maybe_retune(r.entries.data(), r.entries.size());
-        else if (ordered) force_retune(r.entries.data(), r.entries.size());
+        if (ordered_done) maybe_retune(r.entries);
+        else if (ordered) force_retune(r.entries);
       }
     } else {
       if (lean) {
@@ -1817,7 +1858,7 @@ struct DevicePipeline {
         if (!overflow) {
           fill_counters(r);
           copy_out(r.entries, h_ctr->num_unique);
-          if (psort_used) maybe_retune(r.entries.data(), r.entries.size());
+          if (psort_used) maybe_retune(r.entries);
         }
       } else {
         download_output(r, ev[5]);

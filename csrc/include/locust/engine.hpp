@@ -8,6 +8,8 @@
 // CpuWordCount is the golden oracle and the `--backend cpu` path (main.cu:489-527).
 #pragma once
 
+#include <cstddef>
+#include <iterator>
 #include <memory>
 #include <string>
 #include <vector>
@@ -63,63 +65,168 @@ struct WordCountEntry {
 };
 static_assert(sizeof(WordCountEntry) == 40, "WordCountEntry 40 B");
 
+// One segment of compact records (kv.hpp CompactRecord: a header word, then the key's
+// non-zero words) holding `n` entries in key order.
+struct EntrySegment {
+  const u64* words = nullptr;
+  u64 n = 0;
+};
+
 // The entries of a result: an owned vector, or -- zero-copy -- the engine's host-mapped
 // output buffer itself, which the device wrote and which this list keeps alive (`owner`)
-// until it is dropped; the engine then reuses the buffer for a later job.  Vector-like.
+// until it is dropped; the engine then reuses the buffer for a later job.  The device may
+// have written that buffer as 40-B records (adopt) or as compact records (adopt_compact:
+// segments in key order, ~16-24 B per entry).  Iteration decodes
+// compact records on the fly; data() / operator[] turn a compact list into an owned
+// vector first (once).  Vector-like.
 class EntryList {
  public:
   EntryList() = default;
   EntryList(std::vector<WordCountEntry>&& v) : vec_(std::move(v)) {}  // NOLINT: implicit
   EntryList& operator=(std::vector<WordCountEntry>&& v) {
-    owner_.reset();
-    view_ = nullptr;
-    n_ = 0;
+    release();
     vec_ = std::move(v);
     return *this;
   }
   // Borrow n entries at p, kept valid by `owner`.
   void adopt(std::shared_ptr<void> owner, WordCountEntry* p, size_t n) {
+    release();
     vec_.clear();
     vec_.shrink_to_fit();
     owner_ = std::move(owner);
     view_ = p;
     n_ = n;
   }
+  // Borrow compact segments (n entries in all), kept valid by `owner`.
+  void adopt_compact(std::shared_ptr<void> owner, std::vector<EntrySegment> segs, size_t n) {
+    adopt(std::move(owner), nullptr, n);
+    segs_ = std::move(segs);
+    compact_ = true;
+  }
   bool borrowed() const { return owner_ != nullptr; }
+  bool compact() const { return compact_; }
   size_t size() const { return owner_ ? n_ : vec_.size(); }
   bool empty() const { return size() == 0; }
-  WordCountEntry* data() { return owner_ ? view_ : vec_.data(); }
-  const WordCountEntry* data() const { return owner_ ? view_ : vec_.data(); }
+  // Bytes the device wrote for these entries (compact: the segments' words).
+  u64 wire_bytes() const;
+  WordCountEntry* data() {
+    materialize();
+    return owner_ ? view_ : vec_.data();
+  }
+  const WordCountEntry* data() const {
+    materialize();
+    return owner_ ? view_ : vec_.data();
+  }
   WordCountEntry& operator[](size_t i) { return data()[i]; }
   const WordCountEntry& operator[](size_t i) const { return data()[i]; }
-  const WordCountEntry& front() const { return data()[0]; }
-  WordCountEntry* begin() { return data(); }
-  WordCountEntry* end() { return data() + size(); }
-  const WordCountEntry* begin() const { return data(); }
-  const WordCountEntry* end() const { return data() + size(); }
+  WordCountEntry front() const { return *begin(); }
+
+  // Forward iteration over either form; yields entries by value.
+  class const_iterator {
+   public:
+    using iterator_category = std::forward_iterator_tag;
+    using value_type = WordCountEntry;
+    using difference_type = std::ptrdiff_t;
+    using pointer = const WordCountEntry*;
+    using reference = WordCountEntry;
+    const_iterator() = default;
+    WordCountEntry operator*() const {
+      if (flat_) return *flat_;
+      WordCountEntry e;
+      decode_compact(w_, &e.key, &e.count);
+      return e;
+    }
+    const_iterator& operator++() {
+      if (flat_) {
+        ++flat_;
+        return *this;
+      }
+      w_ += 1 + compact_nw(w_[0]);
+      if (--left_ == 0) next_segment();
+      return *this;
+    }
+    const_iterator operator++(int) {
+      const_iterator t = *this;
+      ++*this;
+      return t;
+    }
+    bool operator==(const const_iterator& o) const { return flat_ == o.flat_ && w_ == o.w_; }
+    bool operator!=(const const_iterator& o) const { return !(*this == o); }
+
+   private:
+    friend class EntryList;
+    void next_segment() {
+      w_ = nullptr;
+      while (seg_ != seg_end_) {
+        const EntrySegment& s = *seg_++;
+        if (s.n) {
+          w_ = s.words;
+          left_ = s.n;
+          return;
+        }
+      }
+    }
+    const WordCountEntry* flat_ = nullptr;
+    const u64* w_ = nullptr;
+    u64 left_ = 0;
+    const EntrySegment* seg_ = nullptr;
+    const EntrySegment* seg_end_ = nullptr;
+  };
+  const_iterator begin() const {
+    const_iterator it;
+    if (compact_) {
+      it.seg_ = segs_.data();
+      it.seg_end_ = segs_.data() + segs_.size();
+      it.next_segment();
+    } else if (size()) {
+      it.flat_ = owner_ ? view_ : vec_.data();
+    }
+    return it;
+  }
+  const_iterator end() const {
+    const_iterator it;
+    if (!compact_ && size()) it.flat_ = (owner_ ? view_ : vec_.data()) + size();
+    return it;
+  }
   // Owned storage of n entries (a borrowed prefix is copied over).
   void resize(size_t n) {
     if (owner_) {
-      std::vector<WordCountEntry> v(view_, view_ + std::min(n, n_));
-      owner_.reset();
-      view_ = nullptr;
-      n_ = 0;
+      std::vector<WordCountEntry> v;
+      v.reserve(n);
+      for (auto it = begin(); it != end() && v.size() < n; ++it) v.push_back(*it);
+      release();
       vec_ = std::move(v);
     }
     vec_.resize(n);
   }
   void assign(const WordCountEntry* b, const WordCountEntry* e) {
-    owner_.reset();
-    view_ = nullptr;
-    n_ = 0;
+    release();
     vec_.assign(b, e);
   }
 
  private:
-  std::vector<WordCountEntry> vec_;
-  std::shared_ptr<void> owner_;
-  WordCountEntry* view_ = nullptr;
-  size_t n_ = 0;
+  void release() const {
+    owner_.reset();
+    view_ = nullptr;
+    n_ = 0;
+    segs_.clear();
+    compact_ = false;
+  }
+  // compact -> an owned vector (the buffer is released)
+  void materialize() const {
+    if (!compact_) return;
+    std::vector<WordCountEntry> v;
+    v.reserve(n_);
+    for (auto it = begin(); it != end(); ++it) v.push_back(*it);
+    release();
+    vec_ = std::move(v);
+  }
+  mutable std::vector<WordCountEntry> vec_;
+  mutable std::shared_ptr<void> owner_;
+  mutable WordCountEntry* view_ = nullptr;
+  mutable size_t n_ = 0;
+  mutable std::vector<EntrySegment> segs_;
+  mutable bool compact_ = false;
 };
 
 struct WordCountResult {

@@ -331,6 +331,13 @@ struct OrderedExtra {
   // Records `out` holds: a job with more distinct keys writes none (the host sees
   // num_unique > out_cap and takes another path).
   u64 out_cap = ~0ull;
+  // Compact host output (kv.hpp compact records) instead of the 40-B
+  // records at `out`: virtual partition v writes its entries, in key order, from word
+  // 5 * (entries before v) of `cout` -- where its 40-B records would have started, so the
+  // look-back is unchanged and the capacity is out_cap records' worth of words -- and
+  // ctab[v] = entries | words << 32 (host-mapped, every v of the launch; ~0: not written).
+  u64* cout = nullptr;
+  u64* ctab = nullptr;
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,

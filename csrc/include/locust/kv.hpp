@@ -85,6 +85,29 @@ LOCUST_HD inline int unpack_key(const uint64_t* w, char* out) {
   return n;
 }
 
+// Compact result record (the host drain format of the ordered kernels and the shuffle's
+// shared output): 8-B words
+//   [count << kCompactCountShift | nw] [key word 0] ... [key word nw - 1]
+// where nw (1-4) counts the key's words up to its last non-zero one (the rest are NUL
+// padding).  English and synthetic keys are mostly <= 8 or <= 16 bytes: 16-24 B per entry
+// instead of 40 B across PCIe.  The 40-B KeyIntValuePair stays the kiv file format.
+constexpr int kCompactCountShift = 8;
+constexpr int kCompactMaxWords = 1 + kKeyWords;
+LOCUST_HD inline uint32_t key_words_used(const uint64_t* w) {
+  return w[3] ? 4u : w[2] ? 3u : w[1] ? 2u : 1u;
+}
+LOCUST_HD inline uint32_t compact_nw(uint64_t header) { return (uint32_t)(header & 7u); }
+LOCUST_HD inline uint64_t compact_header(uint64_t count, uint32_t nw) {
+  return (count << kCompactCountShift) | nw;
+}
+// Decodes the record at p; returns its length in words.
+LOCUST_HD inline uint32_t decode_compact(const uint64_t* p, PackedKey* key, uint64_t* count) {
+  const uint32_t nw = compact_nw(p[0]);
+  *count = p[0] >> kCompactCountShift;
+  for (int j = 0; j < kKeyWords; ++j) key->w[j] = (uint32_t)j < nw ? p[1 + j] : 0ull;
+  return 1 + nw;
+}
+
 LOCUST_HD inline int key_compare(const uint64_t* a, const uint64_t* b) {
   for (int j = 0; j < kKeyWords; ++j) {
     if (a[j] != b[j]) return a[j] < b[j] ? -1 : 1;

@@ -19,6 +19,7 @@
 namespace locust {
 
 struct WordCountEntry;
+class EntryList;
 
 constexpr int kDictParts = 256;
 constexpr u32 kPartDistinctWeight = 3;  // work of one distinct key, in tokens
@@ -49,8 +50,7 @@ void part_map_default_first_byte(PartMapTables* t);
 // work (count + kPartDistinctWeight per distinct key, the ordered kernel's part_w measure)
 // and at most `max_distinct` distinct keys each, cut only between different first words.
 // Returns the largest partition's predicted work (0 for no entries: default map).
-u64 part_map_from_entries(const WordCountEntry* e, size_t n, PartMapTables* t,
-                          u32 max_distinct = 1024);
+u64 part_map_from_entries(const EntryList& e, PartMapTables* t, u32 max_distinct = 1024);
 
 inline u32 part_map_lookup(const PartMapTables& t, u64 w0) { return part_of_w0(t.lo, w0); }
 

@@ -18,6 +18,17 @@ namespace locust {
 
 u64 TextInput::lines() const { return source ? source->lines() : num_lines; }
 
+u64 EntryList::wire_bytes() const {
+  if (!compact_) return (u64)size() * sizeof(WordCountEntry);
+  u64 words = 0;
+  for (const EntrySegment& s : segs_) {
+    const u64* p = s.words;
+    for (u64 i = 0; i < s.n; ++i) p += 1 + compact_nw(p[0]);
+    words += (u64)(p - s.words);
+  }
+  return words * 8;
+}
+
 u64 count_lines(const char* data, u64 bytes) {
   u64 n = 0;
   const char* p = data;
@@ -482,8 +493,7 @@ void write_kiv_results(const std::string& path, const WordCountResult& r) {
   std::vector<KeyIntValuePair> v;
   v.reserve(e.size());
   EntryVals vals(r);
-  for (size_t i = 0; i < e.size(); ++i)
-    v.push_back(to_kiv(e[i].key.w, (i64)vals.next(e[i]), (i64)e[i].count, path));
+  for (const WordCountEntry x : e) v.push_back(to_kiv(x.key.w, (i64)vals.next(x), (i64)x.count, path));
   write_kiv_file(path, v);
 }
 
@@ -623,7 +633,7 @@ void format_gpu_output(const WordCountResult& r, std::string* out) {
   out->reserve(out->size() + e.size() * 48);
   char buf[kKeyBytes + 1];
   EntryVals vals(r);
-  for (const auto& x : e) {
+  for (const WordCountEntry x : e) {
     const u64 val = vals.next(x);
     int n = unpack_key(x.key.w, buf);
     if (n == 0) continue;
@@ -641,7 +651,7 @@ void format_cpu_output(const WordCountResult& r, std::string* out) {
   const EntryList& e = r.entries;
   out->reserve(out->size() + e.size() * 32);
   char buf[kKeyBytes + 1];
-  for (const auto& x : e) {
+  for (const WordCountEntry x : e) {
     int n = unpack_key(x.key.w, buf);
     if (n == 0) continue;
     out->append("print key: ");

@@ -930,6 +930,45 @@ struct PartialsSource {
   }
 };
 
+// The compact records (kv.hpp) of m sorted entries into dst, consecutive lanes on
+// consecutive words (whole lines of the host-mapped output).  word(i, j): word j of sorted
+// entry i, j < kKeyWords a key word, j == kKeyWords its count.  Scratch (LDS): s_coff
+// [m] u32, s_own [5 m] u16, s_scan >= kPartBlock / 64 u32.  Returns the words (uniform).
+template <class Word>
+__device__ u32 write_compact_records(u64* __restrict__ dst, u32 m, Word word, u32* s_coff,
+                                     u16* s_own, u32* s_scan) {
+  constexpr u32 kPer = kPartSlots / kPartBlock;  // entries per thread
+  u32 nw[kPer], tot = 0;
+#pragma unroll
+  for (u32 r = 0; r < kPer; ++r) {
+    const u32 i = threadIdx.x * kPer + r;
+    nw[r] = 0;
+    if (i < m) {
+      const u64 kw[kKeyWords] = {word(i, 0), word(i, 1), word(i, 2), word(i, 3)};
+      nw[r] = key_words_used(kw);
+      tot += 1 + nw[r];
+    }
+  }
+  u32 total = 0;
+  u32 at = dev::block_exclusive_scan<u32, kPartBlock>(tot, s_scan, &total);
+#pragma unroll
+  for (u32 r = 0; r < kPer; ++r) {
+    const u32 i = threadIdx.x * kPer + r;
+    if (i < m) {
+      s_coff[i] = at | (nw[r] << 29);  // at < 5 * kPartSlots < 2^29
+      for (u32 k = 0; k <= nw[r]; ++k) s_own[at + k] = (u16)i;
+      at += 1 + nw[r];
+    }
+  }
+  __syncthreads();
+  for (u32 q = threadIdx.x; q < total; q += kPartBlock) {
+    const u32 i = s_own[q], c = s_coff[i];
+    const u32 k = q - (c & ((1u << 29) - 1u));
+    dst[q] = k == 0 ? compact_header(word(i, kKeyWords), c >> 29) : word(i, k - 1);
+  }
+  return total;
+}
+
 template <class Src>
 __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     Src src, MapCounters* __restrict__ ctr,
@@ -1151,6 +1190,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   if (threadIdx.x == 0) dev::publish_aggregate(status, v, agg);
   ORD_STAMP(2);
   u64 pre = 0;
+  u32 cwords = ~0u;  // compact words written (ex.cout), ~0u: none
   if (small) {
     // ---- small partition: all-pairs ranks: rank_i = #{j : key_j < key_i}, the sorted
     // position in one pass, no bucket sort.  Wave 0 resolves the look-back meanwhile. ----
@@ -1272,7 +1312,15 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     __syncthreads();
     const u64 base_m = pre & kOrdM;
     if (((pre >> kOrdOvfShift) & 511u) == 0) {  // uniform per workgroup
-      if (out && base_m + m <= ex.out_cap) {  // 8 B per lane, consecutive lanes
+      if (ex.cout && base_m + m <= ex.out_cap) {  // compact records from the staged ones
+        // scratch past the staged records and words 1-3: s_list[46 KB, 64 KB)
+        u32* s_coff = reinterpret_cast<u32*>(s_k123 + 3 * kSmallRank);
+        u16* s_own = reinterpret_cast<u16*>(s_coff + kSmallRank);
+        cwords = write_compact_records(
+            ex.cout + kOutWords * base_m, m,
+            [&](u32 i, u32 j) { return s_out[kOutWords * i + j]; }, s_coff, s_own,
+            reinterpret_cast<u32*>(s_scan));
+      } else if (out && base_m + m <= ex.out_cap) {  // 8 B per lane, consecutive lanes
         u64* dst = reinterpret_cast<u64*>(out + base_m);
         for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = s_out[q];
       }
@@ -1496,7 +1544,18 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       const LdsSlot& sl = s_tab[s_slot[i]];
       return wd == 0 ? sl.w[0] : wd < (u32)kKeyWords ? sl.w[wd] ^ kWordMagic : sl.count;
     };
-    if (out && base_m + m <= ex.out_cap) {
+    if (ex.cout && base_m + m <= ex.out_cap) {
+      // scratch past the sorted (w0, slot) arrays: s_list[24 KB, 52 KB)
+      u32* s_coff = s_list + 3 * kPartSlots;
+      u16* s_own = reinterpret_cast<u16*>(s_coff + kPartSlots);
+      cwords = write_compact_records(
+          ex.cout + kOutWords * base_m, m,
+          [&](u32 i, u32 j) {
+            const LdsSlot& sl = s_tab[s_slot[i]];
+            return j == 0 ? sl.w[0] : j < (u32)kKeyWords ? sl.w[j] ^ kWordMagic : sl.count;
+          },
+          s_coff, s_own, reinterpret_cast<u32*>(s_scan));
+    } else if (out && base_m + m <= ex.out_cap) {
       u64* dst = reinterpret_cast<u64*>(out + base_m);
       for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = word(q);
     }
@@ -1519,6 +1578,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   const u64 base_tok = pre >> kOrdTokShift;
   const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   ORD_STAMP(5);
+  if (ex.ctab && threadIdx.x == 0)
+    ex.ctab[v] = cwords == ~0u ? ~0ull : (u64)m | ((u64)cwords << 32);
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 6] = m;
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 11] = __builtin_amdgcn_s_memrealtime();
   if (ex.part_w && threadIdx.x == 0 && vj == 0 && vk > 0) {  // partition work, for the retuning

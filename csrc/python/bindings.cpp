@@ -445,7 +445,28 @@ PYBIND11_MODULE(_locust, m) {
       .def_property_readonly("num_unique", [](const PyResult& p) { return p.r.num_unique; })
       .def_property_readonly("overflow_lines", [](const PyResult& p) { return p.r.overflow_lines; })
       .def_property_readonly("truncated", [](const PyResult& p) { return p.r.truncated; })
-      .def_property_readonly("max_key_len", [](const PyResult& p) { return p.r.max_key_len; });
+      .def_property_readonly("max_key_len", [](const PyResult& p) { return p.r.max_key_len; })
+      .def_property_readonly("compact", [](const PyResult& p) { return p.r.entries.compact(); },
+                             "entries are the device's compact records (kv.hpp)")
+      .def_property_readonly("wire_bytes", [](const PyResult& p) { return p.r.entries.wire_bytes(); },
+                             "bytes the device wrote for the entries (compact or 40-B records)")
+      .def_static("from_compact", [](const std::vector<u64>& words,
+                                     const std::vector<std::pair<u64, u64>>& segs, u64 val_base) {
+        // host-side decoder test: segments (word offset, entries) over a word buffer
+        auto buf = std::make_shared<std::vector<u64>>(words);
+        std::vector<EntrySegment> sv;
+        u64 n = 0;
+        for (const auto& sg : segs) {
+          LOCUST_CHECK_ARG(sg.first <= buf->size(), "segment beyond the words");
+          sv.push_back({buf->data() + sg.first, sg.second});
+          n += sg.second;
+        }
+        PyResult p;
+        p.r.entries.adopt_compact(buf, std::move(sv), n);
+        p.r.val_base = val_base;
+        p.r.num_unique = n;
+        return p;
+      }, py::arg("words"), py::arg("segments"), py::arg("val_base") = 0);
 
   py::class_<PyGpuEngine>(m, "GpuEngine")
       .def(py::init<const JobConfig&, u64, u64>(), py::arg("cfg"), py::arg("max_bytes"),
@@ -720,7 +741,7 @@ PYBIND11_MODULE(_locust, m) {
       e[i].count = keys[i].second;
     }
     PartMapTables t;
-    const u64 pred = part_map_from_entries(e.data(), e.size(), &t, max_distinct);
+    const u64 pred = part_map_from_entries(EntryList(std::move(e)), &t, max_distinct);
     py::dict d;
     d["lo"] = std::vector<u64>(t.lo, t.lo + kDictParts + 1);
     d["predicted_max"] = pred;

@@ -1,0 +1,62 @@
+"""Compact result records: the ordered kernels drain their output to
+host memory as [count << 8 | nw][key words...] (csrc/include/locust/kv.hpp), one segment
+per virtual partition, and EntryList decodes them on the fly.  Here: the host decoder on
+hand-built segments against the packed-key oracle; the GPU twin (the kernels' own compact
+output byte-identical to the CPU engine, and the wire bytes it saves) is
+tests/test_gpu_engine.py::test_compact_output_*."""
+import struct
+
+import locust_amd as lc
+from locust_amd.utils import oracle
+
+
+def _pack(key: bytes):
+    key = key.ljust(32, b"\0")
+    return [struct.unpack(">Q", key[8 * j:8 * j + 8])[0] for j in range(4)]
+
+
+def _record(key: bytes, count: int):
+    w = _pack(key)
+    nw = max(j + 1 for j in range(4) if w[j]) if any(w) else 1
+    return [(count << 8) | nw] + w[:nw]
+
+
+def test_decode_segments_with_gaps_and_empty():
+    keys = [(b"a", 3), (b"abcdefgh", 1), (b"abcdefghi", 7), (b"b" * 17, 2), (b"z" * 31, 9),
+            (b"zz", 1)]
+    words, segs = [], []
+    # segment 0: two records; then a gap (the kernel leaves room for 40-B records); an
+    # empty segment; segment 2: the rest
+    seg0 = _record(*keys[0]) + _record(*keys[1])
+    words += seg0 + [0xdeadbeef] * 5
+    segs.append((0, 2))
+    segs.append((len(words), 0))
+    start = len(words)
+    for k, c in keys[2:]:
+        words += _record(k, c)
+    segs.append((start, len(keys) - 2))
+    r = lc._C.Result.from_compact(words, segs, val_base=100)
+    assert r.compact and r.num_unique == len(keys)
+    ent = r.entries()
+    assert [(k, c) for k, _v, c in ent] == keys
+    vals = [v for _k, v, _c in ent]
+    assert vals[0] == 100 and vals == [100 + sum(c for _k, c in keys[:i]) for i in range(len(keys))]
+    # the wire bytes are the records' words, not the gap
+    assert r.wire_bytes == 8 * (len(seg0) + sum(len(_record(k, c)) for k, c in keys[2:]))
+    assert r.wire_bytes < 40 * len(keys)
+    # the formatted output is the oracle's
+    want = [(k, 100 + sum(c for _k, c in keys[:i]), c) for i, (k, c) in enumerate(keys)]
+    assert r.format() == b"".join(b"print key: %s \t val: %d \t count: %d\n" % e for e in want)
+
+
+def test_decode_hamlet_sized(hamlet):
+    ent = oracle.wordcount(hamlet)[0]
+    words, segs, at = [], [], 0
+    for i in range(0, len(ent), 97):  # 97-entry segments
+        chunk = ent[i:i + 97]
+        segs.append((len(words), len(chunk)))
+        for k, _v, c in chunk:
+            words += _record(k, c)
+    r = lc._C.Result.from_compact(words, segs)
+    assert r.entries() == ent
+    assert r.wire_bytes / len(ent) < 20  # English keys: ~2 words per entry

@@ -279,3 +279,33 @@ def test_starting_map_and_in_job_plan_match_oracle(hamlet, monkeypatch, default_
         for _ in range(3):
             r = eng.run(text)
             assert r.num_tokens == ntok and r.entries() == ent
+
+
+@pytest.mark.parametrize("graph", [-1, 0, 1])
+def test_compact_output_hamlet(hamlet, graph):
+    """The ordered kernel drains compact records (kv.hpp) into host memory: byte-identical
+    entries, and fewer bytes across PCIe than 40 per entry.  graph -1
+    (auto, lean launches), 0 (event-timed) and 1 (replayed graph) each keep the flag."""
+    cfg = lc.make_config("gpu", reduce_path="lds", check=True, graph=graph)
+    eng = lc._C.GpuEngine(cfg, len(hamlet), 5000)
+    eng.load(hamlet)
+    ent = oracle.wordcount(hamlet)[0]
+    for _ in range(3):
+        r = eng.run_loaded()
+        assert r.compact and r.entries() == ent
+    assert r.wire_bytes < 0.55 * 40 * len(ent), r.wire_bytes
+
+
+def test_compact_output_large_ordered():
+    """A one-pass synthetic input past kPartBuildMaxTokens: the partials + ordered kernels
+    (PartialsSource) write compact records too; long keys (up to 31 bytes) use 4 words."""
+    text = lc._C.HostText.generate(lines=120000, seed=3, first_block=0).to_bytes()
+    text += b"".join(b"%s\n" % (b"x" * n + b"%d" % n) for n in range(1, 30))
+    want = lc._C.cpu_run(lc.make_config("cpu"), text)
+    cfg = lc.make_config("gpu", reduce_path="lds", check=True)
+    eng = lc._C.GpuEngine(cfg, len(text), text.count(b"\n") + 1)
+    eng.load(text)
+    for _ in range(2):
+        r = eng.run_loaded()
+        assert r.compact and r.entries() == want.entries()
+        assert r.wire_bytes < 0.6 * 40 * r.num_unique
