@@ -741,7 +741,7 @@ PYBIND11_MODULE(_locust, m) {
       e[i].count = keys[i].second;
     }
     PartMapTables t;
-    const u64 pred = part_map_from_entries(EntryList(std::move(e)), &t, max_distinct);
+    const u64 pred = part_map_from_entries(EntryList(std::vector<WordCountEntry>(e)), &t, max_distinct);
     py::dict d;
     d["lo"] = std::vector<u64>(t.lo, t.lo + kDictParts + 1);
     d["predicted_max"] = pred;
