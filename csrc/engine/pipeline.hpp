@@ -1634,8 +1634,10 @@ struct DevicePipeline {
   // An ordered launch writing the mapped output writes compact records (kv.hpp): the
   // drain across PCIe shrinks from 40 B per entry to ~16-24 B.
   void set_compact_out(OrderedExtra& ex, bool mapped) {
-    ord_compact = mapped;
-    if (!mapped) return;
+    // LOCUST_COMPACT_OUT=0: 40-B records instead (read per job: tools/env_ab.py A/B)
+    const char* e = std::getenv("LOCUST_COMPACT_OUT");
+    ord_compact = mapped && !(e && e[0] == '0');
+    if (!ord_compact) return;
     ex.cout = reinterpret_cast<u64*>(d_out_mapped);
     ex.ctab = d_ctab_mapped;
     ex.out_cap = std::min<u64>(ex.out_cap, h_out_cap);

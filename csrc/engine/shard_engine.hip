@@ -587,11 +587,14 @@ class GpuShardEngine final : public ShardEngine {
 
   // merge -> report -> C3 -> emit -> the headers and reports to the host.  region: the
   // shared output region, or kExchNoRegion to take the root's from its all-gathered header.
+  // The merge counts its range (n_out, tokens) without emitting it; the report and C3 then
+  // give every rank its offset, and ONE emit writes the range from the merge slots straight
+  // into the shared host output as compact records (no device range buffer, no second pass
+  // over it).
   void enqueue_range_tail(u32 P, int me, u32 C, u32 G, u64 region, const ExchCollectives& coll) {
     DevicePipeline& m = *mp_;
-    launch_merge_slots_limited(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, C, xb_.merged,
-                               xb_.rctr, xb_.gsend, G, LookbackScratch{xb_.lb_status, xb_.lb_tile},
-                               m.stream);
+    launch_merge_rank_slots(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, C, xb_.merged,
+                            xb_.rctr, LookbackScratch{xb_.lb_status, xb_.lb_tile}, m.stream);
     launch_exch_report(xb_.a2a_recv, P, C, xb_.ctl, xb_.rctr, G, xb_.msg3_send, m.stream);
     coll.allgather(xb_.msg3_send, xb_.msg3_all, sizeof(ExchMsg3));
     enqueue_emit(P, me, G, region);
@@ -603,11 +606,14 @@ class GpuShardEngine final : public ShardEngine {
   }
   void enqueue_emit(u32 P, int me, u32 G, u64 region) {
     ++out_seq_;
-    launch_exch_emit(xb_.gsend, xb_.msg3_all,
-                     region == kExchNoRegion ? reinterpret_cast<const ExchMsg1*>(xb_.msg1_all)
-                                             : nullptr,
-                     region, out_->regions, out_->region_records, P, (u32)me, G,
-                     out_->d_records, out_->d_stamps, out_seq_, xb_.done, mp_->stream);
+    launch_merge_emit_compact(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, xb_.C,
+                              xb_.merged, xb_.msg3_all,
+                              region == kExchNoRegion
+                                  ? reinterpret_cast<const ExchMsg1*>(xb_.msg1_all)
+                                  : nullptr,
+                              region, out_->regions, out_->region_records, P, (u32)me, G,
+                              reinterpret_cast<u64*>(out_->d_records), out_->d_stamps, out_seq_,
+                              xb_.done, LookbackScratch{xb_.lb_status, xb_.lb_tile}, mp_->stream);
   }
 
   void enqueue_exchange(const ExchMsg1& hdr, const std::vector<PackedKey>& samples, u32 P,
@@ -705,6 +711,10 @@ class GpuShardEngine final : public ShardEngine {
   void enqueue_exchange_emit(u32 P, int me) override {
     ensure_out(out_->region_records, out_->regions + 1);
     job_region_ = 0;
+    // the same merge emitted again: its look-back scratch and ticket from zero
+    LOCUST_HIP_CHECK(hipMemsetAsync(xb_.lb_status, 0, merge_scratch_words((u64)P * xb_.C) * 8,
+                                    mp_->stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(xb_.lb_tile, 0, sizeof(u32), mp_->stream));
     enqueue_emit(P, me, xb_.G, 0);
   }
 
@@ -757,10 +767,16 @@ class GpuShardEngine final : public ShardEngine {
         if (++spins > 64) std::this_thread::yield();
       }
     }
-    range_entries_.adopt(leases_[job_region_],
-                         reinterpret_cast<WordCountEntry*>(out_->records()) +
-                             job_region_ * out_->region_records,
-                         n);
+    // rank p's compact segment starts at word kOutWords x (region start + lower ranks' n_out)
+    std::vector<EntrySegment> segs;
+    const u64* words = reinterpret_cast<const u64*>(out_->records());
+    u64 at = job_region_ * out_->region_records;
+    for (u32 p = 0; p < P; ++p) {
+      const u64 np = std::min<u64>(R[p].n_out, G);
+      if (np) segs.push_back({words + (u64)kOutWords * at, np});
+      at += np;
+    }
+    range_entries_.adopt_compact(leases_[job_region_], std::move(segs), n);
     *total_count = t;
     *num_unique = n;
   }
@@ -1119,7 +1135,6 @@ class GpuShardEngine final : public ShardEngine {
     MapCounters* rctr = nullptr;
     char* a2a_send = nullptr;
     char* a2a_recv = nullptr;
-    OutRecord* gsend = nullptr;  // this rank's merged range (val local)
     KeyCount* merged = nullptr;
     u64* lb_status = nullptr;
     u32* lb_tile = nullptr;
@@ -1187,7 +1202,6 @@ class GpuShardEngine final : public ShardEngine {
     u64 off = 0;
     auto take = [&](u64 bytes) { const u64 o = off; off += al(bytes); return o; };
     const u64 o_as = take(slots_bytes), o_ar = take(slots_bytes),
-              o_gs = take(exch_gslot_bytes((u32)xb_.cap_g)),
               o_mg = take(xb_.cap_pc * sizeof(KeyCount)),
               o_lb = take(merge_scratch_words(xb_.cap_pc) * 8 + 8), o_lt = take(8);
     LOCUST_HIP_CHECK(hipMalloc(&xb_.data_dev, off));
@@ -1195,7 +1209,6 @@ class GpuShardEngine final : public ShardEngine {
     char* b = xb_.data_dev;
     xb_.a2a_send = b + o_as;
     xb_.a2a_recv = b + o_ar;
-    xb_.gsend = reinterpret_cast<OutRecord*>(b + o_gs);
     xb_.merged = reinterpret_cast<KeyCount*>(b + o_mg);
     xb_.lb_status = reinterpret_cast<u64*>(b + o_lb);
     xb_.lb_tile = reinterpret_cast<u32*>(b + o_lt);

@@ -83,7 +83,6 @@ LOCUST_HD inline u64 exch_msg1_bytes(u32 samples) { return sizeof(ExchMsg1) + (u
 // All-to-all slot: a SlotHeader (two KeyCount records) + slot_records KeyCount records.
 LOCUST_HD inline u64 exch_slot_bytes(u32 slot_records) { return (u64)(2 + slot_records) * sizeof(KeyCount); }
 // Range buffer: gather_records (key, count) 40-B records (the size is in ExchMsg3).
-LOCUST_HD inline u64 exch_gslot_bytes(u32 gather_records) { return (u64)gather_records * 40; }
 // Next job's slot size for a largest observed bucket / range of `used` records.
 inline u32 exch_grow(u64 used) {
   const u64 want = used + used / 8 + 64;

@@ -452,27 +452,34 @@ void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey*
 // ---------------- exchange.hip (device-resident shuffle, locust/exch.hpp) ----------------
 // Merge of nslots all-to-all slots (as launch_merge_slots) writing at most out_limit
 // output records (counters still count all of them).
-void launch_merge_slots_limited(const KeyCount* slots, u32 nslots, u32 slot_records,
-                                KeyCount* merged, MapCounters* ctr, OutRecord* out,
-                                u64 out_limit, LookbackScratch lb, hipStream_t s);
+// The shuffle tail in two launches around the C3 all-gather:
+// launch_merge_rank_slots merges the received slots into `merged` and sums the distinct
+// keys / tokens into acc->num_unique / acc->total_count (zeroed beforehand: the report
+// re-zeroes them); launch_merge_emit_compact then writes this rank's range as compact
+// records (kv.hpp) straight into the shared host output -- region `region` (or the root's,
+// root_msg), word kOutWords x (region x region_records + the lower ranks' records) of
+// `dst` -- and stamps `seq` when the whole range is out (locust/shm.hpp).  Nothing is
+// written when a report flags a problem.  `lb`: merge_scratch_words status words + a tile
+// counter, reset by launch_merge_rank_slots (a second emit of the same merge needs them
+// zeroed again).
+void launch_merge_rank_slots(const KeyCount* slots, u32 nslots, u32 slot_records,
+                             KeyCount* merged, MapCounters* acc, LookbackScratch lb,
+                             hipStream_t s);
+void launch_merge_emit_compact(const KeyCount* slots, u32 nslots, u32 slot_records,
+                               const KeyCount* merged, const ExchMsg3* msg3_all,
+                               const ExchMsg1* root_msg, u64 region, u32 regions,
+                               u64 region_records, u32 P, u32 me, u32 gather_records, u64* dst,
+                               u64* stamps, u64 seq, u32* done, LookbackScratch lb,
+                               hipStream_t s);
 void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, const u32* d_n,
                       u32 slot_records, ExchCtl* ctl, hipStream_t s,
                       u64* trace = nullptr);
 void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchCtl* ctl, u32 P,
                       u32 slot_records, char* send, hipStream_t s);
+// (rctr: launch_merge_rank_slots' accumulators, re-zeroed once read)
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
-                        const MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
+                        MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
                         hipStream_t s);
-// This rank's range (`range`) -> dst (the shared host output's records, device view) in
-// region `region` (root_msg != nullptr: the region the root's all-gathered ExchMsg1
-// names) at its global offset; the last workgroup stores `seq`
-// into stamps[me] (system-scope release) after every workgroup's writes.  `done`: a device
-// u32, zero before the launch and left zero.
-void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const ExchMsg1* root_msg,
-                      u64 region, u32 regions, u64 region_records, u32 P, u32 me,
-                      u32 gather_records, OutRecord* dst, u64* stamps, u64 seq, u32* done,
-                      hipStream_t s);
-
 // ---- device self-test of the string library (tests only; StringTestOut in engine.hpp) ----
 void launch_string_selftest(const char* blob, const u32* off, u32 n, const char* delims,
                             const int* ints, StringTestOut* out, hipStream_t s);

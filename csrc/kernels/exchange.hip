@@ -238,7 +238,8 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
                                                          const ExchCtl* __restrict__ ctl,
                                                          const MapCounters* __restrict__ rctr,
                                                          u32 gather_records,
-                                                         ExchMsg3* __restrict__ msg3) {
+                                                         ExchMsg3* __restrict__ msg3,
+                                                         MapCounters* __restrict__ reset) {
   const u64 sb = exch_slot_bytes(slot_records);
   bool bad = false;
   for (u32 q = threadIdx.x; q < P; q += 64) {
@@ -257,59 +258,10 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
     m.total = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : rctr->total_count;
     *msg3 = m;
   }
-}
-
-// This rank's key range (n_out(me) 40-B {key, count} records) -> the shared host output at
-// its global offset (the records of the lower ranks come first: rank order is key order;
-// the reference's global val is the prefix of the counts, rebuilt on the host).  Every
-// rank drains its own range over its own PCIe link at once -- no gather to the root, no
-// root-side concatenation.  8-B words, consecutive lanes on consecutive words (whole PCIe
-// write lines).  Completion: every workgroup fences its writes at system scope and
-// counts itself done; the last one stores `seq` into this rank's stamp with a system-scope
-// release, which the root's host polls before it reads the output (locust/shm.hpp).
-__global__ __launch_bounds__(256) void exch_emit_kernel(
-    const OutRecord* __restrict__ src, const ExchMsg3* __restrict__ msg3_all,
-    const ExchMsg1* __restrict__ root_msg, u64 region, u32 regions, u64 region_records, u32 P,
-    u32 me, u32 gather_records, OutRecord* __restrict__ dst, u64* __restrict__ stamps, u64 seq,
-    u32* __restrict__ done) {
-  __shared__ u64 s_roff, s_n;
-  __shared__ u32 s_bad;
-  if (threadIdx.x == 0) {
-    // the region: the host's, or the one the root announced in its all-gathered header
-    if (root_msg) region = root_msg->out_region;
-    u64 r = 0;
-    u32 bad = 0;
-    for (u32 q = 0; q < P && q < kExchMaxRanks; ++q) {
-      const ExchMsg3 m = msg3_all[q];
-      bad |= (u32)m.status | m.flags;
-      if (q < me) r += m.n_out <= gather_records ? m.n_out : gather_records;
-    }
-    const u64 n = msg3_all[me].n_out;
-    s_n = n <= gather_records ? n : gather_records;
-    // no free region (the host grows the output and emits again), or a range that would
-    // not fit its region (cannot happen with agreed sizes): write nothing, stamp nothing
-    s_bad = bad | (region >= regions || r + s_n > region_records ? 1u : 0u);
-    s_roff = region * region_records + r;
-  }
   __syncthreads();
-  if (s_bad) return;  // the host sees the reports: no output, no stamp
-  const u64 N = s_n;
-  const u64* in = reinterpret_cast<const u64*>(src);
-  u64* out = reinterpret_cast<u64*>(dst + s_roff);
-  // (word indices fit 32 bits: a range is < 2^29 records)
-  const u32 nq = (u32)(kOutWords * N);
-  for (u32 q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
-    out[q] = in[q];
-  }
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const u32 prev = atomicAdd(done, 1u);
-    if (prev == gridDim.x - 1) {
-      __threadfence_system();
-      *done = 0u;  // the next job's launch is stream-ordered behind this one
-      __hip_atomic_store(stamps + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+  if (threadIdx.x == 0 && reset) {  // the next merge's accumulators (launch_merge_rank_slots)
+    reset->num_unique = 0;
+    reset->total_count = 0;
   }
 }
 
@@ -348,22 +300,11 @@ void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchC
 }
 
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
-                        const MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
+                        MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
                         hipStream_t s) {
+  // rctr holds launch_merge_rank_slots' accumulators: read, then re-zeroed for the next job
   exch_report_kernel<<<dim3(1), dim3(64), 0, s>>>(recv, P, slot_records, ctl, rctr,
-                                                   gather_records, msg3);
-  LOCUST_HIP_LAUNCH_CHECK();
-}
-
-void launch_exch_emit(const OutRecord* range, const ExchMsg3* msg3_all, const ExchMsg1* root_msg,
-                      u64 region, u32 regions, u64 region_records, u32 P, u32 me,
-                      u32 gather_records, OutRecord* dst, u64* stamps, u64 seq, u32* done,
-                      hipStream_t s) {
-  const u64 words = (u64)kOutWords * gather_records;
-  const u64 blocks = std::min<u64>(std::max<u64>(div_up(words ? words : 1, 256), 1), 2048);
-  exch_emit_kernel<<<dim3((u32)blocks), dim3(256), 0, s>>>(range, msg3_all, root_msg, region,
-                                                           regions, region_records, P, me,
-                                                           gather_records, dst, stamps, seq, done);
+                                                   gather_records, msg3, rctr);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

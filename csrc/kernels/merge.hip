@@ -149,9 +149,11 @@ __device__ __forceinline__ u32 run_lower_bound(const KeyCount* __restrict__ run,
 
 // kMergeSub threads per record, one per run of a group of kMergeSub runs: 8x the waves of a
 // thread-per-record search, so the dependent probe chains of many records overlap.
+// acc (optional, zeroed): the merge's distinct keys and token total, summed here by atomics
+// (one per wave) -- the shuffle tail reports them before anything is emitted.
 __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
     RunsView view, KeyCount* __restrict__ merged, LookbackScratch lb, u32 emit_tiles,
-    SlotHeader* __restrict__ hdr_out) {
+    SlotHeader* __restrict__ hdr_out, MapCounters* __restrict__ acc) {
   __shared__ RunTable t;
   if (blockIdx.x == 0) {
     // merge_emit's look-back scratch, reset here (stream order) instead of by a memset
@@ -168,6 +170,8 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
   const u32 nruns = t.nruns;
   const u64 work = (u64)t.off[nruns] * kMergeSub;
   const u32 sub = threadIdx.x % kMergeSub;
+  u32 my_firsts = 0;  // (acc) first copies this thread emitted, and their counts
+  u64 my_tokens = 0;
   // whole groups of kMergeSub lanes enter or leave the loop together (shuffles below)
   for (u64 gt = (u64)blockIdx.x * kMergeBlock + threadIdx.x; gt < work;
        gt += (u64)gridDim.x * kMergeBlock) {
@@ -208,6 +212,96 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
       for (int j = 0; j < kKeyWords; ++j) out.w[j] = k[j];
       out.count = dup ? 0 : rec.count + others;  // later copies of a key carry nothing
       merged[(u64)i + before] = out;
+      my_firsts += dup ? 0u : 1u;
+      my_tokens += out.count;
+    }
+  }
+  if (acc) {
+    const u32 f = dev::wave_reduce_sum(my_firsts);
+    const u64 tk = dev::wave_reduce_sum(my_tokens);
+    if (dev::lane_id() == 0 && f) {
+      atomicAdd(&acc->num_unique, f);
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc->total_count), (unsigned long long)tk);
+    }
+  }
+}
+
+// The shuffle tail's emit: this rank's merged key range straight from
+// the merge slots into the shared host output as compact records (kv.hpp), at word
+// kOutWords x (the region's first record + the lower ranks' records) -- rank p's segment
+// starts where its 40-B records would have, so the root needs only the all-gathered
+// counts.  Per tile: the first copies' sizes, a block scan and a look-back over the words
+// give each record's offset; the tile is staged in LDS and written with consecutive lanes
+// on consecutive words.  Every workgroup fences at system scope and counts itself done;
+// the last stores `seq` into this rank's stamp (locust/shm.hpp).
+__global__ __launch_bounds__(kMergeBlock) void merge_emit_compact_kernel(
+    const KeyCount* __restrict__ merged, RunsView view, const ExchMsg3* __restrict__ msg3_all,
+    const ExchMsg1* __restrict__ root_msg, u64 region, u32 regions, u64 region_records, u32 P,
+    u32 me, u32 gather_records, u64* __restrict__ dst, u64* __restrict__ stamps, u64 seq,
+    u32* __restrict__ done, u64* __restrict__ status, u32* __restrict__ tile_ctr) {
+  __shared__ u64 s_scan[kMergeBlock / 64 + 1];
+  __shared__ u32 s_tile, s_bad;
+  __shared__ u64 s_prefix, s_base;
+  __shared__ RunTable t;
+  __shared__ __attribute__((aligned(16))) u64 s_out[kEmitTile * kOutWords];
+  if (threadIdx.x == 0) {
+    // the region: the host's, or the one the root announced in its all-gathered header
+    if (root_msg) region = root_msg->out_region;
+    u64 r = 0;
+    u32 bad = 0;
+    for (u32 q = 0; q < P && q < kExchMaxRanks; ++q) {
+      const ExchMsg3 m = msg3_all[q];
+      bad |= (u32)m.status | m.flags;
+      if (q < me) r += m.n_out <= gather_records ? m.n_out : gather_records;
+    }
+    const u64 n = msg3_all[me].n_out;
+    // a failed or overflowing job, no free region (the host grows the output and emits
+    // again) or a range past its region: write nothing, stamp nothing
+    s_bad = bad | (n > gather_records || region >= regions || r + n > region_records ? 1u : 0u);
+    s_base = (u64)kOutWords * (region * region_records + r);
+  }
+  __syncthreads();
+  if (s_bad) return;  // uniform over the grid: the host sees the reports
+  const u32 tile = dev::acquire_tile(tile_ctr, &s_tile);
+  load_runs(view, t);
+  const u32 total = t.off[t.nruns];
+  const u32 ntiles = total ? (u32)div_up(total, (u64)kEmitTile) : 1u;
+  if (tile < ntiles) {  // uniform per workgroup; nobody waits on tiles past the end
+    const u32 i0 = tile * kEmitTile + threadIdx.x * kEmitItems;
+    KeyCount v[kEmitItems];
+    u32 nw[kEmitItems];
+    u64 words = 0;
+#pragma unroll
+    for (int e = 0; e < kEmitItems; ++e) {
+      const u32 i = i0 + e;
+      v[e].count = 0;
+      if (i < total) v[e] = merged[i];
+      nw[e] = v[e].count ? key_words_used(v[e].w) : 0u;
+      words += v[e].count ? 1u + nw[e] : 0u;
+    }
+    u64 tile_words = 0;
+    u64 at = dev::block_exclusive_scan<u64, kMergeBlock>(words, s_scan, &tile_words);
+    const u64 before = dev::block_lookback(status, tile, tile_words, &s_prefix);
+#pragma unroll
+    for (int e = 0; e < kEmitItems; ++e) {
+      if (!v[e].count) continue;
+      u64* o = s_out + at;
+      o[0] = compact_header(v[e].count, nw[e]);
+      for (u32 j = 0; j < nw[e]; ++j) o[1 + j] = v[e].w[j];
+      at += 1 + nw[e];
+    }
+    __syncthreads();
+    u64* out = dst + s_base + before;
+    for (u32 q = threadIdx.x; q < (u32)tile_words; q += kMergeBlock) out[q] = s_out[q];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u32 prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {
+      __threadfence_system();
+      *done = 0u;  // the next job's launch is stream-ordered behind this one
+      __hip_atomic_store(stamps + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -288,7 +382,7 @@ void launch_merge_view(const RunsView& v, u64 cap, KeyCount* merged, MapCounters
   const u32 rank_grid = (u32)std::min<u64>(div_up(c * kMergeSub, kMergeBlock), 8192);
   const u32 emit_grid = (u32)div_up(c, (u64)kEmitTile);
   merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(v, merged, lb, emit_grid,
-                                                                  hdr_out);
+                                                                  hdr_out, nullptr);
   LOCUST_HIP_LAUNCH_CHECK();
   merge_emit_kernel<<<dim3(emit_grid), dim3(kMergeBlock), 0, s>>>(merged, v, ctr, out, ctr_out,
                                                                   lb.status, lb.tile_counter,
@@ -314,12 +408,31 @@ void launch_merge_slots(const KeyCount* slots, u32 nslots, u32 slot_records, Key
                     (u64)nslots * slot_records, merged, ctr, out, ctr_out, lb, hdr_out, s);
 }
 
-void launch_merge_slots_limited(const KeyCount* slots, u32 nslots, u32 slot_records,
-                                KeyCount* merged, MapCounters* ctr, OutRecord* out,
-                                u64 out_limit, LookbackScratch lb, hipStream_t s) {
-  launch_merge_view(RunsView{nullptr, nullptr, nullptr, slots, nslots, slot_records},
-                    (u64)nslots * slot_records, merged, ctr, out, nullptr, lb, nullptr, s,
-                    out_limit);
+void launch_merge_rank_slots(const KeyCount* slots, u32 nslots, u32 slot_records,
+                             KeyCount* merged, MapCounters* acc, LookbackScratch lb,
+                             hipStream_t s) {
+  const RunsView v{nullptr, nullptr, nullptr, slots, nslots, slot_records};
+  const u64 c = std::max<u64>((u64)nslots * slot_records, 1);
+  const u32 rank_grid = (u32)std::min<u64>(div_up(c * kMergeSub, kMergeBlock), 8192);
+  merge_rank_kernel<<<dim3(rank_grid), dim3(kMergeBlock), 0, s>>>(
+      v, merged, lb, (u32)div_up(c, (u64)kEmitTile), nullptr, acc);
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_merge_emit_compact(const KeyCount* slots, u32 nslots, u32 slot_records,
+                               const KeyCount* merged, const ExchMsg3* msg3_all,
+                               const ExchMsg1* root_msg, u64 region, u32 regions,
+                               u64 region_records, u32 P, u32 me, u32 gather_records, u64* dst,
+                               u64* stamps, u64 seq, u32* done, LookbackScratch lb,
+                               hipStream_t s) {
+  const RunsView v{nullptr, nullptr, nullptr, slots, nslots, slot_records};
+  const u64 c = std::max<u64>((u64)nslots * slot_records, 1);
+  // tiles past this rank's merged slots exit at once (their count still completes the grid)
+  const u32 grid = (u32)div_up(c, (u64)kEmitTile);
+  merge_emit_compact_kernel<<<dim3(grid), dim3(kMergeBlock), 0, s>>>(
+      merged, v, msg3_all, root_msg, region, regions, region_records, P, me, gather_records, dst,
+      stamps, seq, done, lb.status, lb.tile_counter);
+  LOCUST_HIP_LAUNCH_CHECK();
 }
 
 // Loads this file's code object (one module per file) now rather than at its first launch.
