@@ -1,0 +1,1550 @@
+// Out-of-line members of DevicePipeline (csrc/engine/pipeline.hpp): the engine's host-side
+// job logic -- construction and sizing, uploads, the map / Process / Reduce enqueue paths,
+// partition-map retuning, graph capture, streaming and the result hand-over -- compiled once
+// here instead of in every translation unit that includes the header.
+#include "pipeline.hpp"
+
+namespace locust {
+namespace detail {
+
+u64 DevicePipeline::piece_target() {
+  static const u64 b = [] {
+    const char* e = std::getenv("LOCUST_PIECE_MB");
+    const long mb = e ? std::atol(e) : 12;
+    return (u64)std::max<long>(mb, 4) << 20;
+  }();
+  return b;
+}
+
+void DevicePipeline::issue_piece_copies(const char* src) {
+  ensure_piece_events(pieces.size());
+  for (size_t k = 0; k < pieces.size(); ++k) {
+    const u64 off = pieces[k].first, len = pieces[k].second;
+    hipStream_t cs = piece_stream(k);
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
+    LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
+  }
+  pieces_issued = true;
+}
+
+void DevicePipeline::ensure_plan() {
+  if (d_plan) return;
+  const u64 slots = 2 * kPlanCap;  // load factor <= 0.5
+  const u64 ctr_b = align_up(sizeof(MapCounters), 256), tab_b = align_up(slots * sizeof(DictSlot), 256);
+  plan_zero_bytes = ctr_b + tab_b + kPlanCap * 8;
+  const u64 total = plan_zero_bytes + 256 + (4 + 4 + 1) * kPlanCap * 8 + kPlanCap * 4 + 4096;
+  LOCUST_HIP_CHECK(hipMalloc(&d_plan, total));
+  char* c = d_plan;
+  d_plan_ctr = reinterpret_cast<MapCounters*>(c);
+  plan_dict.table = reinterpret_cast<DictSlot*>(c + ctr_b);
+  plan_dict.ucount = reinterpret_cast<u64*>(c + ctr_b + tab_b);
+  c = d_plan + align_up(plan_zero_bytes, 256);
+  for (int j = 0; j < kKeyWords; ++j, c += kPlanCap * 8) plan_dict.ukeys.w[j] = reinterpret_cast<u64*>(c);
+  for (int j = 0; j < kKeyWords; ++j, c += kPlanCap * 8) plan_keys.w[j] = reinterpret_cast<u64*>(c);
+  plan_dict.uval = reinterpret_cast<u64*>(c);
+  c += kPlanCap * 8;
+  plan_dict.urank = reinterpret_cast<u32*>(c);
+  plan_dict.mask = (u32)(slots - 1);
+  plan_dict.ucap = (u32)kPlanCap;
+}
+
+void DevicePipeline::enqueue_devplan(const char* host, u64 len0, const DelimMask& dm,
+                       const char* dev_text) {
+  u64 n = std::min<u64>(len0, kPlanSampleBytes);
+  if (n < len0) {
+    const void* nl = memrchr(host, '\n', (size_t)n);
+    if (nl) n = (u64)(static_cast<const char*>(nl) - host) + 1;
+  }
+  launch_map_fast(dev_text ? dev_text : d_text, n, dm, cfg.emits_per_line, cfg.max_key_len,
+                  plan_keys, nullptr, kPlanCap, d_plan_ctr, lb_map, stream);
+  launch_dict_insert(plan_keys, nullptr, &d_plan_ctr->num_records, kPlanCap, plan_dict,
+                     d_plan_ctr, stream);
+  launch_part_plan(plan_dict.ukeys.w[0], plan_dict.ucount, &d_plan_ctr->num_unique,
+                   plan_dict.ucap, d_pmap, stream);
+}
+
+void DevicePipeline::warm_modules_once(int device) {
+  static std::mutex mu;
+  static u64 warmed = 0;  // bit per device
+  std::lock_guard<std::mutex> lk(mu);
+  const u64 bit = 1ull << (device & 63);
+  if (warmed & bit) return;
+  warm_kernel_modules();
+  warmed |= bit;
+}
+
+DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines, u64 cap_records)
+    : cfg(c) {
+  LOCUST_CHECK_ARG(cfg.emits_per_line > 0, "emits_per_line must be > 0");
+  LOCUST_CHECK_ARG(cfg.max_key_len > 0 && cfg.max_key_len <= kKeyBytes - 1,
+                   "max_key_len must be in [1, 31]");
+  cap_bytes = std::max<u64>(max_bytes, 1);
+  cap_lines = std::max<u64>(max_lines, 1);
+  bool streaming = false;
+  if (cfg.chunk_bytes && cap_bytes > cfg.chunk_bytes && !cap_records) {
+    // streaming engine: one pass holds a chunk; its token capacity is bounded by bytes
+    cap_bytes = cfg.chunk_bytes;
+    cap_lines = cap_bytes;
+    streaming = true;
+  }
+  cap = cap_records ? cap_records
+                    : std::min<u64>(cap_lines * (u64)cfg.emits_per_line, cap_bytes / 2 + 1);
+  // The dictionary of a streamed input collects the distinct keys of ALL chunks, and
+  // its sort/emit buffers are record-sized: give small chunks room for 2^20 of them.
+  if (streaming) cap = std::max<u64>(cap, 1ull << 20);
+  cap = std::max<u64>(cap, 1);
+  LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
+  LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
+  warm_modules_once(cfg.device);
+  LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  for (auto& e : ev) LOCUST_HIP_CHECK(hipEventCreate(&e));
+
+  const bool compat = cfg.map_path == MapPath::kCompat;
+  const u64 slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
+  const u64 t_line = div_up(cap_bytes, kLineIdxTile) + 1;
+  const u64 t_compact = div_up(cap_lines, 256) + 1;
+  const u64 t_map = div_up(cap_bytes, kMapTileBytesMin) + 1;
+  const u64 t_heads = div_up(cap, kReduceTile) + 1;
+  const u64 t_scan = div_up(cap, kReduceTile) + 1;
+  const u64 rx_zero_words = radix_zero_bytes(cap) / 4;
+  // Hash table: >= 2x the distinct keys it can see (load factor <= 0.5), capped at
+  // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
+  dict_slots = 1024;
+  // dense distinct-key capacity: every key of a pass, at most 16M (a 2^25-slot table)
+  ucap = std::min<u64>(cap, 1ull << 24);
+  while (dict_slots < 2 * ucap) dict_slots <<= 1;
+  // [table | ucount | uval | rank]
+  dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
+                    ucap * 4;
+  const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
+  sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1);
+
+  SizingPlan sz;
+  sz.add<char>(cap_bytes + 64);
+  sz.add<u64>(compat ? cap_lines + 1 : 1);  // the line index: compat map only
+  sz.add<char>(64);
+  for (int j = 0; j < kKeyWords; ++j) {
+    sz.add<u64>(slot_cap);
+    sz.add<u64>(cap);
+    sz.add<u64>(cap);
+    sz.add<u64>(cap);
+  }
+  sz.add<u32>(compat ? cap_lines : 1);
+  for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
+  sz.add<u32>(cap);
+  sz.add<u8>(align_up(cap, 16) + 16);
+  if (cap <= kPartBuildMaxTokens && cap_bytes < kMapLargeInput) {
+    part_off_tiles = div_up(cap_bytes, kMapTileBytesMin);
+  } else if (!streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
+    // large single passes (the two-kernel ordered build): 1 KiB tiles below
+    // kMapLargeInput, 4 KiB tiles (whole inputs or upload pieces) above
+    part_off_tiles = std::max<u64>(div_up(std::min<u64>(cap_bytes, kMapLargeInput), kMapTileBytesMin),
+                                   div_up(cap_bytes, kMapTileBytesLarge) + kMaxPieces);
+    large_ordered = cap > kPartBuildMaxTokens;
+  }
+  if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartTable);
+  if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartOccWords);
+  partial_slots_cap = large_ordered ? (u32)std::clamp<u64>(div_up(cap_bytes, kPieceBytes) + 3,
+                                                           kOrdWorkers, kMaxPartialSlots)
+                                    : 0u;
+  const u64 partial_slots = (u64)kDictParts * partial_slots_cap;
+  if (partial_slots) {
+    sz.add<KeyCount>(partial_slots * kPartSlotsHost);
+    sz.add<u32>(partial_slots);
+  }
+  sz.add<OutRecord>(cap);
+  sz.add<KeyCount>(slot_records_cap() + kSlotHeaderRecords);
+  sz.add<PackedKey>(kMaxSamples);
+  sz.add<PackedKey>(kMaxRanks);
+  sz.add<u64>(kMaxRanks + 1);
+  sz.add<u64>(1);
+  sz.add<char>(sync_bytes);
+  sz.add<u32>(rx_zero_words);
+  sz.add<u32>(rx_part_words);
+  sz.add<SortPlan>(1);
+  for (int b = 0; b < 2; ++b) {
+    sz.add<u64>(cap);
+    sz.add<u32>(cap);
+  }
+  for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
+  sz.add<char>(dict_zero_bytes);
+  arena.size = align_up(sz.bytes + 4096, kDevPageBytes);
+  {
+    size_t got = 0;  // the process-wide block cache (locust/devcache.hpp)
+    arena.base = static_cast<char*>(dev_block_alloc(arena.size, &got));
+    arena_block = got;
+  }
+
+  d_text = arena.take<char>(cap_bytes + 64);
+  d_nl = arena.take<u64>(compat ? cap_lines + 1 : 1);
+  d_delims = arena.take<char>(64);
+  for (int j = 0; j < kKeyWords; ++j) {
+    slots.w[j] = arena.take<u64>(slot_cap);
+    tokens.w[j] = arena.take<u64>(cap);
+    sorted.w[j] = arena.take<u64>(cap);
+    heads.w[j] = arena.take<u64>(cap);
+  }
+  d_line_counts = arena.take<u32>(compat ? cap_lines : 1);
+  d_counts = arena.take<u64>(cap);
+  d_sorted_counts = arena.take<u64>(cap);
+  d_prefix = arena.take<u64>(cap);
+  d_head_val = arena.take<u64>(cap);
+  d_head_count = arena.take<u64>(cap);
+  d_perm = arena.take<u32>(cap);
+  d_parts = arena.take<u8>(align_up(cap, 16) + 16);
+  if (part_off_tiles) d_part_off = arena.take<u32>(part_off_tiles * kPartTable);
+  if (part_off_tiles) d_part_occ = arena.take<u32>(part_off_tiles * kPartOccWords);
+  if (partial_slots) {
+    d_partials = arena.take<KeyCount>(partial_slots * kPartSlotsHost);
+    d_partial_n = arena.take<u32>(partial_slots);
+  }
+  d_out = arena.take<OutRecord>(cap);
+  // room for a gather slot header in front: d_records - kSlotHeaderRecords is the slot
+  d_records = arena.take<KeyCount>(slot_records_cap() + kSlotHeaderRecords) + kSlotHeaderRecords;
+  d_samples = arena.take<PackedKey>(kMaxSamples);
+  d_splitters = arena.take<PackedKey>(kMaxRanks);
+  d_offsets = arena.take<u64>(kMaxRanks + 1);
+  d_offset = arena.take<u64>(1);
+
+  // sync block: [MapCounters | tile counters | status regions]
+  d_sync = arena.take<char>(sync_bytes);
+  d_ctr = reinterpret_cast<MapCounters*>(d_sync);
+  u32* counters = reinterpret_cast<u32*>(d_sync + 128);
+  u64* st = reinterpret_cast<u64*>(d_sync + 256);
+  lb_line = {st, counters + 0};
+  st += t_line;
+  lb_compact = {st, counters + 1};
+  st += t_compact;
+  lb_map = {st, counters + 2};
+  st += t_map;
+  lb_heads = {st, counters + 3};
+  st += t_heads;
+  lb_scan = {st, counters + 4};
+  st += t_scan;
+  lb_dict = {st, counters + 5};
+
+  rx.cap = cap;
+  rx.tile_counters = arena.take<u32>(rx_zero_words);
+  rx.status = rx.tile_counters + kNumPositions;
+  rx.hist_part = arena.take<u32>(rx_part_words);
+  rx.plan = arena.take<SortPlan>(1);
+  for (int b = 0; b < 2; ++b) {
+    rx.keys[b] = arena.take<u64>(cap);
+    rx.vals[b] = arena.take<u32>(cap);
+  }
+  for (int j = 0; j < kKeyWords; ++j) dict.ukeys.w[j] = arena.take<u64>(ucap);
+  {
+    char* z = arena.take<char>(dict_zero_bytes);
+    dict.table = reinterpret_cast<DictSlot*>(z);
+    dict.ucount = reinterpret_cast<u64*>(z + align_up(dict_slots * sizeof(DictSlot), 256));
+    dict.uval = reinterpret_cast<u64*>(reinterpret_cast<char*>(dict.ucount) + align_up(ucap * 8, 256));
+    d_rank = reinterpret_cast<u32*>(reinterpret_cast<char*>(dict.uval) + align_up(ucap * 8, 256));
+    dict.mask = (u32)(dict_slots - 1);
+    dict.ucap = (u32)ucap;
+    dict.urank = d_rank;
+  }
+
+  char delim_buf[64] = {0};
+  LOCUST_CHECK_ARG(cfg.delimiters.size() < sizeof(delim_buf), "too many delimiters");
+  std::memcpy(delim_buf, cfg.delimiters.data(), cfg.delimiters.size());
+  // on this pipeline's own stream: a legacy-stream copy would conflict with another
+  // thread's graph capture (loopback ranks share the process)
+  LOCUST_HIP_CHECK(
+      hipMemcpyAsync(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice, stream));
+  LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+
+  // A streaming engine reads files through its two staging halves; its one-pass buffer
+  // is pinned only when a caller stages text there (input_buffer(), a one-pass job).
+  if (!streaming) ensure_h_text();
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
+  // Output records and the counter snapshot are host-mapped: the emit kernel writes them
+  // over PCIe directly (zero-copy), so a dictionary run needs no D2H copy at all.  The
+  // kernels that write it directly emit at most kMappedOutMax records (larger results
+  // take the radix path, whose download grows the buffer), so a streaming engine with a
+  // 16M-key dictionary does not pin 800 MB per output buffer.
+  grow_host_out(std::min<u64>(ucap, kMappedOutMax));
+  // and a second one: a job's result holds its buffer while the next job runs, so jobs
+  // alternate between two -- allocated here, not inside the second job (pinning a
+  // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job)
+  out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+  use_out(0);
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_done, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  *h_done = 0;
+  LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_done), h_done, 0));
+  LOCUST_HIP_CHECK(
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&d_ctr_mapped), h_ctr_mapped, 0));
+  LOCUST_HIP_CHECK(hipMalloc(&d_pmap, sizeof(PartMapTables)));
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_pmap, sizeof(PartMapTables), hipHostMallocDefault));
+  part_map_default(h_pmap);
+  LOCUST_HIP_CHECK(hipMemcpyAsync(d_pmap, h_pmap, sizeof(PartMapTables), hipMemcpyHostToDevice,
+                                  stream));
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_pw, kDictParts * sizeof(u32),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(h_pw, 0, kDictParts * sizeof(u32));
+  LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_pw), h_pw, 0));
+  LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
+  std::memset(h_ctr, 0, sizeof(MapCounters));
+  if (large_ordered && cfg.map_path == MapPath::kFast) {
+    // what a piecewise pass needs, made here and not inside the first job: the copy
+    // streams and piece events, and the plan's scratch
+    ensure_piece_events(partial_slots_cap);
+    if (devplan_env) ensure_plan();
+    warm_copy_streams();
+  }
+}
+
+void DevicePipeline::warm_copy_streams() {
+  if (!h_text || !cstream || !cstream2) return;
+  const u64 n = std::min<u64>(cap_bytes, kPieceBytes);
+  for (hipStream_t s : {cstream, cstream2, stream}) {
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, n, hipMemcpyHostToDevice, s));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_text + 1, 0, 16, s));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(h_u64, d_text, 8, hipMemcpyDeviceToHost, s));
+    LOCUST_HIP_CHECK(hipStreamSynchronize(s));
+  }
+}
+
+DevicePipeline::~DevicePipeline() {
+  if (retune_job.valid()) retune_job.wait();
+  if (stream) (void)hipStreamSynchronize(stream);
+  for (auto& g : dict_graphs) (void)hipGraphExecDestroy(g.exec);
+  for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
+  if (d_ord_trace) (void)hipFree(d_ord_trace);
+  if (d_partials_trace) (void)hipFree(d_partials_trace);
+  if (d_map_trace) (void)hipFree(d_map_trace);
+  if (cstream) (void)hipStreamSynchronize(cstream);
+  if (cstream2) (void)hipStreamSynchronize(cstream2);
+
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  for (int b = 0; b < 2; ++b) {
+    if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
+    if (ev_consumed[b]) (void)hipEventDestroy(ev_consumed[b]);
+    if (h_stage[b]) (void)hipHostFree(h_stage[b]);
+  }
+  for (int i = 0; i < kRingPieces; ++i) {
+    if (h_ring[i]) (void)hipHostFree(h_ring[i]);
+    if (ev_ring[i]) (void)hipEventDestroy(ev_ring[i]);
+  }
+  for (auto e : ev_piece) (void)hipEventDestroy(e);
+  if (ev_fork) (void)hipEventDestroy(ev_fork);
+  if (cstream) (void)hipStreamDestroy(cstream);
+  if (cstream2) (void)hipStreamDestroy(cstream2);
+
+  if (d_text_alt) dev_block_free(d_text_alt, d_text_alt_block);
+  if (d_dctr) (void)hipFree(d_dctr);
+  if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
+  if (stream) (void)hipStreamDestroy(stream);
+  if (arena.base) dev_block_free(arena.base, arena_block);  // every stream synchronised above
+  for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_keys,
+                  (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped, (void*)h_pmap,
+                  (void*)h_pw, (void*)h_done})
+    if (p) (void)hipHostFree(p);
+  if (d_pmap) (void)hipFree(d_pmap);
+  if (d_plan) (void)hipFree(d_plan);
+}
+
+void DevicePipeline::use_out(size_t i) {
+  out_idx = i;
+  h_out = out_pool[i]->h;
+  d_out_mapped = out_pool[i]->d;
+  h_out_cap = out_pool[i]->cap;
+  h_ctab = out_pool[i]->ctab_h;
+  d_ctab_mapped = out_pool[i]->ctab_d;
+}
+
+void DevicePipeline::select_out() {
+  if (!out_pool.empty() && out_pool[out_idx].use_count() == 1) return;
+  for (size_t i = 0; i < out_pool.size(); ++i)
+    if (out_pool[i].use_count() == 1) return use_out(i);
+  if (retune_job.valid()) {
+    // a background retune reads a buffer a result no longer needs: let it finish (it is
+    // near the end by now) rather than pin a new buffer (~2 ms for a large engine's)
+    retune_job.wait();
+    poll_retune();
+    for (size_t i = 0; i < out_pool.size(); ++i)
+      if (out_pool[i].use_count() == 1) return use_out(i);
+  }
+  const u64 t0 = now_ns();
+  out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+  use_out(out_pool.size() - 1);
+  LOCUST_LOG_DEBUG("output buffer #%zu: %llu records, %.2f ms", out_pool.size(),
+                   (unsigned long long)h_out_cap, (now_ns() - t0) * 1e-6);
+}
+
+void DevicePipeline::grow_host_out(u64 n) {
+  select_out();
+  if (n <= h_out_cap) return;
+  sync();  // the device may still write the buffer being replaced
+  out_pool[out_idx] = std::make_shared<HostOut>(n);
+  use_out(out_idx);
+}
+
+void DevicePipeline::grow_host_keys(u64 n) {
+  if (n <= h_keys_cap) return;
+  if (h_keys) LOCUST_HIP_CHECK(hipHostFree(h_keys));
+  h_keys_cap = std::max<u64>(n, 1);
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, h_keys_cap * kKeyWords * sizeof(u64),
+                                 hipHostMallocDefault));
+}
+
+void DevicePipeline::wait_done(u32 seq, bool bounded_sync) {
+  const u64 t0 = now_ns();
+  while (__atomic_load_n(h_done, __ATOMIC_ACQUIRE) != seq) {
+    if (now_ns() - t0 > 2000000) {  // 2 ms
+      if (bounded_sync) sync();
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+}
+
+void DevicePipeline::enqueue_upload(const TextInput& in) {
+  const u64 t0 = now_ns();
+  prepare_upload(in);
+  const u64 t1 = now_ns();
+  enqueue_upload_device(in);
+  if ((int)log_level() >= (int)LogLevel::kDebug)
+    LOCUST_LOG_DEBUG("upload: mode %d, %zu pieces, host %.3f ms, enqueue %.3f ms",
+                     (int)upload_mode, pieces.size(), (t1 - t0) * 1e-6, (now_ns() - t1) * 1e-6);
+}
+
+void DevicePipeline::prepare_upload(const TextInput& in) {
+  ensure_h_text();
+  map_text = d_text;
+  pieces.clear();
+  if (use_zero_copy(in)) {
+    upload_mode = Upload::kZeroCopy;
+    map_text = d_h_text;
+  } else if (in.data != h_text && in.bytes && host_pinned(in.data)) {
+    upload_mode = Upload::kDirect;
+    plan_pieces(in);
+    return;
+  } else {
+    upload_mode = Upload::kStaged;
+  }
+  if (in.data != h_text && in.bytes) std::memcpy(h_text, in.data, in.bytes);
+  std::memset(h_text + in.bytes, 0, 16);
+  plan_pieces(in);
+}
+
+void DevicePipeline::plan_pieces(const TextInput& in) {
+  if (cfg.map_path != MapPath::kFast || !large_ordered || in.bytes < 2 * kPieceBytes) return;
+  const u64 npieces = std::min<u64>(partial_slots_cap, kMaxPieces);
+  const u64 piece = std::max<u64>({kPieceBytes, std::min<u64>(piece_target(), in.bytes / 4),
+                                   div_up(in.bytes, npieces > 3 ? npieces - 3 : 1)});
+  u64 pos = 0;
+  while (pos < in.bytes && pieces.size() < npieces) {
+    // Short first pieces start the map early, a short last piece keeps the work after
+    // the final copy small: P/4, P/2, P, ..., P, (rest - P/4), P/4 (a P/8 tail measured
+    // no better).  The last piece allowed takes the rest (line alignment shortens the
+    // others).
+    const u64 rest = in.bytes - pos, tail = piece / 4;
+    u64 want = piece;
+    if (pieces.size() == 0) want = piece / 4;
+    else if (pieces.size() == 1) want = piece / 2;
+    else if (rest <= tail + tail / 2) want = rest;
+    else if (rest <= piece + tail) want = rest - tail;
+    want = std::min(want, rest);
+    u64 end = pieces.size() + 1 == npieces ? in.bytes : pos + want;
+    if (end < in.bytes) {
+      const void* nl = memrchr(in.data + pos, '\n', (size_t)(end - pos));
+      if (!nl) {  // a line longer than a piece: no pieces at all
+        pieces.clear();
+        return;
+      }
+      end = (u64)(static_cast<const char*>(nl) - in.data) + 1;
+    }
+    pieces.emplace_back(pos, end - pos);
+    pos = end;
+  }
+  if (pos < in.bytes) pieces.clear();
+}
+
+void DevicePipeline::ensure_piece_events(size_t n) {
+  if (!cstream) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+  if (!cstream2) LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream2, hipStreamNonBlocking));
+  if (!ev_fork) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+  while (ev_piece.size() < n) {
+    hipEvent_t e;
+    LOCUST_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev_piece.push_back(e);
+  }
+}
+
+void DevicePipeline::enqueue_upload_device(const TextInput& in) {
+  if (!pieces.empty()) {
+    // the pieces' copies go out first (outside a graph capture: there they need the fork
+    // from `stream`, made in enqueue_map); their maps follow in enqueue_map
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    LOCUST_HIP_CHECK(hipStreamIsCapturing(stream, &cst));
+    if (cst == hipStreamCaptureStatusNone)
+      issue_piece_copies(upload_mode == Upload::kDirect ? in.data : h_text);
+  } else if (upload_mode == Upload::kDirect) {
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, in.data, in.bytes, hipMemcpyHostToDevice, stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
+  } else if (upload_mode == Upload::kStaged) {
+    LOCUST_HIP_CHECK(hipMemcpyAsync(d_text, h_text, in.bytes + 16, hipMemcpyHostToDevice, stream));
+  }
+  if (!skip_sync_reset) LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+}
+
+bool DevicePipeline::use_job_graph(const TextInput& in) const {
+  if (cfg.map_path == MapPath::kFast && large_ordered && in.bytes >= 2 * kPieceBytes) return false;
+  if (cfg.graph < 0 && lean_job(in)) return false;  // auto: lean direct launches instead
+  const bool radix_ok = cfg.sort_path == SortPath::kRadix && cfg.map_path == MapPath::kFast &&
+                        table_tiles(in.bytes) > 0 && radix_mapped() && psort_enabled();
+  if (cfg.graph >= 0) return cfg.graph > 0 && (cfg.sort_path == SortPath::kDict || radix_ok);
+  return (cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast) || radix_ok;
+}
+
+bool DevicePipeline::lean_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("LOCUST_LEAN");
+    return !e || e[0] != '0';
+  }();
+  return on;
+}
+
+void DevicePipeline::launch_dict_graph(const TextInput& in, bool compat) {
+  u64 sig = 0;
+  for (const auto& pc : pieces) sig = (sig ^ pc.first) * 0x100000001b3ull;
+  if (!pieces.empty()) sig |= 1;
+  const GraphKey key{in.bytes, in.num_lines, upload_mode == Upload::kDirect ? in.data : nullptr,
+                     map_text, upload_mode, d_out_mapped, skip_sync_reset, sig};
+  const DictGraph* hit = nullptr;
+  for (const auto& g : dict_graphs)
+    if (g.key == key) hit = &g;
+  if (!hit) {
+    if (dict_graphs.size() >= 6) {  // shapes or buffers changed a lot: drop the oldest
+      LOCUST_HIP_CHECK(hipGraphExecDestroy(dict_graphs.front().exec));
+      dict_graphs.erase(dict_graphs.begin());
+    }
+    hipGraph_t g = nullptr;
+    LOCUST_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    enqueue_upload_device(in);
+    enqueue_map(in);
+    bool ordered;  // dictionary: the ordered kernel; radix: the partitioned sort
+    if (cfg.sort_path == SortPath::kDict) {
+      ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr, /*self_clean=*/true);
+    } else {
+      enqueue_radix_job((u32)in.num_lines, compat, nullptr, nullptr);
+      ordered = psort_used;
+      job_self_cleaned = false;
+    }
+    LOCUST_HIP_CHECK(hipStreamEndCapture(stream, &g));
+    hipGraphExec_t exec = nullptr;
+    LOCUST_HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+    LOCUST_HIP_CHECK(hipGraphDestroy(g));
+    dict_graphs.push_back({key, exec, ordered, job_self_cleaned, ordered && ord_compact});
+    hit = &dict_graphs.back();
+  }
+  graph_ordered = hit->ordered;
+  job_self_cleaned = hit->clean;
+  ord_compact = hit->compact;
+  if (cfg.sort_path == SortPath::kRadix) psort_used = hit->ordered;
+  parts_ready = cfg.map_path == MapPath::kFast;  // what enqueue_map sets when not replaying
+  part_tiles = cfg.map_path != MapPath::kFast ? 0u : pieces.empty() ? table_tiles(in.bytes)
+                                                                       : piece_tiles();
+  LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
+}
+
+void DevicePipeline::enqueue_map(const TextInput& in) {
+  plan_pass = false;  // decided per pass (decide_plan) where the map can write occupancy
+  parts_ready = cfg.map_path == MapPath::kFast;
+  devplan_used = false;
+  partial_nslots = 0;
+  // combining needs the 4 KiB grouped map: upload pieces, or one launch past kMapLargeInput
+  map_combined = combine_map && large_ordered && cfg.map_path == MapPath::kFast &&
+                 (!pieces.empty() ? piece_tiles() > 0
+                                  : in.bytes >= kMapLargeInput && table_tiles(in.bytes) > 0);
+  if (cfg.map_path == MapPath::kCompat) {
+    launch_line_index(d_text, in.bytes, d_nl, d_ctr, lb_line, stream);
+    launch_map_compat(d_text, in.bytes, d_nl, (u32)in.num_lines, d_delims, cfg.emits_per_line,
+                      cfg.max_key_len, slots, d_line_counts, d_ctr, stream);
+  } else if (!pieces.empty()) {
+    // piece k: H2D on the copy stream, then its map on the compute stream once it landed
+    // (4 KiB tiles; the table rows of the pieces follow each other)
+    ensure_piece_events(pieces.size());
+    part_tiles = piece_tiles();
+    const char* src = upload_mode == Upload::kDirect ? in.data : h_text;
+    const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
+    // The copies need no fork from `stream` outside a graph capture (nothing earlier in
+    // the job touches d_text, and the previous job ended with a host sync).  A fork made
+    // the first copy on a copy stream wait on the host for the compute queue's marker:
+    // one job in ~8 stalled 8-9 ms inside hipMemcpyAsync (measured; none without it).
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    LOCUST_HIP_CHECK(hipStreamIsCapturing(stream, &cst));
+    if (cst != hipStreamCaptureStatusNone) {
+      LOCUST_HIP_CHECK(hipEventRecord(ev_fork, stream));
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_fork, 0));
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream2, ev_fork, 0));
+    }
+    // a combining large pass (run() / the shard engine take the two-kernel ordered build
+    // next): aggregate each piece right after its map, into slot k -- on the same stream:
+    // beside the next map on a third stream both kernels ran ~1.6x slower and every
+    // cross-queue hand-off cost ~20 us (measured), while the copies leave room for both
+    const bool agg = map_combined && large_ordered_ok() && pieces.size() <= partial_slots_cap;
+    devplan_used = agg && devplan_env && !devplan_failed && !pm_tuned;
+    if (devplan_used) {  // zeroed while piece 0 is on its way
+      ensure_plan();
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_plan, 0, plan_zero_bytes, stream));
+    }
+    const u64 t_enq = now_ns();
+    // the padding after the text: off the copy streams (a 16-byte fill at an unaligned
+    // address is two blit kernels there, ~15 us in front of the last piece's event)
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_text + in.bytes, 0, 16, stream));
+    u64 tile_off = 0;
+    const bool issued = pieces_issued;
+    pieces_issued = false;
+    for (size_t k = 0; k < pieces.size(); ++k) {
+      const u64 off = pieces[k].first, len = pieces[k].second;
+      if (!issued) {
+        hipStream_t cs = piece_stream(k);
+        LOCUST_HIP_CHECK(hipMemcpyAsync(d_text + off, src + off, len, hipMemcpyHostToDevice, cs));
+        LOCUST_HIP_CHECK(hipEventRecord(ev_piece[k], cs));
+      }
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_piece[k], 0));
+      if (k == 0 && devplan_used) enqueue_devplan(src, len, dm);
+      launch_map_fast(d_text + off, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, d_parts,
+                      cap, d_ctr, lb_map, stream, map_trace(),
+                      part_tiles ? d_part_off + tile_off * kPartTable : nullptr, part_map(),
+                      /*large_tiles=*/true, map_combined ? d_counts : nullptr);
+      const u64 t1 = tile_off + div_up(len, kMapTileBytesLarge);
+      if (agg)
+        launch_dict_partials(tokens, d_counts, d_part_off, (u32)tile_off, (u32)t1, 1, (u32)k,
+                             (u32)pieces.size(), cap, d_partials, d_partial_n, stream,
+                             partials_trace());
+      tile_off = t1;
+    }
+    if ((int)log_level() >= (int)LogLevel::kDebug)
+      LOCUST_LOG_DEBUG("piecewise map enqueued in %.3f ms", (now_ns() - t_enq) * 1e-6);
+    if (agg) partial_nslots = (u32)pieces.size();
+  } else {
+    part_tiles = table_tiles(in.bytes);
+    // A large pass in one launch (below the piecewise size): the same in-job plan as the
+    // piecewise pass, from the first MiB of the text, before the map tags the tokens --
+    // a first-letter map overflows the ordered kernel's LDS tables on ~80K distinct keys
+    // (measured: 1/8 of synth1m, 5.7 ms first job with the HBM-table fallback).
+    devplan_used = large_ordered && part_tiles && cfg.sort_path == SortPath::kDict &&
+                   devplan_env && !devplan_failed && !pm_tuned;
+    if (devplan_used) {
+      ensure_plan();
+      LOCUST_HIP_CHECK(hipMemsetAsync(d_plan, 0, plan_zero_bytes, stream));
+      enqueue_devplan(upload_mode == Upload::kDirect || upload_mode == Upload::kZeroCopy ? in.data
+                                                                                       : h_text,
+                      in.bytes, make_delim_mask(cfg.delimiters.c_str()), map_text);
+    }
+    decide_plan(in.bytes);
+    launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
+                    cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
+                    stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
+                    map_combined ? d_counts : nullptr, plan_small() ? d_part_occ : nullptr);
+  }
+}
+
+void DevicePipeline::enqueue_process(u32 num_lines, bool compat, bool with_counts, u64 host_n,
+                       bool allow_psort) {
+  if (allow_psort && psort_ok(compat, with_counts)) {
+    // one kernel, one workgroup per key range of the map's partition table (psort.hip)
+    launch_psort(tokens, d_part_off, part_tiles, cap, sorted, d_ctr, d_pw, stream, ord_trace());
+    psort_used = true;
+    return;
+  }
+  psort_used = false;
+  if (compat)
+    launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
+                         lb_compact, stream);
+  if (!cfg.sync_plan) {
+    host_n = kUnknownCount;
+  } else if (host_n == kUnknownCount) {
+    LOCUST_HIP_CHECK(hipMemcpyAsync(h_u64, &d_ctr->num_records, sizeof(u32),
+                                    hipMemcpyDeviceToHost, stream));
+    sync();
+    host_n = *reinterpret_cast<const u32*>(h_u64);
+  }
+  radix_sort(tokens, &d_ctr->num_records, host_n, rx, with_counts ? d_counts : nullptr, sorted,
+             with_counts ? d_sorted_counts : nullptr, d_perm, h_plan, stream);
+}
+
+void DevicePipeline::enqueue_radix_job(u32 num_lines, bool compat, hipEvent_t after_process,
+                         hipEvent_t after_reduce) {
+  radix_fused = cfg.reduce_path == ReducePath::kLds &&
+                radix_mapped() && psort_ok(compat, false);
+  if (radix_fused) {
+    // Process + Reduce in one kernel, records straight into the mapped output; it
+    // re-zeroes its scratch and, in a lean job, tells the host itself (psort.hip)
+    PsortReduceArgs ra;
+    ra.out = d_out_mapped;
+    ra.out_cap = h_out_cap;
+    ra.ctr_out = d_ctr_mapped;
+    ra.status = lb_dict.status;
+    ra.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
+    ra.map_lb = lb_map;
+    ra.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+    if (done_pending) {
+      ra.host_done = d_done;
+      ra.host_done_value = done_pending;
+      done_pending = 0;
+    }
+    launch_psort_reduce(tokens, d_part_off, part_tiles, cap, d_ctr, d_pw, ra, stream, ord_trace());
+    psort_used = true;
+    if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+    if (after_reduce) LOCUST_HIP_CHECK(hipEventRecord(after_reduce, stream));
+    return;
+  }
+  enqueue_process(num_lines, compat, false, kUnknownCount, /*allow_psort=*/true);
+  if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+  const bool mapped = radix_mapped();
+  if (cfg.reduce_path == ReducePath::kLds) {
+    // LDS path: mark + compact + adjacent difference + records in one kernel
+    launch_reduce_fused(sorted, cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? h_out_cap : cap,
+                        mapped ? d_ctr_mapped : nullptr, lb_heads, stream);
+  } else {
+    // global path: the reference's kernel sequence (kernFindUniqBool, partition,
+    // kernGetCount) as separate launches
+    enqueue_reduce_core(false);
+    if (mapped)
+      launch_pack_output(heads, d_head_val, d_head_count, cap, d_ctr, d_out_mapped, stream,
+                         d_ctr_mapped);
+    else
+      enqueue_pack_output();
+  }
+  if (after_reduce) LOCUST_HIP_CHECK(hipEventRecord(after_reduce, stream));
+}
+
+void DevicePipeline::redo_radix_general(u32 num_lines) {
+  redo_process_general(num_lines);
+  LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+  LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.tile_counter, 0, 4, stream));
+  enqueue_reduce_core(false);
+  enqueue_pack_output();
+}
+
+void DevicePipeline::enqueue_reduce_core(bool with_counts) {
+  const u64* prefix = nullptr;
+  if (with_counts) {
+    launch_scan_counts(d_sorted_counts, cap, d_prefix, d_ctr, lb_scan, stream);
+    prefix = d_prefix;
+  }
+  launch_mark_compact_heads(sorted, prefix, cap, cfg.reduce_path, heads, d_head_val, d_ctr,
+                            lb_heads, stream);
+  launch_adjacent_diff(d_head_val, cap, cfg.reduce_path, d_head_count, d_ctr, stream);
+}
+
+void DevicePipeline::enqueue_dict_insert(u32 num_lines, bool compat, bool with_counts) {
+  if (compat)
+    launch_compact_slots(d_line_counts, num_lines, cfg.emits_per_line, slots, tokens, d_ctr,
+                         lb_compact, stream);
+  if (!compat && parts_ready && cap <= kPartBuildMaxTokens) {
+    launch_dict_part_build(tokens, with_counts ? d_counts : nullptr, d_parts,
+                           &d_ctr->num_records, cap, dict, d_ctr, stream);
+    return;
+  }
+  LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+  launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
+                     d_ctr, stream);
+}
+
+void DevicePipeline::enqueue_partials() {
+  if (partial_nslots) return;
+  partial_nslots = kOrdWorkers;
+  launch_dict_partials(tokens, map_combined ? d_counts : nullptr, d_part_off, 0, part_tiles,
+                       kOrdWorkers, 0, kOrdWorkers, cap, d_partials, d_partial_n, stream,
+                       partials_trace());
+}
+
+void DevicePipeline::set_tile_source(OrderedExtra& ex, bool with_counts) const {
+  if (part_tiles && parts_ready && !with_counts) {
+    ex.part_off = d_part_off;
+    ex.part_tiles = part_tiles;
+    // the in-job plan while the map is untuned (a retuned map is already balanced: the
+    // plan would only add its ~2 us)
+    if (plan_small()) ex.part_occ = d_part_occ;
+  }
+}
+
+u64 DevicePipeline::retune_wanted() const {
+  if (devplan_used && !pm_tuned) {  // a planned pass: hand over to the exact map
+    if (const char* v = std::getenv("LOCUST_PART_TUNE"))
+      if (v[0] == '0') return 0;
+    return ~0ull / 8;
+  }
+  if (const char* v = std::getenv("LOCUST_PART_TUNE"))
+    if (v[0] == '0') return 0;
+  u64 sum = 0, mx = 0;
+  for (int p = 0; p < kDictParts; ++p) {
+    sum += h_pw[p];
+    mx = std::max<u64>(mx, h_pw[p]);
+  }
+  if (sum < (1u << 13) || mx * kDictParts <= 2 * sum) return 0;  // small or balanced
+  if (pm_predicted_max && mx * 4 <= pm_predicted_max * 5) return 0;  // as good as it gets
+  return mx;
+}
+
+void DevicePipeline::force_retune(const EntryList& e) {
+  const u64 n = e.size();
+  // a device-planned map overflowed: this engine keeps the host-side map from now on
+  // (tuned from this output, or the default with tuning off) -- d_pmap holds the plan
+  const bool planned = devplan_used;
+  if (planned) {
+    devplan_failed = true;
+    devplan_used = false;
+  }
+  const char* v = std::getenv("LOCUST_PART_TUNE");
+  const bool tune = n && !(v && v[0] == '0');
+  PartMapTables t;
+  u64 pred = 0;
+  if (tune)
+    pred = part_map_from_entries(e, &t);
+  else
+    part_map_default(&t);
+  // The same map again (e.g. one first word with more distinct keys than an LDS table:
+  // no cut can split it): a new upload would change nothing, so keep it.
+  if (!planned && (!tune || std::memcmp(&t, h_pmap, sizeof(t)) == 0)) return;
+  if (planned && !pred) return upload_pmap(t, 0);
+  retune_with(~0ull / 8, pred, t);
+}
+
+void DevicePipeline::maybe_retune(const EntryList& e) {
+  if (const u64 mx = retune_wanted()) {
+    if (large_ordered && e.size() > (1u << 16)) return retune_async(mx, e);
+    PartMapTables t;
+    retune_with(mx, part_map_from_entries(e, &t), t);
+  }
+}
+
+void DevicePipeline::retune_async(u64 mx, const EntryList& e) {
+  if (retune_job.valid()) return;  // one at a time
+  std::shared_ptr<HostOut> hold = out_pool[out_idx];
+  // a borrowed list: the copy shares the buffer (and its segments), not the entries
+  retune_job = std::async(std::launch::async, [hold, mx, e] {
+    RetuneTask r;
+    r.mx = mx;
+    r.pred = part_map_from_entries(e, &r.t);
+    return r;
+  });
+}
+
+void DevicePipeline::poll_retune() {
+  if (!retune_job.valid() ||
+      retune_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
+    return;
+  RetuneTask r = retune_job.get();
+  retune_with(r.mx, r.pred, r.t);
+}
+
+void DevicePipeline::maybe_retune_records(const KeyCount* d_recs, u64 n, bool force) {
+  const bool planned = force && devplan_used;
+  if (planned) {  // as force_retune
+    devplan_failed = true;
+    devplan_used = false;
+  }
+  const u64 mx = force ? ~0ull / 8 : retune_wanted();
+  if (planned && (!n || [] {
+        const char* v = std::getenv("LOCUST_PART_TUNE");
+        return v && v[0] == '0';
+      }())) {
+    PartMapTables t;
+    part_map_default(&t);
+    return upload_pmap(t, 0);
+  }
+  if (!mx || !n) return;
+  std::vector<KeyCount> h(n);
+  LOCUST_HIP_CHECK(hipMemcpyAsync(h.data(), d_recs, n * sizeof(KeyCount), hipMemcpyDeviceToHost,
+                                  stream));
+  sync();
+  std::vector<WordCountEntry> e(n);
+  for (u64 i = 0; i < n; ++i) {
+    for (int w = 0; w < kKeyWords; ++w) e[i].key.w[w] = h[i].w[w];
+    e[i].count = h[i].count;
+  }
+  PartMapTables t;
+  const u64 pred = part_map_from_entries(EntryList(std::move(e)), &t);
+  if (force && !planned && std::memcmp(&t, h_pmap, sizeof(t)) == 0) return;  // as force_retune
+  retune_with(mx, pred, t);
+}
+
+void DevicePipeline::retune_with(u64 mx, u64 pred, const PartMapTables& t) {
+  if (!pred || pred * 5 >= mx * 4) {  // < 20 % better: keep the map, stop asking
+    pm_predicted_max = mx;
+    return;
+  }
+  upload_pmap(t, pred);
+  ++pm_retunes;
+  if (large_ordered) pm_tuned = true;
+  LOCUST_LOG_DEBUG("partition map retuned (#%u): max partition work %llu -> %llu",
+                   pm_retunes, (unsigned long long)mx, (unsigned long long)pred);
+}
+
+void DevicePipeline::enqueue_dict_ordered(bool with_counts, bool mapped, bool self_clean) {
+  OrderedExtra ex;
+  ex.pm = part_map();
+  ex.part_w = d_pw;
+  ex.split_min = split_min;
+  if (self_clean) set_self_clean(ex);
+  if (self_clean && done_pending) {  // the kernel itself tells the host it is done
+    ex.host_done = d_done;
+    ex.host_done_value = done_pending;
+    done_pending = 0;
+  }
+  set_tile_source(ex, with_counts);
+  set_compact_out(ex, mapped);
+  launch_dict_ordered(tokens, with_counts ? d_counts : nullptr, d_parts, &d_ctr->num_records,
+                      cap, d_ctr, mapped ? d_out_mapped : d_out, mapped ? d_ctr_mapped : nullptr,
+                      lb_dict, stream, ord_trace(), ex);
+}
+
+u64* DevicePipeline::ord_trace() {
+  static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
+  if (!on) return nullptr;
+  if (!d_ord_trace) {
+    LOCUST_HIP_CHECK(hipMalloc(&d_ord_trace, kDictParts * 32 * sizeof(u64)));
+    LOCUST_HIP_CHECK(hipMemset(d_ord_trace, 0, kDictParts * 32 * sizeof(u64)));
+  }
+  return d_ord_trace;
+}
+
+u64* DevicePipeline::map_trace() {
+  static const bool on = std::getenv("LOCUST_MAP_TRACE") != nullptr;
+  if (!on) return nullptr;
+  if (!d_map_trace) {
+    LOCUST_HIP_CHECK(hipMalloc(&d_map_trace, 4096 * 8 * sizeof(u64)));
+    LOCUST_HIP_CHECK(hipMemset(d_map_trace, 0, 4096 * 8 * sizeof(u64)));
+  }
+  return d_map_trace;
+}
+
+void DevicePipeline::print_map_trace() {
+  if (!d_map_trace) return;
+  std::vector<u64> t(4096 * 8);
+  LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_map_trace, t.size() * 8, hipMemcpyDeviceToHost));
+  u64 t0 = ~0ull;
+  for (int i = 0; i < 4096; ++i)
+    if (t[i * 8]) t0 = std::min(t0, t[i * 8]);
+  for (int i = 0; i < 4096; ++i) {
+    const u64* x = &t[i * 8];
+    if (!x[0] || !x[5]) continue;
+    std::fprintf(stderr, "map tile=%4d entry=%6.2f acquired=%6.2f staged=%6.2f masks=%6.2f "
+                 "prefix=%6.2f reserved=%6.2f done=%6.2f us\n", i, (x[0] - t0) * 0.01,
+                 (x[1] - t0) * 0.01, (x[2] - t0) * 0.01, (x[3] - t0) * 0.01,
+                 (x[4] - t0) * 0.01, x[6] ? (x[6] - t0) * 0.01 : 0.0, (x[5] - t0) * 0.01);
+  }
+}
+
+u64* DevicePipeline::partials_trace() {
+  static const bool on = std::getenv("LOCUST_ORD_TRACE") != nullptr;
+  if (!on) return nullptr;
+  if (!d_partials_trace) {
+    LOCUST_HIP_CHECK(hipMalloc(&d_partials_trace, (u64)kDictParts * kMaxPartialSlots * 8 * sizeof(u64)));
+    LOCUST_HIP_CHECK(hipMemset(d_partials_trace, 0, (u64)kDictParts * kMaxPartialSlots * 8 * sizeof(u64)));
+  }
+  return d_partials_trace;
+}
+
+void DevicePipeline::print_partials_trace() {
+  if (!d_partials_trace) return;
+  const u64 ns = std::max<u32>(partial_nslots, 1), nb = (u64)kDictParts * ns;
+  std::vector<u64> t(nb * 8);  // slot b = p * ns + k
+  LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_partials_trace, t.size() * 8, hipMemcpyDeviceToHost));
+  LOCUST_HIP_CHECK(hipMemset(d_partials_trace, 0, t.size() * 8));
+  u64 t0 = ~0ull, t1 = 0, tok = 0;
+  for (u64 b = 0; b < nb; ++b) {
+    if (!t[b * 8]) continue;
+    t0 = std::min(t0, t[b * 8]);
+    t1 = std::max(t1, t[b * 8 + 3]);
+    tok += t[b * 8 + 4];
+  }
+  std::fprintf(stderr, "partials span=%.2f us, tokens=%llu\n", (t1 - t0) * 0.01,
+               (unsigned long long)tok);
+  for (u64 b = 0; b < nb; ++b) {
+    const u64* x = &t[b * 8];
+    if (!x[0]) continue;
+    std::fprintf(stderr, "partials b=%4llu p=%3llu k=%llu in=%7.2f clear=%6.2f insert=%7.2f "
+                 "out=%7.2f tok=%7llu distinct=%5llu\n", (unsigned long long)b,
+                 (unsigned long long)(b / ns), (unsigned long long)(b % ns),
+                 (x[0] - t0) * 0.01, (x[1] - x[0]) * 0.01, (x[2] - x[1]) * 0.01,
+                 (x[3] - t0) * 0.01, (unsigned long long)x[4], (unsigned long long)x[5]);
+  }
+}
+
+void DevicePipeline::print_psort_trace() {
+  if (!d_ord_trace) return;
+  std::vector<u64> t(kDictParts * 16);
+  LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
+  u64 first_in = ~0ull, last_out = 0;
+  int last_p = -1;
+  for (int p = 0; p < kDictParts; ++p) {
+    const u64* x = &t[p * 16];
+    if (!x[10]) continue;
+    first_in = std::min(first_in, x[10]);
+    if (x[11] > last_out) {
+      last_out = x[11];
+      last_p = p;
+    }
+  }
+  if (last_p >= 0)
+    std::fprintf(stderr, "psort span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
+                 (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 16 + 5]);
+  for (int p = 0; p < kDictParts; ++p) {
+    const u64* x = &t[p * 16];
+    if (!x[0] || !x[4]) continue;
+    auto d = [&](int a, int b) { return (unsigned long long)(x[a] && x[b] ? x[b] - x[a] : 0); };
+    std::fprintf(stderr, "psort p=%3d m=%5llu passes=%2llu list=%6llu keys=%6llu sort=%6llu "
+                 "write=%6llu | in=%6.2f out=%6.2f us\n", p, (unsigned long long)x[5],
+                 (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4),
+                 (x[10] - first_in) * 0.01, (x[11] - first_in) * 0.01);
+  }
+}
+
+void DevicePipeline::print_ord_trace() {
+  if (!d_ord_trace) return;
+  std::vector<u64> t(kDictParts * 32);
+  LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
+  // stamps: 0 start, 1 built, 2 published, 8 histogram, 7 bucketed, 9 ranked, 3 sorted,
+  // 4 prefix known, 5 written; 6 = distinct keys; 10 / 11 = entry / exit on the 100 MHz
+  // device-wide clock (the kernel's critical path across workgroups)
+  u64 first_in = ~0ull, last_out = 0;
+  int last_p = -1;
+  for (int p = 0; p < kDictParts; ++p) {
+    const u64* x = &t[p * 32];
+    if (!x[10]) continue;
+    first_in = std::min(first_in, x[10]);
+    if (x[11] > last_out) {
+      last_out = x[11];
+      last_p = p;
+    }
+  }
+  if (last_p >= 0)
+    std::fprintf(stderr, "ord span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
+                 (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 32 + 6]);
+  for (int p = 0; p < kDictParts; ++p) {
+    const u64* x = &t[p * 32];
+    if (!x[0] || !x[6]) continue;
+    auto d = [&](int a, int b) { return (unsigned long long)(x[a] && x[b] ? x[b] - x[a] : 0); };
+    std::fprintf(stderr,
+                 "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
+                 " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
+                 " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu\n",
+                 p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
+                 d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
+                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16));
+  }
+}
+
+bool DevicePipeline::enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process,
+                        bool self_clean) {
+  job_self_cleaned = false;
+  if (!compat && ordered_ok()) {
+    job_self_cleaned = self_clean && cfg.map_path == MapPath::kFast;
+    enqueue_dict_ordered(with_counts, /*mapped=*/true, job_self_cleaned);
+    if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+    return true;
+  }
+  if (!compat && !with_counts && large_ordered_ok()) {
+    // large pass: per-slice partials (Process), then merge + sort + records (Reduce)
+    enqueue_partials();
+    if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+    OrderedExtra ex;
+    ex.pm = part_map();
+    ex.part_w = d_pw;
+    ex.out_cap = h_out_cap;
+    set_compact_out(ex, true);
+    launch_dict_ordered_partials(d_partials, d_partial_n, partial_nslots, d_ctr, d_out_mapped,
+                                 d_ctr_mapped,
+                                 lb_dict, stream, ord_trace(), ex);
+    return true;
+  }
+  enqueue_process_dict(num_lines, compat, with_counts);
+  if (after_process) LOCUST_HIP_CHECK(hipEventRecord(after_process, stream));
+  enqueue_emit_dict(/*mapped=*/true);
+  return false;
+}
+
+void DevicePipeline::redo_dict_on_table(u32 num_lines, bool with_counts) {
+  LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->num_unique, 0, sizeof(u32), stream));
+  LOCUST_HIP_CHECK(hipMemsetAsync(&d_ctr->flags, 0, sizeof(u32), stream));
+  LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+  launch_dict_insert(tokens, with_counts ? d_counts : nullptr, &d_ctr->num_records, cap, dict,
+                     d_ctr, stream);
+  enqueue_rank();
+  enqueue_emit_dict(/*mapped=*/true);
+  sync();
+  *h_ctr = *h_ctr_mapped;
+}
+
+void DevicePipeline::finish_dict_with_radix(u32 num_lines, bool with_counts) {
+  if (h_ctr->flags & kCtrDictOverflow) {
+    // table overflow: sort every record and reduce the reference way
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_heads.tile_counter, 0, 4, stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+    LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.tile_counter, 0, 4, stream));
+    enqueue_process(num_lines, false, with_counts, h_ctr->num_records);
+    enqueue_reduce_core(with_counts);
+    enqueue_pack_output();
+    return;
+  }
+  LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.status, 0, 8 * (div_up(cap, kReduceTile) + 1), stream));
+  LOCUST_HIP_CHECK(hipMemsetAsync(lb_scan.tile_counter, 0, 4, stream));
+  radix_sort(dict.ukeys, &d_ctr->num_unique, h_ctr->num_unique, rx, dict.ucount, sorted,
+             d_sorted_counts, d_perm, h_plan, stream);
+  enqueue_reduce_dict();
+}
+
+void DevicePipeline::download_output(WordCountResult& r, hipEvent_t done) {
+  read_counters();
+  const u64 u = h_ctr->num_unique;
+  grow_host_out(u);
+  if (u)
+    launch_copy_to_mapped(d_out_mapped, d_out, u * sizeof(OutRecord), stream);
+  if (done) LOCUST_HIP_CHECK(hipEventRecord(done, stream));
+  sync();
+  fill_counters(r);
+  copy_out(r.entries, u);
+}
+
+void DevicePipeline::set_compact_out(OrderedExtra& ex, bool mapped) {
+  // LOCUST_COMPACT_OUT=0: 40-B records instead (read per job: tools/env_ab.py A/B)
+  const char* e = std::getenv("LOCUST_COMPACT_OUT");
+  ord_compact = mapped && !(e && e[0] == '0');
+  if (!ord_compact) return;
+  ex.cout = reinterpret_cast<u64*>(d_out_mapped);
+  ex.ctab = d_ctab_mapped;
+  ex.out_cap = std::min<u64>(ex.out_cap, h_out_cap);
+}
+
+void DevicePipeline::copy_out(EntryList& e, u64 u, bool compact) {
+  static_assert(sizeof(WordCountEntry) == sizeof(OutRecord), "entry layout");
+  static_assert(offsetof(WordCountEntry, count) == offsetof(OutRecord, count), "entry layout");
+  LOCUST_CHECK_ARG(u <= h_out_cap, "output larger than its buffer");
+  if (!compact) return e.adopt(out_pool[out_idx], reinterpret_cast<WordCountEntry*>(h_out), u);
+  std::vector<EntrySegment> segs;
+  segs.reserve(64);
+  const u64* words = reinterpret_cast<const u64*>(h_out);
+  u64 at = 0;  // entries before v: its segment starts at word kOutWords * at
+  for (int v = 0; v < kDictParts; ++v) {
+    const u64 t = h_ctab[v];
+    LOCUST_CHECK_ARG(t != ~0ull, "compact output: partition " + std::to_string(v) + " not written");
+    const u64 m = t & 0xffffffffull;
+    if (m) segs.push_back({words + kOutWords * at, m});
+    at += m;
+  }
+  LOCUST_CHECK_ARG(at == u, "compact output: " + std::to_string(at) + " entries, expected " +
+                                std::to_string(u));
+  e.adopt_compact(out_pool[out_idx], std::move(segs), u);
+}
+
+void DevicePipeline::fill_counters(WordCountResult& r) const {
+  r.num_tokens = h_ctr->total_count ? h_ctr->total_count : h_ctr->num_records;
+  r.num_unique = h_ctr->num_unique;
+  r.overflow_lines = h_ctr->overflow_lines;
+  r.truncated = h_ctr->truncated;
+  r.max_key_len = h_ctr->max_key_len;
+}
+
+WordCountResult DevicePipeline::run_ref_timed(const TextInput& in) {
+  check_input(in);
+  WordCountResult r;
+  r.num_lines = in.num_lines;
+  const bool compat = cfg.map_path == MapPath::kCompat;
+  const bool dict_path = cfg.sort_path == SortPath::kDict;
+  const u64 w0 = now_ns();
+  enqueue_upload(in);
+  sync();
+  const u64 t0 = now_ns();
+  enqueue_map(in);  // map timer: the launch only (main.cu:405-407)
+  const u64 t1 = now_ns();
+  if (dict_path) {
+    enqueue_process_dict((u32)in.num_lines, compat);
+  } else {
+    enqueue_process((u32)in.num_lines, compat, false, kUnknownCount, /*allow_psort=*/true);
+  }
+  sync();  // process timer ends once the sort is done (thrust::sort returns)
+  if (!dict_path && psort_used) {
+    read_counters();
+    if (h_ctr->flags & kCtrSortOverflow) {  // a partition outgrew the LDS sort
+      redo_process_general((u32)in.num_lines);
+      sync();
+    }
+  }
+  const u64 t2 = now_ns();
+  if (dict_path) {
+    enqueue_emit_dict(/*mapped=*/true);  // the last reduce kernel: launch only (B4)
+  } else {
+    enqueue_reduce_core(false);
+    enqueue_pack_output();
+  }
+  const u64 t3 = now_ns();
+  if (dict_path) {
+    sync();
+    *h_ctr = *h_ctr_mapped;
+    if (dict_fallback_needed()) {
+      finish_dict_with_radix((u32)in.num_lines);
+      download_output(r, nullptr);
+    } else {
+      fill_counters(r);
+      copy_out(r.entries, h_ctr->num_unique);
+    }
+  } else {
+    download_output(r, nullptr);
+  }
+  r.times.ref_map_ms = (t1 - t0) * 1e-6;
+  r.times.ref_process_ms = (t2 - t1) * 1e-6;
+  r.times.ref_reduce_ms = (t3 - t2) * 1e-6;
+  r.times.wall_ms = (now_ns() - w0) * 1e-6;
+  if (cfg.check) validate_result(r);
+  return r;
+}
+
+WordCountResult DevicePipeline::run(const TextInput& in) {
+  TraceRange tr("locust:job");
+  poll_retune();
+  select_out();  // the previous result may still hold the last output buffer
+  // The previous job left d_sync zeroed (self-cleaning ordered run): no reset this time.
+  const bool clean_start = sync_clean;
+  sync_clean = false;
+  if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
+      cfg.map_path == MapPath::kFast)
+    return run_stream(in);
+  if (cfg.ref_timers) return run_ref_timed(in);
+  check_input(in);
+  WordCountResult r;
+  r.num_lines = in.num_lines;
+  const u64 t0 = now_ns();
+  const bool compat = cfg.map_path == MapPath::kCompat;
+  const bool dict_path = cfg.sort_path == SortPath::kDict;
+  struct ClearOnExit {  // only this entry point's dictionary pass combines in the map
+    bool& f;
+    ~ClearOnExit() { f = false; }
+  } clear_combine{combine_map};
+  combine_map = dict_path && !compat && large_ordered;
+  const bool graphed = use_job_graph(in);
+  // lean: a small single-pass job launched directly, no stage events, completion polled
+  const bool lean = !graphed && lean_job(in);
+  split_stages = !lean && !graphed;
+  skip_sync_reset = clean_start && !compat;
+  if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+  if (lean) {
+    enqueue_upload(in);
+    enqueue_map(in);
+  } else if (graphed) {
+    prepare_upload(in);
+    launch_dict_graph(in, compat);
+    LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));  // a replay has no stage split
+    r.times.graph = true;
+  } else {
+    enqueue_upload(in);
+    // Auto mode, piecewise pass: no stage markers between the kernels (the pass
+    // interleaves Map and Process anyway); graph=0 keeps the split
+    split_stages = pieces.empty() || cfg.graph == 0;
+    if (split_stages) LOCUST_HIP_CHECK(hipEventRecord(ev[1], stream));
+    enqueue_map(in);
+    if (split_stages) {
+      LOCUST_HIP_CHECK(hipEventRecord(ev[2], stream));
+      // a piecewise pass interleaves Process (the per-piece partials) with Map: one
+      // boundary, and no marker between the last partials and the ordered kernel
+      if (!pieces.empty()) LOCUST_HIP_CHECK(hipEventRecord(ev[3], stream));
+    }
+  }
+  if (dict_path) {
+    bool ordered = graph_ordered;
+    if (lean) {
+      done_pending = ++done_seq;
+      ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr, /*self_clean=*/true);
+      if (done_pending) publish_done(done_seq);
+      done_pending = 0;
+    } else if (!graphed) {
+      ordered = enqueue_dict_job((u32)in.num_lines, compat, false,
+                                 split_stages && pieces.empty() ? ev[3] : nullptr,
+                                 /*self_clean=*/true);
+      if (split_stages) LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+    }
+    skip_sync_reset = false;
+    const u64 t_launched = now_ns();
+    if (lean)
+      wait_done(done_seq);
+    else
+      sync();  // the one host synchronisation of a dictionary run
+    const u64 t_synced = now_ns();
+    r.times.host_launch_ms = (t_launched - t0) * 1e-6;
+    r.times.host_wait_ms = (t_synced - t_launched) * 1e-6;
+    *h_ctr = *h_ctr_mapped;
+    if (ordered && h_ctr->num_unique > h_out_cap) h_ctr->flags |= kCtrDictOverflow;  // no records
+    const bool ordered_done = ordered && !(h_ctr->flags & kCtrDictOverflow);
+    sync_clean = ordered_done && !compat && job_self_cleaned;  // the kernel re-zeroed its scratch
+    if (ordered) print_ord_trace();
+    print_partials_trace();
+    print_map_trace();
+    if (ordered && !ordered_done) ++fallbacks;
+    if (devplan_used) ++planned_passes;
+    if (ordered && !ordered_done) redo_dict_on_table((u32)in.num_lines, map_combined);
+    if (!ordered_done && dict_fallback_needed()) {
+      finish_dict_with_radix((u32)in.num_lines, map_combined);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      download_output(r, ev[5]);
+      if (ordered) force_retune(r.entries);
+    } else {
+      fill_counters(r);
+      copy_out(r.entries, h_ctr->num_unique, ordered_done && ord_compact);
+      r.times.host_copy_ms = (now_ns() - t_synced) * 1e-6;
+      if (ordered_done) maybe_retune(r.entries);
+      else if (ordered) force_retune(r.entries);
+    }
+  } else {
+    if (lean) {
+      done_pending = ++done_seq;  // the fused kernel publishes it itself
+      enqueue_radix_job((u32)in.num_lines, compat, nullptr, nullptr);
+      if (done_pending) publish_done(done_seq);
+      done_pending = 0;
+    } else if (!graphed) {
+      enqueue_radix_job((u32)in.num_lines, compat, ev[3], ev[4]);
+    }
+    skip_sync_reset = false;
+    bool overflow;
+    if (radix_mapped()) {  // records and counters already in host memory
+      if (lean) {
+        wait_done(done_seq);
+      } else {
+        if (!graphed) LOCUST_HIP_CHECK(hipEventRecord(ev[5], stream));
+        sync();  // the one host synchronisation of a radix run
+      }
+      *h_ctr = *h_ctr_mapped;
+      overflow = (h_ctr->flags & kCtrSortOverflow) != 0;
+      // a fused run re-zeroed its scratch (not replayed from a graph: those reset it)
+      sync_clean = lean && radix_fused && !overflow && !compat;
+      if (psort_used) print_psort_trace();
+      if (!overflow) {
+        fill_counters(r);
+        copy_out(r.entries, h_ctr->num_unique);
+        if (psort_used) maybe_retune(r.entries);
+      }
+    } else {
+      download_output(r, ev[5]);
+      overflow = (h_ctr->flags & kCtrSortOverflow) != 0;
+    }
+    if (overflow) {  // a partition outgrew the LDS sort: the device-wide sort instead
+      redo_radix_general((u32)in.num_lines);
+      LOCUST_HIP_CHECK(hipEventRecord(ev[4], stream));
+      download_output(r, ev[5]);
+    }
+  }
+  r.times.wall_ms = (now_ns() - t0) * 1e-6;
+  r.times.lean = lean;
+  if (lean) {  // no device timestamps: the job's wall time
+    r.times.gpu_ms = r.times.wall_ms;
+  } else {
+    if (!graphed && split_stages) {
+      r.times.h2d_ms = ms_between(ev[0], ev[1]);
+      r.times.map_ms = ms_between(ev[1], ev[2]);
+      r.times.process_ms = ms_between(ev[2], ev[3]);
+      r.times.reduce_ms = ms_between(ev[3], ev[4]);
+      r.times.d2h_ms = ms_between(ev[4], ev[5]);
+    }
+    r.times.gpu_ms = ms_between(ev[0], ev[5]);
+  }
+  if (cfg.check) validate_result(r);
+  return r;
+}
+
+bool DevicePipeline::host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: clear the sticky error
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+void DevicePipeline::ensure_stream_buffers(bool staging, u64 nchunks) {
+  if (!cstream) {
+    LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_copied[b], hipEventDisableTiming));
+      LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_consumed[b], hipEventDisableTiming));
+    }
+    size_t got = 0;  // the process-wide block cache, like the arena
+    d_text_alt = static_cast<char*>(dev_block_alloc(cap_bytes + 64, &got));
+    d_text_alt_block = got;
+    LOCUST_HIP_CHECK(hipMalloc(&d_dctr, sizeof(MapCounters)));
+  }
+  if (staging && !h_stage[0])
+    for (int b = 0; b < 2; ++b)
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_stage[b], cap_bytes + 64, hipHostMallocDefault));
+  if (nchunks > h_chunk_cap) {
+    if (h_chunk_ctr) LOCUST_HIP_CHECK(hipHostFree(h_chunk_ctr));
+    h_chunk_cap = std::max<u64>(nchunks, 64);
+    LOCUST_HIP_CHECK(hipHostMalloc(&h_chunk_ctr, h_chunk_cap * sizeof(MapCounters),
+                                   hipHostMallocDefault));
+  }
+}
+
+char* DevicePipeline::ensure_h_text() {
+  if (h_text) return h_text;
+  LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    d_h_text = nullptr;  // not device-visible: always DMA
+  }
+  return h_text;
+}
+
+std::vector<std::pair<u64, u64>> DevicePipeline::plan_chunks(const TextInput& in) const {
+  std::vector<std::pair<u64, u64>> out;
+  u64 pos = 0;
+  while (pos < in.bytes) {
+    u64 end = std::min<u64>(pos + cap_bytes, in.bytes);
+    if (end < in.bytes) {
+      const void* nl = memrchr(in.data + pos, '\n', (size_t)(end - pos));
+      if (!nl)
+        throw Error("a line longer than the engine's chunk size (" + std::to_string(cap_bytes) +
+                    " B) at byte " + std::to_string(pos));
+      end = (u64)(static_cast<const char*>(nl) - in.data) + 1;
+    }
+    out.emplace_back(pos, end - pos);
+    pos = end;
+  }
+  return out;
+}
+
+size_t DevicePipeline::enqueue_stream_insert(const TextInput& in) {
+  const auto chunks = plan_chunks(in);
+  const bool pinned = host_pinned(in.data);
+  size_t k = 0;
+  return enqueue_stream_chunks(!pinned, chunks.size(), [&](int b, const char** src) -> u64 {
+    if (k >= chunks.size()) return 0;
+    const u64 off = chunks[k].first, len = chunks[k].second;
+    ++k;
+    *src = in.data + off;
+    if (!pinned) {  // pageable input: host copy into the pinned half
+      std::memcpy(h_stage[b], in.data + off, len);
+      *src = h_stage[b];
+    }
+    return len;
+  });
+}
+
+size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
+  LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
+                   "inputs larger than the engine capacity stream through the dictionary "
+                   "path with the fast map (sort=dict, map=fast)");
+  const u64 max_chunks = div_up(std::max<u64>(src_text.size(), 1), cap_bytes / 2) + 2;
+  ensure_stream_buffers(false, max_chunks);
+  const u64 piece = std::min<u64>(cap_bytes, kRingPieceMax);
+  if (ring_piece != piece) {
+    for (int i = 0; i < kRingPieces; ++i) {
+      if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
+      LOCUST_HIP_CHECK(hipHostMalloc(&h_ring[i], piece + 64, hipHostMallocDefault));
+      if (!ev_ring[i]) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
+    }
+    ring_piece = piece;
+  }
+  const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
+  LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
+  LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));
+  // the copy stream must not overwrite a text buffer before the reset is queued
+  LOCUST_HIP_CHECK(hipEventRecord(ev_copied[1], stream));
+  LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_copied[1], 0));
+  size_t k = 0;  // chunks closed
+  u64 fill = 0;  // bytes in chunk k
+  auto chunk_text = [&](size_t c) { return (c & 1) ? d_text_alt : d_text; };
+  auto close_chunk = [&] {
+    const int b = (int)(k & 1);
+    char* dtext = chunk_text(k);
+    LOCUST_CHECK_ARG(k < h_chunk_cap, "more stream chunks than planned");
+    LOCUST_HIP_CHECK(hipMemsetAsync(dtext + fill, 0, 16, cstream));
+    LOCUST_HIP_CHECK(hipEventRecord(ev_copied[b], cstream));
+    LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
+    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+    launch_map_fast(dtext, fill, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap,
+                    d_ctr, lb_map, stream);
+    LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
+                                    hipMemcpyDeviceToHost, stream));
+    launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
+    ++k;
+    fill = 0;
+  };
+  for (u64 r = 0;; ++r) {
+    const int slot = (int)(r % kRingPieces);
+    // the slot's previous H2D must have drained before the source refills it
+    if (r >= (u64)kRingPieces) LOCUST_HIP_CHECK(hipEventSynchronize(ev_ring[slot]));
+    const u64 n = src_text.next(h_ring[slot], piece);
+    if (!n) break;
+    if (fill + n > cap_bytes) close_chunk();
+    // a chunk buffer is refilled only after the map two chunks back consumed it
+    if (fill == 0 && k >= 2)
+      LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[k & 1], 0));
+    LOCUST_HIP_CHECK(hipMemcpyAsync(chunk_text(k) + fill, h_ring[slot], n, hipMemcpyHostToDevice,
+                                    cstream));
+    LOCUST_HIP_CHECK(hipEventRecord(ev_ring[slot], cstream));
+    fill += n;
+  }
+  if (fill) close_chunk();
+  // hand the dictionary's counters to the single-pass stages that follow
+  LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_unique, &d_dctr->num_unique, sizeof(u32),
+                                  hipMemcpyDeviceToDevice, stream));
+  LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->flags, &d_dctr->flags, sizeof(u32),
+                                  hipMemcpyDeviceToDevice, stream));
+  return k;
+}
+
+void DevicePipeline::stream_stats(size_t nchunks, WordCountResult& r) const {
+  r.num_tokens = r.overflow_lines = r.truncated = r.max_key_len = 0;
+  for (size_t k = 0; k < nchunks; ++k) {
+    const MapCounters& c = h_chunk_ctr[k];
+    r.num_tokens += c.num_records;
+    r.overflow_lines += c.overflow_lines;
+    r.truncated += c.truncated;
+    r.max_key_len = std::max<u64>(r.max_key_len, c.max_key_len);
+  }
+  r.chunks = nchunks;
+}
+
+WordCountResult DevicePipeline::run_source(TextSource& src) {
+  sync_clean = false;
+  select_out();
+  WordCountResult r = finish_stream(0, [&] { return enqueue_stream_source(src); });
+  r.num_lines = src.lines();
+  return r;
+}
+
+void DevicePipeline::download_keys(const KeysSoA& src, u64 n, std::vector<PackedKey>* out) {
+  out->resize(n);
+  if (!n) return;
+  grow_host_keys(n);
+  for (int w = 0; w < kKeyWords; ++w)
+    LOCUST_HIP_CHECK(hipMemcpyAsync(h_keys + (u64)w * n, src.w[w], n * sizeof(u64),
+                                    hipMemcpyDeviceToHost, stream));
+  sync();
+  for (u64 i = 0; i < n; ++i)
+    for (int w = 0; w < kKeyWords; ++w) (*out)[i].w[w] = h_keys[(u64)w * n + i];
+}
+
+void DevicePipeline::set_num_records(u64 n) {
+  LOCUST_CHECK_ARG(n <= cap, "too many records for engine capacity");
+  LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+  h_u64[0] = n;  // little endian: low 32 bits == num_records
+  LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_records, h_u64, sizeof(u32),
+                                  hipMemcpyHostToDevice, stream));
+}
+
+void DevicePipeline::upload_keys(const KeysSoA& dst, const PackedKey* keys, u64 n) {
+  grow_host_keys(n);
+  for (u64 i = 0; i < n; ++i)
+    for (int w = 0; w < kKeyWords; ++w) h_keys[(u64)w * n + i] = keys[i].w[w];
+  if (n)
+    for (int w = 0; w < kKeyWords; ++w)
+      LOCUST_HIP_CHECK(hipMemcpyAsync(dst.w[w], h_keys + (u64)w * n, n * sizeof(u64),
+                                      hipMemcpyHostToDevice, stream));
+}
+
+}  // namespace detail
+}  // namespace locust

@@ -182,6 +182,12 @@ class PyGpuEngine {
     py::gil_scoped_release nogil;
     return PyResult{eng_.run(t.input())};
   }
+  // A file streamed through a streaming engine (the CLI's run_direct past one pass).
+  PyResult run_file(const std::string& path) {
+    py::gil_scoped_release nogil;
+    auto src = open_file_source(path);
+    return PyResult{eng_.run_source(*src)};
+  }
 
  private:
   GpuWordCount eng_;
@@ -476,6 +482,8 @@ PYBIND11_MODULE(_locust, m) {
       .def("run_loaded", &PyGpuEngine::run_loaded)
       .def("stats", &PyGpuEngine::stats)
       .def("run_text", &PyGpuEngine::run_text, py::arg("text"))
+      .def("run_file", &PyGpuEngine::run_file, py::arg("path"),
+           "Stream a file through this (streaming) engine, piece by piece.")
       .def("map_stage", &PyGpuEngine::map_stage)
       .def("reduce_stage", &PyGpuEngine::reduce_stage)
       .def("sort_keys", &PyGpuEngine::sort_keys)

@@ -20,3 +20,5 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kexch -o kexch -- python3 tools/exch_prof.py --jobs 20 > $O/kexch.log 2>&1 || { tail -20 $O/kexch.log; exit 1; }
 python3 tools/kstats.py $O/kexch > $O/kexch.summary.txt 2>&1 || true
 head -12 $O/kexch.summary.txt
+timeout -k 10 200 python tools/rss_engines.py --engines 8 --mb 512 > $O/rss_engines.txt 2>&1 || { tail -20 $O/rss_engines.txt; exit 1; }
+cat $O/rss_engines.txt
