@@ -29,7 +29,7 @@ LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -ldl -lpthread
 
 HIP_SRCS  := $(wildcard csrc/kernels/*.hip csrc/engine/*.hip csrc/comm/*.hip)
 CPP_SRCS  := $(wildcard csrc/engine/*.cpp csrc/io/*.cpp csrc/comm/*.cpp)
-HDRS      := $(wildcard csrc/include/locust/*.hpp csrc/include/locust/device/*.hpp csrc/engine/*.hpp)
+HDRS      := $(wildcard csrc/include/locust/*.hpp csrc/include/locust/device/*.hpp csrc/engine/*.hpp csrc/kernels/*.hpp)
 
 HIP_OBJS  := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 CPP_OBJS  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CPP_SRCS))

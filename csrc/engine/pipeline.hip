@@ -222,6 +222,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   lb_scan = {st, counters + 4};
   st += t_scan;
   lb_dict = {st, counters + 5};
+  d_fuse = counters + 6;  // counters[6..7]: the fused launch's ticket and tiles done
 
   rx.cap = cap;
   rx.tile_counters = arena.take<u32>(rx_zero_words);
@@ -555,7 +556,7 @@ void DevicePipeline::launch_dict_graph(const TextInput& in, bool compat) {
   LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
 }
 
-void DevicePipeline::enqueue_map(const TextInput& in) {
+void DevicePipeline::enqueue_map(const TextInput& in, bool launch) {
   plan_pass = false;  // decided per pass (decide_plan) where the map can write occupancy
   parts_ready = cfg.map_path == MapPath::kFast;
   devplan_used = false;
@@ -642,6 +643,7 @@ void DevicePipeline::enqueue_map(const TextInput& in) {
                       in.bytes, make_delim_mask(cfg.delimiters.c_str()), map_text);
     }
     decide_plan(in.bytes);
+    if (launch)
     launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                     cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                     stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
@@ -1038,6 +1040,36 @@ void DevicePipeline::print_ord_trace() {
   }
 }
 
+bool DevicePipeline::fuse_ok(const TextInput& in) const {
+  const char* e = std::getenv("LOCUST_FUSE");
+  if (e && e[0] == '0') return false;
+  return cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict && pieces.empty() &&
+         in.bytes > 0 && in.bytes < kMapLargeInput && cap <= kPartBuildMaxTokens && !large_ordered &&
+         table_tiles(in.bytes) == div_up(in.bytes, (u64)kMapTileBytesMin);
+}
+
+bool DevicePipeline::enqueue_map_ordered(const TextInput& in) {
+  enqueue_map(in, /*launch=*/false);
+  job_self_cleaned = true;  // the ordered half re-zeroes the scratch, the fuse counters too
+  OrderedExtra ex;
+  ex.pm = part_map();
+  ex.part_w = d_pw;
+  ex.split_min = split_min;
+  set_self_clean(ex);
+  if (done_pending) {  // the kernel itself tells the host it is done
+    ex.host_done = d_done;
+    ex.host_done_value = done_pending;
+    done_pending = 0;
+  }
+  set_tile_source(ex, false);
+  set_compact_out(ex, true);
+  ex.fuse = d_fuse;
+  launch_map_ordered(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
+                     cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, part_map(),
+                     d_out_mapped, d_ctr_mapped, lb_dict, stream, ord_trace(), ex);
+  return true;
+}
+
 bool DevicePipeline::enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process,
                         bool self_clean) {
   job_self_cleaned = false;
@@ -1231,9 +1263,11 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
   split_stages = !lean && !graphed;
   skip_sync_reset = clean_start && !compat;
   if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
+  // lean dictionary jobs of a small pass: Map and the ordered build in one launch
+  const bool fused = lean && dict_path && !compat && fuse_ok(in);
   if (lean) {
     enqueue_upload(in);
-    enqueue_map(in);
+    if (!fused) enqueue_map(in);
   } else if (graphed) {
     prepare_upload(in);
     launch_dict_graph(in, compat);
@@ -1257,7 +1291,9 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
     bool ordered = graph_ordered;
     if (lean) {
       done_pending = ++done_seq;
-      ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr, /*self_clean=*/true);
+      ordered = fused ? enqueue_map_ordered(in)
+                      : enqueue_dict_job((u32)in.num_lines, compat, false, nullptr,
+                                         /*self_clean=*/true);
       if (done_pending) publish_done(done_seq);
       done_pending = 0;
     } else if (!graphed) {

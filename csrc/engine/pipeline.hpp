@@ -448,7 +448,15 @@ struct DevicePipeline {
     return in.bytes <= kZeroCopyMaxBytes;
   }
 
-  void enqueue_map(const TextInput& in);
+  // launch = false: the pass's bookkeeping only (partition table, plan decision, flags) --
+  // the fused map + ordered launch maps the text itself (enqueue_map_ordered).
+  void enqueue_map(const TextInput& in, bool launch = true);
+  // The headline job's Map + Process + Reduce in ONE launch (dict.hip map_ordered_kernel):
+  // small single-pass dictionary jobs with the fast map and its partition table.
+  // LOCUST_FUSE=0 (read per job): the two launches instead.
+  u32* d_fuse = nullptr;  // [ticket, tiles done] in the sync block (zeroed with it)
+  bool fuse_ok(const TextInput& in) const;
+  bool enqueue_map_ordered(const TextInput& in);
 
   // Compaction (compat path) + radix sort of `tokens` into `sorted` (and counts).
   // host_n: record count when the host already knows it.  With sync_plan the count is

@@ -594,8 +594,8 @@ class GpuShardEngine final : public ShardEngine {
   void enqueue_range_tail(u32 P, int me, u32 C, u32 G, u64 region, const ExchCollectives& coll) {
     DevicePipeline& m = *mp_;
     launch_merge_rank_slots(reinterpret_cast<const KeyCount*>(xb_.a2a_recv), P, C, xb_.merged,
-                            xb_.rctr, LookbackScratch{xb_.lb_status, xb_.lb_tile}, m.stream);
-    launch_exch_report(xb_.a2a_recv, P, C, xb_.ctl, xb_.rctr, G, xb_.msg3_send, m.stream);
+                            xb_.acc, LookbackScratch{xb_.lb_status, xb_.lb_tile}, m.stream);
+    launch_exch_report(xb_.a2a_recv, P, C, xb_.ctl, xb_.acc, G, xb_.msg3_send, m.stream);
     coll.allgather(xb_.msg3_send, xb_.msg3_all, sizeof(ExchMsg3));
     enqueue_emit(P, me, G, region);
     LOCUST_HIP_CHECK(hipMemcpy2DAsync(xb_.h_hdrs, sizeof(ExchMsg1), xb_.msg1_all,
@@ -1132,7 +1132,7 @@ class GpuShardEngine final : public ShardEngine {
     ExchMsg3* msg3_all = nullptr;
     u32* zero_n = nullptr;
     u32* done = nullptr;
-    MapCounters* rctr = nullptr;
+    u64* acc = nullptr;  // the merge's (firsts, tokens) accumulators (kMergeAccSpread pairs)
     char* a2a_send = nullptr;
     char* a2a_recv = nullptr;
     KeyCount* merged = nullptr;
@@ -1162,7 +1162,7 @@ class GpuShardEngine final : public ShardEngine {
     const u64 o_m1 = take(mb), o_m1a = take(mb * P), o_ctl = take(sizeof(ExchCtl)),
               o_cta = take(sizeof(ExchCtl) * P), o_m3 = take(sizeof(ExchMsg3)),
               o_m3a = take(sizeof(ExchMsg3) * P), o_zn = take(8), o_dn = take(8),
-              o_rc = take(sizeof(MapCounters));
+              o_rc = take(kMergeAccSpread * 2 * sizeof(u64));
     LOCUST_HIP_CHECK(hipMalloc(&xb_.ctl_dev, off));
     // zeroed in stream order: a null-stream hipMemset is not ordered with the engine's
     // non-blocking stream, and with four ranks sharing a GPU it landed after this job's
@@ -1180,7 +1180,7 @@ class GpuShardEngine final : public ShardEngine {
     xb_.msg3_all = reinterpret_cast<ExchMsg3*>(b + o_m3a);
     xb_.zero_n = reinterpret_cast<u32*>(b + o_zn);
     xb_.done = reinterpret_cast<u32*>(b + o_dn);
-    xb_.rctr = reinterpret_cast<MapCounters*>(b + o_rc);
+    xb_.acc = reinterpret_cast<u64*>(b + o_rc);
     LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_msg1, mb, hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_hdrs, sizeof(ExchMsg1) * P, hipHostMallocDefault));
     LOCUST_HIP_CHECK(hipHostMalloc(&xb_.h_msg3, sizeof(ExchMsg3) * P, hipHostMallocDefault));

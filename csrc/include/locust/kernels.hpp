@@ -338,11 +338,22 @@ struct OrderedExtra {
   // ctab[v] = entries | words << 32 (host-mapped, every v of the launch; ~0: not written).
   u64* cout = nullptr;
   u64* ctab = nullptr;
+  // The fused map + ordered kernel's counters ([0] ticket, [1] tiles done; zeroed before
+  // the launch, re-zeroed by the self-clean): launch_map_ordered.
+  u32* fuse = nullptr;
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
                          u64* trace = nullptr, const OrderedExtra& ex = OrderedExtra{});
+// The fast map (1 KiB tiles, part_off table, optional part_occ) and the ordered build over
+// it (TileSource) in one launch (dict.hip map_ordered_kernel): ex.part_off / part_tiles
+// (= ceil(bytes / 1 KiB), bytes < kMapLargeInput) and ex.fuse are required; everything else
+// as launch_map_fast followed by launch_dict_ordered.
+void launch_map_ordered(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
+                        int max_key_len, KeysSoA tokens, u8* parts, u64 cap, MapCounters* ctr,
+                        PartMap pm, OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
+                        hipStream_t s, u64* trace, const OrderedExtra& ex);
 // Writes `value` to the host-mapped `word` once everything earlier on `s` has completed
 // (signal.hip; the lean job path polls it instead of synchronising the stream).
 void launch_signal_host(u32* word, u32 value, hipStream_t s);
@@ -454,17 +465,18 @@ void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey*
 // output records (counters still count all of them).
 // The shuffle tail in two launches around the C3 all-gather:
 // launch_merge_rank_slots merges the received slots into `merged` and sums the distinct
-// keys / tokens into acc->num_unique / acc->total_count (zeroed beforehand: the report
-// re-zeroes them); launch_merge_emit_compact then writes this rank's range as compact
+// keys / tokens into `acc`, kMergeAccSpread (firsts, tokens) u64 pairs (zeroed beforehand:
+// launch_exch_report sums and re-zeroes them); launch_merge_emit_compact then writes this
+// rank's range as compact
 // records (kv.hpp) straight into the shared host output -- region `region` (or the root's,
 // root_msg), word kOutWords x (region x region_records + the lower ranks' records) of
 // `dst` -- and stamps `seq` when the whole range is out (locust/shm.hpp).  Nothing is
 // written when a report flags a problem.  `lb`: merge_scratch_words status words + a tile
 // counter, reset by launch_merge_rank_slots (a second emit of the same merge needs them
 // zeroed again).
+constexpr int kMergeAccSpread = 64;
 void launch_merge_rank_slots(const KeyCount* slots, u32 nslots, u32 slot_records,
-                             KeyCount* merged, MapCounters* acc, LookbackScratch lb,
-                             hipStream_t s);
+                             KeyCount* merged, u64* acc, LookbackScratch lb, hipStream_t s);
 void launch_merge_emit_compact(const KeyCount* slots, u32 nslots, u32 slot_records,
                                const KeyCount* merged, const ExchMsg3* msg3_all,
                                const ExchMsg1* root_msg, u64 region, u32 regions,
@@ -476,10 +488,9 @@ void launch_exch_plan(const char* msg1_all, u32 P, u32 S, ConstKeysSoA keys, con
                       u64* trace = nullptr);
 void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchCtl* ctl, u32 P,
                       u32 slot_records, char* send, hipStream_t s);
-// (rctr: launch_merge_rank_slots' accumulators, re-zeroed once read)
+// (acc: launch_merge_rank_slots' accumulators, summed and re-zeroed here)
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
-                        MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
-                        hipStream_t s);
+                        u64* acc, u32 gather_records, ExchMsg3* msg3, hipStream_t s);
 // ---- device self-test of the string library (tests only; StringTestOut in engine.hpp) ----
 void launch_string_selftest(const char* blob, const u32* off, u32 n, const char* delims,
                             const int* ints, StringTestOut* out, hipStream_t s);

@@ -32,6 +32,7 @@
 #include "locust/device/wave.hpp"
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
+#include "map_tile.hpp"
 
 namespace locust {
 namespace {
@@ -969,11 +970,14 @@ __device__ u32 write_compact_records(u64* __restrict__ dst, u32 m, Word word, u3
   return total;
 }
 
+// The ordered kernel's workgroup (dict_ordered_kernel, and the partition workgroups of the
+// fused map + ordered kernel).  guess: the partition whose runs are worth prefetching while
+// the ticket atomic is in flight (the block index of a plain launch; ~0u: none).
 template <class Src>
-__global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
+__device__ __forceinline__ void ordered_partition(
     Src src, MapCounters* __restrict__ ctr,
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, const OrderedExtra& ex, u32 guess_p) {
 #define ORD_STAMP(k_)                                                          \
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
@@ -1027,7 +1031,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
   // Tickets almost always come out in dispatch order: prefetch the run table for
   // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.
-  const typename Src::Pre guess = vplan ? typename Src::Pre{} : src.prefetch(blockIdx.x);
+  const bool guessing = !vplan && guess_p != ~0u;
+  const typename Src::Pre guess = guessing ? src.prefetch(guess_p) : typename Src::Pre{};
   u32 v, p, vj = 0, vk = 1;
   if (!vplan) {
     v = p = dev::acquire_tile(tile_ctr, &s_tile);
@@ -1092,7 +1097,8 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     trace[(u64)v * 32 + 19] = 0;
   }
   const typename Src::Pre first =
-      vplan ? (vk ? src.prefetch(p) : typename Src::Pre{}) : p == blockIdx.x ? guess : src.prefetch(p);
+      vplan ? (vk ? src.prefetch(p) : typename Src::Pre{})
+            : guessing && p == guess_p ? guess : src.prefetch(p);
   // The in-partition counting sort of a large partition buckets keys by the 8 bits of
   // (w0 - wlo) just below the width of [wlo, whi], the first words actually present: 256
   // order-preserving buckets -- the second byte for keys sharing a first byte, finer bytes
@@ -1148,6 +1154,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   // takes its slice with ONE LDS atomic and its lanes' offsets come from two ballots --
   // no block scan, one barrier.  Token sums and the overflow flag ride along.
   u32* s_rk = s_list + 3 * kPartSlots + 2 * kSmallRank;         // [kSmallRank] ranks
+  u32* s_rkw = s_rk + kSmallRank;  // [kSmallRank] compact word offsets (weighted ranks)
   u64* s_out = reinterpret_cast<u64*>(s_rk + 2 * kSmallRank);    // [5 x kSmallRank] records
   u64* s_k123 = s_out + 6 * kSmallRank;                          // [3 x kSmallRank] words 1-3
   {
@@ -1175,7 +1182,10 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         ++d;
       }
     }
-    if (threadIdx.x < kSmallRank) s_rk[threadIdx.x] = 0;
+    if (threadIdx.x < kSmallRank) {
+      s_rk[threadIdx.x] = 0;
+      s_rkw[threadIdx.x] = 0;
+    }
   }
   __syncthreads();  // the compacted (w0, slot) arrays and the sums are complete
   const u32 m = s_cm;
@@ -1261,6 +1271,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
         }
         const u32 j0 = sl * m / S, j1 = (sl + 1) * m / S;
         u32 cnt = 0;
+        u32 wcnt = 0;  // compact words of the smaller keys: this key's compact offset
         for (u32 j = j0; j < j1; j += 4) {
           u64 c0[4], c1[4], c2[4], c3[4];
 #pragma unroll
@@ -1280,12 +1291,16 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
                             (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
                              (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
             cnt += lt ? 1u : 0u;
+            wcnt += lt ? 2u + (c1[q] != 0) + (c2[q] != 0) + (c3[q] != 0) : 0u;
           }
         }
         if (trace)
           atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 18]),
                     (unsigned long long)__builtin_amdgcn_s_memtime());
-        if (own && cnt) atomicAdd(&s_rk[i], cnt);
+        if (own && cnt) {
+          atomicAdd(&s_rk[i], cnt);
+          atomicAdd(&s_rkw[i], wcnt);
+        }
       }
       if (trace && dev::lane_id() == 0)  // the slowest ranking wave's end
         atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 16]),
@@ -1297,29 +1312,42 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
       dev::st_agent(&status[v], dev::kLbInc | (pre + agg));
     ORD_STAMP(3);
     ORD_STAMP(4);
-    // stage the 40-B records (= KeyCount) in sorted order, then write them with
-    // consecutive lanes on consecutive words (full lines: matters most for the host-mapped
-    // output)
+    // stage the 40-B records (= KeyCount) in sorted order -- or, for the host output, the
+    // compact records at their weighted ranks -- then write them with consecutive lanes on
+    // consecutive words (full lines: matters most for the host-mapped output)
+    const bool cstage = ex.cout && !ex.recs && !ex.sorted.w[0];
+    __shared__ u32 s_cwords;
     for (u32 i = threadIdx.x; i < m; i += kPartBlock) {
       const LdsSlot& sl = s_tab[s_slot[i]];
-      u64* o = s_out + kOutWords * s_rk[i];
-      o[0] = sl.w[0];
-      o[1] = sl.w[1] ^ kWordMagic;
-      o[2] = sl.w[2] ^ kWordMagic;
-      o[3] = sl.w[3] ^ kWordMagic;
-      o[4] = sl.count;
+      const u64 w1 = sl.w[1] ^ kWordMagic, w2 = sl.w[2] ^ kWordMagic, w3 = sl.w[3] ^ kWordMagic;
+      if (cstage) {
+        const u32 nw = w3 ? 4u : w2 ? 3u : w1 ? 2u : 1u;
+        u64* o = s_out + s_rkw[i];
+        o[0] = compact_header(sl.count, nw);
+        o[1] = sl.w[0];
+        if (nw > 1) o[2] = w1;
+        if (nw > 2) o[3] = w2;
+        if (nw > 3) o[4] = w3;
+        if (s_rk[i] == m - 1) s_cwords = s_rkw[i] + 1 + nw;  // the last key's end
+      } else {
+        u64* o = s_out + kOutWords * s_rk[i];
+        o[0] = sl.w[0];
+        o[1] = w1;
+        o[2] = w2;
+        o[3] = w3;
+        o[4] = sl.count;
+      }
     }
     __syncthreads();
     const u64 base_m = pre & kOrdM;
     if (((pre >> kOrdOvfShift) & 511u) == 0) {  // uniform per workgroup
-      if (ex.cout && base_m + m <= ex.out_cap) {  // compact records from the staged ones
-        // scratch past the staged records and words 1-3: s_list[46 KB, 64 KB)
-        u32* s_coff = reinterpret_cast<u32*>(s_k123 + 3 * kSmallRank);
-        u16* s_own = reinterpret_cast<u16*>(s_coff + kSmallRank);
-        cwords = write_compact_records(
-            ex.cout + kOutWords * base_m, m,
-            [&](u32 i, u32 j) { return s_out[kOutWords * i + j]; }, s_coff, s_own,
-            reinterpret_cast<u32*>(s_scan));
+      if (cstage) {  // the staged compact records, at the word their 40-B ones would start
+        const u32 cw = m ? s_cwords : 0u;
+        if (base_m + m <= ex.out_cap) {
+          u64* dst = ex.cout + kOutWords * base_m;
+          for (u32 q = threadIdx.x; q < cw; q += kPartBlock) dst[q] = s_out[q];
+          cwords = cw;
+        }
       } else if (out && base_m + m <= ex.out_cap) {  // 8 B per lane, consecutive lanes
         u64* dst = reinterpret_cast<u64*>(out + base_m);
         for (u32 q = threadIdx.x; q < kOutWords * m; q += kPartBlock) dst[q] = s_out[q];
@@ -1652,6 +1680,10 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
           *tile_ctr = 0;
           *ex.map_lb.tile_counter = 0;
           *ex.done_counter = 0;
+          if (ex.fuse) {  // the fused kernel's ticket and tiles-done counters
+            ex.fuse[0] = 0;
+            ex.fuse[1] = 0;
+          }
         }
       }
       if (ex.host_done && threadIdx.x == 0) {  // every workgroup's writes are out
@@ -1663,6 +1695,65 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   }
 }
 #undef ORD_STAMP
+
+template <class Src>
+__global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
+    Src src, MapCounters* __restrict__ ctr,
+    OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
+  ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, blockIdx.x);
+}
+
+// Map + ordered build of a small pass in ONE launch: ntiles +
+// kDictParts workgroups draw tickets as they start; tickets below ntiles map their 1 KiB
+// tile (maptile::map_tile: tokens, tags, the tile's row of the partition table), release
+// it and count it done; the others are the ordered kernel's partition workgroups, which
+// wait until every tile is counted.  Every tile ticket went to a workgroup already running
+// when a partition workgroup drew its own, so the wait always ends (no dependence on
+// dispatch order or on other kernels sharing the GPU).  What this buys over two launches:
+// no kernel boundary between Map and Process, and the first partition workgroups clear
+// their tables and take their tickets while the map tiles still wait on PCIe.
+// fuse[0]: ticket, fuse[1]: tiles done (zeroed; the ordered kernel's self-clean re-zeroes).
+__global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
+    const char* __restrict__ text, u64 bytes, maptile::Delims d, int E, int max_key,
+    KeysSoA tokens, u8* __restrict__ parts, u64 out_cap, PartMap pm, u32* __restrict__ part_occ,
+    TileSource src, MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
+    MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr,
+    u64* __restrict__ trace, OrderedExtra ex) {
+  __shared__ u32 s_ticket;
+  u32* fuse = ex.fuse;
+  if (threadIdx.x == 0) s_ticket = atomicAdd(&fuse[0], 1u);
+  __syncthreads();
+  const u32 t = s_ticket;
+  if (t < src.ntiles) {
+    maptile::map_tile<1, kPartBlock>(t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
+                                     nullptr, const_cast<u32*>(src.part_off), pm, nullptr,
+                                     part_occ);
+    // every wave's stores are in L2 after the barrier; the agent-scope fence makes them
+    // visible to the other XCDs before the tile is counted
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      atomicAdd(&fuse[1], 1u);
+    }
+    return;
+  }
+  if (threadIdx.x == 0) {
+    // bounded (~1 s): a wait that cannot end marks the run as overflowed instead -- the host
+    // then redoes the Process stage from the tokens after the stream has drained
+    u32 spins = 0;
+    while (__hip_atomic_load(&fuse[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < src.ntiles) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins == (1u << 24)) {
+        atomicOr(&ctr->flags, kCtrDictOverflow);
+        break;
+      }
+    }
+    __threadfence();  // acquire: the tiles' tokens and table rows
+  }
+  __syncthreads();
+  ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, ~0u);
+}
 
 // rank[i] += #{ j in tile : key[j] < key[i] }, persistent over (i-tile, j-tile) pairs.
 constexpr int kRankI = 256;
@@ -1913,6 +2004,23 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
     dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
         src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   }
+  LOCUST_HIP_LAUNCH_CHECK();
+}
+
+void launch_map_ordered(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
+                        int max_key_len, KeysSoA tokens, u8* parts, u64 cap, MapCounters* ctr,
+                        PartMap pm, OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
+                        hipStream_t s, u64* trace, const OrderedExtra& ex) {
+  LOCUST_CHECK_ARG(ex.fuse && ex.part_off && ex.part_tiles &&
+                       ex.part_tiles == div_up(bytes, (u64)kMapTileBytesMin) &&
+                       bytes < kMapLargeInput && bytes > 0,
+                   "fused map + ordered: a small pass with its partition table");
+  const maptile::Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
+  const TileSource src{ConstKeysSoA{{tokens.w[0], tokens.w[1], tokens.w[2], tokens.w[3]}},
+                       ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
+  map_ordered_kernel<<<dim3(ex.part_tiles + kDictParts), dim3(kPartBlock), 0, s>>>(
+      text, bytes, d, emits_per_line, max_key_len, tokens, parts, cap, pm,
+      const_cast<u32*>(ex.part_occ), src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -236,10 +236,10 @@ __global__ __launch_bounds__(256) void exch_pack_kernel(const KeyCount* __restri
 __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict__ recv, u32 P,
                                                          u32 slot_records,
                                                          const ExchCtl* __restrict__ ctl,
-                                                         const MapCounters* __restrict__ rctr,
+                                                         u64* __restrict__ acc,
                                                          u32 gather_records,
-                                                         ExchMsg3* __restrict__ msg3,
-                                                         MapCounters* __restrict__ reset) {
+                                                         ExchMsg3* __restrict__ msg3) {
+  static_assert(kMergeAccSpread == 64, "one accumulator pair per lane");
   const u64 sb = exch_slot_bytes(slot_records);
   bool bad = false;
   for (u32 q = threadIdx.x; q < P; q += 64) {
@@ -247,21 +247,21 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
     bad |= h->status != kSlotOk || h->n > slot_records;
   }
   const u64 any = dev::ballot(bad);
+  // the merge's range: its (firsts, tokens) pairs, then zeroed for the next job
+  const u64 n_range = dev::wave_reduce_sum(acc[2 * threadIdx.x]);
+  const u64 tok_range = dev::wave_reduce_sum(acc[2 * threadIdx.x + 1]);
+  acc[2 * threadIdx.x] = 0;
+  acc[2 * threadIdx.x + 1] = 0;
   if (threadIdx.x == 0) {
     ExchMsg3 m{};
     const u32 cf = ctl->flags;
-    const u64 n_out = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : rctr->num_unique;
+    const u64 n_out = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : n_range;
     m.status = 0;
     m.flags = cf | (any ? kExchRecvTruncated : 0u) | (n_out > gather_records ? kExchGatherOverflow : 0u);
     m.max_bucket = ctl->max_bucket;
     m.n_out = n_out;
-    m.total = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : rctr->total_count;
+    m.total = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : tok_range;
     *msg3 = m;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && reset) {  // the next merge's accumulators (launch_merge_rank_slots)
-    reset->num_unique = 0;
-    reset->total_count = 0;
   }
 }
 
@@ -300,11 +300,9 @@ void launch_exch_pack(const KeyCount* recs, const u32* d_n, u64 cap, const ExchC
 }
 
 void launch_exch_report(const char* recv, u32 P, u32 slot_records, const ExchCtl* ctl,
-                        MapCounters* rctr, u32 gather_records, ExchMsg3* msg3,
-                        hipStream_t s) {
-  // rctr holds launch_merge_rank_slots' accumulators: read, then re-zeroed for the next job
-  exch_report_kernel<<<dim3(1), dim3(64), 0, s>>>(recv, P, slot_records, ctl, rctr,
-                                                   gather_records, msg3, rctr);
+                        u64* acc, u32 gather_records, ExchMsg3* msg3, hipStream_t s) {
+  exch_report_kernel<<<dim3(1), dim3(64), 0, s>>>(recv, P, slot_records, ctl, acc,
+                                                   gather_records, msg3);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 
