@@ -222,7 +222,9 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   lb_scan = {st, counters + 4};
   st += t_scan;
   lb_dict = {st, counters + 5};
-  d_fuse = counters + 6;  // counters[6..7]: the fused launch's ticket and tiles done
+  // counters[6] is the ordered kernels' done counter (lb_dict.tile_counter + 1);
+  // counters[8..9]: the fused launch's ticket and tiles done
+  d_fuse = counters + 8;
 
   rx.cap = cap;
   rx.tile_counters = arena.take<u32>(rx_zero_words);
@@ -267,8 +269,10 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   grow_host_out(std::min<u64>(ucap, kMappedOutMax));
   // and a second one: a job's result holds its buffer while the next job runs, so jobs
   // alternate between two -- allocated here, not inside the second job (pinning a
-  // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job)
-  out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+  // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job).  A streaming engine's jobs
+  // take hundreds of ms: its second buffer is pinned when a second job needs it (host
+  // memory of `--gpus N` file ranks, one streaming engine each).
+  if (!streaming) out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
   use_out(0);
   LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                  hipHostMallocMapped | hipHostMallocCoherent));
@@ -1473,7 +1477,7 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
                    "path with the fast map (sort=dict, map=fast)");
   const u64 max_chunks = div_up(std::max<u64>(src_text.size(), 1), cap_bytes / 2) + 2;
   ensure_stream_buffers(false, max_chunks);
-  const u64 piece = std::min<u64>(cap_bytes, kRingPieceMax);
+  const u64 piece = std::min<u64>(cap_bytes, cfg.ring_piece_bytes ? cfg.ring_piece_bytes : kRingPieceMax);
   if (ring_piece != piece) {
     for (int i = 0; i < kRingPieces; ++i) {
       if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));

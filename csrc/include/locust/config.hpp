@@ -48,6 +48,9 @@ struct JobConfig {
   // > 0: a device pass holds at most this many text bytes; larger inputs stream through
   // in line-aligned chunks (dictionary path).  0: one pass holds the whole input.
   u64 chunk_bytes = 0;
+  // Streamed files: bytes per piece of the pinned read ring (0: 16 MiB).  Ranks of one
+  // process each keep a ring, so `MapReduce <file> --gpus N` shrinks it with N.
+  u64 ring_piece_bytes = 0;
   // Map input read straight from pinned host memory instead of an H2D copy: -1 auto
   // (inputs <= kZeroCopyMaxBytes), 0 never, 1 always (fast map path only).
   int zero_copy_text = -1;

@@ -2,6 +2,7 @@
 // its engine allocates anything).  Build: hipcc --offload-arch=gfx950 -O2 tools/rss_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstring>
 
 // "RssAnon/RssFile/RssShmem" of /proc/self/status, kB.
 static void rss(char* out, size_t n) {
@@ -18,6 +19,32 @@ static void rss(char* out, size_t n) {
 }
 
 __global__ void touch(int* p) { p[threadIdx.x] = threadIdx.x; }
+
+// The mappings holding >= 8 MiB of resident memory (/proc/self/smaps): where the runtime's
+// first-use RSS lives (address range, name, Rss, Anonymous).
+static void big_mappings(const char* when) {
+  std::FILE* f = std::fopen("/proc/self/smaps", "r");
+  if (!f) return;
+  char line[512], head[512] = {0};
+  unsigned long long rss = 0, anon = 0, v = 0;
+  auto flush = [&] {
+    if (head[0] && rss >= 8192) std::printf("  [%s] %8llu kB rss %8llu kB anon  %s", when, rss, anon, head);
+  };
+  while (std::fgets(line, sizeof(line), f)) {
+    if (std::sscanf(line, "Rss: %llu", &v) == 1) { rss = v; continue; }
+    if (std::sscanf(line, "Anonymous: %llu", &v) == 1) { anon = v; continue; }
+    // a mapping header: "start-end perms offset dev inode [name]"
+    unsigned long long a0, a1;
+    if (std::sscanf(line, "%llx-%llx", &a0, &a1) == 2 && std::strchr(line, ' ') &&
+        line[std::strcspn(line, " ") - 1] != ':') {
+      flush();
+      std::snprintf(head, sizeof(head), "%s", line);
+      rss = anon = 0;
+    }
+  }
+  flush();
+  std::fclose(f);
+}
 
 #define STEP(what, call)                                                         \
   do {                                                                           \
@@ -38,6 +65,7 @@ int main() {
   STEP("hipFree(0)", hipFree(nullptr));
   hipStream_t s;
   STEP("hipStreamCreate", hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  big_mappings("stream");
   int* d = nullptr;
   STEP("hipMalloc 1 GiB", hipMalloc(&d, 1ull << 30));
   touch<<<1, 64, 0, s>>>(d);
@@ -48,5 +76,8 @@ int main() {
   STEP("hipHostMalloc mapped 16 MiB", hipHostMalloc(&m, 16ull << 20, hipHostMallocMapped));
   STEP("hipMemcpyAsync H2D 64 MiB", hipMemcpyAsync(d, h, 64ull << 20, hipMemcpyHostToDevice, s));
   STEP("sync", hipStreamSynchronize(s));
+  big_mappings("copy");
+  hipStream_t s2[4];
+  for (int k = 0; k < 4; ++k) STEP("another stream", hipStreamCreateWithFlags(&s2[k], hipStreamNonBlocking));
   return 0;
 }
