@@ -320,6 +320,8 @@ def synth_point(args, rank: int, world: int, dr=None) -> dict:
             "GB_per_s": round(total_bytes / (ms * 1e-3) / 1e9, 3), "bytes": total_bytes,
             "strategy": strategy, "tokens": res.num_tokens if rank == 0 else None,
             "unique": res.num_unique if rank == 0 else None, "gen_s": round(gen_s, 2),
+            "output_bytes_per_key": (round(res.wire_bytes / max(res.num_unique, 1), 2)
+                                     if rank == 0 else None),
             "stages_ms": {k: round(v, 4) for k, v in stages.items()}}
 
 
@@ -582,6 +584,9 @@ def main() -> int:
         "stages_ms_median": {k: round(v, 4) for k, v in stages.items()},
         "tokens": res.num_tokens,
         "unique": res.num_unique,
+        # bytes the device wrote into host memory per result key (compact records: a header
+        # word + the key's non-zero words; 40 for the 40-B record paths)
+        "output_bytes_per_key": round(res.wire_bytes / max(res.num_unique, 1), 2),
         "rccl_ranks": rccl_ranks,
     }
     if cpu:
