@@ -94,10 +94,14 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   if (streaming) cap = std::max<u64>(cap, 1ull << 20);
   cap = std::max<u64>(cap, 1);
   LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
+  // construction phases, logged at LOCUST_LOG=debug (the cold CLI breakdown's engine_ms)
+  u64 tc[6] = {now_ns(), 0, 0, 0, 0, 0};
   LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
   warm_modules_once(cfg.device);
+  tc[1] = now_ns();
   LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto& e : ev) LOCUST_HIP_CHECK(hipEventCreate(&e));
+  tc[2] = now_ns();
 
   const bool compat = cfg.map_path == MapPath::kCompat;
   const u64 slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
@@ -256,6 +260,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
       hipMemcpyAsync(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice, stream));
   LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
 
+  tc[3] = now_ns();
   // A streaming engine reads files through its two staging halves; its one-pass buffer
   // is pinned only when a caller stages text there (input_buffer(), a one-pass job).
   if (!streaming) ensure_h_text();
@@ -294,6 +299,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
   LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
   std::memset(h_ctr, 0, sizeof(MapCounters));
+  tc[4] = now_ns();
   if (large_ordered && cfg.map_path == MapPath::kFast) {
     // what a piecewise pass needs, made here and not inside the first job: the copy
     // streams and piece events, and the plan's scratch
@@ -301,6 +307,12 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
     if (devplan_env) ensure_plan();
     warm_copy_streams();
   }
+  tc[5] = now_ns();
+  LOCUST_LOG_DEBUG("engine (%llu B text, %llu records): modules %.2f ms, stream %.2f ms, device "
+                   "arena %.2f ms (%.1f MiB), pinned host buffers %.2f ms, copy streams %.2f ms",
+                   (unsigned long long)cap_bytes, (unsigned long long)cap, (tc[1] - tc[0]) * 1e-6,
+                   (tc[2] - tc[1]) * 1e-6, (tc[3] - tc[2]) * 1e-6, arena.size / 1048576.0,
+                   (tc[4] - tc[3]) * 1e-6, (tc[5] - tc[4]) * 1e-6);
 }
 
 void DevicePipeline::warm_copy_streams() {
