@@ -115,3 +115,21 @@ def test_shm_segment_placed_before_reserve(capfd):
         assert "to NUMA node 1000 failed" in capfd.readouterr().err
     finally:
         os.environ.pop("LOCUST_LOG", None)
+
+
+def test_rank_slices_from_fake_sysfs(tmp_path):
+    """The shared output's placement end to end on the fake two-socket tree: each rank's
+    node comes from its GPU's PCI address (placement_for_bdf, what GpuShardEngine::numa_node
+    reads), and the plan puts every rank's slice of every region on that node."""
+    sysr = fake_sys(tmp_path)
+    bdfs = [f"{dom:04x}:{bus:02x}:00.0" for dom, bus, _node in GPUS]
+    nodes = [lc._C.gpu_placement(b, sysr)[1] for b in bdfs]
+    assert nodes == [0, 0, 1, 1]
+    region = 4 * 4096 * 64
+    plan = lc._C.plan_rank_slices(4096, region, 3, nodes)
+    for k in range(3):  # per region: ranks 0-1 (node 0), then ranks 2-3 (node 1)
+        base = 4096 + k * region
+        for r, node in enumerate(nodes):
+            lo = base + region * r // 4
+            hit = [n for off, ln, n in plan if off <= lo < off + ln]
+            assert hit == [node], (k, r, plan)
