@@ -86,3 +86,17 @@ def test_json_in_every_mode(tmp_path, cli):
     for p_ in range(3):
         for q in range(3):
             assert d["ranks"][p_]["sent_to"][q] == d["ranks"][q]["recv_from"][p_]
+
+
+def test_library_does_not_link_rccl():
+    """RCCL is dlopen'ed on first use (csrc/comm/rccl_comm.hip): neither liblocust.so nor
+    the CLI lists it among the libraries the dynamic loader maps at start (DT_NEEDED)."""
+    import shutil
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    readelf = shutil.which("readelf") or "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    for f in ("locust_amd/_lib/liblocust.so", "build/MapReduce"):
+        out = subprocess.run([readelf, "-d", os.path.join(root, f)], capture_output=True,
+                             text=True, timeout=60).stdout
+        needed = [ln for ln in out.splitlines() if "NEEDED" in ln]
+        assert needed, out
+        assert not any("rccl" in ln for ln in needed), needed
