@@ -1741,10 +1741,12 @@ __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
   if (threadIdx.x == 0) {
     // bounded (~1 s): a wait that cannot end marks the run as overflowed instead -- the host
     // then redoes the Process stage from the tokens after the stream has drained
+    // relaxed polls (an acquire per poll invalidates the caches the map tiles are using:
+    // measured 90 us fused kernels), then one acquire once every tile is counted
     u32 spins = 0;
-    while (__hip_atomic_load(&fuse[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < src.ntiles) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins == (1u << 24)) {
+    while (__hip_atomic_load(&fuse[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < src.ntiles) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins == (1u << 22)) {
         atomicOr(&ctr->flags, kCtrDictOverflow);
         break;
       }

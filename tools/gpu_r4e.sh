@@ -1,0 +1,21 @@
+# Headline kernels, fused vs two launches, compact vs 40-B: kernel stats of the CLI on whole
+# Hamlet under each setting, ordered-kernel phase traces, and the in-process A/B.
+# Usage: bash tools/gpu_r4e.sh TAG
+set -e
+cd $GRAFT_REPO_ROOT
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4e}
+mkdir -p $O
+export TMPDIR=/tmp
+CLI=$GRAFT_REPO_ROOT/build/MapReduce
+H=$GRAFT_REPO_ROOT/data/hamlet.txt
+cd /tmp
+for v in "fused:LOCUST_FUSE=1" "two:LOCUST_FUSE=0" "two40:LOCUST_FUSE=0 LOCUST_COMPACT_OUT=0" "fused40:LOCUST_FUSE=1 LOCUST_COMPACT_OUT=0"; do
+  n=${v%%:*}; e=${v#*:}
+  env $e timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/k_$n -o run --output-format csv -- $CLI $H --warmup 5 --iters 40 --quiet > /dev/null
+  echo "== $n ($e)"; python3 $GRAFT_REPO_ROOT/tools/kstats.py $O/k_$n/run_kernel_stats.csv | head -3
+done
+cd $GRAFT_REPO_ROOT
+LOCUST_FUSE=0 LOCUST_ORD_TRACE=1 timeout -k 10 60 $CLI $H --warmup 5 --iters 3 --quiet > /dev/null 2> $O/ordtrace_two.txt || true
+tail -12 $O/ordtrace_two.txt
+timeout -k 10 200 python tools/env_ab.py "LOCUST_FUSE=1" "LOCUST_FUSE=0" "LOCUST_FUSE=0,LOCUST_COMPACT_OUT=0" --config hamlet4500 > $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 1; }
+tail -3 $O/ab.txt
