@@ -1,6 +1,7 @@
 // Shared host-side pieces: logging, errors, env config, tokenizer oracle, result checks.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdarg>
 #include <cstring>
 #include <string>
@@ -64,6 +65,18 @@ u64 now_ns() {
   return (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
       .count();
+}
+
+u64 process_rss_kb(bool peak) {
+  std::FILE* f = std::fopen("/proc/self/status", "r");
+  if (!f) return 0;
+  char line[256];
+  unsigned long long kb = 0;
+  const char* key = peak ? "VmHWM: %llu kB" : "VmRSS: %llu kB";
+  while (std::fgets(line, sizeof(line), f))
+    if (std::sscanf(line, key, &kb) == 1) break;
+  std::fclose(f);
+  return kb;
 }
 
 void apply_env_overrides(JobConfig& cfg) {

@@ -178,6 +178,8 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
         std::unique_ptr<ShardEngine> eng =
             gpu ? make_gpu_shard_engine(job, std::max<u64>(in.bytes, 1), std::max<u64>(in.lines, 1))
                 : make_cpu_shard_engine(job);
+        LOCUST_LOG_DEBUG("rank %d: engine built, process rss %llu kB", r,
+                         (unsigned long long)process_rss_kb());
         std::unique_ptr<TextSource> keep;
         const TextInput shard = in.load(*eng, &keep);
         // the same engines and communicators across jobs, like a long-lived rank
@@ -185,6 +187,9 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
           LOCUST_CHECK_ARG(!shard.source || schedule.size() == 1,
                            "a streamed file shard is read once: one job per run");
           DistResult d = run_distributed(schedule[j], *comm, *eng, shard);
+          LOCUST_LOG_DEBUG("rank %d: job %zu done, process rss %llu kB (peak %llu kB)", r, j,
+                           (unsigned long long)process_rss_kb(),
+                           (unsigned long long)process_rss_kb(true));
           d.input_bytes = shard.bytes;
           d.input_streamed = shard.source != nullptr;
           d.peer_p2p = gpu ? peers_of(job.device) : -1;

@@ -62,5 +62,7 @@ bool fault_injected(int rank, const char* stage);
 
 // Monotonic host clock in nanoseconds.
 u64 now_ns();
+// Resident host memory of this process, kB: VmRSS (peak = false) or VmHWM (peak = true).
+u64 process_rss_kb(bool peak = false);
 
 }  // namespace locust

@@ -19,3 +19,9 @@ LOCUST_FUSE=0 LOCUST_ORD_TRACE=1 timeout -k 10 60 $CLI $H --warmup 5 --iters 3 -
 tail -12 $O/ordtrace_two.txt
 timeout -k 10 200 python tools/env_ab.py "LOCUST_FUSE=1" "LOCUST_FUSE=0" "LOCUST_FUSE=0,LOCUST_COMPACT_OUT=0" --config hamlet4500 > $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 1; }
 tail -3 $O/ab.txt
+# where a multi-rank file job's host memory goes: per-rank RSS stamps (LOCUST_LOG=debug)
+F=/tmp/locust_rss_$$.txt
+timeout -k 10 200 $CLI --gen $F --gen-bytes $((4<<30)) --seed 7 > /dev/null
+LOCUST_LOG=debug timeout -k 10 300 $CLI $F --gpus 8 --comm loopback --quiet --json $O/rss8.json > /dev/null 2> $O/rss8.err || true
+rm -f $F
+grep -E "rss|engine \(" $O/rss8.err | head -40
