@@ -433,6 +433,7 @@ int run_direct(const CliArgs& a) {
     in.first_line = 0;
     st.read = now_ns();
     for (int i = 0; i < a.warmup + a.iters; ++i) {
+      const u64 tj = now_ns();
       if (i < a.warmup) {
         eng.run(in);
       } else {
@@ -440,6 +441,8 @@ int run_direct(const CliArgs& a) {
         walls.push_back(r.times.wall_ms);
       }
       if (i == 0) st.first = now_ns();
+      LOCUST_LOG_DEBUG("job %d: %.3f ms host (the job's own wall %.3f ms)", i, (now_ns() - tj) * 1e-6,
+                       i < a.warmup ? 0.0 : r.times.wall_ms);
     }
     r.num_lines = in.num_lines;
   }

@@ -98,18 +98,27 @@ u64 part_map_from_entries(const EntryList& entries, PartMapTables* t, u32 max_di
     total += work;
   }
   if (!total) return 0;
-  u64 target = std::max<u64>(1, (total + kDictParts - 1) / kDictParts);
-  for (int tries = 0; tries < 400; ++tries) {
-    PartMapTables cand;
-    u64 worst = 0;
-    if (assign(g, target, max_distinct, &cand, &worst) <= (u32)kDictParts) {
-      *t = cand;
-      return worst;
-    }
-    target += target / 16 + 1;  // too many ranges: coarser
-    if (tries > 100) max_distinct += max_distinct / 8 + 1;
+  // The smallest work target whose greedy sweep fits kDictParts ranges: the range count
+  // only falls as the target grows, so a binary search finds it in ~log2(total) sweeps
+  // (a linear 1/16 step search took up to 400: 1.6 ms of host time for Hamlet's output).
+  // If even target = total does not fit, the distinct-key cap is what binds: raise it.
+  PartMapTables cand;
+  u64 worst = 0;
+  for (int widen = 0; widen < 64; ++widen) {
+    if (assign(g, total, max_distinct, &cand, &worst) <= (u32)kDictParts) break;
+    max_distinct += max_distinct / 8 + 1;
   }
-  return 0;  // unreachable in practice: the default map stays
+  u64 lo = std::max<u64>(1, (total + kDictParts - 1) / kDictParts), hi = total;
+  while (lo < hi) {  // invariant: hi fits
+    const u64 mid = lo + (hi - lo) / 2;
+    if (assign(g, mid, max_distinct, &cand, &worst) <= (u32)kDictParts)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  if (assign(g, hi, max_distinct, &cand, &worst) > (u32)kDictParts) return 0;  // default map stays
+  *t = cand;
+  return worst;
 }
 
 }  // namespace locust

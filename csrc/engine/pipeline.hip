@@ -271,7 +271,8 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   // kernels that write it directly emit at most kMappedOutMax records (larger results
   // take the radix path, whose download grows the buffer), so a streaming engine with a
   // 16M-key dictionary does not pin 800 MB per output buffer.
-  grow_host_out(std::min<u64>(ucap, kMappedOutMax));
+  out_pool.push_back(std::make_shared<HostOut>(std::min<u64>(ucap, kMappedOutMax)));
+  use_out(0);
   // and a second one: a job's result holds its buffer while the next job runs, so jobs
   // alternate between two -- allocated here, not inside the second job (pinning a
   // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job).  A streaming engine's jobs

@@ -100,21 +100,24 @@ def test_rank_slices_plan():
     assert [s[2] for s in p8] == [0] + list(range(1, 8)) + list(range(8)) * 2
 
 
-def test_shm_segment_placed_before_reserve(capfd):
+def test_shm_segment_placed_before_reserve():
     """The plan is applied to the mapping before posix_fallocate reserves the pages (shmem
     keeps it as the object's policy): every page lands on its slice's node.  This box has
     node 0 only, so the plan binds everything there and a slice naming an absent node is
-    logged and skipped, not fatal."""
-    os.environ["LOCUST_LOG"] = "info"
-    try:
-        nodes = lc._C.shm_placement_probe(64 * 4096, [(0, 32 * 4096, 0), (32 * 4096, 32 * 4096, 0)])
-        assert nodes == [0] * 64
-        assert "preferred on NUMA node 0" in capfd.readouterr().err
-        nodes = lc._C.shm_placement_probe(8 * 4096, [(0, 8 * 4096, 1000)])
-        assert len(nodes) == 8
-        assert "to NUMA node 1000 failed" in capfd.readouterr().err
-    finally:
-        os.environ.pop("LOCUST_LOG", None)
+    logged and skipped, not fatal.  (A child process: the log level is read once.)"""
+    import subprocess
+    import sys
+
+    code = ("import locust_amd as lc\n"
+            "print(lc._C.shm_placement_probe(64 * 4096, [(0, 32 * 4096, 0), (32 * 4096, 32 * 4096, 0)]))\n"
+            "print(len(lc._C.shm_placement_probe(8 * 4096, [(0, 8 * 4096, 1000)])))\n")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, LOCUST_LOG="info"))
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.splitlines()
+    assert out[0] == str([0] * 64) and out[1] == "8"
+    assert "preferred on NUMA node 0" in p.stderr
+    assert "to NUMA node 1000 failed" in p.stderr
 
 
 def test_rank_slices_from_fake_sysfs(tmp_path):
