@@ -1635,14 +1635,20 @@ __device__ __forceinline__ void ordered_partition(
       ctr_out->flags = ctr->flags | (ovf_total ? kCtrDictOverflow : 0u);
     }
     if (ex.hdr) {  // the gather slot's header: this rank's records are complete
-      SlotHeader h = ex.tmpl;
-      h.status = ovf_total ? kSlotRedo : h.status;
-      h.n = u;
-      h.tokens = ctr->num_records;
-      h.overflow_lines = ctr->overflow_lines;
-      h.truncated = ctr->truncated;
-      h.max_key_len = ctr->max_key_len;
-      *ex.hdr = h;
+      // field by field from the template: a whole-struct copy went through private memory
+      // (64 B of scratch per lane for every ordered kernel, and its setup at each launch)
+      SlotHeader* hd = ex.hdr;
+      hd->status = ovf_total ? kSlotRedo : ex.tmpl.status;
+      hd->record_flags = ex.tmpl.record_flags;
+      hd->n = u;
+      hd->lines = ex.tmpl.lines;
+      hd->tokens = ctr->num_records;
+      hd->overflow_lines = ctr->overflow_lines;
+      hd->truncated = ctr->truncated;
+      hd->max_key_len = ctr->max_key_len;
+      hd->slot_cap = ex.tmpl.slot_cap;
+      hd->pad[0] = ex.tmpl.pad[0];
+      hd->pad[1] = ex.tmpl.pad[1];
     }
   }
   if (ex.self_clean) {
@@ -1726,7 +1732,8 @@ __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
   __syncthreads();
   const u32 t = s_ticket;
   if (t < src.ntiles) {
-    maptile::map_tile<1, kPartBlock>(t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
+    __shared__ maptile::MapTileLds<1, kPartBlock> lds;
+    maptile::map_tile<1, kPartBlock>(lds, t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
                                      nullptr, const_cast<u32*>(src.part_off), pm, nullptr,
                                      part_occ);
     // every wave's stores are in L2 after the barrier; the agent-scope fence makes them

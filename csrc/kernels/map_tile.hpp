@@ -26,6 +26,10 @@ constexpr int kPost = 64;  // right overhang staged after the tile (>= 40 for pa
 
 // Delimiter set incl. '\n' and NUL (a NUL also kills the rest of its line, see
 // backward_line_ordinal), held in scalar registers.
+// (Passed by reference to the kernel's own argument: a by-value copy inside a device
+// function became a private array that the backend promoted to LDS -- 32 B x 1,024 threads
+// of it, and every membership test a dynamically indexed LDS read: the map kernel took
+// 20 us instead of 13.)
 struct Delims {
   u64 m0, m1, m2, m3;
   __device__ __forceinline__ bool has(u32 c) const {
@@ -60,7 +64,7 @@ struct TileText {
 // suppresses every later emit (and the overflow count) of the line, exactly as dead bytes
 // would, so a NUL further back need not be found.
 template <typename TT>
-__device__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32 cap,
+__device__ __forceinline__ u32 backward_line_ordinal(const TT& tt, i64 pos, const Delims& d, u32 cap,
                                      bool* dead) {
   const int lane = lane_id();
   u32 count = 0;
@@ -122,40 +126,62 @@ __device__ __forceinline__ void pack_token(const unsigned char* s_text, int o, u
   }
 }
 
+// The tile's LDS, declared __shared__ by the calling kernel and passed in: LDS variables
+// declared inside a device function are lowered to module scope, where every kernel of the
+// file that reaches any instantiation pays for all of them (map_fast_kernel<1, 1024> grew
+// from 4.4 to 37 KB of LDS that way).
+template <int kSteps, int kBlock>
+struct MapTileLds {
+  static constexpr int kSeg = kSteps * 64;
+  static constexpr int kTile = (kBlock / 64) * kSeg;
+  static constexpr int kStaged = kPre + kTile + kPost;
+  static constexpr bool kCombineTile = kSteps > 1;
+  static constexpr int kListPerWave = kSteps > 1 ? kSeg / 2 : 1;
+  __attribute__((aligned(16))) unsigned char text[kStaged];
+  u64 prefix;
+  u32 wave_cnt[kBlock / 64];
+  // partition grouping (with part_off): per-partition counts, then offsets
+  u32 pcnt[kPartTable];
+  // per-tile combining (large grouped tiles with `counts`): the first short key (<= 7 bytes,
+  // one word) of each partition claims a slot; its repeats in the tile become one record
+  u64 hot[kCombineTile ? kDictParts : 1];
+  u32 hotc[kCombineTile ? kDictParts : 1];
+  // the partition map's range starts (PartMap), staged once per tile: 2 KB, searched per token
+  u64 plo[kDictParts + 1];
+  // grouped large tiles: each wave's token starts (LDS offset | length << 16), at most one
+  // per two bytes of its segment
+  u32 list[(kBlock / 64) * kListPerWave];
+};
+
 // One map tile (the body of map_fast_kernel): kBlock threads, tile index `tile` -- the
 // block index of map_fast_kernel, or a ticket of the fused map + ordered kernel (dict.hip).
 template <int kSteps, int kBlock>
 __device__ __forceinline__ void map_tile(
-    const u32 tile, const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key,
-    KeysSoA out, u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr,
-    u64* __restrict__ trace, u32* __restrict__ part_off, PartMap pm, u64* __restrict__ counts,
-    u32* __restrict__ part_occ) {
+    MapTileLds<kSteps, kBlock>& lds, const u32 tile, const char* __restrict__ text, u64 bytes,
+    const Delims& d, int E, int max_key, KeysSoA out, u8* __restrict__ parts, u64 out_cap,
+    MapCounters* __restrict__ ctr, u64* __restrict__ trace, u32* __restrict__ part_off, PartMap pm,
+    u64* __restrict__ counts, u32* __restrict__ part_occ) {
   // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
   // at entry, tile acquired, text staged, masks done, prefix known, keys written.
   const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
 #define MAP_STAMP(k_)                                                           \
   if (trace && threadIdx.x == 0 && tile < 4096) trace[(u64)tile * 8 + (k_)] = __builtin_amdgcn_s_memrealtime()
-  constexpr int kSeg = kSteps * 64;
-  constexpr int kTile = (kBlock / 64) * kSeg;
-  constexpr int kStaged = kPre + kTile + kPost;
-  __shared__ __attribute__((aligned(16))) unsigned char s_text[kStaged];
-  __shared__ u64 s_prefix;
-  __shared__ u32 s_wave_cnt[kBlock / 64];
-  // partition grouping (with part_off): per-partition counts, then offsets
-  __shared__ u32 s_pcnt[kPartTable];
-  // per-tile combining (large grouped tiles with `counts`): the first short key (<= 7 bytes,
-  // one word) of each partition claims a slot; its repeats in the tile become one record
-  constexpr bool kCombineTile = kSteps > 1;
-  __shared__ u64 s_hot[kCombineTile ? kDictParts : 1];
-  __shared__ u32 s_hotc[kCombineTile ? kDictParts : 1];
-  const bool combine = kCombineTile && part_off && counts;
-  // the partition map's range starts (PartMap), staged once per tile: 2 KB, searched per token
-  __shared__ u64 s_plo[kDictParts + 1];
-  // grouped large tiles: each wave's token starts (LDS offset | length << 16), at most one
-  // per two bytes of its segment
-  constexpr int kListPerWave = kSteps > 1 ? kSeg / 2 : 1;
+  using L = MapTileLds<kSteps, kBlock>;
+  constexpr int kSeg = L::kSeg;
+  constexpr int kTile = L::kTile;
+  constexpr int kStaged = L::kStaged;
+  constexpr bool kCombineTile = L::kCombineTile;
+  constexpr int kListPerWave = L::kListPerWave;
   constexpr int kListRounds = kListPerWave / 64 > 0 ? kListPerWave / 64 : 1;
-  __shared__ u32 s_list[(kBlock / 64) * kListPerWave];
+  unsigned char* s_text = lds.text;
+  u64& s_prefix = lds.prefix;
+  u32* s_wave_cnt = lds.wave_cnt;
+  u32* s_pcnt = lds.pcnt;
+  u64* s_hot = lds.hot;
+  u32* s_hotc = lds.hotc;
+  u64* s_plo = lds.plo;
+  u32* s_list = lds.list;
+  const bool combine = kCombineTile && part_off && counts;
   const int lane = lane_id(), w = wave_id();
   const u64 num_tiles = div_up(bytes, (u64)kTile);
   // Tokens are emitted in no particular order across tiles (every consumer sorts or

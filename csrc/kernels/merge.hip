@@ -304,7 +304,9 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_compact_kernel(
       if (!v[e].count) continue;
       u64* o = s_out + at;
       o[0] = compact_header(v[e].count, nw[e]);
-      for (u32 j = 0; j < nw[e]; ++j) o[1 + j] = v[e].w[j];
+#pragma unroll
+      for (u32 j = 0; j < (u32)kKeyWords; ++j)  // static indices: v stays in registers
+        if (j < nw[e]) o[1 + j] = v[e].w[j];
       at += 1 + nw[e];
     }
     __syncthreads();

@@ -37,8 +37,9 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ trace,
     u32* __restrict__ part_off, PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_occ) {
-  map_tile<kSteps, kBlock>(blockIdx.x, text, bytes, d, E, max_key, out, parts, out_cap, ctr, trace,
-                           part_off, pm, counts, part_occ);
+  __shared__ MapTileLds<kSteps, kBlock> lds;
+  map_tile<kSteps, kBlock>(lds, blockIdx.x, text, bytes, d, E, max_key, out, parts, out_cap, ctr,
+                           trace, part_off, pm, counts, part_occ);
 }
 
 }  // namespace

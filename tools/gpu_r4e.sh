@@ -25,3 +25,12 @@ timeout -k 10 200 $CLI --gen $F --gen-bytes $((4<<30)) --seed 7 > /dev/null
 LOCUST_LOG=debug timeout -k 10 300 $CLI $F --gpus 8 --comm loopback --quiet --json $O/rss8.json > /dev/null 2> $O/rss8.err || true
 rm -f $F
 grep -E "rss|engine \(" $O/rss8.err | head -40
+# control: the round-3 closing build (a worktree under ab/r3, built in-tree), same box
+if [ -x ab/r3/build/MapReduce ]; then
+  cd /tmp
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/k_r3 -o run --output-format csv -- $GRAFT_REPO_ROOT/ab/r3/build/MapReduce $H --warmup 5 --iters 40 --quiet > /dev/null
+  echo "== r3 control"; python3 $GRAFT_REPO_ROOT/tools/kstats.py $O/k_r3/run_kernel_stats.csv | head -3
+  cd $GRAFT_REPO_ROOT
+  timeout -k 10 200 python ab/r3/bench.py --steps 200 --warmup 20 --no-extra > $O/bench_r3.json 2> $O/bench_r3.err && python -c "import json;print('r3 control headline', json.load(open('$O/bench_r3.json'))['value'])"
+  timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-extra > $O/bench_now.json 2> $O/bench_now.err && python -c "import json;print('now headline', json.load(open('$O/bench_now.json'))['value'])"
+fi
