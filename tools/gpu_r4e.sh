@@ -6,6 +6,9 @@ cd $GRAFT_REPO_ROOT
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4e}
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_engine.py tests/test_dist.py tests/test_switches.py \
+  tests/test_compact.py -x -q --timeout 200 --timeout-method thread -m gpu > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
+tail -1 $O/pytest.txt
 CLI=$GRAFT_REPO_ROOT/build/MapReduce
 H=$GRAFT_REPO_ROOT/data/hamlet.txt
 cd /tmp
