@@ -1040,9 +1040,42 @@ void DevicePipeline::print_ord_trace() {
       last_p = p;
     }
   }
+  // a fused launch (map_ordered_kernel) also stamps its map tiles: start 21, counted 22
+  u64 tile_in = ~0ull, tile_out = 0;
+  int ntile = 0;
+  for (int p = 0; p < kDictParts; ++p) {
+    const u64* x = &t[p * 32];
+    if (!x[21]) continue;
+    ++ntile;
+    tile_in = std::min(tile_in, x[21]);
+    if (x[22] >= x[23]) tile_out = std::max(tile_out, x[22]);
+  }
+  if (ntile) first_in = std::min(first_in, tile_in);
   if (last_p >= 0)
     std::fprintf(stderr, "ord span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
                  (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 32 + 6]);
+  if (ntile) {
+    u64 wait_end = 0;
+    for (int p = 0; p < kDictParts; ++p)
+      if (t[p * 32 + 20]) wait_end = std::max(wait_end, t[p * 32 + 20]);
+    std::vector<double> body, fence;
+    for (int p = 0; p < kDictParts; ++p) {
+      const u64* x = &t[p * 32];
+      if (!x[21]) continue;
+      body.push_back((x[23] - x[21]) * 0.01);
+      if (x[22] >= x[23]) fence.push_back((x[22] - x[23]) * 0.01);  // a worker's first tile
+    }
+    std::sort(body.begin(), body.end());
+    std::sort(fence.begin(), fence.end());
+    if (fence.empty()) fence.push_back(0.0);
+    std::fprintf(stderr,
+                 "fused: %d tiles stamped, first tile start %.2f us, last tile counted %.2f us, "
+                 "last partition wait end %.2f us; tile body median %.2f max %.2f us, release "
+                 "median %.2f max %.2f us\n",
+                 ntile, (tile_in - first_in) * 0.01, (tile_out - first_in) * 0.01,
+                 wait_end ? (wait_end - first_in) * 0.01 : 0.0, body[body.size() / 2],
+                 body.back(), fence[fence.size() / 2], fence.back());
+  }
   for (int p = 0; p < kDictParts; ++p) {
     const u64* x = &t[p * 32];
     if (!x[0] || !x[6]) continue;
@@ -1050,19 +1083,22 @@ void DevicePipeline::print_ord_trace() {
     std::fprintf(stderr,
                  "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
                  " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
-                 " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu\n",
+                 " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu"
+                 " | waited=%6.2f us\n",
                  p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
                  d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
-                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16));
+                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16),
+                 x[20] ? (x[20] - x[10]) * 0.01 : 0.0);
   }
 }
 
 bool DevicePipeline::fuse_ok(const TextInput& in) const {
   const char* e = std::getenv("LOCUST_FUSE");
-  if (e && e[0] == '0') return false;
+  if (!e || e[0] != '1') return false;  // opt-in: measured slower than two launches
   return cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict && pieces.empty() &&
          in.bytes > 0 && in.bytes < kMapLargeInput && cap <= kPartBuildMaxTokens && !large_ordered &&
-         table_tiles(in.bytes) == div_up(in.bytes, (u64)kMapTileBytesMin);
+         table_tiles(in.bytes) == div_up(in.bytes, (u64)kMapTileBytesMin) &&
+         table_tiles(in.bytes) <= (u64)kFuseMaxTiles;
 }
 
 bool DevicePipeline::enqueue_map_ordered(const TextInput& in) {

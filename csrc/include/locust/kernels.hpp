@@ -66,6 +66,9 @@ constexpr int kMapSegStepsSmall = 4;
 constexpr int kMapSegStepsLarge = 16;
 constexpr int kMapTileBytesMin = (kMapBlock / 64) * kMapSegStepsSmall * 64;
 constexpr u64 kMapLargeInput = 8ull << 20;  // switch to large tiles above 8 MiB
+// the fused map + ordered launch (map_ordered_kernel) maps at most this many 1 KiB tiles:
+// one per workgroup of its kDictParts
+constexpr u32 kFuseMaxTiles = 256;
 constexpr int kLineIdxBlock = 256;
 constexpr int kLineIdxItems = 16;                             // bytes per thread
 constexpr int kLineIdxTile = kLineIdxBlock * kLineIdxItems;

@@ -977,7 +977,8 @@ template <class Src>
 __device__ __forceinline__ void ordered_partition(
     Src src, MapCounters* __restrict__ ctr,
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr, u64* __restrict__ trace, const OrderedExtra& ex, u32 guess_p) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, const OrderedExtra& ex, u32 guess_p,
+    u64 rt_in = 0) {
 #define ORD_STAMP(k_)                                                          \
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
@@ -997,7 +998,9 @@ __device__ __forceinline__ void ordered_partition(
   // sharing the GPU (the TCP / loopback rehearsals) could fill the CUs with spinning
   // workgroups whose predecessors were never dispatched: measured as multi-second stalls
   // and a hang with four ranks on one GPU.
-  const u64 rt_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz, device-wide
+  // 100 MHz, device-wide; a fused launch passes its workgroup's start (before the tile wait)
+  const u64 rt_now = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  const u64 rt_entry = rt_in ? rt_in : rt_now;
   // v: this workgroup's virtual partition = its ticket (the look-back order); p: the map
   // partition whose tokens it reads; (vj, vk): its share of p (see OrderedExtra::part_occ).
   // Without a plan, v == p and vk == 1.
@@ -1091,6 +1094,7 @@ __device__ __forceinline__ void ordered_partition(
   ORD_STAMP(0);
   if (trace && threadIdx.x == 0) {
     trace[(u64)v * 32 + 10] = rt_entry;
+    trace[(u64)v * 32 + 20] = rt_in ? rt_now : 0;  // fused: the tile wait's end
     trace[(u64)v * 32 + 16] = 0;
     trace[(u64)v * 32 + 17] = ~0ull;
     trace[(u64)v * 32 + 18] = 0;
@@ -1710,16 +1714,19 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
   ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, blockIdx.x);
 }
 
-// Map + ordered build of a small pass in ONE launch: ntiles +
-// kDictParts workgroups draw tickets as they start; tickets below ntiles map their 1 KiB
-// tile (maptile::map_tile: tokens, tags, the tile's row of the partition table), release
-// it and count it done; the others are the ordered kernel's partition workgroups, which
-// wait until every tile is counted.  Every tile ticket went to a workgroup already running
-// when a partition workgroup drew its own, so the wait always ends (no dependence on
-// dispatch order or on other kernels sharing the GPU).  What this buys over two launches:
-// no kernel boundary between Map and Process, and the first partition workgroups clear
-// their tables and take their tickets while the map tiles still wait on PCIe.
-// fuse[0]: ticket, fuse[1]: tiles done (zeroed; the ordered kernel's self-clean re-zeroes).
+// Map + ordered build of a small pass in ONE launch: kDictParts
+// workgroups, each first a map worker -- it claims 1 KiB tiles from a queue (fuse[0]) and
+// maps them (maptile::map_tile: tokens, tags, the tile's row of the partition table) until
+// the queue is empty, then releases its tiles once and counts them (fuse[1]) -- and then
+// one of the ordered kernel's partition workgroups, which waits until every tile is
+// counted.  A workgroup waits only once the queue is empty, i.e. once every tile is held by
+// a running workgroup, so the wait always ends (no dependence on dispatch order or on other
+// kernels sharing the GPU).  Roles by ticket over ntiles + kDictParts workgroups (the first
+// version) put the tiles wherever the ticket race put them: one workgroup per CU (the
+// ordered kernel's LDS), so XCDs that drew few tiles filled with waiting partitions and
+// ~60 partitions dispatched only after the first ones finished (trace: last entries at
+// 41 us of a 51 us kernel).  The fused path takes passes of at most kFuseMaxTiles tiles.
+// fuse[0]: tile queue, fuse[1]: tiles done (the ordered kernel's self-clean re-zeroes both).
 __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
     const char* __restrict__ text, u64 bytes, maptile::Delims d, int E, int max_key,
     KeysSoA tokens, u8* __restrict__ parts, u64 out_cap, PartMap pm, u32* __restrict__ part_occ,
@@ -1727,29 +1734,42 @@ __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
     MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr,
     u64* __restrict__ trace, OrderedExtra ex) {
   __shared__ u32 s_ticket;
+  __shared__ maptile::MapTileLds<1, kPartBlock> lds;
   u32* fuse = ex.fuse;
-  if (threadIdx.x == 0) s_ticket = atomicAdd(&fuse[0], 1u);
-  __syncthreads();
-  const u32 t = s_ticket;
-  if (t < src.ntiles) {
-    __shared__ maptile::MapTileLds<1, kPartBlock> lds;
+  // diagnostics (LOCUST_ORD_TRACE): tile t's start / body end / counted at
+  // trace[t * 32 + 21 / 23 / 22]
+  const u64 rt0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  u32 mapped = 0, first = 0;
+  for (;;) {
+    if (threadIdx.x == 0) s_ticket = atomicAdd(&fuse[0], 1u);
+    __syncthreads();
+    const u32 t = s_ticket;
+    __syncthreads();  // every thread has read the ticket before the next claim
+    if (t >= src.ntiles) break;
+    const u64 rt1 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     maptile::map_tile<1, kPartBlock>(lds, t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
                                      nullptr, const_cast<u32*>(src.part_off), pm, nullptr,
                                      part_occ);
-    // every wave's stores are in L2 after the barrier; the agent-scope fence makes them
-    // visible to the other XCDs before the tile is counted
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      atomicAdd(&fuse[1], 1u);
+    __syncthreads();  // the tile's LDS is free; every wave's stores are issued
+    if (trace && threadIdx.x == 0 && t < kDictParts) {
+      trace[(u64)t * 32 + 21] = rt1;
+      trace[(u64)t * 32 + 23] = __builtin_amdgcn_s_memrealtime();
     }
-    return;
+    if (!mapped) first = t;
+    ++mapped;
   }
   if (threadIdx.x == 0) {
+    if (mapped) {
+      // the agent-scope release writes this XCD's L2 back: the tiles' tokens and table rows
+      // become visible to the other XCDs before they are counted
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      atomicAdd(&fuse[1], mapped);
+      if (trace && first < kDictParts) trace[(u64)first * 32 + 22] = __builtin_amdgcn_s_memrealtime();
+    }
     // bounded (~1 s): a wait that cannot end marks the run as overflowed instead -- the host
-    // then redoes the Process stage from the tokens after the stream has drained
-    // relaxed polls (an acquire per poll invalidates the caches the map tiles are using:
-    // measured 90 us fused kernels), then one acquire once every tile is counted
+    // then redoes the Process stage from the tokens after the stream has drained.  Relaxed
+    // polls (an acquire per poll invalidates the L2 the map tiles are using: measured 90 us
+    // fused kernels), then one acquire once every tile is counted.
     u32 spins = 0;
     while (__hip_atomic_load(&fuse[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < src.ntiles) {
       __builtin_amdgcn_s_sleep(8);
@@ -1758,10 +1778,10 @@ __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
         break;
       }
     }
-    __threadfence();  // acquire: the tiles' tokens and table rows
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-  ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, ~0u);
+  ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, ~0u, rt0 | 1u);
 }
 
 // rank[i] += #{ j in tile : key[j] < key[i] }, persistent over (i-tile, j-tile) pairs.
@@ -2022,12 +2042,12 @@ void launch_map_ordered(const char* text, u64 bytes, const DelimMask& dm, int em
                         hipStream_t s, u64* trace, const OrderedExtra& ex) {
   LOCUST_CHECK_ARG(ex.fuse && ex.part_off && ex.part_tiles &&
                        ex.part_tiles == div_up(bytes, (u64)kMapTileBytesMin) &&
-                       bytes < kMapLargeInput && bytes > 0,
+                       ex.part_tiles <= (u64)kFuseMaxTiles && bytes > 0,
                    "fused map + ordered: a small pass with its partition table");
   const maptile::Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   const TileSource src{ConstKeysSoA{{tokens.w[0], tokens.w[1], tokens.w[2], tokens.w[3]}},
                        ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
-  map_ordered_kernel<<<dim3(ex.part_tiles + kDictParts), dim3(kPartBlock), 0, s>>>(
+  map_ordered_kernel<<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
       text, bytes, d, emits_per_line, max_key_len, tokens, parts, cap, pm,
       const_cast<u32*>(ex.part_occ), src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   LOCUST_HIP_LAUNCH_CHECK();

@@ -16,7 +16,7 @@ WORKER = os.path.join(ROOT, "tests", "switch_worker.py")
 CASES = [
     ({"LOCUST_CHECK": "1"}, "single"),
     ({"LOCUST_COMPACT_OUT": "0"}, "single"),
-    ({"LOCUST_FUSE": "0"}, "single"),
+    ({"LOCUST_FUSE": "1"}, "single"),
     ({"LOCUST_MAP_PATH": "compat"}, "single"),
     ({"LOCUST_SORT": "radix", "LOCUST_REDUCE_PATH": "global"}, "single"),
     ({"LOCUST_SORT": "radix", "LOCUST_PSORT": "0"}, "single"),
