@@ -409,7 +409,7 @@ int run_direct(const CliArgs& a) {
   const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
   WordCountResult r;
   std::vector<double> walls;
-  LOCUST_LOG_INFO("rss before the engine: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+  LOCUST_LOG_INFO("before the engine: %s", process_rss_breakdown().c_str());
   Startup& st = g_startup;
   (void)visible_device_count();  // the HIP runtime's own start-up, timed apart
   st.init = now_ns();
@@ -417,7 +417,7 @@ int run_direct(const CliArgs& a) {
     cfg.chunk_bytes = chunk;
     GpuWordCount eng(cfg, size, size);
     st.engine = st.read = now_ns();  // the file is read by the job, piece by piece
-    LOCUST_LOG_INFO("rss with the streaming engine: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+    LOCUST_LOG_INFO("with the streaming engine: %s", process_rss_breakdown().c_str());
     for (int i = 0; i < a.warmup + a.iters; ++i) {
       auto src = open_file_source(a.file);
       r = eng.run_source(*src);
@@ -447,10 +447,10 @@ int run_direct(const CliArgs& a) {
     r.num_lines = in.num_lines;
   }
   st.jobs = now_ns();
-  LOCUST_LOG_INFO("rss after the job: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+  LOCUST_LOG_INFO("after the job: %s", process_rss_breakdown().c_str());
   std::printf("Length: %i\n", (int)r.num_lines);
   print_gpu_result(a, r, walls);
-  LOCUST_LOG_INFO("rss after the output: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+  LOCUST_LOG_INFO("after the output: %s", process_rss_breakdown().c_str());
   return 0;
 }
 
@@ -539,7 +539,7 @@ int run(const CliArgs& a) {
     std::vector<DistResult> ranks;
     DistResult dr = file_ranks ? run_single_process_file(dc, a.file, a.comm, &ranks)
                                : run_single_process_multi_gpu(dc, text.input, a.comm, &ranks);
-    LOCUST_LOG_INFO("rss after the job: %llu kB (peak %llu kB)", rss_kb(), peak_rss_kb());
+    LOCUST_LOG_INFO("after the job: %s", process_rss_breakdown().c_str());
     if (file_ranks && !cpu) std::printf("Length: %i\n", (int)dr.result.num_lines);
     std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));

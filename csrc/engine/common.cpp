@@ -1,6 +1,8 @@
 // Shared host-side pieces: logging, errors, env config, tokenizer oracle, result checks.
 #include <algorithm>
 #include <chrono>
+#include <malloc.h>
+
 #include <cstdio>
 #include <cstdarg>
 #include <cstring>
@@ -77,6 +79,31 @@ u64 process_rss_kb(bool peak) {
     if (std::sscanf(line, key, &kb) == 1) break;
   std::fclose(f);
   return kb;
+}
+
+std::string process_rss_breakdown() {
+  std::FILE* f = std::fopen("/proc/self/status", "r");
+  if (!f) return "rss unknown";
+  char line[256];
+  unsigned long long rss = 0, hwm = 0, anon = 0, file = 0, shmem = 0, v = 0;
+  while (std::fgets(line, sizeof(line), f)) {
+    if (std::sscanf(line, "VmRSS: %llu kB", &v) == 1) rss = v;
+    if (std::sscanf(line, "VmHWM: %llu kB", &v) == 1) hwm = v;
+    if (std::sscanf(line, "RssAnon: %llu kB", &v) == 1) anon = v;
+    if (std::sscanf(line, "RssFile: %llu kB", &v) == 1) file = v;
+    if (std::sscanf(line, "RssShmem: %llu kB", &v) == 1) shmem = v;
+  }
+  std::fclose(f);
+  // the heap's share of anon: bytes in use (arena + mmap'ed chunks) and the arenas' size
+  const struct mallinfo2 mi = mallinfo2();
+  char buf[256];
+  std::snprintf(buf, sizeof(buf),
+                "rss %llu kB (anon %llu, file %llu, shmem %llu; peak %llu; malloc in use %llu kB, "
+                "arenas %llu kB, mmap'ed %llu kB)",
+                rss, anon, file, shmem, hwm,
+                (unsigned long long)((mi.uordblks + mi.hblkhd) >> 10),
+                (unsigned long long)(mi.arena >> 10), (unsigned long long)(mi.hblkhd >> 10));
+  return buf;
 }
 
 void apply_env_overrides(JobConfig& cfg) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -143,6 +144,17 @@ size_t dev_block_cached(size_t* bytes) {
   std::lock_guard<std::mutex> lk(c.mu);
   if (bytes) *bytes = c.held;
   return c.free.size();
+}
+
+void* pinned_alloc(size_t bytes, unsigned flags, const char* what) {
+  static std::atomic<unsigned long long> total{0};
+  void* p = nullptr;
+  LOCUST_HIP_CHECK(hipHostMalloc(&p, bytes, flags));
+  const unsigned long long t = total.fetch_add(bytes) + bytes;
+  if (bytes >= (1u << 20))
+    LOCUST_LOG_DEBUG("pinned %.1f MiB: %s (allocated so far %.1f MiB)", bytes / 1048576.0, what,
+                     t / 1048576.0);
+  return p;
 }
 
 }  // namespace locust

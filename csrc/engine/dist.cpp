@@ -588,6 +588,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
       r.num_unique = me == 0 ? r.entries.size() : R[me].n_out;
       const u64 t3 = now_ns();
       res.map_ms = (t1 - t0) * 1e-6;
+      LOCUST_LOG_DEBUG("map done: %s", process_rss_breakdown().c_str());
       res.shuffle_ms = (t2 - t1) * 1e-6;  // the whole device exchange
       res.reduce_ms = (t3 - t2) * 1e-6;
       res.total_ms = (t3 - t0) * 1e-6;
@@ -690,6 +691,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
     r.num_unique = r.entries.size();
     const u64 t3 = now_ns();
     res.map_ms = (t1 - t0) * 1e-6;
+    LOCUST_LOG_DEBUG("map done: %s", process_rss_breakdown().c_str());
     res.shuffle_ms = (t2 - t1) * 1e-6;
     res.reduce_ms = (t3 - t2) * 1e-6;
     res.gather_ms = 0;
@@ -806,6 +808,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   r.num_unique = me == 0 && cfg.gather ? r.entries.size() : uniq;
   const u64 t4 = now_ns();
   res.map_ms = (t1 - t0) * 1e-6;
+  LOCUST_LOG_DEBUG("map done: %s", process_rss_breakdown().c_str());
   res.shuffle_ms = (t2 - t1) * 1e-6;
   res.reduce_ms = (t3 - t2) * 1e-6;
   res.gather_ms = (t4 - t3) * 1e-6;

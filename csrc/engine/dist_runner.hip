@@ -178,18 +178,19 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
         std::unique_ptr<ShardEngine> eng =
             gpu ? make_gpu_shard_engine(job, std::max<u64>(in.bytes, 1), std::max<u64>(in.lines, 1))
                 : make_cpu_shard_engine(job);
-        LOCUST_LOG_DEBUG("rank %d: engine built, process rss %llu kB", r,
-                         (unsigned long long)process_rss_kb());
+        LOCUST_LOG_DEBUG("rank %d: engine built, process %s", r, process_rss_breakdown().c_str());
+        if (schedule.size() == 1) eng->out_regions = 1;  // one job: one output region
         std::unique_ptr<TextSource> keep;
         const TextInput shard = in.load(*eng, &keep);
+        LOCUST_LOG_DEBUG("rank %d: shard ready (%s), process %s", r,
+                         shard.source ? "streamed" : "in memory", process_rss_breakdown().c_str());
         // the same engines and communicators across jobs, like a long-lived rank
         for (size_t j = 0; j < schedule.size(); ++j) {
           LOCUST_CHECK_ARG(!shard.source || schedule.size() == 1,
                            "a streamed file shard is read once: one job per run");
           DistResult d = run_distributed(schedule[j], *comm, *eng, shard);
-          LOCUST_LOG_DEBUG("rank %d: job %zu done, process rss %llu kB (peak %llu kB)", r, j,
-                           (unsigned long long)process_rss_kb(),
-                           (unsigned long long)process_rss_kb(true));
+          LOCUST_LOG_DEBUG("rank %d: job %zu done, process %s", r, j,
+                           process_rss_breakdown().c_str());
           d.input_bytes = shard.bytes;
           d.input_streamed = shard.source != nullptr;
           d.peer_p2p = gpu ? peers_of(job.device) : -1;

@@ -407,8 +407,8 @@ void DevicePipeline::grow_host_keys(u64 n) {
   if (n <= h_keys_cap) return;
   if (h_keys) LOCUST_HIP_CHECK(hipHostFree(h_keys));
   h_keys_cap = std::max<u64>(n, 1);
-  LOCUST_HIP_CHECK(hipHostMalloc(&h_keys, h_keys_cap * kKeyWords * sizeof(u64),
-                                 hipHostMallocDefault));
+  h_keys = static_cast<u64*>(pinned_alloc(h_keys_cap * kKeyWords * sizeof(u64), hipHostMallocDefault,
+                                          "key staging"));
 }
 
 void DevicePipeline::wait_done(u32 seq, bool bounded_sync) {
@@ -1054,6 +1054,17 @@ void DevicePipeline::print_ord_trace() {
   if (last_p >= 0)
     std::fprintf(stderr, "ord span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
                  (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 32 + 6]);
+  {  // self-clean handshake: each workgroup's release + done count (25), the last one's
+     // re-zeroing done (24; stale values from earlier jobs are older than this job's exits)
+    u64 done_max = 0, clean = 0;
+    for (int p = 0; p < kDictParts; ++p) {
+      done_max = std::max(done_max, t[p * 32 + 25]);
+      clean = std::max(clean, t[p * 32 + 24]);
+    }
+    if (last_p >= 0 && done_max >= last_out)
+      std::fprintf(stderr, "ord tail: last exit -> last done count %.2f us, -> self-clean done %.2f us\n",
+                   (done_max - last_out) * 0.01, clean >= last_out ? (clean - last_out) * 0.01 : -1.0);
+  }
   if (ntile) {
     u64 wait_end = 0;
     for (int p = 0; p < kDictParts; ++p)
@@ -1466,7 +1477,7 @@ void DevicePipeline::ensure_stream_buffers(bool staging, u64 nchunks) {
   }
   if (staging && !h_stage[0])
     for (int b = 0; b < 2; ++b)
-      LOCUST_HIP_CHECK(hipHostMalloc(&h_stage[b], cap_bytes + 64, hipHostMallocDefault));
+      h_stage[b] = static_cast<char*>(pinned_alloc(cap_bytes + 64, hipHostMallocDefault, "chunk staging"));
   if (nchunks > h_chunk_cap) {
     if (h_chunk_ctr) LOCUST_HIP_CHECK(hipHostFree(h_chunk_ctr));
     h_chunk_cap = std::max<u64>(nchunks, 64);
@@ -1477,7 +1488,7 @@ void DevicePipeline::ensure_stream_buffers(bool staging, u64 nchunks) {
 
 char* DevicePipeline::ensure_h_text() {
   if (h_text) return h_text;
-  LOCUST_HIP_CHECK(hipHostMalloc(&h_text, cap_bytes + 64, hipHostMallocDefault));
+  h_text = static_cast<char*>(pinned_alloc(cap_bytes + 64, hipHostMallocDefault, "input text buffer"));
   if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_h_text), h_text, 0) != hipSuccess) {
     (void)hipGetLastError();
     d_h_text = nullptr;  // not device-visible: always DMA
@@ -1530,7 +1541,7 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
   if (ring_piece != piece) {
     for (int i = 0; i < kRingPieces; ++i) {
       if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
-      LOCUST_HIP_CHECK(hipHostMalloc(&h_ring[i], piece + 64, hipHostMallocDefault));
+      h_ring[i] = static_cast<char*>(pinned_alloc(piece + 64, hipHostMallocDefault, "read ring piece"));
       if (!ev_ring[i]) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
     }
     ring_piece = piece;

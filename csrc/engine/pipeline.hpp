@@ -295,8 +295,9 @@ struct DevicePipeline {
     // fine-grained: the kernels write it straight over PCIe (coarse-grained buffers
     // measured no faster, profiles/r1_s3/out_coherence_ab.txt)
     explicit HostOut(u64 n) : cap(std::max<u64>(n, 1)) {
-      LOCUST_HIP_CHECK(hipHostMalloc(&h, cap * sizeof(OutRecord) + kDictParts * sizeof(u64),
-                                     hipHostMallocMapped | hipHostMallocCoherent));
+      h = static_cast<OutRecord*>(pinned_alloc(cap * sizeof(OutRecord) + kDictParts * sizeof(u64),
+                                               hipHostMallocMapped | hipHostMallocCoherent,
+                                               "mapped result buffer"));
       LOCUST_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
       ctab_h = reinterpret_cast<u64*>(h + cap);
       ctab_d = reinterpret_cast<u64*>(d + cap);

@@ -1267,9 +1267,9 @@ class GpuShardEngine final : public ShardEngine {
       std::memset(p, 0, bytes);  // first touch: every page on its slice's node
       LOCUST_HIP_CHECK(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
     } else {
-      LOCUST_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b->p), bytes,
-                                     hipHostMallocPortable | hipHostMallocMapped |
-                                         hipHostMallocCoherent));
+      b->p = static_cast<char*>(pinned_alloc(
+          bytes, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent,
+          "shared output (ranks in one process)"));
       std::memset(b->p, 0, kShmHeaderBytes);  // the stamps
     }
     reg[name] = b;
@@ -1306,8 +1306,8 @@ class GpuShardEngine final : public ShardEngine {
   std::shared_ptr<OutSegment> out_;
   std::vector<std::shared_ptr<RegionLease>> leases_;  // root: one per region
   u64 out_group_ = 0, out_seq_ = 0, job_region_ = 0;
-  // Room for `records` per region and at least `regions` regions (0: as now, 2 for a new
-  // output); returns whether a new generation was mapped.  Every rank calls it with the
+  // Room for `records` per region and at least `regions` regions (0: as now, out_regions
+  // for a new output); returns whether a new generation was mapped.  Every rank calls it with the
   // same arguments at the same point of the job sequence.
   bool ensure_out(u64 records, u32 regions) {
     LOCUST_CHECK_ARG(exch_group != 0, "device exchange: the communicator has no group id");
@@ -1317,7 +1317,7 @@ class GpuShardEngine final : public ShardEngine {
       out_group_ = exch_group;
       out_seq_ = 0;
     }
-    const u32 K = std::max<u32>(regions, out_ ? out_->regions : 2u);
+    const u32 K = std::max<u32>(regions, out_ ? out_->regions : std::max<u32>(out_regions, 1u));
     if (out_ && records <= out_->region_records && K <= out_->regions) return false;
     u64 R = std::max<u64>(records, 4096);
     if (out_ && records > out_->region_records)

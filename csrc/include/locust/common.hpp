@@ -64,5 +64,7 @@ bool fault_injected(int rank, const char* stage);
 u64 now_ns();
 // Resident host memory of this process, kB: VmRSS (peak = false) or VmHWM (peak = true).
 u64 process_rss_kb(bool peak = false);
+// "rss N kB (anon A, file F, shmem S; peak P)" from /proc/self/status (debug logs)
+std::string process_rss_breakdown();
 
 }  // namespace locust

@@ -26,4 +26,9 @@ void dev_block_trim();
 // Cached blocks / bytes (tests, logs).
 size_t dev_block_cached(size_t* bytes = nullptr);
 
+// Pinned host memory (hipHostMalloc with `flags`) for `what`, logged at LOCUST_LOG=debug
+// when >= 1 MiB with the process's running total of pinned allocations: where a
+// multi-rank run's host memory goes.  Throws locust::Error on failure.
+void* pinned_alloc(size_t bytes, unsigned flags, const char* what);
+
 }  // namespace locust

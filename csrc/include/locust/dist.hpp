@@ -253,6 +253,10 @@ class ShardEngine {
   // Records a slot can hold on this rank (the all-gather uses the minimum over ranks).
   virtual u64 slot_capacity() const { return 0; }
   u32 slot_records = 0;  // agreed slot size for the next job (0: kSlotRecordsMin)
+  // Regions of a new shared host output (the device exchange): 2 lets jobs whose results
+  // stay alive in turn write without growing it; a one-job run (the CLI on a file) sets 1.
+  // Every rank of a group must set the same value.
+  u32 out_regions = 2;
 
   // ---- shuffle strategy on the device (locust/exch.hpp) ----
   // Every rank's key range ends in ONE shared host output (locust/shm.hpp), written by

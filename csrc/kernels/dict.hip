@@ -1670,6 +1670,7 @@ __device__ __forceinline__ void ordered_partition(
       else
         __threadfence();
       s_count = atomicAdd(ex.done_counter, 1u) == (u32)kDictParts - 1 ? 1u : 0u;
+      if (trace) trace[(u64)v * 32 + 25] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (s_count) {
@@ -1696,6 +1697,8 @@ __device__ __forceinline__ void ordered_partition(
           }
         }
       }
+      __syncthreads();
+      if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 24] = __builtin_amdgcn_s_memrealtime();
       if (ex.host_done && threadIdx.x == 0) {  // every workgroup's writes are out
         __threadfence_system();
         __hip_atomic_store(ex.host_done, ex.host_done_value, __ATOMIC_RELEASE,
@@ -1747,7 +1750,7 @@ __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
     __syncthreads();  // every thread has read the ticket before the next claim
     if (t >= src.ntiles) break;
     const u64 rt1 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
-    maptile::map_tile<1, kPartBlock>(lds, t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
+    maptile::map_tile<1, kPartBlock, true>(lds, t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
                                      nullptr, const_cast<u32*>(src.part_off), pm, nullptr,
                                      part_occ);
     __syncthreads();  // the tile's LDS is free; every wave's stores are issued
@@ -1760,9 +1763,10 @@ __global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
   }
   if (threadIdx.x == 0) {
     if (mapped) {
-      // the agent-scope release writes this XCD's L2 back: the tiles' tokens and table rows
-      // become visible to the other XCDs before they are counted
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // the tiles' tokens and table rows went out as agent-scope stores (through the L2):
+      // once they are complete (the workgroup-scope release waits for every store of this
+      // workgroup -- the barrier above ordered the other waves' before it) the tiles count
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       atomicAdd(&fuse[1], mapped);
       if (trace && first < kDictParts) trace[(u64)first * 32 + 22] = __builtin_amdgcn_s_memrealtime();
     }
