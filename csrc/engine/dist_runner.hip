@@ -311,10 +311,10 @@ DistResult run_single_process_file(const DistConfig& cfg_in, const std::string& 
   // sized by their own bytes (chunk_bytes = 0 keeps them one pass)
   cfg.job.chunk_bytes = any_stream ? chunk : 0;
   // every streaming rank keeps a pinned read ring of 4 pieces: 16 MiB pieces for one rank,
-  // 16 / P MiB (>= 4) for P ranks of this process -- they share the host's memory
+  // 16 / P MiB (>= 2) for P ranks of this process -- they share the host's memory
   // bandwidth anyway, and 8 rings of 64 MiB were a fifth of the process's RSS
   if (!cfg.job.ring_piece_bytes && P > 1)
-    cfg.job.ring_piece_bytes = std::max<u64>(4ull << 20, (16ull << 20) / (u64)P);
+    cfg.job.ring_piece_bytes = std::max<u64>(2ull << 20, (16ull << 20) / (u64)P);
   return run_ranks({cfg}, inputs, comm, per_rank)[0];
 }
 

@@ -38,6 +38,9 @@ class GpuShardEngine final : public ShardEngine {
   bool device_buffers() const override { return true; }
   void* stream() override { return mp_->stream; }
   bool run_whole(const TextInput& shard, WordCountResult* r) override {
+    // a shard read from a source (a file range larger than one pass) streams through
+    // map_local's chunked path; the single-engine run() takes text in memory only
+    if (shard.source) return false;
     *r = mp_->run(shard);
     mp_->sync_clean = false;  // the shard entry points reset the scratch themselves
     return true;

@@ -67,9 +67,9 @@ def _cpu_want(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus,chunk_mb", [(2, 64), (4, 64), (2, 0), (3, 0)])
+@pytest.mark.parametrize("gpus,chunk_mb", [(1, 64), (2, 64), (4, 64), (2, 0), (3, 0)])
 def test_gpu_ranks_file_shards(tmp_path, cli, gpus, chunk_mb):
-    """A 320 MB generated file at --gpus 2/4 (loopback ranks on the test box's GPU): with
+    """A 320 MB generated file at --gpus 1/2/4 (loopback ranks on the test box's GPU): with
     --chunk-mb 64 every rank streams its 80-160 MB range through its pinned ring; without,
     every range fits one pass and is read straight into the rank's pinned buffer.  Output
     identical to the CPU engine; --json reports each rank's bytes."""

@@ -2,6 +2,10 @@
 // its engine allocates anything).  Build: hipcc --offload-arch=gfx950 -O2 tools/rss_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <atomic>
+#include <vector>
+#include <cstdlib>
+#include <thread>
 #include <cstring>
 
 // "RssAnon/RssFile/RssShmem" of /proc/self/status, kB.
@@ -79,5 +83,71 @@ int main() {
   big_mappings("copy");
   hipStream_t s2[4];
   for (int k = 0; k < 4; ++k) STEP("another stream", hipStreamCreateWithFlags(&s2[k], hipStreamNonBlocking));
+  // streams beyond the hardware queues: what their first kernel, first H2D copy and
+  // first D2H copy cost (a multi-rank run's engines each bring 2-3 streams)
+  hipStream_t s3[12];
+  for (int k = 0; k < 12; ++k) {
+    STEP("stream", hipStreamCreateWithFlags(&s3[k], hipStreamNonBlocking));
+    touch<<<1, 64, 0, s3[k]>>>(d);
+    STEP("  its first kernel", hipStreamSynchronize(s3[k]));
+    STEP("  its first H2D 4 MiB", hipMemcpyAsync(d, h, 4ull << 20, hipMemcpyHostToDevice, s3[k]));
+    STEP("  sync", hipStreamSynchronize(s3[k]));
+    STEP("  its first D2H 4 MiB", hipMemcpyAsync(h, d, 4ull << 20, hipMemcpyDeviceToHost, s3[k]));
+    STEP("  sync", hipStreamSynchronize(s3[k]));
+  }
+  // large device arenas (a 256 MiB-chunk engine reserves ~34 GB), device-to-device
+  // copies, memsets, events and a registered host range
+  void* big[3] = {};
+  for (int k = 0; k < 3; ++k) STEP("hipMalloc 32 GiB", hipMalloc(&big[k], 32ull << 30));
+  STEP("D2D 64 MiB", hipMemcpyAsync(big[0], big[1], 64ull << 20, hipMemcpyDeviceToDevice, s));
+  STEP("  sync", hipStreamSynchronize(s));
+  STEP("memset 64 MiB", hipMemsetAsync(big[2], 0, 64ull << 20, s));
+  STEP("  sync", hipStreamSynchronize(s));
+  hipEvent_t evs[64];
+  for (int k = 0; k < 64; ++k) (void)hipEventCreateWithFlags(&evs[k], hipEventDisableTiming);
+  STEP("64 events", hipSuccess);
+  void* reg = std::malloc(64ull << 20);
+  std::memset(reg, 1, 64ull << 20);
+  STEP("malloc+touch 64 MiB", hipSuccess);
+  STEP("hipHostRegister it", hipHostRegister(reg, 64ull << 20, hipHostRegisterMapped));
+  for (int k = 0; k < 3; ++k) STEP("hipFree 32 GiB", hipFree(big[k]));
+  // a thread of its own (the multi-rank CLI's ranks are threads)
+  for (int t = 0; t < 4; ++t) {
+    std::thread th([&] {
+      (void)hipSetDevice(0);
+      hipStream_t ts;
+      STEP("thread: stream", hipStreamCreateWithFlags(&ts, hipStreamNonBlocking));
+      touch<<<1, 64, 0, ts>>>(d);
+      STEP("thread:  first kernel", hipStreamSynchronize(ts));
+      STEP("thread:  first H2D 4 MiB", hipMemcpyAsync(d, h, 4ull << 20, hipMemcpyHostToDevice, ts));
+      STEP("thread:  sync", hipStreamSynchronize(ts));
+    });
+    th.join();
+  }
+  // eight threads copying at the same time, each on a stream of its own (the multi-rank
+  // CLI's ranks stream their shards concurrently)
+  {
+    std::vector<std::thread> ths;
+    std::atomic<int> ready{0};
+    void* dd = nullptr;
+    (void)hipMalloc(&dd, 8ull * (64ull << 20));
+    for (int t = 0; t < 8; ++t)
+      ths.emplace_back([&, t] {
+        (void)hipSetDevice(0);
+        hipStream_t ts;
+        (void)hipStreamCreateWithFlags(&ts, hipStreamNonBlocking);
+        void* hh = nullptr;
+        (void)hipHostMalloc(&hh, 64ull << 20, hipHostMallocDefault);
+        ready.fetch_add(1);
+        while (ready.load() < 8) {
+        }
+        for (int k = 0; k < 16; ++k)
+          (void)hipMemcpyAsync(static_cast<char*>(dd) + (size_t)t * (64ull << 20), hh, 64ull << 20,
+                               hipMemcpyHostToDevice, ts);
+        (void)hipStreamSynchronize(ts);
+      });
+    for (auto& th : ths) th.join();
+    STEP("8 threads x concurrent H2D", hipSuccess);
+  }
   return 0;
 }
