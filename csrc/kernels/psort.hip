@@ -64,6 +64,13 @@ __device__ __forceinline__ void reduce_tail(u32 p, u32 U, u64 pfx, MapCounters* 
     MapCounters c = *ctr;
     *ra.ctr_out = c;
   }
+  // the host first (records, counters out), then the device scratch re-zeroing, which the
+  // next job's kernels behind this one on the stream see complete (as dict.hip)
+  if (ra.host_done && threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(ra.host_done, ra.host_done_value, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __syncthreads();
   if (!(flags & kCtrSortOverflow)) {
     for (u32 i = threadIdx.x; i < ra.map_words; i += kPsBlock) ra.map_lb.status[i] = 0;
@@ -79,11 +86,6 @@ __device__ __forceinline__ void reduce_tail(u32 p, u32 U, u64 pfx, MapCounters* 
       *ra.map_lb.tile_counter = 0;
       *ra.done_counter = 0;
     }
-  }
-  if (ra.host_done && threadIdx.x == 0) {
-    __threadfence_system();
-    __hip_atomic_store(ra.host_done, ra.host_done_value, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
