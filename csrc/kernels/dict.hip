@@ -449,9 +449,7 @@ __global__ __launch_bounds__(kPartBlock) void dict_part_build_kernel(
 constexpr u64 kOrdM = (1ull << 20) - 1;        // look-back value: [m:20][ovf:9][tokens:33]
 constexpr u32 kSplitMinTokens = 128;           // planned workgroups: tokens per extra sibling
 constexpr u32 kPlanRows = 16;                  // table rows the plan estimates tokens from
-constexpr u32 kRankChunk = 8;                  // candidates per rank work item
 constexpr u32 kSmallRank = 256;                // partitions up to here: all-pairs ranks
-__device__ __forceinline__ u32 div_up_u32(u32 a, u32 b) { return (a + b - 1) / b; }
 constexpr int kOrdOvfShift = 20;
 constexpr int kOrdTokShift = 29;
 
@@ -989,7 +987,6 @@ __device__ __forceinline__ void ordered_partition(
   __shared__ u64 s_prefix;
   __shared__ u32 s_cm, s_cfull;  // compaction: distinct keys, overflow flag
   __shared__ u64 s_ctok;         // compaction: tokens
-  __shared__ u64 s_wlo, s_whi;   // large partitions: first-word range of the keys present
   __shared__ u64 s_wand[kKeyWords], s_wor[kKeyWords];  // large partitions: AND / OR per key
                                                         // word (its varying bytes)
   __shared__ u32 s_rstart[256], s_rwsum[4];  // large partitions: LdsRadix digit starts
@@ -1103,18 +1100,6 @@ __device__ __forceinline__ void ordered_partition(
   const typename Src::Pre first =
       vplan ? (vk ? src.prefetch(p) : typename Src::Pre{})
             : guessing && p == guess_p ? guess : src.prefetch(p);
-  // The in-partition counting sort of a large partition buckets keys by the 8 bits of
-  // (w0 - wlo) just below the width of [wlo, whi], the first words actually present: 256
-  // order-preserving buckets -- the second byte for keys sharing a first byte, finer bytes
-  // for a narrow range ('th').  (The partition map's own bounds are no substitute: the
-  // first partition starts at 0, so its keys -- all 'A...', say -- fell into 2 buckets
-  // and their all-pairs ranking ran 7x longer than any other partition's.)
-  u64 wlo = 0;
-  u32 bshift = 0;
-  auto bucket_of = [&](u64 w0) -> u32 {
-    const u64 b = (w0 - wlo) >> bshift;
-    return b < 255u ? (u32)b : 255u;
-  };
   for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
 #pragma unroll
     for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
@@ -1125,8 +1110,6 @@ __device__ __forceinline__ void ordered_partition(
     s_cm = 0;
     s_ctok = 0;
     s_cfull = 0;
-    s_wlo = ~0ull;
-    s_whi = 0;
   }
   __syncthreads();
   ORD_STAMP(14);  // table cleared
@@ -1369,25 +1352,63 @@ __device__ __forceinline__ void ordered_partition(
       }
     }
   } else {
-  // ---- sort the partition's keys: counting sort on the SECOND key byte (all keys here
-  // share the first), then rank inside each second-byte bucket by all-pairs compares --
-  // buckets are small, there are few barriers, and no bitonic network over m keys ----
-  u64* s_w0b = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);  // [kPartSlots]
-  u32* s_slotb = s_list + 5 * kPartSlots;                        // [kPartSlots]
-  u32* s_hist = s_list + 6 * kPartSlots;                         // [256]
-  u32* s_off = s_hist + 256;                                     // [256]
-  u32* s_cur = s_off + 256;                                      // [256]
-  u32* s_ioff = s_cur + 256;                                     // [257] rank work items
-  u32* s_rank = s_ioff + 260;                                    // [kPartSlots]
-  if (threadIdx.x < 256) {
-    s_hist[threadIdx.x] = 0;
-    s_cur[threadIdx.x] = 0;
-  }
-  __syncthreads();
-  if (!any_full && m > 1) {
+  // ---- sort the partition's distinct keys ----
+  __syncthreads();  // the build's table, (w0, slot) lists and token window are complete
+  if (!any_full && m > 1 && m <= (u32)kPartBlock) {
+    // Bitonic network over the next power of two N >= m, one key per thread, (w0, slot) in
+    // registers; padding sorts last (w0 = ~0: no key is all 0xFF bytes).  Strides below
+    // 64 exchange through cross-lane shuffles, the 10 longer ones (N = 1024) through
+    // double-buffered LDS with one barrier each.  Keys tied on their first word compare
+    // their other words in the table (ord_greater).  The LSD radix below took ~61K cycles
+    // for a 1,022-key partition of synth1m (10-14 byte passes, 3-4 barriers each): the
+    // ordered kernel's records could not start their PCIe drain before that.
+    const u32 N = m <= 64u ? 64u : 1u << (32 - __clz((int)(m - 1)));
+    u64* s_bw = reinterpret_cast<u64*>(s_list + 3 * kPartSlots);  // [2][kPartBlock]
+    u32* s_bs = s_list + 7 * kPartSlots;                           // [2][kPartBlock]
+    const u32 t = threadIdx.x;
+    u64 w = ~0ull;
+    u32 sl = 0xFFFFFFFFu;
+    if (t < m) {
+      w = s_w0[t];
+      sl = s_slot[t];
+    }
+    int buf = 0;
+    for (u32 k = 2; k <= N; k <<= 1) {
+      for (u32 jj = k >> 1; jj > 0; jj >>= 1) {
+        u64 pw;
+        u32 ps;
+        if (jj >= 64u) {  // partner in another wave (uniform branch)
+          if (t < N) {
+            s_bw[buf * kPartBlock + t] = w;
+            s_bs[buf * kPartBlock + t] = sl;
+          }
+          __syncthreads();
+          pw = t < N ? s_bw[buf * kPartBlock + (t ^ jj)] : ~0ull;
+          ps = t < N ? s_bs[buf * kPartBlock + (t ^ jj)] : 0xFFFFFFFFu;
+          buf ^= 1;
+        } else {
+          pw = (u64)__shfl_xor((long long)w, (int)jj, 64);
+          ps = (u32)__shfl_xor((int)sl, (int)jj, 64);
+        }
+        if (t < N) {
+          const bool up = (t & k) == 0, lower = (t & jj) == 0;
+          const bool less = ord_greater(pw, ps, w, sl, s_tab);  // mine < partner
+          if ((lower == up) ? !less : less) {
+            w = pw;
+            sl = ps;
+          }
+        }
+      }
+    }
+    __syncthreads();  // every thread has its first (w0, slot) loaded
+    if (t < m) {
+      s_w0[t] = w;
+      s_slot[t] = sl;
+    }
+  } else if (!any_full && m > 1) {
     // LSD radix sort of the partition's distinct keys in LDS over the bytes that vary
     // (dev::LdsRadix, as the partitioned token sort): word 3 down to word 0, low byte to
-    // high, stable.  The bucket + all-pairs ranking below degenerated on skewed key sets
+    // high, stable.  A bucket + all-pairs ranking degenerated on skewed key sets
     // -- most keys in one bucket, long keys tied on their first word: up to 295K cycles
     // for one 1,003-key partition of the synthetic text (git history keeps that path).
     using Radix = dev::LdsRadix<kPartBlock, kPartSlots, u16>;
@@ -1449,109 +1470,6 @@ __device__ __forceinline__ void ordered_partition(
       if (d < m) {
         s_w0[d] = pw[r];
         s_slot[d] = ps[r];
-      }
-    }
-  } else if (!any_full && m > 1) {
-    {
-      u64 lo = ~0ull, hi = 0;
-      for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
-        const u64 w = s_w0[a];
-        lo = w < lo ? w : lo;
-        hi = w > hi ? w : hi;
-      }
-      lo = ~dev::wave_reduce_max(~lo);
-      hi = dev::wave_reduce_max(hi);
-      if (dev::lane_id() == 0) {
-        atomicMin(reinterpret_cast<unsigned long long*>(&s_wlo), (unsigned long long)lo);
-        atomicMax(reinterpret_cast<unsigned long long*>(&s_whi), (unsigned long long)hi);
-      }
-      __syncthreads();
-      wlo = s_wlo;
-      const u64 span = s_whi - wlo + 1;  // > 0: w0 = ~0 is no key
-      const u32 span_bits = 64u - (u32)__clzll((long long)(span - 1 | 1));
-      bshift = span_bits > 8u ? span_bits - 8u : 0u;
-    }
-    for (u32 a = threadIdx.x; a < m; a += kPartBlock) atomicAdd(&s_hist[bucket_of(s_w0[a])], 1u);
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of 256 bucket sizes by one wave
-      const u32 l = threadIdx.x;
-      const u32 h0 = s_hist[4 * l], h1 = s_hist[4 * l + 1], h2 = s_hist[4 * l + 2],
-                h3 = s_hist[4 * l + 3];
-      const u32 sum4 = h0 + h1 + h2 + h3;
-      const u32 ex = dev::wave_inclusive_scan(sum4) - sum4;
-      s_off[4 * l] = ex;
-      s_off[4 * l + 1] = ex + h0;
-      s_off[4 * l + 2] = ex + h0 + h1;
-      s_off[4 * l + 3] = ex + h0 + h1 + h2;
-      // rank work items of a bucket of B keys: B keys x ceil(B / kRankChunk) chunks
-      const u32 i0 = h0 * div_up_u32(h0, kRankChunk), i1 = h1 * div_up_u32(h1, kRankChunk),
-                i2 = h2 * div_up_u32(h2, kRankChunk), i3 = h3 * div_up_u32(h3, kRankChunk);
-      const u32 isum = i0 + i1 + i2 + i3;
-      const u32 iinc = dev::wave_inclusive_scan(isum);
-      const u32 iex = iinc - isum;
-      s_ioff[4 * l] = iex;
-      s_ioff[4 * l + 1] = iex + i0;
-      s_ioff[4 * l + 2] = iex + i0 + i1;
-      s_ioff[4 * l + 3] = iex + i0 + i1 + i2;
-      if (l == 63) s_ioff[256] = iinc;
-    }
-    for (u32 a = threadIdx.x; a < m; a += kPartBlock) s_rank[a] = 0;
-    __syncthreads();
-    ORD_STAMP(8);  // histogram + bucket scan
-    for (u32 a = threadIdx.x; a < m; a += kPartBlock) {
-      const u64 w = s_w0[a];
-      const u32 b = bucket_of(w);
-      const u32 q = s_off[b] + atomicAdd(&s_cur[b], 1u);
-      s_w0b[q] = w;
-      s_slotb[q] = s_slot[a];
-    }
-    __syncthreads();
-    ORD_STAMP(7);  // bucketed by the second byte
-    {
-      // Ranks inside each bucket, pair-parallel: work item = (key, chunk of kRankChunk
-      // candidates); consecutive lanes take consecutive keys of the same chunk, so the
-      // candidate reads are LDS broadcasts, and every lane of the workgroup is busy even
-      // when a partition has few keys and one big bucket.
-      const u32 items = s_ioff[256];
-      for (u32 e = threadIdx.x; e < items; e += kPartBlock) {
-        // bucket of the item: the last b with s_ioff[b] <= e, by an 8-step binary search
-        // every round -- walking on from the previous round's bucket crossed up to ~100
-        // small buckets per 1,024-item stride, one dependent LDS read each (the hot
-        // partitions' rank phase took 16-24 K cycles, most of it in that walk)
-        u32 b = 0;
-#pragma unroll
-        for (u32 step = 128; step; step >>= 1)
-          if (s_ioff[b + step] <= e) b += step;
-        const u32 B = s_hist[b], base = s_off[b];
-        const u32 local = e - s_ioff[b];
-        const u32 chunk = local / B, i = local - chunk * B;
-        const u32 q = base + i;
-        const u64 w = s_w0b[q];
-        const u32 j0 = base + chunk * kRankChunk, j1 = min(j0 + kRankChunk, base + B);
-        // all candidates' loads in flight at once; past the bucket end the sentinel ~0
-        // (no key is all 0xFF bytes) counts as neither smaller nor equal
-        u64 o[kRankChunk];
-#pragma unroll
-        for (u32 t = 0; t < kRankChunk; ++t) o[t] = j0 + t < j1 ? s_w0b[j0 + t] : ~0ull;
-        u32 cnt = 0;
-        bool tie = false;
-#pragma unroll
-        for (u32 t = 0; t < kRankChunk; ++t) {
-          cnt += o[t] < w ? 1u : 0u;
-          tie |= o[t] == w && j0 + t != q;
-        }
-        if (tie)  // keys sharing their first 8 bytes: order by the remaining words
-          for (u32 j = j0; j < j1; ++j)
-            if (j != q && s_w0b[j] == w) cnt += ord_greater(w, s_slotb[q], w, s_slotb[j], s_tab);
-        if (cnt) atomicAdd(&s_rank[q], cnt);
-      }
-      __syncthreads();
-      ORD_STAMP(9);  // ranks
-      for (u32 q = threadIdx.x; q < m; q += kPartBlock) {
-        const u64 w = s_w0b[q];
-        const u32 d = s_off[bucket_of(w)] + s_rank[q];
-        s_w0[d] = w;
-        s_slot[d] = s_slotb[q];
       }
     }
   }
