@@ -390,16 +390,6 @@ unsigned long long peak_rss_kb() {
   return kb;
 }
 
-// Resident host memory now (kB, /proc/self/statm), for LOCUST_LOG=info.
-unsigned long long rss_kb() {
-  std::FILE* f = std::fopen("/proc/self/statm", "r");
-  if (!f) return 0;
-  unsigned long long size = 0, res = 0;
-  if (std::fscanf(f, "%llu %llu", &size, &res) != 2) res = 0;
-  std::fclose(f);
-  return res * (unsigned long long)sysconf(_SC_PAGESIZE) / 1024;
-}
-
 // Stream threshold: files past one device pass (--chunk-mb, default 256 MiB) stream.
 constexpr u64 kDefaultStreamChunk = 256ull << 20;
 

@@ -141,7 +141,7 @@ class EntryList {
         ++flat_;
         return *this;
       }
-      w_ += 1 + compact_nw(w_[0]);
+      w_ += compact_record_words(w_[0]);
       if (--left_ == 0) next_segment();
       return *this;
     }

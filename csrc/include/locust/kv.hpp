@@ -86,26 +86,74 @@ LOCUST_HD inline int unpack_key(const uint64_t* w, char* out) {
 }
 
 // Compact result record (the host drain format of the ordered kernels and the shuffle's
-// shared output): 8-B words
-//   [count << kCompactCountShift | nw] [key word 0] ... [key word nw - 1]
-// where nw (1-4) counts the key's words up to its last non-zero one (the rest are NUL
-// padding).  English and synthetic keys are mostly <= 8 or <= 16 bytes: 16-24 B per entry
-// instead of 40 B across PCIe.  The 40-B KeyIntValuePair stays the kiv file format.
-constexpr int kCompactCountShift = 8;
+// shared output): a run of 8-B words.  kb = the key's bytes up to its
+// last non-zero one (1-32; the rest of the packed key is NUL padding).
+//   short (count < 2^24): word 0 = [key bytes 0-3 : 32][count : 24][0 : 1][kb : 6][0 : 1]
+//                         then ceil((kb - 4) / 8) words of key bytes 4, 5, ... (big-endian)
+//   long:                 word 0 = [count : 56][0 : 1][kb : 6][1 : 1]
+//                         then ceil(kb / 8) packed key words
+// (bit 0 first).  English and synthetic keys of 5-12 bytes take 16 B instead of 40 B, and
+// keys of up to 4 bytes one word.  The 40-B KeyIntValuePair stays the kiv file format.
+constexpr uint64_t kCompactShortMax = (1ull << 24) - 1;
 constexpr int kCompactMaxWords = 1 + kKeyWords;
 LOCUST_HD inline uint32_t key_words_used(const uint64_t* w) {
   return w[3] ? 4u : w[2] ? 3u : w[1] ? 2u : 1u;
 }
-LOCUST_HD inline uint32_t compact_nw(uint64_t header) { return (uint32_t)(header & 7u); }
-LOCUST_HD inline uint64_t compact_header(uint64_t count, uint32_t nw) {
-  return (count << kCompactCountShift) | nw;
+// Bytes of a packed key up to its last non-zero one (0 for the empty key).
+LOCUST_HD inline uint32_t key_bytes_used(const uint64_t* w) {
+  const uint32_t nw = key_words_used(w);
+  const uint64_t last = nw == 4 ? w[3] : nw == 3 ? w[2] : nw == 2 ? w[1] : w[0];
+  return last ? 8u * nw - ((uint32_t)__builtin_ctzll(last) >> 3) : 0u;
+}
+LOCUST_HD inline uint32_t compact_words_for(uint32_t kb, uint64_t count) {
+  return count <= kCompactShortMax ? 1u + (kb > 4u ? (kb + 3u) >> 3 : 0u) : 1u + ((kb + 7u) >> 3);
+}
+LOCUST_HD inline uint32_t compact_words(const uint64_t* w, uint64_t count) {
+  return compact_words_for(key_bytes_used(w), count);
+}
+// Words of the record starting with header word h.
+LOCUST_HD inline uint32_t compact_record_words(uint64_t h) {
+  const uint32_t kb = (uint32_t)(h >> 1) & 63u;
+  return (h & 1u) ? 1u + ((kb + 7u) >> 3) : 1u + (kb > 4u ? (kb + 3u) >> 3 : 0u);
+}
+// All words of a key's record into o[0..kCompactMaxWords) (static indices: callers keep o
+// in registers); returns how many of them the record uses.
+LOCUST_HD inline uint32_t compact_record(const uint64_t* w, uint64_t count, uint64_t* o) {
+  const uint32_t kb = key_bytes_used(w);
+  if (count <= kCompactShortMax) {
+    o[0] = ((w[0] >> 32) << 32) | (count << 8) | ((uint64_t)kb << 1);
+    o[1] = (w[0] << 32) | (w[1] >> 32);
+    o[2] = (w[1] << 32) | (w[2] >> 32);
+    o[3] = (w[2] << 32) | (w[3] >> 32);
+    o[4] = w[3] << 32;
+  } else {
+    o[0] = (count << 8) | ((uint64_t)kb << 1) | 1u;
+    o[1] = w[0];
+    o[2] = w[1];
+    o[3] = w[2];
+    o[4] = w[3];
+  }
+  return compact_words_for(kb, count);
 }
 // Decodes the record at p; returns its length in words.
 LOCUST_HD inline uint32_t decode_compact(const uint64_t* p, PackedKey* key, uint64_t* count) {
-  const uint32_t nw = compact_nw(p[0]);
-  *count = p[0] >> kCompactCountShift;
-  for (int j = 0; j < kKeyWords; ++j) key->w[j] = (uint32_t)j < nw ? p[1 + j] : 0ull;
-  return 1 + nw;
+  const uint64_t h = p[0];
+  const uint32_t n = compact_record_words(h);
+  if (h & 1u) {
+    *count = h >> 8;
+    for (uint32_t j = 0; j < (uint32_t)kKeyWords; ++j) key->w[j] = j + 1 < n ? p[1 + j] : 0ull;
+  } else {
+    *count = (h >> 8) & kCompactShortMax;
+    // key word j = [bytes 8j..8j+3 : the previous word's low half][bytes 8j+4.. : this
+    // extra word's high half]
+    uint64_t hi = h >> 32;
+    for (uint32_t j = 0; j < (uint32_t)kKeyWords; ++j) {
+      const uint64_t e = j + 1 < n ? p[1 + j] : 0ull;
+      key->w[j] = (hi << 32) | (e >> 32);
+      hi = e & 0xFFFFFFFFull;
+    }
+  }
+  return n;
 }
 
 LOCUST_HD inline int key_compare(const uint64_t* a, const uint64_t* b) {

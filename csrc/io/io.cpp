@@ -23,7 +23,7 @@ u64 EntryList::wire_bytes() const {
   u64 words = 0;
   for (const EntrySegment& s : segs_) {
     const u64* p = s.words;
-    for (u64 i = 0; i < s.n; ++i) p += 1 + compact_nw(p[0]);
+    for (u64 i = 0; i < s.n; ++i) p += compact_record_words(p[0]);
     words += (u64)(p - s.words);
   }
   return words * 8;

@@ -944,8 +944,8 @@ __device__ u32 write_compact_records(u64* __restrict__ dst, u32 m, Word word, u3
     nw[r] = 0;
     if (i < m) {
       const u64 kw[kKeyWords] = {word(i, 0), word(i, 1), word(i, 2), word(i, 3)};
-      nw[r] = key_words_used(kw);
-      tot += 1 + nw[r];
+      nw[r] = compact_words(kw, word(i, kKeyWords));
+      tot += nw[r];
     }
   }
   u32 total = 0;
@@ -954,16 +954,20 @@ __device__ u32 write_compact_records(u64* __restrict__ dst, u32 m, Word word, u3
   for (u32 r = 0; r < kPer; ++r) {
     const u32 i = threadIdx.x * kPer + r;
     if (i < m) {
-      s_coff[i] = at | (nw[r] << 29);  // at < 5 * kPartSlots < 2^29
-      for (u32 k = 0; k <= nw[r]; ++k) s_own[at + k] = (u16)i;
-      at += 1 + nw[r];
+      s_coff[i] = at;
+      for (u32 k = 0; k < nw[r]; ++k) s_own[at + k] = (u16)i;
+      at += nw[r];
     }
   }
   __syncthreads();
   for (u32 q = threadIdx.x; q < total; q += kPartBlock) {
-    const u32 i = s_own[q], c = s_coff[i];
-    const u32 k = q - (c & ((1u << 29) - 1u));
-    dst[q] = k == 0 ? compact_header(word(i, kKeyWords), c >> 29) : word(i, k - 1);
+    const u32 i = s_own[q];
+    const u32 k = q - s_coff[i];
+    const u64 kw[kKeyWords] = {word(i, 0), word(i, 1), word(i, 2), word(i, 3)};
+    u64 o[kCompactMaxWords];
+    (void)compact_record(kw, word(i, kKeyWords), o);
+    // selects, not an indexed register array (that would go through scratch)
+    dst[q] = k == 0 ? o[0] : k == 1 ? o[1] : k == 2 ? o[2] : k == 3 ? o[3] : o[4];
   }
   return total;
 }
@@ -1144,6 +1148,7 @@ __device__ __forceinline__ void ordered_partition(
   u32* s_rkw = s_rk + kSmallRank;  // [kSmallRank] compact word offsets (weighted ranks)
   u64* s_out = reinterpret_cast<u64*>(s_rk + 2 * kSmallRank);    // [5 x kSmallRank] records
   u64* s_k123 = s_out + 6 * kSmallRank;                          // [3 x kSmallRank] words 1-3
+  u32* s_cw = reinterpret_cast<u32*>(s_k123 + 3 * kSmallRank);   // [kSmallRank] compact words
   {
     const u64 b0 = dev::ballot(mine >= 1), b1 = dev::ballot(mine >= 2);
     const u64 wfull = dev::ballot(full);
@@ -1163,8 +1168,14 @@ __device__ __forceinline__ void ordered_partition(
         s_w0[d] = s_tab[slot].w[0];
         s_slot[d] = slot;
         if (d < kSmallRank) {
+          u64 kw[kKeyWords];
+          kw[0] = s_tab[slot].w[0];
 #pragma unroll
-          for (int j = 1; j < kKeyWords; ++j) s_k123[3 * d + j - 1] = s_tab[slot].w[j] ^ kWordMagic;
+          for (int j = 1; j < kKeyWords; ++j) {
+            kw[j] = s_tab[slot].w[j] ^ kWordMagic;
+            s_k123[3 * d + j - 1] = kw[j];
+          }
+          s_cw[d] = compact_words(kw, s_tab[slot].count);
         }
         ++d;
       }
@@ -1261,6 +1272,7 @@ __device__ __forceinline__ void ordered_partition(
         u32 wcnt = 0;  // compact words of the smaller keys: this key's compact offset
         for (u32 j = j0; j < j1; j += 4) {
           u64 c0[4], c1[4], c2[4], c3[4];
+          u32 cw[4];
 #pragma unroll
           for (u32 q = 0; q < 4; ++q) {
             const bool in = j + q < j1;
@@ -1269,6 +1281,7 @@ __device__ __forceinline__ void ordered_partition(
             c1[q] = s_k123[3 * jj];
             c2[q] = s_k123[3 * jj + 1];
             c3[q] = s_k123[3 * jj + 2];
+            cw[q] = s_cw[jj];
           }
 #pragma unroll
           for (u32 q = 0; q < 4; ++q) {
@@ -1278,7 +1291,7 @@ __device__ __forceinline__ void ordered_partition(
                             (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
                              (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
             cnt += lt ? 1u : 0u;
-            wcnt += lt ? 2u + (c1[q] != 0) + (c2[q] != 0) + (c3[q] != 0) : 0u;
+            wcnt += lt ? cw[q] : 0u;
           }
         }
         if (trace)
@@ -1308,14 +1321,14 @@ __device__ __forceinline__ void ordered_partition(
       const LdsSlot& sl = s_tab[s_slot[i]];
       const u64 w1 = sl.w[1] ^ kWordMagic, w2 = sl.w[2] ^ kWordMagic, w3 = sl.w[3] ^ kWordMagic;
       if (cstage) {
-        const u32 nw = w3 ? 4u : w2 ? 3u : w1 ? 2u : 1u;
+        const u64 kw[kKeyWords] = {sl.w[0], w1, w2, w3};
+        u64 rec[kCompactMaxWords];
+        const u32 nwd = compact_record(kw, sl.count, rec);
         u64* o = s_out + s_rkw[i];
-        o[0] = compact_header(sl.count, nw);
-        o[1] = sl.w[0];
-        if (nw > 1) o[2] = w1;
-        if (nw > 2) o[3] = w2;
-        if (nw > 3) o[4] = w3;
-        if (s_rk[i] == m - 1) s_cwords = s_rkw[i] + 1 + nw;  // the last key's end
+#pragma unroll
+        for (u32 q = 0; q < (u32)kCompactMaxWords; ++q)
+          if (q < nwd) o[q] = rec[q];
+        if (s_rk[i] == m - 1) s_cwords = s_rkw[i] + nwd;  // the last key's end
       } else {
         u64* o = s_out + kOutWords * s_rk[i];
         o[0] = sl.w[0];

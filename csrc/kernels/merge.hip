@@ -293,8 +293,8 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_compact_kernel(
       const u32 i = i0 + e;
       v[e].count = 0;
       if (i < total) v[e] = merged[i];
-      nw[e] = v[e].count ? key_words_used(v[e].w) : 0u;
-      words += v[e].count ? 1u + nw[e] : 0u;
+      nw[e] = v[e].count ? compact_words(v[e].w, v[e].count) : 0u;
+      words += nw[e];
     }
     u64 tile_words = 0;
     u64 at = dev::block_exclusive_scan<u64, kMergeBlock>(words, s_scan, &tile_words);
@@ -303,11 +303,12 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_compact_kernel(
     for (int e = 0; e < kEmitItems; ++e) {
       if (!v[e].count) continue;
       u64* o = s_out + at;
-      o[0] = compact_header(v[e].count, nw[e]);
+      u64 rec[kCompactMaxWords];
+      (void)compact_record(v[e].w, v[e].count, rec);
 #pragma unroll
-      for (u32 j = 0; j < (u32)kKeyWords; ++j)  // static indices: v stays in registers
-        if (j < nw[e]) o[1 + j] = v[e].w[j];
-      at += 1 + nw[e];
+      for (u32 j = 0; j < (u32)kCompactMaxWords; ++j)  // static indices: registers, no scratch
+        if (j < nw[e]) o[j] = rec[j];
+      at += nw[e];
     }
     __syncthreads();
     u64* out = dst + s_base + before;

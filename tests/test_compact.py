@@ -1,5 +1,5 @@
 """Compact result records: the ordered kernels drain their output to
-host memory as [count << 8 | nw][key words...] (csrc/include/locust/kv.hpp), one segment
+host memory as variable-length runs of 8-B words (csrc/include/locust/kv.hpp), one segment
 per virtual partition, and EntryList decodes them on the fly.  Here: the host decoder on
 hand-built segments against the packed-key oracle; the GPU twin (the kernels' own compact
 output byte-identical to the CPU engine, and the wire bytes it saves) is
@@ -16,14 +16,23 @@ def _pack(key: bytes):
 
 
 def _record(key: bytes, count: int):
+    """kv.hpp's compact record, written independently: short form (count < 2^24) packs key
+    bytes 0-3 into the header word, then key bytes 4.. in 8-byte words; long form keeps a
+    56-bit count and the packed key words."""
+    kb = len(key.rstrip(b"\0"))
+    if count < (1 << 24):
+        head = (int.from_bytes(key[:4].ljust(4, b"\0"), "big") << 32) | (count << 8) | (kb << 1)
+        rest = key[4:kb]
+        extra = [int.from_bytes(rest[i:i + 8].ljust(8, b"\0"), "big") for i in range(0, len(rest), 8)]
+        return [head] + extra
     w = _pack(key)
-    nw = max(j + 1 for j in range(4) if w[j]) if any(w) else 1
-    return [(count << 8) | nw] + w[:nw]
+    return [(count << 8) | (kb << 1) | 1] + w[:(kb + 7) // 8]
 
 
 def test_decode_segments_with_gaps_and_empty():
-    keys = [(b"a", 3), (b"abcdefgh", 1), (b"abcdefghi", 7), (b"b" * 17, 2), (b"z" * 31, 9),
-            (b"zz", 1)]
+    keys = [(b"a", 3), (b"abcd", 5), (b"abcde", 1 << 24), (b"abcdefgh", 1), (b"abcdefghi", 7),
+            (b"abcdefghijkl", 2), (b"abcdefghijklm", 3), (b"b" * 17, 2), (b"b" * 20, 1 << 30),
+            (b"z" * 29, 4), (b"z" * 31, 9), (b"zz", 1)]
     words, segs = [], []
     # segment 0: two records; then a gap (the kernel leaves room for 40-B records); an
     # empty segment; segment 2: the rest
@@ -59,4 +68,4 @@ def test_decode_hamlet_sized(hamlet):
             words += _record(k, c)
     r = lc._C.Result.from_compact(words, segs)
     assert r.entries() == ent
-    assert r.wire_bytes / len(ent) < 20  # English keys: ~2 words per entry
+    assert r.wire_bytes / len(ent) < 15  # English keys: one or two words per entry (14.1 B)
