@@ -1595,11 +1595,12 @@ __device__ __forceinline__ void ordered_partition(
     __syncthreads();
     if (threadIdx.x == 0) {
       // release this workgroup's counter / status writes (and, when the host is told of the
-      // end, its host-mapped records: system scope)
+      // end, its host-mapped records: system scope); release only -- the last workgroup
+      // acquires (an acq_rel fence here also invalidated this XCD's caches, every time)
       if (ex.host_done)
-        __threadfence_system();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       else
-        __threadfence();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       s_count = atomicAdd(ex.done_counter, 1u) == (u32)kDictParts - 1 ? 1u : 0u;
       if (trace) trace[(u64)v * 32 + 25] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1611,11 +1612,9 @@ __device__ __forceinline__ void ordered_partition(
       // released them before counting itself done).  The re-zeroing below touches device
       // scratch only, which the next job's kernels -- behind this one on the stream -- see
       // complete; the host's turnaround overlaps it (it took 3.8 us before the publish).
-      if (ex.host_done && threadIdx.x == 0) {
-        __threadfence_system();
+      if (ex.host_done && threadIdx.x == 0)  // a system-scope release store
         __hip_atomic_store(ex.host_done, ex.host_done_value, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-      }
       if (!(flags & kCtrDictOverflow)) {
         for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
         for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;

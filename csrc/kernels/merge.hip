@@ -314,12 +314,14 @@ __global__ __launch_bounds__(kMergeBlock) void merge_emit_compact_kernel(
     u64* out = dst + s_base + before;
     for (u32 q = threadIdx.x; q < (u32)tile_words; q += kMergeBlock) out[q] = s_out[q];
   }
-  __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
+    // this workgroup's records (host memory): one system-scope release, not an acq_rel
+    // fence in every thread
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     const u32 prev = atomicAdd(done, 1u);
     if (prev == gridDim.x - 1) {
-      __threadfence_system();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's records
       *done = 0u;  // the next job's launch is stream-ordered behind this one
       __hip_atomic_store(stamps + me, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }

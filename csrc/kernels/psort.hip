@@ -53,7 +53,9 @@ __device__ __forceinline__ void reduce_tail(u32 p, u32 U, u64 pfx, MapCounters* 
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence_system();  // this workgroup's records (host-mapped) and counter writes
+    // this workgroup's records (host-mapped) and counter writes; release only (the last
+    // workgroup acquires)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     s_last = atomicAdd(ra.done_counter, 1u) == (u32)kDictParts - 1 ? 1u : 0u;
   }
   __syncthreads();
@@ -66,11 +68,9 @@ __device__ __forceinline__ void reduce_tail(u32 p, u32 U, u64 pfx, MapCounters* 
   }
   // the host first (records, counters out), then the device scratch re-zeroing, which the
   // next job's kernels behind this one on the stream see complete (as dict.hip)
-  if (ra.host_done && threadIdx.x == 0) {
-    __threadfence_system();
+  if (ra.host_done && threadIdx.x == 0)  // a system-scope release store
     __hip_atomic_store(ra.host_done, ra.host_done_value, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-  }
   __syncthreads();
   if (!(flags & kCtrSortOverflow)) {
     for (u32 i = threadIdx.x; i < ra.map_words; i += kPsBlock) ra.map_lb.status[i] = 0;
