@@ -531,9 +531,7 @@ class GpuShardEngine final : public ShardEngine {
   void exch_map_enqueue(const TextInput& shard, u32 P, u32 S) override {
     ensure_exch_ctl(P, S);
     async_combined_ = enqueue_async_map(shard);
-    if (S)
-      launch_sample_keys(local_keys_, local_n_, S,
-                         reinterpret_cast<PackedKey*>(xb_.msg1_send + sizeof(ExchMsg1)), mp_->stream);
+    // the samples go out with the header (enqueue_msg1_plan): one launch for both
   }
   // Returns whether the token count is the combining map's (map_tokens).
   bool enqueue_async_map(const TextInput& shard) {
@@ -585,7 +583,8 @@ class GpuShardEngine final : public ShardEngine {
       // exch_map_enqueue ran the map and wrote the samples; the header from the counters
       // (from the ordered kernel's counter snapshot: a small pass re-zeroes d_ctr itself)
       launch_exch_header(m.d_ctr_mapped, h, async_combined_,
-                         reinterpret_cast<ExchMsg1*>(xb_.msg1_send), m.stream);
+                         reinterpret_cast<ExchMsg1*>(xb_.msg1_send), m.stream, local_keys_,
+                         local_n_, S);
     } else {
       std::memcpy(xb_.h_msg1, &h, sizeof(ExchMsg1));
       if (S) std::memcpy(xb_.h_msg1 + sizeof(ExchMsg1), samples.data(), (u64)S * sizeof(PackedKey));

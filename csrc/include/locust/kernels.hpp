@@ -455,9 +455,12 @@ void launch_sample_keys(ConstKeysSoA sorted, const u32* d_n, u32 num_samples, Pa
                         hipStream_t s);
 // This rank's ExchMsg1 from the device counters (asynchronous-map exchange, exchange.hip):
 // tmpl's status (host-side failure) or kExchMapRedo on a partition overflow; n_local,
-// tokens (map_tokens of a combining map, else num_records) and the map statistics.
+// tokens (map_tokens of a combining map, else num_records) and the map statistics.  With
+// num_samples, the same launch writes the samples of `sorted` (as launch_sample_keys) as
+// PackedKeys right behind the header.
 void launch_exch_header(const MapCounters* ctr, const ExchMsg1& tmpl, bool combined,
-                        ExchMsg1* out, hipStream_t s);
+                        ExchMsg1* out, hipStream_t s, ConstKeysSoA sorted = ConstKeysSoA{},
+                        const u32* d_n = nullptr, u32 num_samples = 0);
 // offsets[p] = lower_bound(sorted, splitter[p-1]) for p in 1..P-1, offsets[0] = 0,
 // offsets[P] = n.
 void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey* splitters,

@@ -5,6 +5,7 @@
 // on the host between collectives (dist.cpp: choose_splitters, bucket_offsets, the count
 // and total all-gathers) is taken here on the device, so the whole exchange is enqueued
 // behind the map with no host round trip.
+#include <algorithm>
 #include <cstdlib>
 
 #include "locust/device/wave.hpp"
@@ -265,23 +266,42 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
   }
 }
 
+// The header, and (S > 0) the S samples behind it in the same launch: one dependent
+// launch less between the ordered kernel and the all-gather (each is ~4.7 us on the
+// exchange's critical path, profiles/r4/kexch_v2.summary.txt).
 __global__ void exch_header_kernel(const MapCounters* __restrict__ ctr, ExchMsg1 h,
-                                   u32 combined, ExchMsg1* __restrict__ out) {
-  if (threadIdx.x != 0) return;
-  if (!h.status && (ctr->flags & kCtrDictOverflow)) h.status = kExchMapRedo;
-  h.n_local = h.status ? 0 : ctr->num_unique;
-  h.tokens = combined ? ctr->map_tokens : ctr->num_records;
-  h.overflow_lines = ctr->overflow_lines;
-  h.truncated = ctr->truncated;
-  h.max_key_len = ctr->max_key_len;
-  *out = h;
+                                   u32 combined, ExchMsg1* __restrict__ out, ConstKeysSoA sorted,
+                                   const u32* __restrict__ d_n, u32 S) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (!h.status && (ctr->flags & kCtrDictOverflow)) h.status = kExchMapRedo;
+    h.n_local = h.status ? 0 : ctr->num_unique;
+    h.tokens = combined ? ctr->map_tokens : ctr->num_records;
+    h.overflow_lines = ctr->overflow_lines;
+    h.truncated = ctr->truncated;
+    h.max_key_len = ctr->max_key_len;
+    *out = h;
+  }
+  if (!S) return;
+  // sample[k] = keys[floor((k + 0.5) n / S)], "+inf" for an empty shard (launch_sample_keys)
+  PackedKey* smp = reinterpret_cast<PackedKey*>(out + 1);
+  const u32 n = *d_n;
+  for (u32 k = blockIdx.x * blockDim.x + threadIdx.x; k < S; k += gridDim.x * blockDim.x) {
+    PackedKey q;
+    const u64 i = n ? ((2ull * k + 1) * n) / (2ull * S) : 0;
+#pragma unroll
+    for (int w = 0; w < kKeyWords; ++w) q.w[w] = n ? sorted.w[w][i] : ~0ull;
+    smp[k] = q;
+  }
 }
 
 }  // namespace
 
 void launch_exch_header(const MapCounters* ctr, const ExchMsg1& tmpl, bool combined,
-                        ExchMsg1* out, hipStream_t s) {
-  exch_header_kernel<<<dim3(1), dim3(64), 0, s>>>(ctr, tmpl, combined ? 1u : 0u, out);
+                        ExchMsg1* out, hipStream_t s, ConstKeysSoA sorted, const u32* d_n,
+                        u32 num_samples) {
+  LOCUST_CHECK_ARG(!num_samples || d_n, "exchange header: samples need the key count");
+  exch_header_kernel<<<dim3(std::max<u32>(1u, (num_samples + 63) / 64)), dim3(64), 0, s>>>(
+      ctr, tmpl, combined ? 1u : 0u, out, sorted, d_n, num_samples);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

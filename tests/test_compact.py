@@ -6,6 +6,8 @@ output byte-identical to the CPU engine, and the wire bytes it saves) is
 tests/test_gpu_engine.py::test_compact_output_*."""
 import struct
 
+import pytest
+
 import locust_amd as lc
 from locust_amd.utils import oracle
 
@@ -69,3 +71,18 @@ def test_decode_hamlet_sized(hamlet):
     r = lc._C.Result.from_compact(words, segs)
     assert r.entries() == ent
     assert r.wire_bytes / len(ent) < 15  # English keys: one or two words per entry (14.1 B)
+
+
+@pytest.mark.gpu
+def test_gpu_compact_long_counts():
+    """Counts of 2^24 and more take the long record form (kv.hpp): two keys past it -- one
+    of 2 bytes, one of 13 -- through the large-pass ordered kernel, next to short-form keys."""
+    n1, n2 = (1 << 24) + 8, (1 << 24) + 16
+    text = (b"aa aa aa aa aa aa aa aa\n" * (n1 // 8) + b"bbbbbbbbbbbbb bbbbbbbbbbbbb\n" * (n2 // 2)
+            + b"".join(b"zebra%d\n" % i for i in range(1000)))
+    r = lc.wordcount_text(text, backend="gpu")
+    assert r.compact
+    ent = r.entries()
+    assert ent[0] == (b"aa", 0, n1) and ent[1] == (b"bbbbbbbbbbbbb", n1, n2)
+    assert len(ent) == 1002 and all(c == 1 for _k, _v, c in ent[2:])
+    assert sorted(k for k, _v, _c in ent[2:]) == sorted(b"zebra%d" % i for i in range(1000))
