@@ -1606,7 +1606,8 @@ __device__ __forceinline__ void ordered_partition(
     }
     __syncthreads();
     if (s_count) {
-      __threadfence();  // acquire every other workgroup's
+      // acquire every other workgroup's (acquire only: this one released its own already)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // Tell the host first: every workgroup's records, counters and headers are out (each
       // released them before counting itself done).  The re-zeroing below touches device

@@ -60,7 +60,7 @@ __device__ __forceinline__ void reduce_tail(u32 p, u32 U, u64 pfx, MapCounters* 
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();  // acquire every other workgroup's
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every other workgroup's (acquire only)
   const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x == 0 && ra.ctr_out) {
     MapCounters c = *ctr;
