@@ -149,5 +149,32 @@ int main() {
     for (auto& th : ths) th.join();
     STEP("8 threads x concurrent H2D", hipSuccess);
   }
+  // eight threads launching kernels at the same time, each on a stream of its own, with
+  // an event per launch the host waits on (the rank threads' map loops do both)
+  {
+    std::vector<std::thread> ths;
+    std::atomic<int> ready{0};
+    for (int t = 0; t < 8; ++t)
+      ths.emplace_back([&, t] {
+        (void)hipSetDevice(0);
+        hipStream_t ts;
+        (void)hipStreamCreateWithFlags(&ts, hipStreamNonBlocking);
+        hipEvent_t ev;
+        (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        ready.fetch_add(1);
+        while (ready.load() < 8) {
+        }
+        for (int k = 0; k < 2000; ++k) {
+          touch<<<64, 256, 0, ts>>>(d + t);
+          if (k % 16 == 0) {
+            (void)hipEventRecord(ev, ts);
+            (void)hipEventSynchronize(ev);
+          }
+        }
+        (void)hipStreamSynchronize(ts);
+      });
+    for (auto& th : ths) th.join();
+    STEP("8 threads x concurrent kernels", hipSuccess);
+  }
   return 0;
 }
