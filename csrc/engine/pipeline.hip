@@ -10,7 +10,7 @@ namespace detail {
 u64 DevicePipeline::piece_target() {
   static const u64 b = [] {
     const char* e = std::getenv("LOCUST_PIECE_MB");
-    const long mb = e ? std::atol(e) : 12;
+    const long mb = e ? std::atol(e) : 10;
     return (u64)std::max<long>(mb, 4) << 20;
   }();
   return b;

@@ -105,9 +105,11 @@ struct DevicePipeline {
   // Large single-pass inputs travel in line-aligned pieces on the copy stream, each mapped
   // and aggregated as soon as it lands (the H2D overlaps map + partials); set by
   // prepare_upload.  At least kPieceBytes each (inputs from 2 x kPieceBytes on), middle
-  // pieces min(piece_target(), bytes / 4) (LOCUST_PIECE_MB, default 12: fewer copies run
+  // pieces min(piece_target(), bytes / 4) (LOCUST_PIECE_MB, default 10: fewer copies run
   // the link closer to a single DMA's rate -- synth1m with 4 / 8 / 12 / 16 MiB targets:
-  // 1.24 / 1.21 / 1.185 / 1.19 ms), at most partial_slots_cap of them.
+  // 1.24 / 1.21 / 1.185 / 1.19 ms in round 3; with round 4's shorter ordered kernel 10 MiB
+  // beats 12 (median 1.047 vs 1.060 ms over five alternating rounds,
+  // profiles/r4/piece_ab.txt)), at most partial_slots_cap of them.
   static constexpr u64 kPieceBytes = 4ull << 20;
   static constexpr u64 kDevPageBytes = 2ull << 20;  // device allocations: whole 2 MiB pages
   static u64 piece_target();
