@@ -74,7 +74,8 @@ debug:
 # --backend cpu.  (GPU ASan / xnack+ is not available on the GPU pool.)
 ASAN_SRCS := csrc/engine/common.cpp csrc/engine/cpu_wordcount.cpp csrc/engine/dist.cpp \
              csrc/io/io.cpp csrc/io/gen.cpp csrc/comm/tcp_comm.cpp csrc/cli/main.cpp \
-             csrc/engine/trace.cpp csrc/engine/shm.cpp csrc/engine/numa.cpp csrc/cli/asan_stubs.cpp
+             csrc/engine/trace.cpp csrc/engine/shm.cpp csrc/engine/numa.cpp csrc/engine/stage.cpp \
+             csrc/cli/asan_stubs.cpp
 asan: $(BUILD)/asan/MapReduce
 $(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
 	@mkdir -p $(dir $@)

@@ -4,6 +4,7 @@
 // (xnack+) is not available on the GPU pool.
 #include "locust/dist.hpp"
 #include "locust/engine.hpp"
+#include "locust/stage.hpp"
 
 namespace locust {
 
@@ -26,6 +27,11 @@ DistResult run_single_process_multi_gpu(const DistConfig&, const TextInput&, Loc
 }
 DistResult run_single_process_file(const DistConfig&, const std::string&, LocalComm,
                                    std::vector<DistResult>*) {
+  no_gpu();
+}
+std::vector<WordCountEntry> merge_runs_device(const JobConfig&,
+                                              const std::vector<std::vector<KeyCount>>&,
+                                              double*) {
   no_gpu();
 }
 int visible_device_count() { return 0; }

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -29,6 +30,7 @@
 #include "locust/engine.hpp"
 #include "locust/gen.hpp"
 #include "locust/io.hpp"
+#include "locust/stage.hpp"
 
 using namespace locust;
 
@@ -50,6 +52,8 @@ struct CliArgs {
   std::string spill_dir = "/tmp";
   SpillFormat spill_fmt = SpillFormat::kText;
   std::vector<std::string> inputs;
+  int reducer = 0, reducers = 1;  // --reducer r/R: key range r of R (stage 2)
+  std::string result_file;        // --result-file: the result lines go there, not stdout
   int warmup = 0, iters = 1;
   std::string json;
   std::string export_kiv;  // final results as KeyIntValuePair records (--export-kiv FILE)
@@ -61,6 +65,27 @@ struct CliArgs {
 void usage() {
   std::printf("Missing or invalid arguments.\n");
   std::printf("mapreduce <filename> [line_start] [line_end] [node_num] [stage]\n");
+}
+
+void help() {
+  std::printf(
+      "usage: MapReduce <file> [line_start line_end [node_num stage]] [flags]\n"
+      "       MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]\n"
+      "\n"
+      "  stage 0: the whole job; 1: map only, writes the combined spill <spill-dir>/out.<node>.*\n"
+      "  and its index; 2: reduce only, merges spills (--inputs a,b,... or out.<node>.*)\n"
+      "\n"
+      "  --backend gpu|cpu          --reduce-path lds|global   --map-path fast|compat\n"
+      "  --sort dict|radix          --gpus N                   --comm auto|loopback|rccl\n"
+      "  --strategy auto|gather|shuffle                        --device N\n"
+      "  --emits-per-line N         --max-key N                --ref-compat\n"
+      "  --stage map|reduce         --spill-dir DIR            --spill-format text|binary|kiv\n"
+      "  --inputs a,b,...           --reducer r/R              --result-file FILE\n"
+      "  --export-kiv FILE          --json FILE|-              --quiet --check --combine\n"
+      "  --warmup N --iters N       --chunk-mb N               --ref-timers\n"
+      "  --help\n"
+      "\n"
+      "Environment: LOCUST_LOG=info|debug and the LOCUST_* switches in docs/ENVIRONMENT.md.\n");
 }
 
 std::vector<std::string> split(const std::string& s, char c) {
@@ -132,6 +157,16 @@ bool parse(int argc, char** argv, CliArgs* a) {
       a->export_kiv = need("--export-kiv");
     } else if (s == "--inputs") {
       a->inputs = split(need("--inputs"), ',');
+    } else if (s == "--reducer") {
+      const std::string v = need("--reducer");
+      const size_t sl = v.find('/');
+      if (sl == std::string::npos) throw Error("--reducer r/R");
+      a->reducer = std::atoi(v.substr(0, sl).c_str());
+      a->reducers = std::atoi(v.substr(sl + 1).c_str());
+      if (a->reducers < 1 || a->reducer < 0 || a->reducer >= a->reducers)
+        throw Error("--reducer r/R needs 0 <= r < R");
+    } else if (s == "--result-file") {
+      a->result_file = need("--result-file");
     } else if (s == "--warmup") {
       a->warmup = std::atoi(need("--warmup").c_str());
     } else if (s == "--iters") {
@@ -175,10 +210,22 @@ bool parse(int argc, char** argv, CliArgs* a) {
   return true;
 }
 
+const char* spill_ext(SpillFormat f) {
+  return f == SpillFormat::kBinary ? ".kv" : f == SpillFormat::kKiv ? ".kiv" : ".txt";
+}
 std::string spill_path(const CliArgs& a, int node) {
-  return a.spill_dir + "/out." + std::to_string(node) +
-         (a.spill_fmt == SpillFormat::kBinary ? ".kv" : a.spill_fmt == SpillFormat::kKiv ? ".kiv"
-                                                                                   : ".txt");
+  return a.spill_dir + "/out." + std::to_string(node) + spill_ext(a.spill_fmt);
+}
+// Stage 2 without --inputs: this node's spill in the --spill-format named, else whichever
+// of out.N.txt / .kv / .kiv exists (read_spill tells the formats apart by content).
+std::string find_spill(const CliArgs& a, int node) {
+  const std::string want = spill_path(a, node);
+  if (access(want.c_str(), R_OK) == 0) return want;
+  for (SpillFormat f : {SpillFormat::kText, SpillFormat::kBinary, SpillFormat::kKiv}) {
+    const std::string p = a.spill_dir + "/out." + std::to_string(node) + spill_ext(f);
+    if (access(p.c_str(), R_OK) == 0) return p;
+  }
+  return want;  // (its open fails with the path in the message)
 }
 
 // --json: one record per run, in every mode: counts, honest and
@@ -393,54 +440,221 @@ unsigned long long peak_rss_kb() {
 // Stream threshold: files past one device pass (--chunk-mb, default 256 MiB) stream.
 constexpr u64 kDefaultStreamChunk = 256ull << 20;
 
+// The RSS stamps of --json runs at LOCUST_LOG=info (reading /proc costs the one-shot CLI).
+void log_rss(const char* when) {
+  if ((int)log_level() >= (int)LogLevel::kInfo)
+    LOCUST_LOG_INFO("%s: %s", when, process_rss_breakdown().c_str());
+}
+
 int run_direct(const CliArgs& a) {
   JobConfig cfg = a.cfg;
   const u64 size = file_size(a.file);
   const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
   WordCountResult r;
   std::vector<double> walls;
-  LOCUST_LOG_INFO("before the engine: %s", process_rss_breakdown().c_str());
+  log_rss("before the engine");
   Startup& st = g_startup;
   (void)visible_device_count();  // the HIP runtime's own start-up, timed apart
   st.init = now_ns();
+  // The engine outlives the output: its teardown (stream, pinned buffers) is not a job's
+  std::unique_ptr<GpuWordCount> eng;
   if (size > chunk) {
     cfg.chunk_bytes = chunk;
-    GpuWordCount eng(cfg, size, size);
+    eng.reset(new GpuWordCount(cfg, size, size));
     st.engine = st.read = now_ns();  // the file is read by the job, piece by piece
-    LOCUST_LOG_INFO("with the streaming engine: %s", process_rss_breakdown().c_str());
+    log_rss("with the streaming engine");
     for (int i = 0; i < a.warmup + a.iters; ++i) {
       auto src = open_file_source(a.file);
-      r = eng.run_source(*src);
+      r = eng->run_source(*src);
       if (i >= a.warmup) walls.push_back(r.times.wall_ms);
       if (i == 0) st.first = now_ns();
     }
   } else {
-    GpuWordCount eng(cfg, std::max<u64>(size, 1), std::max<u64>(size, 1));
+    eng.reset(new GpuWordCount(cfg, std::max<u64>(size, 1), std::max<u64>(size, 1)));
     st.engine = now_ns();
     TextInput in;
-    in.data = eng.input_buffer();
-    in.bytes = read_file_into(a.file, eng.input_buffer(), std::max<u64>(size, 1), &in.num_lines);
+    in.data = eng->input_buffer();
+    in.bytes = read_file_into(a.file, eng->input_buffer(), std::max<u64>(size, 1), &in.num_lines);
     in.first_line = 0;
     st.read = now_ns();
+    std::vector<u64> stamps;  // per job: start, after run(), after the result is stored
+    stamps.reserve(3 * (size_t)(a.warmup + a.iters));
     for (int i = 0; i < a.warmup + a.iters; ++i) {
-      const u64 tj = now_ns();
+      stamps.push_back(now_ns());
       if (i < a.warmup) {
-        eng.run(in);
+        eng->run(in);
+        stamps.push_back(now_ns());
       } else {
-        r = eng.run(in);
+        WordCountResult x = eng->run(in);
+        stamps.push_back(now_ns());
+        r = std::move(x);
         walls.push_back(r.times.wall_ms);
       }
-      if (i == 0) st.first = now_ns();
-      LOCUST_LOG_DEBUG("job %d: %.3f ms host (the job's own wall %.3f ms)", i, (now_ns() - tj) * 1e-6,
-                       i < a.warmup ? 0.0 : r.times.wall_ms);
+      stamps.push_back(now_ns());
+      if (i == 0) st.first = stamps.back();
     }
+    if ((int)log_level() >= (int)LogLevel::kDebug)
+      for (size_t k = 0; k + 2 < stamps.size(); k += 3)
+        LOCUST_LOG_DEBUG("job %zu: starts %+.3f ms, run() %.3f ms, result stored %.3f ms", k / 3,
+                         (stamps[k] - st.read) * 1e-6, (stamps[k + 1] - stamps[k]) * 1e-6,
+                         (stamps[k + 2] - stamps[k + 1]) * 1e-6);
     r.num_lines = in.num_lines;
   }
   st.jobs = now_ns();
-  LOCUST_LOG_INFO("after the job: %s", process_rss_breakdown().c_str());
+  log_rss("after the job");
   std::printf("Length: %i\n", (int)r.num_lines);
   print_gpu_result(a, r, walls);
-  LOCUST_LOG_INFO("after the output: %s", process_rss_breakdown().c_str());
+  log_rss("after the output");
+  const u64 t_down = now_ns();
+  eng.reset();
+  LOCUST_LOG_DEBUG("engine teardown %.3f ms", (now_ns() - t_down) * 1e-6);
+  return 0;
+}
+
+// The result lines to stdout, or to --result-file (a range reducer on a worker daemon,
+// whose reply carries only the tail of stdout).
+void emit_results(const CliArgs& a, const std::string& out) {
+  if (a.result_file.empty()) {
+    std::fflush(stdout);
+    write_all(stdout, out);
+    return;
+  }
+  std::FILE* f = std::fopen(a.result_file.c_str(), "wb");
+  if (!f) throw Error("cannot write " + a.result_file);
+  write_all(f, out);
+  if (std::fclose(f) != 0) throw Error("error closing " + a.result_file);
+}
+
+// ---------------- stage 1: map only -> spill (main.cu:421-433) ----------------
+// The combined map output -- one (key, count) record per distinct key, in key order -- and
+// its index.  A GPU line window is found by a newline scan and read straight from the file
+// into the engine's pinned buffer; past one device pass (--chunk-mb, 256 MiB) it streams
+// through a streaming engine, so host memory stays bounded for any window size.
+// --ref-compat keeps the reference's spill: one "key \t1" record per token, sorted.
+int run_map_stage(const CliArgs& a) {
+  const bool cpu = a.cfg.backend == Backend::kCpu;
+  const char* dev = cpu ? "CPU" : "GPU";
+  const std::string path = spill_path(a, a.node);
+  WordCountResult r;
+  std::vector<KeyCount> recs;
+  u64 lines = 0, bytes = 0;
+  bool streamed = false;
+  const u64 t0 = now_ns();
+  if (cpu || a.cfg.ref_compat) {
+    const bool use_window = a.window && !(cpu && a.cfg.ref_compat);
+    LoadedText text = load_lines(a.file, use_window ? a.line_start : -1,
+                                 use_window ? a.line_end : -1, a.cfg.ref_compat);
+    lines = text.input.num_lines;
+    bytes = text.input.bytes;
+    if (a.cfg.ref_compat) {
+      std::vector<PackedKey> toks;
+      if (cpu) {
+        toks = CpuWordCount(a.cfg).run_map_stage(text.input, &r);
+      } else {
+        GpuWordCount eng(a.cfg, std::max<u64>(bytes, 1), std::max<u64>(lines, 1));
+        toks = eng.run_map_stage(text.input, &r);
+      }
+      r.num_tokens = toks.size();
+      recs = tokens_to_records(toks);
+    } else {
+      r = CpuWordCount(a.cfg).run(text.input);
+      recs = entries_to_records(r.entries);
+    }
+  } else {
+    LineWindow w;
+    if (a.window) {
+      w = find_line_window(a.file, a.line_start, a.line_end);
+    } else {
+      w.end = file_size(a.file);
+    }
+    bytes = w.end - w.begin;
+    JobConfig cfg = a.cfg;
+    cfg.graph = 0;  // stage events: the map and sort times printed below
+    const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
+    if (bytes > chunk) {
+      cfg.chunk_bytes = chunk;
+      GpuWordCount eng(cfg, bytes, bytes);
+      auto src = open_file_range_source(a.file, w.begin, w.end);
+      r = eng.run_source(*src);
+      lines = src->lines();
+      streamed = true;
+      recs = entries_to_records(r.entries);
+    } else {
+      GpuWordCount eng(cfg, std::max<u64>(bytes, 1), std::max<u64>(bytes, 1));
+      TextInput in;
+      in.data = eng.input_buffer();
+      in.bytes = read_file_range_into(a.file, eng.input_buffer(), w.begin, bytes, &lines);
+      in.num_lines = lines;
+      r = eng.run(in);
+      recs = entries_to_records(r.entries);
+    }
+    if (a.window) lines = w.lines;
+  }
+  const u64 t1 = now_ns();
+  SpillIndex idx;
+  write_spill(path, recs, a.spill_fmt, &idx);
+  write_spill_index(spill_index_path(path), idx);
+  const u64 t2 = now_ns();
+  if (!cpu) std::printf("Length: %i\n", (int)lines);
+  for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
+  // event-timed on the GPU: H2D + map, then compaction/combine + sort
+  std::printf("%s mapping %lld nanoseconds \n", dev, ns(r.times.h2d_ms + r.times.map_ms));
+  std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev,
+              ns(r.times.process_ms + r.times.reduce_ms));
+  if (!a.json.empty()) {
+    JsonOut j = json_head(a, "map_stage");
+    r.num_lines = lines;
+    json_counts(j, r);
+    j.u("spill_records", recs.size());
+    j.u("spill_bytes", idx.spill_bytes);
+    j.str("spill", path);
+    j.kv("combined", a.cfg.ref_compat ? "false" : "true");
+    j.kv("streamed", streamed ? "true" : "false");
+    j.u("input_bytes", bytes);
+    j.num("map_ms", r.times.h2d_ms + r.times.map_ms);
+    j.num("process_ms", r.times.process_ms + r.times.reduce_ms);
+    j.num("job_ms", (t1 - t0) * 1e-6);
+    j.num("spill_write_ms", (t2 - t1) * 1e-6);
+    j.u("peak_rss_kb", peak_rss_kb());
+    emit_json(a, j.done());
+  }
+  std::printf("MODE_MULTI: Finished map\n");
+  return 0;
+}
+
+// ---------------- stage 2: reduce only (main.cu:437-486) ----------------
+// Every spill is a sorted run (the reference's reducer needed one pre-sorted file, B7):
+// this reducer's key range of each is read (an index seek) and merged, counts summed --
+// never expanded into tokens.  --reducer r/R: key range r of R, with its global val base.
+int run_reduce_stage(const CliArgs& a) {
+  const bool cpu = a.cfg.backend == Backend::kCpu;
+  std::vector<std::string> files = a.inputs;
+  if (files.empty()) files.push_back(find_spill(a, a.node));
+  ReduceStageStats st;
+  WordCountResult r = reduce_spills(a.cfg, files, a.reducer, a.reducers, &st);
+  std::printf("%s reduce %lld nanoseconds \n", cpu ? "CPU" : "GPU", ns(st.merge_ms));
+  std::string out;
+  if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r, &out);
+  emit_results(a, out);
+  if (!a.json.empty()) {
+    JsonOut j = json_head(a, "reduce_stage");
+    json_counts(j, r);
+    j.u("input_files", st.input_files);
+    j.u("indexed_files", st.indexed_files);
+    j.u("records_read", st.records_read);
+    j.u("input_records", st.run_records);
+    j.kv("reducer", std::to_string(a.reducer));
+    j.kv("reducers", std::to_string(a.reducers));
+    j.u("val_base", r.val_base);
+    j.num("read_ms", st.read_ms);
+    j.num("setup_ms", st.setup_ms);
+    j.num("merge_ms", st.merge_ms);
+    j.num("wall_ms", r.times.wall_ms);
+    j.u("peak_rss_kb", peak_rss_kb());
+    emit_json(a, j.done());
+  }
+  if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r);
+  std::printf("\nDone\n");
   return 0;
 }
 
@@ -452,44 +666,8 @@ int run(const CliArgs& a) {
     std::printf("Using custom start and end locations: (%i, %i)\n", (int)a.line_start,
                 (int)a.line_end);
 
-  // ---------------- stage 2: reduce only ----------------
-  if (a.stage == 2) {
-    std::vector<std::string> files = a.inputs;
-    if (files.empty()) files.push_back(spill_path(a, a.node));
-    std::vector<KeyCount> recs;
-    for (const auto& f : files) {
-      auto r = read_spill(f);
-      recs.insert(recs.end(), r.begin(), r.end());
-    }
-    std::vector<PackedKey> toks = records_to_tokens(recs);
-    WordCountResult r;
-    if (cpu) {
-      CpuWordCount eng(a.cfg);
-      r = eng.run_reduce_stage(toks.data(), toks.size());
-    } else {
-      // capacity: records = min(lines x emits, bytes / 2 + 1) must hold every token
-      GpuWordCount eng(a.cfg, 2 * toks.size() + 2,
-                       std::max<u64>(1, div_up(toks.size(), a.cfg.emits_per_line)) + 1);
-      r = eng.run_reduce_stage(toks.data(), toks.size());
-    }
-    std::printf("%s reduce %lld nanoseconds \n", dev, ns(r.times.process_ms + r.times.reduce_ms));
-    std::string out;
-    if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r, &out);
-    std::fflush(stdout);
-    write_all(stdout, out);
-    if (!a.json.empty()) {
-      JsonOut j = json_head(a, "reduce_stage");
-      json_counts(j, r);
-      j.u("input_records", recs.size());
-      j.u("input_files", files.size());
-      j.num("process_ms", r.times.process_ms);
-      j.num("reduce_ms", r.times.reduce_ms);
-      j.num("wall_ms", r.times.wall_ms);
-      emit_json(a, j.done());
-    }
-    std::printf("\nDone\n");
-    return 0;
-  }
+  if (a.stage == 2) return run_reduce_stage(a);
+  if (a.stage == 1) return run_map_stage(a);
 
   // CPU build ignores the line window (its loadFile takes none, main.cu:242) -- only
   // reproduced under --ref-compat.
@@ -529,7 +707,7 @@ int run(const CliArgs& a) {
     std::vector<DistResult> ranks;
     DistResult dr = file_ranks ? run_single_process_file(dc, a.file, a.comm, &ranks)
                                : run_single_process_multi_gpu(dc, text.input, a.comm, &ranks);
-    LOCUST_LOG_INFO("after the job: %s", process_rss_breakdown().c_str());
+    log_rss("after the job");
     if (file_ranks && !cpu) std::printf("Length: %i\n", (int)dr.result.num_lines);
     std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
@@ -540,38 +718,6 @@ int run(const CliArgs& a) {
     write_all(stdout, out);
     write_json_dist(a, dr, ranks);
     std::printf("\nDone\n");
-    return 0;
-  }
-
-  // ---------------- stage 1: map only -> spill ----------------
-  if (a.stage == 1) {
-    WordCountResult stats;
-    std::vector<PackedKey> toks;
-    const u64 t0 = now_ns();
-    if (cpu) {
-      CpuWordCount eng(a.cfg);
-      toks = eng.run_map_stage(text.input, &stats);
-    } else {
-      GpuWordCount eng(a.cfg, text.input.bytes, text.input.num_lines);
-      toks = eng.run_map_stage(text.input, &stats);
-    }
-    const u64 t1 = now_ns();
-    for (u64 k = 0; k < stats.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
-    std::printf("%s mapping %lld nanoseconds \n", dev, 0ll);
-    std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, (long long)(t1 - t0));
-    const std::vector<KeyCount> recs = tokens_to_records(toks);
-    write_spill(spill_path(a, a.node), recs, a.spill_fmt);
-    if (!a.json.empty()) {
-      JsonOut j = json_head(a, "map_stage");
-      stats.num_lines = text.input.num_lines;
-      if (!stats.num_tokens) stats.num_tokens = toks.size();
-      json_counts(j, stats);
-      j.u("spill_records", recs.size());
-      j.str("spill", spill_path(a, a.node));
-      j.num("map_process_ms", (t1 - t0) * 1e-6);
-      emit_json(a, j.done());
-    }
-    std::printf("MODE_MULTI: Finished map\n");
     return 0;
   }
 
@@ -617,6 +763,11 @@ int main(int argc, char** argv) {
   // before any thread or RCCL use (see locust_amd/__init__.py); a user's setting wins
   g_startup.main = now_ns();
   setenv("NCCL_GRAPH_REGISTER", "0", 0);
+  for (int i = 1; i < argc; ++i)
+    if (std::strcmp(argv[i], "--help") == 0 || std::strcmp(argv[i], "-h") == 0) {
+      help();
+      return 0;
+    }
   std::printf("Running\n");
   CliArgs a;
   try {

@@ -1,6 +1,7 @@
 // Single-GPU WordCount engine (GpuWordCount): the public API over the device pipeline
 // (csrc/engine/pipeline.hpp).
 #include "pipeline.hpp"
+#include "locust/stage.hpp"
 
 namespace locust {
 
@@ -41,20 +42,34 @@ std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCoun
   Impl& m = *impl_;
   m.sync_clean = false;  // this entry point dirties d_sync
   m.check_input(in);
+  const u64 t0 = now_ns();
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[0], m.stream));
   m.enqueue_upload(in);
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[1], m.stream));
   m.enqueue_map(in);
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[2], m.stream));
   m.enqueue_process((u32)in.num_lines, m.cfg.map_path == MapPath::kCompat, false, kUnknownCount,
                     /*allow_psort=*/true);
+  LOCUST_HIP_CHECK(hipEventRecord(m.ev[3], m.stream));
   m.read_counters();
+  StageTimes tm;
+  tm.h2d_ms = DevicePipeline::ms_between(m.ev[0], m.ev[1]);
+  tm.map_ms = DevicePipeline::ms_between(m.ev[1], m.ev[2]);
+  tm.process_ms = DevicePipeline::ms_between(m.ev[2], m.ev[3]);
   if (m.h_ctr->flags & kCtrSortOverflow) {  // a partition outgrew the LDS sort
+    LOCUST_HIP_CHECK(hipEventRecord(m.ev[2], m.stream));
     m.redo_process_general((u32)in.num_lines);
+    LOCUST_HIP_CHECK(hipEventRecord(m.ev[3], m.stream));
     m.read_counters();
+    tm.process_ms = DevicePipeline::ms_between(m.ev[2], m.ev[3]);
   }
   std::vector<PackedKey> out;
   m.download_keys(m.sorted, m.h_ctr->num_records, &out);
+  tm.wall_ms = (now_ns() - t0) * 1e-6;
   if (stats) {
     stats->num_lines = in.num_lines;
     m.fill_counters(*stats);
+    stats->times = tm;
   }
   return out;
 }
@@ -172,6 +187,109 @@ WordCountResult GpuWordCount::merge_runs(const std::vector<std::vector<KeyCount>
   m.fill_counters(r);
   m.copy_out(r.entries, m.h_ctr->num_unique);
   return r;
+}
+
+namespace {
+
+struct RunSlice {
+  const KeyCount* p;
+  u64 n;
+};
+
+// Merges the slices (each sorted, distinct keys) into `out` (appended, key order) on
+// `eng`, whose capacity is `limit` records: one launch_merge_sorted_runs per group of
+// <= 64 runs holding <= limit records and a total count below the kernel's 2^40; more
+// runs merge in rounds, more records split at the median key of the largest run.
+void merge_slices(GpuWordCount& eng, u64 limit, std::vector<RunSlice> runs,
+                  std::vector<WordCountEntry>* out) {
+  runs.erase(std::remove_if(runs.begin(), runs.end(), [](const RunSlice& r) { return r.n == 0; }),
+             runs.end());
+  if (runs.empty()) return;
+  u64 total = 0, count = 0;
+  for (const RunSlice& r : runs) {
+    total += r.n;
+    for (u64 i = 0; i < r.n; ++i) count += r.p[i].count;
+  }
+  if (runs.size() == 1) {
+    for (u64 i = 0; i < runs[0].n; ++i) {
+      WordCountEntry e;
+      for (int w = 0; w < kKeyWords; ++w) e.key.w[w] = runs[0].p[i].w[w];
+      e.count = runs[0].p[i].count;
+      out->push_back(e);
+    }
+    return;
+  }
+  if (total <= limit && count <= kMergeMaxCount) {
+    if (runs.size() <= (size_t)kMaxMergeRunsHost) {
+      std::vector<std::vector<KeyCount>> v(runs.size());
+      for (size_t q = 0; q < runs.size(); ++q) v[q].assign(runs[q].p, runs[q].p + runs[q].n);
+      WordCountResult r = eng.merge_runs(v);
+      for (const WordCountEntry e : r.entries) out->push_back(e);
+      return;
+    }
+    // rounds: every group of 64 runs becomes one run
+    std::vector<std::vector<KeyCount>> level;
+    for (size_t g = 0; g < runs.size(); g += kMaxMergeRunsHost) {
+      std::vector<RunSlice> grp(runs.begin() + (long)g,
+                                runs.begin() + (long)std::min(runs.size(), g + kMaxMergeRunsHost));
+      std::vector<WordCountEntry> e;
+      merge_slices(eng, limit, grp, &e);
+      std::vector<KeyCount> run(e.size());
+      for (size_t i = 0; i < e.size(); ++i) {
+        for (int w = 0; w < kKeyWords; ++w) run[i].w[w] = e[i].key.w[w];
+        run[i].count = e[i].count;
+      }
+      level.push_back(std::move(run));
+    }
+    std::vector<RunSlice> next;
+    for (const auto& r : level) next.push_back({r.data(), r.size()});
+    return merge_slices(eng, limit, next, out);
+  }
+  if (total <= runs.size()) {  // one record per run left and still too much count: host
+    std::vector<std::vector<KeyCount>> v(runs.size());
+    for (size_t q = 0; q < runs.size(); ++q) v[q].assign(runs[q].p, runs[q].p + runs[q].n);
+    for (const WordCountEntry e : merge_runs_host(v)) out->push_back(e);
+    return;
+  }
+  // split by key range at the median of the largest run: both halves shrink
+  size_t big = 0;
+  for (size_t q = 1; q < runs.size(); ++q)
+    if (runs[q].n > runs[big].n) big = q;
+  const KeyCount pivot = runs[big].p[runs[big].n / 2];
+  std::vector<RunSlice> left, right;
+  for (const RunSlice& r : runs) {
+    const KeyCount* m = std::lower_bound(r.p, r.p + r.n, pivot, record_less);
+    left.push_back({r.p, (u64)(m - r.p)});
+    right.push_back({m, r.n - (u64)(m - r.p)});
+  }
+  merge_slices(eng, limit, left, out);
+  merge_slices(eng, limit, right, out);
+}
+
+}  // namespace
+
+std::vector<WordCountEntry> merge_runs_device(const JobConfig& cfg,
+                                              const std::vector<std::vector<KeyCount>>& runs,
+                                              double* setup_ms) {
+  u64 total = 0;
+  for (const auto& r : runs) total += r.size();
+  std::vector<WordCountEntry> out;
+  if (!total) return out;
+  out.reserve(total);
+  JobConfig c = cfg;
+  c.chunk_bytes = 0;  // one pass: the engine holds a merge's records
+  u64 limit = std::min<u64>(total, kMergeMaxRecords);
+  // LOCUST_MERGE_MAX_RECORDS: a lower per-launch record limit (tests of the key-range split)
+  if (const char* e = std::getenv("LOCUST_MERGE_MAX_RECORDS"))
+    limit = std::max<u64>(2, std::min<u64>(limit, (u64)std::atoll(e)));
+  // capacity = min(lines x emits, bytes / 2 + 1) >= limit
+  const u64 t0 = now_ns();
+  GpuWordCount eng(c, 2 * limit + 2, limit + 1);
+  if (setup_ms) *setup_ms = (now_ns() - t0) * 1e-6;
+  std::vector<RunSlice> slices;
+  for (const auto& r : runs) slices.push_back({r.data(), r.size()});
+  merge_slices(eng, limit, slices, &out);
+  return out;
 }
 
 }  // namespace locust

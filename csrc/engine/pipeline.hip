@@ -70,6 +70,9 @@ void DevicePipeline::warm_modules_once(int device) {
   const u64 bit = 1ull << (device & 63);
   if (warmed & bit) return;
   warm_kernel_modules();
+  // the first roctx range of a process initialises the library (~0.12 ms, measured inside
+  // a fresh engine's first job): pay it here
+  { TraceRange warm("locust:warm"); }
   warmed |= bit;
 }
 
@@ -308,6 +311,9 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
     if (devplan_env) ensure_plan();
     warm_copy_streams();
   }
+  // the retune worker of a small engine is made here, not inside its first job (a
+  // streaming engine's jobs take hundreds of ms: it makes it when first needed)
+  if (!streaming) retune_worker.start();
   tc[5] = now_ns();
   LOCUST_LOG_DEBUG("engine (%llu B text, %llu records): modules %.2f ms, stream %.2f ms, device "
                    "arena %.2f ms (%.1f MiB), pinned host buffers %.2f ms, copy streams %.2f ms",
@@ -328,7 +334,7 @@ void DevicePipeline::warm_copy_streams() {
 }
 
 DevicePipeline::~DevicePipeline() {
-  if (retune_job.valid()) retune_job.wait();
+  retune_worker.stop();  // its task may hold an output buffer
   if (stream) (void)hipStreamSynchronize(stream);
   for (auto& g : dict_graphs) (void)hipGraphExecDestroy(g.exec);
   for (auto& g : graph_cache) (void)hipGraphExecDestroy(g.exec);
@@ -380,10 +386,10 @@ void DevicePipeline::select_out() {
   if (!out_pool.empty() && out_pool[out_idx].use_count() == 1) return;
   for (size_t i = 0; i < out_pool.size(); ++i)
     if (out_pool[i].use_count() == 1) return use_out(i);
-  if (retune_job.valid()) {
+  if (retune_pending) {
     // a background retune reads a buffer a result no longer needs: let it finish (it is
     // near the end by now) rather than pin a new buffer (~2 ms for a large engine's)
-    retune_job.wait();
+    retune_worker.wait_idle();
     poll_retune();
     for (size_t i = 0; i < out_pool.size(); ++i)
       if (out_pool[i].use_count() == 1) return use_out(i);
@@ -832,31 +838,26 @@ void DevicePipeline::force_retune(const EntryList& e) {
 }
 
 void DevicePipeline::maybe_retune(const EntryList& e) {
-  if (const u64 mx = retune_wanted()) {
-    if (large_ordered && e.size() > (1u << 16)) return retune_async(mx, e);
-    PartMapTables t;
-    retune_with(mx, part_map_from_entries(e, &t), t);
-  }
-}
-
-void DevicePipeline::retune_async(u64 mx, const EntryList& e) {
-  if (retune_job.valid()) return;  // one at a time
-  std::shared_ptr<HostOut> hold = out_pool[out_idx];
+  const u64 mx = retune_wanted();
+  if (!mx || retune_pending) return;  // one at a time
+  retune_pending = true;
+  retune_task.mx = mx;
+  retune_task.pred = 0;
   // a borrowed list: the copy shares the buffer (and its segments), not the entries
-  retune_job = std::async(std::launch::async, [hold, mx, e] {
-    RetuneTask r;
-    r.mx = mx;
-    r.pred = part_map_from_entries(e, &r.t);
-    return r;
+  retune_task.hold = out_pool[out_idx];
+  retune_task.entries = e;
+  retune_worker.submit([this] {
+    RetuneTask& r = retune_task;
+    r.pred = part_map_from_entries(r.entries, &r.t);
+    r.entries = EntryList();
+    r.hold.reset();
   });
 }
 
 void DevicePipeline::poll_retune() {
-  if (!retune_job.valid() ||
-      retune_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
-    return;
-  RetuneTask r = retune_job.get();
-  retune_with(r.mx, r.pred, r.t);
+  if (!retune_pending || !retune_worker.idle()) return;
+  retune_pending = false;
+  retune_with(retune_task.mx, retune_task.pred, retune_task.t);
 }
 
 void DevicePipeline::maybe_retune_records(const KeyCount* d_recs, u64 n, bool force) {

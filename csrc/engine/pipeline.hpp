@@ -33,6 +33,7 @@
 #include "locust/kernels.hpp"
 #include "locust/partmap.hpp"
 #include "locust/trace.hpp"
+#include "locust/worker.hpp"
 
 namespace locust {
 
@@ -568,17 +569,20 @@ struct DevicePipeline {
                                     stream));
     pm_predicted_max = pred;
   }
+  // The map is built on the engine's worker thread (part_map_from_entries took ~0.15 ms of
+  // a small first job's wall time inline, ~2 ms over 200K entries); the next job takes it
+  // if it is ready and otherwise runs on what it has (the in-job plan, or the current map).
+  // The task holds the output buffer, which the pool then skips.
   void maybe_retune(const EntryList& e);
-  // A large output's map is built on a host thread (part_map_from_entries over 200K
-  // entries took ~2 ms of the first job's wall time); the next job takes it if it is ready
-  // and otherwise runs on what it has (the in-job plan, or the current map).  The task
-  // holds the output buffer, which the pool then skips.
   struct RetuneTask {
     u64 mx = 0, pred = 0;
     PartMapTables t;
+    std::shared_ptr<HostOut> hold;
+    EntryList entries;
   };
-  std::future<RetuneTask> retune_job;
-  void retune_async(u64 mx, const EntryList& e);
+  RetuneTask retune_task;
+  bool retune_pending = false;  // a task was handed to the worker and not adopted yet
+  TaskWorker retune_worker;
   // Before a job: adopt a finished background retune (never waits).
   void poll_retune();
   // The same when the sorted output is device KeyCount records (the distributed map): one

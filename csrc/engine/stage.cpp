@@ -1,0 +1,228 @@
+// Reduce side of the stage split (see locust/stage.hpp).
+#include "locust/stage.hpp"
+
+#include <algorithm>
+#include <queue>
+
+namespace locust {
+
+void combine_adjacent(std::vector<KeyCount>* recs) {
+  std::vector<KeyCount>& v = *recs;
+  size_t o = 0;
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (o && key_compare(v[o - 1].w, v[i].w) == 0)
+      v[o - 1].count += v[i].count;
+    else
+      v[o++] = v[i];
+  }
+  v.resize(o);
+}
+
+void sort_combine(std::vector<KeyCount>* recs) {
+  std::sort(recs->begin(), recs->end(), record_less);
+  combine_adjacent(recs);
+}
+
+std::vector<WordCountEntry> merge_runs_host(const std::vector<std::vector<KeyCount>>& runs) {
+  struct Head {
+    const KeyCount* p;
+    const KeyCount* end;
+  };
+  auto later = [](const Head& a, const Head& b) { return key_compare(a.p->w, b.p->w) > 0; };
+  std::priority_queue<Head, std::vector<Head>, decltype(later)> q(later);
+  size_t total = 0;
+  for (const auto& r : runs) {
+    total += r.size();
+    if (!r.empty()) q.push({r.data(), r.data() + r.size()});
+  }
+  std::vector<WordCountEntry> out;
+  out.reserve(total);
+  while (!q.empty()) {
+    Head h = q.top();
+    q.pop();
+    if (!out.empty() && key_compare(out.back().key.w, h.p->w) == 0) {
+      out.back().count += h.p->count;
+    } else {
+      WordCountEntry e;
+      for (int w = 0; w < kKeyWords; ++w) e.key.w[w] = h.p->w[w];
+      e.count = h.p->count;
+      out.push_back(e);
+    }
+    if (++h.p != h.end) q.push(h);
+  }
+  return out;
+}
+
+SpillIndex index_records(const std::vector<KeyCount>& recs) {
+  SpillIndex idx;
+  idx.sorted = idx.distinct = true;
+  idx.records = recs.size();
+  idx.stride = std::max<u64>(16, div_up(recs.size(), 256));
+  u64 cum = 0;
+  for (u64 i = 0; i < recs.size(); ++i) {
+    if (i % idx.stride == 0) {
+      SpillSample s;
+      for (int w = 0; w < kKeyWords; ++w) s.key.w[w] = recs[i].w[w];
+      s.record = i;
+      s.offset = i;  // in-memory: the record number
+      s.count_before = cum;
+      idx.samples.push_back(s);
+    }
+    cum += recs[i].count;
+  }
+  idx.total_count = cum;
+  return idx;
+}
+
+std::vector<PackedKey> plan_reducer_splitters(const std::vector<SpillIndex>& idx, int reducers) {
+  LOCUST_CHECK_ARG(reducers >= 1, "reducers must be >= 1");
+  struct W {
+    PackedKey key;
+    u64 weight;
+  };
+  std::vector<W> all;
+  u64 total = 0;
+  for (const SpillIndex& x : idx)
+    for (size_t j = 0; j < x.samples.size(); ++j) {
+      const u64 next = j + 1 < x.samples.size() ? x.samples[j + 1].record : x.records;
+      const u64 wgt = next > x.samples[j].record ? next - x.samples[j].record : 1;
+      all.push_back({x.samples[j].key, wgt});
+      total += wgt;
+    }
+  std::sort(all.begin(), all.end(),
+            [](const W& a, const W& b) { return key_compare(a.key.w, b.key.w) < 0; });
+  // Splitter i is the first sample key at which the weight of the samples BEFORE it
+  // reaches i/R of the total: equal keys are one unit, so the cut does not depend on the
+  // order of the indexes.  An empty or tiny input repeats its last key (empty ranges).
+  std::vector<PackedKey> spl;
+  u64 before = 0;
+  size_t j = 0;
+  for (int i = 1; i < reducers; ++i) {
+    const long double target = (long double)total * i / reducers;
+    while (j < all.size() && (long double)before < target) {
+      const size_t k0 = j;
+      while (j < all.size() && key_compare(all[j].key.w, all[k0].key.w) == 0) before += all[j++].weight;
+    }
+    PackedKey k{};
+    if (j < all.size()) {
+      k = all[j].key;
+    } else {
+      for (int w = 0; w < kKeyWords; ++w) k.w[w] = ~0ull;  // beyond every key
+    }
+    spl.push_back(k);
+  }
+  return spl;
+}
+
+namespace {
+
+// [lo, hi) membership; a null bound is open.
+bool below(const u64* k, const PackedKey* lo) { return lo && key_compare(k, lo->w) < 0; }
+bool at_or_above(const u64* k, const PackedKey* hi) { return hi && key_compare(k, hi->w) >= 0; }
+
+}  // namespace
+
+WordCountResult reduce_spills(const JobConfig& cfg, const std::vector<std::string>& files,
+                              int reducer, int reducers, ReduceStageStats* stats) {
+  LOCUST_CHECK_ARG(reducers >= 1 && reducer >= 0 && reducer < reducers,
+                   "--reducer r/R needs 0 <= r < R");
+  LOCUST_CHECK_ARG(!files.empty(), "no spill files to reduce");
+  ReduceStageStats st;
+  st.input_files = files.size();
+  const u64 t0 = now_ns();
+  const size_t nf = files.size();
+  std::vector<SpillIndex> idx(nf);
+  std::vector<char> indexed(nf, 0);
+  std::vector<std::vector<KeyCount>> loaded(nf);
+  for (size_t k = 0; k < nf; ++k) {
+    if (read_spill_index(files[k], &idx[k]) && idx[k].sorted) {
+      indexed[k] = 1;
+      ++st.indexed_files;
+      continue;
+    }
+    // no (current) index: the whole spill, sorted and combined here (a reference-format
+    // file: one "key \t1" line per token, sorted by one mapper only -- B7)
+    loaded[k] = read_spill(files[k]);
+    st.records_read += loaded[k].size();
+    bool sorted = true;
+    for (size_t i = 1; i < loaded[k].size() && sorted; ++i)
+      sorted = key_compare(loaded[k][i - 1].w, loaded[k][i].w) <= 0;
+    if (sorted)
+      combine_adjacent(&loaded[k]);
+    else
+      sort_combine(&loaded[k]);
+    idx[k] = index_records(loaded[k]);
+    ++st.loaded_files;
+  }
+  if (reducers > 1) st.splitters = plan_reducer_splitters(idx, reducers);
+  const PackedKey* lo = reducer > 0 ? &st.splitters[(size_t)reducer - 1] : nullptr;
+  const PackedKey* hi = reducer < reducers - 1 ? &st.splitters[(size_t)reducer] : nullptr;
+
+  u64 val_base = 0;
+  std::vector<std::vector<KeyCount>> runs;
+  runs.reserve(nf);
+  for (size_t k = 0; k < nf; ++k) {
+    std::vector<KeyCount> run;
+    if (!indexed[k]) {
+      for (const KeyCount& r : loaded[k]) {
+        if (below(r.w, lo))
+          val_base += r.count;
+        else if (at_or_above(r.w, hi))
+          break;
+        else
+          run.push_back(r);
+      }
+      std::vector<KeyCount>().swap(loaded[k]);
+    } else {
+      const SpillIndex& x = idx[k];
+      if (x.samples.empty()) continue;
+      // start at the last sample below the range (its count_before is exact)
+      size_t j = 0;
+      if (lo) {
+        const auto it = std::lower_bound(
+            x.samples.begin(), x.samples.end(), *lo,
+            [](const SpillSample& s, const PackedKey& key) { return key_compare(s.key.w, key.w) < 0; });
+        j = it == x.samples.begin() ? 0 : (size_t)(it - x.samples.begin()) - 1;
+      }
+      SpillReader rd(files[k]);
+      rd.seek(x.samples[j].offset);
+      u64 base = x.samples[j].count_before;
+      KeyCount r;
+      while (rd.next(&r)) {
+        ++st.records_read;
+        if (below(r.w, lo)) {
+          base += r.count;
+          continue;
+        }
+        if (at_or_above(r.w, hi)) break;
+        if (!run.empty() && key_compare(run.back().w, r.w) == 0)
+          run.back().count += r.count;  // a sorted but not combined spill
+        else
+          run.push_back(r);
+      }
+      val_base += base;
+    }
+    st.run_records += run.size();
+    if (!run.empty()) runs.push_back(std::move(run));
+  }
+  const u64 t1 = now_ns();
+  WordCountResult res;
+  std::vector<WordCountEntry> merged = cfg.backend == Backend::kCpu
+                                           ? merge_runs_host(runs)
+                                           : merge_runs_device(cfg, runs, &st.setup_ms);
+  const u64 t2 = now_ns();
+  res.val_base = val_base;
+  res.num_unique = merged.size();
+  for (const WordCountEntry& e : merged) res.num_tokens += e.count;
+  for (const WordCountEntry& e : merged)
+    res.max_key_len = std::max<u64>(res.max_key_len, key_bytes_used(e.key.w));
+  res.entries = std::move(merged);
+  st.read_ms = (t1 - t0) * 1e-6;
+  st.merge_ms = (t2 - t1) * 1e-6 - st.setup_ms;
+  res.times.reduce_ms = st.merge_ms;
+  res.times.wall_ms = (t2 - t0) * 1e-6;
+  if (stats) *stats = std::move(st);
+  return res;
+}
+
+}  // namespace locust

@@ -47,6 +47,16 @@ u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64
 LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
                             bool ref_compat);
 u64 count_lines(const char* data, u64 bytes);
+// The byte range [begin, end) of the line window [line_start, line_end) of a file (the
+// reference's per-node line ranges, main.cu:369-374) and its line count, found by a parallel
+// newline scan of the file up to the window's end in bounded memory (never the whole file
+// in memory).  line_end < 0: to the end of the file.
+struct LineWindow {
+  u64 begin = 0, end = 0;  // bytes
+  u64 lines = 0;           // lines in [begin, end) (a final line without '\n' counts)
+};
+LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_end,
+                            u32 threads = 0);
 
 // ---- spill files (map-output checkpoint) ----
 enum class SpillFormat { kText, kBinary, kKiv };
@@ -56,9 +66,57 @@ enum class SpillFormat { kText, kBinary, kKiv };
 // KeyValue.h:13-18: char key[30], int value @32, int count @36), after a 32-byte header
 // ("LCSTKIV1", version, record size 40, record count); a spill stores value = the
 // record's count and count = 0, as the reference's map emits (key, 1, 0).
-void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt);
+//
+// Stage 1 writes its COMBINED map output: one record per distinct key with its count, in
+// key order (the reference writes one "key \t1" line per token, main.cu:421-433; --ref-compat
+// keeps that).  Next to every spill it writes a sparse index, <spill>.idx: every stride-th
+// record's key, record number, byte offset and the token count of the records before it.
+// A reducer seeks with it to its key range and knows the count of every smaller key (its
+// global val base) without reading them; the samples also give the reducers' splitters.
+struct SpillSample {
+  PackedKey key;
+  u64 record = 0, offset = 0, count_before = 0;
+};
+struct SpillIndex {
+  bool sorted = false;     // keys never decrease
+  bool distinct = false;   // and never repeat
+  u64 records = 0, total_count = 0;
+  u64 spill_bytes = 0;     // size of the spill it describes (a stale index is ignored)
+  u64 stride = 1;
+  std::vector<SpillSample> samples;  // samples[0] is record 0
+};
+// Writes the spill; with idx, also fills it (the caller writes it with write_spill_index).
+void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt,
+                 SpillIndex* idx = nullptr);
+std::string spill_index_path(const std::string& spill);
+void write_spill_index(const std::string& path, const SpillIndex& idx);
+// False when absent, unreadable or not matching the spill's current size.
+bool read_spill_index(const std::string& spill, SpillIndex* idx);
 // Reads any of the three (detected by magic).  Text keys lose the writer's trailing space.
 std::vector<KeyCount> read_spill(const std::string& path);
+// Sequential reader of any spill format from a record's byte offset (an index sample's).
+class SpillReader {
+ public:
+  explicit SpillReader(const std::string& path);
+  ~SpillReader();
+  SpillReader(const SpillReader&) = delete;
+  SpillReader& operator=(const SpillReader&) = delete;
+  SpillFormat format() const { return fmt_; }
+  u64 first_record_offset() const { return first_; }
+  u64 bytes() const { return size_; }
+  void seek(u64 offset);
+  // The next record and its byte offset; false at the end.
+  bool next(KeyCount* rec, u64* offset = nullptr);
+
+ private:
+  bool fill();
+  std::string path_;
+  std::FILE* f_ = nullptr;
+  SpillFormat fmt_ = SpillFormat::kText;
+  u64 size_ = 0, first_ = 0, pos_ = 0;  // pos_: file offset of buf_[at_]
+  std::vector<char> buf_;
+  size_t at_ = 0, len_ = 0;
+};
 // Final (key, val, count) results as KeyIntValuePair records (value = val), the reference's
 // reduce output array (main.cu:470-473); the same header.  Values past INT_MAX and keys
 // past 29 bytes are refused.
@@ -70,7 +128,10 @@ struct KivRecord {
 };
 std::vector<KivRecord> read_kiv(const std::string& path);
 std::vector<KeyCount> tokens_to_records(const std::vector<PackedKey>& toks);
-std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs);
+std::vector<KeyCount> entries_to_records(const EntryList& e);
+
+// Records in packed-key order (== the reference's unsigned byte order, KeyValue.h:23-28).
+inline bool record_less(const KeyCount& a, const KeyCount& b) { return key_compare(a.w, b.w) < 0; }
 
 // ---- output ----
 // GPU build format (main.cu:132): "print key: %s \t val: %d \t count: %d\n".

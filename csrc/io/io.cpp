@@ -340,6 +340,85 @@ u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64
 
 u64 file_size(const std::string& path) { return Fd(path).size(); }
 
+LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_end, u32 threads) {
+  Fd f(path);
+  const u64 n = f.size();
+  const u64 s = (u64)std::max<i64>(line_start, 0);
+  const bool open_end = line_end < 0;
+  const u64 e = open_end ? ~0ull : std::max<u64>((u64)line_end, s);
+  constexpr u64 kNone = ~0ull;
+  // Line k starts after the k-th '\n' (line 0 at byte 0): find the starts of lines s and e.
+  u64 at[2] = {s == 0 ? 0 : kNone, open_end ? kNone : (e == 0 ? 0 : kNone)};
+  const u64 want[2] = {s, e};
+  const u32 T = std::max<u32>(1, io_threads(threads, n));
+  const u64 B = 8ull << 20;  // bytes per thread and round: T x 8 MiB in memory at most
+  std::vector<std::vector<char>> buf(T, std::vector<char>(B));
+  std::vector<u64> nls(T), got(T);
+  std::vector<char> ok(T, 1);
+  u64 seen = 0;      // newlines before the current block
+  u64 after_nl = 0;  // offset just after the last newline seen
+  u64 base = 0;
+  auto done = [&] { return at[0] != kNone && (open_end ? false : at[1] != kNone); };
+  while (base < n && !done()) {
+    auto work = [&](u32 t) {
+      const u64 a = base + (u64)t * B;
+      got[t] = a < n ? std::min<u64>(B, n - a) : 0;
+      nls[t] = 0;
+      if (got[t]) ok[t] = pread_slice(f.fd, buf[t].data(), a, 0, got[t], true, &nls[t]);
+    };
+    if (T == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (u32 t = 1; t < T; ++t) th.emplace_back(work, t);
+      work(0);
+      for (auto& x : th) x.join();
+    }
+    for (u32 t = 0; t < T && got[t]; ++t) {
+      if (!ok[t]) throw Error("short read: " + path);
+      const char* blk = buf[t].data();
+      const u64 blk_off = base + (u64)t * B;
+      for (int k = 0; k < 2; ++k) {
+        if (at[k] != kNone || (k == 1 && open_end) || seen + nls[t] < want[k]) continue;
+        const char* p = blk;  // the (want - seen)-th newline of this block ends line want - 1
+        for (u64 left = want[k] - seen;; --left) {
+          const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(blk + got[t] - p)));
+          if (left == 1) {
+            at[k] = blk_off + (u64)(nl - blk) + 1;
+            break;
+          }
+          p = nl + 1;
+        }
+      }
+      if (nls[t]) {
+        const void* r = memrchr(blk, '\n', (size_t)got[t]);
+        after_nl = blk_off + (u64)(static_cast<const char*>(r) - blk) + 1;
+      }
+      seen += nls[t];
+    }
+    base += (u64)T * B;
+  }
+  LineWindow w;
+  if (at[0] != kNone && at[1] != kNone && !open_end) {
+    w.begin = at[0];
+    w.end = std::max(at[0], at[1]);
+    w.lines = e - s;
+    return w;
+  }
+  // the scan reached EOF: `seen` newlines, plus a final line without one when the last
+  // byte is not a newline (it starts at after_nl)
+  const bool unterminated = n > after_nl;
+  const u64 total = seen + (unterminated ? 1 : 0);
+  if (s >= total) {
+    w.begin = w.end = n;
+    return w;
+  }
+  w.begin = at[0] != kNone ? at[0] : after_nl;  // (only line s == seen can be unfound)
+  w.end = n;
+  w.lines = std::min(total, e) - s;
+  return w;
+}
+
 u64 read_file_into(const std::string& path, char* dst, u64 cap, u64* lines, u32 threads) {
   Fd f(path);
   const u64 n = f.size();
@@ -519,91 +598,303 @@ std::vector<KivRecord> read_kiv(const std::string& path) {
   return out;
 }
 
-void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt) {
+namespace {
+constexpr char kIdxMagic[8] = {'L', 'C', 'S', 'T', 'I', 'D', 'X', '1'};
+constexpr u64 kIndexSamples = 256;  // samples per spill (<= 16 KiB of index), every >= 16th record
+struct IndexHeader {
+  char magic[8];
+  u32 version, flags;  // flags: 1 sorted, 2 distinct
+  u64 records, total_count, spill_bytes, nsamples, stride, reserved;
+};
+static_assert(sizeof(IndexHeader) == 64, "index header 64 B");
+struct IndexRecord {
+  u64 key[kKeyWords];
+  u64 record, offset, count_before, reserved;
+};
+static_assert(sizeof(IndexRecord) == 64, "index record 64 B");
+
+// Index bookkeeping while a spill is written record by record.
+struct IndexBuilder {
+  SpillIndex* idx;
+  const KeyCount* prev = nullptr;
+  u64 i = 0, cum = 0;
+  IndexBuilder(SpillIndex* x, u64 n) : idx(x) {
+    if (!idx) return;
+    *idx = SpillIndex();
+    idx->sorted = idx->distinct = true;
+    idx->records = n;
+    idx->stride = std::max<u64>(16, div_up(n, kIndexSamples));
+  }
+  void add(const KeyCount& r, u64 offset) {
+    if (!idx) return;
+    if (prev) {
+      const int c = key_compare(prev->w, r.w);
+      if (c > 0) idx->sorted = idx->distinct = false;
+      if (c == 0) idx->distinct = false;
+    }
+    if (i % idx->stride == 0) {
+      SpillSample smp;
+      for (int w = 0; w < kKeyWords; ++w) smp.key.w[w] = r.w[w];
+      smp.record = i;
+      smp.offset = offset;
+      smp.count_before = cum;
+      idx->samples.push_back(smp);
+    }
+    cum += r.count;
+    prev = &r;
+    ++i;
+  }
+  void finish(u64 bytes) {
+    if (!idx) return;
+    idx->records = i;
+    idx->total_count = cum;
+    idx->spill_bytes = bytes;
+  }
+};
+}  // namespace
+
+void write_spill(const std::string& path, const std::vector<KeyCount>& recs, SpillFormat fmt,
+                 SpillIndex* idx) {
+  std::vector<KeyCount> live;  // the reference skips empty keys (main.cu:118)
+  const std::vector<KeyCount>* src = &recs;
+  for (const auto& r : recs)
+    if (!r.w[0]) {
+      live.reserve(recs.size());
+      for (const auto& x : recs)
+        if (x.w[0]) live.push_back(x);
+      src = &live;
+      break;
+    }
+  IndexBuilder ib(idx, src->size());
   if (fmt == SpillFormat::kKiv) {
     std::vector<KeyIntValuePair> v;
-    v.reserve(recs.size());
-    for (const auto& r : recs)
-      if (r.w[0]) v.push_back(to_kiv(r.w, (i64)r.count, 0, path));
+    v.reserve(src->size());
+    u64 off = sizeof(SpillHeader);
+    for (const auto& r : *src) {
+      v.push_back(to_kiv(r.w, (i64)r.count, 0, path));
+      ib.add(r, off);
+      off += sizeof(KeyIntValuePair);
+    }
     write_kiv_file(path, v);
+    ib.finish(off);
     return;
   }
   std::FILE* f = std::fopen(path.c_str(), "wb");
   if (!f) throw Error("cannot write spill file: " + path);
+  u64 bytes = 0;
   if (fmt == SpillFormat::kBinary) {
     SpillHeader h{};
     std::memcpy(h.magic, kMagic, 8);
     h.version = 1;
     h.key_words = kKeyWords;
-    h.count = recs.size();
+    h.count = src->size();
     std::fwrite(&h, sizeof(h), 1, f);
-    if (!recs.empty()) std::fwrite(recs.data(), sizeof(KeyCount), recs.size(), f);
+    if (!src->empty()) std::fwrite(src->data(), sizeof(KeyCount), src->size(), f);
+    bytes = sizeof(h);
+    for (const auto& r : *src) {
+      ib.add(r, bytes);
+      bytes += sizeof(KeyCount);
+    }
   } else {
     std::string s;
-    s.reserve(recs.size() * 12);
+    s.reserve(std::min<size_t>(src->size(), 1u << 20) * 16);
     char buf[kKeyBytes + 1];
-    for (const auto& r : recs) {
-      int n = unpack_key(r.w, buf);
-      if (n == 0) continue;  // the reference skips empty keys (main.cu:118)
+    for (const auto& r : *src) {
+      ib.add(r, bytes + s.size());
+      const int n = unpack_key(r.w, buf);
       s.append(buf, (size_t)n);
       s.append(" \t");
       append_u64(&s, r.count);
       s.push_back('\n');
+      if (s.size() >= (8u << 20)) {  // bounded buffer: spills of any size
+        write_all(f, s);
+        bytes += s.size();
+        s.clear();
+      }
     }
     write_all(f, s);
+    bytes += s.size();
   }
   if (std::fclose(f) != 0) throw Error("error closing spill file: " + path);
+  ib.finish(bytes);
+}
+
+std::string spill_index_path(const std::string& spill) { return spill + ".idx"; }
+
+void write_spill_index(const std::string& path, const SpillIndex& idx) {
+  std::FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw Error("cannot write spill index: " + path);
+  IndexHeader h{};
+  std::memcpy(h.magic, kIdxMagic, 8);
+  h.version = 1;
+  h.flags = (idx.sorted ? 1u : 0u) | (idx.distinct ? 2u : 0u);
+  h.records = idx.records;
+  h.total_count = idx.total_count;
+  h.spill_bytes = idx.spill_bytes;
+  h.nsamples = idx.samples.size();
+  h.stride = idx.stride;
+  std::fwrite(&h, sizeof(h), 1, f);
+  for (const SpillSample& x : idx.samples) {
+    IndexRecord r{};
+    for (int w = 0; w < kKeyWords; ++w) r.key[w] = x.key.w[w];
+    r.record = x.record;
+    r.offset = x.offset;
+    r.count_before = x.count_before;
+    std::fwrite(&r, sizeof(r), 1, f);
+  }
+  if (std::fclose(f) != 0) throw Error("error closing spill index: " + path);
+}
+
+bool read_spill_index(const std::string& spill, SpillIndex* idx) {
+  std::FILE* f = std::fopen(spill_index_path(spill).c_str(), "rb");
+  if (!f) return false;
+  IndexHeader h{};
+  bool ok = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, kIdxMagic, 8) == 0 &&
+            h.version == 1 && h.nsamples <= (1u << 24) && h.stride >= 1;
+  std::vector<IndexRecord> v(ok ? h.nsamples : 0);
+  ok = ok && (v.empty() || std::fread(v.data(), sizeof(IndexRecord), v.size(), f) == v.size());
+  std::fclose(f);
+  u64 size = 0;
+  try {
+    size = file_size(spill);
+  } catch (const std::exception&) {
+    return false;
+  }
+  if (!ok || size != h.spill_bytes) return false;  // absent, damaged or stale
+  *idx = SpillIndex();
+  idx->sorted = (h.flags & 1u) != 0;
+  idx->distinct = (h.flags & 2u) != 0;
+  idx->records = h.records;
+  idx->total_count = h.total_count;
+  idx->spill_bytes = h.spill_bytes;
+  idx->stride = h.stride;
+  idx->samples.resize(v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    for (int w = 0; w < kKeyWords; ++w) idx->samples[i].key.w[w] = v[i].key[w];
+    idx->samples[i].record = v[i].record;
+    idx->samples[i].offset = v[i].offset;
+    idx->samples[i].count_before = v[i].count_before;
+  }
+  return true;
+}
+
+SpillReader::SpillReader(const std::string& path) : path_(path), buf_(1u << 20) {
+  f_ = std::fopen(path.c_str(), "rb");
+  if (!f_) throw Error("cannot open spill file: " + path);
+  size_ = file_size(path);
+  char m[sizeof(SpillHeader)] = {};
+  const size_t got = std::fread(m, 1, sizeof(m), f_);
+  if (got == sizeof(SpillHeader) && std::memcmp(m, kKivMagic, 8) == 0) {
+    SpillHeader h;
+    std::memcpy(&h, m, sizeof(h));
+    if (h.version != 1 || h.key_words != sizeof(KeyIntValuePair))
+      throw Error("not a kiv file: " + path);
+    if (size_ < sizeof(h) + h.count * sizeof(KeyIntValuePair)) throw Error("truncated kiv file: " + path);
+    fmt_ = SpillFormat::kKiv;
+    first_ = sizeof(h);
+    size_ = sizeof(h) + h.count * sizeof(KeyIntValuePair);
+  } else if (got == sizeof(SpillHeader) && std::memcmp(m, kMagic, 8) == 0) {
+    SpillHeader h;
+    std::memcpy(&h, m, sizeof(h));
+    if (h.version != 1 || h.key_words != kKeyWords) throw Error("unsupported spill file: " + path);
+    if (size_ < sizeof(h) + h.count * sizeof(KeyCount)) throw Error("truncated spill: " + path);
+    fmt_ = SpillFormat::kBinary;
+    first_ = sizeof(h);
+    size_ = sizeof(h) + h.count * sizeof(KeyCount);
+  } else {
+    fmt_ = SpillFormat::kText;
+    first_ = 0;
+  }
+  seek(first_);
+}
+
+SpillReader::~SpillReader() {
+  if (f_) std::fclose(f_);
+}
+
+void SpillReader::seek(u64 offset) {
+  LOCUST_CHECK_ARG(offset >= first_ && offset <= size_, "spill offset out of range: " + path_);
+  if (std::fseek(f_, (long)offset, SEEK_SET) != 0) throw Error("cannot seek in " + path_);
+  pos_ = offset;
+  at_ = len_ = 0;
+}
+
+bool SpillReader::fill() {  // keeps the unread tail, appends the next read
+  if (at_ > 0) {
+    std::memmove(buf_.data(), buf_.data() + at_, len_ - at_);
+    pos_ += at_;
+    len_ -= at_;
+    at_ = 0;
+  }
+  if (len_ == buf_.size()) buf_.resize(buf_.size() * 2);  // a text line longer than the buffer
+  const u64 end_of_data = size_;
+  const u64 file_at = pos_ + len_;
+  if (file_at >= end_of_data) return false;
+  const size_t want = (size_t)std::min<u64>(buf_.size() - len_, end_of_data - file_at);
+  const size_t k = std::fread(buf_.data() + len_, 1, want, f_);
+  if (k == 0) throw Error("short read: " + path_);
+  len_ += k;
+  return true;
+}
+
+bool SpillReader::next(KeyCount* rec, u64* offset) {
+  if (fmt_ != SpillFormat::kText) {
+    const size_t rs = 40;
+    while (len_ - at_ < rs)
+      if (!fill()) {
+        if (len_ != at_) throw Error("truncated spill: " + path_);
+        return false;
+      }
+    if (offset) *offset = pos_ + at_;
+    const char* p = buf_.data() + at_;
+    if (fmt_ == SpillFormat::kBinary) {
+      std::memcpy(rec, p, sizeof(KeyCount));
+    } else {
+      KeyIntValuePair k;
+      std::memcpy(&k, p, sizeof(k));
+      pack_key(k.key, (int)strnlen(k.key, sizeof(k.key)), rec->w);  // bounded (B11)
+      if (k.value < 0) throw Error("negative count in kiv spill: " + path_);
+      rec->count = (u64)k.value;  // value = the record's count (map output)
+    }
+    at_ += rs;
+    return true;
+  }
+  // text: "<key> \t<count>\n"; the reference's key keeps a trailing space (B8: stripped)
+  for (;;) {
+    const char* p = buf_.data() + at_;
+    const char* e = buf_.data() + len_;
+    const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p)));
+    if (!nl && fill()) continue;
+    if (!nl) nl = e;  // a final line without '\n'
+    if (nl == p) {
+      if (p == e) return false;
+      ++at_;  // an empty line
+      continue;
+    }
+    if (offset) *offset = pos_ + at_;
+    const char* tab = static_cast<const char*>(memchr(p, '\t', (size_t)(nl - p)));
+    const char* key_end = tab ? tab : nl;
+    if (key_end > p && key_end[-1] == ' ') --key_end;
+    pack_key(p, (int)(key_end - p), rec->w);
+    u64 cnt = 1;
+    if (tab) {
+      cnt = 0;
+      const char* q = tab + 1;
+      while (q < nl && (*q == ' ' || *q == '\t')) ++q;
+      for (; q < nl && *q >= '0' && *q <= '9'; ++q) cnt = cnt * 10 + (u64)(*q - '0');
+    }
+    rec->count = cnt;
+    at_ = (size_t)(nl - buf_.data()) + (nl < e ? 1 : 0);
+    return true;
+  }
 }
 
 std::vector<KeyCount> read_spill(const std::string& path) {
-  std::FILE* f = std::fopen(path.c_str(), "rb");
-  if (!f) throw Error("cannot open spill file: " + path);
-  std::fseek(f, 0, SEEK_END);
-  long sz = std::ftell(f);
-  std::fseek(f, 0, SEEK_SET);
-  std::string data((size_t)std::max<long>(sz, 0), '\0');
-  if (sz > 0 && std::fread(&data[0], 1, (size_t)sz, f) != (size_t)sz) {
-    std::fclose(f);
-    throw Error("short read: " + path);
-  }
-  std::fclose(f);
+  SpillReader rd(path);
   std::vector<KeyCount> recs;
-  if (data.size() >= sizeof(SpillHeader) && std::memcmp(data.data(), kKivMagic, 8) == 0) {
-    for (const auto& k : read_kiv(path)) {  // value = the record's count (map output)
-      KeyCount r{};
-      for (int w = 0; w < kKeyWords; ++w) r.w[w] = k.key.w[w];
-      if (k.value < 0) throw Error("negative count in kiv spill: " + path);
-      r.count = (u64)k.value;
-      recs.push_back(r);
-    }
-    return recs;
-  }
-  if (data.size() >= sizeof(SpillHeader) && std::memcmp(data.data(), kMagic, 8) == 0) {
-    SpillHeader h;
-    std::memcpy(&h, data.data(), sizeof(h));
-    if (h.version != 1 || h.key_words != kKeyWords) throw Error("unsupported spill file: " + path);
-    if (data.size() < sizeof(h) + h.count * sizeof(KeyCount)) throw Error("truncated spill: " + path);
-    recs.resize(h.count);
-    if (h.count) std::memcpy(recs.data(), data.data() + sizeof(h), h.count * sizeof(KeyCount));
-    return recs;
-  }
-  // text format: "<key> \t<count>\n"
-  size_t p = 0;
-  while (p < data.size()) {
-    size_t nl = data.find('\n', p);
-    if (nl == std::string::npos) nl = data.size();
-    std::string line = data.substr(p, nl - p);
-    p = nl + 1;
-    if (line.empty()) continue;
-    size_t tab = line.find('\t');
-    std::string key = tab == std::string::npos ? line : line.substr(0, tab);
-    if (!key.empty() && key.back() == ' ') key.pop_back();  // B8 fix
-    const u64 cnt = tab == std::string::npos ? 1 : std::strtoull(line.c_str() + tab + 1, nullptr, 10);
-    KeyCount r{};
-    pack_key(key.data(), (int)key.size(), r.w);
-    r.count = cnt;
-    recs.push_back(r);
-  }
+  if (rd.format() != SpillFormat::kText) recs.reserve((rd.bytes() - rd.first_record_offset()) / 40);
+  KeyCount r;
+  while (rd.next(&r)) recs.push_back(r);
   return recs;
 }
 
@@ -616,15 +907,16 @@ std::vector<KeyCount> tokens_to_records(const std::vector<PackedKey>& toks) {
   return recs;
 }
 
-std::vector<PackedKey> records_to_tokens(const std::vector<KeyCount>& recs) {
-  std::vector<PackedKey> toks;
-  toks.reserve(recs.size());
-  for (const auto& r : recs) {
-    PackedKey k;
-    for (int w = 0; w < kKeyWords; ++w) k.w[w] = r.w[w];
-    for (u64 c = 0; c < r.count; ++c) toks.push_back(k);
+std::vector<KeyCount> entries_to_records(const EntryList& e) {
+  std::vector<KeyCount> recs;
+  recs.reserve(e.size());
+  for (const WordCountEntry x : e) {
+    KeyCount r;
+    for (int w = 0; w < kKeyWords; ++w) r.w[w] = x.key.w[w];
+    r.count = x.count;
+    recs.push_back(r);
   }
-  return toks;
+  return recs;
 }
 
 // ---------------- output ----------------

@@ -16,6 +16,7 @@
 #include "locust/engine.hpp"
 #include "locust/gen.hpp"
 #include "locust/io.hpp"
+#include "locust/stage.hpp"
 #include "locust/numa.hpp"
 #include "locust/partmap.hpp"
 #include "locust/shm.hpp"
@@ -796,5 +797,60 @@ PYBIND11_MODULE(_locust, m) {
     }
     return out;
   });
+  m.def("find_line_window", [](const std::string& path, i64 s, i64 e) {
+    py::gil_scoped_release nogil;
+    const LineWindow w = find_line_window(path, s, e);
+    return std::make_tuple(w.begin, w.end, w.lines);
+  }, py::arg("path"), py::arg("line_start"), py::arg("line_end"),
+        "(begin, end, lines) of the line window [line_start, line_end) of a file");
+  m.def("spill_index", [](const std::string& spill) -> py::object {
+    SpillIndex x;
+    if (!read_spill_index(spill, &x)) return py::none();
+    py::dict d;
+    d["sorted"] = x.sorted;
+    d["distinct"] = x.distinct;
+    d["records"] = x.records;
+    d["total_count"] = x.total_count;
+    d["spill_bytes"] = x.spill_bytes;
+    d["stride"] = x.stride;
+    py::list smp;
+    for (const SpillSample& v : x.samples)
+      smp.append(py::make_tuple(py::bytes(key_to_string(v.key)), v.record, v.offset, v.count_before));
+    d["samples"] = smp;
+    return d;
+  }, py::arg("spill"), "The spill's sparse index (<spill>.idx), or None.");
+  m.def("reducer_splitters", [](const std::vector<std::string>& spills, int reducers) {
+    std::vector<SpillIndex> idx(spills.size());
+    for (size_t k = 0; k < spills.size(); ++k) {
+      if (!read_spill_index(spills[k], &idx[k])) {
+        std::vector<KeyCount> v = read_spill(spills[k]);
+        sort_combine(&v);
+        idx[k] = index_records(v);
+      }
+    }
+    py::list out;
+    for (const PackedKey& k : plan_reducer_splitters(idx, reducers)) out.append(py::bytes(key_to_string(k)));
+    return out;
+  }, py::arg("spills"), py::arg("reducers"));
+  m.def("reduce_spills", [](const JobConfig& cfg, const std::vector<std::string>& files, int reducer,
+                           int reducers) {
+    ReduceStageStats st;
+    WordCountResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = reduce_spills(cfg, files, reducer, reducers, &st);
+    }
+    py::dict d;
+    d["input_files"] = st.input_files;
+    d["indexed_files"] = st.indexed_files;
+    d["loaded_files"] = st.loaded_files;
+    d["records_read"] = st.records_read;
+    d["run_records"] = st.run_records;
+    d["read_ms"] = st.read_ms;
+    d["setup_ms"] = st.setup_ms;
+    d["merge_ms"] = st.merge_ms;
+    return py::make_tuple(PyResult{std::move(r)}, d);
+  }, py::arg("cfg"), py::arg("files"), py::arg("reducer") = 0, py::arg("reducers") = 1,
+        "Stage 2 over spill files: (result, stats); key range `reducer` of `reducers`.");
   py::register_exception<Error>(m, "LocustError");
 }

@@ -1,7 +1,7 @@
 """One process of tests/test_switches.py: runs a fixed set of WordCount jobs under the
 LOCUST_* environment it was started with and checks every result against the oracle.
 
-    python tests/switch_worker.py single|stream|dist
+    python tests/switch_worker.py single|stream|dist|merge
 
 Exit status 0 = every job matched; the failure is printed otherwise.  A separate process
 per setting because many switches are read once per process (or per engine)."""
@@ -41,6 +41,26 @@ def main(kind: str) -> None:
             for strategy in ("shuffle", "auto"):
                 res = lc.run_multi(synth, world, strategy=strategy, comm="loopback")
                 check(res, synth, f"loopback {world} {strategy}")
+    elif kind == "merge":
+        # stage 2 on the device over 70 spills (rounds of 64 runs) of the synthetic text's
+        # line windows; a low LOCUST_MERGE_MAX_RECORDS also splits merges by key range
+        import tempfile
+
+        lines = synth.split(b"\n")
+        with tempfile.TemporaryDirectory() as d:
+            files = []
+            for k in range(70):
+                part = b"\n".join(lines[k::70]) + b"\n"
+                recs = [(key, c) for key, _v, c in oracle.wordcount(part)[0]]
+                files.append(os.path.join(d, f"out.{k}.kv"))
+                lc._C.write_spill(files[-1], recs, "binary")
+            for reducers in (1, 3):
+                got = []
+                for r in range(reducers):
+                    res, _st = lc._C.reduce_spills(lc.make_config("gpu"), files, r, reducers)
+                    got += res.entries()
+                ent = oracle.wordcount(synth)[0]
+                assert got == ent, f"device merge of 70 spills, {reducers} reducers"
     else:
         raise SystemExit(f"unknown kind {kind}")
     print("switch worker ok:", kind, {k: v for k, v in os.environ.items()

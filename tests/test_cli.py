@@ -47,8 +47,14 @@ def test_stage_split_cpu(cli, hamlet, tmp_path):
 def test_spill_text_format(cli, tmp_path):
     (tmp_path / "in.txt").write_bytes(b"b a b\n")
     run(cli, tmp_path / "in.txt", 0, 1, 3, 1, "--backend", "cpu", "--spill-dir", tmp_path)
-    # reference writer format "%s \t%d\n" (main.cu:121), sorted
-    assert (tmp_path / "out.3.txt").read_bytes() == b"a \t1\nb \t1\nb \t1\n"
+    # the reference writer's format "%s \t%d\n" (main.cu:121), combined: one line per key
+    assert (tmp_path / "out.3.txt").read_bytes() == b"a \t1\nb \t2\n"
+    # --ref-compat: the reference's own spill, one line per token, sorted (the CPU build
+    # loads the whole file and drops its last line, B1)
+    (tmp_path / "in.txt").write_bytes(b"b a b\nlast\n")
+    run(cli, tmp_path / "in.txt", 0, 1, 4, 1, "--backend", "cpu", "--spill-dir", tmp_path,
+        "--ref-compat")
+    assert (tmp_path / "out.4.txt").read_bytes() == b"a \t1\nb \t1\nb \t1\n"
 
 
 def test_multi_rank_cpu_cli(cli, hamlet):
@@ -74,9 +80,11 @@ def test_json_in_every_mode(tmp_path, cli):
     full = run()
     assert full["mode"] == "full" and full["unique"] == 5608 and full["tokens"] == 32940
     m = run("0", "700", "0", "1", "--spill-dir", str(tmp_path))
-    assert m["mode"] == "map_stage" and m["tokens"] == 4896 and m["spill_records"] == 4896
+    assert m["mode"] == "map_stage" and m["tokens"] == 4896 and m["spill_records"] == 1566
+    assert m["combined"] is True and m["lines"] == 700
     r = run("0", "0", "0", "2", "--spill-dir", str(tmp_path))
-    assert r["mode"] == "reduce_stage" and r["unique"] == 1566 and r["input_records"] == 4896
+    assert r["mode"] == "reduce_stage" and r["unique"] == 1566 and r["input_records"] == 1566
+    assert r["tokens"] == 4896 and r["indexed_files"] == 1
     d = run("--gpus", "3")
     assert d["mode"] == "multi_gpu" and d["unique"] == 5608 and len(d["ranks"]) == 3
     for k, rk in enumerate(d["ranks"]):

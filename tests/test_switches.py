@@ -24,6 +24,7 @@ CASES = [
     ({"LOCUST_GRAPH": "0"}, "single"),
     ({"LOCUST_GRAPH": "1"}, "single"),
     ({"LOCUST_PIECE_MB": "4"}, "single"),
+    ({"LOCUST_MERGE_MAX_RECORDS": "100"}, "merge"),
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PART_DEFAULT": "byte"}, "single"),
     ({"LOCUST_VPLAN": "0", "LOCUST_DEVPLAN": "0"}, "single"),
     ({"LOCUST_VPLAN_MIN_KB": "64", "LOCUST_SPLIT_MIN": "256"}, "single"),

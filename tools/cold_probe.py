@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="synth1m")
     ap.add_argument("--engines", type=int, default=2)
+    ap.add_argument("--jobs", type=int, default=3)
     a = ap.parse_args()
     synth = a.config in bench.SYNTH
     text = bench.synth_shard(a.config, 0, 1) if synth else bench.load_text(a.config)
@@ -33,15 +34,17 @@ def main():
             e.load(text)
             run = e.run_loaded
         t1 = time.perf_counter()
-        walls = []
-        for _ in range(3):
+        walls, splits = [], []
+        for _ in range(a.jobs):
             s = time.perf_counter()
             r = run()
             walls.append((time.perf_counter() - s) * 1e3)
-        tm = {k2: round(v, 3) for k2, v in r.times().items() if isinstance(v, float)}
+            t = r.times()
+            splits.append("/".join(f"{t[x]:.3f}" for x in ("host_launch_ms", "host_wait_ms",
+                                                            "host_copy_ms")))
         print(f"engine {k}: ctor {(t1 - t0) * 1e3:.2f} ms, jobs "
               + " / ".join(f"{w:.3f}" for w in walls) + f" ms; unique {r.num_unique}; "
-              f"last job times {tm}", flush=True)
+              "launch/wait/copy per job: " + "  ".join(splits), flush=True)
 
 
 if __name__ == "__main__":
