@@ -537,7 +537,7 @@ def main() -> int:
                 f"{'1M lines' if args.config == 'synth1m' else f'{total_bytes / 1e9:.3g} GB'} in total, "
                 f"1/N per GPU generated into pinned host memory")
         model = (f"WordCount {args.config}: dictionary path, "
-                 + ("one pass, line-aligned upload pieces of up to 12 MiB, two-kernel ordered build"
+                 + ("one pass, line-aligned upload pieces of 10 MiB (LOCUST_PIECE_MB), two-kernel ordered build"
                     if nbytes <= CHUNK_BYTES else
                     f"streamed in {chunk_bytes_for(nbytes) >> 20} MiB chunks")
                  + ", full H2D->D2H job per step")

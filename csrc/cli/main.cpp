@@ -54,6 +54,7 @@ struct CliArgs {
   std::vector<std::string> inputs;
   int reducer = 0, reducers = 1;  // --reducer r/R: key range r of R (stage 2)
   std::string result_file;        // --result-file: the result lines go there, not stdout
+  int out_format = 0;             // --output-format: 0 by mode, 1 gpu (with val), 2 cpu
   int warmup = 0, iters = 1;
   std::string json;
   std::string export_kiv;  // final results as KeyIntValuePair records (--export-kiv FILE)
@@ -81,6 +82,7 @@ void help() {
       "  --emits-per-line N         --max-key N                --ref-compat\n"
       "  --stage map|reduce         --spill-dir DIR            --spill-format text|binary|kiv\n"
       "  --inputs a,b,...           --reducer r/R              --result-file FILE\n"
+      "  --output-format gpu|cpu    (result lines with val, or the CPU build's)\n"
       "  --export-kiv FILE          --json FILE|-              --quiet --check --combine\n"
       "  --warmup N --iters N       --chunk-mb N               --ref-timers\n"
       "  --help\n"
@@ -167,6 +169,10 @@ bool parse(int argc, char** argv, CliArgs* a) {
         throw Error("--reducer r/R needs 0 <= r < R");
     } else if (s == "--result-file") {
       a->result_file = need("--result-file");
+    } else if (s == "--output-format") {
+      const std::string v = need("--output-format");
+      if (v != "gpu" && v != "cpu") throw Error("--output-format gpu|cpu");
+      a->out_format = v == "gpu" ? 1 : 2;
     } else if (s == "--warmup") {
       a->warmup = std::atoi(need("--warmup").c_str());
     } else if (s == "--iters") {
@@ -336,6 +342,7 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
                     : root.strategy == DistStrategy::kLocal   ? "local"
                                                               : "shuffle");
   j.num("wall_ms", root.total_ms);
+  j.str("comm", !ranks.empty() && ranks[0].rccl_clique ? "rccl" : "loopback");
   j.u("peak_rss_kb", peak_rss_kb());
   std::string rk = "[";
   for (size_t r = 0; r < ranks.size(); ++r) {
@@ -405,6 +412,31 @@ int generate(const CliArgs& a) {
   return 0;
 }
 
+// The result lines: the GPU build's "print key: k \t val: v \t count: c" (main.cu:132) or
+// the CPU build's "print key: k \t value: c" (main.cu:286).  By default the backend's own
+// build -- except --gpus N, always the GPU build's (the multi-GPU mode; --backend cpu there
+// only rehearses its ranks, docs/PARITY.md) -- and --output-format overrides.
+void format_results(const CliArgs& a, bool cpu_default, const WordCountResult& r,
+                    std::string* out) {
+  if (a.quiet) return;
+  const bool cpu = a.out_format ? a.out_format == 2 : cpu_default;
+  (cpu ? format_cpu_output : format_gpu_output)(r, out);
+}
+
+// The result lines to stdout, or to --result-file (a range reducer on a worker daemon,
+// whose reply carries only the tail of stdout).
+void emit_results(const CliArgs& a, const std::string& out) {
+  if (a.result_file.empty()) {
+    std::fflush(stdout);
+    write_all(stdout, out);
+    return;
+  }
+  std::FILE* f = std::fopen(a.result_file.c_str(), "wb");
+  if (!f) throw Error("cannot write " + a.result_file);
+  write_all(f, out);
+  if (std::fclose(f) != 0) throw Error("error closing " + a.result_file);
+}
+
 void print_gpu_result(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
   const bool rt = a.cfg.ref_timers;
   std::printf("GPU mapping %lld nanoseconds \n", ns(rt ? r.times.ref_map_ms : r.times.map_ms));
@@ -416,9 +448,8 @@ void print_gpu_result(const CliArgs& a, const WordCountResult& r, const std::vec
     LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",
                     (unsigned long long)r.truncated, a.cfg.max_key_len);
   std::string out;
-  if (!a.quiet) format_gpu_output(r, &out);
-  std::fflush(stdout);
-  write_all(stdout, out);
+  format_results(a, false, r, &out);
+  emit_results(a, out);
   std::fflush(stdout);
   write_json(a, r, walls);
   if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r);
@@ -509,20 +540,6 @@ int run_direct(const CliArgs& a) {
   eng.reset();
   LOCUST_LOG_DEBUG("engine teardown %.3f ms", (now_ns() - t_down) * 1e-6);
   return 0;
-}
-
-// The result lines to stdout, or to --result-file (a range reducer on a worker daemon,
-// whose reply carries only the tail of stdout).
-void emit_results(const CliArgs& a, const std::string& out) {
-  if (a.result_file.empty()) {
-    std::fflush(stdout);
-    write_all(stdout, out);
-    return;
-  }
-  std::FILE* f = std::fopen(a.result_file.c_str(), "wb");
-  if (!f) throw Error("cannot write " + a.result_file);
-  write_all(f, out);
-  if (std::fclose(f) != 0) throw Error("error closing " + a.result_file);
 }
 
 // ---------------- stage 1: map only -> spill (main.cu:421-433) ----------------
@@ -634,7 +651,7 @@ int run_reduce_stage(const CliArgs& a) {
   WordCountResult r = reduce_spills(a.cfg, files, a.reducer, a.reducers, &st);
   std::printf("%s reduce %lld nanoseconds \n", cpu ? "CPU" : "GPU", ns(st.merge_ms));
   std::string out;
-  if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r, &out);
+  format_results(a, cpu, r, &out);
   emit_results(a, out);
   if (!a.json.empty()) {
     JsonOut j = json_head(a, "reduce_stage");
@@ -686,7 +703,10 @@ int run(const CliArgs& a) {
   // A whole file is never loaded: every rank reads only its own line-aligned byte range
   // (run_single_process_file); a line window is loaded first, then sharded.
   const bool multi = (a.gpus > 1 || (a.gpus_given && !cpu)) && a.stage == 0;
-  const bool file_ranks = multi && !use_window && !a.cfg.ref_compat;
+  // (the compat map sizes its slots per line: its ranks get the loaded text, whose line
+  // count is exact, not a file range sized by bytes)
+  const bool file_ranks = multi && !use_window && !a.cfg.ref_compat &&
+                          a.cfg.map_path != MapPath::kCompat;
   LoadedText text;
   if (!file_ranks) {
     text = load_lines(a.file, use_window ? a.line_start : -1, use_window ? a.line_end : -1,
@@ -701,21 +721,20 @@ int run(const CliArgs& a) {
     dc.job.combine = true;
     dc.world = std::max(1, a.gpus);
     dc.strategy = a.strategy;
-    LOCUST_LOG_INFO("%d ranks in one process over %s", dc.world,
-                    resolve_local_comm(dc, a.comm) == LocalComm::kRccl ? "an RCCL clique"
-                                                                       : "loopback");
     std::vector<DistResult> ranks;
     DistResult dr = file_ranks ? run_single_process_file(dc, a.file, a.comm, &ranks)
                                : run_single_process_multi_gpu(dc, text.input, a.comm, &ranks);
+    // the communicator the ranks actually used (a failed clique falls back to loopback)
+    LOCUST_LOG_INFO("%d ranks in one process over %s", dc.world,
+                    !ranks.empty() && ranks[0].rccl_clique ? "an RCCL clique" : "loopback");
     log_rss("after the job");
     if (file_ranks && !cpu) std::printf("Length: %i\n", (int)dr.result.num_lines);
     std::printf("%s mapping %lld nanoseconds \n", dev, ns(dr.map_ms));
     std::printf("%s stream compaction and sorting %lld nanoseconds \n", dev, ns(dr.shuffle_ms));
     std::printf("%s reduce %lld nanoseconds \n", dev, ns(dr.reduce_ms));
     std::string out;
-    if (!a.quiet) format_gpu_output(dr.result, &out);
-    std::fflush(stdout);
-    write_all(stdout, out);
+    format_results(a, false, dr.result, &out);
+    emit_results(a, out);
     write_json_dist(a, dr, ranks);
     std::printf("\nDone\n");
     return 0;
@@ -748,9 +767,8 @@ int run(const CliArgs& a) {
     LOCUST_LOG_WARN("%llu tokens longer than %d chars were truncated",
                     (unsigned long long)r.truncated, a.cfg.max_key_len);
   std::string out;
-  if (!a.quiet) (cpu ? format_cpu_output : format_gpu_output)(r, &out);
-  std::fflush(stdout);
-  write_all(stdout, out);
+  format_results(a, cpu, r, &out);
+  emit_results(a, out);
   write_json(a, r, walls);
   if (!a.export_kiv.empty()) write_kiv_results(a.export_kiv, r);
   std::printf("\nDone\n");

@@ -566,7 +566,7 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
         res.sent_bytes += res.sent_to[(size_t)p];
         res.recv_bytes += res.recv_from[(size_t)p];
       }
-      res.output_bytes = R[me].n_out * sizeof(WordCountEntry);
+      res.output_bytes = R[me].out_words * 8;  // compact records the emit wrote
       res.range_tokens = R[me].total;
       res.range_unique = R[me].n_out;
       res.strategy = to_root ? DistStrategy::kGather : DistStrategy::kShuffle;

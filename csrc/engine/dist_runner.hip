@@ -36,11 +36,24 @@ int visible_device_count() {
   return n;
 }
 
+// auto = loopback: ranks in one process exchange by peer-to-peer device copies over xGMI.
+// The RCCL clique (ncclCommInitAll + a driving thread per GPU) stays opt-in (--comm rccl)
+// until a run with real RCCL peers has been recorded; the benchmark's ranks are
+// separate processes on RCCL either way.
 LocalComm resolve_local_comm(const DistConfig& cfg, LocalComm comm) {
   if (cfg.job.backend != Backend::kGpu) return LocalComm::kLoopback;
-  if (comm != LocalComm::kAuto) return comm;
-  return cfg.world > 1 && cfg.job.device + cfg.world <= visible_device_count() ? LocalComm::kRccl
-                                                                                : LocalComm::kLoopback;
+  return comm == LocalComm::kAuto ? LocalComm::kLoopback : comm;
+}
+
+// Which ordered pairs of `devices` can access each other directly (queried, not enabled).
+static std::vector<int> query_peer_access(const std::vector<int>& devices) {
+  const size_t n = devices.size();
+  std::vector<int> m(n * n, 0);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j)
+      if (i != j && devices[i] != devices[j])
+        LOCUST_HIP_CHECK(hipDeviceCanAccessPeer(&m[i * n + j], devices[i], devices[j]));
+  return m;
 }
 
 std::vector<int> enable_peer_access(const std::vector<int>& devices) {
@@ -125,11 +138,12 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
   }
   // Peer access for the loopback data plane's device-to-device copies (RCCL sets up its own
   // transports): one enable per ordered pair of distinct devices, logged per pair.
+  // An RCCL clique reports the pairs that could access each other directly (its own
+  // transports decide what it uses).
   std::vector<int> p2p;
-  if (gpu && !rccl && devs.size() > 1) p2p = enable_peer_access(devs);
+  if (gpu && devs.size() > 1) p2p = rccl ? query_peer_access(devs) : enable_peer_access(devs);
   auto peers_of = [&](int dev) -> int {
-    if (devs.size() < 2) return -1;
-    if (p2p.empty()) return (int)devs.size() - 1;  // RCCL: its transports decide
+    if (devs.size() < 2 || p2p.empty()) return -1;
     const size_t n = devs.size();
     const size_t i = (size_t)(std::find(devs.begin(), devs.end(), dev) - devs.begin());
     int k = 0;
@@ -194,6 +208,7 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
           d.input_bytes = shard.bytes;
           d.input_streamed = shard.source != nullptr;
           d.peer_p2p = gpu ? peers_of(job.device) : -1;
+          d.rccl_clique = rccl;
           if (per_rank && j + 1 == schedule.size()) {  // the last job's stats (no entries)
             DistResult& pr = (*per_rank)[(size_t)r];
             pr = d;

@@ -313,7 +313,14 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   }
   // the retune worker of a small engine is made here, not inside its first job (a
   // streaming engine's jobs take hundreds of ms: it makes it when first needed)
-  if (!streaming) retune_worker.start();
+  if (!streaming) {
+    retune_worker.start();
+    // a first kernel launch on this engine's stream (its hardware queue's first dispatch,
+    // kernel-argument space): here, not inside the first job -- a fresh engine's first job
+    // spent ~35 us more than later ones enqueuing its launches (measured, bench cold_start)
+    launch_signal_host(d_done, 0, stream);
+    LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+  }
   tc[5] = now_ns();
   LOCUST_LOG_DEBUG("engine (%llu B text, %llu records): modules %.2f ms, stream %.2f ms, device "
                    "arena %.2f ms (%.1f MiB), pinned host buffers %.2f ms, copy streams %.2f ms",

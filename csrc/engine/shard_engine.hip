@@ -1145,7 +1145,7 @@ class GpuShardEngine final : public ShardEngine {
     ExchMsg3* msg3_all = nullptr;
     u32* zero_n = nullptr;
     u32* done = nullptr;
-    u64* acc = nullptr;  // the merge's (firsts, tokens) accumulators (kMergeAccSpread pairs)
+    u64* acc = nullptr;  // the merge's (firsts, tokens, words) accumulators (kMergeAccSpread triples)
     char* a2a_send = nullptr;
     char* a2a_recv = nullptr;
     KeyCount* merged = nullptr;
@@ -1175,7 +1175,7 @@ class GpuShardEngine final : public ShardEngine {
     const u64 o_m1 = take(mb), o_m1a = take(mb * P), o_ctl = take(sizeof(ExchCtl)),
               o_cta = take(sizeof(ExchCtl) * P), o_m3 = take(sizeof(ExchMsg3)),
               o_m3a = take(sizeof(ExchMsg3) * P), o_zn = take(8), o_dn = take(8),
-              o_rc = take(kMergeAccSpread * 2 * sizeof(u64));
+              o_rc = take(kMergeAccSpread * 3 * sizeof(u64));
     LOCUST_HIP_CHECK(hipMalloc(&xb_.ctl_dev, off));
     // zeroed in stream order: a null-stream hipMemset is not ordered with the engine's
     // non-blocking stream, and with four ranks sharing a GPU it landed after this job's

@@ -367,6 +367,7 @@ struct DistResult {
   u64 input_bytes = 0;           // bytes of its shard it read / mapped
   bool input_streamed = false;   // ... streamed from its file range (larger than one pass)
   int peer_p2p = -1;             // peers of its GPU with direct (xGMI) access; -1: no peers
+  bool rccl_clique = false;      // ... exchanged over an RCCL clique (else loopback copies)
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
@@ -380,10 +381,9 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts);
 
 // One process drives `cfg.world` ranks (threads) over the visible GPUs (round robin);
 // rank 0's result is returned.  With Backend::kCpu the ranks use the CPU shard engine.
-// comm: kAuto = an RCCL clique (ncclCommInitAll over xGMI) when there are several ranks
-// and every rank gets a GPU of its own (falling back to loopback, with a warning, if the
-// clique cannot be created); else loopback (one rank, or N ranks rehearsed on fewer GPUs:
-// RCCL refuses two ranks per device).  Loopback ranks on distinct GPUs get peer access
+// comm: kAuto = kLoopback (device-to-device copies between the ranks' buffers); kRccl =
+// an RCCL clique (ncclCommInitAll over xGMI; every rank needs a GPU of its own: RCCL
+// refuses two ranks per device).  Loopback ranks on distinct GPUs get peer access
 // enabled pairwise first, so their device copies go GPU to GPU.
 // Ranks in one process never share host memory for their input: each rank thread copies
 // (or reads) its own shard into its engine's pinned buffer, first touched on its NUMA node.

@@ -61,7 +61,8 @@ struct ExchMsg3 {       // 64 B
   u64 max_bucket;       // largest bucket this rank had to send
   u64 n_out;            // distinct keys of this rank's key range
   u64 total;            // token total of this rank's key range
-  u64 pad[4];
+  u64 out_words;        // 8-B words of its compact result records (the host output it writes)
+  u64 pad[3];
 };
 static_assert(sizeof(ExchMsg3) == 64, "ExchMsg3 64 B");
 

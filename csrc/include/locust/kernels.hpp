@@ -471,7 +471,8 @@ void launch_bucket_offsets(ConstKeysSoA sorted, const u32* d_n, const PackedKey*
 // output records (counters still count all of them).
 // The shuffle tail in two launches around the C3 all-gather:
 // launch_merge_rank_slots merges the received slots into `merged` and sums the distinct
-// keys / tokens into `acc`, kMergeAccSpread (firsts, tokens) u64 pairs (zeroed beforehand:
+// keys / tokens / compact words into `acc`, kMergeAccSpread (firsts, tokens, words) u64
+// triples (zeroed beforehand:
 // launch_exch_report sums and re-zeroes them); launch_merge_emit_compact then writes this
 // rank's range as compact
 // records (kv.hpp) straight into the shared host output -- region `region` (or the root's,

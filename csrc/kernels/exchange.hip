@@ -240,7 +240,7 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
                                                          u64* __restrict__ acc,
                                                          u32 gather_records,
                                                          ExchMsg3* __restrict__ msg3) {
-  static_assert(kMergeAccSpread == 64, "one accumulator pair per lane");
+  static_assert(kMergeAccSpread == 64, "one accumulator triple per lane");
   const u64 sb = exch_slot_bytes(slot_records);
   bool bad = false;
   for (u32 q = threadIdx.x; q < P; q += 64) {
@@ -248,11 +248,13 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
     bad |= h->status != kSlotOk || h->n > slot_records;
   }
   const u64 any = dev::ballot(bad);
-  // the merge's range: its (firsts, tokens) pairs, then zeroed for the next job
-  const u64 n_range = dev::wave_reduce_sum(acc[2 * threadIdx.x]);
-  const u64 tok_range = dev::wave_reduce_sum(acc[2 * threadIdx.x + 1]);
-  acc[2 * threadIdx.x] = 0;
-  acc[2 * threadIdx.x + 1] = 0;
+  // the merge's range: its (firsts, tokens, words) triples, then zeroed for the next job
+  const u64 n_range = dev::wave_reduce_sum(acc[3 * threadIdx.x]);
+  const u64 tok_range = dev::wave_reduce_sum(acc[3 * threadIdx.x + 1]);
+  const u64 words_range = dev::wave_reduce_sum(acc[3 * threadIdx.x + 2]);
+  acc[3 * threadIdx.x] = 0;
+  acc[3 * threadIdx.x + 1] = 0;
+  acc[3 * threadIdx.x + 2] = 0;
   if (threadIdx.x == 0) {
     ExchMsg3 m{};
     const u32 cf = ctl->flags;
@@ -262,6 +264,7 @@ __global__ __launch_bounds__(64) void exch_report_kernel(const char* __restrict_
     m.max_bucket = ctl->max_bucket;
     m.n_out = n_out;
     m.total = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : tok_range;
+    m.out_words = (cf & (kExchAbort | kExchTooManySamples)) ? 0 : words_range;
     *msg3 = m;
   }
 }

@@ -149,14 +149,14 @@ __device__ __forceinline__ u32 run_lower_bound(const KeyCount* __restrict__ run,
 
 // kMergeSub threads per record, one per run of a group of kMergeSub runs: 8x the waves of a
 // thread-per-record search, so the dependent probe chains of many records overlap.
-// acc (optional, zeroed): the merge's distinct keys and token total -- the shuffle tail
-// reports them before anything is emitted -- as kMergeAccSpread (firsts, tokens) pairs:
-// block b adds its sums to pair b % kMergeAccSpread (one same-address atomic per block
+// acc (optional, zeroed): the merge's distinct keys, token total and compact-record words
+// -- the shuffle tail reports them before anything is emitted -- as kMergeAccSpread
+// (firsts, tokens, words) triples: block b adds its sums to triple b % kMergeAccSpread (one same-address atomic per block
 // serialised ~25K wave atomics at the memory side: 0.4 ms per job at synth1m scale).
 __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
     RunsView view, KeyCount* __restrict__ merged, LookbackScratch lb, u32 emit_tiles,
     SlotHeader* __restrict__ hdr_out, u64* __restrict__ acc) {
-  __shared__ u64 s_acc[2 * (kMergeBlock / 64)];
+  __shared__ u64 s_acc[3 * (kMergeBlock / 64)];
   __shared__ RunTable t;
   if (blockIdx.x == 0) {
     // merge_emit's look-back scratch, reset here (stream order) instead of by a memset
@@ -173,8 +173,9 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
   const u32 nruns = t.nruns;
   const u64 work = (u64)t.off[nruns] * kMergeSub;
   const u32 sub = threadIdx.x % kMergeSub;
-  u32 my_firsts = 0;  // (acc) first copies this thread emitted, and their counts
-  u64 my_tokens = 0;
+  u32 my_firsts = 0;  // (acc) first copies this thread emitted, their counts and the
+  u64 my_tokens = 0;  // words of their compact records (what the emit writes to the host)
+  u64 my_words = 0;
   // whole groups of kMergeSub lanes enter or leave the loop together (shuffles below)
   for (u64 gt = (u64)blockIdx.x * kMergeBlock + threadIdx.x; gt < work;
        gt += (u64)gridDim.x * kMergeBlock) {
@@ -217,27 +218,32 @@ __global__ __launch_bounds__(kMergeBlock) void merge_rank_kernel(
       merged[(u64)i + before] = out;
       my_firsts += dup ? 0u : 1u;
       my_tokens += out.count;
+      my_words += dup ? 0u : compact_words(out.w, out.count);
     }
   }
   if (acc) {  // uniform: every thread of the block gets here
     const u64 f = dev::wave_reduce_sum((u64)my_firsts);
     const u64 tk = dev::wave_reduce_sum(my_tokens);
+    const u64 wd = dev::wave_reduce_sum(my_words);
     if (dev::lane_id() == 0) {
-      s_acc[2 * dev::wave_id()] = f;
-      s_acc[2 * dev::wave_id() + 1] = tk;
+      s_acc[3 * dev::wave_id()] = f;
+      s_acc[3 * dev::wave_id() + 1] = tk;
+      s_acc[3 * dev::wave_id() + 2] = wd;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      u64 bf = 0, bt = 0;
+      u64 bf = 0, bt = 0, bw = 0;
 #pragma unroll
       for (int w = 0; w < kMergeBlock / 64; ++w) {
-        bf += s_acc[2 * w];
-        bt += s_acc[2 * w + 1];
+        bf += s_acc[3 * w];
+        bt += s_acc[3 * w + 1];
+        bw += s_acc[3 * w + 2];
       }
       if (bf) {
-        u64* a = acc + 2 * (blockIdx.x % kMergeAccSpread);
+        u64* a = acc + 3 * (blockIdx.x % kMergeAccSpread);
         atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)bf);
         atomicAdd(reinterpret_cast<unsigned long long*>(a + 1), (unsigned long long)bt);
+        atomicAdd(reinterpret_cast<unsigned long long*>(a + 2), (unsigned long long)bw);
       }
     }
   }

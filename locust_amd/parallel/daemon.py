@@ -231,7 +231,7 @@ class _Handler(socketserver.BaseRequestHandler):
 
     def _writes_outside_root(self, argv: list[str]) -> str | None:
         """The CLI's file-writing flags may only target the daemon root."""
-        writing = {"--spill-dir", "--gen", "--json"}
+        writing = {"--spill-dir", "--gen", "--json", "--result-file", "--export-kiv"}
         for i, a in enumerate(argv[:-1]):
             if a in writing:
                 try:

@@ -23,11 +23,13 @@ modes here:
 
 3. The reference's stage-split WordCount over daemons (map -> spill files -> reduce)::
 
-       python -m locust_amd.parallel.launch --hosts hosts.txt --wordcount data/hamlet.txt
+       python -m locust_amd.parallel.launch --hosts hosts.txt --wordcount data/hamlet.txt \\
+           [--reducers R]
 
-   Line ranges go to the hosts as stage-1 commands (``--spill-format binary``), the
-   spills are fetched, and the reduce stage (which sorts its inputs, unlike the
-   reference's, bug B7) runs here over all of them and prints the usual output.
+   Line ranges go to the hosts as stage-1 commands (combined, indexed binary spills); the
+   spills go to the reducer hosts, and R key-range reducers (``--reducer r/R``, default one
+   per host) each merge their slice of every spill -- summing counts, never expanding
+   them -- and write it with its global val; the launcher prints the slices in order.
 """
 from __future__ import annotations
 
@@ -260,15 +262,65 @@ def _fetch(host: Host, path: str, dest: str, token: str | None) -> None:
                 break
 
 
+def _put(host: Host, path: str, src: str, token: str | None) -> None:
+    """Copy local file `src` to `path` under the daemon's root (32 MiB frames)."""
+    with open(src, "rb") as f:
+        first = True
+        while True:
+            data = f.read(32 << 20)
+            if not first and not data:
+                break
+            req = {"op": "put", "path": path, "data": base64.b64encode(data).decode(),
+                   "append": not first}
+            if token:
+                req["token"] = token
+            rep = request(host.addr, host.port, req, timeout=120)
+            if not rep.get("ok"):
+                raise RuntimeError(f"put {path} to {host}: {rep.get('error')}")
+            first = False
+            if not data:
+                break
+
+
+def count_lines(path: str) -> int:
+    """Lines of a file (a final line without a newline counts): the native parallel scan
+    when the extension is built, else a Python pass."""
+    try:
+        from .. import _C  # type: ignore[attr-defined]
+
+        return int(_C.find_line_window(path, 0, -1)[2])
+    except Exception:  # noqa: BLE001 -- no native module on this host: count here
+        n, last = 0, b"\n"
+        with open(path, "rb") as f:
+            for block in iter(lambda: f.read(1 << 24), b""):
+                n += block.count(b"\n")
+                last = block[-1:]
+        return n + (0 if last == b"\n" else 1)
+
+
 def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | None = None,
                           backend: str = "gpu", workdir: str | None = None,
-                          remote_root: str | None = None, extra: list[str] | None = None) -> int:
-    """Map on every host (line ranges), fetch the spills, reduce them here."""
+                          remote_root: str | None = None, extra: list[str] | None = None,
+                          reducers: int | None = None, out=None) -> int:
+    """The reference's distributed WordCount (README.md:18-29): map on every host (line
+    ranges), then R key-range reducers on the hosts (default R = number of hosts).
+
+    1. Host k runs stage 1 on lines [k*L/H, (k+1)*L/H): its combined (key, count) spill
+       out.k.kv and index out.k.kv.idx land in its daemon root.
+    2. The spills and indexes are fetched here once and copied to every reducer host's
+       root (``spills/``).
+    3. Reducer r (on host r mod H) runs stage 2 with ``--reducer r/R``: it computes the
+       same splitters as every other reducer from the indexes, reads its key range of each
+       spill (an index seek) and writes its result lines, with their global val, to
+       ``result.r.txt``.
+    4. The results are fetched and concatenated in reducer order -- the single-stage
+       output byte for byte.  The first failing stage stops the job (its exit code)."""
     import tempfile
 
-    with open(path, "rb") as f:
-        nlines = sum(1 for _ in f)
+    out = out or sys.stdout.buffer
+    nlines = count_lines(path)
     parts = len(hosts)
+    reducers = max(1, reducers or parts)
     bounds = [(nlines * k // parts, nlines * (k + 1) // parts) for k in range(parts)]
     hello = []
     for h in hosts:
@@ -279,10 +331,10 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
         if not rep.get("ok"):
             raise RuntimeError(f"{h}: {rep.get('error')}")
         hello.append(rep)
+    roots = [remote_root or hello[k]["root"] for k in range(parts)]
     runs = []
     for k, (h, (s, e)) in enumerate(zip(hosts, bounds)):
-        root = remote_root or hello[k]["root"]
-        argv = [cli, os.path.abspath(path), str(s), str(e), str(k), "1", "--spill-dir", root,
+        argv = [cli, os.path.abspath(path), str(s), str(e), str(k), "1", "--spill-dir", roots[k],
                 "--spill-format", "binary", "--backend", backend] + list(extra or [])
         runs.append(_RemoteRun(h, argv, {}, token))
     rc = _join_all(runs, "map stage")
@@ -292,13 +344,35 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
     os.makedirs(tmp, exist_ok=True)
     local = []
     for k, h in enumerate(hosts):
-        dest = os.path.join(tmp, f"out.{k}.kv")
-        _fetch(h, f"out.{k}.kv", dest, token)
-        local.append(dest)
-    # reduce here over every spill: `MapReduce - 0 0 0 2 --inputs a,b,...`
-    r = subprocess.run([cli, path, "0", "0", "0", "2", "--inputs", ",".join(local),
-                        "--backend", backend] + list(extra or []))
-    return r.returncode
+        for suffix in ("", ".idx"):
+            _fetch(h, f"out.{k}.kv{suffix}", os.path.join(tmp, f"out.{k}.kv{suffix}"), token)
+        local.append(os.path.join(tmp, f"out.{k}.kv"))
+    placed: set[int] = set()
+    runs = []
+    for r in range(reducers):
+        hk = r % parts
+        if hk not in placed:
+            for k in range(parts):
+                for suffix in ("", ".idx"):
+                    _put(hosts[hk], f"spills/out.{k}.kv{suffix}", local[k] + suffix, token)
+            placed.add(hk)
+        inputs = ",".join(f"{roots[hk]}/spills/out.{k}.kv" for k in range(parts))
+        argv = [cli, os.path.abspath(path), "0", "0", str(r), "2", "--inputs", inputs,
+                "--reducer", f"{r}/{reducers}", "--result-file", f"{roots[hk]}/result.{r}.txt",
+                "--backend", backend] + list(extra or [])
+        runs.append(_RemoteRun(hosts[hk], argv, {}, token))
+    rc = _join_all(runs, "reduce stage")
+    if rc:
+        return rc
+    out.write(b"Running\n")
+    for r in range(reducers):
+        dest = os.path.join(tmp, f"result.{r}.txt")
+        _fetch(hosts[r % parts], f"result.{r}.txt", dest, token)
+        with open(dest, "rb") as f:
+            out.write(f.read())
+    out.write(b"\nDone\n")
+    out.flush()
+    return 0
 
 
 def main(argv=None) -> int:
@@ -316,6 +390,10 @@ def main(argv=None) -> int:
     ap.add_argument("--wordcount", metavar="FILE", help="stage-split WordCount of FILE (mode 3)")
     ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--cli", default=None, help="path of the MapReduce binary")
+    ap.add_argument("--reducers", type=int, default=0,
+                    help="key-range reducers of --wordcount (default: one per host)")
+    ap.add_argument("--output-format", choices=["gpu", "cpu"], default=None,
+                    help="--wordcount result lines: GPU build's (with val) or CPU build's")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -328,8 +406,9 @@ def main(argv=None) -> int:
             ap.error("--wordcount needs --hosts")
         from .._native import cli_path
 
+        extra = ["--output-format", a.output_format] if a.output_format else []
         return stage_split_wordcount(a.wordcount, load_hosts(a.hosts), a.cli or cli_path(),
-                                     token, a.backend)
+                                     token, a.backend, extra=extra, reducers=a.reducers or None)
     if not cmd:
         ap.error("no command given (put it after --)")
     if a.hosts:

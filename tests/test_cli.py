@@ -58,9 +58,16 @@ def test_spill_text_format(cli, tmp_path):
 
 
 def test_multi_rank_cpu_cli(cli, hamlet):
+    # --gpus N is the multi-GPU mode: GPU-format lines (val) whatever engine the ranks run
+    # (docs/PARITY.md C18); --output-format picks either format in any mode
     p = run(cli, "data/hamlet.txt", "--backend", "cpu", "--gpus", 4)
     entries = oracle.wordcount(hamlet)[0]
     assert result_lines(p.stdout) == oracle.format_gpu(entries)
+    p = run(cli, "data/hamlet.txt", "--backend", "cpu", "--gpus", 2, "--output-format", "cpu")
+    assert result_lines(p.stdout) == oracle.format_cpu(entries)
+    p = run(cli, "data/hamlet.txt", "--backend", "cpu", "--output-format", "gpu")
+    assert result_lines(p.stdout) == oracle.format_gpu(entries)
+    assert run(cli, "x", "--output-format", "tsv", check=False).returncode == 2
 
 
 def test_json_in_every_mode(tmp_path, cli):

@@ -40,7 +40,9 @@ def test_device_exchange_across_processes(tmp_path, world):
         assert r["comm"] == "tcpdev"
         assert [i["device_exchange"] for i in r["infos"]] == [True] * 4
         assert [i["host_syncs"] for i in r["infos"]][:2] == [2, 1]
-        assert all(i["output_bytes"] == i["range_unique"] * 40 for i in r["infos"])
+        # compact records the merge counted as it emitted: 8-40 B per key
+        assert all(8 * i["range_unique"] <= i["output_bytes"] <= 40 * i["range_unique"]
+                   for i in r["infos"])
 
 
 @pytest.mark.gpu

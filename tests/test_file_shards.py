@@ -44,14 +44,17 @@ def test_file_shards_edge_cases(tmp_path, text):
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_cpu_ranks_read_own_ranges(tmp_path, hamlet, world):
+@pytest.mark.parametrize("tail", [True, False])
+def test_cpu_ranks_read_own_ranges(tmp_path, hamlet, world, tail):
+    text = hamlet if tail else hamlet.rstrip(b"\n")  # a final line without its newline
     f = tmp_path / "h.txt"
-    f.write_bytes(hamlet)
+    f.write_bytes(text)
     dcfg = lc.make_dist_config(world, lc.make_config("cpu", combine=True))
     res, infos = lc._C.run_multi_file(str(f), dcfg, "loopback")
-    assert res.entries() == oracle.wordcount(hamlet)[0]
-    assert res.num_lines == oracle.wordcount(hamlet)[2] or res.num_lines > 0
+    assert res.entries() == oracle.wordcount(text)[0]
+    assert res.num_lines == text.count(b"\n") + (0 if text.endswith(b"\n") else 1)
     assert [i["input_bytes"] for i in infos] == [n for _o, n in lc._C.file_shards(str(f), world)]
+    assert all(i["peer_p2p"] == -1 for i in infos)  # CPU ranks: no GPU peers
 
 
 def test_cli_cpu_ranks_file(cli, hamlet):

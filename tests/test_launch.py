@@ -141,18 +141,32 @@ def test_launch_remote_ranks(tmp_path):
     assert launch.launch_remote(SELFTEST, [h1], 1, token="wrong") != 0
 
 
-def test_stage_split_wordcount_over_daemons(tmp_path, hamlet, cli, capfd):
+@pytest.mark.parametrize("reducers", [1, 2, 3])
+def test_stage_split_wordcount_over_daemons(tmp_path, hamlet, cli, capfd, reducers):
+    """3 local daemons map line ranges; R key-range reducers on the daemons each merge their
+    slice of every spill; the concatenation is the single-stage output byte for byte,
+    val included (GPU-format lines)."""
     hosts = [start_daemon(tmp_path)[0] for _ in range(3)]
     f = tmp_path / "h.txt"
     f.write_bytes(hamlet)
     rc = launch.stage_split_wordcount(str(f), hosts, cli, token=TOKEN, backend="cpu",
-                                      workdir=str(tmp_path / "spills"))
+                                      workdir=str(tmp_path / "spills"), reducers=reducers,
+                                      extra=["--output-format", "gpu"])
     assert rc == 0
     out = capfd.readouterr().out
-    ent = oracle.wordcount(hamlet)[0]
-    body = out[out.index("print key:"):out.rindex("\nDone")].rstrip("\n")
-    same = body == oracle.format_cpu(ent).decode().rstrip("\n")
-    assert same, body[:300]  # (no full diff: the output is 5,608 lines)
+    single = subprocess.run([cli, str(f), "--backend", "cpu", "--output-format", "gpu"],
+                            capture_output=True, timeout=120).stdout.decode()
+    body = out[out.index("print key:"):out.rindex("\nDone")]
+    want = single[single.index("print key:"):single.rindex("\nDone")]
+    assert body == want, body[:300]  # (no full diff: the output is 5,608 lines)
+    assert out.startswith("Running\n") and out.endswith("\nDone\n")
+
+
+def test_daemon_confines_result_files(tmp_path, cli):
+    h, _root = start_daemon(tmp_path)
+    rep = request(h.addr, h.port, {"op": "run", "token": TOKEN, "argv": [
+        cli, "x", "0", "0", "0", "2", "--result-file", "/tmp/elsewhere.txt"]})
+    assert not rep["ok"] and "--result-file" in rep["error"]
 
 
 def test_bootstrap_port_from_torchrun_store(tmp_path):

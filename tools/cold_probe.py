@@ -22,7 +22,9 @@ def main():
     a = ap.parse_args()
     synth = a.config in bench.SYNTH
     text = bench.synth_shard(a.config, 0, 1) if synth else bench.load_text(a.config)
+    r = None
     for k in range(a.engines):
+        r = None  # the previous engine's last result: released outside the timed jobs
         t0 = time.perf_counter()
         if synth:
             cfg = lc.make_config("gpu", reduce_path="lds", chunk_bytes=bench.CHUNK_BYTES)
