@@ -292,7 +292,91 @@ def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
     mine = (t1 - t0) * 1e3 / steps
     ms = dr.allreduce_max(mine)
     med = {k: statistics.median(v) for k, v in parts.items()}
+    _LAST_INFOS[:] = infos  # the timed jobs' per-rank records, for scale_diag
     return ms, med, res, info["strategy"]
+
+
+_LAST_INFOS: list = []
+
+
+# ---------------------------------------------------------------------------------------
+# N > 1: a self-diagnosing line
+# ---------------------------------------------------------------------------------------
+def nccl_debug_setup() -> str | None:
+    """RCCL's INFO log into per-process files (never stdout, which carries the JSON line),
+    so every rank can read which transport each of its peer pairs uses.  Must run before
+    the communicator exists (RCCL reads the variables at init).  A user's NCCL_DEBUG_FILE
+    wins (the log then goes where they said, and the transports are not parsed)."""
+    if "NCCL_DEBUG_FILE" in os.environ:
+        return None
+    import tempfile
+
+    d = os.path.join(tempfile.gettempdir(),
+                     f"locust_nccl_{os.environ.get('MASTER_PORT', '0')}_{os.getuid()}")
+    os.makedirs(d, exist_ok=True)
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,GRAPH,P2P,SHM,NET")
+    os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "nccl.%h.%p.log")
+    return d
+
+
+def nccl_transports(d: str | None, rank: int) -> dict:
+    """{peer rank: sorted transports} of this process's channels, from its RCCL INFO log
+    ("Channel 00/0 : 0[0] -> 1[1] via P2P/IPC")."""
+    import glob
+    import re
+
+    if not d:
+        return {}
+    pat = re.compile(r"Channel \d+/\d+ ?: +(\d+)\[[^\]]*\] -> (\d+)\[[^\]]*\] via (\S.*?)\s*$")
+    out: dict = {}
+    for f in glob.glob(os.path.join(d, f"nccl.*.{os.getpid()}.log")):
+        with open(f, errors="replace") as fh:
+            for ln in fh:
+                m = pat.search(ln)
+                if m and int(m.group(1)) == rank:
+                    out.setdefault(m.group(2), set()).add(m.group(3))
+    return {k: sorted(v) for k, v in sorted(out.items(), key=lambda kv: int(kv[0]))}
+
+
+def scale_diag(dr, args, local_rank: int, nccl_dir: str | None, infos=None) -> dict:
+    """Every rank's view of the last timed jobs, gathered to all ranks: per-rank stage
+    medians (map / exchange / merge / emit), bytes sent to and received from each peer,
+    its GPU's direct-access row and RCCL's transport per peer, and its peak RSS.  The
+    summary gives the min / max over ranks of each stage."""
+    import resource
+    import socket
+
+    infos = infos if infos is not None else list(_LAST_INFOS)
+    names = {"map": "map_ms", "exchange": "shuffle_ms", "merge": "reduce_ms", "emit": "gather_ms"}
+    device = local_rank if args.comm == "rccl" else 0
+    mine = {
+        "rank": dr.rank, "host": socket.gethostname(), "pid": os.getpid(),
+        "device": device if args.backend == "gpu" else None,
+        "stages_ms": {k: round(statistics.median(i[v] for i in infos), 4) if infos else None
+                      for k, v in names.items()},
+        "sent_to": infos[-1]["sent_to"] if infos else [],
+        "recv_from": infos[-1]["recv_from"] if infos else [],
+        "peak_rss_kb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss,
+        "comm": dr.comm_name,
+        "transport": nccl_transports(nccl_dir, dr.rank) if args.comm == "rccl" else
+                     {str(p): [args.comm] for p in range(dr.size) if p != dr.rank},
+    }
+    if args.backend == "gpu":
+        import locust_amd as lc
+
+        mine["peer_access_row"] = list(lc._C.peer_access_row(device))
+    ranks = [json.loads(b) for b in dr.allgather_bytes(json.dumps(mine).encode())]
+    for r in ranks:  # the access row in rank terms: can rank r's GPU reach rank q's directly
+        row = r.pop("peer_access_row", None)
+        r["peer_access"] = ([None if q["device"] == r["device"] else row[q["device"]]
+                             for q in ranks] if row is not None else None)
+    summary = {}
+    for k in names:
+        v = [r["stages_ms"][k] for r in ranks if r["stages_ms"][k] is not None]
+        summary[k] = [min(v), max(v)] if v else None
+    return {"stages_ms_min_max": summary, "ranks": ranks,
+            "nccl_debug_dir": nccl_dir, "peak_rss_kb_max": max(r["peak_rss_kb"] for r in ranks)}
 
 
 def synth_point(args, rank: int, world: int, dr=None) -> dict:
@@ -313,16 +397,23 @@ def synth_point(args, rank: int, world: int, dr=None) -> dict:
         dr.use_engine(dr.add_engine(nbytes, nlines))
         _load(dr, text)
         ms, stages, res, strategy = time_dist(dr, steps, warmup, "auto")
+        synth_infos = list(_LAST_INFOS)
         sizes = [0.0] * world
         total_bytes = int(sum(_allgather_float(dr, float(text.size), sizes)))
         dr.use_engine(0)
-    return {"lines": lines, "n_gpus": world, "ms_per_step": round(ms, 4),
+    point = {"lines": lines, "n_gpus": world, "ms_per_step": round(ms, 4),
             "GB_per_s": round(total_bytes / (ms * 1e-3) / 1e9, 3), "bytes": total_bytes,
             "strategy": strategy, "tokens": res.num_tokens if rank == 0 else None,
             "unique": res.num_unique if rank == 0 else None, "gen_s": round(gen_s, 2),
             "output_bytes_per_key": (round(res.wire_bytes / max(res.num_unique, 1), 2)
                                      if rank == 0 else None),
             "stages_ms": {k: round(v, 4) for k, v in stages.items()}}
+    if dr is not None:
+        d = scale_diag(dr, args, int(os.environ.get("LOCAL_RANK", "0")), None, synth_infos)
+        point["diag"] = {"stages_ms_min_max": d["stages_ms_min_max"],
+                         "sent_to": [r["sent_to"] for r in d["ranks"]],
+                         "recv_from": [r["recv_from"] for r in d["ranks"]]}
+    return point
 
 
 def _allgather_float(dr, v: float, out: list) -> list:
@@ -511,9 +602,11 @@ def main() -> int:
                 "vs_baseline_hamlet700": round(c700["wall_ms"] / 27.132, 4)}
             extra["synth1m"] = synth_point(args, rank, n)
     else:
+        nccl_dir = nccl_debug_setup() if args.comm == "rccl" else None
         dr = dist_rank(text, n, rank, local_rank, args.comm, args.backend)
         rccl_ranks = dr.comm_count if dr.comm_name == "rccl" else None
         ms, stages, res, strategy = time_dist(dr, args.steps, args.warmup, args.strategy)
+        extra["scale_diag"] = scale_diag(dr, args, local_rank, nccl_dir)
         if not args.no_extra and args.strategy == "auto" and strategy != "shuffle":
             # The sample-sort all-to-all shuffle on the same job (the path large inputs
             # take), so every scaling run also records the all-to-all path.

@@ -35,6 +35,7 @@ std::vector<WordCountEntry> merge_runs_device(const JobConfig&,
   no_gpu();
 }
 int visible_device_count() { return 0; }
+std::vector<int> peer_access_row(int) { return {}; }
 LocalComm resolve_local_comm(const DistConfig&, LocalComm) { return LocalComm::kLoopback; }
 
 }  // namespace locust

@@ -510,14 +510,17 @@ int run_direct(const CliArgs& a) {
     st.read = now_ns();
     std::vector<u64> stamps;  // per job: start, after run(), after the result is stored
     stamps.reserve(3 * (size_t)(a.warmup + a.iters));
+    std::vector<StageTimes> jt;  // per job: its own host split (launch / wait / copy)
+    jt.reserve((size_t)(a.warmup + a.iters));
     for (int i = 0; i < a.warmup + a.iters; ++i) {
       stamps.push_back(now_ns());
       if (i < a.warmup) {
-        eng->run(in);
+        jt.push_back(eng->run(in).times);
         stamps.push_back(now_ns());
       } else {
         WordCountResult x = eng->run(in);
         stamps.push_back(now_ns());
+        jt.push_back(x.times);
         r = std::move(x);
         walls.push_back(r.times.wall_ms);
       }
@@ -526,8 +529,10 @@ int run_direct(const CliArgs& a) {
     }
     if ((int)log_level() >= (int)LogLevel::kDebug)
       for (size_t k = 0; k + 2 < stamps.size(); k += 3)
-        LOCUST_LOG_DEBUG("job %zu: starts %+.3f ms, run() %.3f ms, result stored %.3f ms", k / 3,
-                         (stamps[k] - st.read) * 1e-6, (stamps[k + 1] - stamps[k]) * 1e-6,
+        LOCUST_LOG_DEBUG("job %zu: starts %+.3f ms, run() %.3f ms (launch %.3f, wait %.3f, copy "
+                         "%.3f), result stored %.3f ms", k / 3, (stamps[k] - st.read) * 1e-6,
+                         (stamps[k + 1] - stamps[k]) * 1e-6, jt[k / 3].host_launch_ms,
+                         jt[k / 3].host_wait_ms, jt[k / 3].host_copy_ms,
                          (stamps[k + 2] - stamps[k + 1]) * 1e-6);
     r.num_lines = in.num_lines;
   }

@@ -45,6 +45,14 @@ LocalComm resolve_local_comm(const DistConfig& cfg, LocalComm comm) {
   return comm == LocalComm::kAuto ? LocalComm::kLoopback : comm;
 }
 
+std::vector<int> peer_access_row(int device) {
+  const int n = visible_device_count();
+  std::vector<int> row((size_t)std::max(n, 0), 0);
+  for (int d = 0; d < n; ++d)
+    if (d != device) LOCUST_HIP_CHECK(hipDeviceCanAccessPeer(&row[(size_t)d], device, d));
+  return row;
+}
+
 // Which ordered pairs of `devices` can access each other directly (queried, not enabled).
 static std::vector<int> query_peer_access(const std::vector<int>& devices) {
   const size_t n = devices.size();

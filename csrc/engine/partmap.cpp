@@ -55,10 +55,7 @@ void part_map_default(PartMapTables* t) {
 
 namespace {
 
-struct Group {  // the distinct keys sharing one first word
-  u64 w0, work;
-  u32 distinct;
-};
+using Group = PartGroup;
 
 // One greedy sweep with target work `target`; fills lo[] when the ranges fit into
 // kDictParts partitions and returns their count (else kDictParts + 1).
@@ -85,18 +82,28 @@ u32 assign(const std::vector<Group>& g, u64 target, u32 max_distinct, PartMapTab
 
 }  // namespace
 
-u64 part_map_from_entries(const EntryList& entries, PartMapTables* t, u32 max_distinct) {
-  part_map_default(t);
-  std::vector<Group> g;
-  u64 total = 0;
+void part_map_groups(const EntryList& entries, std::vector<PartGroup>* out) {
+  std::vector<Group>& g = *out;
+  g.clear();
   for (const WordCountEntry e : entries) {  // compact lists decode on the fly
     const u64 w0 = e.key.w[0];
     const u64 work = e.count + kPartDistinctWeight;
     if (g.empty() || g.back().w0 != w0) g.push_back({w0, 0, 0});
     g.back().work += work;
     g.back().distinct += 1;
-    total += work;
   }
+}
+
+u64 part_map_from_entries(const EntryList& entries, PartMapTables* t, u32 max_distinct) {
+  std::vector<Group> g;
+  part_map_groups(entries, &g);
+  return part_map_from_groups(g, t, max_distinct);
+}
+
+u64 part_map_from_groups(const std::vector<PartGroup>& g, PartMapTables* t, u32 max_distinct) {
+  part_map_default(t);
+  u64 total = 0;
+  for (const Group& x : g) total += x.work;
   if (!total) return 0;
   // The smallest work target whose greedy sweep fits kDictParts ranges: the range count
   // only falls as the target grows, so a binary search finds it in ~log2(total) sweeps

@@ -394,9 +394,10 @@ void DevicePipeline::select_out() {
   for (size_t i = 0; i < out_pool.size(); ++i)
     if (out_pool[i].use_count() == 1) return use_out(i);
   if (retune_pending) {
-    // a background retune reads a buffer a result no longer needs: let it finish (it is
-    // near the end by now) rather than pin a new buffer (~2 ms for a large engine's)
-    retune_worker.wait_idle();
+    // a background retune reads a buffer a result no longer needs: wait until it has let
+    // go of it (one pass over the output) rather than pin a new buffer (~2 ms for a large
+    // engine's)
+    while (!retune_task.released.load(std::memory_order_acquire)) std::this_thread::yield();
     poll_retune();
     for (size_t i = 0; i < out_pool.size(); ++i)
       if (out_pool[i].use_count() == 1) return use_out(i);
@@ -853,11 +854,15 @@ void DevicePipeline::maybe_retune(const EntryList& e) {
   // a borrowed list: the copy shares the buffer (and its segments), not the entries
   retune_task.hold = out_pool[out_idx];
   retune_task.entries = e;
+  retune_task.released.store(false, std::memory_order_relaxed);
   retune_worker.submit([this] {
     RetuneTask& r = retune_task;
-    r.pred = part_map_from_entries(r.entries, &r.t);
+    // the one pass over the output first, then the buffer is free for the next jobs
+    part_map_groups(r.entries, &r.groups);
     r.entries = EntryList();
     r.hold.reset();
+    r.released.store(true, std::memory_order_release);
+    r.pred = part_map_from_groups(r.groups, &r.t);
   });
 }
 
@@ -1309,8 +1314,13 @@ WordCountResult DevicePipeline::run_ref_timed(const TextInput& in) {
 
 WordCountResult DevicePipeline::run(const TextInput& in) {
   TraceRange tr("locust:job");
+  const u64 tp = now_ns();
   poll_retune();
+  const u64 tq = now_ns();
   select_out();  // the previous result may still hold the last output buffer
+  if ((int)log_level() >= (int)LogLevel::kDebug)
+    LOCUST_LOG_DEBUG("job prologue: retune adoption %.3f ms, output buffer %.3f ms",
+                     (tq - tp) * 1e-6, (now_ns() - tq) * 1e-6);
   // The previous job left d_sync zeroed (self-cleaning ordered run): no reset this time.
   const bool clean_start = sync_clean;
   sync_clean = false;

@@ -579,6 +579,8 @@ struct DevicePipeline {
     PartMapTables t;
     std::shared_ptr<HostOut> hold;
     EntryList entries;
+    std::vector<PartGroup> groups;
+    std::atomic<bool> released{true};  // the worker has let go of the output buffer
   };
   RetuneTask retune_task;
   bool retune_pending = false;  // a task was handed to the worker and not adopted yet

@@ -388,6 +388,9 @@ std::vector<TextInput> shard_text(const TextInput& in, int parts);
 // Ranks in one process never share host memory for their input: each rank thread copies
 // (or reads) its own shard into its engine's pinned buffer, first touched on its NUMA node.
 enum class LocalComm : int { kAuto = 0, kLoopback = 1, kRccl = 2 };
+// hipDeviceCanAccessPeer(device, d) for every visible d (1 = direct xGMI access; the
+// device's own entry is 0).  Empty without a GPU runtime.
+std::vector<int> peer_access_row(int device);
 DistResult run_single_process_multi_gpu(const DistConfig& cfg, const TextInput& whole,
                                         LocalComm comm = LocalComm::kAuto,
                                         std::vector<DistResult>* per_rank = nullptr);

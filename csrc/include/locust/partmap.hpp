@@ -13,6 +13,7 @@
 #pragma once
 
 #include <cstddef>
+#include <vector>
 
 #include "locust/common.hpp"
 
@@ -51,6 +52,15 @@ void part_map_default_first_byte(PartMapTables* t);
 // and at most `max_distinct` distinct keys each, cut only between different first words.
 // Returns the largest partition's predicted work (0 for no entries: default map).
 u64 part_map_from_entries(const EntryList& e, PartMapTables* t, u32 max_distinct = 1024);
+// The same in two steps: the output's first-word groups (one pass; the retune worker makes
+// them first and then lets go of the job's output buffer), and the map from them.
+struct PartGroup {  // the distinct keys sharing one first word
+  u64 w0, work;
+  u32 distinct;
+};
+void part_map_groups(const EntryList& e, std::vector<PartGroup>* g);
+u64 part_map_from_groups(const std::vector<PartGroup>& g, PartMapTables* t,
+                         u32 max_distinct = 1024);
 
 inline u32 part_map_lookup(const PartMapTables& t, u64 w0) { return part_of_w0(t.lo, w0); }
 

@@ -260,6 +260,9 @@ py::dict dist_to_dict(const DistResult& d) {
   x["input_bytes"] = d.input_bytes;
   x["input_streamed"] = d.input_streamed;
   x["peer_p2p"] = d.peer_p2p;
+  x["rccl_clique"] = d.rccl_clique;
+  x["sent_to"] = d.sent_to;
+  x["recv_from"] = d.recv_from;
   return x;
 }
 
@@ -370,6 +373,27 @@ class PyDistRank {
     double m = v;
     for (double x : all) m = std::max(m, x);
     return m;
+  }
+  // Every rank's bytes (any length) on every rank: lengths first, then padded payloads.
+  py::list allgather_bytes(const std::string& mine) {
+    const u64 P = (u64)comm_->size();
+    std::vector<u64> lens(P);
+    std::vector<char> all;
+    u64 mx = 0;
+    {
+      py::gil_scoped_release nogil;
+      const u64 n = mine.size();
+      comm_->allgather_host(&n, lens.data(), sizeof(u64));
+      for (u64 l : lens) mx = std::max(mx, l);
+      std::string pad = mine;
+      pad.resize(std::max<u64>(mx, 1));
+      all.resize(std::max<u64>(mx, 1) * P);
+      comm_->allgather_host(pad.data(), all.data(), std::max<u64>(mx, 1));
+    }
+    py::list out;
+    for (u64 r = 0; r < P; ++r)
+      out.append(py::bytes(all.data() + r * std::max<u64>(mx, 1), lens[r]));
+    return out;
   }
   int rank() const { return comm_->rank(); }
   int size() const { return comm_->size(); }
@@ -522,6 +546,8 @@ PYBIND11_MODULE(_locust, m) {
   m.def("peer_access", &enable_peer_access, py::arg("devices"),
         "Enable peer access between every pair of the devices; returns the n x n matrix "
         "(row-major) of direct-access flags.");
+  m.def("peer_access_row", &peer_access_row, py::arg("device"),
+        "hipDeviceCanAccessPeer(device, d) for every visible device d.");
   m.def("device_count", &visible_device_count,
         "Visible GPUs (initialises the HIP runtime in this process).");
   m.def("local_comm_for", [](const DistConfig& cfg, const std::string& comm) {
@@ -637,6 +663,7 @@ PYBIND11_MODULE(_locust, m) {
       .def("set_strategy", &PyDistRank::set_strategy)
       .def("barrier", &PyDistRank::barrier)
       .def("allreduce_max", &PyDistRank::allreduce_max)
+      .def("allgather_bytes", &PyDistRank::allgather_bytes)
       .def_property_readonly("rank", &PyDistRank::rank)
       .def_property_readonly("size", &PyDistRank::size);
 

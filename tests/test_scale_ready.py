@@ -44,6 +44,37 @@ def _gpus() -> int:
         return 0
 
 
+def check_scale_diag(d: dict, world: int, comm: str, gpu: bool) -> None:
+    """The N > 1 line diagnoses itself: per-rank min/max of every
+    stage, bytes per peer, each pair's direct access and transport, per-rank peak RSS."""
+    diag = d["scale_diag"]
+    for k in ("map", "exchange", "merge", "emit"):
+        lo, hi = diag["stages_ms_min_max"][k]
+        assert 0 <= lo <= hi, (k, lo, hi)
+    ranks = diag["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(world))
+    for r in ranks:
+        assert len(r["sent_to"]) == world and len(r["recv_from"]) == world
+        assert r["sent_to"][r["rank"]] == 0 and r["peak_rss_kb"] > 0
+        others = {str(q) for q in range(world) if q != r["rank"]}
+        if comm == "rccl":  # the pairs RCCL logged a channel for (its ring and p2p setup)
+            assert r["transport"] and set(r["transport"]) <= others, r
+        else:
+            assert set(r["transport"]) == others, r
+            assert all(v == [comm] for v in r["transport"].values())
+        if gpu:
+            assert len(r["peer_access"]) == world and r["device"] is not None
+        else:
+            assert r["peer_access"] is None
+    for p in range(world):  # what p sent to q is what q received from p
+        for q in range(world):
+            assert ranks[p]["sent_to"][q] == ranks[q]["recv_from"][p]
+    assert diag["peak_rss_kb_max"] == max(r["peak_rss_kb"] for r in ranks)
+    sy = d["synth1m"]["diag"]
+    assert len(sy["sent_to"]) == world and set(sy["stages_ms_min_max"]) == {"map", "exchange",
+                                                                             "merge", "emit"}
+
+
 def _synth10g_want(total: int, world: int):
     """The CPU engine over the concatenation of bench.synth_shard's N shards."""
     sys.path.insert(0, ROOT)
@@ -91,6 +122,25 @@ def test_bench_synth10g_cpu_ranks():
     assert d["unique"] == want.num_unique and d["tokens"] == want.num_tokens
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_cpu_tcp_twin_diagnoses_itself(world, tmp_path):
+    d = _line(_bench("--gpus", str(world), "--backend", "cpu", "--comm", "tcp", "--steps", "3",
+                     "--warmup", "1", "--synth-lines", "20000"))
+    check_scale_diag(d, world, "tcp", gpu=False)
+    # the report tool turns lines into the scaling table
+    f = tmp_path / "scale.json"
+    one = dict(d, n_gpus=1, value=d["value"] * 0.9, scale_diag=None)
+    one["synth1m"] = dict(d["synth1m"], ms_per_step=d["synth1m"]["ms_per_step"] * 1.5)
+    f.write_text(json.dumps({"runs": [{"tail": "noise\n" + json.dumps(one)}, {"parsed": d}]}))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale_report.py"), str(f)],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    rows = [ln for ln in out.stdout.splitlines() if ln.startswith("| 1 ") or ln.startswith(f"| {world} ")]
+    assert len(rows) == 2, out.stdout
+    strong = float(rows[1].split("|")[6])
+    assert abs(strong - 1.5 / world) < 0.02, rows
+
+
 @pytest.mark.parametrize("gpus", [2, 3])
 def test_cli_cpu_ranks_synth_file(tmp_path, cli, gpus):
     f = tmp_path / "s.txt"
@@ -107,6 +157,7 @@ def test_bench_self_spawned_tcpdev_one_gpu():
     d = _line(_bench("--gpus", "2", "--comm", "tcpdev", "--steps", "5", "--warmup", "2",
                      "--synth-lines", "100000"))
     assert d["n_gpus"] == 2 and d["synth1m"]["n_gpus"] == 2
+    check_scale_diag(d, 2, "tcpdev", gpu=True)
     whole = lc._C.HostText.generate(lines=100000, seed=1, first_block=0).to_bytes()
     assert d["synth1m"]["unique"] == lc._C.cpu_run(lc.make_config("cpu"), whole).num_unique
 
@@ -132,6 +183,7 @@ needs_peers = pytest.mark.skipif(WORLD < 2, reason="needs >= 2 GPUs (RCCL: one r
 def test_bench_self_spawned_rccl_world():
     d = _line(_bench("--gpus", str(WORLD), "--steps", "5", "--warmup", "2"))
     assert d["n_gpus"] == WORLD and d["rccl_ranks"] == WORLD
+    check_scale_diag(d, WORLD, "rccl", gpu=True)
     assert d["synth1m"]["n_gpus"] == WORLD and d["synth1m"]["unique"] == SYNTH1M_UNIQUE
     assert d["unique"] == len(oracle.wordcount(open(os.path.join(ROOT, "data", "hamlet.txt"), "rb").read())[0])
 
