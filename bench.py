@@ -339,6 +339,21 @@ def nccl_transports(d: str | None, rank: int) -> dict:
     return {k: sorted(v) for k, v in sorted(out.items(), key=lambda kv: int(kv[0]))}
 
 
+def _rss_breakdown() -> dict:
+    """Resident memory now, by kind (/proc/self/status, kB): anonymous, file-backed (device
+    memory the GPU driver maps into the process counts here), shared."""
+    out = {}
+    try:
+        with open("/proc/self/status") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                if k in ("VmRSS", "RssAnon", "RssFile", "RssShmem"):
+                    out[k] = int(v.split()[0])
+    except OSError:
+        pass
+    return out
+
+
 def scale_diag(dr, args, local_rank: int, nccl_dir: str | None, infos=None) -> dict:
     """Every rank's view of the last timed jobs, gathered to all ranks: per-rank stage
     medians (map / exchange / merge / emit), bytes sent to and received from each peer,
@@ -358,6 +373,7 @@ def scale_diag(dr, args, local_rank: int, nccl_dir: str | None, infos=None) -> d
         "sent_to": infos[-1]["sent_to"] if infos else [],
         "recv_from": infos[-1]["recv_from"] if infos else [],
         "peak_rss_kb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss,
+        "rss_now_kb": _rss_breakdown(),
         "comm": dr.comm_name,
         "transport": nccl_transports(nccl_dir, dr.rank) if args.comm == "rccl" else
                      {str(p): [args.comm] for p in range(dr.size) if p != dr.rank},

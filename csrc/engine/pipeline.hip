@@ -282,6 +282,12 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   // take hundreds of ms: its second buffer is pinned when a second job needs it (host
   // memory of `--gpus N` file ranks, one streaming engine each).
   if (!streaming) out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+  // and a third for small engines: the partition map's retune reads the first job's
+  // output on the worker thread, so a caller holding each job's result (the CLI, a
+  // Python loop) found both buffers taken at its third job and waited ~0.2 ms for the
+  // worker (measured); pinning it here costs well under a millisecond of construction
+  if (!streaming && h_out_cap * sizeof(OutRecord) <= (8ull << 20))
+    out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
   use_out(0);
   LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
                                  hipHostMallocMapped | hipHostMallocCoherent));
@@ -855,20 +861,29 @@ void DevicePipeline::maybe_retune(const EntryList& e) {
   retune_task.hold = out_pool[out_idx];
   retune_task.entries = e;
   retune_task.released.store(false, std::memory_order_relaxed);
+  retune_task.t_submit = now_ns();
   retune_worker.submit([this] {
     RetuneTask& r = retune_task;
+    r.t_start = now_ns();
     // the one pass over the output first, then the buffer is free for the next jobs
     part_map_groups(r.entries, &r.groups);
     r.entries = EntryList();
     r.hold.reset();
+    r.t_released = now_ns();
     r.released.store(true, std::memory_order_release);
     r.pred = part_map_from_groups(r.groups, &r.t);
+    r.t_done = now_ns();
   });
 }
 
 void DevicePipeline::poll_retune() {
   if (!retune_pending || !retune_worker.idle()) return;
   retune_pending = false;
+  const RetuneTask& r = retune_task;
+  LOCUST_LOG_DEBUG("retune on the worker: started %.3f ms after the job, output read in %.3f "
+                   "ms, map built in %.3f ms (%zu first-word groups)",
+                   (r.t_start - r.t_submit) * 1e-6, (r.t_released - r.t_start) * 1e-6,
+                   (r.t_done - r.t_released) * 1e-6, r.groups.size());
   retune_with(retune_task.mx, retune_task.pred, retune_task.t);
 }
 

@@ -581,6 +581,7 @@ struct DevicePipeline {
     EntryList entries;
     std::vector<PartGroup> groups;
     std::atomic<bool> released{true};  // the worker has let go of the output buffer
+    u64 t_submit = 0, t_start = 0, t_released = 0, t_done = 0;  // (debug log)
   };
   RetuneTask retune_task;
   bool retune_pending = false;  // a task was handed to the worker and not adopted yet
