@@ -201,6 +201,9 @@ bool parse(int argc, char** argv, CliArgs* a) {
       pos.push_back(s);
     }
   }
+  if (a->cfg.emits_per_line <= 0) throw Error("--emits-per-line must be > 0");
+  if (a->cfg.max_key_len < 1 || a->cfg.max_key_len > kKeyBytes - 1)
+    throw Error("--max-key must be in [1, " + std::to_string(kKeyBytes - 1) + "]");
   if (!a->gen_out.empty()) return true;
   if (pos.empty()) return false;
   a->file = pos[0];
@@ -249,7 +252,14 @@ struct JsonOut {
     kv(k, b);
   }
   void u(const char* k, unsigned long long v) { kv(k, std::to_string(v)); }
-  void str(const char* k, const std::string& v) { kv(k, "\"" + v + "\""); }
+  void str(const char* k, const std::string& v) {
+    std::string e;
+    for (char c : v) {
+      if (c == '"' || c == '\\') e.push_back('\\');
+      e.push_back(c);
+    }
+    kv(k, "\"" + e + "\"");
+  }
   std::string done() const { return body + "}"; }
 };
 
@@ -630,6 +640,9 @@ int run_map_stage(const CliArgs& a) {
     j.u("spill_records", recs.size());
     j.u("spill_bytes", idx.spill_bytes);
     j.str("spill", path);
+    j.str("input", a.file);
+    j.kv("line_start", std::to_string(a.window ? a.line_start : 0));
+    j.kv("line_end", std::to_string(a.window ? a.line_end : -1));
     j.kv("combined", a.cfg.ref_compat ? "false" : "true");
     j.kv("streamed", streamed ? "true" : "false");
     j.u("input_bytes", bytes);

@@ -261,7 +261,11 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   // thread's graph capture (loopback ranks share the process)
   LOCUST_HIP_CHECK(
       hipMemcpyAsync(d_delims, delim_buf, sizeof(delim_buf), hipMemcpyHostToDevice, stream));
+  // the counters and look-back words start zeroed, as a self-cleaning job leaves them: the
+  // first job skips its reset memset (a fill kernel, and ~13 us of a first enqueue)
+  LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
   LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
+  sync_clean = true;
 
   tc[3] = now_ns();
   // A streaming engine reads files through its two staging halves; its one-pass buffer

@@ -282,6 +282,33 @@ def _put(host: Host, path: str, src: str, token: str | None) -> None:
                 break
 
 
+def _spill_done(host: Host, k: int, s: int, e: int, path: str, token: str | None) -> bool:
+    """Host k's stage-1 output of lines [s, e) of `path` is complete: its map record names
+    the same input and range, and the spill's index is present (the reducer checks the
+    index against the spill's size)."""
+    import json
+
+    def get(name):
+        req = {"op": "get", "path": name, "offset": 0, "length": 1 << 20}
+        if token:
+            req["token"] = token
+        try:
+            rep = request(host.addr, host.port, req, timeout=60)
+        except (OSError, ProtocolError):
+            return None
+        return base64.b64decode(rep["data"]) if rep.get("ok") else None
+
+    rec, idx = get(f"out.{k}.map.json"), get(f"out.{k}.kv.idx")
+    if rec is None or idx is None:
+        return False
+    try:
+        m = json.loads(rec)
+    except ValueError:
+        return False
+    return (m.get("mode") == "map_stage" and m.get("input") == path and
+            m.get("line_start") == s and m.get("line_end") == e)
+
+
 def count_lines(path: str) -> int:
     """Lines of a file (a final line without a newline counts): the native parallel scan
     when the extension is built, else a Python pass."""
@@ -301,7 +328,8 @@ def count_lines(path: str) -> int:
 def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | None = None,
                           backend: str = "gpu", workdir: str | None = None,
                           remote_root: str | None = None, extra: list[str] | None = None,
-                          reducers: int | None = None, out=None) -> int:
+                          reducers: int | None = None, out=None, resume: bool = False,
+                          mapped: list | None = None) -> int:
     """The reference's distributed WordCount (README.md:18-29): map on every host (line
     ranges), then R key-range reducers on the hosts (default R = number of hosts).
 
@@ -314,7 +342,12 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
        spill (an index seek) and writes its result lines, with their global val, to
        ``result.r.txt``.
     4. The results are fetched and concatenated in reducer order -- the single-stage
-       output byte for byte.  The first failing stage stops the job (its exit code)."""
+       output byte for byte.  The first failing stage stops the job (its exit code).
+
+    resume: the map outputs are the job's checkpoint -- a host whose
+    spill and index from an earlier run of the same line range are still in its root
+    (the index is valid for the spill's size and names the range) is not mapped again.
+    `mapped` (optional) receives the hosts' indexes that ran stage 1."""
     import tempfile
 
     out = out or sys.stdout.buffer
@@ -334,10 +367,15 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
     roots = [remote_root or hello[k]["root"] for k in range(parts)]
     runs = []
     for k, (h, (s, e)) in enumerate(zip(hosts, bounds)):
+        if resume and _spill_done(h, k, s, e, os.path.abspath(path), token):
+            continue
         argv = [cli, os.path.abspath(path), str(s), str(e), str(k), "1", "--spill-dir", roots[k],
-                "--spill-format", "binary", "--backend", backend] + list(extra or [])
+                "--spill-format", "binary", "--backend", backend,
+                "--json", f"{roots[k]}/out.{k}.map.json"] + list(extra or [])
         runs.append(_RemoteRun(h, argv, {}, token))
-    rc = _join_all(runs, "map stage")
+        if mapped is not None:
+            mapped.append(k)
+    rc = _join_all(runs, "map stage") if runs else 0
     if rc:
         return rc
     tmp = workdir or tempfile.mkdtemp(prefix="locust_spills_")

@@ -262,3 +262,37 @@ def test_launch_local_hands_listener_to_rank0(tmp_path):
         "dr.barrier()\n")
     env = {"PYTHONPATH": lc.REPO_ROOT}
     assert launch.launch_local([sys.executable, str(script)], 3, timeout=120, extra_env=env) == 0
+
+
+def test_stage_split_resumes_from_map_outputs(tmp_path, hamlet, cli, capfd):
+    """The spills are the job's checkpoint: a rerun with resume maps only
+    the hosts whose stage-1 output is missing, and gives the same output."""
+    hosts_roots = [start_daemon(tmp_path) for _ in range(3)]
+    hosts = [h for h, _r in hosts_roots]
+    f = tmp_path / "h.txt"
+    f.write_bytes(hamlet)
+    kw = dict(token=TOKEN, backend="cpu", reducers=2, extra=["--output-format", "gpu"])
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, workdir=str(tmp_path / "w1"),
+                                        mapped=mapped, **kw) == 0
+    first = capfd.readouterr().out
+    assert mapped == [0, 1, 2]
+    os.remove(os.path.join(hosts_roots[1][1], "out.1.kv.idx"))  # host 1 lost its map output
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, workdir=str(tmp_path / "w2"),
+                                        mapped=mapped, resume=True, **kw) == 0
+    assert mapped == [1]
+    assert capfd.readouterr().out == first
+
+
+def test_stage_split_map_failure_propagates(tmp_path, cli, capfd):
+    """A failing map stage stops the job with its exit code (the reference's slave ACKed
+    whatever happened, slave.py:19-20); no reducer runs."""
+    hosts = [start_daemon(tmp_path)[0] for _ in range(2)]
+    f = tmp_path / "t.txt"
+    f.write_bytes(b"a b\nc\n")
+    rc = launch.stage_split_wordcount(str(f), hosts, cli, token=TOKEN, backend="cpu",
+                                      workdir=str(tmp_path / "w"), extra=["--emits-per-line", "0"])
+    assert rc == 2  # the CLI's error exit
+    cap = capfd.readouterr()
+    assert "map stage failed" in cap.err and "print key" not in cap.out
