@@ -374,6 +374,7 @@ def scale_diag(dr, args, local_rank: int, nccl_dir: str | None, infos=None) -> d
         "recv_from": infos[-1]["recv_from"] if infos else [],
         "peak_rss_kb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss,
         "rss_now_kb": _rss_breakdown(),
+        "pinned_bytes": infos[-1].get("pinned_bytes", 0) if infos else 0,
         "comm": dr.comm_name,
         "transport": nccl_transports(nccl_dir, dr.rank) if args.comm == "rccl" else
                      {str(p): [args.comm] for p in range(dr.size) if p != dr.rank},

@@ -354,6 +354,11 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
   j.num("wall_ms", root.total_ms);
   j.str("comm", !ranks.empty() && ranks[0].rccl_clique ? "rccl" : "loopback");
   j.u("peak_rss_kb", peak_rss_kb());
+  {  // page-locked host memory: every rank's engine, plus the shared output block once
+    u64 pinned = ranks.empty() ? 0 : ranks[0].shared_pinned_bytes;
+    for (const DistResult& d : ranks) pinned += d.pinned_bytes;
+    j.u("pinned_bytes", pinned);
+  }
   std::string rk = "[";
   for (size_t r = 0; r < ranks.size(); ++r) {
     const DistResult& d = ranks[r];
@@ -377,6 +382,7 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
     x.u("input_bytes", d.input_bytes);
     x.kv("input_streamed", d.input_streamed ? "true" : "false");
     x.kv("peer_p2p", std::to_string(d.peer_p2p));
+    x.u("pinned_bytes", d.pinned_bytes);
     rk += (r ? ", " : "") + x.done();
   }
   j.kv("ranks", rk + "]");

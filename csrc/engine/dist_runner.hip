@@ -217,6 +217,8 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
           d.input_streamed = shard.source != nullptr;
           d.peer_p2p = gpu ? peers_of(job.device) : -1;
           d.rccl_clique = rccl;
+          d.pinned_bytes = eng->host_pinned_bytes();
+          d.shared_pinned_bytes = eng->shared_pinned_bytes();
           if (per_rank && j + 1 == schedule.size()) {  // the last job's stats (no entries)
             DistResult& pr = (*per_rank)[(size_t)r];
             pr = d;

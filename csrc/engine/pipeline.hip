@@ -16,6 +16,22 @@ u64 DevicePipeline::piece_target() {
   return b;
 }
 
+u64 DevicePipeline::pinned_bytes() const {
+  u64 b = 0;
+  if (h_text) b += cap_bytes + 64;
+  for (const auto& o : out_pool) b += o->cap * sizeof(OutRecord) + kDictParts * sizeof(u64);
+  for (int k = 0; k < 2; ++k)
+    if (h_stage[k]) b += cap_bytes + 64;
+  for (int i = 0; i < kRingPieces; ++i)
+    if (h_ring[i]) b += ring_piece + 64;
+  b += h_keys_cap * kKeyWords * sizeof(u64);
+  b += h_chunk_cap * sizeof(MapCounters);
+  b += 2 * sizeof(MapCounters) + sizeof(SortPlan) + 2 * sizeof(PartMapTables) +
+       kMaxSamples * sizeof(PackedKey) + (kMaxRanks + 8) * sizeof(u64) + 64 +
+       kDictParts * sizeof(u32);
+  return b;
+}
+
 void DevicePipeline::issue_piece_copies(const char* src) {
   ensure_piece_events(pieces.size());
   for (size_t k = 0; k < pieces.size(); ++k) {

@@ -114,6 +114,10 @@ struct DevicePipeline {
   static constexpr u64 kPieceBytes = 4ull << 20;
   static constexpr u64 kDevPageBytes = 2ull << 20;  // device allocations: whole 2 MiB pages
   static u64 piece_target();
+  // Page-locked host memory this engine holds now (its buffers; not the HIP runtime's own
+  // per-device memory): the input text, the output pool, the stream staging / read ring,
+  // the key staging and the small control blocks.
+  u64 pinned_bytes() const;
   static constexpr u64 kMaxPieces = kMaxPartialSlots;
   std::vector<std::pair<u64, u64>> pieces;
   // run() opts a large dictionary pass into the combining map (records + d_counts);

@@ -46,6 +46,10 @@ class GpuShardEngine final : public ShardEngine {
     return true;
   }
   char* input_buffer() override { return mp_->ensure_h_text(); }
+  u64 host_pinned_bytes() const override { return mp_->pinned_bytes(); }
+  u64 shared_pinned_bytes() const override {
+    return out_ ? shm_segment_bytes(out_->region_records * out_->regions, sizeof(OutRecord)) : 0;
+  }
 
   u64 map_local(const TextInput& shard, bool combine, DistStrategy plan) override {
     DevicePipeline& m = *mp_;

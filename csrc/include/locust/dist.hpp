@@ -174,6 +174,10 @@ class ShardEngine {
   // Pinned host staging buffer for the shard text (nullptr if the engine has none).  A
   // shard whose data already points here is uploaded without a host copy.
   virtual char* input_buffer() { return nullptr; }
+  // Page-locked host memory this rank's engine holds (0: a CPU engine); the shared output
+  // block of ranks in one process is counted apart (shared_pinned_bytes, once per process).
+  virtual u64 host_pinned_bytes() const { return 0; }
+  virtual u64 shared_pinned_bytes() const { return 0; }
   // Map + sort (+ combine) this rank's shard.  Returns the number of local records.
   // `plan` is the strategy the driver expects to take: kGather lets an engine skip the
   // local sort (records may be unsorted); prepare_shuffle() must then be called before
@@ -368,6 +372,8 @@ struct DistResult {
   bool input_streamed = false;   // ... streamed from its file range (larger than one pass)
   int peer_p2p = -1;             // peers of its GPU with direct (xGMI) access; -1: no peers
   bool rccl_clique = false;      // ... exchanged over an RCCL clique (else loopback copies)
+  u64 pinned_bytes = 0;          // page-locked host memory of its engine (its GPU's share)
+  u64 shared_pinned_bytes = 0;   // the shared output block the ranks of a process write
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,

@@ -261,6 +261,8 @@ py::dict dist_to_dict(const DistResult& d) {
   x["input_streamed"] = d.input_streamed;
   x["peer_p2p"] = d.peer_p2p;
   x["rccl_clique"] = d.rccl_clique;
+  x["pinned_bytes"] = d.pinned_bytes;
+  x["shared_pinned_bytes"] = d.shared_pinned_bytes;
   x["sent_to"] = d.sent_to;
   x["recv_from"] = d.recv_from;
   return x;

@@ -94,6 +94,7 @@ def test_json_in_every_mode(tmp_path, cli):
     assert r["tokens"] == 4896 and r["indexed_files"] == 1
     d = run("--gpus", "3")
     assert d["mode"] == "multi_gpu" and d["unique"] == 5608 and len(d["ranks"]) == 3
+    assert d["comm"] == "loopback" and d["pinned_bytes"] == 0  # CPU ranks pin nothing
     for k, rk in enumerate(d["ranks"]):
         assert rk["rank"] == k and len(rk["sent_to"]) == 3 and rk["sent_to"][k] == 0
         assert rk["sent_bytes"] == sum(rk["sent_to"]) and rk["recv_bytes"] == sum(rk["recv_from"])

@@ -162,6 +162,9 @@ def test_multi_rank_cli_first_job_on_device(tmp_path, cli, gpus):
         assert 8 * rk["range_unique"] <= rk["output_bytes"] <= 40 * rk["range_unique"], rk
     assert sum(rk["range_unique"] for rk in rec["ranks"]) == want.num_unique
     assert sum(rk["output_bytes"] for rk in rec["ranks"]) == _compact_bytes(want.entries())
+    # page-locked host memory per rank (its engine) and in all (plus the shared output)
+    assert all(rk["pinned_bytes"] > 0 for rk in rec["ranks"])
+    assert rec["pinned_bytes"] > sum(rk["pinned_bytes"] for rk in rec["ranks"])
 
 
 def _compact_bytes(entries) -> int:
