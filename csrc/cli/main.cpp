@@ -305,6 +305,7 @@ struct Startup {
   u64 main = 0, init = 0, engine = 0, read = 0, first = 0, jobs = 0, out = 0;
 };
 Startup g_startup;
+const char* g_part_map = nullptr;  // "cache" / "default": run_direct's starting map
 
 void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
   if (a.json.empty()) return;
@@ -324,6 +325,7 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
   j.num("wall_ms_median", med);
   j.kv("iters", std::to_string(w.size()));
   j.u("chunks", r.chunks);
+  if (g_part_map) j.str("part_map", g_part_map);  // the one-shot CLI's starting map
   // peak resident memory of this process image (VmHWM: unlike getrusage's ru_maxrss it is
   // not inherited through the fork + exec that started us)
   j.u("max_rss_kb", peak_rss_kb());
@@ -505,9 +507,17 @@ int run_direct(const CliArgs& a) {
   st.init = now_ns();
   // The engine outlives the output: its teardown (stream, pinned buffers) is not a job's
   std::unique_ptr<GpuWordCount> eng;
+  // the partition map tuned by an earlier run on this file (io.hpp partition-map cache)
+  const std::string pmc = partmap_cache_path(a.file, cfg);
+  std::vector<u64> cached;
+  auto start_map = [&]() {
+    g_part_map = load_partmap_cache(pmc, &cached) && eng->set_partition_map(cached) ? "cache"
+                                                                                    : "default";
+  };
   if (size > chunk) {
     cfg.chunk_bytes = chunk;
     eng.reset(new GpuWordCount(cfg, size, size));
+    start_map();
     st.engine = st.read = now_ns();  // the file is read by the job, piece by piece
     log_rss("with the streaming engine");
     for (int i = 0; i < a.warmup + a.iters; ++i) {
@@ -518,6 +528,7 @@ int run_direct(const CliArgs& a) {
     }
   } else {
     eng.reset(new GpuWordCount(cfg, std::max<u64>(size, 1), std::max<u64>(size, 1)));
+    start_map();
     st.engine = now_ns();
     TextInput in;
     in.data = eng->input_buffer();
@@ -557,7 +568,10 @@ int run_direct(const CliArgs& a) {
   std::printf("Length: %i\n", (int)r.num_lines);
   print_gpu_result(a, r, walls);
   log_rss("after the output");
+  // keep this run's tuned map for the next run on the file (after the output: not a job's)
   const u64 t_down = now_ns();
+  std::vector<u64> lo;
+  if (!pmc.empty() && eng->partition_map(&lo) && lo != cached) save_partmap_cache(pmc, lo);
   eng.reset();
   LOCUST_LOG_DEBUG("engine teardown %.3f ms", (now_ns() - t_down) * 1e-6);
   return 0;

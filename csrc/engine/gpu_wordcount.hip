@@ -38,6 +38,31 @@ GpuWordCount::Stats GpuWordCount::stats() const {
   return s;
 }
 
+bool GpuWordCount::partition_map(std::vector<u64>* lo) {
+  Impl& m = *impl_;
+  if (m.retune_pending) {  // the last job's retune: let it finish and adopt it
+    m.retune_worker.wait_idle();
+    m.poll_retune();
+  }
+  lo->assign(m.h_pmap->lo, m.h_pmap->lo + kDictParts + 1);
+  return m.pm_retunes > 0;
+}
+
+bool GpuWordCount::set_partition_map(const std::vector<u64>& lo) {
+  Impl& m = *impl_;
+  if (lo.size() != (size_t)kDictParts + 1 || lo[0] != 0) return false;
+  for (size_t i = 1; i < lo.size(); ++i)
+    if (lo[i] < lo[i - 1]) return false;
+  PartMapTables t;
+  for (size_t i = 0; i < lo.size(); ++i) t.lo[i] = lo[i];
+  t.lo[kDictParts] = ~0ull;
+  m.sync();  // no job may still read the old tables (they are uploaded in stream order anyway)
+  m.upload_pmap(t, 0);
+  ++m.pm_retunes;  // a tuned map: no in-job plan (decide_plan), retunes only on imbalance
+  if (m.large_ordered) m.pm_tuned = true;  // (large passes: no device plan either)
+  return true;
+}
+
 std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput& in, WordCountResult* stats) {
   Impl& m = *impl_;
   m.sync_clean = false;  // this entry point dirties d_sync

@@ -302,6 +302,14 @@ class GpuWordCount {
   };
   Stats stats() const;
 
+  // The partition map (kDictParts + 1 ascending range starts, partmap.hpp) -- a
+  // load-balancing hint only: any ascending map gives the same results.  partition_map()
+  // finishes a background retune first and returns false while the map is still the data-
+  // independent default; set_partition_map() starts this engine on a map tuned earlier (the
+  // CLI's per-file cache), returning false (map unchanged) for a malformed one.
+  bool partition_map(std::vector<u64>* lo);
+  bool set_partition_map(const std::vector<u64>& lo);
+
   // Stage split: map + process only, returning the sorted tokens of
   // this input; and reduce-only over (possibly unsorted) tokens.
   std::vector<PackedKey> run_map_stage(const TextInput& in, WordCountResult* stats);

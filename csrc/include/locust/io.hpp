@@ -133,6 +133,18 @@ std::vector<KeyCount> entries_to_records(const EntryList& e);
 // Records in packed-key order (== the reference's unsigned byte order, KeyValue.h:23-28).
 inline bool record_less(const KeyCount& a, const KeyCount& b) { return key_compare(a.w, b.w) < 0; }
 
+// ---- per-file partition-map cache (the one-shot CLI) ----
+// A process of `./MapReduce <file>` runs one job, on the data-independent starting map;
+// the map tuned from its output (a load-balancing hint, kDictParts + 1 words) is kept in
+// a small cache keyed by the input file's identity (real path, size, mtime, inode) and the
+// job's tokenizer settings, so the next run on the same file starts tuned -- the role
+// MIOpen's performance database plays for its kernels.  A stale or damaged entry can only
+// cost speed: any ascending map gives the same results.  Directory: LOCUST_CACHE_DIR, else
+// $XDG_CACHE_HOME/locust, else ~/.cache/locust; LOCUST_PART_CACHE=0 disables it ("").
+std::string partmap_cache_path(const std::string& input, const JobConfig& cfg);
+bool load_partmap_cache(const std::string& path, std::vector<u64>* lo);
+void save_partmap_cache(const std::string& path, const std::vector<u64>& lo);  // best effort
+
 // ---- output ----
 // GPU build format (main.cu:132): "print key: %s \t val: %d \t count: %d\n".
 void format_gpu_output(const WordCountResult& r, std::string* out);

@@ -1,4 +1,5 @@
 #include "locust/io.hpp"
+#include "locust/partmap.hpp"
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -8,6 +9,7 @@
 #include <atomic>
 #include <cerrno>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -917,6 +919,80 @@ std::vector<KeyCount> entries_to_records(const EntryList& e) {
     recs.push_back(r);
   }
   return recs;
+}
+
+// ---------------- partition-map cache ----------------
+namespace {
+constexpr char kPmcMagic[8] = {'L', 'C', 'S', 'T', 'P', 'M', 'C', '1'};
+u64 fnv1a(u64 h, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+}  // namespace
+
+std::string partmap_cache_path(const std::string& input, const JobConfig& cfg) {
+  if (const char* e = std::getenv("LOCUST_PART_CACHE"))
+    if (e[0] == '0') return "";
+  std::string dir;
+  if (const char* d = std::getenv("LOCUST_CACHE_DIR"); d && *d) {
+    dir = d;
+  } else if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) {
+    dir = std::string(x) + "/locust";
+  } else if (const char* h = std::getenv("HOME"); h && *h) {
+    dir = std::string(h) + "/.cache/locust";
+  } else {
+    return "";
+  }
+  struct stat st;
+  char real[4096];
+  if (::stat(input.c_str(), &st) != 0 || !::realpath(input.c_str(), real)) return "";
+  u64 h = 1469598103934665603ull;
+  h = fnv1a(h, real, std::strlen(real));
+  const u64 id[5] = {(u64)st.st_size, (u64)st.st_mtim.tv_sec, (u64)st.st_mtim.tv_nsec,
+                     (u64)st.st_ino, (u64)st.st_dev};
+  h = fnv1a(h, id, sizeof(id));
+  const int tok[4] = {cfg.emits_per_line, cfg.max_key_len, (int)cfg.map_path, (int)cfg.sort_path};
+  h = fnv1a(h, tok, sizeof(tok));
+  h = fnv1a(h, cfg.delimiters.data(), cfg.delimiters.size());
+  char name[64];
+  std::snprintf(name, sizeof(name), "/partmap-%016llx.bin", (unsigned long long)h);
+  return dir + name;
+}
+
+bool load_partmap_cache(const std::string& path, std::vector<u64>* lo) {
+  if (path.empty()) return false;
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  char magic[8];
+  u32 n = 0;
+  bool ok = std::fread(magic, 8, 1, f) == 1 && std::memcmp(magic, kPmcMagic, 8) == 0 &&
+            std::fread(&n, sizeof(n), 1, f) == 1 && n == (u32)kDictParts + 1;
+  if (ok) {
+    lo->resize(n);
+    ok = std::fread(lo->data(), sizeof(u64), n, f) == n;
+  }
+  std::fclose(f);
+  return ok;
+}
+
+void save_partmap_cache(const std::string& path, const std::vector<u64>& lo) {
+  if (path.empty() || lo.size() != (size_t)kDictParts + 1) return;
+  const size_t slash = path.rfind('/');
+  if (slash != std::string::npos) {  // the directory, mode 0700 (best effort, one level up too)
+    const std::string dir = path.substr(0, slash);
+    const size_t up = dir.rfind('/');
+    if (up != std::string::npos && up > 0) (void)::mkdir(dir.substr(0, up).c_str(), 0700);
+    (void)::mkdir(dir.c_str(), 0700);
+  }
+  const std::string tmp = path + "." + std::to_string((long long)::getpid()) + ".tmp";
+  std::FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const u32 n = (u32)lo.size();
+  bool ok = std::fwrite(kPmcMagic, 8, 1, f) == 1 && std::fwrite(&n, sizeof(n), 1, f) == 1 &&
+            std::fwrite(lo.data(), sizeof(u64), n, f) == n;
+  ok = std::fclose(f) == 0 && ok;
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) (void)::unlink(tmp.c_str());
 }
 
 // ---------------- output ----------------

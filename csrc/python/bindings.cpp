@@ -89,6 +89,7 @@ class PyGpuEngine {
   }
   PyGpuEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
       : eng_(cfg, max_bytes, max_lines), max_bytes_(max_bytes) {}
+  GpuWordCount& engine() { return eng_; }
   PyResult run(const std::string& text) {
     py::gil_scoped_release nogil;
     return PyResult{eng_.run(as_input(text))};
@@ -508,6 +509,14 @@ PYBIND11_MODULE(_locust, m) {
       .def("load", &PyGpuEngine::load)
       .def("run_loaded", &PyGpuEngine::run_loaded)
       .def("stats", &PyGpuEngine::stats)
+      .def("partition_map", [](PyGpuEngine& e) {
+        std::vector<u64> lo;
+        const bool tuned = e.engine().partition_map(&lo);
+        return py::make_tuple(tuned, lo);
+      }, "(tuned, the kDictParts + 1 range starts) after any background retune")
+      .def("set_partition_map", [](PyGpuEngine& e, const std::vector<u64>& lo) {
+        return e.engine().set_partition_map(lo);
+      }, py::arg("lo"))
       .def("run_text", &PyGpuEngine::run_text, py::arg("text"))
       .def("run_file", &PyGpuEngine::run_file, py::arg("path"),
            "Stream a file through this (streaming) engine, piece by piece.")
@@ -881,5 +890,12 @@ PYBIND11_MODULE(_locust, m) {
     return py::make_tuple(PyResult{std::move(r)}, d);
   }, py::arg("cfg"), py::arg("files"), py::arg("reducer") = 0, py::arg("reducers") = 1,
         "Stage 2 over spill files: (result, stats); key range `reducer` of `reducers`.");
+  m.def("partmap_cache_path", &partmap_cache_path, py::arg("input"), py::arg("cfg"));
+  m.def("load_partmap_cache", [](const std::string& path) -> py::object {
+    std::vector<u64> lo;
+    if (!load_partmap_cache(path, &lo)) return py::none();
+    return py::cast(lo);
+  }, py::arg("path"));
+  m.def("save_partmap_cache", &save_partmap_cache, py::arg("path"), py::arg("lo"));
   py::register_exception<Error>(m, "LocustError");
 }

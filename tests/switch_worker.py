@@ -1,7 +1,7 @@
 """One process of tests/test_switches.py: runs a fixed set of WordCount jobs under the
 LOCUST_* environment it was started with and checks every result against the oracle.
 
-    python tests/switch_worker.py single|stream|dist|merge
+    python tests/switch_worker.py single|stream|dist|merge|cli
 
 Exit status 0 = every job matched; the failure is printed otherwise.  A separate process
 per setting because many switches are read once per process (or per engine)."""
@@ -61,6 +61,31 @@ def main(kind: str) -> None:
                     got += res.entries()
                 ent = oracle.wordcount(synth)[0]
                 assert got == ent, f"device merge of 70 spills, {reducers} reducers"
+    elif kind == "cli":
+        # the one-shot CLI twice on one file: the second run starts from the partition map
+        # the first one tuned (unless LOCUST_PART_CACHE=0); the output never changes
+        import json
+        import subprocess
+        import tempfile
+
+        with tempfile.TemporaryDirectory() as d:
+            env = dict(os.environ)
+            if env.get("LOCUST_CACHE_DIR", None) == "":
+                env["LOCUST_CACHE_DIR"] = os.path.join(d, "cache")
+            f = os.path.join(d, "h.txt")
+            with open(f, "wb") as fh:
+                fh.write(hamlet)
+            maps = []
+            for _ in range(2):
+                j = os.path.join(d, "r.json")
+                p = subprocess.run([lc.cli_path(), f, "--json", j], capture_output=True,
+                                   env=env, timeout=120)
+                assert p.returncode == 0, p.stderr.decode()[-2000:]
+                got = b"".join(l + b"\n" for l in p.stdout.split(b"\n") if l.startswith(b"print key:"))
+                assert got == oracle.format_gpu(oracle.wordcount(hamlet)[0]), "CLI output"
+                maps.append(json.load(open(j))["part_map"])
+            off = os.environ.get("LOCUST_PART_CACHE") == "0"
+            assert maps == (["default", "default"] if off else ["default", "cache"]), maps
     else:
         raise SystemExit(f"unknown kind {kind}")
     print("switch worker ok:", kind, {k: v for k, v in os.environ.items()

@@ -25,6 +25,8 @@ CASES = [
     ({"LOCUST_GRAPH": "1"}, "single"),
     ({"LOCUST_PIECE_MB": "4"}, "single"),
     ({"LOCUST_MERGE_MAX_RECORDS": "100"}, "merge"),
+    ({"LOCUST_CACHE_DIR": "", "LOCUST_PART_CACHE": "1"}, "cli"),
+    ({"LOCUST_PART_CACHE": "0"}, "cli"),
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PART_DEFAULT": "byte"}, "single"),
     ({"LOCUST_VPLAN": "0", "LOCUST_DEVPLAN": "0"}, "single"),
     ({"LOCUST_VPLAN_MIN_KB": "64", "LOCUST_SPLIT_MIN": "256"}, "single"),
