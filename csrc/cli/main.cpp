@@ -587,67 +587,10 @@ int run_map_stage(const CliArgs& a) {
   const bool cpu = a.cfg.backend == Backend::kCpu;
   const char* dev = cpu ? "CPU" : "GPU";
   const std::string path = spill_path(a, a.node);
-  WordCountResult r;
-  std::vector<KeyCount> recs;
-  u64 lines = 0, bytes = 0;
-  bool streamed = false;
-  const u64 t0 = now_ns();
-  if (cpu || a.cfg.ref_compat) {
-    const bool use_window = a.window && !(cpu && a.cfg.ref_compat);
-    LoadedText text = load_lines(a.file, use_window ? a.line_start : -1,
-                                 use_window ? a.line_end : -1, a.cfg.ref_compat);
-    lines = text.input.num_lines;
-    bytes = text.input.bytes;
-    if (a.cfg.ref_compat) {
-      std::vector<PackedKey> toks;
-      if (cpu) {
-        toks = CpuWordCount(a.cfg).run_map_stage(text.input, &r);
-      } else {
-        GpuWordCount eng(a.cfg, std::max<u64>(bytes, 1), std::max<u64>(lines, 1));
-        toks = eng.run_map_stage(text.input, &r);
-      }
-      r.num_tokens = toks.size();
-      recs = tokens_to_records(toks);
-    } else {
-      r = CpuWordCount(a.cfg).run(text.input);
-      recs = entries_to_records(r.entries);
-    }
-  } else {
-    LineWindow w;
-    if (a.window) {
-      w = find_line_window(a.file, a.line_start, a.line_end);
-    } else {
-      w.end = file_size(a.file);
-    }
-    bytes = w.end - w.begin;
-    JobConfig cfg = a.cfg;
-    cfg.graph = 0;  // stage events: the map and sort times printed below
-    const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
-    if (bytes > chunk) {
-      cfg.chunk_bytes = chunk;
-      GpuWordCount eng(cfg, bytes, bytes);
-      auto src = open_file_range_source(a.file, w.begin, w.end);
-      r = eng.run_source(*src);
-      lines = src->lines();
-      streamed = true;
-      recs = entries_to_records(r.entries);
-    } else {
-      GpuWordCount eng(cfg, std::max<u64>(bytes, 1), std::max<u64>(bytes, 1));
-      TextInput in;
-      in.data = eng.input_buffer();
-      in.bytes = read_file_range_into(a.file, eng.input_buffer(), w.begin, bytes, &lines);
-      in.num_lines = lines;
-      r = eng.run(in);
-      recs = entries_to_records(r.entries);
-    }
-    if (a.window) lines = w.lines;
-  }
-  const u64 t1 = now_ns();
-  SpillIndex idx;
-  write_spill(path, recs, a.spill_fmt, &idx);
-  write_spill_index(spill_index_path(path), idx);
-  const u64 t2 = now_ns();
-  if (!cpu) std::printf("Length: %i\n", (int)lines);
+  const MapStageResult m = map_stage(a.cfg, a.file, a.window ? a.line_start : -1,
+                                     a.window ? a.line_end : -1, path, a.spill_fmt);
+  const WordCountResult& r = m.result;
+  if (!cpu) std::printf("Length: %i\n", (int)m.lines);
   for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
   // event-timed on the GPU: H2D + map, then compaction/combine + sort
   std::printf("%s mapping %lld nanoseconds \n", dev, ns(r.times.h2d_ms + r.times.map_ms));
@@ -655,21 +598,20 @@ int run_map_stage(const CliArgs& a) {
               ns(r.times.process_ms + r.times.reduce_ms));
   if (!a.json.empty()) {
     JsonOut j = json_head(a, "map_stage");
-    r.num_lines = lines;
     json_counts(j, r);
-    j.u("spill_records", recs.size());
-    j.u("spill_bytes", idx.spill_bytes);
+    j.u("spill_records", m.spill_records);
+    j.u("spill_bytes", m.index.spill_bytes);
     j.str("spill", path);
     j.str("input", a.file);
     j.kv("line_start", std::to_string(a.window ? a.line_start : 0));
     j.kv("line_end", std::to_string(a.window ? a.line_end : -1));
     j.kv("combined", a.cfg.ref_compat ? "false" : "true");
-    j.kv("streamed", streamed ? "true" : "false");
-    j.u("input_bytes", bytes);
+    j.kv("streamed", m.streamed ? "true" : "false");
+    j.u("input_bytes", m.input_bytes);
     j.num("map_ms", r.times.h2d_ms + r.times.map_ms);
     j.num("process_ms", r.times.process_ms + r.times.reduce_ms);
-    j.num("job_ms", (t1 - t0) * 1e-6);
-    j.num("spill_write_ms", (t2 - t1) * 1e-6);
+    j.num("job_ms", m.job_ms);
+    j.num("spill_write_ms", m.spill_write_ms);
     j.u("peak_rss_kb", peak_rss_kb());
     emit_json(a, j.done());
   }

@@ -114,6 +114,74 @@ std::vector<PackedKey> plan_reducer_splitters(const std::vector<SpillIndex>& idx
   return spl;
 }
 
+MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, i64 line_start,
+                         i64 line_end, const std::string& spill, SpillFormat fmt) {
+  constexpr u64 kDefaultStreamChunk = 256ull << 20;
+  const bool cpu = cfg_in.backend == Backend::kCpu;
+  const bool window = line_start >= 0;
+  MapStageResult out;
+  WordCountResult& r = out.result;
+  std::vector<KeyCount> recs;
+  const u64 t0 = now_ns();
+  if (cpu || cfg_in.ref_compat) {
+    const bool use_window = window && !(cpu && cfg_in.ref_compat);
+    LoadedText text = load_lines(file, use_window ? line_start : -1, use_window ? line_end : -1,
+                                 cfg_in.ref_compat);
+    out.lines = text.input.num_lines;
+    out.input_bytes = text.input.bytes;
+    if (cfg_in.ref_compat) {
+      std::vector<PackedKey> toks;
+      if (cpu) {
+        toks = CpuWordCount(cfg_in).run_map_stage(text.input, &r);
+      } else {
+        GpuWordCount eng(cfg_in, std::max<u64>(out.input_bytes, 1), std::max<u64>(out.lines, 1));
+        toks = eng.run_map_stage(text.input, &r);
+      }
+      r.num_tokens = toks.size();
+      recs = tokens_to_records(toks);
+    } else {
+      r = CpuWordCount(cfg_in).run(text.input);
+      recs = entries_to_records(r.entries);
+    }
+  } else {
+    LineWindow w;
+    if (window)
+      w = find_line_window(file, line_start, line_end);
+    else
+      w.end = file_size(file);
+    out.input_bytes = w.end - w.begin;
+    JobConfig cfg = cfg_in;
+    cfg.graph = 0;  // stage events: the map and sort times
+    const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
+    if (out.input_bytes > chunk) {
+      cfg.chunk_bytes = chunk;
+      GpuWordCount eng(cfg, out.input_bytes, out.input_bytes);
+      auto src = open_file_range_source(file, w.begin, w.end);
+      r = eng.run_source(*src);
+      out.lines = src->lines();
+      out.streamed = true;
+    } else {
+      GpuWordCount eng(cfg, std::max<u64>(out.input_bytes, 1), std::max<u64>(out.input_bytes, 1));
+      TextInput in;
+      in.data = eng.input_buffer();
+      in.bytes = read_file_range_into(file, eng.input_buffer(), w.begin, out.input_bytes, &out.lines);
+      in.num_lines = out.lines;
+      r = eng.run(in);
+    }
+    recs = entries_to_records(r.entries);  // before the engine (and its buffers) goes
+    if (window) out.lines = w.lines;
+  }
+  r.entries = EntryList{};
+  r.num_lines = out.lines;
+  const u64 t1 = now_ns();
+  write_spill(spill, recs, fmt, &out.index);
+  write_spill_index(spill_index_path(spill), out.index);
+  out.spill_records = recs.size();
+  out.job_ms = (t1 - t0) * 1e-6;
+  out.spill_write_ms = (now_ns() - t1) * 1e-6;
+  return out;
+}
+
 namespace {
 
 // [lo, hi) membership; a null bound is open.

@@ -44,6 +44,25 @@ SpillIndex index_records(const std::vector<KeyCount>& recs);
 // (independent of the order of `idx`).
 std::vector<PackedKey> plan_reducer_splitters(const std::vector<SpillIndex>& idx, int reducers);
 
+// ---- stage 1 ----
+struct MapStageResult {
+  WordCountResult result;  // counts and stage times (entries released after the spill)
+  u64 lines = 0, input_bytes = 0;
+  u64 spill_records = 0;
+  bool streamed = false;   // the window streamed through the engine (larger than a pass)
+  double job_ms = 0, spill_write_ms = 0;
+  SpillIndex index;
+};
+// Stage 1 over the line window [line_start, line_end) of `file` (line_start < 0: the whole
+// file): the job's combined output -- one (key, count) record per distinct key, key order
+// -- spilled to `spill` in `fmt`, with its index at spill_index_path(spill).  GPU: the
+// window is found by find_line_window and read into the engine's pinned buffer, or
+// streamed past one device pass (chunk_bytes, default 256 MiB), with hipEvent stage times.
+// cfg.ref_compat: the reference's spill instead -- one record per token, sorted -- from the
+// reference's loader (the CPU build ignores the window and drops the last line, B1).
+MapStageResult map_stage(const JobConfig& cfg, const std::string& file, i64 line_start,
+                         i64 line_end, const std::string& spill, SpillFormat fmt);
+
 struct ReduceStageStats {
   u64 input_files = 0, indexed_files = 0, loaded_files = 0;
   u64 records_read = 0;  // spill records read (below the range and inside it)

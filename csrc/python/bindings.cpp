@@ -890,6 +890,30 @@ PYBIND11_MODULE(_locust, m) {
     return py::make_tuple(PyResult{std::move(r)}, d);
   }, py::arg("cfg"), py::arg("files"), py::arg("reducer") = 0, py::arg("reducers") = 1,
         "Stage 2 over spill files: (result, stats); key range `reducer` of `reducers`.");
+  m.def("map_stage", [](const JobConfig& cfg, const std::string& file, i64 s, i64 e,
+                        const std::string& spill, const std::string& fmt) {
+    MapStageResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = map_stage(cfg, file, s, e, spill,
+                    fmt == "binary" ? SpillFormat::kBinary : fmt == "kiv" ? SpillFormat::kKiv
+                                                                         : SpillFormat::kText);
+    }
+    py::dict d;
+    d["lines"] = r.lines;
+    d["tokens"] = r.result.num_tokens;
+    d["unique"] = r.result.num_unique;
+    d["spill_records"] = r.spill_records;
+    d["spill_bytes"] = r.index.spill_bytes;
+    d["input_bytes"] = r.input_bytes;
+    d["streamed"] = r.streamed;
+    d["map_ms"] = r.result.times.h2d_ms + r.result.times.map_ms;
+    d["process_ms"] = r.result.times.process_ms + r.result.times.reduce_ms;
+    d["job_ms"] = r.job_ms;
+    return d;
+  }, py::arg("cfg"), py::arg("file"), py::arg("line_start"), py::arg("line_end"),
+        py::arg("spill"), py::arg("fmt") = "binary",
+        "Stage 1 over a line window: the combined, indexed spill (see locust/stage.hpp).");
   m.def("partmap_cache_path", &partmap_cache_path, py::arg("input"), py::arg("cfg"));
   m.def("load_partmap_cache", [](const std::string& path) -> py::object {
     std::vector<u64> lo;

@@ -46,6 +46,8 @@ from .config import make_config, make_dist_config  # noqa: E402
 from .models.wordcount import (  # noqa: E402
     Engine,
     WordCount,
+    map_stage,
+    reduce_stage,
     run_multi,
     wordcount_file,
     wordcount_text,
@@ -65,6 +67,8 @@ __all__ = [
     "make_dist_config",
     "Engine",
     "WordCount",
+    "map_stage",
+    "reduce_stage",
     "run_multi",
     "wordcount_file",
     "wordcount_text",

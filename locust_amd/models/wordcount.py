@@ -80,6 +80,24 @@ def wordcount_file(path: str, line_start: int = -1, line_end: int = -1, backend:
     return Engine(cfg, max(len(text), 1), max(nlines, 1)).run(text)
 
 
+def map_stage(path: str, spill: str, line_start: int = -1, line_end: int = -1,
+              backend: str = "gpu", fmt: str = "binary", cfg=None, **kw) -> dict:
+    """Stage 1 of the reference's split job (main.cu:421-433), count-carrying: the line
+    window's combined (key, count) records -> ``spill`` (+ ``spill + ".idx"``); returns
+    the counts, spill size and stage times.  ``fmt``: text | binary | kiv."""
+    cfg = cfg if cfg is not None else make_config(backend, **kw)
+    return _C.map_stage(cfg, path, line_start, line_end, spill, fmt)
+
+
+def reduce_stage(spills: list[str], reducer: int = 0, reducers: int = 1,
+                 backend: str = "gpu", cfg=None, **kw):
+    """Stage 2: key range ``reducer`` of ``reducers`` over the spills, merged with counts
+    summed (the device merge on the GPU); returns (result, stats).  The result's entries
+    carry the global val; concatenating reducers 0..R-1 gives the single-stage result."""
+    cfg = cfg if cfg is not None else make_config(backend, **kw)
+    return _C.reduce_spills(cfg, list(spills), reducer, reducers)
+
+
 def run_multi(text: bytes, world: int, backend: str = "gpu", combine: bool = True,
               samples_per_rank: int = 64, strategy: str | None = None, comm: str = "auto",
               **kw):

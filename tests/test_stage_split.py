@@ -260,3 +260,19 @@ def test_gpu_stage1_streams_large_window(cli, tmp_path):
     run(cli, f, 50_000, 350_000, 1, 1, "--backend", "cpu", "--spill-dir", tmp_path,
         "--spill-format", "binary")
     assert lc._C.read_spill(str(tmp_path / "out.0.kv")) == lc._C.read_spill(str(tmp_path / "out.1.kv"))
+
+
+def test_python_stage_api(hamlet, tmp_path):
+    """locust_amd.map_stage / reduce_stage: the stage split from Python."""
+    f = tmp_path / "h.txt"
+    f.write_bytes(hamlet)
+    spills = []
+    for k, (s, e) in enumerate([(0, 2000), (2000, 4463)]):
+        spills.append(str(tmp_path / f"s{k}.kv"))
+        m = lc.map_stage(str(f), spills[-1], s, e, backend="cpu")
+        assert m["lines"] == e - s and m["spill_records"] == m["unique"]
+    got = []
+    for r in range(2):
+        res, st = lc.reduce_stage(spills, r, 2, backend="cpu")
+        got += res.entries()
+    assert got == oracle.wordcount(hamlet)[0]
