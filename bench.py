@@ -192,6 +192,11 @@ def _time_single(text, steps: int, warmup: int, sort: str, graph: int):
         run = lambda: eng.run_text(text)  # noqa: E731
     for _ in range(warmup):
         res = run()
+    # the end of the warmup: the partition map's retune from the first job's output runs on
+    # the engine's worker thread; take it now rather than a few timed jobs in (a short
+    # warmup -- the driver's is 5 jobs -- can end before the worker does)
+    if warmup:
+        eng.partition_map()
     # The timed loop is the jobs alone (each returns its complete result object); the
     # per-stage bookkeeping is a separate pass so the harness is not inside the timing.
     t0 = time.perf_counter()
