@@ -955,6 +955,8 @@ void DevicePipeline::enqueue_dict_ordered(bool with_counts, bool mapped, bool se
   ex.pm = part_map();
   ex.part_w = d_pw;
   ex.split_min = split_min;
+  ex.split_floor = split_floor;
+  ex.split_fused = split_fused;
   if (self_clean) set_self_clean(ex);
   if (self_clean && done_pending) {  // the kernel itself tells the host it is done
     ex.host_done = d_done;
@@ -1142,11 +1144,11 @@ void DevicePipeline::print_ord_trace() {
     std::fprintf(stderr,
                  "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
                  " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
-                 " | clear=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu"
+                 " | clear=%5llu fill=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu"
                  " | waited=%6.2f us\n",
                  p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
                  d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
-                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16),
+                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 26), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16),
                  x[20] ? (x[20] - x[10]) * 0.01 : 0.0);
   }
 }
@@ -1167,6 +1169,8 @@ bool DevicePipeline::enqueue_map_ordered(const TextInput& in) {
   ex.pm = part_map();
   ex.part_w = d_pw;
   ex.split_min = split_min;
+  ex.split_floor = split_floor;
+  ex.split_fused = split_fused;
   set_self_clean(ex);
   if (done_pending) {  // the kernel itself tells the host it is done
     ex.host_done = d_done;

@@ -167,6 +167,16 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_SPLIT_MIN");
     return e ? (u32)std::max(0, std::atoi(e)) : 0u;
   }();
+  // LOCUST_SPLIT_FLOOR (read at construction): a partition of fewer tokens never splits
+  const u32 split_floor = [] {
+    const char* e = std::getenv("LOCUST_SPLIT_FLOOR");
+    return e ? (u32)std::max(0, std::atoi(e)) : 0u;
+  }();
+  // LOCUST_SPLIT_FUSED=0 (A/B): siblings gather their samples and their tokens separately
+  const u32 split_fused = [] {
+    const char* e = std::getenv("LOCUST_SPLIT_FUSED");
+    return e && e[0] == '0' ? 0u : 1u;
+  }();
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {

@@ -326,6 +326,8 @@ struct OrderedExtra {
   // at most kPartBlock tiles; larger ones keep one workgroup per partition.)
   const u32* part_occ = nullptr;
   u32 split_min = 0;            // planned workgroups: tokens per extra sibling (0: default)
+  u32 split_floor = 0;          // ... and the fewest tokens of a partition that splits at all
+  u32 split_fused = 1;          // siblings: one gather for the samples and the inserts
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};
   // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x

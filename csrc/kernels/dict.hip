@@ -272,8 +272,60 @@ __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 
 // round (the tokens were written by the map on other XCDs: these are L2 misses).  Longer
 // keys' further words are rare (English words fit in 8 bytes) and gathered after.
 constexpr int kGatherBatch = 4;
-// [rlo, rhi) (rlast: no upper bound): only keys whose first word lies in the range are
-// inserted (a virtual partition's share of its map partition; the default takes all).
+// Inserts one batch of gathered tokens: k[r][0] (and k[r][1] if eager_w1) and c[r] are
+// loaded for list entry idx[r].  [rlo, rhi) (rlast: no upper bound): only keys whose first
+// word lies in the range are inserted (a virtual partition's share of its map partition;
+// the default takes all); the further words of those are gathered here.
+template <int kB>
+__device__ __forceinline__ bool insert_gathered(ConstKeysSoA tokens, const u32* idx,
+                                                u64 (*k)[kKeyWords], u64* c, LdsSlot* s_tab,
+                                                u64 rlo, u64 rhi, bool rlast, bool eager_w1,
+                                                bool weighted) {
+  bool full = false;
+#pragma unroll
+  for (int r = 0; r < kB; ++r)  // outside the range: neither gathered nor inserted
+    if (k[r][0] < rlo || (!rlast && k[r][0] >= rhi)) k[r][0] = 0;
+#pragma unroll
+  for (int r = 0; r < kB; ++r) {
+    if (!(k[r][0] & 0xffull))
+      k[r][1] = 0;
+    else if (!eager_w1)
+      k[r][1] = tokens.w[1][idx[r]];
+  }
+#pragma unroll
+  for (int r = 0; r < kB; ++r)
+    if (k[r][1] & 0xffull) {
+      k[r][2] = tokens.w[2][idx[r]];
+      if (k[r][2] & 0xffull) k[r][3] = tokens.w[3][idx[r]];
+    }
+#pragma unroll
+  for (int r = 0; r < kB; ++r) {
+    bool live = k[r][0] != 0 && c[r] != 0;
+    // Hot keys: the lanes holding the same key as the wave's first live lane are combined
+    // into one insert by that lane (Zipfian text: a hot partition's waves are mostly one
+    // or two keys, and 64 LDS atomics on one slot serialise).
+    const u64 lm = dev::ballot(live);
+    if (lm) {
+      const int L = __ffsll((unsigned long long)lm) - 1;
+      bool same = live;
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) {
+        const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)k[r][j], L);
+        const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(k[r][j] >> 32), L);
+        same &= k[r][j] == (((u64)hi << 32) | lo);
+      }
+      const u64 sm = dev::ballot(same);
+      if (__popcll(sm) > 1) {
+        const u64 tot = weighted ? dev::wave_reduce_sum(same ? c[r] : 0ull) : (u64)__popcll(sm);
+        if (dev::lane_id() == L) c[r] = tot;
+        else if (same) live = false;
+      }
+    }
+    if (live) full |= !part_lds_insert(s_tab, k[r], c[r], key_hash(k[r]));
+  }
+  return full;
+}
+
 template <int kGatherBatch = kGatherBatch>
 // eager_w1: load key word 1 of every token together with word 0 (one round trip for
 // the keys of 8-15 bytes, whose word 1 was a second, dependent load); word 1 of a
@@ -300,49 +352,30 @@ __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* co
       c[r] = ok ? (counts ? counts[idx[r]] : 1ull) : 0;
       k[r][2] = k[r][3] = 0;
     }
-#pragma unroll
-    for (int r = 0; r < kGatherBatch; ++r)  // outside the range: neither gathered nor inserted
-      if (k[r][0] < rlo || (!rlast && k[r][0] >= rhi)) k[r][0] = 0;
-#pragma unroll
-    for (int r = 0; r < kGatherBatch; ++r) {
-      if (!(k[r][0] & 0xffull))
-        k[r][1] = 0;
-      else if (!eager_w1)
-        k[r][1] = tokens.w[1][idx[r]];
-    }
-#pragma unroll
-    for (int r = 0; r < kGatherBatch; ++r)
-      if (k[r][1] & 0xffull) {
-        k[r][2] = tokens.w[2][idx[r]];
-        if (k[r][2] & 0xffull) k[r][3] = tokens.w[3][idx[r]];
-      }
-#pragma unroll
-    for (int r = 0; r < kGatherBatch; ++r) {
-      bool live = k[r][0] != 0 && c[r] != 0;
-      // Hot keys: the lanes holding the same key as the wave's first live lane are combined
-      // into one insert by that lane (Zipfian text: a hot partition's waves are mostly one
-      // or two keys, and 64 LDS atomics on one slot serialise).
-      const u64 lm = dev::ballot(live);
-      if (lm) {
-        const int L = __ffsll((unsigned long long)lm) - 1;
-        bool same = live;
-#pragma unroll
-        for (int j = 0; j < kKeyWords; ++j) {
-          const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)k[r][j], L);
-          const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(k[r][j] >> 32), L);
-          same &= k[r][j] == (((u64)hi << 32) | lo);
-        }
-        const u64 sm = dev::ballot(same);
-        if (__popcll(sm) > 1) {
-          const u64 tot = counts ? dev::wave_reduce_sum(same ? c[r] : 0ull) : (u64)__popcll(sm);
-          if (dev::lane_id() == L) c[r] = tot;
-          else if (same) live = false;
-        }
-      }
-      if (live) full |= !part_lds_insert(s_tab, k[r], c[r], key_hash(k[r]));
-    }
+    full |= insert_gathered<kGatherBatch>(tokens, idx, k, c, s_tab, rlo, rhi, rlast, eager_w1,
+                                          counts != nullptr);
   }
   return full;
+}
+
+// Ascending sort of one u64 per lane across the wave (bitonic network over the 64 lanes).
+__device__ __forceinline__ u64 wave_sort_u64(u64 x) {
+  const u32 lane = (u32)dev::lane_id();
+#pragma unroll
+  for (u32 k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (u32 j = k >> 1; j; j >>= 1) {
+      const u64 o = __shfl_xor((unsigned long long)x, (int)j, 64);
+      const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      x = keep_min ? (o < x ? o : x) : (o > x ? o : x);
+    }
+  return x;
+}
+
+__device__ __forceinline__ u64 readlane_u64(u64 x, u32 lane) {
+  const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)x, (int)lane);
+  const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(x >> 32), (int)lane);
+  return ((u64)hi << 32) | lo;
 }
 
 // Per round: every thread loads 16 partition bytes (the next round's load is issued before
@@ -682,9 +715,13 @@ struct TileSource {
   // it the same way and agree on every cut: each key lands in exactly one sibling, which
   // then inserts only its own range.  `pre`: this thread's run (tile threadIdx.x; the plan
   // admits at most kPartBlock tiles).
+  // fused (LOCUST_SPLIT_FUSED, default on; a partition of at most kGatherBatch x 1,024
+  // tokens): the tokens' first two words are loaded once, the samples taken from those
+  // registers and sorted by every wave in registers -- one global round trip per sibling
+  // instead of two, and no LDS rank pass (the cuts are the same: same sample positions).
   static constexpr u32 kSplitSamples = 64;
   __device__ bool build_split(u32 p, Pre pre, u32 j, u32 K, LdsSlot* s_tab, u32* s_list,
-                              u32* s_scan, u64* stamp) const {
+                              u32* s_scan, u64* stamp, bool fused) const {
     u64* s_samp = reinterpret_cast<u64*>(s_list + kPartWindow - 256);  // [64]
     u64* s_sort = reinterpret_cast<u64*>(s_list + kPartWindow - 128);  // [64]
     const u32 a = pre.a, len = threadIdx.x < ntiles ? pre.b - pre.a : 0u;
@@ -693,7 +730,50 @@ struct TileSource {
     const u32 lim = min(n, (u32)kPartWindow - 256);  // the sample area sits at the list's end
     for (u32 k = 0; k < len && at + k < lim; ++k) s_list[at + k] = a + k;
     __syncthreads();
+    if (stamp && threadIdx.x == 0) stamp[26] = __builtin_amdgcn_s_memtime();
     const u32 S = lim < kSplitSamples ? lim : kSplitSamples;
+    const bool last = j + 1 >= K;
+    // a list cut short by the sample area is an overflow: the host redoes the pass
+    bool full = n > lim;
+    if (fused && lim <= (u32)(kGatherBatch * kPartBlock)) {
+      u32 idx[kGatherBatch];
+      u64 k[kGatherBatch][kKeyWords];
+      u64 c[kGatherBatch];
+#pragma unroll
+      for (int r = 0; r < kGatherBatch; ++r) {
+        const u32 e = (u32)r * kPartBlock + threadIdx.x;
+        idx[r] = e < lim ? s_list[e] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int r = 0; r < kGatherBatch; ++r) {
+        const bool ok = idx[r] < n_cap;
+        k[r][0] = ok ? tokens.w[0][idx[r]] : 0;
+        k[r][1] = ok ? tokens.w[1][idx[r]] : 0;
+        c[r] = ok ? 1ull : 0ull;
+        k[r][2] = k[r][3] = 0;
+      }
+      // list position e is sample s when s = ceil(e S / lim) lands on it (S <= lim: the
+      // positions floor(s lim / S) are distinct)
+#pragma unroll
+      for (int r = 0; r < kGatherBatch; ++r) {
+        const u32 e = (u32)r * kPartBlock + threadIdx.x;
+        if (e < lim) {
+          const u32 sidx = (u32)(((u64)e * S + lim - 1) / lim);
+          if (sidx < S && (u32)((u64)sidx * lim / S) == e) s_samp[sidx] = idx[r] < n_cap ? k[r][0] : 0ull;
+        }
+      }
+      __syncthreads();
+      const u32 lane = (u32)dev::lane_id();
+      const u64 srt = wave_sort_u64(lane < S ? s_samp[lane] : ~0ull);  // the S samples first
+      const u64 lo = j == 0 || !S ? 0ull : readlane_u64(srt, (u32)((u64)j * S / K));
+      const u64 hi = last || !S ? ~0ull : readlane_u64(srt, (u32)((u64)(j + 1) * S / K));
+      if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
+      if (!(lo == hi && !last))
+        full |= insert_gathered<kGatherBatch>(tokens, idx, k, c, s_tab, lo, hi, last, true, false);
+      if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
+      __syncthreads();  // the list area is reused after the build
+      return full;
+    }
     if (threadIdx.x < S) {
       const u32 idx = s_list[(u32)((u64)threadIdx.x * lim / S)];
       s_samp[threadIdx.x] = idx < n_cap ? tokens.w[0][idx] : 0ull;
@@ -709,12 +789,9 @@ struct TileSource {
       s_sort[r] = w;
     }
     __syncthreads();
-    const bool last = j + 1 >= K;
     const u64 lo = j == 0 || !S ? 0ull : s_sort[(u64)j * S / K];
     const u64 hi = last || !S ? ~0ull : s_sort[(u64)(j + 1) * S / K];
     if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
-    // a list cut short by the sample area is an overflow: the host redoes the pass
-    bool full = n > lim;
     if (!(lo == hi && !last))  // else an empty range (a hot first word took it)
       full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last, true);
     if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
@@ -1065,7 +1142,8 @@ __device__ __forceinline__ void ordered_partition(
     u32 K = 0;
     if (occupied) {
       const u32 extra = T ? (u32)((u64)tp * (u32)(kDictParts - E) / T) : 0u;
-      K = 1u + min(extra, tp / (ex.split_min ? ex.split_min : kSplitMinTokens));
+      K = tp < ex.split_floor ? 1u
+                              : 1u + min(extra, tp / (ex.split_min ? ex.split_min : kSplitMinTokens));
     }
     u32 kinc = 0;
     if (threadIdx.x < kDictParts) {
@@ -1100,6 +1178,7 @@ __device__ __forceinline__ void ordered_partition(
     trace[(u64)v * 32 + 17] = ~0ull;
     trace[(u64)v * 32 + 18] = 0;
     trace[(u64)v * 32 + 19] = 0;
+    trace[(u64)v * 32 + 26] = 0;
   }
   const typename Src::Pre first =
       vplan ? (vk ? src.prefetch(p) : typename Src::Pre{})
@@ -1121,7 +1200,7 @@ __device__ __forceinline__ void ordered_partition(
   if constexpr (kTiles) {
     if (vk > 1)
       full = src.build_split(p, first, vj, vk, s_tab, s_list, reinterpret_cast<u32*>(s_scan),
-                             trace ? trace + (u64)v * 32 : nullptr);
+                             trace ? trace + (u64)v * 32 : nullptr, ex.split_fused != 0);
     else if (vk == 1)
       full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr);
   } else {

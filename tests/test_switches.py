@@ -30,6 +30,8 @@ CASES = [
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PART_DEFAULT": "byte"}, "single"),
     ({"LOCUST_VPLAN": "0", "LOCUST_DEVPLAN": "0"}, "single"),
     ({"LOCUST_VPLAN_MIN_KB": "64", "LOCUST_SPLIT_MIN": "256"}, "single"),
+    ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FUSED": "0"}, "single"),
+    ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FLOOR": "512"}, "single"),
     ({"LOCUST_DEV_CACHE": "0"}, "stream"),
     ({"LOCUST_DEV_CACHE_GB": "1", "LOCUST_CHUNK_MB": "1"}, "stream"),
     ({"LOCUST_ORD_TRACE": "1", "LOCUST_MAP_TRACE": "1", "LOCUST_ROCTX": "0",
