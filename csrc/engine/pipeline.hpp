@@ -177,6 +177,11 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_SPLIT_FUSED");
     return e && e[0] == '0' ? 0u : 1u;
   }();
+  // LOCUST_RANK_W0=0 (A/B): the all-pairs ranking reads all four key words per candidate
+  const u32 rank_w0 = [] {
+    const char* e = std::getenv("LOCUST_RANK_W0");
+    return e && e[0] == '0' ? 0u : 1u;
+  }();
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {

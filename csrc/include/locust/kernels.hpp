@@ -328,6 +328,7 @@ struct OrderedExtra {
   u32 split_min = 0;            // planned workgroups: tokens per extra sibling (0: default)
   u32 split_floor = 0;          // ... and the fewest tokens of a partition that splits at all
   u32 split_fused = 1;          // siblings: one gather for the samples and the inserts
+  u32 rank_w0 = 1;              // all-pairs ranks: further key words read only on a first-word tie
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};
   // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x

@@ -1349,28 +1349,55 @@ __device__ __forceinline__ void ordered_partition(
         const u32 j0 = sl * m / S, j1 = (sl + 1) * m / S;
         u32 cnt = 0;
         u32 wcnt = 0;  // compact words of the smaller keys: this key's compact offset
-        for (u32 j = j0; j < j1; j += 4) {
-          u64 c0[4], c1[4], c2[4], c3[4];
-          u32 cw[4];
+        if (ex.rank_w0) {
+          // first words only (12 of the 36 LDS bytes per candidate): the further words are
+          // read for a candidate whose first word equals this key's -- rare (keys of 8+
+          // bytes sharing their first 8), and a divergent branch
+          for (u32 j = j0; j < j1; j += 4) {
+            u64 c0[4];
+            u32 cw[4];
 #pragma unroll
-          for (u32 q = 0; q < 4; ++q) {
-            const bool in = j + q < j1;
-            const u32 jj = in ? j + q : j0;
-            c0[q] = s_w0[jj];
-            c1[q] = s_k123[3 * jj];
-            c2[q] = s_k123[3 * jj + 1];
-            c3[q] = s_k123[3 * jj + 2];
-            cw[q] = s_cw[jj];
+            for (u32 q = 0; q < 4; ++q) {
+              const u32 jj = j + q < j1 ? j + q : j0;
+              c0[q] = s_w0[jj];
+              cw[q] = s_cw[jj];
+            }
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) {
+              const u32 jj = j + q;
+              bool lt = jj < j1 && c0[q] < k0;
+              if (jj < j1 && c0[q] == k0 && jj != i) {
+                const u64 c1 = s_k123[3 * jj], c2 = s_k123[3 * jj + 1], c3 = s_k123[3 * jj + 2];
+                lt = c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)));
+              }
+              cnt += lt ? 1u : 0u;
+              wcnt += lt ? cw[q] : 0u;
+            }
           }
+        } else {
+          for (u32 j = j0; j < j1; j += 4) {
+            u64 c0[4], c1[4], c2[4], c3[4];
+            u32 cw[4];
 #pragma unroll
-          for (u32 q = 0; q < 4; ++q) {
-            // (a bitwise, branch-free form of this compare measured 1 % slower here: the
-            // short-circuit exits early for most candidates, whose first words differ)
-            const bool lt = j + q < j1 &&
-                            (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
-                             (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
-            cnt += lt ? 1u : 0u;
-            wcnt += lt ? cw[q] : 0u;
+            for (u32 q = 0; q < 4; ++q) {
+              const bool in = j + q < j1;
+              const u32 jj = in ? j + q : j0;
+              c0[q] = s_w0[jj];
+              c1[q] = s_k123[3 * jj];
+              c2[q] = s_k123[3 * jj + 1];
+              c3[q] = s_k123[3 * jj + 2];
+              cw[q] = s_cw[jj];
+            }
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) {
+              // (a bitwise, branch-free form of this compare measured 1 % slower here: the
+              // short-circuit exits early for most candidates, whose first words differ)
+              const bool lt = j + q < j1 &&
+                              (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
+                               (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
+              cnt += lt ? 1u : 0u;
+              wcnt += lt ? cw[q] : 0u;
+            }
           }
         }
         if (trace)
