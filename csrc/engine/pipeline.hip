@@ -1145,11 +1145,11 @@ void DevicePipeline::print_ord_trace() {
     std::fprintf(stderr,
                  "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
                  " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
-                 " | clear=%5llu fill=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu"
+                 " | clear=%5llu scan=%5llu fill=%5llu ld=%5llu srt=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu"
                  " | waited=%6.2f us\n",
                  p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
                  d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
-                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 26), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16),
+                 (x[11] - first_in) * 0.01, d(0, 14), d(14, 28), d(28, 26), d(26, 27), d(27, 12), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16),
                  x[20] ? (x[20] - x[10]) * 0.01 : 0.0);
   }
 }
@@ -1268,6 +1268,7 @@ void DevicePipeline::set_compact_out(OrderedExtra& ex, bool mapped) {
   ex.cout = reinterpret_cast<u64*>(d_out_mapped);
   ex.ctab = d_ctab_mapped;
   ex.out_cap = std::min<u64>(ex.out_cap, h_out_cap);
+  ex.reserve = ord_reserve && ex.self_clean && !ex.recs && !ex.sorted.w[0] && !ex.hdr;
 }
 
 void DevicePipeline::copy_out(EntryList& e, u64 u, bool compact) {
@@ -1278,12 +1279,14 @@ void DevicePipeline::copy_out(EntryList& e, u64 u, bool compact) {
   std::vector<EntrySegment> segs;
   segs.reserve(64);
   const u64* words = reinterpret_cast<const u64*>(h_out);
-  u64 at = 0;  // entries before v: its segment starts at word kOutWords * at
+  u64 at = 0;  // entries so far
   for (int v = 0; v < kDictParts; ++v) {
     const u64 t = h_ctab[v];
     LOCUST_CHECK_ARG(t != ~0ull, "compact output: partition " + std::to_string(v) + " not written");
-    const u64 m = t & 0xffffffffull;
-    if (m) segs.push_back({words + kOutWords * at, m});
+    const u64 m = t & 0xffffull, first = t >> 32;  // first: where its entries start
+    LOCUST_CHECK_ARG(first + m <= h_out_cap, "compact output: partition " + std::to_string(v) +
+                                                 " past the buffer");
+    if (m) segs.push_back({words + kOutWords * first, m});
     at += m;
   }
   LOCUST_CHECK_ARG(at == u, "compact output: " + std::to_string(at) + " entries, expected " +

@@ -182,6 +182,13 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_RANK_W0");
     return e && e[0] == '0' ? 0u : 1u;
   }();
+  // LOCUST_ORD_RESERVE=1: the host-output ordered build reserves its partitions' output
+  // with an atomic instead of placing it by the look-back (OrderedExtra::reserve; measured
+  // no faster: the span shrinks, the PCIe drain of the records moves into the tail)
+  const bool ord_reserve = [] {
+    const char* e = std::getenv("LOCUST_ORD_RESERVE");
+    return e && e[0] == '1';
+  }();
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {

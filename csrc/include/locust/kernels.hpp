@@ -341,9 +341,16 @@ struct OrderedExtra {
   // records at `out`: virtual partition v writes its entries, in key order, from word
   // 5 * (entries before v) of `cout` -- where its 40-B records would have started, so the
   // look-back is unchanged and the capacity is out_cap records' worth of words -- and
-  // ctab[v] = entries | words << 32 (host-mapped, every v of the launch; ~0: not written).
+  // ctab[v] = entries | words << 16 | first entry << 32 (host-mapped, every v of the launch;
+  // ~0: not written).
   u64* cout = nullptr;
   u64* ctab = nullptr;
+  // With cout + self_clean, no recs / sorted / hdr: no look-back -- a virtual partition
+  // reserves its entries with one atomic on status[kDictParts] (arrival order, not key
+  // order: ctab[v] carries where they went), so no workgroup waits for the slowest one
+  // before it; the last workgroup to finish publishes the totals (LOCUST_ORD_RESERVE=1;
+  // off by default: docs/PERFORMANCE.md round 5).
+  bool reserve = false;
   // The fused map + ordered kernel's counters ([0] ticket, [1] tiles done; zeroed before
   // the launch, re-zeroed by the self-clean): launch_map_ordered.
   u32* fuse = nullptr;

@@ -728,6 +728,7 @@ struct TileSource {
     u32 n = 0;
     const u32 at = dev::block_exclusive_scan<u32, kPartBlock>(len, s_scan, &n);
     const u32 lim = min(n, (u32)kPartWindow - 256);  // the sample area sits at the list's end
+    if (stamp && threadIdx.x == 0) stamp[28] = __builtin_amdgcn_s_memtime();
     for (u32 k = 0; k < len && at + k < lim; ++k) s_list[at + k] = a + k;
     __syncthreads();
     if (stamp && threadIdx.x == 0) stamp[26] = __builtin_amdgcn_s_memtime();
@@ -762,6 +763,7 @@ struct TileSource {
           if (sidx < S && (u32)((u64)sidx * lim / S) == e) s_samp[sidx] = idx[r] < n_cap ? k[r][0] : 0ull;
         }
       }
+      if (stamp && threadIdx.x == 0) stamp[27] = __builtin_amdgcn_s_memtime();  // its loads are in
       __syncthreads();
       const u32 lane = (u32)dev::lane_id();
       const u64 srt = wave_sort_u64(lane < S ? s_samp[lane] : ~0ull);  // the S samples first
@@ -1179,6 +1181,8 @@ __device__ __forceinline__ void ordered_partition(
     trace[(u64)v * 32 + 18] = 0;
     trace[(u64)v * 32 + 19] = 0;
     trace[(u64)v * 32 + 26] = 0;
+    trace[(u64)v * 32 + 27] = 0;
+    trace[(u64)v * 32 + 28] = 0;
   }
   const typename Src::Pre first =
       vplan ? (vk ? src.prefetch(p) : typename Src::Pre{})
@@ -1274,14 +1278,22 @@ __device__ __forceinline__ void ordered_partition(
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
-  if (threadIdx.x == 0) dev::publish_aggregate(status, v, agg);
+  // (ex.reserve: no look-back -- the workgroup reserves its output words with one atomic
+  // on status[kDictParts] below, in arrival order, and ctab[v] tells the host where)
+  if (threadIdx.x == 0 && !ex.reserve) dev::publish_aggregate(status, v, agg);
   ORD_STAMP(2);
   u64 pre = 0;
   u32 cwords = ~0u;  // compact words written (ex.cout), ~0u: none
   if (small) {
     // ---- small partition: all-pairs ranks: rank_i = #{j : key_j < key_i}, the sorted
     // position in one pass, no bucket sort.  Wave 0 resolves the look-back meanwhile. ----
-    if (dev::wave_id() == 0) {
+    if (dev::wave_id() == 0 && ex.reserve) {
+      if (dev::lane_id() == 0) {
+        s_prefix = atomicAdd(reinterpret_cast<unsigned long long*>(&status[kDictParts]),
+                             (unsigned long long)agg);
+        if (trace) trace[(u64)v * 32 + 15] = __builtin_amdgcn_s_memtime();  // reserved
+      }
+    } else if (dev::wave_id() == 0) {
       // Look-back in ONE round trip: wave 0 reads every predecessor's status word at once
       // (4 per lane, p < 256) instead of walking back 64 words per dependent round trip
       // (~1-2 us each across XCDs).  prefix = the highest inclusive value found + the
@@ -1414,7 +1426,7 @@ __device__ __forceinline__ void ordered_partition(
     }
     __syncthreads();
     pre = s_prefix;
-    if (threadIdx.x == 0 && v != 0)  // inclusive value for later walkers (large partitions)
+    if (threadIdx.x == 0 && v != 0 && !ex.reserve)  // inclusive value for later walkers
       dev::st_agent(&status[v], dev::kLbInc | (pre + agg));
     ORD_STAMP(3);
     ORD_STAMP(4);
@@ -1595,8 +1607,14 @@ __device__ __forceinline__ void ordered_partition(
   __syncthreads();
   ORD_STAMP(3);
   if (dev::wave_id() == 0) {
-    const u64 e = dev::wave_lookback_resolve(status, v, agg);
-    if (dev::lane_id() == 0) s_prefix = e;
+    if (ex.reserve) {
+      if (dev::lane_id() == 0)
+        s_prefix = atomicAdd(reinterpret_cast<unsigned long long*>(&status[kDictParts]),
+                             (unsigned long long)agg);
+    } else {
+      const u64 e = dev::wave_lookback_resolve(status, v, agg);
+      if (dev::lane_id() == 0) s_prefix = e;
+    }
   }
   __syncthreads();
   pre = s_prefix;
@@ -1648,7 +1666,8 @@ __device__ __forceinline__ void ordered_partition(
   const u32 ovf_before = (u32)((pre >> kOrdOvfShift) & 511u);
   ORD_STAMP(5);
   if (ex.ctab && threadIdx.x == 0)
-    ex.ctab[v] = cwords == ~0u ? ~0ull : (u64)m | ((u64)cwords << 32);
+    ex.ctab[v] = cwords == ~0u ? ~0ull : (u64)m | ((u64)cwords << 16) | (base_m << 32);
+  static_assert((u64)kPartSlots * kCompactMaxWords < (1u << 16), "ctab: entries / words fields");
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 6] = m;
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + 11] = __builtin_amdgcn_s_memrealtime();
   if (ex.part_w && threadIdx.x == 0 && vj == 0 && vk > 0) {  // partition work, for the retuning
@@ -1656,11 +1675,9 @@ __device__ __forceinline__ void ordered_partition(
     const u64 w = (tok + (u64)kPartDistinctWeight * m) * (vplan ? vk : 1u);
     ex.part_w[p] = (u32)(w < 0xffffffffull ? w : 0xffffffffull);
   }
-  // ---- the last partition publishes the run's counters ----
-  const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
-  if (v == kDictParts - 1 && threadIdx.x == 0) {
-    const u32 u = (u32)(base_m + m);
-    const u64 total = base_tok + tok;
+  // ---- the run's counters: the last partition's look-back prefix, or (ex.reserve) the
+  // reservation word's total, read by the last workgroup to finish ----
+  auto publish_totals = [&](u32 u, u64 total, u64 ovf_total) {
     ctr->num_unique = u;
     ctr->total_count = total;
     if (ovf_total) ctr->flags |= kCtrDictOverflow;
@@ -1691,7 +1708,10 @@ __device__ __forceinline__ void ordered_partition(
       hd->pad[0] = ex.tmpl.pad[0];
       hd->pad[1] = ex.tmpl.pad[1];
     }
-  }
+  };
+  const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
+  if (!ex.reserve && v == kDictParts - 1 && threadIdx.x == 0)
+    publish_totals((u32)(base_m + m), base_tok + tok, ovf_total);
   if (ex.self_clean) {
     // Self-cleaning job: the LAST workgroup to finish (not partition 255 -- a partition
     // resolves its prefix from its predecessors' aggregates, so later ones may finish
@@ -1714,7 +1734,14 @@ __device__ __forceinline__ void ordered_partition(
     if (s_count) {
       // acquire every other workgroup's (acquire only: this one released its own already)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ex.reserve) {  // every workgroup has added its aggregate: the run's totals
+        const u64 tot = __hip_atomic_load(&status[kDictParts], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        const u64 ovf = (tot >> kOrdOvfShift) & 511u;
+        if (threadIdx.x == 0) publish_totals((u32)(tot & kOrdM), tot >> kOrdTokShift, ovf);
+        if (ovf) flags |= kCtrDictOverflow;
+      }
       // Tell the host first: every workgroup's records, counters and headers are out (each
       // released them before counting itself done).  The re-zeroing below touches device
       // scratch only, which the next job's kernels -- behind this one on the stream -- see
@@ -1724,7 +1751,7 @@ __device__ __forceinline__ void ordered_partition(
                            __HIP_MEMORY_SCOPE_SYSTEM);
       if (!(flags & kCtrDictOverflow)) {
         for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
-        for (u32 i = threadIdx.x; i < (u32)kDictParts; i += kPartBlock) status[i] = 0;
+        for (u32 i = threadIdx.x; i <= (u32)kDictParts; i += kPartBlock) status[i] = 0;
         if (threadIdx.x == 0) {
           // the accumulated counters; num_unique / total_count are assignments the next
           // run overwrites, and stay readable for what follows this kernel
