@@ -958,6 +958,8 @@ void DevicePipeline::enqueue_dict_ordered(bool with_counts, bool mapped, bool se
   ex.split_floor = split_floor;
   ex.split_fused = split_fused;
   ex.rank_w0 = rank_w0;
+  ex.early_publish = early_publish;
+  ex.small_table = small_table;
   if (self_clean) set_self_clean(ex);
   if (self_clean && done_pending) {  // the kernel itself tells the host it is done
     ex.host_done = d_done;
@@ -1173,6 +1175,8 @@ bool DevicePipeline::enqueue_map_ordered(const TextInput& in) {
   ex.split_floor = split_floor;
   ex.split_fused = split_fused;
   ex.rank_w0 = rank_w0;
+  ex.early_publish = early_publish;
+  ex.small_table = small_table;
   set_self_clean(ex);
   if (done_pending) {  // the kernel itself tells the host it is done
     ex.host_done = d_done;

@@ -182,6 +182,17 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_RANK_W0");
     return e && e[0] == '0' ? 0u : 1u;
   }();
+  // LOCUST_EARLY_PUBLISH=0 (A/B): the ordered kernel publishes its aggregate after writing
+  // the compacted key arrays instead of before
+  const u32 early_publish = [] {
+    const char* e = std::getenv("LOCUST_EARLY_PUBLISH");
+    return e && e[0] == '0' ? 0u : 1u;
+  }();
+  // LOCUST_SMALL_TABLE=0 (A/B): every ordered-kernel partition clears its whole LDS table
+  const u32 small_table = [] {
+    const char* e = std::getenv("LOCUST_SMALL_TABLE");
+    return e && e[0] == '0' ? 0u : 1u;
+  }();
   // LOCUST_ORD_RESERVE=1: the host-output ordered build reserves its partitions' output
   // with an atomic instead of placing it by the look-back (OrderedExtra::reserve; measured
   // no faster: the span shrinks, the PCIe drain of the records moves into the tail)

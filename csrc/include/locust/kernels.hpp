@@ -329,6 +329,8 @@ struct OrderedExtra {
   u32 split_floor = 0;          // ... and the fewest tokens of a partition that splits at all
   u32 split_fused = 1;          // siblings: one gather for the samples and the inserts
   u32 rank_w0 = 1;              // all-pairs ranks: further key words read only on a first-word tie
+  u32 early_publish = 1;        // publish (keys, tokens) before writing the compacted arrays
+  u32 small_table = 1;          // tile-source partitions clear 512 table slots unless they need more
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};
   // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x

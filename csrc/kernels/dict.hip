@@ -217,6 +217,11 @@ static_assert(kPartSlots == kPartSlotsHost, "partial slot size");
 constexpr int kPartWindow = kPartBlock * 16;  // partition bytes scanned per round
 constexpr u32 kOrdTagWindow = kPartBlock * 32;  // ordered build: tags scanned per round
 constexpr int kPartPerThread = kPartSlots / kPartBlock;
+// The ordered kernel's tile-source partitions clear only the first kSmallTable slots of
+// their table; one of more than kSmallTableTokens tokens (so possibly more distinct keys
+// than 3/4 of that) clears the rest before its first insert (OrderedExtra::small_table).
+constexpr u32 kSmallTable = 512;
+constexpr u32 kSmallTableTokens = kSmallTable * 3 / 4;
 
 // A key not placed within kPartProbes slots reports the table full (the caller falls back):
 // probing a nearly full table to the end made an overflowing pass quadratic.  (512: a
@@ -229,10 +234,12 @@ constexpr int kPartProbes = 512;
 // 1,936 of 2,048 on synth1m) still fits instead of sending the whole pass to the fallback;
 // a table at 31/32 stops at kPartProbes as before (no quadratic overflowing pass).
 constexpr u32 kPartOccFull = kPartSlots - kPartSlots / 32;
+// mask (optional): a table of mask + 1 <= kPartSlots slots (a power of two; the ordered
+// kernel's small partitions clear and use only the first kSmallTable slots).
 __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 c, u64 h,
-                                                u32* occ = nullptr) {
-  u32 slot = (u32)(h >> 8) & (kPartSlots - 1);
-  const int limit = occ ? kPartSlots : kPartProbes;
+                                                u32* occ = nullptr, u32 mask = kPartSlots - 1) {
+  u32 slot = (u32)(h >> 8) & mask;
+  const int limit = occ ? kPartSlots : (int)min((u32)kPartProbes, mask + 1);
   for (int probe = 0; probe < limit;) {
     if (occ && probe >= kPartProbes && (probe & 63) == 0 &&
         __hip_atomic_load(occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= kPartOccFull)
@@ -260,7 +267,7 @@ __device__ __forceinline__ bool part_lds_insert(LdsSlot* tab, const u64* k, u64 
         return true;
       }
     }
-    slot = (slot + 1) & (kPartSlots - 1);
+    slot = (slot + 1) & mask;
     ++probe;
   }
   return false;
@@ -280,7 +287,7 @@ template <int kB>
 __device__ __forceinline__ bool insert_gathered(ConstKeysSoA tokens, const u32* idx,
                                                 u64 (*k)[kKeyWords], u64* c, LdsSlot* s_tab,
                                                 u64 rlo, u64 rhi, bool rlast, bool eager_w1,
-                                                bool weighted) {
+                                                bool weighted, u32 mask = kPartSlots - 1) {
   bool full = false;
 #pragma unroll
   for (int r = 0; r < kB; ++r)  // outside the range: neither gathered nor inserted
@@ -321,7 +328,7 @@ __device__ __forceinline__ bool insert_gathered(ConstKeysSoA tokens, const u32* 
         else if (same) live = false;
       }
     }
-    if (live) full |= !part_lds_insert(s_tab, k[r], c[r], key_hash(k[r]));
+    if (live) full |= !part_lds_insert(s_tab, k[r], c[r], key_hash(k[r]), nullptr, mask);
   }
   return full;
 }
@@ -333,7 +340,8 @@ template <int kGatherBatch = kGatherBatch>
 __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* counts,
                                               const u32* s_list, u32 lim, u32 n_cap,
                                               LdsSlot* s_tab, u64 rlo = 0, u64 rhi = ~0ull,
-                                              bool rlast = true, bool eager_w1 = false) {
+                                              bool rlast = true, bool eager_w1 = false,
+                                              u32 mask = kPartSlots - 1) {
   bool full = false;
   for (u32 e0 = 0; e0 < lim; e0 += kGatherBatch * kPartBlock) {
     u32 idx[kGatherBatch];
@@ -353,7 +361,7 @@ __device__ __forceinline__ bool gather_insert(ConstKeysSoA tokens, const u64* co
       k[r][2] = k[r][3] = 0;
     }
     full |= insert_gathered<kGatherBatch>(tokens, idx, k, c, s_tab, rlo, rhi, rlast, eager_w1,
-                                          counts != nullptr);
+                                          counts != nullptr, mask);
   }
   return full;
 }
@@ -672,8 +680,21 @@ struct TileSource {
   // each thread's own tile runs instead, as the partials kernel does, measured slower
   // here: 21 vs 13.5 us span -- a small pass has ~180 tiles, so most lanes idle while the
   // hot tiles' lanes insert serially; the list spreads the tokens over all 1,024.)
+  // The table mask for a partition of ntok tokens (uniform), growing a small table (the
+  // caller's barrier follows before any insert); thread 0 records it in *s_tmask.
+  __device__ static u32 grow_table(u32 ntok, u32 mask, LdsSlot* s_tab, u32* s_tmask) {
+    if (mask == (u32)kPartSlots - 1 || ntok <= kSmallTableTokens) return mask;
+    for (u32 i = mask + 1 + threadIdx.x; i < (u32)kPartSlots; i += kPartBlock) {
+#pragma unroll
+      for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
+      s_tab[i].count = 0;
+    }
+    if (threadIdx.x == 0) *s_tmask = kPartSlots - 1;
+    return kPartSlots - 1;
+  }
+  // mask: the cleared table's (kPartSlots - 1, or kSmallTable - 1 with small_table)
   __device__ bool build(u32 p, Pre pre, LdsSlot* s_tab, u32* s_list, u32& s_count,
-                        u64* stamp) const {
+                        u64* stamp, u32 mask = kPartSlots - 1, u32* s_tmask = nullptr) const {
     bool full = false;
     for (u32 t0 = 0; t0 < ntiles; t0 += kPartBlock) {
       const u32 t = t0 + threadIdx.x;
@@ -699,8 +720,13 @@ struct TileSource {
       if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
       const u32 cnt = s_count;
       full |= cnt > (u32)kPartWindow;  // the host redoes the Process stage on the HBM table
+      if (t0 == 0 && mask != (u32)kPartSlots - 1) {  // uniform: a small table, grown if needed
+        const u32 m2 = grow_table(ntiles > (u32)kPartBlock ? ~0u : cnt, mask, s_tab, s_tmask);
+        if (m2 != mask) __syncthreads();
+        mask = m2;
+      }
       full |= gather_insert(tokens, nullptr, s_list, min(cnt, (u32)kPartWindow), n_cap, s_tab, 0,
-                            ~0ull, true, true);
+                            ~0ull, true, true, mask);
       if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
       __syncthreads();
       if (threadIdx.x == 0) s_count = 0;
@@ -721,13 +747,15 @@ struct TileSource {
   // instead of two, and no LDS rank pass (the cuts are the same: same sample positions).
   static constexpr u32 kSplitSamples = 64;
   __device__ bool build_split(u32 p, Pre pre, u32 j, u32 K, LdsSlot* s_tab, u32* s_list,
-                              u32* s_scan, u64* stamp, bool fused) const {
+                              u32* s_scan, u64* stamp, bool fused,
+                              u32 mask = kPartSlots - 1, u32* s_tmask = nullptr) const {
     u64* s_samp = reinterpret_cast<u64*>(s_list + kPartWindow - 256);  // [64]
     u64* s_sort = reinterpret_cast<u64*>(s_list + kPartWindow - 128);  // [64]
     const u32 a = pre.a, len = threadIdx.x < ntiles ? pre.b - pre.a : 0u;
     u32 n = 0;
     const u32 at = dev::block_exclusive_scan<u32, kPartBlock>(len, s_scan, &n);
     const u32 lim = min(n, (u32)kPartWindow - 256);  // the sample area sits at the list's end
+    mask = grow_table(n, mask, s_tab, s_tmask);  // (the barrier after the fill covers it)
     if (stamp && threadIdx.x == 0) stamp[28] = __builtin_amdgcn_s_memtime();
     for (u32 k = 0; k < len && at + k < lim; ++k) s_list[at + k] = a + k;
     __syncthreads();
@@ -771,7 +799,8 @@ struct TileSource {
       const u64 hi = last || !S ? ~0ull : readlane_u64(srt, (u32)((u64)(j + 1) * S / K));
       if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
       if (!(lo == hi && !last))
-        full |= insert_gathered<kGatherBatch>(tokens, idx, k, c, s_tab, lo, hi, last, true, false);
+        full |= insert_gathered<kGatherBatch>(tokens, idx, k, c, s_tab, lo, hi, last, true, false,
+                                              mask);
       if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
       __syncthreads();  // the list area is reused after the build
       return full;
@@ -795,7 +824,7 @@ struct TileSource {
     const u64 hi = last || !S ? ~0ull : s_sort[(u64)(j + 1) * S / K];
     if (stamp && threadIdx.x == 0) stamp[12] = __builtin_amdgcn_s_memtime();
     if (!(lo == hi && !last))  // else an empty range (a hot first word took it)
-      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last, true);
+      full |= gather_insert(tokens, nullptr, s_list, lim, n_cap, s_tab, lo, hi, last, true, mask);
     if (stamp && threadIdx.x == 0) stamp[13] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // the list area is reused after the build
     return full;
@@ -1187,7 +1216,11 @@ __device__ __forceinline__ void ordered_partition(
   const typename Src::Pre first =
       vplan ? (vk ? src.prefetch(p) : typename Src::Pre{})
             : guessing && p == guess_p ? guess : src.prefetch(p);
-  for (int i = threadIdx.x; i < kPartSlots; i += kPartBlock) {
+  // the table's slots in use: all, or (small_table) the first kSmallTable until a build
+  // finds more tokens (TileSource::grow_table)
+  __shared__ u32 s_tmask;
+  const u32 tmask0 = kTiles && ex.small_table ? kSmallTable - 1 : (u32)kPartSlots - 1;
+  for (int i = threadIdx.x; i <= (int)tmask0; i += kPartBlock) {
 #pragma unroll
     for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
     s_tab[i].count = 0;
@@ -1197,6 +1230,7 @@ __device__ __forceinline__ void ordered_partition(
     s_cm = 0;
     s_ctok = 0;
     s_cfull = 0;
+    s_tmask = tmask0;
   }
   __syncthreads();
   ORD_STAMP(14);  // table cleared
@@ -1204,9 +1238,11 @@ __device__ __forceinline__ void ordered_partition(
   if constexpr (kTiles) {
     if (vk > 1)
       full = src.build_split(p, first, vj, vk, s_tab, s_list, reinterpret_cast<u32*>(s_scan),
-                             trace ? trace + (u64)v * 32 : nullptr, ex.split_fused != 0);
+                             trace ? trace + (u64)v * 32 : nullptr, ex.split_fused != 0, tmask0,
+                             &s_tmask);
     else if (vk == 1)
-      full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr);
+      full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr,
+                       tmask0, &s_tmask);
   } else {
     full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr);
   }
@@ -1214,12 +1250,14 @@ __device__ __forceinline__ void ordered_partition(
   // ---- compact: dense (w0, slot) arrays in the list area ----
   u64* s_w0 = reinterpret_cast<u64*>(s_list);            // [kPartSlots]
   u32* s_slot = s_list + 2 * kPartSlots;                 // [kPartSlots]
+  const u32 nslots = s_tmask + 1;  // (the build's barriers publish a grown table's mask)
   u32 mine = 0;
   u64 wsum = 0;
 #pragma unroll
   for (int r = 0; r < kPartPerThread; ++r) {
-    const LdsSlot& sl = s_tab[threadIdx.x * kPartPerThread + r];
-    if (sl.w[0]) {
+    const u32 slot = threadIdx.x * kPartPerThread + r;
+    const LdsSlot& sl = s_tab[slot < nslots ? slot : 0];
+    if (slot < nslots && sl.w[0]) {
       ++mine;
       wsum += sl.count;
     }
@@ -1232,22 +1270,13 @@ __device__ __forceinline__ void ordered_partition(
   u64* s_out = reinterpret_cast<u64*>(s_rk + 2 * kSmallRank);    // [5 x kSmallRank] records
   u64* s_k123 = s_out + 6 * kSmallRank;                          // [3 x kSmallRank] words 1-3
   u32* s_cw = reinterpret_cast<u32*>(s_k123 + 3 * kSmallRank);   // [kSmallRank] compact words
-  {
-    const u64 b0 = dev::ballot(mine >= 1), b1 = dev::ballot(mine >= 2);
-    const u64 wfull = dev::ballot(full);
-    const u64 wtok_incl = dev::wave_inclusive_scan(wsum);
-    u32 wbase = 0;
-    if (dev::lane_id() == 63) {
-      wbase = atomicAdd(&s_cm, (u32)(__popcll(b0) + __popcll(b1)));
-      atomicAdd(reinterpret_cast<unsigned long long*>(&s_ctok), (unsigned long long)wtok_incl);
-      if (wfull) s_cfull = 1u;
-    }
-    wbase = (u32)__builtin_amdgcn_readlane((int)wbase, 63);
-    u32 d = wbase + dev::lanes_below(b0) + dev::lanes_below(b1);
+  // this thread's live slots from position d on: (w0, slot) and, for the small path, the
+  // key's other words and compact size
+  auto write_compacted = [&](u32 d) {
 #pragma unroll
     for (int r = 0; r < kPartPerThread; ++r) {
       const u32 slot = threadIdx.x * kPartPerThread + r;
-      if (s_tab[slot].w[0]) {
+      if (slot < nslots && s_tab[slot].w[0]) {
         s_w0[d] = s_tab[slot].w[0];
         s_slot[d] = slot;
         if (d < kSmallRank) {
@@ -1267,8 +1296,23 @@ __device__ __forceinline__ void ordered_partition(
       s_rk[threadIdx.x] = 0;
       s_rkw[threadIdx.x] = 0;
     }
+  };
+  u32 cpos = 0;
+  {
+    const u64 b0 = dev::ballot(mine >= 1), b1 = dev::ballot(mine >= 2);
+    const u64 wfull = dev::ballot(full);
+    const u64 wtok_incl = dev::wave_inclusive_scan(wsum);
+    u32 wbase = 0;
+    if (dev::lane_id() == 63) {
+      wbase = atomicAdd(&s_cm, (u32)(__popcll(b0) + __popcll(b1)));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&s_ctok), (unsigned long long)wtok_incl);
+      if (wfull) s_cfull = 1u;
+    }
+    wbase = (u32)__builtin_amdgcn_readlane((int)wbase, 63);
+    cpos = wbase + dev::lanes_below(b0) + dev::lanes_below(b1);
+    if (!ex.early_publish) write_compacted(cpos);
   }
-  __syncthreads();  // the compacted (w0, slot) arrays and the sums are complete
+  __syncthreads();  // the sums are complete (and, unless early_publish, the arrays)
   const u32 m = s_cm;
   const int any_full = s_cfull != 0u;
   const u64 tok = s_ctok;
@@ -1282,6 +1326,10 @@ __device__ __forceinline__ void ordered_partition(
   // on status[kDictParts] below, in arrival order, and ctab[v] tells the host where)
   if (threadIdx.x == 0 && !ex.reserve) dev::publish_aggregate(status, v, agg);
   ORD_STAMP(2);
+  if (ex.early_publish) {  // the arrays after the publish: successors stop waiting sooner
+    write_compacted(cpos);
+    __syncthreads();
+  }
   u64 pre = 0;
   u32 cwords = ~0u;  // compact words written (ex.cout), ~0u: none
   if (small) {
