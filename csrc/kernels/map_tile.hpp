@@ -126,6 +126,17 @@ __device__ __forceinline__ void pack_token(const unsigned char* s_text, int o, u
   }
 }
 
+// Tile of block b of a G-block launch with consecutive tiles on one XCD: the blocks of a
+// launch go to the XCDs round-robin (b = 8 k + x runs on XCD x), so XCD x takes the x-th
+// eighth of the tiles in order.  A bijection on [0, G).  Neighbouring tiles then read their
+// overlapping context and adjacent lines of the zero-copy text through one XCD: the fast
+// map's staging of a Hamlet-sized input 7.9 -> 6.35 us (tools/micro/stage_read.hip).
+__device__ __forceinline__ u32 xcd_tile(u32 b, u32 G) {
+  constexpr u32 kXcds = 8;
+  const u32 q = G / kXcds, r = G % kXcds, x = b % kXcds, k = b / kXcds;
+  return x * q + (x < r ? x : r) + k;
+}
+
 // The tile's LDS, declared __shared__ by the calling kernel and passed in: LDS variables
 // declared inside a device function are lowered to module scope, where every kernel of the
 // file that reaches any instantiation pays for all of them (map_fast_kernel<1, 1024> grew
@@ -288,26 +299,10 @@ __device__ __forceinline__ void map_tile(
   }
   dmask[kSteps] = ballot(d.has(s_text[seg_lds + kSteps * 64 + lane]));  // lookahead
 
-  // ---- phase 2: wave counts -> tile prefix (look-back) ----
-  if (lane == 0) s_wave_cnt[w] = emitted;
-  __syncthreads();
-  MAP_STAMP(3);
-  u32 wave_excl = 0, tile_total = 0;
-#pragma unroll
-  for (int i = 0; i < kBlock / 64; ++i) {
-    const u32 v = s_wave_cnt[i];
-    if (i < w) wave_excl += v;
-    tile_total += v;
-  }
-  // this tile's slice of the token array: one atomic per tile (a combining tile reserves
-  // its records once it has counted them)
-  if (threadIdx.x == 0 && !combine) s_prefix = tile_total ? atomicAdd(&ctr->num_records, tile_total) : 0;
-  __syncthreads();
-  const u64 prefix = s_prefix;
-  MAP_STAMP(4);
-  if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
-
-  // ---- phase 3 (grouped): keys by partition inside the tile's slice ----
+  // ---- small grouped tiles (kSteps == 1, part_off): the token's partition and its rank
+  // in the tile's partition run are drawn before the first barrier, and the tile's slice
+  // of the token array is reserved while wave 0 scans the partition counts -- the global
+  // atomic's round trip overlaps the scan, and the tile takes two barriers, not four ----
   if constexpr (kSteps == 1) {
     if (part_off) {
       const u64 m = emit_mask[0];
@@ -320,8 +315,18 @@ __device__ __forceinline__ void map_tile(
         part = part_of(kw[0]);
         loc = atomicAdd(&s_pcnt[part], 1u);
       }
-      __syncthreads();
-      if (threadIdx.x < 64) {  // exclusive scan of the 256 partition counts by one wave
+      if (lane == 0) s_wave_cnt[w] = emitted;
+      __syncthreads();  // wave counts and partition counts complete
+      MAP_STAMP(3);
+      if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
+      if (threadIdx.x < 64) {
+        u32 tile_total = 0;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; ++i) tile_total += s_wave_cnt[i];
+        // issued now, its value needed only after the scan below
+        u64 slice = 0;
+        if (threadIdx.x == 0 && tile_total) slice = atomicAdd(&ctr->num_records, tile_total);
+        // exclusive scan of the 256 partition counts by one wave
         const u32 l = threadIdx.x;
         const u32 h0 = s_pcnt[4 * l], h1 = s_pcnt[4 * l + 1], h2 = s_pcnt[4 * l + 2],
                   h3 = s_pcnt[4 * l + 3];
@@ -340,8 +345,11 @@ __device__ __forceinline__ void map_tile(
         s_pcnt[4 * l + 2] = ex + h0 + h1;
         s_pcnt[4 * l + 3] = ex + h0 + h1 + h2;
         if (l == 63) s_pcnt[kDictParts] = inc;
+        if (threadIdx.x == 0) s_prefix = slice;
       }
       __syncthreads();
+      const u64 prefix = s_prefix;
+      MAP_STAMP(4);
       for (int i = threadIdx.x; i < kPartTable; i += kBlock)
         map_store<kWT>(&part_off[(u64)tile * kPartTable + i], (u32)(prefix + s_pcnt[i]));
       u32 trunc = 0, maxlen = 0;
@@ -363,6 +371,26 @@ __device__ __forceinline__ void map_tile(
       return;
     }
   }
+
+  // ---- phase 2: wave counts -> tile prefix (look-back) ----
+  if (lane == 0) s_wave_cnt[w] = emitted;
+  __syncthreads();
+  MAP_STAMP(3);
+  u32 wave_excl = 0, tile_total = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / 64; ++i) {
+    const u32 v = s_wave_cnt[i];
+    if (i < w) wave_excl += v;
+    tile_total += v;
+  }
+  // this tile's slice of the token array: one atomic per tile (a combining tile reserves
+  // its records once it has counted them)
+  if (threadIdx.x == 0 && !combine) s_prefix = tile_total ? atomicAdd(&ctr->num_records, tile_total) : 0;
+  __syncthreads();
+  const u64 prefix = s_prefix;
+  MAP_STAMP(4);
+  if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
+
   if constexpr (kSteps > 1) {
     if (part_off) {
       // ---- phase 3 (grouped, large tiles): a lane owns a byte, so only the ~1 in 7 lanes

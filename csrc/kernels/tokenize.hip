@@ -23,6 +23,8 @@
 //    packed key, and writes it straight into the dense SoA output.  The map output is
 //    born compacted, so the reference's 116,000-slot thrust::partition (main.cu:411) has
 //    nothing left to do.
+#include <cstdlib>
+
 #include "locust/hip_check.hpp"
 #include "locust/kernels.hpp"
 #include "map_tile.hpp"
@@ -36,9 +38,11 @@ template <int kSteps, int kBlock>
 __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ trace,
-    u32* __restrict__ part_off, PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_occ) {
+    u32* __restrict__ part_off, PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_occ,
+    u32 xcd_order) {
   __shared__ MapTileLds<kSteps, kBlock> lds;
-  map_tile<kSteps, kBlock>(lds, blockIdx.x, text, bytes, d, E, max_key, out, parts, out_cap, ctr,
+  const u32 tile = xcd_order ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  map_tile<kSteps, kBlock>(lds, tile, text, bytes, d, E, max_key, out, parts, out_cap, ctr,
                            trace, part_off, pm, counts, part_occ);
 }
 
@@ -50,6 +54,12 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
                      PartMap pm, bool large_tiles, u64* counts, u32* part_occ) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
+  // LOCUST_MAP_XCD=0 (A/B, read at the first launch): tiles in block order instead of
+  // consecutive tiles per XCD (xcd_tile)
+  static const u32 xcd_order = [] {
+    const char* e = std::getenv("LOCUST_MAP_XCD");
+    return e && e[0] == '0' ? 0u : 1u;
+  }();
   if (bytes < kMapLargeInput && !large_tiles) {
     // Small inputs: 1 KiB tiles as 16 waves x ONE 64-byte step -- the same text per
     // workgroup (and the same PCIe reads), the least serial work per wave.  Measured A/B
@@ -59,13 +69,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, trace, part_off, pm,
-        nullptr, part_off ? part_occ : nullptr);
+        nullptr, part_off ? part_occ : nullptr, xcd_order);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, trace, part_off, pm,
-        part_off ? counts : nullptr, nullptr);
+        part_off ? counts : nullptr, nullptr, xcd_order);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }

@@ -5,6 +5,9 @@ one fresh process per variant, in alternating order, each timing `--steps` jobs 
 
     python tools/ab_procs.py "LOCUST_PART_TUNE=0" "LOCUST_PART_TUNE=0,LOCUST_PART_DEFAULT=letters" \\
         [--config hamlet4500|hamlet700|synth1m] [--rounds 5] [--steps 300] [--warmup 30]
+
+A variant's ROOT=<dir> runs it from another built tree (e.g. a previous commit exported
+with `git archive` and built with make): code changes without a switch of their own.
 """
 import argparse
 import json
@@ -31,8 +34,17 @@ def env_of(variant: str) -> dict:
     env = dict(os.environ)
     for kv in filter(None, variant.split(",")):
         k, _, v = kv.partition("=")
-        env[k.strip()] = v.strip()
+        if k.strip() != "ROOT":
+            env[k.strip()] = v.strip()
     return env
+
+
+def root_of(variant: str) -> str:
+    for kv in filter(None, variant.split(",")):
+        k, _, v = kv.partition("=")
+        if k.strip() == "ROOT":
+            return os.path.abspath(os.path.join(ROOT, v.strip()))
+    return ROOT
 
 
 def main() -> int:
@@ -48,7 +60,7 @@ def main() -> int:
     for r in range(a.rounds):
         order = a.variants if r % 2 == 0 else a.variants[::-1]
         for v in order:
-            p = subprocess.run([sys.executable, "-c", CHILD, ROOT, a.config, str(a.steps),
+            p = subprocess.run([sys.executable, "-c", CHILD, root_of(v), a.config, str(a.steps),
                                 str(a.warmup)], env=env_of(v), capture_output=True, text=True,
                                timeout=300)
             if p.returncode:
