@@ -1148,11 +1148,12 @@ void DevicePipeline::print_ord_trace() {
                  "ord p=%3d m=%5llu build=%6llu publish=%5llu sort=%6llu wait=%6llu write=%6llu"
                  " | hist=%5llu bucket=%5llu rank=%6llu scatter=%5llu | in=%6.2f out=%6.2f us"
                  " | clear=%5llu scan=%5llu fill=%5llu ld=%5llu srt=%5llu list=%5llu gather=%5llu lbk=%6llu rank0=%6llu cand=%6llu tie=%6llu ranks=%6llu"
-                 " | waited=%6.2f us\n",
+                 " | waited=%6.2f us | counted=%6.2f us after exit\n",
                  p, (unsigned long long)x[6], d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(4, 5),
                  d(2, 8), d(8, 7), d(7, 9), d(9, 3), (x[10] - first_in) * 0.01,
                  (x[11] - first_in) * 0.01, d(0, 14), d(14, 28), d(28, 26), d(26, 27), d(27, 12), d(14, 12), d(12, 13), d(2, 15), x[17] != ~0ull ? d(2, 17) : 0ull, d(2, 18), d(2, 19), d(2, 16),
-                 x[20] ? (x[20] - x[10]) * 0.01 : 0.0);
+                 x[20] ? (x[20] - x[10]) * 0.01 : 0.0,
+                 x[25] >= x[11] ? (x[25] - x[11]) * 0.01 : -1.0);
   }
 }
 
