@@ -1003,10 +1003,13 @@ void DevicePipeline::print_map_trace() {
   for (int i = 0; i < 4096; ++i) {
     const u64* x = &t[i * 8];
     if (!x[0] || !x[5]) continue;
+    // (small grouped tiles: 6 = wave 0's masks done, 7 = its keys packed and ranked, 3 =
+    // the barrier after; large grouped tiles: 6 = records reserved)
     std::fprintf(stderr, "map tile=%4d entry=%6.2f acquired=%6.2f staged=%6.2f masks=%6.2f "
-                 "prefix=%6.2f reserved=%6.2f done=%6.2f us\n", i, (x[0] - t0) * 0.01,
-                 (x[1] - t0) * 0.01, (x[2] - t0) * 0.01, (x[3] - t0) * 0.01,
-                 (x[4] - t0) * 0.01, x[6] ? (x[6] - t0) * 0.01 : 0.0, (x[5] - t0) * 0.01);
+                 "prefix=%6.2f reserved=%6.2f done=%6.2f w0masks=%6.2f w0packed=%6.2f us\n", i,
+                 (x[0] - t0) * 0.01, (x[1] - t0) * 0.01, (x[2] - t0) * 0.01, (x[3] - t0) * 0.01,
+                 (x[4] - t0) * 0.01, x[6] ? (x[6] - t0) * 0.01 : 0.0, (x[5] - t0) * 0.01,
+                 x[6] ? (x[6] - t0) * 0.01 : 0.0, x[7] ? (x[7] - t0) * 0.01 : 0.0);
   }
 }
 

@@ -305,6 +305,7 @@ __device__ __forceinline__ void map_tile(
   // atomic's round trip overlaps the scan, and the tile takes two barriers, not four ----
   if constexpr (kSteps == 1) {
     if (part_off) {
+      MAP_STAMP(6);  // (wave 0's) masks
       const u64 m = emit_mask[0];
       const bool em = (m >> lane) & 1ull;
       u64 kw[kKeyWords] = {0, 0, 0, 0};
@@ -316,6 +317,7 @@ __device__ __forceinline__ void map_tile(
         loc = atomicAdd(&s_pcnt[part], 1u);
       }
       if (lane == 0) s_wave_cnt[w] = emitted;
+      MAP_STAMP(7);  // (wave 0's) keys packed and ranked
       __syncthreads();  // wave counts and partition counts complete
       MAP_STAMP(3);
       if (lane == 0 && overflow) atomicAdd(&ctr->overflow_lines, overflow);
