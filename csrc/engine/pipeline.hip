@@ -1399,9 +1399,12 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
   if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
   // lean dictionary jobs of a small pass: Map and the ordered build in one launch
   const bool fused = lean && dict_path && !compat && fuse_ok(in);
+  const bool dbg = (int)log_level() >= (int)LogLevel::kDebug;
+  u64 t_map = 0;
   if (lean) {
     enqueue_upload(in);
     if (!fused) enqueue_map(in);
+    if (dbg) t_map = now_ns();
   } else if (graphed) {
     prepare_upload(in);
     launch_dict_graph(in, compat);
@@ -1439,6 +1442,9 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
     }
     skip_sync_reset = false;
     const u64 t_launched = now_ns();
+    if (dbg && lean)
+      LOCUST_LOG_DEBUG("lean job: map launched +%.4f ms, ordered launched +%.4f ms",
+                       (t_map - t0) * 1e-6, (t_launched - t0) * 1e-6);
     if (lean)
       wait_done(done_seq);
     else
