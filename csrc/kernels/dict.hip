@@ -1134,22 +1134,53 @@ __device__ __forceinline__ void ordered_partition(
         }
         tp = (u32)((u64)sum * nt / kPlanRows);
       } else {
-        // occupancy: thread (word w, tile slice) ORs its tiles' word w
+        // occupancy: thread (word w, tile slice) ORs its tiles' word w -- every load issued
+        // before the first is used (one round trip, not one per tile: nt <= kPartBlock)
         const u32 i = threadIdx.x - kDictParts, w = i % kPartOccWords;
-        for (u32 t = i / kPartOccWords; t < nt; t += (kPartBlock - kDictParts) / kPartOccWords)
-          occw |= ex.part_occ[(u64)t * kPartOccWords + w];
+        constexpr u32 kStride = (kPartBlock - kDictParts) / kPartOccWords;
+        constexpr u32 kLoads = (kPartBlock + kStride - 1) / kStride;
+        u32 o[kLoads];
+#pragma unroll
+        for (u32 k = 0; k < kLoads; ++k) {
+          const u32 t = i / kPartOccWords + k * kStride;
+          o[k] = t < nt ? ex.part_occ[(u64)t * kPartOccWords + w] : 0u;
+        }
+#pragma unroll
+        for (u32 k = 0; k < kLoads; ++k) occw |= o[k];
       }
     }
   }
   // Tickets almost always come out in dispatch order: prefetch the run table for
-  // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.
-  const bool guessing = !vplan && guess_p != ~0u;
+  // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.  (With
+  // a plan too: a plan that splits nothing keeps v = p, and the guess holds.)
+  const bool guessing = guess_p != ~0u;
   const typename Src::Pre guess = guessing ? src.prefetch(guess_p) : typename Src::Pre{};
+  // The ticket atomic is issued first and the table cleared while it and the plan's loads
+  // are in flight (the clear needs neither).  The table's slots in use: all, or
+  // (small_table) the first kSmallTable until a build finds more tokens (grow_table).
+  __shared__ u32 s_tmask;
+  u32 ticket = 0;
+  if (threadIdx.x == 0) ticket = atomicAdd(tile_ctr, 1u);  // its value is waited for below
+  const u32 tmask0 = kTiles && ex.small_table ? kSmallTable - 1 : (u32)kPartSlots - 1;
+  for (int i = threadIdx.x; i <= (int)tmask0; i += kPartBlock) {
+#pragma unroll
+    for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
+    s_tab[i].count = 0;
+  }
+  if (threadIdx.x == 0) {
+    s_count = 0;
+    s_cm = 0;
+    s_ctok = 0;
+    s_cfull = 0;
+    s_tmask = tmask0;
+    s_tile = ticket;
+  }
   u32 v, p, vj = 0, vk = 1;
+  bool identity = !vplan;  // v = p: one workgroup per map partition
   if (!vplan) {
-    v = p = dev::acquire_tile(tile_ctr, &s_tile);
+    __syncthreads();  // s_tile (and the cleared table)
+    v = p = s_tile;
   } else {
-    if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
     if (threadIdx.x < kPartOccWords) s_occ[threadIdx.x] = 0;
     __syncthreads();
     if (threadIdx.x >= kDictParts && occw) atomicOr(&s_occ[(threadIdx.x - kDictParts) % kPartOccWords], occw);
@@ -1190,10 +1221,16 @@ __device__ __forceinline__ void ordered_partition(
     }
     __syncthreads();
     const u32 V = s_vpre[kDictParts];
+    // nothing split (V == E): one workgroup per map partition, v = p, as without a plan --
+    // the run table prefetched for the guessed partition is then usually the right one
+    identity = V == E;
     // the map partition holding v: the last q with s_vpre[q] <= v (s_vpre[256] = V > v)
     p = 0;
     vk = 0;  // v >= V: an idle workgroup -- an empty virtual partition in the chain
-    if (v < V) {
+    if (identity) {
+      p = v;
+      vk = 1;
+    } else if (v < V) {
 #pragma unroll
       for (u32 step = kDictParts / 2; step; step >>= 1)
         if (s_vpre[p + step] <= v) p += step;
@@ -1213,25 +1250,8 @@ __device__ __forceinline__ void ordered_partition(
     trace[(u64)v * 32 + 27] = 0;
     trace[(u64)v * 32 + 28] = 0;
   }
-  const typename Src::Pre first =
-      vplan ? (vk ? src.prefetch(p) : typename Src::Pre{})
-            : guessing && p == guess_p ? guess : src.prefetch(p);
-  // the table's slots in use: all, or (small_table) the first kSmallTable until a build
-  // finds more tokens (TileSource::grow_table)
-  __shared__ u32 s_tmask;
-  const u32 tmask0 = kTiles && ex.small_table ? kSmallTable - 1 : (u32)kPartSlots - 1;
-  for (int i = threadIdx.x; i <= (int)tmask0; i += kPartBlock) {
-#pragma unroll
-    for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
-    s_tab[i].count = 0;
-  }
-  if (threadIdx.x == 0) {
-    s_count = 0;
-    s_cm = 0;
-    s_ctok = 0;
-    s_cfull = 0;
-    s_tmask = tmask0;
-  }
+  const typename Src::Pre first = identity && guessing && p == guess_p ? guess
+                                  : vk ? src.prefetch(p) : typename Src::Pre{};
   __syncthreads();
   ORD_STAMP(14);  // table cleared
   bool full = false;
