@@ -248,6 +248,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   // counters[6] is the ordered kernels' done counter (lb_dict.tile_counter + 1);
   // counters[8..9]: the fused launch's ticket and tiles done
   d_fuse = counters + 8;
+  d_plan_flag = counters + 7;  // OrderedExtra::plan_flag
 
   rx.cap = cap;
   rx.tile_counters = arena.take<u32>(rx_zero_words);
@@ -704,7 +705,8 @@ void DevicePipeline::enqueue_map(const TextInput& in, bool launch) {
     launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                     cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                     stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
-                    map_combined ? d_counts : nullptr, plan_small() ? d_part_occ : nullptr);
+                    map_combined ? d_counts : nullptr, plan_small() ? d_part_occ : nullptr,
+                    plan_small() && plan_trigger ? d_plan_flag : nullptr);
   }
 }
 
@@ -826,6 +828,8 @@ void DevicePipeline::set_tile_source(OrderedExtra& ex, bool with_counts) const {
     // the in-job plan while the map is untuned (a retuned map is already balanced: the
     // plan would only add its ~2 us)
     if (plan_small()) ex.part_occ = d_part_occ;
+    // ... and only when the map saw a crowded partition (plan_trigger)
+    if (plan_small() && plan_trigger) ex.plan_flag = d_plan_flag;
   }
 }
 
@@ -1188,6 +1192,7 @@ bool DevicePipeline::enqueue_map_ordered(const TextInput& in) {
     done_pending = 0;
   }
   set_tile_source(ex, false);
+  ex.plan_flag = nullptr;  // the fused map does not raise it: plan every pass
   set_compact_out(ex, true);
   ex.fuse = d_fuse;
   launch_map_ordered(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),

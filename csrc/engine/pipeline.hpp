@@ -157,6 +157,13 @@ struct DevicePipeline {
     return (u64)(e ? std::max(0, std::atoi(e)) : 0) << 10;
   }();
   bool plan_pass = false;  // this pass's map writes occupancy and its ordered kernel plans
+  // LOCUST_PLAN_TRIGGER=0 (read at construction): a planned pass plans in every job instead
+  // of only when the map saw kPlanTrigger tokens of one partition in a tile (plan_flag)
+  const bool plan_trigger = [] {
+    const char* e = std::getenv("LOCUST_PLAN_TRIGGER");
+    return !(e && e[0] == '0');
+  }();
+  u32* d_plan_flag = nullptr;
   bool plan_small() const { return plan_pass; }
   void decide_plan(u64 pass_bytes) {
     plan_pass = vplan && pm_retunes == 0 && pass_bytes >= vplan_min_bytes;

@@ -121,7 +121,7 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace = nullptr,
                      u32* part_off = nullptr, PartMap pm = PartMap{}, bool large_tiles = false,
-                     u64* counts = nullptr, u32* part_occ = nullptr);
+                     u64* counts = nullptr, u32* part_occ = nullptr, u32* plan_flag = nullptr);
 
 // ---------------- radix_sort.hip ----------------
 constexpr int kSortBlock = 256;
@@ -325,6 +325,11 @@ struct OrderedExtra {
   // of 256 workgroups idle and puts 's'/'t' on the critical path without it.  (Inputs of
   // at most kPartBlock tiles; larger ones keep one workgroup per partition.)
   const u32* part_occ = nullptr;
+  // With part_occ (optional, zeroed device word): the map sets it when a tile holds
+  // kPlanTrigger tokens of one partition; the ordered kernel plans only then (otherwise
+  // one workgroup per map partition, without the plan's loads), and the self-clean
+  // re-zeroes it.  Null: plan every pass.
+  u32* plan_flag = nullptr;
   u32 split_min = 0;            // planned workgroups: tokens per extra sibling (0: default)
   u32 split_floor = 0;          // ... and the fewest tokens of a partition that splits at all
   u32 split_fused = 1;          // siblings: one gather for the samples and the inserts

@@ -1120,7 +1120,8 @@ __device__ __forceinline__ void ordered_partition(
   __shared__ u32 s_vred[8];
   __shared__ u32 s_occ[kPartOccWords];
   u32 tp = 0, occw = 0;  // (plan) loaded before the ticket: one round trip for all
-  if (vplan) {
+  // the plan's loads: partition thread q its estimated tokens, the others the occupancy
+  auto plan_loads = [&]() {
     if constexpr (kTiles) {
       const u32 nt = src.ntiles;
       if (threadIdx.x < kDictParts) {
@@ -1149,7 +1150,13 @@ __device__ __forceinline__ void ordered_partition(
         for (u32 k = 0; k < kLoads; ++k) occw |= o[k];
       }
     }
-  }
+  };
+  // plan_flag: plan only if the map saw a crowded partition -- the flag's load rides with
+  // the ticket and the guessed prefetch; the plan's own loads wait for it
+  const bool triggered = vplan && ex.plan_flag != nullptr;
+  u32 flag = 0;
+  if (triggered) flag = __hip_atomic_load(ex.plan_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (vplan && !triggered) plan_loads();
   // Tickets almost always come out in dispatch order: prefetch the run table for
   // p = blockIdx.x while the ticket atomic is in flight, reload only on a mismatch.  (With
   // a plan too: a plan that splits nothing keeps v = p, and the guess holds.)
@@ -1174,6 +1181,10 @@ __device__ __forceinline__ void ordered_partition(
     s_cfull = 0;
     s_tmask = tmask0;
     s_tile = ticket;
+  }
+  if (triggered) {  // uniform: every thread read the same word
+    vplan = flag != 0;
+    if (vplan) plan_loads();
   }
   u32 v, p, vj = 0, vk = 1;
   bool identity = !vplan;  // v = p: one workgroup per map partition
@@ -1832,6 +1843,7 @@ __device__ __forceinline__ void ordered_partition(
           *tile_ctr = 0;
           *ex.map_lb.tile_counter = 0;
           *ex.done_counter = 0;
+          if (ex.plan_flag) *ex.plan_flag = 0;
           if (ex.fuse) {  // the fused kernel's ticket and tiles-done counters
             ex.fuse[0] = 0;
             ex.fuse[1] = 0;

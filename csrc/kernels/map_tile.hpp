@@ -126,6 +126,11 @@ __device__ __forceinline__ void pack_token(const unsigned char* s_text, int o, u
   }
 }
 
+// Tokens of one partition in one 1 KiB tile from which the map asks the ordered kernel to
+// plan (split) the pass: whole Hamlet peaks at 27 under the starting map (most tiles below
+// 16), a pass whose keys crowd one partition puts ~150 there.
+constexpr u32 kPlanTrigger = 48;
+
 // Tile of block b of a G-block launch with consecutive tiles on one XCD: the blocks of a
 // launch go to the XCDs round-robin (b = 8 k + x runs on XCD x), so XCD x takes the x-th
 // eighth of the tiles in order.  A bijection on [0, G).  Neighbouring tiles then read their
@@ -182,7 +187,7 @@ __device__ __forceinline__ void map_tile(
     MapTileLds<kSteps, kBlock>& lds, const u32 tile, const char* __restrict__ text, u64 bytes,
     const Delims& d, int E, int max_key, KeysSoA out, u8* __restrict__ parts, u64 out_cap,
     MapCounters* __restrict__ ctr, u64* __restrict__ trace, u32* __restrict__ part_off, PartMap pm,
-    u64* __restrict__ counts, u32* __restrict__ part_occ) {
+    u64* __restrict__ counts, u32* __restrict__ part_occ, u32* __restrict__ plan_flag = nullptr) {
   // trace (diagnostics, LOCUST_MAP_TRACE): per tile, s_memrealtime (100 MHz, device-wide)
   // at entry, tile acquired, text staged, masks done, prefix known, keys written.
   const u64 t_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -332,6 +337,12 @@ __device__ __forceinline__ void map_tile(
         const u32 l = threadIdx.x;
         const u32 h0 = s_pcnt[4 * l], h1 = s_pcnt[4 * l + 1], h2 = s_pcnt[4 * l + 2],
                   h3 = s_pcnt[4 * l + 3];
+        // a partition crowding this tile (kPlanTrigger tokens of ~180): the ordered kernel
+        // plans this pass (OrderedExtra::plan_flag); one atomic per such tile
+        if (plan_flag && dev::ballot(h0 >= kPlanTrigger || h1 >= kPlanTrigger ||
+                                     h2 >= kPlanTrigger || h3 >= kPlanTrigger) &&
+            l == 0)
+          atomicOr(plan_flag, 1u);
         if (part_occ) {  // the tile's 256-bit partition occupancy: 8 words, lane 8w writes w
           u32 occ = ((h0 ? 1u : 0u) | (h1 ? 2u : 0u) | (h2 ? 4u : 0u) | (h3 ? 8u : 0u)) << (4 * (l & 7));
           occ |= (u32)__shfl_xor((int)occ, 1, 64);

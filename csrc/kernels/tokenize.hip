@@ -39,11 +39,11 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ trace,
     u32* __restrict__ part_off, PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_occ,
-    u32 xcd_order) {
+    u32 xcd_order, u32* __restrict__ plan_flag) {
   __shared__ MapTileLds<kSteps, kBlock> lds;
   const u32 tile = xcd_order ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   map_tile<kSteps, kBlock>(lds, tile, text, bytes, d, E, max_key, out, parts, out_cap, ctr,
-                           trace, part_off, pm, counts, part_occ);
+                           trace, part_off, pm, counts, part_occ, plan_flag);
 }
 
 }  // namespace
@@ -51,7 +51,8 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
 void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
                      int max_key_len, KeysSoA out, u8* parts, u64 out_cap, MapCounters* ctr,
                      LookbackScratch lb, hipStream_t s, u64* trace, u32* part_off,
-                     PartMap pm, bool large_tiles, u64* counts, u32* part_occ) {
+                     PartMap pm, bool large_tiles, u64* counts, u32* part_occ,
+                     u32* plan_flag) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
   // LOCUST_MAP_XCD=0 (A/B, read at the first launch): tiles in block order instead of
@@ -69,13 +70,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, trace, part_off, pm,
-        nullptr, part_off ? part_occ : nullptr, xcd_order);
+        nullptr, part_off ? part_occ : nullptr, xcd_order, part_off && part_occ ? plan_flag : nullptr);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, trace, part_off, pm,
-        part_off ? counts : nullptr, nullptr, xcd_order);
+        part_off ? counts : nullptr, nullptr, xcd_order, nullptr);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }

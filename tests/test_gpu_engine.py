@@ -281,6 +281,32 @@ def test_starting_map_and_in_job_plan_match_oracle(hamlet, monkeypatch, default_
             assert r.num_tokens == ntok and r.entries() == ent
 
 
+@pytest.mark.parametrize("mode", ["trigger", "always", "off"])
+def test_crowded_partition_plans_and_stays_in_lds(monkeypatch, mode):
+    """12,000 distinct keys that all fall into one partition of the starting map ('w0...'):
+    every 1 KiB tile holds far more than kPlanTrigger tokens of it, so the map raises the
+    plan flag, the ordered kernel splits the partition over sibling workgroups and the job
+    stays on the LDS path -- with the trigger and with the plan forced in every job
+    (LOCUST_PLAN_TRIGGER=0).  Without the plan (LOCUST_VPLAN=0) the one LDS table
+    overflows and the job takes the HBM-table fallback (same entries).  (Past ~16 K tokens
+    in one partition a sibling's token list overflows too: the fallback again.)  Whole
+    Hamlet never raises the flag (27 tokens of one partition per tile at most)."""
+    monkeypatch.setenv("LOCUST_PART_TUNE", "0")
+    if mode == "always":
+        monkeypatch.setenv("LOCUST_PLAN_TRIGGER", "0")
+    if mode == "off":
+        monkeypatch.setenv("LOCUST_VPLAN", "0")
+    words = [b"w%05d" % i for i in range(12000)]
+    text = b"\n".join(b" ".join(words[i:i + 10]) for i in range(0, len(words), 10)) + b"\n"
+    ent, ntok, _ = oracle.wordcount(text)
+    eng = lc._C.GpuEngine(lc.make_config("gpu", reduce_path="lds", check=True), len(text),
+                          text.count(b"\n") + 1)
+    for _ in range(2):
+        r = eng.run(text)
+        assert r.num_tokens == ntok and r.entries() == ent
+    assert (eng.stats()["fallbacks"] == 0) == (mode != "off"), eng.stats()
+
+
 @pytest.mark.parametrize("graph", [-1, 0, 1])
 def test_compact_output_hamlet(hamlet, graph):
     """The ordered kernel drains compact records (kv.hpp) into host memory: byte-identical

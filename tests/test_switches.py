@@ -30,7 +30,8 @@ CASES = [
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PART_DEFAULT": "byte"}, "single"),
     ({"LOCUST_VPLAN": "0", "LOCUST_DEVPLAN": "0"}, "single"),
     ({"LOCUST_VPLAN_MIN_KB": "64", "LOCUST_SPLIT_MIN": "256"}, "single"),
-    ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FUSED": "0", "LOCUST_RANK_W0": "0"}, "single"),
+    ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FUSED": "0", "LOCUST_RANK_W0": "0",
+      "LOCUST_PLAN_TRIGGER": "0"}, "single"),
     ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FLOOR": "512", "LOCUST_SMALL_TABLE": "0"}, "single"),
     ({"LOCUST_ORD_RESERVE": "1", "LOCUST_EARLY_PUBLISH": "0"}, "single"),
     ({"LOCUST_MAP_XCD": "0"}, "single"),
