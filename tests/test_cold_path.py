@@ -91,3 +91,21 @@ def test_fresh_engine_first_job_is_cheap(hamlet):
         del eng
     first, steady = min(firsts), min(steadies)
     assert first < 2 * steady + 50e-6, (firsts, steadies)
+
+
+def test_plan_runs_only_when_the_map_saw_crowding():
+    """The in-job plan: the map raises OrderedExtra::plan_flag from a
+    tile's partition counts (kPlanTrigger), the ordered kernel loads the flag with its
+    ticket and plans only when it is up, and the self-clean re-zeroes it for the next job.
+    Whole Hamlet peaks at 27 tokens of one partition per 1 KiB tile under the starting map,
+    below the trigger (profiles/r5/partmap/hamlet_default_map_partitions.txt)."""
+    mt = _src("csrc", "kernels", "map_tile.hpp")
+    trig = int(re.search(r"constexpr u32 kPlanTrigger = (\d+);", mt).group(1))
+    assert 27 < trig <= 64
+    assert "atomicOr(plan_flag, 1u)" in mt
+    d = _src("csrc", "kernels", "dict.hip")
+    assert "__hip_atomic_load(ex.plan_flag" in d
+    assert "vplan = flag != 0;" in d
+    assert "if (ex.plan_flag) *ex.plan_flag = 0;" in d
+    p = _src("csrc", "engine", "pipeline.hip")
+    assert "ex.plan_flag = d_plan_flag" in p and "ex.plan_flag = nullptr;" in p  # fused: always
