@@ -22,8 +22,8 @@ CHILD = r"""
 import json, sys, time
 sys.path.insert(0, sys.argv[1])
 import bench
-cfg, steps, warmup = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-text = bench.synth_shard(cfg, 0, 1) if cfg in bench.SYNTH else bench.load_text(cfg)
+cfg, steps, warmup, rep = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+text = bench.synth_shard(cfg, 0, 1) if cfg in bench.SYNTH else bench.load_text(cfg) * rep
 first = bench.cold_first_run(text)["first_job_ms"]
 ms, _st, res = bench._time_single(text, steps, warmup, "dict", -1)
 print(json.dumps({"ms": ms, "first": first, "unique": res.num_unique}))
@@ -54,6 +54,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--repeat", type=int, default=1, help="text configs: the text N times over")
     a = ap.parse_args()
     got = {v: [] for v in a.variants}
     firsts = {v: [] for v in a.variants}
@@ -61,7 +62,7 @@ def main() -> int:
         order = a.variants if r % 2 == 0 else a.variants[::-1]
         for v in order:
             p = subprocess.run([sys.executable, "-c", CHILD, root_of(v), a.config, str(a.steps),
-                                str(a.warmup)], env=env_of(v), capture_output=True, text=True,
+                                str(a.warmup), str(a.repeat)], env=env_of(v), capture_output=True, text=True,
                                timeout=300)
             if p.returncode:
                 print(p.stderr[-2000:], file=sys.stderr)
