@@ -156,7 +156,13 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
   sz.add<u32>(cap);
   sz.add<u8>(align_up(cap, 16) + 16);
-  if (cap <= kPartBuildMaxTokens && cap_bytes < kMapLargeInput) {
+  // A pass of at most small_pass_bytes (1 KiB tiles <= kPartBlock: the in-job plan's
+  // range) takes the one-kernel ordered build whatever its worst-case token count: natural
+  // text has a third of the tokens the capacity allows, and the large build's device plan
+  // cost ~0.2 ms of a 0.3 ms untuned job at 3-5x Hamlet (docs/PERFORMANCE.md round 5).
+  small_pass = cap > kPartBuildMaxTokens && cap_bytes <= small_pass_bytes && !streaming &&
+               cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict;
+  if ((cap <= kPartBuildMaxTokens || small_pass) && cap_bytes < kMapLargeInput) {
     part_off_tiles = div_up(cap_bytes, kMapTileBytesMin);
   } else if (!streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
     // large single passes (the two-kernel ordered build): 1 KiB tiles below

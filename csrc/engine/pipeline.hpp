@@ -97,6 +97,14 @@ struct DevicePipeline {
   u32 part_tiles = 0;
   // Large single passes: the two-kernel ordered build's partial slots (dict.hip).
   bool large_ordered = false;
+  // LOCUST_SMALL_PASS_KB (construction, default 1024; 0: off): an engine for at most this
+  // many bytes keeps the one-kernel ordered build (and its in-job plan) even when its
+  // worst-case token count passes kPartBuildMaxTokens
+  const u64 small_pass_bytes = [] {
+    const char* e = std::getenv("LOCUST_SMALL_PASS_KB");
+    return (u64)(e ? std::max(0, std::atoi(e)) : 1024) << 10;
+  }();
+  bool small_pass = false;
   KeyCount* d_partials = nullptr;
   u32* d_partial_n = nullptr;
   u32 partial_slots_cap = 0;  // slots per partition d_partials holds
@@ -568,7 +576,7 @@ struct DevicePipeline {
   }
   // Process + Reduce of the dictionary path in ONE kernel (ordered partitions, see
   // launch_dict_ordered) when the tokens carry partition tags and the pass is small.
-  bool ordered_ok() const { return parts_ready && cap <= kPartBuildMaxTokens; }
+  bool ordered_ok() const { return parts_ready && (cap <= kPartBuildMaxTokens || small_pass); }
   // Two-kernel ordered build of a large pass (the map wrote its partition table).
   bool large_ordered_ok() const {
     return large_ordered && parts_ready && part_tiles > 0 && cap > kPartBuildMaxTokens;

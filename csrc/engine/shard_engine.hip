@@ -62,7 +62,8 @@ class GpuShardEngine final : public ShardEngine {
     LOCUST_CHECK_ARG(!shard.source || streamed,
                      "a shard read from a source must be larger than one device pass");
     const bool small_ordered = combine && cfg_.sort_path == SortPath::kDict && !streamed &&
-                               cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
+                               cfg_.map_path == MapPath::kFast &&
+                               (m.cap <= kPartBuildMaxTokens || m.small_pass);
     if (streamed) {
       // a shard larger than one device pass: chunked H2D + map into one dictionary
       LOCUST_CHECK_ARG(combine && cfg_.sort_path == SortPath::kDict,
@@ -205,7 +206,7 @@ class GpuShardEngine final : public ShardEngine {
   bool small_ordered_ok(const TextInput& shard, bool combine) const {
     const DevicePipeline& m = *mp_;
     return combine && cfg_.sort_path == SortPath::kDict && shard.bytes <= m.cap_bytes &&
-           cfg_.map_path == MapPath::kFast && m.cap <= kPartBuildMaxTokens;
+           cfg_.map_path == MapPath::kFast && (m.cap <= kPartBuildMaxTokens || m.small_pass);
   }
   // Host half of a small ordered pass (run for every job): returns the graph key of the
   // device half and the device half itself, which captures everything it needs by value

@@ -34,7 +34,7 @@ CASES = [
       "LOCUST_PLAN_TRIGGER": "0"}, "single"),
     ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FLOOR": "512", "LOCUST_SMALL_TABLE": "0"}, "single"),
     ({"LOCUST_ORD_RESERVE": "1", "LOCUST_EARLY_PUBLISH": "0"}, "single"),
-    ({"LOCUST_MAP_XCD": "0"}, "single"),
+    ({"LOCUST_MAP_XCD": "0", "LOCUST_SMALL_PASS_KB": "0"}, "single"),
     ({"LOCUST_ORD_RESERVE": "1", "LOCUST_FUSE": "1", "LOCUST_PART_TUNE": "0"}, "single"),
     ({"LOCUST_DEV_CACHE": "0"}, "stream"),
     ({"LOCUST_DEV_CACHE_GB": "1", "LOCUST_CHUNK_MB": "1"}, "stream"),
