@@ -20,7 +20,8 @@ void part_map_default_first_byte(PartMapTables* t) {
 // each, cut on the second byte: lowercase four ([.., 'g'), ['g', 'n'), ['n', 't'),
 // ['t', ..)), uppercase three (ALL-CAPS words / [a-m] / [n-z] second letters); digits and
 // every UTF-8 lead byte (0xC2-0xF4) one each; the remaining byte ranges one each; the 'th'
-// words three more (below).  251 partitions (asserted below); the rest stay empty.  A first-byte map left ~50 of the 256 partitions
+// words three more and the 'co' words two more (below).  253 partitions (asserted below);
+// the rest stay empty.  A first-byte map left ~50 of the 256 partitions
 // occupied on English text, so the ordered kernel split the hot letters across sibling
 // workgroups that each scan the whole letter's tokens (whole Hamlet: ordered kernel 28.1
 // vs 22.1 us with a tuned map, profiles/r3_s4/).  Data-independent: no input is sampled.
@@ -35,7 +36,9 @@ void part_map_default(PartMapTables* t) {
   // The 'th' words -- English's most frequent digram and word (the, that, this, thou, ...;
   // 2,525 of Hamlet's 32,940 tokens in one ['tg', 'tn') partition, the untuned job's
   // critical path) -- are cut on their third byte as well: [th, the), [the, thf),
-  // [thf, tho), [tho, tn).  LOCUST_PART_DEFAULT=letters: without (A/B).
+  // [thf, tho), [tho, tn); and the 'co' words (com-, con-: the two-letter prefix with the
+  // most distinct English words; 209 of Hamlet's 5,608 keys in ['cn', 'ct'), whose ranking
+  // then led the kernel) at 'com' and 'cop'.  LOCUST_PART_DEFAULT=letters: without (A/B).
   const char* dv = std::getenv("LOCUST_PART_DEFAULT");
   const bool th = !(dv && dv[0] == 'l');
   cut(0x00, 0);    // controls, space, punctuation before the digits
@@ -56,12 +59,16 @@ void part_map_default(PartMapTables* t) {
       cut3('t', 'h', 'o');
     }
     cut(c, 'n');
+    if (th && c == 'c') {  // com- / con-: the English prefix with the most distinct words
+      cut3('c', 'o', 'm');
+      cut3('c', 'o', 'p');
+    }
     cut(c, 't');
   }
   cut(0x7B, 0);    // {|}~ DEL, UTF-8 continuation bytes, C0/C1
   for (u32 b = 0xC2; b <= 0xF4; ++b) cut(b, 0);
   cut(0xF5, 0);    // bytes no UTF-8 text starts with
-  LOCUST_CHECK_ARG(lo.size() == (th ? 251u : 248u) && lo.size() <= (size_t)kDictParts,
+  LOCUST_CHECK_ARG(lo.size() == (th ? 253u : 248u) && lo.size() <= (size_t)kDictParts,
                    "default partition map: unexpected partition count");
   for (u32 p = 0; p < (u32)kDictParts; ++p) t->lo[p] = p < lo.size() ? lo[p] : ~0ull;
   t->lo[kDictParts] = ~0ull;

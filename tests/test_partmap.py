@@ -58,7 +58,7 @@ def test_default_map_for_empty_input():
     lo = m["lo"]
     assert m["predicted_max"] == 0 and lo[0] == 0 and len(lo) == 257
     used = [x for x in lo[:256] if x != (1 << 64) - 1]
-    assert used == sorted(used) and len(set(used)) == len(used) == 251
+    assert used == sorted(used) and len(set(used)) == len(used) == 253
     part = lambda k: lc._C.part_of_key(lo, k)  # noqa: E731
     # lowercase: four ranges per first letter, cut at the second letters g, n, t
     assert len({part(b"a" + bytes([c])) for c in range(ord("a"), ord("z") + 1)}) == 4
@@ -68,6 +68,8 @@ def test_default_map_for_empty_input():
     assert part(b"tg") == part(b"than") == part(b"thd") < part(b"the") == part(b"they")
     assert part(b"they") < part(b"this") == part(b"thin") < part(b"thou") == part(b"tm")
     assert part(b"tea") < part(b"the") < part(b"to") < part(b"tu")
+    # 'co' words: [cn, com) [com, cop) [cop, ct)
+    assert part(b"cold") < part(b"come") == part(b"content") < part(b"court") < part(b"cu")
     assert part(b"ta") < part(b"tz") < part(b"ua")
     # uppercase: ALL-CAPS / [a-m] / [n-z] second bytes
     assert part(b"HAMLET") != part(b"Hamlet") != part(b"Horatio")
