@@ -16,6 +16,7 @@
 //   --ref-timers (stage times taken where the reference's host timers were)
 // and a synthetic-text generator (BASELINE configs "1M lines" / "10 GB"):
 //   MapReduce --gen FILE (--gen-lines N | --gen-bytes N) [--seed S] [--vocab V]
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -44,6 +45,8 @@ struct CliArgs {
   int node = 0;
   int stage = 0;
   bool window = false;
+  bool byte_range = false;  // --byte-range A:B (stage 1): a byte window instead of lines
+  u64 byte_begin = 0, byte_end = ~0ull;
   JobConfig cfg;
   int gpus = 1;
   bool gpus_given = false;   // --gpus on the command line (even --gpus 1: RCCL rank)
@@ -82,6 +85,7 @@ void help() {
       "  --emits-per-line N         --max-key N                --ref-compat\n"
       "  --stage map|reduce         --spill-dir DIR            --spill-format text|binary|kiv\n"
       "  --inputs a,b,...           --reducer r/R              --result-file FILE\n"
+      "  --byte-range A:B           (stage 1: bytes [A, B) moved to line starts; B empty: EOF)\n"
       "  --output-format gpu|cpu    (result lines with val, or the CPU build's)\n"
       "  --export-kiv FILE          --json FILE|-              --quiet --check --combine\n"
       "  --warmup N --iters N       --chunk-mb N               --ref-timers\n"
@@ -167,6 +171,19 @@ bool parse(int argc, char** argv, CliArgs* a) {
       a->reducers = std::atoi(v.substr(sl + 1).c_str());
       if (a->reducers < 1 || a->reducer < 0 || a->reducer >= a->reducers)
         throw Error("--reducer r/R needs 0 <= r < R");
+    } else if (s == "--byte-range") {
+      const std::string v = need("--byte-range");
+      const size_t c = v.find(':');
+      if (c == std::string::npos || c == 0) throw Error("--byte-range A:B");
+      char* endp = nullptr;
+      a->byte_begin = std::strtoull(v.c_str(), &endp, 10);
+      if (endp != v.c_str() + c) throw Error("--byte-range A:B");
+      if (c + 1 < v.size()) {
+        a->byte_end = std::strtoull(v.c_str() + c + 1, &endp, 10);
+        if (*endp) throw Error("--byte-range A:B");
+      }
+      if (a->byte_end < a->byte_begin) throw Error("--byte-range A:B needs A <= B");
+      a->byte_range = true;
     } else if (s == "--result-file") {
       a->result_file = need("--result-file");
     } else if (s == "--output-format") {
@@ -216,6 +233,10 @@ bool parse(int argc, char** argv, CliArgs* a) {
     a->node = (int)std::strtol(pos[3].c_str(), nullptr, 10);
     if (pos.size() > 4) a->stage = (int)std::strtol(pos[4].c_str(), nullptr, 10);
   }
+  if (a->byte_range) {
+    if (a->stage != 1) throw Error("--byte-range is a stage-1 (map) flag");
+    a->window = false;  // the byte window replaces the positional line window
+  }
   return true;
 }
 
@@ -255,6 +276,12 @@ struct JsonOut {
   void str(const char* k, const std::string& v) {
     std::string e;
     for (char c : v) {
+      if ((unsigned char)c < 0x20) {  // control bytes (a TAB delimiter) as \u00XX
+        char u[8];
+        std::snprintf(u, sizeof(u), "\\u%04x", (unsigned)(unsigned char)c);
+        e += u;
+        continue;
+      }
       if (c == '"' || c == '\\') e.push_back('\\');
       e.push_back(c);
     }
@@ -587,8 +614,16 @@ int run_map_stage(const CliArgs& a) {
   const bool cpu = a.cfg.backend == Backend::kCpu;
   const char* dev = cpu ? "CPU" : "GPU";
   const std::string path = spill_path(a, a.node);
-  const MapStageResult m = map_stage(a.cfg, a.file, a.window ? a.line_start : -1,
-                                     a.window ? a.line_end : -1, path, a.spill_fmt);
+  MapWindow win;
+  if (a.byte_range) {
+    win.by_bytes = true;
+    win.byte_begin = a.byte_begin;
+    win.byte_end = a.byte_end;
+  } else if (a.window) {
+    win.line_start = a.line_start;
+    win.line_end = a.line_end;
+  }
+  const MapStageResult m = map_stage(a.cfg, a.file, win, path, a.spill_fmt);
   const WordCountResult& r = m.result;
   if (!cpu) std::printf("Length: %i\n", (int)m.lines);
   for (u64 k = 0; k < r.overflow_lines; ++k) std::printf("WARN: Exceeded emit limit\n");
@@ -605,12 +640,33 @@ int run_map_stage(const CliArgs& a) {
     j.str("input", a.file);
     j.kv("line_start", std::to_string(a.window ? a.line_start : 0));
     j.kv("line_end", std::to_string(a.window ? a.line_end : -1));
+    if (a.byte_range) {  // the range asked for, and the bytes it moved to
+      j.u("byte_range_begin", a.byte_begin);
+      j.kv("byte_range_end", a.byte_end == ~0ull ? "-1" : std::to_string(a.byte_end));
+    }
+    j.u("byte_begin", m.byte_begin);
+    j.u("byte_end", m.byte_end);
+    {  // the input's identity and the tokenizer settings (a resume checks both)
+      struct stat st {};
+      if (::stat(a.file.c_str(), &st) == 0) {
+        j.u("input_size", (unsigned long long)st.st_size);
+        j.u("input_mtime_ns", (unsigned long long)st.st_mtim.tv_sec * 1000000000ull +
+                                  (unsigned long long)st.st_mtim.tv_nsec);
+        j.u("input_inode", (unsigned long long)st.st_ino);
+      }
+      j.kv("emits_per_line", std::to_string(a.cfg.emits_per_line));
+      j.kv("max_key", std::to_string(a.cfg.max_key_len));
+      j.str("delimiters", a.cfg.delimiters);
+    }
     j.kv("combined", a.cfg.ref_compat ? "false" : "true");
     j.kv("streamed", m.streamed ? "true" : "false");
     j.u("input_bytes", m.input_bytes);
     j.num("map_ms", r.times.h2d_ms + r.times.map_ms);
     j.num("process_ms", r.times.process_ms + r.times.reduce_ms);
     j.num("job_ms", m.job_ms);
+    j.num("window_ms", m.window_ms);
+    j.num("setup_ms", m.setup_ms);
+    j.num("run_ms", m.run_ms);
     j.num("spill_write_ms", m.spill_write_ms);
     j.u("peak_rss_kb", peak_rss_kb());
     emit_json(a, j.done());

@@ -114,21 +114,45 @@ std::vector<PackedKey> plan_reducer_splitters(const std::vector<SpillIndex>& idx
   return spl;
 }
 
-MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, i64 line_start,
-                         i64 line_end, const std::string& spill, SpillFormat fmt) {
+MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, const MapWindow& win,
+                         const std::string& spill, SpillFormat fmt) {
   constexpr u64 kDefaultStreamChunk = 256ull << 20;
   const bool cpu = cfg_in.backend == Backend::kCpu;
-  const bool window = line_start >= 0;
+  const bool lwin = !win.by_bytes && win.line_start >= 0;
+  LOCUST_CHECK_ARG(!(win.by_bytes && cfg_in.ref_compat),
+                   "a byte window is not a reference-compatible stage 1 (use a line window)");
   MapStageResult out;
   WordCountResult& r = out.result;
   std::vector<KeyCount> recs;
   const u64 t0 = now_ns();
+  LineWindow w;
+  if (win.by_bytes) {
+    w = byte_window(file, win.byte_begin, win.byte_end);
+  } else if (lwin && !cfg_in.ref_compat) {
+    w = find_line_window(file, win.line_start, win.line_end);
+  } else {
+    w.end = file_size(file);
+  }
+  out.byte_begin = w.begin;
+  out.byte_end = w.end;
+  out.input_bytes = w.end - w.begin;
+  const u64 tw = now_ns();
+  out.window_ms = (tw - t0) * 1e-6;
+  u64 ts = tw, tr = tw;
   if (cpu || cfg_in.ref_compat) {
-    const bool use_window = window && !(cpu && cfg_in.ref_compat);
-    LoadedText text = load_lines(file, use_window ? line_start : -1, use_window ? line_end : -1,
-                                 cfg_in.ref_compat);
+    LoadedText text;
+    if (!cfg_in.ref_compat) {  // the window's bytes (a line or byte window, or the file)
+      std::vector<char> buf(out.input_bytes);
+      read_file_range_into(file, buf.data(), w.begin, out.input_bytes, nullptr);
+      text = text_from_buffer(buf.data(), buf.size(), -1, -1, false);
+    } else {
+      const bool use_window = lwin && !(cpu && cfg_in.ref_compat);
+      text = load_lines(file, use_window ? win.line_start : -1, use_window ? win.line_end : -1,
+                        cfg_in.ref_compat);
+      out.input_bytes = text.input.bytes;
+    }
     out.lines = text.input.num_lines;
-    out.input_bytes = text.input.bytes;
+    ts = now_ns();
     if (cfg_in.ref_compat) {
       std::vector<PackedKey> toks;
       if (cpu) {
@@ -143,37 +167,39 @@ MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, i64 l
       r = CpuWordCount(cfg_in).run(text.input);
       recs = entries_to_records(r.entries);
     }
+    tr = now_ns();
   } else {
-    LineWindow w;
-    if (window)
-      w = find_line_window(file, line_start, line_end);
-    else
-      w.end = file_size(file);
-    out.input_bytes = w.end - w.begin;
     JobConfig cfg = cfg_in;
     cfg.graph = 0;  // stage events: the map and sort times
     const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
     if (out.input_bytes > chunk) {
       cfg.chunk_bytes = chunk;
       GpuWordCount eng(cfg, out.input_bytes, out.input_bytes);
+      ts = now_ns();
       auto src = open_file_range_source(file, w.begin, w.end);
       r = eng.run_source(*src);
+      tr = now_ns();
       out.lines = src->lines();
       out.streamed = true;
+      recs = entries_to_records(r.entries);  // before the engine (and its buffers) goes
     } else {
       GpuWordCount eng(cfg, std::max<u64>(out.input_bytes, 1), std::max<u64>(out.input_bytes, 1));
+      ts = now_ns();
       TextInput in;
       in.data = eng.input_buffer();
       in.bytes = read_file_range_into(file, eng.input_buffer(), w.begin, out.input_bytes, &out.lines);
       in.num_lines = out.lines;
       r = eng.run(in);
+      tr = now_ns();
+      recs = entries_to_records(r.entries);
     }
-    recs = entries_to_records(r.entries);  // before the engine (and its buffers) goes
-    if (window) out.lines = w.lines;
+    if (lwin) out.lines = w.lines;
   }
   r.entries = EntryList{};
   r.num_lines = out.lines;
   const u64 t1 = now_ns();
+  out.setup_ms = (ts - tw) * 1e-6;
+  out.run_ms = (tr - ts) * 1e-6;
   write_spill(spill, recs, fmt, &out.index);
   write_spill_index(spill_index_path(spill), out.index);
   out.spill_records = recs.size();

@@ -49,14 +49,27 @@ LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 lin
 u64 count_lines(const char* data, u64 bytes);
 // The byte range [begin, end) of the line window [line_start, line_end) of a file (the
 // reference's per-node line ranges, main.cu:369-374) and its line count, found by a parallel
-// newline scan of the file up to the window's end in bounded memory (never the whole file
-// in memory).  line_end < 0: to the end of the file.
+// newline scan in bounded memory (never the whole file in memory).  line_end < 0: to the
+// end of the file.  The scan starts from a per-file sparse line index (the newline count
+// at every 8 MiB block start, cached under the file's identity like the partition map:
+// line_index_cache_path), so only the first window that passes a block pays for it.
 struct LineWindow {
   u64 begin = 0, end = 0;  // bytes
   u64 lines = 0;           // lines in [begin, end) (a final line without '\n' counts)
 };
 LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_end,
                             u32 threads = 0);
+// The sparse line index's cache file ("" when disabled: LOCUST_LINE_CACHE=0, or no cache
+// directory / no such file).  Same directory rules as partmap_cache_path.
+std::string line_index_cache_path(const std::string& input);
+// The first line start at or after byte `off`: off when off == 0 or byte off-1 is '\n',
+// else just after the next '\n' (the file size when there is none).
+u64 line_start_at(const std::string& path, u64 off);
+// A byte window [begin, end) of a file moved to line starts (line_start_at of both ends),
+// exactly as file_shards cuts: windows [a0, a1), [a1, a2), ... of any offsets hold every
+// line once.  Only the bytes from each end to its next newline are read; lines = 0 (the
+// reader of the range counts them).
+LineWindow byte_window(const std::string& path, u64 begin, u64 end);
 
 // ---- spill files (map-output checkpoint) ----
 enum class SpillFormat { kText, kBinary, kKiv };

@@ -45,23 +45,42 @@ SpillIndex index_records(const std::vector<KeyCount>& recs);
 std::vector<PackedKey> plan_reducer_splitters(const std::vector<SpillIndex>& idx, int reducers);
 
 // ---- stage 1 ----
+// The part of the input a map stage reads: a line window (the reference's per-node line
+// ranges, main.cu:369-374) or a byte window whose ends move to line starts (byte_window),
+// which a launcher gets from the file size alone -- no newline scan of the prefix.
+struct MapWindow {
+  i64 line_start = -1, line_end = -1;  // line_start < 0: no line window
+  bool by_bytes = false;
+  u64 byte_begin = 0, byte_end = ~0ull;
+};
 struct MapStageResult {
   WordCountResult result;  // counts and stage times (entries released after the spill)
   u64 lines = 0, input_bytes = 0;
+  u64 byte_begin = 0, byte_end = 0;  // the bytes of the file mapped
   u64 spill_records = 0;
   bool streamed = false;   // the window streamed through the engine (larger than a pass)
   double job_ms = 0, spill_write_ms = 0;
+  // job_ms = window_ms (finding the window's bytes) + setup_ms (engine construction) +
+  // run_ms (read / stream + map + combine) + the records' copy out of the engine
+  double window_ms = 0, setup_ms = 0, run_ms = 0;
   SpillIndex index;
 };
-// Stage 1 over the line window [line_start, line_end) of `file` (line_start < 0: the whole
-// file): the job's combined output -- one (key, count) record per distinct key, key order
-// -- spilled to `spill` in `fmt`, with its index at spill_index_path(spill).  GPU: the
-// window is found by find_line_window and read into the engine's pinned buffer, or
-// streamed past one device pass (chunk_bytes, default 256 MiB), with hipEvent stage times.
-// cfg.ref_compat: the reference's spill instead -- one record per token, sorted -- from the
-// reference's loader (the CPU build ignores the window and drops the last line, B1).
-MapStageResult map_stage(const JobConfig& cfg, const std::string& file, i64 line_start,
-                         i64 line_end, const std::string& spill, SpillFormat fmt);
+// Stage 1 over a window of `file` (none: the whole file): the job's combined output -- one
+// (key, count) record per distinct key, key order -- spilled to `spill` in `fmt`, with its
+// index at spill_index_path(spill).  GPU: the window's bytes (find_line_window or
+// byte_window) are read into the engine's pinned buffer, or streamed past one device pass
+// (chunk_bytes, default 256 MiB), with hipEvent stage times.  cfg.ref_compat: the
+// reference's spill instead -- one record per token, sorted -- from the reference's loader
+// (the CPU build ignores the window and drops the last line, B1); not with a byte window.
+MapStageResult map_stage(const JobConfig& cfg, const std::string& file, const MapWindow& win,
+                         const std::string& spill, SpillFormat fmt);
+inline MapStageResult map_stage(const JobConfig& cfg, const std::string& file, i64 line_start,
+                                i64 line_end, const std::string& spill, SpillFormat fmt) {
+  MapWindow w;
+  w.line_start = line_start;
+  w.line_end = line_end;
+  return map_stage(cfg, file, w, spill, fmt);
+}
 
 struct ReduceStageStats {
   u64 input_files = 0, indexed_files = 0, loaded_files = 0;

@@ -298,10 +298,32 @@ std::unique_ptr<TextSource> open_file_range_source(const std::string& path, u64 
   return std::unique_ptr<TextSource>(new FileTextSource(path, threads, begin, end));
 }
 
-// Cut k of P lies at the start of the first line that begins at or after byte size*k/P:
-// the byte after the first '\n' at or after offset size*k/P - 1 (the reference's per-node
-// line ranges, main.cu:369-374, as byte ranges).  Only small windows around the cuts are
-// read -- never the whole file.
+namespace {
+
+// The first line start at or after byte `off` of an open file of n bytes: off itself when
+// off == 0 or byte off-1 is a '\n', else the byte after the next '\n' (n when none).  Reads
+// only from off-1 up to that newline.
+u64 line_start_at_fd(int fd, u64 n, u64 off, std::vector<char>* buf, const std::string& path) {
+  if (off == 0) return 0;
+  if (off >= n) return n;
+  u64 at = off - 1;
+  while (at < n) {
+    const u64 len = std::min<u64>(buf->size(), n - at);
+    const ssize_t got = ::pread(fd, buf->data(), (size_t)len, (off_t)at);
+    if (got < 0 && errno == EINTR) continue;
+    if (got <= 0) throw Error("short read: " + path);
+    const void* nl = std::memchr(buf->data(), '\n', (size_t)got);
+    if (nl) return at + (u64)(static_cast<const char*>(nl) - buf->data()) + 1;
+    at += (u64)got;
+  }
+  return n;
+}
+
+}  // namespace
+
+// Cut k of P lies at the start of the first line that begins at or after byte size*k/P
+// (the reference's per-node line ranges, main.cu:369-374, as byte ranges).  Only small
+// windows around the cuts are read -- never the whole file.
 std::vector<FileRange> file_shards(const std::string& path, int parts) {
   LOCUST_CHECK_ARG(parts >= 1, "parts must be >= 1");
   Fd f(path);
@@ -309,25 +331,28 @@ std::vector<FileRange> file_shards(const std::string& path, int parts) {
   std::vector<u64> cut((size_t)parts + 1, n);
   cut[0] = 0;
   std::vector<char> buf(64 << 10);
-  for (int k = 1; k < parts; ++k) {
-    const u64 target = n * (u64)k / (u64)parts;
-    u64 at = std::max<u64>(target, 1) - 1, found = n;
-    while (at < n) {
-      const u64 len = std::min<u64>(buf.size(), n - at);
-      const ssize_t got = ::pread(f.fd, buf.data(), (size_t)len, (off_t)at);
-      if (got <= 0) throw Error("short read: " + path);
-      const void* nl = std::memchr(buf.data(), '\n', (size_t)got);
-      if (nl) {
-        found = at + (u64)(static_cast<const char*>(nl) - buf.data()) + 1;
-        break;
-      }
-      at += (u64)got;
-    }
-    cut[(size_t)k] = std::max(cut[(size_t)k - 1], target == 0 ? 0 : found);
-  }
+  for (int k = 1; k < parts; ++k)
+    cut[(size_t)k] = std::max(cut[(size_t)k - 1],
+                              line_start_at_fd(f.fd, n, n * (u64)k / (u64)parts, &buf, path));
   std::vector<FileRange> out((size_t)parts);
   for (int k = 0; k < parts; ++k) out[(size_t)k] = {cut[(size_t)k], cut[(size_t)k + 1] - cut[(size_t)k]};
   return out;
+}
+
+u64 line_start_at(const std::string& path, u64 off) {
+  Fd f(path);
+  std::vector<char> buf(64 << 10);
+  return line_start_at_fd(f.fd, f.size(), off, &buf, path);
+}
+
+LineWindow byte_window(const std::string& path, u64 begin, u64 end) {
+  Fd f(path);
+  const u64 n = f.size();
+  std::vector<char> buf(64 << 10);
+  LineWindow w;
+  w.begin = line_start_at_fd(f.fd, n, begin, &buf, path);
+  w.end = std::max(w.begin, end >= n ? n : line_start_at_fd(f.fd, n, end, &buf, path));
+  return w;  // (lines: counted by whoever reads the range)
 }
 
 u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64* lines,
@@ -342,25 +367,161 @@ u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64
 
 u64 file_size(const std::string& path) { return Fd(path).size(); }
 
+// ---------------- per-file caches: directory and file identity ----------------
+namespace {
+u64 fnv1a(u64 h, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+// LOCUST_CACHE_DIR, else $XDG_CACHE_HOME/locust, else ~/.cache/locust ("" when none).
+std::string cache_dir() {
+  if (const char* d = std::getenv("LOCUST_CACHE_DIR"); d && *d) return d;
+  if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) return std::string(x) + "/locust";
+  if (const char* h = std::getenv("HOME"); h && *h) return std::string(h) + "/.cache/locust";
+  return "";
+}
+
+// FNV-1a of a file's identity: real path, size, mtime, inode, device (false: no such file).
+bool file_identity_hash(const std::string& input, u64* h) {
+  struct stat st;
+  char real[4096];
+  if (::stat(input.c_str(), &st) != 0 || !::realpath(input.c_str(), real)) return false;
+  *h = fnv1a(1469598103934665603ull, real, std::strlen(real));
+  const u64 id[5] = {(u64)st.st_size, (u64)st.st_mtim.tv_sec, (u64)st.st_mtim.tv_nsec,
+                     (u64)st.st_ino, (u64)st.st_dev};
+  *h = fnv1a(*h, id, sizeof(id));
+  return true;
+}
+
+// Best-effort atomic write of a cache file (directory mode 0700, one level up too).
+void save_cache_file(const std::string& path, const std::vector<char>& bytes) {
+  const size_t slash = path.rfind('/');
+  if (slash != std::string::npos) {
+    const std::string dir = path.substr(0, slash);
+    const size_t up = dir.rfind('/');
+    if (up != std::string::npos && up > 0) (void)::mkdir(dir.substr(0, up).c_str(), 0700);
+    (void)::mkdir(dir.c_str(), 0700);
+  }
+  const std::string tmp = path + "." + std::to_string((long long)::getpid()) + ".tmp";
+  std::FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  bool ok = bytes.empty() || std::fwrite(bytes.data(), 1, bytes.size(), f) == bytes.size();
+  ok = std::fclose(f) == 0 && ok;
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) (void)::unlink(tmp.c_str());
+}
+
+// ---- sparse line index (find_line_window) ----
+// nl_before[i] = newlines in [0, i * kLixBlock): a contiguous prefix of the file's blocks,
+// grown by every scan that passes them; complete: a scan reached EOF and `total` is the
+// file's line count (a final line without '\n' counts).
+constexpr u64 kLixBlock = 8ull << 20;
+constexpr char kLixMagic[8] = {'L', 'C', 'S', 'T', 'L', 'I', 'X', '1'};
+struct LineIndex {
+  std::vector<u64> nl_before;
+  bool complete = false;
+  u64 total = 0;
+};
+
+bool load_line_index(const std::string& path, u64 file_bytes, LineIndex* lix) {
+  if (path.empty()) return false;
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  char magic[8];
+  u64 head[4] = {};  // block bytes, file bytes, complete, total
+  u64 m = 0;
+  bool ok = std::fread(magic, 8, 1, f) == 1 && std::memcmp(magic, kLixMagic, 8) == 0 &&
+            std::fread(head, sizeof(head), 1, f) == 1 && head[0] == kLixBlock &&
+            head[1] == file_bytes && std::fread(&m, sizeof(m), 1, f) == 1 && m >= 1 &&
+            (m - 1) * kLixBlock < std::max<u64>(file_bytes, 1);
+  if (ok) {
+    lix->nl_before.resize(m);
+    ok = std::fread(lix->nl_before.data(), sizeof(u64), m, f) == m && lix->nl_before[0] == 0;
+    for (u64 i = 1; ok && i < m; ++i) ok = lix->nl_before[i] >= lix->nl_before[i - 1];
+    lix->complete = head[2] != 0;
+    lix->total = head[3];
+  }
+  std::fclose(f);
+  if (!ok) *lix = LineIndex();
+  return ok;
+}
+
+void save_line_index(const std::string& path, u64 file_bytes, const LineIndex& lix) {
+  if (path.empty() || lix.nl_before.empty()) return;
+  std::vector<char> b(8 + 4 * 8 + 8 + lix.nl_before.size() * 8);
+  char* p = b.data();
+  std::memcpy(p, kLixMagic, 8);
+  const u64 head[4] = {kLixBlock, file_bytes, lix.complete ? 1ull : 0ull, lix.total};
+  std::memcpy(p + 8, head, sizeof(head));
+  const u64 m = lix.nl_before.size();
+  std::memcpy(p + 40, &m, 8);
+  std::memcpy(p + 48, lix.nl_before.data(), m * 8);
+  save_cache_file(path, b);
+}
+}  // namespace
+
+std::string line_index_cache_path(const std::string& input) {
+  if (const char* e = std::getenv("LOCUST_LINE_CACHE"))
+    if (e[0] == '0') return "";
+  const std::string dir = cache_dir();
+  u64 h = 0;
+  if (dir.empty() || !file_identity_hash(input, &h)) return "";
+  char name[64];
+  std::snprintf(name, sizeof(name), "/lines-%016llx.bin", (unsigned long long)h);
+  return dir + name;
+}
+
+// Line k starts after the k-th '\n' (line 0 at byte 0).  The scan starts at the last block
+// of the cached sparse line index that lies before the first newline it needs (so a window
+// deep in a file costs one block, not the file's prefix, once any scan has passed there),
+// runs T threads x 8 MiB blocks per round (never the whole file in memory), and records the
+// newline count at every block start it passes.
 LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_end, u32 threads) {
   Fd f(path);
   const u64 n = f.size();
   const u64 s = (u64)std::max<i64>(line_start, 0);
-  const bool open_end = line_end < 0;
+  bool open_end = line_end < 0;
   const u64 e = open_end ? ~0ull : std::max<u64>((u64)line_end, s);
   constexpr u64 kNone = ~0ull;
-  // Line k starts after the k-th '\n' (line 0 at byte 0): find the starts of lines s and e.
+  constexpr u64 B = kLixBlock;
+  const std::string cpath = line_index_cache_path(path);
+  LineIndex lix;
+  load_line_index(cpath, n, &lix);
+  const u64 m0 = lix.nl_before.size();
+  const bool complete0 = lix.complete;
+  LineWindow w;
+  if (lix.complete) {  // the line count is known: clamp the window to it
+    if (s >= lix.total) {
+      w.begin = w.end = n;
+      return w;
+    }
+    if (!open_end && e >= lix.total) open_end = true;
+  }
   u64 at[2] = {s == 0 ? 0 : kNone, open_end ? kNone : (e == 0 ? 0 : kNone)};
   const u64 want[2] = {s, e};
+  // first block: the last indexed block start with fewer newlines before it than the first
+  // newline still wanted (only EOF wanted: the last indexed block)
+  const u64 first_want = at[0] == kNone ? s : (at[1] == kNone && !open_end ? e : kNone);
+  u64 blk0 = 0;
+  if (m0) {
+    if (first_want == kNone) {
+      blk0 = m0 - 1;
+    } else {
+      const auto it = std::lower_bound(lix.nl_before.begin(), lix.nl_before.end(), first_want);
+      blk0 = (u64)(it - lix.nl_before.begin()) - 1;  // nl_before[0] == 0 < first_want
+    }
+  }
   const u32 T = std::max<u32>(1, io_threads(threads, n));
-  const u64 B = 8ull << 20;  // bytes per thread and round: T x 8 MiB in memory at most
   std::vector<std::vector<char>> buf(T, std::vector<char>(B));
   std::vector<u64> nls(T), got(T);
   std::vector<char> ok(T, 1);
-  u64 seen = 0;      // newlines before the current block
-  u64 after_nl = 0;  // offset just after the last newline seen
-  u64 base = 0;
-  auto done = [&] { return at[0] != kNone && (open_end ? false : at[1] != kNone); };
+  u64 base = blk0 * B;
+  u64 seen = m0 ? lix.nl_before[blk0] : 0;  // newlines before `base`
+  u64 after_nl = kNone;                     // offset just after the last newline seen
+  auto done = [&] {
+    return at[0] != kNone && (open_end ? lix.complete : at[1] != kNone);
+  };
   while (base < n && !done()) {
     auto work = [&](u32 t) {
       const u64 a = base + (u64)t * B;
@@ -380,6 +541,7 @@ LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_en
       if (!ok[t]) throw Error("short read: " + path);
       const char* blk = buf[t].data();
       const u64 blk_off = base + (u64)t * B;
+      if (blk_off / B == lix.nl_before.size()) lix.nl_before.push_back(seen);
       for (int k = 0; k < 2; ++k) {
         if (at[k] != kNone || (k == 1 && open_end) || seen + nls[t] < want[k]) continue;
         const char* p = blk;  // the (want - seen)-th newline of this block ends line want - 1
@@ -400,22 +562,27 @@ LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_en
     }
     base += (u64)T * B;
   }
-  LineWindow w;
+  if (base >= n && !lix.complete) {  // the scan reached EOF: the file's line count
+    // a final line without a newline counts; bytes after the scan's start with no newline
+    // among them are such a line
+    const u64 last_nl_end = after_nl != kNone ? after_nl : blk0 * B;
+    lix.complete = true;
+    lix.total = seen + (n > last_nl_end ? 1 : 0);
+  }
+  if (lix.nl_before.size() > m0 || lix.complete != complete0) save_line_index(cpath, n, lix);
   if (at[0] != kNone && at[1] != kNone && !open_end) {
     w.begin = at[0];
     w.end = std::max(at[0], at[1]);
     w.lines = e - s;
     return w;
   }
-  // the scan reached EOF: `seen` newlines, plus a final line without one when the last
-  // byte is not a newline (it starts at after_nl)
-  const bool unterminated = n > after_nl;
-  const u64 total = seen + (unterminated ? 1 : 0);
+  // the window runs to EOF (the line count is known now)
+  const u64 total = lix.total;
   if (s >= total) {
     w.begin = w.end = n;
     return w;
   }
-  w.begin = at[0] != kNone ? at[0] : after_nl;  // (only line s == seen can be unfound)
+  w.begin = at[0];  // (found: line s < total starts after the s-th newline, or at 0)
   w.end = n;
   w.lines = std::min(total, e) - s;
   return w;
@@ -924,34 +1091,14 @@ std::vector<KeyCount> entries_to_records(const EntryList& e) {
 // ---------------- partition-map cache ----------------
 namespace {
 constexpr char kPmcMagic[8] = {'L', 'C', 'S', 'T', 'P', 'M', 'C', '1'};
-u64 fnv1a(u64 h, const void* p, size_t n) {
-  const unsigned char* b = static_cast<const unsigned char*>(p);
-  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
-  return h;
-}
 }  // namespace
 
 std::string partmap_cache_path(const std::string& input, const JobConfig& cfg) {
   if (const char* e = std::getenv("LOCUST_PART_CACHE"))
     if (e[0] == '0') return "";
-  std::string dir;
-  if (const char* d = std::getenv("LOCUST_CACHE_DIR"); d && *d) {
-    dir = d;
-  } else if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) {
-    dir = std::string(x) + "/locust";
-  } else if (const char* h = std::getenv("HOME"); h && *h) {
-    dir = std::string(h) + "/.cache/locust";
-  } else {
-    return "";
-  }
-  struct stat st;
-  char real[4096];
-  if (::stat(input.c_str(), &st) != 0 || !::realpath(input.c_str(), real)) return "";
-  u64 h = 1469598103934665603ull;
-  h = fnv1a(h, real, std::strlen(real));
-  const u64 id[5] = {(u64)st.st_size, (u64)st.st_mtim.tv_sec, (u64)st.st_mtim.tv_nsec,
-                     (u64)st.st_ino, (u64)st.st_dev};
-  h = fnv1a(h, id, sizeof(id));
+  const std::string dir = cache_dir();
+  u64 h = 0;
+  if (dir.empty() || !file_identity_hash(input, &h)) return "";
   const int tok[4] = {cfg.emits_per_line, cfg.max_key_len, (int)cfg.map_path, (int)cfg.sort_path};
   h = fnv1a(h, tok, sizeof(tok));
   h = fnv1a(h, cfg.delimiters.data(), cfg.delimiters.size());
@@ -978,21 +1125,12 @@ bool load_partmap_cache(const std::string& path, std::vector<u64>* lo) {
 
 void save_partmap_cache(const std::string& path, const std::vector<u64>& lo) {
   if (path.empty() || lo.size() != (size_t)kDictParts + 1) return;
-  const size_t slash = path.rfind('/');
-  if (slash != std::string::npos) {  // the directory, mode 0700 (best effort, one level up too)
-    const std::string dir = path.substr(0, slash);
-    const size_t up = dir.rfind('/');
-    if (up != std::string::npos && up > 0) (void)::mkdir(dir.substr(0, up).c_str(), 0700);
-    (void)::mkdir(dir.c_str(), 0700);
-  }
-  const std::string tmp = path + "." + std::to_string((long long)::getpid()) + ".tmp";
-  std::FILE* f = std::fopen(tmp.c_str(), "wb");
-  if (!f) return;
   const u32 n = (u32)lo.size();
-  bool ok = std::fwrite(kPmcMagic, 8, 1, f) == 1 && std::fwrite(&n, sizeof(n), 1, f) == 1 &&
-            std::fwrite(lo.data(), sizeof(u64), n, f) == n;
-  ok = std::fclose(f) == 0 && ok;
-  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) (void)::unlink(tmp.c_str());
+  std::vector<char> b(8 + sizeof(n) + n * sizeof(u64));
+  std::memcpy(b.data(), kPmcMagic, 8);
+  std::memcpy(b.data() + 8, &n, sizeof(n));
+  std::memcpy(b.data() + 8 + sizeof(n), lo.data(), n * sizeof(u64));
+  save_cache_file(path, b);
 }
 
 // ---------------- output ----------------

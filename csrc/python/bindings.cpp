@@ -841,6 +841,14 @@ PYBIND11_MODULE(_locust, m) {
     return std::make_tuple(w.begin, w.end, w.lines);
   }, py::arg("path"), py::arg("line_start"), py::arg("line_end"),
         "(begin, end, lines) of the line window [line_start, line_end) of a file");
+  m.def("byte_window", [](const std::string& path, u64 a, u64 b) {
+    py::gil_scoped_release nogil;
+    const LineWindow w = byte_window(path, a, b);
+    return std::make_tuple(w.begin, w.end, w.lines);
+  }, py::arg("path"), py::arg("begin"), py::arg("end"),
+        "(begin, end, 0): bytes [begin, end) of a file moved to line starts");
+  m.def("line_start_at", &line_start_at, py::arg("path"), py::arg("offset"));
+  m.def("line_index_cache_path", &line_index_cache_path, py::arg("path"));
   m.def("spill_index", [](const std::string& spill) -> py::object {
     SpillIndex x;
     if (!read_spill_index(spill, &x)) return py::none();

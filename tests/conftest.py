@@ -27,3 +27,17 @@ def hamlet() -> bytes:
 @pytest.fixture(scope="session")
 def cli() -> str:
     return os.path.join(ROOT, "build", "MapReduce")
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _private_cache_dir(tmp_path_factory):
+    """Per-session cache directory (partition maps, sparse line indexes): tests never read
+    or write the user's ~/.cache/locust.  A test that wants its own sets LOCUST_CACHE_DIR."""
+    if "LOCUST_CACHE_DIR" in os.environ:
+        yield
+        return
+    os.environ["LOCUST_CACHE_DIR"] = str(tmp_path_factory.mktemp("locust_cache"))
+    try:
+        yield
+    finally:
+        os.environ.pop("LOCUST_CACHE_DIR", None)
