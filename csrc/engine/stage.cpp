@@ -98,8 +98,9 @@ std::vector<PackedKey> plan_reducer_splitters(const std::vector<SpillIndex>& idx
   u64 before = 0;
   size_t j = 0;
   for (int i = 1; i < reducers; ++i) {
-    const long double target = (long double)total * i / reducers;
-    while (j < all.size() && (long double)before < target) {
+    // before < total * i / R, exactly (the launcher's Python planner mirrors this)
+    const unsigned __int128 target = (unsigned __int128)total * (unsigned)i;
+    while (j < all.size() && (unsigned __int128)before * (unsigned)reducers < target) {
       const size_t k0 = j;
       while (j < all.size() && key_compare(all[j].key.w, all[k0].key.w) == 0) before += all[j++].weight;
     }

@@ -26,8 +26,14 @@ changes here:
   are opened with ``O_NOFOLLOW`` and the opened file's real path is checked again.
 
 Requests (JSON frames, see protocol.py): ``hello``, ``run`` {argv, env, timeout},
-``get`` {path, offset, length}, ``put`` {path, data, append}.  The reference's
-unauthenticated raw-text form (``"<x> prog args..."``) is recognised and refused.
+``get`` {path, offset, length}, ``put`` {path, data, append}, ``stat`` {path} (size, mtime,
+inode of an input file: a resume checks that the input is unchanged) and ``pull`` {peer,
+src, dest, size, ranges}: this daemon fetches byte ranges of a file from a peer daemon
+(same token) into a file of its own root, each at its own offset -- a sparse copy of the
+spill of the same size, so the spill's index stays valid.  Reducers get their key range of
+every spill this way, straight from the mapper hosts (the reference's missing inter-node
+transfer), never through the launcher.  The reference's unauthenticated
+raw-text form (``"<x> prog args..."``) is recognised and refused.
 """
 from __future__ import annotations
 
@@ -204,6 +210,9 @@ class _Handler(socketserver.BaseRequestHandler):
             if not isinstance(env, dict) or not _env_allowed(env):
                 return {"ok": False, "error": "run: env may only set the rank layout "
                                              "(RANK, WORLD_SIZE, MASTER_*, ...) and LOCUST_*"}
+            # the CLI's per-file caches (partition maps, line indexes) stay inside the root
+            env = dict(env)
+            env["LOCUST_CACHE_DIR"] = os.path.join(self.server.root, "cache")
             t0 = time.time()
             # always run from the repository root (module imports resolve to this package)
             rc, out, err = _run(argv, env, _REPO, req.get("timeout"), sock)
@@ -227,7 +236,54 @@ class _Handler(socketserver.BaseRequestHandler):
             with os.fdopen(self._open_checked(path, flags), "ab" if req.get("append") else "wb") as f:
                 f.write(base64.b64decode(req.get("data", "")))
             return {"ok": True}
+        if op == "stat":
+            st = os.stat(str(req.get("path", "")))
+            return {"ok": True, "size": st.st_size, "mtime_ns": st.st_mtime_ns,
+                    "inode": st.st_ino}
+        if op == "pull":
+            return self._pull(req)
         return {"ok": False, "error": f"unknown op {op!r}"}
+
+    def _pull(self, req: dict) -> dict:
+        """Byte ranges of `src` on a peer daemon into `dest` under this root, each written at
+        its own offset; `size` (optional) sets the file's length (the rest stays a hole)."""
+        from .protocol import request as _request
+
+        peer = req.get("peer")
+        if not (isinstance(peer, list) and len(peer) == 2 and isinstance(peer[0], str)
+                and isinstance(peer[1], int)):
+            return {"ok": False, "error": "pull: peer must be [address, port]"}
+        ranges = req.get("ranges") or [[0, -1]]
+        dest = self._path(req.get("dest", ""))
+        os.makedirs(os.path.dirname(dest), exist_ok=True)
+        fd = self._open_checked(dest, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+        got = 0
+        frame = 32 << 20
+        try:
+            for off, length in ranges:
+                off, length = int(off), int(length)
+                pos = off
+                while length < 0 or pos < off + length:
+                    want = frame if length < 0 else min(frame, off + length - pos)
+                    rep = _request(peer[0], peer[1], {"op": "get", "token": self.server.token,
+                                                      "path": str(req.get("src", "")),
+                                                      "offset": pos, "length": want},
+                                   timeout=120)
+                    if not rep.get("ok"):
+                        return {"ok": False, "error": f"pull from {peer[0]}:{peer[1]}: "
+                                                      f"{rep.get('error')}"}
+                    data = base64.b64decode(rep["data"])
+                    if data:
+                        os.pwrite(fd, data, pos)
+                    pos += len(data)
+                    got += len(data)
+                    if rep.get("eof") or not data:
+                        break
+            if req.get("size") is not None:
+                os.ftruncate(fd, int(req["size"]))
+        finally:
+            os.close(fd)
+        return {"ok": True, "bytes": got}
 
     def _writes_outside_root(self, argv: list[str]) -> str | None:
         """The CLI's file-writing flags may only target the daemon root."""

@@ -26,10 +26,11 @@ modes here:
        python -m locust_amd.parallel.launch --hosts hosts.txt --wordcount data/hamlet.txt \\
            [--reducers R]
 
-   Line ranges go to the hosts as stage-1 commands (combined, indexed binary spills); the
-   spills go to the reducer hosts, and R key-range reducers (``--reducer r/R``, default one
-   per host) each merge their slice of every spill -- summing counts, never expanding
-   them -- and write it with its global val; the launcher prints the slices in order.
+   Byte ranges (cut at line starts by the CLI) go to the hosts as stage-1 commands
+   (combined, indexed binary spills); R key-range reducers (``--reducer r/R``, default
+   one per host) pull their key range of every spill straight from the mapper daemons,
+   merge it -- summing counts, never expanding them -- and write it with its global val;
+   the launcher, which only ever holds the spills' indexes, prints the slices in order.
 """
 from __future__ import annotations
 
@@ -262,51 +263,54 @@ def _fetch(host: Host, path: str, dest: str, token: str | None) -> None:
                 break
 
 
-def _put(host: Host, path: str, src: str, token: str | None) -> None:
-    """Copy local file `src` to `path` under the daemon's root (32 MiB frames)."""
-    with open(src, "rb") as f:
-        first = True
-        while True:
-            data = f.read(32 << 20)
-            if not first and not data:
-                break
-            req = {"op": "put", "path": path, "data": base64.b64encode(data).decode(),
-                   "append": not first}
-            if token:
-                req["token"] = token
-            rep = request(host.addr, host.port, req, timeout=120)
-            if not rep.get("ok"):
-                raise RuntimeError(f"put {path} to {host}: {rep.get('error')}")
-            first = False
-            if not data:
-                break
+def _req(host: Host, obj: dict, token: str | None, timeout: float = 120) -> dict:
+    if token:
+        obj = dict(obj, token=token)
+    return request(host.addr, host.port, obj, timeout=timeout)
 
 
-def _spill_done(host: Host, k: int, s: int, e: int, path: str, token: str | None) -> bool:
-    """Host k's stage-1 output of lines [s, e) of `path` is complete: its map record names
-    the same input and range, and the spill's index is present (the reducer checks the
-    index against the spill's size)."""
+def _get_small(host: Host, name: str, token: str | None, limit: int = 1 << 20) -> bytes | None:
+    """A small file of a daemon's root (a map record, an index), or None."""
+    try:
+        rep = _req(host, {"op": "get", "path": name, "offset": 0, "length": limit}, token, 60)
+    except (OSError, ProtocolError):
+        return None
+    return base64.b64decode(rep["data"]) if rep.get("ok") else None
+
+
+def _spill_done(host: Host, k: int, argv: list[str], path: str, token: str | None) -> bool:
+    """Host k's stage-1 output from an earlier run can stand in for this one:
+    the launcher's record of that run names the same command line (input, byte range,
+    backend, tokenizer flags), the map record's input identity (size, mtime, inode) equals
+    the input file's on that host now, and the spill is present at the size its index
+    describes."""
     import json
 
-    def get(name):
-        req = {"op": "get", "path": name, "offset": 0, "length": 1 << 20}
-        if token:
-            req["token"] = token
-        try:
-            rep = request(host.addr, host.port, req, timeout=60)
-        except (OSError, ProtocolError):
-            return None
-        return base64.b64decode(rep["data"]) if rep.get("ok") else None
+    from .spillindex import parse_index
 
-    rec, idx = get(f"out.{k}.map.json"), get(f"out.{k}.kv.idx")
-    if rec is None or idx is None:
+    job, rec, idx = (_get_small(host, n, token) for n in
+                     (f"out.{k}.launch.json", f"out.{k}.map.json", f"out.{k}.kv.idx"))
+    if job is None or rec is None or idx is None:
         return False
     try:
-        m = json.loads(rec)
-    except ValueError:
+        j, m, x = json.loads(job), json.loads(rec), parse_index(idx)
+        st = _req(host, {"op": "stat", "path": path}, token, 60)
+        sp = _req(host, {"op": "get", "path": f"out.{k}.kv", "offset": 0, "length": 0}, token, 60)
+    except (ValueError, OSError, ProtocolError):
         return False
-    return (m.get("mode") == "map_stage" and m.get("input") == path and
-            m.get("line_start") == s and m.get("line_end") == e)
+    if not (st.get("ok") and sp.get("ok")):
+        return False
+    return (j.get("argv") == argv and m.get("mode") == "map_stage" and m.get("input") == path
+            and m.get("input_size") == st["size"] and m.get("input_mtime_ns") == st["mtime_ns"]
+            and m.get("input_inode") == st["inode"] and sp.get("size") == x.spill_bytes
+            and m.get("spill_bytes") == x.spill_bytes)
+
+
+def _put_bytes(host: Host, path: str, data: bytes, token: str | None) -> None:
+    rep = _req(host, {"op": "put", "path": path, "data": base64.b64encode(data).decode(),
+                      "append": False}, token)
+    if not rep.get("ok"):
+        raise RuntimeError(f"put {path} to {host}: {rep.get('error')}")
 
 
 def count_lines(path: str) -> int:
@@ -329,73 +333,103 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
                           backend: str = "gpu", workdir: str | None = None,
                           remote_root: str | None = None, extra: list[str] | None = None,
                           reducers: int | None = None, out=None, resume: bool = False,
-                          mapped: list | None = None) -> int:
-    """The reference's distributed WordCount (README.md:18-29): map on every host (line
-    ranges), then R key-range reducers on the hosts (default R = number of hosts).
+                          mapped: list | None = None, traffic: dict | None = None) -> int:
+    """The reference's distributed WordCount (README.md:18-29): map on every host, then R
+    key-range reducers on the hosts (default R = number of hosts).
 
-    1. Host k runs stage 1 on lines [k*L/H, (k+1)*L/H): its combined (key, count) spill
-       out.k.kv and index out.k.kv.idx land in its daemon root.
-    2. The spills and indexes are fetched here once and copied to every reducer host's
-       root (``spills/``).
-    3. Reducer r (on host r mod H) runs stage 2 with ``--reducer r/R``: it computes the
-       same splitters as every other reducer from the indexes, reads its key range of each
-       spill (an index seek) and writes its result lines, with their global val, to
-       ``result.r.txt``.
+    1. Host k runs stage 1 on bytes [k*S/H, (k+1)*S/H) of the S-byte input, both ends moved
+       to line starts by the CLI (``--byte-range``): the launcher needs the file's size only,
+       and no mapper scans the file's prefix for its window (the reference passes line
+       numbers, main.cu:369-374).  Its combined (key, count) spill out.k.kv and index
+       out.k.kv.idx land in its daemon root.
+    2. Only the indexes come here (a few KiB each).  From them the launcher plans the same
+       splitters every reducer computes and, for reducer r and spill k, the byte slice the
+       reducer reads: the header, and from the last index sample below its key range to the
+       first record past it.
+    3. Reducer r (on host r mod H) has its daemon pull those slices straight from the
+       mapper daemons (``pull``: a sparse file at the spill's own offsets, plus the index),
+       or reads the spill in place when it mapped it itself; then it runs stage 2 with
+       ``--reducer r/R`` and writes its result lines, with their global val, to
+       ``result.r.txt``.  No spill byte passes through the launcher.
     4. The results are fetched and concatenated in reducer order -- the single-stage
        output byte for byte.  The first failing stage stops the job (its exit code).
 
-    resume: the map outputs are the job's checkpoint -- a host whose
-    spill and index from an earlier run of the same line range are still in its root
-    (the index is valid for the spill's size and names the range) is not mapped again.
-    `mapped` (optional) receives the hosts' indexes that ran stage 1."""
+    resume: the map outputs are the job's checkpoint -- a host whose spill
+    and index from an earlier run of the same command on the unchanged input are still in
+    its root is not mapped again (_spill_done).  `mapped` (optional) receives the hosts that
+    ran stage 1; `traffic` (optional) gets the bytes each reducer pulled per spill, the
+    bytes the launcher fetched, and the splitters."""
+    import json
     import tempfile
 
+    from .spillindex import parse_index, plan_splitters, reducer_range, reducer_slices
+
     out = out or sys.stdout.buffer
-    nlines = count_lines(path)
+    apath = os.path.abspath(path)
+    size = os.path.getsize(apath)
     parts = len(hosts)
     reducers = max(1, reducers or parts)
-    bounds = [(nlines * k // parts, nlines * (k + 1) // parts) for k in range(parts)]
     hello = []
     for h in hosts:
-        req = {"op": "hello"}
-        if token:
-            req["token"] = token
-        rep = request(h.addr, h.port, req)
+        rep = _req(h, {"op": "hello"}, token)
         if not rep.get("ok"):
             raise RuntimeError(f"{h}: {rep.get('error')}")
         hello.append(rep)
     roots = [remote_root or hello[k]["root"] for k in range(parts)]
-    runs = []
-    for k, (h, (s, e)) in enumerate(zip(hosts, bounds)):
-        if resume and _spill_done(h, k, s, e, os.path.abspath(path), token):
-            continue
-        argv = [cli, os.path.abspath(path), str(s), str(e), str(k), "1", "--spill-dir", roots[k],
+    runs, argvs, ran = [], {}, []
+    for k, h in enumerate(hosts):
+        a, b = size * k // parts, size * (k + 1) // parts
+        rng = f"{a}:{b}" if k < parts - 1 else f"{a}:"
+        argv = [cli, apath, "0", "0", str(k), "1", "--byte-range", rng, "--spill-dir", roots[k],
                 "--spill-format", "binary", "--backend", backend,
                 "--json", f"{roots[k]}/out.{k}.map.json"] + list(extra or [])
+        argvs[k] = argv
+        if resume and _spill_done(h, k, argv, apath, token):
+            continue
+        _put_bytes(h, f"out.{k}.launch.json", b"", token)  # (void until this map succeeds)
         runs.append(_RemoteRun(h, argv, {}, token))
-        if mapped is not None:
-            mapped.append(k)
+        ran.append(k)
+    if mapped is not None:
+        mapped.extend(ran)
     rc = _join_all(runs, "map stage") if runs else 0
     if rc:
         return rc
-    tmp = workdir or tempfile.mkdtemp(prefix="locust_spills_")
+    for k in ran:
+        _put_bytes(hosts[k], f"out.{k}.launch.json", json.dumps({"argv": argvs[k]}).encode(), token)
+    tmp = workdir or tempfile.mkdtemp(prefix="locust_results_")
     os.makedirs(tmp, exist_ok=True)
-    local = []
+    fetched = 0
+    idx = []
     for k, h in enumerate(hosts):
-        for suffix in ("", ".idx"):
-            _fetch(h, f"out.{k}.kv{suffix}", os.path.join(tmp, f"out.{k}.kv{suffix}"), token)
-        local.append(os.path.join(tmp, f"out.{k}.kv"))
-    placed: set[int] = set()
+        data = _get_small(hosts[k], f"out.{k}.kv.idx", token, 64 << 20)
+        if data is None:
+            raise RuntimeError(f"{h}: no spill index out.{k}.kv.idx")
+        fetched += len(data)
+        idx.append(parse_index(data))
+    spl = plan_splitters(idx, reducers)
+    pulled = [[0] * parts for _ in range(reducers)]
     runs = []
     for r in range(reducers):
         hk = r % parts
-        if hk not in placed:
-            for k in range(parts):
-                for suffix in ("", ".idx"):
-                    _put(hosts[hk], f"spills/out.{k}.kv{suffix}", local[k] + suffix, token)
-            placed.add(hk)
-        inputs = ",".join(f"{roots[hk]}/spills/out.{k}.kv" for k in range(parts))
-        argv = [cli, os.path.abspath(path), "0", "0", str(r), "2", "--inputs", inputs,
+        lo, hi = reducer_range(spl, r)
+        inputs = []
+        for k in range(parts):
+            if k == hk:  # its own map output: read in place
+                inputs.append(f"{roots[hk]}/out.{k}.kv")
+                continue
+            dest = f"spills/r{r}/out.{k}.kv"
+            for name, rngs, sz in ((dest, reducer_slices(idx[k], lo, hi), idx[k].spill_bytes),
+                                   (dest + ".idx", [(0, -1)], None)):
+                rep = _req(hosts[hk], {"op": "pull", "peer": [hosts[k].addr, hosts[k].port],
+                                       "src": f"out.{k}.kv" + name[len(dest):], "dest": name,
+                                       "size": sz, "ranges": [list(x) for x in rngs]},
+                           token, 600)
+                if not rep.get("ok"):
+                    raise RuntimeError(f"reducer {r} on {hosts[hk]}: {rep.get('error')}")
+                if sz is not None:
+                    pulled[r][k] += rep["bytes"]
+            inputs.append(f"{roots[hk]}/{dest}")
+        argv = [cli, apath, "0", "0", str(r), "2", "--inputs", ",".join(inputs),
                 "--reducer", f"{r}/{reducers}", "--result-file", f"{roots[hk]}/result.{r}.txt",
                 "--backend", backend] + list(extra or [])
         runs.append(_RemoteRun(hosts[hk], argv, {}, token))
@@ -406,10 +440,14 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
     for r in range(reducers):
         dest = os.path.join(tmp, f"result.{r}.txt")
         _fetch(hosts[r % parts], f"result.{r}.txt", dest, token)
+        fetched += os.path.getsize(dest)
         with open(dest, "rb") as f:
             out.write(f.read())
     out.write(b"\nDone\n")
     out.flush()
+    if traffic is not None:
+        traffic.update({"pulled": pulled, "launcher_fetched": fetched, "splitters": spl,
+                        "indexes": idx})
     return 0
 
 

@@ -296,3 +296,114 @@ def test_stage_split_map_failure_propagates(tmp_path, cli, capfd):
     assert rc == 2  # the CLI's error exit
     cap = capfd.readouterr()
     assert "map stage failed" in cap.err and "print key" not in cap.out
+
+
+def _range_bytes(spills, lo, hi):
+    from locust_amd.parallel.spillindex import range_record_bytes, read_binary_spill
+
+    return [range_record_bytes(read_binary_spill(open(p, "rb").read()), lo, hi) for p in spills]
+
+
+@pytest.mark.parametrize("reducers", [2, 3, 5])
+def test_reducers_pull_only_their_range_peer_to_peer(tmp_path, cli, capfd, reducers):
+    """no launcher hub.  The launcher fetches only the spills' indexes
+    and the result lines; each reducer pulls its key range of every other host's spill
+    straight from that host's daemon -- at most 1.2x the bytes of the records in its range
+    (plus headers); the output is the single-stage output."""
+    from locust_amd.parallel.spillindex import reducer_range
+
+    hosts_roots = [start_daemon(tmp_path) for _ in range(3)]
+    hosts = [h for h, _ in hosts_roots]
+    f = tmp_path / "g.txt"
+    subprocess.run([cli, "--gen", str(f), "--gen-lines", "60000", "--seed", "3"], check=True,
+                   capture_output=True, timeout=120)
+    traffic = {}
+    rc = launch.stage_split_wordcount(str(f), hosts, cli, token=TOKEN, backend="cpu",
+                                      workdir=str(tmp_path / "w"), reducers=reducers,
+                                      extra=["--output-format", "gpu"], traffic=traffic)
+    assert rc == 0
+    out = capfd.readouterr().out
+    single = subprocess.run([cli, str(f), "--backend", "cpu", "--output-format", "gpu"],
+                            capture_output=True, timeout=120).stdout.decode()
+    assert out[out.index("print key:"):out.rindex("\nDone")] == \
+        single[single.index("print key:"):single.rindex("\nDone")]
+    spills = [os.path.join(root, f"out.{k}.kv") for k, (_h, root) in enumerate(hosts_roots)]
+    spill_total = sum(os.path.getsize(p) for p in spills)
+    idx_total = sum(os.path.getsize(p + ".idx") for p in spills)
+    results = len(out.encode())
+    # the launcher held the indexes and the results, never a spill
+    assert traffic["launcher_fetched"] <= idx_total + results
+    assert traffic["launcher_fetched"] < spill_total
+    spl = traffic["splitters"]
+    for r in range(reducers):
+        lo, hi = reducer_range(spl, r)
+        want = _range_bytes(spills, lo, hi)
+        for k in range(3):
+            if k == r % 3:
+                assert traffic["pulled"][r][k] == 0  # its own spill: read in place
+                continue
+            assert traffic["pulled"][r][k] <= 1.2 * want[k] + 32 + 2 * 40 * 16, (r, k)
+        remote = sum(want[k] for k in range(3) if k != r % 3)
+        assert sum(traffic["pulled"][r]) <= 1.2 * remote + 3 * (32 + 40 * 32), r
+
+
+def test_python_splitters_match_native(tmp_path, cli):
+    from locust_amd.parallel.spillindex import BEYOND, parse_index, plan_splitters
+
+    f = tmp_path / "g.txt"
+    subprocess.run([cli, "--gen", str(f), "--gen-lines", "20000", "--seed", "9"], check=True,
+                   capture_output=True, timeout=120)
+    n = os.path.getsize(f)
+    spills = []
+    for k in range(4):
+        subprocess.run([cli, str(f), "0", "0", str(k), "1", "--byte-range",
+                        f"{n * k // 4}:{n * (k + 1) // 4}", "--spill-dir", str(tmp_path),
+                        "--spill-format", "binary", "--backend", "cpu"], check=True,
+                       capture_output=True, timeout=120)
+        spills.append(str(tmp_path / f"out.{k}.kv"))
+    idx = [parse_index(open(p + ".idx", "rb").read()) for p in spills]
+    for R in (1, 2, 3, 7, 64, 5000):
+        py = plan_splitters(idx, R)
+        nat = lc._C.reducer_splitters(spills, R)
+        import struct
+
+        def words(b):
+            b = b.ljust(32, b"\0")
+            return tuple(struct.unpack(">4Q", b))
+        assert [words(b) for b in nat] == py, R
+        assert R < 5000 or py[-1] == BEYOND  # more reducers than keys: empty tail ranges
+
+
+def test_stage_split_resume_checks_input_and_command(tmp_path, hamlet, cli, capfd):
+    """a resume reuses a map output only for the same command on the unchanged
+    input -- an input edited in place, or other tokenizer flags, map again."""
+    hosts = [start_daemon(tmp_path)[0] for _ in range(2)]
+    f = tmp_path / "h.txt"
+    f.write_bytes(hamlet)
+    kw = dict(token=TOKEN, backend="cpu", reducers=2)
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, mapped=mapped,
+                                        extra=["--output-format", "gpu"], **kw) == 0
+    assert mapped == [0, 1]
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, mapped=mapped, resume=True,
+                                        extra=["--output-format", "gpu"], **kw) == 0
+    assert mapped == []  # unchanged: nothing mapped again
+    capfd.readouterr()
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, mapped=mapped, resume=True,
+                                        extra=["--output-format", "gpu", "--emits-per-line", "5"],
+                                        **kw) == 0
+    assert mapped == [0, 1]  # other tokenizer flags
+    out5 = capfd.readouterr().out
+    ent, _n, _ = oracle.wordcount(hamlet, emits=5)
+    assert out5[out5.index("print key:"):out5.rindex("\nDone")].encode().rstrip(b"\n") == \
+        oracle.format_gpu(ent).rstrip(b"\n")
+    f.write_bytes(hamlet.replace(b"Hamlet", b"Omelet"))  # same size, edited in place
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, mapped=mapped, resume=True,
+                                        extra=["--output-format", "gpu", "--emits-per-line", "5"],
+                                        **kw) == 0
+    assert mapped == [0, 1]
+    out = capfd.readouterr().out
+    assert "Omelet" in out and "print key: Hamlet " not in out

@@ -55,7 +55,9 @@ def test_every_switch_has_a_case():
             if f.endswith((".cpp", ".hpp", ".hip")):
                 used |= set(re.findall(r'getenv\("(LOCUST_[A-Z0-9_]+)"',
                                        open(os.path.join(d, f), errors="replace").read()))
-    covered = {k for env, _ in CASES for k in env} | {"LOCUST_FAULT"}  # test_dist*.py
+    covered = {k for env, _ in CASES for k in env} | {
+        "LOCUST_FAULT",        # test_dist*.py, test_scale_ready.py
+        "LOCUST_LINE_CACHE"}   # test_line_index.py
     assert used and not sorted(used - covered)
 
 

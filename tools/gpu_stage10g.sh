@@ -1,36 +1,63 @@
-# The reference's stage split at 10 GiB (VERDICT r4 next #1): a --gen-made file mapped as
-# N line windows (N stage-1 processes, each reading only its window: combined, indexed
-# spills), then one stage 2 over all spills and R key-range reducers; the result lines must
-# equal the single-stage run's.  Prints every process's peak RSS, wall time and spill size.
-# Usage: bash tools/gpu_stage10g.sh TAG [GIB] [WINDOWS] [REDUCERS]
+# The reference's stage split at 10 GiB (VERDICT r5 next #1): a --gen-made file mapped as
+# N windows (N stage-1 processes: combined, indexed spills), then one stage 2 over all
+# spills and R key-range reducers; the result lines must equal the single-stage run's.
+# MODE bytes (default): the launcher's way -- byte ranges size*k/N, moved to line starts by
+# the CLI (--byte-range), no prefix scan.  MODE lines: the reference's line windows, found
+# through the cached sparse line index (the line count pass builds it).
+# Prints every process's peak RSS, wall time, spill size and the map job's split:
+# window (finding its bytes) / setup (engine construction) / run (read + map + combine).
+# Usage: bash tools/gpu_stage10g.sh TAG [GIB] [WINDOWS] [REDUCERS] [MODE]
 set -e
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-stage10g}
 G=${2:-10}
 N=${3:-8}
 R=${4:-3}
+MODE=${5:-bytes}
 mkdir -p $O
 D=/tmp/locust_stage_$$
 F=$D/big.txt
 mkdir -p $D
+export LOCUST_CACHE_DIR=$D/cache
 trap 'rm -rf $D' EXIT
 timeout -k 10 300 ./build/MapReduce --gen $F --gen-bytes $((G<<30)) --seed 7 > $O/gen.txt
-L=$(python3 -c "import locust_amd as l; print(l._C.find_line_window('$F', 0, -1)[2])")
-echo "$G GiB, $L lines, $N windows, $R reducers" | tee $O/summary.txt
+S=$(stat -c %s $F)
+if [ "$MODE" = lines ]; then
+  t0=$(date +%s.%N)
+  L=$(python3 -c "import locust_amd as l; print(l._C.find_line_window('$F', 0, -1)[2])")
+  t1=$(date +%s.%N)
+  echo "$G GiB, $L lines (counted in $(python3 -c "print('%.2f' % ($t1-$t0))") s), $N line windows, $R reducers" | tee $O/summary.txt
+else
+  echo "$G GiB ($S bytes), $N byte windows, $R reducers" | tee $O/summary.txt
+fi
 t0=$(date +%s.%N)
 timeout -k 10 300 ./build/MapReduce $F --json $O/single.json > $D/single.out
 t1=$(date +%s.%N)
 grep "^print key:" $D/single.out > $D/single.lines
-python3 -c "import json,sys; d=json.load(open('$O/single.json')); print('single stage: %.2f s process, peak RSS %d kB, unique %d' % ($t1-$t0, d['max_rss_kb'], d['unique']))" | tee -a $O/summary.txt
+python3 -c "import json,sys; d=json.load(open('$O/single.json')); s=d['startup']; print('single stage: %.2f s process, job %.1f ms (engine %.1f, read %.1f, first job %.1f), peak RSS %d kB, unique %d' % ($t1-$t0, s['engine_ms']+s['read_ms']+s['first_job_ms'], s['engine_ms'], s['read_ms'], s['first_job_ms'], d['max_rss_kb'], d['unique']))" | tee -a $O/summary.txt
 INPUTS=""
 for k in $(seq 0 $((N-1))); do
-  s=$((L*k/N)); e=$((L*(k+1)/N))
+  if [ "$MODE" = lines ]; then
+    s=$((L*k/N)); e=$((L*(k+1)/N)); W="$s $e"; RANGE=""
+  else
+    a=$((S*k/N)); b=$((S*(k+1)/N)); W="0 0"; RANGE="--byte-range $a:$b"
+  fi
   t0=$(date +%s.%N)
-  timeout -k 10 300 ./build/MapReduce $F $s $e $k 1 --spill-dir $D --spill-format binary --json $O/map$k.json > $O/map$k.out
+  timeout -k 10 300 ./build/MapReduce $F $W $k 1 $RANGE --spill-dir $D --spill-format binary --json $O/map$k.json > $O/map$k.out
   t1=$(date +%s.%N)
-  python3 -c "import json; d=json.load(open('$O/map$k.json')); print('map %d [%d, %d): %.2f s process, job %.1f ms, streamed %s, spill %d B (%d records), peak RSS %d kB' % ($k, $s, $e, $t1-$t0, d['job_ms'], d['streamed'], d['spill_bytes'], d['spill_records'], d['peak_rss_kb']))" | tee -a $O/summary.txt
+  python3 -c "import json; d=json.load(open('$O/map$k.json')); print('map %d bytes [%d, %d): %.2f s process, job %.1f ms (window %.1f, setup %.1f, run %.1f), map %.1f ms, streamed %s, spill %d B (%d records), peak RSS %d kB' % ($k, d['byte_begin'], d['byte_end'], $t1-$t0, d['job_ms'], d['window_ms'], d['setup_ms'], d['run_ms'], d['map_ms'], d['streamed'], d['spill_bytes'], d['spill_records'], d['peak_rss_kb']))" | tee -a $O/summary.txt
   INPUTS="$INPUTS${INPUTS:+,}$D/out.$k.kv"
 done
+python3 - $O $N <<'PY' | tee -a $O/summary.txt
+import json, statistics, sys
+o, n = sys.argv[1], int(sys.argv[2])
+jobs = [json.load(open(f"{o}/map{k}.json"))["job_ms"] for k in range(n)]
+st = json.load(open(f"{o}/single.json"))["startup"]
+single = st["engine_ms"] + st["read_ms"] + st["first_job_ms"]  # the same parts as a map's job_ms
+med = statistics.median(jobs)
+print("maps: median %.1f ms, spread %.2f..%.2f of median, sum %.1f ms; single-stage job %.1f ms, sum/single %.2f"
+      % (med, min(jobs) / med, max(jobs) / med, sum(jobs), single, sum(jobs) / single))
+PY
 t0=$(date +%s.%N)
 timeout -k 10 300 ./build/MapReduce $F 0 0 0 2 --inputs $INPUTS --json $O/reduce.json > $D/reduce.out
 t1=$(date +%s.%N)
