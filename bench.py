@@ -380,6 +380,11 @@ def scale_diag(dr, args, local_rank: int, nccl_dir: str | None, infos=None) -> d
         "peak_rss_kb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss,
         "rss_now_kb": _rss_breakdown(),
         "pinned_bytes": infos[-1].get("pinned_bytes", 0) if infos else 0,
+        # the HBM plan's outcome: this rank's engine device memory, its GPU's free / total
+        # memory when the engine was built (plan_device_pass, csrc/include/locust/engine.hpp)
+        "hbm_device_bytes": infos[-1].get("hbm_device_bytes", 0) if infos else 0,
+        "hbm_free_bytes": infos[-1].get("hbm_free_bytes", 0) if infos else 0,
+        "hbm_total_bytes": infos[-1].get("hbm_total_bytes", 0) if infos else 0,
         "comm": dr.comm_name,
         "transport": nccl_transports(nccl_dir, dr.rank) if args.comm == "rccl" else
                      {str(p): [args.comm] for p in range(dr.size) if p != dr.rank},
@@ -398,7 +403,8 @@ def scale_diag(dr, args, local_rank: int, nccl_dir: str | None, infos=None) -> d
         v = [r["stages_ms"][k] for r in ranks if r["stages_ms"][k] is not None]
         summary[k] = [min(v), max(v)] if v else None
     return {"stages_ms_min_max": summary, "ranks": ranks,
-            "nccl_debug_dir": nccl_dir, "peak_rss_kb_max": max(r["peak_rss_kb"] for r in ranks)}
+            "nccl_debug_dir": nccl_dir, "peak_rss_kb_max": max(r["peak_rss_kb"] for r in ranks),
+            "hbm_device_bytes_max": max(r["hbm_device_bytes"] for r in ranks)}
 
 
 def synth_point(args, rank: int, world: int, dr=None) -> dict:

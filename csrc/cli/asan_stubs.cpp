@@ -18,6 +18,7 @@ GpuWordCount::~GpuWordCount() = default;
 WordCountResult GpuWordCount::run(const TextInput&) { no_gpu(); }
 WordCountResult GpuWordCount::run_source(TextSource&) { no_gpu(); }
 char* GpuWordCount::input_buffer() { no_gpu(); }
+GpuWordCount::Stats GpuWordCount::stats() const { no_gpu(); }
 bool GpuWordCount::partition_map(std::vector<u64>*) { no_gpu(); }
 bool GpuWordCount::set_partition_map(const std::vector<u64>&) { no_gpu(); }
 std::vector<PackedKey> GpuWordCount::run_map_stage(const TextInput&, WordCountResult*) { no_gpu(); }

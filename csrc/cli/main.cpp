@@ -334,6 +334,19 @@ struct Startup {
 Startup g_startup;
 const char* g_part_map = nullptr;  // "cache" / "default": run_direct's starting map
 
+// The GPU engine's HBM plan (plan_device_pass): its device memory, the GPU's free and
+// total memory before it, and whether the input streams (chunk size, map window).
+GpuWordCount::Stats g_engine_stats;
+bool g_engine_stats_set = false;
+void json_hbm(JsonOut& j, const GpuWordCount::Stats& s) {
+  j.u("hbm_device_bytes", s.device_bytes);
+  j.u("hbm_free_bytes", s.hbm_free);
+  j.u("hbm_total_bytes", s.hbm_total);
+  j.kv("device_streaming", s.streaming ? "true" : "false");
+  j.u("device_chunk_bytes", s.chunk_bytes);
+  j.u("device_map_window", s.map_window);
+}
+
 void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<double>& walls) {
   if (a.json.empty()) return;
   std::vector<double> w = walls;
@@ -353,6 +366,7 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
   j.kv("iters", std::to_string(w.size()));
   j.u("chunks", r.chunks);
   if (g_part_map) j.str("part_map", g_part_map);  // the one-shot CLI's starting map
+  if (g_engine_stats_set) json_hbm(j, g_engine_stats);
   // peak resident memory of this process image (VmHWM: unlike getrusage's ru_maxrss it is
   // not inherited through the fork + exec that started us)
   j.u("max_rss_kb", peak_rss_kb());
@@ -387,6 +401,13 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
     u64 pinned = ranks.empty() ? 0 : ranks[0].shared_pinned_bytes;
     for (const DistResult& d : ranks) pinned += d.pinned_bytes;
     j.u("pinned_bytes", pinned);
+    u64 hbm = 0;
+    for (const DistResult& d : ranks) hbm += d.hbm_device_bytes;
+    j.u("hbm_device_bytes", hbm);  // every rank's engines (one GPU or several)
+    if (!ranks.empty()) j.u("hbm_total_bytes", ranks[0].hbm_total_bytes);
+    u64 used = 0;
+    for (const DistResult& d : ranks) used = std::max(used, d.hbm_used_bytes);
+    j.u("hbm_used_bytes_max", used);
   }
   std::string rk = "[";
   for (size_t r = 0; r < ranks.size(); ++r) {
@@ -412,6 +433,10 @@ void write_json_dist(const CliArgs& a, const DistResult& root, const std::vector
     x.kv("input_streamed", d.input_streamed ? "true" : "false");
     x.kv("peer_p2p", std::to_string(d.peer_p2p));
     x.u("pinned_bytes", d.pinned_bytes);
+    x.u("hbm_device_bytes", d.hbm_device_bytes);
+    x.u("hbm_free_bytes", d.hbm_free_bytes);
+    x.u("hbm_total_bytes", d.hbm_total_bytes);
+    x.u("hbm_used_bytes", d.hbm_used_bytes);
     rk += (r ? ", " : "") + x.done();
   }
   j.kv("ranks", rk + "]");
@@ -544,6 +569,8 @@ int run_direct(const CliArgs& a) {
   if (size > chunk) {
     cfg.chunk_bytes = chunk;
     eng.reset(new GpuWordCount(cfg, size, size));
+    g_engine_stats = eng->stats();
+    g_engine_stats_set = true;
     start_map();
     st.engine = st.read = now_ns();  // the file is read by the job, piece by piece
     log_rss("with the streaming engine");
@@ -555,6 +582,8 @@ int run_direct(const CliArgs& a) {
     }
   } else {
     eng.reset(new GpuWordCount(cfg, std::max<u64>(size, 1), std::max<u64>(size, 1)));
+    g_engine_stats = eng->stats();
+    g_engine_stats_set = true;
     start_map();
     st.engine = now_ns();
     TextInput in;
@@ -668,6 +697,7 @@ int run_map_stage(const CliArgs& a) {
     j.num("setup_ms", m.setup_ms);
     j.num("run_ms", m.run_ms);
     j.num("spill_write_ms", m.spill_write_ms);
+    if (!cpu && !a.cfg.ref_compat) json_hbm(j, m.engine);
     j.u("peak_rss_kb", peak_rss_kb());
     emit_json(a, j.done());
   }

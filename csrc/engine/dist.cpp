@@ -131,8 +131,24 @@ static bool dist_local_enabled() {
   return on;
 }
 
+namespace {
+DistResult run_distributed_job(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
+                               const TextInput& shard);
+}  // namespace
+
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
                            const TextInput& shard) {
+  DistResult res = run_distributed_job(cfg, comm, eng, shard);
+  res.hbm_device_bytes = eng.device_bytes();  // the HBM plan's outcome, per rank
+  res.hbm_free_bytes = eng.hbm_free();
+  res.hbm_total_bytes = eng.hbm_total();
+  res.hbm_used_bytes = eng.hbm_used_now();
+  return res;
+}
+
+namespace {
+DistResult run_distributed_job(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,
+                               const TextInput& shard) {
   const int P = comm.size();
   const int me = comm.rank();
   log_rank() = me;
@@ -819,5 +835,6 @@ DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngin
   r.times.wall_ms = res.total_ms;
   return res;
 }
+}  // namespace
 
 }  // namespace locust

@@ -197,6 +197,13 @@ std::vector<DistResult> run_ranks(const std::vector<DistConfig>& schedule,
         // Ranks are threads of one process here: no stream capture while other ranks may
         // allocate or copy (hipGraph replay is for one-process-per-GPU runs).
         if (P > 1) job.graph = 0;
+        // the ranks on this rank's GPU share its HBM: each plans against its share
+        if (gpu) {
+          int share = 0;
+          for (int q = 0; q < P; ++q)
+            share += (rccl ? cfg.job.device + q : (cfg.job.device + q) % ndev) == job.device;
+          job.hbm_share = std::max(share, 1);
+        }
         std::unique_ptr<ShardEngine> eng =
             gpu ? make_gpu_shard_engine(job, std::max<u64>(in.bytes, 1), std::max<u64>(in.lines, 1))
                 : make_cpu_shard_engine(job);

@@ -25,8 +25,7 @@ u64 GpuWordCount::text_capacity() const { return impl_->cap_bytes; }
 
 WordCountResult GpuWordCount::run(const TextInput& in) { return impl_->run(in); }
 WordCountResult GpuWordCount::run_source(TextSource& src) {
-  LOCUST_CHECK_ARG(impl_->cfg.chunk_bytes && impl_->cap_bytes <= impl_->cfg.chunk_bytes,
-                   "run_source needs a streaming engine (chunk_bytes set)");
+  LOCUST_CHECK_ARG(impl_->streaming, "run_source needs a streaming engine (chunk_bytes set)");
   return impl_->run_source(src);
 }
 GpuWordCount::Stats GpuWordCount::stats() const {
@@ -35,6 +34,12 @@ GpuWordCount::Stats GpuWordCount::stats() const {
   s.fallbacks = impl_->fallbacks;
   s.planned_passes = impl_->planned_passes;
   s.devplan_failed = impl_->devplan_failed;
+  s.device_bytes = impl_->device_bytes();
+  s.hbm_free = impl_->hbm_free;
+  s.hbm_total = impl_->hbm_total;
+  s.streaming = impl_->streaming;
+  s.chunk_bytes = impl_->cap_bytes;
+  s.map_window = impl_->map_window;
   return s;
 }
 
@@ -171,6 +176,7 @@ WordCountResult GpuWordCount::reduce_sorted(const PackedKey* sorted, u64 n) {
   Impl& m = *impl_;
   m.sync_clean = false;  // this entry point dirties d_sync
   WordCountResult r;
+  m.ensure_radix_full();
   m.set_num_records(n);
   m.upload_keys(m.sorted, sorted, n);
   m.enqueue_reduce_core(false);

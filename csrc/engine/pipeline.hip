@@ -92,30 +92,199 @@ void DevicePipeline::warm_modules_once(int device) {
   warmed |= bit;
 }
 
+// The arena's layout for a planned pass: the same sequence of buffers the constructor
+// takes, so plan_device_pass prices an engine exactly before it exists.
+DevicePipeline::ArenaShape DevicePipeline::shape_arena(const JobConfig& cfg, const DevicePassPlan& p,
+                                                       u64 small_pass_bytes) {
+  ArenaShape sh;
+  const bool compat = cfg.map_path == MapPath::kCompat;
+  const u64 cap_bytes = p.chunk_bytes, pass_bytes = p.pass_bytes, cap_lines = p.cap_lines;
+  const u64 cap = p.cap, ucap = p.ucap, rcap = p.rcap;
+  const bool streaming = p.streaming;
+  // the reference algorithm's head buffers (boundary mark, prefix, adjacent difference):
+  // a dictionary engine whose sort buffers hold its distinct keys only never reduces
+  // that way until ensure_radix_full makes them
+  const u64 hcap = rcap < cap ? 1 : rcap;
+  sh.slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
+  sh.t_line = div_up(pass_bytes, kLineIdxTile) + 1;
+  sh.t_compact = div_up(cap_lines, 256) + 1;
+  sh.t_map = div_up(pass_bytes, kMapTileBytesMin) + 1;
+  sh.t_heads = div_up(cap, kReduceTile) + 1;
+  sh.t_scan = div_up(cap, kReduceTile) + 1;
+  sh.rx_zero_words = radix_zero_bytes(rcap) / 4;
+  // Hash table: >= 2x the distinct keys it can see (load factor <= 0.5), capped at
+  // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
+  sh.dict_slots = 1024;
+  while (sh.dict_slots < 2 * ucap) sh.dict_slots <<= 1;
+  // [table | ucount | uval | rank]
+  sh.dict_zero_bytes = align_up(sh.dict_slots * sizeof(DictSlot), 256) +
+                       2 * align_up(ucap * 8, 256) + ucap * 4;
+  sh.rx_part_words = (u64)radix_hist_blocks(rcap) * kNumPositions * 256;
+  sh.sync_bytes = 256 + 8 * (sh.t_line + sh.t_compact + sh.t_map + sh.t_heads + sh.t_scan +
+                             kDictParts + 1);
+
+  SizingPlan sz;
+  sz.add<char>(cap_bytes + 64);
+  sz.add<u64>(compat ? cap_lines + 1 : 1);  // the line index: compat map only
+  sz.add<char>(64);
+  for (int j = 0; j < kKeyWords; ++j) {
+    sz.add<u64>(sh.slot_cap);
+    sz.add<u64>(cap);   // tokens
+    sz.add<u64>(rcap);  // sorted
+    sz.add<u64>(hcap);  // heads
+  }
+  sz.add<u32>(compat ? cap_lines : 1);
+  sz.add<u64>(cap);   // d_counts (per token)
+  sz.add<u64>(rcap);  // d_sorted_counts
+  for (int k = 0; k < 3; ++k) sz.add<u64>(hcap);  // d_prefix, d_head_val, d_head_count
+  sz.add<u32>(rcap);
+  sz.add<u8>(align_up(cap, 16) + 16);
+  // A pass of at most small_pass_bytes (1 KiB tiles <= kPartBlock: the in-job plan's
+  // range) takes the one-kernel ordered build whatever its worst-case token count: natural
+  // text has a third of the tokens the capacity allows, and the large build's device plan
+  // cost ~0.2 ms of a 0.3 ms untuned job at 3-5x Hamlet (docs/PERFORMANCE.md round 5).
+  sh.small_pass = cap > kPartBuildMaxTokens && cap_bytes <= small_pass_bytes && !streaming &&
+                  cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict;
+  if ((cap <= kPartBuildMaxTokens || sh.small_pass) && cap_bytes < kMapLargeInput) {
+    sh.part_off_tiles = div_up(cap_bytes, kMapTileBytesMin);
+  } else if (!streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
+    // large single passes (the two-kernel ordered build): 1 KiB tiles below
+    // kMapLargeInput, 4 KiB tiles (whole inputs or upload pieces) above
+    sh.part_off_tiles =
+        std::max<u64>(div_up(std::min<u64>(cap_bytes, kMapLargeInput), kMapTileBytesMin),
+                      div_up(cap_bytes, kMapTileBytesLarge) + kMaxPieces);
+    sh.large_ordered = cap > kPartBuildMaxTokens;
+  }
+  if (sh.part_off_tiles) sz.add<u32>(sh.part_off_tiles * kPartTable);
+  if (sh.part_off_tiles) sz.add<u32>(sh.part_off_tiles * kPartOccWords);
+  sh.partial_slots_cap = sh.large_ordered
+                             ? (u32)std::clamp<u64>(div_up(cap_bytes, kPieceBytes) + 3,
+                                                    kOrdWorkers, kMaxPartialSlots)
+                             : 0u;
+  const u64 partial_slots = (u64)kDictParts * sh.partial_slots_cap;
+  if (partial_slots) {
+    sz.add<KeyCount>(partial_slots * kPartSlotsHost);
+    sz.add<u32>(partial_slots);
+  }
+  sz.add<OutRecord>(rcap);
+  sz.add<KeyCount>(std::max<u64>(cap, kSlotRecordsMin) + kSlotHeaderRecords);  // d_records
+  sz.add<PackedKey>(kMaxSamples);
+  sz.add<PackedKey>(kMaxRanks);
+  sz.add<u64>(kMaxRanks + 1);
+  sz.add<u64>(1);
+  sz.add<char>(sh.sync_bytes);
+  sz.add<u32>(sh.rx_zero_words);
+  sz.add<u32>(sh.rx_part_words);
+  sz.add<SortPlan>(1);
+  for (int b = 0; b < 2; ++b) {
+    sz.add<u64>(rcap);
+    sz.add<u32>(rcap);
+  }
+  for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
+  sz.add<char>(sh.dict_zero_bytes);
+  sh.arena_bytes = align_up(sz.bytes + 4096, kDevPageBytes);
+  return sh;
+}
+
+// The every-token sort / reduce buffers a dictionary engine leaves out of its arena
+// (rcap == ucap): sorted and head keys, sorted counts, prefix, head val / count, the
+// permutation, the output records and the radix scratch, at cap.
+static u64 radix_full_bytes(u64 cap) {
+  SizingPlan sz;
+  for (int j = 0; j < kKeyWords; ++j) {
+    sz.add<u64>(cap);
+    sz.add<u64>(cap);
+  }
+  for (int k = 0; k < 4; ++k) sz.add<u64>(cap);
+  sz.add<u32>(cap);
+  sz.add<OutRecord>(cap);
+  sz.add<u32>(radix_zero_bytes(cap) / 4);
+  sz.add<u32>((u64)radix_hist_blocks(cap) * kNumPositions * 256);
+  for (int b = 0; b < 2; ++b) {
+    sz.add<u64>(cap);
+    sz.add<u32>(cap);
+  }
+  return align_up(sz.bytes + 4096, DevicePipeline::kDevPageBytes);
+}
+
+void DevicePipeline::ensure_radix_full() {
+  if (rcap >= cap) return;
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  LOCUST_HIP_CHECK(hipStreamIsCapturing(stream, &cst));
+  LOCUST_CHECK_ARG(cst == hipStreamCaptureStatusNone,
+                   "internal: the every-token sort buffers must exist before a capture");
+  const u64 bytes = radix_full_bytes(cap);
+  LOCUST_LOG_INFO("dictionary engine enters the every-token sort: +%.1f MiB of device memory",
+                  bytes / 1048576.0);
+  sync();  // nothing in flight may still use the buffers being replaced
+  for (auto& g : dict_graphs) LOCUST_HIP_CHECK(hipGraphExecDestroy(g.exec));
+  dict_graphs.clear();
+  for (auto& g : graph_cache) LOCUST_HIP_CHECK(hipGraphExecDestroy(g.exec));
+  graph_cache.clear();
+  size_t got = 0;
+  radix_base = static_cast<char*>(dev_block_alloc(bytes, &got));
+  radix_block = got;
+  Arena a;
+  a.base = radix_base;
+  a.size = bytes;
+  for (int j = 0; j < kKeyWords; ++j) {
+    sorted.w[j] = a.take<u64>(cap);
+    heads.w[j] = a.take<u64>(cap);
+  }
+  d_sorted_counts = a.take<u64>(cap);
+  d_prefix = a.take<u64>(cap);
+  d_head_val = a.take<u64>(cap);
+  d_head_count = a.take<u64>(cap);
+  d_perm = a.take<u32>(cap);
+  d_out = a.take<OutRecord>(cap);
+  const u64 zw = radix_zero_bytes(cap) / 4;
+  rx.cap = cap;
+  rx.tile_counters = a.take<u32>(zw);
+  rx.status = rx.tile_counters + kNumPositions;
+  rx.hist_part = a.take<u32>((u64)radix_hist_blocks(cap) * kNumPositions * 256);
+  for (int b = 0; b < 2; ++b) {
+    rx.keys[b] = a.take<u64>(cap);
+    rx.vals[b] = a.take<u32>(cap);
+  }
+  LOCUST_HIP_CHECK(hipMemsetAsync(rx.tile_counters, 0, zw * 4, stream));
+  rcap = cap;
+  ++layout_gen;
+}
+
+u64 DevicePipeline::device_bytes() const {
+  u64 b = arena.size + (radix_base ? radix_full_bytes(cap) : 0);
+  if (d_text_alt) b += cap_bytes + 64;
+  if (d_plan) b += plan_zero_bytes;  // (+ the plan's key arrays: small)
+  return b;
+}
+
 DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines, u64 cap_records)
     : cfg(c) {
   LOCUST_CHECK_ARG(cfg.emits_per_line > 0, "emits_per_line must be > 0");
   LOCUST_CHECK_ARG(cfg.max_key_len > 0 && cfg.max_key_len <= kKeyBytes - 1,
                    "max_key_len must be in [1, 31]");
-  cap_bytes = std::max<u64>(max_bytes, 1);
-  cap_lines = std::max<u64>(max_lines, 1);
-  bool streaming = false;
-  if (cfg.chunk_bytes && cap_bytes > cfg.chunk_bytes && !cap_records) {
-    // streaming engine: one pass holds a chunk; its token capacity is bounded by bytes
-    cap_bytes = cfg.chunk_bytes;
-    cap_lines = cap_bytes;
-    streaming = true;
-  }
-  cap = cap_records ? cap_records
-                    : std::min<u64>(cap_lines * (u64)cfg.emits_per_line, cap_bytes / 2 + 1);
-  // The dictionary of a streamed input collects the distinct keys of ALL chunks, and
-  // its sort/emit buffers are record-sized: give small chunks room for 2^20 of them.
-  if (streaming) cap = std::max<u64>(cap, 1ull << 20);
-  cap = std::max<u64>(cap, 1);
-  LOCUST_CHECK_ARG(cap < (1ull << 30), "more than 2^30 records per GPU call");
   // construction phases, logged at LOCUST_LOG=debug (the cold CLI breakdown's engine_ms)
   u64 tc[6] = {now_ns(), 0, 0, 0, 0, 0};
   LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
+  {  // the device pass, planned against the HBM this engine may use (engine.hpp)
+    size_t fr = 0, tot = 0;
+    LOCUST_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+    hbm_free = fr;
+    hbm_total = tot;
+    const DevicePassPlan plan = plan_device_pass(cfg, max_bytes, max_lines, cap_records, fr);
+    cap_bytes = plan.chunk_bytes;
+    cap_lines = plan.cap_lines;
+    cap = plan.cap;
+    ucap = plan.ucap;
+    rcap = plan.rcap;
+    map_window = plan.map_window;
+    pass_bytes = plan.pass_bytes;
+    streaming = plan.streaming;
+    if (plan.streaming && !(cfg.chunk_bytes && max_bytes > cfg.chunk_bytes))
+      LOCUST_LOG_INFO("device pass: %llu B input planned as a stream of %llu B chunks (%s)",
+                      (unsigned long long)max_bytes, (unsigned long long)cap_bytes,
+                      plan.why.c_str());
+  }
   warm_modules_once(cfg.device);
   tc[1] = now_ns();
   LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -123,81 +292,30 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   tc[2] = now_ns();
 
   const bool compat = cfg.map_path == MapPath::kCompat;
-  const u64 slot_cap = compat ? cap_lines * (u64)cfg.emits_per_line : 1;
-  const u64 t_line = div_up(cap_bytes, kLineIdxTile) + 1;
-  const u64 t_compact = div_up(cap_lines, 256) + 1;
-  const u64 t_map = div_up(cap_bytes, kMapTileBytesMin) + 1;
-  const u64 t_heads = div_up(cap, kReduceTile) + 1;
-  const u64 t_scan = div_up(cap, kReduceTile) + 1;
-  const u64 rx_zero_words = radix_zero_bytes(cap) / 4;
-  // Hash table: >= 2x the distinct keys it can see (load factor <= 0.5), capped at
-  // 2^25 slots (16M distinct keys per call; beyond that the radix path takes over).
-  dict_slots = 1024;
-  // dense distinct-key capacity: every key of a pass, at most 16M (a 2^25-slot table)
-  ucap = std::min<u64>(cap, 1ull << 24);
-  while (dict_slots < 2 * ucap) dict_slots <<= 1;
-  // [table | ucount | uval | rank]
-  dict_zero_bytes = align_up(dict_slots * sizeof(DictSlot), 256) + 2 * align_up(ucap * 8, 256) +
-                    ucap * 4;
-  const u64 rx_part_words = (u64)radix_hist_blocks(cap) * kNumPositions * 256;
-  sync_bytes = 256 + 8 * (t_line + t_compact + t_map + t_heads + t_scan + kDictParts + 1);
-
-  SizingPlan sz;
-  sz.add<char>(cap_bytes + 64);
-  sz.add<u64>(compat ? cap_lines + 1 : 1);  // the line index: compat map only
-  sz.add<char>(64);
-  for (int j = 0; j < kKeyWords; ++j) {
-    sz.add<u64>(slot_cap);
-    sz.add<u64>(cap);
-    sz.add<u64>(cap);
-    sz.add<u64>(cap);
-  }
-  sz.add<u32>(compat ? cap_lines : 1);
-  for (int k = 0; k < 5; ++k) sz.add<u64>(cap);
-  sz.add<u32>(cap);
-  sz.add<u8>(align_up(cap, 16) + 16);
-  // A pass of at most small_pass_bytes (1 KiB tiles <= kPartBlock: the in-job plan's
-  // range) takes the one-kernel ordered build whatever its worst-case token count: natural
-  // text has a third of the tokens the capacity allows, and the large build's device plan
-  // cost ~0.2 ms of a 0.3 ms untuned job at 3-5x Hamlet (docs/PERFORMANCE.md round 5).
-  small_pass = cap > kPartBuildMaxTokens && cap_bytes <= small_pass_bytes && !streaming &&
-               cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict;
-  if ((cap <= kPartBuildMaxTokens || small_pass) && cap_bytes < kMapLargeInput) {
-    part_off_tiles = div_up(cap_bytes, kMapTileBytesMin);
-  } else if (!streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
-    // large single passes (the two-kernel ordered build): 1 KiB tiles below
-    // kMapLargeInput, 4 KiB tiles (whole inputs or upload pieces) above
-    part_off_tiles = std::max<u64>(div_up(std::min<u64>(cap_bytes, kMapLargeInput), kMapTileBytesMin),
-                                   div_up(cap_bytes, kMapTileBytesLarge) + kMaxPieces);
-    large_ordered = cap > kPartBuildMaxTokens;
-  }
-  if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartTable);
-  if (part_off_tiles) sz.add<u32>(part_off_tiles * kPartOccWords);
-  partial_slots_cap = large_ordered ? (u32)std::clamp<u64>(div_up(cap_bytes, kPieceBytes) + 3,
-                                                           kOrdWorkers, kMaxPartialSlots)
-                                    : 0u;
+  const u64 hcap = rcap < cap ? 1 : rcap;  // (shape_arena)
+  DevicePassPlan plan;
+  plan.streaming = streaming;
+  plan.chunk_bytes = cap_bytes;
+  plan.pass_bytes = pass_bytes;
+  plan.map_window = map_window;
+  plan.cap_lines = cap_lines;
+  plan.cap = cap;
+  plan.ucap = ucap;
+  plan.rcap = rcap;
+  const ArenaShape sh = shape_arena(cfg, plan, small_pass_bytes);
+  const u64 slot_cap = sh.slot_cap;
+  const u64 t_line = sh.t_line, t_compact = sh.t_compact, t_map = sh.t_map;
+  const u64 t_heads = sh.t_heads, t_scan = sh.t_scan;
+  const u64 rx_zero_words = sh.rx_zero_words, rx_part_words = sh.rx_part_words;
+  dict_slots = sh.dict_slots;
+  dict_zero_bytes = sh.dict_zero_bytes;
+  sync_bytes = sh.sync_bytes;
+  small_pass = sh.small_pass;
+  part_off_tiles = sh.part_off_tiles;
+  large_ordered = sh.large_ordered;
+  partial_slots_cap = sh.partial_slots_cap;
   const u64 partial_slots = (u64)kDictParts * partial_slots_cap;
-  if (partial_slots) {
-    sz.add<KeyCount>(partial_slots * kPartSlotsHost);
-    sz.add<u32>(partial_slots);
-  }
-  sz.add<OutRecord>(cap);
-  sz.add<KeyCount>(slot_records_cap() + kSlotHeaderRecords);
-  sz.add<PackedKey>(kMaxSamples);
-  sz.add<PackedKey>(kMaxRanks);
-  sz.add<u64>(kMaxRanks + 1);
-  sz.add<u64>(1);
-  sz.add<char>(sync_bytes);
-  sz.add<u32>(rx_zero_words);
-  sz.add<u32>(rx_part_words);
-  sz.add<SortPlan>(1);
-  for (int b = 0; b < 2; ++b) {
-    sz.add<u64>(cap);
-    sz.add<u32>(cap);
-  }
-  for (int j = 0; j < kKeyWords; ++j) sz.add<u64>(ucap);
-  sz.add<char>(dict_zero_bytes);
-  arena.size = align_up(sz.bytes + 4096, kDevPageBytes);
+  arena.size = sh.arena_bytes;
   {
     size_t got = 0;  // the process-wide block cache (locust/devcache.hpp)
     arena.base = static_cast<char*>(dev_block_alloc(arena.size, &got));
@@ -210,16 +328,16 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   for (int j = 0; j < kKeyWords; ++j) {
     slots.w[j] = arena.take<u64>(slot_cap);
     tokens.w[j] = arena.take<u64>(cap);
-    sorted.w[j] = arena.take<u64>(cap);
-    heads.w[j] = arena.take<u64>(cap);
+    sorted.w[j] = arena.take<u64>(rcap);
+    heads.w[j] = arena.take<u64>(hcap);
   }
   d_line_counts = arena.take<u32>(compat ? cap_lines : 1);
   d_counts = arena.take<u64>(cap);
-  d_sorted_counts = arena.take<u64>(cap);
-  d_prefix = arena.take<u64>(cap);
-  d_head_val = arena.take<u64>(cap);
-  d_head_count = arena.take<u64>(cap);
-  d_perm = arena.take<u32>(cap);
+  d_sorted_counts = arena.take<u64>(rcap);
+  d_prefix = arena.take<u64>(hcap);
+  d_head_val = arena.take<u64>(hcap);
+  d_head_count = arena.take<u64>(hcap);
+  d_perm = arena.take<u32>(rcap);
   d_parts = arena.take<u8>(align_up(cap, 16) + 16);
   if (part_off_tiles) d_part_off = arena.take<u32>(part_off_tiles * kPartTable);
   if (part_off_tiles) d_part_occ = arena.take<u32>(part_off_tiles * kPartOccWords);
@@ -227,7 +345,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
     d_partials = arena.take<KeyCount>(partial_slots * kPartSlotsHost);
     d_partial_n = arena.take<u32>(partial_slots);
   }
-  d_out = arena.take<OutRecord>(cap);
+  d_out = arena.take<OutRecord>(rcap);
   // room for a gather slot header in front: d_records - kSlotHeaderRecords is the slot
   d_records = arena.take<KeyCount>(slot_records_cap() + kSlotHeaderRecords) + kSlotHeaderRecords;
   d_samples = arena.take<PackedKey>(kMaxSamples);
@@ -256,14 +374,14 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   d_fuse = counters + 8;
   d_plan_flag = counters + 7;  // OrderedExtra::plan_flag
 
-  rx.cap = cap;
+  rx.cap = rcap;
   rx.tile_counters = arena.take<u32>(rx_zero_words);
   rx.status = rx.tile_counters + kNumPositions;
   rx.hist_part = arena.take<u32>(rx_part_words);
   rx.plan = arena.take<SortPlan>(1);
   for (int b = 0; b < 2; ++b) {
-    rx.keys[b] = arena.take<u64>(cap);
-    rx.vals[b] = arena.take<u32>(cap);
+    rx.keys[b] = arena.take<u64>(rcap);
+    rx.vals[b] = arena.take<u32>(rcap);
   }
   for (int j = 0; j < kKeyWords; ++j) dict.ukeys.w[j] = arena.take<u64>(ucap);
   {
@@ -355,11 +473,14 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
     LOCUST_HIP_CHECK(hipStreamSynchronize(stream));
   }
   tc[5] = now_ns();
-  LOCUST_LOG_DEBUG("engine (%llu B text, %llu records): modules %.2f ms, stream %.2f ms, device "
-                   "arena %.2f ms (%.1f MiB), pinned host buffers %.2f ms, copy streams %.2f ms",
-                   (unsigned long long)cap_bytes, (unsigned long long)cap, (tc[1] - tc[0]) * 1e-6,
-                   (tc[2] - tc[1]) * 1e-6, (tc[3] - tc[2]) * 1e-6, arena.size / 1048576.0,
-                   (tc[4] - tc[3]) * 1e-6, (tc[5] - tc[4]) * 1e-6);
+  LOCUST_LOG_DEBUG("engine (%llu B text, %llu tokens, %llu records%s): modules %.2f ms, stream "
+                   "%.2f ms, device arena %.2f ms (%.1f MiB of %.1f GiB free), pinned host "
+                   "buffers %.2f ms, copy streams %.2f ms",
+                   (unsigned long long)cap_bytes, (unsigned long long)cap,
+                   (unsigned long long)rcap, streaming ? ", streaming" : "",
+                   (tc[1] - tc[0]) * 1e-6, (tc[2] - tc[1]) * 1e-6, (tc[3] - tc[2]) * 1e-6,
+                   arena.size / 1048576.0, hbm_free / 1073741824.0, (tc[4] - tc[3]) * 1e-6,
+                   (tc[5] - tc[4]) * 1e-6);
 }
 
 void DevicePipeline::warm_copy_streams() {
@@ -401,6 +522,7 @@ DevicePipeline::~DevicePipeline() {
   if (cstream2) (void)hipStreamDestroy(cstream2);
 
   if (d_text_alt) dev_block_free(d_text_alt, d_text_alt_block);
+  if (radix_base) dev_block_free(radix_base, radix_block);
   if (d_dctr) (void)hipFree(d_dctr);
   if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
   if (stream) (void)hipStreamDestroy(stream);
@@ -718,6 +840,7 @@ void DevicePipeline::enqueue_map(const TextInput& in, bool launch) {
 
 void DevicePipeline::enqueue_process(u32 num_lines, bool compat, bool with_counts, u64 host_n,
                        bool allow_psort) {
+  ensure_radix_full();  // every token is sorted: a dictionary engine grows its buffers
   if (allow_psort && psort_ok(compat, with_counts)) {
     // one kernel, one workgroup per key range of the map's partition table (psort.hip)
     launch_psort(tokens, d_part_off, part_tiles, cap, sorted, d_ctr, d_pw, stream, ord_trace());
@@ -742,6 +865,7 @@ void DevicePipeline::enqueue_process(u32 num_lines, bool compat, bool with_count
 
 void DevicePipeline::enqueue_radix_job(u32 num_lines, bool compat, hipEvent_t after_process,
                          hipEvent_t after_reduce) {
+  ensure_radix_full();
   radix_fused = cfg.reduce_path == ReducePath::kLds &&
                 radix_mapped() && psort_ok(compat, false);
   if (radix_fused) {
@@ -754,7 +878,7 @@ void DevicePipeline::enqueue_radix_job(u32 num_lines, bool compat, hipEvent_t af
     ra.status = lb_dict.status;
     ra.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
     ra.map_lb = lb_map;
-    ra.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+    ra.map_words = (u32)(div_up(pass_bytes, kMapTileBytesMin) + 1);
     if (done_pending) {
       ra.host_done = d_done;
       ra.host_done_value = done_pending;
@@ -795,6 +919,7 @@ void DevicePipeline::redo_radix_general(u32 num_lines) {
 }
 
 void DevicePipeline::enqueue_reduce_core(bool with_counts) {
+  ensure_radix_full();
   const u64* prefix = nullptr;
   if (with_counts) {
     launch_scan_counts(d_sorted_counts, cap, d_prefix, d_ctr, lb_scan, stream);
@@ -1387,7 +1512,7 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
   // The previous job left d_sync zeroed (self-cleaning ordered run): no reset this time.
   const bool clean_start = sync_clean;
   sync_clean = false;
-  if (in.bytes > cap_bytes && cfg.sort_path == SortPath::kDict &&
+  if (in.bytes > pass_bytes && cfg.sort_path == SortPath::kDict &&
       cfg.map_path == MapPath::kFast)
     return run_stream(in);
   if (cfg.ref_timers) return run_ref_timed(in);
@@ -1565,9 +1690,11 @@ void DevicePipeline::ensure_stream_buffers(bool staging, u64 nchunks) {
   if (staging && !h_stage[0])
     for (int b = 0; b < 2; ++b)
       h_stage[b] = static_cast<char*>(pinned_alloc(cap_bytes + 64, hipHostMallocDefault, "chunk staging"));
+  // per-window counter snapshots (folded when full: at most 4096 pinned)
+  nchunks = std::min<u64>(std::max<u64>(nchunks, 64), 4096);
   if (nchunks > h_chunk_cap) {
     if (h_chunk_ctr) LOCUST_HIP_CHECK(hipHostFree(h_chunk_ctr));
-    h_chunk_cap = std::max<u64>(nchunks, 64);
+    h_chunk_cap = nchunks;
     LOCUST_HIP_CHECK(hipHostMalloc(&h_chunk_ctr, h_chunk_cap * sizeof(MapCounters),
                                    hipHostMallocDefault));
   }
@@ -1618,13 +1745,49 @@ size_t DevicePipeline::enqueue_stream_insert(const TextInput& in) {
   });
 }
 
+void DevicePipeline::snapshot_window_counters() {
+  if (win_pending == h_chunk_cap) {  // full: fold the snapshots so far (one host sync)
+    sync();
+    for (u64 k = 0; k < win_pending; ++k) {
+      const MapCounters& c = h_chunk_ctr[k];
+      win_acc.num_records += c.num_records;
+      win_acc.overflow_lines += c.overflow_lines;
+      win_acc.truncated += c.truncated;
+      win_acc.max_key_len = std::max(win_acc.max_key_len, c.max_key_len);
+    }
+    win_pending = 0;
+  }
+  LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[win_pending], d_ctr, sizeof(MapCounters),
+                                  hipMemcpyDeviceToHost, stream));
+  ++win_pending;
+}
+
+void DevicePipeline::enqueue_map_window(const char* dtext, u64 len, const DelimMask& dm) {
+  LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
+  launch_map_fast(dtext, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap,
+                  d_ctr, lb_map, stream);
+  snapshot_window_counters();
+  launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
+}
+
+u64 DevicePipeline::window_len(const char* p, u64 n) const {
+  if (n <= map_window) return n;
+  const void* nl = memrchr(p, '\n', (size_t)map_window);
+  if (nl) return (u64)(static_cast<const char*>(nl) - p) + 1;
+  // one line longer than a window: it alone (its tokens are capped at emits_per_line)
+  nl = std::memchr(p + map_window, '\n', (size_t)(n - map_window));
+  return nl ? (u64)(static_cast<const char*>(nl) - p) + 1 : n;
+}
+
 size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
   LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
                    "inputs larger than the engine capacity stream through the dictionary "
                    "path with the fast map (sort=dict, map=fast)");
-  const u64 max_chunks = div_up(std::max<u64>(src_text.size(), 1), cap_bytes / 2) + 2;
-  ensure_stream_buffers(false, max_chunks);
   const u64 piece = std::min<u64>(cap_bytes, cfg.ring_piece_bytes ? cfg.ring_piece_bytes : kRingPieceMax);
+  // a map window closes before a piece would overflow it: windows >= map_window - piece
+  const u64 min_window = map_window > piece ? map_window - piece : std::max<u64>(map_window / 2, 1);
+  ensure_stream_buffers(false, div_up(std::max<u64>(src_text.size(), 1), min_window) + 2);
+  reset_window_counters();
   if (ring_piece != piece) {
     for (int i = 0; i < kRingPieces; ++i) {
       if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
@@ -1639,25 +1802,25 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
   // the copy stream must not overwrite a text buffer before the reset is queued
   LOCUST_HIP_CHECK(hipEventRecord(ev_copied[1], stream));
   LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_copied[1], 0));
-  size_t k = 0;  // chunks closed
-  u64 fill = 0;  // bytes in chunk k
+  size_t k = 0;     // chunks closed
+  u64 fill = 0;     // bytes in chunk k
+  u64 mapped = 0;   // bytes of chunk k already mapped (the windows so far)
+  int last_slot = -1;  // the ring slot of the last piece copied into chunk k
   auto chunk_text = [&](size_t c) { return (c & 1) ? d_text_alt : d_text; };
+  // Map + insert chunk k's bytes [mapped, fill) as one window, once their copies landed.
+  auto map_pending = [&] {
+    if (fill == mapped) return;
+    LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_ring[last_slot], 0));
+    enqueue_map_window(chunk_text(k) + mapped, fill - mapped, dm);
+    mapped = fill;
+  };
   auto close_chunk = [&] {
     const int b = (int)(k & 1);
-    char* dtext = chunk_text(k);
-    LOCUST_CHECK_ARG(k < h_chunk_cap, "more stream chunks than planned");
-    LOCUST_HIP_CHECK(hipMemsetAsync(dtext + fill, 0, 16, cstream));
-    LOCUST_HIP_CHECK(hipEventRecord(ev_copied[b], cstream));
-    LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
-    LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
-    launch_map_fast(dtext, fill, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap,
-                    d_ctr, lb_map, stream);
+    map_pending();
+    // the chunk buffer is free for its refill two chunks on once its last map ran
     LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
-    LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
-                                    hipMemcpyDeviceToHost, stream));
-    launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
     ++k;
-    fill = 0;
+    fill = mapped = 0;
   };
   for (u64 r = 0;; ++r) {
     const int slot = (int)(r % kRingPieces);
@@ -1665,13 +1828,17 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
     if (r >= (u64)kRingPieces) LOCUST_HIP_CHECK(hipEventSynchronize(ev_ring[slot]));
     const u64 n = src_text.next(h_ring[slot], piece);
     if (!n) break;
-    if (fill + n > cap_bytes) close_chunk();
-    // a chunk buffer is refilled only after the map two chunks back consumed it
+    if (fill + n > cap_bytes)
+      close_chunk();
+    else if (fill - mapped + n > map_window)
+      map_pending();  // the window so far, before this piece would overflow it
+    // a chunk buffer is refilled only after the maps two chunks back consumed it
     if (fill == 0 && k >= 2)
       LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[k & 1], 0));
     LOCUST_HIP_CHECK(hipMemcpyAsync(chunk_text(k) + fill, h_ring[slot], n, hipMemcpyHostToDevice,
                                     cstream));
     LOCUST_HIP_CHECK(hipEventRecord(ev_ring[slot], cstream));
+    last_slot = slot;
     fill += n;
   }
   if (fill) close_chunk();
@@ -1684,8 +1851,11 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
 }
 
 void DevicePipeline::stream_stats(size_t nchunks, WordCountResult& r) const {
-  r.num_tokens = r.overflow_lines = r.truncated = r.max_key_len = 0;
-  for (size_t k = 0; k < nchunks; ++k) {
+  r.num_tokens = win_acc.num_records;
+  r.overflow_lines = win_acc.overflow_lines;
+  r.truncated = win_acc.truncated;
+  r.max_key_len = win_acc.max_key_len;
+  for (u64 k = 0; k < win_pending; ++k) {
     const MapCounters& c = h_chunk_ctr[k];
     r.num_tokens += c.num_records;
     r.overflow_lines += c.overflow_lines;
@@ -1734,4 +1904,78 @@ void DevicePipeline::upload_keys(const KeysSoA& dst, const PackedKey* keys, u64 
 }
 
 }  // namespace detail
+
+DevicePassPlan plan_device_pass(const JobConfig& cfg, u64 max_bytes, u64 max_lines,
+                                u64 cap_records, u64 free_bytes) {
+  using detail::DevicePipeline;
+  const u64 E = (u64)std::max(cfg.emits_per_line, 1);
+  const u64 share = (u64)std::max(cfg.hbm_share, 1);
+  const u64 budget = (u64)((long double)free_bytes * kHbmUsable) / share;
+  auto make = [&](bool stream, u64 chunk) {
+    DevicePassPlan p;
+    p.streaming = stream;
+    if (stream) {
+      p.chunk_bytes = std::max<u64>(chunk, 1);
+      p.map_window = std::min<u64>(p.chunk_bytes, kStreamMapWindow);
+      p.pass_bytes = p.map_window;
+      p.cap_lines = p.map_window;
+      // a window's tokens (a byte in two); the dictionary of a streamed input collects
+      // the distinct keys of ALL windows: room for 2^20 of them even in small windows
+      p.cap = std::max<u64>(p.map_window / 2 + 1, 1ull << 20);
+    } else {
+      p.chunk_bytes = std::max<u64>(max_bytes, 1);
+      p.pass_bytes = p.chunk_bytes;
+      p.map_window = p.chunk_bytes;  // (an input streamed through it anyway: chunk-sized maps)
+      p.cap_lines = std::max<u64>(max_lines, 1);
+      p.cap = cap_records ? cap_records : std::min<u64>(p.cap_lines * E, p.chunk_bytes / 2 + 1);
+    }
+    p.cap = std::max<u64>(p.cap, 1);
+    // dense distinct-key capacity: every key of a pass, at most 16M (a 2^25-slot table)
+    p.ucap = std::min<u64>(p.cap, 1ull << 24);
+    // a dictionary engine's sort / reduce buffers hold its distinct keys (every ordered and
+    // table path emits <= ucap of them); a receiver (cap_records) or a radix engine sorts
+    // every record
+    p.rcap = cfg.sort_path == SortPath::kDict && !cap_records ? p.ucap : p.cap;
+    p.device_bytes = DevicePipeline::shape_arena(cfg, p, DevicePipeline::small_pass_limit()).arena_bytes;
+    if (stream) p.device_bytes += p.chunk_bytes + 64;  // the second chunk buffer
+    p.budget_bytes = budget;
+    return p;
+  };
+  const bool streamable = !cap_records && cfg.sort_path == SortPath::kDict &&
+                          cfg.map_path == MapPath::kFast;
+  const bool asked = cfg.chunk_bytes && max_bytes > cfg.chunk_bytes && !cap_records;
+  DevicePassPlan p = make(asked, cfg.chunk_bytes);
+  if (!asked && streamable) {
+    std::string why;
+    if (p.cap >= (1ull << 30))
+      why = "more than 2^30 tokens in one pass";
+    else if (free_bytes && p.device_bytes > budget)
+      why = "one pass would need " + std::to_string(p.device_bytes >> 20) + " MiB of the " +
+            std::to_string(budget >> 20) + " MiB of HBM this engine may use";
+    if (!why.empty()) {
+      const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
+      if (max_bytes > chunk) {
+        p = make(true, chunk);
+        p.why = why;
+      }
+    }
+  }
+  LOCUST_CHECK_ARG(p.cap < (1ull << 30),
+                   "more than 2^30 records per GPU call (" + std::to_string(p.cap) +
+                       "); inputs this large stream on the dictionary path with the fast map");
+  if (free_bytes && p.device_bytes > budget) {
+    char msg[512];
+    std::snprintf(msg, sizeof(msg),
+                  "device pass of %llu B needs %.2f GiB of HBM but this engine may use %.2f GiB "
+                  "(%.2f GiB free x %.2f / %d engine(s) on the GPU)%s",
+                  (unsigned long long)p.chunk_bytes, p.device_bytes / 1073741824.0,
+                  budget / 1073741824.0, free_bytes / 1073741824.0, kHbmUsable,
+                  std::max(cfg.hbm_share, 1),
+                  p.streaming ? ": use a smaller --chunk-mb (LOCUST_CHUNK_MB)"
+                              : ": stream it with --chunk-mb (dictionary path, fast map)");
+    throw Error(msg);
+  }
+  return p;
+}
+
 }  // namespace locust

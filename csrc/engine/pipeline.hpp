@@ -70,6 +70,36 @@ constexpr u32 kMaxRanks = 1024;
 struct DevicePipeline {
   JobConfig cfg;
   u64 cap_bytes = 0, cap_lines = 0, cap = 0;
+  // ---- HBM plan (plan_device_pass, locust/engine.hpp) ----
+  // pass_bytes: the largest input one pass takes (== cap_bytes, except in a streaming
+  // engine, whose chunks of cap_bytes are mapped in windows of map_window bytes, so its
+  // token buffers hold one window's tokens, not one chunk's).  rcap: the records the
+  // sort / reduce buffers hold -- every token on the radix path, the distinct keys (ucap)
+  // on the dictionary path until a general radix pass needs every token
+  // (ensure_radix_full grows them on first use).
+  u64 pass_bytes = 0, map_window = 0, rcap = 0;
+  bool streaming = false;
+  u64 layout_gen = 0;  // bumped when buffers move: captured sequences are keyed by it
+  char* radix_base = nullptr;
+  size_t radix_block = 0;
+  u64 hbm_free = 0, hbm_total = 0;  // the device's memory before this engine's allocations
+  // The arena's layout for a planned pass (shape_arena: the constructor's sizing, also
+  // what plan_device_pass prices before an engine exists).
+  struct ArenaShape {
+    u64 slot_cap = 0, t_line = 0, t_compact = 0, t_map = 0, t_heads = 0, t_scan = 0;
+    u64 rx_zero_words = 0, rx_part_words = 0, dict_slots = 0, dict_zero_bytes = 0;
+    u64 sync_bytes = 0, part_off_tiles = 0, arena_bytes = 0;
+    u32 partial_slots_cap = 0;
+    bool small_pass = false, large_ordered = false;
+  };
+  static ArenaShape shape_arena(const JobConfig& cfg, const DevicePassPlan& p,
+                                u64 small_pass_bytes);
+  // Grows the sort / reduce buffers to every token (cap) -- a dictionary engine entering
+  // the reference algorithm (its table overflowed, an uncombined shuffle, a reducer); it
+  // drops the captured graphs, whose pointers change.  No-op when rcap == cap.
+  void ensure_radix_full();
+  // Device memory this engine holds (arena, radix growth, the second stream chunk, plan).
+  u64 device_bytes() const;
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   Arena arena;
@@ -100,10 +130,11 @@ struct DevicePipeline {
   // LOCUST_SMALL_PASS_KB (construction, default 1024; 0: off): an engine for at most this
   // many bytes keeps the one-kernel ordered build (and its in-job plan) even when its
   // worst-case token count passes kPartBuildMaxTokens
-  const u64 small_pass_bytes = [] {
+  static u64 small_pass_limit() {
     const char* e = std::getenv("LOCUST_SMALL_PASS_KB");
     return (u64)(e ? std::max(0, std::atoi(e)) : 1024) << 10;
-  }();
+  }
+  const u64 small_pass_bytes = small_pass_limit();
   bool small_pass = false;
   KeyCount* d_partials = nullptr;
   u32* d_partial_n = nullptr;
@@ -257,8 +288,23 @@ struct DevicePipeline {
   void issue_piece_copies(const char* src);
   hipEvent_t ev_copied[2] = {}, ev_consumed[2] = {};
   MapCounters* d_dctr = nullptr;     // dictionary counters that persist across chunks
-  MapCounters* h_chunk_ctr = nullptr;  // pinned per-chunk map counter snapshots
+  MapCounters* h_chunk_ctr = nullptr;  // pinned per-window map counter snapshots
   u64 h_chunk_cap = 0;
+  // Streamed maps (one per window): snapshots pending in h_chunk_ctr, and the sum of the
+  // ones folded when it filled up (stream_stats adds both).
+  u64 win_pending = 0;
+  MapCounters win_acc{};
+  void reset_window_counters() {
+    win_pending = 0;
+    win_acc = MapCounters{};
+  }
+  // Queues the snapshot of d_ctr after a window's map (folding the full array first).
+  void snapshot_window_counters();
+  // Map + dictionary insert of one window [dtext, dtext + len) of a streamed chunk.
+  void enqueue_map_window(const char* dtext, u64 len, const DelimMask& dm);
+  // Bytes of the next map window of host text [p, p + n): at most map_window bytes cut
+  // after a '\n', or one line longer than that (<= emits_per_line tokens).
+  u64 window_len(const char* p, u64 n) const;
 
   char* h_text = nullptr;
   char* d_h_text = nullptr;    // device view of the pinned h_text (zero-copy map input)
@@ -375,7 +421,7 @@ struct DevicePipeline {
   void grow_host_keys(u64 n);
 
   void check_input(const TextInput& in) const {
-    if (in.bytes > cap_bytes || in.num_lines > cap_lines)
+    if (in.bytes > pass_bytes || in.num_lines > cap_lines)
       throw Error("input (" + std::to_string(in.bytes) + " B, " + std::to_string(in.num_lines) +
                   " lines) exceeds engine capacity (" + std::to_string(cap_bytes) + " B, " +
                   std::to_string(cap_lines) + " lines)");
@@ -555,6 +601,7 @@ struct DevicePipeline {
   void enqueue_reduce_core(bool with_counts);
 
   void enqueue_pack_output() {
+    ensure_radix_full();
     launch_pack_output(heads, d_head_val, d_head_count, cap, d_ctr, d_out, stream);
   }
 
@@ -597,7 +644,7 @@ struct DevicePipeline {
   void set_self_clean(OrderedExtra& ex) const {
     ex.self_clean = true;
     ex.map_lb = lb_map;
-    ex.map_words = (u32)(div_up(cap_bytes, kMapTileBytesMin) + 1);
+    ex.map_words = (u32)(div_up(pass_bytes, kMapTileBytesMin) + 1);
     ex.done_counter = lb_dict.tile_counter + 1;  // the sync block's spare counter word
   }
   // Device view of this pipeline's partition map (tables live at fixed addresses, so
@@ -683,7 +730,7 @@ struct DevicePipeline {
   }
   // Radix-fallback reduce: scan of the sorted counts -> records in d_out.
   void enqueue_reduce_dict() {
-    launch_scan_pack(sorted, d_sorted_counts, cap, d_ctr, d_out, lb_scan, stream);
+    launch_scan_pack(sorted, d_sorted_counts, rcap, d_ctr, d_out, lb_scan, stream);
   }
   // After the counters are read: a dictionary run whose distinct-key count exceeded the
   // rank sort's range (or whose table overflowed) is finished on the radix path.
@@ -758,9 +805,10 @@ struct DevicePipeline {
     LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
                      "inputs larger than the engine capacity stream through the dictionary "
                      "path with the fast map (sort=dict, map=fast)");
-    LOCUST_CHECK_ARG(cap >= cap_bytes / 2 + 1,
+    LOCUST_CHECK_ARG(cap >= map_window / 2 + 1,
                      "a streaming engine must be sized by bytes (max_lines >= max_bytes / 40)");
-    ensure_stream_buffers(staging, max_chunks);
+    ensure_stream_buffers(staging, max_chunks * (div_up(cap_bytes, map_window) + 1));
+    reset_window_counters();
     const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
     LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
     LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));
@@ -776,20 +824,20 @@ struct DevicePipeline {
       const char* src = nullptr;
       const u64 len = produce(b, &src);
       if (!len) break;
-      LOCUST_CHECK_ARG(k < h_chunk_cap, "more stream chunks than planned");
       if (k >= 2) LOCUST_HIP_CHECK(hipStreamWaitEvent(cstream, ev_consumed[b], 0));
       LOCUST_HIP_CHECK(hipMemcpyAsync(dtext, src, len, hipMemcpyHostToDevice, cstream));
       LOCUST_HIP_CHECK(hipMemsetAsync(dtext + len, 0, 16, cstream));
       LOCUST_HIP_CHECK(hipEventRecord(ev_copied[b], cstream));
 
       LOCUST_HIP_CHECK(hipStreamWaitEvent(stream, ev_copied[b], 0));
-      LOCUST_HIP_CHECK(hipMemsetAsync(d_sync, 0, sync_bytes, stream));
-      launch_map_fast(dtext, len, dm, cfg.emits_per_line, cfg.max_key_len, tokens, nullptr, cap, d_ctr,
-                      lb_map, stream);
+      // the chunk in windows of <= map_window bytes (cut after a newline, found in the
+      // host copy): the token buffers hold one window
+      for (u64 off = 0; off < len;) {
+        const u64 wl = window_len(src + off, len - off);
+        enqueue_map_window(dtext + off, wl, dm);
+        off += wl;
+      }
       LOCUST_HIP_CHECK(hipEventRecord(ev_consumed[b], stream));
-      LOCUST_HIP_CHECK(hipMemcpyAsync(&h_chunk_ctr[k], d_ctr, sizeof(MapCounters),
-                                      hipMemcpyDeviceToHost, stream));
-      launch_dict_insert(tokens, nullptr, &d_ctr->num_records, cap, dict, d_dctr, stream);
     }
     // hand the dictionary's counters to the single-pass stages that follow
     LOCUST_HIP_CHECK(hipMemcpyAsync(&d_ctr->num_unique, &d_dctr->num_unique, sizeof(u32),

@@ -47,6 +47,19 @@ class GpuShardEngine final : public ShardEngine {
   }
   char* input_buffer() override { return mp_->ensure_h_text(); }
   u64 host_pinned_bytes() const override { return mp_->pinned_bytes(); }
+  u64 device_bytes() const override {
+    return mp_->device_bytes() + (rp_ ? rp_->device_bytes() : 0);
+  }
+  u64 hbm_free() const override { return mp_->hbm_free; }
+  u64 hbm_total() const override { return mp_->hbm_total; }
+  u64 hbm_used_now() const override {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return (u64)(tot - fr);
+  }
   u64 shared_pinned_bytes() const override {
     return out_ ? shm_segment_bytes(out_->region_records * out_->regions, sizeof(OutRecord)) : 0;
   }
@@ -58,7 +71,7 @@ class GpuShardEngine final : public ShardEngine {
     sorted_local_ = true;
     distinct_local_ = true;  // every path below yields distinct keys except combine=false
     stream_chunks_ = 0;
-    const bool streamed = shard.bytes > m.cap_bytes;
+    const bool streamed = shard.bytes > m.pass_bytes;
     LOCUST_CHECK_ARG(!shard.source || streamed,
                      "a shard read from a source must be larger than one device pass");
     const bool small_ordered = combine && cfg_.sort_path == SortPath::kDict && !streamed &&
@@ -205,7 +218,7 @@ class GpuShardEngine final : public ShardEngine {
   // samples late).
   bool small_ordered_ok(const TextInput& shard, bool combine) const {
     const DevicePipeline& m = *mp_;
-    return combine && cfg_.sort_path == SortPath::kDict && shard.bytes <= m.cap_bytes &&
+    return combine && cfg_.sort_path == SortPath::kDict && shard.bytes <= m.pass_bytes &&
            cfg_.map_path == MapPath::kFast && (m.cap <= kPartBuildMaxTokens || m.small_pass);
   }
   // Host half of a small ordered pass (run for every job): returns the graph key of the
@@ -453,7 +466,8 @@ class GpuShardEngine final : public ShardEngine {
     std::copy(map_half.first.begin(), map_half.first.end(), key.begin());
     std::copy(tail.first.begin(), tail.first.end(), key.begin() + 6);
     key[12] = reinterpret_cast<u64>(recv);
-    key[13] = (root ? 1 : 0) | (rp_gen_ << 1);
+    key[13] = (root ? 1 : 0) | (rp_gen_ << 1) | (m.layout_gen << 32) |
+              ((rp_ ? rp_->layout_gen : 0) << 48);
     for (auto& g : slot_graphs_)
       if (g.key == key) {
         LOCUST_HIP_CHECK(hipGraphLaunch(g.exec, m.stream));
@@ -527,7 +541,7 @@ class GpuShardEngine final : public ShardEngine {
   bool exch_map_async_ok(const TextInput& shard) const override {
     const DevicePipeline& m = *mp_;
     if (cfg_.sort_path != SortPath::kDict || cfg_.map_path != MapPath::kFast) return false;
-    if (shard.bytes > m.cap_bytes || shard.num_lines > m.cap_lines) return false;
+    if (shard.bytes > m.pass_bytes || shard.num_lines > m.cap_lines) return false;
     if (small_ordered_ok(shard, true)) return true;
     return m.large_ordered && m.cap > kPartBuildMaxTokens && m.table_tiles(shard.bytes) > 0;
   }

@@ -180,6 +180,7 @@ MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, const
       auto src = open_file_range_source(file, w.begin, w.end);
       r = eng.run_source(*src);
       tr = now_ns();
+      out.engine = eng.stats();
       out.lines = src->lines();
       out.streamed = true;
       recs = entries_to_records(r.entries);  // before the engine (and its buffers) goes
@@ -192,6 +193,7 @@ MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, const
       in.num_lines = out.lines;
       r = eng.run(in);
       tr = now_ns();
+      out.engine = eng.stats();
       recs = entries_to_records(r.entries);
     }
     if (lwin) out.lines = w.lines;

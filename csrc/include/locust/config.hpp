@@ -63,6 +63,9 @@ struct JobConfig {
   // done (includes the map kernel), Reduce = until the last reduce kernel is LAUNCHED.
   // Adds host synchronisations, so it is a separate measurement mode.
   bool ref_timers = false;
+  // Engines sharing one GPU's HBM (ranks of one process on one device): each plans its
+  // device pass against free memory / hbm_share (plan_device_pass, engine.hpp).
+  int hbm_share = 1;
 };
 constexpr u64 kZeroCopyMaxBytes = 1ull << 20;
 

@@ -177,6 +177,12 @@ class ShardEngine {
   // Page-locked host memory this rank's engine holds (0: a CPU engine); the shared output
   // block of ranks in one process is counted apart (shared_pinned_bytes, once per process).
   virtual u64 host_pinned_bytes() const { return 0; }
+  // HBM: the engine's device allocations, and its GPU's free / total memory before them
+  virtual u64 device_bytes() const { return 0; }
+  virtual u64 hbm_free() const { return 0; }
+  virtual u64 hbm_total() const { return 0; }
+  // device memory in use on its GPU now (every engine and process on it)
+  virtual u64 hbm_used_now() const { return 0; }
   virtual u64 shared_pinned_bytes() const { return 0; }
   // Map + sort (+ combine) this rank's shard.  Returns the number of local records.
   // `plan` is the strategy the driver expects to take: kGather lets an engine skip the
@@ -374,6 +380,10 @@ struct DistResult {
   bool rccl_clique = false;      // ... exchanged over an RCCL clique (else loopback copies)
   u64 pinned_bytes = 0;          // page-locked host memory of its engine (its GPU's share)
   u64 shared_pinned_bytes = 0;   // the shared output block the ranks of a process write
+  u64 hbm_device_bytes = 0;      // device memory of its engine (the HBM plan, engine.hpp)
+  u64 hbm_free_bytes = 0;        // its GPU's free memory when the engine was built
+  u64 hbm_total_bytes = 0;
+  u64 hbm_used_bytes = 0;        // its GPU's memory in use after the job (all engines on it)
 };
 
 DistResult run_distributed(const DistConfig& cfg, Communicator& comm, ShardEngine& eng,

@@ -277,6 +277,40 @@ std::unique_ptr<TextSource> open_file_source(const std::string& path, u32 thread
 std::unique_ptr<TextSource> open_file_range_source(const std::string& path, u64 begin, u64 end,
                                                    u32 threads = 0);
 
+// ---- HBM budget planning (SURVEY.md §5.7 "HBM budget accounting per GPU") ----
+// The reference sizes everything by compile-time constants (main.cu:18-20: 5,800 lines,
+// 116,000 emits; three cudaMallocs at :393,402,451).  Here an engine's device pass is
+// planned from its input size and the GPU's free memory before anything is allocated:
+//  * the token buffers hold one map launch's worst case (a byte in two a token); a
+//    streaming engine maps each chunk in windows of <= kStreamMapWindow bytes, so its
+//    token buffers do not grow with --chunk-mb;
+//  * the sort / reduce buffers of a dictionary engine hold the distinct keys only (ucap);
+//    the reference algorithm's every-token buffers are made on first use
+//    (DevicePipeline::ensure_radix_full);
+//  * a one-pass input whose engine would not fit its share of HBM (free / hbm_share, at
+//    most kHbmUsable of it), or that exceeds 2^30 tokens, is planned as a stream of
+//    chunk_bytes chunks (default kDefaultStreamChunk) on the dictionary path; a plan that
+//    still does not fit is refused with the sizes in the message.
+struct DevicePassPlan {
+  bool streaming = false;
+  u64 chunk_bytes = 0;   // device text buffer: the one pass, or one stream chunk
+  u64 pass_bytes = 0;    // largest input one pass takes (a streaming engine: map_window)
+  u64 map_window = 0;    // a streamed chunk's map windows (0: not streaming)
+  u64 cap_lines = 0;
+  u64 cap = 0;           // tokens one map launch may emit
+  u64 ucap = 0;          // distinct keys of the dictionary
+  u64 rcap = 0;          // records the sort / reduce buffers hold
+  u64 device_bytes = 0;  // the engine's planned device allocations
+  u64 budget_bytes = 0;  // the HBM it may use
+  std::string why;       // why the input was planned as a stream ("" if asked for)
+};
+constexpr u64 kStreamMapWindow = 32ull << 20;
+constexpr u64 kDefaultStreamChunk = 256ull << 20;
+constexpr double kHbmUsable = 0.9;
+// free_bytes: the device's free memory (hipMemGetInfo).  Throws when no plan fits.
+DevicePassPlan plan_device_pass(const JobConfig& cfg, u64 max_bytes, u64 max_lines,
+                                u64 cap_records, u64 free_bytes);
+
 class GpuWordCount {
  public:
   // Capacity is fixed at construction: max_text_bytes / max_lines per device pass.  With
@@ -299,6 +333,10 @@ class GpuWordCount {
   struct Stats {
     u32 retunes = 0, fallbacks = 0, planned_passes = 0;
     bool devplan_failed = false;
+    // HBM: this engine's device allocations, and the GPU's free / total memory before them
+    u64 device_bytes = 0, hbm_free = 0, hbm_total = 0;
+    bool streaming = false;
+    u64 chunk_bytes = 0, map_window = 0;
   };
   Stats stats() const;
 

@@ -64,6 +64,7 @@ struct MapStageResult {
   // run_ms (read / stream + map + combine) + the records' copy out of the engine
   double window_ms = 0, setup_ms = 0, run_ms = 0;
   SpillIndex index;
+  GpuWordCount::Stats engine;  // the GPU engine's HBM plan (device bytes, free HBM, chunks)
 };
 // Stage 1 over a window of `file` (none: the whole file): the job's combined output -- one
 // (key, count) record per distinct key, key order -- spilled to `spill` in `fmt`, with its

@@ -85,6 +85,12 @@ class PyGpuEngine {
     d["fallbacks"] = st.fallbacks;
     d["planned_passes"] = st.planned_passes;
     d["devplan_failed"] = st.devplan_failed;
+    d["device_bytes"] = st.device_bytes;
+    d["hbm_free"] = st.hbm_free;
+    d["hbm_total"] = st.hbm_total;
+    d["streaming"] = st.streaming;
+    d["chunk_bytes"] = st.chunk_bytes;
+    d["map_window"] = st.map_window;
     return d;
   }
   PyGpuEngine(const JobConfig& cfg, u64 max_bytes, u64 max_lines)
@@ -264,6 +270,10 @@ py::dict dist_to_dict(const DistResult& d) {
   x["rccl_clique"] = d.rccl_clique;
   x["pinned_bytes"] = d.pinned_bytes;
   x["shared_pinned_bytes"] = d.shared_pinned_bytes;
+  x["hbm_device_bytes"] = d.hbm_device_bytes;
+  x["hbm_free_bytes"] = d.hbm_free_bytes;
+  x["hbm_total_bytes"] = d.hbm_total_bytes;
+  x["hbm_used_bytes"] = d.hbm_used_bytes;
   x["sent_to"] = d.sent_to;
   x["recv_from"] = d.recv_from;
   return x;
@@ -452,7 +462,27 @@ PYBIND11_MODULE(_locust, m) {
       .def_readwrite("chunk_bytes", &JobConfig::chunk_bytes)
       .def_readwrite("zero_copy_text", &JobConfig::zero_copy_text)
       .def_readwrite("graph", &JobConfig::graph)
-      .def_readwrite("ref_timers", &JobConfig::ref_timers);
+      .def_readwrite("ref_timers", &JobConfig::ref_timers)
+      .def_readwrite("hbm_share", &JobConfig::hbm_share);
+  m.def("plan_device_pass", [](const JobConfig& cfg, u64 max_bytes, u64 max_lines, u64 cap_records,
+                               u64 free_bytes) {
+    const DevicePassPlan p = plan_device_pass(cfg, max_bytes, max_lines, cap_records, free_bytes);
+    py::dict d;
+    d["streaming"] = p.streaming;
+    d["chunk_bytes"] = p.chunk_bytes;
+    d["pass_bytes"] = p.pass_bytes;
+    d["map_window"] = p.map_window;
+    d["cap_lines"] = p.cap_lines;
+    d["cap"] = p.cap;
+    d["ucap"] = p.ucap;
+    d["rcap"] = p.rcap;
+    d["device_bytes"] = p.device_bytes;
+    d["budget_bytes"] = p.budget_bytes;
+    d["why"] = p.why;
+    return d;
+  }, py::arg("cfg"), py::arg("max_bytes"), py::arg("max_lines"), py::arg("cap_records") = 0,
+        py::arg("free_bytes") = 0,
+        "The HBM plan of an engine's device pass (no GPU needed): sizes and device bytes.");
 
   py::enum_<DistStrategy>(m, "DistStrategy")
       .value("auto", DistStrategy::kAuto)
