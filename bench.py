@@ -279,8 +279,10 @@ def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
 
     dr.set_strategy(getattr(lc._C.DistStrategy, strategy))
     res = None
+    stamp(f"{strategy}:warmup")
     for _ in range(warmup):  # holds each result like the timed loop (steady buffer pool)
         res, _info = dr.run_loaded()
+    stamp(f"{strategy}:timed")
     parts = {"map_ms": [], "shuffle_ms": [], "reduce_ms": [], "gather_ms": [],
              "sent_bytes": [], "recv_bytes": []}
     infos = []
@@ -302,6 +304,114 @@ def time_dist(dr, steps: int, warmup: int, strategy: str = "auto"):
 
 
 _LAST_INFOS: list = []
+
+
+# ---------------------------------------------------------------------------------------
+# progress stamps and the watchdog: a run that hangs still ends with
+# ONE JSON line, inside the budget, saying where every rank was
+# ---------------------------------------------------------------------------------------
+_PARTIAL: dict = {}  # what rank 0 has measured so far (scale_diag, ...) for a failure line
+DEFAULT_BUDGET_S = 480.0  # below the driver's timeout for one N of the scaling run
+
+
+def progress_dir() -> str:
+    """Where the ranks of this run stamp their progress: LOCUST_PROGRESS_DIR (set by the
+    self-spawning parent), else a directory named after the rendezvous (MASTER_PORT and
+    torchrun's run id), so every rank of one run -- and only of it -- shares it."""
+    d = os.environ.get("LOCUST_PROGRESS_DIR")
+    if not d:
+        tag = f"{os.environ.get('MASTER_PORT', 'local')}_{os.environ.get('TORCHELASTIC_RUN_ID', '')}"
+        d = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"locust_bench_progress_{tag}")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+_STAGE = ["start", 0.0]  # this rank's last Python stage and when it was entered
+
+
+def _native_stage():
+    try:
+        import locust_amd as lc
+
+        return list(lc._C.native_stage())
+    except Exception:  # noqa: BLE001 -- no extension yet (or built without it)
+        return None
+
+
+def stamp(stage: str | None = None) -> None:
+    """This rank's last stage and when it got there, the distributed job stage its native
+    code last entered, and a heartbeat time (atomic replace of rank<r>.json).  stage=None:
+    a heartbeat only (the watchdog thread, every second)."""
+    rank = int(os.environ.get("RANK", "0"))
+    if stage is not None:
+        _STAGE[:] = [stage, time.time()]
+    try:
+        d = progress_dir()
+        tmp = os.path.join(d, f".rank{rank}.{os.getpid()}")
+        with open(tmp, "w") as f:
+            json.dump({"rank": rank, "stage": _STAGE[0], "t": _STAGE[1], "beat": time.time(),
+                       "native": _native_stage() if "locust_amd" in sys.modules else None,
+                       "pid": os.getpid()}, f)
+        os.replace(tmp, os.path.join(d, f"rank{rank}.json"))
+    except OSError:
+        pass  # diagnostics only
+
+
+def read_progress(world: int, d: str | None = None) -> dict:
+    d = d or progress_dir()
+    now = time.time()
+    out = {}
+    for r in range(world):
+        try:
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                x = json.load(f)
+            out[str(r)] = {"stage": x["stage"], "age_s": round(now - x["t"], 1),
+                           # the native job stage it last entered and how many so far
+                           "native_stage": (x.get("native") or [None])[0],
+                           "native_stages": (x.get("native") or [None, None])[1],
+                           # seconds since its watchdog thread last wrote: a live process
+                           # (stuck) beats every second, a dead one stops
+                           "heartbeat_age_s": round(now - x.get("beat", x["t"]), 1)}
+        except (OSError, ValueError, KeyError):
+            out[str(r)] = {"stage": None, "age_s": None}
+    return out
+
+
+def failure_line(world: int, reason: str, d: str | None = None) -> str:
+    """The one JSON line of a failed run: no value, the reason, every rank's last stage
+    and whatever rank 0 had measured (its scale_diag, when it got that far)."""
+    line = {"metric": METRIC, "value": None, "unit": "ms", "n_gpus": world,
+            "higher_is_better": False, "status": "failed", "reason": reason,
+            "progress": read_progress(world, d)}
+    line.update({k: v for k, v in _PARTIAL.items() if k not in line})
+    return json.dumps(line)
+
+
+def start_watchdog(budget_s: float, rank: int, world: int) -> None:
+    """On expiry rank 0 prints the failure line and every rank exits 124 (rank 0 first: its
+    line must be out before the launcher tears the job down).  os._exit, never an exec."""
+    import threading
+
+    if budget_s <= 0:
+        return
+    deadline = time.time() + budget_s + (0 if rank == 0 else 20)
+
+    def run():
+        while time.time() < deadline:
+            time.sleep(1.0)
+            stamp()  # heartbeat (and the native stage the job is in)
+        if rank == 0:
+            try:
+                print(failure_line(world, f"watchdog: the {budget_s:.0f} s budget expired"),
+                      flush=True)
+            except Exception:  # noqa: BLE001 -- the exit below must happen regardless
+                pass
+        print(f"bench: rank {rank}: watchdog budget expired at stage "
+              f"{read_progress(world).get(str(rank), {}).get('stage')}", file=sys.stderr,
+              flush=True)
+        os._exit(124)
+
+    threading.Thread(target=run, daemon=True, name="bench-watchdog").start()
 
 
 # ---------------------------------------------------------------------------------------
@@ -456,14 +566,21 @@ def _allgather_float(dr, v: float, out: list) -> list:
 # ---------------------------------------------------------------------------------------
 # self-spawned ranks (--gpus N without a launcher)
 # ---------------------------------------------------------------------------------------
-def spawn_ranks(n: int, argv: list[str]) -> int:
+def spawn_ranks(n: int, argv: list[str], budget_s: float = DEFAULT_BUDGET_S) -> int:
     """Start N rank processes of this script and relay rank 0's JSON line.  The parent
     never touches the GPU (children, never an exec).  The first failing rank stops the
-    run: the others are killed and its exit code is returned."""
+    run: the others are killed, ONE failure line (status "failed", every rank's last
+    progress stamp, what rank 0 had measured) is printed and its exit code returned.  A
+    parent watchdog ends a run that outlives the ranks' own budget the same way."""
     import signal
     import socket
     import subprocess
+    import tempfile
     import threading
+
+    pdir = tempfile.mkdtemp(prefix="locust_bench_progress_")
+    deadline = time.time() + budget_s + 40 if budget_s > 0 else None
+    reason = ""
 
     boot = socket.socket()  # the bootstrap listener, inherited by rank 0 (no port race)
     boot.bind(("127.0.0.1", 0))
@@ -477,7 +594,8 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                        LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
-                       MASTER_PORT=str(master_port), LOCUST_PORT=str(boot.getsockname()[1]))
+                       MASTER_PORT=str(master_port), LOCUST_PORT=str(boot.getsockname()[1]),
+                       LOCUST_PROGRESS_DIR=pdir)
             env.pop("LOCUST_LISTEN_FD", None)
             fds: tuple = ()
             if r == 0:
@@ -499,8 +617,13 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
                 alive = True
             elif rc != 0 and not failed:
                 failed = rc if rc > 0 else 128 - rc
-                print(f"bench: rank {r} failed with exit code {rc}", file=sys.stderr)
+                reason = f"rank {r} failed with exit code {rc}"
+                print(f"bench: {reason}", file=sys.stderr)
         if failed or not alive:
+            break
+        if deadline and time.time() > deadline:
+            failed, reason = 124, f"parent watchdog: the ranks outlived {budget_s + 40:.0f} s"
+            print(f"bench: {reason}", file=sys.stderr)
             break
         time.sleep(0.05)
     for p in procs:
@@ -514,11 +637,15 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
                     continue
         p.wait()
     reader.join(timeout=10)
-    if failed:
-        return failed
     lines = [ln for ln in b"".join(out0).decode(errors="replace").splitlines() if ln.strip()]
+    if failed:
+        # rank 0's own failure line (its watchdog) if it printed one, else one made here
+        mine = [ln for ln in lines if '"status": "failed"' in ln]
+        print(mine[-1] if mine else failure_line(n, reason, pdir), flush=True)
+        return failed
     if not lines:
         print("bench: rank 0 printed no result line", file=sys.stderr)
+        print(failure_line(n, "rank 0 printed no result line", pdir), flush=True)
         return 1
     print(lines[-1], flush=True)
     return 0
@@ -552,15 +679,21 @@ def main() -> int:
                     help="lines of the synth1m strong-scaling extra (default 1M; tests)")
     ap.add_argument("--synth-bytes", type=int, default=0,
                     help="total bytes of --config synth10g (default 10 GB; tests)")
+    ap.add_argument("--budget-s", type=float,
+                    default=float(os.environ.get("LOCUST_BENCH_BUDGET_S", DEFAULT_BUDGET_S)),
+                    help="watchdog: a run still going after this many seconds ends with one "
+                         "failure line (status 'failed', every rank's last stage); 0: off")
     args = ap.parse_args()
     if args.backend == "cpu" and args.comm == "rccl" and args.gpus > 1:
         ap.error("--backend cpu needs --comm tcp")
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return spawn_ranks(args.gpus, sys.argv[1:])
+        return spawn_ranks(args.gpus, sys.argv[1:], args.budget_s)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    stamp("start")
+    start_watchdog(args.budget_s, rank, world)
     if args.backend == "gpu" and args.comm == "rccl":
         # this rank's process on its GPU's NUMA node before the first GPU call (the pinned
         # shard is first touched there; locust_amd/parallel/numa.py)
@@ -601,9 +734,12 @@ def main() -> int:
 
         res = lc._C.cpu_run(lc.make_config("cpu"), text)
     elif n == 1 and not args.force_dist:
+        stamp("single:headline")
         if synth and not args.no_extra:
             extra["cold_start"] = cold_first_run(text)  # before any warm engine exists
         ms, stages, res = bench_single(text, args.steps, args.warmup)
+        _PARTIAL["partial"] = {"ms_per_step": round(ms, 4)}
+        stamp("single:extras")
         if not args.no_extra and args.config == "hamlet4500":
             ms700, st700, _ = bench_single(load_text("hamlet700"), args.steps, args.warmup)
             extra["hamlet700"] = {"ms_per_step": round(ms700, 4), "vs_baseline":
@@ -631,15 +767,21 @@ def main() -> int:
             extra["synth1m"] = synth_point(args, rank, n)
     else:
         nccl_dir = nccl_debug_setup() if args.comm == "rccl" else None
+        stamp("connect")
         dr = dist_rank(text, n, rank, local_rank, args.comm, args.backend)
         rccl_ranks = dr.comm_count if dr.comm_name == "rccl" else None
+        stamp("headline")
         ms, stages, res, strategy = time_dist(dr, args.steps, args.warmup, args.strategy)
+        _PARTIAL["partial"] = {"ms_per_step": round(ms, 4), "strategy": strategy}
+        stamp("scale_diag")
         extra["scale_diag"] = scale_diag(dr, args, local_rank, nccl_dir)
+        _PARTIAL["scale_diag"] = extra["scale_diag"]
         if not args.no_extra and args.strategy == "auto" and strategy != "shuffle":
             # The sample-sort all-to-all shuffle on the same job (the path large inputs
             # take), so every scaling run also records the all-to-all path.
             ks, kw = (args.steps, args.warmup) if not synth else (min(args.steps, 10),
                                                                   min(args.warmup, 3))
+            stamp("extra:shuffle")
             try:  # a side measurement: its failure must not cost the headline line
                 mss, sts, _, _ = time_dist(dr, ks, kw, "shuffle")
                 extra["shuffle_path"] = {"ms_per_step": round(mss, 4),
@@ -648,7 +790,9 @@ def main() -> int:
                 print(f"rank {rank}: shuffle extra failed: {e}", file=sys.stderr)
                 extra["shuffle_path"] = {"error": str(e)[:300]}
         if not args.no_extra and not synth:
+            stamp("extra:synth1m")
             extra["synth1m"] = synth_point(args, rank, n, dr)
+    stamp("done")
     if rank != 0:
         return 0
     if synth:

@@ -643,6 +643,11 @@ int run_map_stage(const CliArgs& a) {
   const bool cpu = a.cfg.backend == Backend::kCpu;
   const char* dev = cpu ? "CPU" : "GPU";
   const std::string path = spill_path(a, a.node);
+  // the HIP runtime's own start-up (once per process, ~0.1-0.2 s), timed apart from the
+  // job like run_direct's: job_ms is this window's work, comparable across processes
+  const u64 t_init = now_ns();
+  if (!cpu) (void)visible_device_count();
+  const double runtime_init_ms = (now_ns() - t_init) * 1e-6;
   MapWindow win;
   if (a.byte_range) {
     win.by_bytes = true;
@@ -693,6 +698,7 @@ int run_map_stage(const CliArgs& a) {
     j.num("map_ms", r.times.h2d_ms + r.times.map_ms);
     j.num("process_ms", r.times.process_ms + r.times.reduce_ms);
     j.num("job_ms", m.job_ms);
+    j.num("runtime_init_ms", runtime_init_ms);
     j.num("window_ms", m.window_ms);
     j.num("setup_ms", m.setup_ms);
     j.num("run_ms", m.run_ms);

@@ -1,5 +1,6 @@
 // Shared host-side pieces: logging, errors, env config, tokenizer oracle, result checks.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <malloc.h>
 
@@ -7,6 +8,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <string>
+#include <thread>
 
 #include "locust/config.hpp"
 #include "locust/dstring.hpp"
@@ -53,6 +55,17 @@ void throw_error(const char* file, int line, const std::string& msg) {
   throw Error(rank + msg + " (" + where + ")");
 }
 
+namespace {
+std::atomic<const char*> g_stage{"none"};
+std::atomic<u64> g_stages{0};
+}  // namespace
+void set_current_stage(const char* stage) {
+  g_stage.store(stage, std::memory_order_relaxed);
+  g_stages.fetch_add(1, std::memory_order_relaxed);
+}
+const char* current_stage() { return g_stage.load(std::memory_order_relaxed); }
+u64 stages_entered() { return g_stages.load(std::memory_order_relaxed); }
+
 bool fault_injected(int rank, const char* stage) {
   const char* e = std::getenv("LOCUST_FAULT");
   if (!e || !*e) return false;
@@ -60,7 +73,17 @@ bool fault_injected(int rank, const char* stage) {
   auto colon = s.find(':');
   if (colon == std::string::npos) return false;
   int r = std::atoi(s.substr(0, colon).c_str());
-  return r == rank && s.substr(colon + 1) == stage;
+  if (r != rank) return false;
+  const std::string what = s.substr(colon + 1);
+  if (what == std::string("hang_") + stage) {
+    // a rank that stops answering (the SCALE watchdog's test, tests/test_scale_ready.py):
+    // it never returns, like a peer stuck in a collective
+    std::fprintf(stderr, "locust: rank %d: injected hang (LOCUST_FAULT) in stage '%s'\n", rank,
+                 stage);
+    std::fflush(stderr);
+    for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+  }
+  return what == stage;
 }
 
 u64 now_ns() {

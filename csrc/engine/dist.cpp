@@ -158,6 +158,7 @@ DistResult run_distributed_job(const DistConfig& cfg, Communicator& comm, ShardE
   std::string local_msg;
   // Runs a local step, returning its status (0 ok) instead of throwing.
   auto local = [&](const char* stage, const std::function<void()>& fn) -> i32 {
+    set_current_stage(stage);
     if (fault_injected(me, stage)) {
       local_msg = std::string("injected fault (LOCUST_FAULT) in stage '") + stage + "'";
       return 1;

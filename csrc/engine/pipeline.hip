@@ -1953,9 +1953,14 @@ DevicePassPlan plan_device_pass(const JobConfig& cfg, u64 max_bytes, u64 max_lin
       why = "one pass would need " + std::to_string(p.device_bytes >> 20) + " MiB of the " +
             std::to_string(budget >> 20) + " MiB of HBM this engine may use";
     if (!why.empty()) {
-      const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
-      if (max_bytes > chunk) {
-        p = make(true, chunk);
+      // the chunk asked for covers the whole input, and one pass of it does not fit
+      LOCUST_CHECK_ARG(!cfg.chunk_bytes,
+                       "--chunk-mb " + std::to_string(cfg.chunk_bytes >> 20) +
+                           " asks for one device pass of the whole " +
+                           std::to_string(max_bytes) + " B input: " + why +
+                           "; use a smaller --chunk-mb (LOCUST_CHUNK_MB)");
+      if (max_bytes > kDefaultStreamChunk) {
+        p = make(true, kDefaultStreamChunk);
         p.why = why;
       }
     }

@@ -59,6 +59,11 @@ LOCUST_HD inline u64 align_up(u64 a, u64 b) { return div_up(a, b) * b; }
 // throw at the start of <stage> (map|shuffle|reduce|gather) so tests can verify that a
 // failing rank turns into a clean, agreed-upon job failure instead of a hang.
 bool fault_injected(int rank, const char* stage);
+// The distributed job stage this process last entered (a string literal), and how many it
+// has entered: read by a watchdog thread (bench.py) while the job may be stuck in it.
+void set_current_stage(const char* stage);
+const char* current_stage();
+u64 stages_entered();
 
 // Monotonic host clock in nanoseconds.
 u64 now_ns();

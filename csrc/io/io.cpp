@@ -523,21 +523,35 @@ LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_en
     return at[0] != kNone && (open_end ? lix.complete : at[1] != kNone);
   };
   while (base < n && !done()) {
+    // Blocks to read this round: T, or only the one the index says holds the next wanted
+    // newline.  Line s found and line e not yet: first jump over the window's bytes to the
+    // last indexed block before line e's newline (they need no scan).
+    u32 Tr = T;
+    const u64 next_want = at[0] == kNone ? s : (at[1] == kNone && !open_end ? e : kNone);
+    if (next_want != kNone && !lix.nl_before.empty()) {
+      const auto it = std::lower_bound(lix.nl_before.begin(), lix.nl_before.end(), next_want);
+      const u64 jb = (u64)(it - lix.nl_before.begin()) - 1;  // nl_before[0] == 0 < next_want
+      if (jb * B > base) {
+        base = jb * B;
+        seen = lix.nl_before[jb];
+      }
+      if (jb * B == base && jb + 1 < lix.nl_before.size()) Tr = 1;  // it lies in this block
+    }
     auto work = [&](u32 t) {
       const u64 a = base + (u64)t * B;
-      got[t] = a < n ? std::min<u64>(B, n - a) : 0;
+      got[t] = a < n && t < Tr ? std::min<u64>(B, n - a) : 0;
       nls[t] = 0;
       if (got[t]) ok[t] = pread_slice(f.fd, buf[t].data(), a, 0, got[t], true, &nls[t]);
     };
-    if (T == 1) {
+    if (Tr == 1) {
       work(0);
     } else {
       std::vector<std::thread> th;
-      for (u32 t = 1; t < T; ++t) th.emplace_back(work, t);
+      for (u32 t = 1; t < Tr; ++t) th.emplace_back(work, t);
       work(0);
       for (auto& x : th) x.join();
     }
-    for (u32 t = 0; t < T && got[t]; ++t) {
+    for (u32 t = 0; t < Tr && got[t]; ++t) {
       if (!ok[t]) throw Error("short read: " + path);
       const char* blk = buf[t].data();
       const u64 blk_off = base + (u64)t * B;
@@ -560,7 +574,7 @@ LineWindow find_line_window(const std::string& path, i64 line_start, i64 line_en
       }
       seen += nls[t];
     }
-    base += (u64)T * B;
+    base += (u64)Tr * B;
   }
   if (base >= n && !lix.complete) {  // the scan reached EOF: the file's line count
     // a final line without a newline counts; bytes after the scan's start with no newline

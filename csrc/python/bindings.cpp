@@ -879,6 +879,8 @@ PYBIND11_MODULE(_locust, m) {
         "(begin, end, 0): bytes [begin, end) of a file moved to line starts");
   m.def("line_start_at", &line_start_at, py::arg("path"), py::arg("offset"));
   m.def("line_index_cache_path", &line_index_cache_path, py::arg("path"));
+  m.def("native_stage", [] { return py::make_tuple(std::string(current_stage()), stages_entered()); },
+        "(the distributed stage this process last entered, stages entered so far)");
   m.def("spill_index", [](const std::string& spill) -> py::object {
     SpillIndex x;
     if (!read_spill_index(spill, &x)) return py::none();

@@ -47,7 +47,8 @@ def test_gpus_without_enough_gpus_fails_loudly():
         pytest.skip("this box has the GPUs")
     p = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--no-extra", timeout=120)
     assert p.returncode != 0
-    assert not p.stdout.strip()  # no result line at all
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and json.loads(lines[0])["value"] is None  # a failure line only
     assert "needs GPU" in p.stderr
 
 
@@ -60,10 +61,16 @@ def test_gpus_must_match_world_size():
 
 
 def test_failed_rank_fails_the_run():
-    # LOCUST_FAULT makes rank 1's map throw: the parent must exit non-zero, print nothing
+    # LOCUST_FAULT makes rank 1's map throw: the parent exits non-zero and prints ONE
+    # failure line -- no value, the failing rank, every rank's last stage
     env = dict(os.environ, LOCUST_FAULT="1:map")
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--backend", "cpu", "--comm", "tcp", "--steps", "2", "--warmup", "1",
                         "--no-extra"], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=120)
-    assert p.returncode != 0 and not p.stdout.strip(), (p.returncode, p.stdout)
+    assert p.returncode != 0, (p.returncode, p.stdout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["status"] == "failed" and d["value"] is None and "rank" in d["reason"]
+    assert sorted(d["progress"]) == ["0", "1"]

@@ -71,6 +71,9 @@ def test_oversize_chunk_is_refused_at_planning_time():
         plan(400 * GiB, chunk_mb=200_000)
     with pytest.raises(Exception, match="HBM"):
         plan(10 * GiB, chunk_mb=4096, free=8 * GiB)
+    # a chunk that covers the whole input asks for one pass of it: refused, not streamed
+    with pytest.raises(Exception, match="smaller --chunk-mb"):
+        plan(10 * GiB, chunk_mb=400_000)
     # a radix engine cannot stream: refused with the 2^30 bound, not silently wrong
     with pytest.raises(Exception, match="2\\^30"):
         plan(4 * GiB, sort="radix")

@@ -204,3 +204,74 @@ def test_cli_rccl_clique_synth1m_file(tmp_path, cli):
     out, rec = _cli_ranks(cli, f, WORLD, ["--comm", "rccl", "--strategy", "shuffle"])
     _check_cli(out, rec, f, WORLD, device=True)
     assert rec["unique"] == SYNTH1M_UNIQUE
+
+
+# ---------------------------------------------------------------------------------------
+# a run that hangs still ends with one line: a rank stuck in a stage
+# (LOCUST_FAULT=<rank>:hang_<stage> never returns) -> the watchdog's failure line within
+# the budget, with every rank's last stage, native stage and heartbeat
+# ---------------------------------------------------------------------------------------
+def _hung_line(p, world: int, budget: float, elapsed: float) -> dict:
+    assert p.returncode != 0, (p.returncode, p.stdout[-2000:])
+    assert elapsed < budget + 60, elapsed
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["status"] == "failed" and d["value"] is None and d["n_gpus"] == world
+    assert "budget" in d["reason"] or "watchdog" in d["reason"], d["reason"]
+    prog = d["progress"]
+    assert sorted(prog) == [str(r) for r in range(world)]
+    for r in prog.values():  # every rank was alive (beating) and inside a job stage
+        assert r["stage"] is not None and r["heartbeat_age_s"] is not None
+    return d
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_watchdog_cpu_tcp_twin_hang(world):
+    import time
+
+    env = dict(os.environ, LOCUST_FAULT="1:hang_map")
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world),
+                        "--backend", "cpu", "--comm", "tcp", "--steps", "3", "--warmup", "1",
+                        "--no-extra", "--budget-s", "12"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=150)
+    d = _hung_line(p, world, 12, time.time() - t0)
+    assert d["progress"]["1"]["native_stage"] == "map"
+
+
+def test_bench_watchdog_under_torchrun_cpu_twin():
+    """The driver's form for N > 1: torch.distributed.run starts the ranks; rank 0's own
+    watchdog prints the failure line before the launcher tears the job down."""
+    import socket
+    import time
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, LOCUST_FAULT="1:hang_map")
+    env.pop("LOCUST_PROGRESS_DIR", None)
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend",
+                        "cpu", "--comm", "tcp", "--steps", "3", "--warmup", "1", "--no-extra",
+                        "--budget-s", "15"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=240)
+    _hung_line(p, 2, 15 + 30, time.time() - t0)
+
+
+@pytest.mark.gpu
+def test_bench_watchdog_tcpdev_one_gpu_hang():
+    """The one-GPU twin of the device exchange path (tcpdev: TCP control, device data
+    plane): rank 1 hangs in the exchange; the line still comes, inside the budget."""
+    import time
+
+    env = dict(os.environ, LOCUST_FAULT="1:hang_exchange")
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm",
+                        "tcpdev", "--steps", "3", "--warmup", "1", "--no-extra", "--strategy",
+                        "shuffle", "--budget-s", "25"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=110)
+    _hung_line(p, 2, 25, time.time() - t0)
