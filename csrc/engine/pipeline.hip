@@ -370,8 +370,6 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   st += t_scan;
   lb_dict = {st, counters + 5};
   // counters[6] is the ordered kernels' done counter (lb_dict.tile_counter + 1);
-  // counters[8..9]: the fused launch's ticket and tiles done
-  d_fuse = counters + 8;
   d_plan_flag = counters + 7;  // OrderedExtra::plan_flag
 
   rx.cap = rcap;
@@ -742,7 +740,7 @@ void DevicePipeline::launch_dict_graph(const TextInput& in, bool compat) {
   LOCUST_HIP_CHECK(hipGraphLaunch(hit->exec, stream));
 }
 
-void DevicePipeline::enqueue_map(const TextInput& in, bool launch) {
+void DevicePipeline::enqueue_map(const TextInput& in) {
   plan_pass = false;  // decided per pass (decide_plan) where the map can write occupancy
   parts_ready = cfg.map_path == MapPath::kFast;
   devplan_used = false;
@@ -829,7 +827,6 @@ void DevicePipeline::enqueue_map(const TextInput& in, bool launch) {
                       in.bytes, make_delim_mask(cfg.delimiters.c_str()), map_text);
     }
     decide_plan(in.bytes);
-    if (launch)
     launch_map_fast(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
                     cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, lb_map,
                     stream, map_trace(), part_tiles ? d_part_off : nullptr, part_map(), false,
@@ -1034,6 +1031,7 @@ void DevicePipeline::maybe_retune(const EntryList& e) {
 void DevicePipeline::poll_retune() {
   if (!retune_pending || !retune_worker.idle()) return;
   retune_pending = false;
+  retune_worker.rethrow_error();  // a failed retune surfaces here, on the job's thread
   const RetuneTask& r = retune_task;
   LOCUST_LOG_DEBUG("retune on the worker: started %.3f ms after the job, output read in %.3f "
                    "ms, map built in %.3f ms (%zu first-word groups)",
@@ -1090,11 +1088,6 @@ void DevicePipeline::enqueue_dict_ordered(bool with_counts, bool mapped, bool se
   ex.pm = part_map();
   ex.part_w = d_pw;
   ex.split_min = split_min;
-  ex.split_floor = split_floor;
-  ex.split_fused = split_fused;
-  ex.rank_w0 = rank_w0;
-  ex.early_publish = early_publish;
-  ex.small_table = small_table;
   if (self_clean) set_self_clean(ex);
   if (self_clean && done_pending) {  // the kernel itself tells the host it is done
     ex.host_done = d_done;
@@ -1231,17 +1224,6 @@ void DevicePipeline::print_ord_trace() {
       last_p = p;
     }
   }
-  // a fused launch (map_ordered_kernel) also stamps its map tiles: start 21, counted 22
-  u64 tile_in = ~0ull, tile_out = 0;
-  int ntile = 0;
-  for (int p = 0; p < kDictParts; ++p) {
-    const u64* x = &t[p * 32];
-    if (!x[21]) continue;
-    ++ntile;
-    tile_in = std::min(tile_in, x[21]);
-    if (x[22] >= x[23]) tile_out = std::max(tile_out, x[22]);
-  }
-  if (ntile) first_in = std::min(first_in, tile_in);
   if (last_p >= 0)
     std::fprintf(stderr, "ord span=%.2f us (first entry -> last exit), last p=%d m=%llu\n",
                  (last_out - first_in) * 0.01, last_p, (unsigned long long)t[last_p * 32 + 6]);
@@ -1256,28 +1238,7 @@ void DevicePipeline::print_ord_trace() {
       std::fprintf(stderr, "ord tail: last exit -> last done count %.2f us, -> self-clean done %.2f us\n",
                    (done_max - last_out) * 0.01, clean >= last_out ? (clean - last_out) * 0.01 : -1.0);
   }
-  if (ntile) {
-    u64 wait_end = 0;
-    for (int p = 0; p < kDictParts; ++p)
-      if (t[p * 32 + 20]) wait_end = std::max(wait_end, t[p * 32 + 20]);
-    std::vector<double> body, fence;
-    for (int p = 0; p < kDictParts; ++p) {
-      const u64* x = &t[p * 32];
-      if (!x[21]) continue;
-      body.push_back((x[23] - x[21]) * 0.01);
-      if (x[22] >= x[23]) fence.push_back((x[22] - x[23]) * 0.01);  // a worker's first tile
-    }
-    std::sort(body.begin(), body.end());
-    std::sort(fence.begin(), fence.end());
-    if (fence.empty()) fence.push_back(0.0);
-    std::fprintf(stderr,
-                 "fused: %d tiles stamped, first tile start %.2f us, last tile counted %.2f us, "
-                 "last partition wait end %.2f us; tile body median %.2f max %.2f us, release "
-                 "median %.2f max %.2f us\n",
-                 ntile, (tile_in - first_in) * 0.01, (tile_out - first_in) * 0.01,
-                 wait_end ? (wait_end - first_in) * 0.01 : 0.0, body[body.size() / 2],
-                 body.back(), fence[fence.size() / 2], fence.back());
-  }
+
   for (int p = 0; p < kDictParts; ++p) {
     const u64* x = &t[p * 32];
     if (!x[0] || !x[6]) continue;
@@ -1293,43 +1254,6 @@ void DevicePipeline::print_ord_trace() {
                  x[20] ? (x[20] - x[10]) * 0.01 : 0.0,
                  x[25] >= x[11] ? (x[25] - x[11]) * 0.01 : -1.0);
   }
-}
-
-bool DevicePipeline::fuse_ok(const TextInput& in) const {
-  const char* e = std::getenv("LOCUST_FUSE");
-  if (!e || e[0] != '1') return false;  // opt-in: measured slower than two launches
-  return cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict && pieces.empty() &&
-         in.bytes > 0 && in.bytes < kMapLargeInput && cap <= kPartBuildMaxTokens && !large_ordered &&
-         table_tiles(in.bytes) == div_up(in.bytes, (u64)kMapTileBytesMin) &&
-         table_tiles(in.bytes) <= (u64)kFuseMaxTiles;
-}
-
-bool DevicePipeline::enqueue_map_ordered(const TextInput& in) {
-  enqueue_map(in, /*launch=*/false);
-  job_self_cleaned = true;  // the ordered half re-zeroes the scratch, the fuse counters too
-  OrderedExtra ex;
-  ex.pm = part_map();
-  ex.part_w = d_pw;
-  ex.split_min = split_min;
-  ex.split_floor = split_floor;
-  ex.split_fused = split_fused;
-  ex.rank_w0 = rank_w0;
-  ex.early_publish = early_publish;
-  ex.small_table = small_table;
-  set_self_clean(ex);
-  if (done_pending) {  // the kernel itself tells the host it is done
-    ex.host_done = d_done;
-    ex.host_done_value = done_pending;
-    done_pending = 0;
-  }
-  set_tile_source(ex, false);
-  ex.plan_flag = nullptr;  // the fused map does not raise it: plan every pass
-  set_compact_out(ex, true);
-  ex.fuse = d_fuse;
-  launch_map_ordered(map_text, in.bytes, make_delim_mask(cfg.delimiters.c_str()),
-                     cfg.emits_per_line, cfg.max_key_len, tokens, d_parts, cap, d_ctr, part_map(),
-                     d_out_mapped, d_ctr_mapped, lb_dict, stream, ord_trace(), ex);
-  return true;
 }
 
 bool DevicePipeline::enqueue_dict_job(u32 num_lines, bool compat, bool with_counts, hipEvent_t after_process,
@@ -1405,14 +1329,11 @@ void DevicePipeline::download_output(WordCountResult& r, hipEvent_t done) {
 }
 
 void DevicePipeline::set_compact_out(OrderedExtra& ex, bool mapped) {
-  // LOCUST_COMPACT_OUT=0: 40-B records instead (read per job: tools/env_ab.py A/B)
-  const char* e = std::getenv("LOCUST_COMPACT_OUT");
-  ord_compact = mapped && !(e && e[0] == '0');
+  ord_compact = mapped;
   if (!ord_compact) return;
   ex.cout = reinterpret_cast<u64*>(d_out_mapped);
   ex.ctab = d_ctab_mapped;
   ex.out_cap = std::min<u64>(ex.out_cap, h_out_cap);
-  ex.reserve = ord_reserve && ex.self_clean && !ex.recs && !ex.sorted.w[0] && !ex.hdr;
 }
 
 void DevicePipeline::copy_out(EntryList& e, u64 u, bool compact) {
@@ -1533,13 +1454,11 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
   split_stages = !lean && !graphed;
   skip_sync_reset = clean_start && !compat;
   if (!lean) LOCUST_HIP_CHECK(hipEventRecord(ev[0], stream));
-  // lean dictionary jobs of a small pass: Map and the ordered build in one launch
-  const bool fused = lean && dict_path && !compat && fuse_ok(in);
   const bool dbg = (int)log_level() >= (int)LogLevel::kDebug;
   u64 t_map = 0;
   if (lean) {
     enqueue_upload(in);
-    if (!fused) enqueue_map(in);
+    enqueue_map(in);
     if (dbg) t_map = now_ns();
   } else if (graphed) {
     prepare_upload(in);
@@ -1564,9 +1483,8 @@ WordCountResult DevicePipeline::run(const TextInput& in) {
     bool ordered = graph_ordered;
     if (lean) {
       done_pending = ++done_seq;
-      ordered = fused ? enqueue_map_ordered(in)
-                      : enqueue_dict_job((u32)in.num_lines, compat, false, nullptr,
-                                         /*self_clean=*/true);
+      ordered = enqueue_dict_job((u32)in.num_lines, compat, false, nullptr,
+                                 /*self_clean=*/true);
       if (done_pending) publish_done(done_seq);
       done_pending = 0;
     } else if (!graphed) {

@@ -213,39 +213,6 @@ struct DevicePipeline {
     const char* e = std::getenv("LOCUST_SPLIT_MIN");
     return e ? (u32)std::max(0, std::atoi(e)) : 0u;
   }();
-  // LOCUST_SPLIT_FLOOR (read at construction): a partition of fewer tokens never splits
-  const u32 split_floor = [] {
-    const char* e = std::getenv("LOCUST_SPLIT_FLOOR");
-    return e ? (u32)std::max(0, std::atoi(e)) : 0u;
-  }();
-  // LOCUST_SPLIT_FUSED=0 (A/B): siblings gather their samples and their tokens separately
-  const u32 split_fused = [] {
-    const char* e = std::getenv("LOCUST_SPLIT_FUSED");
-    return e && e[0] == '0' ? 0u : 1u;
-  }();
-  // LOCUST_RANK_W0=0 (A/B): the all-pairs ranking reads all four key words per candidate
-  const u32 rank_w0 = [] {
-    const char* e = std::getenv("LOCUST_RANK_W0");
-    return e && e[0] == '0' ? 0u : 1u;
-  }();
-  // LOCUST_EARLY_PUBLISH=0 (A/B): the ordered kernel publishes its aggregate after writing
-  // the compacted key arrays instead of before
-  const u32 early_publish = [] {
-    const char* e = std::getenv("LOCUST_EARLY_PUBLISH");
-    return e && e[0] == '0' ? 0u : 1u;
-  }();
-  // LOCUST_SMALL_TABLE=0 (A/B): every ordered-kernel partition clears its whole LDS table
-  const u32 small_table = [] {
-    const char* e = std::getenv("LOCUST_SMALL_TABLE");
-    return e && e[0] == '0' ? 0u : 1u;
-  }();
-  // LOCUST_ORD_RESERVE=1: the host-output ordered build reserves its partitions' output
-  // with an atomic instead of placing it by the look-back (OrderedExtra::reserve; measured
-  // no faster: the span shrinks, the PCIe drain of the records moves into the tail)
-  const bool ord_reserve = [] {
-    const char* e = std::getenv("LOCUST_ORD_RESERVE");
-    return e && e[0] == '1';
-  }();
   // Scratch of the merge kernels (launch_merge_*: they reset it themselves): the heads and
   // scan regions, which lie back to back -- 2 * (cap / kReduceTile + 1) status words.
   LookbackScratch lb_merge(u64 n) const {
@@ -550,15 +517,7 @@ struct DevicePipeline {
     return in.bytes <= kZeroCopyMaxBytes;
   }
 
-  // launch = false: the pass's bookkeeping only (partition table, plan decision, flags) --
-  // the fused map + ordered launch maps the text itself (enqueue_map_ordered).
-  void enqueue_map(const TextInput& in, bool launch = true);
-  // The headline job's Map + Process + Reduce in ONE launch (dict.hip map_ordered_kernel):
-  // small single-pass dictionary jobs with the fast map and its partition table.
-  // LOCUST_FUSE=0 (read per job): the two launches instead.
-  u32* d_fuse = nullptr;  // [ticket, tiles done] in the sync block (zeroed with it)
-  bool fuse_ok(const TextInput& in) const;
-  bool enqueue_map_ordered(const TextInput& in);
+  void enqueue_map(const TextInput& in);
 
   // Compaction (compat path) + radix sort of `tokens` into `sorted` (and counts).
   // host_n: record count when the host already knows it.  With sync_plan the count is

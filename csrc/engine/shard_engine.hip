@@ -254,31 +254,20 @@ class GpuShardEngine final : public ShardEngine {
     const bool no_reset = m.sync_clean;
     m.sync_clean = false;
     m.parts_ready = true;  // set before enqueue: ordered_ok() is consulted while capturing
-    // Map and ordered build in one launch (DevicePipeline::enqueue_map_ordered), as the
-    // single-GPU job does
-    const bool fused = m.fuse_ok(shard);
     const DevicePipeline::GraphKeyArr key{
         (spec_samples ? 2u : 3u) | (hdr ? 0x100u : 0u) | (no_reset ? 0x200u : 0u) |
-            (fused ? 0x400u : 0u) | ((u64)slot_recs << 32),
+            ((u64)slot_recs << 32),
         shard.bytes, shard.num_lines, reinterpret_cast<u64>(m.map_text), (u64)m.upload_mode,
         m.upload_mode == DevicePipeline::Upload::kDirect ? reinterpret_cast<u64>(shard.data) : 0};
-    DeviceHalf enqueue = [this, shard, spec_samples, ex, no_reset, fused]() mutable {
+    DeviceHalf enqueue = [this, shard, spec_samples, ex, no_reset]() mutable {
       DevicePipeline& m = *mp_;
       m.skip_sync_reset = no_reset;
       m.enqueue_upload_device(shard);
       m.skip_sync_reset = false;
-      m.enqueue_map(shard, /*launch=*/!fused);
+      m.enqueue_map(shard);
       m.set_tile_source(ex, false);
-      if (fused) {
-        ex.fuse = m.d_fuse;
-        launch_map_ordered(m.map_text, shard.bytes, make_delim_mask(m.cfg.delimiters.c_str()),
-                           m.cfg.emits_per_line, m.cfg.max_key_len, m.tokens, m.d_parts, m.cap,
-                           m.d_ctr, m.part_map(), nullptr, m.d_ctr_mapped, m.lb_dict, m.stream,
-                           m.ord_trace(), ex);
-      } else {
-        launch_dict_ordered(m.tokens, nullptr, m.d_parts, &m.d_ctr->num_records, m.cap, m.d_ctr,
-                            nullptr, m.d_ctr_mapped, m.lb_dict, m.stream, m.ord_trace(), ex);
-      }
+      launch_dict_ordered(m.tokens, nullptr, m.d_parts, &m.d_ctr->num_records, m.cap, m.d_ctr,
+                          nullptr, m.d_ctr_mapped, m.lb_dict, m.stream, m.ord_trace(), ex);
       if (spec_samples) {
         launch_sample_keys(local_keys_, local_n_, kSpecSamples, m.d_samples, m.stream);
         LOCUST_HIP_CHECK(hipMemcpyAsync(m.h_small, m.d_samples, kSpecSamples * sizeof(PackedKey),

@@ -66,9 +66,6 @@ constexpr int kMapSegStepsSmall = 4;
 constexpr int kMapSegStepsLarge = 16;
 constexpr int kMapTileBytesMin = (kMapBlock / 64) * kMapSegStepsSmall * 64;
 constexpr u64 kMapLargeInput = 8ull << 20;  // switch to large tiles above 8 MiB
-// the fused map + ordered launch (map_ordered_kernel) maps at most this many 1 KiB tiles:
-// one per workgroup of its kDictParts
-constexpr u32 kFuseMaxTiles = 256;
 constexpr int kLineIdxBlock = 256;
 constexpr int kLineIdxItems = 16;                             // bytes per thread
 constexpr int kLineIdxTile = kLineIdxBlock * kLineIdxItems;
@@ -331,11 +328,6 @@ struct OrderedExtra {
   // re-zeroes it.  Null: plan every pass.
   u32* plan_flag = nullptr;
   u32 split_min = 0;            // planned workgroups: tokens per extra sibling (0: default)
-  u32 split_floor = 0;          // ... and the fewest tokens of a partition that splits at all
-  u32 split_fused = 1;          // siblings: one gather for the samples and the inserts
-  u32 rank_w0 = 1;              // all-pairs ranks: further key words read only on a first-word tie
-  u32 early_publish = 1;        // publish (keys, tokens) before writing the compacted arrays
-  u32 small_table = 1;          // tile-source partitions clear 512 table slots unless they need more
   // The partition map the tokens' partitions were computed with (default: first byte).
   PartMap pm{};
   // Optional (host-mapped): part_w[p] = partition p's work (tokens + kPartDistinctWeight x
@@ -352,28 +344,11 @@ struct OrderedExtra {
   // ~0: not written).
   u64* cout = nullptr;
   u64* ctab = nullptr;
-  // With cout + self_clean, no recs / sorted / hdr: no look-back -- a virtual partition
-  // reserves its entries with one atomic on status[kDictParts] (arrival order, not key
-  // order: ctab[v] carries where they went), so no workgroup waits for the slowest one
-  // before it; the last workgroup to finish publishes the totals (LOCUST_ORD_RESERVE=1;
-  // off by default: docs/PERFORMANCE.md round 5).
-  bool reserve = false;
-  // The fused map + ordered kernel's counters ([0] ticket, [1] tiles done; zeroed before
-  // the launch, re-zeroed by the self-clean): launch_map_ordered.
-  u32* fuse = nullptr;
 };
 void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts,
                          const u32* d_n, u64 cap, MapCounters* ctr, OutRecord* out,
                          MapCounters* ctr_out, LookbackScratch lb, hipStream_t s,
                          u64* trace = nullptr, const OrderedExtra& ex = OrderedExtra{});
-// The fast map (1 KiB tiles, part_off table, optional part_occ) and the ordered build over
-// it (TileSource) in one launch (dict.hip map_ordered_kernel): ex.part_off / part_tiles
-// (= ceil(bytes / 1 KiB), bytes < kMapLargeInput) and ex.fuse are required; everything else
-// as launch_map_fast followed by launch_dict_ordered.
-void launch_map_ordered(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
-                        int max_key_len, KeysSoA tokens, u8* parts, u64 cap, MapCounters* ctr,
-                        PartMap pm, OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
-                        hipStream_t s, u64* trace, const OrderedExtra& ex);
 // Writes `value` to the host-mapped `word` once everything earlier on `s` has completed
 // (signal.hip; the lean job path polls it instead of synchronising the stream).
 void launch_signal_host(u32* word, u32 value, hipStream_t s);

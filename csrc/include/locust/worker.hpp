@@ -9,8 +9,10 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
+#include <stdexcept>
 #include <thread>
 #include <utility>
 
@@ -30,11 +32,14 @@ class TaskWorker {
   }
   // No task queued or running (never blocks).
   bool idle() const { return !busy_.load(std::memory_order_acquire); }
-  // Runs f on the worker thread; the caller makes sure the worker is idle.
+  // Runs f on the worker thread.  The worker must be idle (one task at a time): a submit
+  // over a queued or running task is refused loudly instead of replacing it.
   void submit(std::function<void()> f) {
     start();
     {
       std::lock_guard<std::mutex> lk(mu_);
+      if (busy_.load(std::memory_order_acquire) || task_)
+        throw std::logic_error("TaskWorker::submit: the worker is still busy with a task");
       task_ = std::move(f);
       busy_.store(true, std::memory_order_release);
     }
@@ -43,6 +48,16 @@ class TaskWorker {
   void wait_idle() {
     std::unique_lock<std::mutex> lk(mu_);
     idle_cv_.wait(lk, [&] { return !busy_.load(std::memory_order_acquire); });
+  }
+  // The exception the last task threw (cleared), rethrown on the caller's thread -- a task
+  // never takes the process down with std::terminate on the worker thread.
+  void rethrow_error() {
+    std::exception_ptr e;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      std::swap(e, error_);
+    }
+    if (e) std::rethrow_exception(e);
   }
   // Finishes the running task, then ends the thread.
   void stop() {
@@ -63,9 +78,15 @@ class TaskWorker {
         std::function<void()> f = std::move(task_);
         task_ = nullptr;
         lk.unlock();
-        f();
+        std::exception_ptr err;
+        try {
+          f();
+        } catch (...) {
+          err = std::current_exception();
+        }
         f = nullptr;  // captured state is released before the worker reports idle
         lk.lock();
+        if (err) error_ = err;
         busy_.store(false, std::memory_order_release);
         idle_cv_.notify_all();
         continue;
@@ -77,6 +98,7 @@ class TaskWorker {
   std::mutex mu_;
   std::condition_variable cv_, idle_cv_;
   std::function<void()> task_;
+  std::exception_ptr error_;
   std::atomic<bool> busy_{false};
   bool stop_ = false;
 };

@@ -219,7 +219,7 @@ constexpr u32 kOrdTagWindow = kPartBlock * 32;  // ordered build: tags scanned p
 constexpr int kPartPerThread = kPartSlots / kPartBlock;
 // The ordered kernel's tile-source partitions clear only the first kSmallTable slots of
 // their table; one of more than kSmallTableTokens tokens (so possibly more distinct keys
-// than 3/4 of that) clears the rest before its first insert (OrderedExtra::small_table).
+// than 3/4 of that) clears the rest before its first insert (grow_table).
 constexpr u32 kSmallTable = 512;
 constexpr u32 kSmallTableTokens = kSmallTable * 3 / 4;
 
@@ -692,7 +692,7 @@ struct TileSource {
     if (threadIdx.x == 0) *s_tmask = kPartSlots - 1;
     return kPartSlots - 1;
   }
-  // mask: the cleared table's (kPartSlots - 1, or kSmallTable - 1 with small_table)
+  // mask: the cleared table's (kPartSlots - 1, or kSmallTable - 1 for tile sources)
   __device__ bool build(u32 p, Pre pre, LdsSlot* s_tab, u32* s_list, u32& s_count,
                         u64* stamp, u32 mask = kPartSlots - 1, u32* s_tmask = nullptr) const {
     bool full = false;
@@ -741,14 +741,14 @@ struct TileSource {
   // it the same way and agree on every cut: each key lands in exactly one sibling, which
   // then inserts only its own range.  `pre`: this thread's run (tile threadIdx.x; the plan
   // admits at most kPartBlock tiles).
-  // fused (LOCUST_SPLIT_FUSED, default on; a partition of at most kGatherBatch x 1,024
-  // tokens): the tokens' first two words are loaded once, the samples taken from those
-  // registers and sorted by every wave in registers -- one global round trip per sibling
-  // instead of two, and no LDS rank pass (the cuts are the same: same sample positions).
+  // A partition of at most kGatherBatch x 1,024 tokens: the tokens' first two words are
+  // loaded once, the samples taken from those registers and sorted by every wave in
+  // registers -- one global round trip per sibling, no LDS rank pass; larger ones sample
+  // the list first, then gather (the cuts are the same: same sample positions).
   static constexpr u32 kSplitSamples = 64;
   __device__ bool build_split(u32 p, Pre pre, u32 j, u32 K, LdsSlot* s_tab, u32* s_list,
-                              u32* s_scan, u64* stamp, bool fused,
-                              u32 mask = kPartSlots - 1, u32* s_tmask = nullptr) const {
+                              u32* s_scan, u64* stamp, u32 mask = kPartSlots - 1,
+                              u32* s_tmask = nullptr) const {
     u64* s_samp = reinterpret_cast<u64*>(s_list + kPartWindow - 256);  // [64]
     u64* s_sort = reinterpret_cast<u64*>(s_list + kPartWindow - 128);  // [64]
     const u32 a = pre.a, len = threadIdx.x < ntiles ? pre.b - pre.a : 0u;
@@ -764,7 +764,7 @@ struct TileSource {
     const bool last = j + 1 >= K;
     // a list cut short by the sample area is an overflow: the host redoes the pass
     bool full = n > lim;
-    if (fused && lim <= (u32)(kGatherBatch * kPartBlock)) {
+    if (lim <= (u32)(kGatherBatch * kPartBlock)) {
       u32 idx[kGatherBatch];
       u64 k[kGatherBatch][kKeyWords];
       u64 c[kGatherBatch];
@@ -1080,15 +1080,13 @@ __device__ u32 write_compact_records(u64* __restrict__ dst, u32 m, Word word, u3
   return total;
 }
 
-// The ordered kernel's workgroup (dict_ordered_kernel, and the partition workgroups of the
-// fused map + ordered kernel).  guess: the partition whose runs are worth prefetching while
-// the ticket atomic is in flight (the block index of a plain launch; ~0u: none).
+// The ordered kernel's workgroup (dict_ordered_kernel).  guess: the partition whose runs
+// are worth prefetching while the ticket atomic is in flight (the block index; ~0u: none).
 template <class Src>
 __device__ __forceinline__ void ordered_partition(
     Src src, MapCounters* __restrict__ ctr,
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
-    u32* __restrict__ tile_ctr, u64* __restrict__ trace, const OrderedExtra& ex, u32 guess_p,
-    u64 rt_in = 0) {
+    u32* __restrict__ tile_ctr, u64* __restrict__ trace, const OrderedExtra& ex, u32 guess_p) {
 #define ORD_STAMP(k_)                                                          \
   if (trace && threadIdx.x == 0) trace[(u64)v * 32 + (k_)] = __builtin_amdgcn_s_memtime()
   __shared__ LdsSlot s_tab[kPartSlots];
@@ -1107,9 +1105,8 @@ __device__ __forceinline__ void ordered_partition(
   // sharing the GPU (the TCP / loopback rehearsals) could fill the CUs with spinning
   // workgroups whose predecessors were never dispatched: measured as multi-second stalls
   // and a hang with four ranks on one GPU.
-  // 100 MHz, device-wide; a fused launch passes its workgroup's start (before the tile wait)
-  const u64 rt_now = trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  const u64 rt_entry = rt_in ? rt_in : rt_now;
+  // 100 MHz, device-wide
+  const u64 rt_entry = trace ? __builtin_amdgcn_s_memrealtime() : 0;
   // v: this workgroup's virtual partition = its ticket (the look-back order); p: the map
   // partition whose tokens it reads; (vj, vk): its share of p (see OrderedExtra::part_occ).
   // Without a plan, v == p and vk == 1.
@@ -1163,12 +1160,12 @@ __device__ __forceinline__ void ordered_partition(
   const bool guessing = guess_p != ~0u;
   const typename Src::Pre guess = guessing ? src.prefetch(guess_p) : typename Src::Pre{};
   // The ticket atomic is issued first and the table cleared while it and the plan's loads
-  // are in flight (the clear needs neither).  The table's slots in use: all, or
-  // (small_table) the first kSmallTable until a build finds more tokens (grow_table).
+  // are in flight (the clear needs neither).  The table's slots in use: all, or (tile
+  // sources) the first kSmallTable until a build finds more tokens (grow_table).
   __shared__ u32 s_tmask;
   u32 ticket = 0;
   if (threadIdx.x == 0) ticket = atomicAdd(tile_ctr, 1u);  // its value is waited for below
-  const u32 tmask0 = kTiles && ex.small_table ? kSmallTable - 1 : (u32)kPartSlots - 1;
+  const u32 tmask0 = kTiles ? kSmallTable - 1 : (u32)kPartSlots - 1;
   for (int i = threadIdx.x; i <= (int)tmask0; i += kPartBlock) {
 #pragma unroll
     for (int j = 0; j < kKeyWords; ++j) s_tab[i].w[j] = 0;
@@ -1215,8 +1212,7 @@ __device__ __forceinline__ void ordered_partition(
     u32 K = 0;
     if (occupied) {
       const u32 extra = T ? (u32)((u64)tp * (u32)(kDictParts - E) / T) : 0u;
-      K = tp < ex.split_floor ? 1u
-                              : 1u + min(extra, tp / (ex.split_min ? ex.split_min : kSplitMinTokens));
+      K = 1u + min(extra, tp / (ex.split_min ? ex.split_min : kSplitMinTokens));
     }
     u32 kinc = 0;
     if (threadIdx.x < kDictParts) {
@@ -1252,7 +1248,7 @@ __device__ __forceinline__ void ordered_partition(
   ORD_STAMP(0);
   if (trace && threadIdx.x == 0) {
     trace[(u64)v * 32 + 10] = rt_entry;
-    trace[(u64)v * 32 + 20] = rt_in ? rt_now : 0;  // fused: the tile wait's end
+    trace[(u64)v * 32 + 20] = 0;
     trace[(u64)v * 32 + 16] = 0;
     trace[(u64)v * 32 + 17] = ~0ull;
     trace[(u64)v * 32 + 18] = 0;
@@ -1269,8 +1265,7 @@ __device__ __forceinline__ void ordered_partition(
   if constexpr (kTiles) {
     if (vk > 1)
       full = src.build_split(p, first, vj, vk, s_tab, s_list, reinterpret_cast<u32*>(s_scan),
-                             trace ? trace + (u64)v * 32 : nullptr, ex.split_fused != 0, tmask0,
-                             &s_tmask);
+                             trace ? trace + (u64)v * 32 : nullptr, tmask0, &s_tmask);
     else if (vk == 1)
       full = src.build(p, first, s_tab, s_list, s_count, trace ? trace + (u64)v * 32 : nullptr,
                        tmask0, &s_tmask);
@@ -1341,9 +1336,8 @@ __device__ __forceinline__ void ordered_partition(
     }
     wbase = (u32)__builtin_amdgcn_readlane((int)wbase, 63);
     cpos = wbase + dev::lanes_below(b0) + dev::lanes_below(b1);
-    if (!ex.early_publish) write_compacted(cpos);
   }
-  __syncthreads();  // the sums are complete (and, unless early_publish, the arrays)
+  __syncthreads();  // the sums are complete
   const u32 m = s_cm;
   const int any_full = s_cfull != 0u;
   const u64 tok = s_ctok;
@@ -1353,26 +1347,17 @@ __device__ __forceinline__ void ordered_partition(
   // ---- publish (distinct keys, tokens, overflow) now; the look-back resolves after the
   // sort, which does not need the prefix -- so waiting for predecessors overlaps it ----
   const u64 agg = (u64)m | ((u64)(any_full ? 1 : 0) << kOrdOvfShift) | (tok << kOrdTokShift);
-  // (ex.reserve: no look-back -- the workgroup reserves its output words with one atomic
-  // on status[kDictParts] below, in arrival order, and ctab[v] tells the host where)
-  if (threadIdx.x == 0 && !ex.reserve) dev::publish_aggregate(status, v, agg);
+  if (threadIdx.x == 0) dev::publish_aggregate(status, v, agg);
   ORD_STAMP(2);
-  if (ex.early_publish) {  // the arrays after the publish: successors stop waiting sooner
-    write_compacted(cpos);
-    __syncthreads();
-  }
+  // the compacted arrays after the publish: successors stop waiting sooner
+  write_compacted(cpos);
+  __syncthreads();
   u64 pre = 0;
   u32 cwords = ~0u;  // compact words written (ex.cout), ~0u: none
   if (small) {
     // ---- small partition: all-pairs ranks: rank_i = #{j : key_j < key_i}, the sorted
     // position in one pass, no bucket sort.  Wave 0 resolves the look-back meanwhile. ----
-    if (dev::wave_id() == 0 && ex.reserve) {
-      if (dev::lane_id() == 0) {
-        s_prefix = atomicAdd(reinterpret_cast<unsigned long long*>(&status[kDictParts]),
-                             (unsigned long long)agg);
-        if (trace) trace[(u64)v * 32 + 15] = __builtin_amdgcn_s_memtime();  // reserved
-      }
-    } else if (dev::wave_id() == 0) {
+    if (dev::wave_id() == 0) {
       // Look-back in ONE round trip: wave 0 reads every predecessor's status word at once
       // (4 per lane, p < 256) instead of walking back 64 words per dependent round trip
       // (~1-2 us each across XCDs).  prefix = the highest inclusive value found + the
@@ -1440,55 +1425,28 @@ __device__ __forceinline__ void ordered_partition(
         const u32 j0 = sl * m / S, j1 = (sl + 1) * m / S;
         u32 cnt = 0;
         u32 wcnt = 0;  // compact words of the smaller keys: this key's compact offset
-        if (ex.rank_w0) {
-          // first words only (12 of the 36 LDS bytes per candidate): the further words are
-          // read for a candidate whose first word equals this key's -- rare (keys of 8+
-          // bytes sharing their first 8), and a divergent branch
-          for (u32 j = j0; j < j1; j += 4) {
-            u64 c0[4];
-            u32 cw[4];
+        // first words only (12 of the 36 LDS bytes per candidate): the further words are
+        // read for a candidate whose first word equals this key's -- rare (keys of 8+
+        // bytes sharing their first 8), and a divergent branch
+        for (u32 j = j0; j < j1; j += 4) {
+          u64 c0[4];
+          u32 cw[4];
 #pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-              const u32 jj = j + q < j1 ? j + q : j0;
-              c0[q] = s_w0[jj];
-              cw[q] = s_cw[jj];
-            }
-#pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-              const u32 jj = j + q;
-              bool lt = jj < j1 && c0[q] < k0;
-              if (jj < j1 && c0[q] == k0 && jj != i) {
-                const u64 c1 = s_k123[3 * jj], c2 = s_k123[3 * jj + 1], c3 = s_k123[3 * jj + 2];
-                lt = c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)));
-              }
-              cnt += lt ? 1u : 0u;
-              wcnt += lt ? cw[q] : 0u;
-            }
+          for (u32 q = 0; q < 4; ++q) {
+            const u32 jj = j + q < j1 ? j + q : j0;
+            c0[q] = s_w0[jj];
+            cw[q] = s_cw[jj];
           }
-        } else {
-          for (u32 j = j0; j < j1; j += 4) {
-            u64 c0[4], c1[4], c2[4], c3[4];
-            u32 cw[4];
 #pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-              const bool in = j + q < j1;
-              const u32 jj = in ? j + q : j0;
-              c0[q] = s_w0[jj];
-              c1[q] = s_k123[3 * jj];
-              c2[q] = s_k123[3 * jj + 1];
-              c3[q] = s_k123[3 * jj + 2];
-              cw[q] = s_cw[jj];
+          for (u32 q = 0; q < 4; ++q) {
+            const u32 jj = j + q;
+            bool lt = jj < j1 && c0[q] < k0;
+            if (jj < j1 && c0[q] == k0 && jj != i) {
+              const u64 c1 = s_k123[3 * jj], c2 = s_k123[3 * jj + 1], c3 = s_k123[3 * jj + 2];
+              lt = c1 < k1 || (c1 == k1 && (c2 < k2 || (c2 == k2 && c3 < k3)));
             }
-#pragma unroll
-            for (u32 q = 0; q < 4; ++q) {
-              // (a bitwise, branch-free form of this compare measured 1 % slower here: the
-              // short-circuit exits early for most candidates, whose first words differ)
-              const bool lt = j + q < j1 &&
-                              (c0[q] < k0 || (c0[q] == k0 && (c1[q] < k1 || (c1[q] == k1 &&
-                               (c2[q] < k2 || (c2[q] == k2 && c3[q] < k3))))));
-              cnt += lt ? 1u : 0u;
-              wcnt += lt ? cw[q] : 0u;
-            }
+            cnt += lt ? 1u : 0u;
+            wcnt += lt ? cw[q] : 0u;
           }
         }
         if (trace)
@@ -1505,7 +1463,7 @@ __device__ __forceinline__ void ordered_partition(
     }
     __syncthreads();
     pre = s_prefix;
-    if (threadIdx.x == 0 && v != 0 && !ex.reserve)  // inclusive value for later walkers
+    if (threadIdx.x == 0 && v != 0)  // inclusive value for later walkers
       dev::st_agent(&status[v], dev::kLbInc | (pre + agg));
     ORD_STAMP(3);
     ORD_STAMP(4);
@@ -1686,14 +1644,8 @@ __device__ __forceinline__ void ordered_partition(
   __syncthreads();
   ORD_STAMP(3);
   if (dev::wave_id() == 0) {
-    if (ex.reserve) {
-      if (dev::lane_id() == 0)
-        s_prefix = atomicAdd(reinterpret_cast<unsigned long long*>(&status[kDictParts]),
-                             (unsigned long long)agg);
-    } else {
-      const u64 e = dev::wave_lookback_resolve(status, v, agg);
-      if (dev::lane_id() == 0) s_prefix = e;
-    }
+    const u64 e = dev::wave_lookback_resolve(status, v, agg);
+    if (dev::lane_id() == 0) s_prefix = e;
   }
   __syncthreads();
   pre = s_prefix;
@@ -1754,8 +1706,7 @@ __device__ __forceinline__ void ordered_partition(
     const u64 w = (tok + (u64)kPartDistinctWeight * m) * (vplan ? vk : 1u);
     ex.part_w[p] = (u32)(w < 0xffffffffull ? w : 0xffffffffull);
   }
-  // ---- the run's counters: the last partition's look-back prefix, or (ex.reserve) the
-  // reservation word's total, read by the last workgroup to finish ----
+  // ---- the run's counters: the last partition's look-back prefix ----
   auto publish_totals = [&](u32 u, u64 total, u64 ovf_total) {
     ctr->num_unique = u;
     ctr->total_count = total;
@@ -1789,7 +1740,7 @@ __device__ __forceinline__ void ordered_partition(
     }
   };
   const u64 ovf_total = ovf_before + (any_full ? 1u : 0u);  // uniform per workgroup
-  if (!ex.reserve && v == kDictParts - 1 && threadIdx.x == 0)
+  if (v == kDictParts - 1 && threadIdx.x == 0)
     publish_totals((u32)(base_m + m), base_tok + tok, ovf_total);
   if (ex.self_clean) {
     // Self-cleaning job: the LAST workgroup to finish (not partition 255 -- a partition
@@ -1813,14 +1764,7 @@ __device__ __forceinline__ void ordered_partition(
     if (s_count) {
       // acquire every other workgroup's (acquire only: this one released its own already)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (ex.reserve) {  // every workgroup has added its aggregate: the run's totals
-        const u64 tot = __hip_atomic_load(&status[kDictParts], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-        const u64 ovf = (tot >> kOrdOvfShift) & 511u;
-        if (threadIdx.x == 0) publish_totals((u32)(tot & kOrdM), tot >> kOrdTokShift, ovf);
-        if (ovf) flags |= kCtrDictOverflow;
-      }
+      const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // Tell the host first: every workgroup's records, counters and headers are out (each
       // released them before counting itself done).  The re-zeroing below touches device
       // scratch only, which the next job's kernels -- behind this one on the stream -- see
@@ -1844,10 +1788,6 @@ __device__ __forceinline__ void ordered_partition(
           *ex.map_lb.tile_counter = 0;
           *ex.done_counter = 0;
           if (ex.plan_flag) *ex.plan_flag = 0;
-          if (ex.fuse) {  // the fused kernel's ticket and tiles-done counters
-            ex.fuse[0] = 0;
-            ex.fuse[1] = 0;
-          }
         }
       }
       __syncthreads();
@@ -1863,77 +1803,6 @@ __global__ __launch_bounds__(kPartBlock) void dict_ordered_kernel(
     OutRecord* __restrict__ out, MapCounters* __restrict__ ctr_out, u64* __restrict__ status,
     u32* __restrict__ tile_ctr, u64* __restrict__ trace, OrderedExtra ex) {
   ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, blockIdx.x);
-}
-
-// Map + ordered build of a small pass in ONE launch: kDictParts
-// workgroups, each first a map worker -- it claims 1 KiB tiles from a queue (fuse[0]) and
-// maps them (maptile::map_tile: tokens, tags, the tile's row of the partition table) until
-// the queue is empty, then releases its tiles once and counts them (fuse[1]) -- and then
-// one of the ordered kernel's partition workgroups, which waits until every tile is
-// counted.  A workgroup waits only once the queue is empty, i.e. once every tile is held by
-// a running workgroup, so the wait always ends (no dependence on dispatch order or on other
-// kernels sharing the GPU).  Roles by ticket over ntiles + kDictParts workgroups (the first
-// version) put the tiles wherever the ticket race put them: one workgroup per CU (the
-// ordered kernel's LDS), so XCDs that drew few tiles filled with waiting partitions and
-// ~60 partitions dispatched only after the first ones finished (trace: last entries at
-// 41 us of a 51 us kernel).  The fused path takes passes of at most kFuseMaxTiles tiles.
-// fuse[0]: tile queue, fuse[1]: tiles done (the ordered kernel's self-clean re-zeroes both).
-__global__ __launch_bounds__(kPartBlock) void map_ordered_kernel(
-    const char* __restrict__ text, u64 bytes, maptile::Delims d, int E, int max_key,
-    KeysSoA tokens, u8* __restrict__ parts, u64 out_cap, PartMap pm, u32* __restrict__ part_occ,
-    TileSource src, MapCounters* __restrict__ ctr, OutRecord* __restrict__ out,
-    MapCounters* __restrict__ ctr_out, u64* __restrict__ status, u32* __restrict__ tile_ctr,
-    u64* __restrict__ trace, OrderedExtra ex) {
-  __shared__ u32 s_ticket;
-  __shared__ maptile::MapTileLds<1, kPartBlock> lds;
-  u32* fuse = ex.fuse;
-  // diagnostics (LOCUST_ORD_TRACE): tile t's start / body end / counted at
-  // trace[t * 32 + 21 / 23 / 22]
-  const u64 rt0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  u32 mapped = 0, first = 0;
-  for (;;) {
-    if (threadIdx.x == 0) s_ticket = atomicAdd(&fuse[0], 1u);
-    __syncthreads();
-    const u32 t = s_ticket;
-    __syncthreads();  // every thread has read the ticket before the next claim
-    if (t >= src.ntiles) break;
-    const u64 rt1 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
-    maptile::map_tile<1, kPartBlock, true>(lds, t, text, bytes, d, E, max_key, tokens, parts, out_cap, ctr,
-                                     nullptr, const_cast<u32*>(src.part_off), pm, nullptr,
-                                     part_occ);
-    __syncthreads();  // the tile's LDS is free; every wave's stores are issued
-    if (trace && threadIdx.x == 0 && t < kDictParts) {
-      trace[(u64)t * 32 + 21] = rt1;
-      trace[(u64)t * 32 + 23] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (!mapped) first = t;
-    ++mapped;
-  }
-  if (threadIdx.x == 0) {
-    if (mapped) {
-      // the tiles' tokens and table rows went out as agent-scope stores (through the L2):
-      // once they are complete (the workgroup-scope release waits for every store of this
-      // workgroup -- the barrier above ordered the other waves' before it) the tiles count
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      atomicAdd(&fuse[1], mapped);
-      if (trace && first < kDictParts) trace[(u64)first * 32 + 22] = __builtin_amdgcn_s_memrealtime();
-    }
-    // bounded (~1 s): a wait that cannot end marks the run as overflowed instead -- the host
-    // then redoes the Process stage from the tokens after the stream has drained.  Relaxed
-    // polls (an acquire per poll invalidates the L2 the map tiles are using: measured 90 us
-    // fused kernels), then one acquire once every tile is counted.
-    u32 spins = 0;
-    while (__hip_atomic_load(&fuse[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < src.ntiles) {
-      __builtin_amdgcn_s_sleep(8);
-      if (++spins == (1u << 22)) {
-        atomicOr(&ctr->flags, kCtrDictOverflow);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  ordered_partition(src, ctr, out, ctr_out, status, tile_ctr, trace, ex, ~0u, rt0 | 1u);
 }
 
 // rank[i] += #{ j in tile : key[j] < key[i] }, persistent over (i-tile, j-tile) pairs.
@@ -2185,23 +2054,6 @@ void launch_dict_ordered(ConstKeysSoA tokens, const u64* counts, const u8* parts
     dict_ordered_kernel<TagSource><<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
         src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   }
-  LOCUST_HIP_LAUNCH_CHECK();
-}
-
-void launch_map_ordered(const char* text, u64 bytes, const DelimMask& dm, int emits_per_line,
-                        int max_key_len, KeysSoA tokens, u8* parts, u64 cap, MapCounters* ctr,
-                        PartMap pm, OutRecord* out, MapCounters* ctr_out, LookbackScratch lb,
-                        hipStream_t s, u64* trace, const OrderedExtra& ex) {
-  LOCUST_CHECK_ARG(ex.fuse && ex.part_off && ex.part_tiles &&
-                       ex.part_tiles == div_up(bytes, (u64)kMapTileBytesMin) &&
-                       ex.part_tiles <= (u64)kFuseMaxTiles && bytes > 0,
-                   "fused map + ordered: a small pass with its partition table");
-  const maptile::Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
-  const TileSource src{ConstKeysSoA{{tokens.w[0], tokens.w[1], tokens.w[2], tokens.w[3]}},
-                       ex.part_off, ex.part_tiles, (u32)std::min<u64>(cap, 0xFFFFFFFFu)};
-  map_ordered_kernel<<<dim3(kDictParts), dim3(kPartBlock), 0, s>>>(
-      text, bytes, d, emits_per_line, max_key_len, tokens, parts, cap, pm,
-      const_cast<u32*>(ex.part_occ), src, ctr, out, ctr_out, lb.status, lb.tile_counter, trace, ex);
   LOCUST_HIP_LAUNCH_CHECK();
 }
 

@@ -169,20 +169,9 @@ struct MapTileLds {
   u32 list[(kBlock / 64) * kListPerWave];
 };
 
-// One map tile (the body of map_fast_kernel): kBlock threads, tile index `tile` -- the
-// block index of map_fast_kernel, or a ticket of the fused map + ordered kernel (dict.hip).
-// A store of the map's output.  kWT (the fused kernel): agent-scope atomic stores, written
-// through this XCD's L2, so the tile needs no L2 write-back before it is counted (an
-// agent-scope release fence per tile cost 3-12 us of buffer_wbl2, measured).
-template <bool kWT, class T>
-__device__ __forceinline__ void map_store(T* p, T v) {
-  if constexpr (kWT)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = v;
-}
-
-template <int kSteps, int kBlock, bool kWT = false>
+// One map tile (the body of map_fast_kernel): kBlock threads, tile index `tile` (the
+// XCD-ordered block index of map_fast_kernel).
+template <int kSteps, int kBlock>
 __device__ __forceinline__ void map_tile(
     MapTileLds<kSteps, kBlock>& lds, const u32 tile, const char* __restrict__ text, u64 bytes,
     const Delims& d, int E, int max_key, KeysSoA out, u8* __restrict__ parts, u64 out_cap,
@@ -348,7 +337,7 @@ __device__ __forceinline__ void map_tile(
           occ |= (u32)__shfl_xor((int)occ, 1, 64);
           occ |= (u32)__shfl_xor((int)occ, 2, 64);
           occ |= (u32)__shfl_xor((int)occ, 4, 64);
-          if ((l & 7) == 0) map_store<kWT>(&part_occ[(u64)tile * kPartOccWords + (l >> 3)], occ);
+          if ((l & 7) == 0) part_occ[(u64)tile * kPartOccWords + (l >> 3)] = occ;
         }
         const u32 sum4 = h0 + h1 + h2 + h3;
         const u32 inc = dev::wave_inclusive_scan(sum4);
@@ -364,7 +353,7 @@ __device__ __forceinline__ void map_tile(
       const u64 prefix = s_prefix;
       MAP_STAMP(4);
       for (int i = threadIdx.x; i < kPartTable; i += kBlock)
-        map_store<kWT>(&part_off[(u64)tile * kPartTable + i], (u32)(prefix + s_pcnt[i]));
+        part_off[(u64)tile * kPartTable + i] = (u32)(prefix + s_pcnt[i]);
       u32 trunc = 0, maxlen = 0;
       if (em) {
         const u64 idx = prefix + s_pcnt[part] + loc;
@@ -372,8 +361,8 @@ __device__ __forceinline__ void map_tile(
         maxlen = len;
         if (idx < out_cap) {
 #pragma unroll
-          for (int j = 0; j < kKeyWords; ++j) map_store<kWT>(&out.w[j][idx], kw[j]);
-          if (parts) map_store<kWT>(&parts[idx], (u8)part);
+          for (int j = 0; j < kKeyWords; ++j) out.w[j][idx] = kw[j];
+          if (parts) parts[idx] = (u8)part;
         }
       }
       trunc = dev::wave_reduce_sum(trunc);

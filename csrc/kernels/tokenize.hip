@@ -39,9 +39,10 @@ __global__ __launch_bounds__(kBlock) void map_fast_kernel(
     const char* __restrict__ text, u64 bytes, Delims d, int E, int max_key, KeysSoA out,
     u8* __restrict__ parts, u64 out_cap, MapCounters* __restrict__ ctr, u64* __restrict__ trace,
     u32* __restrict__ part_off, PartMap pm, u64* __restrict__ counts, u32* __restrict__ part_occ,
-    u32 xcd_order, u32* __restrict__ plan_flag) {
+    u32* __restrict__ plan_flag) {
   __shared__ MapTileLds<kSteps, kBlock> lds;
-  const u32 tile = xcd_order ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  // consecutive tiles per XCD: neighbouring tiles share L2 lines of the text and tables
+  const u32 tile = xcd_tile(blockIdx.x, gridDim.x);
   map_tile<kSteps, kBlock>(lds, tile, text, bytes, d, E, max_key, out, parts, out_cap, ctr,
                            trace, part_off, pm, counts, part_occ, plan_flag);
 }
@@ -55,12 +56,6 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
                      u32* plan_flag) {
   if (bytes == 0) return;
   const Delims d{dm.m[0] | 1ull | (1ull << '\n'), dm.m[1], dm.m[2], dm.m[3]};
-  // LOCUST_MAP_XCD=0 (A/B, read at the first launch): tiles in block order instead of
-  // consecutive tiles per XCD (xcd_tile)
-  static const u32 xcd_order = [] {
-    const char* e = std::getenv("LOCUST_MAP_XCD");
-    return e && e[0] == '0' ? 0u : 1u;
-  }();
   if (bytes < kMapLargeInput && !large_tiles) {
     // Small inputs: 1 KiB tiles as 16 waves x ONE 64-byte step -- the same text per
     // workgroup (and the same PCIe reads), the least serial work per wave.  Measured A/B
@@ -70,13 +65,13 @@ void launch_map_fast(const char* text, u64 bytes, const DelimMask& dm, int emits
     constexpr int kBlock = kMapTileBytesMin;  // one byte per lane: 16 waves of 64 lanes
     map_fast_kernel<1, kBlock><<<dim3((u32)tiles), dim3(kBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, trace, part_off, pm,
-        nullptr, part_off ? part_occ : nullptr, xcd_order, part_off && part_occ ? plan_flag : nullptr);
+        nullptr, part_off ? part_occ : nullptr, part_off && part_occ ? plan_flag : nullptr);
   } else {
     constexpr int kTile = (kMapBlock / 64) * kMapSegStepsLarge * 64;
     const u64 tiles = div_up(bytes, (u64)kTile);
     map_fast_kernel<kMapSegStepsLarge, kMapBlock><<<dim3((u32)tiles), dim3(kMapBlock), 0, s>>>(
         text, bytes, d, emits_per_line, max_key_len, out, parts, out_cap, ctr, trace, part_off, pm,
-        part_off ? counts : nullptr, nullptr, xcd_order, nullptr);
+        part_off ? counts : nullptr, nullptr, nullptr);
   }
   LOCUST_HIP_LAUNCH_CHECK();
 }

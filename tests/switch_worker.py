@@ -26,8 +26,10 @@ def main(kind: str) -> None:
     # ~2.6 MB of synthetic text: a one-pass "large" input (piecewise upload, partials build)
     synth = lc.gen_text(lines=60_000, seed=7)
     if kind == "single":
+        # 5x Hamlet (~0.94 MiB): past 2^18 worst-case tokens, within LOCUST_SMALL_PASS_KB --
+        # the small-pass route (or, with it off, the large build) of the one-pass engine
         for text, what in ((hamlet, "hamlet"), (oracle.window(hamlet, 0, 700), "hamlet700"),
-                           (synth, "synth")):
+                           (hamlet * 5, "hamlet5x"), (synth, "synth")):
             eng = lc.Engine(lc.make_config("gpu"), len(text), text.count(b"\n") + 1)
             for j in range(3):  # first job, retuned job, steady job
                 check(eng.run(text), text, f"{what} job {j}")

@@ -15,8 +15,6 @@ WORKER = os.path.join(ROOT, "tests", "switch_worker.py")
 # (environment, workload).  Each switch appears at least once with a non-default value.
 CASES = [
     ({"LOCUST_CHECK": "1"}, "single"),
-    ({"LOCUST_COMPACT_OUT": "0"}, "single"),
-    ({"LOCUST_FUSE": "1"}, "single"),
     ({"LOCUST_MAP_PATH": "compat"}, "single"),
     ({"LOCUST_SORT": "radix", "LOCUST_REDUCE_PATH": "global"}, "single"),
     ({"LOCUST_SORT": "radix", "LOCUST_PSORT": "0"}, "single"),
@@ -30,12 +28,8 @@ CASES = [
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PART_DEFAULT": "byte"}, "single"),
     ({"LOCUST_VPLAN": "0", "LOCUST_DEVPLAN": "0"}, "single"),
     ({"LOCUST_VPLAN_MIN_KB": "64", "LOCUST_SPLIT_MIN": "256"}, "single"),
-    ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FUSED": "0", "LOCUST_RANK_W0": "0",
-      "LOCUST_PLAN_TRIGGER": "0"}, "single"),
-    ({"LOCUST_PART_TUNE": "0", "LOCUST_SPLIT_FLOOR": "512", "LOCUST_SMALL_TABLE": "0"}, "single"),
-    ({"LOCUST_ORD_RESERVE": "1", "LOCUST_EARLY_PUBLISH": "0"}, "single"),
-    ({"LOCUST_MAP_XCD": "0", "LOCUST_SMALL_PASS_KB": "0"}, "single"),
-    ({"LOCUST_ORD_RESERVE": "1", "LOCUST_FUSE": "1", "LOCUST_PART_TUNE": "0"}, "single"),
+    ({"LOCUST_PART_TUNE": "0", "LOCUST_PLAN_TRIGGER": "0"}, "single"),
+    ({"LOCUST_SMALL_PASS_KB": "0"}, "single"),
     ({"LOCUST_DEV_CACHE": "0"}, "stream"),
     ({"LOCUST_DEV_CACHE_GB": "1", "LOCUST_CHUNK_MB": "1"}, "stream"),
     ({"LOCUST_ORD_TRACE": "1", "LOCUST_MAP_TRACE": "1", "LOCUST_ROCTX": "0",
