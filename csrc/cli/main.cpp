@@ -39,6 +39,21 @@ namespace {
 
 unsigned long long peak_rss_kb();
 
+// A one-shot GPU run ends with _exit once its output is flushed (the
+// HIP runtime's teardown -- streams, pinned and device memory, code objects -- took most of
+// the ~80 ms outside main()).  Off with LOCUST_FAST_EXIT=0, and under a profiler (rocprofv3
+// preloads its tool library and flushes its traces at the runtime's exit).
+bool fast_exit_ok() {
+  if (const char* e = std::getenv("LOCUST_FAST_EXIT"))
+    if (e[0] == '0') return false;
+  if (const char* p = std::getenv("LD_PRELOAD"))
+    if (std::strstr(p, "rocprof") || std::strstr(p, "roctracer")) return false;
+  for (char** e = environ; e && *e; ++e)
+    if (std::strncmp(*e, "ROCPROF", 7) == 0) return false;
+  return true;
+}
+bool g_fast_exit = false;  // run() left its GPU state for the process exit to reclaim
+
 struct CliArgs {
   std::string file;
   i64 line_start = -1, line_end = -1;
@@ -382,6 +397,11 @@ void write_json(const CliArgs& a, const WordCountResult& r, const std::vector<do
     st.num("later_jobs_ms", ms(t.first, t.jobs));
     st.num("output_ms", ms(t.jobs, end));
     st.num("main_to_json_ms", ms(t.main, end));
+    // before main(): the loader and the libraries' static initialisation, split at this
+    // library's own (LOCUST_T0: the spawner's CLOCK_MONOTONIC ns, tools/cli_cold.py)
+    st.num("library_to_main_ms", ms(library_init_ns(), t.main));
+    if (const char* t0 = std::getenv("LOCUST_T0"))
+      st.num("spawn_to_library_ms", ms((u64)std::strtoull(t0, nullptr, 10), library_init_ns()));
     j.kv("startup", st.done());
   }
   emit_json(a, j.done());
@@ -628,6 +648,13 @@ int run_direct(const CliArgs& a) {
   const u64 t_down = now_ns();
   std::vector<u64> lo;
   if (!pmc.empty() && eng->partition_map(&lo) && lo != cached) save_partmap_cache(pmc, lo);
+  if (fast_exit_ok()) {
+    // the process ends right after this (main: _exit): the driver reclaims the engine's
+    // queues and memory with the process -- no per-buffer teardown
+    (void)eng.release();
+    g_fast_exit = true;
+    return 0;
+  }
   eng.reset();
   LOCUST_LOG_DEBUG("engine teardown %.3f ms", (now_ns() - t_down) * 1e-6);
   return 0;
@@ -865,7 +892,12 @@ int main(int argc, char** argv) {
       usage();
       return -1;
     }
-    return run(a);
+    const int rc = run(a);
+    if (rc == 0 && (g_fast_exit || (a.cfg.backend == Backend::kGpu && fast_exit_ok()))) {
+      std::fflush(nullptr);
+      _exit(0);  // skip the HIP runtime's teardown (fast_exit_ok)
+    }
+    return rc;
   } catch (const std::exception& e) {
     std::fflush(stdout);
     std::fprintf(stderr, "MapReduce: error: %s\n", e.what());

@@ -86,6 +86,11 @@ bool fault_injected(int rank, const char* stage) {
   return what == stage;
 }
 
+namespace {
+const u64 g_library_init_ns = now_ns();
+}  // namespace
+u64 library_init_ns() { return g_library_init_ns; }
+
 u64 now_ns() {
   return (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())

@@ -67,6 +67,9 @@ u64 stages_entered();
 
 // Monotonic host clock in nanoseconds.
 u64 now_ns();
+// now_ns() when this library's static initialisation ran (the process's start-up split:
+// loader + the HIP runtime's static init before it, the rest of static init after).
+u64 library_init_ns();
 // Resident host memory of this process, kB: VmRSS (peak = false) or VmHWM (peak = true).
 u64 process_rss_kb(bool peak = false);
 // "rss N kB (anon A, file F, shmem S; peak P)" from /proc/self/status (debug logs)

@@ -101,9 +101,11 @@ def reduce_stage(spills: list[str], reducer: int = 0, reducers: int = 1,
 def run_multi(text: bytes, world: int, backend: str = "gpu", combine: bool = True,
               samples_per_rank: int = 64, strategy: str | None = None, comm: str = "auto",
               **kw):
-    """Multi-rank WordCount in this process, one thread per rank.  comm="auto": an RCCL
-    clique (ncclCommInitAll over xGMI) when every rank has a GPU of its own, else the
-    loopback communicator (device copies; rehearses N ranks on fewer GPUs)."""
+    """Multi-rank WordCount in this process, one thread per rank.  comm="auto" (and
+    "loopback"): the loopback communicator -- ranks exchange by peer-to-peer device copies
+    (over xGMI when the ranks' GPUs differ; rehearses N ranks on fewer GPUs).  comm="rccl":
+    an RCCL clique (ncclCommInitAll), one GPU per rank -- opt-in until a run with real RCCL
+    peers has been recorded (csrc/engine/dist_runner.hip resolve_local_comm)."""
     dcfg = make_dist_config(world, make_config(backend, combine=combine, **kw),
                             samples_per_rank=samples_per_rank, strategy=strategy)
     return _C.run_multi(text, dcfg, comm)

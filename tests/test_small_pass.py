@@ -19,13 +19,13 @@ def _inputs(hamlet: bytes):
     rng = random.Random(17)
     yield "hamlet3x", hamlet * 3
     yield "hamlet5x", hamlet * 5
-    yield "one_key", b"\n".join(b" ".join([b"the"] * 10) for _ in range(80_000)) + b"\n"
+    yield "one_key", b"\n".join(b" ".join([b"the"] * 10) for _ in range(20_000)) + b"\n"
     alpha = b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ"
     words = {bytes(rng.choice(alpha) for _ in range(rng.randrange(4, 12))) for _ in range(90_000)}
     words = sorted(words)
     rng.shuffle(words)
     yield "random_distinct", b"\n".join(b" ".join(words[i:i + 8]) for i in range(0, len(words), 8)) + b"\n"
-    crowd = [b"w%06d" % i for i in range(60_000)]  # every key in one starting-map partition
+    crowd = [b"w%06d" % i for i in range(120_000)]  # every key in one starting-map partition
     yield "crowded", b"\n".join(b" ".join(crowd[i:i + 10]) for i in range(0, len(crowd), 10)) + b"\n"
 
 

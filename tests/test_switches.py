@@ -25,6 +25,7 @@ CASES = [
     ({"LOCUST_MERGE_MAX_RECORDS": "100"}, "merge"),
     ({"LOCUST_CACHE_DIR": "", "LOCUST_PART_CACHE": "1"}, "cli"),
     ({"LOCUST_PART_CACHE": "0"}, "cli"),
+    ({"LOCUST_FAST_EXIT": "0"}, "cli"),
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PART_DEFAULT": "byte"}, "single"),
     ({"LOCUST_VPLAN": "0", "LOCUST_DEVPLAN": "0"}, "single"),
     ({"LOCUST_VPLAN_MIN_KB": "64", "LOCUST_SPLIT_MIN": "256"}, "single"),
@@ -51,7 +52,8 @@ def test_every_switch_has_a_case():
                                        open(os.path.join(d, f), errors="replace").read()))
     covered = {k for env, _ in CASES for k in env} | {
         "LOCUST_FAULT",        # test_dist*.py, test_scale_ready.py
-        "LOCUST_LINE_CACHE"}   # test_line_index.py
+        "LOCUST_LINE_CACHE",   # test_line_index.py
+        "LOCUST_T0"}           # tools/cli_cold.py (timestamps only)
     assert used and not sorted(used - covered)
 
 

@@ -4,7 +4,7 @@ one fresh process per variant, in alternating order, each timing `--steps` jobs 
 `--warmup` on a fresh engine (bench._time_single); prints per-variant medians over rounds.
 
     python tools/ab_procs.py "LOCUST_PART_TUNE=0" "LOCUST_PART_TUNE=0,LOCUST_PART_DEFAULT=letters" \\
-        [--config hamlet4500|hamlet700|synth1m] [--rounds 5] [--steps 300] [--warmup 30]
+        [--config hamlet4500|hamlet700|synth1m|file:PATH] [--rounds 5] [--steps 300] [--warmup 30]
 
 A variant's ROOT=<dir> runs it from another built tree (e.g. a previous commit exported
 with `git archive` and built with make): code changes without a switch of their own.
@@ -23,7 +23,10 @@ import json, sys, time
 sys.path.insert(0, sys.argv[1])
 import bench
 cfg, steps, warmup, rep = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
-text = bench.synth_shard(cfg, 0, 1) if cfg in bench.SYNTH else bench.load_text(cfg) * rep
+if cfg.startswith("file:"):
+    text = open(cfg[5:], "rb").read() * rep
+else:
+    text = bench.synth_shard(cfg, 0, 1) if cfg in bench.SYNTH else bench.load_text(cfg) * rep
 first = bench.cold_first_run(text)["first_job_ms"]
 ms, _st, res = bench._time_single(text, steps, warmup, "dict", -1)
 print(json.dumps({"ms": ms, "first": first, "unique": res.num_unique}))
