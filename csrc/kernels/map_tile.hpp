@@ -1,5 +1,5 @@
-// The fast map's tile (Map stage): shared by map_fast_kernel (tokenize.hip) and the fused
-// map + ordered kernel (dict.hip).  See tokenize.hip for the algorithm.
+// The fast map's tile (Map stage): the body of map_fast_kernel (tokenize.hip).  See
+// tokenize.hip for the algorithm.
 #pragma once
 
 #include "locust/device/hash.hpp"
@@ -142,6 +142,21 @@ __device__ __forceinline__ u32 xcd_tile(u32 b, u32 G) {
   return x * q + (x < r ? x : r) + k;
 }
 
+// The partition map's range starts in LDS, skewed: entry i at i + (i >> 5).  A binary
+// search's lanes read entries 2^k apart -- without the skew every such entry of a level
+// sits on the same ds_read_b64 bank ((a/4) mod 64: entries 32 apart share one), up to
+// 4-way conflicts per level (0.18 of the map's LDS cycles); with it the
+// entries of any level fall on distinct banks.
+constexpr int kPloSkewed = kDictParts + 1 + ((kDictParts + 1) >> 5) + 1;
+__device__ __forceinline__ int plo_at(int i) { return i + (i >> 5); }
+__device__ __forceinline__ u32 part_of_w0_skewed(const u64* s_plo, u64 w0) {
+  u32 p = 0;
+#pragma unroll
+  for (u32 step = kDictParts / 2; step; step >>= 1)
+    if (s_plo[plo_at((int)(p + step))] <= w0) p += step;
+  return p;
+}
+
 // The tile's LDS, declared __shared__ by the calling kernel and passed in: LDS variables
 // declared inside a device function are lowered to module scope, where every kernel of the
 // file that reaches any instantiation pays for all of them (map_fast_kernel<1, 1024> grew
@@ -162,8 +177,9 @@ struct MapTileLds {
   // one word) of each partition claims a slot; its repeats in the tile become one record
   u64 hot[kCombineTile ? kDictParts : 1];
   u32 hotc[kCombineTile ? kDictParts : 1];
-  // the partition map's range starts (PartMap), staged once per tile: 2 KB, searched per token
-  u64 plo[kDictParts + 1];
+  // the partition map's range starts (PartMap), staged once per tile (skewed: plo_at), 2 KB,
+  // searched per token
+  u64 plo[kPloSkewed];
   // grouped large tiles: each wave's token starts (LDS offset | length << 16), at most one
   // per two bytes of its segment
   u32 list[(kBlock / 64) * kListPerWave];
@@ -214,9 +230,11 @@ __device__ __forceinline__ void map_tile(
     }
 
   if (pm.lo)  // visible after the staging barrier below
-    for (int i = threadIdx.x; i <= kDictParts; i += kBlock) s_plo[i] = pm.lo[i];
+    for (int i = threadIdx.x; i <= kDictParts; i += kBlock) s_plo[plo_at(i)] = pm.lo[i];
   // Partition of a packed key: binary search of its first word (default: first byte).
-  auto part_of = [&](u64 w0) -> u32 { return pm.lo ? part_of_w0(s_plo, w0) : (u32)(w0 >> 56); };
+  auto part_of = [&](u64 w0) -> u32 {
+    return pm.lo ? part_of_w0_skewed(s_plo, w0) : (u32)(w0 >> 56);
+  };
 
   // ---- stage the tile (+ context) into LDS with 16-B loads ----
   const i64 tile_base = (i64)tile * kTile;

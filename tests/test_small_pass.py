@@ -46,7 +46,10 @@ def test_small_pass_route_matches_oracle(hamlet, monkeypatch, small_pass_kb):
             assert r.num_tokens == ntok, (name, j)
             assert r.entries() == ent, f"{name} job {j}: entries differ from the oracle"
         st = eng.stats()
-        # a fallback redoes the job on the HBM table (still exact, above); the one-key and
-        # Hamlet inputs never need one
-        if name in ("hamlet3x", "hamlet5x", "one_key"):
+        # a fallback redoes the job on the HBM table (still exact, above).  Hamlet never
+        # needs one; one key repeated 200,000 times is one partition past the LDS token
+        # window in every job, whatever the plan (all its quantile cuts are the same key)
+        if name.startswith("hamlet"):
             assert st["fallbacks"] == 0, (name, st)
+        if name == "one_key":
+            assert st["fallbacks"] == 3, (name, st)
