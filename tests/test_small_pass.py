@@ -24,9 +24,9 @@ def _inputs(hamlet: bytes):
     words = {bytes(rng.choice(alpha) for _ in range(rng.randrange(4, 12))) for _ in range(90_000)}
     words = sorted(words)
     rng.shuffle(words)
-    yield "random_distinct", b"\n".join(b" ".join(words[i:i + 8]) for i in range(0, len(words), 8)) + b"\n"
+    yield "random_distinct", b"\n".join(b" ".join(words[i:i + 4]) for i in range(0, len(words), 4)) + b"\n"
     crowd = [b"w%06d" % i for i in range(120_000)]  # every key in one starting-map partition
-    yield "crowded", b"\n".join(b" ".join(crowd[i:i + 10]) for i in range(0, len(crowd), 10)) + b"\n"
+    yield "crowded", b"\n".join(b" ".join(crowd[i:i + 5]) for i in range(0, len(crowd), 5)) + b"\n"
 
 
 @pytest.mark.parametrize("small_pass_kb", [None, "0"])
@@ -47,9 +47,11 @@ def test_small_pass_route_matches_oracle(hamlet, monkeypatch, small_pass_kb):
             assert r.entries() == ent, f"{name} job {j}: entries differ from the oracle"
         st = eng.stats()
         # a fallback redoes the job on the HBM table (still exact, above).  Hamlet never
-        # needs one; one key repeated 200,000 times is one partition past the LDS token
-        # window in every job, whatever the plan (all its quantile cuts are the same key)
+        # needs one.  One key repeated 200,000 times: on the small-pass route it is one
+        # partition past the LDS token window in every job, whatever the plan (all its
+        # quantile cuts are the same key); the large build's per-tile combining folds it
+        # into one record per tile first, so it never falls back
         if name.startswith("hamlet"):
             assert st["fallbacks"] == 0, (name, st)
         if name == "one_key":
-            assert st["fallbacks"] == 3, (name, st)
+            assert st["fallbacks"] == (3 if small_pass_kb is None else 0), (name, st)
