@@ -19,28 +19,20 @@ void part_map_default_first_byte(PartMapTables* t) {
 // letter far more often than with any other byte, so the letters get several partitions
 // each, cut on the second byte: lowercase four ([.., 'g'), ['g', 'n'), ['n', 't'),
 // ['t', ..)), uppercase three (ALL-CAPS words / [a-m] / [n-z] second letters); digits and
-// every UTF-8 lead byte (0xC2-0xF4) one each; the remaining byte ranges one each; the 'th'
-// words three more and the 'co' words two more (below).  253 partitions (asserted below);
-// the rest stay empty.  A first-byte map left ~50 of the 256 partitions
-// occupied on English text, so the ordered kernel split the hot letters across sibling
-// workgroups that each scan the whole letter's tokens (whole Hamlet: ordered kernel 28.1
-// vs 22.1 us with a tuned map, profiles/r3_s4/).  Data-independent: no input is sampled.
+// every UTF-8 lead byte (0xC2-0xF4) one each; the remaining byte ranges one each.  248
+// partitions (asserted below); the rest stay empty.  A first-byte map left ~50 of the 256
+// partitions occupied on English text, so the ordered kernel split the hot letters across
+// sibling workgroups that each scan the whole letter's tokens (whole Hamlet: ordered
+// kernel 28.1 vs 22.1 us with a tuned map, profiles/r3_s4/).  Data-independent: no input
+// is sampled.  Round 5 added third-byte cuts fitted to Hamlet ('th', 'co' words); on 7
+// held-out texts they were 0.998-1.040x the plain letters map and helped only the fixture
+// (profiles/r6/partmap/heldout.md), so round 6 removed them.  The letters map beat the
+// first-byte map on 7 of the 8 texts there (LOCUST_PART_DEFAULT=byte keeps that A/B).
 void part_map_default(PartMapTables* t) {
   if (const char* e = std::getenv("LOCUST_PART_DEFAULT"); e && e[0] == 'b')  // A/B: "byte"
     return part_map_default_first_byte(t);
   std::vector<u64> lo;
   auto cut = [&](u32 b0, u32 b1) { lo.push_back(((u64)b0 << 56) | ((u64)b1 << 48)); };
-  auto cut3 = [&](u32 b0, u32 b1, u32 b2) {
-    lo.push_back(((u64)b0 << 56) | ((u64)b1 << 48) | ((u64)b2 << 40));
-  };
-  // The 'th' words -- English's most frequent digram and word (the, that, this, thou, ...;
-  // 2,525 of Hamlet's 32,940 tokens in one ['tg', 'tn') partition, the untuned job's
-  // critical path) -- are cut on their third byte as well: [th, the), [the, thf),
-  // [thf, tho), [tho, tn); and the 'co' words (com-, con-: the two-letter prefix with the
-  // most distinct English words; 209 of Hamlet's 5,608 keys in ['cn', 'ct'), whose ranking
-  // then led the kernel) at 'com' and 'cop'.  LOCUST_PART_DEFAULT=letters: without (A/B).
-  const char* dv = std::getenv("LOCUST_PART_DEFAULT");
-  const bool th = !(dv && dv[0] == 'l');
   cut(0x00, 0);    // controls, space, punctuation before the digits
   for (u32 d = '0'; d <= '9'; ++d) cut(d, 0);
   cut(0x3A, 0);    // :;<=>?@
@@ -53,22 +45,13 @@ void part_map_default(PartMapTables* t) {
   for (u32 c = 'a'; c <= 'z'; ++c) {
     cut(c, 0);
     cut(c, 'g');
-    if (th && c == 't') {
-      cut3('t', 'h', 'e');
-      cut3('t', 'h', 'f');
-      cut3('t', 'h', 'o');
-    }
     cut(c, 'n');
-    if (th && c == 'c') {  // com- / con-: the English prefix with the most distinct words
-      cut3('c', 'o', 'm');
-      cut3('c', 'o', 'p');
-    }
     cut(c, 't');
   }
   cut(0x7B, 0);    // {|}~ DEL, UTF-8 continuation bytes, C0/C1
   for (u32 b = 0xC2; b <= 0xF4; ++b) cut(b, 0);
   cut(0xF5, 0);    // bytes no UTF-8 text starts with
-  LOCUST_CHECK_ARG(lo.size() == (th ? 253u : 248u) && lo.size() <= (size_t)kDictParts,
+  LOCUST_CHECK_ARG(lo.size() == 248u && lo.size() <= (size_t)kDictParts,
                    "default partition map: unexpected partition count");
   for (u32 p = 0; p < (u32)kDictParts; ++p) t->lo[p] = p < lo.size() ? lo[p] : ~0ull;
   t->lo[kDictParts] = ~0ull;

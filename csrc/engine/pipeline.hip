@@ -1704,7 +1704,9 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
   const u64 piece = std::min<u64>(cap_bytes, cfg.ring_piece_bytes ? cfg.ring_piece_bytes : kRingPieceMax);
   // a map window closes before a piece would overflow it: windows >= map_window - piece
   const u64 min_window = map_window > piece ? map_window - piece : std::max<u64>(map_window / 2, 1);
+  const u64 t_setup = now_ns();
   ensure_stream_buffers(false, div_up(std::max<u64>(src_text.size(), 1), min_window) + 2);
+  const u64 t_bufs = now_ns();
   reset_window_counters();
   if (ring_piece != piece) {
     for (int i = 0; i < kRingPieces; ++i) {
@@ -1714,6 +1716,9 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
     }
     ring_piece = piece;
   }
+  if ((int)log_level() >= (int)LogLevel::kDebug)
+    LOCUST_LOG_DEBUG("stream setup: copy stream / second chunk / counters %.2f ms, read ring %.2f ms",
+                     (t_bufs - t_setup) * 1e-6, (now_ns() - t_bufs) * 1e-6);
   const DelimMask dm = make_delim_mask(cfg.delimiters.c_str());
   LOCUST_HIP_CHECK(hipMemsetAsync(dict.table, 0, dict_zero_bytes, stream));
   LOCUST_HIP_CHECK(hipMemsetAsync(d_dctr, 0, sizeof(MapCounters), stream));

@@ -51,25 +51,21 @@ def test_large_vocabulary_respects_distinct_cap():
 
 
 def test_default_map_for_empty_input():
-    """The starting map: ascending ranges, letters split on their second byte (the 'th'
-    words on their third as well), digits and UTF-8 lead bytes one partition each, the
-    empty tail past the last range."""
+    """The starting map: ascending ranges, letters split on their second byte, digits and
+    UTF-8 lead bytes one partition each, the empty tail past the last range.  No cuts
+    fitted to one text (round 6 removed Hamlet's 'th'/'co' third-byte cuts after they were
+    neutral on held-out inputs, profiles/r6/partmap/heldout.md)."""
     m = lc._C.part_map_build([])
     lo = m["lo"]
     assert m["predicted_max"] == 0 and lo[0] == 0 and len(lo) == 257
     used = [x for x in lo[:256] if x != (1 << 64) - 1]
-    assert used == sorted(used) and len(set(used)) == len(used) == 253
+    assert used == sorted(used) and len(set(used)) == len(used) == 248
     part = lambda k: lc._C.part_of_key(lo, k)  # noqa: E731
     # lowercase: four ranges per first letter, cut at the second letters g, n, t
-    assert len({part(b"a" + bytes([c])) for c in range(ord("a"), ord("z") + 1)}) == 4
-    # (two-byte 't' keys: "th" sorts before "the", "ti".."tm" after "tho": five ranges)
-    assert len({part(b"t" + bytes([c])) for c in range(ord("a"), ord("z") + 1)}) == 5
-    # 'th' words: [th, the) [the, thf) [thf, tho) [tho, tn)
-    assert part(b"tg") == part(b"than") == part(b"thd") < part(b"the") == part(b"they")
-    assert part(b"they") < part(b"this") == part(b"thin") < part(b"thou") == part(b"tm")
-    assert part(b"tea") < part(b"the") < part(b"to") < part(b"tu")
-    # 'co' words: [cn, com) [com, cop) [cop, ct)
-    assert part(b"cold") < part(b"come") == part(b"content") < part(b"court") < part(b"cu")
+    for c0 in b"act":
+        assert len({part(bytes([c0, c])) for c in range(ord("a"), ord("z") + 1)}) == 4
+    assert part(b"tg") == part(b"the") == part(b"thou") == part(b"tm") < part(b"to")
+    assert part(b"cold") == part(b"come") == part(b"court") < part(b"cu")
     assert part(b"ta") < part(b"tz") < part(b"ua")
     # uppercase: ALL-CAPS / [a-m] / [n-z] second bytes
     assert part(b"HAMLET") != part(b"Hamlet") != part(b"Horatio")

@@ -3,7 +3,7 @@ env_ab.py shares HW queues and caches between the variants' engines): every roun
 one fresh process per variant, in alternating order, each timing `--steps` jobs after
 `--warmup` on a fresh engine (bench._time_single); prints per-variant medians over rounds.
 
-    python tools/ab_procs.py "LOCUST_PART_TUNE=0" "LOCUST_PART_TUNE=0,LOCUST_PART_DEFAULT=letters" \\
+    python tools/ab_procs.py "LOCUST_PART_TUNE=0" "LOCUST_PART_TUNE=0,LOCUST_PART_DEFAULT=byte" \\
         [--config hamlet4500|hamlet700|synth1m|file:PATH] [--rounds 5] [--steps 300] [--warmup 30]
 
 A variant's ROOT=<dir> runs it from another built tree (e.g. a previous commit exported

@@ -1,10 +1,12 @@
 """The starting partition map on text it was not fitted to.
 
 The one-shot CLI's first job partitions the ordered build with a data-independent starting
-map (csrc/engine/partmap.cpp): the letters split on their second byte, plus third-byte cuts
-at 'th' / 'the' / 'tho' / 'co' words that round 5 chose by measuring Hamlet -- the
-benchmark fixture itself.  Here every map is timed on inputs none of them was fitted to,
-untuned (LOCUST_PART_TUNE=0: every job starts from the map, as a one-job process does):
+map (csrc/engine/partmap.cpp): the letters split on their second byte.  Round 5 had added
+third-byte cuts at 'th' / 'the' / 'tho' / 'co' words chosen by measuring Hamlet -- the
+benchmark fixture itself; this tool's first run (profiles/r6/partmap/heldout.md) timed
+them against the plain letters map on inputs none of the maps was fitted to, they did not
+help there, and round 6 removed them.  Every map is timed untuned (LOCUST_PART_TUNE=0:
+every job starts from the map, as a one-job process does) on:
 
   * synthetic text of Hamlet's size with other seeds, vocabularies and Zipf exponents
     (the native generator: English-like word lengths, Zipf-distributed ranks);
@@ -12,9 +14,8 @@ untuned (LOCUST_PART_TUNE=0: every job starts from the map, as a one-job process
     VERDICT.md, README.md, BASELINE.md), concatenated to Hamlet's size;
   * a different distribution altogether: the repository's Python sources.
 
-Variants (one fresh process each, alternating, tools/ab_procs.py): the default map,
-LOCUST_PART_DEFAULT=letters (the same letters map without the fitted third-byte cuts) and
-LOCUST_PART_DEFAULT=byte (first byte only).  Writes a table (markdown) to --out.
+Variants (one fresh process each, alternating, tools/ab_procs.py): the default (letters)
+map and LOCUST_PART_DEFAULT=byte (first byte only).  Writes a table (markdown) to --out.
 
     python tools/partmap_heldout.py --out profiles/r6/partmap/heldout.md [--rounds 3]
 """
@@ -31,8 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 HAMLET = 191_734
-VARIANTS = {"default (fitted cuts)": "LOCUST_PART_TUNE=0",
-            "letters (no fitted cuts)": "LOCUST_PART_TUNE=0,LOCUST_PART_DEFAULT=letters",
+VARIANTS = {"letters (default)": "LOCUST_PART_TUNE=0",
             "first byte": "LOCUST_PART_TUNE=0,LOCUST_PART_DEFAULT=byte"}
 
 
@@ -54,7 +54,7 @@ def inputs(d: str) -> dict:
                                                                    recursive=True)))
     code += b"".join(open(p, "rb").read() for p in sorted(glob.glob(os.path.join(ROOT, "tests", "*.py"))))
     out["Python sources"] = (code * (HAMLET // max(len(code), 1) + 1))[:HAMLET]
-    out["hamlet (fitted: reference)"] = open(os.path.join(ROOT, "data", "hamlet.txt"), "rb").read()
+    out["hamlet (the benchmark fixture)"] = open(os.path.join(ROOT, "data", "hamlet.txt"), "rb").read()
     paths = {}
     for name, text in out.items():
         cut = text.rfind(b"\n")
@@ -97,7 +97,7 @@ def main() -> int:
         f.write(f"Median ms per job over {a.rounds} fresh processes per variant ({a.steps} jobs "
                 f"each after {a.warmup} warm-up jobs); first = a fresh engine's first job.  "
                 "`tools/partmap_heldout.py`.\n\n")
-        f.write("| input | bytes | " + " | ".join(VARIANTS) + " | default vs letters |\n")
+        f.write("| input | bytes | " + " | ".join(VARIANTS) + " | letters vs first byte |\n")
         f.write("|---|---:|" + "---:|" * len(VARIANTS) + "---:|\n")
         for name, size, vals in rows:
             cells = " | ".join(f"{ms:.4f} (first {fj:.4f})" for ms, fj in vals)
