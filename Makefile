@@ -90,3 +90,8 @@ clean:
 kbench: $(BUILD)/kbench
 $(BUILD)/kbench: tools/kbench/kbench.hip $(LIB) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-value -Wno-unused-result -o $@ $< -L$(LIBDIR) -llocust -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+# diagnostics: what a GPU process's exit costs by how much of the GPU it touched
+exit_probe: $(BUILD)/exit_probe
+$(BUILD)/exit_probe: tools/exit_probe.hip
+	$(HIPCC) $(HIPFLAGS) -o $@ $<

@@ -3,6 +3,8 @@
 // partition-map retuning, graph capture, streaming and the result hand-over -- compiled once
 // here instead of in every translation unit that includes the header.
 #include "pipeline.hpp"
+#include <exception>
+#include <thread>
 
 namespace locust {
 namespace detail {
@@ -285,6 +287,29 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
                       (unsigned long long)max_bytes, (unsigned long long)cap_bytes,
                       plan.why.c_str());
   }
+  // A streaming engine's copy stream, second chunk buffer and pinned read ring (~20 ms:
+  // a second hardware queue, 64 MiB of page locking) are made on a helper thread while
+  // this one loads the kernel modules, creates the compute stream and lays out the arena
+  // (stage 1's per-process setup); joined before the constructor ends.
+  std::thread prep;
+  std::exception_ptr prep_err;
+  struct PrepJoin {
+    std::thread& t;
+    ~PrepJoin() {
+      if (t.joinable()) t.join();
+    }
+  } prep_join{prep};
+  if (streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
+    prep = std::thread([this, &prep_err] {
+      try {
+        LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
+        ensure_stream_buffers(false, 64);
+        ensure_read_ring(stream_ring_piece());
+      } catch (...) {
+        prep_err = std::current_exception();
+      }
+    });
+  }
   warm_modules_once(cfg.device);
   tc[1] = now_ns();
   LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -452,6 +477,8 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
   LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
   std::memset(h_ctr, 0, sizeof(MapCounters));
+  if (prep.joinable()) prep.join();
+  if (prep_err) std::rethrow_exception(prep_err);
   tc[4] = now_ns();
   if (large_ordered && cfg.map_path == MapPath::kFast) {
     // what a piecewise pass needs, made here and not inside the first job: the copy
@@ -1618,6 +1645,20 @@ void DevicePipeline::ensure_stream_buffers(bool staging, u64 nchunks) {
   }
 }
 
+u64 DevicePipeline::stream_ring_piece() const {
+  return std::min<u64>(cap_bytes, cfg.ring_piece_bytes ? cfg.ring_piece_bytes : kRingPieceMax);
+}
+
+void DevicePipeline::ensure_read_ring(u64 piece) {
+  if (ring_piece == piece) return;
+  for (int i = 0; i < kRingPieces; ++i) {
+    if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
+    h_ring[i] = static_cast<char*>(pinned_alloc(piece + 64, hipHostMallocDefault, "read ring piece"));
+    if (!ev_ring[i]) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
+  }
+  ring_piece = piece;
+}
+
 char* DevicePipeline::ensure_h_text() {
   if (h_text) return h_text;
   h_text = static_cast<char*>(pinned_alloc(cap_bytes + 64, hipHostMallocDefault, "input text buffer"));
@@ -1701,21 +1742,14 @@ size_t DevicePipeline::enqueue_stream_source(TextSource& src_text) {
   LOCUST_CHECK_ARG(cfg.sort_path == SortPath::kDict && cfg.map_path == MapPath::kFast,
                    "inputs larger than the engine capacity stream through the dictionary "
                    "path with the fast map (sort=dict, map=fast)");
-  const u64 piece = std::min<u64>(cap_bytes, cfg.ring_piece_bytes ? cfg.ring_piece_bytes : kRingPieceMax);
+  const u64 piece = stream_ring_piece();
   // a map window closes before a piece would overflow it: windows >= map_window - piece
   const u64 min_window = map_window > piece ? map_window - piece : std::max<u64>(map_window / 2, 1);
   const u64 t_setup = now_ns();
   ensure_stream_buffers(false, div_up(std::max<u64>(src_text.size(), 1), min_window) + 2);
   const u64 t_bufs = now_ns();
   reset_window_counters();
-  if (ring_piece != piece) {
-    for (int i = 0; i < kRingPieces; ++i) {
-      if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
-      h_ring[i] = static_cast<char*>(pinned_alloc(piece + 64, hipHostMallocDefault, "read ring piece"));
-      if (!ev_ring[i]) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
-    }
-    ring_piece = piece;
-  }
+  ensure_read_ring(piece);
   if ((int)log_level() >= (int)LogLevel::kDebug)
     LOCUST_LOG_DEBUG("stream setup: copy stream / second chunk / counters %.2f ms, read ring %.2f ms",
                      (t_bufs - t_setup) * 1e-6, (now_ns() - t_bufs) * 1e-6);

@@ -742,6 +742,9 @@ struct DevicePipeline {
   static bool host_pinned(const void* p);
 
   void ensure_stream_buffers(bool staging, u64 nchunks);
+  // the read ring's piece size for a TextSource stream, and its (re)allocation
+  u64 stream_ring_piece() const;
+  void ensure_read_ring(u64 piece);
 
   char* ensure_h_text();
 

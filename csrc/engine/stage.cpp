@@ -173,29 +173,33 @@ MapStageResult map_stage(const JobConfig& cfg_in, const std::string& file, const
     JobConfig cfg = cfg_in;
     cfg.graph = 0;  // stage events: the map and sort times
     const u64 chunk = cfg.chunk_bytes ? cfg.chunk_bytes : kDefaultStreamChunk;
+    // the engine outlives the job in out.engine_keep: its teardown (~25 ms of pinned and
+    // device frees for a streaming engine) is the caller's, and a one-shot CLI skips it
     if (out.input_bytes > chunk) {
       cfg.chunk_bytes = chunk;
-      GpuWordCount eng(cfg, out.input_bytes, out.input_bytes);
+      auto eng = std::make_shared<GpuWordCount>(cfg, out.input_bytes, out.input_bytes);
       ts = now_ns();
       auto src = open_file_range_source(file, w.begin, w.end);
-      r = eng.run_source(*src);
+      r = eng->run_source(*src);
       tr = now_ns();
-      out.engine = eng.stats();
+      out.engine = eng->stats();
       out.lines = src->lines();
       out.streamed = true;
-      recs = entries_to_records(r.entries);  // before the engine (and its buffers) goes
+      out.engine_keep = eng;
     } else {
-      GpuWordCount eng(cfg, std::max<u64>(out.input_bytes, 1), std::max<u64>(out.input_bytes, 1));
+      auto eng = std::make_shared<GpuWordCount>(cfg, std::max<u64>(out.input_bytes, 1),
+                                                std::max<u64>(out.input_bytes, 1));
       ts = now_ns();
       TextInput in;
-      in.data = eng.input_buffer();
-      in.bytes = read_file_range_into(file, eng.input_buffer(), w.begin, out.input_bytes, &out.lines);
+      in.data = eng->input_buffer();
+      in.bytes = read_file_range_into(file, eng->input_buffer(), w.begin, out.input_bytes, &out.lines);
       in.num_lines = out.lines;
-      r = eng.run(in);
+      r = eng->run(in);
       tr = now_ns();
-      out.engine = eng.stats();
-      recs = entries_to_records(r.entries);
+      out.engine = eng->stats();
+      out.engine_keep = eng;
     }
+    recs = entries_to_records(r.entries);
     if (lwin) out.lines = w.lines;
   }
   r.entries = EntryList{};

@@ -18,6 +18,7 @@
 // output byte for byte, val included.
 #pragma once
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -65,6 +66,9 @@ struct MapStageResult {
   double window_ms = 0, setup_ms = 0, run_ms = 0;
   SpillIndex index;
   GpuWordCount::Stats engine;  // the GPU engine's HBM plan (device bytes, free HBM, chunks)
+  // the GPU engine itself, alive until the last copy of the result goes (a one-shot CLI
+  // leaks it into its _exit instead of tearing it down)
+  std::shared_ptr<void> engine_keep;
 };
 // Stage 1 over a window of `file` (none: the whole file): the job's combined output -- one
 // (key, count) record per distinct key, key order -- spilled to `spill` in `fmt`, with its

@@ -30,11 +30,15 @@ if [ "$MODE" = lines ]; then
 else
   echo "$G GiB ($S bytes), $N byte windows, $R reducers" | tee $O/summary.txt
 fi
-t0=$(date +%s.%N)
-timeout -k 10 300 ./build/MapReduce $F --json $O/single.json > $D/single.out
-t1=$(date +%s.%N)
+# the single stage three times (its engine setup alone varied 27-170 ms between runs):
+# the comparison takes the median job
+for i in 0 1 2; do
+  t0=$(date +%s.%N)
+  timeout -k 10 300 ./build/MapReduce $F --json $O/single$i.json > $D/single.out
+  t1=$(date +%s.%N)
+  python3 -c "import json,sys; d=json.load(open('$O/single$i.json')); s=d['startup']; print('single stage %d: %.2f s process, job %.1f ms (engine %.1f, read %.1f, first job %.1f), peak RSS %d kB, unique %d' % ($i, $t1-$t0, s['engine_ms']+s['read_ms']+s['first_job_ms'], s['engine_ms'], s['read_ms'], s['first_job_ms'], d['max_rss_kb'], d['unique']))" | tee -a $O/summary.txt
+done
 grep "^print key:" $D/single.out > $D/single.lines
-python3 -c "import json,sys; d=json.load(open('$O/single.json')); s=d['startup']; print('single stage: %.2f s process, job %.1f ms (engine %.1f, read %.1f, first job %.1f), peak RSS %d kB, unique %d' % ($t1-$t0, s['engine_ms']+s['read_ms']+s['first_job_ms'], s['engine_ms'], s['read_ms'], s['first_job_ms'], d['max_rss_kb'], d['unique']))" | tee -a $O/summary.txt
 INPUTS=""
 for k in $(seq 0 $((N-1))); do
   if [ "$MODE" = lines ]; then
@@ -52,22 +56,25 @@ python3 - $O $N <<'PY' | tee -a $O/summary.txt
 import json, statistics, sys
 o, n = sys.argv[1], int(sys.argv[2])
 jobs = [json.load(open(f"{o}/map{k}.json"))["job_ms"] for k in range(n)]
-st = json.load(open(f"{o}/single.json"))["startup"]
-single = st["engine_ms"] + st["read_ms"] + st["first_job_ms"]  # the same parts as a map's job_ms
+singles = []
+for i in range(3):
+    st = json.load(open(f"{o}/single{i}.json"))["startup"]
+    singles.append(st["engine_ms"] + st["read_ms"] + st["first_job_ms"])  # a map's job_ms parts
+single = statistics.median(singles)
 med = statistics.median(jobs)
-print("maps: median %.1f ms, spread %.2f..%.2f of median, sum %.1f ms; single-stage job %.1f ms, sum/single %.2f"
+print("maps: median %.1f ms, spread %.2f..%.2f of median, sum %.1f ms; single-stage job median %.1f ms, sum/single %.2f"
       % (med, min(jobs) / med, max(jobs) / med, sum(jobs), single, sum(jobs) / single))
 PY
 t0=$(date +%s.%N)
 timeout -k 10 300 ./build/MapReduce $F 0 0 0 2 --inputs $INPUTS --json $O/reduce.json > $D/reduce.out
 t1=$(date +%s.%N)
 grep "^print key:" $D/reduce.out > $D/reduce.lines
-python3 -c "import json; d=json.load(open('$O/reduce.json')); print('reduce: %.2f s process, read %.1f ms, setup %.1f ms, merge %.1f ms, records %d, peak RSS %d kB' % ($t1-$t0, d['read_ms'], d['setup_ms'], d['merge_ms'], d['input_records'], d['peak_rss_kb']))" | tee -a $O/summary.txt
+python3 -c "import json; d=json.load(open('$O/reduce.json')); print('reduce: %.2f s process, runtime init %.1f ms, read %.1f ms, setup %.1f ms, merge %.1f ms, records %d, peak RSS %d kB' % ($t1-$t0, d['runtime_init_ms'], d['read_ms'], d['setup_ms'], d['merge_ms'], d['input_records'], d['peak_rss_kb']))" | tee -a $O/summary.txt
 cmp $D/single.lines $D/reduce.lines && echo "stage split == single stage ($(wc -l < $D/single.lines) lines)" | tee -a $O/summary.txt
 rm -f $D/ranges.lines
 for r in $(seq 0 $((R-1))); do
   timeout -k 10 300 ./build/MapReduce $F 0 0 $r 2 --inputs $INPUTS --reducer $r/$R --result-file $D/res.$r --json $O/reducer$r.json > /dev/null
   cat $D/res.$r >> $D/ranges.lines
-  python3 -c "import json; d=json.load(open('$O/reducer$r.json')); print('reducer $r/$R: records read %d, merged %d, val base %d, peak RSS %d kB' % (d['records_read'], d['input_records'], d['val_base'], d['peak_rss_kb']))" | tee -a $O/summary.txt
+  python3 -c "import json; d=json.load(open('$O/reducer$r.json')); print('reducer $r/$R: records read %d, merged %d, val base %d, read %.1f ms, setup %.1f ms, merge %.1f ms, peak RSS %d kB' % (d['records_read'], d['input_records'], d['val_base'], d['read_ms'], d['setup_ms'], d['merge_ms'], d['peak_rss_kb']))" | tee -a $O/summary.txt
 done
 cmp $D/single.lines $D/ranges.lines && echo "$R key-range reducers == single stage" | tee -a $O/summary.txt
