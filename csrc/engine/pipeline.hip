@@ -3,8 +3,6 @@
 // partition-map retuning, graph capture, streaming and the result hand-over -- compiled once
 // here instead of in every translation unit that includes the header.
 #include "pipeline.hpp"
-#include <exception>
-#include <thread>
 
 namespace locust {
 namespace detail {
@@ -287,29 +285,6 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
                       (unsigned long long)max_bytes, (unsigned long long)cap_bytes,
                       plan.why.c_str());
   }
-  // A streaming engine's copy stream, second chunk buffer and pinned read ring (~20 ms:
-  // a second hardware queue, 64 MiB of page locking) are made on a helper thread while
-  // this one loads the kernel modules, creates the compute stream and lays out the arena
-  // (stage 1's per-process setup); joined before the constructor ends.
-  std::thread prep;
-  std::exception_ptr prep_err;
-  struct PrepJoin {
-    std::thread& t;
-    ~PrepJoin() {
-      if (t.joinable()) t.join();
-    }
-  } prep_join{prep};
-  if (streaming && cfg.map_path == MapPath::kFast && cfg.sort_path == SortPath::kDict) {
-    prep = std::thread([this, &prep_err] {
-      try {
-        LOCUST_HIP_CHECK(hipSetDevice(cfg.device));
-        ensure_stream_buffers(false, 64);
-        ensure_read_ring(stream_ring_piece());
-      } catch (...) {
-        prep_err = std::current_exception();
-      }
-    });
-  }
   warm_modules_once(cfg.device);
   tc[1] = now_ns();
   LOCUST_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -477,8 +452,6 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   LOCUST_HIP_CHECK(hipHostMalloc(&h_small, kMaxSamples * sizeof(PackedKey), hipHostMallocDefault));
   LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
   std::memset(h_ctr, 0, sizeof(MapCounters));
-  if (prep.joinable()) prep.join();
-  if (prep_err) std::rethrow_exception(prep_err);
   tc[4] = now_ns();
   if (large_ordered && cfg.map_path == MapPath::kFast) {
     // what a piecewise pass needs, made here and not inside the first job: the copy

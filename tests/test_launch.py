@@ -407,3 +407,23 @@ def test_stage_split_resume_checks_input_and_command(tmp_path, hamlet, cli, capf
     assert mapped == [0, 1]
     out = capfd.readouterr().out
     assert "Omelet" in out and "print key: Hamlet " not in out
+
+
+def test_stage_split_resume_remaps_a_truncated_spill(tmp_path, hamlet, cli, capfd):
+    """a spill shorter than its index's spill_bytes (a map killed while writing,
+    a disk that filled) is mapped again on resume, the intact one is reused."""
+    hosts_roots = [start_daemon(tmp_path) for _ in range(2)]
+    hosts = [h for h, _ in hosts_roots]
+    f = tmp_path / "h.txt"
+    f.write_bytes(hamlet)
+    kw = dict(token=TOKEN, backend="cpu", reducers=2, extra=["--output-format", "gpu"])
+    assert launch.stage_split_wordcount(str(f), hosts, cli, **kw) == 0
+    first = capfd.readouterr().out
+    spill = os.path.join(hosts_roots[0][1], "out.0.kv")
+    with open(spill, "r+b") as fh:
+        fh.truncate(os.path.getsize(spill) - 40)
+    mapped = []
+    assert launch.stage_split_wordcount(str(f), hosts, cli, mapped=mapped, resume=True, **kw) == 0
+    assert mapped == [0]
+    out = capfd.readouterr().out
+    assert out[out.index("print key:"):] == first[first.index("print key:"):]
