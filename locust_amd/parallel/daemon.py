@@ -254,6 +254,13 @@ class _Handler(socketserver.BaseRequestHandler):
                 and isinstance(peer[1], int)):
             return {"ok": False, "error": "pull: peer must be [address, port]"}
         ranges = req.get("ranges") or [[0, -1]]
+        try:
+            ranges = [(int(o), int(n)) for o, n in ranges]
+            size = None if req.get("size") is None else int(req["size"])
+        except (TypeError, ValueError):
+            return {"ok": False, "error": "pull: ranges must be [offset, length] integer pairs"}
+        if any(o < 0 or n < -1 for o, n in ranges) or (size is not None and size < 0):
+            return {"ok": False, "error": "pull: negative offset, length or size"}
         dest = self._path(req.get("dest", ""))
         os.makedirs(os.path.dirname(dest), exist_ok=True)
         fd = self._open_checked(dest, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
@@ -261,7 +268,6 @@ class _Handler(socketserver.BaseRequestHandler):
         frame = 32 << 20
         try:
             for off, length in ranges:
-                off, length = int(off), int(length)
                 pos = off
                 while length < 0 or pos < off + length:
                     want = frame if length < 0 else min(frame, off + length - pos)
@@ -279,8 +285,8 @@ class _Handler(socketserver.BaseRequestHandler):
                     got += len(data)
                     if rep.get("eof") or not data:
                         break
-            if req.get("size") is not None:
-                os.ftruncate(fd, int(req["size"]))
+            if size is not None:
+                os.ftruncate(fd, size)
         finally:
             os.close(fd)
         return {"ok": True, "bytes": got}

@@ -427,3 +427,22 @@ def test_stage_split_resume_remaps_a_truncated_spill(tmp_path, hamlet, cli, capf
     assert mapped == [0]
     out = capfd.readouterr().out
     assert out[out.index("print key:"):] == first[first.index("print key:"):]
+
+
+def test_daemon_pull_validates_and_confines(tmp_path):
+    """The `pull` op: byte ranges of a peer daemon's file written at their offsets under
+    this daemon's root (the rest a hole); bad ranges and paths outside the root refused."""
+    (a, _ra), (b, rb) = start_daemon(tmp_path), start_daemon(tmp_path)
+    tok = {"token": TOKEN}
+    assert request(a.addr, a.port, {"op": "put", **tok, "path": "src.bin",
+                                    "data": "MDEyMzQ1Njc4OQ=="})["ok"]  # b"0123456789"
+    peer = [a.addr, a.port]
+    rep = request(b.addr, b.port, {"op": "pull", **tok, "peer": peer, "src": "src.bin",
+                                   "dest": "got.bin", "ranges": [[2, 3], [7, 2]], "size": 10})
+    assert rep["ok"] and rep["bytes"] == 5
+    assert open(os.path.join(rb, "got.bin"), "rb").read() == b"\x00\x00234\x00\x0078\x00"
+    for bad in ({"ranges": [[-1, 4]]}, {"ranges": [[0, 4]], "size": -5}, {"ranges": [["x", 1]]},
+                {"ranges": [[0, 4]], "dest": "../escape.bin"}, {"peer": "nowhere"}):
+        req = {"op": "pull", **tok, "peer": peer, "src": "src.bin", "dest": "bad.bin", **bad}
+        assert not request(b.addr, b.port, req)["ok"], bad
+    assert not os.path.exists(os.path.join(os.path.dirname(rb), "escape.bin"))
