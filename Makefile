@@ -95,3 +95,8 @@ $(BUILD)/kbench: tools/kbench/kbench.hip $(LIB) $(HDRS)
 exit_probe: $(BUILD)/exit_probe
 $(BUILD)/exit_probe: tools/exit_probe.hip
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
+# diagnostics: the streaming source's host read throughput (page cache -> ring pieces)
+read_probe: $(BUILD)/read_probe
+$(BUILD)/read_probe: tools/read_probe.cpp $(LIB)
+	$(CXX) -O2 -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< -L$(LIBDIR) -llocust -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread

@@ -489,7 +489,7 @@ int generate(const CliArgs& a) {
       const size_t cut = buf.rfind('\n', a.gen.bytes - bytes - 1);
       if (cut == std::string::npos || a.gen.bytes == bytes) break;
       buf.resize(cut + 1);
-      nl = (u64)std::count(buf.begin(), buf.end(), '\n');
+      nl = count_newlines(buf.data(), buf.size());
     }
     write_all(f, buf);
     lines += nl;

@@ -47,6 +47,10 @@ u64 read_file_range_into(const std::string& path, char* dst, u64 off, u64 n, u64
 LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
                             bool ref_compat);
 u64 count_lines(const char* data, u64 bytes);
+// The '\n' bytes of [data, data + bytes): 32 bytes per compare with AVX2 when the CPU has it
+// (16 with SSE2), counts summed in byte lanes -- the streamed reads count every piece's
+// newlines, and std::count's scalar loop ran at ~1 GB/s per thread (tools/read_probe.cpp).
+u64 count_newlines(const char* data, u64 bytes);
 // The byte range [begin, end) of the line window [line_start, line_end) of a file (the
 // reference's per-node line ranges, main.cu:369-374) and its line count, found by a parallel
 // newline scan in bounded memory (never the whole file in memory).  line_end < 0: to the

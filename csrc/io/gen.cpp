@@ -1,5 +1,6 @@
 // Synthetic text generator (see locust/gen.hpp for the shape it reproduces).
 #include "locust/gen.hpp"
+#include "locust/io.hpp"
 
 #include <algorithm>
 #include <cctype>
@@ -232,7 +233,7 @@ u64 gen_text(const GenSpec& spec, std::string* out) {
     const size_t cut = b.rfind('\n', room ? room - 1 : 0);
     if (room && cut != std::string::npos) {
       out->append(b, 0, cut + 1);
-      lines += (u64)std::count(b.begin(), b.begin() + (long)cut + 1, '\n');
+      lines += count_newlines(b.data(), cut + 1);
     }
     return false;
   });
@@ -256,7 +257,7 @@ u64 gen_text_into(const GenSpec& spec, char* buf, u64 cap, u64* lines_out) {
     if (cut != std::string::npos) {
       std::memcpy(buf + pos, b.data(), cut + 1);
       pos += cut + 1;
-      lines += (u64)std::count(b.begin(), b.begin() + (long)cut + 1, '\n');
+      lines += count_newlines(b.data(), cut + 1);
     }
     full = true;
     return false;

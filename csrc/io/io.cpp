@@ -2,6 +2,7 @@
 #include "locust/partmap.hpp"
 
 #include <fcntl.h>
+#include <immintrin.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -31,16 +32,65 @@ u64 EntryList::wire_bytes() const {
   return words * 8;
 }
 
-u64 count_lines(const char* data, u64 bytes) {
-  u64 n = 0;
-  const char* p = data;
-  const char* end = data + bytes;
-  while (p < end) {
-    const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
-    ++n;
-    p = nl ? nl + 1 : end;
+namespace {
+
+// Byte-lane counters: each of 255 rounds adds at most 1 per lane, then one SAD folds them.
+__attribute__((target("avx2"))) u64 count_newlines_avx2(const char* p, u64 n) {
+  const __m256i nl = _mm256_set1_epi8('\n');
+  const __m256i zero = _mm256_setzero_si256();
+  u64 total = 0, i = 0;
+  while (n - i >= 128) {
+    const u64 rounds = std::min<u64>((n - i) / 128, 255);
+    __m256i a0 = zero, a1 = zero, a2 = zero, a3 = zero;
+    for (u64 r = 0; r < rounds; ++r, i += 128) {
+      const __m256i* q = reinterpret_cast<const __m256i*>(p + i);
+      a0 = _mm256_sub_epi8(a0, _mm256_cmpeq_epi8(_mm256_loadu_si256(q + 0), nl));
+      a1 = _mm256_sub_epi8(a1, _mm256_cmpeq_epi8(_mm256_loadu_si256(q + 1), nl));
+      a2 = _mm256_sub_epi8(a2, _mm256_cmpeq_epi8(_mm256_loadu_si256(q + 2), nl));
+      a3 = _mm256_sub_epi8(a3, _mm256_cmpeq_epi8(_mm256_loadu_si256(q + 3), nl));
+    }
+    const __m256i s = _mm256_add_epi64(
+        _mm256_add_epi64(_mm256_sad_epu8(a0, zero), _mm256_sad_epu8(a1, zero)),
+        _mm256_add_epi64(_mm256_sad_epu8(a2, zero), _mm256_sad_epu8(a3, zero)));
+    total += (u64)_mm256_extract_epi64(s, 0) + (u64)_mm256_extract_epi64(s, 1) +
+             (u64)_mm256_extract_epi64(s, 2) + (u64)_mm256_extract_epi64(s, 3);
   }
-  return n;
+  for (; i < n; ++i) total += p[i] == '\n';
+  return total;
+}
+
+u64 count_newlines_sse2(const char* p, u64 n) {
+  const __m128i nl = _mm_set1_epi8('\n');
+  const __m128i zero = _mm_setzero_si128();
+  u64 total = 0, i = 0;
+  while (n - i >= 64) {
+    const u64 rounds = std::min<u64>((n - i) / 64, 255);
+    __m128i a0 = zero, a1 = zero, a2 = zero, a3 = zero;
+    for (u64 r = 0; r < rounds; ++r, i += 64) {
+      const __m128i* q = reinterpret_cast<const __m128i*>(p + i);
+      a0 = _mm_sub_epi8(a0, _mm_cmpeq_epi8(_mm_loadu_si128(q + 0), nl));
+      a1 = _mm_sub_epi8(a1, _mm_cmpeq_epi8(_mm_loadu_si128(q + 1), nl));
+      a2 = _mm_sub_epi8(a2, _mm_cmpeq_epi8(_mm_loadu_si128(q + 2), nl));
+      a3 = _mm_sub_epi8(a3, _mm_cmpeq_epi8(_mm_loadu_si128(q + 3), nl));
+    }
+    const __m128i s = _mm_add_epi64(_mm_add_epi64(_mm_sad_epu8(a0, zero), _mm_sad_epu8(a1, zero)),
+                                    _mm_add_epi64(_mm_sad_epu8(a2, zero), _mm_sad_epu8(a3, zero)));
+    total += (u64)_mm_cvtsi128_si64(s) + (u64)_mm_cvtsi128_si64(_mm_unpackhi_epi64(s, s));
+  }
+  for (; i < n; ++i) total += p[i] == '\n';
+  return total;
+}
+
+}  // namespace
+
+u64 count_newlines(const char* data, u64 bytes) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  return avx2 ? count_newlines_avx2(data, bytes) : count_newlines_sse2(data, bytes);
+}
+
+u64 count_lines(const char* data, u64 bytes) {
+  // every '\n' ends a line, and a last line without one counts too
+  return count_newlines(data, bytes) + (bytes && data[bytes - 1] != '\n' ? 1 : 0);
 }
 
 LoadedText text_from_buffer(const char* data, u64 bytes, i64 line_start, i64 line_end,
@@ -115,7 +165,7 @@ bool pread_slice(int fd, char* dst, u64 off, u64 a, u64 b, bool count_nl, u64* n
     if (k <= 0) return false;
     pos += (u64)k;
   }
-  *nl = count_nl ? (u64)std::count(dst + a, dst + b, '\n') : 0;
+  *nl = count_nl ? count_newlines(dst + a, b - a) : 0;
   return true;
 }
 
@@ -250,7 +300,7 @@ class FileTextSource final : public TextSource {
     LOCUST_CHECK_ARG(carry_.size() < cap, "a line longer than the stream chunk in " + path_);
     std::memcpy(dst, carry_.data(), carry_.size());
     u64 n = carry_.size();
-    u64 nl = (u64)std::count(carry_.begin(), carry_.end(), '\n');
+    u64 nl = count_newlines(carry_.data(), carry_.size());
     carry_.clear();
     const u64 want = std::min<u64>(cap - n, size_ - pos_);
     if (want && pool_) {
@@ -268,7 +318,7 @@ class FileTextSource final : public TextSource {
                           " B) in " + path_);
       const u64 cut = (u64)(static_cast<const char*>(p) - dst) + 1;
       carry_.assign(dst + cut, dst + n);
-      nl -= (u64)std::count(dst + cut, dst + n, '\n');  // (none: cut is after the last)
+      nl -= count_newlines(dst + cut, n - cut);  // (none: cut is after the last)
       n = cut;
     } else if (n && dst[n - 1] != '\n') {
       ++nl;  // the final line without its newline

@@ -878,6 +878,14 @@ PYBIND11_MODULE(_locust, m) {
   }, py::arg("path"), py::arg("begin"), py::arg("end"),
         "(begin, end, 0): bytes [begin, end) of a file moved to line starts");
   m.def("line_start_at", &line_start_at, py::arg("path"), py::arg("offset"));
+  m.def("count_newlines", [](py::bytes b) {
+    const std::string_view v = b;
+    return count_newlines(v.data(), v.size());
+  });
+  m.def("count_lines", [](py::bytes b) {
+    const std::string_view v = b;
+    return count_lines(v.data(), v.size());
+  });
   m.def("line_index_cache_path", &line_index_cache_path, py::arg("path"));
   m.def("native_stage", [] { return py::make_tuple(std::string(current_stage()), stages_entered()); },
         "(the distributed stage this process last entered, stages entered so far)");

@@ -185,3 +185,20 @@ def test_cli_byte_range_refusals(cli, tmp_path):
         p = subprocess.run([cli, f, *args, "--spill-dir", str(tmp_path), "--backend", "cpu"],
                            capture_output=True, timeout=60)
         assert p.returncode != 0, args
+
+
+def test_count_newlines_simd_matches_python():
+    """count_newlines (AVX2 / SSE2 byte-lane counters, 255 rounds per fold) against
+    bytes.count at every alignment and length around the vector and fold boundaries."""
+    import random
+
+    rng = random.Random(7)
+    base = bytes(rng.choice(b"ab\n\n \xff\x0a\x8a") for _ in range(300_000))
+    for off in range(0, 40):
+        for n in list(range(0, 140)) + [255 * 128 - 1, 255 * 128, 255 * 128 + 129, 200_000]:
+            chunk = base[off:off + n]
+            assert lc._C.count_newlines(chunk) == chunk.count(b"\n"), (off, n)
+    allnl = b"\n" * (255 * 128 * 3 + 77)  # every lane at its 255 limit before a fold
+    assert lc._C.count_newlines(allnl) == len(allnl)
+    for t in (b"", b"a", b"a\n", b"\n", b"a\n\nb", b"a\nb\n"):
+        assert lc._C.count_lines(t) == len(t.split(b"\n")) - (1 if t.endswith(b"\n") or not t else 0)
