@@ -69,6 +69,18 @@ def main() -> int:
         rates.sort()
         if rates:
             print(f"H2D GB/s per copy: median {rates[len(rates) // 2]:.1f}, min {rates[0]:.1f}")
+    cd = [(e - s) / 1e3 for s, e, _n, _r in h2d]
+    if cd:
+        sc = sorted(cd)
+        print(f"H2D copy us: median {sc[len(sc) // 2]:.1f}, min {sc[0]:.1f}, max {sc[-1]:.1f}; "
+              f"first copies {', '.join('%.0f' % x for x in cd[:6])}; last {', '.join('%.0f' % x for x in cd[-4:])}")
+        print(f"first H2D at {(h2d[0][0] - t0) / 1e6:.2f} ms, first map at {(maps[0][0] - t0) / 1e6:.2f} ms, "
+              f"last map ends {(maps[-1][1] - t0) / 1e6:.2f} ms, first activity: "
+              f"{min(ks + cs)[2][:40]}")
+        gaps = [(h2d[i + 1][0] - h2d[i][1]) / 1e3 for i in range(len(h2d) - 1)]
+        if gaps:
+            sg = sorted(gaps)
+            print(f"gap between H2D copies us: median {sg[len(sg) // 2]:.1f}, max {sg[-1]:.1f}")
     print(f"first {a.first} windows (ms from job start):")
     for i, (s, e, _n, _r) in enumerate(maps[:a.first]):
         nxt = [x for x in ins if x[0] >= e][:1]
