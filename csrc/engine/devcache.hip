@@ -2,12 +2,15 @@
 #include "locust/devcache.hpp"
 
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
+#include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "locust/common.hpp"
@@ -146,10 +149,69 @@ size_t dev_block_cached(size_t* bytes) {
   return c.free.size();
 }
 
+namespace {
+
+// pinned_alloc's huge-page buffers: base -> mapped length (never destroyed: engines may be
+// freed from static destructors or left to the process exit)
+struct HugePinned {
+  std::mutex mu;
+  std::unordered_map<void*, size_t> len;
+};
+HugePinned& huge_pinned() {
+  static HugePinned* h = new HugePinned;
+  return *h;
+}
+
+constexpr size_t kHugePinMin = 4ull << 20;
+
+void* huge_pinned_alloc(size_t bytes) {
+  static const bool on = [] {
+    const char* e = std::getenv("LOCUST_HUGE_PIN");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return nullptr;
+  const size_t n = (bytes + kPage - 1) / kPage * kPage;
+  void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (m == MAP_FAILED) return nullptr;
+  (void)::madvise(m, n, MADV_HUGEPAGE);
+  std::memset(m, 0, n);  // first touch: the pages exist (huge where THP allows) on this node
+  if (hipHostRegister(m, n, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    ::munmap(m, n);
+    return nullptr;
+  }
+  HugePinned& h = huge_pinned();
+  std::lock_guard<std::mutex> lk(h.mu);
+  h.len[m] = n;
+  return m;
+}
+
+}  // namespace
+
+void pinned_free(void* p) {
+  if (!p) return;
+  size_t n = 0;
+  {
+    HugePinned& h = huge_pinned();
+    std::lock_guard<std::mutex> lk(h.mu);
+    auto it = h.len.find(p);
+    if (it != h.len.end()) {
+      n = it->second;
+      h.len.erase(it);
+    }
+  }
+  if (n) {
+    (void)hipHostUnregister(p);
+    ::munmap(p, n);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+
 void* pinned_alloc(size_t bytes, unsigned flags, const char* what) {
   static std::atomic<unsigned long long> total{0};
-  void* p = nullptr;
-  LOCUST_HIP_CHECK(hipHostMalloc(&p, bytes, flags));
+  void* p = flags == hipHostMallocDefault && bytes >= kHugePinMin ? huge_pinned_alloc(bytes) : nullptr;
+  if (!p) LOCUST_HIP_CHECK(hipHostMalloc(&p, bytes, flags));
   const unsigned long long t = total.fetch_add(bytes) + bytes;
   if (bytes >= (1u << 20))
     LOCUST_LOG_DEBUG("pinned %.1f MiB: %s (allocated so far %.1f MiB)", bytes / 1048576.0, what,

@@ -508,10 +508,10 @@ DevicePipeline::~DevicePipeline() {
   for (int b = 0; b < 2; ++b) {
     if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
     if (ev_consumed[b]) (void)hipEventDestroy(ev_consumed[b]);
-    if (h_stage[b]) (void)hipHostFree(h_stage[b]);
+    pinned_free(h_stage[b]);
   }
   for (int i = 0; i < kRingPieces; ++i) {
-    if (h_ring[i]) (void)hipHostFree(h_ring[i]);
+    pinned_free(h_ring[i]);
     if (ev_ring[i]) (void)hipEventDestroy(ev_ring[i]);
   }
   for (auto e : ev_piece) (void)hipEventDestroy(e);
@@ -525,9 +525,10 @@ DevicePipeline::~DevicePipeline() {
   if (h_chunk_ctr) (void)hipHostFree(h_chunk_ctr);
   if (stream) (void)hipStreamDestroy(stream);
   if (arena.base) dev_block_free(arena.base, arena_block);  // every stream synchronised above
-  for (void* p : {(void*)h_text, (void*)h_ctr, (void*)h_plan, (void*)h_keys,
-                  (void*)h_small, (void*)h_u64, (void*)h_ctr_mapped, (void*)h_pmap,
-                  (void*)h_pw, (void*)h_done})
+  pinned_free(h_text);
+  pinned_free(h_keys);
+  for (void* p : {(void*)h_ctr, (void*)h_plan, (void*)h_small, (void*)h_u64,
+                  (void*)h_ctr_mapped, (void*)h_pmap, (void*)h_pw, (void*)h_done})
     if (p) (void)hipHostFree(p);
   if (d_pmap) (void)hipFree(d_pmap);
   if (d_plan) (void)hipFree(d_plan);
@@ -572,7 +573,7 @@ void DevicePipeline::grow_host_out(u64 n) {
 
 void DevicePipeline::grow_host_keys(u64 n) {
   if (n <= h_keys_cap) return;
-  if (h_keys) LOCUST_HIP_CHECK(hipHostFree(h_keys));
+  pinned_free(h_keys);
   h_keys_cap = std::max<u64>(n, 1);
   h_keys = static_cast<u64*>(pinned_alloc(h_keys_cap * kKeyWords * sizeof(u64), hipHostMallocDefault,
                                           "key staging"));
@@ -1625,7 +1626,7 @@ u64 DevicePipeline::stream_ring_piece() const {
 void DevicePipeline::ensure_read_ring(u64 piece) {
   if (ring_piece == piece) return;
   for (int i = 0; i < kRingPieces; ++i) {
-    if (h_ring[i]) LOCUST_HIP_CHECK(hipHostFree(h_ring[i]));
+    pinned_free(h_ring[i]);
     h_ring[i] = static_cast<char*>(pinned_alloc(piece + 64, hipHostMallocDefault, "read ring piece"));
     if (!ev_ring[i]) LOCUST_HIP_CHECK(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
   }

@@ -370,9 +370,7 @@ struct DevicePipeline {
       ctab_h = reinterpret_cast<u64*>(h + cap);
       ctab_d = reinterpret_cast<u64*>(d + cap);
     }
-    ~HostOut() {
-      if (h) (void)hipHostFree(h);
-    }
+    ~HostOut() { pinned_free(h); }
     HostOut(const HostOut&) = delete;
     HostOut& operator=(const HostOut&) = delete;
   };

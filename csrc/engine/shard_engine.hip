@@ -1254,7 +1254,7 @@ class GpuShardEngine final : public ShardEngine {
         (void)hipHostUnregister(p);
         ::munmap(p, mapped);
       } else {
-        (void)hipHostFree(p);
+        pinned_free(p);
       }
     }
   };

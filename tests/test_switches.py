@@ -32,6 +32,7 @@ CASES = [
     ({"LOCUST_PART_TUNE": "0", "LOCUST_PLAN_TRIGGER": "0"}, "single"),
     ({"LOCUST_SMALL_PASS_KB": "0"}, "single"),
     ({"LOCUST_DEV_CACHE": "0"}, "stream"),
+    ({"LOCUST_HUGE_PIN": "0"}, "stream"),
     ({"LOCUST_DEV_CACHE_GB": "1", "LOCUST_CHUNK_MB": "1"}, "stream"),
     ({"LOCUST_ORD_TRACE": "1", "LOCUST_MAP_TRACE": "1", "LOCUST_ROCTX": "0",
       "LOCUST_LOG": "debug"}, "single"),
