@@ -164,7 +164,7 @@ HugePinned& huge_pinned() {
 
 constexpr size_t kHugePinMin = 4ull << 20;
 
-void* huge_pinned_alloc(size_t bytes) {
+void* huge_pinned_alloc(size_t bytes, unsigned flags) {
   static const bool on = [] {
     const char* e = std::getenv("LOCUST_HUGE_PIN");
     return !(e && e[0] == '0');
@@ -175,7 +175,10 @@ void* huge_pinned_alloc(size_t bytes) {
   if (m == MAP_FAILED) return nullptr;
   (void)::madvise(m, n, MADV_HUGEPAGE);
   std::memset(m, 0, n);  // first touch: the pages exist (huge where THP allows) on this node
-  if (hipHostRegister(m, n, hipHostRegisterMapped) != hipSuccess) {
+  // registered memory is fine-grained (coherent) unless registered coarse-grained, so the
+  // mapped + coherent result buffers the kernels write over PCIe may take this path too
+  const unsigned rf = hipHostRegisterMapped | ((flags & hipHostMallocPortable) ? hipHostRegisterPortable : 0u);
+  if (hipHostRegister(m, n, rf) != hipSuccess) {
     (void)hipGetLastError();
     ::munmap(m, n);
     return nullptr;
@@ -210,7 +213,8 @@ void pinned_free(void* p) {
 
 void* pinned_alloc(size_t bytes, unsigned flags, const char* what) {
   static std::atomic<unsigned long long> total{0};
-  void* p = flags == hipHostMallocDefault && bytes >= kHugePinMin ? huge_pinned_alloc(bytes) : nullptr;
+  constexpr unsigned kHugeFlags = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+  void* p = (flags & ~kHugeFlags) == 0 && bytes >= kHugePinMin ? huge_pinned_alloc(bytes, flags) : nullptr;
   if (!p) LOCUST_HIP_CHECK(hipHostMalloc(&p, bytes, flags));
   const unsigned long long t = total.fetch_add(bytes) + bytes;
   if (bytes >= (1u << 20))

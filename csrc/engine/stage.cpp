@@ -2,7 +2,9 @@
 #include "locust/stage.hpp"
 
 #include <algorithm>
+#include <exception>
 #include <queue>
+#include <thread>
 
 namespace locust {
 
@@ -259,52 +261,81 @@ WordCountResult reduce_spills(const JobConfig& cfg, const std::vector<std::strin
   const PackedKey* lo = reducer > 0 ? &st.splitters[(size_t)reducer - 1] : nullptr;
   const PackedKey* hi = reducer < reducers - 1 ? &st.splitters[(size_t)reducer] : nullptr;
 
-  u64 val_base = 0;
-  std::vector<std::vector<KeyCount>> runs;
-  runs.reserve(nf);
-  for (size_t k = 0; k < nf; ++k) {
+  // Each spill's part of the range, read on a thread of its own (index seek, then the
+  // records up to the range's end): the spills are independent files.
+  struct Part {
     std::vector<KeyCount> run;
+    u64 base = 0, read = 0;
+  };
+  std::vector<Part> parts(nf);
+  auto extract = [&](size_t k) {
+    Part& pt = parts[k];
+    std::vector<KeyCount>& run = pt.run;
     if (!indexed[k]) {
       for (const KeyCount& r : loaded[k]) {
         if (below(r.w, lo))
-          val_base += r.count;
+          pt.base += r.count;
         else if (at_or_above(r.w, hi))
           break;
         else
           run.push_back(r);
       }
       std::vector<KeyCount>().swap(loaded[k]);
-    } else {
-      const SpillIndex& x = idx[k];
-      if (x.samples.empty()) continue;
-      // start at the last sample below the range (its count_before is exact)
-      size_t j = 0;
-      if (lo) {
-        const auto it = std::lower_bound(
-            x.samples.begin(), x.samples.end(), *lo,
-            [](const SpillSample& s, const PackedKey& key) { return key_compare(s.key.w, key.w) < 0; });
-        j = it == x.samples.begin() ? 0 : (size_t)(it - x.samples.begin()) - 1;
-      }
-      SpillReader rd(files[k]);
-      rd.seek(x.samples[j].offset);
-      u64 base = x.samples[j].count_before;
-      KeyCount r;
-      while (rd.next(&r)) {
-        ++st.records_read;
-        if (below(r.w, lo)) {
-          base += r.count;
-          continue;
-        }
-        if (at_or_above(r.w, hi)) break;
-        if (!run.empty() && key_compare(run.back().w, r.w) == 0)
-          run.back().count += r.count;  // a sorted but not combined spill
-        else
-          run.push_back(r);
-      }
-      val_base += base;
+      return;
     }
-    st.run_records += run.size();
-    if (!run.empty()) runs.push_back(std::move(run));
+    const SpillIndex& x = idx[k];
+    if (x.samples.empty()) return;
+    // start at the last sample below the range (its count_before is exact)
+    size_t j = 0;
+    if (lo) {
+      const auto it = std::lower_bound(
+          x.samples.begin(), x.samples.end(), *lo,
+          [](const SpillSample& s, const PackedKey& key) { return key_compare(s.key.w, key.w) < 0; });
+      j = it == x.samples.begin() ? 0 : (size_t)(it - x.samples.begin()) - 1;
+    }
+    SpillReader rd(files[k]);
+    rd.seek(x.samples[j].offset);
+    u64 base = x.samples[j].count_before;
+    KeyCount r;
+    while (rd.next(&r)) {
+      ++pt.read;
+      if (below(r.w, lo)) {
+        base += r.count;
+        continue;
+      }
+      if (at_or_above(r.w, hi)) break;
+      if (!run.empty() && key_compare(run.back().w, r.w) == 0)
+        run.back().count += r.count;  // a sorted but not combined spill
+      else
+        run.push_back(r);
+    }
+    pt.base = base;
+  };
+  {
+    const size_t nt = std::min<size_t>(nf, 8);
+    std::vector<std::exception_ptr> err(nt);
+    auto worker = [&](size_t t) {
+      try {
+        for (size_t k = t; k < nf; k += nt) extract(k);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(worker, t);
+    worker(0);
+    for (auto& x : th) x.join();
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+  u64 val_base = 0;
+  std::vector<std::vector<KeyCount>> runs;
+  runs.reserve(nf);
+  for (Part& pt : parts) {
+    val_base += pt.base;
+    st.records_read += pt.read;
+    st.run_records += pt.run.size();
+    if (!pt.run.empty()) runs.push_back(std::move(pt.run));
   }
   const u64 t1 = now_ns();
   WordCountResult res;

@@ -29,9 +29,10 @@ size_t dev_block_cached(size_t* bytes = nullptr);
 // Pinned host memory (hipHostMalloc with `flags`) for `what`, logged at LOCUST_LOG=debug
 // when >= 1 MiB with the process's running total of pinned allocations: where a
 // multi-rank run's host memory goes.  Throws locust::Error on failure.
-// A default-flag buffer of >= 4 MiB (read rings, chunk staging, one-pass text, key
-// downloads) is instead anonymous memory advised to transparent huge pages, first-touched
-// here and hipHostRegister'ed (mapped): page-locking 64 MiB took 8-12 ms through
+// A buffer of >= 4 MiB (read rings, chunk staging, one-pass text, key downloads, the
+// mapped result buffers) is instead anonymous memory advised to transparent huge pages,
+// first-touched here and hipHostRegister'ed (mapped; registered memory is fine-grained
+// unless asked otherwise, like a coherent hipHostMalloc): page-locking 64 MiB took 8-12 ms through
 // hipHostMalloc -- the 4 KiB page faults -- and 3.7 ms this way (tools/micro/pin_probe.hip;
 // LOCUST_HUGE_PIN=0: hipHostMalloc for everything).  Free with pinned_free.
 void* pinned_alloc(size_t bytes, unsigned flags, const char* what);
