@@ -214,6 +214,8 @@ void pinned_free(void* p) {
 void* pinned_alloc(size_t bytes, unsigned flags, const char* what) {
   static std::atomic<unsigned long long> total{0};
   constexpr unsigned kHugeFlags = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
+  // (small buffers too measured no different: the map's zero-copy staging of whole Hamlet
+  // from 2 MiB pages, profiles/r6/map/huge_text_ab.txt)
   void* p = (flags & ~kHugeFlags) == 0 && bytes >= kHugePinMin ? huge_pinned_alloc(bytes, flags) : nullptr;
   if (!p) LOCUST_HIP_CHECK(hipHostMalloc(&p, bytes, flags));
   const unsigned long long t = total.fetch_add(bytes) + bytes;
