@@ -174,6 +174,9 @@ void* huge_pinned_alloc(size_t bytes, unsigned flags) {
   void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (m == MAP_FAILED) return nullptr;
   (void)::madvise(m, n, MADV_HUGEPAGE);
+  // a child process (subprocess spawns) must not share these pages copy-on-write: a write
+  // by this process before the child's exec would move the page under the device mapping
+  (void)::madvise(m, n, MADV_DONTFORK);
   std::memset(m, 0, n);  // first touch: the pages exist (huge where THP allows) on this node
   // registered memory is fine-grained (coherent) unless registered coarse-grained, so the
   // mapped + coherent result buffers the kernels write over PCIe may take this path too

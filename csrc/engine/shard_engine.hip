@@ -1273,6 +1273,7 @@ class GpuShardEngine final : public ShardEngine {
       b->p = static_cast<char*>(p);
       b->mapped = bytes;
       (void)::madvise(p, bytes, MADV_HUGEPAGE);  // fewer GPU-side translations
+      (void)::madvise(p, bytes, MADV_DONTFORK);  // registered below: no copy-on-write children
       place_slices(p, plan);
       std::memset(p, 0, bytes);  // first touch: every page on its slice's node
       LOCUST_HIP_CHECK(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
