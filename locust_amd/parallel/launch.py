@@ -408,7 +408,9 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
         idx.append(parse_index(data))
     spl = plan_splitters(idx, reducers)
     pulled = [[0] * parts for _ in range(reducers)]
-    runs = []
+    # every (reducer, remote spill) pull at once: each is one request to the reducer host's
+    # daemon, which fetches from the mapper's daemon (both serve requests on threads)
+    pulls, inputs_of = [], []
     for r in range(reducers):
         hk = r % parts
         lo, hi = reducer_range(spl, r)
@@ -420,16 +422,25 @@ def stage_split_wordcount(path: str, hosts: list[Host], cli: str, token: str | N
             dest = f"spills/r{r}/out.{k}.kv"
             for name, rngs, sz in ((dest, reducer_slices(idx[k], lo, hi), idx[k].spill_bytes),
                                    (dest + ".idx", [(0, -1)], None)):
-                rep = _req(hosts[hk], {"op": "pull", "peer": [hosts[k].addr, hosts[k].port],
-                                       "src": f"out.{k}.kv" + name[len(dest):], "dest": name,
-                                       "size": sz, "ranges": [list(x) for x in rngs]},
-                           token, 600)
-                if not rep.get("ok"):
-                    raise RuntimeError(f"reducer {r} on {hosts[hk]}: {rep.get('error')}")
-                if sz is not None:
-                    pulled[r][k] += rep["bytes"]
+                pulls.append((r, k, sz, {"op": "pull", "peer": [hosts[k].addr, hosts[k].port],
+                                         "src": f"out.{k}.kv" + name[len(dest):], "dest": name,
+                                         "size": sz, "ranges": [list(x) for x in rngs]}))
             inputs.append(f"{roots[hk]}/{dest}")
-        argv = [cli, apath, "0", "0", str(r), "2", "--inputs", ",".join(inputs),
+        inputs_of.append(inputs)
+    if pulls:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(max_workers=min(16, len(pulls))) as pool:
+            reps = list(pool.map(lambda x: _req(hosts[x[0] % parts], x[3], token, 600), pulls))
+        for (r, k, sz, _q), rep in zip(pulls, reps):
+            if not rep.get("ok"):
+                raise RuntimeError(f"reducer {r} on {hosts[r % parts]}: {rep.get('error')}")
+            if sz is not None:
+                pulled[r][k] += rep["bytes"]
+    runs = []
+    for r in range(reducers):
+        hk = r % parts
+        argv = [cli, apath, "0", "0", str(r), "2", "--inputs", ",".join(inputs_of[r]),
                 "--reducer", f"{r}/{reducers}", "--result-file", f"{roots[hk]}/result.{r}.txt",
                 "--backend", backend] + list(extra or [])
         runs.append(_RemoteRun(hosts[hk], argv, {}, token))
