@@ -237,16 +237,34 @@ WordCountResult reduce_spills(const JobConfig& cfg, const std::vector<std::strin
   std::vector<SpillIndex> idx(nf);
   std::vector<char> indexed(nf, 0);
   std::vector<std::vector<KeyCount>> loaded(nf);
-  for (size_t k = 0; k < nf; ++k) {
+  // Up to 8 threads over the spills, in both passes below: the files are independent.
+  auto for_each_spill = [nf](const auto& fn) {
+    const size_t nt = std::min<size_t>(nf, 8);
+    std::vector<std::exception_ptr> err(nt);
+    auto worker = [&](size_t t) {
+      try {
+        for (size_t k = t; k < nf; k += nt) fn(k);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(worker, t);
+    worker(0);
+    for (auto& x : th) x.join();
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  };
+  std::vector<u64> nread(nf, 0);
+  for_each_spill([&](size_t k) {
     if (read_spill_index(files[k], &idx[k]) && idx[k].sorted) {
       indexed[k] = 1;
-      ++st.indexed_files;
-      continue;
+      return;
     }
     // no (current) index: the whole spill, sorted and combined here (a reference-format
     // file: one "key \t1" line per token, sorted by one mapper only -- B7)
     loaded[k] = read_spill(files[k]);
-    st.records_read += loaded[k].size();
+    nread[k] = loaded[k].size();
     bool sorted = true;
     for (size_t i = 1; i < loaded[k].size() && sorted; ++i)
       sorted = key_compare(loaded[k][i - 1].w, loaded[k][i].w) <= 0;
@@ -255,14 +273,17 @@ WordCountResult reduce_spills(const JobConfig& cfg, const std::vector<std::strin
     else
       sort_combine(&loaded[k]);
     idx[k] = index_records(loaded[k]);
-    ++st.loaded_files;
+  });
+  for (size_t k = 0; k < nf; ++k) {
+    st.indexed_files += indexed[k] ? 1 : 0;
+    st.loaded_files += indexed[k] ? 0 : 1;
+    st.records_read += nread[k];
   }
   if (reducers > 1) st.splitters = plan_reducer_splitters(idx, reducers);
   const PackedKey* lo = reducer > 0 ? &st.splitters[(size_t)reducer - 1] : nullptr;
   const PackedKey* hi = reducer < reducers - 1 ? &st.splitters[(size_t)reducer] : nullptr;
 
-  // Each spill's part of the range, read on a thread of its own (index seek, then the
-  // records up to the range's end): the spills are independent files.
+  // Each spill's part of the range (index seek, then the records up to the range's end).
   struct Part {
     std::vector<KeyCount> run;
     u64 base = 0, read = 0;
@@ -311,23 +332,7 @@ WordCountResult reduce_spills(const JobConfig& cfg, const std::vector<std::strin
     }
     pt.base = base;
   };
-  {
-    const size_t nt = std::min<size_t>(nf, 8);
-    std::vector<std::exception_ptr> err(nt);
-    auto worker = [&](size_t t) {
-      try {
-        for (size_t k = t; k < nf; k += nt) extract(k);
-      } catch (...) {
-        err[t] = std::current_exception();
-      }
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nt; ++t) th.emplace_back(worker, t);
-    worker(0);
-    for (auto& x : th) x.join();
-    for (auto& e : err)
-      if (e) std::rethrow_exception(e);
-  }
+  for_each_spill(extract);
   u64 val_base = 0;
   std::vector<std::vector<KeyCount>> runs;
   runs.reserve(nf);
