@@ -481,6 +481,9 @@ def main(argv=None) -> int:
                     help="key-range reducers of --wordcount (default: one per host)")
     ap.add_argument("--output-format", choices=["gpu", "cpu"], default=None,
                     help="--wordcount result lines: GPU build's (with val) or CPU build's")
+    ap.add_argument("--resume", action="store_true",
+                    help="--wordcount: keep the map outputs of an earlier run of the same "
+                         "command on the unchanged input (only missing or stale ones map again)")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -495,7 +498,8 @@ def main(argv=None) -> int:
 
         extra = ["--output-format", a.output_format] if a.output_format else []
         return stage_split_wordcount(a.wordcount, load_hosts(a.hosts), a.cli or cli_path(),
-                                     token, a.backend, extra=extra, reducers=a.reducers or None)
+                                     token, a.backend, extra=extra, reducers=a.reducers or None,
+                                     resume=a.resume)
     if not cmd:
         ap.error("no command given (put it after --)")
     if a.hosts:

@@ -446,3 +446,33 @@ def test_daemon_pull_validates_and_confines(tmp_path):
         req = {"op": "pull", **tok, "peer": peer, "src": "src.bin", "dest": "bad.bin", **bad}
         assert not request(b.addr, b.port, req)["ok"], bad
     assert not os.path.exists(os.path.join(os.path.dirname(rb), "escape.bin"))
+
+
+def test_launcher_cli_wordcount_resume(tmp_path, hamlet, cli, capfd, monkeypatch):
+    """`python -m locust_amd.parallel.launch --hosts H --wordcount F [--resume]`: the second
+    run with --resume maps nothing again and prints the same output."""
+    hosts_roots = [start_daemon(tmp_path) for _ in range(2)]
+    hf = tmp_path / "hosts.txt"
+    hf.write_text("".join(f"{h.addr} {h.port}\n" for h, _ in hosts_roots))
+    tf = tmp_path / "token"
+    tf.write_text(TOKEN + "\n")
+    f = tmp_path / "h.txt"
+    f.write_bytes(hamlet)
+    base = ["--hosts", str(hf), "--token-file", str(tf), "--wordcount", str(f), "--backend",
+            "cpu", "--cli", cli, "--output-format", "gpu"]
+    assert launch.main(base) == 0
+    first = capfd.readouterr().out
+    ran = []
+    real = launch._RemoteRun
+
+    def spy(h, argv, env, token):
+        ran.append(argv[5])  # the stage
+        return real(h, argv, env, token)
+
+    monkeypatch.setattr(launch, "_RemoteRun", spy)
+    assert launch.main(base + ["--resume"]) == 0
+    assert ran == ["2", "2"]  # reducers only: both map outputs reused
+    assert capfd.readouterr().out == first
+    ent, _n, _ = oracle.wordcount(hamlet)
+    assert first[first.index("print key:"):first.rindex("\nDone")].encode().rstrip(b"\n") == \
+        oracle.format_gpu(ent).rstrip(b"\n")
