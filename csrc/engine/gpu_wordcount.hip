@@ -309,6 +309,7 @@ std::vector<WordCountEntry> merge_runs_device(const JobConfig& cfg,
   out.reserve(total);
   JobConfig c = cfg;
   c.chunk_bytes = 0;  // one pass: the engine holds a merge's records
+  c.records_only = true;
   u64 limit = std::min<u64>(total, kMergeMaxRecords);
   // LOCUST_MERGE_MAX_RECORDS: a lower per-launch record limit (tests of the key-range split)
   if (const char* e = std::getenv("LOCUST_MERGE_MAX_RECORDS"))

@@ -409,7 +409,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   tc[3] = now_ns();
   // A streaming engine reads files through its two staging halves; its one-pass buffer
   // is pinned only when a caller stages text there (input_buffer(), a one-pass job).
-  if (!streaming) ensure_h_text();
+  if (!streaming && !cfg.records_only) ensure_h_text();
   LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr, sizeof(MapCounters), hipHostMallocDefault));
   LOCUST_HIP_CHECK(hipHostMalloc(&h_plan, sizeof(SortPlan), hipHostMallocDefault));
   // Output records and the counter snapshot are host-mapped: the emit kernel writes them
@@ -424,12 +424,12 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   // 12 MiB mapped buffer took ~1 ms of a cold CLI-style job).  A streaming engine's jobs
   // take hundreds of ms: its second buffer is pinned when a second job needs it (host
   // memory of `--gpus N` file ranks, one streaming engine each).
-  if (!streaming) out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
+  if (!streaming && !cfg.records_only) out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
   // and a third for small engines: the partition map's retune reads the first job's
   // output on the worker thread, so a caller holding each job's result (the CLI, a
   // Python loop) found both buffers taken at its third job and waited ~0.2 ms for the
   // worker (measured); pinning it here costs well under a millisecond of construction
-  if (!streaming && h_out_cap * sizeof(OutRecord) <= (8ull << 20))
+  if (!streaming && !cfg.records_only && h_out_cap * sizeof(OutRecord) <= (8ull << 20))
     out_pool.push_back(std::make_shared<HostOut>(h_out_cap));
   use_out(0);
   LOCUST_HIP_CHECK(hipHostMalloc(&h_ctr_mapped, sizeof(MapCounters),
@@ -453,7 +453,7 @@ DevicePipeline::DevicePipeline(const JobConfig& c, u64 max_bytes, u64 max_lines,
   LOCUST_HIP_CHECK(hipHostMalloc(&h_u64, (kMaxRanks + 8) * sizeof(u64), hipHostMallocDefault));
   std::memset(h_ctr, 0, sizeof(MapCounters));
   tc[4] = now_ns();
-  if (large_ordered && cfg.map_path == MapPath::kFast) {
+  if (large_ordered && cfg.map_path == MapPath::kFast && !cfg.records_only) {
     // what a piecewise pass needs, made here and not inside the first job: the copy
     // streams and piece events, and the plan's scratch
     ensure_piece_events(partial_slots_cap);

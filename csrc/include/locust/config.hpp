@@ -66,6 +66,11 @@ struct JobConfig {
   // Engines sharing one GPU's HBM (ranks of one process on one device): each plans its
   // device pass against free memory / hbm_share (plan_device_pass, engine.hpp).
   int hbm_share = 1;
+  // An engine that only merges (key, count) records -- stage 2's device merge: no text is
+  // ever uploaded, so construction skips the text buffer, the spare output buffers and the
+  // piecewise upload's copy queues (two hardware queues and their warm-up copies: 50 ms of
+  // a reducer's ~90 ms setup, measured).
+  bool records_only = false;
 };
 constexpr u64 kZeroCopyMaxBytes = 1ull << 20;
 
