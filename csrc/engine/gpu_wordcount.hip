@@ -15,7 +15,9 @@ struct GpuWordCount::Impl : DevicePipeline {
 };
 
 GpuWordCount::GpuWordCount(const JobConfig& cfg, u64 max_text_bytes, u64 max_lines)
-    : impl_(new Impl(cfg, max_text_bytes, max_lines)) {}
+    : impl_(new Impl(cfg, max_text_bytes, max_lines)) {
+  impl_->warm_first_job();
+}
 GpuWordCount::~GpuWordCount() = default;
 
 const JobConfig& GpuWordCount::config() const { return impl_->cfg; }

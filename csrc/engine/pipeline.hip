@@ -981,6 +981,7 @@ u64 DevicePipeline::retune_wanted() const {
 }
 
 void DevicePipeline::force_retune(const EntryList& e) {
+  if (warming) return;
   const u64 n = e.size();
   // a device-planned map overflowed: this engine keeps the host-side map from now on
   // (tuned from this output, or the default with tuning off) -- d_pmap holds the plan
@@ -1004,7 +1005,28 @@ void DevicePipeline::force_retune(const EntryList& e) {
   retune_with(~0ull / 8, pred, t);
 }
 
+void DevicePipeline::warm_first_job() {
+  if (streaming || cfg.records_only || cfg.sort_path != SortPath::kDict ||
+      cfg.map_path != MapPath::kFast || cap_bytes < 2)
+    return;
+  TextInput in;
+  in.data = ensure_h_text();
+  in.bytes = 2;
+  in.num_lines = 1;
+  if (!lean_job(in)) return;
+  h_text[0] = 'a';
+  h_text[1] = '\n';
+  warming = true;
+  struct Reset {
+    bool& w;
+    ~Reset() { w = false; }
+  } reset{warming};
+  const WordCountResult r = run(in);
+  LOCUST_CHECK_ARG(r.num_unique == 1, "engine warm-up job: unexpected result");
+}
+
 void DevicePipeline::maybe_retune(const EntryList& e) {
+  if (warming) return;
   const u64 mx = retune_wanted();
   if (!mx || retune_pending) return;  // one at a time
   retune_pending = true;
@@ -1123,7 +1145,7 @@ u64* DevicePipeline::map_trace() {
 }
 
 void DevicePipeline::print_map_trace() {
-  if (!d_map_trace) return;
+  if (!d_map_trace || warming) return;
   std::vector<u64> t(4096 * 8);
   LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_map_trace, t.size() * 8, hipMemcpyDeviceToHost));
   u64 t0 = ~0ull;
@@ -1153,7 +1175,7 @@ u64* DevicePipeline::partials_trace() {
 }
 
 void DevicePipeline::print_partials_trace() {
-  if (!d_partials_trace) return;
+  if (!d_partials_trace || warming) return;
   const u64 ns = std::max<u32>(partial_nslots, 1), nb = (u64)kDictParts * ns;
   std::vector<u64> t(nb * 8);  // slot b = p * ns + k
   LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_partials_trace, t.size() * 8, hipMemcpyDeviceToHost));
@@ -1208,7 +1230,7 @@ void DevicePipeline::print_psort_trace() {
 }
 
 void DevicePipeline::print_ord_trace() {
-  if (!d_ord_trace) return;
+  if (!d_ord_trace || warming) return;
   std::vector<u64> t(kDictParts * 32);
   LOCUST_HIP_CHECK(hipMemcpy(t.data(), d_ord_trace, t.size() * 8, hipMemcpyDeviceToHost));
   // stamps: 0 start, 1 built, 2 published, 8 histogram, 7 bucketed, 9 ranked, 3 sorted,

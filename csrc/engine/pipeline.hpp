@@ -630,6 +630,12 @@ struct DevicePipeline {
   // if it is ready and otherwise runs on what it has (the in-job plan, or the current map).
   // The task holds the output buffer, which the pool then skips.
   void maybe_retune(const EntryList& e);
+  // One two-byte job at construction (GpuWordCount engines that run lean jobs): the map and
+  // the ordered build launched once on this engine's stream with their own argument
+  // blocks, so a fresh engine's first real job does not enqueue them for the first time
+  // (~15-20 us more than later jobs, tools/cold_probe.py).  No retune, no trace output.
+  void warm_first_job();
+  bool warming = false;
   struct RetuneTask {
     u64 mx = 0, pred = 0;
     PartMapTables t;
