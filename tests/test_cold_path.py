@@ -109,3 +109,21 @@ def test_plan_runs_only_when_the_map_saw_crowding():
     assert "if (ex.plan_flag) *ex.plan_flag = 0;" in d
     p = _src("csrc", "engine", "pipeline.hip")
     assert "ex.plan_flag = d_plan_flag" in p
+
+
+def test_engine_runs_a_warm_up_job_without_side_effects():
+    """GpuWordCount's constructor runs one two-byte lean job (warm_first_job): the map and
+    the ordered build are enqueued once on the engine's stream before its first real job
+    (cold probe: the first job's enqueue 20 -> 7-10 us).  The warm-up job must not retune
+    the partition map from its one-key output nor print traces."""
+    g = _src("csrc", "engine", "gpu_wordcount.hip")
+    ctor = _body(g, "GpuWordCount::GpuWordCount(const JobConfig& cfg, u64 max_text_bytes, u64 max_lines)")
+    assert "warm_first_job();" in ctor
+    s = _src("csrc", "engine", "pipeline.hip")
+    warm = _body(s, "void DevicePipeline::warm_first_job()")
+    assert "lean_job(in)" in warm and "warming = true;" in warm and "run(in)" in warm
+    for fn in ("void DevicePipeline::maybe_retune(const EntryList& e)",
+               "void DevicePipeline::force_retune(const EntryList& e)",
+               "void DevicePipeline::print_ord_trace()", "void DevicePipeline::print_map_trace()"):
+        body = _body(s, fn)
+        assert "warming" in body.split("\n", 3)[1] + body.split("\n", 3)[2], fn
