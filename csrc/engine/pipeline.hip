@@ -1006,7 +1006,9 @@ void DevicePipeline::force_retune(const EntryList& e) {
 }
 
 void DevicePipeline::warm_first_job() {
-  if (streaming || cfg.records_only || cfg.sort_path != SortPath::kDict ||
+  // small single-pass engines only: there the two-byte job launches the real job's kernels
+  // (a large pass plans, pieces and aggregates differently)
+  if (streaming || large_ordered || cfg.records_only || cfg.sort_path != SortPath::kDict ||
       cfg.map_path != MapPath::kFast || cap_bytes < 2)
     return;
   TextInput in;
@@ -1016,6 +1018,8 @@ void DevicePipeline::warm_first_job() {
   if (!lean_job(in)) return;
   h_text[0] = 'a';
   h_text[1] = '\n';
+  // the engine's statistics describe the caller's jobs only
+  const u64 fb = fallbacks, pp = planned_passes;
   warming = true;
   struct Reset {
     bool& w;
@@ -1023,6 +1027,8 @@ void DevicePipeline::warm_first_job() {
   } reset{warming};
   const WordCountResult r = run(in);
   LOCUST_CHECK_ARG(r.num_unique == 1, "engine warm-up job: unexpected result");
+  fallbacks = fb;
+  planned_passes = pp;
 }
 
 void DevicePipeline::maybe_retune(const EntryList& e) {
