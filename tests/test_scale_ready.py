@@ -238,6 +238,12 @@ def test_bench_watchdog_cpu_tcp_twin_hang(world):
                        capture_output=True, text=True, timeout=150)
     d = _hung_line(p, world, 12, time.time() - t0)
     assert d["progress"]["1"]["native_stage"] == "map"
+    # the scaling table shows the failed N with its reason and the ranks' last stages
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale_report.py"), "-"],
+                         input=p.stdout, capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert f"| {world} | failed |" in out.stdout and f"N={world}: failed (" in out.stdout
+    assert "r1: " in out.stdout
 
 
 def test_bench_watchdog_under_torchrun_cpu_twin():

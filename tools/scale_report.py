@@ -1,6 +1,6 @@
 """The 1/2/4/8-GPU table of a scaling run.
 
-    python tools/scale_report.py SCALE_r05.json [more.json ...] [--md OUT.md]
+    python tools/scale_report.py SCALE_r05.json [more.json ...] [--md OUT.md]   ("-": stdin)
 
 Takes the driver's SCALE_r*.json (or any file holding bench.py result lines: a JSON
 document at any nesting, JSON lines, or text with the lines inside) and prints, per GPU
@@ -12,7 +12,11 @@ count N:
   throughput and strong efficiency T(1) / (N x T(N)) against the N = 1 synth1m point;
 * from the line's scale_diag (N > 1): the min / max over ranks of the map, exchange,
   merge and emit stages, the bytes each rank sent (max over ranks), whether every pair of
-  GPUs had direct access, the RCCL transports seen, and the largest per-rank peak RSS.
+  GPUs had direct access, the RCCL transports seen, and the largest per-rank peak RSS;
+* the exchange strategy of the headline and of synth1m ("local" at N = 1), the largest
+  per-rank engine device memory (HBM plan);
+* a run that failed ("status": "failed", the watchdog's line): its reason and every rank's
+  last stage instead of the numbers.
 """
 from __future__ import annotations
 
@@ -47,7 +51,7 @@ def bench_lines(obj) -> list[dict]:
 def load(paths: list[str]) -> list[dict]:
     lines = []
     for p in paths:
-        text = open(p, errors="replace").read()
+        text = sys.stdin.read() if p == "-" else open(p, errors="replace").read()
         try:
             lines += bench_lines(json.loads(text))
         except ValueError:
@@ -71,8 +75,16 @@ def table(lines: list[dict]) -> str:
     rows = ["| N | headline ms | weak eff | synth1m ms | GB/s | strong eff | map ms | exchange ms | "
             "merge ms | emit ms | max sent MB | all pairs direct | transports | max RSS MB |",
             "|---:|---:|---:|---:|---:|---:|---|---|---|---|---:|---|---|---:|"]
+    fails = []
     for ln in lines:
         n = ln["n_gpus"]
+        if ln.get("status") == "failed" or ln.get("value") is None:
+            prog = ln.get("progress") or {}
+            stages = ", ".join(f"r{r}: {v.get('stage', '?')}" if isinstance(v, dict) else f"r{r}: {v}"
+                               for r, v in sorted(prog.items(), key=lambda kv: str(kv[0])))
+            fails.append(f"N={n}: failed ({ln.get('reason', '?')}); last stages: {stages or '-'}")
+            rows.append(f"| {n} | failed | - | - | - | - | - | - | - | - | - | - | - | - |")
+            continue
         sy = ln.get("synth1m") or {}
         sms = sy.get("ms_per_step")
         weak = f"{t1 / ln['value']:.2f}" if t1 else "-"
@@ -95,9 +107,19 @@ def table(lines: list[dict]) -> str:
             f"{sy.get('GB_per_s', '-')} | {strong} | {_mm(st.get('map'))} | "
             f"{_mm(st.get('exchange'))} | {_mm(st.get('merge'))} | {_mm(st.get('emit'))} | "
             f"{sent / 1e6:.2f} | {direct} | {', '.join(tr) or '-'} | - |")
+    extra = []
+    for ln in lines:
+        if ln.get("value") is None:
+            continue
+        d = ln.get("scale_diag") or {}
+        hbm = d.get("hbm_device_bytes_max")
+        extra.append(f"N={ln['n_gpus']}: strategy {ln.get('strategy') or '-'} (headline), "
+                     f"{(ln.get('synth1m') or {}).get('strategy', '-')} (synth1m)"
+                     + (f"; engine device memory max {hbm / 2**30:.2f} GiB per rank" if hbm else ""))
     note = ("\nweak eff = T(1) / T(N) of the headline (per-rank work fixed); strong eff = "
             "T(1) / (N x T(N)) of synth1m (total work fixed), against the N = 1 synth1m point.\n")
-    return "\n".join(rows) + "\n" + note
+    tail = "".join(f"\n{x}" for x in extra + fails)
+    return "\n".join(rows) + "\n" + note + (tail + "\n" if tail else "")
 
 
 def main(argv=None) -> int:
