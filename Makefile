@@ -100,3 +100,8 @@ $(BUILD)/exit_probe: tools/exit_probe.hip
 read_probe: $(BUILD)/read_probe
 $(BUILD)/read_probe: tools/read_probe.cpp $(LIB)
 	$(CXX) -O2 -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< -L$(LIBDIR) -llocust -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+# diagnostics: each kernel file's code-object load time in a fresh process
+module_probe: $(BUILD)/module_probe
+$(BUILD)/module_probe: tools/micro/module_probe.cpp $(LIB)
+	$(CXX) -O2 -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< -L$(LIBDIR) -llocust -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
