@@ -1,0 +1,68 @@
+"""A longer randomized soak of the GPU paths than the test suite's (tests/test_fuzz.py runs
+3 seeds per path): `--seeds` random byte texts per size (delimiter runs, NUL, CR, 0xFF,
+lines up to 2,000 B, with and without a final newline) through every GPU path, fresh
+engines and one reused engine, each result compared entry by entry with the pure-Python
+oracle.  Prints one line per path and exits non-zero on the first mismatch.
+
+    python tools/fuzz_soak.py [--seeds 30] [--out FILE]
+"""
+import argparse
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import locust_amd as lc  # noqa: E402
+from locust_amd.utils import oracle  # noqa: E402
+from test_fuzz import GPU_PATHS, SIZES, random_text  # noqa: E402
+
+EXTRA_PATHS = [dict(zero_copy_text=1), dict(zero_copy_text=0)]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seeds", type=int, default=30)
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    lines = []
+
+    def say(s):
+        lines.append(s)
+        print(s, flush=True)
+
+    texts = []
+    for seed in range(a.seeds):
+        rng = random.Random(5000 + seed)
+        for size in SIZES:
+            texts.append((seed, size, random_text(rng, size)))
+    want = [oracle.wordcount(t) for _, _, t in texts]
+    for opts in GPU_PATHS + EXTRA_PATHS:
+        t0 = time.time()
+        for (seed, size, text), (ent, ntok, _) in zip(texts, want):
+            r = lc.wordcount_text(text, backend="gpu", check=True, **opts)
+            if r.num_tokens != ntok or r.entries() != ent:
+                say(f"MISMATCH path={opts} seed={seed} size={size}")
+                return 1
+        say(f"path {opts or 'default'}: {len(texts)} texts match the oracle ({time.time() - t0:.1f} s)")
+    eng = lc._C.GpuEngine(lc.make_config("gpu", check=True), 300_000, 300_000)
+    n = 0
+    for (seed, size, text), (ent, _n, _) in zip(texts, want):
+        if size > 300_000:
+            continue
+        if eng.run(text).entries() != ent:
+            say(f"MISMATCH reused engine seed={seed} size={size}")
+            return 1
+        n += 1
+    say(f"one reused engine: {n} texts back to back match the oracle")
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write("\n".join(lines) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
