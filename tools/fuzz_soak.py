@@ -2,7 +2,8 @@
 3 seeds per path): `--seeds` random byte texts per size (delimiter runs, NUL, CR, 0xFF,
 lines up to 2,000 B, with and without a final newline) through every GPU path, fresh
 engines and one reused engine, each result compared entry by entry with the pure-Python
-oracle.  Prints one line per path and exits non-zero on the first mismatch.
+oracle; then ~2 MB texts streamed through small chunks against the CPU engine.  Prints
+one line per path and exits non-zero on the first mismatch.
 
     python tools/fuzz_soak.py [--seeds 30] [--out FILE]
 """
@@ -58,6 +59,34 @@ def main() -> int:
             return 1
         n += 1
     say(f"one reused engine: {n} texts back to back match the oracle")
+    # streamed passes: ~2 MB random texts through engines with small chunks (line-aligned
+    # chunk cuts, map windows, one dictionary across chunks), pageable and pinned input,
+    # against the CPU engine (itself matched to the oracle by tests/test_fuzz.py)
+    t0 = time.time()
+    m = 0
+    for seed in range(max(1, a.seeds // 10)):
+        rng = random.Random(9000 + seed)
+        parts, size = [], 0
+        while size < 2 << 20:
+            piece = random_text(rng, rng.choice([4096, 60_000, 200_000]))
+            piece = piece[: piece.rfind(b"\n") + 1] or b"x\n"
+            parts.append(piece)
+            size += len(piece)
+        text = b"".join(parts)
+        ref = lc._C.cpu_run(lc.make_config("cpu"), text).entries()
+        for chunk in (4 << 10, 64 << 10, 1 << 20):
+            if max(len(x) for x in text.split(b"\n")) + 1 >= chunk:
+                continue  # a line longer than the chunk is refused by design
+            eng = lc._C.GpuEngine(lc.make_config("gpu", check=True, chunk_bytes=chunk), 1 << 30, 1 << 30)
+            if eng.run(text).entries() != ref:
+                say(f"MISMATCH streamed pageable seed={seed} chunk={chunk}")
+                return 1
+            if eng.run_text(lc._C.HostText.from_bytes(text)).entries() != ref:
+                say(f"MISMATCH streamed pinned seed={seed} chunk={chunk}")
+                return 1
+            m += 2
+    say(f"streamed: {m} runs of ~2 MB texts (chunks 4 KiB / 64 KiB / 1 MiB) match the CPU engine "
+        f"({time.time() - t0:.1f} s)")
     if a.out:
         with open(a.out, "w") as f:
             f.write("\n".join(lines) + "\n")
