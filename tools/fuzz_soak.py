@@ -2,7 +2,8 @@
 3 seeds per path): `--seeds` random byte texts per size (delimiter runs, NUL, CR, 0xFF,
 lines up to 2,000 B, with and without a final newline) through every GPU path, fresh
 engines and one reused engine, each result compared entry by entry with the pure-Python
-oracle; then ~2 MB texts streamed through small chunks against the CPU engine.  Prints
+oracle; then ~2 MB texts streamed through small chunks against the CPU engine, and
+multi-rank jobs (loopback ranks on the GPU, both strategies) against the oracle.  Prints
 one line per path and exits non-zero on the first mismatch.
 
     python tools/fuzz_soak.py [--seeds 30] [--out FILE]
@@ -86,6 +87,22 @@ def main() -> int:
                 return 1
             m += 2
     say(f"streamed: {m} runs of ~2 MB texts (chunks 4 KiB / 64 KiB / 1 MiB) match the CPU engine "
+        f"({time.time() - t0:.1f} s)")
+    # multi-rank jobs in this process (loopback ranks sharing the GPU: the exchange logic of
+    # an N-GPU run), both strategies, several world sizes, against the oracle
+    t0 = time.time()
+    k = 0
+    for i, ((seed, size, text), (ent, _n, _)) in enumerate(zip(texts, want)):
+        if i % 9 not in (4, 7, 8) or i >= 9 * max(1, a.seeds // 5):
+            continue  # a few sizes (4 KiB .. 200 KB) of every fifth seed
+        for world in (2, 3, 8):
+            for strategy in ("gather", "shuffle"):
+                r = lc.run_multi(text, world, strategy=strategy)
+                if r.entries() != ent:
+                    say(f"MISMATCH multi-rank world={world} {strategy} seed={seed} size={size}")
+                    return 1
+                k += 1
+    say(f"multi-rank (loopback, 2/3/8 ranks, gather and shuffle): {k} jobs match the oracle "
         f"({time.time() - t0:.1f} s)")
     if a.out:
         with open(a.out, "w") as f:
