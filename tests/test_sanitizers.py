@@ -50,3 +50,36 @@ def test_stage_split_and_generator_under_asan(asan_cli, tmp_path):
 def test_gpu_backend_fails_loudly_in_host_build(asan_cli):
     r = run([asan_cli, os.path.join(ROOT, "data", "hamlet.txt")])
     assert r.returncode == 2 and b"no GPU backend" in r.stderr
+
+
+def test_byte_windows_and_threaded_reducers_under_asan(asan_cli, tmp_path):
+    """Round 6 paths: byte-range stage-1 windows (line-start moves, the cached line index)
+    and stage 2 reading every spill's key range on its own thread, with R key-range
+    reducers -- clean under ASan/UBSan, and the reducers' slices concatenate to the
+    single-stage result."""
+    g = tmp_path / "g.txt"
+    r = run([asan_cli, "--gen", str(g), "--gen-lines", "8000", "--seed", "5"])
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    size = g.stat().st_size
+    spills = []
+    for k in range(3):
+        a, b = size * k // 3, size * (k + 1) // 3
+        r = run([asan_cli, str(g), "0", "0", str(k), "1", "--byte-range", f"{a}:{b}",
+                 "--backend", "cpu", "--spill-dir", str(tmp_path), "--spill-format", "binary"])
+        assert r.returncode == 0, r.stderr.decode()[-3000:]
+        spills.append(str(tmp_path / f"out.{k}.kv"))
+    r = run([asan_cli, str(g), "1000", "3000", "9", "1", "--backend", "cpu", "--spill-dir",
+             str(tmp_path), "--spill-format", "binary"])  # a line window via the line index
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    whole = run([asan_cli, str(g), "--backend", "cpu", "--output-format", "gpu"])
+    assert whole.returncode == 0, whole.stderr.decode()[-3000:]
+    want = [ln for ln in whole.stdout.split(b"\n") if ln.startswith(b"print key:")]
+    got = []
+    for rr in range(2):
+        res = tmp_path / f"res.{rr}"
+        r = run([asan_cli, str(g), "0", "0", str(rr), "2", "--inputs", ",".join(spills),
+                 "--reducer", f"{rr}/2", "--result-file", str(res), "--backend", "cpu",
+                 "--output-format", "gpu"])
+        assert r.returncode == 0, r.stderr.decode()[-3000:]
+        got += [ln for ln in res.read_bytes().split(b"\n") if ln.startswith(b"print key:")]
+    assert got == want
