@@ -4,6 +4,7 @@
 #   make            -> locust_amd/_lib/liblocust.so, locust_amd/_locust*.so, build/MapReduce
 #   make debug      -> same with -O0 -g
 #   make asan       -> host-only ASan/UBSan build of the CPU engine + CLI (build/asan/)
+#   make tsan       -> host-only ThreadSanitizer build of the same (build/tsan/)
 #   make clean
 #
 # Device code targets gfx950 (MI355X) only.  Device helpers are header-only, so no
@@ -80,6 +81,16 @@ asan: $(BUILD)/asan/MapReduce
 $(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) -std=c++17 -Icsrc/include -I$(ROCM)/include -O1 -g -fsanitize=address,undefined \
+	  -fno-omit-frame-pointer -o $@ $(ASAN_SRCS) -L$(ROCM)/lib -lrocprofiler-sdk-roctx \
+	  -Wl,-rpath,$(ROCM)/lib -lpthread
+
+# Host-only ThreadSanitizer build of the same sources: the host threads (parallel preads,
+# the streamed source's read pool, stage 2's per-spill readers, the CPU engine's ranks and
+# TCP communicator threads) checked for data races.
+tsan: $(BUILD)/tsan/MapReduce
+$(BUILD)/tsan/MapReduce: $(ASAN_SRCS) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) -std=c++17 -Icsrc/include -I$(ROCM)/include -O1 -g -fsanitize=thread \
 	  -fno-omit-frame-pointer -o $@ $(ASAN_SRCS) -L$(ROCM)/lib -lrocprofiler-sdk-roctx \
 	  -Wl,-rpath,$(ROCM)/lib -lpthread
 

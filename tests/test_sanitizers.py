@@ -83,3 +83,43 @@ def test_byte_windows_and_threaded_reducers_under_asan(asan_cli, tmp_path):
         assert r.returncode == 0, r.stderr.decode()[-3000:]
         got += [ln for ln in res.read_bytes().split(b"\n") if ln.startswith(b"print key:")]
     assert got == want
+
+
+TSAN = os.path.join(ROOT, "build", "tsan", "MapReduce")
+
+
+@pytest.fixture(scope="module")
+def tsan_cli():
+    r = subprocess.run(["make", "-C", ROOT, "tsan"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return TSAN
+
+
+def test_threaded_host_paths_under_tsan(tsan_cli, tmp_path):
+    """ThreadSanitizer over the host threads (SURVEY.md §5.2 race detection): the parallel
+    preads of a whole-file read, byte-range windows, a line window through the per-file line
+    index (its block scan runs on threads and saves the cache), and stage 2's per-spill
+    readers -- no data race reported (halt_on_error), and the reducers' output equals the
+    single stage's."""
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", LOCUST_CACHE_DIR=str(tmp_path / "c"))
+
+    def trun(*args):
+        r = subprocess.run([tsan_cli, *map(str, args)], capture_output=True, env=env, timeout=600)
+        assert r.returncode == 0, r.stderr.decode()[-4000:]
+        return r
+
+    g = tmp_path / "g.txt"
+    trun("--gen", g, "--gen-bytes", 24_000_000, "--seed", 4)  # 2-3 pread threads per read
+    whole = trun(g, "--backend", "cpu", "--output-format", "gpu")
+    size = g.stat().st_size
+    spills = []
+    for k in range(3):
+        trun(g, 0, 0, k, 1, "--byte-range", f"{size * k // 3}:{size * (k + 1) // 3}", "--backend",
+             "cpu", "--spill-dir", tmp_path, "--spill-format", "binary")
+        spills.append(str(tmp_path / f"out.{k}.kv"))
+    trun(g, 100_000, 400_000, 9, 1, "--backend", "cpu", "--spill-dir", tmp_path, "--spill-format",
+         "binary")  # a line window: the line index's threaded block scan
+    r = trun(g, 0, 0, 0, 2, "--inputs", ",".join(spills), "--backend", "cpu", "--output-format",
+             "gpu")
+    keys = lambda out: [ln for ln in out.split(b"\n") if ln.startswith(b"print key:")]  # noqa: E731
+    assert keys(r.stdout) == keys(whole.stdout)
