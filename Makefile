@@ -87,7 +87,15 @@ $(BUILD)/asan/MapReduce: $(ASAN_SRCS) $(HDRS)
 # Host-only ThreadSanitizer build of the same sources: the host threads (parallel preads,
 # the streamed source's read pool, stage 2's per-spill readers, the CPU engine's ranks and
 # TCP communicator threads) checked for data races.
-tsan: $(BUILD)/tsan/MapReduce
+TSAN_PROBE_SRCS := tools/read_probe.cpp csrc/io/io.cpp csrc/engine/common.cpp csrc/engine/trace.cpp \
+                   csrc/engine/numa.cpp
+tsan: $(BUILD)/tsan/MapReduce $(BUILD)/tsan/read_probe
+# the streamed file source (FileTextSource: read pool threads, whole-line carry) alone
+$(BUILD)/tsan/read_probe: $(TSAN_PROBE_SRCS) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) -std=c++17 -Icsrc/include -I$(ROCM)/include -O1 -g -fsanitize=thread \
+	  -fno-omit-frame-pointer -o $@ $(TSAN_PROBE_SRCS) -L$(ROCM)/lib -lrocprofiler-sdk-roctx \
+	  -Wl,-rpath,$(ROCM)/lib -lpthread
 $(BUILD)/tsan/MapReduce: $(ASAN_SRCS) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) -std=c++17 -Icsrc/include -I$(ROCM)/include -O1 -g -fsanitize=thread \

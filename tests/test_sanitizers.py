@@ -98,9 +98,9 @@ def tsan_cli():
 def test_threaded_host_paths_under_tsan(tsan_cli, tmp_path):
     """ThreadSanitizer over the host threads (SURVEY.md §5.2 race detection): the parallel
     preads of a whole-file read, byte-range windows, a line window through the per-file line
-    index (its block scan runs on threads and saves the cache), and stage 2's per-spill
-    readers -- no data race reported (halt_on_error), and the reducers' output equals the
-    single stage's."""
+    index (its block scan runs on threads and saves the cache), stage 2's per-spill readers
+    and the streamed file source's read pool -- no data race reported (halt_on_error), and
+    the results equal the single stage's / the file's line count."""
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", LOCUST_CACHE_DIR=str(tmp_path / "c"))
 
     def trun(*args):
@@ -123,3 +123,10 @@ def test_threaded_host_paths_under_tsan(tsan_cli, tmp_path):
              "gpu")
     keys = lambda out: [ln for ln in out.split(b"\n") if ln.startswith(b"print key:")]  # noqa: E731
     assert keys(r.stdout) == keys(whole.stdout)
+    # the streamed source the GPU engine reads files through (read pool threads, 16 MiB
+    # pieces, whole-line carry): every piece's lines counted, no race
+    p = subprocess.run([os.path.join(ROOT, "build", "tsan", "read_probe"), str(g), "0", "3", "8"],
+                       capture_output=True, env=env, timeout=600)
+    assert p.returncode == 0, p.stderr.decode()[-4000:]
+    n = g.read_bytes().count(b"\n")
+    assert p.stdout.decode().count(f" {n} lines") == 6, p.stdout.decode()
