@@ -127,3 +127,18 @@ def test_engine_runs_a_warm_up_job_without_side_effects():
                "void DevicePipeline::print_ord_trace()", "void DevicePipeline::print_map_trace()"):
         body = _body(s, fn)
         assert "warming" in body.split("\n", 3)[1] + body.split("\n", 3)[2], fn
+
+
+@pytest.mark.gpu
+def test_warm_up_job_with_letter_delimiters(hamlet):
+    """The construction warm-up job picks a token byte outside the job's delimiter set: an
+    engine whose delimiters include 'a' builds, and its jobs match the oracle."""
+    import locust_amd as lc
+    from locust_amd.utils import oracle
+
+    delims = " ,.-;:'()\"\ta"
+    cfg = lc.make_config("gpu", delimiters=delims)
+    eng = lc._C.GpuEngine(cfg, len(hamlet), hamlet.count(b"\n") + 1)
+    want = oracle.wordcount(hamlet, delims=delims.encode())[0]
+    for _ in range(2):
+        assert eng.run(hamlet).entries() == want
