@@ -82,3 +82,39 @@ def test_oversize_chunk_is_refused_at_planning_time():
 def test_receiver_engines_keep_every_record():
     p = plan(1, lines=1, cap_records=3_000_000)
     assert p["cap"] == p["rcap"] == 3_000_000 and not p["streaming"]
+
+
+@pytest.mark.gpu
+def test_cli_json_reports_the_hbm_plan(tmp_path):
+    """`--json` carries the engine's device bytes, the GPU's free / total HBM and the pass
+    shape -- one engine, a streamed engine, and every rank of a loopback run."""
+    import json
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "build", "MapReduce")
+    hamlet = os.path.join(root, "data", "hamlet.txt")
+
+    def run(*args):
+        j = tmp_path / "r.json"
+        p = subprocess.run([cli, *map(str, args), "--json", str(j), "--quiet"], capture_output=True,
+                           timeout=300)
+        assert p.returncode == 0, p.stderr.decode()[-2000:]
+        return json.loads(j.read_text())
+
+    one = run(hamlet)
+    assert 0 < one["hbm_device_bytes"] < 4 * GiB
+    assert 200 * GiB < one["hbm_total_bytes"] and 0 < one["hbm_free_bytes"] <= one["hbm_total_bytes"]
+    assert one["device_streaming"] is False
+    g = tmp_path / "g.txt"
+    subprocess.run([cli, "--gen", str(g), "--gen-bytes", str(6 << 20), "--seed", "2"], check=True,
+                   capture_output=True, timeout=120)
+    st = run(g, "--chunk-mb", 1)
+    assert st["device_streaming"] is True and st["device_chunk_bytes"] == MiB
+    assert 0 < st["device_map_window"] <= 32 * MiB
+    ranks = run(g, "--gpus", 2, "--comm", "loopback")
+    assert len(ranks["ranks"]) == 2
+    assert ranks["hbm_device_bytes"] == sum(r["hbm_device_bytes"] for r in ranks["ranks"]) > 0
+    assert all(r["hbm_total_bytes"] == ranks["hbm_total_bytes"] for r in ranks["ranks"])
+    assert 0 < ranks["hbm_used_bytes_max"] <= ranks["hbm_total_bytes"]
