@@ -124,3 +124,8 @@ $(BUILD)/read_probe: tools/read_probe.cpp $(LIB)
 module_probe: $(BUILD)/module_probe
 $(BUILD)/module_probe: tools/micro/module_probe.cpp $(LIB)
 	$(CXX) -O2 -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< -L$(LIBDIR) -llocust -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+# diagnostics: instruction-fetch cost of straight-line code vs loops, cold and warm
+icache_probe: $(BUILD)/icache_probe
+$(BUILD)/icache_probe: tools/micro/icache_probe.hip
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
