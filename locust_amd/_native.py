@@ -1,6 +1,6 @@
 """Loader for the native extension (``locust_amd/_locust*.so`` + ``_lib/liblocust.so``).
 
-The extension is built in-tree by ``make`` (or :func:`locust_amd.build`).  Import fails
+The extension is built in-tree by ``make`` (or ``python __graft_entry__.py``, which runs it).  Import fails
 loudly when it is missing: there is no pure-Python fallback for the engine, so a GPU test
 can never silently pass on a Python stand-in.
 """
@@ -28,7 +28,7 @@ def load():
     except ImportError as e:  # pragma: no cover - exercised only on a broken checkout
         raise ImportError(
             "locust_amd native extension is not built; run `make -j8` in "
-            f"{REPO_ROOT} (or locust_amd.build()). Original error: {e}"
+            f"{REPO_ROOT} (or `python __graft_entry__.py`). Original error: {e}"
         ) from e
     return sys.modules[__name__.rsplit(".", 1)[0] + "._locust"]
 
