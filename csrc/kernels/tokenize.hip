@@ -4,16 +4,17 @@
 // strtok_r over " ,.-;:'()\"\t", at most EMITS_PER_LINE tokens per line, value 1), but the
 // work is spread over bytes instead of lines:
 //
-//  * A 256-thread workgroup owns a tile of 4 wave segments (STEPS x 64 bytes each).  The
-//    tile plus 64 bytes of left context and 64 bytes of right overhang is staged into LDS
-//    with 16-byte vector loads, so every later byte access is an LDS read.
+//  * A workgroup owns a tile of wave segments (STEPS x 64 bytes each): 16 waves x one step
+//    (1 KiB) for inputs below kMapLargeInput, 4 waves x 16 steps (4 KiB) above.  The tile
+//    plus 128 bytes of left context (kPre) and 64 bytes of right overhang (kPost) is staged
+//    into LDS with 16-byte vector loads, so every later byte access is an LDS read.
 //  * Each step, every lane looks at one byte.  The delimiter set lives in four u64 kernel
 //    arguments (SGPRs), so the membership test is a few VALU ops.  Ballots give the step's
 //    delimiter mask; token start = not-delimiter && previous byte is a delimiter.  The
 //    per-line ordinal (for the 20-emit cap) is the popcount of starts since the last
 //    '\n', carried across steps; the ordinal carried INTO a segment comes from a backward
 //    scan to the previous newline, stopped once it exceeds the cap.
-//  * Emit counts are summed across the 4 waves; one atomic per tile reserves the tile's
+//  * Emit counts are summed across the tile's waves; one atomic per tile reserves the tile's
 //    slice of the token array (tokens are not kept in text order across tiles: every
 //    consumer hashes or sorts them, so no ticket and no look-back chain is needed -- the
 //    tiles all start at once and the zero-copy text reads overlap), then each emitting
@@ -22,7 +23,9 @@
 //    aligned u64 words, funnel-shifts, masks and byte-swaps them into the big-endian
 //    packed key, and writes it straight into the dense SoA output.  The map output is
 //    born compacted, so the reference's 116,000-slot thrust::partition (main.cu:411) has
-//    nothing left to do.
+//    nothing left to do.  With a partition map (part_off) the tile writes its tokens
+//    grouped by partition and records where each partition's run starts (map_tile.hpp),
+//    which is how the ordered kernel finds a partition's tokens.
 #include <cstdlib>
 
 #include "locust/hip_check.hpp"
