@@ -60,8 +60,9 @@ struct LookbackScratch {
 
 // ---------------- map.hip ----------------
 constexpr int kMapBlock = 256;
-// Tile = 4 waves x steps x 64 B.  Small inputs use 4 steps (1 KiB tiles: more workgroups
-// in flight), large inputs 16 steps (4 KiB tiles: fewer look-back hops and overlaps).
+// Tile bytes = 4 waves x steps x 64 B.  Small inputs: 1 KiB tiles (run as 16 waves x one
+// 64-B step, launch_map_fast: more workgroups in flight; 768-B tiles measured neutral,
+// profiles/r6/map/tile768_ab.txt), large inputs 16 steps (4 KiB tiles: fewer overlaps).
 constexpr int kMapSegStepsSmall = 4;
 constexpr int kMapSegStepsLarge = 16;
 constexpr int kMapTileBytesMin = (kMapBlock / 64) * kMapSegStepsSmall * 64;
