@@ -1449,7 +1449,9 @@ __device__ __forceinline__ void ordered_partition(
             wcnt += lt ? cw[q] : 0u;
           }
         }
-        if (trace)
+        // one lane per wave: 64 lanes' same-address atomics serialise and inflated the
+        // traced ranking / look-back phases by ~10 us
+        if (trace && dev::lane_id() == 0)
           atomicMax(reinterpret_cast<unsigned long long*>(&trace[(u64)v * 32 + 18]),
                     (unsigned long long)__builtin_amdgcn_s_memtime());
         if (own && cnt) {
