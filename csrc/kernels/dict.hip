@@ -1764,16 +1764,19 @@ __device__ __forceinline__ void ordered_partition(
     }
     __syncthreads();
     if (s_count) {
+      // Tell the host first: every workgroup's records, counters and headers are out --
+      // each one, this one included, released them at system scope (L2 written back, the
+      // writes waited for) before counting itself done, and this one saw all 256 counts.
+      // So the store is relaxed: a release here wrote the L2 back again and waited for the
+      // acquire's load below, two more memory round trips before the host could see it.
+      // The re-zeroing below touches device scratch only, which the next job's kernels --
+      // behind this one on the stream -- see complete; the host's turnaround overlaps it.
+      if (ex.host_done && threadIdx.x == 0)
+        __hip_atomic_store(ex.host_done, ex.host_done_value, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       // acquire every other workgroup's (acquire only: this one released its own already)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const u32 flags = __hip_atomic_load(&ctr->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // Tell the host first: every workgroup's records, counters and headers are out (each
-      // released them before counting itself done).  The re-zeroing below touches device
-      // scratch only, which the next job's kernels -- behind this one on the stream -- see
-      // complete; the host's turnaround overlaps it (it took 3.8 us before the publish).
-      if (ex.host_done && threadIdx.x == 0)  // a system-scope release store
-        __hip_atomic_store(ex.host_done, ex.host_done_value, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
       if (!(flags & kCtrDictOverflow)) {
         for (u32 i = threadIdx.x; i < ex.map_words; i += kPartBlock) ex.map_lb.status[i] = 0;
         for (u32 i = threadIdx.x; i <= (u32)kDictParts; i += kPartBlock) status[i] = 0;
